@@ -1,0 +1,655 @@
+/*
+ * oracle.c -- CPU restatement of the Vosk/Kaldi hot path (TEST INFRASTRUCTURE
+ * ONLY; see oracle.h for the parity status: unpinned vs Kaldi, bit-exact
+ * contract vs the HIP kernels).
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off).  Contraction must stay
+ * off: every fused multiply-add below is an explicit fmaf(), every other
+ * product/sum is rounded separately, exactly as in the HIP kernels.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ===================================================================== */
+/* MFCC                                                                  */
+/* Kaldi feat/feature-window.cc (ExtractWindow/ProcessWindow),            */
+/* feat/mel-computations.cc (MelBanks), feat/feature-mfcc.cc (Compute),   */
+/* matrix/matrix-functions.cc (ComputeDctMatrix).  Reference call site:   */
+/* src/model.cc:218-221 (mfcc.conf -> OnlineNnet2FeaturePipeline).        */
+/* Deviation (documented): radix-2 complex FFT instead of Kaldi's         */
+/* split-radix real FFT; sums as sequential fp32 chains; custom log.      */
+/* ===================================================================== */
+
+static int frame_length(const orc_mfcc_opts* o) { return (int)(o->samp_freq * 0.001f * o->frame_length_ms); }
+static int frame_shift(const orc_mfcc_opts* o) { return (int)(o->samp_freq * 0.001f * o->frame_shift_ms); }
+static int padded_length(const orc_mfcc_opts* o) {
+  int n = frame_length(o), p = 1;
+  if (!o->round_to_power_of_two) return n;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+int orc_mfcc_num_frames(const orc_mfcc_opts* o, long n) {
+  int L = frame_length(o), S = frame_shift(o);
+  if (n < L) return 0;
+  return (int)(1 + (n - L) / S);
+}
+
+/* natural log, x > 0 normal: log(m*2^e) = e*ln2 + log1p(m-1),
+   m in [sqrt(.5), sqrt(2)); log1p via a degree-10 polynomial (Horner fmaf) */
+float orc_logf(float x) {
+  static const float C[11] = {1.000000000e+00f, -5.000000000e-01f, 3.333330154e-01f,
+                              -2.500002384e-01f, 2.000257671e-01f, -1.666804254e-01f,
+                              1.421260685e-01f,  -1.239922047e-01f, 1.192392558e-01f,
+                              -1.172722951e-01f, 6.740232557e-02f};
+  union { float f; uint32_t u; } v;
+  v.f = x;
+  int e = (int)((v.u >> 23) & 0xff) - 127;
+  v.u = (v.u & 0x7fffffu) | 0x3f800000u;
+  float m = v.f;
+  if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+  float f = m - 1.0f;
+  float p = C[10];
+  for (int i = 9; i >= 0; i--) p = fmaf(p, f, C[i]);
+  return fmaf((float)e, 0.693147182f, f * p);
+}
+
+static float mel_scale(float f) { return 1127.0f * logf(1.0f + f / 700.0f); }
+
+int orc_mfcc(const orc_mfcc_opts* o, const float* wave, long n, float* out) {
+  const int L = frame_length(o), S = frame_shift(o), N = padded_length(o);
+  const int nf = orc_mfcc_num_frames(o, n);
+  const int nb = o->num_bins, nc = o->num_ceps;
+  if (N & (N - 1)) return -1; /* only power-of-two FFT sizes */
+  float* win = (float*)malloc(sizeof(float) * L);
+  double a = 2.0 * M_PI / (L - 1);
+  for (int i = 0; i < L; i++) {
+    double c = cos(a * i), w;
+    switch (o->window_type) {
+      case 0: w = pow(0.5 - 0.5 * c, 0.85); break;
+      case 1: w = 0.54 - 0.46 * c; break;
+      case 2: w = 0.5 - 0.5 * c; break;
+      case 3: w = 1.0; break;
+      default: w = o->blackman_coeff - 0.5 * c + (0.5 - o->blackman_coeff) * cos(2 * a * i); break;
+    }
+    win[i] = (float)w;
+  }
+  /* mel banks: float arithmetic as MelBanks::MelBanks */
+  const int nfft = N / 2;
+  float* melw = (float*)calloc((size_t)nb * nfft, sizeof(float));
+  int* first = (int*)malloc(sizeof(int) * nb);
+  int* last = (int*)malloc(sizeof(int) * nb);
+  {
+    float nyq = 0.5f * o->samp_freq;
+    float hi = o->high_freq > 0.0f ? o->high_freq : nyq + o->high_freq;
+    float width = o->samp_freq / (float)N;
+    float ml = mel_scale(o->low_freq), mh = mel_scale(hi);
+    float delta = (mh - ml) / (float)(nb + 1);
+    for (int b = 0; b < nb; b++) {
+      float left = ml + (float)b * delta, center = ml + (float)(b + 1) * delta,
+            right = ml + (float)(b + 2) * delta;
+      first[b] = -1;
+      last[b] = -1;
+      for (int i = 0; i < nfft; i++) {
+        float mel = mel_scale(width * (float)i);
+        if (mel > left && mel < right) {
+          float w = mel <= center ? (mel - left) / (center - left) : (right - mel) / (right - center);
+          melw[(size_t)b * nfft + i] = w;
+          if (first[b] < 0) first[b] = i;
+          last[b] = i;
+        }
+      }
+    }
+  }
+  float* dct = (float*)malloc(sizeof(float) * nc * nb);
+  {
+    float norm0 = (float)sqrt(1.0 / (double)nb);
+    float norm = (float)sqrt(2.0 / (double)nb);
+    for (int j = 0; j < nb; j++) dct[j] = norm0;
+    for (int k = 1; k < nc; k++)
+      for (int j = 0; j < nb; j++)
+        dct[k * nb + j] = (float)((double)norm * cos(M_PI / nb * (j + 0.5) * k));
+  }
+  float* lift = (float*)malloc(sizeof(float) * nc);
+  for (int i = 0; i < nc; i++) {
+    double q = o->cepstral_lifter;
+    lift[i] = q != 0.0 ? (float)(1.0 + 0.5 * q * sin(M_PI * i / q)) : 1.0f;
+  }
+  float* twr = (float*)malloc(sizeof(float) * (N / 2));
+  float* twi = (float*)malloc(sizeof(float) * (N / 2));
+  for (int k = 0; k < N / 2; k++) {
+    twr[k] = (float)cos(2.0 * M_PI * k / N);
+    twi[k] = (float)(-sin(2.0 * M_PI * k / N));
+  }
+  int logn = 0;
+  while ((1 << logn) < N) logn++;
+  float* re = (float*)malloc(sizeof(float) * N);
+  float* im = (float*)malloc(sizeof(float) * N);
+  float* x = (float*)malloc(sizeof(float) * L);
+  float* mel = (float*)malloc(sizeof(float) * nb);
+
+  for (int f = 0; f < nf; f++) {
+    const float* src = wave + (long)f * S;
+    for (int i = 0; i < L; i++) x[i] = src[i];
+    if (o->remove_dc_offset) {
+      float sum = 0.0f;
+      for (int i = 0; i < L; i++) sum = sum + x[i];
+      float c = -sum / (float)L;
+      for (int i = 0; i < L; i++) x[i] = x[i] + c;
+    }
+    float log_energy = 0.0f;
+    if (o->use_energy) {
+      float e = 0.0f;
+      for (int i = 0; i < L; i++) e = fmaf(x[i], x[i], e);
+      log_energy = orc_logf(e > 1.1920929e-07f ? e : 1.1920929e-07f);
+    }
+    if (o->preemph_coeff != 0.0f) {
+      for (int i = L - 1; i > 0; i--) x[i] = x[i] - o->preemph_coeff * x[i - 1];
+      x[0] = x[0] - o->preemph_coeff * x[0];
+    }
+    for (int i = 0; i < L; i++) x[i] = x[i] * win[i];
+    /* radix-2 DIT complex FFT of the zero-padded frame */
+    for (int i = 0; i < N; i++) {
+      int r = 0;
+      for (int b = 0; b < logn; b++) r |= ((i >> b) & 1) << (logn - 1 - b);
+      re[r] = i < L ? x[i] : 0.0f;
+      im[r] = 0.0f;
+    }
+    for (int len = 2; len <= N; len <<= 1) {
+      int half = len >> 1, step = N / len;
+      for (int i = 0; i < N; i += len)
+        for (int j = 0; j < half; j++) {
+          float wr = twr[j * step], wi = twi[j * step];
+          float br = re[i + j + half], bi = im[i + j + half];
+          float tr = br * wr - bi * wi;
+          float ti = br * wi + bi * wr;
+          float ur = re[i + j], ui = im[i + j];
+          re[i + j] = ur + tr;
+          im[i + j] = ui + ti;
+          re[i + j + half] = ur - tr;
+          im[i + j + half] = ui - ti;
+        }
+    }
+    /* power spectrum bins 0..N/2-1, mel energies, floor, log */
+    for (int b = 0; b < nb; b++) {
+      float e = 0.0f;
+      if (first[b] >= 0)
+        for (int i = first[b]; i <= last[b]; i++) {
+          float p = re[i] * re[i] + im[i] * im[i];
+          e = fmaf(melw[(size_t)b * nfft + i], p, e);
+        }
+      if (e < 1.1920929e-07f) e = 1.1920929e-07f;
+      mel[b] = orc_logf(e);
+    }
+    float* o_row = out + (size_t)f * nc;
+    for (int k = 0; k < nc; k++) {
+      float c = 0.0f;
+      for (int j = 0; j < nb; j++) c = fmaf(dct[k * nb + j], mel[j], c);
+      o_row[k] = c * lift[k];
+    }
+    if (o->use_energy) o_row[0] = log_energy;
+  }
+  free(win); free(melw); free(first); free(last); free(dct); free(lift);
+  free(twr); free(twi); free(re); free(im); free(x); free(mel);
+  return nf;
+}
+
+/* ===================================================================== */
+/* nnet3 forward (Kaldi nnet3/nnet-simple-component.cc, nnet-descriptor) */
+/* Whole-utterance evaluation with the input replicated at both edges    */
+/* (DecodableNnetSimpleLooped pads with the first/last frame [K]).        */
+/* Reference call site: src/model.cc:233-246, src/recognizer.cc:39-43.    */
+/* ===================================================================== */
+#define ORC_MARGIN 256
+
+typedef struct { int lo, hi; float* v; } node_vals;
+
+static float node_at(const orc_net* net, node_vals* nv, int node, int t, int col) {
+  node_vals* n = &nv[node];
+  if (node == 0) { /* input: replicate the first / last frame */
+    if (t < 0) t = 0;
+    if (t > n->hi) t = n->hi;
+    return n->v[(size_t)t * net->dim[node] + col];
+  }
+  return n->v[(size_t)(t - n->lo) * net->dim[node] + col];
+}
+
+/* evaluate node `i`'s descriptor at time t into x[in_dim] */
+static void eval_desc(const orc_net* net, node_vals* nv, int i, int t, float* x) {
+  const int* p = net->prog + net->prog_begin[i];
+  int nparts = *p++;
+  int col = 0;
+  for (int q = 0; q < nparts; q++) {
+    int pdim = *p++;
+    int ninstr = *p++;
+    const int* code = p;
+    p += 4 * ninstr;
+    for (int d = 0; d < pdim; d++) {
+      float stack[16];
+      int sp = 0;
+      for (int k = 0; k < ninstr; k++) {
+        int op = code[4 * k], node = code[4 * k + 1], off = code[4 * k + 2], fi = code[4 * k + 3];
+        if (op == 0) stack[sp++] = node_at(net, nv, node, t + off, fi + d);
+        else if (op == 1) stack[sp - 1] = net->progf[fi] * stack[sp - 1];
+        else if (op == 2) { stack[sp - 2] = stack[sp - 2] + stack[sp - 1]; sp--; }
+        else stack[sp++] = net->progf[fi];
+      }
+      x[col + d] = stack[0];
+    }
+    col += pdim;
+  }
+}
+
+/* time range over which node i is computable given its inputs' ranges */
+static void node_range(const orc_net* net, node_vals* nv, int i, int* lo, int* hi) {
+  const int* p = net->prog + net->prog_begin[i];
+  int nparts = *p++;
+  int L = -1000000000, H = 1000000000;
+  int tb = net->toff_begin[i], tc = net->toff_count[i];
+  for (int q = 0; q < nparts; q++) {
+    p++;
+    int ninstr = *p++;
+    for (int k = 0; k < ninstr; k++) {
+      if (p[4 * k] == 0) {
+        int node = p[4 * k + 1], off = p[4 * k + 2];
+        if (node == 0) continue; /* the input is edge-replicated: unbounded */
+        for (int z = 0; z < (tc ? tc : 1); z++) {
+          int to = tc ? net->toffs[tb + z] : 0;
+          if (nv[node].lo - off - to > L) L = nv[node].lo - off - to;
+          if (nv[node].hi - off - to < H) H = nv[node].hi - off - to;
+        }
+      }
+    }
+    p += 4 * ninstr;
+  }
+  *lo = L;
+  *hi = H;
+}
+
+/* mark the times each node must be computed at (backward from the outputs) */
+static void mark_needed(const orc_net* net, node_vals* nv, unsigned char** need, int i) {
+  const int* p = net->prog + net->prog_begin[i];
+  int nparts = *p++;
+  int tb = net->toff_begin[i], tc = net->toff_count[i];
+  for (int q = 0; q < nparts; q++) {
+    p++;
+    int ninstr = *p++;
+    for (int k = 0; k < ninstr; k++) {
+      if (p[4 * k] != 0) continue;
+      int node = p[4 * k + 1], off = p[4 * k + 2];
+      if (node == 0) continue;
+      for (int t = nv[i].lo; t <= nv[i].hi; t++) {
+        if (!need[i][t - nv[i].lo]) continue;
+        for (int z = 0; z < (tc ? tc : 1); z++) {
+          int tt = t + off + (tc ? net->toffs[tb + z] : 0);
+          need[node][tt - nv[node].lo] = 1;
+        }
+      }
+    }
+    p += 4 * ninstr;
+  }
+}
+
+#define ORC_TB 16
+int orc_nnet_forward(const orc_net* net, const float* feats, int T, float* out) {
+  const int NN = net->num_nodes;
+  node_vals* nv = (node_vals*)calloc(NN, sizeof(node_vals));
+  unsigned char** need = (unsigned char**)calloc(NN, sizeof(unsigned char*));
+  nv[0].lo = 0;
+  nv[0].hi = T - 1; /* clamp bounds for the replicated input */
+  nv[0].v = (float*)feats;
+  int maxk = 0, maxd = 0;
+  for (int i = 1; i < NN; i++) {
+    int lo, hi;
+    node_range(net, nv, i, &lo, &hi);
+    if (lo < -ORC_MARGIN) lo = -ORC_MARGIN;
+    if (hi > T - 1 + ORC_MARGIN) hi = T - 1 + ORC_MARGIN;
+    if (hi < lo) return -1;
+    nv[i].lo = lo;
+    nv[i].hi = hi;
+    need[i] = (unsigned char*)calloc(hi - lo + 1, 1);
+    int k = net->in_dim[i] * (net->toff_count[i] ? net->toff_count[i] : 1);
+    if (k > maxk) maxk = k;
+    if (net->dim[i] > maxd) maxd = net->dim[i];
+  }
+  const int on = net->output_node, OD = net->dim[on];
+  const int rows = (T + net->fss - 1) / net->fss;
+  for (int j = 0; j < rows; j++) {
+    int t = j * net->fss;
+    if (t < nv[on].lo || t > nv[on].hi) return -2;
+    need[on][t - nv[on].lo] = 1;
+  }
+  for (int i = NN - 1; i >= 1; i--) mark_needed(net, nv, need, i);
+
+  float* xb = (float*)malloc(sizeof(float) * (size_t)ORC_TB * (maxk + 1));
+  float* acc = (float*)malloc(sizeof(float) * (size_t)ORC_TB * (maxd + 1));
+  int tlist[ORC_TB];
+  for (int i = 1; i < NN; i++) {
+    const int D = net->dim[i], ID = net->in_dim[i];
+    const int tc = net->toff_count[i], tb = net->toff_begin[i];
+    const int K = ID * (tc ? tc : 1);
+    nv[i].v = (float*)malloc(sizeof(float) * (size_t)(nv[i].hi - nv[i].lo + 1) * D);
+    float* WT = NULL; /* transposed weights [K][D] so the n-loop vectorises */
+    if (net->kind[i] == 1) {
+      const float* W = net->params + net->w_off[i];
+      WT = (float*)malloc(sizeof(float) * (size_t)K * D);
+      for (int n = 0; n < D; n++)
+        for (int k = 0; k < K; k++) WT[(size_t)k * D + n] = W[(size_t)n * K + k];
+    }
+    int t = nv[i].lo;
+    while (t <= nv[i].hi) {
+      int nb = 0;
+      while (t <= nv[i].hi && nb < ORC_TB) {
+        if (need[i][t - nv[i].lo]) tlist[nb++] = t;
+        t++;
+      }
+      for (int b = 0; b < nb; b++) {
+        float* x = xb + (size_t)b * K;
+        if (tc) for (int z = 0; z < tc; z++) eval_desc(net, nv, i, tlist[b] + net->toffs[tb + z], x + z * ID);
+        else eval_desc(net, nv, i, tlist[b], x);
+      }
+      for (int b = 0; b < nb; b++) {
+        const float* x = xb + (size_t)b * K;
+        float* y = nv[i].v + (size_t)(tlist[b] - nv[i].lo) * D;
+        switch (net->kind[i]) {
+          case 1: { /* affine: y = (fmaf chain over k, from 0) + b */
+            float* a = acc + (size_t)b * D;
+            for (int n = 0; n < D; n++) a[n] = 0.0f;
+            for (int k = 0; k < K; k++) {
+              const float xk = x[k];
+              const float* w = WT + (size_t)k * D;
+              for (int n = 0; n < D; n++) a[n] = fmaf(xk, w[n], a[n]);
+            }
+            const float* B = net->b_off[i] >= 0 ? net->params + net->b_off[i] : NULL;
+            if (B) for (int n = 0; n < D; n++) y[n] = a[n] + B[n];
+            else memcpy(y, a, sizeof(float) * D);
+            break;
+          }
+          case 2: /* RectifiedLinear: ApplyFloor(0) */
+            for (int n = 0; n < D; n++) y[n] = x[n] < 0.0f ? 0.0f : x[n];
+            break;
+          case 3: { /* BatchNorm test mode / ScaleAndOffset: x*s + o */
+            const float* s = net->params + net->s_off[i];
+            const float* o = net->params + net->o_off[i];
+            for (int n = 0; n < D; n++) y[n] = x[n] * s[n] + o[n];
+            break;
+          }
+          default:
+            memcpy(y, x, sizeof(float) * D);
+        }
+      }
+    }
+    free(WT);
+  }
+  for (int j = 0; j < rows; j++) {
+    int t = j * net->fss;
+    const float* v = nv[on].v + (size_t)(t - nv[on].lo) * OD;
+    for (int n = 0; n < OD; n++) out[(size_t)j * OD + n] = v[n] * net->acoustic_scale;
+  }
+  for (int i = 1; i < NN; i++) { free(nv[i].v); free(need[i]); }
+  free(nv); free(need); free(xb); free(acc);
+  return rows;
+}
+
+/* ===================================================================== */
+/* Token passing (Kaldi decoder/lattice-faster-decoder.cc:               */
+/* InitDecoding, GetCutoff, ProcessEmitting, ProcessNonemitting,         */
+/* FinalizeDecoding/GetBestPath).  Reference call sites:                 */
+/* src/recognizer.cc:39-43 (decoder), :318 (endpoint), :790 (best path); */
+/* options src/model.cc:135-137.                                         */
+/* Order-independent formulation (documented in DESIGN.md): a token is    */
+/* created iff its cost beats the frame's FINAL emitting cutoff, and a    */
+/* token's backpointer is the min of (cost, arc index).                   */
+/* ===================================================================== */
+static inline uint32_t ford(float f) {
+  union { float f; uint32_t u; } v;
+  v.f = f;
+  return (v.u & 0x80000000u) ? ~v.u : (v.u | 0x80000000u);
+}
+static inline float funord(uint32_t k) {
+  union { float f; uint32_t u; } v;
+  v.u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return v.f;
+}
+#define EMPTY_KEY 0xffffffffffffffffull
+
+typedef struct { int prev, arc; } orc_link;
+
+typedef struct {
+  uint64_t* key;     /* per state: packed (ord(cost) << 32 | arc) for the frame being built */
+  int* prevtok;      /* per state: arena index of the winner's source token */
+  int* pos;          /* per state: position in the new token list */
+  int* inq;          /* per state: queued flag for the epsilon closure */
+  int* toks; int ntoks, cap;        /* new-frame states */
+  orc_link* arena; int narena, acap;
+} dstate;
+
+static void push_tok(dstate* d, int s) {
+  if (d->ntoks == d->cap) { d->cap *= 2; d->toks = (int*)realloc(d->toks, sizeof(int) * d->cap); }
+  d->pos[s] = d->ntoks;
+  d->toks[d->ntoks++] = s;
+}
+
+/* relax dest with (tot, arc) from source token index `src_idx`; returns 1 if improved */
+static int relax(dstate* d, int dest, float tot, int arc, int src_idx) {
+  uint64_t k = ((uint64_t)ford(tot) << 32) | (uint32_t)arc;
+  uint64_t old = d->key[dest];
+  if (old == EMPTY_KEY) push_tok(d, dest);
+  if (k < old) {
+    d->key[dest] = k;
+    d->prevtok[dest] = src_idx;
+    return 1;
+  }
+  return 0;
+}
+
+static int cmp_float(const void* a, const void* b) {
+  float x = *(const float*)a, y = *(const float*)b;
+  return x < y ? -1 : x > y ? 1 : 0;
+}
+
+static float kth_smallest(const float* c, int n, int k, float* tmp) {
+  memcpy(tmp, c, sizeof(float) * n);
+  qsort(tmp, n, sizeof(float), cmp_float);
+  return tmp[k];
+}
+
+/* epsilon closure over the tokens in d->toks (frame under construction) */
+static void eps_closure(const orc_graph* g, dstate* d, int base, float cutoff) {
+  int* queue = (int*)malloc(sizeof(int) * (g->num_states + 1));
+  int qh = 0, qt = 0;
+  for (int i = 0; i < d->ntoks; i++) { queue[qt++] = d->toks[i]; d->inq[d->toks[i]] = 1; }
+  while (qh != qt) {
+    int s = queue[qh];
+    qh = (qh + 1) % (g->num_states + 1);
+    d->inq[s] = 0;
+    float c = funord((uint32_t)(d->key[s] >> 32));
+    if (c > cutoff) continue;
+    int src_idx = base + d->pos[s];
+    for (int64_t a = g->eps_begin[s]; a < g->arc_begin[s + 1]; a++) {
+      float tot = c + g->weight[a];
+      if (tot < cutoff) {
+        int dest = g->nextstate[a];
+        if (relax(d, dest, tot, (int)a, src_idx) && !d->inq[dest]) {
+          d->inq[dest] = 1;
+          queue[qt] = dest;
+          qt = (qt + 1) % (g->num_states + 1);
+        }
+      }
+    }
+  }
+  free(queue);
+}
+
+/* move the frame under construction into the arena; returns its base index */
+static void commit_frame(dstate* d, int base, int* cur_state, float* cur_cost, int* cur_idx) {
+  for (int i = 0; i < d->ntoks; i++) {
+    int s = d->toks[i];
+    if (d->narena == d->acap) { d->acap *= 2; d->arena = (orc_link*)realloc(d->arena, sizeof(orc_link) * d->acap); }
+    d->arena[base + i].prev = d->prevtok[s];
+    d->arena[base + i].arc = (int)(uint32_t)(d->key[s] & 0xffffffffu);
+    d->narena++;
+    cur_state[i] = s;
+    cur_cost[i] = funord((uint32_t)(d->key[s] >> 32));
+    cur_idx[i] = base + i;
+  }
+  for (int i = 0; i < d->ntoks; i++) d->key[d->toks[i]] = EMPTY_KEY;
+}
+
+int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const orc_dec_opts* o,
+               int use_final, orc_dec_result* r) {
+  const int S = g->num_states;
+  dstate d;
+  d.key = (uint64_t*)malloc(sizeof(uint64_t) * S);
+  for (int s = 0; s < S; s++) d.key[s] = EMPTY_KEY;
+  d.prevtok = (int*)malloc(sizeof(int) * S);
+  d.pos = (int*)malloc(sizeof(int) * S);
+  d.inq = (int*)calloc(S, sizeof(int));
+  d.cap = 1024;
+  d.toks = (int*)malloc(sizeof(int) * d.cap);
+  d.acap = 1 << 16;
+  d.arena = (orc_link*)malloc(sizeof(orc_link) * d.acap);
+  d.narena = 0;
+  int* cur_state = (int*)malloc(sizeof(int) * S);
+  float* cur_cost = (float*)malloc(sizeof(float) * S);
+  int* cur_idx = (int*)malloc(sizeof(int) * S);
+  float* tmp = (float*)malloc(sizeof(float) * S);
+  double offsets_sum = 0.0;
+
+  /* InitDecoding: start token (cost 0, no predecessor), closure with cutoff = beam */
+  d.ntoks = 0;
+  relax(&d, g->start, 0.0f, -1, -1);
+  d.key[g->start] = ((uint64_t)ford(0.0f) << 32) | 0xffffffffu;
+  eps_closure(g, &d, 0, o->beam);
+  int ncur = d.ntoks;
+  commit_frame(&d, 0, cur_state, cur_cost, cur_idx);
+  if (r->ntok) r->ntok[0] = ncur;
+  if (r->best) {
+    float b = INFINITY;
+    for (int i = 0; i < ncur; i++) if (cur_cost[i] < b) b = cur_cost[i];
+    r->best[0] = b;
+  }
+
+  for (int f = 0; f < F; f++) {
+    const float* L = llh + (size_t)f * stride;
+    /* ---- GetCutoff */
+    float best = INFINITY;
+    int best_i = -1;
+    for (int i = 0; i < ncur; i++)
+      if (cur_cost[i] < best || (cur_cost[i] == best && cur_state[i] < cur_state[best_i])) {
+        best = cur_cost[i];
+        best_i = i;
+      }
+    if (best_i < 0) break; /* no surviving tokens */
+    float beam_cutoff = best + o->beam, adaptive, cutoff;
+    float max_cut = INFINITY, min_cut = INFINITY;
+    if (ncur > o->max_active) max_cut = kth_smallest(cur_cost, ncur, o->max_active, tmp);
+    if (max_cut < beam_cutoff) {
+      adaptive = max_cut - best + o->beam_delta;
+      cutoff = max_cut;
+    } else {
+      if (ncur > o->min_active) {
+        if (o->min_active == 0) min_cut = best;
+        else min_cut = kth_smallest(cur_cost, ncur, o->min_active, tmp);
+      }
+      if (min_cut > beam_cutoff) {
+        adaptive = min_cut - best + o->beam_delta;
+        cutoff = min_cut;
+      } else {
+        adaptive = o->beam;
+        cutoff = beam_cutoff;
+      }
+    }
+    /* ---- ProcessEmitting */
+    float cost_offset = -best;
+    float next_cutoff = INFINITY;
+    {
+      int s = cur_state[best_i];
+      for (int64_t a = g->arc_begin[s]; a < g->eps_begin[s]; a++) {
+        float nw = ((g->weight[a] + cost_offset) - L[g->tid2pdf[g->ilabel[a]]]) + best;
+        if (nw + adaptive < next_cutoff) next_cutoff = nw + adaptive;
+      }
+    }
+    float m = INFINITY;
+    int64_t examined = 0;
+    for (int i = 0; i < ncur; i++) {
+      if (!(cur_cost[i] <= cutoff)) continue;
+      int s = cur_state[i];
+      for (int64_t a = g->arc_begin[s]; a < g->eps_begin[s]; a++) {
+        float ac = cost_offset - L[g->tid2pdf[g->ilabel[a]]];
+        float tot = (cur_cost[i] + ac) + g->weight[a];
+        if (tot < m) m = tot;
+        examined++;
+      }
+    }
+    if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
+    d.ntoks = 0;
+    for (int i = 0; i < ncur; i++) {
+      if (!(cur_cost[i] <= cutoff)) continue;
+      int s = cur_state[i];
+      for (int64_t a = g->arc_begin[s]; a < g->eps_begin[s]; a++) {
+        float ac = cost_offset - L[g->tid2pdf[g->ilabel[a]]];
+        float tot = (cur_cost[i] + ac) + g->weight[a];
+        if (tot < next_cutoff) relax(&d, g->nextstate[a], tot, (int)a, cur_idx[i]);
+      }
+    }
+    int base = d.narena;
+    /* ---- ProcessNonemitting */
+    eps_closure(g, &d, base, next_cutoff);
+    ncur = d.ntoks;
+    commit_frame(&d, base, cur_state, cur_cost, cur_idx);
+    offsets_sum += cost_offset;
+    if (r->ntok) r->ntok[f + 1] = ncur;
+    if (r->cutoff) r->cutoff[f] = cutoff;
+    if (r->next_cutoff) r->next_cutoff[f] = next_cutoff;
+    if (r->arcs_emit) r->arcs_emit[f] = examined;
+    if (r->best) {
+      float b = INFINITY;
+      for (int i = 0; i < ncur; i++) if (cur_cost[i] < b) b = cur_cost[i];
+      r->best[f + 1] = b;
+    }
+    if (ncur == 0) break;
+  }
+
+  /* ---- best path end: with final costs if any token is final */
+  int end = -1;
+  float end_cost = INFINITY, best_nofinal = INFINITY, best_final = INFINITY;
+  for (int i = 0; i < ncur; i++) {
+    float c = cur_cost[i];
+    if (c < best_nofinal) best_nofinal = c;
+    float fc = g->final_cost[cur_state[i]];
+    if (fc != INFINITY) {
+      float cf = c + fc;
+      if (cf < best_final) best_final = cf;
+    }
+  }
+  int any_final = best_final != INFINITY;
+  for (int i = 0; i < ncur; i++) {
+    float c = (use_final && any_final) ? cur_cost[i] + g->final_cost[cur_state[i]] : cur_cost[i];
+    if (c < end_cost || (c == end_cost && end >= 0 && cur_state[i] < cur_state[end])) {
+      end_cost = c;
+      end = i;
+    }
+  }
+  r->final_relative_cost = any_final ? best_final - best_nofinal : INFINITY;
+  r->path_len = 0;
+  if (end >= 0) {
+    r->end_state = cur_state[end];
+    r->best_tot = end_cost;
+    r->best_cost = (double)end_cost - offsets_sum;
+    int n = 0;
+    for (int k = cur_idx[end]; k >= 0 && d.arena[k].arc >= 0; k = d.arena[k].prev) n++;
+    r->path_len = n;
+    int k = cur_idx[end];
+    for (int j = n - 1; j >= 0; j--) {
+      if (j < r->path_cap) r->path[j] = d.arena[k].arc;
+      k = d.arena[k].prev;
+    }
+  }
+  free(d.key); free(d.prevtok); free(d.pos); free(d.inq); free(d.toks); free(d.arena);
+  free(cur_state); free(cur_cost); free(cur_idx); free(tmp);
+  return end >= 0 ? 0 : -1;
+}

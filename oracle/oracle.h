@@ -1,0 +1,93 @@
+/*
+ * oracle.h -- CPU restatement of the Vosk/Kaldi hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library, and only as the checker
+ * (or the timed CPU baseline).  The product (libvosk.so) never links it.
+ *
+ * PARITY STATUS: "parity unpinned" against real Kaldi.  The reference's
+ * arithmetic lives in Kaldi/OpenFST, which are not vendored in
+ * /root/reference, cannot be built here and ship no
+ * golden vectors for MFCC / nnet3 / decoder values.  The only recorded
+ * outputs (python/example/colab/vosk.ipynb) need vosk-model-small-en-us-0.15,
+ * which is absent.  This oracle restates the published Kaldi algorithms
+ * (citations per function in oracle.c) with a fully specified fp32
+ * operation order; the HIP kernels reproduce that order, so GPU-vs-oracle
+ * parity is checked bit-exactly.
+ */
+#ifndef VAMD_ORACLE_H
+#define VAMD_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- MFCC (Kaldi feat/feature-mfcc.cc et al.) ---------------- */
+typedef struct {
+  float samp_freq, frame_shift_ms, frame_length_ms, preemph_coeff;
+  float low_freq, high_freq, cepstral_lifter, blackman_coeff;
+  int num_bins, num_ceps, use_energy, remove_dc_offset;
+  int window_type; /* 0 povey, 1 hamming, 2 hanning, 3 rectangular, 4 blackman */
+  int round_to_power_of_two;
+} orc_mfcc_opts;
+
+int orc_mfcc_num_frames(const orc_mfcc_opts* o, long num_samples);
+/* wave: float samples (int16 range).  out: [frames][num_ceps]. returns frames */
+int orc_mfcc(const orc_mfcc_opts* o, const float* wave, long num_samples, float* out);
+float orc_logf(float x);
+
+/* ---------------- nnet3 forward (whole utterance, edge-replicated input) ---- */
+typedef struct {
+  int num_nodes;      /* topological order; node 0 is the feature input */
+  const int* kind;    /* 0 input, 1 affine, 2 relu, 3 mul_add, 4 identity */
+  const int* dim;     /* output dim per node */
+  const int* in_dim;  /* descriptor dim per node (before TDNN splicing) */
+  const int64_t* w_off; const int64_t* b_off; const int64_t* s_off; const int64_t* o_off;
+  const float* params;
+  const int* toff_begin; const int* toff_count; const int* toffs;
+  const int* prog_begin; const int* prog; const float* progf;
+  int output_node, fss;
+  float acoustic_scale;
+} orc_net;
+
+/* out: [ceil(T/fss)][dim(output)] */
+int orc_nnet_forward(const orc_net* net, const float* feats, int T, float* out);
+
+/* ---------------- token-passing decoder (Kaldi decoder/lattice-faster-decoder.cc) */
+typedef struct {
+  float beam, beam_delta;
+  int max_active, min_active;
+} orc_dec_opts;
+
+typedef struct {
+  int num_states, start;
+  const int64_t* arc_begin; /* [S+1] */
+  const int64_t* eps_begin; /* [S]   */
+  const int* ilabel; const int* olabel; const int* nextstate;
+  const float* weight; const float* final_cost;
+  const int* tid2pdf;
+} orc_graph;
+
+typedef struct {
+  int* ntok;          /* [F+1] tokens per frame (frame 0 = after init) */
+  float* best;        /* [F+1] min tot_cost per frame                  */
+  float* cutoff;      /* [F]   GetCutoff result per frame               */
+  float* next_cutoff; /* [F]   emitting cutoff per frame                */
+  int64_t* arcs_emit; /* [F]   emitting arcs examined (roofline counter) */
+  int* path;          /* traceback arc indices (forward order)          */
+  int path_cap, path_len;
+  double best_cost;   /* offset-corrected cost of the best path (+final) */
+  float best_tot;     /* raw tot_cost of the chosen end token            */
+  int end_state;
+  float final_relative_cost;
+} orc_dec_result;
+
+int orc_decode(const orc_graph* g, const float* llh, int num_frames, int llh_stride,
+               const orc_dec_opts* o, int use_final, orc_dec_result* r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,405 @@
+"""ctypes driver for the C oracle (oracle/liboracle.so) -- test infrastructure.
+
+Parses a model directory with the independent Python readers in
+``vosk-api_amd/tools`` (not the product's C++ readers), builds the oracle's
+node program and graph arrays, and runs MFCC / nnet3 forward / token passing
+on the CPU.  Used only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(REPO, "vosk-api_amd", "tools"))
+import kaldi_formats as kf  # noqa: E402
+import np_kaldi as nk  # noqa: E402
+
+LIB_PATH = os.path.join(REPO, "oracle", "build", "liboracle.so")
+
+
+def load_lib():
+    if not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle")])
+    lib = C.CDLL(LIB_PATH)
+    lib.orc_mfcc.restype = C.c_int
+    lib.orc_mfcc_num_frames.restype = C.c_int
+    lib.orc_logf.restype = C.c_float
+    lib.orc_logf.argtypes = [C.c_float]
+    lib.orc_nnet_forward.restype = C.c_int
+    lib.orc_decode.restype = C.c_int
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = load_lib()
+    return _lib
+
+
+class OrcMfccOpts(C.Structure):
+    _fields_ = [("samp_freq", C.c_float), ("frame_shift_ms", C.c_float),
+                ("frame_length_ms", C.c_float), ("preemph_coeff", C.c_float),
+                ("low_freq", C.c_float), ("high_freq", C.c_float),
+                ("cepstral_lifter", C.c_float), ("blackman_coeff", C.c_float),
+                ("num_bins", C.c_int), ("num_ceps", C.c_int), ("use_energy", C.c_int),
+                ("remove_dc_offset", C.c_int), ("window_type", C.c_int),
+                ("round_to_power_of_two", C.c_int)]
+
+
+def mfcc_opts(conf: dict) -> OrcMfccOpts:
+    o = nk.MfccOpts(conf)
+    wt = {"povey": 0, "hamming": 1, "hanning": 2, "rectangular": 3, "blackman": 4}[o.window_type]
+    return OrcMfccOpts(o.samp_freq, o.frame_shift_ms, o.frame_length_ms, o.preemph,
+                       o.low_freq, o.high_freq, o.cepstral_lifter, o.blackman_coeff,
+                       o.num_bins, o.num_ceps, int(o.use_energy), int(o.remove_dc), wt,
+                       int(o.round_pow2))
+
+
+def mfcc(wave, conf: dict) -> np.ndarray:
+    o = mfcc_opts(conf)
+    w = np.ascontiguousarray(wave, np.float32)
+    n = lib().orc_mfcc_num_frames(C.byref(o), C.c_long(len(w)))
+    out = np.zeros((max(n, 0), o.num_ceps), np.float32)
+    if n > 0:
+        lib().orc_mfcc(C.byref(o), w.ctypes.data_as(C.c_void_p), C.c_long(len(w)),
+                       out.ctypes.data_as(C.c_void_p))
+    return out
+
+
+# ----------------------------------------------------------------------------
+# nnet3 program
+# ----------------------------------------------------------------------------
+class OrcNet(C.Structure):
+    _fields_ = [("num_nodes", C.c_int), ("kind", C.c_void_p), ("dim", C.c_void_p),
+                ("in_dim", C.c_void_p), ("w_off", C.c_void_p), ("b_off", C.c_void_p),
+                ("s_off", C.c_void_p), ("o_off", C.c_void_p), ("params", C.c_void_p),
+                ("toff_begin", C.c_void_p), ("toff_count", C.c_void_p), ("toffs", C.c_void_p),
+                ("prog_begin", C.c_void_p), ("prog", C.c_void_p), ("progf", C.c_void_p),
+                ("output_node", C.c_int), ("fss", C.c_int), ("acoustic_scale", C.c_float)]
+
+
+def bn_scale_offset_f32(fields):
+    """Double-precision derivation rounded once (matches the product)."""
+    mean = np.asarray(fields["<StatsMean>"], np.float64)
+    var = np.asarray(fields["<StatsVar>"], np.float64)
+    eps = float(np.float32(fields.get("<Epsilon>", 1e-3)))
+    tr = float(np.float32(fields.get("<TargetRms>", 1.0)))
+    s = tr / np.sqrt(np.maximum(var, 0.0) + eps)
+    return s.astype(np.float32), (-mean * s).astype(np.float32)
+
+
+class OracleNet:
+    """Whole-utterance nnet3 forward on the CPU oracle."""
+
+    AFFINE = {"FixedAffineComponent", "AffineComponent", "NaturalGradientAffineComponent",
+              "LinearComponent", "TdnnComponent"}
+    IDENT = {"NoOpComponent", "GeneralDropoutComponent", "DropoutComponent",
+             "SpecAugmentTimeMaskComponent"}
+
+    def __init__(self, nn: kf.Nnet3, acoustic_scale=1.0, fss=3):
+        g = nk.NnetGraph(nn)
+        self.graph = g
+        comps = {k: (t, dict(f) if isinstance(f, list) else f) for k, (t, f) in nn.components.items()}
+        # topological order from the output
+        order, seen = [], set()
+
+        def deps(d, out):
+            if d[0] == "node":
+                out.append(d[1])
+            elif d[0] in ("append", "sum"):
+                for e in d[1]:
+                    deps(e, out)
+            elif d[0] in ("offset", "replace_index", "round", "ifdefined"):
+                deps(d[1], out)
+            elif d[0] == "scale":
+                deps(d[2], out)
+
+        def topo(n):
+            if n in seen:
+                return
+            seen.add(n)
+            nd = g.nodes[n]
+            ds = []
+            if nd["kind"] in ("component", "output"):
+                deps(nd["input"], ds)
+            if nd["kind"] == "dimrange":
+                ds.append(nd["src"])
+            for x in ds:
+                topo(x)
+            order.append(n)
+
+        topo("output")
+        out_desc = g.nodes["output"]["input"]
+        assert out_desc[0] == "node"
+        # nodes of the program: input first, then component nodes (dim-range
+        # nodes are resolved into column offsets)
+        prog_nodes = ["input"] + [n for n in order if g.nodes[n]["kind"] == "component"]
+        idx = {n: i for i, n in enumerate(prog_nodes)}
+        params = []
+        poff = [0]
+
+        def addp(a):
+            a = np.ascontiguousarray(a, np.float32).ravel()
+            off = poff[0]
+            params.append(a)
+            poff[0] += a.size
+            return off
+
+        kind, dim, in_dim, w_off, b_off, s_off, o_off = [], [], [], [], [], [], []
+        toff_begin, toff_count, toffs = [], [], []
+        prog_begin, prog, progf = [], [], []
+
+        def node_dim(n):
+            nd = g.nodes[n]
+            if nd["kind"] == "input":
+                return nd["dim"]
+            if nd["kind"] == "dimrange":
+                return nd["dim"]
+            t, f = comps[nd["component"]]
+            if "<LinearParams>" in f:
+                return f["<LinearParams>"].shape[0]
+            if "<Params>" in f:
+                return f["<Params>"].shape[0]
+            return f["<Dim>"]
+
+        def desc_dim(d):
+            if d[0] == "node":
+                return node_dim(d[1])
+            if d[0] == "append":
+                return sum(desc_dim(e) for e in d[1])
+            if d[0] == "const":
+                return d[2]
+            if d[0] == "scale":
+                return desc_dim(d[2])
+            return desc_dim(d[1])
+
+        def resolve(n):
+            nd = g.nodes[n]
+            if nd["kind"] == "dimrange":
+                src, col = resolve(nd["src"])
+                return src, col + nd["offset"]
+            return idx[n], 0
+
+        def compile_desc(d, toff, code):
+            k = d[0]
+            if k == "node":
+                ni, col = resolve(d[1])
+                code.append((0, ni, toff, col))
+            elif k == "offset":
+                compile_desc(d[1], toff + d[2], code)
+            elif k == "ifdefined":
+                compile_desc(d[1], toff, code)
+            elif k == "scale":
+                compile_desc(d[2], toff, code)
+                progf.append(d[1])
+                code.append((1, 0, 0, len(progf) - 1))
+            elif k == "sum":
+                compile_desc(d[1][0], toff, code)
+                for e in d[1][1:]:
+                    compile_desc(e, toff, code)
+                    code.append((2, 0, 0, 0))
+            elif k == "const":
+                progf.append(d[1])
+                code.append((3, 0, 0, len(progf) - 1))
+            else:
+                raise ValueError(f"descriptor {k} unsupported by the oracle")
+
+        for n in prog_nodes:
+            if n == "input":
+                kind.append(0); dim.append(g.nodes[n]["dim"]); in_dim.append(0)
+                w_off.append(-1); b_off.append(-1); s_off.append(-1); o_off.append(-1)
+                toff_begin.append(0); toff_count.append(0)
+                prog_begin.append(len(prog)); prog.append(0)
+                continue
+            nd = g.nodes[n]
+            t, f = comps[nd["component"]]
+            d = nd["input"]
+            parts = d[1] if d[0] == "append" else [d]
+            prog_begin.append(len(prog))
+            prog.append(len(parts))
+            for p in parts:
+                code = []
+                compile_desc(p, 0, code)
+                prog.append(desc_dim(p))
+                prog.append(len(code))
+                for c in code:
+                    prog.extend(c)
+            in_dim.append(desc_dim(d))
+            dim.append(node_dim(n))
+            wo = bo = so = oo = -1
+            if t == "TdnnComponent":
+                toff_begin.append(len(toffs)); toff_count.append(len(f["<TimeOffsets>"]))
+                toffs.extend(int(x) for x in f["<TimeOffsets>"])
+            else:
+                toff_begin.append(0); toff_count.append(0)
+            if t in self.AFFINE:
+                kind.append(1)
+                W = f["<LinearParams>"] if "<LinearParams>" in f else f["<Params>"]
+                wo = addp(W)
+                b = f.get("<BiasParams>")
+                if b is not None and len(b):
+                    bo = addp(b)
+            elif t == "RectifiedLinearComponent":
+                kind.append(2)
+            elif t == "BatchNormComponent":
+                kind.append(3)
+                s, o = bn_scale_offset_f32(f)
+                reps = dim[-1] // len(s)
+                so, oo = addp(np.tile(s, reps)), addp(np.tile(o, reps))
+            elif t == "ScaleAndOffsetComponent":
+                kind.append(3)
+                reps = dim[-1] // len(f["<Scales>"])
+                so, oo = addp(np.tile(f["<Scales>"], reps)), addp(np.tile(f["<Offsets>"], reps))
+            elif t in self.IDENT:
+                kind.append(4)
+            else:
+                raise ValueError(f"component {t} unsupported by the oracle")
+            w_off.append(wo); b_off.append(bo); s_off.append(so); o_off.append(oo)
+
+        self.arrays = dict(
+            kind=np.array(kind, np.int32), dim=np.array(dim, np.int32),
+            in_dim=np.array(in_dim, np.int32), w_off=np.array(w_off, np.int64),
+            b_off=np.array(b_off, np.int64), s_off=np.array(s_off, np.int64),
+            o_off=np.array(o_off, np.int64),
+            params=np.concatenate(params) if params else np.zeros(1, np.float32),
+            toff_begin=np.array(toff_begin, np.int32), toff_count=np.array(toff_count, np.int32),
+            toffs=np.array(toffs if toffs else [0], np.int32),
+            prog_begin=np.array(prog_begin, np.int32), prog=np.array(prog, np.int32),
+            progf=np.array(progf if progf else [0.0], np.float32))
+        a = self.arrays
+        self.out_dim = int(dim[idx[out_desc[1]]])
+        self.fss = fss
+        self.net = OrcNet(len(prog_nodes), *(a[k].ctypes.data for k in
+                                              ("kind", "dim", "in_dim", "w_off", "b_off",
+                                               "s_off", "o_off", "params", "toff_begin",
+                                               "toff_count", "toffs", "prog_begin", "prog",
+                                               "progf")),
+                          idx[out_desc[1]], fss, acoustic_scale)
+
+    def forward(self, feats: np.ndarray) -> np.ndarray:
+        feats = np.ascontiguousarray(feats, np.float32)
+        T = feats.shape[0]
+        rows = (T + self.fss - 1) // self.fss
+        out = np.zeros((rows, self.out_dim), np.float32)
+        r = lib().orc_nnet_forward(C.byref(self.net), feats.ctypes.data_as(C.c_void_p),
+                                   C.c_int(T), out.ctypes.data_as(C.c_void_p))
+        assert r == rows, r
+        return out
+
+
+# ----------------------------------------------------------------------------
+# decoder
+# ----------------------------------------------------------------------------
+class OrcGraph(C.Structure):
+    _fields_ = [("num_states", C.c_int), ("start", C.c_int), ("arc_begin", C.c_void_p),
+                ("eps_begin", C.c_void_p), ("ilabel", C.c_void_p), ("olabel", C.c_void_p),
+                ("nextstate", C.c_void_p), ("weight", C.c_void_p), ("final_cost", C.c_void_p),
+                ("tid2pdf", C.c_void_p)]
+
+
+class OrcDecOpts(C.Structure):
+    _fields_ = [("beam", C.c_float), ("beam_delta", C.c_float), ("max_active", C.c_int),
+                ("min_active", C.c_int)]
+
+
+class OrcDecResult(C.Structure):
+    _fields_ = [("ntok", C.c_void_p), ("best", C.c_void_p), ("cutoff", C.c_void_p),
+                ("next_cutoff", C.c_void_p), ("arcs_emit", C.c_void_p), ("path", C.c_void_p),
+                ("path_cap", C.c_int), ("path_len", C.c_int), ("best_cost", C.c_double),
+                ("best_tot", C.c_float), ("end_state", C.c_int),
+                ("final_relative_cost", C.c_float)]
+
+
+class OracleGraph:
+    """CSR graph with per-state emitting arcs first (stable), as the product."""
+
+    def __init__(self, fst: kf.Fst, tid2pdf: np.ndarray):
+        S = fst.num_states
+        src = np.repeat(np.arange(S), np.diff(fst.row))
+        eps = (fst.ilabel == 0).astype(np.int64)
+        order = np.lexsort((np.arange(fst.num_arcs), eps, src))
+        self.ilabel = np.ascontiguousarray(fst.ilabel[order], np.int32)
+        self.olabel = np.ascontiguousarray(fst.olabel[order], np.int32)
+        self.weight = np.ascontiguousarray(fst.weight[order], np.float32)
+        self.nextstate = np.ascontiguousarray(fst.nextstate[order], np.int32)
+        self.arc_begin = np.ascontiguousarray(fst.row, np.int64)
+        n_emit = np.bincount(src, weights=1 - eps, minlength=S).astype(np.int64)
+        self.eps_begin = np.ascontiguousarray(self.arc_begin[:-1] + n_emit, np.int64)
+        self.final = np.ascontiguousarray(fst.final, np.float32)
+        self.tid2pdf = np.ascontiguousarray(tid2pdf, np.int32)
+        self.start = fst.start
+        self.num_states = S
+        self.g = OrcGraph(S, fst.start, self.arc_begin.ctypes.data, self.eps_begin.ctypes.data,
+                          self.ilabel.ctypes.data, self.olabel.ctypes.data,
+                          self.nextstate.ctypes.data, self.weight.ctypes.data,
+                          self.final.ctypes.data, self.tid2pdf.ctypes.data)
+
+    def decode(self, llh: np.ndarray, beam=13.0, max_active=7000, min_active=200,
+               beam_delta=0.5, use_final=True):
+        llh = np.ascontiguousarray(llh, np.float32)
+        F = llh.shape[0]
+        ntok = np.zeros(F + 1, np.int32)
+        best = np.zeros(F + 1, np.float32)
+        cut = np.zeros(max(F, 1), np.float32)
+        ncut = np.zeros(max(F, 1), np.float32)
+        ex = np.zeros(max(F, 1), np.int64)
+        cap = 4 * F + 64
+        path = np.zeros(cap, np.int32)
+        res = OrcDecResult(ntok.ctypes.data, best.ctypes.data, cut.ctypes.data, ncut.ctypes.data,
+                           ex.ctypes.data, path.ctypes.data, cap, 0, 0.0, 0.0, -1, 0.0)
+        o = OrcDecOpts(beam, beam_delta, max_active, min_active)
+        rc = lib().orc_decode(C.byref(self.g), llh.ctypes.data_as(C.c_void_p), C.c_int(F),
+                              C.c_int(llh.shape[1]), C.byref(o), C.c_int(int(use_final)),
+                              C.byref(res))
+        p = path[:res.path_len].copy()
+        words = [int(self.olabel[a]) for a in p if self.olabel[a] != 0]
+        return dict(rc=rc, ntok=ntok, best=best, cutoff=cut[:F], next_cutoff=ncut[:F],
+                    arcs_emit=ex[:F], path=p, words=words, best_cost=res.best_cost,
+                    best_tot=res.best_tot, end_state=res.end_state,
+                    final_relative_cost=res.final_relative_cost)
+
+
+class OracleModel:
+    """All oracle pieces for a model directory (V2 layout)."""
+
+    def __init__(self, model_dir: str):
+        self.dir = model_dir
+        self.mfcc_conf = kf.parse_conf(os.path.join(model_dir, "conf", "mfcc.conf"))
+        self.model_conf = kf.parse_conf(os.path.join(model_dir, "conf", "model.conf"))
+        self.tm, self.nn = kf.read_final_mdl(os.path.join(model_dir, "am", "final.mdl"))
+        self.fst = kf.read_fst(os.path.join(model_dir, "graph", "HCLG.fst"))
+        self.words = kf.read_symbol_table(os.path.join(model_dir, "graph", "words.txt"))
+        mc = self.model_conf
+        self.acoustic_scale = float(mc.get("acoustic-scale", 0.1))
+        self.fss = int(mc.get("frame-subsampling-factor", 1))
+        self.beam = float(mc.get("beam", 16.0))
+        self.max_active = int(mc.get("max-active", 2 ** 31 - 1))
+        self.min_active = int(mc.get("min-active", 200))
+        self.beam_delta = float(mc.get("beam-delta", 0.5))
+        self.net = OracleNet(self.nn, self.acoustic_scale, self.fss)
+        self.graph = OracleGraph(self.fst, self.tm.tid2pdf)
+
+    def features(self, wave):
+        return mfcc(wave, self.mfcc_conf)
+
+    def loglikes(self, wave):
+        return self.net.forward(self.features(wave))
+
+    def decode_llh(self, llh, use_final=True):
+        return self.graph.decode(llh, self.beam, self.max_active, self.min_active,
+                                 self.beam_delta, use_final)
+
+    def recognize(self, wave):
+        r = self.decode_llh(self.loglikes(wave))
+        r["text"] = " ".join(self.words[w] for w in r["words"])
+        return r

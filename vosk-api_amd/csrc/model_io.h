@@ -1,0 +1,177 @@
+// Readers for the on-disk model formats a Vosk model directory uses.
+//
+// Kaldi binary objects (TransitionModel, nnet3 AmNnetSimple), OpenFST
+// const/vector StdArc FSTs, symbol tables and ParseOptions config files.
+// Reference call sites: src/model.cc:180-207 (model.conf), :218-228
+// (mfcc.conf), :233-243 (final.mdl), :278-300 (HCLG.fst, words.txt).
+// The formats themselves are third-party (Kaldi / OpenFST, not vendored in
+// the reference); the restatement is documented in
+// vosk-api_amd/tools/kaldi_formats.py, which writes the same bytes.
+#pragma once
+
+#include <cmath>
+#include <limits>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace vamd {
+
+struct Matrix {
+  int rows = 0, cols = 0;
+  std::vector<float> data;  // row-major
+  const float* row(int r) const { return data.data() + (size_t)r * cols; }
+};
+
+// ---------------------------------------------------------------------------
+// Config-file options (Kaldi ParseOptions syntax: --key=value)
+// ---------------------------------------------------------------------------
+std::map<std::string, std::string> ReadConfigFile(const std::string& path);
+
+struct MfccOptions {
+  float samp_freq = 16000.f, frame_shift_ms = 10.f, frame_length_ms = 25.f;
+  float dither = 1.0f, preemph_coeff = 0.97f;
+  bool remove_dc_offset = true, round_to_power_of_two = true, snip_edges = true;
+  std::string window_type = "povey";
+  float blackman_coeff = 0.42f;
+  int num_bins = 23, num_ceps = 13;
+  bool use_energy = true, raw_energy = true, htk_compat = false;
+  float energy_floor = 0.f, low_freq = 20.f, high_freq = 0.f, cepstral_lifter = 22.f;
+  bool allow_downsample = false, allow_upsample = false;
+  int WindowShift() const { return (int)(samp_freq * 0.001f * frame_shift_ms); }
+  int WindowSize() const { return (int)(samp_freq * 0.001f * frame_length_ms); }
+  int PaddedWindowSize() const {
+    int n = WindowSize();
+    if (!round_to_power_of_two) return n;
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+  }
+  void Apply(const std::map<std::string, std::string>& kv);
+};
+
+struct DecoderOptions {  // LatticeIncrementalDecoderConfig defaults [K]
+  float beam = 16.f, lattice_beam = 10.f, beam_delta = 0.5f, hash_ratio = 2.f;
+  int max_active = std::numeric_limits<int>::max(), min_active = 200, prune_interval = 25;
+};
+
+struct DecodableOptions {  // NnetSimpleLoopedComputationOptions defaults [K]
+  float acoustic_scale = 0.1f;
+  int frame_subsampling_factor = 1, frames_per_chunk = 20, extra_left_context_initial = 0;
+};
+
+struct EndpointRule {
+  bool must_contain_nonsilence;
+  float min_trailing_silence, max_relative_cost, min_utterance_length;
+};
+
+struct EndpointConfig {  // OnlineEndpointConfig defaults [K]
+  std::vector<int> silence_phones;
+  EndpointRule rule[5] = {
+      {false, 5.0f, std::numeric_limits<float>::infinity(), 0.0f},
+      {true, 0.5f, 2.0f, 0.0f},
+      {true, 1.0f, 8.0f, 0.0f},
+      {true, 2.0f, std::numeric_limits<float>::infinity(), 0.0f},
+      {false, 0.0f, std::numeric_limits<float>::infinity(), 20.0f}};
+};
+
+// Applies the option keys registered by src/model.cc:180-186 (decoder,
+// endpoint, decodable option groups) from a parsed config map.
+void ApplyModelOptions(const std::map<std::string, std::string>& kv, DecoderOptions* dec,
+                       DecodableOptions* dcb, EndpointConfig* ep);
+
+// ---------------------------------------------------------------------------
+// Transition model (tables only: tid -> pdf, tid -> phone)
+// ---------------------------------------------------------------------------
+struct TransitionModel {
+  std::vector<int> tid2pdf;    // index 0 unused
+  std::vector<int> tid2phone;  // index 0 unused
+  int num_pdfs = 0;
+  int NumTransitionIds() const { return (int)tid2pdf.size() - 1; }
+};
+
+// ---------------------------------------------------------------------------
+// nnet3
+// ---------------------------------------------------------------------------
+struct Component {
+  std::string type;
+  std::map<std::string, float> f;
+  std::map<std::string, int> i;
+  std::map<std::string, bool> b;
+  std::map<std::string, std::vector<float>> v;
+  std::map<std::string, Matrix> m;
+  std::vector<int> time_offsets;
+};
+
+// Descriptor expression (nnet3 descriptor language).
+struct Desc {
+  enum Kind { NODE, OFFSET, SCALE, SUM, APPEND, REPLACE_INDEX, ROUND, CONST, IFDEFINED } kind;
+  std::string node;
+  int t = 0;          // OFFSET: time offset; REPLACE_INDEX: value; ROUND: modulus
+  float scale = 1.f;  // SCALE / CONST value
+  int dim = 0;        // CONST dim
+  std::vector<Desc> args;
+};
+Desc ParseDescriptor(const std::string& s);
+
+struct NnetNode {
+  enum Kind { INPUT, COMPONENT, DIM_RANGE, OUTPUT } kind;
+  std::string name;
+  int dim = 0;               // INPUT, DIM_RANGE
+  std::string component;     // COMPONENT
+  std::string src;           // DIM_RANGE source node
+  int dim_offset = 0;        // DIM_RANGE
+  Desc input;                // COMPONENT / OUTPUT
+};
+
+struct Nnet {
+  std::vector<NnetNode> nodes;  // in config order
+  std::unordered_map<std::string, int> node_index;
+  std::unordered_map<std::string, Component> components;
+  int left_context = 0, right_context = 0;
+  const NnetNode& Node(const std::string& n) const;
+  bool HasNode(const std::string& n) const { return node_index.count(n) != 0; }
+  int OutputDimOf(const std::string& node) const;  // dim of a node's value
+  int DescDim(const Desc& d) const;
+};
+
+void ReadFinalMdl(const std::string& path, TransitionModel* tm, Nnet* nnet);
+
+// ---------------------------------------------------------------------------
+// Decode graph (StdArc FST) in CSR form, emitting arcs first per state.
+// ---------------------------------------------------------------------------
+struct Graph {
+  int start = 0;
+  std::vector<float> final_cost;  // +inf = not final
+  // per state: arcs [arc_begin[s], eps_begin[s]) have ilabel != 0,
+  // [eps_begin[s], arc_begin[s+1]) have ilabel == 0
+  std::vector<int64_t> arc_begin;
+  std::vector<int64_t> eps_begin;
+  std::vector<int> ilabel, olabel, nextstate;
+  std::vector<float> weight;
+  std::map<int, std::string> osyms;  // from the FST header, if present
+  int NumStates() const { return (int)final_cost.size(); }
+  int64_t NumArcs() const { return (int64_t)ilabel.size(); }
+};
+
+void ReadFstGraph(const std::string& path, Graph* g);
+
+struct SymbolTable {
+  std::unordered_map<int, std::string> id2sym;
+  std::unordered_map<std::string, int> sym2id;
+  std::string Find(int id) const {
+    auto it = id2sym.find(id);
+    return it == id2sym.end() ? std::string() : it->second;
+  }
+  int Find(const std::string& s) const {
+    auto it = sym2id.find(s);
+    return it == sym2id.end() ? -1 : it->second;
+  }
+};
+void ReadSymbolTable(const std::string& path, SymbolTable* t);
+
+bool FileExists(const std::string& path);
+
+}  // namespace vamd

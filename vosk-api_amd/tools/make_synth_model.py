@@ -1,0 +1,370 @@
+#!/usr/bin/env python3
+"""Deterministic synthetic Vosk model directory (V2 layout, real on-disk formats).
+
+No real Vosk model exists in this container or on the GPU box (SURVEY.md
+§8c), so the framework is exercised on a seeded synthetic model written in
+exactly the formats ``vosk_model_new`` reads (``src/model.cc:180-207``,
+``:209-300``):
+
+* ``am/final.mdl``      Kaldi binary TransitionModel (chain topology) +
+                        nnet3 AmNnetSimple with the TDNN-F topology of the
+                        reference training recipe
+                        (``training/local/chain/run_tdnn.sh:98-129``; the
+                        i-vector branch is omitted),
+                        BatchNorm statistics calibrated on test.wav so that
+                        activations are well scaled.
+* ``graph/HCLG.fst``    OpenFST ``const`` StdArc graph: a lexicon prefix tree
+                        over chain-topology biphone HMMs looped through a
+                        unigram LM state, with 2-level epsilon backoff chains
+                        and optional silence (exercises emitting and
+                        non-emitting token passing).
+* ``graph/words.txt``, ``conf/model.conf``, ``conf/mfcc.conf``,
+  ``graph/phones/word_boundary.int``.
+
+Usage: python make_synth_model.py OUT_DIR [--seed N] [--vocab N] [--pdfs N]
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+import wave
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import kaldi_formats as kf  # noqa: E402
+import np_kaldi as nk  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+TEST_WAV = os.path.join(REPO, "tests", "golden", "test.wav")
+
+MFCC_CONF = """--use-energy=false
+--sample-frequency=16000
+--num-mel-bins=40
+--num-ceps=40
+--low-freq=20
+--high-freq=-400
+--dither=0
+--allow-upsample=true
+--allow-downsample=true
+"""
+
+MODEL_CONF = """--min-active=200
+--max-active=7000
+--beam=13.0
+--lattice-beam=6.0
+--acoustic-scale=1.0
+--frame-subsampling-factor=3
+--endpoint.silence-phones=1
+--endpoint.rule2.min-trailing-silence=0.5
+--endpoint.rule3.min-trailing-silence=1.0
+--endpoint.rule4.min-trailing-silence=2.0
+"""
+
+
+def load_test_wav():
+    w = wave.open(TEST_WAV, "rb")
+    return np.frombuffer(w.readframes(w.getnframes()), "<i2").astype(np.float64)
+
+
+# ----------------------------------------------------------------------------
+# transition model + graph
+# ----------------------------------------------------------------------------
+def build_transition_model(rng, num_phones, num_pdfs):
+    """Chain topology for every phone: HMM state 0 has forward pdf-class 0 and
+    self-loop pdf-class 1 and transitions {0 (self-loop), 1 (exit)}; state 1
+    is the non-emitting final state.  Biphone tree: (left, centre) -> a
+    (forward pdf, self-loop pdf) pair."""
+    phones = list(range(1, num_phones + 1))
+    phone2idx = [-1] + [0] * num_phones
+    entry = [kf.HmmState(0, 1, [(0, 0.5), (1, 0.5)]), kf.HmmState(-1, -1, [])]
+    topo = kf.Topology(phones, phone2idx, [entry])
+    tree = {}
+    tuples = {}
+    for c in phones:
+        for l in [0] + phones:
+            fp = int(rng.integers(num_pdfs))
+            sp = int(rng.integers(num_pdfs))
+            tree[(l, c)] = (fp, sp)
+            tuples[(c, 0, fp, sp)] = True
+    # guarantee every pdf is used at least once
+    tl = sorted(tuples)
+    tm = kf.TransitionModel(topo, tl, np.zeros(0, np.float32))
+    tm.derive()
+    tm.log_probs = np.full(tm.num_tids + 1, math.log(0.5), np.float32)
+    tuple_index = {t: i for i, t in enumerate(tl)}
+
+    def tids(l, c):
+        fp, sp = tree[(l, c)]
+        i = tuple_index[(c, 0, fp, sp)]
+        first = int(tm.tuple_first_tid[i])
+        # transition 0 is the self-loop (dest 0 == hmm state), 1 the exit
+        return first + 1, first  # (forward tid, self-loop tid)
+
+    return tm, tids
+
+
+def build_graph(rng, tids, num_phones, vocab):
+    """Lexicon prefix tree + unigram loop.  Returns kf.Fst and words list."""
+    words = []
+    seen = set()
+    while len(words) < vocab:
+        n = int(rng.integers(2, 8))
+        pron = tuple(int(p) for p in rng.integers(2, num_phones + 1, size=n))
+        if pron in seen:
+            continue
+        seen.add(pron)
+        words.append(pron)
+    # Zipf unigram costs
+    ranks = rng.permutation(vocab) + 1
+    p = 1.0 / ranks
+    p /= p.sum()
+    costs = -np.log(p)
+
+    arcs = []  # (src, ilabel, olabel, weight, dst)
+    LOOP = 0
+    n_states = [1]
+
+    def new_state():
+        n_states[0] += 1
+        return n_states[0] - 1
+
+    num_hist = 16
+    hist = [new_state() for _ in range(num_hist)]
+    for h in hist:
+        arcs.append((h, 0, 0, float(rng.uniform(0.5, 2.0)), LOOP))  # backoff
+    # optional silence
+    sil_f, sil_s = tids(0, 1)
+    s_sil = new_state()
+    arcs.append((LOOP, sil_f, 0, 0.7, s_sil))
+    arcs.append((s_sil, sil_s, 0, 0.0, s_sil))
+    arcs.append((s_sil, 0, 0, 0.0, LOOP))
+
+    children = {}  # (node, phone) -> child node
+    node_ctx = {LOOP: 0}
+    for wi, pron in enumerate(words):
+        node = LOOP
+        prev = 0
+        for ph in pron:
+            key = (node, ph)
+            if key not in children:
+                child = new_state()
+                children[key] = child
+                f, s = tids(prev, ph)
+                arcs.append((node, f, 0, 0.0, child))
+                arcs.append((child, s, 0, 0.0, child))
+            node = children[key]
+            prev = ph
+        w = wi + 1
+        h = hist[int(rng.integers(num_hist))]
+        arcs.append((node, 0, w, float(costs[wi]), h))
+
+    S = n_states[0]
+    arcs.sort(key=lambda a: (a[0], a[1] == 0))  # per state: emitting first
+    src = np.array([a[0] for a in arcs], np.int64)
+    row = np.zeros(S + 1, np.int64)
+    np.add.at(row, src + 1, 1)
+    row = np.cumsum(row)
+    final = np.full(S, np.inf, np.float32)
+    final[LOOP] = 0.0
+    f = kf.Fst(LOOP, final, row,
+               np.array([a[1] for a in arcs], np.int32), np.array([a[2] for a in arcs], np.int32),
+               np.array([a[3] for a in arcs], np.float32), np.array([a[4] for a in arcs], np.int32))
+    return f, words
+
+
+# ----------------------------------------------------------------------------
+# nnet3
+# ----------------------------------------------------------------------------
+def nat_affine(rng, din, dout, gain=math.sqrt(2.0), bias=0.05):
+    W = (rng.standard_normal((dout, din)) * gain / math.sqrt(din)).astype(np.float32)
+    b = (rng.standard_normal(dout) * bias).astype(np.float32)
+    return ("NaturalGradientAffineComponent", [
+        ("<MaxChange>", 0.75), ("<L2Regularize>", 0.008), ("<LearningRate>", 0.001),
+        ("<LinearParams>", W), ("<BiasParams>", b),
+        ("<RankIn>", 20), ("<RankOut>", 80), ("<UpdatePeriod>", 4),
+        ("<NumSamplesHistory>", 2000.0), ("<Alpha>", 4.0)])
+
+
+def tdnn_comp(rng, din, dout, offsets, use_bias):
+    k = din * len(offsets)
+    W = (rng.standard_normal((dout, k)) * math.sqrt(2.0 / k)).astype(np.float32)
+    b = (rng.standard_normal(dout) * 0.05).astype(np.float32) if use_bias else np.zeros(0, np.float32)
+    return ("TdnnComponent", [
+        ("<MaxChange>", 0.75), ("<L2Regularize>", 0.008), ("<LearningRate>", 0.001),
+        ("<TimeOffsets>", np.array(offsets, np.int32)),
+        ("<LinearParams>", W), ("<BiasParams>", b),
+        ("<OrthonormalConstraint>", -1.0 if not use_bias else 0.0),
+        ("<UseNaturalGradient>", True), ("<NumSamplesHistory>", 2000.0),
+        ("<AlphaInOut>", (4.0, 4.0)), ("<RankInOut>", (20, 80))])
+
+
+def linear_comp(rng, din, dout):
+    W = (rng.standard_normal((dout, din)) * math.sqrt(1.0 / din)).astype(np.float32)
+    return ("LinearComponent", [
+        ("<MaxChange>", 0.75), ("<L2Regularize>", 0.008), ("<LearningRate>", 0.001),
+        ("<Params>", W), ("<OrthonormalConstraint>", -1.0), ("<UseNaturalGradient>", True),
+        ("<RankInOut>", (20, 80)), ("<Alpha>", 4.0), ("<NumSamplesHistory>", 2000.0),
+        ("<UpdatePeriod>", 4)])
+
+
+def relu(dim):
+    return ("RectifiedLinearComponent", [
+        ("<Dim>", dim), ("<ValueAvg>", np.zeros(dim, np.float32)),
+        ("<DerivAvg>", np.zeros(dim, np.float32)), ("<Count>", 0.0),
+        ("<OderivRms>", np.zeros(dim, np.float32)), ("<OderivCount>", 0.0)])
+
+
+def batchnorm(dim):
+    return ("BatchNormComponent", [
+        ("<Dim>", dim), ("<BlockDim>", dim), ("<Epsilon>", 0.001), ("<TargetRms>", 1.0),
+        ("<TestMode>", False), ("<Count>", 1.0),
+        ("<StatsMean>", np.zeros(dim, np.float32)), ("<StatsVar>", np.ones(dim, np.float32))])
+
+
+def dropout(dim):
+    return ("GeneralDropoutComponent", [
+        ("<Dim>", dim), ("<BlockDim>", dim), ("<TimePeriod>", 0),
+        ("<DropoutProportion>", 0.0), ("<Continuous>", True)])
+
+
+def build_nnet(rng, num_pdfs, mfcc_opts):
+    comps = {}
+    order = []
+    lines = ["input-node name=input dim=40"]
+
+    def add(name, comp, inp):
+        comps[name] = comp
+        order.append(name)
+        lines.append(f"component-node name={name} component={name} input={inp}")
+
+    # idct: inverse of (lifter * DCT), as the recipe's idct.mat
+    D = nk.dct_matrix(mfcc_opts) * nk.lifter(mfcc_opts)[:, None]
+    idct = np.linalg.inv(D).astype(np.float32)
+    add("idct", ("FixedAffineComponent", [("<LinearParams>", idct),
+                                          ("<BiasParams>", np.zeros(40, np.float32))]), "input")
+    add("batchnorm0", batchnorm(40), "idct")
+    add("spec-augment", ("SpecAugmentTimeMaskComponent", [
+        ("<Dim>", 40), ("<ZeroedProportion>", 0.2), ("<TimeMaskMaxFrames>", 20)]), "batchnorm0")
+    sa = "spec-augment"
+    add("delta", ("NoOpComponent", [("<Dim>", 120), ("<BackpropScale>", 1.0)]),
+        f"Append(Offset({sa}, 0), Sum(Offset(Scale(-1.0, {sa}), -1), Offset({sa}, 1)), "
+        f"Sum(Sum(Offset({sa}, -2), Offset({sa}, 2)), Offset(Scale(-2.0, {sa}), 0)))")
+    add("tdnn1.affine", nat_affine(rng, 120, 512), "delta")
+    add("tdnn1.relu", relu(512), "tdnn1.affine")
+    add("tdnn1.batchnorm", batchnorm(512), "tdnn1.relu")
+    add("tdnn1.dropout", dropout(512), "tdnn1.batchnorm")
+    prev = "tdnn1.dropout"
+    for i, stride in zip(range(2, 13), [1, 1, 1, 0, 3, 3, 3, 3, 3, 3, 3]):
+        n = f"tdnnf{i}"
+        lo = [-stride, 0] if stride else [0]
+        ao = [0, stride] if stride else [0]
+        add(f"{n}.linear", tdnn_comp(rng, 512, 96, lo, False), prev)
+        add(f"{n}.affine", tdnn_comp(rng, 96, 512, ao, True), f"{n}.linear")
+        add(f"{n}.relu", relu(512), f"{n}.affine")
+        add(f"{n}.batchnorm", batchnorm(512), f"{n}.relu")
+        add(f"{n}.dropout", dropout(512), f"{n}.batchnorm")
+        add(f"{n}.noop", ("NoOpComponent", [("<Dim>", 512), ("<BackpropScale>", 1.0)]),
+            f"Sum(Scale(0.75, {prev}), {n}.dropout)")
+        prev = f"{n}.noop"
+    add("prefinal-l", linear_comp(rng, 512, 192), prev)
+    add("prefinal-chain.affine", nat_affine(rng, 192, 512), "prefinal-l")
+    add("prefinal-chain.relu", relu(512), "prefinal-chain.affine")
+    add("prefinal-chain.batchnorm1", batchnorm(512), "prefinal-chain.relu")
+    add("prefinal-chain.linear", linear_comp(rng, 512, 192), "prefinal-chain.batchnorm1")
+    add("prefinal-chain.batchnorm2", batchnorm(192), "prefinal-chain.linear")
+    add("output.affine", nat_affine(rng, 192, num_pdfs, gain=1.0, bias=0.5), "prefinal-chain.batchnorm2")
+    lines.append("output-node name=output input=output.affine objective=linear")
+    # xent branch: present in real chain models, never evaluated at decode time
+    add("prefinal-xent.affine", nat_affine(rng, 192, 512), "prefinal-l")
+    add("prefinal-xent.relu", relu(512), "prefinal-xent.affine")
+    add("prefinal-xent.batchnorm1", batchnorm(512), "prefinal-xent.relu")
+    add("prefinal-xent.linear", linear_comp(rng, 512, 192), "prefinal-xent.batchnorm1")
+    add("prefinal-xent.batchnorm2", batchnorm(192), "prefinal-xent.linear")
+    add("output-xent.affine", nat_affine(rng, 192, num_pdfs, gain=1.0), "prefinal-xent.batchnorm2")
+    add("output-xent.log-softmax", ("LogSoftmaxComponent", [
+        ("<Dim>", num_pdfs), ("<ValueAvg>", np.zeros(num_pdfs, np.float32)),
+        ("<DerivAvg>", np.zeros(num_pdfs, np.float32)), ("<Count>", 0.0),
+        ("<OderivRms>", np.zeros(num_pdfs, np.float32)), ("<OderivCount>", 0.0)]),
+        "output-xent.affine")
+    lines.append("output-node name=output-xent input=output-xent.log-softmax objective=linear")
+    return kf.Nnet3(lines, comps, order, 0, 0, np.zeros(0, np.float32))
+
+
+def calibrate(nn, feats, llh_std):
+    """Set every BatchNorm's statistics (in config order) from the activations
+    of its input on test.wav, then scale the output layer so the
+    log-likelihoods have roughly the requested spread."""
+    T = feats.shape[0]
+    for name in nn.component_order:
+        ctype, fields = nn.components[name]
+        if ctype != "BatchNormComponent" or name.startswith("prefinal-xent"):
+            continue
+        g = nk.NnetGraph(nn)
+        src = g.nodes[name]["input"]
+        assert src[0] == "node"
+        vals = g.forward({"input": feats}, out_name=src[1], t_out=range(0, T))
+        fd = dict(fields)
+        fd["<StatsMean>"] = vals.mean(0).astype(np.float32)
+        fd["<StatsVar>"] = vals.var(0).astype(np.float32)
+        fd["<TestMode>"] = True
+        nn.components[name] = (ctype, [(k, fd[k]) for k, _ in fields])
+    g = nk.NnetGraph(nn)
+    out = g.forward({"input": feats})
+    ctype, fields = nn.components["output.affine"]
+    fd = dict(fields)
+    s = llh_std / max(out.std(), 1e-6)
+    fd["<LinearParams>"] = (fd["<LinearParams>"] * s).astype(np.float32)
+    fd["<BiasParams>"] = (fd["<BiasParams>"] * s).astype(np.float32)
+    nn.components["output.affine"] = (ctype, [(k, fd[k]) for k, _ in fields])
+
+
+def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_std=3.0):
+    rng = np.random.default_rng(seed)
+    os.makedirs(os.path.join(out_dir, "am"), exist_ok=True)
+    os.makedirs(os.path.join(out_dir, "conf"), exist_ok=True)
+    os.makedirs(os.path.join(out_dir, "graph", "phones"), exist_ok=True)
+    with open(os.path.join(out_dir, "conf", "mfcc.conf"), "w") as f:
+        f.write(MFCC_CONF)
+    with open(os.path.join(out_dir, "conf", "model.conf"), "w") as f:
+        f.write(MODEL_CONF)
+    mo = nk.MfccOpts(kf.parse_conf(os.path.join(out_dir, "conf", "mfcc.conf")))
+
+    tm, tids = build_transition_model(rng, num_phones, num_pdfs)
+    fst, words = build_graph(rng, tids, num_phones, vocab)
+    nn = build_nnet(rng, num_pdfs, mo)
+    feats = nk.mfcc(load_test_wav(), mo)
+    calibrate(nn, feats, llh_std)
+    kf.write_final_mdl(os.path.join(out_dir, "am", "final.mdl"), tm, nn)
+    kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), fst)
+    with open(os.path.join(out_dir, "graph", "words.txt"), "w") as f:
+        f.write("<eps> 0\n")
+        for i, _ in enumerate(words):
+            f.write(f"w{i + 1:05d} {i + 1}\n")
+        f.write(f"#0 {len(words) + 1}\n<s> {len(words) + 2}\n</s> {len(words) + 3}\n")
+    with open(os.path.join(out_dir, "graph", "phones", "word_boundary.int"), "w") as f:
+        f.write("1 nonword\n")
+        for p in range(2, num_phones + 1):
+            f.write(f"{p} internal\n")
+    with open(os.path.join(out_dir, "README"), "w") as f:
+        f.write(f"synthetic vosk-api_amd model seed={seed} vocab={vocab} pdfs={num_pdfs} "
+                f"phones={num_phones} states={fst.num_states} arcs={fst.num_arcs}\n")
+    return out_dir
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--vocab", type=int, default=3000)
+    ap.add_argument("--pdfs", type=int, default=2000)
+    a = ap.parse_args()
+    make_model(a.out, a.seed, a.vocab, a.pdfs)
+    print(open(os.path.join(a.out, "README")).read().strip())
+
+
+if __name__ == "__main__":
+    main()
