@@ -1,0 +1,64 @@
+/* vosk_amd_engine.h -- diagnostic C ABI of libvosk.so's GPU engine.
+ *
+ * Not part of the reference interface.  These entry points expose the
+ * engine's stages (MFCC, looped nnet3, token passing, traceback) with plain
+ * pointers so that kernel-level parity tests and the benchmark can drive the
+ * same code path the vosk_* API uses (Model -> Engine, src/recognizer.cc:
+ * 297-323 equivalent) and compare it with the CPU oracle.  All functions
+ * return < 0 (or NULL) on error; vamd_last_error() returns the message.
+ */
+#ifndef VOSK_AMD_ENGINE_H
+#define VOSK_AMD_ENGINE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct VamdEngine VamdEngine;
+
+/* host-only (no GPU needed): nnet plan of a model directory */
+const char *vamd_plan_describe(const char *model_dir, int frames_per_chunk);
+/* [fpc, fss, left_ctx, right_ctx, priming, out_dim, ops, stored nodes] */
+int vamd_plan_info(const char *model_dir, int frames_per_chunk, int *out8, double *flops_per_chunk);
+
+const char *vamd_last_error(void);
+int vamd_device_count(void);
+
+/* frames_per_chunk <= 0 uses the model's decodable option (default 20->21);
+ * flags: 1 = collect per-frame decoder stats, 2 = keep decoded LLH rows. */
+VamdEngine *vamd_engine_new(const char *model_dir, int frames_per_chunk, int max_streams,
+                            int flags);
+void vamd_engine_free(VamdEngine *e);
+/* human-readable nnet plan / engine description (owned by the engine) */
+const char *vamd_engine_describe(VamdEngine *e);
+/* plan facts: [fpc, fss, left_ctx, right_ctx, priming, out_dim, ops, ring] */
+int vamd_engine_info(VamdEngine *e, int *out8, double *flops_per_chunk);
+
+int vamd_stream_new(VamdEngine *e);
+int vamd_stream_free(VamdEngine *e, int stream);
+int vamd_stream_reset(VamdEngine *e, int stream, int pipeline);
+/* queue samples (int16-range floats); finished=1 marks end of input */
+int vamd_stream_accept(VamdEngine *e, int stream, const float *samples, int n, int finished);
+/* run batched engine steps over the listed streams until no work remains */
+int vamd_engine_advance(VamdEngine *e, const int *streams, int n);
+int vamd_stream_frames_decoded(VamdEngine *e, int stream);
+int vamd_stream_error(VamdEngine *e, int stream);
+/* feature rows [first, first+n) from the device ring, n*dim floats */
+int vamd_stream_features(VamdEngine *e, int stream, int first, int n, float *out);
+/* decoded log-likelihood rows (flag 2): copies up to cap floats, returns count */
+long long vamd_stream_llh(VamdEngine *e, int stream, float *out, long long cap);
+/* per-frame stats of the last advance (flag 1): 8 floats per frame
+ * {ntok_in, ntok_out, arcs_emit, arcs_eps, best, cutoff, next_cutoff, adaptive_beam} */
+int vamd_stream_stats(VamdEngine *e, int stream, float *out, int cap_frames);
+/* decode externally supplied log-likelihoods [nframes][out_dim] */
+int vamd_stream_decode_llh(VamdEngine *e, int stream, const float *llh, int nframes, int reset);
+/* best path: arc indices into the graph (emitting-first CSR order) */
+int vamd_stream_best_path(VamdEngine *e, int stream, int use_final, int *arcs, int cap,
+                          double *cost, float *final_relative_cost);
+/* engine counters: [steps, launches, mfcc frames, chunk jobs, frames decoded] */
+int vamd_engine_counters(VamdEngine *e, long long *out5);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

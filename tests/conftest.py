@@ -1,0 +1,82 @@
+import os
+import shutil
+import sys
+import wave
+
+import numpy as np
+import pytest
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+PKG = os.path.join(REPO, "vosk-api_amd")
+for p in (PKG, os.path.join(PKG, "tools"), os.path.join(REPO, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+MODEL_CACHE = os.environ.get("VAMD_MODEL_CACHE", os.path.join(
+    os.environ.get("TMPDIR", "/tmp"), "vamd_models"))
+SYNTH_VERSION = "v1"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+
+
+def _make(name, **kw):
+    import make_synth_model as msm
+    path = os.path.join(MODEL_CACHE, f"{name}_{SYNTH_VERSION}")
+    if not os.path.exists(os.path.join(path, "README")):
+        tmp = path + f".tmp{os.getpid()}"
+        shutil.rmtree(tmp, ignore_errors=True)
+        msm.make_model(tmp, **kw)
+        shutil.rmtree(path, ignore_errors=True)
+        os.rename(tmp, path)
+    return path
+
+
+@pytest.fixture(scope="session")
+def synth_model():
+    """Seeded synthetic model in the real Kaldi/OpenFST on-disk formats."""
+    return _make("synth", seed=7, vocab=3000, num_pdfs=2000)
+
+
+@pytest.fixture(scope="session")
+def synth_model_noep(synth_model):
+    """Same model with endpointing disabled (single segment per stream)."""
+    path = os.path.join(MODEL_CACHE, f"synth_noep_{SYNTH_VERSION}")
+    if not os.path.exists(os.path.join(path, "README")):
+        tmp = path + f".tmp{os.getpid()}"
+        shutil.rmtree(tmp, ignore_errors=True)
+        shutil.copytree(synth_model, tmp)
+        with open(os.path.join(tmp, "conf", "model.conf"), "a") as f:
+            for r in range(1, 6):
+                f.write(f"--endpoint.rule{r}.min-utterance-length=1e9\n")
+        shutil.rmtree(path, ignore_errors=True)
+        os.rename(tmp, path)
+    return path
+
+
+@pytest.fixture(scope="session")
+def test_wave():
+    w = wave.open(os.path.join(REPO, "tests", "golden", "test.wav"), "rb")
+    return np.frombuffer(w.readframes(w.getnframes()), "<i2").astype(np.float32)
+
+
+def perturbed_stream(base, i, seconds=None, sr=16000):
+    """Synthetic stream i (BASELINE.md workload): test.wav tiled, circularly
+    shifted by (i*7919) mod len, gain U[0.5,1.5], N(0,10 LSB) noise."""
+    rng = np.random.default_rng(1234 + i)
+    n = len(base) if seconds is None else int(seconds * sr)
+    reps = int(np.ceil(n / len(base))) + 1
+    x = np.tile(base, reps)
+    sh = (i * 7919) % len(base)
+    x = x[sh:sh + n].astype(np.float64)
+    x = x * rng.uniform(0.5, 1.5) + rng.normal(0.0, 10.0, n)
+    return np.clip(np.round(x), -32768, 32767).astype(np.float32)
+
+
+def has_gpu():
+    try:
+        from vosk import engine
+        return engine.device_count() > 0
+    except Exception:
+        return False

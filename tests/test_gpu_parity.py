@@ -1,0 +1,152 @@
+"""GPU parity: HIP kernels (through libvosk.so's engine ABI) vs the CPU oracle.
+
+Bit-exact contract (see oracle/oracle.h): MFCC features, nnet3
+log-likelihoods, per-frame decoder statistics and the best path are compared
+with exact equality; path costs are compared exactly as well.
+"""
+import numpy as np
+import pytest
+
+from conftest import perturbed_stream
+import oracle_py
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def oracle(synth_model):
+    return oracle_py.OracleModel(synth_model)
+
+
+def _engine(model, fpc=0, streams=8, stats=True, llh=True):
+    from vosk import engine
+    return engine.Engine(model, frames_per_chunk=fpc, max_streams=streams, stats=stats,
+                         keep_llh=llh)
+
+
+def _feed(e, s, wave, chunk=3200, finish=True):
+    for i in range(0, len(wave), chunk):
+        e.accept(s, wave[i:i + chunk])
+        e.advance([s])
+    if finish:
+        e.accept(s, np.zeros(0, np.float32), finished=True)
+        e.advance([s])
+
+
+def test_mfcc_bit_exact(synth_model, oracle, test_wave):
+    e = _engine(synth_model)
+    s = e.new_stream()
+    e.accept(s, test_wave[:16000 * 2])
+    e.advance([s])
+    ref = oracle.features(test_wave[:16000 * 2])
+    n = ref.shape[0]
+    got = e.features(s, 0, min(n, 64), ref.shape[1])
+    np.testing.assert_array_equal(got, ref[:got.shape[0]])
+    got2 = e.features(s, n - 64, 64, ref.shape[1])
+    np.testing.assert_array_equal(got2, ref[n - 64:])
+
+
+@pytest.mark.parametrize("fpc", [51, 21])
+def test_llh_bit_exact(synth_model, oracle, test_wave, fpc):
+    e = _engine(synth_model, fpc=fpc)
+    s = e.new_stream()
+    _feed(e, s, test_wave)
+    llh = e.llh(s)
+    ref = oracle.loglikes(test_wave)
+    assert llh.shape == ref.shape, (llh.shape, ref.shape)
+    np.testing.assert_array_equal(llh, ref)
+
+
+def test_decoder_from_oracle_llh(synth_model, oracle, test_wave):
+    ref_llh = oracle.loglikes(test_wave)
+    r = oracle.decode_llh(ref_llh)
+    e = _engine(synth_model)
+    s = e.new_stream()
+    e.decode_llh(s, ref_llh, reset=True)
+    st = e.stats(s)
+    assert st.shape[0] == ref_llh.shape[0]
+    np.testing.assert_array_equal(st[:, 1].astype(int), r["ntok"][1:])
+    np.testing.assert_array_equal(st[:, 4], r["best"][1:])
+    np.testing.assert_array_equal(st[:, 5], r["cutoff"])
+    np.testing.assert_array_equal(st[:, 6], r["next_cutoff"])
+    arcs, cost, frel = e.best_path(s, use_final=True)
+    np.testing.assert_array_equal(arcs, r["path"])
+    assert cost == pytest.approx(r["best_cost"], abs=1e-6)
+
+
+def test_end_to_end_single_stream(synth_model, oracle, test_wave):
+    e = _engine(synth_model)
+    s = e.new_stream()
+    _feed(e, s, test_wave)
+    r = oracle.recognize(test_wave)
+    arcs, cost, _ = e.best_path(s, use_final=True)
+    np.testing.assert_array_equal(arcs, r["path"])
+    assert e.frames_decoded(s) == len(r["ntok"]) - 1
+    assert e.error(s) == 0
+
+
+def test_batched_streams_match_oracle(synth_model, oracle, test_wave):
+    """Eight different streams advanced together in the same batched steps."""
+    n = 8
+    e = _engine(synth_model, fpc=51, streams=n, stats=False, llh=False)
+    waves = [perturbed_stream(test_wave, i, seconds=3.0 + 0.37 * i) for i in range(n)]
+    ss = [e.new_stream() for _ in range(n)]
+    chunk = 8000
+    pos = [0] * n
+    while any(p < len(w) for p, w in zip(pos, waves)):
+        for k in range(n):
+            if pos[k] < len(waves[k]):
+                e.accept(ss[k], waves[k][pos[k]:pos[k] + chunk])
+                pos[k] += chunk
+        e.advance(ss)
+    for k in range(n):
+        e.accept(ss[k], np.zeros(0, np.float32), finished=True)
+    e.advance(ss)
+    for k in range(n):
+        r = oracle.recognize(waves[k])
+        arcs, _, _ = e.best_path(ss[k], use_final=True)
+        np.testing.assert_array_equal(arcs, r["path"], err_msg=f"stream {k}")
+
+
+@pytest.mark.parametrize("nsamples", [0, 100, 399, 400, 1000, 16000])
+def test_short_inputs(synth_model, oracle, test_wave, nsamples):
+    e = _engine(synth_model)
+    s = e.new_stream()
+    w = test_wave[:nsamples]
+    _feed(e, s, w)
+    nf = oracle.features(w).shape[0] if nsamples else 0
+    expect_frames = (nf + 2) // 3
+    assert e.frames_decoded(s) == expect_frames
+    if expect_frames:
+        r = oracle.recognize(w)
+        arcs, _, _ = e.best_path(s, use_final=True)
+        np.testing.assert_array_equal(arcs, r["path"])
+
+
+def test_decoder_reset_continues_frames(synth_model, oracle, test_wave):
+    """InitDecoding mid-stream: the nnet continues, the decoder restarts."""
+    e = _engine(synth_model)
+    s = e.new_stream()
+    half = len(test_wave) // 2
+    _feed(e, s, test_wave[:half], finish=False)
+    f1 = e.frames_decoded(s)
+    e.reset(s, pipeline=False)
+    _feed(e, s, test_wave[half:])
+    llh = e.llh(s)
+    ref = oracle.loglikes(test_wave)
+    np.testing.assert_array_equal(llh, ref)
+    r = oracle.decode_llh(ref[f1:])
+    arcs, _, _ = e.best_path(s, use_final=True)
+    np.testing.assert_array_equal(arcs, r["path"])
+
+
+def test_pipeline_reset_restarts(synth_model, oracle, test_wave):
+    e = _engine(synth_model)
+    s = e.new_stream()
+    _feed(e, s, test_wave[:20000])
+    e.reset(s, pipeline=True)
+    w = test_wave[30000:70000]
+    _feed(e, s, w)
+    r = oracle.recognize(w)
+    arcs, _, _ = e.best_path(s, use_final=True)
+    np.testing.assert_array_equal(arcs, r["path"])

@@ -28,6 +28,13 @@ struct Fatal : std::runtime_error {
       ::vamd::LogMessage("LOG", _os.str());                        \
     }                                                              \
   } while (0)
+#define VAMD_LOG_VERBOSE(msg)                                      \
+  do {                                                             \
+    if (::vamd::LogLevel() > 0) {                                  \
+      std::ostringstream _os; _os << msg;                          \
+      ::vamd::LogMessage("VLOG[1]", _os.str());                    \
+    }                                                              \
+  } while (0)
 #define VAMD_WARN(msg)                                             \
   do {                                                             \
     if (::vamd::LogLevel() >= -1) {                                \

@@ -1,0 +1,717 @@
+// GPU engine (see engine.h).
+#include "engine.h"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+
+#include "common.h"
+#include "kernels.h"
+
+#define HIPCHECK(x)                                                                  \
+  do {                                                                               \
+    hipError_t _e = (x);                                                             \
+    if (_e != hipSuccess) VAMD_ERR("HIP error " << hipGetErrorString(_e) << " at " \
+                                                << __FILE__ << ":" << __LINE__);     \
+  } while (0)
+
+namespace vamd {
+
+namespace {
+int Pow2AtLeast(long long n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+size_t Align256(size_t x) { return (x + 255) & ~(size_t)255; }
+float MelScale(float f) { return 1127.0f * logf(1.0f + f / 700.0f); }
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// model directory loading (src/model.cc:106-341, src/batch_model.cc:23-54)
+// ---------------------------------------------------------------------------
+void ModelData::Load(const std::string& path) {
+  dir = path;
+  std::string mdl, hclg, words_txt, wb, mfcc_conf, conf_file;
+  if (FileExists(path + "/am/final.mdl") && FileExists(path + "/conf/model.conf")) {
+    // V2 layout (src/model.cc:180-207)
+    ApplyModelOptions(ReadConfigFile(path + "/conf/model.conf"), &dec, &dcb, &endpoint);
+    mdl = path + "/am/final.mdl";
+    hclg = path + "/graph/HCLG.fst";
+    words_txt = path + "/graph/words.txt";
+    wb = path + "/graph/phones/word_boundary.int";
+    mfcc_conf = path + "/conf/mfcc.conf";
+  } else if (FileExists(path + "/final.mdl") && FileExists(path + "/mfcc.conf")) {
+    // V1 layout: hard-coded options (src/model.cc:132-158)
+    std::map<std::string, std::string> kv = {
+        {"max-active", "7000"}, {"beam", "13.0"}, {"lattice-beam", "6.0"},
+        {"acoustic-scale", "1.0"}, {"frame-subsampling-factor", "3"},
+        {"endpoint.silence-phones", "1:2:3:4:5:6:7:8:9:10"},
+        {"endpoint.rule2.min-trailing-silence", "0.5"},
+        {"endpoint.rule3.min-trailing-silence", "1.0"},
+        {"endpoint.rule4.min-trailing-silence", "2.0"}};
+    ApplyModelOptions(kv, &dec, &dcb, &endpoint);
+    mdl = path + "/final.mdl";
+    hclg = path + "/HCLG.fst";
+    words_txt = path + "/words.txt";
+    wb = path + "/word_boundary.int";
+    mfcc_conf = path + "/mfcc.conf";
+  } else {
+    VAMD_ERR("Folder '" << path << "' does not contain model files. Make sure you specified "
+                           "the model path properly in Model constructor.");
+  }
+  VAMD_LOG("Decoding params beam=" << dec.beam << " max-active=" << dec.max_active
+                                   << " lattice-beam=" << dec.lattice_beam);
+  if (!FileExists(mfcc_conf)) VAMD_ERR("Failed to find feature config file (only MFCC front-ends are supported)");
+  mfcc.Apply(ReadConfigFile(mfcc_conf));
+  mfcc.allow_downsample = true;
+  ReadFinalMdl(mdl, &tm, &nnet);
+  std::string ivec = path + "/ivector/final.ie";
+  if (FileExists(ivec))
+    VAMD_WARN("i-vector extractor present but not supported yet; the nnet 'ivector' input "
+              "must be absent (see DESIGN.md next rows)");
+  if (FileExists(path + "/am/global_cmvn.stats") || FileExists(path + "/conf/pitch.conf"))
+    VAMD_ERR("global CMVN / pitch front-ends are not supported yet");
+  if (!FileExists(hclg))
+    VAMD_ERR("no static " << hclg << " (lookahead HCLr.fst+Gr.fst graphs need the host expansion "
+                                     "of SURVEY.md 8f-2, not implemented yet)");
+  VAMD_LOG("Loading HCLG from " << hclg);
+  ReadFstGraph(hclg, &graph);
+  if (!graph.osyms.empty()) {
+    for (auto& [id, sym] : graph.osyms) { words.id2sym[id] = sym; words.sym2id[sym] = id; }
+  } else {
+    VAMD_LOG("Loading words from " << words_txt);
+    ReadSymbolTable(words_txt, &words);
+  }
+  has_word_boundary = FileExists(wb);
+  int max_phone = 0;
+  for (int p : tm.tid2phone) max_phone = std::max(max_phone, p);
+  phone_is_silence.assign(max_phone + 1, 0);
+  for (int p : endpoint.silence_phones)
+    if (p >= 0 && p <= max_phone) phone_is_silence[p] = 1;
+}
+
+void ModelData::LoadBatchLayout(const std::string& path) {
+  // src/batch_model.cc:26-54 reads model/conf/model.conf, model/am/final.mdl,
+  // model/graph/HCLG.fst, model/graph/words.txt with batch overrides (:69-88).
+  Load(path);
+  dec.max_active = 7000;
+  dec.beam = 13.0f;
+  dec.lattice_beam = 6.0f;
+  dcb.acoustic_scale = 1.0f;
+  dcb.frame_subsampling_factor = 3;
+}
+
+// ---------------------------------------------------------------------------
+void* Engine::DevAlloc(size_t bytes) {
+  void* p = nullptr;
+  HIPCHECK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+  dev_allocs_.push_back(p);
+  return p;
+}
+
+template <class T>
+T* Engine::Upload(const std::vector<T>& v) {
+  T* d = (T*)DevAlloc(sizeof(T) * v.size());
+  if (!v.empty()) HIPCHECK(hipMemcpy(d, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+  return d;
+}
+
+int Engine::NumFramesFor(long long samples) const {
+  const int L = md_->mfcc.WindowSize(), S = md_->mfcc.WindowShift();
+  if (samples < L) return 0;
+  return (int)(1 + (samples - L) / S);
+}
+
+Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : md_(md), cfg_(cfg) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    VAMD_ERR("no HIP device available: the MI355X engine requires a GPU (there is no CPU fallback)");
+  HIPCHECK(hipSetDevice(cfg_.device));
+  HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  const ModelData& m = *md_;
+  const int fss = m.dcb.frame_subsampling_factor;
+  int fpc = cfg_.frames_per_chunk;
+  if (fpc % fss) fpc += fss - fpc % fss;  // GetChunkSize rounding [K]
+  cfg_.frames_per_chunk = fpc;
+  plan_ = BuildNnetPlan(m.nnet, fpc, fss, m.dcb.acoustic_scale);
+  if (LogLevel() > 0) VAMD_LOG(plan_.Describe());
+  for (int pdf : m.tm.tid2pdf)
+    if (pdf >= plan_.out_dim) VAMD_ERR("transition model pdf " << pdf << " >= nnet output dim");
+
+  // ---- MFCC tables (float arithmetic as Kaldi MelBanks / FeatureWindowFunction)
+  const MfccOptions& o = m.mfcc;
+  if (o.dither != 0.0f)
+    VAMD_WARN("dither=" << o.dither << " ignored: the pipeline is deterministic (dither 0)");
+  if (o.htk_compat || !o.snip_edges) VAMD_ERR("htk-compat / snip-edges=false are not supported");
+  const int L = o.WindowSize(), N = o.PaddedWindowSize();
+  if (N > 512 || (N & (N - 1))) VAMD_ERR("FFT size " << N << " unsupported (power of two <= 512)");
+  if (o.num_bins > 64 || o.num_ceps > 64) VAMD_ERR("num-mel-bins / num-ceps must be <= 64");
+  if (plan_.input_dim != o.num_ceps)
+    VAMD_ERR("nnet input dim " << plan_.input_dim << " != num-ceps " << o.num_ceps);
+  {
+    std::vector<float> win(L);
+    double a = 2.0 * M_PI / (L - 1);
+    for (int i = 0; i < L; i++) {
+      double c = cos(a * i), w;
+      if (o.window_type == "povey") w = pow(0.5 - 0.5 * c, 0.85);
+      else if (o.window_type == "hamming") w = 0.54 - 0.46 * c;
+      else if (o.window_type == "hanning") w = 0.5 - 0.5 * c;
+      else if (o.window_type == "rectangular") w = 1.0;
+      else if (o.window_type == "blackman")
+        w = o.blackman_coeff - 0.5 * c + (0.5 - o.blackman_coeff) * cos(2 * a * i);
+      else VAMD_ERR("unsupported window type " << o.window_type);
+      win[i] = (float)w;
+    }
+    const int nfft = N / 2, nb = o.num_bins, nc = o.num_ceps;
+    std::vector<float> melw((size_t)nb * nfft, 0.0f);
+    std::vector<int> first(nb, -1), last(nb, -1);
+    float nyq = 0.5f * o.samp_freq;
+    float hi = o.high_freq > 0.0f ? o.high_freq : nyq + o.high_freq;
+    float width = o.samp_freq / (float)N;
+    float ml = MelScale(o.low_freq), mh = MelScale(hi);
+    float delta = (mh - ml) / (float)(nb + 1);
+    for (int b = 0; b < nb; b++) {
+      float left = ml + (float)b * delta, center = ml + (float)(b + 1) * delta,
+            right = ml + (float)(b + 2) * delta;
+      for (int i = 0; i < nfft; i++) {
+        float mel = MelScale(width * (float)i);
+        if (mel > left && mel < right) {
+          float w = mel <= center ? (mel - left) / (center - left) : (right - mel) / (right - center);
+          melw[(size_t)b * nfft + i] = w;
+          if (first[b] < 0) first[b] = i;
+          last[b] = i;
+        }
+      }
+    }
+    std::vector<float> dct((size_t)nc * nb);
+    float norm0 = (float)sqrt(1.0 / (double)nb), norm = (float)sqrt(2.0 / (double)nb);
+    for (int j = 0; j < nb; j++) dct[j] = norm0;
+    for (int k = 1; k < nc; k++)
+      for (int j = 0; j < nb; j++) dct[(size_t)k * nb + j] = (float)((double)norm * cos(M_PI / nb * (j + 0.5) * k));
+    std::vector<float> lift(nc);
+    for (int i = 0; i < nc; i++) {
+      double q = o.cepstral_lifter;
+      lift[i] = q != 0.0 ? (float)(1.0 + 0.5 * q * sin(M_PI * i / q)) : 1.0f;
+    }
+    std::vector<float> twr(N / 2), twi(N / 2);
+    for (int k = 0; k < N / 2; k++) {
+      twr[k] = (float)cos(2.0 * M_PI * k / N);
+      twi[k] = (float)(-sin(2.0 * M_PI * k / N));
+    }
+    int log2n = 0;
+    while ((1 << log2n) < N) log2n++;
+    mfcc_.frame_length = L;
+    mfcc_.frame_shift = o.WindowShift();
+    mfcc_.padded = N;
+    mfcc_.log2n = log2n;
+    mfcc_.num_bins = nb;
+    mfcc_.num_ceps = nc;
+    mfcc_.nfft = nfft;
+    mfcc_.use_energy = o.use_energy ? 1 : 0;
+    mfcc_.remove_dc = o.remove_dc_offset ? 1 : 0;
+    mfcc_.preemph = o.preemph_coeff;
+    mfcc_.window = Upload(win);
+    mfcc_.melw = Upload(melw);
+    mfcc_.mel_first = Upload(first);
+    mfcc_.mel_last = Upload(last);
+    mfcc_.dct = Upload(dct);
+    mfcc_.lifter = Upload(lift);
+    mfcc_.twr = Upload(twr);
+    mfcc_.twi = Upload(twi);
+  }
+
+  // ---- rings
+  jobs_per_slot_ = plan_.priming_chunks + 2;
+  const int step_frames = cfg_.max_step_samples / o.WindowShift() + 2;
+  ring_ = std::max(512, plan_.RingFrames(jobs_per_slot_));
+  ring_ = std::max(ring_, Pow2AtLeast((long long)jobs_per_slot_ * fpc + plan_.left_context +
+                                      plan_.right_context + step_frames + fpc + 16));
+  sample_ring_ = Pow2AtLeast((long long)cfg_.max_step_samples + 2 * L + o.WindowShift() + 64);
+  const int S = cfg_.max_slots;
+  std::vector<float*> ring_ptrs(plan_.nodes.size());
+  std::vector<int> ring_dims(plan_.nodes.size());
+  for (size_t i = 0; i < plan_.nodes.size(); i++) {
+    size_t bytes = sizeof(float) * (size_t)S * ring_ * plan_.nodes[i].dim;
+    ring_ptrs[i] = (float*)DevAlloc(bytes);
+    HIPCHECK(hipMemset(ring_ptrs[i], 0, bytes));
+    ring_dims[i] = plan_.nodes[i].dim;
+  }
+  d_ring_ptrs_ = Upload(ring_ptrs);
+  d_ring_dims_ = Upload(ring_dims);
+  rings_.base = d_ring_ptrs_;
+  rings_.dim = d_ring_dims_;
+  rings_.mask = ring_ - 1;
+  rings_.ring = ring_;
+  rings_.input_node = plan_.input_node;
+  d_samples_ = (float*)DevAlloc(sizeof(float) * (size_t)S * sample_ring_);
+
+  // ---- nnet ops
+  std::vector<float*> vec_ptrs;
+  for (auto& v : plan_.vecs) vec_ptrs.push_back(Upload(v));
+  const float* const* d_vecs = Upload(vec_ptrs);
+  for (auto& op : plan_.ops) {
+    NnetOpArgs a;
+    memset(&a, 0, sizeof(a));
+    a.N = op.N;
+    a.K = op.K;
+    a.P = (int)op.pattern.size();
+    a.pattern = Upload(op.pattern);
+    a.rings = rings_;
+    a.vecs = d_vecs;
+    a.out_node = op.out_node;
+    int bk = 32;
+    if (op.kind == Op::GEMM) {
+      a.W = Upload(plan_.mats[op.weight].data);
+      if ((int)op.segs.size() > kMaxSegs) VAMD_ERR("too many input segments in op " << op.name);
+      a.nsegs = (int)op.segs.size();
+      for (size_t i = 0; i < op.segs.size(); i++) {
+        const ASegment& s = op.segs[i];
+        a.segs[i] = DevSeg{s.node, s.offset, s.col0, s.dim, s.src_col};
+        if (s.dim % 4 || s.src_col % 4 || plan_.nodes[s.node].dim % 4)
+          VAMD_ERR("op " << op.name << ": segment dims must be multiples of 4");
+        while (bk > 8 && (s.col0 % bk || s.dim % bk)) bk >>= 1;
+        if (s.col0 % bk || s.dim % bk) VAMD_ERR("op " << op.name << ": K segments must be multiples of 8");
+      }
+      if (op.K % 4) VAMD_ERR("op " << op.name << ": K must be a multiple of 4");
+    } else {
+      a.nparts = (int)op.parts.size();
+      if (a.nparts > kMaxParts) VAMD_ERR("too many descriptor parts in op " << op.name);
+      int ni = 0;
+      for (size_t i = 0; i < op.parts.size(); i++) {
+        const GPart& gp = op.parts[i];
+        a.parts[i] = DevPart{gp.col0, gp.dim, ni, (int)gp.prog.size()};
+        for (auto& g : gp.prog) {
+          if (ni >= kMaxInstr) VAMD_ERR("descriptor program too long in op " << op.name);
+          a.instr[ni++] = DevInstr{g.op, g.node, g.offset, g.src_col, g.c};
+        }
+      }
+    }
+    if ((int)op.epi.size() > kMaxStages) VAMD_ERR("too many fused stages in op " << op.name);
+    a.nstages = (int)op.epi.size();
+    for (size_t i = 0; i < op.epi.size(); i++) {
+      const EpiStage& e = op.epi[i];
+      a.stages[i] = DevStage{e.kind, e.vec0, e.vec1, e.node, e.offset, e.src_col, e.scaled ? 1 : 0, e.c};
+    }
+    op_args_.push_back(a);
+    op_bk_.push_back(bk);
+  }
+
+  // ---- graph: per state {arc_begin, eps_begin, arc_end, final bits}; per arc
+  // {nextstate, weight bits, pdf (-1 for epsilon), ilabel}
+  const Graph& g = m.graph;
+  if (g.NumArcs() >= INT_MAX) VAMD_ERR("graph too large for 32-bit arc indices");
+  {
+    std::vector<int4> sinfo(g.NumStates());
+    for (int s = 0; s < g.NumStates(); s++) {
+      float fc = g.final_cost[s];
+      int fb;
+      memcpy(&fb, &fc, 4);
+      sinfo[s] = make_int4((int)g.arc_begin[s], (int)g.eps_begin[s], (int)g.arc_begin[s + 1], fb);
+    }
+    std::vector<int4> arcs(g.NumArcs());
+    std::vector<int> src(g.NumArcs());
+    for (int s = 0; s < g.NumStates(); s++)
+      for (int64_t a = g.arc_begin[s]; a < g.arc_begin[s + 1]; a++) {
+        int wb;
+        memcpy(&wb, &g.weight[a], 4);
+        int il = g.ilabel[a];
+        int pdf = -1;
+        if (il != 0) {
+          if (il <= 0 || il >= (int)m.tm.tid2pdf.size()) VAMD_ERR("graph ilabel " << il << " is not a transition id");
+          pdf = m.tm.tid2pdf[il];
+        }
+        arcs[a] = make_int4(g.nextstate[a], wb, pdf, il);
+        src[a] = s;
+      }
+    d_sinfo_ = Upload(sinfo);
+    d_arcs_ = Upload(arcs);
+    d_arc_src_ = Upload(src);
+  }
+
+  // ---- decoder state
+  const long long NS = g.NumStates();
+  max_jobs_ = S * jobs_per_slot_;
+  max_dec_frames_ = max_jobs_ * plan_.opc;
+  d_llh_ = (float*)DevAlloc(sizeof(float) * (size_t)max_jobs_ * plan_.opc * plan_.out_dim);
+  dec_.sinfo = d_sinfo_;
+  dec_.arcs = d_arcs_;
+  dec_.arc_src = d_arc_src_;
+  dec_.num_states = (int)NS;
+  dec_.start_state = g.start;
+  dec_.beam = m.dec.beam;
+  dec_.beam_delta = m.dec.beam_delta;
+  dec_.max_active = m.dec.max_active;
+  dec_.min_active = m.dec.min_active;
+  dec_.P = plan_.out_dim;
+  dec_.llh = d_llh_;
+  dec_.key = (unsigned long long*)DevAlloc(sizeof(unsigned long long) * S * NS);
+  dec_.posmap = (int*)DevAlloc(sizeof(int) * 2 * S * NS);
+  dec_.stamp = (int*)DevAlloc(sizeof(int) * S * NS);
+  const long long MT = cfg_.max_tokens;
+  dec_.cur_state = (int*)DevAlloc(sizeof(int) * S * MT);
+  dec_.cur_cost = (float*)DevAlloc(sizeof(float) * S * MT);
+  dec_.new_list = (int*)DevAlloc(sizeof(int) * S * MT);
+  dec_.front_a = (int*)DevAlloc(sizeof(int) * S * MT);
+  dec_.front_b = (int*)DevAlloc(sizeof(int) * S * MT);
+  dec_.arena = (int2*)DevAlloc(sizeof(int2) * S * cfg_.arena_tokens);
+  dec_.max_tok = (int)MT;
+  dec_.arena_cap = cfg_.arena_tokens;
+  d_slots_ = (DecSlot*)DevAlloc(sizeof(DecSlot) * S);
+  HIPCHECK(hipMemset(d_slots_, 0, sizeof(DecSlot) * S));
+  dec_.slots = d_slots_;
+  d_stats_ = (FrameStat*)DevAlloc(sizeof(FrameStat) * max_dec_frames_);
+  dec_.stats = cfg_.collect_stats ? d_stats_ : nullptr;
+  LaunchInitKeys(dec_.key, dec_.stamp, S * NS, stream_);
+  HIPCHECK(hipMemsetAsync(dec_.posmap, 0, sizeof(int) * 2 * S * NS, stream_));
+
+  // ---- staging
+  stage_bytes_ = Align256(sizeof(float) * (size_t)S * cfg_.max_step_samples) +
+                 Align256(sizeof(SampleJob) * S) + Align256(sizeof(MfccJob) * S) +
+                 Align256(sizeof(DevJob) * max_jobs_) + Align256(sizeof(DecJob) * S) + 1024;
+  HIPCHECK(hipHostMalloc((void**)&h_stage_, stage_bytes_, hipHostMallocDefault));
+  d_stage_ = (char*)DevAlloc(stage_bytes_);
+  HIPCHECK(hipHostMalloc((void**)&h_slots_, sizeof(DecSlot) * S, hipHostMallocDefault));
+  HIPCHECK(hipHostMalloc((void**)&h_stats_, sizeof(FrameStat) * max_dec_frames_, hipHostMallocDefault));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  slots_.resize(S);
+  VAMD_LOG("engine: slots=" << S << " fpc=" << fpc << " priming=" << plan_.priming_chunks
+                            << " ring=" << ring_ << " ops=" << plan_.ops.size()
+                            << " graph states=" << NS << " arcs=" << g.NumArcs());
+}
+
+Engine::~Engine() {
+  if (stream_) hipStreamSynchronize(stream_);
+  for (void* p : dev_allocs_) hipFree(p);
+  if (h_stage_) hipHostFree(h_stage_);
+  if (h_slots_) hipHostFree(h_slots_);
+  if (h_stats_) hipHostFree(h_stats_);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+int Engine::AllocSlot() {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (size_t i = 0; i < slots_.size(); i++)
+    if (!slots_[i].used) {
+      slots_[i] = SlotHost();
+      slots_[i].used = true;
+      slots_[i].next_chunk = -plan_.priming_chunks;
+      return (int)i;
+    }
+  VAMD_ERR("all " << slots_.size() << " stream slots of the engine are in use");
+}
+
+void Engine::FreeSlot(int slot) {
+  std::lock_guard<std::mutex> lk(mu_);
+  slots_.at(slot).used = false;
+}
+
+void Engine::ResetPipeline(int slot) {
+  std::lock_guard<std::mutex> lk(mu_);
+  SlotHost& h = slots_.at(slot);
+  h.pending.clear();
+  h.pending_pos = 0;
+  h.samples = 0;
+  h.frames = 0;
+  h.next_chunk = -plan_.priming_chunks;
+  h.out_ready = 0;
+  h.decoded = 0;
+  h.finished = false;
+  h.need_reset = true;
+  h.err = 0;
+}
+
+void Engine::ResetDecoder(int slot) {
+  std::lock_guard<std::mutex> lk(mu_);
+  SlotHost& h = slots_.at(slot);
+  h.decoded = 0;
+  h.need_reset = true;
+}
+
+void Engine::AcceptSamples(int slot, const float* x, int n) {
+  std::lock_guard<std::mutex> lk(mu_);
+  SlotHost& h = slots_.at(slot);
+  if (h.finished) VAMD_ERR("AcceptSamples after InputFinished");
+  if (h.pending_pos > 0 && h.pending_pos == h.pending.size()) {
+    h.pending.clear();
+    h.pending_pos = 0;
+  }
+  h.pending.insert(h.pending.end(), x, x + n);
+}
+
+void Engine::InputFinished(int slot) {
+  std::lock_guard<std::mutex> lk(mu_);
+  slots_.at(slot).finished = true;
+}
+
+int Engine::NumFramesDecoded(int slot) const { return slots_.at(slot).decoded; }
+int Engine::NumFramesReady(int slot) const { return slots_.at(slot).out_ready; }
+bool Engine::InputIsFinished(int slot) const { return slots_.at(slot).finished; }
+int Engine::PendingSamples(int slot) const {
+  const SlotHost& h = slots_.at(slot);
+  return (int)(h.pending.size() - h.pending_pos);
+}
+int Engine::DecoderError(int slot) const { return slots_.at(slot).err; }
+const std::vector<FrameStat>& Engine::LastStats(int slot) const { return slots_.at(slot).stats; }
+
+bool Engine::BuildStep(const std::vector<int>& slots) {
+  st_samples_.clear();
+  st_sample_data_.clear();
+  st_mfcc_.clear();
+  st_mfcc_total_ = 0;
+  st_jobs_.clear();
+  st_dec_.clear();
+  const int fpc = plan_.fpc, opc = plan_.opc, fss = plan_.fss, R = plan_.right_context;
+  int stats_rows = 0;
+  bool any = false;
+  for (int s : slots) {
+    SlotHost& h = slots_.at(s);
+    if (!h.used) continue;
+    h.stats.clear();
+    // 1. samples
+    int avail = (int)(h.pending.size() - h.pending_pos);
+    int n = std::min(avail, cfg_.max_step_samples);
+    if (n > 0) {
+      st_samples_.push_back(SampleJob{s, (int)(h.samples & (sample_ring_ - 1)), n,
+                                      (int)st_sample_data_.size()});
+      st_sample_data_.insert(st_sample_data_.end(), h.pending.begin() + h.pending_pos,
+                             h.pending.begin() + h.pending_pos + n);
+      h.pending_pos += n;
+      h.samples += n;
+      any = true;
+    }
+    // 2. MFCC frames
+    int nf_total = NumFramesFor(h.samples);
+    if (nf_total > h.frames) {
+      st_mfcc_.push_back(MfccJob{s, h.frames, nf_total - h.frames, st_mfcc_total_});
+      st_mfcc_total_ += nf_total - h.frames;
+      h.frames = nf_total;
+      any = true;
+    }
+    // 3. chunk jobs (DecodableNnetLoopedOnline::NumFramesReady semantics)
+    const bool fin = h.finished && h.pending_pos == h.pending.size();
+    const int T = h.frames;
+    const int need_out = fin ? (T + fss - 1) / fss : 0;
+    int first_real = -1, dec_frames = 0, njobs = 0;
+    while (njobs < jobs_per_slot_) {
+      const int c = h.next_chunk;
+      bool ready;
+      if (fin) ready = T > 0 && (c < 0 || c * opc < need_out);
+      else ready = T >= (std::max(c, 0) + 1) * fpc + R;
+      if (!ready) break;
+      if (c >= 0) {
+        if (first_real < 0) first_real = (int)st_jobs_.size();
+        int valid = fin ? std::min(opc, need_out - c * opc) : opc;
+        dec_frames += valid;
+      }
+      st_jobs_.push_back(DevJob{s, c * fpc, fin ? T - 1 : INT_MAX, 0});
+      h.next_chunk++;
+      njobs++;
+      any = true;
+    }
+    h.out_ready += dec_frames;
+    if (dec_frames > 0 || h.need_reset) {
+      if (dec_frames > 0 || h.samples > 0 || fin) {
+        st_dec_.push_back(DecJob{s, first_real < 0 ? 0 : first_real * opc, dec_frames,
+                                 h.need_reset ? 1 : 0, stats_rows, 0, 0, 0});
+        stats_rows += dec_frames;
+        if (h.need_reset) h.decoded = 0;
+        h.need_reset = false;
+        h.decoded += dec_frames;
+        any = true;
+      }
+    }
+  }
+  return any;
+}
+
+void Engine::RunStep() {
+  // pack the step's inputs into one pinned buffer -> one H2D copy
+  size_t off = 0;
+  auto put = [&](const void* src, size_t bytes) {
+    size_t o = off;
+    if (bytes) memcpy(h_stage_ + o, src, bytes);
+    off += Align256(bytes);
+    return o;
+  };
+  size_t o_data = put(st_sample_data_.data(), sizeof(float) * st_sample_data_.size());
+  size_t o_sj = put(st_samples_.data(), sizeof(SampleJob) * st_samples_.size());
+  size_t o_mj = put(st_mfcc_.data(), sizeof(MfccJob) * st_mfcc_.size());
+  size_t o_dj = put(st_jobs_.data(), sizeof(DevJob) * st_jobs_.size());
+  size_t o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
+  if (off > stage_bytes_) VAMD_ERR("step staging overflow");
+  HIPCHECK(hipMemcpyAsync(d_stage_, h_stage_, off, hipMemcpyHostToDevice, stream_));
+  int launches = 0;
+  LaunchAppendSamples((const SampleJob*)(d_stage_ + o_sj), (int)st_samples_.size(),
+                      (const float*)(d_stage_ + o_data), d_samples_, sample_ring_, stream_);
+  launches += !st_samples_.empty();
+  LaunchMfcc(mfcc_, (const MfccJob*)(d_stage_ + o_mj), (int)st_mfcc_.size(), st_mfcc_total_,
+             d_samples_, sample_ring_, rings_, stream_);
+  launches += st_mfcc_total_ > 0;
+  if (!st_jobs_.empty()) {
+    const DevJob* dj = (const DevJob*)(d_stage_ + o_dj);
+    for (size_t i = 0; i < plan_.ops.size(); i++) {
+      NnetOpArgs a = op_args_[i];
+      a.M = (int)st_jobs_.size() * a.P;
+      a.jobs = dj;
+      a.llh = d_llh_;
+      if (plan_.ops[i].kind == Op::GEMM) LaunchNnetGemm(a, op_bk_[i], stream_);
+      else LaunchNnetGather(a, stream_);
+      launches++;
+    }
+  }
+  if (!st_dec_.empty()) {
+    DecArgs d = dec_;
+    d.jobs = (const DecJob*)(d_stage_ + o_ej);
+    LaunchDecode(d, (int)st_dec_.size(), stream_);
+    launches++;
+    HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(),
+                            hipMemcpyDeviceToHost, stream_));
+    int rows = 0;
+    for (auto& j : st_dec_) rows += j.nframes;
+    if (cfg_.collect_stats && rows)
+      HIPCHECK(hipMemcpyAsync(h_stats_, d_stats_, sizeof(FrameStat) * rows,
+                              hipMemcpyDeviceToHost, stream_));
+  }
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(stream_));
+  counters_.steps++;
+  counters_.launches += launches;
+  counters_.frames_mfcc += st_mfcc_total_;
+  counters_.chunk_jobs += st_jobs_.size();
+  for (auto& j : st_dec_) {
+    SlotHost& h = slots_[j.slot];
+    const DecSlot& ds = h_slots_[j.slot];
+    if (ds.frames != h.decoded)
+      VAMD_WARN("decoder frame count mismatch on slot " << j.slot << ": " << ds.frames << " vs "
+                                                         << h.decoded);
+    h.err = ds.err;
+    if (ds.err) VAMD_WARN("decoder error flags " << ds.err << " on stream slot " << j.slot);
+    counters_.frames_decoded += j.nframes;
+    if (cfg_.collect_llh && j.nframes) {
+      size_t n = (size_t)j.nframes * plan_.out_dim, o = h.llh.size();
+      h.llh.resize(o + n);
+      HIPCHECK(hipMemcpy(h.llh.data() + o, d_llh_ + (size_t)j.llh_row0 * plan_.out_dim,
+                         sizeof(float) * n, hipMemcpyDeviceToHost));
+    }
+    if (cfg_.collect_stats)
+      h.stats.insert(h.stats.end(), h_stats_ + j.stats_row0, h_stats_ + j.stats_row0 + j.nframes);
+  }
+}
+
+void Engine::Advance(const std::vector<int>& slots) {
+  std::lock_guard<std::mutex> lk(mu_);
+  while (BuildStep(slots)) RunStep();
+}
+
+void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
+                       std::vector<PathResult>* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  out->assign(slots.size(), PathResult());
+  if (slots.empty()) return;
+  int maxf = 0;
+  for (int s : slots) maxf = std::max(maxf, slots_.at(s).decoded);
+  int cap = 4 * maxf + 64;
+  const int n = (int)slots.size();
+  for (int attempt = 0; attempt < 3; attempt++) {
+    size_t bytes = Align256(sizeof(int) * n) + Align256(sizeof(int) * (size_t)n * cap) +
+                   4 * Align256(sizeof(int) * n);
+    char* d = nullptr;
+    HIPCHECK(hipMalloc((void**)&d, bytes));
+    std::vector<char> h(bytes);
+    size_t o_req = 0, o_path = Align256(sizeof(int) * n);
+    size_t o_len = o_path + Align256(sizeof(int) * (size_t)n * cap);
+    size_t o_cost = o_len + Align256(sizeof(int) * n);
+    size_t o_rel = o_cost + Align256(sizeof(int) * n);
+    size_t o_st = o_rel + Align256(sizeof(int) * n);
+    HIPCHECK(hipMemcpyAsync(d + o_req, slots.data(), sizeof(int) * n, hipMemcpyHostToDevice, stream_));
+    TraceArgs t;
+    t.sinfo = d_sinfo_;
+    t.arena = dec_.arena;
+    t.cur_state = dec_.cur_state;
+    t.cur_cost = dec_.cur_cost;
+    t.slots = d_slots_;
+    t.req_slot = (const int*)(d + o_req);
+    t.use_final = use_final ? 1 : 0;
+    t.max_tok = dec_.max_tok;
+    t.arena_cap = dec_.arena_cap;
+    t.path_cap = cap;
+    t.path = (int*)(d + o_path);
+    t.path_len = (int*)(d + o_len);
+    t.end_cost = (float*)(d + o_cost);
+    t.final_rel = (float*)(d + o_rel);
+    t.end_state = (int*)(d + o_st);
+    LaunchTraceback(t, n, stream_);
+    HIPCHECK(hipMemcpyAsync(h.data(), d, bytes, hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(),
+                            hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipStreamSynchronize(stream_));
+    HIPCHECK(hipFree(d));
+    bool retry = false;
+    for (int i = 0; i < n; i++) {
+      int len = ((int*)(h.data() + o_len))[i];
+      if (len > cap) { retry = true; cap = len + 64; }
+    }
+    if (retry) continue;
+    for (int i = 0; i < n; i++) {
+      PathResult& r = (*out)[i];
+      int len = ((int*)(h.data() + o_len))[i];
+      const int* p = (const int*)(h.data() + o_path) + (size_t)i * cap;
+      r.arcs.assign(p, p + len);
+      std::reverse(r.arcs.begin(), r.arcs.end());
+      r.end_cost = ((float*)(h.data() + o_cost))[i];
+      r.final_relative_cost = ((float*)(h.data() + o_rel))[i];
+      r.end_state = ((int*)(h.data() + o_st))[i];
+      r.cost = (double)r.end_cost - h_slots_[slots[i]].offset_sum;
+      if (slots_.at(slots[i]).decoded == 0) r.arcs.clear();
+    }
+    return;
+  }
+  VAMD_ERR("traceback path buffer could not be sized");
+}
+
+void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset) {
+  std::lock_guard<std::mutex> lk(mu_);
+  SlotHost& h = slots_.at(slot);
+  const int P = plan_.out_dim;
+  int done = 0;
+  bool first = true;
+  while (first || done < nframes) {
+    const int n = std::min(nframes - done, max_dec_frames_);
+    if (n > 0)
+      HIPCHECK(hipMemcpyAsync(d_llh_, llh + (size_t)done * P, sizeof(float) * n * P,
+                              hipMemcpyHostToDevice, stream_));
+    st_samples_.clear();
+    st_sample_data_.clear();
+    st_mfcc_.clear();
+    st_mfcc_total_ = 0;
+    st_jobs_.clear();
+    st_dec_.clear();
+    h.stats.clear();
+    const bool rs = first && (reset || h.need_reset);
+    st_dec_.push_back(DecJob{slot, 0, n, rs ? 1 : 0, 0, 0, 0, 0});
+    if (rs) h.decoded = 0;
+    h.need_reset = false;
+    h.decoded += n;
+    RunStep();
+    done += n;
+    first = false;
+  }
+}
+
+void Engine::DebugFeatures(int slot, int first, int n, std::vector<float>* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  const int dim = plan_.input_dim;
+  std::vector<float> ring((size_t)ring_ * dim);
+  float* base = nullptr;
+  HIPCHECK(hipMemcpy(&base, d_ring_ptrs_ + plan_.input_node, sizeof(float*), hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(ring.data(), base + (size_t)slot * ring_ * dim, sizeof(float) * ring.size(),
+                     hipMemcpyDeviceToHost));
+  out->resize((size_t)n * dim);
+  for (int i = 0; i < n; i++)
+    memcpy(out->data() + (size_t)i * dim, ring.data() + (size_t)((first + i) & (ring_ - 1)) * dim,
+           sizeof(float) * dim);
+}
+
+}  // namespace vamd

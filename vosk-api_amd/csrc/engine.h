@@ -1,0 +1,171 @@
+// GPU engine: owns the device copy of one model and the device-resident state
+// of up to `max_slots` concurrent streams, and advances any set of streams
+// through MFCC -> looped nnet3 -> token passing in batched launches.
+//
+// It is the MI355X replacement of what the reference obtains from Kaldi's
+// online2 / nnet3 / decoder libraries (CPU path, src/recognizer.cc:297-323)
+// and from BatchedThreadedNnet3CudaOnlinePipeline + CudaDecoder (batch path,
+// src/batch_model.cc:69-98).  Streams are independent: one engine step batches
+// every stream that has work, so the single-stream Recognizer and the
+// BatchRecognizer share the same kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "engine_dev.h"
+#include "model_io.h"
+#include "nnet_plan.h"
+
+namespace vamd {
+
+// Host copy of everything read from a model directory.
+struct ModelData {
+  std::string dir;
+  MfccOptions mfcc;
+  DecoderOptions dec;
+  DecodableOptions dcb;
+  EndpointConfig endpoint;
+  TransitionModel tm;
+  Nnet nnet;
+  Graph graph;
+  SymbolTable words;
+  std::vector<char> phone_is_silence;  // indexed by phone id
+  bool has_word_boundary = false;
+  // Loads a V2 (am/, conf/, graph/) or V1 (flat) layout (src/model.cc:106-128).
+  void Load(const std::string& dir);
+  void LoadBatchLayout(const std::string& dir);  // src/batch_model.cc:23-54
+};
+
+struct EngineConfig {
+  int frames_per_chunk = 21;
+  int max_slots = 64;
+  int max_step_samples = 8192;  // samples consumed per stream per step
+  int max_tokens = 1 << 16;     // token list capacity per stream per frame
+  long long arena_tokens = 1 << 21;  // backpointer arena per stream
+  int device = 0;
+  bool collect_stats = false;
+  bool collect_llh = false;  // tests: keep a host copy of every decoded LLH row
+};
+
+struct PathResult {
+  std::vector<int> arcs;  // best path arc indices (forward order)
+  float end_cost = 0;     // tot_cost (+ final) of the end token
+  double cost = 0;        // offset-corrected path cost
+  float final_relative_cost = 0;
+  int end_state = -1;
+};
+
+struct EngineCounters {
+  long long steps = 0, launches = 0, frames_mfcc = 0, chunk_jobs = 0, frames_decoded = 0;
+};
+
+class Engine {
+ public:
+  Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  const NnetPlan& plan() const { return plan_; }
+  const ModelData& model() const { return *md_; }
+  const EngineConfig& config() const { return cfg_; }
+  std::mutex& mutex() { return mu_; }
+
+  int AllocSlot();
+  void FreeSlot(int slot);
+  // New utterance: features restart at sample 0, decoder restarts.
+  void ResetPipeline(int slot);
+  // InitDecoding: the decoder restarts, the feature/nnet pipeline continues.
+  void ResetDecoder(int slot);
+  void AcceptSamples(int slot, const float* x, int n);
+  void InputFinished(int slot);
+  // Runs batched steps until the given streams have no runnable work.
+  void Advance(const std::vector<int>& slots);
+  int NumFramesDecoded(int slot) const;
+  int NumFramesReady(int slot) const;  // output frames available to the decoder
+  bool InputIsFinished(int slot) const;
+  int PendingSamples(int slot) const;
+  int DecoderError(int slot) const;
+  // Best path of the current utterance (batched over slots).
+  void BestPaths(const std::vector<int>& slots, bool use_final, std::vector<PathResult>* out);
+  // Optional per-frame decoder statistics of the last Advance (collect_stats).
+  const std::vector<FrameStat>& LastStats(int slot) const;
+  const EngineCounters& counters() const { return counters_; }
+  // Tests: feature rows from the device ring; LLH rows decoded so far
+  // (collect_llh); decoding of externally supplied log-likelihoods.
+  void DebugFeatures(int slot, int first_frame, int n, std::vector<float>* out);
+  const std::vector<float>& DecodedLlh(int slot) const { return slots_.at(slot).llh; }
+  void DecodeExternal(int slot, const float* llh, int nframes, bool reset);
+
+ private:
+  struct SlotHost {
+    bool used = false;
+    std::vector<float> pending;
+    size_t pending_pos = 0;
+    long long samples = 0;   // samples pushed to the device since pipeline reset
+    int frames = 0;          // MFCC frames computed
+    int next_chunk = 0;      // next chunk index (negative while priming)
+    int out_ready = 0;       // output frames computed
+    int decoded = 0;         // frames decoded since the decoder reset
+    bool finished = false;
+    bool need_reset = true;
+    int err = 0;
+    std::vector<FrameStat> stats;
+    std::vector<float> llh;
+  };
+  bool BuildStep(const std::vector<int>& slots);
+  void RunStep();
+  int NumFramesFor(long long samples) const;
+
+  std::shared_ptr<const ModelData> md_;
+  EngineConfig cfg_;
+  NnetPlan plan_;
+  std::mutex mu_;
+  hipStream_t stream_ = nullptr;
+  int ring_ = 0, sample_ring_ = 0, jobs_per_slot_ = 0;
+  std::vector<SlotHost> slots_;
+  EngineCounters counters_;
+
+  // device: model
+  MfccDev mfcc_{};
+  std::vector<void*> dev_allocs_;
+  std::vector<NnetOpArgs> op_args_;
+  std::vector<int> op_bk_;
+  float** d_ring_ptrs_ = nullptr;
+  int* d_ring_dims_ = nullptr;
+  RingSet rings_{};
+  int4* d_sinfo_ = nullptr;
+  int4* d_arcs_ = nullptr;
+  int* d_arc_src_ = nullptr;
+  // device: per-stream state
+  float* d_samples_ = nullptr;
+  float* d_llh_ = nullptr;
+  DecArgs dec_{};
+  DecSlot* d_slots_ = nullptr;
+  FrameStat* d_stats_ = nullptr;
+  // step staging (pinned host + device mirror)
+  char* h_stage_ = nullptr;
+  char* d_stage_ = nullptr;
+  size_t stage_bytes_ = 0;
+  DecSlot* h_slots_ = nullptr;
+  FrameStat* h_stats_ = nullptr;
+  // current step
+  std::vector<SampleJob> st_samples_;
+  std::vector<float> st_sample_data_;
+  std::vector<MfccJob> st_mfcc_;
+  int st_mfcc_total_ = 0;
+  std::vector<DevJob> st_jobs_;
+  std::vector<DecJob> st_dec_;
+  int max_jobs_ = 0, max_dec_frames_ = 0;
+
+  void* DevAlloc(size_t bytes);
+  template <class T> T* Upload(const std::vector<T>& v);
+};
+
+}  // namespace vamd

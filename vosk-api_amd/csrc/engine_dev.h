@@ -1,0 +1,137 @@
+// Plain-old-data structures shared by the host engine and the HIP kernels.
+#pragma once
+
+#include <cstdint>
+
+namespace vamd {
+
+constexpr int kMaxSegs = 16;
+constexpr int kMaxStages = 8;
+constexpr int kMaxParts = 8;
+constexpr int kMaxInstr = 48;
+
+// One chunk job of one stream slot: the op rows of this job are at times
+// base_t + pattern[k]; reads of the feature input are clamped to
+// [0, clamp_max] (Kaldi replicates the first / last frame).
+struct DevJob {
+  int slot, base_t, clamp_max, pad;
+};
+
+struct DevSeg { int node, offset, col0, dim, src_col; };
+struct DevStage { int kind, vec0, vec1, node, offset, src_col, scaled; float c; };
+struct DevInstr { int op, node, offset, src_col; float c; };
+struct DevPart { int col0, dim, instr0, ninstr; };
+
+struct RingSet {
+  float* const* base;  // per stored node: [slots][ring][dim]
+  const int* dim;      // per stored node
+  int mask;            // ring - 1 (power of two)
+  int ring;
+  int input_node;
+};
+
+struct NnetOpArgs {
+  int M, N, K, P;          // rows, cols, reduction, pattern length (rows per job)
+  const int* pattern;      // [P]
+  const float* W;          // [N][K] (GEMM only)
+  const DevJob* jobs;
+  RingSet rings;
+  const float* const* vecs;
+  int out_node;            // -1: write log-likelihood rows
+  float* llh;              // [M][N] when out_node < 0
+  int nsegs, nstages, nparts;
+  DevSeg segs[kMaxSegs];
+  DevStage stages[kMaxStages];
+  DevPart parts[kMaxParts];
+  DevInstr instr[kMaxInstr];
+};
+
+// ---- MFCC
+struct MfccDev {
+  int frame_length, frame_shift, padded, log2n, num_bins, num_ceps, nfft;
+  int use_energy, remove_dc;
+  float preemph;
+  const float* window;   // [frame_length]
+  const float* melw;     // [num_bins][nfft] dense
+  const int* mel_first;  // [num_bins]
+  const int* mel_last;   // [num_bins]
+  const float* dct;      // [num_ceps][num_bins]
+  const float* lifter;   // [num_ceps]
+  const float* twr;      // [padded/2]
+  const float* twi;      // [padded/2]
+};
+
+struct MfccJob {  // frames [first, first+count) of one slot; rows [row0, row0+count)
+  int slot, first, count, row0;
+};
+
+struct SampleJob {  // append count samples from staging[src] to ring position pos
+  int slot, pos, count, src;
+};
+
+// ---- decoder
+struct DecSlot {
+  int ntok;         // tokens of the current frame
+  int cur_base;     // arena index of the current frame's first token
+  int arena_used;
+  int frames;       // frames decoded since the last reset
+  int parity;       // which posmap half holds the current frame
+  int stamp;        // epsilon-closure round stamp
+  int err;          // bit 0: token list overflow, bit 1: arena overflow, bit 2: no tokens
+  int pad;
+  double offset_sum;
+};
+
+struct DecJob {
+  int slot, llh_row0, nframes, reset, stats_row0, pad0, pad1, pad2;
+};
+
+struct FrameStat {
+  int ntok_in, ntok_out, arcs_emit, arcs_eps;
+  float best, cutoff, next_cutoff, adaptive_beam;
+};
+
+struct DecArgs {
+  const int4* sinfo;     // per state {arc_begin, eps_begin, arc_end, final cost bits}
+  const int4* arcs;      // per arc {nextstate, weight bits, pdf (-1 eps), ilabel}
+  const int* arc_src;    // per arc source state
+  int num_states, start_state;
+  float beam, beam_delta;
+  int max_active, min_active;
+  int P;
+  const float* llh;
+  const DecJob* jobs;
+  unsigned long long* key;  // [slots][S]
+  int* posmap;              // [slots][2][S]
+  int* stamp;               // [slots][S]
+  int* cur_state;           // [slots][max_tok]
+  float* cur_cost;          // [slots][max_tok]
+  int* new_list;            // [slots][max_tok]
+  int* front_a;             // [slots][max_tok]
+  int* front_b;             // [slots][max_tok]
+  int2* arena;              // [slots][arena_cap]
+  DecSlot* slots;
+  FrameStat* stats;
+  int max_tok;
+  long long arena_cap;
+};
+
+struct TraceArgs {
+  const int4* sinfo;
+  const int2* arena;
+  const int* cur_state;
+  const float* cur_cost;
+  const DecSlot* slots;
+  const int* req_slot;   // [n] slots to trace
+  int use_final;
+  int max_tok;
+  long long arena_cap;
+  int path_cap;
+  int* path;             // [n][path_cap] reversed arc indices
+  int* path_len;         // [n]
+  float* end_cost;       // [n] (with final cost if used)
+  float* final_rel;      // [n] final relative cost
+  int* end_state;        // [n]
+};
+
+}  // namespace vamd

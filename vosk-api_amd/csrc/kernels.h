@@ -1,0 +1,22 @@
+// Host-callable launchers for the HIP kernels (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "engine_dev.h"
+
+namespace vamd {
+
+void LaunchAppendSamples(const SampleJob* jobs, int njobs, const float* staging, float* ring,
+                         int ring_len, hipStream_t s);
+void LaunchMfcc(const MfccDev& m, const MfccJob* jobs, int njobs, int total_frames,
+                const float* sample_ring, int sample_ring_len, const RingSet& rings,
+                hipStream_t s);
+// GEMM ops: bk = K-step (8, 16 or 32; must divide every segment boundary)
+void LaunchNnetGemm(const NnetOpArgs& a, int bk, hipStream_t s);
+void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s);
+void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s);
+void LaunchTraceback(const TraceArgs& a, int n, hipStream_t s);
+void LaunchInitKeys(unsigned long long* key, int* stamp, long long n_states_total, hipStream_t s);
+
+}  // namespace vamd

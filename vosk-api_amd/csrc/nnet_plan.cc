@@ -525,7 +525,9 @@ struct Builder {
   }
 
   void Schedule(int fpc, int fss, int llh, const std::map<int, int>& producer) {
-    if (fpc % fss) VAMD_ERR("frames_per_chunk must be a multiple of frame_subsampling_factor");
+    if (fss < 1) VAMD_ERR("bad frame_subsampling_factor " << fss);
+    if (fpc < fss) fpc = fss;
+    if (fpc % fss) fpc += fss - fpc % fss;  // GetChunkSize rounding [K]
     plan.fpc = fpc;
     plan.fss = fss;
     plan.opc = fpc / fss;
@@ -562,7 +564,8 @@ struct Builder {
       plan.ops[o].pattern = a;
     }
     // priming: smallest P such that every needed value is computed correctly
-    for (int P = 0; P <= 16; P++) {
+    const int max_p = span / fpc + 4;
+    for (int P = 0; P <= max_p; P++) {
       std::vector<std::set<int>> correct(plan.nodes.size());
       bool ok = true;
       int max_age = 0;
@@ -597,7 +600,7 @@ struct Builder {
         plan.max_age = max_age;
         break;
       }
-      if (P == 16) VAMD_ERR("could not find a priming schedule for the nnet");
+      if (P == max_p) VAMD_ERR("could not find a priming schedule for the nnet");
     }
     plan.flops_per_chunk = 0;
     for (auto& o : plan.ops)

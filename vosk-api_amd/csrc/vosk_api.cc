@@ -1,0 +1,394 @@
+// C ABI (include/vosk_api.h, include/vosk_amd_engine.h).
+//
+// Error conventions of the reference (src/vosk_api.cc:30-282): constructors
+// return NULL on any exception, accept_waveform returns -1, *_free(NULL) is a
+// no-op.  Unlike the reference, the batch entry points are always compiled
+// (the GPU path is the only path).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <sstream>
+#include <string>
+
+#include "common.h"
+#include "vosk_impl.h"
+#include "../../include/vosk_api.h"
+#include "../../include/vosk_amd_engine.h"
+
+using namespace vamd;
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+#define API_TRY try {
+#define API_CATCH(ret)                                   \
+  }                                                      \
+  catch (const std::exception& e) {                      \
+    g_last_error = e.what();                             \
+    return ret;                                          \
+  }                                                      \
+  catch (...) {                                          \
+    g_last_error = "unknown exception";                  \
+    return ret;                                          \
+  }
+#define API_CATCH_VOID                                   \
+  }                                                      \
+  catch (const std::exception& e) {                      \
+    g_last_error = e.what();                             \
+    VAMD_WARN(e.what());                                 \
+  }                                                      \
+  catch (...) {                                          \
+    g_last_error = "unknown exception";                  \
+  }
+
+extern "C" {
+
+VoskModel* vosk_model_new(const char* model_path) {
+  API_TRY
+  return (VoskModel*)new Model(model_path);
+  API_CATCH(nullptr)
+}
+
+void vosk_model_free(VoskModel* model) {
+  if (!model) return;
+  ((Model*)model)->Unref();
+}
+
+int vosk_model_find_word(VoskModel* model, const char* word) {
+  API_TRY
+  return ((Model*)model)->FindWord(word);
+  API_CATCH(-1)
+}
+
+VoskSpkModel* vosk_spk_model_new(const char* model_path) {
+  g_last_error = "speaker (x-vector) models are not supported by this build";
+  VAMD_WARN(g_last_error << " (" << (model_path ? model_path : "") << ")");
+  return nullptr;
+}
+
+void vosk_spk_model_free(VoskSpkModel*) {}
+
+VoskRecognizer* vosk_recognizer_new(VoskModel* model, float sample_rate) {
+  API_TRY
+  return (VoskRecognizer*)new Recognizer((Model*)model, sample_rate);
+  API_CATCH(nullptr)
+}
+
+VoskRecognizer* vosk_recognizer_new_spk(VoskModel* model, float sample_rate, VoskSpkModel* spk) {
+  API_TRY
+  if (spk) VAMD_WARN("speaker model ignored (x-vector path not implemented)");
+  return (VoskRecognizer*)new Recognizer((Model*)model, sample_rate);
+  API_CATCH(nullptr)
+}
+
+VoskRecognizer* vosk_recognizer_new_grm(VoskModel* model, float sample_rate, const char* grammar) {
+  API_TRY
+  VAMD_WARN("Runtime graphs are not supported by this model build; decoding with the static graph");
+  (void)grammar;
+  return (VoskRecognizer*)new Recognizer((Model*)model, sample_rate);
+  API_CATCH(nullptr)
+}
+
+void vosk_recognizer_set_spk_model(VoskRecognizer* recognizer, VoskSpkModel* spk_model) {
+  if (recognizer == nullptr || spk_model == nullptr) return;
+}
+
+void vosk_recognizer_set_max_alternatives(VoskRecognizer* r, int n) {
+  if (r) ((Recognizer*)r)->SetMaxAlternatives(n);
+}
+void vosk_recognizer_set_words(VoskRecognizer* r, int words) {
+  if (r) ((Recognizer*)r)->SetWords(words != 0);
+}
+void vosk_recognizer_set_partial_words(VoskRecognizer* r, int pw) {
+  if (r) ((Recognizer*)r)->SetPartialWords(pw != 0);
+}
+void vosk_recognizer_set_nlsml(VoskRecognizer* r, int nlsml) {
+  if (r) ((Recognizer*)r)->SetNLSML(nlsml != 0);
+}
+
+int vosk_recognizer_accept_waveform(VoskRecognizer* r, const char* data, int length) {
+  API_TRY
+  return ((Recognizer*)r)->AcceptWaveform(data, length) ? 1 : 0;
+  API_CATCH(-1)
+}
+
+int vosk_recognizer_accept_waveform_s(VoskRecognizer* r, const short* data, int length) {
+  API_TRY
+  return ((Recognizer*)r)->AcceptWaveform(data, length) ? 1 : 0;
+  API_CATCH(-1)
+}
+
+int vosk_recognizer_accept_waveform_f(VoskRecognizer* r, const float* data, int length) {
+  API_TRY
+  return ((Recognizer*)r)->AcceptWaveform(data, length) ? 1 : 0;
+  API_CATCH(-1)
+}
+
+const char* vosk_recognizer_result(VoskRecognizer* r) { return ((Recognizer*)r)->Result(); }
+const char* vosk_recognizer_partial_result(VoskRecognizer* r) {
+  return ((Recognizer*)r)->PartialResult();
+}
+const char* vosk_recognizer_final_result(VoskRecognizer* r) { return ((Recognizer*)r)->FinalResult(); }
+void vosk_recognizer_reset(VoskRecognizer* r) { ((Recognizer*)r)->Reset(); }
+void vosk_recognizer_free(VoskRecognizer* r) { delete (Recognizer*)r; }
+
+void vosk_set_log_level(int log_level) { SetLogLevel(log_level); }
+
+void vosk_gpu_init() {
+  API_TRY
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) VAMD_ERR("no HIP device");
+  const char* lr = getenv("LOCAL_RANK");
+  (void)hipSetDevice(lr ? atoi(lr) % n : 0);
+  API_CATCH_VOID
+}
+
+void vosk_gpu_thread_init() {
+  const char* lr = getenv("LOCAL_RANK");
+  int n = 0;
+  if (hipGetDeviceCount(&n) == hipSuccess && n > 0) (void)hipSetDevice(lr ? atoi(lr) % n : 0);
+}
+
+VoskBatchModel* vosk_batch_model_new() {
+  API_TRY
+  const char* dir = getenv("VOSK_BATCH_MODEL_DIR");
+  return (VoskBatchModel*)new BatchModel(dir && *dir ? dir : "model");
+  API_CATCH(nullptr)
+}
+
+void vosk_batch_model_free(VoskBatchModel* model) { delete (BatchModel*)model; }
+
+void vosk_batch_model_wait(VoskBatchModel* model) {
+  API_TRY
+  ((BatchModel*)model)->WaitForCompletion();
+  API_CATCH_VOID
+}
+
+VoskBatchRecognizer* vosk_batch_recognizer_new(VoskBatchModel* model, float sample_rate) {
+  API_TRY
+  return (VoskBatchRecognizer*)new BatchRecognizer((BatchModel*)model, sample_rate);
+  API_CATCH(nullptr)
+}
+
+void vosk_batch_recognizer_free(VoskBatchRecognizer* r) { delete (BatchRecognizer*)r; }
+
+void vosk_batch_recognizer_accept_waveform(VoskBatchRecognizer* r, const char* data, int length) {
+  API_TRY
+  ((BatchRecognizer*)r)->AcceptWaveform(data, length);
+  API_CATCH_VOID
+}
+
+void vosk_batch_recognizer_set_nlsml(VoskBatchRecognizer* r, int nlsml) {
+  if (r) ((BatchRecognizer*)r)->SetNLSML(nlsml != 0);
+}
+
+void vosk_batch_recognizer_finish_stream(VoskBatchRecognizer* r) {
+  API_TRY
+  ((BatchRecognizer*)r)->FinishStream();
+  API_CATCH_VOID
+}
+
+const char* vosk_batch_recognizer_front_result(VoskBatchRecognizer* r) {
+  return ((BatchRecognizer*)r)->FrontResult();
+}
+
+void vosk_batch_recognizer_pop(VoskBatchRecognizer* r) { ((BatchRecognizer*)r)->Pop(); }
+
+int vosk_batch_recognizer_get_pending_chunks(VoskBatchRecognizer* r) {
+  return ((BatchRecognizer*)r)->GetNumPendingChunks();
+}
+
+// ---------------------------------------------------------------------------
+// diagnostic engine ABI
+// ---------------------------------------------------------------------------
+struct VamdEngine {
+  std::shared_ptr<ModelData> md;
+  std::unique_ptr<Engine> eng;
+  std::string desc;
+};
+
+const char* vamd_last_error(void) { return g_last_error.c_str(); }
+
+int vamd_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+VamdEngine* vamd_engine_new(const char* model_dir, int fpc, int max_streams, int flags) {
+  API_TRY
+  auto e = std::make_unique<VamdEngine>();
+  e->md = std::make_shared<ModelData>();
+  e->md->Load(model_dir);
+  EngineConfig cfg;
+  cfg.frames_per_chunk = fpc > 0 ? fpc : e->md->dcb.frames_per_chunk;
+  cfg.max_slots = max_streams > 0 ? max_streams : 8;
+  cfg.collect_stats = (flags & 1) != 0;
+  cfg.collect_llh = (flags & 2) != 0;
+  const char* d = getenv("VOSK_AMD_DEVICE");
+  cfg.device = d ? atoi(d) : 0;
+  const char* at = getenv("VOSK_AMD_ARENA_TOKENS");
+  if (at) cfg.arena_tokens = atoll(at);
+  e->eng.reset(new Engine(e->md, cfg));
+  e->desc = e->eng->plan().Describe();
+  return e.release();
+  API_CATCH(nullptr)
+}
+
+void vamd_engine_free(VamdEngine* e) { delete e; }
+
+const char* vamd_engine_describe(VamdEngine* e) { return e->desc.c_str(); }
+
+const char* vamd_plan_describe(const char* model_dir, int fpc) {
+  static thread_local std::string out;
+  API_TRY
+  ModelData md;
+  md.Load(model_dir);
+  NnetPlan p = BuildNnetPlan(md.nnet, fpc > 0 ? fpc : md.dcb.frames_per_chunk,
+                             md.dcb.frame_subsampling_factor, md.dcb.acoustic_scale);
+  std::ostringstream os;
+  os << p.Describe() << "graph states=" << md.graph.NumStates() << " arcs=" << md.graph.NumArcs()
+     << " words=" << md.words.id2sym.size() << "\n";
+  out = os.str();
+  return out.c_str();
+  API_CATCH(nullptr)
+}
+
+int vamd_plan_info(const char* model_dir, int fpc, int* o, double* flops) {
+  API_TRY
+  ModelData md;
+  md.Load(model_dir);
+  NnetPlan p = BuildNnetPlan(md.nnet, fpc > 0 ? fpc : md.dcb.frames_per_chunk,
+                             md.dcb.frame_subsampling_factor, md.dcb.acoustic_scale);
+  o[0] = p.fpc; o[1] = p.fss; o[2] = p.left_context; o[3] = p.right_context;
+  o[4] = p.priming_chunks; o[5] = p.out_dim; o[6] = (int)p.ops.size(); o[7] = (int)p.nodes.size();
+  if (flops) *flops = p.flops_per_chunk;
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_engine_info(VamdEngine* e, int* o, double* flops) {
+  API_TRY
+  const NnetPlan& p = e->eng->plan();
+  o[0] = p.fpc; o[1] = p.fss; o[2] = p.left_context; o[3] = p.right_context;
+  o[4] = p.priming_chunks; o[5] = p.out_dim; o[6] = (int)p.ops.size(); o[7] = 0;
+  if (flops) *flops = p.flops_per_chunk;
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_stream_new(VamdEngine* e) {
+  API_TRY
+  int s = e->eng->AllocSlot();
+  e->eng->ResetPipeline(s);
+  return s;
+  API_CATCH(-1)
+}
+
+int vamd_stream_free(VamdEngine* e, int s) {
+  API_TRY
+  e->eng->FreeSlot(s);
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_stream_reset(VamdEngine* e, int s, int pipeline) {
+  API_TRY
+  if (pipeline) e->eng->ResetPipeline(s);
+  else e->eng->ResetDecoder(s);
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_stream_accept(VamdEngine* e, int s, const float* x, int n, int finished) {
+  API_TRY
+  if (n > 0) e->eng->AcceptSamples(s, x, n);
+  if (finished) e->eng->InputFinished(s);
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_engine_advance(VamdEngine* e, const int* streams, int n) {
+  API_TRY
+  e->eng->Advance(std::vector<int>(streams, streams + n));
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_stream_frames_decoded(VamdEngine* e, int s) {
+  API_TRY
+  return e->eng->NumFramesDecoded(s);
+  API_CATCH(-1)
+}
+
+int vamd_stream_error(VamdEngine* e, int s) {
+  API_TRY
+  return e->eng->DecoderError(s);
+  API_CATCH(-1)
+}
+
+int vamd_stream_features(VamdEngine* e, int s, int first, int n, float* out) {
+  API_TRY
+  std::vector<float> v;
+  e->eng->DebugFeatures(s, first, n, &v);
+  memcpy(out, v.data(), sizeof(float) * v.size());
+  return n;
+  API_CATCH(-1)
+}
+
+long long vamd_stream_llh(VamdEngine* e, int s, float* out, long long cap) {
+  API_TRY
+  const std::vector<float>& v = e->eng->DecodedLlh(s);
+  long long n = std::min<long long>(cap, (long long)v.size());
+  if (out && n > 0) memcpy(out, v.data(), sizeof(float) * n);
+  return (long long)v.size();
+  API_CATCH(-1)
+}
+
+int vamd_stream_stats(VamdEngine* e, int s, float* out, int cap) {
+  API_TRY
+  const std::vector<FrameStat>& st = e->eng->LastStats(s);
+  int n = std::min<int>(cap, (int)st.size());
+  for (int i = 0; i < n; i++) {
+    const FrameStat& f = st[i];
+    float* o = out + 8 * i;
+    o[0] = (float)f.ntok_in; o[1] = (float)f.ntok_out; o[2] = (float)f.arcs_emit;
+    o[3] = (float)f.arcs_eps; o[4] = f.best; o[5] = f.cutoff; o[6] = f.next_cutoff;
+    o[7] = f.adaptive_beam;
+  }
+  return (int)st.size();
+  API_CATCH(-1)
+}
+
+int vamd_stream_decode_llh(VamdEngine* e, int s, const float* llh, int nframes, int reset) {
+  API_TRY
+  e->eng->DecodeExternal(s, llh, nframes, reset != 0);
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_stream_best_path(VamdEngine* e, int s, int use_final, int* arcs, int cap, double* cost,
+                          float* frel) {
+  API_TRY
+  std::vector<PathResult> pr;
+  e->eng->BestPaths({s}, use_final != 0, &pr);
+  const PathResult& p = pr[0];
+  for (int i = 0; i < (int)p.arcs.size() && i < cap; i++) arcs[i] = p.arcs[i];
+  if (cost) *cost = p.cost;
+  if (frel) *frel = p.final_relative_cost;
+  return (int)p.arcs.size();
+  API_CATCH(-1)
+}
+
+int vamd_engine_counters(VamdEngine* e, long long* o) {
+  API_TRY
+  const EngineCounters& c = e->eng->counters();
+  o[0] = c.steps; o[1] = c.launches; o[2] = c.frames_mfcc; o[3] = c.chunk_jobs;
+  o[4] = c.frames_decoded;
+  return 0;
+  API_CATCH(-1)
+}
+
+}  // extern "C"

@@ -1,0 +1,495 @@
+// Vosk object layer (see vosk_impl.h).
+#include "vosk_impl.h"
+
+#include <cmath>
+#include <cstdlib>
+#include <sstream>
+
+#include "common.h"
+
+namespace vamd {
+
+static int EnvInt(const char* name, int def) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : def;
+}
+
+static int DeviceFromEnv() {
+  // one process per GPU: LOCAL_RANK (torchrun) or VOSK_AMD_DEVICE
+  int d = EnvInt("VOSK_AMD_DEVICE", -1);
+  if (d >= 0) return d;
+  return EnvInt("LOCAL_RANK", 0);
+}
+
+// ---------------------------------------------------------------------------
+// best-path post-processing
+// ---------------------------------------------------------------------------
+std::vector<WordSeg> PathWords(const ModelData& m, const std::vector<int>& arcs) {
+  // Word spans from the best path: a word ends at the frame its output label
+  // is emitted; it starts at its first non-silence frame after the previous
+  // word.  (Approximation of WordAlignLattice + MBR times, src/recognizer.cc:
+  // 430-482; exact word alignment is the next row, see DESIGN.md.)
+  std::vector<WordSeg> out;
+  int t = 0, seg_start = -1;
+  for (int a : arcs) {
+    const int il = m.graph.ilabel[a];
+    if (il != 0) {
+      const int ph = m.tm.tid2phone[il];
+      if (seg_start < 0 && !(ph < (int)m.phone_is_silence.size() && m.phone_is_silence[ph]))
+        seg_start = t;
+      t++;
+    }
+    const int ol = m.graph.olabel[a];
+    if (ol != 0) {
+      int st = seg_start >= 0 ? seg_start : (out.empty() ? 0 : out.back().end);
+      out.push_back(WordSeg{ol, st, std::max(st, t)});
+      seg_start = -1;
+    }
+  }
+  return out;
+}
+
+int TrailingSilenceFrames(const ModelData& m, const std::vector<int>& arcs) {
+  // online2/online-endpoint.cc TrailingSilenceLength [K]
+  int n = 0;
+  for (auto it = arcs.rbegin(); it != arcs.rend(); ++it) {
+    const int il = m.graph.ilabel[*it];
+    if (il == 0) continue;
+    const int ph = m.tm.tid2phone[il];
+    if (ph < (int)m.phone_is_silence.size() && m.phone_is_silence[ph]) n++;
+    else break;
+  }
+  return n;
+}
+
+bool EndpointRulesFire(const EndpointConfig& c, int frames_decoded, int trailing_sil,
+                       float frame_shift_s, float final_relative_cost) {
+  const float utt = frames_decoded * frame_shift_s, sil = trailing_sil * frame_shift_s;
+  for (int r = 0; r < 5; r++) {
+    const EndpointRule& rule = c.rule[r];
+    const bool contains_nonsilence = utt > sil;
+    if ((contains_nonsilence || !rule.must_contain_nonsilence) &&
+        sil >= rule.min_trailing_silence && final_relative_cost <= rule.max_relative_cost &&
+        utt >= rule.min_utterance_length) {
+      VAMD_LOG_VERBOSE("Endpointing rule " << r + 1 << " activated");
+      return true;
+    }
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// Model (src/model.cc:106-128, refcount :343-354)
+// ---------------------------------------------------------------------------
+Model::Model(const std::string& path) : md_(std::make_shared<ModelData>()) { md_->Load(path); }
+
+int Model::FindWord(const std::string& w) const { return md_->words.Find(w); }
+
+Engine* Model::StreamEngine() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!engine_) {
+    EngineConfig cfg;
+    cfg.frames_per_chunk = md_->dcb.frames_per_chunk;
+    cfg.max_slots = EnvInt("VOSK_AMD_MAX_STREAMS", 64);
+    cfg.device = DeviceFromEnv();
+    cfg.max_step_samples = 4096;
+    engine_.reset(new Engine(md_, cfg));
+  }
+  return engine_.get();
+}
+
+// ---------------------------------------------------------------------------
+// Recognizer (src/recognizer.cc)
+// ---------------------------------------------------------------------------
+Recognizer::Recognizer(Model* model, float sr) : model_(model), sample_frequency_(sr) {
+  if (std::fabs(sr - model->data()->mfcc.samp_freq) > 0.5f)
+    VAMD_ERR("sample rate " << sr << " != model rate " << model->data()->mfcc.samp_freq
+                            << " (resampling is a next row, see DESIGN.md)");
+  engine_ = model->StreamEngine();
+  slot_ = engine_->AllocSlot();
+  model_->Ref();
+}
+
+Recognizer::~Recognizer() {
+  engine_->FreeSlot(slot_);
+  model_->Unref();
+}
+
+void Recognizer::CleanUp() {  // src/recognizer.cc:188-224
+  frame_offset_ += engine_->NumFramesDecoded(slot_);
+  if (state_ == RECOGNIZER_FINALIZED || frame_offset_ > 20000) {
+    samples_round_start_ += samples_processed_;
+    samples_processed_ = 0;
+    frame_offset_ = 0;
+    engine_->ResetPipeline(slot_);
+  } else {
+    engine_->ResetDecoder(slot_);
+  }
+}
+
+bool Recognizer::AcceptWaveform(const char* data, int len) {
+  std::vector<float> w(len / 2);
+  const short* s = reinterpret_cast<const short*>(data);
+  for (int i = 0; i < len / 2; i++) w[i] = s[i];
+  return AcceptWaveform(w);
+}
+
+bool Recognizer::AcceptWaveform(const short* data, int len) {
+  std::vector<float> w(data, data + len);
+  return AcceptWaveform(w);
+}
+
+bool Recognizer::AcceptWaveform(const float* data, int len) {
+  std::vector<float> w(data, data + len);
+  return AcceptWaveform(w);
+}
+
+bool Recognizer::AcceptWaveform(std::vector<float>& w) {  // src/recognizer.cc:297-323
+  if (!(state_ == RECOGNIZER_RUNNING || state_ == RECOGNIZER_INITIALIZED)) CleanUp();
+  state_ = RECOGNIZER_RUNNING;
+  const int step = (int)(sample_frequency_ * 0.2f);
+  for (size_t i = 0; i < w.size(); i += step) {
+    const int n = (int)std::min<size_t>(step, w.size() - i);
+    engine_->AcceptSamples(slot_, w.data() + i, n);
+    engine_->Advance({slot_});
+  }
+  samples_processed_ += w.size();
+  return EndpointDetected();
+}
+
+bool Recognizer::EndpointDetected() {
+  const int frames = engine_->NumFramesDecoded(slot_);
+  if (frames == 0) return false;
+  std::vector<PathResult> pr;
+  engine_->BestPaths({slot_}, false, &pr);
+  const ModelData& m = *model_->data();
+  const float shift = 0.01f * m.dcb.frame_subsampling_factor;
+  return EndpointRulesFire(m.endpoint, frames, TrailingSilenceFrames(m, pr[0].arcs), shift,
+                           pr[0].final_relative_cost);
+}
+
+std::string Recognizer::WordsText(const std::vector<WordSeg>& w) const {
+  std::ostringstream text;
+  for (size_t i = 0; i < w.size(); i++) {
+    if (i) text << " ";
+    text << model_->data()->words.Find(w[i].word);
+  }
+  return text.str();
+}
+
+const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729 (1-best form)
+  if (engine_->NumFramesDecoded(slot_) == 0) return StoreEmptyReturn();
+  std::vector<PathResult> pr;
+  engine_->BestPaths({slot_}, true, &pr);
+  const ModelData& m = *model_->data();
+  std::vector<WordSeg> w = PathWords(m, pr[0].arcs);
+  const double shift = 0.01 * m.dcb.frame_subsampling_factor;
+  if (max_alternatives_ > 0 && !nlsml_) {
+    Json obj, entry;
+    for (auto& ws : w) {
+      if (words_) {
+        Json word;
+        word["word"] = Json::Str(m.words.Find(ws.word));
+        word["start"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.start) * shift);
+        word["end"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.end) * shift);
+        entry["result"].Append(word);
+      }
+    }
+    entry["text"] = Json::Str(WordsText(w));
+    entry["confidence"] = Json::Float(-pr[0].cost);
+    obj["alternatives"].Append(entry);
+    return StoreReturn(obj.Dump());
+  }
+  if (max_alternatives_ > 0 && nlsml_) {
+    std::stringstream ss;
+    ss << "<?xml version=\"1.0\"?>\n<result grammar=\"default\">\n";
+    ss << "<interpretation grammar=\"default\" confidence=\"" << (float)(-pr[0].cost) << "\">\n";
+    ss << "<input mode=\"speech\">" << WordsText(w) << "</input>\n";
+    ss << "<instance>" << WordsText(w) << "</instance>\n";
+    ss << "</interpretation>\n</result>\n";
+    return StoreReturn(ss.str());
+  }
+  Json obj;
+  for (auto& ws : w) {
+    if (words_) {
+      Json word;
+      word["word"] = Json::Str(m.words.Find(ws.word));
+      word["start"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.start) * shift);
+      word["end"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.end) * shift);
+      word["conf"] = Json::Float(1.0);
+      obj["result"].Append(word);
+    }
+  }
+  obj["text"] = Json::Str(WordsText(w));
+  return StoreReturn(obj.Dump());
+}
+
+const char* Recognizer::PartialResult() {  // src/recognizer.cc:732-806
+  if (state_ != RECOGNIZER_RUNNING) return StoreEmptyReturn();
+  Json res;
+  if (engine_->NumFramesDecoded(slot_) == 0) {
+    res["partial"] = Json::Str("");
+    return StoreReturn(res.Dump());
+  }
+  std::vector<PathResult> pr;
+  engine_->BestPaths({slot_}, false, &pr);
+  const ModelData& m = *model_->data();
+  std::vector<WordSeg> w = PathWords(m, pr[0].arcs);
+  if (partial_words_) {
+    const double shift = 0.01 * m.dcb.frame_subsampling_factor;
+    for (auto& ws : w) {
+      Json word;
+      word["word"] = Json::Str(m.words.Find(ws.word));
+      word["start"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.start) * shift);
+      word["end"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.end) * shift);
+      word["conf"] = Json::Float(1.0);
+      res["partial_result"].Append(word);
+    }
+  }
+  res["partial"] = Json::Str(WordsText(w));
+  return StoreReturn(res.Dump());
+}
+
+const char* Recognizer::Result() {  // src/recognizer.cc:808-816
+  if (state_ != RECOGNIZER_RUNNING) return StoreEmptyReturn();
+  state_ = RECOGNIZER_ENDPOINT;
+  return GetResult();
+}
+
+const char* Recognizer::FinalResult() {  // src/recognizer.cc:818-844
+  if (state_ != RECOGNIZER_RUNNING) return StoreEmptyReturn();
+  engine_->InputFinished(slot_);
+  engine_->Advance({slot_});
+  state_ = RECOGNIZER_FINALIZED;
+  GetResult();
+  return last_result_.c_str();
+}
+
+void Recognizer::Reset() {  // src/recognizer.cc:846-853
+  StoreEmptyReturn();
+  state_ = RECOGNIZER_ENDPOINT;
+}
+
+const char* Recognizer::StoreEmptyReturn() {  // src/recognizer.cc:855-871
+  if (!max_alternatives_) return StoreReturn("{\"text\": \"\"}");
+  if (nlsml_)
+    return StoreReturn("<?xml version=\"1.0\"?>\n<result grammar=\"default\">\n"
+                       "<interpretation confidence=\"1.0\">\n<instance/>\n"
+                       "<input><noinput/></input>\n</interpretation>\n</result>\n");
+  return StoreReturn("{\"alternatives\" : [{\"text\": \"\", \"confidence\" : 1.0}] }");
+}
+
+const char* Recognizer::StoreReturn(const std::string& s) {
+  last_result_ = s;
+  return last_result_.c_str();
+}
+
+// ---------------------------------------------------------------------------
+// BatchModel / BatchRecognizer (src/batch_model.cc, src/batch_recognizer.cc)
+// ---------------------------------------------------------------------------
+BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>()) {
+  md_->LoadBatchLayout(dir);
+  EngineConfig cfg;
+  // frames_per_chunk = max(51, right context rounded up to 3) (batch_model.cc:84-88)
+  Nnet& nn = md_->nnet;
+  NnetPlan probe = BuildNnetPlan(nn, 51, md_->dcb.frame_subsampling_factor, md_->dcb.acoustic_scale);
+  int rc = probe.right_context;
+  cfg.frames_per_chunk = std::max(51, rc + 3 - rc % 3);
+  cfg.max_slots = EnvInt("VOSK_AMD_BATCH_SLOTS", 256);
+  cfg.device = DeviceFromEnv();
+  cfg.max_step_samples = cfg.frames_per_chunk * md_->mfcc.WindowShift() + 512;
+  cfg.arena_tokens = EnvInt("VOSK_AMD_ARENA_TOKENS", 1 << 22);
+  engine_.reset(new Engine(md_, cfg));
+  samples_per_chunk_ = cfg.frames_per_chunk * md_->mfcc.WindowShift();
+  worker_ = std::thread([this] { Worker(); });
+}
+
+BatchModel::~BatchModel() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (worker_.joinable()) worker_.join();
+}
+
+void BatchModel::Register(BatchRecognizer* r) {
+  std::lock_guard<std::mutex> lk(mu_);
+  queues_[r];
+}
+
+void BatchModel::Unregister(BatchRecognizer* r) {
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] { return queues_[r].empty() && in_flight_ == 0; });
+  queues_.erase(r);
+}
+
+void BatchModel::Push(BatchRecognizer* r, std::vector<float>&& chunk, bool last) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    queues_[r].push_back(Chunk{std::move(chunk), last});
+  }
+  cv_.notify_all();
+}
+
+int BatchModel::PendingChunks(const BatchRecognizer* r) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = queues_.find(const_cast<BatchRecognizer*>(r));
+  return it == queues_.end() ? 0 : (int)it->second.size();
+}
+
+void BatchModel::WaitForCompletion() {  // src/batch_model.cc:118-121
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] {
+    if (in_flight_) return false;
+    for (auto& q : queues_)
+      if (!q.second.empty()) return false;
+    return true;
+  });
+}
+
+void BatchModel::Worker() {
+  const ModelData& m = *md_;
+  const float shift = 0.01f * m.dcb.frame_subsampling_factor;
+  while (true) {
+    std::vector<std::pair<BatchRecognizer*, Chunk>> batch;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] {
+        if (stop_) return true;
+        for (auto& q : queues_)
+          if (!q.second.empty()) return true;
+        return false;
+      });
+      if (stop_) return;
+      for (auto& q : queues_)
+        if (!q.second.empty()) {
+          batch.emplace_back(q.first, std::move(q.second.front()));
+          q.second.pop_front();
+        }
+      in_flight_ = 1;
+    }
+    try {
+      std::vector<int> slots;
+      for (auto& [r, c] : batch) {
+        if (!c.data.empty()) engine_->AcceptSamples(r->slot(), c.data.data(), (int)c.data.size());
+        if (c.last) engine_->InputFinished(r->slot());
+        slots.push_back(r->slot());
+      }
+      engine_->Advance(slots);
+      // endpoint (reset_on_endpoint, batch_model.cc:72) and end-of-stream results
+      std::vector<int> tb;
+      for (auto& [r, c] : batch)
+        if (engine_->NumFramesDecoded(r->slot()) > 0) tb.push_back(r->slot());
+      std::vector<PathResult> nofinal, withfinal;
+      engine_->BestPaths(tb, false, &nofinal);
+      size_t k = 0;
+      for (auto& [r, c] : batch) {
+        const int s = r->slot();
+        const int frames = engine_->NumFramesDecoded(s);
+        if (c.last) {
+          std::vector<PathResult> fr;
+          if (frames > 0) engine_->BestPaths({s}, true, &fr);
+          r->PushResult(frames > 0 ? PathWords(m, fr[0].arcs) : std::vector<WordSeg>(),
+                        r->segment_offset_);
+          if (frames > 0) k++;
+          continue;
+        }
+        if (frames == 0) continue;
+        const PathResult& p = nofinal[k++];
+        if (EndpointRulesFire(m.endpoint, frames, TrailingSilenceFrames(m, p.arcs), shift,
+                              p.final_relative_cost)) {
+          std::vector<PathResult> fr;
+          engine_->BestPaths({s}, true, &fr);
+          r->PushResult(PathWords(m, fr[0].arcs), r->segment_offset_);
+          r->segment_offset_ += frames * shift;
+          engine_->ResetDecoder(s);
+        }
+      }
+    } catch (const std::exception& e) {
+      VAMD_WARN("batch step failed: " << e.what());
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      in_flight_ = 0;
+    }
+    done_cv_.notify_all();
+  }
+}
+
+BatchRecognizer::BatchRecognizer(BatchModel* model, float sr) : model_(model), sample_frequency_(sr) {
+  if (std::fabs(sr - model->data().mfcc.samp_freq) > 0.5f)
+    VAMD_ERR("sample rate " << sr << " != model rate (resampling is a next row)");
+  slot_ = model_->engine()->AllocSlot();
+  model_->engine()->ResetPipeline(slot_);
+  model_->Register(this);
+}
+
+BatchRecognizer::~BatchRecognizer() {
+  model_->Unregister(this);
+  model_->engine()->FreeSlot(slot_);
+}
+
+void BatchRecognizer::AcceptWaveform(const char* data, int len) {  // batch_recognizer.cc:115-181
+  const short* s = reinterpret_cast<const short*>(data);
+  buffer_.insert(buffer_.end(), s, s + len / 2);
+  const int spc = model_->samples_per_chunk();
+  size_t i = 0;
+  while (i + spc <= buffer_.size()) {
+    model_->Push(this, std::vector<float>(buffer_.begin() + i, buffer_.begin() + i + spc), false);
+    i += spc;
+  }
+  if (i) buffer_.erase(buffer_.begin(), buffer_.begin() + i);
+}
+
+void BatchRecognizer::FinishStream() {  // batch_recognizer.cc:37-41
+  model_->Push(this, std::move(buffer_), true);
+  buffer_.clear();
+}
+
+void BatchRecognizer::PushResult(const std::vector<WordSeg>& words, double offset) {
+  // batch_recognizer.cc:43-107 (1-best form; MBR confidences are a next row)
+  const ModelData& m = model_->data();
+  std::string out;
+  std::stringstream text;
+  for (size_t i = 0; i < words.size(); i++) {
+    if (i) text << " ";
+    text << m.words.Find(words[i].word);
+  }
+  if (nlsml_) {
+    std::stringstream ss;
+    ss << "<?xml version=\"1.0\"?>\n<result grammar=\"default\">\n";
+    ss << "<interpretation grammar=\"default\" confidence=\"" << (words.empty() ? 0.0f : 1.0f)
+       << "\">\n<input mode=\"speech\">" << text.str() << "</input>\n<instance>" << text.str()
+       << "</instance>\n</interpretation>\n</result>\n";
+    out = ss.str();
+  } else {
+    Json obj;
+    for (auto& w : words) {
+      Json word;
+      word["word"] = Json::Str(m.words.Find(w.word));
+      word["start"] = Json::Float(std::round((double)w.start) * 0.03 + offset);
+      word["end"] = Json::Float(std::round((double)w.end) * 0.03 + offset);
+      word["conf"] = Json::Float(1.0);
+      obj["result"].Append(word);
+    }
+    obj["text"] = Json::Str(text.str());
+    out = obj.Dump();
+  }
+  std::lock_guard<std::mutex> lk(rmu_);
+  results_.push_back(out);
+}
+
+const char* BatchRecognizer::FrontResult() {
+  std::lock_guard<std::mutex> lk(rmu_);
+  if (results_.empty()) return "";
+  front_ = results_.front();
+  return front_.c_str();
+}
+
+void BatchRecognizer::Pop() {
+  std::lock_guard<std::mutex> lk(rmu_);
+  if (!results_.empty()) results_.pop_front();
+}
+
+}  // namespace vamd

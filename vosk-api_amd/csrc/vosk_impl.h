@@ -1,0 +1,153 @@
+// Vosk object layer on top of the GPU engine: Model, Recognizer, BatchModel,
+// BatchRecognizer.  Mirrors the reference's objects (src/model.h:41-104,
+// src/recognizer.h:43-111, src/batch_model.h:43-66,
+// src/batch_recognizer.h:28-53) and their state machines.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <queue>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "engine.h"
+#include "json_out.h"
+
+namespace vamd {
+
+// One decoded word of the best path (frames are decoder frames).
+struct WordSeg {
+  int word;
+  int start, end;
+};
+std::vector<WordSeg> PathWords(const ModelData& m, const std::vector<int>& arcs);
+int TrailingSilenceFrames(const ModelData& m, const std::vector<int>& arcs);
+// OnlineEndpointConfig rules (Kaldi online2/online-endpoint.cc [K]).
+bool EndpointRulesFire(const EndpointConfig& c, int frames_decoded, int trailing_sil,
+                       float frame_shift_s, float final_relative_cost);
+
+class Model {
+ public:
+  explicit Model(const std::string& path);
+  void Ref() { ref_.fetch_add(1); }
+  void Unref() {
+    if (ref_.fetch_sub(1) == 1) delete this;
+  }
+  int FindWord(const std::string& w) const;
+  const std::shared_ptr<ModelData>& data() const { return md_; }
+  // Engine shared by this model's streaming recognizers (created lazily).
+  Engine* StreamEngine();
+
+ private:
+  ~Model() = default;
+  std::shared_ptr<ModelData> md_;
+  std::unique_ptr<Engine> engine_;
+  std::mutex mu_;
+  std::atomic<int> ref_{1};
+};
+
+enum RecognizerState { RECOGNIZER_INITIALIZED, RECOGNIZER_RUNNING, RECOGNIZER_ENDPOINT,
+                       RECOGNIZER_FINALIZED };
+
+class Recognizer {
+ public:
+  Recognizer(Model* model, float sample_frequency);
+  ~Recognizer();
+  void SetMaxAlternatives(int n) { max_alternatives_ = n; }
+  void SetWords(bool w) { words_ = w; }
+  void SetPartialWords(bool w) { partial_words_ = w; }
+  void SetNLSML(bool n) { nlsml_ = n; }
+  bool AcceptWaveform(const char* data, int len);
+  bool AcceptWaveform(const short* data, int len);
+  bool AcceptWaveform(const float* data, int len);
+  const char* Result();
+  const char* PartialResult();
+  const char* FinalResult();
+  void Reset();
+
+ private:
+  bool AcceptWaveform(std::vector<float>& wave);
+  void CleanUp();
+  bool EndpointDetected();
+  const char* GetResult();
+  const char* StoreEmptyReturn();
+  const char* StoreReturn(const std::string& s);
+  std::string WordsText(const std::vector<WordSeg>& w) const;
+
+  Model* model_;
+  Engine* engine_;
+  int slot_;
+  float sample_frequency_;
+  int max_alternatives_ = 0;
+  bool words_ = false, partial_words_ = false, nlsml_ = false;
+  int frame_offset_ = 0;
+  long long samples_processed_ = 0, samples_round_start_ = 0;
+  RecognizerState state_ = RECOGNIZER_INITIALIZED;
+  bool finalized_decoder_ = false;
+  std::string last_result_;
+  std::vector<float> resample_buf_;
+};
+
+class BatchRecognizer;
+
+class BatchModel {
+ public:
+  explicit BatchModel(const std::string& dir = "model");
+  ~BatchModel();
+  void WaitForCompletion();
+  Engine* engine() { return engine_.get(); }
+  const ModelData& data() const { return *md_; }
+  int samples_per_chunk() const { return samples_per_chunk_; }
+  void Register(BatchRecognizer* r);
+  void Unregister(BatchRecognizer* r);
+  void Push(BatchRecognizer* r, std::vector<float>&& chunk, bool last);
+  int PendingChunks(const BatchRecognizer* r);
+
+ private:
+  void Worker();
+  std::shared_ptr<ModelData> md_;
+  std::unique_ptr<Engine> engine_;
+  int samples_per_chunk_ = 0;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  struct Chunk { std::vector<float> data; bool last; };
+  std::map<BatchRecognizer*, std::deque<Chunk>> queues_;
+  int in_flight_ = 0;
+  bool stop_ = false;
+  std::thread worker_;
+};
+
+class BatchRecognizer {
+ public:
+  BatchRecognizer(BatchModel* model, float sample_frequency);
+  ~BatchRecognizer();
+  void AcceptWaveform(const char* data, int len);
+  void FinishStream();
+  void SetNLSML(bool n) { nlsml_ = n; }
+  const char* FrontResult();
+  void Pop();
+  int GetNumPendingChunks() { return model_->PendingChunks(this); }
+
+  // called from the batch worker
+  int slot() const { return slot_; }
+  void PushResult(const std::vector<WordSeg>& words, double offset_s);
+  double segment_offset_ = 0;  // seconds at the start of the current segment
+  int frames_before_segment_ = 0;
+
+ private:
+  BatchModel* model_;
+  int slot_;
+  float sample_frequency_;
+  bool nlsml_ = false;
+  std::vector<float> buffer_;
+  std::mutex rmu_;
+  std::deque<std::string> results_;
+  std::string front_;
+};
+
+}  // namespace vamd

@@ -1,0 +1,164 @@
+"""ctypes wrapper of the diagnostic engine ABI (include/vosk_amd_engine.h).
+
+Drives the same GPU engine the vosk_* API uses, stage by stage, for the
+parity tests and the benchmark.  Every call raises if the native library
+reports an error; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _c
+
+_vp = C.c_void_p
+_SIGS = {
+    "vamd_last_error": (C.c_char_p, []),
+    "vamd_device_count": (C.c_int, []),
+    "vamd_plan_describe": (C.c_char_p, [C.c_char_p, C.c_int]),
+    "vamd_plan_info": (C.c_int, [C.c_char_p, C.c_int, _vp, _vp]),
+    "vamd_engine_new": (_vp, [C.c_char_p, C.c_int, C.c_int, C.c_int]),
+    "vamd_engine_free": (None, [_vp]),
+    "vamd_engine_describe": (C.c_char_p, [_vp]),
+    "vamd_engine_info": (C.c_int, [_vp, _vp, _vp]),
+    "vamd_stream_new": (C.c_int, [_vp]),
+    "vamd_stream_free": (C.c_int, [_vp, C.c_int]),
+    "vamd_stream_reset": (C.c_int, [_vp, C.c_int, C.c_int]),
+    "vamd_stream_accept": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int]),
+    "vamd_engine_advance": (C.c_int, [_vp, _vp, C.c_int]),
+    "vamd_stream_frames_decoded": (C.c_int, [_vp, C.c_int]),
+    "vamd_stream_error": (C.c_int, [_vp, C.c_int]),
+    "vamd_stream_features": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, _vp]),
+    "vamd_stream_llh": (C.c_longlong, [_vp, C.c_int, _vp, C.c_longlong]),
+    "vamd_stream_stats": (C.c_int, [_vp, C.c_int, _vp, C.c_int]),
+    "vamd_stream_decode_llh": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int]),
+    "vamd_stream_best_path": (C.c_int, [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _vp]),
+    "vamd_engine_counters": (C.c_int, [_vp, _vp]),
+}
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(_c, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+STATS_FIELDS = ("ntok_in", "ntok_out", "arcs_emit", "arcs_eps", "best", "cutoff",
+                "next_cutoff", "adaptive_beam")
+
+
+def _err():
+    return (_c.vamd_last_error() or b"").decode()
+
+
+def _chk(r):
+    if r is None or (isinstance(r, int) and r < 0):
+        raise RuntimeError("libvosk engine error: " + _err())
+    return r
+
+
+def plan_describe(model_dir, frames_per_chunk=0):
+    r = _c.vamd_plan_describe(str(model_dir).encode(), frames_per_chunk)
+    if r is None:
+        raise RuntimeError("vamd_plan_describe failed: " + _err())
+    return r.decode()
+
+
+def plan_info(model_dir, frames_per_chunk=0):
+    info = np.zeros(8, np.int32)
+    fl = C.c_double(0)
+    _chk(_c.vamd_plan_info(str(model_dir).encode(), frames_per_chunk, info.ctypes.data,
+                           C.addressof(fl)))
+    keys = ("fpc", "fss", "left_context", "right_context", "priming", "out_dim", "ops", "nodes")
+    d = dict(zip(keys, (int(x) for x in info)))
+    d["flops_per_chunk"] = fl.value
+    return d
+
+
+def device_count():
+    return _c.vamd_device_count()
+
+
+class Engine:
+    def __init__(self, model_dir, frames_per_chunk=0, max_streams=8, stats=False, keep_llh=False):
+        flags = (1 if stats else 0) | (2 if keep_llh else 0)
+        h = _c.vamd_engine_new(str(model_dir).encode(), frames_per_chunk, max_streams, flags)
+        if not h:
+            raise RuntimeError("vamd_engine_new failed: " + _err())
+        self.h = h
+        info = np.zeros(8, np.int32)
+        fl = C.c_double(0)
+        _chk(_c.vamd_engine_info(h, info.ctypes.data, C.addressof(fl)))
+        (self.fpc, self.fss, self.left_context, self.right_context, self.priming,
+         self.out_dim, self.num_ops, _) = [int(x) for x in info]
+        self.flops_per_chunk = fl.value
+
+    def close(self):
+        if self.h:
+            _c.vamd_engine_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def describe(self):
+        return _c.vamd_engine_describe(self.h).decode()
+
+    def new_stream(self):
+        return _chk(_c.vamd_stream_new(self.h))
+
+    def free_stream(self, s):
+        _chk(_c.vamd_stream_free(self.h, s))
+
+    def reset(self, s, pipeline=True):
+        _chk(_c.vamd_stream_reset(self.h, s, 1 if pipeline else 0))
+
+    def accept(self, s, samples, finished=False):
+        x = np.ascontiguousarray(samples, np.float32)
+        _chk(_c.vamd_stream_accept(self.h, s, x.ctypes.data, len(x), 1 if finished else 0))
+
+    def advance(self, streams):
+        a = np.ascontiguousarray(streams, np.int32)
+        _chk(_c.vamd_engine_advance(self.h, a.ctypes.data, len(a)))
+
+    def frames_decoded(self, s):
+        return _chk(_c.vamd_stream_frames_decoded(self.h, s))
+
+    def error(self, s):
+        return _chk(_c.vamd_stream_error(self.h, s))
+
+    def features(self, s, first, n, dim):
+        out = np.zeros((n, dim), np.float32)
+        _chk(_c.vamd_stream_features(self.h, s, first, n, out.ctypes.data))
+        return out
+
+    def llh(self, s):
+        n = _c.vamd_stream_llh(self.h, s, None, 0)
+        _chk(n)
+        out = np.zeros(n, np.float32)
+        _c.vamd_stream_llh(self.h, s, out.ctypes.data, n)
+        return out.reshape(-1, self.out_dim)
+
+    def stats(self, s, cap=100000):
+        out = np.zeros((cap, 8), np.float32)
+        n = _chk(_c.vamd_stream_stats(self.h, s, out.ctypes.data, cap))
+        return out[:min(n, cap)]
+
+    def decode_llh(self, s, llh, reset=True):
+        x = np.ascontiguousarray(llh, np.float32)
+        _chk(_c.vamd_stream_decode_llh(self.h, s, x.ctypes.data, x.shape[0], 1 if reset else 0))
+
+    def best_path(self, s, use_final=True, cap=1 << 20):
+        arcs = np.zeros(cap, np.int32)
+        cost = C.c_double(0)
+        frel = C.c_float(0)
+        n = _chk(_c.vamd_stream_best_path(self.h, s, 1 if use_final else 0, arcs.ctypes.data,
+                                           cap, C.addressof(cost), C.addressof(frel)))
+        return arcs[:n].copy(), cost.value, frel.value
+
+    def counters(self):
+        out = np.zeros(5, np.int64)
+        _chk(_c.vamd_engine_counters(self.h, out.ctypes.data))
+        return dict(zip(("steps", "launches", "mfcc_frames", "chunk_jobs", "frames_decoded"),
+                        out.tolist()))
