@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""Aggregate real-time factor of the Vosk hot path on MI355X.
+
+Workload (BASELINE.json configs[2], the largest single-GPU configuration):
+BatchRecognizer-style decoding of 256 concurrent synthetic 16 kHz streams per
+GPU through libvosk.so's GPU engine -- MFCC -> looped TDNN-F nnet3 (fp32 MFMA)
+-> token-passing beam search (beam 13, max-active 7000) -- with the
+frames_per_chunk = 51 chunking of src/batch_model.cc:84-88.  A "step" is one
+engine pass that advances every stream by one 8160-sample chunk (0.51 s of
+audio); stream audio is resident in HBM before the timed region (per-step
+PCIe traffic is excluded; see DESIGN.md for the host-fed rate).
+
+Model: no Vosk model is available offline, so a seeded synthetic model with
+the reference recipe's TDNN-F topology (training/local/chain/run_tdnn.sh:
+98-129, random-init weights, BatchNorm calibrated on test.wav) and a 20k-word
+lexicon-tree HCLG is generated in the real Kaldi/OpenFST formats.  Streams
+are test.wav tiled, shifted, gained and noised per BASELINE.md.
+
+Multi-GPU: one process per GPU (torchrun); streams are sharded by rank with
+no data-path collective ("scaling": "weak"); a barrier brackets the timed
+region and the MAX elapsed time over ranks is used.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import wave
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "vosk-api_amd")
+for _p in (PKG, os.path.join(PKG, "tools"), os.path.join(REPO, "tests")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3   # dense fp32 MFMA peak (MI355X_MICROARCH.md)
+SR = 16000
+
+
+def load_wave():
+    w = wave.open(os.path.join(REPO, "tests", "golden", "test.wav"), "rb")
+    return np.frombuffer(w.readframes(w.getnframes()), "<i2").astype(np.float32)
+
+
+def stream_audio(base, i, n):
+    from conftest import perturbed_stream
+    return perturbed_stream(base, i, seconds=n / SR)
+
+
+def bench_model(rank, dist):
+    import make_synth_model
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", "bench_v1")
+    if rank == 0 and not os.path.exists(os.path.join(cache, "README")):
+        make_synth_model.make_model(cache, seed=11, vocab=20000, num_pdfs=2000)
+    if dist is not None:
+        dist.barrier()
+    return cache
+
+
+def cpu_baseline(model, base, streams, seconds, workers):
+    """Oracle (single-threaded C restatement) timed on host cores: one stream
+    per worker process at a time (the transcribe_scp.py Pool pattern)."""
+    import multiprocessing as mp
+    jobs = [(model, i, seconds) for i in range(streams)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(workers, initializer=_cpu_init, initargs=(model,)) as pool:
+        t0 = time.time()
+        res = pool.map(_cpu_job, jobs, chunksize=1)
+        wall = time.time() - t0
+    audio = sum(r[0] for r in res)
+    return audio / wall, audio, wall
+
+
+_ORC = {}
+
+
+def _cpu_init(model):
+    import oracle_py
+    _ORC["m"] = oracle_py.OracleModel(model)
+    _ORC["base"] = load_wave()
+
+
+def _cpu_job(args):
+    model, i, seconds = args
+    x = stream_audio(_ORC["base"], 10_000 + i, int(seconds * SR))
+    t = time.time()
+    _ORC["m"].recognize(x)
+    return len(x) / SR, time.time() - t
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--streams", type=int, default=256, help="streams per GPU")
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-streams", type=int, default=32)
+    ap.add_argument("--cpu-seconds", type=float, default=60.0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    os.environ["VOSK_AMD_DEVICE"] = str(local_rank)
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        tdist.init_process_group(backend=backend)
+        dist = tdist
+
+    model = args.model or bench_model(rank, dist)
+    import vosk
+    from vosk import engine as ve
+    vosk.SetLogLevel(-1)
+    if ve.device_count() == 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    S = args.streams
+    e = ve.Engine(model, frames_per_chunk=51, max_streams=S, stats=True, time_kernels=True)
+    chunk = e.fpc * 160
+    e.set_step_samples(chunk)
+    base = load_wave()
+    total_steps = args.warmup + args.steps + 2
+    streams = []
+    for i in range(S):
+        s = e.new_stream()
+        e.preload(s, stream_audio(base, rank * S + i, total_steps * chunk), finished=False)
+        streams.append(s)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        e.step(streams)
+    e.stage_times(reset=True)
+    lat = []
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        e.step(streams)  # synchronises the engine stream before returning
+        lat.append(time.perf_counter() - ts)
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        dev = "cuda" if torch.cuda.is_available() else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    audio_s = args.steps * S * chunk / SR * world
+    xrt = audio_s / elapsed
+
+    st = e.stage_times()
+    tot = e.decoder_totals()
+    errs = sum(1 for s in streams if e.error(s))
+    # decoder roofline: algorithmic bytes per launch:
+    # 16*T_in + 16*E + 8*E + 16*T_new + 20*L, L = T_new backpointer links
+    E = tot["arcs_emit"] + tot["arcs_eps"]
+    dec_bytes = 16 * tot["tok_in"] + 24 * E + 16 * tot["tok_out"] + 20 * tot["tok_out"]
+    dec_ms, dec_n = st["decode"]
+    nnet_ms, nnet_n = st["nnet"]
+    front_ms, front_n = st["front"]
+    dec_launch_ms = dec_ms / max(dec_n, 1)
+    dec_gbs = (dec_bytes / max(dec_n, 1)) / (dec_launch_ms * 1e-3) / 1e9 if dec_n else 0.0
+    nnet_flops = e.flops_per_chunk * S * args.steps
+    nnet_tflops = nnet_flops / (nnet_ms * 1e-3) / 1e12 if nnet_ms else 0.0
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", "r01_decode_pmc.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    if dec_ms >= nnet_ms:
+        roofline = {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(dec_gbs, 3),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dec_gbs / HBM_PEAK_GBS,
+                    "traffic": traffic, "avg_launch_ms": round(dec_launch_ms, 4),
+                    "alg_bytes_per_launch": dec_bytes / max(dec_n, 1)}
+    else:
+        roofline = {"bound": "mfma", "kernel": "nnet_gemm_kernel (all ops)",
+                    "achieved": round(nnet_tflops, 4), "peak": FP32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": nnet_tflops / FP32_PEAK_TFLOPS, "traffic": None}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        workers = min(16, os.cpu_count() or 1)
+        v, a, w = cpu_baseline(model, base, args.cpu_streams, args.cpu_seconds, workers)
+        cpu = {"value": round(v, 3), "unit": "xRT", "cores": workers, "kind": "port",
+               "sample": f"{args.cpu_streams} synthetic streams x {args.cpu_seconds:.0f} s through "
+                         f"the C oracle (MFCC + nnet3 + token passing), {workers} worker processes, "
+                         f"{a:.0f} s audio in {w:.1f} s wall"}
+
+    if rank == 0:
+        lat_ms = np.array(lat) * 1e3
+        out = {
+            "metric": "aggregate real-time factor (xRT) + p50 per-chunk latency, vosk-model-small-en-us",
+            "value": round(xrt, 2), "unit": "xRT", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic: test.wav tiled/shifted/gain/noise per BASELINE.md; seeded "
+                    "random-init synthetic model (recipe TDNN-F topology, 20k-word HCLG)",
+            "config": {"workload": "config3: BatchRecognizer-equivalent, 256 streams/GPU, "
+                                   "GPU MFCC + nnet3 + WFST beam search, 1xMI355X per rank",
+                       "streams_per_gpu": S, "global_streams": S * world,
+                       "chunk_samples": chunk, "frames_per_chunk": e.fpc,
+                       "beam": 13.0, "max_active": 7000, "parallelism": f"dp{world}"},
+            "p50_chunk_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),
+            "p90_chunk_latency_ms": round(float(np.percentile(lat_ms, 90)), 3),
+            "p99_chunk_latency_ms": round(float(np.percentile(lat_ms, 99)), 3),
+            "roofline": roofline,
+            "stages_ms_per_step": {"front": round(front_ms / args.steps, 4),
+                                   "nnet": round(nnet_ms / args.steps, 4),
+                                   "decode": round(dec_ms / args.steps, 4),
+                                   "gpu_step": round(st["step"][0] / args.steps, 4)},
+            "nnet_tflops": round(nnet_tflops, 4),
+            "decoder": {"frames": tot["frames"],
+                        "tokens_per_frame": round(tot["tok_out"] / max(tot["frames"], 1), 1),
+                        "arcs_per_frame": round(E / max(tot["frames"], 1), 1),
+                        "stream_errors": errs},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -25,7 +25,8 @@ const char *vamd_last_error(void);
 int vamd_device_count(void);
 
 /* frames_per_chunk <= 0 uses the model's decodable option (default 20->21);
- * flags: 1 = collect per-frame decoder stats, 2 = keep decoded LLH rows. */
+ * flags: 1 = collect per-frame decoder stats, 2 = keep decoded LLH rows,
+ *        4 = HIP-event timing of each stage on the engine's stream. */
 VamdEngine *vamd_engine_new(const char *model_dir, int frames_per_chunk, int max_streams,
                             int flags);
 void vamd_engine_free(VamdEngine *e);
@@ -55,6 +56,19 @@ int vamd_stream_decode_llh(VamdEngine *e, int stream, const float *llh, int nfra
 /* best path: arc indices into the graph (emitting-first CSR order) */
 int vamd_stream_best_path(VamdEngine *e, int stream, int use_final, int *arcs, int cap,
                           double *cost, float *final_relative_cost);
+/* upload a stream's whole audio into HBM (read by later steps, no per-step
+ * host->device copy); finished=1 marks end of input after it */
+int vamd_stream_preload(VamdEngine *e, int stream, const float *samples, long long n, int finished);
+/* exactly one batched step over the listed streams: 1 = ran, 0 = idle */
+int vamd_engine_step(VamdEngine *e, const int *streams, int n);
+/* samples each stream consumes per step (default: chunk + margin) */
+int vamd_engine_set_step_samples(VamdEngine *e, int n);
+/* HIP-event stage times (flag 4): ms and launch counts for
+ * [samples+MFCC, nnet ops, decoder, whole step]; reset=1 clears them */
+int vamd_engine_stage_times(VamdEngine *e, double *ms4, long long *launches4, int reset);
+/* decoder work since the last stage-time reset (flag 1): [frames, tokens in,
+ * tokens out, emitting arcs examined, epsilon arcs examined] */
+int vamd_engine_decoder_totals(VamdEngine *e, long long *out5);
 /* engine counters: [steps, launches, mfcc frames, chunk jobs, frames decoded] */
 int vamd_engine_counters(VamdEngine *e, long long *out5);
 

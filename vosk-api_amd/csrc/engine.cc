@@ -374,6 +374,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   d_stage_ = (char*)DevAlloc(stage_bytes_);
   HIPCHECK(hipHostMalloc((void**)&h_slots_, sizeof(DecSlot) * S, hipHostMallocDefault));
   HIPCHECK(hipHostMalloc((void**)&h_stats_, sizeof(FrameStat) * max_dec_frames_, hipHostMallocDefault));
+  for (auto& ev : ev_) HIPCHECK(hipEventCreate(&ev));
   HIPCHECK(hipStreamSynchronize(stream_));
   slots_.resize(S);
   VAMD_LOG("engine: slots=" << S << " fpc=" << fpc << " priming=" << plan_.priming_chunks
@@ -383,6 +384,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
 
 Engine::~Engine() {
   if (stream_) hipStreamSynchronize(stream_);
+  for (auto& ev : ev_)
+    if (ev) hipEventDestroy(ev);
+  for (auto& h : slots_)
+    if (h.resident) hipFree(h.resident);
   for (void* p : dev_allocs_) hipFree(p);
   if (h_stage_) hipHostFree(h_stage_);
   if (h_slots_) hipHostFree(h_slots_);
@@ -420,6 +425,10 @@ void Engine::ResetPipeline(int slot) {
   h.finished = false;
   h.need_reset = true;
   h.err = 0;
+  if (h.resident) hipFree(h.resident);
+  h.resident = nullptr;
+  h.resident_n = h.resident_pos = 0;
+  h.resident_finish = false;
 }
 
 void Engine::ResetDecoder(int slot) {
@@ -440,6 +449,19 @@ void Engine::AcceptSamples(int slot, const float* x, int n) {
   h.pending.insert(h.pending.end(), x, x + n);
 }
 
+void Engine::PreloadSamples(int slot, const float* x, long long n, bool finished) {
+  std::lock_guard<std::mutex> lk(mu_);
+  SlotHost& h = slots_.at(slot);
+  if (h.resident && h.resident_pos < h.resident_n) VAMD_ERR("previous preloaded audio not consumed");
+  if (h.resident) hipFree(h.resident);
+  h.resident = nullptr;
+  HIPCHECK(hipMalloc((void**)&h.resident, sizeof(float) * std::max<long long>(n, 1)));
+  if (n) HIPCHECK(hipMemcpy(h.resident, x, sizeof(float) * n, hipMemcpyHostToDevice));
+  h.resident_n = n;
+  h.resident_pos = 0;
+  h.resident_finish = finished;
+}
+
 void Engine::InputFinished(int slot) {
   std::lock_guard<std::mutex> lk(mu_);
   slots_.at(slot).finished = true;
@@ -457,6 +479,7 @@ const std::vector<FrameStat>& Engine::LastStats(int slot) const { return slots_.
 
 bool Engine::BuildStep(const std::vector<int>& slots) {
   st_samples_.clear();
+  st_sample_src_.clear();
   st_sample_data_.clear();
   st_mfcc_.clear();
   st_mfcc_total_ = 0;
@@ -469,17 +492,28 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
     SlotHost& h = slots_.at(s);
     if (!h.used) continue;
     h.stats.clear();
-    // 1. samples
-    int avail = (int)(h.pending.size() - h.pending_pos);
-    int n = std::min(avail, cfg_.max_step_samples);
-    if (n > 0) {
-      st_samples_.push_back(SampleJob{s, (int)(h.samples & (sample_ring_ - 1)), n,
-                                      (int)st_sample_data_.size()});
-      st_sample_data_.insert(st_sample_data_.end(), h.pending.begin() + h.pending_pos,
-                             h.pending.begin() + h.pending_pos + n);
-      h.pending_pos += n;
+    // 1. samples: HBM-resident audio first, then host-fed samples
+    if (h.resident && h.resident_pos < h.resident_n) {
+      int n = (int)std::min<long long>(h.resident_n - h.resident_pos, cfg_.max_step_samples);
+      SampleJob j{s, (int)(h.samples & (sample_ring_ - 1)), n, 0, h.resident + h.resident_pos};
+      st_samples_.push_back(j);
+      st_sample_src_.push_back(-1);
+      h.resident_pos += n;
       h.samples += n;
+      if (h.resident_pos == h.resident_n && h.resident_finish) h.finished = true;
       any = true;
+    } else {
+      int avail = (int)(h.pending.size() - h.pending_pos);
+      int n = std::min(avail, cfg_.max_step_samples);
+      if (n > 0) {
+        st_samples_.push_back(SampleJob{s, (int)(h.samples & (sample_ring_ - 1)), n, 0, nullptr});
+        st_sample_src_.push_back((int)st_sample_data_.size());
+        st_sample_data_.insert(st_sample_data_.end(), h.pending.begin() + h.pending_pos,
+                               h.pending.begin() + h.pending_pos + n);
+        h.pending_pos += n;
+        h.samples += n;
+        any = true;
+      }
     }
     // 2. MFCC frames
     int nf_total = NumFramesFor(h.samples);
@@ -490,7 +524,8 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
       any = true;
     }
     // 3. chunk jobs (DecodableNnetLoopedOnline::NumFramesReady semantics)
-    const bool fin = h.finished && h.pending_pos == h.pending.size();
+    const bool fin = h.finished && h.pending_pos == h.pending.size() &&
+                     (!h.resident || h.resident_pos == h.resident_n);
     const int T = h.frames;
     const int need_out = fin ? (T + fss - 1) / fss : 0;
     int first_real = -1, dec_frames = 0, njobs = 0;
@@ -536,19 +571,27 @@ void Engine::RunStep() {
     return o;
   };
   size_t o_data = put(st_sample_data_.data(), sizeof(float) * st_sample_data_.size());
+  for (size_t i = 0; i < st_samples_.size(); i++)
+    if (st_sample_src_[i] >= 0)
+      st_samples_[i].src = (const float*)(d_stage_ + o_data) + st_sample_src_[i];
   size_t o_sj = put(st_samples_.data(), sizeof(SampleJob) * st_samples_.size());
   size_t o_mj = put(st_mfcc_.data(), sizeof(MfccJob) * st_mfcc_.size());
   size_t o_dj = put(st_jobs_.data(), sizeof(DevJob) * st_jobs_.size());
   size_t o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
   if (off > stage_bytes_) VAMD_ERR("step staging overflow");
+  const bool tk = cfg_.time_kernels;
+  if (tk) HIPCHECK(hipEventRecord(ev_[0], stream_));
   HIPCHECK(hipMemcpyAsync(d_stage_, h_stage_, off, hipMemcpyHostToDevice, stream_));
   int launches = 0;
-  LaunchAppendSamples((const SampleJob*)(d_stage_ + o_sj), (int)st_samples_.size(),
-                      (const float*)(d_stage_ + o_data), d_samples_, sample_ring_, stream_);
+  if (tk) HIPCHECK(hipEventRecord(ev_[1], stream_));
+  LaunchAppendSamples((const SampleJob*)(d_stage_ + o_sj), (int)st_samples_.size(), d_samples_,
+                      sample_ring_, stream_);
   launches += !st_samples_.empty();
   LaunchMfcc(mfcc_, (const MfccJob*)(d_stage_ + o_mj), (int)st_mfcc_.size(), st_mfcc_total_,
              d_samples_, sample_ring_, rings_, stream_);
   launches += st_mfcc_total_ > 0;
+  if (tk) HIPCHECK(hipEventRecord(ev_[2], stream_));
+  const int l_front = launches;
   if (!st_jobs_.empty()) {
     const DevJob* dj = (const DevJob*)(d_stage_ + o_dj);
     for (size_t i = 0; i < plan_.ops.size(); i++) {
@@ -561,11 +604,16 @@ void Engine::RunStep() {
       launches++;
     }
   }
+  if (tk) HIPCHECK(hipEventRecord(ev_[3], stream_));
+  const int l_nnet = launches - l_front;
   if (!st_dec_.empty()) {
     DecArgs d = dec_;
     d.jobs = (const DecJob*)(d_stage_ + o_ej);
     LaunchDecode(d, (int)st_dec_.size(), stream_);
     launches++;
+  }
+  if (tk) HIPCHECK(hipEventRecord(ev_[4], stream_));
+  if (!st_dec_.empty()) {
     HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(),
                             hipMemcpyDeviceToHost, stream_));
     int rows = 0;
@@ -576,6 +624,18 @@ void Engine::RunStep() {
   }
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipStreamSynchronize(stream_));
+  if (tk) {
+    float a = 0, b = 0, c = 0, t = 0;
+    HIPCHECK(hipEventElapsedTime(&a, ev_[1], ev_[2]));
+    HIPCHECK(hipEventElapsedTime(&b, ev_[2], ev_[3]));
+    HIPCHECK(hipEventElapsedTime(&c, ev_[3], ev_[4]));
+    HIPCHECK(hipEventElapsedTime(&t, ev_[0], ev_[4]));
+    times_.ms[0] += a; times_.ms[1] += b; times_.ms[2] += c; times_.ms[3] += t;
+    times_.launches[0] += l_front;
+    times_.launches[1] += l_nnet;
+    times_.launches[2] += st_dec_.empty() ? 0 : 1;
+    times_.launches[3] += 1;
+  }
   counters_.steps++;
   counters_.launches += launches;
   counters_.frames_mfcc += st_mfcc_total_;
@@ -595,14 +655,30 @@ void Engine::RunStep() {
       HIPCHECK(hipMemcpy(h.llh.data() + o, d_llh_ + (size_t)j.llh_row0 * plan_.out_dim,
                          sizeof(float) * n, hipMemcpyDeviceToHost));
     }
-    if (cfg_.collect_stats)
+    if (cfg_.collect_stats) {
       h.stats.insert(h.stats.end(), h_stats_ + j.stats_row0, h_stats_ + j.stats_row0 + j.nframes);
+      for (int f = 0; f < j.nframes; f++) {
+        const FrameStat& fs = h_stats_[j.stats_row0 + f];
+        times_.dec[0]++;
+        times_.dec[1] += fs.ntok_in;
+        times_.dec[2] += fs.ntok_out;
+        times_.dec[3] += fs.arcs_emit;
+        times_.dec[4] += fs.arcs_eps;
+      }
+    }
   }
 }
 
 void Engine::Advance(const std::vector<int>& slots) {
   std::lock_guard<std::mutex> lk(mu_);
   while (BuildStep(slots)) RunStep();
+}
+
+bool Engine::Step(const std::vector<int>& slots) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!BuildStep(slots)) return false;
+  RunStep();
+  return true;
 }
 
 void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
@@ -683,6 +759,7 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
       HIPCHECK(hipMemcpyAsync(d_llh_, llh + (size_t)done * P, sizeof(float) * n * P,
                               hipMemcpyHostToDevice, stream_));
     st_samples_.clear();
+    st_sample_src_.clear();
     st_sample_data_.clear();
     st_mfcc_.clear();
     st_mfcc_total_ = 0;

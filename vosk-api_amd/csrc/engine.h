@@ -51,6 +51,16 @@ struct EngineConfig {
   int device = 0;
   bool collect_stats = false;
   bool collect_llh = false;  // tests: keep a host copy of every decoded LLH row
+  bool time_kernels = false; // HIP-event timing of each stage on the engine stream
+};
+
+// HIP-event times accumulated on the engine stream (time_kernels).
+struct StageTimes {
+  double ms[4] = {0, 0, 0, 0};     // 0 samples+MFCC, 1 nnet ops, 2 decoder, 3 whole step
+  long long launches[4] = {0, 0, 0, 0};
+  // decoder work totals (collect_stats): frames, tokens in, tokens out,
+  // emitting arcs examined, epsilon arcs examined
+  long long dec[5] = {0, 0, 0, 0, 0};
 };
 
 struct PathResult {
@@ -84,6 +94,14 @@ class Engine {
   // InitDecoding: the decoder restarts, the feature/nnet pipeline continues.
   void ResetDecoder(int slot);
   void AcceptSamples(int slot, const float* x, int n);
+  // Uploads a stream's whole audio into HBM; later steps read it from there
+  // (no host->device copy inside the steps).  finished: end of input after it.
+  void PreloadSamples(int slot, const float* x, long long n, bool finished);
+  // Exactly one batched step over the given streams; returns false if idle.
+  bool Step(const std::vector<int>& slots);
+  void SetStepSamples(int n) { cfg_.max_step_samples = n; }
+  const StageTimes& stage_times() const { return times_; }
+  void ResetStageTimes() { times_ = StageTimes(); }
   void InputFinished(int slot);
   // Runs batched steps until the given streams have no runnable work.
   void Advance(const std::vector<int>& slots);
@@ -118,6 +136,9 @@ class Engine {
     int err = 0;
     std::vector<FrameStat> stats;
     std::vector<float> llh;
+    float* resident = nullptr;  // HBM-resident audio (PreloadSamples)
+    long long resident_n = 0, resident_pos = 0;
+    bool resident_finish = false;
   };
   bool BuildStep(const std::vector<int>& slots);
   void RunStep();
@@ -131,6 +152,8 @@ class Engine {
   int ring_ = 0, sample_ring_ = 0, jobs_per_slot_ = 0;
   std::vector<SlotHost> slots_;
   EngineCounters counters_;
+  StageTimes times_;
+  hipEvent_t ev_[5] = {};
 
   // device: model
   MfccDev mfcc_{};
@@ -157,6 +180,7 @@ class Engine {
   FrameStat* h_stats_ = nullptr;
   // current step
   std::vector<SampleJob> st_samples_;
+  std::vector<int> st_sample_src_;  // offset into st_sample_data_, -1 = resident
   std::vector<float> st_sample_data_;
   std::vector<MfccJob> st_mfcc_;
   int st_mfcc_total_ = 0;

@@ -65,8 +65,9 @@ struct MfccJob {  // frames [first, first+count) of one slot; rows [row0, row0+c
   int slot, first, count, row0;
 };
 
-struct SampleJob {  // append count samples from staging[src] to ring position pos
-  int slot, pos, count, src;
+struct SampleJob {  // append count samples from src[] to ring position pos
+  int slot, pos, count, pad;
+  const float* src;  // staging buffer (host-fed) or the stream's HBM-resident audio
 };
 
 // ---- decoder

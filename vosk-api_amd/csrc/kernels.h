@@ -7,8 +7,8 @@
 
 namespace vamd {
 
-void LaunchAppendSamples(const SampleJob* jobs, int njobs, const float* staging, float* ring,
-                         int ring_len, hipStream_t s);
+void LaunchAppendSamples(const SampleJob* jobs, int njobs, float* ring, int ring_len,
+                         hipStream_t s);
 void LaunchMfcc(const MfccDev& m, const MfccJob* jobs, int njobs, int total_frames,
                 const float* sample_ring, int sample_ring_len, const RingSet& rings,
                 hipStream_t s);

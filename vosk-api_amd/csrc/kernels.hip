@@ -73,19 +73,17 @@ __device__ __forceinline__ float dev_logf(float x) {
 // ===========================================================================
 // samples
 // ===========================================================================
-__global__ void append_samples_kernel(const SampleJob* jobs, const float* staging, float* ring,
-                                      int ring_len) {
+__global__ void append_samples_kernel(const SampleJob* jobs, float* ring, int ring_len) {
   const SampleJob j = jobs[blockIdx.x];
   float* r = ring + (size_t)j.slot * ring_len;
   for (int i = threadIdx.x; i < j.count; i += blockDim.x)
-    r[(j.pos + i) & (ring_len - 1)] = staging[j.src + i];
+    r[(j.pos + i) & (ring_len - 1)] = j.src[i];
 }
 
-void LaunchAppendSamples(const SampleJob* jobs, int njobs, const float* staging, float* ring,
-                         int ring_len, hipStream_t s) {
+void LaunchAppendSamples(const SampleJob* jobs, int njobs, float* ring, int ring_len,
+                         hipStream_t s) {
   if (njobs <= 0) return;
-  hipLaunchKernelGGL(append_samples_kernel, dim3(njobs), dim3(256), 0, s, jobs, staging, ring,
-                     ring_len);
+  hipLaunchKernelGGL(append_samples_kernel, dim3(njobs), dim3(256), 0, s, jobs, ring, ring_len);
 }
 
 // ===========================================================================

@@ -227,6 +227,7 @@ VamdEngine* vamd_engine_new(const char* model_dir, int fpc, int max_streams, int
   cfg.max_slots = max_streams > 0 ? max_streams : 8;
   cfg.collect_stats = (flags & 1) != 0;
   cfg.collect_llh = (flags & 2) != 0;
+  cfg.time_kernels = (flags & 4) != 0;
   const char* d = getenv("VOSK_AMD_DEVICE");
   cfg.device = d ? atoi(d) : 0;
   const char* at = getenv("VOSK_AMD_ARENA_TOKENS");
@@ -379,6 +380,47 @@ int vamd_stream_best_path(VamdEngine* e, int s, int use_final, int* arcs, int ca
   if (cost) *cost = p.cost;
   if (frel) *frel = p.final_relative_cost;
   return (int)p.arcs.size();
+  API_CATCH(-1)
+}
+
+int vamd_stream_preload(VamdEngine* e, int s, const float* x, long long n, int finished) {
+  API_TRY
+  e->eng->PreloadSamples(s, x, n, finished != 0);
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_engine_step(VamdEngine* e, const int* streams, int n) {
+  API_TRY
+  return e->eng->Step(std::vector<int>(streams, streams + n)) ? 1 : 0;
+  API_CATCH(-1)
+}
+
+int vamd_engine_set_step_samples(VamdEngine* e, int n) {
+  API_TRY
+  if (n <= 0) VAMD_ERR("step samples must be positive");
+  e->eng->SetStepSamples(n);
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_engine_stage_times(VamdEngine* e, double* ms4, long long* launches4, int reset) {
+  API_TRY
+  const StageTimes& t = e->eng->stage_times();
+  for (int i = 0; i < 4; i++) {
+    if (ms4) ms4[i] = t.ms[i];
+    if (launches4) launches4[i] = t.launches[i];
+  }
+  if (reset) e->eng->ResetStageTimes();
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_engine_decoder_totals(VamdEngine* e, long long* o5) {
+  API_TRY
+  const StageTimes& t = e->eng->stage_times();
+  for (int i = 0; i < 5; i++) o5[i] = t.dec[i];
+  return 0;
   API_CATCH(-1)
 }
 

@@ -35,6 +35,11 @@ _SIGS = {
     "vamd_stream_decode_llh": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int]),
     "vamd_stream_best_path": (C.c_int, [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _vp]),
     "vamd_engine_counters": (C.c_int, [_vp, _vp]),
+    "vamd_stream_preload": (C.c_int, [_vp, C.c_int, _vp, C.c_longlong, C.c_int]),
+    "vamd_engine_step": (C.c_int, [_vp, _vp, C.c_int]),
+    "vamd_engine_decoder_totals": (C.c_int, [_vp, _vp]),
+    "vamd_engine_set_step_samples": (C.c_int, [_vp, C.c_int]),
+    "vamd_engine_stage_times": (C.c_int, [_vp, _vp, _vp, C.c_int]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(_c, _name)
@@ -78,8 +83,9 @@ def device_count():
 
 
 class Engine:
-    def __init__(self, model_dir, frames_per_chunk=0, max_streams=8, stats=False, keep_llh=False):
-        flags = (1 if stats else 0) | (2 if keep_llh else 0)
+    def __init__(self, model_dir, frames_per_chunk=0, max_streams=8, stats=False, keep_llh=False,
+                 time_kernels=False):
+        flags = (1 if stats else 0) | (2 if keep_llh else 0) | (4 if time_kernels else 0)
         h = _c.vamd_engine_new(str(model_dir).encode(), frames_per_chunk, max_streams, flags)
         if not h:
             raise RuntimeError("vamd_engine_new failed: " + _err())
@@ -156,6 +162,29 @@ class Engine:
         n = _chk(_c.vamd_stream_best_path(self.h, s, 1 if use_final else 0, arcs.ctypes.data,
                                            cap, C.addressof(cost), C.addressof(frel)))
         return arcs[:n].copy(), cost.value, frel.value
+
+    def preload(self, s, samples, finished=True):
+        x = np.ascontiguousarray(samples, np.float32)
+        _chk(_c.vamd_stream_preload(self.h, s, x.ctypes.data, len(x), 1 if finished else 0))
+
+    def step(self, streams):
+        a = np.ascontiguousarray(streams, np.int32)
+        return _chk(_c.vamd_engine_step(self.h, a.ctypes.data, len(a))) == 1
+
+    def set_step_samples(self, n):
+        _chk(_c.vamd_engine_set_step_samples(self.h, n))
+
+    def stage_times(self, reset=False):
+        ms = np.zeros(4, np.float64)
+        ln = np.zeros(4, np.int64)
+        _chk(_c.vamd_engine_stage_times(self.h, ms.ctypes.data, ln.ctypes.data, 1 if reset else 0))
+        names = ("front", "nnet", "decode", "step")
+        return {n: (float(m), int(l)) for n, m, l in zip(names, ms, ln)}
+
+    def decoder_totals(self):
+        out = np.zeros(5, np.int64)
+        _chk(_c.vamd_engine_decoder_totals(self.h, out.ctypes.data))
+        return dict(zip(("frames", "tok_in", "tok_out", "arcs_emit", "arcs_eps"), out.tolist()))
 
     def counters(self):
         out = np.zeros(5, np.int64)
