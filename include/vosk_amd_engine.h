@@ -21,6 +21,12 @@ const char *vamd_plan_describe(const char *model_dir, int frames_per_chunk);
 /* [fpc, fss, left_ctx, right_ctx, priming, out_dim, ops, stored nodes] */
 int vamd_plan_info(const char *model_dir, int frames_per_chunk, int *out8, double *flops_per_chunk);
 
+/* JSON bytes of a word list exactly as the recognizer writes results
+ * (json.h dump format): {list_key: [{conf,end,start,word}...], text_key: ...} */
+const char *vamd_json_words(const char *list_key, const char *text_key, int n,
+                            const char *const *words, const double *start, const double *end,
+                            const double *conf);
+
 const char *vamd_last_error(void);
 int vamd_device_count(void);
 

@@ -270,6 +270,29 @@ int vamd_plan_info(const char* model_dir, int fpc, int* o, double* flops) {
   API_CATCH(-1)
 }
 
+const char* vamd_json_words(const char* list_key, const char* text_key, int n,
+                            const char* const* words, const double* start, const double* end,
+                            const double* conf) {
+  static thread_local std::string out;
+  API_TRY
+  Json obj;
+  std::string text;
+  for (int i = 0; i < n; i++) {
+    Json w;
+    w["word"] = Json::Str(words[i]);
+    w["start"] = Json::Float(start[i]);
+    w["end"] = Json::Float(end[i]);
+    if (conf) w["conf"] = Json::Float(conf[i]);
+    obj[list_key].Append(w);
+    if (i) text += " ";
+    text += words[i];
+  }
+  obj[text_key] = Json::Str(text);
+  out = obj.Dump();
+  return out.c_str();
+  API_CATCH(nullptr)
+}
+
 int vamd_engine_info(VamdEngine* e, int* o, double* flops) {
   API_TRY
   const NnetPlan& p = e->eng->plan();
