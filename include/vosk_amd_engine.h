@@ -75,6 +75,9 @@ int vamd_engine_stage_times(VamdEngine *e, double *ms4, long long *launches4, in
 /* decoder work since the last stage-time reset (flag 1): [frames, tokens in,
  * tokens out, emitting arcs examined, epsilon arcs examined] */
 int vamd_engine_decoder_totals(VamdEngine *e, long long *out5);
+/* decoder phase clocks (env VOSK_AMD_DEC_PROFILE=1), summed over streams:
+ * [cutoff, seed, expand, compact, eps-closure, commit, 0, frames] */
+int vamd_engine_decoder_phases(VamdEngine *e, long long *out8);
 /* engine counters: [steps, launches, mfcc frames, chunk jobs, frames decoded] */
 int vamd_engine_counters(VamdEngine *e, long long *out5);
 

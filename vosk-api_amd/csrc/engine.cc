@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -251,6 +252,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   std::vector<float*> vec_ptrs;
   for (auto& v : plan_.vecs) vec_ptrs.push_back(Upload(v));
   const float* const* d_vecs = Upload(vec_ptrs);
+  auto is_in = [&](int node) { return node == plan_.input_node ? 1 : 0; };
   for (auto& op : plan_.ops) {
     NnetOpArgs a;
     memset(&a, 0, sizeof(a));
@@ -261,14 +263,17 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     a.rings = rings_;
     a.vecs = d_vecs;
     a.out_node = op.out_node;
-    int bk = 32;
+    a.out_base = op.out_node >= 0 ? ring_ptrs[op.out_node] : nullptr;
+    a.out_ldim = op.out_node >= 0 ? ring_dims[op.out_node] : 0;
+    int bk = 64;
     if (op.kind == Op::GEMM) {
       a.W = Upload(plan_.mats[op.weight].data);
       if ((int)op.segs.size() > kMaxSegs) VAMD_ERR("too many input segments in op " << op.name);
       a.nsegs = (int)op.segs.size();
       for (size_t i = 0; i < op.segs.size(); i++) {
         const ASegment& s = op.segs[i];
-        a.segs[i] = DevSeg{s.node, s.offset, s.col0, s.dim, s.src_col};
+        a.segs[i] = DevSeg{ring_ptrs[s.node], ring_dims[s.node], is_in(s.node), s.offset, s.col0,
+                           s.dim, s.src_col};
         if (s.dim % 4 || s.src_col % 4 || plan_.nodes[s.node].dim % 4)
           VAMD_ERR("op " << op.name << ": segment dims must be multiples of 4");
         while (bk > 8 && (s.col0 % bk || s.dim % bk)) bk >>= 1;
@@ -284,7 +289,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
         a.parts[i] = DevPart{gp.col0, gp.dim, ni, (int)gp.prog.size()};
         for (auto& g : gp.prog) {
           if (ni >= kMaxInstr) VAMD_ERR("descriptor program too long in op " << op.name);
-          a.instr[ni++] = DevInstr{g.op, g.node, g.offset, g.src_col, g.c};
+          a.instr[ni++] = DevInstr{g.op == GInstr::PUSH ? ring_ptrs[g.node] : nullptr, g.op,
+                                   g.op == GInstr::PUSH ? ring_dims[g.node] : 0,
+                                   g.op == GInstr::PUSH ? is_in(g.node) : 0, g.offset, g.src_col,
+                                   g.c};
         }
       }
     }
@@ -292,7 +300,18 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     a.nstages = (int)op.epi.size();
     for (size_t i = 0; i < op.epi.size(); i++) {
       const EpiStage& e = op.epi[i];
-      a.stages[i] = DevStage{e.kind, e.vec0, e.vec1, e.node, e.offset, e.src_col, e.scaled ? 1 : 0, e.c};
+      DevStage d;
+      d.base = e.kind == EpiStage::ADD_NODE ? ring_ptrs[e.node] : nullptr;
+      d.v0 = e.vec0 >= 0 ? vec_ptrs[e.vec0] : nullptr;
+      d.v1 = e.vec1 >= 0 ? vec_ptrs[e.vec1] : nullptr;
+      d.kind = e.kind;
+      d.ldim = e.kind == EpiStage::ADD_NODE ? ring_dims[e.node] : 0;
+      d.is_input = e.kind == EpiStage::ADD_NODE ? is_in(e.node) : 0;
+      d.offset = e.offset;
+      d.src_col = e.src_col;
+      d.scaled = e.scaled ? 1 : 0;
+      d.c = e.c;
+      a.stages[i] = d;
     }
     op_args_.push_back(a);
     op_bk_.push_back(bk);
@@ -311,7 +330,6 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
       sinfo[s] = make_int4((int)g.arc_begin[s], (int)g.eps_begin[s], (int)g.arc_begin[s + 1], fb);
     }
     std::vector<int4> arcs(g.NumArcs());
-    std::vector<int> src(g.NumArcs());
     for (int s = 0; s < g.NumStates(); s++)
       for (int64_t a = g.arc_begin[s]; a < g.arc_begin[s + 1]; a++) {
         int wb;
@@ -322,12 +340,12 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
           if (il <= 0 || il >= (int)m.tm.tid2pdf.size()) VAMD_ERR("graph ilabel " << il << " is not a transition id");
           pdf = m.tm.tid2pdf[il];
         }
-        arcs[a] = make_int4(g.nextstate[a], wb, pdf, il);
-        src[a] = s;
+        const int d = g.nextstate[a];
+        const bool dest_eps = g.eps_begin[d] < g.arc_begin[d + 1];
+        arcs[a] = make_int4(d, wb, pdf, (int)((unsigned)s | (dest_eps ? 0x80000000u : 0u)));
       }
     d_sinfo_ = Upload(sinfo);
     d_arcs_ = Upload(arcs);
-    d_arc_src_ = Upload(src);
   }
 
   // ---- decoder state
@@ -337,7 +355,6 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   d_llh_ = (float*)DevAlloc(sizeof(float) * (size_t)max_jobs_ * plan_.opc * plan_.out_dim);
   dec_.sinfo = d_sinfo_;
   dec_.arcs = d_arcs_;
-  dec_.arc_src = d_arc_src_;
   dec_.num_states = (int)NS;
   dec_.start_state = g.start;
   dec_.beam = m.dec.beam;
@@ -352,6 +369,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   const long long MT = cfg_.max_tokens;
   dec_.cur_state = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.cur_cost = (float*)DevAlloc(sizeof(float) * S * MT);
+  dec_.cur_pos = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.new_list = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.front_a = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.front_b = (int*)DevAlloc(sizeof(int) * S * MT);
@@ -363,6 +381,11 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   dec_.slots = d_slots_;
   d_stats_ = (FrameStat*)DevAlloc(sizeof(FrameStat) * max_dec_frames_);
   dec_.stats = cfg_.collect_stats ? d_stats_ : nullptr;
+  dec_.prof = nullptr;
+  if (getenv("VOSK_AMD_DEC_PROFILE")) {
+    dec_.prof = (long long*)DevAlloc(sizeof(long long) * 8 * S);
+    HIPCHECK(hipMemset(dec_.prof, 0, sizeof(long long) * 8 * S));
+  }
   LaunchInitKeys(dec_.key, dec_.stamp, S * NS, stream_);
   HIPCHECK(hipMemsetAsync(dec_.posmap, 0, sizeof(int) * 2 * S * NS, stream_));
 
@@ -707,6 +730,7 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
     t.arena = dec_.arena;
     t.cur_state = dec_.cur_state;
     t.cur_cost = dec_.cur_cost;
+    t.cur_pos = dec_.cur_pos;
     t.slots = d_slots_;
     t.req_slot = (const int*)(d + o_req);
     t.use_final = use_final ? 1 : 0;
@@ -775,6 +799,16 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     done += n;
     first = false;
   }
+}
+
+void Engine::DecoderPhaseClocks(long long* out8) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int i = 0; i < 8; i++) out8[i] = 0;
+  if (!dec_.prof) return;
+  std::vector<long long> h((size_t)8 * slots_.size());
+  HIPCHECK(hipMemcpy(h.data(), dec_.prof, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
+  for (size_t s = 0; s < slots_.size(); s++)
+    for (int i = 0; i < 8; i++) out8[i] += h[s * 8 + i];
 }
 
 void Engine::DebugFeatures(int slot, int first, int n, std::vector<float>* out) {

@@ -120,6 +120,9 @@ class Engine {
   void DebugFeatures(int slot, int first_frame, int n, std::vector<float>* out);
   const std::vector<float>& DecodedLlh(int slot) const { return slots_.at(slot).llh; }
   void DecodeExternal(int slot, const float* llh, int nframes, bool reset);
+  // VOSK_AMD_DEC_PROFILE=1: summed s_memtime clocks per decoder phase
+  // [cutoff, seed, expand, compact, eps, commit, -, frames]
+  void DecoderPhaseClocks(long long* out8);
 
  private:
   struct SlotHost {
@@ -165,7 +168,6 @@ class Engine {
   RingSet rings_{};
   int4* d_sinfo_ = nullptr;
   int4* d_arcs_ = nullptr;
-  int* d_arc_src_ = nullptr;
   // device: per-stream state
   float* d_samples_ = nullptr;
   float* d_llh_ = nullptr;

@@ -17,9 +17,12 @@ struct DevJob {
   int slot, base_t, clamp_max, pad;
 };
 
-struct DevSeg { int node, offset, col0, dim, src_col; };
-struct DevStage { int kind, vec0, vec1, node, offset, src_col, scaled; float c; };
-struct DevInstr { int op, node, offset, src_col; float c; };
+// Ring references carry the resolved ring base pointer and row length so the
+// kernels never chase a pointer table before a data load.
+struct DevSeg { const float* base; int ldim, is_input, offset, col0, dim, src_col; };
+struct DevStage { const float* base; const float* v0; const float* v1; int kind, ldim, is_input,
+                  offset, src_col, scaled; float c; };
+struct DevInstr { const float* base; int op, ldim, is_input, offset, src_col; float c; };
 struct DevPart { int col0, dim, instr0, ninstr; };
 
 struct RingSet {
@@ -38,6 +41,8 @@ struct NnetOpArgs {
   RingSet rings;
   const float* const* vecs;
   int out_node;            // -1: write log-likelihood rows
+  float* out_base;         // ring of out_node
+  int out_ldim;
   float* llh;              // [M][N] when out_node < 0
   int nsegs, nstages, nparts;
   DevSeg segs[kMaxSegs];
@@ -93,9 +98,10 @@ struct FrameStat {
 };
 
 struct DecArgs {
+  long long* prof;       // optional per-slot phase clocks [slots][8] (diagnostics)
   const int4* sinfo;     // per state {arc_begin, eps_begin, arc_end, final cost bits}
-  const int4* arcs;      // per arc {nextstate, weight bits, pdf (-1 eps), ilabel}
-  const int* arc_src;    // per arc source state
+  const int4* arcs;      // per arc {nextstate, weight bits, pdf (-1 eps),
+                         //          source state | (nextstate has eps arcs) << 31}
   int num_states, start_state;
   float beam, beam_delta;
   int max_active, min_active;
@@ -107,6 +113,7 @@ struct DecArgs {
   int* stamp;               // [slots][S]
   int* cur_state;           // [slots][max_tok]
   float* cur_cost;          // [slots][max_tok]
+  int* cur_pos;             // [slots][max_tok] list position (arena offset from cur_base)
   int* new_list;            // [slots][max_tok]
   int* front_a;             // [slots][max_tok]
   int* front_b;             // [slots][max_tok]
@@ -122,6 +129,7 @@ struct TraceArgs {
   const int2* arena;
   const int* cur_state;
   const float* cur_cost;
+  const int* cur_pos;
   const DecSlot* slots;
   const int* req_slot;   // [n] slots to trace
   int use_final;

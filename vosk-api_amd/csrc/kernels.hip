@@ -212,13 +212,13 @@ void LaunchMfcc(const MfccDev& m, const MfccJob* jobs, int njobs, int total, con
 // ===========================================================================
 // nnet3 ops
 // ===========================================================================
-__device__ __forceinline__ const float* ring_row(const RingSet& r, int node, int slot, int tau,
-                                                int clamp_max) {
-  if (node == r.input_node) {
+__device__ __forceinline__ const float* ring_at(const float* base, int ldim, int is_input,
+                                               const RingSet& r, int slot, int tau, int clamp_max) {
+  if (is_input) {
     if (tau < 0) tau = 0;
     if (tau > clamp_max) tau = clamp_max;
   }
-  return r.base[node] + ((size_t)slot * r.ring + (tau & r.mask)) * r.dim[node];
+  return base + ((size_t)slot * r.ring + (tau & r.mask)) * ldim;
 }
 
 __device__ __forceinline__ float apply_stages(const NnetOpArgs& a, float x, int col, int slot,
@@ -226,15 +226,16 @@ __device__ __forceinline__ float apply_stages(const NnetOpArgs& a, float x, int 
   for (int s = 0; s < a.nstages; s++) {
     const DevStage& st = a.stages[s];
     switch (st.kind) {
-      case 0: x = x + a.vecs[st.vec0][col]; break;                   // bias
-      case 1: x = x < 0.0f ? 0.0f : x; break;                        // ReLU
-      case 2: x = x * a.vecs[st.vec0][col] + a.vecs[st.vec1][col]; break;  // BN / scale+offset
-      case 3: {                                                      // bypass Sum()
-        float z = ring_row(a.rings, st.node, slot, tau + st.offset, clamp_max)[st.src_col + col];
+      case 0: x = x + st.v0[col]; break;                       // bias
+      case 1: x = x < 0.0f ? 0.0f : x; break;                  // ReLU
+      case 2: x = x * st.v0[col] + st.v1[col]; break;          // BN / scale+offset
+      case 3: {                                                // bypass Sum()
+        float z = ring_at(st.base, st.ldim, st.is_input, a.rings, slot, tau + st.offset,
+                          clamp_max)[st.src_col + col];
         x = st.scaled ? (st.c * z) + x : z + x;
         break;
       }
-      default: x = x * st.c; break;                                  // scale
+      default: x = x * st.c; break;                            // scale
     }
   }
   return x;
@@ -254,102 +255,143 @@ __device__ __forceinline__ void store_out(const NnetOpArgs& a, int r, int col, i
   if (a.out_node < 0) {
     a.llh[(size_t)r * a.N + col] = v;
   } else {
-    float* dst = a.rings.base[a.out_node] +
-                 ((size_t)slot * a.rings.ring + (tau & a.rings.mask)) * a.rings.dim[a.out_node];
+    float* dst = a.out_base + ((size_t)slot * a.rings.ring + (tau & a.rings.mask)) * a.out_ldim;
     dst[col] = v;
   }
 }
 
-// 64x64 output tile per 256-thread workgroup; each wave owns a 32x32 block
-// computed with v_mfma_f32_32x32x2_f32 (f32 in, f32 accumulate, exact
-// k-ordered fma chain).  A rows are gathered from the stored-node rings at
-// (tau + segment offset): the TDNN splice happens in the LDS staging.
-template <int BK>
-__global__ __launch_bounds__(256) void nnet_gemm_kernel(NnetOpArgs a) {
-  __shared__ float As[64][BK + 1];
-  __shared__ float Bs[BK][65];
+// Output tile 64 x (32*WN) per workgroup of 2 x WN waves, each wave owning a
+// 32x32 block computed with v_mfma_f32_32x32x2_f32 (f32 in, f32 accumulate:
+// an exact k-ordered fma chain).  A rows are gathered from the stored-node
+// time rings at (tau + segment offset): the TDNN splice happens in the LDS
+// staging.  K-steps are software pipelined: the next step's global loads
+// are issued into registers before the current step's MFMAs, then written to
+// the other half of a double-buffered LDS tile (one barrier per K-step).
+template <int BK, int WN>
+__global__ __launch_bounds__(128 * WN) void nnet_gemm_kernel(NnetOpArgs a) {
+  constexpr int BN = 32 * WN, NT = 128 * WN;
+  constexpr int Q = BK / 4;             // float4 per row per K-step
+  constexpr int NA = (64 * Q + NT - 1) / NT, NB = (BN * Q + NT - 1) / NT;
+  __shared__ float As[2][64][BK + 1];
+  __shared__ float Bs[2][BK][BN + 1];
+  __shared__ int Rinfo[3][64];  // per tile row: slot, tau, clamp
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
-  constexpr int Q = BK / 4;           // float4 per row per K-step
-  constexpr int NV = 64 * Q;          // float4 per tile
-  // per-thread A rows (fixed across K-steps)
-  int r_slot[(NV + 255) / 256], r_tau[(NV + 255) / 256], r_clamp[(NV + 255) / 256];
-  bool r_ok[(NV + 255) / 256];
-#pragma unroll
-  for (int v = 0; v < (NV + 255) / 256; v++) {
-    const int idx = tid + v * 256;
-    const int row = idx / Q;
-    const int gr = m0 + row;
-    r_ok[v] = idx < NV && gr < a.M;
-    r_slot[v] = 0; r_tau[v] = 0; r_clamp[v] = 0;
-    if (r_ok[v]) row_info(a, gr, &r_slot[v], &r_tau[v], &r_clamp[v]);
+  const int wr = wave / WN, wc = wave - wr * WN;
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * BN;
+  if (tid < 64) {
+    int sl = 0, ta = 0, cl = 0;
+    if (m0 + tid < a.M) row_info(a, m0 + tid, &sl, &ta, &cl);
+    Rinfo[0][tid] = sl;
+    Rinfo[1][tid] = ta;
+    Rinfo[2][tid] = cl;
   }
-  floatx16 acc;
+  __syncthreads();
+  int r_slot[NA], r_tau[NA], r_clamp[NA];
+  bool r_ok[NA];
 #pragma unroll
-  for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+  for (int v = 0; v < NA; v++) {
+    const int idx = tid + v * NT, row = (idx / Q) & 63;
+    r_ok[v] = idx < 64 * Q && m0 + (idx / Q) < a.M;
+    r_slot[v] = Rinfo[0][row];
+    r_tau[v] = Rinfo[1][row];
+    r_clamp[v] = Rinfo[2][row];
+  }
+  float4 ra[NA], rb[NB];
   int seg = 0;
-  for (int k0 = 0; k0 < a.K; k0 += BK) {
+  auto load = [&](int k0) {
     while (!(k0 >= a.segs[seg].col0 && k0 < a.segs[seg].col0 + a.segs[seg].dim)) seg++;
     const DevSeg S = a.segs[seg];
 #pragma unroll
-    for (int v = 0; v < (NV + 255) / 256; v++) {
-      const int idx = tid + v * 256;
-      if (idx < NV) {
-        const int row = idx / Q, q = idx - row * Q;
-        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r_ok[v]) {
-          const float* p = ring_row(a.rings, S.node, r_slot[v], r_tau[v] + S.offset, r_clamp[v]);
-          val = *reinterpret_cast<const float4*>(p + S.src_col + (k0 - S.col0) + 4 * q);
-        }
-        As[row][4 * q + 0] = val.x;
-        As[row][4 * q + 1] = val.y;
-        As[row][4 * q + 2] = val.z;
-        As[row][4 * q + 3] = val.w;
+    for (int v = 0; v < NA; v++) {
+      const int idx = tid + v * NT, row = idx / Q, q = idx - row * Q;
+      ra[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r_ok[v]) {
+        const float* p = ring_at(S.base, S.ldim, S.is_input, a.rings, r_slot[v],
+                                 r_tau[v] + S.offset, r_clamp[v]);
+        ra[v] = *reinterpret_cast<const float4*>(p + S.src_col + (k0 - S.col0) + 4 * q);
       }
     }
 #pragma unroll
-    for (int v = 0; v < (NV + 255) / 256; v++) {
-      const int idx = tid + v * 256;
-      if (idx < NV) {
-        const int n = idx / Q, q = idx - n * Q;
-        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (n0 + n < a.N)
-          val = *reinterpret_cast<const float4*>(a.W + (size_t)(n0 + n) * a.K + k0 + 4 * q);
-        Bs[4 * q + 0][n] = val.x;
-        Bs[4 * q + 1][n] = val.y;
-        Bs[4 * q + 2][n] = val.z;
-        Bs[4 * q + 3][n] = val.w;
+    for (int v = 0; v < NB; v++) {
+      const int idx = tid + v * NT, n = idx / Q, q = idx - n * Q;
+      rb[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < BN * Q && n0 + n < a.N)
+        rb[v] = *reinterpret_cast<const float4*>(a.W + (size_t)(n0 + n) * a.K + k0 + 4 * q);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < NA; v++) {
+      const int idx = tid + v * NT, row = idx / Q, q = idx - row * Q;
+      if (idx < 64 * Q) {
+        As[buf][row][4 * q + 0] = ra[v].x;
+        As[buf][row][4 * q + 1] = ra[v].y;
+        As[buf][row][4 * q + 2] = ra[v].z;
+        As[buf][row][4 * q + 3] = ra[v].w;
       }
     }
-    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < NB; v++) {
+      const int idx = tid + v * NT, n = idx / Q, q = idx - n * Q;
+      if (idx < BN * Q) {
+        Bs[buf][4 * q + 0][n] = rb[v].x;
+        Bs[buf][4 * q + 1][n] = rb[v].y;
+        Bs[buf][4 * q + 2][n] = rb[v].z;
+        Bs[buf][4 * q + 3][n] = rb[v].w;
+      }
+    }
+  };
+  floatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+  const int nk = a.K / BK;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ks++) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load((ks + 1) * BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
-      const float av = As[wr * 32 + (lane & 31)][kk + (lane >> 5)];
-      const float bv = Bs[kk + (lane >> 5)][wc * 32 + (lane & 31)];
+      const float av = As[buf][wr * 32 + (lane & 31)][kk + (lane >> 5)];
+      const float bv = Bs[buf][kk + (lane >> 5)][wc * 32 + (lane & 31)];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
     }
+    if (ks + 1 < nk) store(buf ^ 1);
     __syncthreads();
   }
   const int col = n0 + wc * 32 + (lane & 31);
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    const int row = m0 + wr * 32 + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+    const int lr = wr * 32 + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+    const int row = m0 + lr;
     if (row < a.M && col < a.N) {
-      int slot, tau, clamp;
-      row_info(a, row, &slot, &tau, &clamp);
+      const int slot = Rinfo[0][lr], tau = Rinfo[1][lr], clamp = Rinfo[2][lr];
       const float v = apply_stages(a, acc[j], col, slot, tau, clamp);
       store_out(a, row, col, slot, tau, v);
     }
   }
 }
 
+template <int BK>
+static void LaunchGemmBK(const NnetOpArgs& a, int wn, hipStream_t s) {
+  if (wn == 3) {
+    dim3 grid((a.M + 63) / 64, (a.N + 95) / 96);
+    hipLaunchKernelGGL((nnet_gemm_kernel<BK, 3>), grid, dim3(384), 0, s, a);
+  } else {
+    dim3 grid((a.M + 63) / 64, (a.N + 63) / 64);
+    hipLaunchKernelGGL((nnet_gemm_kernel<BK, 2>), grid, dim3(256), 0, s, a);
+  }
+}
+
 void LaunchNnetGemm(const NnetOpArgs& a, int bk, hipStream_t s) {
   if (a.M <= 0) return;
-  dim3 grid((a.M + 63) / 64, (a.N + 63) / 64);
-  if (bk == 32) hipLaunchKernelGGL(nnet_gemm_kernel<32>, grid, dim3(256), 0, s, a);
-  else if (bk == 16) hipLaunchKernelGGL(nnet_gemm_kernel<16>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(nnet_gemm_kernel<8>, grid, dim3(256), 0, s, a);
+  // a 96-wide N tile for the TDNN-F bottlenecks (N = 96): no idle wave columns
+  const int wn = (a.N % 96 == 0 && a.N % 64 != 0) ? 3 : 2;
+  if (bk == 64) LaunchGemmBK<64>(a, wn, s);
+  else if (bk == 32) LaunchGemmBK<32>(a, wn, s);
+  else if (bk == 16) LaunchGemmBK<16>(a, wn, s);
+  else LaunchGemmBK<8>(a, wn, s);
 }
 
 __global__ __launch_bounds__(256) void nnet_gather_kernel(NnetOpArgs a) {
@@ -366,7 +408,9 @@ __global__ __launch_bounds__(256) void nnet_gather_kernel(NnetOpArgs a) {
   int sp = 0;
   for (int i = 0; i < P.ninstr; i++) {
     const DevInstr in = a.instr[P.instr0 + i];
-    if (in.op == 0) stack[sp++] = ring_row(a.rings, in.node, slot, tau + in.offset, clamp)[in.src_col + d];
+    if (in.op == 0)
+      stack[sp++] = ring_at(in.base, in.ldim, in.is_input, a.rings, slot, tau + in.offset,
+                            clamp)[in.src_col + d];
     else if (in.op == 1) stack[sp - 1] = in.c * stack[sp - 1];
     else if (in.op == 2) { stack[sp - 2] = stack[sp - 2] + stack[sp - 1]; sp--; }
     else stack[sp++] = in.c;
@@ -387,7 +431,9 @@ void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s) {
 constexpr int DT = 1024;         // threads per decoder workgroup
 constexpr int DW = DT / 64;      // waves
 constexpr int kLlhLds = 8192;    // log-likelihood row staged in LDS up to this size
+constexpr int kTokLds = 4096;    // current-frame tokens cached in LDS up to this count
 constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
+constexpr unsigned kDestEps = 0x80000000u;  // arcs[].w: nextstate has epsilon arcs
 
 struct DecShared {
   int scan[DT + 1];   // exclusive prefix sums of the chunk's degrees
@@ -397,7 +443,7 @@ struct DecShared {
   unsigned long long red_u[DW];
   float red_f[DW];
   int red_i[DW];
-  int n_new, n_next, total, sel_k;
+  int n_new, n_next, n_front0, total, sel_k;
   unsigned sel_prefix, sel_mask;
   float seed;
   int bad;
@@ -468,8 +514,19 @@ __device__ __forceinline__ int owner(const DecShared& sh, int it) {
   return lo;
 }
 
-// exact k-th smallest (0-based) of cost[0..n) by 4-pass 8-bit radix select
-__device__ float kth_smallest(DecShared& sh, const float* cost, int n, int k) {
+// current-frame tokens: LDS cache when they fit, else global (agent loads)
+struct TokView {
+  int* gs;
+  float* gc;
+  const int* ls;
+  const float* lc;
+  bool lds;
+  __device__ __forceinline__ int s(int i) const { return lds ? ls[i] : AG_LD(&gs[i]); }
+  __device__ __forceinline__ float c(int i) const { return lds ? lc[i] : AG_LD(&gc[i]); }
+};
+
+// exact k-th smallest (0-based) of the token costs by 4-pass 8-bit radix select
+__device__ float kth_smallest(DecShared& sh, const TokView& tv, int n, int k) {
   if (threadIdx.x == 0) {
     sh.sel_prefix = 0;
     sh.sel_mask = 0;
@@ -481,20 +538,31 @@ __device__ float kth_smallest(DecShared& sh, const float* cost, int n, int k) {
     __syncthreads();
     const unsigned prefix = sh.sel_prefix, mask = sh.sel_mask;
     for (int i = threadIdx.x; i < n; i += DT) {
-      const unsigned u = ford(AG_LD(&cost[i]));
+      const unsigned u = ford(tv.c(i));
       if ((u & mask) == prefix) atomicAdd(&sh.hist[(u >> shift) & 255u], 1u);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      int kk = sh.sel_k;
-      unsigned b = 0;
-      for (; b < 256; b++) {
-        if (kk < (int)sh.hist[b]) break;
-        kk -= (int)sh.hist[b];
+    if (threadIdx.x < 64) {  // wave 0: prefix over the 256 buckets (4 per lane)
+      const int l = threadIdx.x;
+      const int h0 = sh.hist[4 * l], h1 = sh.hist[4 * l + 1], h2 = sh.hist[4 * l + 2],
+                h3 = sh.hist[4 * l + 3];
+      const int tot = h0 + h1 + h2 + h3;
+      int incl = tot;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o, 64);
+        if (l >= o) incl += u;
       }
-      sh.sel_k = kk;
-      sh.sel_prefix = prefix | (b << shift);
-      sh.sel_mask = mask | (255u << shift);
+      const int excl = incl - tot;
+      const int kk = sh.sel_k;
+      if (kk >= excl && kk < incl) {  // exactly one lane holds the bucket
+        int r = kk - excl, b = 4 * l;
+        if (r >= h0) { r -= h0; b++;
+          if (r >= h1) { r -= h1; b++;
+            if (r >= h2) { r -= h2; b++; } } }
+        sh.sel_k = r;
+        sh.sel_prefix = prefix | ((unsigned)b << shift);
+        sh.sel_mask = mask | (255u << shift);
+      }
     }
   }
   __syncthreads();
@@ -508,15 +576,17 @@ struct DecPtrs {
   int* stamp;
   int* cs;
   float* cc;
-  int* nl;
-  int* fa;
+  int* cp;   // list position of each current token (arena index = cur_base + cp)
+  int* nl;   // tokens of the frame under construction
+  int* fa;   // epsilon frontiers / compaction scratch
   int* fb;
   int2* arena;
 };
 
-// relax dest with (tot, arc); appends newly created tokens; returns improvement
-__device__ __forceinline__ bool relax(const DecArgs& a, DecShared& sh, const DecPtrs& p, int dest,
-                                      float tot, int arc) {
+// relax dest with (tot, arc); appends a newly created token to the frame
+// list.  Returns 1 if improved, 2 if created (created implies improved).
+__device__ __forceinline__ int relax(const DecArgs& a, DecShared& sh, const DecPtrs& p, int dest,
+                                     float tot, int arc) {
   const unsigned long long k = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
   const unsigned long long old = atomicMin(&p.key[dest], k);
   if (old == kEmpty) {
@@ -527,17 +597,26 @@ __device__ __forceinline__ bool relax(const DecArgs& a, DecShared& sh, const Dec
     } else {
       sh.bad |= 1;
     }
+    return 2;
   }
-  return k < old;
+  return k < old ? 1 : 0;
 }
 
-// epsilon closure of the frame under construction (ProcessNonemitting)
+__device__ __forceinline__ void push_front(const DecArgs& a, DecShared& sh, int* list, int* count,
+                                           int s) {
+  const int q = atomicAdd(count, 1);
+  if (q < a.max_tok) AG_ST(&list[q], s);
+  else sh.bad |= 1;
+}
+
+// ProcessNonemitting: epsilon closure in rounds over frontiers that only
+// hold states with epsilon arcs (round 0: created by the emitting pass).
 __device__ void eps_closure(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st, float cutoff,
-                            int* arcs_eps) {
-  int nfront = sh.n_new < a.max_tok ? sh.n_new : a.max_tok;
-  const int* front = p.nl;
-  int* next = p.fa;
+                            int nfront, int* arcs_eps) {
+  int* front = p.fa;
+  int* next = p.fb;
   int examined = 0;
+  nfront = nfront < a.max_tok ? nfront : a.max_tok;
   while (nfront > 0) {
     st.stamp++;
     const int stamp = st.stamp;
@@ -550,7 +629,7 @@ __device__ void eps_closure(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot
       if (i < nfront) {
         const int s = AG_LD(&front[i]);
         c = funord((uint32_t)(AG_LD(&p.key[s]) >> 32));
-        if (c <= cutoff) {
+        if (c < cutoff) {  // created tokens are < cutoff; dead ones are not
           const int4 si = a.sinfo[s];
           ab = si.y;
           deg = si.z - si.y;
@@ -567,63 +646,70 @@ __device__ void eps_closure(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot
         const int arc = sh.abeg[j] + (it - sh.scan[j]);
         const int4 A = a.arcs[arc];
         const float tot = sh.tcost[j] + __int_as_float(A.y);
-        if (tot < cutoff) {
-          if (relax(a, sh, p, A.x, tot, arc) && atomicExch(&p.stamp[A.x], stamp) != stamp) {
-            const int q = atomicAdd(&sh.n_next, 1);
-            if (q < a.max_tok) AG_ST(&next[q], A.x);
-            else sh.bad |= 1;
-          }
-        }
+        if (tot < cutoff && relax(a, sh, p, A.x, tot, arc) && ((unsigned)A.w & kDestEps) &&
+            atomicExch(&p.stamp[A.x], stamp) != stamp)
+          push_front(a, sh, next, &sh.n_next, A.x);
       }
       __syncthreads();
     }
     nfront = sh.n_next < a.max_tok ? sh.n_next : a.max_tok;
+    int* t = front;
     front = next;
-    next = (next == p.fa) ? p.fb : p.fa;
+    next = t;
   }
   *arcs_eps += examined;
 }
 
-// move the frame under construction into the arena + current token arrays
-__device__ void commit(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st, float* best_out) {
+// Move the frame under construction into the arena + current token arrays
+// (global, and the LDS cache when it fits); reset its keys.  List entries
+// whose cost is not below `cutoff` (dead: created by the single emitting
+// pass above the final next_cutoff) keep their arena slot unused.
+__device__ void commit(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st, int* TS, float* TC,
+                       bool* lds, float cutoff, float* best_out) {
   __syncthreads();
   const int n = sh.n_new < a.max_tok ? sh.n_new : a.max_tok;
   const int base = st.arena_used;
-  bool ok = (long long)base + n <= a.arena_cap;
+  const bool ok = (long long)base + n <= a.arena_cap;
+  if (threadIdx.x == 0) sh.n_next = 0;
+  __syncthreads();
   float best = __int_as_float(0x7f800000);
-  if (ok) {
-    for (int j = threadIdx.x; j < n; j += DT) {
-      const int s = AG_LD(&p.nl[j]);
-      const unsigned long long k = AG_LD(&p.key[s]);
-      const int arc = (int)(unsigned)(k & 0xffffffffu);
-      const float cost = funord((uint32_t)(k >> 32));
-      int prev = -1;
-      if (arc >= 0) {
-        const int src = a.arc_src[arc];
-        prev = a.arcs[arc].z >= 0 ? st.cur_base + AG_LD(&p.pos_cur[src])
-                                  : base + AG_LD(&p.pos_new[src]);
-      }
-      p.arena[base + j] = make_int2(prev, arc);
-      AG_ST(&p.cs[j], s);
-      AG_ST(&p.cc[j], cost);
-      best = fminf(best, cost);
-    }
-  }
-  // keys must be reset even if the arena overflowed
   for (int j = threadIdx.x; j < n; j += DT) {
     const int s = AG_LD(&p.nl[j]);
+    const unsigned long long k = AG_LD(&p.key[s]);
+    const int arc = (int)(unsigned)(k & 0xffffffffu);
+    const float cost = funord((uint32_t)(k >> 32));
+    if (ok && cost < cutoff) {
+      int prev = -1;
+      if (arc >= 0) {
+        const int4 A = a.arcs[arc];
+        const int src = (int)((unsigned)A.w & 0x7fffffffu);
+        prev = A.z >= 0 ? st.cur_base + AG_LD(&p.pos_cur[src]) : base + AG_LD(&p.pos_new[src]);
+      }
+      p.arena[base + j] = make_int2(prev, arc);
+      const int q = atomicAdd(&sh.n_next, 1);
+      AG_ST(&p.cs[q], s);
+      AG_ST(&p.cc[q], cost);
+      AG_ST(&p.cp[q], j);
+      if (q < kTokLds) {
+        TS[q] = s;
+        TC[q] = cost;
+      }
+      best = fminf(best, cost);
+    }
     AG_ST(&p.key[s], kEmpty);
   }
   best = block_min_f(sh, best);
   if (!ok) sh.bad |= 2;
   __syncthreads();
+  const int live = sh.n_next;
   if (ok) {
     st.cur_base = base;
     st.arena_used = base + n;
-    st.ntok = n;
+    st.ntok = live;
   } else {
     st.ntok = 0;
   }
+  *lds = live <= kTokLds;
   int* t = p.pos_cur;
   p.pos_cur = p.pos_new;
   p.pos_new = t;
@@ -631,9 +717,52 @@ __device__ void commit(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st,
   *best_out = best;
 }
 
+// one emitting expansion pass over the current tokens (ProcessEmitting):
+// mode 0 = minimum only, 1 = relax below `bound` (+ minimum)
+__device__ float expand_emitting(const DecArgs& a, DecShared& sh, DecPtrs& p, const TokView& tv,
+                                 int ntok, float cutoff, float cost_offset, const float* Lp,
+                                 int mode, float bound, int* examined) {
+  float m = __int_as_float(0x7f800000);
+  for (int c0 = 0; c0 < ntok; c0 += DT) {
+    const int i = c0 + threadIdx.x;
+    int deg = 0, ab = 0;
+    float c = 0.0f;
+    if (i < ntok) {
+      c = tv.c(i);
+      if (c <= cutoff) {
+        const int4 si = a.sinfo[tv.s(i)];
+        ab = si.x;
+        deg = si.y - si.x;
+      }
+    }
+    block_scan(sh, deg);
+    sh.abeg[threadIdx.x] = ab;
+    sh.tcost[threadIdx.x] = c;
+    __syncthreads();
+    const int total = sh.total;
+    *examined += total;
+    for (int it = threadIdx.x; it < total; it += DT) {
+      const int j = owner(sh, it);
+      const int arc = sh.abeg[j] + (it - sh.scan[j]);
+      const int4 A = a.arcs[arc];
+      const float ac = cost_offset - Lp[A.z];
+      const float tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
+      m = fminf(m, tot);
+      if (mode == 1 && tot < bound) {
+        if (relax(a, sh, p, A.x, tot, arc) == 2 && ((unsigned)A.w & kDestEps))
+          push_front(a, sh, p.fa, &sh.n_front0, A.x);
+      }
+    }
+    __syncthreads();
+  }
+  return block_min_f(sh, m);
+}
+
 __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   __shared__ DecShared sh;
   __shared__ float L[kLlhLds];
+  __shared__ int TS[kTokLds];
+  __shared__ float TC[kTokLds];
   const DecJob job = a.jobs[blockIdx.x];
   const int slot = job.slot;
   const long long S = a.num_states;
@@ -645,12 +774,24 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   p.stamp = a.stamp + slot * S;
   p.cs = a.cur_state + (long long)slot * a.max_tok;
   p.cc = a.cur_cost + (long long)slot * a.max_tok;
+  p.cp = a.cur_pos + (long long)slot * a.max_tok;
   p.nl = a.new_list + (long long)slot * a.max_tok;
   p.fa = a.front_a + (long long)slot * a.max_tok;
   p.fb = a.front_b + (long long)slot * a.max_tok;
   p.arena = a.arena + (long long)slot * a.arena_cap;
   if (threadIdx.x == 0) sh.bad = 0;
   int arcs_eps = 0;
+  bool lds = false;
+  // optional phase clocks (diagnostics): thread 0 stamps s_memtime
+  const bool prof = a.prof != nullptr && threadIdx.x == 0;
+  long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tstamp = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#define DEC_PHASE(i)                                                     \
+  if (prof) {                                                            \
+    const long long _t = (long long)__builtin_amdgcn_s_memtime();        \
+    pacc[i] += _t - tstamp;                                              \
+    tstamp = _t;                                                         \
+  }
 
   if (job.reset) {  // InitDecoding: start token, closure with cutoff = beam
     st.ntok = 0;
@@ -665,11 +806,18 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       AG_ST(&p.key[a.start_state], ((unsigned long long)ford(0.0f) << 32) | 0xffffffffu);
       AG_ST(&p.nl[0], a.start_state);
       AG_ST(&p.pos_new[a.start_state], 0);
+      AG_ST(&p.fa[0], a.start_state);
     }
     __syncthreads();
-    eps_closure(a, sh, p, st, a.beam, &arcs_eps);
+    eps_closure(a, sh, p, st, a.beam, 1, &arcs_eps);
     float b;
-    commit(a, sh, p, st, &b);
+    commit(a, sh, p, st, TS, TC, &lds, a.beam, &b);
+  } else if (st.ntok > 0 && st.ntok <= kTokLds) {
+    for (int i = threadIdx.x; i < st.ntok; i += DT) {
+      TS[i] = AG_LD(&p.cs[i]);
+      TC[i] = AG_LD(&p.cc[i]);
+    }
+    lds = true;
   }
 
   for (int f = 0; f < job.nframes; f++) {
@@ -681,11 +829,11 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       Lp = L;
     }
     const int ntok = st.ntok;
+    const TokView tv{p.cs, p.cc, TS, TC, lds};
     // ---- GetCutoff
     unsigned long long bk = kEmpty;
     for (int i = threadIdx.x; i < ntok; i += DT) {
-      const unsigned long long k =
-          ((unsigned long long)ford(AG_LD(&p.cc[i])) << 32) | (unsigned)AG_LD(&p.cs[i]);
+      const unsigned long long k = ((unsigned long long)ford(tv.c(i)) << 32) | (unsigned)tv.s(i);
       bk = k < bk ? k : bk;
     }
     bk = block_min_u64(sh, bk);
@@ -694,13 +842,33 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     const float beam_cutoff = best + a.beam;
     float max_cut = __int_as_float(0x7f800000), min_cut = __int_as_float(0x7f800000);
     float adaptive, cutoff;
-    if (ntok > a.max_active) max_cut = kth_smallest(sh, p.cc, ntok, a.max_active);
+    // The k-th smallest cost is only needed when it can change the outcome:
+    // max_cut < beam_cutoff  <=>  more than max_active costs are < beam_cutoff,
+    // min_cut > beam_cutoff  <=>  at most min_active costs are <= beam_cutoff.
+    bool need_max = ntok > a.max_active, need_min = ntok > a.min_active && a.min_active > 0;
+    if (need_max || need_min) {
+      int lt = 0, le = 0;
+      for (int i = threadIdx.x; i < ntok; i += DT) {
+        const float c = tv.c(i);
+        lt += c < beam_cutoff;
+        le += c <= beam_cutoff;
+      }
+      block_scan(sh, lt);
+      const int n_lt = sh.total;
+      block_scan(sh, le);
+      const int n_le = sh.total;
+      need_max = need_max && n_lt > a.max_active;
+      need_min = need_min && n_le <= a.min_active;
+    }
+    if (need_max) max_cut = kth_smallest(sh, tv, ntok, a.max_active);
     if (max_cut < beam_cutoff) {
       adaptive = max_cut - best + a.beam_delta;
       cutoff = max_cut;
     } else {
       if (ntok > a.min_active)
-        min_cut = a.min_active == 0 ? best : kth_smallest(sh, p.cc, ntok, a.min_active);
+        min_cut = a.min_active == 0 ? best
+                  : need_min ? kth_smallest(sh, tv, ntok, a.min_active)
+                             : beam_cutoff;  // proven <= beam_cutoff: the exact value is unused
       if (min_cut > beam_cutoff) {
         adaptive = min_cut - best + a.beam_delta;
         cutoff = min_cut;
@@ -710,62 +878,54 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       }
     }
     const float cost_offset = -best;
-    // ---- ProcessEmitting: seed from the best token's arcs
-    if (threadIdx.x == 0) {
-      float seed = __int_as_float(0x7f800000);
+    DEC_PHASE(0);
+    // ---- ProcessEmitting: Kaldi's seed from the best token's arcs (wave 0)
+    if (threadIdx.x < 64) {
+      float sd = __int_as_float(0x7f800000);
       const int4 si = a.sinfo[best_state];
-      for (int arc = si.x; arc < si.y; arc++) {
+      for (int arc = si.x + (int)threadIdx.x; arc < si.y; arc += 64) {
         const int4 A = a.arcs[arc];
         const float nw = ((__int_as_float(A.y) + cost_offset) - Lp[A.z]) + best;
-        if (nw + adaptive < seed) seed = nw + adaptive;
+        sd = fminf(sd, nw + adaptive);
       }
-      sh.seed = seed;
-      sh.n_new = 0;
+      sd = wave_min_f(sd);
+      if (threadIdx.x == 0) {
+        sh.seed = sd;
+        sh.n_new = 0;
+        sh.n_front0 = 0;
+      }
     }
-    // pass A: minimum tot over all emitting expansions; pass B: relax
-    float m = __int_as_float(0x7f800000);
-    float next_cutoff = 0.0f;
+    __syncthreads();
+    DEC_PHASE(1);
+    const float seed = sh.seed;
     int examined = 0;
-    for (int pass = 0; pass < 2; pass++) {
-      for (int c0 = 0; c0 < ntok; c0 += DT) {
-        const int i = c0 + threadIdx.x;
-        int deg = 0, ab = 0;
-        float c = 0.0f;
-        if (i < ntok) {
-          c = AG_LD(&p.cc[i]);
-          if (c <= cutoff) {
-            const int4 si = a.sinfo[AG_LD(&p.cs[i])];
-            ab = si.x;
-            deg = si.y - si.x;
-          }
-        }
-        block_scan(sh, deg);
-        sh.abeg[threadIdx.x] = ab;
-        sh.tcost[threadIdx.x] = c;
-        __syncthreads();
-        const int total = sh.total;
-        if (pass == 0) examined += total;
-        for (int it = threadIdx.x; it < total; it += DT) {
-          const int j = owner(sh, it);
-          const int arc = sh.abeg[j] + (it - sh.scan[j]);
-          const int4 A = a.arcs[arc];
-          const float ac = cost_offset - Lp[A.z];
-          const float tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
-          if (pass == 0) m = fminf(m, tot);
-          else if (tot < next_cutoff) relax(a, sh, p, A.x, tot, arc);
-        }
-        __syncthreads();
-      }
-      if (pass == 0) {
-        m = block_min_f(sh, m);
-        next_cutoff = sh.seed;
-        if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
-      }
+    float next_cutoff;
+    if (seed != __int_as_float(0x7f800000)) {
+      // single pass: relax below the seed bound (a superset), then drop the
+      // tokens whose best cost is not below the final next_cutoff -- exactly
+      // the tokens a relax-below-next_cutoff pass creates, with the same keys
+      const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed, &examined);
+      DEC_PHASE(2);
+      next_cutoff = seed;
+      if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
+      // tokens whose best cost is not below next_cutoff stay in the list as
+      // dead entries: never expanded (cost >= cutoff), dropped at commit
+    } else {
+      const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f, &examined);
+      next_cutoff = seed;
+      if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
+      int dummy = 0;
+      expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy);
     }
+    __syncthreads();
+    DEC_PHASE(3);
     // ---- ProcessNonemitting
-    eps_closure(a, sh, p, st, next_cutoff, &arcs_eps);
+    eps_closure(a, sh, p, st, next_cutoff, sh.n_front0, &arcs_eps);
+    DEC_PHASE(4);
     float new_best;
-    commit(a, sh, p, st, &new_best);
+    commit(a, sh, p, st, TS, TC, &lds, next_cutoff, &new_best);
+    DEC_PHASE(5);
+    if (prof) pacc[7]++;
     st.offset_sum += (double)cost_offset;
     st.frames++;
     if (threadIdx.x == 0 && a.stats) {
@@ -788,6 +948,9 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   if (sh.bad) st.err |= sh.bad;
   if (st.ntok == 0 && !st.err) st.err |= 4;
   if (threadIdx.x == 0) a.slots[slot] = st;
+  if (prof)
+    for (int i = 0; i < 8; i++) a.prof[slot * 8 + i] += pacc[i];
+#undef DEC_PHASE
 }
 
 void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s) {
@@ -845,7 +1008,7 @@ __global__ __launch_bounds__(256) void traceback_kernel(TraceArgs a) {
     int* out = a.path + (long long)blockIdx.x * a.path_cap;
     if (endpos >= 0) {
       const int2* arena = a.arena + (long long)slot * a.arena_cap;
-      int k = st.cur_base + endpos;
+      int k = st.cur_base + a.cur_pos[(long long)slot * a.max_tok + endpos];
       while (k >= 0) {
         const int2 e = arena[k];
         if (e.y < 0) break;

@@ -447,6 +447,13 @@ int vamd_engine_decoder_totals(VamdEngine* e, long long* o5) {
   API_CATCH(-1)
 }
 
+int vamd_engine_decoder_phases(VamdEngine* e, long long* o8) {
+  API_TRY
+  e->eng->DecoderPhaseClocks(o8);
+  return 0;
+  API_CATCH(-1)
+}
+
 int vamd_engine_counters(VamdEngine* e, long long* o) {
   API_TRY
   const EngineCounters& c = e->eng->counters();

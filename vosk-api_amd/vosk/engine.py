@@ -38,6 +38,7 @@ _SIGS = {
     "vamd_stream_preload": (C.c_int, [_vp, C.c_int, _vp, C.c_longlong, C.c_int]),
     "vamd_engine_step": (C.c_int, [_vp, _vp, C.c_int]),
     "vamd_engine_decoder_totals": (C.c_int, [_vp, _vp]),
+    "vamd_engine_decoder_phases": (C.c_int, [_vp, _vp]),
     "vamd_engine_set_step_samples": (C.c_int, [_vp, C.c_int]),
     "vamd_engine_stage_times": (C.c_int, [_vp, _vp, _vp, C.c_int]),
 }
@@ -185,6 +186,12 @@ class Engine:
         out = np.zeros(5, np.int64)
         _chk(_c.vamd_engine_decoder_totals(self.h, out.ctypes.data))
         return dict(zip(("frames", "tok_in", "tok_out", "arcs_emit", "arcs_eps"), out.tolist()))
+
+    def decoder_phases(self):
+        out = np.zeros(8, np.int64)
+        _chk(_c.vamd_engine_decoder_phases(self.h, out.ctypes.data))
+        names = ("cutoff", "seed", "expand", "compact", "eps", "commit", "_", "frames")
+        return dict(zip(names, out.tolist()))
 
     def counters(self):
         out = np.zeros(5, np.int64)
