@@ -32,10 +32,14 @@ int vamd_device_count(void);
 
 /* frames_per_chunk <= 0 uses the model's decodable option (default 20->21);
  * flags: 1 = collect per-frame decoder stats, 2 = keep decoded LLH rows,
- *        4 = HIP-event timing of each stage on the engine's stream. */
+ *        4 = HIP-event timing of each stage on the engine's stream,
+ *        8 = two-stream pipeline (decoder of step i-1 beside the nnet of step
+ *            i; decoder results lag one step, vamd_engine_flush drains). */
 VamdEngine *vamd_engine_new(const char *model_dir, int frames_per_chunk, int max_streams,
                             int flags);
 void vamd_engine_free(VamdEngine *e);
+/* pipeline mode: run the pending decoder step (no-op otherwise) */
+int vamd_engine_flush(VamdEngine *e);
 /* human-readable nnet plan / engine description (owned by the engine) */
 const char *vamd_engine_describe(VamdEngine *e);
 /* plan facts: [fpc, fss, left_ctx, right_ctx, priming, out_dim, ops, ring] */

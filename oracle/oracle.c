@@ -40,6 +40,16 @@ int orc_mfcc_num_frames(const orc_mfcc_opts* o, long n) {
 
 /* natural log, x > 0 normal: log(m*2^e) = e*ln2 + log1p(m-1),
    m in [sqrt(.5), sqrt(2)); log1p via a degree-10 polynomial (Horner fmaf) */
+/* Canonical affine summation order shared with the GPU engine
+   (vosk-api_amd/csrc/nnet_plan.h GemmKSlices / kernels.hip): K is cut into
+   orc_kslices(K) equal slices, slice sums added left to right.  Inside a
+   slice the fmaf chain starts from 0 and walks each aligned group of eight k
+   as 0,4,1,5,2,6,3,7 (the pair order in which a 32x32x2 MFMA fed with one
+   float4 per lane accumulates).  Kaldi's own order is whatever its BLAS does
+   (matrix/kaldi-matrix.cc AddMatMat -> cblas_sgemm), so any fixed order is a
+   faithful restatement of the arithmetic. */
+int orc_kslices(int K) { return (K >= 512 && K % 256 == 0) ? K / 256 : 1; }
+
 float orc_logf(float x) {
   static const float C[11] = {1.000000000e+00f, -5.000000000e-01f, 3.333330154e-01f,
                               -2.500002384e-01f, 2.000257671e-01f, -1.666804254e-01f,
@@ -326,6 +336,7 @@ int orc_nnet_forward(const orc_net* net, const float* feats, int T, float* out) 
 
   float* xb = (float*)malloc(sizeof(float) * (size_t)ORC_TB * (maxk + 1));
   float* acc = (float*)malloc(sizeof(float) * (size_t)ORC_TB * (maxd + 1));
+  float* part = (float*)malloc(sizeof(float) * (size_t)ORC_TB * (maxd + 1));
   int tlist[ORC_TB];
   for (int i = 1; i < NN; i++) {
     const int D = net->dim[i], ID = net->in_dim[i];
@@ -355,13 +366,25 @@ int orc_nnet_forward(const orc_net* net, const float* feats, int T, float* out) 
         const float* x = xb + (size_t)b * K;
         float* y = nv[i].v + (size_t)(tlist[b] - nv[i].lo) * D;
         switch (net->kind[i]) {
-          case 1: { /* affine: y = (fmaf chain over k, from 0) + b */
+          case 1: { /* affine: y = (sum over k-slices of fmaf chains from 0) + b */
             float* a = acc + (size_t)b * D;
-            for (int n = 0; n < D; n++) a[n] = 0.0f;
-            for (int k = 0; k < K; k++) {
-              const float xk = x[k];
-              const float* w = WT + (size_t)k * D;
-              for (int n = 0; n < D; n++) a[n] = fmaf(xk, w[n], a[n]);
+            float* p = part + (size_t)b * D;
+            const int ns = orc_kslices(K), kw = K / ns;
+            for (int z = 0; z < ns; z++) {
+              for (int n = 0; n < D; n++) p[n] = 0.0f;
+              const int ke = (z + 1) * kw;
+              for (int kg = z * kw; kg < ke; kg += 8) {
+                for (int i = 0; i < 8 && kg + i < ke; i++) {
+                  /* 0,4,1,5,2,6,3,7 in a full group; a (GPU-unsupported)
+                     partial tail group is walked in order */
+                  const int k = kg + 8 <= ke ? kg + ((i & 1) << 2) + (i >> 1) : kg + i;
+                  const float xk = x[k];
+                  const float* w = WT + (size_t)k * D;
+                  for (int n = 0; n < D; n++) p[n] = fmaf(xk, w[n], p[n]);
+                }
+              }
+              if (z == 0) memcpy(a, p, sizeof(float) * D);
+              else for (int n = 0; n < D; n++) a[n] = a[n] + p[n];
             }
             const float* B = net->b_off[i] >= 0 ? net->params + net->b_off[i] : NULL;
             if (B) for (int n = 0; n < D; n++) y[n] = a[n] + B[n];
@@ -390,7 +413,7 @@ int orc_nnet_forward(const orc_net* net, const float* feats, int T, float* out) 
     for (int n = 0; n < OD; n++) out[(size_t)j * OD + n] = v[n] * net->acoustic_scale;
   }
   for (int i = 1; i < NN; i++) { free(nv[i].v); free(need[i]); }
-  free(nv); free(need); free(xb); free(acc);
+  free(nv); free(need); free(xb); free(acc); free(part);
   return rows;
 }
 

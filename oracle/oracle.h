@@ -36,6 +36,7 @@ typedef struct {
 int orc_mfcc_num_frames(const orc_mfcc_opts* o, long num_samples);
 /* wave: float samples (int16 range).  out: [frames][num_ceps]. returns frames */
 int orc_mfcc(const orc_mfcc_opts* o, const float* wave, long num_samples, float* out);
+int orc_kslices(int K);
 float orc_logf(float x);
 
 /* ---------------- nnet3 forward (whole utterance, edge-replicated input) ---- */

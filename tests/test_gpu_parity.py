@@ -108,6 +108,30 @@ def test_batched_streams_match_oracle(synth_model, oracle, test_wave):
         np.testing.assert_array_equal(arcs, r["path"], err_msg=f"stream {k}")
 
 
+def test_pipelined_steps_match_oracle(synth_model, oracle, test_wave):
+    """Two-stream pipeline (bench.py's mode): HBM-preloaded audio, one chunk
+    per stream per step, the decoder of step i-1 beside the nnet of step i;
+    transcripts and every decoded LLH row identical to the oracle."""
+    from vosk import engine
+    n = 6
+    e = engine.Engine(synth_model, frames_per_chunk=51, max_streams=n, keep_llh=True,
+                      pipeline=True)
+    e.set_step_samples(51 * 160)
+    waves = [perturbed_stream(test_wave, i, seconds=2.5 + 0.41 * i) for i in range(n)]
+    ss = [e.new_stream() for _ in range(n)]
+    for s, w in zip(ss, waves):
+        e.preload(s, w, finished=True)
+    steps = 0
+    while e.step(ss):
+        steps += 1
+        assert steps < 1000
+    for k in range(n):
+        r = oracle.recognize(waves[k])
+        np.testing.assert_array_equal(e.llh(ss[k]), oracle.loglikes(waves[k]), err_msg=f"llh {k}")
+        arcs, _, _ = e.best_path(ss[k], use_final=True)
+        np.testing.assert_array_equal(arcs, r["path"], err_msg=f"stream {k}")
+
+
 @pytest.mark.parametrize("nsamples", [0, 100, 399, 400, 1000, 16000])
 def test_short_inputs(synth_model, oracle, test_wave, nsamples):
     e = _engine(synth_model)

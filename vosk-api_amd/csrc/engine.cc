@@ -131,6 +131,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     VAMD_ERR("no HIP device available: the MI355X engine requires a GPU (there is no CPU fallback)");
   HIPCHECK(hipSetDevice(cfg_.device));
   HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  HIPCHECK(hipStreamCreateWithFlags(&dstream_, hipStreamNonBlocking));
   const ModelData& m = *md_;
   const int fss = m.dcb.frame_subsampling_factor;
   int fpc = cfg_.frames_per_chunk;
@@ -245,6 +246,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   rings_.dim = d_ring_dims_;
   rings_.mask = ring_ - 1;
   rings_.ring = ring_;
+  rings_.slots = S;
   rings_.input_node = plan_.input_node;
   d_samples_ = (float*)DevAlloc(sizeof(float) * (size_t)S * sample_ring_);
 
@@ -280,6 +282,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
         if (s.col0 % bk || s.dim % bk) VAMD_ERR("op " << op.name << ": K segments must be multiples of 8");
       }
       if (op.K % 4) VAMD_ERR("op " << op.name << ": K must be a multiple of 4");
+      a.kslices = GemmKSlices(op.K);
+      if (op.K % 8) VAMD_ERR("op " << op.name << ": K must be a multiple of 8");
+      if (a.kslices > 1 && !GemmStreamable(a))
+        VAMD_ERR("op " << op.name << ": split-K op must fit the streaming GEMM kernel");
     } else {
       a.nparts = (int)op.parts.size();
       if (a.nparts > kMaxParts) VAMD_ERR("too many descriptor parts in op " << op.name);
@@ -352,7 +358,9 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   const long long NS = g.NumStates();
   max_jobs_ = S * jobs_per_slot_;
   max_dec_frames_ = max_jobs_ * plan_.opc;
-  d_llh_ = (float*)DevAlloc(sizeof(float) * (size_t)max_jobs_ * plan_.opc * plan_.out_dim);
+  for (int i = 0; i < 2; i++)
+    d_llh_buf_[i] = (float*)DevAlloc(sizeof(float) * (size_t)max_jobs_ * plan_.opc * plan_.out_dim);
+  d_llh_ = d_llh_buf_[0];
   dec_.sinfo = d_sinfo_;
   dec_.arcs = d_arcs_;
   dec_.num_states = (int)NS;
@@ -393,8 +401,9 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   stage_bytes_ = Align256(sizeof(float) * (size_t)S * cfg_.max_step_samples) +
                  Align256(sizeof(SampleJob) * S) + Align256(sizeof(MfccJob) * S) +
                  Align256(sizeof(DevJob) * max_jobs_) + Align256(sizeof(DecJob) * S) + 1024;
-  HIPCHECK(hipHostMalloc((void**)&h_stage_, stage_bytes_, hipHostMallocDefault));
-  d_stage_ = (char*)DevAlloc(stage_bytes_);
+  // two halves: a pipelined decoder batch keeps its jobs while the next step stages
+  HIPCHECK(hipHostMalloc((void**)&h_stage_, 2 * stage_bytes_, hipHostMallocDefault));
+  d_stage_ = (char*)DevAlloc(2 * stage_bytes_);
   HIPCHECK(hipHostMalloc((void**)&h_slots_, sizeof(DecSlot) * S, hipHostMallocDefault));
   HIPCHECK(hipHostMalloc((void**)&h_stats_, sizeof(FrameStat) * max_dec_frames_, hipHostMallocDefault));
   for (auto& ev : ev_) HIPCHECK(hipEventCreate(&ev));
@@ -406,16 +415,18 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
 }
 
 Engine::~Engine() {
-  if (stream_) hipStreamSynchronize(stream_);
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  if (dstream_) (void)hipStreamSynchronize(dstream_);
   for (auto& ev : ev_)
-    if (ev) hipEventDestroy(ev);
+    if (ev) (void)hipEventDestroy(ev);
   for (auto& h : slots_)
-    if (h.resident) hipFree(h.resident);
-  for (void* p : dev_allocs_) hipFree(p);
-  if (h_stage_) hipHostFree(h_stage_);
-  if (h_slots_) hipHostFree(h_slots_);
-  if (h_stats_) hipHostFree(h_stats_);
-  if (stream_) hipStreamDestroy(stream_);
+    if (h.resident) (void)hipFree(h.resident);
+  for (void* p : dev_allocs_) (void)hipFree(p);
+  if (h_stage_) (void)hipHostFree(h_stage_);
+  if (h_slots_) (void)hipHostFree(h_slots_);
+  if (h_stats_) (void)hipHostFree(h_stats_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+  if (dstream_) (void)hipStreamDestroy(dstream_);
 }
 
 int Engine::AllocSlot() {
@@ -432,11 +443,13 @@ int Engine::AllocSlot() {
 
 void Engine::FreeSlot(int slot) {
   std::lock_guard<std::mutex> lk(mu_);
+  FlushLocked();
   slots_.at(slot).used = false;
 }
 
 void Engine::ResetPipeline(int slot) {
   std::lock_guard<std::mutex> lk(mu_);
+  FlushLocked();
   SlotHost& h = slots_.at(slot);
   h.pending.clear();
   h.pending_pos = 0;
@@ -448,7 +461,7 @@ void Engine::ResetPipeline(int slot) {
   h.finished = false;
   h.need_reset = true;
   h.err = 0;
-  if (h.resident) hipFree(h.resident);
+  if (h.resident) (void)hipFree(h.resident);
   h.resident = nullptr;
   h.resident_n = h.resident_pos = 0;
   h.resident_finish = false;
@@ -456,6 +469,7 @@ void Engine::ResetPipeline(int slot) {
 
 void Engine::ResetDecoder(int slot) {
   std::lock_guard<std::mutex> lk(mu_);
+  FlushLocked();
   SlotHost& h = slots_.at(slot);
   h.decoded = 0;
   h.need_reset = true;
@@ -476,7 +490,7 @@ void Engine::PreloadSamples(int slot, const float* x, long long n, bool finished
   std::lock_guard<std::mutex> lk(mu_);
   SlotHost& h = slots_.at(slot);
   if (h.resident && h.resident_pos < h.resident_n) VAMD_ERR("previous preloaded audio not consumed");
-  if (h.resident) hipFree(h.resident);
+  if (h.resident) (void)hipFree(h.resident);
   h.resident = nullptr;
   HIPCHECK(hipMalloc((void**)&h.resident, sizeof(float) * std::max<long long>(n, 1)));
   if (n) HIPCHECK(hipMemcpy(h.resident, x, sizeof(float) * n, hipMemcpyHostToDevice));
@@ -514,7 +528,6 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
   for (int s : slots) {
     SlotHost& h = slots_.at(s);
     if (!h.used) continue;
-    h.stats.clear();
     // 1. samples: HBM-resident audio first, then host-fed samples
     if (h.resident && h.resident_pos < h.resident_n) {
       int n = (int)std::min<long long>(h.resident_n - h.resident_pos, cfg_.max_step_samples);
@@ -577,6 +590,7 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
         if (h.need_reset) h.decoded = 0;
         h.need_reset = false;
         h.decoded += dec_frames;
+        h.decoded_at_build = h.decoded;
         any = true;
       }
     }
@@ -584,102 +598,41 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
   return any;
 }
 
-void Engine::RunStep() {
-  // pack the step's inputs into one pinned buffer -> one H2D copy
-  size_t off = 0;
-  auto put = [&](const void* src, size_t bytes) {
-    size_t o = off;
-    if (bytes) memcpy(h_stage_ + o, src, bytes);
-    off += Align256(bytes);
-    return o;
-  };
-  size_t o_data = put(st_sample_data_.data(), sizeof(float) * st_sample_data_.size());
-  for (size_t i = 0; i < st_samples_.size(); i++)
-    if (st_sample_src_[i] >= 0)
-      st_samples_[i].src = (const float*)(d_stage_ + o_data) + st_sample_src_[i];
-  size_t o_sj = put(st_samples_.data(), sizeof(SampleJob) * st_samples_.size());
-  size_t o_mj = put(st_mfcc_.data(), sizeof(MfccJob) * st_mfcc_.size());
-  size_t o_dj = put(st_jobs_.data(), sizeof(DevJob) * st_jobs_.size());
-  size_t o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
-  if (off > stage_bytes_) VAMD_ERR("step staging overflow");
-  const bool tk = cfg_.time_kernels;
-  if (tk) HIPCHECK(hipEventRecord(ev_[0], stream_));
-  HIPCHECK(hipMemcpyAsync(d_stage_, h_stage_, off, hipMemcpyHostToDevice, stream_));
-  int launches = 0;
-  if (tk) HIPCHECK(hipEventRecord(ev_[1], stream_));
-  LaunchAppendSamples((const SampleJob*)(d_stage_ + o_sj), (int)st_samples_.size(), d_samples_,
-                      sample_ring_, stream_);
-  launches += !st_samples_.empty();
-  LaunchMfcc(mfcc_, (const MfccJob*)(d_stage_ + o_mj), (int)st_mfcc_.size(), st_mfcc_total_,
-             d_samples_, sample_ring_, rings_, stream_);
-  launches += st_mfcc_total_ > 0;
-  if (tk) HIPCHECK(hipEventRecord(ev_[2], stream_));
-  const int l_front = launches;
-  if (!st_jobs_.empty()) {
-    const DevJob* dj = (const DevJob*)(d_stage_ + o_dj);
-    for (size_t i = 0; i < plan_.ops.size(); i++) {
-      NnetOpArgs a = op_args_[i];
-      a.M = (int)st_jobs_.size() * a.P;
-      a.jobs = dj;
-      a.llh = d_llh_;
-      if (plan_.ops[i].kind == Op::GEMM) LaunchNnetGemm(a, op_bk_[i], stream_);
-      else LaunchNnetGather(a, stream_);
-      launches++;
-    }
-  }
-  if (tk) HIPCHECK(hipEventRecord(ev_[3], stream_));
-  const int l_nnet = launches - l_front;
-  if (!st_dec_.empty()) {
-    DecArgs d = dec_;
-    d.jobs = (const DecJob*)(d_stage_ + o_ej);
-    LaunchDecode(d, (int)st_dec_.size(), stream_);
-    launches++;
-  }
-  if (tk) HIPCHECK(hipEventRecord(ev_[4], stream_));
-  if (!st_dec_.empty()) {
-    HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(),
-                            hipMemcpyDeviceToHost, stream_));
-    int rows = 0;
-    for (auto& j : st_dec_) rows += j.nframes;
-    if (cfg_.collect_stats && rows)
-      HIPCHECK(hipMemcpyAsync(h_stats_, d_stats_, sizeof(FrameStat) * rows,
-                              hipMemcpyDeviceToHost, stream_));
-  }
-  HIPCHECK(hipGetLastError());
-  HIPCHECK(hipStreamSynchronize(stream_));
-  if (tk) {
-    float a = 0, b = 0, c = 0, t = 0;
-    HIPCHECK(hipEventElapsedTime(&a, ev_[1], ev_[2]));
-    HIPCHECK(hipEventElapsedTime(&b, ev_[2], ev_[3]));
-    HIPCHECK(hipEventElapsedTime(&c, ev_[3], ev_[4]));
-    HIPCHECK(hipEventElapsedTime(&t, ev_[0], ev_[4]));
-    times_.ms[0] += a; times_.ms[1] += b; times_.ms[2] += c; times_.ms[3] += t;
-    times_.launches[0] += l_front;
-    times_.launches[1] += l_nnet;
-    times_.launches[2] += st_dec_.empty() ? 0 : 1;
-    times_.launches[3] += 1;
-  }
-  counters_.steps++;
-  counters_.launches += launches;
-  counters_.frames_mfcc += st_mfcc_total_;
-  counters_.chunk_jobs += st_jobs_.size();
-  for (auto& j : st_dec_) {
+void Engine::LaunchDecodeBatch(const DecBatch& b, hipStream_t s) {
+  if (b.jobs.empty()) return;
+  DecArgs d = dec_;
+  d.jobs = (const DecJob*)(d_stage_ + (size_t)b.half * stage_bytes_ + b.o_ej);
+  d.llh = d_llh_buf_[b.half];
+  LaunchDecode(d, (int)b.jobs.size(), s);
+  HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(),
+                          hipMemcpyDeviceToHost, s));
+  int rows = 0;
+  for (auto& j : b.jobs) rows += j.nframes;
+  if (cfg_.collect_stats && rows)
+    HIPCHECK(hipMemcpyAsync(h_stats_, d_stats_, sizeof(FrameStat) * rows, hipMemcpyDeviceToHost, s));
+  counters_.launches++;
+}
+
+// Host side of a finished decoder launch (its stream has been synchronized).
+void Engine::FinishDecodeBatch(const DecBatch& b) {
+  for (size_t i = 0; i < b.jobs.size(); i++) {
+    const DecJob& j = b.jobs[i];
     SlotHost& h = slots_[j.slot];
     const DecSlot& ds = h_slots_[j.slot];
-    if (ds.frames != h.decoded)
+    if (ds.frames != b.expect[i])
       VAMD_WARN("decoder frame count mismatch on slot " << j.slot << ": " << ds.frames << " vs "
-                                                         << h.decoded);
+                                                         << b.expect[i]);
     h.err = ds.err;
     if (ds.err) VAMD_WARN("decoder error flags " << ds.err << " on stream slot " << j.slot);
     counters_.frames_decoded += j.nframes;
     if (cfg_.collect_llh && j.nframes) {
       size_t n = (size_t)j.nframes * plan_.out_dim, o = h.llh.size();
       h.llh.resize(o + n);
-      HIPCHECK(hipMemcpy(h.llh.data() + o, d_llh_ + (size_t)j.llh_row0 * plan_.out_dim,
+      HIPCHECK(hipMemcpy(h.llh.data() + o, d_llh_buf_[b.half] + (size_t)j.llh_row0 * plan_.out_dim,
                          sizeof(float) * n, hipMemcpyDeviceToHost));
     }
     if (cfg_.collect_stats) {
-      h.stats.insert(h.stats.end(), h_stats_ + j.stats_row0, h_stats_ + j.stats_row0 + j.nframes);
+      h.stats.assign(h_stats_ + j.stats_row0, h_stats_ + j.stats_row0 + j.nframes);
       for (int f = 0; f < j.nframes; f++) {
         const FrameStat& fs = h_stats_[j.stats_row0 + f];
         times_.dec[0]++;
@@ -692,14 +645,131 @@ void Engine::RunStep() {
   }
 }
 
+// One step: stage inputs (one pinned H2D copy), samples -> MFCC -> nnet ops on
+// the main stream; the decoder runs this step's LLH in order (no pipeline) or
+// the previous step's LLH concurrently on the decoder stream (pipeline).
+void Engine::RunStep(bool allow_pipeline) {
+  const bool pipe = cfg_.pipeline && allow_pipeline;
+  if (!pipe) FlushLocked();
+  const int hf = half_;
+  char* hs = h_stage_ + (size_t)hf * stage_bytes_;
+  char* dsg = d_stage_ + (size_t)hf * stage_bytes_;
+  size_t off = 0;
+  auto put = [&](const void* src, size_t bytes) {
+    size_t o = off;
+    if (bytes) memcpy(hs + o, src, bytes);
+    off += Align256(bytes);
+    return o;
+  };
+  size_t o_data = put(st_sample_data_.data(), sizeof(float) * st_sample_data_.size());
+  for (size_t i = 0; i < st_samples_.size(); i++)
+    if (st_sample_src_[i] >= 0)
+      st_samples_[i].src = (const float*)(dsg + o_data) + st_sample_src_[i];
+  size_t o_sj = put(st_samples_.data(), sizeof(SampleJob) * st_samples_.size());
+  size_t o_mj = put(st_mfcc_.data(), sizeof(MfccJob) * st_mfcc_.size());
+  size_t o_dj = put(st_jobs_.data(), sizeof(DevJob) * st_jobs_.size());
+  DecBatch cur;
+  cur.jobs = st_dec_;
+  cur.o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
+  cur.half = hf;
+  for (auto& j : st_dec_) cur.expect.push_back(slots_[j.slot].decoded_at_build);
+  if (off > stage_bytes_) VAMD_ERR("step staging overflow");
+  const bool tk = cfg_.time_kernels;
+  if (tk) HIPCHECK(hipEventRecord(ev_[0], stream_));
+  HIPCHECK(hipMemcpyAsync(dsg, hs, off, hipMemcpyHostToDevice, stream_));
+  int launches = 0;
+  if (tk) HIPCHECK(hipEventRecord(ev_[1], stream_));
+  LaunchAppendSamples((const SampleJob*)(dsg + o_sj), (int)st_samples_.size(), d_samples_,
+                      sample_ring_, stream_);
+  launches += !st_samples_.empty();
+  LaunchMfcc(mfcc_, (const MfccJob*)(dsg + o_mj), (int)st_mfcc_.size(), st_mfcc_total_,
+             d_samples_, sample_ring_, rings_, stream_);
+  launches += st_mfcc_total_ > 0;
+  if (tk) HIPCHECK(hipEventRecord(ev_[2], stream_));
+  const int l_front = launches;
+  if (!st_jobs_.empty()) {
+    const DevJob* dj = (const DevJob*)(dsg + o_dj);
+    for (size_t i = 0; i < plan_.ops.size(); i++) {
+      NnetOpArgs a = op_args_[i];
+      a.M = (int)st_jobs_.size() * a.P;
+      a.jobs = dj;
+      a.llh = d_llh_buf_[hf];
+      if (plan_.ops[i].kind == Op::GEMM) LaunchNnetGemm(a, op_bk_[i], stream_);
+      else LaunchNnetGather(a, stream_);
+      launches++;
+    }
+  }
+  if (tk) HIPCHECK(hipEventRecord(ev_[3], stream_));
+  const int l_nnet = launches - l_front;
+  // decoder: this step's batch in order, or the previous one beside the nnet
+  const DecBatch* db = nullptr;
+  hipStream_t dst = stream_;
+  if (!pipe) {
+    if (!cur.jobs.empty()) db = &cur;
+  } else if (pend_active_) {
+    db = &pend_;
+    dst = dstream_;
+    if (tk) HIPCHECK(hipStreamWaitEvent(dstream_, ev_[0], 0));
+  }
+  if (tk) HIPCHECK(hipEventRecord(ev_[5], dst));
+  if (db) LaunchDecodeBatch(*db, dst);
+  if (tk) HIPCHECK(hipEventRecord(ev_[6], dst));
+  if (tk) HIPCHECK(hipEventRecord(ev_[4], stream_));
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(stream_));
+  if (pipe) HIPCHECK(hipStreamSynchronize(dstream_));
+  if (tk) {
+    float a = 0, b = 0, c = 0, t = 0, t2 = 0;
+    HIPCHECK(hipEventElapsedTime(&a, ev_[1], ev_[2]));
+    HIPCHECK(hipEventElapsedTime(&b, ev_[2], ev_[3]));
+    HIPCHECK(hipEventElapsedTime(&c, ev_[5], ev_[6]));
+    HIPCHECK(hipEventElapsedTime(&t, ev_[0], ev_[4]));
+    HIPCHECK(hipEventElapsedTime(&t2, ev_[0], ev_[6]));
+    times_.ms[0] += a; times_.ms[1] += b; times_.ms[2] += c; times_.ms[3] += std::max(t, t2);
+    times_.launches[0] += l_front;
+    times_.launches[1] += l_nnet;
+    times_.launches[2] += db ? 1 : 0;
+    times_.launches[3] += 1;
+  }
+  counters_.steps++;
+  counters_.launches += launches;
+  counters_.frames_mfcc += st_mfcc_total_;
+  counters_.chunk_jobs += st_jobs_.size();
+  if (db) FinishDecodeBatch(*db);
+  half_ ^= 1;
+  if (pipe) {
+    pend_active_ = !cur.jobs.empty();
+    if (pend_active_) pend_ = std::move(cur);
+  }
+}
+
 void Engine::Advance(const std::vector<int>& slots) {
   std::lock_guard<std::mutex> lk(mu_);
   while (BuildStep(slots)) RunStep();
+  FlushLocked();
+}
+
+void Engine::Flush() {
+  std::lock_guard<std::mutex> lk(mu_);
+  FlushLocked();
+}
+
+void Engine::FlushLocked() {
+  if (!pend_active_) return;
+  pend_active_ = false;
+  LaunchDecodeBatch(pend_, dstream_);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(dstream_));
+  FinishDecodeBatch(pend_);
 }
 
 bool Engine::Step(const std::vector<int>& slots) {
   std::lock_guard<std::mutex> lk(mu_);
-  if (!BuildStep(slots)) return false;
+  if (!BuildStep(slots)) {
+    if (!pend_active_) return false;
+    FlushLocked();  // pipeline tail: only the pending decoder batch is left
+    return true;
+  }
   RunStep();
   return true;
 }
@@ -707,6 +777,7 @@ bool Engine::Step(const std::vector<int>& slots) {
 void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
                        std::vector<PathResult>* out) {
   std::lock_guard<std::mutex> lk(mu_);
+  FlushLocked();
   out->assign(slots.size(), PathResult());
   if (slots.empty()) return;
   int maxf = 0;
@@ -773,6 +844,7 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
 
 void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset) {
   std::lock_guard<std::mutex> lk(mu_);
+  FlushLocked();
   SlotHost& h = slots_.at(slot);
   const int P = plan_.out_dim;
   int done = 0;
@@ -795,7 +867,8 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     if (rs) h.decoded = 0;
     h.need_reset = false;
     h.decoded += n;
-    RunStep();
+    h.decoded_at_build = h.decoded;
+    RunStep(false);
     done += n;
     first = false;
   }
@@ -803,6 +876,7 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
 
 void Engine::DecoderPhaseClocks(long long* out8) {
   std::lock_guard<std::mutex> lk(mu_);
+  FlushLocked();
   for (int i = 0; i < 8; i++) out8[i] = 0;
   if (!dec_.prof) return;
   std::vector<long long> h((size_t)8 * slots_.size());
@@ -817,8 +891,9 @@ void Engine::DebugFeatures(int slot, int first, int n, std::vector<float>* out) 
   std::vector<float> ring((size_t)ring_ * dim);
   float* base = nullptr;
   HIPCHECK(hipMemcpy(&base, d_ring_ptrs_ + plan_.input_node, sizeof(float*), hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy(ring.data(), base + (size_t)slot * ring_ * dim, sizeof(float) * ring.size(),
-                     hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy2D(ring.data(), sizeof(float) * dim, base + (size_t)slot * dim,
+                       sizeof(float) * dim * cfg_.max_slots, sizeof(float) * dim, ring_,
+                       hipMemcpyDeviceToHost));
   out->resize((size_t)n * dim);
   for (int i = 0; i < n; i++)
     memcpy(out->data() + (size_t)i * dim, ring.data() + (size_t)((first + i) & (ring_ - 1)) * dim,

@@ -52,6 +52,11 @@ struct EngineConfig {
   bool collect_stats = false;
   bool collect_llh = false;  // tests: keep a host copy of every decoded LLH row
   bool time_kernels = false; // HIP-event timing of each stage on the engine stream
+  // Two-stream pipeline: step i runs samples+MFCC+nnet of step i on the main
+  // stream while the decoder consumes step i-1's log-likelihoods on a second
+  // stream (double-buffered LLH + staging).  Decoder results lag one step;
+  // every call that reads or resets decoder state drains the pipeline first.
+  bool pipeline = false;
 };
 
 // HIP-event times accumulated on the engine stream (time_kernels).
@@ -103,8 +108,11 @@ class Engine {
   const StageTimes& stage_times() const { return times_; }
   void ResetStageTimes() { times_ = StageTimes(); }
   void InputFinished(int slot);
-  // Runs batched steps until the given streams have no runnable work.
+  // Runs batched steps until the given streams have no runnable work
+  // (drains the pipeline).
   void Advance(const std::vector<int>& slots);
+  // Pipeline mode: runs the pending decoder step, if any.
+  void Flush();
   int NumFramesDecoded(int slot) const;
   int NumFramesReady(int slot) const;  // output frames available to the decoder
   bool InputIsFinished(int slot) const;
@@ -133,7 +141,8 @@ class Engine {
     int frames = 0;          // MFCC frames computed
     int next_chunk = 0;      // next chunk index (negative while priming)
     int out_ready = 0;       // output frames computed
-    int decoded = 0;         // frames decoded since the decoder reset
+    int decoded = 0;         // frames decoded since the decoder reset (incl. a pending batch)
+    int decoded_at_build = 0;
     bool finished = false;
     bool need_reset = true;
     int err = 0;
@@ -143,8 +152,17 @@ class Engine {
     long long resident_n = 0, resident_pos = 0;
     bool resident_finish = false;
   };
+  struct DecBatch {  // one decoder launch's jobs, staged in one staging half
+    std::vector<DecJob> jobs;
+    std::vector<int> expect;  // decoded-frame count each job's slot must reach
+    size_t o_ej = 0;
+    int half = 0;
+  };
   bool BuildStep(const std::vector<int>& slots);
-  void RunStep();
+  void RunStep(bool allow_pipeline = true);
+  void LaunchDecodeBatch(const DecBatch& b, hipStream_t s);
+  void FinishDecodeBatch(const DecBatch& b);
+  void FlushLocked();
   int NumFramesFor(long long samples) const;
 
   std::shared_ptr<const ModelData> md_;
@@ -152,11 +170,15 @@ class Engine {
   NnetPlan plan_;
   std::mutex mu_;
   hipStream_t stream_ = nullptr;
+  hipStream_t dstream_ = nullptr;  // decoder stream (pipeline mode)
   int ring_ = 0, sample_ring_ = 0, jobs_per_slot_ = 0;
   std::vector<SlotHost> slots_;
   EngineCounters counters_;
   StageTimes times_;
-  hipEvent_t ev_[5] = {};
+  hipEvent_t ev_[7] = {};
+  int half_ = 0;            // staging + LLH half of the step being built
+  bool pend_active_ = false;
+  DecBatch pend_;           // pipeline mode: decoder batch waiting for the next step
 
   // device: model
   MfccDev mfcc_{};
@@ -170,7 +192,8 @@ class Engine {
   int4* d_arcs_ = nullptr;
   // device: per-stream state
   float* d_samples_ = nullptr;
-  float* d_llh_ = nullptr;
+  float* d_llh_ = nullptr;  // = d_llh_buf_[0]
+  float* d_llh_buf_[2] = {nullptr, nullptr};
   DecArgs dec_{};
   DecSlot* d_slots_ = nullptr;
   FrameStat* d_stats_ = nullptr;

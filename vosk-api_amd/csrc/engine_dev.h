@@ -26,10 +26,12 @@ struct DevInstr { const float* base; int op, ldim, is_input, offset, src_col; fl
 struct DevPart { int col0, dim, instr0, ninstr; };
 
 struct RingSet {
-  float* const* base;  // per stored node: [slots][ring][dim]
+  float* const* base;  // per stored node: [ring][slots][dim] (time-major: the rows
+                       // of one frame for all streams are adjacent in HBM)
   const int* dim;      // per stored node
   int mask;            // ring - 1 (power of two)
   int ring;
+  int slots;
   int input_node;
 };
 
@@ -45,6 +47,7 @@ struct NnetOpArgs {
   int out_ldim;
   float* llh;              // [M][N] when out_node < 0
   int nsegs, nstages, nparts;
+  int kslices;             // K split into equal slices reduced in fixed order (GemmKSlices)
   DevSeg segs[kMaxSegs];
   DevStage stages[kMaxStages];
   DevPart parts[kMaxParts];

@@ -12,8 +12,12 @@ void LaunchAppendSamples(const SampleJob* jobs, int njobs, float* ring, int ring
 void LaunchMfcc(const MfccDev& m, const MfccJob* jobs, int njobs, int total_frames,
                 const float* sample_ring, int sample_ring_len, const RingSet& rings,
                 hipStream_t s);
-// GEMM ops: bk = K-step (8, 16 or 32; must divide every segment boundary)
+// GEMM ops: bk = LDS-kernel K-step (8, 16 or 32; must divide every segment boundary)
+// N tile width LaunchNnetGemm uses for an N-column op
+inline int GemmTileN(int N) { return (N % 96 == 0 && N % 64 != 0) ? 96 : 64; }
 void LaunchNnetGemm(const NnetOpArgs& a, int bk, hipStream_t s);
+bool GemmStreamable(const NnetOpArgs& a);  // streaming kernel applies (else LDS kernel)
+extern int g_gemm_variant;  // dev override: 1/2 streaming NB=natural/1, 3 LDS (tools/gemm_bench)
 void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s);
 void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s);
 void LaunchTraceback(const TraceArgs& a, int n, hipStream_t s);

@@ -15,7 +15,7 @@
 //                   staged in LDS) with fused bias/ReLU/BatchNorm/bypass
 //                   epilogue (nnet3 components [K]; src/model.cc:233-246)
 //   nnet_gather     descriptor evaluation (Append/Sum/Scale/Offset)
-//   decode          one 1024-thread workgroup per stream, persistent over the
+//   decode          one 512-thread workgroup per stream, persistent over the
 //                   chunk's frames: exact max-active cutoff by LDS radix
 //                   select, load-balanced (token, arc) expansion, 64-bit
 //                   atomicMin token recombination, epsilon closure by rounds
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void mfcc_kernel(MfccDev m, const MfccJob* job
     if (m.use_energy && lane == 0) out = SC[w][1];
     const int in = rings.input_node;
     float* dst = rings.base[in] +
-                 ((size_t)slot * rings.ring + (frame & rings.mask)) * rings.dim[in];
+                 ((size_t)(frame & rings.mask) * rings.slots + slot) * rings.dim[in];
     dst[lane] = out;
   }
 }
@@ -218,7 +218,7 @@ __device__ __forceinline__ const float* ring_at(const float* base, int ldim, int
     if (tau < 0) tau = 0;
     if (tau > clamp_max) tau = clamp_max;
   }
-  return base + ((size_t)slot * r.ring + (tau & r.mask)) * ldim;
+  return base + ((size_t)(tau & r.mask) * r.slots + slot) * ldim;
 }
 
 __device__ __forceinline__ float apply_stages(const NnetOpArgs& a, float x, int col, int slot,
@@ -255,30 +255,200 @@ __device__ __forceinline__ void store_out(const NnetOpArgs& a, int r, int col, i
   if (a.out_node < 0) {
     a.llh[(size_t)r * a.N + col] = v;
   } else {
-    float* dst = a.out_base + ((size_t)slot * a.rings.ring + (tau & a.rings.mask)) * a.out_ldim;
+    float* dst = a.out_base + ((size_t)(tau & a.rings.mask) * a.rings.slots + slot) * a.out_ldim;
     dst[col] = v;
   }
 }
 
-// Output tile 64 x (32*WN) per workgroup of 2 x WN waves, each wave owning a
-// 32x32 block computed with v_mfma_f32_32x32x2_f32 (f32 in, f32 accumulate:
-// an exact k-ordered fma chain).  A rows are gathered from the stored-node
-// time rings at (tau + segment offset): the TDNN splice happens in the LDS
-// staging.  K-steps are software pipelined: the next step's global loads
-// are issued into registers before the current step's MFMAs, then written to
-// the other half of a double-buffered LDS tile (one barrier per K-step).
-template <int BK, int WN>
-__global__ __launch_bounds__(128 * WN) void nnet_gemm_kernel(NnetOpArgs a) {
-  constexpr int BN = 32 * WN, NT = 128 * WN;
-  constexpr int Q = BK / 4;             // float4 per row per K-step
-  constexpr int NA = (64 * Q + NT - 1) / NT, NB = (BN * Q + NT - 1) / NT;
-  __shared__ float As[2][64][BK + 1];
-  __shared__ float Bs[2][BK][BN + 1];
-  __shared__ int Rinfo[3][64];  // per tile row: slot, tau, clamp
+// Epilogue for the 16 accumulator values a lane holds for one column of a
+// 32x32 MFMA block: tile rows lr0 + (j&3) + 8*(j>>2).  Stages run outermost
+// (uniform branches), per-column stage vectors are loaded once per lane, the
+// bypass rows are fetched as one batch of independent loads, and all stores
+// come after all loads.  Per element the arithmetic is exactly apply_stages'.
+template <int TMR>
+__device__ __forceinline__ void epilogue_16(const NnetOpArgs& a, float (&v)[16], int col, int m0,
+                                            int lr0, const int (*Rinfo)[TMR]) {
+  const bool cok = col < a.N;
+  const int cc = cok ? col : 0;
+  for (int s = 0; s < a.nstages; s++) {
+    const DevStage& st = a.stages[s];
+    const int kind = st.kind;
+    if (kind == 0) {
+      const float b = st.v0[cc];
+#pragma unroll
+      for (int j = 0; j < 16; j++) v[j] = v[j] + b;
+    } else if (kind == 1) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) v[j] = v[j] < 0.0f ? 0.0f : v[j];
+    } else if (kind == 2) {
+      const float m = st.v0[cc], c = st.v1[cc];
+#pragma unroll
+      for (int j = 0; j < 16; j++) v[j] = v[j] * m + c;
+    } else if (kind == 3) {
+      float z[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int lr = lr0 + (j & 3) + 8 * (j >> 2);
+        z[j] = 0.0f;
+        if (cok && m0 + lr < a.M)
+          z[j] = ring_at(st.base, st.ldim, st.is_input, a.rings, Rinfo[0][lr],
+                         Rinfo[1][lr] + st.offset, Rinfo[2][lr])[st.src_col + col];
+      }
+      if (st.scaled) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = (st.c * z[j]) + v[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = z[j] + v[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; j++) v[j] = v[j] * st.c;
+    }
+  }
+  if (!cok) return;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const int lr = lr0 + (j & 3) + 8 * (j >> 2);
+    if (m0 + lr < a.M) store_out(a, m0 + lr, col, Rinfo[0][lr], Rinfo[1][lr], v[j]);
+  }
+}
+
+// ---- nnet GEMMs.  Canonical dot-product order (shared with oracle.c): K is
+// cut into GemmKSlices(K) slices whose sums are added left to right; inside a
+// slice the fma chain starts from 0 and visits each aligned group of eight k
+// as (0,4),(1,5),(2,6),(3,7): lane half h of a 32x32x2 MFMA holds k+4h..k+4h+3
+// of a group as one float4, and MFMA j consumes component j (lanes 0-31 give
+// the first k of the pair).
+
+// Streaming kernel: one wave per K-slice of a 32 x (32*NB) output block, so a
+// workgroup is GemmKSlices(K) waves.  No LDS staging and no barriers in the
+// main loop: each lane streams its own A row and B rows as float4 groups
+// straight into registers through a D-deep prefetch ring (L2 serves the
+// reuse of W across blocks).  Slice partials are summed in LDS in slice
+// order by wave 0, which runs the fused epilogue.
+// Requirements (checked on the host): K/slices % (8*D) == 0, segment
+// boundaries multiples of 8.
+template <int NB, int KS>
+__global__ __launch_bounds__(64 * KS) void nnet_gemm_stream_kernel(NnetOpArgs a) {
+  constexpr int D = 4;
+  __shared__ int Rinfo[3][32];
+  __shared__ float Red[KS > 1 ? (KS - 1) * NB * 1024 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / WN, wc = wave - wr * WN;
-  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * BN;
-  if (tid < 64) {
+  const int r = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * (32 * NB);
+  int slot = 0, tau = 0, clamp = 0;
+  if (m0 + r < a.M) row_info(a, m0 + r, &slot, &tau, &clamp);
+  if (tid < 32) {
+    Rinfo[0][tid] = slot;
+    Rinfo[1][tid] = tau;
+    Rinfo[2][tid] = clamp;
+  }
+  const int kw = a.K / KS, kbeg = wave * kw, ngr = kw / 8;
+  const float* bp[NB];
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+    int n = n0 + b * 32 + r;
+    n = n < a.N ? n : a.N - 1;  // columns past N are computed but never stored
+    bp[b] = a.W + (size_t)n * a.K + kbeg + 4 * h;
+  }
+  int seg = 0;
+  while (kbeg >= a.segs[seg].col0 + a.segs[seg].dim) seg++;
+  int kl = kbeg, seg_end;
+  const float* ap;
+  auto seg_ptr = [&]() {
+    const DevSeg& S = a.segs[seg];
+    seg_end = S.col0 + S.dim;
+    ap = ring_at(S.base, S.ldim, S.is_input, a.rings, slot, tau + S.offset, clamp) + S.src_col +
+         (kl - S.col0) + 4 * h;
+  };
+  seg_ptr();
+  float4 ra[D], rb[D][NB];
+  auto load = [&](int d) {
+    if (kl >= seg_end) {  // wave-uniform
+      seg++;
+      seg_ptr();
+    }
+    ra[d] = *reinterpret_cast<const float4*>(ap);
+    ap += 8;
+    kl += 8;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      rb[d][b] = *reinterpret_cast<const float4*>(bp[b]);
+      bp[b] += 8;
+    }
+  };
+  floatx16 acc[NB];
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[b][i] = 0.0f;
+#pragma unroll
+  for (int d = 0; d < D; d++) load(d);
+  for (int g = 0; g < ngr; g += D) {
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d].x, rb[d][b].x, acc[b], 0, 0, 0);
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d].y, rb[d][b].y, acc[b], 0, 0, 0);
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d].z, rb[d][b].z, acc[b], 0, 0, 0);
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d].w, rb[d][b].w, acc[b], 0, 0, 0);
+      if (g + d + D < ngr) load(d);
+    }
+  }
+  float v[NB][16];
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[b][j] = acc[b][j];
+  if (KS > 1) {
+    if (wave > 0) {
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int j = 0; j < 16; j++) Red[((wave - 1) * NB + b) * 1024 + j * 64 + lane] = v[b][j];
+    }
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int z = 1; z < KS; z++)
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+          v[b][j] = v[b][j] + Red[((z - 1) * NB + b) * 1024 + j * 64 + lane];
+  } else {
+    __syncthreads();
+  }
+#pragma unroll
+  for (int b = 0; b < NB; b++) epilogue_16(a, v[b], n0 + b * 32 + r, m0, 4 * h, Rinfo);
+}
+
+// LDS-staged kernel: output tile (32*WM) x (32*NB) per workgroup of WM waves,
+// each wave owning 32 rows x 32*NB columns (NB accumulators sharing one A
+// fragment).  A and B are staged row-major in k with row stride BK+4: one
+// ds_read_b128 per operand feeds four MFMAs, conflict-free in the b128 lane
+// groups.  Register prefetch one K-step ahead; loads are unconditional (rows
+// past M / columns past N read valid memory and are never stored) so no
+// divergent branch pins a wait next to a load.  kslices must be 1.
+template <int BK, int WM, int NB>
+__global__ __launch_bounds__(64 * WM) void nnet_gemm_lds_kernel(NnetOpArgs a) {
+  constexpr int TM = 32 * WM, TN = 32 * NB, NT = 64 * WM;
+  constexpr int Q = BK / 4, LDA = BK + 4;
+  constexpr int NLA = (TM * Q + NT - 1) / NT, NLB = (TN * Q + NT - 1) / NT;
+  __shared__ float4 As4[2][TM * LDA / 4];
+  __shared__ float4 Bs4[2][TN * LDA / 4];
+  __shared__ int Rinfo[3][TM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * TN;
+  if (tid < TM) {
     int sl = 0, ta = 0, cl = 0;
     if (m0 + tid < a.M) row_info(a, m0 + tid, &sl, &ta, &cl);
     Rinfo[0][tid] = sl;
@@ -286,65 +456,54 @@ __global__ __launch_bounds__(128 * WN) void nnet_gemm_kernel(NnetOpArgs a) {
     Rinfo[2][tid] = cl;
   }
   __syncthreads();
-  int r_slot[NA], r_tau[NA], r_clamp[NA];
-  bool r_ok[NA];
+  int r_slot[NLA], r_tau[NLA], r_clamp[NLA];
 #pragma unroll
-  for (int v = 0; v < NA; v++) {
-    const int idx = tid + v * NT, row = (idx / Q) & 63;
-    r_ok[v] = idx < 64 * Q && m0 + (idx / Q) < a.M;
+  for (int v = 0; v < NLA; v++) {
+    const int idx = tid + v * NT, row = (idx / Q) % TM;
     r_slot[v] = Rinfo[0][row];
     r_tau[v] = Rinfo[1][row];
     r_clamp[v] = Rinfo[2][row];
   }
-  float4 ra[NA], rb[NB];
+  float4 ra[NLA], rb[NLB];
   int seg = 0;
   auto load = [&](int k0) {
     while (!(k0 >= a.segs[seg].col0 && k0 < a.segs[seg].col0 + a.segs[seg].dim)) seg++;
     const DevSeg S = a.segs[seg];
 #pragma unroll
-    for (int v = 0; v < NA; v++) {
-      const int idx = tid + v * NT, row = idx / Q, q = idx - row * Q;
-      ra[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r_ok[v]) {
-        const float* p = ring_at(S.base, S.ldim, S.is_input, a.rings, r_slot[v],
-                                 r_tau[v] + S.offset, r_clamp[v]);
-        ra[v] = *reinterpret_cast<const float4*>(p + S.src_col + (k0 - S.col0) + 4 * q);
-      }
+    for (int v = 0; v < NLA; v++) {
+      const int idx = tid + v * NT, q = idx % Q;
+      const float* p = ring_at(S.base, S.ldim, S.is_input, a.rings, r_slot[v],
+                               r_tau[v] + S.offset, r_clamp[v]);
+      ra[v] = *reinterpret_cast<const float4*>(p + S.src_col + (k0 - S.col0) + 4 * q);
     }
 #pragma unroll
-    for (int v = 0; v < NB; v++) {
-      const int idx = tid + v * NT, n = idx / Q, q = idx - n * Q;
-      rb[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (idx < BN * Q && n0 + n < a.N)
-        rb[v] = *reinterpret_cast<const float4*>(a.W + (size_t)(n0 + n) * a.K + k0 + 4 * q);
+    for (int v = 0; v < NLB; v++) {
+      const int idx = tid + v * NT, q = idx % Q;
+      int n = n0 + (idx / Q) % TN;
+      n = n < a.N ? n : a.N - 1;
+      rb[v] = *reinterpret_cast<const float4*>(a.W + (size_t)n * a.K + k0 + 4 * q);
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int v = 0; v < NA; v++) {
+    for (int v = 0; v < NLA; v++) {
       const int idx = tid + v * NT, row = idx / Q, q = idx - row * Q;
-      if (idx < 64 * Q) {
-        As[buf][row][4 * q + 0] = ra[v].x;
-        As[buf][row][4 * q + 1] = ra[v].y;
-        As[buf][row][4 * q + 2] = ra[v].z;
-        As[buf][row][4 * q + 3] = ra[v].w;
-      }
+      if (NLA * NT == TM * Q || idx < TM * Q) As4[buf][(row * LDA) / 4 + q] = ra[v];
     }
 #pragma unroll
-    for (int v = 0; v < NB; v++) {
+    for (int v = 0; v < NLB; v++) {
       const int idx = tid + v * NT, n = idx / Q, q = idx - n * Q;
-      if (idx < BN * Q) {
-        Bs[buf][4 * q + 0][n] = rb[v].x;
-        Bs[buf][4 * q + 1][n] = rb[v].y;
-        Bs[buf][4 * q + 2][n] = rb[v].z;
-        Bs[buf][4 * q + 3][n] = rb[v].w;
-      }
+      if (NLB * NT == TN * Q || idx < TN * Q) Bs4[buf][(n * LDA) / 4 + q] = rb[v];
     }
   };
-  floatx16 acc;
+  floatx16 acc[NB];
 #pragma unroll
-  for (int i = 0; i < 16; i++) acc[i] = 0.0f;
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[b][i] = 0.0f;
   const int nk = a.K / BK;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int aoff = ((wave * 32 + r32) * LDA) / 4 + h, boff = (r32 * LDA) / 4 + h;
   load(0);
   store(0);
   __syncthreads();
@@ -352,46 +511,88 @@ __global__ __launch_bounds__(128 * WN) void nnet_gemm_kernel(NnetOpArgs a) {
     const int buf = ks & 1;
     if (ks + 1 < nk) load((ks + 1) * BK);
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const float av = As[buf][wr * 32 + (lane & 31)][kk + (lane >> 5)];
-      const float bv = Bs[buf][kk + (lane >> 5)][wc * 32 + (lane & 31)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    for (int g = 0; g < BK / 4; g += 2) {
+      const float4 av = As4[buf][aoff + g];
+      float4 bv[NB];
+#pragma unroll
+      for (int b = 0; b < NB; b++) bv[b] = Bs4[buf][boff + b * 8 * LDA + g];
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv[b].x, acc[b], 0, 0, 0);
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv[b].y, acc[b], 0, 0, 0);
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv[b].z, acc[b], 0, 0, 0);
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv[b].w, acc[b], 0, 0, 0);
     }
     if (ks + 1 < nk) store(buf ^ 1);
     __syncthreads();
   }
-  const int col = n0 + wc * 32 + (lane & 31);
+  float v[NB][16];
 #pragma unroll
-  for (int j = 0; j < 16; j++) {
-    const int lr = wr * 32 + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
-    const int row = m0 + lr;
-    if (row < a.M && col < a.N) {
-      const int slot = Rinfo[0][lr], tau = Rinfo[1][lr], clamp = Rinfo[2][lr];
-      const float v = apply_stages(a, acc[j], col, slot, tau, clamp);
-      store_out(a, row, col, slot, tau, v);
-    }
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[b][j] = acc[b][j];
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+    epilogue_16(a, v[b], n0 + b * 32 + r32, m0, wave * 32 + 4 * h, Rinfo);
+}
+
+int g_gemm_variant = 0;  // development override (tools/gemm_bench): 0 = default
+
+template <int BK, int WM, int NB>
+static void LaunchLds(const NnetOpArgs& a, hipStream_t s) {
+  dim3 grid((a.M + 32 * WM - 1) / (32 * WM), (a.N + 32 * NB - 1) / (32 * NB));
+  hipLaunchKernelGGL((nnet_gemm_lds_kernel<BK, WM, NB>), grid, dim3(64 * WM), 0, s, a);
+}
+
+template <int NB>
+static void LaunchStream(const NnetOpArgs& a, hipStream_t s) {
+  dim3 grid((a.M + 31) / 32, (a.N + 32 * NB - 1) / (32 * NB));
+  switch (a.kslices) {
+    case 1: hipLaunchKernelGGL((nnet_gemm_stream_kernel<NB, 1>), grid, dim3(64), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((nnet_gemm_stream_kernel<NB, 2>), grid, dim3(128), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((nnet_gemm_stream_kernel<NB, 4>), grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((nnet_gemm_stream_kernel<NB, 8>), grid, dim3(512), 0, s, a); break;
   }
 }
 
-template <int BK>
-static void LaunchGemmBK(const NnetOpArgs& a, int wn, hipStream_t s) {
-  if (wn == 3) {
-    dim3 grid((a.M + 63) / 64, (a.N + 95) / 96);
-    hipLaunchKernelGGL((nnet_gemm_kernel<BK, 3>), grid, dim3(384), 0, s, a);
-  } else {
-    dim3 grid((a.M + 63) / 64, (a.N + 63) / 64);
-    hipLaunchKernelGGL((nnet_gemm_kernel<BK, 2>), grid, dim3(256), 0, s, a);
-  }
+bool GemmStreamable(const NnetOpArgs& a) {
+  if (a.kslices != 1 && a.kslices != 2 && a.kslices != 4 && a.kslices != 8) return false;
+  if ((a.K / a.kslices) % 32) return false;
+  for (int i = 0; i < a.nsegs; i++)
+    if (a.segs[i].col0 % 8 || a.segs[i].dim % 8) return false;
+  return true;
 }
 
 void LaunchNnetGemm(const NnetOpArgs& a, int bk, hipStream_t s) {
   if (a.M <= 0) return;
-  // a 96-wide N tile for the TDNN-F bottlenecks (N = 96): no idle wave columns
-  const int wn = (a.N % 96 == 0 && a.N % 64 != 0) ? 3 : 2;
-  if (bk == 64) LaunchGemmBK<64>(a, wn, s);
-  else if (bk == 32) LaunchGemmBK<32>(a, wn, s);
-  else if (bk == 16) LaunchGemmBK<16>(a, wn, s);
-  else LaunchGemmBK<8>(a, wn, s);
+  const int nb = GemmTileN(a.N) / 32;
+  int var = g_gemm_variant;
+  if (var == 0) var = (GemmStreamable(a) && a.N <= 512) ? 1 : 3;
+  if ((var == 1 || var == 2) && !GemmStreamable(a)) var = 3;
+  if (var == 1) {
+    if (nb == 3) LaunchStream<3>(a, s);
+    else LaunchStream<2>(a, s);
+  } else if (var == 2) {
+    LaunchStream<1>(a, s);
+  } else {
+    if (a.kslices != 1) return;  // host guarantees streamable ops for split K
+    if (bk >= 32) {
+      if (nb == 3) LaunchLds<32, 2, 3>(a, s);
+      else LaunchLds<32, 4, 2>(a, s);
+    } else if (bk == 16) {
+      if (nb == 3) LaunchLds<16, 2, 3>(a, s);
+      else LaunchLds<16, 4, 2>(a, s);
+    } else {
+      if (nb == 3) LaunchLds<8, 2, 3>(a, s);
+      else LaunchLds<8, 4, 2>(a, s);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void nnet_gather_kernel(NnetOpArgs a) {
@@ -419,6 +620,7 @@ __global__ __launch_bounds__(256) void nnet_gather_kernel(NnetOpArgs a) {
   store_out(a, row, col, slot, tau, v);
 }
 
+
 void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s) {
   long long n = (long long)a.M * a.N;
   if (n <= 0) return;
@@ -428,7 +630,10 @@ void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s) {
 // ===========================================================================
 // token passing
 // ===========================================================================
-constexpr int DT = 1024;         // threads per decoder workgroup
+#ifndef VAMD_DEC_THREADS
+#define VAMD_DEC_THREADS 512
+#endif
+constexpr int DT = VAMD_DEC_THREADS;  // threads per decoder workgroup
 constexpr int DW = DT / 64;      // waves
 constexpr int kLlhLds = 8192;    // log-likelihood row staged in LDS up to this size
 constexpr int kTokLds = 4096;    // current-frame tokens cached in LDS up to this count

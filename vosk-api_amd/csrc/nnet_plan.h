@@ -69,6 +69,14 @@ struct Op {
   std::vector<int> deps;     // op indices this op reads from
 };
 
+// Canonical summation order of every affine dot product (GPU and oracle):
+// K is cut into GemmKSlices(K) equal slices, each an fma chain over its k in
+// increasing order starting from 0, and the slice sums are added left to
+// right; the bias is added last.  Kaldi leaves the order to BLAS; fixing one
+// lets long reductions (K = 1024 bottlenecks) spread over more workgroups and
+// keeps GPU and oracle bit-identical.  Mirrored by orc_kslices() in oracle.c.
+inline int GemmKSlices(int K) { return (K >= 512 && K % 256 == 0) ? K / 256 : 1; }
+
 struct NnetPlan {
   int fpc = 0, fss = 1, opc = 0;  // frames per chunk, subsampling, outputs per chunk
   int out_dim = 0;

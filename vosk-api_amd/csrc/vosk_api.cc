@@ -228,6 +228,7 @@ VamdEngine* vamd_engine_new(const char* model_dir, int fpc, int max_streams, int
   cfg.collect_stats = (flags & 1) != 0;
   cfg.collect_llh = (flags & 2) != 0;
   cfg.time_kernels = (flags & 4) != 0;
+  cfg.pipeline = (flags & 8) != 0;
   const char* d = getenv("VOSK_AMD_DEVICE");
   cfg.device = d ? atoi(d) : 0;
   const char* at = getenv("VOSK_AMD_ARENA_TOKENS");
@@ -236,6 +237,13 @@ VamdEngine* vamd_engine_new(const char* model_dir, int fpc, int max_streams, int
   e->desc = e->eng->plan().Describe();
   return e.release();
   API_CATCH(nullptr)
+}
+
+int vamd_engine_flush(VamdEngine* e) {
+  API_TRY
+  e->eng->Flush();
+  return 0;
+  API_CATCH(-1)
 }
 
 void vamd_engine_free(VamdEngine* e) { delete e; }

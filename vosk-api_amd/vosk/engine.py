@@ -37,6 +37,7 @@ _SIGS = {
     "vamd_engine_counters": (C.c_int, [_vp, _vp]),
     "vamd_stream_preload": (C.c_int, [_vp, C.c_int, _vp, C.c_longlong, C.c_int]),
     "vamd_engine_step": (C.c_int, [_vp, _vp, C.c_int]),
+    "vamd_engine_flush": (C.c_int, [_vp]),
     "vamd_engine_decoder_totals": (C.c_int, [_vp, _vp]),
     "vamd_engine_decoder_phases": (C.c_int, [_vp, _vp]),
     "vamd_engine_set_step_samples": (C.c_int, [_vp, C.c_int]),
@@ -85,8 +86,9 @@ def device_count():
 
 class Engine:
     def __init__(self, model_dir, frames_per_chunk=0, max_streams=8, stats=False, keep_llh=False,
-                 time_kernels=False):
-        flags = (1 if stats else 0) | (2 if keep_llh else 0) | (4 if time_kernels else 0)
+                 time_kernels=False, pipeline=False):
+        flags = ((1 if stats else 0) | (2 if keep_llh else 0) | (4 if time_kernels else 0)
+                 | (8 if pipeline else 0))
         h = _c.vamd_engine_new(str(model_dir).encode(), frames_per_chunk, max_streams, flags)
         if not h:
             raise RuntimeError("vamd_engine_new failed: " + _err())
@@ -167,6 +169,9 @@ class Engine:
     def preload(self, s, samples, finished=True):
         x = np.ascontiguousarray(samples, np.float32)
         _chk(_c.vamd_stream_preload(self.h, s, x.ctypes.data, len(x), 1 if finished else 0))
+
+    def flush(self):
+        _chk(_c.vamd_engine_flush(self.h))
 
     def step(self, streams):
         a = np.ascontiguousarray(streams, np.int32)
