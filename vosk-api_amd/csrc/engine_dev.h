@@ -89,6 +89,7 @@ struct DecSlot {
   int err;          // bit 0: token list overflow, bit 1: arena overflow, bit 2: no tokens
   int pad;
   double offset_sum;
+  unsigned long long best_key;  // min over current tokens of (ordered cost << 32 | state)
 };
 
 struct DecJob {

@@ -688,6 +688,17 @@ __device__ unsigned long long block_min_u64(DecShared& sh, unsigned long long v)
   return r;
 }
 
+__device__ unsigned long long block_sum_u64(DecShared& sh, unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh.red_u[w] = v;
+  __syncthreads();
+  unsigned long long r = 0;
+  for (int i = 0; i < DW; i++) r += sh.red_u[i];
+  return r;
+}
+
 // exclusive scan of deg over the block; writes sh.scan[0..DT], sh.total
 __device__ void block_scan(DecShared& sh, int deg) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -877,7 +888,7 @@ __device__ void commit(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st,
   const bool ok = (long long)base + n <= a.arena_cap;
   if (threadIdx.x == 0) sh.n_next = 0;
   __syncthreads();
-  float best = __int_as_float(0x7f800000);
+  unsigned long long bk = kEmpty;
   for (int j = threadIdx.x; j < n; j += DT) {
     const int s = AG_LD(&p.nl[j]);
     const unsigned long long k = AG_LD(&p.key[s]);
@@ -899,11 +910,12 @@ __device__ void commit(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st,
         TS[q] = s;
         TC[q] = cost;
       }
-      best = fminf(best, cost);
+      const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)s;
+      bk = tk < bk ? tk : bk;
     }
     AG_ST(&p.key[s], kEmpty);
   }
-  best = block_min_f(sh, best);
+  bk = block_min_u64(sh, bk);
   if (!ok) sh.bad |= 2;
   __syncthreads();
   const int live = sh.n_next;
@@ -919,7 +931,8 @@ __device__ void commit(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st,
   p.pos_cur = p.pos_new;
   p.pos_new = t;
   st.parity ^= 1;
-  *best_out = best;
+  st.best_key = bk;  // GetCutoff's best token of the next frame
+  *best_out = funord((uint32_t)(bk >> 32));
 }
 
 // one emitting expansion pass over the current tokens (ProcessEmitting):
@@ -1035,13 +1048,8 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     }
     const int ntok = st.ntok;
     const TokView tv{p.cs, p.cc, TS, TC, lds};
-    // ---- GetCutoff
-    unsigned long long bk = kEmpty;
-    for (int i = threadIdx.x; i < ntok; i += DT) {
-      const unsigned long long k = ((unsigned long long)ford(tv.c(i)) << 32) | (unsigned)tv.s(i);
-      bk = k < bk ? k : bk;
-    }
-    bk = block_min_u64(sh, bk);
+    // ---- GetCutoff (best token: min (cost, state), kept by the previous commit)
+    const unsigned long long bk = st.best_key;
     const float best = funord((uint32_t)(bk >> 32));
     const int best_state = (int)(unsigned)(bk & 0xffffffffu);
     const float beam_cutoff = best + a.beam;
@@ -1052,18 +1060,17 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     // min_cut > beam_cutoff  <=>  at most min_active costs are <= beam_cutoff.
     bool need_max = ntok > a.max_active, need_min = ntok > a.min_active && a.min_active > 0;
     if (need_max || need_min) {
-      int lt = 0, le = 0;
+      unsigned long long cnt = 0;  // (# cost < beam_cutoff) << 32 | # cost <= beam_cutoff
       for (int i = threadIdx.x; i < ntok; i += DT) {
         const float c = tv.c(i);
-        lt += c < beam_cutoff;
-        le += c <= beam_cutoff;
+        cnt += ((unsigned long long)(c < beam_cutoff) << 32) | (unsigned)(c <= beam_cutoff);
       }
-      block_scan(sh, lt);
-      const int n_lt = sh.total;
-      block_scan(sh, le);
-      const int n_le = sh.total;
+      cnt = block_sum_u64(sh, cnt);
+      const int n_lt = (int)(cnt >> 32), n_le = (int)(unsigned)(cnt & 0xffffffffu);
       need_max = need_max && n_lt > a.max_active;
       need_min = need_min && n_le <= a.min_active;
+    } else {
+      __syncthreads();  // the LLH row staged above is read by wave 0 below
     }
     if (need_max) max_cut = kth_smallest(sh, tv, ntok, a.max_active);
     if (max_cut < beam_cutoff) {
