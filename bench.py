@@ -244,7 +244,7 @@ def main():
         if os.environ.get("VOSK_AMD_DEC_PROFILE"):
             out["decoder_phase_clocks_per_frame"] = {
                 k: round(v / max(e.decoder_phases()["frames"], 1), 1)
-                for k, v in e.decoder_phases().items() if k not in ("_", "frames")}
+                for k, v in e.decoder_phases().items() if k != "frames"}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -573,7 +573,9 @@ void LaunchNnetGemm(const NnetOpArgs& a, int bk, hipStream_t s) {
   if (a.M <= 0) return;
   const int nb = GemmTileN(a.N) / 32;
   int var = g_gemm_variant;
-  if (var == 0) var = (GemmStreamable(a) && a.N <= 512) ? 1 : 3;
+  // streaming kernel wherever it applies: faster on every recipe shape and
+  // small in LDS (co-resides with the decoder in pipeline mode)
+  if (var == 0) var = GemmStreamable(a) ? 1 : 3;
   if ((var == 1 || var == 2) && !GemmStreamable(a)) var = 3;
   if (var == 1) {
     if (nb == 3) LaunchStream<3>(a, s);
@@ -635,8 +637,15 @@ void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s) {
 #endif
 constexpr int DT = VAMD_DEC_THREADS;  // threads per decoder workgroup
 constexpr int DW = DT / 64;      // waves
-constexpr int kLlhLds = 8192;    // log-likelihood row staged in LDS up to this size
-constexpr int kTokLds = 4096;    // current-frame tokens cached in LDS up to this count
+constexpr int kLlhLds = 4096;    // log-likelihood row staged in LDS up to this size
+constexpr int kTokLds = 1024;    // current-frame tokens cached in LDS up to this count
+// LDS frame construction: open-addressing table of the frame being built
+constexpr int kHashCap = 4096;   // slots (power of two)
+constexpr int kHashBits = 12;
+constexpr int kNewLds = 3072;    // tokens a frame may create in LDS mode (load <= 0.75)
+constexpr int kFrontLds = 2048;  // epsilon frontier capacity in LDS mode
+constexpr int kMaxProbe = 64;    // longer probe sequences count as overflow
+constexpr int kLdsFrameTokens = 1000;  // frames with more current tokens skip the LDS table
 constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
 constexpr unsigned kDestEps = 0x80000000u;  // arcs[].w: nextstate has epsilon arcs
 
@@ -648,7 +657,7 @@ struct DecShared {
   unsigned long long red_u[DW];
   float red_f[DW];
   int red_i[DW];
-  int n_new, n_next, n_front0, total, sel_k;
+  int n_new, n_next, n_front0, total, sel_k, ovf;
   unsigned sel_prefix, sel_mask;
   float seed;
   int bad;
@@ -935,6 +944,276 @@ __device__ void commit(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st,
   *best_out = funord((uint32_t)(bk >> 32));
 }
 
+// ---- LDS frame construction.  The frame being built lives in an LDS hash
+// table (state, (cost, arc) key, list position, epsilon-round stamp) with
+// LDS token list and frontiers; global memory is only written by the commit
+// (arena, current-token arrays, position map).  A frame that overflows the
+// table, the list or a frontier sets sh.ovf before anything global changed and
+// is re-run on the global-map path (same semantics, same results).
+struct FrameLds {
+  int* hs;                  // [kHashCap] state, -1 = empty
+  unsigned long long* hk;   // [kHashCap] (ordered cost << 32 | arc), kEmpty
+  unsigned short* hp;       // [kHashCap] position in the frame's list
+  int* hst;                 // [kHashCap] epsilon round stamp
+  unsigned short* nl;       // [kNewLds] list -> slot
+  unsigned short* fa;       // [kFrontLds] frontier slots
+  unsigned short* fb;
+};
+
+__device__ __forceinline__ unsigned hash_slot(int s) {
+  return ((unsigned)s * 2654435761u) >> (32 - kHashBits);
+}
+
+__device__ void lds_clear(const FrameLds& t) {
+  for (int h = threadIdx.x; h < kHashCap; h += DT) {
+    t.hs[h] = -1;
+    t.hk[h] = kEmpty;
+    t.hst[h] = 0;
+  }
+}
+
+// relax into the LDS table: returns (slot << 2) | 2 if created, | 1 if
+// improved, | 0 otherwise; -1 on overflow (sh.ovf set)
+__device__ __forceinline__ int relax_lds(DecShared& sh, const FrameLds& t, int dest, float tot,
+                                         int arc) {
+  if (__hip_atomic_load(&sh.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return -1;
+  const unsigned long long k = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
+  unsigned h = hash_slot(dest);
+  for (int probe = 0; probe < kMaxProbe; probe++) {
+    int cur = __hip_atomic_load(&t.hs[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == -1) {
+      cur = atomicCAS(&t.hs[h], -1, dest);
+      if (cur == -1) {
+        const int pos = atomicAdd(&sh.n_new, 1);
+        if (pos < kNewLds) {
+          t.nl[pos] = (unsigned short)h;
+          t.hp[h] = (unsigned short)pos;
+        } else {
+          sh.ovf |= 1;
+        }
+        atomicMin(&t.hk[h], k);
+        return (int)(h << 2) | 2;
+      }
+    }
+    if (cur == dest) {
+      const unsigned long long old = atomicMin(&t.hk[h], k);
+      return (int)(h << 2) | (k < old ? 1 : 0);
+    }
+    h = (h + 1) & (kHashCap - 1);
+  }
+  sh.ovf |= 2;
+  return -1;
+}
+
+__device__ __forceinline__ int lds_find(const FrameLds& t, int s) {
+  unsigned h = hash_slot(s);
+  for (int probe = 0; probe < kMaxProbe; probe++) {
+    if (t.hs[h] == s) return (int)h;
+    if (t.hs[h] == -1) return -1;
+    h = (h + 1) & (kHashCap - 1);
+  }
+  return -1;
+}
+
+__device__ float expand_emitting_lds(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                     const TokView& tv, int ntok, float cutoff, float cost_offset,
+                                     const float* Lp, int mode, float bound, int* examined) {
+  float m = __int_as_float(0x7f800000);
+  for (int c0 = 0; c0 < ntok; c0 += DT) {
+    const int i = c0 + threadIdx.x;
+    int deg = 0, ab = 0;
+    float c = 0.0f;
+    if (i < ntok) {
+      c = tv.c(i);
+      if (c <= cutoff) {
+        const int4 si = a.sinfo[tv.s(i)];
+        ab = si.x;
+        deg = si.y - si.x;
+      }
+    }
+    block_scan(sh, deg);
+    sh.abeg[threadIdx.x] = ab;
+    sh.tcost[threadIdx.x] = c;
+    __syncthreads();
+    const int total = sh.total;
+    *examined += total;
+    for (int it = threadIdx.x; it < total; it += DT) {
+      const int j = owner(sh, it);
+      const int arc = sh.abeg[j] + (it - sh.scan[j]);
+      const int4 A = a.arcs[arc];
+      const float ac = cost_offset - Lp[A.z];
+      const float tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
+      m = fminf(m, tot);
+      if (mode == 1 && tot < bound) {
+        const int r = relax_lds(sh, t, A.x, tot, arc);
+        if (r >= 0 && (r & 3) == 2 && ((unsigned)A.w & kDestEps)) {
+          const int q = atomicAdd(&sh.n_front0, 1);
+          if (q < kFrontLds) t.fa[q] = (unsigned short)(r >> 2);
+          else sh.ovf |= 4;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  return block_min_f(sh, m);
+}
+
+__device__ void eps_closure_lds(const DecArgs& a, DecShared& sh, const FrameLds& t, float cutoff,
+                                int nfront, int* arcs_eps) {
+  unsigned short* front = t.fa;
+  unsigned short* next = t.fb;
+  int examined = 0, round = 0;
+  nfront = nfront < kFrontLds ? nfront : kFrontLds;
+  while (nfront > 0) {
+    round++;
+    __syncthreads();
+    if (threadIdx.x == 0) sh.n_next = 0;
+    for (int c0 = 0; c0 < nfront; c0 += DT) {
+      const int i = c0 + threadIdx.x;
+      int deg = 0, ab = 0;
+      float c = 0.0f;
+      if (i < nfront) {
+        const int h = front[i];
+        c = funord((uint32_t)(t.hk[h] >> 32));
+        if (c < cutoff) {  // created tokens are < cutoff; dead ones are not
+          const int4 si = a.sinfo[t.hs[h]];
+          ab = si.y;
+          deg = si.z - si.y;
+        }
+      }
+      block_scan(sh, deg);
+      sh.abeg[threadIdx.x] = ab;
+      sh.tcost[threadIdx.x] = c;
+      __syncthreads();
+      const int total = sh.total;
+      examined += total;
+      for (int it = threadIdx.x; it < total; it += DT) {
+        const int j = owner(sh, it);
+        const int arc = sh.abeg[j] + (it - sh.scan[j]);
+        const int4 A = a.arcs[arc];
+        const float tot = sh.tcost[j] + __int_as_float(A.y);
+        if (tot < cutoff) {
+          const int r = relax_lds(sh, t, A.x, tot, arc);
+          if (r >= 0 && (r & 3) && ((unsigned)A.w & kDestEps) &&
+              atomicExch(&t.hst[r >> 2], round) != round) {
+            const int q = atomicAdd(&sh.n_next, 1);
+            if (q < kFrontLds) next[q] = (unsigned short)(r >> 2);
+            else sh.ovf |= 8;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    nfront = sh.n_next < kFrontLds ? sh.n_next : kFrontLds;
+    unsigned short* tmp = front;
+    front = next;
+    next = tmp;
+  }
+  *arcs_eps += examined;
+}
+
+// commit of an LDS-built frame (see commit()); clears the table afterwards
+__device__ void commit_lds(const DecArgs& a, DecShared& sh, DecPtrs& p, const FrameLds& t,
+                           DecSlot& st, int* TS, float* TC, bool* lds, float cutoff,
+                           float* best_out) {
+  __syncthreads();
+  const int n = sh.n_new < kNewLds ? sh.n_new : kNewLds;
+  const int base = st.arena_used;
+  const bool ok = (long long)base + n <= a.arena_cap;
+  if (threadIdx.x == 0) sh.n_next = 0;
+  __syncthreads();
+  unsigned long long bk = kEmpty;
+  for (int j = threadIdx.x; j < n; j += DT) {
+    const int h = t.nl[j];
+    const int s = t.hs[h];
+    const unsigned long long k = t.hk[h];
+    const int arc = (int)(unsigned)(k & 0xffffffffu);
+    const float cost = funord((uint32_t)(k >> 32));
+    if (ok && cost < cutoff) {
+      int prev = -1;
+      if (arc >= 0) {
+        const int4 A = a.arcs[arc];
+        const int src = (int)((unsigned)A.w & 0x7fffffffu);
+        if (A.z >= 0) {
+          prev = st.cur_base + AG_LD(&p.pos_cur[src]);
+        } else {
+          const int hsrc = lds_find(t, src);
+          prev = base + (hsrc >= 0 ? t.hp[hsrc] : 0);
+        }
+      }
+      p.arena[base + j] = make_int2(prev, arc);
+      const int q = atomicAdd(&sh.n_next, 1);
+      AG_ST(&p.cs[q], s);
+      AG_ST(&p.cc[q], cost);
+      AG_ST(&p.cp[q], j);
+      AG_ST(&p.pos_new[s], j);
+      if (q < kTokLds) {
+        TS[q] = s;
+        TC[q] = cost;
+      }
+      const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)s;
+      bk = tk < bk ? tk : bk;
+    }
+  }
+  bk = block_min_u64(sh, bk);  // ends with a barrier: the table is no longer read
+  if (!ok) sh.bad |= 2;
+  lds_clear(t);
+  __syncthreads();
+  const int live = sh.n_next;
+  if (ok) {
+    st.cur_base = base;
+    st.arena_used = base + n;
+    st.ntok = live;
+  } else {
+    st.ntok = 0;
+  }
+  *lds = live <= kTokLds;
+  int* tp = p.pos_cur;
+  p.pos_cur = p.pos_new;
+  p.pos_new = tp;
+  st.parity ^= 1;
+  st.best_key = bk;
+  *best_out = funord((uint32_t)(bk >> 32));
+}
+
+// dev self-test of the LDS frame table (tools/gemm_bench): each block inserts
+// `n` random states (each relaxed 3 times) and reports overflow bits and the
+// number of distinct states the table holds
+__global__ __launch_bounds__(DT) void lds_hash_selftest_kernel(int n, int seed, int* out) {
+  __shared__ DecShared sh;
+  __shared__ int t_hs[kHashCap];
+  __shared__ unsigned long long t_hk[kHashCap];
+  __shared__ unsigned short t_hp[kHashCap];
+  __shared__ int t_hst[kHashCap];
+  __shared__ unsigned short t_nl[kNewLds];
+  __shared__ unsigned short t_fa[kFrontLds];
+  __shared__ unsigned short t_fb[kFrontLds];
+  const FrameLds t{t_hs, t_hk, t_hp, t_hst, t_nl, t_fa, t_fb};
+  lds_clear(t);
+  if (threadIdx.x == 0) {
+    sh.n_new = 0;
+    sh.ovf = 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * n; i += DT) {
+    const int k = i % n;
+    const unsigned st = ((unsigned)(k + 1) * 2246822519u + (unsigned)seed * 3266489917u) % 55000u;
+    relax_lds(sh, t, (int)st, (float)(i & 7), i);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int used = 0;
+    for (int h = 0; h < kHashCap; h++) used += t.hs[h] != -1;
+    out[blockIdx.x * 3 + 0] = sh.ovf;
+    out[blockIdx.x * 3 + 1] = sh.n_new;
+    out[blockIdx.x * 3 + 2] = used;
+  }
+}
+
+void LdsHashSelfTest(int n, int blocks, int* out) {
+  hipLaunchKernelGGL(lds_hash_selftest_kernel, dim3(blocks), dim3(DT), 0, 0, n, 7, out);
+}
+
 // one emitting expansion pass over the current tokens (ProcessEmitting):
 // mode 0 = minimum only, 1 = relax below `bound` (+ minimum)
 __device__ float expand_emitting(const DecArgs& a, DecShared& sh, DecPtrs& p, const TokView& tv,
@@ -981,6 +1260,15 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   __shared__ float L[kLlhLds];
   __shared__ int TS[kTokLds];
   __shared__ float TC[kTokLds];
+  __shared__ int t_hs[kHashCap];
+  __shared__ unsigned long long t_hk[kHashCap];
+  __shared__ unsigned short t_hp[kHashCap];
+  __shared__ int t_hst[kHashCap];
+  __shared__ unsigned short t_nl[kNewLds];
+  __shared__ unsigned short t_fa[kFrontLds];
+  __shared__ unsigned short t_fb[kFrontLds];
+  const FrameLds t{t_hs, t_hk, t_hp, t_hst, t_nl, t_fa, t_fb};
+  lds_clear(t);
   const DecJob job = a.jobs[blockIdx.x];
   const int slot = job.slot;
   const long long S = a.num_states;
@@ -1105,37 +1393,81 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
         sh.seed = sd;
         sh.n_new = 0;
         sh.n_front0 = 0;
+        sh.ovf = 0;
       }
     }
     __syncthreads();
     DEC_PHASE(1);
     const float seed = sh.seed;
     int examined = 0;
-    float next_cutoff;
-    if (seed != __int_as_float(0x7f800000)) {
-      // single pass: relax below the seed bound (a superset), then drop the
-      // tokens whose best cost is not below the final next_cutoff -- exactly
-      // the tokens a relax-below-next_cutoff pass creates, with the same keys
-      const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed, &examined);
+    float next_cutoff, new_best;
+    // ---- frame construction in LDS: one emitting pass relaxing below the
+    // seed bound (a superset), then the epsilon closure; tokens whose best
+    // cost is not below the final next_cutoff stay as dead list entries
+    // (never expanded: cost >= cutoff) and are dropped at commit -- exactly
+    // the tokens a relax-below-next_cutoff pass creates, with the same keys.
+    // Frames predicted too large for the LDS table (many current tokens) go
+    // straight to the global maps; a frame that overflows anyway is rebuilt
+    // there (nothing global was written).
+    const bool try_lds = ntok <= kLdsFrameTokens;
+    if (try_lds) {
+      if (seed != __int_as_float(0x7f800000)) {
+        const float m = expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
+                                            &examined);
+        next_cutoff = seed;
+        if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
+      } else {
+        const float m = expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
+                                            &examined);
+        next_cutoff = seed;
+        if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
+        int dummy = 0;
+        expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy);
+      }
+      __syncthreads();
       DEC_PHASE(2);
-      next_cutoff = seed;
-      if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
-      // tokens whose best cost is not below next_cutoff stay in the list as
-      // dead entries: never expanded (cost >= cutoff), dropped at commit
-    } else {
-      const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f, &examined);
-      next_cutoff = seed;
-      if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
-      int dummy = 0;
-      expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy);
+      if (prof) pacc[3] += sh.n_new;  // tokens created by the emitting pass
+      if (!sh.ovf) eps_closure_lds(a, sh, t, next_cutoff, sh.n_front0, &arcs_eps);
+      __syncthreads();
+      DEC_PHASE(4);
     }
-    __syncthreads();
-    DEC_PHASE(3);
-    // ---- ProcessNonemitting
-    eps_closure(a, sh, p, st, next_cutoff, sh.n_front0, &arcs_eps);
-    DEC_PHASE(4);
-    float new_best;
-    commit(a, sh, p, st, TS, TC, &lds, next_cutoff, &new_best);
+    if (try_lds && !sh.ovf) {
+      commit_lds(a, sh, p, t, st, TS, TC, &lds, next_cutoff, &new_best);
+    } else {
+      // ---- global maps: a single emitting pass relaxing below the seed
+      // bound when it is finite (dead entries dropped at commit), else the
+      // exact two-pass form
+      if (prof) pacc[6]++;
+      if (try_lds) {
+        lds_clear(t);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          sh.n_new = 0;
+          sh.n_front0 = 0;
+        }
+        __syncthreads();
+      }
+      examined = 0;
+      arcs_eps = 0;
+      if (seed != __int_as_float(0x7f800000)) {
+        const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
+                                        &examined);
+        next_cutoff = seed;
+        if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
+      } else {
+        const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
+                                        &examined);
+        next_cutoff = seed;
+        if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
+        int dummy = 0;
+        expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy);
+      }
+      __syncthreads();
+      DEC_PHASE(2);
+      eps_closure(a, sh, p, st, next_cutoff, sh.n_front0, &arcs_eps);
+      DEC_PHASE(4);
+      commit(a, sh, p, st, TS, TC, &lds, next_cutoff, &new_best);
+    }
     DEC_PHASE(5);
     if (prof) pacc[7]++;
     st.offset_sum += (double)cost_offset;

@@ -195,7 +195,10 @@ class Engine:
     def decoder_phases(self):
         out = np.zeros(8, np.int64)
         _chk(_c.vamd_engine_decoder_phases(self.h, out.ctypes.data))
-        names = ("cutoff", "seed", "expand", "compact", "eps", "commit", "_", "frames")
+        # clocks per phase; slot 3 sums the tokens the emitting pass created,
+        # slot 6 counts frames rebuilt on the global maps after an LDS overflow
+        names = ("cutoff", "seed", "expand", "created", "eps", "commit", "lds_fallback_frames",
+                 "frames")
         return dict(zip(names, out.tolist()))
 
     def counters(self):
