@@ -331,7 +331,9 @@ __device__ __forceinline__ void epilogue_16(const NnetOpArgs& a, float (&v)[16],
 // boundaries multiples of 8.
 template <int NB, int KS>
 __global__ __launch_bounds__(64 * KS) void nnet_gemm_stream_kernel(NnetOpArgs a) {
-  constexpr int D = 4;
+  // prefetch depth in groups of 8 k; kept shallow for NB = 3 so that a wave
+  // fits beside the decoder's waves on a SIMD (pipeline mode)
+  constexpr int D = NB >= 3 ? 2 : 4;
   __shared__ int Rinfo[3][32];
   __shared__ float Red[KS > 1 ? (KS - 1) * NB * 1024 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(64 * KS) void nnet_gemm_stream_kernel(NnetOpArgs a)
     }
     __syncthreads();
     if (wave != 0) return;
-#pragma unroll
+#pragma unroll 1
     for (int z = 1; z < KS; z++)
 #pragma unroll
       for (int b = 0; b < NB; b++)
