@@ -56,6 +56,22 @@ def synth_model_noep(synth_model):
 
 
 @pytest.fixture(scope="session")
+def synth_model_wide(synth_model):
+    """Same model with a wide beam (30) and max-active 20000: frames with
+    thousands of tokens (decoder capacity and fallback paths)."""
+    path = os.path.join(MODEL_CACHE, f"synth_wide_{SYNTH_VERSION}")
+    if not os.path.exists(os.path.join(path, "README")):
+        tmp = path + f".tmp{os.getpid()}"
+        shutil.rmtree(tmp, ignore_errors=True)
+        shutil.copytree(synth_model, tmp)
+        with open(os.path.join(tmp, "conf", "model.conf"), "a") as f:
+            f.write("--beam=30.0\n--max-active=20000\n")
+        shutil.rmtree(path, ignore_errors=True)
+        os.rename(tmp, path)
+    return path
+
+
+@pytest.fixture(scope="session")
 def test_wave():
     w = wave.open(os.path.join(REPO, "tests", "golden", "test.wav"), "rb")
     return np.frombuffer(w.readframes(w.getnframes()), "<i2").astype(np.float32)

@@ -57,7 +57,22 @@ def test_llh_bit_exact(synth_model, oracle, test_wave, fpc):
     np.testing.assert_array_equal(llh, ref)
 
 
-def test_decoder_from_oracle_llh(synth_model, oracle, test_wave):
+# decoder frame construction: LDS table (default), global maps only, and
+# always-LDS (large frames overflow the table and are rebuilt on the global maps)
+FRAME_PATHS = {"default": None, "global": "0", "lds_then_rebuild": "1000000000"}
+
+
+@pytest.fixture(params=sorted(FRAME_PATHS))
+def frame_path(request, monkeypatch):
+    v = FRAME_PATHS[request.param]
+    if v is None:
+        monkeypatch.delenv("VOSK_AMD_LDS_FRAME_TOKENS", raising=False)
+    else:
+        monkeypatch.setenv("VOSK_AMD_LDS_FRAME_TOKENS", v)
+    return request.param
+
+
+def test_decoder_from_oracle_llh(synth_model, oracle, test_wave, frame_path):
     ref_llh = oracle.loglikes(test_wave)
     r = oracle.decode_llh(ref_llh)
     e = _engine(synth_model)
@@ -74,6 +89,23 @@ def test_decoder_from_oracle_llh(synth_model, oracle, test_wave):
     assert cost == pytest.approx(r["best_cost"], abs=1e-6)
 
 
+def test_decoder_wide_beam_all_paths(synth_model_wide, test_wave, frame_path):
+    """Thousands of tokens per frame: LDS table overflow / global rebuild and
+    the predictive global path give the oracle's best path and statistics."""
+    import oracle_py
+    ow = oracle_py.OracleModel(synth_model_wide)
+    llh = ow.loglikes(test_wave[:64000])
+    r = ow.decode_llh(llh)
+    assert r["ntok"].max() > 3000  # the table capacity is exceeded somewhere
+    e = _engine(synth_model_wide)
+    s = e.new_stream()
+    e.decode_llh(s, llh, reset=True)
+    st = e.stats(s)
+    np.testing.assert_array_equal(st[:, 1].astype(np.int64), r["ntok"][1:])
+    arcs, _, _ = e.best_path(s, use_final=True)
+    np.testing.assert_array_equal(arcs, r["path"])
+
+
 def test_end_to_end_single_stream(synth_model, oracle, test_wave):
     e = _engine(synth_model)
     s = e.new_stream()
@@ -85,7 +117,7 @@ def test_end_to_end_single_stream(synth_model, oracle, test_wave):
     assert e.error(s) == 0
 
 
-def test_batched_streams_match_oracle(synth_model, oracle, test_wave):
+def test_batched_streams_match_oracle(synth_model, oracle, test_wave, frame_path):
     """Eight different streams advanced together in the same batched steps."""
     n = 8
     e = _engine(synth_model, fpc=51, streams=n, stats=False, llh=False)

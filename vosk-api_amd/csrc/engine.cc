@@ -383,6 +383,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   dec_.front_b = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.arena = (int2*)DevAlloc(sizeof(int2) * S * cfg_.arena_tokens);
   dec_.max_tok = (int)MT;
+  // LDS frame construction threshold (kernels.hip kLdsFrameTokens); tests
+  // force either path with VOSK_AMD_LDS_FRAME_TOKENS (0 = always global)
+  dec_.lds_frame_tokens = DecoderLdsFrameTokens();
+  if (const char* lt = getenv("VOSK_AMD_LDS_FRAME_TOKENS")) dec_.lds_frame_tokens = atoi(lt);
   dec_.arena_cap = cfg_.arena_tokens;
   d_slots_ = (DecSlot*)DevAlloc(sizeof(DecSlot) * S);
   HIPCHECK(hipMemset(d_slots_, 0, sizeof(DecSlot) * S));

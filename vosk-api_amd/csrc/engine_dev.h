@@ -125,6 +125,7 @@ struct DecArgs {
   DecSlot* slots;
   FrameStat* stats;
   int max_tok;
+  int lds_frame_tokens;   // frames with more current tokens use the global maps
   long long arena_cap;
 };
 

@@ -20,6 +20,7 @@ bool GemmStreamable(const NnetOpArgs& a);  // streaming kernel applies (else LDS
 extern int g_gemm_variant;  // dev override: 1/2 streaming NB=natural/1, 3 LDS (tools/gemm_bench)
 void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s);
 void LdsHashSelfTest(int n, int blocks, int* out);  // dev (tools/gemm_bench)
+int DecoderLdsFrameTokens();  // default LDS frame-construction threshold
 void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s);
 void LaunchTraceback(const TraceArgs& a, int n, hipStream_t s);
 void LaunchInitKeys(unsigned long long* key, int* stamp, long long n_states_total, hipStream_t s);

@@ -1257,6 +1257,7 @@ __device__ float expand_emitting(const DecArgs& a, DecShared& sh, DecPtrs& p, co
   return block_min_f(sh, m);
 }
 
+template <bool PROF>
 __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   __shared__ DecShared sh;
   __shared__ float L[kLlhLds];
@@ -1291,7 +1292,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   int arcs_eps = 0;
   bool lds = false;
   // optional phase clocks (diagnostics): thread 0 stamps s_memtime
-  const bool prof = a.prof != nullptr && threadIdx.x == 0;
+  const bool prof = PROF && threadIdx.x == 0;
   long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   long long tstamp = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
 #define DEC_PHASE(i)                                                     \
@@ -1411,7 +1412,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     // Frames predicted too large for the LDS table (many current tokens) go
     // straight to the global maps; a frame that overflows anyway is rebuilt
     // there (nothing global was written).
-    const bool try_lds = ntok <= kLdsFrameTokens;
+    const bool try_lds = ntok <= a.lds_frame_tokens;
     if (try_lds) {
       if (seed != __int_as_float(0x7f800000)) {
         const float m = expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
@@ -1499,9 +1500,12 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
 #undef DEC_PHASE
 }
 
+int DecoderLdsFrameTokens() { return kLdsFrameTokens; }
+
 void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s) {
   if (njobs <= 0) return;
-  hipLaunchKernelGGL(decode_kernel, dim3(njobs), dim3(DT), 0, s, a);
+  if (a.prof) hipLaunchKernelGGL(decode_kernel<true>, dim3(njobs), dim3(DT), 0, s, a);
+  else hipLaunchKernelGGL(decode_kernel<false>, dim3(njobs), dim3(DT), 0, s, a);
 }
 
 // ---------------------------------------------------------------------------
