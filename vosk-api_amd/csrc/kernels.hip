@@ -580,7 +580,11 @@ void LaunchNnetGemm(const NnetOpArgs& a, int bk, hipStream_t s) {
   if (var == 0) var = GemmStreamable(a) ? 1 : 3;
   if ((var == 1 || var == 2) && !GemmStreamable(a)) var = 3;
   if (var == 1) {
-    if (nb == 3) LaunchStream<3>(a, s);
+    // small grids: one 32-column block per wave (3x / 2x the waves, more of
+    // the chip busy) beats the wider tile's operand reuse
+    const long long waves = (long long)((a.M + 31) / 32) * ((a.N + 32 * nb - 1) / (32 * nb)) * a.kslices;
+    if (waves < 1500 && g_gemm_variant == 0) LaunchStream<1>(a, s);
+    else if (nb == 3) LaunchStream<3>(a, s);
     else LaunchStream<2>(a, s);
   } else if (var == 2) {
     LaunchStream<1>(a, s);
