@@ -23,6 +23,8 @@
 //   traceback       best-path end selection + backpointer walk
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdint>
 
 #include "engine_dev.h"
@@ -583,7 +585,8 @@ void LaunchNnetGemm(const NnetOpArgs& a, int bk, hipStream_t s) {
     // small grids: one 32-column block per wave (3x / 2x the waves, more of
     // the chip busy) beats the wider tile's operand reuse
     const long long waves = (long long)((a.M + 31) / 32) * ((a.N + 32 * nb - 1) / (32 * nb)) * a.kslices;
-    if (waves < 1500 && g_gemm_variant == 0) LaunchStream<1>(a, s);
+    static const int nb1_waves = getenv("VOSK_AMD_NB1_WAVES") ? atoi(getenv("VOSK_AMD_NB1_WAVES")) : 4000;
+    if (waves < nb1_waves && g_gemm_variant == 0) LaunchStream<1>(a, s);
     else if (nb == 3) LaunchStream<3>(a, s);
     else LaunchStream<2>(a, s);
   } else if (var == 2) {
