@@ -102,8 +102,8 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="decoder in order after the nnet (default: decoder of step i-1 "
                          "concurrently with the nnet of step i on a second HIP stream)")
-    ap.add_argument("--cpu-streams", type=int, default=32)
-    ap.add_argument("--cpu-seconds", type=float, default=60.0)
+    ap.add_argument("--cpu-streams", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=300.0)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))

@@ -35,7 +35,7 @@ def main(out):
         res["kernels"][k] = {"launches_fetch_pass": fn, "launches_write_pass": wn,
                              "fetch_bytes_per_launch": f, "write_bytes_per_launch": w,
                              "hbm_bytes_per_launch": (f or 0) + (w or 0)}
-    dk = [k for k in res["kernels"] if k.endswith("decode_kernel")]
+    dk = [k for k in res["kernels"] if "decode_kernel" in k]
     if dk:
         res["hbm_bytes_per_launch"] = res["kernels"][dk[0]]["hbm_bytes_per_launch"]
         res["kernel"] = dk[0]
