@@ -47,6 +47,11 @@ int vamd_engine_info(VamdEngine *e, int *out8, double *flops_per_chunk);
 
 int vamd_stream_new(VamdEngine *e);
 int vamd_stream_free(VamdEngine *e, int stream);
+/* input sample rate of a stream (default: the model's); others are resampled
+ * on the GPU (windowed sinc, Kaldi LinearResample; replaces the resampling of
+ * the reference's feature pipeline, src/model.cc:221, and batch path,
+ * src/batch_recognizer.cc:27-29).  Set before the stream's first samples. */
+int vamd_stream_set_rate(VamdEngine *e, int stream, int rate);
 int vamd_stream_reset(VamdEngine *e, int stream, int pipeline);
 /* queue samples (int16-range floats); finished=1 marks end of input */
 int vamd_stream_accept(VamdEngine *e, int stream, const float *samples, int n, int finished);

@@ -48,6 +48,61 @@ int orc_mfcc_num_frames(const orc_mfcc_opts* o, long n) {
    float4 per lane accumulates).  Kaldi's own order is whatever its BLAS does
    (matrix/kaldi-matrix.cc AddMatMat -> cblas_sgemm), so any fixed order is a
    faithful restatement of the arithmetic. */
+/* ---- resampling (Kaldi LinearResample, feat/resample.cc) ---------------- */
+static long gcd_l(long a, long b) { while (b) { long t = a % b; a = b; b = t; } return a; }
+
+static float resample_filter(double cutoff, int num_zeros, float t) {
+  float window, filter;
+  if (fabs(t) < num_zeros / (2.0 * cutoff))
+    window = (float)(0.5 * (1 + cos(2.0 * M_PI * cutoff / num_zeros * t)));
+  else
+    window = 0.0f;
+  if (t != 0.0f)
+    filter = (float)(sin(2.0 * M_PI * cutoff * t) / (M_PI * t));
+  else
+    filter = (float)(2.0 * cutoff);
+  return filter * window;
+}
+
+long orc_resample_num_outputs(int rate_in, int rate_out, long n) {
+  /* GetNumOutputSamples with flush */
+  const long g = gcd_l(rate_in, rate_out);
+  const long tick = (long)rate_in / g * rate_out;
+  long interval = n * (tick / rate_in);
+  if (interval <= 0) return 0;
+  const long tpo = tick / rate_out;
+  long last = interval / tpo;
+  if (last * tpo == interval) last--;
+  return last + 1;
+}
+
+long orc_resample(int rate_in, int rate_out, const float* x, long n, float* out, long cap) {
+  const int num_zeros = 6;
+  const double cutoff = 0.5 * (rate_in < rate_out ? rate_in : rate_out);
+  const long g = gcd_l(rate_in, rate_out);
+  const int in_unit = (int)(rate_in / g), out_unit = (int)(rate_out / g);
+  const double ww = num_zeros / (2.0 * cutoff);
+  const long nout = orc_resample_num_outputs(rate_in, rate_out, n);
+  if (nout > cap) return -1;
+  for (long k = 0; k < nout; k++) {
+    const long unit = k / out_unit;
+    const int ph = (int)(k - unit * out_unit);
+    const double output_t = ph / (double)rate_out;
+    const int lo = (int)ceil((output_t - ww) * rate_in), hi = (int)floor((output_t + ww) * rate_in);
+    const long first = lo + unit * in_unit;
+    float acc = 0.0f;
+    for (int j = 0; j <= hi - lo; j++) {
+      const long idx = first + j;
+      if (idx < 0 || idx >= n) continue;
+      const double delta_t = (lo + j) / (double)rate_in - output_t;
+      const float w = resample_filter(cutoff, num_zeros, (float)delta_t) / (float)rate_in;
+      acc = fmaf(w, x[idx], acc);
+    }
+    out[k] = acc;
+  }
+  return nout;
+}
+
 int orc_kslices(int K) { return (K >= 512 && K % 256 == 0) ? K / 256 : 1; }
 
 float orc_logf(float x) {

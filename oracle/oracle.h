@@ -33,6 +33,15 @@ typedef struct {
   int round_to_power_of_two;
 } orc_mfcc_opts;
 
+/* Windowed-sinc resampling (Kaldi feat/resample.cc LinearResample, as the
+   reference uses it: src/batch_recognizer.cc:27-29, filter cutoff
+   min(rate_in, rate_out)/2, 6 zeros), whole signal with end-of-input flush.
+   Output sample k = sequential fmaf chain over the taps of its phase (in tap
+   order, from 0), input samples outside [0, n) contribute nothing.
+   Returns the number of output samples (<= cap) or -1. */
+long orc_resample_num_outputs(int rate_in, int rate_out, long n);
+long orc_resample(int rate_in, int rate_out, const float* x, long n, float* out, long cap);
+
 int orc_mfcc_num_frames(const orc_mfcc_opts* o, long num_samples);
 /* wave: float samples (int16 range).  out: [frames][num_ceps]. returns frames */
 int orc_mfcc(const orc_mfcc_opts* o, const float* wave, long num_samples, float* out);

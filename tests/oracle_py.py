@@ -33,10 +33,24 @@ def load_lib():
     lib.orc_logf.argtypes = [C.c_float]
     lib.orc_nnet_forward.restype = C.c_int
     lib.orc_decode.restype = C.c_int
+    lib.orc_resample_num_outputs.restype = C.c_long
+    lib.orc_resample_num_outputs.argtypes = [C.c_int, C.c_int, C.c_long]
+    lib.orc_resample.restype = C.c_long
+    lib.orc_resample.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_long, C.c_void_p, C.c_long]
     return lib
 
 
 _lib = None
+
+
+def resample(x, rate_in, rate_out):
+    """Whole-signal windowed-sinc resampling with end flush (oracle.c)."""
+    x = np.ascontiguousarray(x, np.float32)
+    n = lib().orc_resample_num_outputs(rate_in, rate_out, len(x))
+    out = np.zeros(max(n, 1), np.float32)
+    got = lib().orc_resample(rate_in, rate_out, x.ctypes.data, len(x), out.ctypes.data, len(out))
+    assert got == n, (got, n)
+    return out[:n]
 
 
 def lib():

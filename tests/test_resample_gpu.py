@@ -1,0 +1,51 @@
+"""Input-rate conversion on the GPU (A3): features of a resampled stream and
+an 8 kHz KaldiRecognizer against the oracle (resample -> MFCC -> decode)."""
+import json
+
+import numpy as np
+import pytest
+
+import oracle_py
+
+pytestmark = pytest.mark.gpu
+
+
+def _at_rate(wave16k, rate):
+    """Test input at another rate (any interpolation will do: it is only data)."""
+    n = int(len(wave16k) * rate / 16000)
+    t = np.arange(n) * (16000.0 / rate)
+    return np.round(np.interp(t, np.arange(len(wave16k)), wave16k)).astype(np.float32)
+
+
+@pytest.mark.parametrize("rate", [8000, 22050, 44100, 48000])
+def test_resampled_features_bit_exact(synth_model, test_wave, rate):
+    from vosk import engine
+    o = oracle_py.OracleModel(synth_model)
+    x = _at_rate(test_wave[:32000], rate)
+    ref = o.features(oracle_py.resample(x, rate, 16000))
+    e = engine.Engine(synth_model, max_streams=2)
+    s = e.new_stream()
+    e.set_rate(s, rate)
+    step = 1237  # odd chunks: outputs span chunk boundaries
+    for i in range(0, len(x), step):
+        e.accept(s, x[i:i + step])
+        e.advance([s])
+    e.accept(s, np.zeros(0, np.float32), finished=True)
+    e.advance([s])
+    n = ref.shape[0]
+    got = e.features(s, 0, n, ref.shape[1])
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_recognizer_8khz_matches_oracle(synth_model_noep, test_wave):
+    import vosk
+    vosk.SetLogLevel(-1)
+    o = oracle_py.OracleModel(synth_model_noep)
+    x = _at_rate(test_wave, 8000)
+    ref = o.recognize(oracle_py.resample(x, 8000, 16000))
+    m = vosk.Model(synth_model_noep)
+    rec = vosk.KaldiRecognizer(m, 8000)
+    data = x.astype("<i2").tobytes()
+    for i in range(0, len(data), 4000):
+        rec.AcceptWaveform(data[i:i + 4000])
+    assert json.loads(rec.FinalResult())["text"] == ref["text"]

@@ -249,6 +249,11 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   rings_.slots = S;
   rings_.input_node = plan_.input_node;
   d_samples_ = (float*)DevAlloc(sizeof(float) * (size_t)S * sample_ring_);
+  // raw input ring for resampled streams: up to 6x the model rate per step
+  raw_ring_ = Pow2AtLeast((long long)cfg_.max_step_samples * 6 + 8192);
+  max_raw_step_ = raw_ring_ - 8192;
+  d_raw_ = (float*)DevAlloc(sizeof(float) * (size_t)S * raw_ring_);
+  d_res_tables_ = (ResampleDev*)DevAlloc(sizeof(ResampleDev) * kMaxResampleTables);
 
   // ---- nnet ops
   std::vector<float*> vec_ptrs;
@@ -403,7 +408,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
 
   // ---- staging
   stage_bytes_ = Align256(sizeof(float) * (size_t)S * cfg_.max_step_samples) +
-                 Align256(sizeof(SampleJob) * S) + Align256(sizeof(MfccJob) * S) +
+                 2 * Align256(sizeof(SampleJob) * S) + Align256(sizeof(ResampleJob) * S) +
+                 Align256(sizeof(MfccJob) * S) +
                  Align256(sizeof(DevJob) * max_jobs_) + Align256(sizeof(DecJob) * S) + 1024;
   // two halves: a pipelined decoder batch keeps its jobs while the next step stages
   HIPCHECK(hipHostMalloc((void**)&h_stage_, 2 * stage_bytes_, hipHostMallocDefault));
@@ -469,6 +475,8 @@ void Engine::ResetPipeline(int slot) {
   h.resident = nullptr;
   h.resident_n = h.resident_pos = 0;
   h.resident_finish = false;
+  h.raw_pushed = 0;
+  h.res_flushed = false;
 }
 
 void Engine::ResetDecoder(int slot) {
@@ -488,6 +496,41 @@ void Engine::AcceptSamples(int slot, const float* x, int n) {
     h.pending_pos = 0;
   }
   h.pending.insert(h.pending.end(), x, x + n);
+}
+
+void Engine::SetSampleRate(int slot, int rate) {
+  std::lock_guard<std::mutex> lk(mu_);
+  SlotHost& h = slots_.at(slot);
+  if (h.samples > 0 || h.raw_pushed > 0) VAMD_ERR("SetSampleRate after samples were accepted");
+  const int model_rate = (int)std::lround(md_->mfcc.samp_freq);
+  if (rate <= 0) VAMD_ERR("bad sample rate " << rate);
+  if (rate == model_rate) {
+    h.rate = 0;
+    h.table = -1;
+    return;
+  }
+  int t = -1;
+  for (size_t i = 0; i < res_tables_.size(); i++)
+    if (res_tables_[i].rate_in == rate) t = (int)i;
+  if (t < 0) {
+    if ((int)res_tables_.size() >= kMaxResampleTables) VAMD_ERR("too many distinct input sample rates");
+    ResampleTable tb = BuildResampleTable(rate, model_rate);
+    ResampleDev d;
+    d.first = Upload(tb.first);
+    d.ntaps = Upload(tb.ntaps);
+    d.w = Upload(tb.w);
+    d.in_unit = tb.in_unit;
+    d.out_unit = tb.out_unit;
+    d.taps = tb.taps;
+    d.pad = 0;
+    t = (int)res_tables_.size();
+    HIPCHECK(hipMemcpy(d_res_tables_ + t, &d, sizeof(d), hipMemcpyHostToDevice));
+    res_tables_.push_back(std::move(tb));
+    VAMD_LOG_VERBOSE("resampling " << rate << " -> " << model_rate << " Hz, " << res_tables_[t].taps
+                                   << " taps");
+  }
+  h.rate = rate;
+  h.table = t;
 }
 
 void Engine::PreloadSamples(int slot, const float* x, long long n, bool finished) {
@@ -522,6 +565,9 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
   st_samples_.clear();
   st_sample_src_.clear();
   st_sample_data_.clear();
+  st_raw_.clear();
+  st_raw_src_.clear();
+  st_res_.clear();
   st_mfcc_.clear();
   st_mfcc_total_ = 0;
   st_jobs_.clear();
@@ -533,7 +579,54 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
     SlotHost& h = slots_.at(s);
     if (!h.used) continue;
     // 1. samples: HBM-resident audio first, then host-fed samples
-    if (h.resident && h.resident_pos < h.resident_n) {
+    if (h.rate != 0) {
+      // resampled stream: raw samples -> raw ring, then the outputs their
+      // windows complete (all remaining ones at end of input) -> sample ring
+      const ResampleTable& T = res_tables_[h.table];
+      const bool from_res = h.resident && h.resident_pos < h.resident_n;
+      const long long avail = from_res ? h.resident_n - h.resident_pos
+                                       : (long long)(h.pending.size() - h.pending_pos);
+      long long n = std::min<long long>(avail, max_raw_step_);
+      if (!from_res)  // host-fed samples share the step's staging buffer
+        n = std::min<long long>(n, (long long)slots_.size() * cfg_.max_step_samples -
+                                       (long long)st_sample_data_.size());
+      if (n < 0) n = 0;
+      auto ends_after = [&](long long nn) {
+        return nn == avail && (from_res ? h.resident_finish : h.finished);
+      };
+      bool flush = !h.res_flushed && ends_after(n);
+      long long tot = T.NumOutputSamples(h.raw_pushed + n, flush);
+      while (tot - h.samples > cfg_.max_step_samples && n > 0) {
+        n -= std::max<long long>(1, (tot - h.samples - cfg_.max_step_samples) * T.in_unit / T.out_unit + 1);
+        if (n < 0) n = 0;
+        flush = false;
+        tot = T.NumOutputSamples(h.raw_pushed + n, false);
+      }
+      if (n > 0) {
+        const int pos = (int)(h.raw_pushed & (raw_ring_ - 1));
+        if (from_res) {
+          st_raw_.push_back(SampleJob{s, pos, (int)n, 0, h.resident + h.resident_pos});
+          st_raw_src_.push_back(-1);
+          h.resident_pos += n;
+          if (h.resident_pos == h.resident_n && h.resident_finish) h.finished = true;
+        } else {
+          st_raw_.push_back(SampleJob{s, pos, (int)n, 0, nullptr});
+          st_raw_src_.push_back((int)st_sample_data_.size());
+          st_sample_data_.insert(st_sample_data_.end(), h.pending.begin() + h.pending_pos,
+                                 h.pending.begin() + h.pending_pos + n);
+          h.pending_pos += n;
+        }
+        h.raw_pushed += n;
+        any = true;
+      }
+      if (tot > h.samples) {
+        st_res_.push_back(ResampleJob{s, (int)(h.samples & (sample_ring_ - 1)), (int)(tot - h.samples),
+                                      h.table, h.samples, h.raw_pushed});
+        h.samples = tot;
+        any = true;
+      }
+      if (flush) h.res_flushed = true;
+    } else if (h.resident && h.resident_pos < h.resident_n) {
       int n = (int)std::min<long long>(h.resident_n - h.resident_pos, cfg_.max_step_samples);
       SampleJob j{s, (int)(h.samples & (sample_ring_ - 1)), n, 0, h.resident + h.resident_pos};
       st_samples_.push_back(j);
@@ -565,7 +658,8 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
     }
     // 3. chunk jobs (DecodableNnetLoopedOnline::NumFramesReady semantics)
     const bool fin = h.finished && h.pending_pos == h.pending.size() &&
-                     (!h.resident || h.resident_pos == h.resident_n);
+                     (!h.resident || h.resident_pos == h.resident_n) &&
+                     (h.rate == 0 || h.res_flushed);
     const int T = h.frames;
     const int need_out = fin ? (T + fss - 1) / fss : 0;
     int first_real = -1, dec_frames = 0, njobs = 0;
@@ -669,7 +763,11 @@ void Engine::RunStep(bool allow_pipeline) {
   for (size_t i = 0; i < st_samples_.size(); i++)
     if (st_sample_src_[i] >= 0)
       st_samples_[i].src = (const float*)(dsg + o_data) + st_sample_src_[i];
+  for (size_t i = 0; i < st_raw_.size(); i++)
+    if (st_raw_src_[i] >= 0) st_raw_[i].src = (const float*)(dsg + o_data) + st_raw_src_[i];
   size_t o_sj = put(st_samples_.data(), sizeof(SampleJob) * st_samples_.size());
+  size_t o_rj = put(st_raw_.data(), sizeof(SampleJob) * st_raw_.size());
+  size_t o_resj = put(st_res_.data(), sizeof(ResampleJob) * st_res_.size());
   size_t o_mj = put(st_mfcc_.data(), sizeof(MfccJob) * st_mfcc_.size());
   size_t o_dj = put(st_jobs_.data(), sizeof(DevJob) * st_jobs_.size());
   DecBatch cur;
@@ -683,6 +781,11 @@ void Engine::RunStep(bool allow_pipeline) {
   HIPCHECK(hipMemcpyAsync(dsg, hs, off, hipMemcpyHostToDevice, stream_));
   int launches = 0;
   if (tk) HIPCHECK(hipEventRecord(ev_[1], stream_));
+  LaunchAppendSamples((const SampleJob*)(dsg + o_rj), (int)st_raw_.size(), d_raw_, raw_ring_,
+                      stream_);
+  LaunchResample((const ResampleJob*)(dsg + o_resj), (int)st_res_.size(), d_res_tables_, d_raw_,
+                 raw_ring_, d_samples_, sample_ring_, stream_);
+  launches += !st_raw_.empty() + !st_res_.empty();
   LaunchAppendSamples((const SampleJob*)(dsg + o_sj), (int)st_samples_.size(), d_samples_,
                       sample_ring_, stream_);
   launches += !st_samples_.empty();
@@ -861,6 +964,9 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     st_samples_.clear();
     st_sample_src_.clear();
     st_sample_data_.clear();
+    st_raw_.clear();
+    st_raw_src_.clear();
+    st_res_.clear();
     st_mfcc_.clear();
     st_mfcc_total_ = 0;
     st_jobs_.clear();

@@ -21,6 +21,7 @@
 #include "engine_dev.h"
 #include "model_io.h"
 #include "nnet_plan.h"
+#include "resample.h"
 
 namespace vamd {
 
@@ -80,6 +81,8 @@ struct EngineCounters {
   long long steps = 0, launches = 0, frames_mfcc = 0, chunk_jobs = 0, frames_decoded = 0;
 };
 
+constexpr int kMaxResampleTables = 32;  // distinct input sample rates per engine
+
 class Engine {
  public:
   Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg);
@@ -98,6 +101,9 @@ class Engine {
   void ResetPipeline(int slot);
   // InitDecoding: the decoder restarts, the feature/nnet pipeline continues.
   void ResetDecoder(int slot);
+  // Input sample rate of a stream (default: the model's); other rates are
+  // resampled on the GPU (resample.h).  Set before the stream's first samples.
+  void SetSampleRate(int slot, int rate);
   void AcceptSamples(int slot, const float* x, int n);
   // Uploads a stream's whole audio into HBM; later steps read it from there
   // (no host->device copy inside the steps).  finished: end of input after it.
@@ -151,6 +157,10 @@ class Engine {
     float* resident = nullptr;  // HBM-resident audio (PreloadSamples)
     long long resident_n = 0, resident_pos = 0;
     bool resident_finish = false;
+    int rate = 0;              // input rate when resampled (0: model rate)
+    int table = -1;            // resample table
+    long long raw_pushed = 0;  // raw (input-rate) samples pushed to the raw ring
+    bool res_flushed = false;  // resampler flushed at end of input
   };
   struct DecBatch {  // one decoder launch's jobs, staged in one staging half
     std::vector<DecJob> jobs;
@@ -192,6 +202,10 @@ class Engine {
   int4* d_arcs_ = nullptr;
   // device: per-stream state
   float* d_samples_ = nullptr;
+  float* d_raw_ = nullptr;  // [slots][raw_ring_] input-rate samples of resampled streams
+  int raw_ring_ = 0, max_raw_step_ = 0;
+  std::vector<ResampleTable> res_tables_;
+  ResampleDev* d_res_tables_ = nullptr;  // [kMaxResampleTables]
   float* d_llh_ = nullptr;  // = d_llh_buf_[0]
   float* d_llh_buf_[2] = {nullptr, nullptr};
   DecArgs dec_{};
@@ -205,6 +219,9 @@ class Engine {
   FrameStat* h_stats_ = nullptr;
   // current step
   std::vector<SampleJob> st_samples_;
+  std::vector<SampleJob> st_raw_;      // raw (input-rate) samples of resampled streams
+  std::vector<int> st_raw_src_;
+  std::vector<ResampleJob> st_res_;
   std::vector<int> st_sample_src_;  // offset into st_sample_data_, -1 = resident
   std::vector<float> st_sample_data_;
   std::vector<MfccJob> st_mfcc_;

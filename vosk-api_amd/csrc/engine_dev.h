@@ -73,6 +73,19 @@ struct MfccJob {  // frames [first, first+count) of one slot; rows [row0, row0+c
   int slot, first, count, row0;
 };
 
+// windowed-sinc resampling (resample.h): output sample k of a stream is the
+// tap-ordered fma chain over raw[first[k % out_unit] + (k / out_unit) * in_unit + j]
+struct ResampleDev {
+  const int* first;   // [out_unit]
+  const int* ntaps;   // [out_unit]
+  const float* w;     // [out_unit][taps]
+  int in_unit, out_unit, taps, pad;
+};
+struct ResampleJob {  // outputs [out_first, out_first + count) into the sample ring
+  int slot, pos, count, table;
+  long long out_first, raw_total;  // raw samples available (later ones read as 0)
+};
+
 struct SampleJob {  // append count samples from src[] to ring position pos
   int slot, pos, count, pad;
   const float* src;  // staging buffer (host-fed) or the stream's HBM-resident audio

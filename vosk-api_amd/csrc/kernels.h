@@ -9,6 +9,8 @@ namespace vamd {
 
 void LaunchAppendSamples(const SampleJob* jobs, int njobs, float* ring, int ring_len,
                          hipStream_t s);
+void LaunchResample(const ResampleJob* jobs, int njobs, const ResampleDev* tables, const float* raw,
+                    int raw_len, float* ring, int ring_len, hipStream_t s);
 void LaunchMfcc(const MfccDev& m, const MfccJob* jobs, int njobs, int total_frames,
                 const float* sample_ring, int sample_ring_len, const RingSet& rings,
                 hipStream_t s);

@@ -88,6 +88,39 @@ void LaunchAppendSamples(const SampleJob* jobs, int njobs, float* ring, int ring
   hipLaunchKernelGGL(append_samples_kernel, dim3(njobs), dim3(256), 0, s, jobs, ring, ring_len);
 }
 
+// one block per job, one thread per output sample (taps ~ 12-40)
+__global__ __launch_bounds__(256) void resample_kernel(const ResampleJob* jobs,
+                                                       const ResampleDev* tables,
+                                                       const float* raw, int raw_len, float* ring,
+                                                       int ring_len) {
+  const ResampleJob j = jobs[blockIdx.x];
+  const ResampleDev t = tables[j.table];
+  const float* src = raw + (size_t)j.slot * raw_len;
+  float* dst = ring + (size_t)j.slot * ring_len;
+  for (int i = threadIdx.x; i < j.count; i += blockDim.x) {
+    const long long k = j.out_first + i;
+    const long long unit = k / t.out_unit;
+    const int ph = (int)(k - unit * t.out_unit);
+    const long long first = t.first[ph] + unit * t.in_unit;
+    const int nt = t.ntaps[ph];
+    const float* w = t.w + (size_t)ph * t.taps;
+    float acc = 0.0f;
+    for (int q = 0; q < nt; q++) {
+      const long long idx = first + q;
+      if (idx < 0 || idx >= j.raw_total) continue;
+      acc = __builtin_fmaf(w[q], src[idx & (raw_len - 1)], acc);
+    }
+    dst[(j.pos + i) & (ring_len - 1)] = acc;
+  }
+}
+
+void LaunchResample(const ResampleJob* jobs, int njobs, const ResampleDev* tables, const float* raw,
+                    int raw_len, float* ring, int ring_len, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(resample_kernel, dim3(njobs), dim3(256), 0, s, jobs, tables, raw, raw_len,
+                     ring, ring_len);
+}
+
 // ===========================================================================
 // MFCC: 4 frames per 256-thread block, one wave per frame
 // ===========================================================================

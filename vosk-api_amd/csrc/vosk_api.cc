@@ -319,6 +319,13 @@ int vamd_stream_new(VamdEngine* e) {
   API_CATCH(-1)
 }
 
+int vamd_stream_set_rate(VamdEngine* e, int s, int rate) {
+  API_TRY
+  e->eng->SetSampleRate(s, rate);
+  return 0;
+  API_CATCH(-1)
+}
+
 int vamd_stream_free(VamdEngine* e, int s) {
   API_TRY
   e->eng->FreeSlot(s);

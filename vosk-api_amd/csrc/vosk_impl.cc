@@ -101,12 +101,25 @@ Engine* Model::StreamEngine() {
 // ---------------------------------------------------------------------------
 // Recognizer (src/recognizer.cc)
 // ---------------------------------------------------------------------------
+// Input at another rate than the model's is resampled on the GPU (windowed
+// sinc, Kaldi LinearResample; the reference's feature pipeline resamples with
+// allow_downsample/upsample, src/model.cc:221).
+static int InputRate(float sr) {
+  const int r = (int)std::lround(sr);
+  if (r <= 0 || std::fabs(sr - r) > 1e-3f) VAMD_ERR("unsupported sample rate " << sr);
+  return r;
+}
+
 Recognizer::Recognizer(Model* model, float sr) : model_(model), sample_frequency_(sr) {
-  if (std::fabs(sr - model->data()->mfcc.samp_freq) > 0.5f)
-    VAMD_ERR("sample rate " << sr << " != model rate " << model->data()->mfcc.samp_freq
-                            << " (resampling is a next row, see DESIGN.md)");
+  const int rate = InputRate(sr);
   engine_ = model->StreamEngine();
   slot_ = engine_->AllocSlot();
+  try {
+    engine_->SetSampleRate(slot_, rate);
+  } catch (...) {
+    engine_->FreeSlot(slot_);
+    throw;
+  }
   model_->Ref();
 }
 
@@ -418,10 +431,18 @@ void BatchModel::Worker() {
 }
 
 BatchRecognizer::BatchRecognizer(BatchModel* model, float sr) : model_(model), sample_frequency_(sr) {
-  if (std::fabs(sr - model->data().mfcc.samp_freq) > 0.5f)
-    VAMD_ERR("sample rate " << sr << " != model rate (resampling is a next row)");
+  // the reference resamples each call independently (flush per call,
+  // src/batch_recognizer.cc:27-29,157-158); here the stream is resampled
+  // continuously (no discontinuity at call boundaries)
+  const int rate = InputRate(sr);
   slot_ = model_->engine()->AllocSlot();
   model_->engine()->ResetPipeline(slot_);
+  try {
+    model_->engine()->SetSampleRate(slot_, rate);
+  } catch (...) {
+    model_->engine()->FreeSlot(slot_);
+    throw;
+  }
   model_->Register(this);
 }
 

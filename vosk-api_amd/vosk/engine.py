@@ -24,6 +24,7 @@ _SIGS = {
     "vamd_engine_info": (C.c_int, [_vp, _vp, _vp]),
     "vamd_stream_new": (C.c_int, [_vp]),
     "vamd_stream_free": (C.c_int, [_vp, C.c_int]),
+    "vamd_stream_set_rate": (C.c_int, [_vp, C.c_int, C.c_int]),
     "vamd_stream_reset": (C.c_int, [_vp, C.c_int, C.c_int]),
     "vamd_stream_accept": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int]),
     "vamd_engine_advance": (C.c_int, [_vp, _vp, C.c_int]),
@@ -116,6 +117,9 @@ class Engine:
 
     def new_stream(self):
         return _chk(_c.vamd_stream_new(self.h))
+
+    def set_rate(self, s, rate):
+        _chk(_c.vamd_stream_set_rate(self.h, s, int(rate)))
 
     def free_stream(self, s):
         _chk(_c.vamd_stream_free(self.h, s))
