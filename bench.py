@@ -52,7 +52,7 @@ def stream_audio(base, i, n):
 
 def bench_model(rank, dist):
     import make_synth_model
-    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", "bench_v1")
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", "bench_v2")
     if rank == 0 and not os.path.exists(os.path.join(cache, "README")):
         make_synth_model.make_model(cache, seed=11, vocab=20000, num_pdfs=2000)
     if dist is not None:
@@ -79,7 +79,7 @@ _ORC = {}
 
 def _cpu_init(model):
     import oracle_py
-    _ORC["m"] = oracle_py.OracleModel(model)
+    _ORC["m"] = oracle_py.OracleModel(model, fpc=51)  # the engine's chunking (i-vector per chunk)
     _ORC["base"] = load_wave()
 
 

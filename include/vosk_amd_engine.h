@@ -63,6 +63,10 @@ int vamd_stream_error(VamdEngine *e, int stream);
 int vamd_stream_features(VamdEngine *e, int stream, int first, int n, float *out);
 /* decoded log-likelihood rows (flag 2): copies up to cap floats, returns count */
 long long vamd_stream_llh(VamdEngine *e, int stream, float *out, long long cap);
+/* i-vector of every chunk computed so far (flag 2), [chunks][ivector dim]:
+ * copies up to cap floats, returns the count; ivector dim 0 = no i-vector input */
+long long vamd_stream_ivectors(VamdEngine *e, int stream, float *out, long long cap);
+int vamd_engine_ivector_dim(VamdEngine *e);
 /* per-frame stats of the last advance (flag 1): 8 floats per frame
  * {ntok_in, ntok_out, arcs_emit, arcs_eps, best, cutoff, next_cutoff, adaptive_beam} */
 int vamd_stream_stats(VamdEngine *e, int stream, float *out, int cap_frames);

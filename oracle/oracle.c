@@ -48,6 +48,218 @@ int orc_mfcc_num_frames(const orc_mfcc_opts* o, long n) {
    float4 per lane accumulates).  Kaldi's own order is whatever its BLAS does
    (matrix/kaldi-matrix.cc AddMatMat -> cblas_sgemm), so any fixed order is a
    faithful restatement of the arithmetic. */
+/* ---- exp for posteriors: 2^k * e^r, |r| <= ln2/2, degree-7 Taylor (Horner,
+   fmaf).  Shared bit-for-bit with kernels.hip dev_expf. */
+float orc_expf(float x) {
+  if (x < -87.0f) return 0.0f;
+  const float k = rintf(x * 1.44269504f);
+  float r = fmaf(-k, 0.693145752f, x);
+  r = fmaf(-k, 1.42860677e-6f, r);
+  float p = 1.98412698e-4f;
+  p = fmaf(p, r, 1.38888889e-3f);
+  p = fmaf(p, r, 8.33333333e-3f);
+  p = fmaf(p, r, 4.16666667e-2f);
+  p = fmaf(p, r, 1.66666667e-1f);
+  p = fmaf(p, r, 0.5f);
+  p = fmaf(p, r, 1.0f);
+  p = fmaf(p, r, 1.0f);
+  return ldexpf(p, (int)k);
+}
+
+/* ---- online i-vector extraction ----------------------------------------- */
+static void iv_lda(const orc_ivector_model* m, const float* src, int t, int t_ready, float* y) {
+  const int D = m->feat_dim, ctx = m->left + m->right + 1, K = ctx * D;
+  float x[64 * 16];
+  for (int c = 0; c < ctx; c++) {
+    int u = t - m->left + c;
+    if (u < 0) u = 0;
+    if (u > t_ready - 1) u = t_ready - 1;
+    memcpy(x + c * D, src + (size_t)u * D, sizeof(float) * D);
+  }
+  for (int i = 0; i < m->lda_rows; i++) {
+    const float* w = m->lda + (size_t)i * m->lda_cols;
+    float a = 0.0f;
+    for (int j = 0; j < K; j++) a = fmaf(w[j], x[j], a);
+    if (m->lda_cols == K + 1) a = a + w[K];
+    y[i] = a;
+  }
+}
+
+static void iv_matvec(const double* Q, int S, const double* x, double* y) {
+  /* Q packed lower triangle (row i: i+1 entries) */
+  for (int i = 0; i < S; i++) {
+    double a = 0.0;
+    for (int j = 0; j < S; j++) {
+      const int r = i > j ? i : j, c = i > j ? j : i;
+      a = a + Q[(size_t)r * (r + 1) / 2 + c] * x[j];
+    }
+    y[i] = a;
+  }
+}
+
+static double iv_dot(const double* a, const double* b, int n) {
+  double s = 0.0;
+  for (int i = 0; i < n; i++) s = s + a[i] * b[i];
+  return s;
+}
+
+static void iv_cgd(const double* Q, const double* b, int S, int max_iters, double* x) {
+  double p[128], r[128], Ap[128];
+  iv_matvec(Q, S, x, Ap);
+  for (int i = 0; i < S; i++) p[i] = b[i] - Ap[i];
+  for (int i = 0; i < S; i++) r[i] = -p[i];
+  double rcur = iv_dot(r, r, S), rrec = rcur;
+  for (int k = 0; k < S + 5 && k != max_iters; k++) {
+    iv_matvec(Q, S, p, Ap);
+    const double alpha = -iv_dot(p, r, S) / iv_dot(p, Ap, S);
+    for (int i = 0; i < S; i++) x[i] = x[i] + alpha * p[i];
+    for (int i = 0; i < S; i++) r[i] = r[i] + alpha * Ap[i];
+    double rnext = iv_dot(r, r, S);
+    if (rnext < 1e-4 * rrec || rnext > 1e4 * rrec) {
+      iv_matvec(Q, S, x, Ap);
+      for (int i = 0; i < S; i++) r[i] = Ap[i] - b[i];
+      rnext = iv_dot(r, r, S);
+      rrec = rnext;
+    }
+    if (rnext <= 2.2250738585072014e-308) break;
+    const double beta = rnext / rcur;
+    for (int i = 0; i < S; i++) p[i] = beta * p[i] - r[i];
+    rcur = rnext;
+  }
+}
+
+int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, const int* requests,
+                        const int* t_ready, int nreq, float* out) {
+  const int D = m->feat_dim, DL = m->lda_rows, S = m->ivec_dim, G = m->num_gauss;
+  const int QS = S * (S + 1) / 2;
+  /* derived extractor terms (IvectorExtractor::ComputeDerivedVars) */
+  double* SIM = (double*)malloc(sizeof(double) * (size_t)G * DL * S);
+  double* U = (double*)malloc(sizeof(double) * (size_t)G * QS);
+  for (int g = 0; g < G; g++) {
+    const double* M = m->M + (size_t)g * DL * S;
+    const double* SI = m->sigma_inv + (size_t)g * DL * DL;
+    double* sm = SIM + (size_t)g * DL * S;
+    for (int d = 0; d < DL; d++)
+      for (int s2 = 0; s2 < S; s2++) {
+        double a = 0.0;
+        for (int e = 0; e < DL; e++) a = a + SI[(size_t)d * DL + e] * M[(size_t)e * S + s2];
+        sm[(size_t)d * S + s2] = a;
+      }
+    double* u = U + (size_t)g * QS;
+    for (int i = 0; i < S; i++)
+      for (int j = 0; j <= i; j++) {
+        double a = 0.0;
+        for (int d = 0; d < DL; d++) a = a + M[(size_t)d * S + i] * sm[(size_t)d * S + j];
+        u[(size_t)i * (i + 1) / 2 + j] = a;
+      }
+  }
+  /* online CMVN (window cmn_window, smoothed with global_frames of global stats) */
+  float* norm = (float*)malloc(sizeof(float) * (size_t)(T > 0 ? T : 1) * D);
+  {
+    double sum[64] = {0}, n = 0.0;
+    const double gcount = m->cmvn[D];
+    for (int t = 0; t < T; t++) {
+      for (int d = 0; d < D; d++) sum[d] = sum[d] + (double)feats[(size_t)t * D + d];
+      n = n + 1.0;
+      if (t - m->cmn_window >= 0) {
+        for (int d = 0; d < D; d++) sum[d] = sum[d] - (double)feats[(size_t)(t - m->cmn_window) * D + d];
+        n = n - 1.0;
+      }
+      double st[64], cnt = n;
+      for (int d = 0; d < D; d++) st[d] = sum[d];
+      if (cnt < m->cmn_window) {
+        double cg = m->cmn_window - cnt;
+        if (cg > m->global_frames) cg = m->global_frames;
+        const double sc = cg / gcount;
+        for (int d = 0; d < D; d++) st[d] = st[d] + sc * m->cmvn[d];
+        cnt = cnt + sc * gcount;
+      }
+      const float alpha = (float)(-1.0 / cnt);
+      for (int d = 0; d < D; d++) {
+        const float off = (float)((double)alpha * st[d]);
+        norm[(size_t)t * D + d] = feats[(size_t)t * D + d] + off;
+      }
+    }
+  }
+  double lin[128] = {0}, cur[128] = {0};
+  double* quad = (double*)calloc(QS, sizeof(double));
+  lin[0] = m->prior_offset;
+  for (int i = 0; i < S; i++) quad[(size_t)i * (i + 1) / 2 + i] = 1.0;
+  cur[0] = m->prior_offset;
+  double nfr = 0.0;
+  int done = 0;
+  const float log_min_post = (float)log((double)m->min_post);
+  float* ll = (float*)malloc(sizeof(float) * G);
+  float xn[256], xr[256];
+  for (int q = 0; q < nreq; q++) {
+    const int f = requests[q];
+    if (f >= done) {
+      for (int t = done; t <= f; t++) {
+        iv_lda(m, norm, t, t_ready[q], xn);
+        for (int g = 0; g < G; g++) {
+          const float* mi = m->means_invvars + (size_t)g * DL;
+          const float* iv = m->inv_vars + (size_t)g * DL;
+          float d1 = 0.0f, d2 = 0.0f;
+          for (int d = 0; d < DL; d++) d1 = fmaf(mi[d], xn[d], d1);
+          for (int d = 0; d < DL; d++) d2 = fmaf(iv[d], xn[d] * xn[d], d2);
+          ll[g] = (m->gconsts[g] + d1) + (-0.5f * d2);
+        }
+        /* num_gselect best, descending, ties by lower index */
+        int sel[16];
+        int ns = 0;
+        for (int k = 0; k < m->num_gselect && k < G; k++) {
+          int b = -1;
+          for (int g = 0; g < G; g++) {
+            int used = 0;
+            for (int j = 0; j < ns; j++) used |= sel[j] == g;
+            if (used) continue;
+            if (b < 0 || ll[g] > ll[b]) b = g;
+          }
+          sel[ns++] = b;
+        }
+        while (ns > 1 && ll[sel[ns - 1]] < ll[sel[0]] + log_min_post) ns--;
+        float e[16], tot = 0.0f;
+        for (int k = 0; k < ns; k++) {
+          e[k] = orc_expf(ll[sel[k]] - ll[sel[0]]);
+          tot = tot + e[k];
+        }
+        iv_lda(m, feats, t, t_ready[q], xr);
+        double tw = 0.0;
+        for (int k = 0; k < ns; k++) {
+          const float post = (e[k] / tot) * (m->posterior_scale * 1.0f);
+          const double w = (double)post;
+          if (w == 0.0) continue;
+          const double* sm = SIM + (size_t)sel[k] * DL * S;
+          for (int s2 = 0; s2 < S; s2++) {
+            double a = 0.0;
+            for (int d = 0; d < DL; d++) a = fma(sm[(size_t)d * S + s2], (double)xr[d], a);
+            lin[s2] = lin[s2] + w * a;
+          }
+          const double* u = U + (size_t)sel[k] * QS;
+          for (int i = 0; i < QS; i++) quad[i] = quad[i] + w * u[i];
+          tw = tw + w;
+        }
+        if (m->max_count > 0.0) {
+          const double mc = m->max_count;
+          const double oldp = (nfr > mc ? nfr : mc) / mc, newn = nfr + tw;
+          const double newp = (newn > mc ? newn : mc) / mc, ch = newp - oldp;
+          if (ch != 0.0) {
+            lin[0] = lin[0] + m->prior_offset * ch;
+            for (int i = 0; i < S; i++) quad[(size_t)i * (i + 1) / 2 + i] += ch;
+          }
+        }
+        nfr = nfr + tw;
+      }
+      done = f + 1;
+      if (nfr > 0.0) iv_cgd(quad, lin, S, m->num_cg_iters, cur);
+    }
+    for (int i = 0; i < S; i++) out[(size_t)q * S + i] = (float)cur[i];
+    out[(size_t)q * S] = out[(size_t)q * S] - (float)m->prior_offset;
+  }
+  free(SIM); free(U); free(norm); free(quad); free(ll);
+  return 0;
+}
+
 /* ---- resampling (Kaldi LinearResample, feat/resample.cc) ---------------- */
 static long gcd_l(long a, long b) { while (b) { long t = a % b; a = b; b = t; } return a; }
 
@@ -298,6 +510,12 @@ static void eval_desc(const orc_net* net, node_vals* nv, int i, int t, float* x)
       for (int k = 0; k < ninstr; k++) {
         int op = code[4 * k], node = code[4 * k + 1], off = code[4 * k + 2], fi = code[4 * k + 3];
         if (op == 0) stack[sp++] = node_at(net, nv, node, t + off, fi + d);
+        else if (op == 4) {
+          int k = t - net->ivec_t0;
+          if (k < 0) k = 0;
+          if (k >= net->ivec_ntimes) k = net->ivec_ntimes - 1;
+          stack[sp++] = net->ivec[(size_t)net->ivec_of_time[k] * net->ivec_dim + fi + d];
+        }
         else if (op == 1) stack[sp - 1] = net->progf[fi] * stack[sp - 1];
         else if (op == 2) { stack[sp - 2] = stack[sp - 2] + stack[sp - 1]; sp--; }
         else stack[sp++] = net->progf[fi];

@@ -60,10 +60,49 @@ typedef struct {
   const int* prog_begin; const int* prog; const float* progf;
   int output_node, fss;
   float acoustic_scale;
+  /* i-vector input (ReplaceIndex(ivector, t, 0), descriptor op 4): the row
+     computed at time t uses ivec[ivec_of_time[clamp(t - ivec_t0)]] -- the
+     i-vector of the looped chunk that first computes row t */
+  const float* ivec; const int* ivec_of_time;
+  int ivec_t0, ivec_ntimes, ivec_dim;
 } orc_net;
 
 /* out: [ceil(T/fss)][dim(output)] */
 int orc_nnet_forward(const orc_net* net, const float* feats, int T, float* out);
+
+/* ---------------- online i-vector extraction ----------------------------------
+   Kaldi online2/online-ivector-feature.cc (OnlineIvectorFeature with
+   use_most_recent_ivector), ivector/ivector-extractor.cc
+   (OnlineIvectorEstimationStats, max_count via prior scaling),
+   matrix/optimization.cc (LinearCgd), as configured by the reference
+   (src/model.cc:247-263).  Operation order is fixed (shared with the GPU):
+   CMVN running double sums, ApplyCmvn float offsets, LDA / UBM dot products
+   as sequential fmaf chains, posteriors with orc_expf, double statistics,
+   CG with sequential dot products and row-wise mat-vecs. */
+float orc_expf(float x);
+typedef struct {
+  int feat_dim;             /* D_in (40) */
+  int left, right;          /* splice context (3, 3) */
+  int lda_rows, lda_cols;   /* lda: [lda_rows][lda_cols], cols = (l+r+1)*D_in (+1 offset) */
+  const float* lda;
+  const double* cmvn;       /* global stats [2][D_in + 1] */
+  int cmn_window, global_frames;
+  int num_gauss;
+  const float* gconsts;     /* [G] */
+  const float* means_invvars; /* [G][lda_rows] */
+  const float* inv_vars;    /* [G][lda_rows] */
+  int ivec_dim;             /* S */
+  const double* M;          /* [G][lda_rows][S] */
+  const double* sigma_inv;  /* [G][lda_rows][lda_rows] (full) */
+  double prior_offset, max_count;
+  int num_gselect, num_cg_iters;
+  float min_post, posterior_scale;
+} orc_ivector_model;
+/* requests[i]: frame whose i-vector is wanted (ascending); t_ready[i]: MFCC
+   frames available at the request (splice clamps at t_ready - 1); out: [nreq][S]
+   with the prior offset removed from dimension 0.  Returns 0. */
+int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, const int* requests,
+                        const int* t_ready, int nreq, float* out);
 
 /* ---------------- token-passing decoder (Kaldi decoder/lattice-faster-decoder.cc) */
 typedef struct {

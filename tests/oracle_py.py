@@ -37,6 +37,11 @@ def load_lib():
     lib.orc_resample_num_outputs.argtypes = [C.c_int, C.c_int, C.c_long]
     lib.orc_resample.restype = C.c_long
     lib.orc_resample.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_long, C.c_void_p, C.c_long]
+    lib.orc_ivector_extract.restype = C.c_int
+    lib.orc_ivector_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                        C.c_int, C.c_void_p]
+    lib.orc_expf.restype = C.c_float
+    lib.orc_expf.argtypes = [C.c_float]
     return lib
 
 
@@ -93,13 +98,64 @@ def mfcc(wave, conf: dict) -> np.ndarray:
 # ----------------------------------------------------------------------------
 # nnet3 program
 # ----------------------------------------------------------------------------
+class OrcIvectorModel(C.Structure):
+    _fields_ = [("feat_dim", C.c_int), ("left", C.c_int), ("right", C.c_int),
+                ("lda_rows", C.c_int), ("lda_cols", C.c_int), ("lda", C.c_void_p),
+                ("cmvn", C.c_void_p), ("cmn_window", C.c_int), ("global_frames", C.c_int),
+                ("num_gauss", C.c_int), ("gconsts", C.c_void_p), ("means_invvars", C.c_void_p),
+                ("inv_vars", C.c_void_p), ("ivec_dim", C.c_int), ("M", C.c_void_p),
+                ("sigma_inv", C.c_void_p), ("prior_offset", C.c_double),
+                ("max_count", C.c_double), ("num_gselect", C.c_int), ("num_cg_iters", C.c_int),
+                ("min_post", C.c_float), ("posterior_scale", C.c_float)]
+
+
+class OracleIvector:
+    """ivector/ directory -> the C oracle's online i-vector extractor
+    (configuration of the reference, src/model.cc:247-263)."""
+
+    def __init__(self, ivector_dir):
+        lda = kf.read_matrix_file(os.path.join(ivector_dir, "final.mat"))
+        cmvn = kf.read_matrix_file(os.path.join(ivector_dir, "global_cmvn.stats"))
+        ubm = kf.read_diag_gmm(os.path.join(ivector_dir, "final.dubm"))
+        ie = kf.read_ivector_extractor(os.path.join(ivector_dir, "final.ie"))
+        sp = kf.parse_conf(os.path.join(ivector_dir, "splice.conf"))
+        self.keep = dict(
+            lda=np.ascontiguousarray(lda, np.float32), cmvn=np.ascontiguousarray(cmvn, np.float64),
+            gc=np.ascontiguousarray(ubm.gconsts, np.float32),
+            mi=np.ascontiguousarray(ubm.means_invvars, np.float32),
+            iv=np.ascontiguousarray(ubm.inv_vars, np.float32),
+            M=np.ascontiguousarray(np.stack(ie.M), np.float64),
+            SI=np.ascontiguousarray(np.stack(ie.sigma_inv), np.float64))
+        k = self.keep
+        left, right = int(sp.get("left-context", 4)), int(sp.get("right-context", 4))
+        D = cmvn.shape[1] - 1
+        self.dim = ie.M[0].shape[1]
+        self.m = OrcIvectorModel(D, left, right, lda.shape[0], lda.shape[1], k["lda"].ctypes.data,
+                                 k["cmvn"].ctypes.data, 600, 200, ubm.gconsts.size,
+                                 k["gc"].ctypes.data, k["mi"].ctypes.data, k["iv"].ctypes.data,
+                                 self.dim, k["M"].ctypes.data, k["SI"].ctypes.data,
+                                 ie.prior_offset, 100.0, 5, 15, 0.025, 0.1)
+
+    def extract(self, feats, requests):
+        feats = np.ascontiguousarray(feats, np.float32)
+        T = feats.shape[0]
+        req = np.ascontiguousarray(requests, np.int32)
+        tr = np.full(len(req), T, np.int32)
+        out = np.zeros((len(req), self.dim), np.float32)
+        lib().orc_ivector_extract(C.byref(self.m), feats.ctypes.data, T, req.ctypes.data,
+                                  tr.ctypes.data, len(req), out.ctypes.data)
+        return out
+
+
 class OrcNet(C.Structure):
     _fields_ = [("num_nodes", C.c_int), ("kind", C.c_void_p), ("dim", C.c_void_p),
                 ("in_dim", C.c_void_p), ("w_off", C.c_void_p), ("b_off", C.c_void_p),
                 ("s_off", C.c_void_p), ("o_off", C.c_void_p), ("params", C.c_void_p),
                 ("toff_begin", C.c_void_p), ("toff_count", C.c_void_p), ("toffs", C.c_void_p),
                 ("prog_begin", C.c_void_p), ("prog", C.c_void_p), ("progf", C.c_void_p),
-                ("output_node", C.c_int), ("fss", C.c_int), ("acoustic_scale", C.c_float)]
+                ("output_node", C.c_int), ("fss", C.c_int), ("acoustic_scale", C.c_float),
+                ("ivec", C.c_void_p), ("ivec_of_time", C.c_void_p), ("ivec_t0", C.c_int),
+                ("ivec_ntimes", C.c_int), ("ivec_dim", C.c_int)]
 
 
 def bn_scale_offset_f32(fields):
@@ -225,10 +281,16 @@ class OracleNet:
             elif k == "const":
                 progf.append(d[1])
                 code.append((3, 0, 0, len(progf) - 1))
+            elif k == "replace_index" and d[1] == ("node", "ivector"):
+                code.append((4, 0, 0, 0))  # the row's chunk i-vector
+                self.ivector_consumers.add(cur_node[0])
             else:
                 raise ValueError(f"descriptor {k} unsupported by the oracle")
 
+        self.ivector_consumers = set()
+        cur_node = [None]
         for n in prog_nodes:
+            cur_node[0] = n
             if n == "input":
                 kind.append(0); dim.append(g.nodes[n]["dim"]); in_dim.append(0)
                 w_off.append(-1); b_off.append(-1); s_off.append(-1); o_off.append(-1)
@@ -300,11 +362,24 @@ class OracleNet:
                                                "progf")),
                           idx[out_desc[1]], fss, acoustic_scale)
 
-    def forward(self, feats: np.ndarray) -> np.ndarray:
+    def forward(self, feats: np.ndarray, ivecs=None, ivec_of_time=None, ivec_t0=0) -> np.ndarray:
+        """ivecs: [chunks][dim] i-vectors; ivec_of_time[t - ivec_t0]: the chunk
+        whose i-vector the rows at time t use."""
         feats = np.ascontiguousarray(feats, np.float32)
         T = feats.shape[0]
         rows = (T + self.fss - 1) // self.fss
         out = np.zeros((rows, self.out_dim), np.float32)
+        if ivecs is not None:
+            iv = np.ascontiguousarray(ivecs, np.float32)
+            it = np.ascontiguousarray(ivec_of_time, np.int32)
+            self._keep = (iv, it)
+            self.net.ivec, self.net.ivec_of_time = iv.ctypes.data, it.ctypes.data
+            self.net.ivec_t0, self.net.ivec_ntimes, self.net.ivec_dim = ivec_t0, len(it), iv.shape[1]
+        else:
+            if self.ivector_consumers:
+                raise ValueError("this nnet has an i-vector input: pass ivecs / ivec_of_time")
+            self.net.ivec = self.net.ivec_of_time = None
+            self.net.ivec_ntimes = 0
         r = lib().orc_nnet_forward(C.byref(self.net), feats.ctypes.data_as(C.c_void_p),
                                    C.c_int(T), out.ctypes.data_as(C.c_void_p))
         assert r == rows, r
@@ -384,9 +459,12 @@ class OracleGraph:
 
 
 class OracleModel:
-    """All oracle pieces for a model directory (V2 layout)."""
+    """All oracle pieces for a model directory (V2 layout).  fpc: looped
+    chunk size in input frames (defaults to the model's decodable option,
+    20 rounded up to the subsampling factor, as the single-stream
+    Recognizer); it matters only with i-vectors (one i-vector per chunk)."""
 
-    def __init__(self, model_dir: str):
+    def __init__(self, model_dir: str, fpc=None):
         self.dir = model_dir
         self.mfcc_conf = kf.parse_conf(os.path.join(model_dir, "conf", "mfcc.conf"))
         self.model_conf = kf.parse_conf(os.path.join(model_dir, "conf", "model.conf"))
@@ -402,12 +480,60 @@ class OracleModel:
         self.beam_delta = float(mc.get("beam-delta", 0.5))
         self.net = OracleNet(self.nn, self.acoustic_scale, self.fss)
         self.graph = OracleGraph(self.fst, self.tm.tid2pdf)
+        fpc = int(fpc or mc.get("frames-per-chunk", 20))
+        self.fpc = fpc + (-fpc) % self.fss
+        idir = os.path.join(model_dir, "ivector")
+        self.ivector = OracleIvector(idir) if os.path.exists(os.path.join(idir, "final.ie")) else None
+        if self.ivector is not None:
+            self._ivector_schedule()
+
+    def _ivector_schedule(self):
+        """Looped-chunk bookkeeping: right context, and for the rows of the
+        i-vector's consumer node the chunk that first computes them (chunk 0,
+        then a periodic window of fpc times per chunk)."""
+        g, fss, fpc = self.net.graph, self.fss, self.fpc
+        opc = fpc // fss
+        self.right_context = max(nk.needed_times(g, [0], "input"))
+        assert len(self.net.ivector_consumers) == 1
+        node = next(iter(self.net.ivector_consumers))
+        sets = [nk.needed_times(g, [c * fpc + fss * i for i in range(opc)], node) for c in range(3)]
+        new1 = sorted(sets[1] - sets[0])
+        new2 = sorted(sets[2] - sets[1] - sets[0])
+        assert new2 == [t + fpc for t in new1] and new1 == list(range(new1[0], new1[0] + fpc)), \
+            "i-vector consumer is not periodic"
+        self._iv_first0 = min(sets[0])
+        self._iv_new1 = new1[0]
+
+    def ivector_requests(self, T):
+        """Frame whose i-vector each chunk uses: the last input frame of the
+        chunk incl. right context (DecodableNnetLoopedOnline), clamped to the
+        utterance (the engine waits for the splice's 3 right-context frames)."""
+        opc = self.fpc // self.fss
+        nch = -(-(-(-T // self.fss)) // opc) if T > 0 else 0
+        return [min((c + 1) * self.fpc + self.right_context, T) - 1 for c in range(nch)]
+
+    def ivectors(self, feats):
+        return self.ivector.extract(feats, self.ivector_requests(feats.shape[0]))
+
+    def _ivec_of_time(self, T, nch):
+        t0 = self._iv_first0
+        t1 = nch * self.fpc + self._iv_new1 + self.fpc
+        times = np.arange(t0, t1)
+        c = np.where(times < self._iv_new1, 0, 1 + (times - self._iv_new1) // self.fpc)
+        return np.minimum(c, max(nch - 1, 0)).astype(np.int32), t0
 
     def features(self, wave):
         return mfcc(wave, self.mfcc_conf)
 
     def loglikes(self, wave):
-        return self.net.forward(self.features(wave))
+        return self.loglikes_feats(self.features(wave))
+
+    def loglikes_feats(self, feats):
+        if self.ivector is None or feats.shape[0] == 0:
+            return self.net.forward(feats)
+        iv = self.ivectors(feats)
+        ivt, t0 = self._ivec_of_time(feats.shape[0], len(iv))
+        return self.net.forward(feats, iv, ivt, t0)
 
     def decode_llh(self, llh, use_final=True):
         return self.graph.decode(llh, self.beam, self.max_active, self.min_active,

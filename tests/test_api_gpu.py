@@ -104,7 +104,8 @@ def test_batch_recognizer_matches_oracle(vosk_mod, synth_model_noep, test_wave, 
     """test_gpu_batch.py pattern: N streams fed 8000 bytes per iteration,
     Wait(), Result(); final text per stream == oracle 1-best."""
     monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_model_noep)
-    oracle = oracle_py.OracleModel(synth_model_noep)
+    # BatchModel chunking: frames_per_chunk = max(51, right context) (batch_model.cc:84-88)
+    oracle = oracle_py.OracleModel(synth_model_noep, fpc=51)
     vosk_mod.GpuInit()
     model = vosk_mod.BatchModel()
     n = 6

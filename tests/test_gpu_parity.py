@@ -18,6 +18,16 @@ def oracle(synth_model):
     return oracle_py.OracleModel(synth_model)
 
 
+_ORACLES = {}
+
+
+def _oracle_fpc(model, fpc):
+    """Oracle with the engine's chunk size (one i-vector per chunk)."""
+    if (model, fpc) not in _ORACLES:
+        _ORACLES[(model, fpc)] = oracle_py.OracleModel(model, fpc=fpc)
+    return _ORACLES[(model, fpc)]
+
+
 def _engine(model, fpc=0, streams=8, stats=True, llh=True):
     from vosk import engine
     return engine.Engine(model, frames_per_chunk=fpc, max_streams=streams, stats=stats,
@@ -52,9 +62,23 @@ def test_llh_bit_exact(synth_model, oracle, test_wave, fpc):
     s = e.new_stream()
     _feed(e, s, test_wave)
     llh = e.llh(s)
-    ref = oracle.loglikes(test_wave)
+    ref = _oracle_fpc(synth_model, fpc).loglikes(test_wave)
     assert llh.shape == ref.shape, (llh.shape, ref.shape)
     np.testing.assert_array_equal(llh, ref)
+
+
+@pytest.mark.parametrize("fpc,chunk", [(51, 3200), (21, 3200), (51, 480), (21, 100000)])
+def test_ivectors_bit_exact(synth_model, test_wave, fpc, chunk):
+    """Online i-vectors (CMVN -> LDA -> UBM posteriors -> stats -> CG), one
+    per chunk, identical to the oracle whatever the feeding granularity."""
+    o = _oracle_fpc(synth_model, fpc)
+    e = _engine(synth_model, fpc=fpc)
+    s = e.new_stream()
+    _feed(e, s, test_wave, chunk=chunk)
+    got = e.ivectors(s)
+    ref = o.ivectors(o.features(test_wave))
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    np.testing.assert_array_equal(got, ref)
 
 
 # decoder frame construction: LDS table (default), global maps only, and
@@ -117,10 +141,11 @@ def test_end_to_end_single_stream(synth_model, oracle, test_wave):
     assert e.error(s) == 0
 
 
-def test_batched_streams_match_oracle(synth_model, oracle, test_wave, frame_path):
+def test_batched_streams_match_oracle(synth_model, test_wave, frame_path):
     """Eight different streams advanced together in the same batched steps."""
+    oracle = _oracle_fpc(synth_model, 51)
     n = 8
-    e = _engine(synth_model, fpc=51, streams=n, stats=False, llh=False)
+    e = _engine(synth_model, fpc=51, streams=n, stats=False, llh=True)
     waves = [perturbed_stream(test_wave, i, seconds=3.0 + 0.37 * i) for i in range(n)]
     ss = [e.new_stream() for _ in range(n)]
     chunk = 8000
@@ -135,16 +160,21 @@ def test_batched_streams_match_oracle(synth_model, oracle, test_wave, frame_path
         e.accept(ss[k], np.zeros(0, np.float32), finished=True)
     e.advance(ss)
     for k in range(n):
+        feats = oracle.features(waves[k])
+        np.testing.assert_array_equal(e.ivectors(ss[k]), oracle.ivectors(feats),
+                                      err_msg=f"ivectors {k}")
+        np.testing.assert_array_equal(e.llh(ss[k]), oracle.loglikes_feats(feats), err_msg=f"llh {k}")
         r = oracle.recognize(waves[k])
         arcs, _, _ = e.best_path(ss[k], use_final=True)
         np.testing.assert_array_equal(arcs, r["path"], err_msg=f"stream {k}")
 
 
-def test_pipelined_steps_match_oracle(synth_model, oracle, test_wave):
+def test_pipelined_steps_match_oracle(synth_model, test_wave):
     """Two-stream pipeline (bench.py's mode): HBM-preloaded audio, one chunk
     per stream per step, the decoder of step i-1 beside the nnet of step i;
     transcripts and every decoded LLH row identical to the oracle."""
     from vosk import engine
+    oracle = _oracle_fpc(synth_model, 51)
     n = 6
     e = engine.Engine(synth_model, frames_per_chunk=51, max_streams=n, keep_llh=True,
                       pipeline=True)

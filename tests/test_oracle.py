@@ -42,10 +42,19 @@ def test_mfcc_is_chunking_invariant(oracle, test_wave):
     np.testing.assert_array_equal(part, full[100:100 + part.shape[0]])
 
 
+def _fixed_ivector(oracle):
+    """One i-vector for every row (net-level tests: no extraction involved)."""
+    dim = oracle.ivector.m.ivec_dim
+    v = np.random.default_rng(5).normal(0, 1, (1, dim)).astype(np.float32)
+    return dict(ivecs=v, ivec_of_time=np.zeros(1, np.int32), ivec_t0=0)
+
+
 def test_nnet_vs_numpy(oracle, test_wave):
     feats = oracle.features(test_wave[:32000])
-    llh = oracle.net.forward(feats)
-    ref = nk.NnetGraph(oracle.nn).forward({"input": feats.astype(np.float64)})
+    iv = _fixed_ivector(oracle)
+    llh = oracle.net.forward(feats, **iv)
+    ref = nk.NnetGraph(oracle.nn).forward({"input": feats.astype(np.float64),
+                                           "ivector_at": lambda t: iv["ivecs"][0].astype(np.float64)})
     assert llh.shape == ref.shape
     assert np.abs(llh - ref).max() <= 2e-5 * np.abs(ref).max()
 
@@ -53,9 +62,10 @@ def test_nnet_vs_numpy(oracle, test_wave):
 def test_nnet_edge_replication(oracle, test_wave):
     """Output frame t only sees inputs t-L..t+R, replicated at the edges."""
     feats = oracle.features(test_wave[:32000])
-    llh = oracle.net.forward(feats)
+    iv = _fixed_ivector(oracle)
+    llh = oracle.net.forward(feats, **iv)
     # the middle of the utterance is unaffected by truncating far-away frames
-    llh2 = oracle.net.forward(feats[60:])
+    llh2 = oracle.net.forward(feats[60:], **iv)
     np.testing.assert_array_equal(llh2[20:50], llh[40:70])
 
 

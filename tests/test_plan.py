@@ -24,9 +24,10 @@ def test_plan_flops_match_recipe(synth_model):
 def test_plan_fuses_component_chains(synth_model):
     d = ve.plan_describe(synth_model, 51)
     ops = [ln for ln in d.splitlines() if ln.strip().startswith(("GEMM", "GATHER"))]
-    # one GEMM per affine-like component + the delta gather; the xent branch is pruned
-    assert len(ops) == 29
-    assert sum(1 for o in ops if "GATHER" in o) == 1
+    # one GEMM per affine-like component + the delta and input2 (delta + the
+    # chunk's i-vector) gathers; the xent branch is pruned
+    assert len(ops) == 30
+    assert sum(1 for o in ops if "GATHER" in o) == 2
     assert not any("xent" in o for o in ops)
     assert any("-> LLH" in o for o in ops)
     # bias + relu + batchnorm + bypass fused into each TDNN-F affine

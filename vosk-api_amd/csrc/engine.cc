@@ -68,10 +68,14 @@ void ModelData::Load(const std::string& path) {
   mfcc.Apply(ReadConfigFile(mfcc_conf));
   mfcc.allow_downsample = true;
   ReadFinalMdl(mdl, &tm, &nnet);
-  std::string ivec = path + "/ivector/final.ie";
-  if (FileExists(ivec))
-    VAMD_WARN("i-vector extractor present but not supported yet; the nnet 'ivector' input "
-              "must be absent (see DESIGN.md next rows)");
+  if (FileExists(path + "/ivector/final.ie")) {
+    VAMD_LOG("Loading i-vector extractor from " << path << "/ivector/final.ie");
+    ReadIvectorModel(path + "/ivector", &ivec);
+    use_ivector = true;
+    if (ivec.feat_dim != mfcc.num_ceps)
+      VAMD_ERR("i-vector extractor expects " << ivec.feat_dim << "-dim features, MFCC gives "
+                                             << mfcc.num_ceps);
+  }
   if (FileExists(path + "/am/global_cmvn.stats") || FileExists(path + "/conf/pitch.conf"))
     VAMD_ERR("global CMVN / pitch front-ends are not supported yet");
   if (!FileExists(hclg))
@@ -255,6 +259,54 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   d_raw_ = (float*)DevAlloc(sizeof(float) * (size_t)S * raw_ring_);
   d_res_tables_ = (ResampleDev*)DevAlloc(sizeof(ResampleDev) * kMaxResampleTables);
 
+  // ---- i-vector extractor (src/model.cc:247-263; OnlineIvectorFeature)
+  use_iv_ = plan_.ivector_node >= 0;
+  if (use_iv_) {
+    if (!m.use_ivector) VAMD_ERR("the nnet has an i-vector input but the model has no ivector/ extractor");
+    const IvectorModel& iv = m.ivec;
+    const int Si = iv.ivec_dim, QS = Si * (Si + 1) / 2;
+    if (Si != plan_.ivector_dim)
+      VAMD_ERR("i-vector dim " << Si << " != nnet i-vector input dim " << plan_.ivector_dim);
+    if (iv.feat_dim != plan_.input_dim) VAMD_ERR("i-vector feature dim != nnet input dim");
+    if (Si > kIvMaxS || QS > kIvMaxQ || iv.feat_dim > kIvMaxD || iv.lda_dim > kIvMaxD ||
+        (iv.left + iv.right + 1) * iv.feat_dim > kIvMaxK || iv.num_gauss > kIvMaxG ||
+        iv.num_gselect > 8 || iv.num_gselect < 1 || iv.cmn_window >= kIvHist || iv.cmn_window < 1 ||
+        iv.left < 0 || iv.right < 0)
+      VAMD_ERR("i-vector extractor dimensions exceed the kernel limits");
+    // normalized-feature ring: one request spans at most its chunk's frames
+    // plus the splice context
+    if (fpc + plan_.right_context + iv.left + iv.right + 8 > kIvNorm)
+      VAMD_ERR("frames-per-chunk too large for the i-vector feature ring");
+    IvectorDev& d = iv_.m;
+    d.feat_dim = iv.feat_dim; d.left = iv.left; d.right = iv.right;
+    d.lda_dim = iv.lda_dim; d.lda_cols = iv.lda.cols; d.num_gauss = iv.num_gauss;
+    d.ivec_dim = Si; d.cmn_window = iv.cmn_window; d.global_frames = iv.global_frames;
+    d.num_gselect = iv.num_gselect; d.num_cg_iters = iv.num_cg_iters;
+    d.min_post = iv.min_post; d.posterior_scale = iv.posterior_scale;
+    d.log_min_post = iv.log_min_post;
+    d.prior_offset = iv.prior_offset; d.max_count = iv.max_count;
+    d.lda = Upload(iv.lda.data);
+    d.cmvn = Upload(iv.cmvn);
+    d.gconsts = Upload(iv.gconsts);
+    d.means_invvars = Upload(iv.means_invvars);
+    d.inv_vars = Upload(iv.inv_vars);
+    d.sigma_inv_m = Upload(iv.sigma_inv_m);
+    d.U = Upload(iv.U);
+    iv_.state = (IvState*)DevAlloc(sizeof(IvState) * S);
+    HIPCHECK(hipMemset(iv_.state, 0, sizeof(IvState) * S));
+    iv_.quad = (double*)DevAlloc(sizeof(double) * (size_t)S * QS);
+    iv_.hist = (float*)DevAlloc(sizeof(float) * (size_t)S * kIvHist * iv.feat_dim);
+    iv_.norm = (float*)DevAlloc(sizeof(float) * (size_t)S * kIvNorm * iv.feat_dim);
+    iv_.in_base = ring_ptrs[plan_.input_node];
+    iv_.in_mask = ring_ - 1;
+    iv_.slots = S;
+    d_ivec_ = (float*)DevAlloc(sizeof(float) * (size_t)S * jobs_per_slot_ * Si);
+    HIPCHECK(hipMemset(d_ivec_, 0, sizeof(float) * (size_t)S * jobs_per_slot_ * Si));
+    iv_.ivec = d_ivec_;
+  } else if (m.use_ivector) {
+    VAMD_WARN("ivector/ extractor present but the nnet has no i-vector input: not used");
+  }
+
   // ---- nnet ops
   std::vector<float*> vec_ptrs;
   for (auto& v : plan_.vecs) vec_ptrs.push_back(Upload(v));
@@ -300,10 +352,13 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
         a.parts[i] = DevPart{gp.col0, gp.dim, ni, (int)gp.prog.size()};
         for (auto& g : gp.prog) {
           if (ni >= kMaxInstr) VAMD_ERR("descriptor program too long in op " << op.name);
-          a.instr[ni++] = DevInstr{g.op == GInstr::PUSH ? ring_ptrs[g.node] : nullptr, g.op,
-                                   g.op == GInstr::PUSH ? ring_dims[g.node] : 0,
-                                   g.op == GInstr::PUSH ? is_in(g.node) : 0, g.offset, g.src_col,
-                                   g.c};
+          if (g.op == GInstr::PUSH_JOB)  // the step's per-job i-vector rows
+            a.instr[ni++] = DevInstr{d_ivec_, g.op, plan_.ivector_dim, 0, 0, g.src_col, g.c};
+          else
+            a.instr[ni++] = DevInstr{g.op == GInstr::PUSH ? ring_ptrs[g.node] : nullptr, g.op,
+                                     g.op == GInstr::PUSH ? ring_dims[g.node] : 0,
+                                     g.op == GInstr::PUSH ? is_in(g.node) : 0, g.offset,
+                                     g.src_col, g.c};
         }
       }
     }
@@ -410,7 +465,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   stage_bytes_ = Align256(sizeof(float) * (size_t)S * cfg_.max_step_samples) +
                  2 * Align256(sizeof(SampleJob) * S) + Align256(sizeof(ResampleJob) * S) +
                  Align256(sizeof(MfccJob) * S) +
-                 Align256(sizeof(DevJob) * max_jobs_) + Align256(sizeof(DecJob) * S) + 1024;
+                 Align256(sizeof(DevJob) * max_jobs_) + Align256(sizeof(DecJob) * S) +
+                 Align256(sizeof(IvStreamJob) * S) + Align256(sizeof(IvReq) * max_jobs_) + 1024;
   // two halves: a pipelined decoder batch keeps its jobs while the next step stages
   HIPCHECK(hipHostMalloc((void**)&h_stage_, 2 * stage_bytes_, hipHostMallocDefault));
   d_stage_ = (char*)DevAlloc(2 * stage_bytes_);
@@ -477,6 +533,7 @@ void Engine::ResetPipeline(int slot) {
   h.resident_finish = false;
   h.raw_pushed = 0;
   h.res_flushed = false;
+  h.iv_reset = true;
 }
 
 void Engine::ResetDecoder(int slot) {
@@ -572,6 +629,8 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
   st_mfcc_total_ = 0;
   st_jobs_.clear();
   st_dec_.clear();
+  st_iv_jobs_.clear();
+  st_iv_reqs_.clear();
   const int fpc = plan_.fpc, opc = plan_.opc, fss = plan_.fss, R = plan_.right_context;
   int stats_rows = 0;
   bool any = false;
@@ -663,12 +722,23 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
     const int T = h.frames;
     const int need_out = fin ? (T + fss - 1) / fss : 0;
     int first_real = -1, dec_frames = 0, njobs = 0;
+    const int jobs0 = (int)st_jobs_.size(), req0 = (int)st_iv_reqs_.size();
+    // with an i-vector input a chunk also waits for the i-vector splice's right
+    // context of its last input frame (OnlineIvectorFeature::NumFramesReady)
+    const int iv_wait = use_iv_ ? iv_.m.right : 0;
     while (njobs < jobs_per_slot_) {
       const int c = h.next_chunk;
       bool ready;
       if (fin) ready = T > 0 && (c < 0 || c * opc < need_out);
-      else ready = T >= (std::max(c, 0) + 1) * fpc + R;
+      else ready = T >= (std::max(c, 0) + 1) * fpc + R + iv_wait;
       if (!ready) break;
+      if (use_iv_ && c >= 0) {
+        // the chunk's i-vector: at its last input frame incl. right context,
+        // clamped to the utterance (DecodableNnetLoopedOnline); priming
+        // jobs (same step, just before) share chunk 0's
+        const int job = (int)st_jobs_.size();
+        st_iv_reqs_.push_back(IvReq{std::min((c + 1) * fpc + R, T) - 1, c == 0 ? jobs0 : job, job + 1, 0});
+      }
       if (c >= 0) {
         if (first_real < 0) first_real = (int)st_jobs_.size();
         int valid = fin ? std::min(opc, need_out - c * opc) : opc;
@@ -678,6 +748,11 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
       h.next_chunk++;
       njobs++;
       any = true;
+    }
+    if ((int)st_iv_reqs_.size() > req0) {
+      st_iv_jobs_.push_back(IvStreamJob{s, req0, (int)st_iv_reqs_.size() - req0, h.iv_reset ? 1 : 0, T,
+                                        0, 0, 0});
+      h.iv_reset = false;
     }
     h.out_ready += dec_frames;
     if (dec_frames > 0 || h.need_reset) {
@@ -770,6 +845,8 @@ void Engine::RunStep(bool allow_pipeline) {
   size_t o_resj = put(st_res_.data(), sizeof(ResampleJob) * st_res_.size());
   size_t o_mj = put(st_mfcc_.data(), sizeof(MfccJob) * st_mfcc_.size());
   size_t o_dj = put(st_jobs_.data(), sizeof(DevJob) * st_jobs_.size());
+  size_t o_ivj = put(st_iv_jobs_.data(), sizeof(IvStreamJob) * st_iv_jobs_.size());
+  size_t o_ivr = put(st_iv_reqs_.data(), sizeof(IvReq) * st_iv_reqs_.size());
   DecBatch cur;
   cur.jobs = st_dec_;
   cur.o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
@@ -792,6 +869,13 @@ void Engine::RunStep(bool allow_pipeline) {
   LaunchMfcc(mfcc_, (const MfccJob*)(dsg + o_mj), (int)st_mfcc_.size(), st_mfcc_total_,
              d_samples_, sample_ring_, rings_, stream_);
   launches += st_mfcc_total_ > 0;
+  if (!st_iv_jobs_.empty()) {
+    IvArgs ia = iv_;
+    ia.jobs = (const IvStreamJob*)(dsg + o_ivj);
+    ia.reqs = (const IvReq*)(dsg + o_ivr);
+    LaunchIvector(ia, (int)st_iv_jobs_.size(), stream_);
+    launches++;
+  }
   if (tk) HIPCHECK(hipEventRecord(ev_[2], stream_));
   const int l_front = launches;
   if (!st_jobs_.empty()) {
@@ -843,6 +927,17 @@ void Engine::RunStep(bool allow_pipeline) {
   counters_.frames_mfcc += st_mfcc_total_;
   counters_.chunk_jobs += st_jobs_.size();
   if (db) FinishDecodeBatch(*db);
+  if (cfg_.collect_llh && !st_iv_reqs_.empty()) {
+    const int Si = plan_.ivector_dim;
+    std::vector<float> rows((size_t)st_jobs_.size() * Si);
+    HIPCHECK(hipMemcpy(rows.data(), d_ivec_, sizeof(float) * rows.size(), hipMemcpyDeviceToHost));
+    for (const IvStreamJob& j : st_iv_jobs_)
+      for (int q = 0; q < j.nreq; q++) {
+        const IvReq& r = st_iv_reqs_[j.req0 + q];
+        const float* v = rows.data() + (size_t)(r.job_hi - 1) * Si;
+        slots_[j.slot].ivecs.insert(slots_[j.slot].ivecs.end(), v, v + Si);
+      }
+  }
   half_ ^= 1;
   if (pipe) {
     pend_active_ = !cur.jobs.empty();
@@ -971,6 +1066,8 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     st_mfcc_total_ = 0;
     st_jobs_.clear();
     st_dec_.clear();
+    st_iv_jobs_.clear();
+    st_iv_reqs_.clear();
     h.stats.clear();
     const bool rs = first && (reset || h.need_reset);
     st_dec_.push_back(DecJob{slot, 0, n, rs ? 1 : 0, 0, 0, 0, 0});

@@ -38,6 +38,8 @@ struct ModelData {
   SymbolTable words;
   std::vector<char> phone_is_silence;  // indexed by phone id
   bool has_word_boundary = false;
+  bool use_ivector = false;            // ivector/final.ie present (src/model.cc:247)
+  IvectorModel ivec;
   // Loads a V2 (am/, conf/, graph/) or V1 (flat) layout (src/model.cc:106-128).
   void Load(const std::string& dir);
   void LoadBatchLayout(const std::string& dir);  // src/batch_model.cc:23-54
@@ -133,6 +135,9 @@ class Engine {
   // (collect_llh); decoding of externally supplied log-likelihoods.
   void DebugFeatures(int slot, int first_frame, int n, std::vector<float>* out);
   const std::vector<float>& DecodedLlh(int slot) const { return slots_.at(slot).llh; }
+  // Tests (collect_llh): the i-vector of every chunk computed so far [chunks][dim]
+  const std::vector<float>& ChunkIvectors(int slot) const { return slots_.at(slot).ivecs; }
+  int IvectorDim() const { return use_iv_ ? plan_.ivector_dim : 0; }
   void DecodeExternal(int slot, const float* llh, int nframes, bool reset);
   // VOSK_AMD_DEC_PROFILE=1: summed s_memtime clocks per decoder phase
   // [cutoff, seed, expand, compact, eps, commit, -, frames]
@@ -161,6 +166,8 @@ class Engine {
     int table = -1;            // resample table
     long long raw_pushed = 0;  // raw (input-rate) samples pushed to the raw ring
     bool res_flushed = false;  // resampler flushed at end of input
+    bool iv_reset = true;      // i-vector state restarts at the next request
+    std::vector<float> ivecs;  // collect_llh: per-chunk i-vectors
   };
   struct DecBatch {  // one decoder launch's jobs, staged in one staging half
     std::vector<DecJob> jobs;
@@ -228,6 +235,12 @@ class Engine {
   int st_mfcc_total_ = 0;
   std::vector<DevJob> st_jobs_;
   std::vector<DecJob> st_dec_;
+  std::vector<IvStreamJob> st_iv_jobs_;
+  std::vector<IvReq> st_iv_reqs_;
+  // i-vector extraction (nnet with a per-chunk i-vector input)
+  bool use_iv_ = false;
+  IvArgs iv_{};
+  float* d_ivec_ = nullptr;  // [max jobs][ivector dim], row per chunk job of a step
   int max_jobs_ = 0, max_dec_frames_ = 0;
 
   void* DevAlloc(size_t bytes);

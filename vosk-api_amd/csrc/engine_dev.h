@@ -105,6 +105,48 @@ struct DecSlot {
   unsigned long long best_key;  // min over current tokens of (ordered cost << 32 | state)
 };
 
+// ---- online i-vector extraction (kernels.hip ivector_kernel)
+constexpr int kIvMaxS = 100, kIvMaxD = 64, kIvMaxK = 320, kIvMaxG = 512, kIvMaxQ = 20 * 256;
+constexpr int kIvHist = 1024, kIvNorm = 256;
+struct IvectorDev {
+  int feat_dim, left, right, lda_dim, lda_cols, num_gauss, ivec_dim, cmn_window;
+  int global_frames, num_gselect, num_cg_iters, pad;
+  float min_post, posterior_scale, log_min_post, pad2;
+  double prior_offset, max_count;
+  const float* lda;            // [lda_dim][lda_cols]
+  const double* cmvn;          // [2][feat_dim + 1]
+  const float* gconsts;        // [G]
+  const float* means_invvars;  // [G][lda_dim]
+  const float* inv_vars;       // [G][lda_dim]
+  const double* sigma_inv_m;   // [G][lda_dim][S]
+  const double* U;             // [G][S(S+1)/2]
+};
+struct IvState {  // per stream, persistent across steps (reset with the pipeline)
+  double sum[kIvMaxD];  // CMVN window sums
+  double nfr;           // posterior-weighted frame count
+  double lin[kIvMaxS];  // linear term (incl. prior)
+  double cur[kIvMaxS];  // current i-vector (CG warm start)
+  int norm_done, stats_done, pad0, pad1;
+};
+struct IvStreamJob {  // one workgroup: the requests of one stream in this step
+  int slot, req0, nreq, reset, t_ready, pad0, pad1, pad2;
+};
+struct IvReq {  // i-vector at `frame` -> rows [job_lo, job_hi) of the per-job buffer
+  int frame, job_lo, job_hi, pad;
+};
+struct IvArgs {
+  IvectorDev m;
+  IvState* state;     // [slots]
+  double* quad;       // [slots][S(S+1)/2]
+  float* hist;        // [slots][kIvHist][feat_dim] raw features (CMVN window)
+  float* norm;        // [slots][kIvNorm][feat_dim] CMVN-normalized features
+  const float* in_base;  // MFCC input ring [ring][slots][feat_dim]
+  int in_mask, slots;
+  float* ivec;        // [jobs][S] per chunk job, prior offset removed
+  const IvStreamJob* jobs;
+  const IvReq* reqs;
+};
+
 struct DecJob {
   int slot, llh_row0, nframes, reset, stats_row0, pad0, pad1, pad2;
 };

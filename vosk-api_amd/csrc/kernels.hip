@@ -658,7 +658,8 @@ __global__ __launch_bounds__(256) void nnet_gather_kernel(NnetOpArgs a) {
                             clamp)[in.src_col + d];
     else if (in.op == 1) stack[sp - 1] = in.c * stack[sp - 1];
     else if (in.op == 2) { stack[sp - 2] = stack[sp - 2] + stack[sp - 1]; sp--; }
-    else stack[sp++] = in.c;
+    else if (in.op == 3) stack[sp++] = in.c;
+    else stack[sp++] = in.base[(size_t)(row / a.P) * in.ldim + in.src_col + d];  // job's i-vector
   }
   const float v = apply_stages(a, stack[0], col, slot, tau, clamp);
   store_out(a, row, col, slot, tau, v);
@@ -669,6 +670,321 @@ void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s) {
   long long n = (long long)a.M * a.N;
   if (n <= 0) return;
   hipLaunchKernelGGL(nnet_gather_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+}
+
+// ===========================================================================
+// Online i-vector extraction: Kaldi OnlineIvectorFeature semantics (online
+// CMVN -> splice -> LDA -> diagonal-UBM top-N posteriors -> stats -> CG),
+// operation for operation as the sequential restatement in oracle/oracle.c
+// orc_ivector_extract (double stats, fixed summation orders), so the result
+// is bit-identical.  One 256-thread workgroup per stream; the per-stream state
+// (CMVN window sums, linear / quadratic terms, current i-vector) persists in
+// HBM across steps.  Small LDS footprint (~25 KB) so it co-resides with the
+// pipelined decoder.
+constexpr int IV_FB = 4;  // frames per stats sub-batch
+
+__device__ float dev_expf(float x) {  // oracle.c orc_expf
+  if (x < -87.0f) return 0.0f;
+  const float k = rintf(x * 1.44269504f);
+  float r = fmaf(-k, 0.693145752f, x);
+  r = fmaf(-k, 1.42860677e-6f, r);
+  float p = 1.98412698e-4f;
+  p = fmaf(p, r, 1.38888889e-3f);
+  p = fmaf(p, r, 8.33333333e-3f);
+  p = fmaf(p, r, 4.16666667e-2f);
+  p = fmaf(p, r, 1.66666667e-1f);
+  p = fmaf(p, r, 0.5f);
+  p = fmaf(p, r, 1.0f);
+  p = fmaf(p, r, 1.0f);
+  return ldexpf(p, (int)k);
+}
+
+struct IvShared {
+  float xs[2][IV_FB][kIvMaxK];  // spliced frames: CMVN-normalized / raw
+  float xl[2][IV_FB][kIvMaxD];  // their LDA projections
+  float ll[IV_FB][kIvMaxG];     // UBM log-likelihoods
+  int sel[IV_FB][8];
+  float post[IV_FB][8];
+  int nsel[IV_FB];
+  double cg[5][kIvMaxS];        // CG: x (= current i-vector), p, r, Ap, b
+  double sc[4];
+};
+
+__device__ void iv_matvec(const double* Q, int S, const double* v, double* y) {
+  const int i = threadIdx.x;
+  if (i < S) {
+    double acc = 0.0;
+    for (int j = 0; j < S; j++) {
+      const int r = i > j ? i : j, c = i > j ? j : i;
+      acc = acc + Q[(size_t)r * (r + 1) / 2 + c] * v[j];
+    }
+    y[i] = acc;
+  }
+}
+
+__device__ double iv_dot(const double* x, const double* y, int n) {
+  double s = 0.0;
+  for (int i = 0; i < n; i++) s = s + x[i] * y[i];
+  return s;
+}
+
+__global__ __launch_bounds__(256) void ivector_kernel(IvArgs a) {
+  __shared__ IvShared sh;
+  const IvStreamJob J = a.jobs[blockIdx.x];
+  const IvectorDev& m = a.m;
+  const int tid = threadIdx.x, slot = J.slot;
+  const int D = m.feat_dim, DL = m.lda_dim, S = m.ivec_dim, G = m.num_gauss;
+  const int QS = S * (S + 1) / 2, K = (m.left + m.right + 1) * D, W = m.cmn_window;
+  IvState* st = a.state + slot;
+  double* quad = a.quad + (size_t)slot * QS;
+  float* hist = a.hist + (size_t)slot * kIvHist * D;
+  float* norm = a.norm + (size_t)slot * kIvNorm * D;
+  auto raw = [&](int u) { return a.in_base + ((size_t)(u & a.in_mask) * a.slots + slot) * D; };
+  const double po = m.prior_offset, mc = m.max_count;
+
+  // ---- state -> registers / LDS (reset: prior-only statistics)
+  double csum = 0.0, lin = 0.0, nfr = 0.0;
+  double qe[kIvMaxQ / 256];
+  bool qdiag[kIvMaxQ / 256];
+#pragma unroll
+  for (int j = 0; j < kIvMaxQ / 256; j++) {
+    const int e = tid + 256 * j;
+    int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= e) i++;
+    while (i * (i + 1) / 2 > e) i--;
+    qdiag[j] = e == i * (i + 1) / 2 + i;
+    qe[j] = e < QS ? (J.reset ? (qdiag[j] ? 1.0 : 0.0) : quad[e]) : 0.0;
+  }
+  int norm_done = 0, stats_done = 0;
+  if (J.reset) {
+    if (tid < S) lin = tid == 0 ? po : 0.0;
+    if (tid < S) sh.cg[0][tid] = tid == 0 ? po : 0.0;
+  } else {
+    if (tid < D) csum = st->sum[tid];
+    if (tid < S) lin = st->lin[tid];
+    if (tid < S) sh.cg[0][tid] = st->cur[tid];
+    nfr = st->nfr;
+    norm_done = st->norm_done;
+    stats_done = st->stats_done;
+  }
+  __syncthreads();
+
+  for (int q = 0; q < J.nreq; q++) {
+    const IvReq R = a.reqs[J.req0 + q];
+    const int f = R.frame;
+    if (f >= stats_done) {
+      // 1. online CMVN through the splice's right context of frame f
+      const int nend = min(f + m.right, J.t_ready - 1) + 1;
+      if (tid < D) {
+        const double gcount = m.cmvn[D];
+        for (int u = norm_done; u < nend; u++) {
+          const float x = raw(u)[tid];
+          csum = csum + (double)x;
+          hist[(size_t)(u % kIvHist) * D + tid] = x;
+          if (u - W >= 0) csum = csum - (double)hist[(size_t)((u - W) % kIvHist) * D + tid];
+          double cnt = (double)min(u + 1, W), stv = csum;
+          if (cnt < W) {
+            double cgf = W - cnt;
+            if (cgf > m.global_frames) cgf = m.global_frames;
+            const double scl = cgf / gcount;
+            stv = stv + scl * m.cmvn[tid];
+            cnt = cnt + scl * gcount;
+          }
+          const float alpha = (float)(-1.0 / cnt);
+          const float off = (float)((double)alpha * stv);
+          norm[(size_t)(u % kIvNorm) * D + tid] = x + off;
+        }
+      }
+      if (nend > norm_done) norm_done = nend;
+      __syncthreads();
+      // 2. statistics of frames [stats_done, f], IV_FB frames at a time
+      for (int t0 = stats_done; t0 <= f; t0 += IV_FB) {
+        const int nf = min(IV_FB, f + 1 - t0);
+        for (int i = tid; i < nf * K; i += 256) {
+          const int fr = i / K, j = i - fr * K, c = j / D, d = j - c * D;
+          int u = t0 + fr - m.left + c;
+          u = max(u, 0);
+          u = min(u, J.t_ready - 1);
+          sh.xs[0][fr][j] = norm[(size_t)(u % kIvNorm) * D + d];
+          sh.xs[1][fr][j] = raw(u)[d];
+        }
+        __syncthreads();
+        for (int i = tid; i < 2 * nf * DL; i += 256) {
+          const int w = i / (nf * DL), r = i - w * nf * DL, fr = r / DL, row = r - fr * DL;
+          const float* lw = m.lda + (size_t)row * m.lda_cols;
+          const float* x = sh.xs[w][fr];
+          float acc = 0.0f;
+          for (int j = 0; j < K; j++) acc = fmaf(lw[j], x[j], acc);
+          if (m.lda_cols == K + 1) acc = acc + lw[K];
+          sh.xl[w][fr][row] = acc;
+        }
+        __syncthreads();
+        for (int i = tid; i < nf * G; i += 256) {
+          const int fr = i / G, g = i - fr * G;
+          const float* mi = m.means_invvars + (size_t)g * DL;
+          const float* iv = m.inv_vars + (size_t)g * DL;
+          const float* x = sh.xl[0][fr];
+          float d1 = 0.0f, d2 = 0.0f;
+          for (int d = 0; d < DL; d++) d1 = fmaf(mi[d], x[d], d1);
+          for (int d = 0; d < DL; d++) d2 = fmaf(iv[d], x[d] * x[d], d2);
+          sh.ll[fr][g] = (m.gconsts[g] + d1) + (-0.5f * d2);
+        }
+        __syncthreads();
+        // top-N Gaussians of a frame (descending, ties to the lower index): one wave
+        {
+          const int wv = tid >> 6, lane = tid & 63;
+          if (wv < nf) {
+            const float* ll = sh.ll[wv];
+            int chosen[8];
+            int ns = 0;
+            for (int k = 0; k < m.num_gselect && k < G; k++) {
+              float bv = 0.0f;
+              int bi = -1;
+              for (int g = lane; g < G; g += 64) {
+                bool used = false;
+                for (int j = 0; j < ns; j++) used |= chosen[j] == g;
+                if (used) continue;
+                if (bi < 0 || ll[g] > bv) { bv = ll[g]; bi = g; }
+              }
+              for (int o = 32; o > 0; o >>= 1) {
+                const float ov = __shfl_xor(bv, o);
+                const int oi = __shfl_xor(bi, o);
+                if (oi >= 0 && (bi < 0 || ov > bv || (ov == bv && oi < bi))) { bv = ov; bi = oi; }
+              }
+              chosen[ns++] = bi;
+            }
+            if (lane == 0) {
+              while (ns > 1 && ll[chosen[ns - 1]] < ll[chosen[0]] + m.log_min_post) ns--;
+              float e[8], tot = 0.0f;
+              for (int k = 0; k < ns; k++) {
+                e[k] = dev_expf(ll[chosen[k]] - ll[chosen[0]]);
+                tot = tot + e[k];
+              }
+              for (int k = 0; k < ns; k++) {
+                sh.sel[wv][k] = chosen[k];
+                sh.post[wv][k] = (e[k] / tot) * (m.posterior_scale * 1.0f);
+              }
+              sh.nsel[wv] = ns;
+            }
+          }
+        }
+        __syncthreads();
+        // accumulate: each thread owns lin[tid] and the packed quad entries tid + 256 j
+        for (int fr = 0; fr < nf; fr++) {
+          const int ns = sh.nsel[fr];
+          double tw = 0.0;
+          for (int k = 0; k < ns; k++) {
+            const double w = (double)sh.post[fr][k];
+            if (w == 0.0) continue;
+            const int g = sh.sel[fr][k];
+            if (tid < S) {
+              const double* sm = m.sigma_inv_m + (size_t)g * DL * S + tid;
+              const float* xr = sh.xl[1][fr];
+              double acc = 0.0;
+              for (int d = 0; d < DL; d++) acc = fma(sm[(size_t)d * S], (double)xr[d], acc);
+              lin = lin + w * acc;
+            }
+            const double* u = m.U + (size_t)g * QS;
+#pragma unroll
+            for (int j = 0; j < kIvMaxQ / 256; j++) {
+              const int e = tid + 256 * j;
+              if (e < QS) qe[j] = qe[j] + w * u[e];
+            }
+            tw = tw + w;
+          }
+          if (mc > 0.0) {
+            const double oldp = (nfr > mc ? nfr : mc) / mc, newn = nfr + tw;
+            const double newp = (newn > mc ? newn : mc) / mc, ch = newp - oldp;
+            if (ch != 0.0) {
+              if (tid == 0) lin = lin + po * ch;
+#pragma unroll
+              for (int j = 0; j < kIvMaxQ / 256; j++)
+                if (qdiag[j] && tid + 256 * j < QS) qe[j] += ch;
+            }
+          }
+          nfr = nfr + tw;
+        }
+        __syncthreads();
+      }
+      stats_done = f + 1;
+      // 3. conjugate gradient from the previous i-vector (Kaldi LinearCgd)
+      if (nfr > 0.0) {
+#pragma unroll
+        for (int j = 0; j < kIvMaxQ / 256; j++)
+          if (tid + 256 * j < QS) quad[tid + 256 * j] = qe[j];
+        double *X = sh.cg[0], *P = sh.cg[1], *Rr = sh.cg[2], *AP = sh.cg[3], *B = sh.cg[4];
+        if (tid < S) B[tid] = lin;
+        __syncthreads();
+        iv_matvec(quad, S, X, AP);
+        __syncthreads();
+        if (tid < S) {
+          P[tid] = B[tid] - AP[tid];
+          Rr[tid] = -P[tid];
+        }
+        __syncthreads();
+        if (tid == 0) sh.sc[0] = iv_dot(Rr, Rr, S);
+        __syncthreads();
+        double rcur = sh.sc[0], rrec = rcur;
+        for (int k = 0; k < S + 5 && k != m.num_cg_iters; k++) {
+          iv_matvec(quad, S, P, AP);
+          __syncthreads();
+          if (tid == 0) sh.sc[1] = -iv_dot(P, Rr, S) / iv_dot(P, AP, S);
+          __syncthreads();
+          const double alpha = sh.sc[1];
+          if (tid < S) {
+            X[tid] = X[tid] + alpha * P[tid];
+            Rr[tid] = Rr[tid] + alpha * AP[tid];
+          }
+          __syncthreads();
+          if (tid == 0) sh.sc[2] = iv_dot(Rr, Rr, S);
+          __syncthreads();
+          double rnext = sh.sc[2];
+          if (rnext < 1e-4 * rrec || rnext > 1e4 * rrec) {
+            iv_matvec(quad, S, X, AP);
+            __syncthreads();
+            if (tid < S) Rr[tid] = AP[tid] - B[tid];
+            __syncthreads();
+            if (tid == 0) sh.sc[3] = iv_dot(Rr, Rr, S);
+            __syncthreads();
+            rnext = sh.sc[3];
+            rrec = rnext;
+          }
+          if (rnext <= 2.2250738585072014e-308) break;
+          const double beta = rnext / rcur;
+          if (tid < S) P[tid] = beta * P[tid] - Rr[tid];
+          __syncthreads();
+          rcur = rnext;
+        }
+        __syncthreads();
+      }
+    }
+    // i-vector rows of the request's chunk jobs (prior offset removed)
+    for (int i = tid; i < (R.job_hi - R.job_lo) * S; i += 256) {
+      const int r = R.job_lo + i / S, s = i % S;
+      float v = (float)sh.cg[0][s];
+      if (s == 0) v = v - (float)po;
+      a.ivec[(size_t)r * S + s] = v;
+    }
+  }
+  // ---- registers / LDS -> state
+  if (tid < D) st->sum[tid] = csum;
+  if (tid < S) {
+    st->lin[tid] = lin;
+    st->cur[tid] = sh.cg[0][tid];
+  }
+#pragma unroll
+  for (int j = 0; j < kIvMaxQ / 256; j++)
+    if (tid + 256 * j < QS) quad[tid + 256 * j] = qe[j];
+  if (tid == 0) {
+    st->nfr = nfr;
+    st->norm_done = norm_done;
+    st->stats_done = stats_done;
+  }
+}
+
+void LaunchIvector(const IvArgs& a, int njobs, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(ivector_kernel, dim3(njobs), dim3(256), 0, s, a);
 }
 
 // ===========================================================================

@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
+#include <iterator>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -245,6 +247,70 @@ struct KReader {
     } else {
       VAMD_ERR("unsupported matrix type " << t << " (compressed matrices are not supported)");
     }
+    return m;
+  }
+  double F64() {
+    Need(1);
+    if (d[p] == 8) {
+      Need(9);
+      double v;
+      memcpy(&v, d.data() + p + 1, 8);
+      p += 9;
+      return v;
+    }
+    return F32();
+  }
+  // double-precision matrix / vector / packed symmetric matrix (DM/FM, DV/FV, DP/FP)
+  std::vector<double> Mat64(int* rows, int* cols) {
+    std::string t = Token();
+    *rows = I32();
+    *cols = I32();
+    size_t n = (size_t)*rows * *cols;
+    std::vector<double> v(n);
+    if (t == "DM") {
+      Need(n * 8);
+      memcpy(v.data(), d.data() + p, n * 8);
+      p += n * 8;
+    } else if (t == "FM") {
+      Need(n * 4);
+      for (size_t i = 0; i < n; i++) { float x; memcpy(&x, d.data() + p, 4); v[i] = x; p += 4; }
+    } else {
+      VAMD_ERR("unsupported matrix type " << t);
+    }
+    return v;
+  }
+  std::vector<double> Vec64() {
+    std::string t = Token();
+    int n = I32();
+    std::vector<double> v(n);
+    if (t == "DV") {
+      Need((size_t)n * 8);
+      memcpy(v.data(), d.data() + p, (size_t)n * 8);
+      p += (size_t)n * 8;
+    } else if (t == "FV") {
+      Need((size_t)n * 4);
+      for (int i = 0; i < n; i++) { float x; memcpy(&x, d.data() + p, 4); v[i] = x; p += 4; }
+    } else {
+      VAMD_ERR("unsupported vector type " << t);
+    }
+    return v;
+  }
+  std::vector<double> SpMat64(int* dim) {  // returned full [dim][dim]
+    std::string t = Token();
+    int n = I32();
+    *dim = n;
+    std::vector<double> m((size_t)n * n);
+    size_t cnt = (size_t)n * (n + 1) / 2, es = t == "DP" ? 8 : 4;
+    if (t != "DP" && t != "FP") VAMD_ERR("unsupported packed matrix type " << t);
+    Need(cnt * es);
+    for (int i = 0; i < n; i++)
+      for (int j = 0; j <= i; j++) {
+        double x;
+        if (es == 8) memcpy(&x, d.data() + p, 8);
+        else { float f; memcpy(&f, d.data() + p, 4); x = f; }
+        p += es;
+        m[(size_t)i * n + j] = m[(size_t)j * n + i] = x;
+      }
     return m;
   }
   std::string Line() {
@@ -729,6 +795,117 @@ void ReadSymbolTable(const std::string& path, SymbolTable* t) {
     t->id2sym[(int)id] = sym;
     t->sym2id[sym] = (int)id;
   }
+}
+
+// ---------------------------------------------------------------------------
+// i-vector extractor directory (src/model.cc:247-263 file set)
+// ---------------------------------------------------------------------------
+void ReadIvectorModel(const std::string& dir, IvectorModel* m) {
+  auto slurp = [](const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) VAMD_ERR("cannot open " << path);
+    return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  };
+  for (auto& [k, v] : ReadConfigFile(dir + "/splice.conf")) {
+    if (k == "left-context") m->left = std::stoi(v);
+    else if (k == "right-context") m->right = std::stoi(v);
+  }
+  if (FileExists(dir + "/online_cmvn.conf"))
+    for (auto& [k, v] : ReadConfigFile(dir + "/online_cmvn.conf")) {
+      if (k == "cmn-window") m->cmn_window = std::stoi(v);
+      else if (k == "global-frames") m->global_frames = std::stoi(v);
+      else if (k == "norm-vars" || k == "normalize-variance") {
+        if (v == "true") VAMD_ERR("online CMVN with variance normalization is not supported");
+      } else {
+        VAMD_WARN("ignoring online CMVN option --" << k);
+      }
+    }
+  {
+    std::string d = slurp(dir + "/final.mat");
+    KReader r(d);
+    m->lda = r.Mat();
+  }
+  {
+    std::string d = slurp(dir + "/global_cmvn.stats");
+    KReader r(d);
+    int rows, cols;
+    m->cmvn = r.Mat64(&rows, &cols);
+    if (rows != 2) VAMD_ERR("bad global_cmvn.stats");
+    m->feat_dim = cols - 1;
+  }
+  {
+    std::string d = slurp(dir + "/final.dubm");
+    KReader r(d);
+    r.Expect("<DiagGMM>");
+    r.Expect("<GCONSTS>");
+    m->gconsts = r.Vector();
+    r.Expect("<WEIGHTS>");
+    r.Vector();
+    r.Expect("<MEANS_INVVARS>");
+    Matrix mi = r.Mat();
+    r.Expect("<INV_VARS>");
+    Matrix iv = r.Mat();
+    m->num_gauss = mi.rows;
+    m->lda_dim = mi.cols;
+    m->means_invvars = mi.data;
+    m->inv_vars = iv.data;
+  }
+  {
+    std::string d = slurp(dir + "/final.ie");
+    KReader r(d);
+    r.Expect("<IvectorExtractor>");
+    r.Expect("<w>");
+    int a, b;
+    r.Mat64(&a, &b);
+    r.Expect("<w_vec>");
+    r.Vec64();
+    r.Expect("<M>");
+    const int G = r.I32();
+    if (G != m->num_gauss) VAMD_ERR("final.ie / final.dubm Gaussian count mismatch");
+    for (int g = 0; g < G; g++) {
+      int rows, cols;
+      std::vector<double> M = r.Mat64(&rows, &cols);
+      if (rows != m->lda_dim) VAMD_ERR("final.ie feature dim mismatch");
+      m->ivec_dim = cols;
+      m->M.insert(m->M.end(), M.begin(), M.end());
+    }
+    r.Expect("<SigmaInv>");
+    for (int g = 0; g < G; g++) {
+      int n;
+      std::vector<double> S = r.SpMat64(&n);
+      m->sigma_inv.insert(m->sigma_inv.end(), S.begin(), S.end());
+    }
+    r.Expect("<IvectorOffset>");
+    m->prior_offset = r.F64();
+  }
+  const int D = m->lda_dim, S = m->ivec_dim, G = m->num_gauss, QS = S * (S + 1) / 2;
+  if (m->lda.rows != D) VAMD_ERR("final.mat output dim != UBM dim");
+  const int K = (m->left + m->right + 1) * m->feat_dim;
+  if (m->lda.cols != K && m->lda.cols != K + 1) VAMD_ERR("final.mat input dim mismatch");
+  // derived terms, IvectorExtractor::ComputeDerivedVars (order shared with oracle.c)
+  m->sigma_inv_m.assign((size_t)G * D * S, 0.0);
+  m->U.assign((size_t)G * QS, 0.0);
+  for (int g = 0; g < G; g++) {
+    const double* M = m->M.data() + (size_t)g * D * S;
+    const double* SI = m->sigma_inv.data() + (size_t)g * D * D;
+    double* sm = m->sigma_inv_m.data() + (size_t)g * D * S;
+    for (int d = 0; d < D; d++)
+      for (int s2 = 0; s2 < S; s2++) {
+        double a = 0.0;
+        for (int e = 0; e < D; e++) a = a + SI[(size_t)d * D + e] * M[(size_t)e * S + s2];
+        sm[(size_t)d * S + s2] = a;
+      }
+    double* u = m->U.data() + (size_t)g * QS;
+    for (int i = 0; i < S; i++)
+      for (int j = 0; j <= i; j++) {
+        double a = 0.0;
+        for (int d = 0; d < D; d++) a = a + M[(size_t)d * S + i] * sm[(size_t)d * S + j];
+        u[(size_t)i * (i + 1) / 2 + j] = a;
+      }
+  }
+  m->log_min_post = (float)std::log((double)m->min_post);
+  VAMD_LOG("i-vector extractor: dim " << S << ", " << G << " Gaussians, LDA " << m->lda.rows << "x"
+                                      << m->lda.cols << ", prior offset " << m->prior_offset);
 }
 
 }  // namespace vamd

@@ -174,4 +174,25 @@ void ReadSymbolTable(const std::string& path, SymbolTable* t);
 
 bool FileExists(const std::string& path);
 
+// Online i-vector extractor (ivector/ of a model directory, src/model.cc:247-263),
+// with the reference's settings: max-count 100 (model.cc:257), Kaldi defaults
+// num-gselect 5, min-post 0.025, posterior-scale 0.1, 15 CG iterations,
+// online CMVN window 600 / 200 global frames.
+struct IvectorModel {
+  int feat_dim = 0, left = 3, right = 3;
+  Matrix lda;                              // [lda_dim][(l+r+1)*feat_dim (+1)]
+  std::vector<double> cmvn;                // global stats [2][feat_dim + 1]
+  int cmn_window = 600, global_frames = 200;
+  int num_gauss = 0, lda_dim = 0;
+  std::vector<float> gconsts, means_invvars, inv_vars;  // [G], [G][lda_dim] x2
+  int ivec_dim = 0;
+  std::vector<double> M, sigma_inv;        // [G][lda_dim][S], [G][lda_dim][lda_dim]
+  double prior_offset = 0.0, max_count = 100.0;
+  int num_gselect = 5, num_cg_iters = 15;
+  float min_post = 0.025f, posterior_scale = 0.1f, log_min_post = 0.f;
+  std::vector<double> sigma_inv_m;         // derived [G][lda_dim][S]
+  std::vector<double> U;                   // derived [G][S(S+1)/2]
+};
+void ReadIvectorModel(const std::string& dir, IvectorModel* m);
+
 }  // namespace vamd

@@ -172,9 +172,21 @@ struct Builder {
         prog->push_back(in);
         break;
       }
+      case Desc::REPLACE_INDEX: {
+        // ReplaceIndex(ivector, t, 0): the chunk's i-vector (Kaldi's looped
+        // decodable supplies one i-vector row per chunk)
+        const Desc& in = d.args[0];
+        if (in.kind != Desc::NODE || !nn.HasNode(in.node) ||
+            nn.Node(in.node).kind != NnetNode::INPUT || in.node == "input" || d.t != 0)
+          VAMD_ERR("ReplaceIndex is supported only as ReplaceIndex(<ivector input>, t, 0)");
+        stored.insert(in.node);
+        TmpInstr instr{GInstr::PUSH_JOB, NRef()};
+        instr.ref.node = in.node;
+        prog->push_back(instr);
+        break;
+      }
       default:
-        VAMD_ERR("descriptor kind " << (int)d.kind << " unsupported in a gather (i-vector "
-                                                    "ReplaceIndex/Round: next rows)");
+        VAMD_ERR("descriptor kind " << (int)d.kind << " unsupported in a gather (Round: next rows)");
     }
   }
 
@@ -396,7 +408,9 @@ struct Builder {
       StoredNode s;
       s.name = name;
       s.dim = nn.HasNode(name) ? nn.OutputDimOf(name) : -1;
-      s.is_input = nn.HasNode(name) && nn.Node(name).kind == NnetNode::INPUT;
+      const bool in = nn.HasNode(name) && nn.Node(name).kind == NnetNode::INPUT;
+      s.is_input = in && name == "input";
+      s.is_ivector = in && name != "input";
       if (s.dim < 0) {  // temporary gather node
         for (auto& o : ops) if (o.name == name) s.dim = o.N;
       }
@@ -404,6 +418,11 @@ struct Builder {
       int i = (int)plan.nodes.size() - 1;
       sidx[name] = i;
       if (s.is_input) { plan.input_node = i; plan.input_dim = s.dim; }
+      if (s.is_ivector) {
+        if (plan.ivector_node >= 0) VAMD_ERR("more than one per-chunk nnet input");
+        plan.ivector_node = i;
+        plan.ivector_dim = s.dim;
+      }
       return i;
     };
     get_stored("input");
@@ -451,6 +470,8 @@ struct Builder {
             g.offset = in.ref.offset;
             g.src_col = in.ref.col;
             dep(g.node);
+          } else if (in.op == GInstr::PUSH_JOB) {
+            g.node = sidx.at(in.ref.node);  // no time dependency, no producer
           }
           gp.prog.push_back(g);
         }

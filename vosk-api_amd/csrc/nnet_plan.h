@@ -28,7 +28,8 @@ namespace vamd {
 struct StoredNode {
   std::string name;
   int dim = 0;
-  bool is_input = false;
+  bool is_input = false;    // the feature input (time ring written by the MFCC kernel)
+  bool is_ivector = false;  // a per-chunk input (no time ring: one row per chunk job)
 };
 
 struct ASegment {  // A columns [col0, col0+dim) <- node(tau + offset)[src_col ...]
@@ -45,7 +46,8 @@ struct EpiStage {
 };
 
 struct GInstr {  // postfix program step for GATHER ops
-  enum Op { PUSH = 0, SCALE = 1, ADD = 2, CONST = 3 };
+  // PUSH_JOB: the chunk job's i-vector row (ReplaceIndex(ivector, t, 0))
+  enum Op { PUSH = 0, SCALE = 1, ADD = 2, CONST = 3, PUSH_JOB = 4 };
   int op, node = -1, offset = 0, src_col = 0;
   float c = 0.f;
 };
@@ -84,6 +86,7 @@ struct NnetPlan {
   int priming_chunks = 0;
   int max_age = 0;  // max (latest computed - oldest read) time distance inside a chunk
   int input_node = -1;
+  int ivector_node = -1, ivector_dim = 0;  // per-chunk i-vector input, if the nnet has one
   std::vector<StoredNode> nodes;
   std::vector<Op> ops;
   std::vector<Matrix> mats;

@@ -386,6 +386,21 @@ long long vamd_stream_llh(VamdEngine* e, int s, float* out, long long cap) {
   API_CATCH(-1)
 }
 
+long long vamd_stream_ivectors(VamdEngine* e, int s, float* out, long long cap) {
+  API_TRY
+  const std::vector<float>& v = e->eng->ChunkIvectors(s);
+  long long n = std::min<long long>(cap, (long long)v.size());
+  if (out && n > 0) memcpy(out, v.data(), sizeof(float) * n);
+  return (long long)v.size();
+  API_CATCH(-1)
+}
+
+int vamd_engine_ivector_dim(VamdEngine* e) {
+  API_TRY
+  return e->eng->IvectorDim();
+  API_CATCH(-1)
+}
+
 int vamd_stream_stats(VamdEngine* e, int s, float* out, int cap) {
   API_TRY
   const std::vector<FrameStat>& st = e->eng->LastStats(s);

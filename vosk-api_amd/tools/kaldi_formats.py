@@ -83,6 +83,31 @@ class KaldiWriter:
         self.i32(a.shape[1])
         self.buf += a.tobytes()
 
+    def f64(self, v: float):
+        self.buf += b"\x08" + struct.pack("<d", float(v))
+
+    def dvector(self, v):
+        a = np.asarray(v, dtype="<f8").ravel()
+        self.token("DV")
+        self.i32(a.size)
+        self.buf += a.tobytes()
+
+    def dmatrix(self, m):
+        a = np.ascontiguousarray(np.asarray(m, dtype="<f8"))
+        assert a.ndim == 2
+        self.token("DM")
+        self.i32(a.shape[0])
+        self.i32(a.shape[1])
+        self.buf += a.tobytes()
+
+    def dspmatrix(self, m):
+        """SpMatrix<double>: lower triangle, row-major packed."""
+        a = np.asarray(m, dtype=np.float64)
+        n = a.shape[0]
+        self.token("DP")
+        self.i32(n)
+        self.buf += np.concatenate([a[i, :i + 1] for i in range(n)]).astype("<f8").tobytes()
+
     def bytes(self) -> bytes:
         return bytes(self.buf)
 
@@ -191,6 +216,40 @@ class KaldiReader:
         else:
             raise ValueError(f"unsupported matrix type {t}")
         return a
+
+    def f64(self) -> float:
+        return self.f32()
+
+    def dvector64(self) -> np.ndarray:
+        t = self.token()
+        n = self.i32()
+        dt = {"FV": "<f4", "DV": "<f8"}[t]
+        a = np.frombuffer(self.d, dt, n, self.p).astype(np.float64)
+        self.p += np.dtype(dt).itemsize * n
+        return a
+
+    def matrix64(self) -> np.ndarray:
+        t = self.token()
+        r = self.i32()
+        c = self.i32()
+        dt = {"FM": "<f4", "DM": "<f8"}[t]
+        a = np.frombuffer(self.d, dt, r * c, self.p).reshape(r, c).astype(np.float64)
+        self.p += np.dtype(dt).itemsize * r * c
+        return a
+
+    def spmatrix64(self) -> np.ndarray:
+        t = self.token()
+        n = self.i32()
+        dt = {"FP": "<f4", "DP": "<f8"}[t]
+        cnt = n * (n + 1) // 2
+        v = np.frombuffer(self.d, dt, cnt, self.p).astype(np.float64)
+        self.p += np.dtype(dt).itemsize * cnt
+        m = np.zeros((n, n))
+        k = 0
+        for i in range(n):
+            m[i, :i + 1] = v[k:k + i + 1]
+            k += i + 1
+        return m + np.tril(m, -1).T
 
     def line(self) -> str:
         e = self.d.index(b"\n", self.p)
@@ -689,3 +748,96 @@ def parse_conf(path: str) -> dict:
             k, v = ln[2:], "true"
         out[k.strip()] = v.strip()
     return out
+
+
+# ----------------------------------------------------------------------------
+# i-vector extractor files (Kaldi gmm/diag-gmm.cc, ivector/ivector-extractor.cc)
+# ----------------------------------------------------------------------------
+@dataclass
+class DiagGmm:
+    gconsts: np.ndarray        # [G]
+    weights: np.ndarray        # [G]
+    means_invvars: np.ndarray  # [G, D]
+    inv_vars: np.ndarray       # [G, D]
+
+
+def diag_gmm_from_params(weights, means, variances) -> DiagGmm:
+    inv = 1.0 / variances
+    D = means.shape[1]
+    gc = (np.log(weights) - 0.5 * (D * np.log(2 * np.pi) + np.log(variances).sum(1) +
+                                   (means * means * inv).sum(1)))
+    return DiagGmm(gc.astype(np.float32), weights.astype(np.float32),
+                   (means * inv).astype(np.float32), inv.astype(np.float32))
+
+
+def write_diag_gmm(path: str, g: DiagGmm):
+    w = KaldiWriter()
+    w.token("<DiagGMM>")
+    w.token("<GCONSTS>"); w.fvector(g.gconsts)
+    w.token("<WEIGHTS>"); w.fvector(g.weights)
+    w.token("<MEANS_INVVARS>"); w.fmatrix(g.means_invvars)
+    w.token("<INV_VARS>"); w.fmatrix(g.inv_vars)
+    w.token("</DiagGMM>")
+    open(path, "wb").write(w.bytes())
+
+
+def read_diag_gmm(path: str) -> DiagGmm:
+    r = KaldiReader(open(path, "rb").read())
+    r.expect("<DiagGMM>")
+    r.expect("<GCONSTS>"); gc = r.vector()
+    r.expect("<WEIGHTS>"); wt = r.vector()
+    r.expect("<MEANS_INVVARS>"); mi = r.matrix()
+    r.expect("<INV_VARS>"); iv = r.matrix()
+    r.expect("</DiagGMM>")
+    return DiagGmm(gc, wt, mi, iv)
+
+
+@dataclass
+class IvectorExtractor:
+    w: np.ndarray          # [G, S] weight projection (unused online)
+    w_vec: np.ndarray      # [G]
+    M: list                # G x [D, S]
+    sigma_inv: list        # G x [D, D] (full, symmetric)
+    prior_offset: float
+
+
+def write_ivector_extractor(path: str, x: IvectorExtractor):
+    w = KaldiWriter()
+    w.token("<IvectorExtractor>")
+    w.token("<w>"); w.dmatrix(x.w)
+    w.token("<w_vec>"); w.dvector(x.w_vec)
+    w.token("<M>"); w.i32(len(x.M))
+    for m in x.M:
+        w.dmatrix(m)
+    w.token("<SigmaInv>")
+    for s in x.sigma_inv:
+        w.dspmatrix(s)
+    w.token("<IvectorOffset>"); w.f64(x.prior_offset)
+    w.token("</IvectorExtractor>")
+    open(path, "wb").write(w.bytes())
+
+
+def read_ivector_extractor(path: str) -> IvectorExtractor:
+    r = KaldiReader(open(path, "rb").read())
+    r.expect("<IvectorExtractor>")
+    r.expect("<w>"); wm = r.matrix64()
+    r.expect("<w_vec>"); wv = r.dvector64()
+    r.expect("<M>")
+    n = r.i32()
+    M = [r.matrix64() for _ in range(n)]
+    r.expect("<SigmaInv>")
+    S = [r.spmatrix64() for _ in range(n)]
+    r.expect("<IvectorOffset>")
+    off = r.f64()
+    r.expect("</IvectorExtractor>")
+    return IvectorExtractor(wm, wv, M, S, off)
+
+
+def write_matrix_file(path: str, m, double=False):
+    w = KaldiWriter()
+    (w.dmatrix if double else w.fmatrix)(m)
+    open(path, "wb").write(w.bytes())
+
+
+def read_matrix_file(path: str) -> np.ndarray:
+    return KaldiReader(open(path, "rb").read()).matrix64()

@@ -231,10 +231,11 @@ def dropout(dim):
         ("<DropoutProportion>", 0.0), ("<Continuous>", True)])
 
 
-def build_nnet(rng, num_pdfs, mfcc_opts):
+def build_nnet(rng, num_pdfs, mfcc_opts, ivector_dim=0):
     comps = {}
     order = []
-    lines = ["input-node name=input dim=40"]
+    lines = ([f"input-node name=ivector dim={ivector_dim}"] if ivector_dim else []) + \
+        ["input-node name=input dim=40"]
 
     def add(name, comp, inp):
         comps[name] = comp
@@ -253,7 +254,12 @@ def build_nnet(rng, num_pdfs, mfcc_opts):
     add("delta", ("NoOpComponent", [("<Dim>", 120), ("<BackpropScale>", 1.0)]),
         f"Append(Offset({sa}, 0), Sum(Offset(Scale(-1.0, {sa}), -1), Offset({sa}, 1)), "
         f"Sum(Sum(Offset({sa}, -2), Offset({sa}, 2)), Offset(Scale(-2.0, {sa}), 0)))")
-    add("tdnn1.affine", nat_affine(rng, 120, 512), "delta")
+    tin = "delta"
+    if ivector_dim:  # run_tdnn.sh:106 no-op input2 = Append(delta, ReplaceIndex(ivector, t, 0))
+        add("input2", ("NoOpComponent", [("<Dim>", 120 + ivector_dim), ("<BackpropScale>", 1.0)]),
+            "Append(delta, ReplaceIndex(ivector, t, 0))")
+        tin = "input2"
+    add("tdnn1.affine", nat_affine(rng, 120 + ivector_dim, 512), tin)
     add("tdnn1.relu", relu(512), "tdnn1.affine")
     add("tdnn1.batchnorm", batchnorm(512), "tdnn1.relu")
     add("tdnn1.dropout", dropout(512), "tdnn1.batchnorm")
@@ -294,7 +300,53 @@ def build_nnet(rng, num_pdfs, mfcc_opts):
     return kf.Nnet3(lines, comps, order, 0, 0, np.zeros(0, np.float32))
 
 
-def calibrate(nn, feats, llh_std):
+def _inputs(feats, ivec):
+    d = {"input": feats}
+    if ivec is not None:
+        d["ivector_at"] = lambda t: ivec
+    return d
+
+
+def build_ivector_extractor(rng, out_dir, feats, ivector_dim=40, num_gauss=512,
+                            prior_offset=100.0):
+    """ivector/ in the recipe's layout (run_ivector_common.sh: PCA over
+    +-3 spliced features, 512-Gaussian diagonal UBM, 40-dim extractor), with
+    seeded random parameters fitted loosely to test.wav."""
+    d = os.path.join(out_dir, "ivector")
+    os.makedirs(d, exist_ok=True)
+    T, D = feats.shape
+    gstats = np.zeros((2, D + 1))
+    gstats[0, :D] = feats.sum(0)
+    gstats[0, D] = T
+    gstats[1, :D] = (feats * feats).sum(0)
+    kf.write_matrix_file(os.path.join(d, "global_cmvn.stats"), gstats, double=True)
+    norm = feats - feats.mean(0)
+    spl = np.concatenate([norm[np.clip(np.arange(T) + o, 0, T - 1)] for o in range(-3, 4)], 1)
+    mu = spl.mean(0)
+    u, sv, vt = np.linalg.svd(spl - mu, full_matrices=False)
+    W = vt[:D] / (sv[:D, None] / math.sqrt(T))  # unit-variance projections
+    lda = np.concatenate([W, -(W @ mu)[:, None]], 1)
+    kf.write_matrix_file(os.path.join(d, "final.mat"), lda.astype(np.float32))
+    x = spl @ W.T - W @ mu
+    means = x[rng.choice(T, num_gauss)] + 0.3 * rng.standard_normal((num_gauss, D))
+    var = np.full((num_gauss, D), 0.6)
+    kf.write_diag_gmm(os.path.join(d, "final.dubm"),
+                      kf.diag_gmm_from_params(np.full(num_gauss, 1.0 / num_gauss), means, var))
+    M = []
+    for g in range(num_gauss):
+        m = 0.15 * rng.standard_normal((D, ivector_dim))
+        m[:, 0] = means[g] / prior_offset
+        M.append(m)
+    ie = kf.IvectorExtractor(np.zeros((num_gauss, ivector_dim)), np.zeros(num_gauss), M,
+                             [np.diag(1.0 / var[g]) for g in range(num_gauss)], prior_offset)
+    kf.write_ivector_extractor(os.path.join(d, "final.ie"), ie)
+    with open(os.path.join(d, "splice.conf"), "w") as f:
+        f.write("--left-context=3\n--right-context=3\n")
+    open(os.path.join(d, "online_cmvn.conf"), "w").close()
+    return d
+
+
+def calibrate(nn, feats, llh_std, ivec=None):
     """Set every BatchNorm's statistics (in config order) from the activations
     of its input on test.wav, then scale the output layer so the
     log-likelihoods have roughly the requested spread."""
@@ -306,14 +358,14 @@ def calibrate(nn, feats, llh_std):
         g = nk.NnetGraph(nn)
         src = g.nodes[name]["input"]
         assert src[0] == "node"
-        vals = g.forward({"input": feats}, out_name=src[1], t_out=range(0, T))
+        vals = g.forward(_inputs(feats, ivec), out_name=src[1], t_out=range(0, T))
         fd = dict(fields)
         fd["<StatsMean>"] = vals.mean(0).astype(np.float32)
         fd["<StatsVar>"] = vals.var(0).astype(np.float32)
         fd["<TestMode>"] = True
         nn.components[name] = (ctype, [(k, fd[k]) for k, _ in fields])
     g = nk.NnetGraph(nn)
-    out = g.forward({"input": feats})
+    out = g.forward(_inputs(feats, ivec))
     ctype, fields = nn.components["output.affine"]
     fd = dict(fields)
     s = llh_std / max(out.std(), 1e-6)
@@ -322,7 +374,8 @@ def calibrate(nn, feats, llh_std):
     nn.components["output.affine"] = (ctype, [(k, fd[k]) for k, _ in fields])
 
 
-def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_std=3.0):
+def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_std=3.0,
+               ivector_dim=40):
     rng = np.random.default_rng(seed)
     os.makedirs(os.path.join(out_dir, "am"), exist_ok=True)
     os.makedirs(os.path.join(out_dir, "conf"), exist_ok=True)
@@ -335,9 +388,14 @@ def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_st
 
     tm, tids = build_transition_model(rng, num_phones, num_pdfs)
     fst, words = build_graph(rng, tids, num_phones, vocab)
-    nn = build_nnet(rng, num_pdfs, mo)
+    nn = build_nnet(rng, num_pdfs, mo, ivector_dim)
     feats = nk.mfcc(load_test_wav(), mo)
-    calibrate(nn, feats, llh_std)
+    ivec = None
+    if ivector_dim:
+        idir = build_ivector_extractor(rng, out_dir, feats, ivector_dim)
+        im = nk.IvectorModel(idir)
+        ivec = im.extract(feats, [feats.shape[0] - 1])[-1]
+    calibrate(nn, feats, llh_std, ivec)
     kf.write_final_mdl(os.path.join(out_dir, "am", "final.mdl"), tm, nn)
     kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), fst)
     with open(os.path.join(out_dir, "graph", "words.txt"), "w") as f:
@@ -351,7 +409,8 @@ def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_st
             f.write(f"{p} internal\n")
     with open(os.path.join(out_dir, "README"), "w") as f:
         f.write(f"synthetic vosk-api_amd model seed={seed} vocab={vocab} pdfs={num_pdfs} "
-                f"phones={num_phones} states={fst.num_states} arcs={fst.num_arcs}\n")
+                f"phones={num_phones} ivector_dim={ivector_dim} states={fst.num_states} "
+                f"arcs={fst.num_arcs}\n")
     return out_dir
 
 

@@ -13,6 +13,7 @@ ReplaceIndex).  Reference call sites: ``src/model.cc:218-221`` (mfcc.conf),
 from __future__ import annotations
 
 import math
+import os
 import re
 
 import numpy as np
@@ -283,7 +284,7 @@ class NnetGraph:
 
     def forward(self, inputs: dict, out_name="output", t_out=None):
         """inputs: name -> [T, dim] array; returns [len(t_out), dim]."""
-        T = next(iter(inputs.values())).shape[0] if "input" not in inputs else inputs["input"].shape[0]
+        T = inputs["input"].shape[0]
         cache = {}
         comps = self.nn.components
 
@@ -327,6 +328,8 @@ class NnetGraph:
             if k == "append":
                 return np.concatenate([desc_val(e, t) for e in d[1]])
             if k == "replace_index":
+                if d[1] == ("node", "ivector") and "ivector_at" in inputs:
+                    return inputs["ivector_at"](t)  # the i-vector of the chunk computing row t
                 return desc_val(d[1], d[3] if d[2] == "t" else t)
             if k == "round":
                 return desc_val(d[1], (t // d[2]) * d[2])
@@ -373,3 +376,172 @@ def apply_component(ctype, f, x):
         reps = len(x) // len(s)
         return x * np.tile(s, reps) + np.tile(o, reps)
     raise ValueError(f"unsupported component {ctype}")
+
+
+# ----------------------------------------------------------------------------
+# Online i-vector extraction (Kaldi online2/online-ivector-feature.cc,
+# ivector/ivector-extractor.cc OnlineIvectorEstimationStats, matrix/
+# optimization.cc LinearCgd) -- float64 restatement used to calibrate the
+# synthetic model and to cross-check the C oracle.  Configuration as the
+# reference sets it (src/model.cc:247-263): splice +-3, LDA, online CMVN with
+# global stats (window 600, global frames 200), 5-best UBM posteriors
+# (min-post 0.025, scale 0.1), max-count 100, 15 CG iterations.
+# ----------------------------------------------------------------------------
+class IvectorModel:
+    def __init__(self, ivector_dir):
+        import kaldi_formats as kf
+        self.lda = kf.read_matrix_file(os.path.join(ivector_dir, "final.mat"))
+        self.cmvn = kf.read_matrix_file(os.path.join(ivector_dir, "global_cmvn.stats"))
+        self.ubm = kf.read_diag_gmm(os.path.join(ivector_dir, "final.dubm"))
+        self.ie = kf.read_ivector_extractor(os.path.join(ivector_dir, "final.ie"))
+        self.left = self.right = 3
+        self.num_gselect, self.min_post, self.post_scale = 5, 0.025, 0.1
+        self.max_count, self.num_cg_iters = 100.0, 15
+        self.cmn_window, self.global_frames = 600, 200
+        self.S = self.ie.M[0].shape[1]
+        self.SigmaInvM = [si @ m for si, m in zip(self.ie.sigma_inv, self.ie.M)]
+        self.U = [m.T @ sm for m, sm in zip(self.ie.M, self.SigmaInvM)]
+
+    def cmvn_feats(self, feats):
+        T, D = feats.shape
+        out = np.zeros_like(feats, dtype=np.float64)
+        s = np.zeros(D)
+        n = 0.0
+        g = self.cmvn
+        for t in range(T):
+            s += feats[t]
+            n += 1
+            if t - self.cmn_window >= 0:
+                s -= feats[t - self.cmn_window]
+                n -= 1
+            st, cnt = s.copy(), n
+            if cnt < self.cmn_window:
+                cg = min(self.cmn_window - cnt, self.global_frames)
+                st = st + cg / g[0, D] * g[0, :D]
+                cnt = cnt + cg / g[0, D] * g[0, D]
+            out[t] = feats[t] - st / cnt
+        return out
+
+    def lda_frame(self, src, t, T_ready):
+        idx = [min(max(t + o, 0), T_ready - 1) for o in range(-self.left, self.right + 1)]
+        x = np.concatenate([src[i] for i in idx])
+        D = x.size
+        if self.lda.shape[1] == D + 1:
+            return self.lda[:, :D] @ x + self.lda[:, D]
+        return self.lda @ x
+
+    def extract(self, feats, requests, finished=True):
+        """i-vectors (prior offset removed) at each requested frame, in
+        order, processing frames as Kaldi's OnlineIvectorFeature::GetFrame."""
+        feats = np.asarray(feats, np.float64)
+        T = feats.shape[0]
+        norm = self.cmvn_feats(feats)
+        S = self.S
+        lin = np.zeros(S)
+        lin[0] = self.ie.prior_offset
+        quad = np.eye(S)
+        nfr = 0.0
+        cur = np.zeros(S)
+        cur[0] = self.ie.prior_offset
+        done = 0
+        ubm = self.ubm
+        out = []
+        for f in requests:
+            if f >= done:
+                for t in range(done, f + 1):
+                    xn = self.lda_frame(norm, t, T)
+                    ll = ubm.gconsts + ubm.means_invvars @ xn - 0.5 * (ubm.inv_vars @ (xn * xn))
+                    order = sorted(range(len(ll)), key=lambda g: (-ll[g], g))[:self.num_gselect]
+                    while len(order) > 1 and ll[order[-1]] < ll[order[0]] + np.log(self.min_post):
+                        order.pop()
+                    e = np.exp(ll[order] - ll[order[0]])
+                    post = e / e.sum() * self.post_scale
+                    xr = self.lda_frame(feats, t, T)
+                    for g, w in zip(order, post):
+                        lin += w * (self.SigmaInvM[g].T @ xr)
+                        quad += w * self.U[g]
+                    tw = post.sum()
+                    old = max(nfr, self.max_count) / self.max_count
+                    new = max(nfr + tw, self.max_count) / self.max_count
+                    if new != old:
+                        lin[0] += self.ie.prior_offset * (new - old)
+                        quad += np.eye(S) * (new - old)
+                    nfr += tw
+                done = f + 1
+                if nfr > 0:
+                    cur = linear_cgd(quad, lin, cur, self.num_cg_iters)
+            v = cur.copy()
+            v[0] -= self.ie.prior_offset
+            out.append(v)
+        return np.array(out)
+
+
+def linear_cgd(A, b, x, max_iters):
+    x = x.copy()
+    p = b - A @ x
+    r = -p
+    rcur = r @ r
+    rrec = rcur
+    for k in range(min(max_iters, len(b) + 5)):
+        Ap = A @ p
+        alpha = -(p @ r) / (p @ Ap)
+        x += alpha * p
+        r += alpha * Ap
+        rnext = r @ r
+        if rnext < 1e-4 * rrec or rnext > 1e4 * rrec:
+            r = A @ x - b
+            rnext = r @ r
+            rrec = rnext
+        if rnext <= np.finfo(np.float64).tiny:
+            break
+        p = (rnext / rcur) * p - r
+        rcur = rnext
+    return x
+
+
+def needed_times(graph, out_times, node):
+    """Times at which `node` is evaluated to compute the output at out_times
+    (dependency cone through the descriptors and TDNN time offsets)."""
+    need = {}
+
+    def visit_desc(d, t, acc):
+        k = d[0]
+        if k == "node":
+            acc.add((d[1], t))
+        elif k == "offset":
+            visit_desc(d[1], t + d[2], acc)
+        elif k == "scale":
+            visit_desc(d[2], t, acc)
+        elif k in ("sum", "append"):
+            for e in d[1]:
+                visit_desc(e, t, acc)
+        elif k == "replace_index":
+            visit_desc(d[1], d[3] if d[2] == "t" else t, acc)
+        elif k == "ifdefined":
+            visit_desc(d[1], t, acc)
+        elif k == "round":
+            visit_desc(d[1], (t // d[2]) * d[2], acc)
+
+    todo = [("output", t) for t in out_times]
+    seen = set(todo)
+    while todo:
+        name, t = todo.pop()
+        need.setdefault(name, set()).add(t)
+        nd = graph.nodes[name]
+        acc = set()
+        if nd["kind"] == "dimrange":
+            acc.add((nd["src"], t))
+        elif nd["kind"] in ("component", "output"):
+            offs = [0]
+            if nd["kind"] == "component":
+                ctype, f = graph.nn.components[nd["component"]]
+                f = dict(f) if isinstance(f, list) else f
+                if ctype == "TdnnComponent":
+                    offs = list(f["<TimeOffsets>"])
+            for o in offs:
+                visit_desc(nd["input"], t + o, acc)
+        for a in acc:
+            if a not in seen:
+                seen.add(a)
+                todo.append(a)
+    return need.get(node, set())

@@ -32,6 +32,8 @@ _SIGS = {
     "vamd_stream_error": (C.c_int, [_vp, C.c_int]),
     "vamd_stream_features": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, _vp]),
     "vamd_stream_llh": (C.c_longlong, [_vp, C.c_int, _vp, C.c_longlong]),
+    "vamd_stream_ivectors": (C.c_longlong, [_vp, C.c_int, _vp, C.c_longlong]),
+    "vamd_engine_ivector_dim": (C.c_int, [_vp]),
     "vamd_stream_stats": (C.c_int, [_vp, C.c_int, _vp, C.c_int]),
     "vamd_stream_decode_llh": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int]),
     "vamd_stream_best_path": (C.c_int, [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _vp]),
@@ -152,6 +154,15 @@ class Engine:
         out = np.zeros(n, np.float32)
         _c.vamd_stream_llh(self.h, s, out.ctypes.data, n)
         return out.reshape(-1, self.out_dim)
+
+    def ivectors(self, s):
+        """Per-chunk i-vectors computed so far (flag collect_llh) [chunks][dim]."""
+        dim = _chk(_c.vamd_engine_ivector_dim(self.h))
+        n = _c.vamd_stream_ivectors(self.h, s, None, 0)
+        _chk(n)
+        out = np.zeros(n, np.float32)
+        _c.vamd_stream_ivectors(self.h, s, out.ctypes.data, n)
+        return out.reshape(-1, dim) if dim else out.reshape(0, 0)
 
     def stats(self, s, cap=100000):
         out = np.zeros((cap, 8), np.float32)
