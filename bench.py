@@ -246,6 +246,7 @@ def main():
                 k: round(v / max(e.decoder_phases()["frames"], 1), 1)
                 for k, v in e.decoder_phases().items() if k != "frames"}
         print(json.dumps(out), flush=True)
+    e.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

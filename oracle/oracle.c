@@ -67,6 +67,28 @@ float orc_expf(float x) {
 }
 
 /* ---- online i-vector extraction ----------------------------------------- */
+/* one row of an affine map in the canonical order (see the nnet affine
+   case in orc_nnet_forward): fmaf chains from 0 over orc_kslices(K) slices,
+   each aligned group of eight walked 0,4,1,5,2,6,3,7, slices summed left to
+   right.  Kaldi leaves these products to BLAS (the LDA's AddMatVec,
+   DiagGmm::LogLikelihoods' AddMatVec pair), so any fixed order restates it;
+   this one is the GPU GEMM's. */
+static float canon_dot(const float* w, const float* x, int K) {
+  const int ns = orc_kslices(K), kw = K / ns;
+  float a = 0.0f;
+  for (int z = 0; z < ns; z++) {
+    float p = 0.0f;
+    const int ke = (z + 1) * kw;
+    for (int kg = z * kw; kg < ke; kg += 8)
+      for (int i = 0; i < 8 && kg + i < ke; i++) {
+        const int k = kg + 8 <= ke ? kg + ((i & 1) << 2) + (i >> 1) : kg + i;
+        p = fmaf(x[k], w[k], p);
+      }
+    a = z == 0 ? p : a + p;
+  }
+  return a;
+}
+
 static void iv_lda(const orc_ivector_model* m, const float* src, int t, int t_ready, float* y) {
   const int D = m->feat_dim, ctx = m->left + m->right + 1, K = ctx * D;
   float x[64 * 16];
@@ -78,8 +100,7 @@ static void iv_lda(const orc_ivector_model* m, const float* src, int t, int t_re
   }
   for (int i = 0; i < m->lda_rows; i++) {
     const float* w = m->lda + (size_t)i * m->lda_cols;
-    float a = 0.0f;
-    for (int j = 0; j < K; j++) a = fmaf(w[j], x[j], a);
+    float a = canon_dot(w, x, K);
     if (m->lda_cols == K + 1) a = a + w[K];
     y[i] = a;
   }
@@ -190,20 +211,26 @@ int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, c
   int done = 0;
   const float log_min_post = (float)log((double)m->min_post);
   float* ll = (float*)malloc(sizeof(float) * G);
-  float xn[256], xr[256];
+  float xn[256], xr[256], xq[512];
+  /* UBM log-likelihoods as one affine row per Gaussian over [x | x*x]:
+     [means_invvars | -0.5 inv_vars] (the -0.5 scaling is exact), gconst last */
+  float* wubm = (float*)malloc(sizeof(float) * (size_t)G * 2 * DL);
+  for (int g = 0; g < G; g++)
+    for (int d = 0; d < DL; d++) {
+      wubm[(size_t)g * 2 * DL + d] = m->means_invvars[(size_t)g * DL + d];
+      wubm[(size_t)g * 2 * DL + DL + d] = -0.5f * m->inv_vars[(size_t)g * DL + d];
+    }
   for (int q = 0; q < nreq; q++) {
     const int f = requests[q];
     if (f >= done) {
       for (int t = done; t <= f; t++) {
         iv_lda(m, norm, t, t_ready[q], xn);
-        for (int g = 0; g < G; g++) {
-          const float* mi = m->means_invvars + (size_t)g * DL;
-          const float* iv = m->inv_vars + (size_t)g * DL;
-          float d1 = 0.0f, d2 = 0.0f;
-          for (int d = 0; d < DL; d++) d1 = fmaf(mi[d], xn[d], d1);
-          for (int d = 0; d < DL; d++) d2 = fmaf(iv[d], xn[d] * xn[d], d2);
-          ll[g] = (m->gconsts[g] + d1) + (-0.5f * d2);
+        for (int d = 0; d < DL; d++) {
+          xq[d] = xn[d];
+          xq[DL + d] = xn[d] * xn[d];
         }
+        for (int g = 0; g < G; g++)
+          ll[g] = canon_dot(wubm + (size_t)g * 2 * DL, xq, 2 * DL) + m->gconsts[g];
         /* num_gselect best, descending, ties by lower index */
         int sel[16];
         int ns = 0;
@@ -256,7 +283,7 @@ int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, c
     for (int i = 0; i < S; i++) out[(size_t)q * S + i] = (float)cur[i];
     out[(size_t)q * S] = out[(size_t)q * S] - (float)m->prior_offset;
   }
-  free(SIM); free(U); free(norm); free(quad); free(ll);
+  free(SIM); free(U); free(norm); free(quad); free(ll); free(wubm);
   return 0;
 }
 

@@ -5,6 +5,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 #include "common.h"
@@ -270,13 +271,9 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     if (iv.feat_dim != plan_.input_dim) VAMD_ERR("i-vector feature dim != nnet input dim");
     if (Si > kIvMaxS || QS > kIvMaxQ || iv.feat_dim > kIvMaxD || iv.lda_dim > kIvMaxD ||
         (iv.left + iv.right + 1) * iv.feat_dim > kIvMaxK || iv.num_gauss > kIvMaxG ||
-        iv.num_gselect > 8 || iv.num_gselect < 1 || iv.cmn_window >= kIvHist || iv.cmn_window < 1 ||
+        iv.num_gselect > 5 || iv.num_gselect < 1 || iv.cmn_window >= kIvHist || iv.cmn_window < 16 ||
         iv.left < 0 || iv.right < 0)
       VAMD_ERR("i-vector extractor dimensions exceed the kernel limits");
-    // normalized-feature ring: one request spans at most its chunk's frames
-    // plus the splice context
-    if (fpc + plan_.right_context + iv.left + iv.right + 8 > kIvNorm)
-      VAMD_ERR("frames-per-chunk too large for the i-vector feature ring");
     IvectorDev& d = iv_.m;
     d.feat_dim = iv.feat_dim; d.left = iv.left; d.right = iv.right;
     d.lda_dim = iv.lda_dim; d.lda_cols = iv.lda.cols; d.num_gauss = iv.num_gauss;
@@ -285,24 +282,115 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     d.min_post = iv.min_post; d.posterior_scale = iv.posterior_scale;
     d.log_min_post = iv.log_min_post;
     d.prior_offset = iv.prior_offset; d.max_count = iv.max_count;
-    d.lda = Upload(iv.lda.data);
     d.cmvn = Upload(iv.cmvn);
-    d.gconsts = Upload(iv.gconsts);
-    d.means_invvars = Upload(iv.means_invvars);
-    d.inv_vars = Upload(iv.inv_vars);
     d.sigma_inv_m = Upload(iv.sigma_inv_m);
     d.U = Upload(iv.U);
+    const int D = iv.feat_dim, DL = iv.lda_dim, G = iv.num_gauss;
+    const int ctx = iv.left + iv.right + 1, K = ctx * D;
     iv_.state = (IvState*)DevAlloc(sizeof(IvState) * S);
     HIPCHECK(hipMemset(iv_.state, 0, sizeof(IvState) * S));
     iv_.quad = (double*)DevAlloc(sizeof(double) * (size_t)S * QS);
-    iv_.hist = (float*)DevAlloc(sizeof(float) * (size_t)S * kIvHist * iv.feat_dim);
-    iv_.norm = (float*)DevAlloc(sizeof(float) * (size_t)S * kIvNorm * iv.feat_dim);
+    iv_.qfull = (double*)DevAlloc(sizeof(double) * (size_t)S * Si * Si);
+    iv_.hist = (float*)DevAlloc(sizeof(float) * (size_t)S * kIvHist * D);
+    // CMVN-normalized features and the UBM input [x | x*x] live in rings laid
+    // out like the activation rings, so the nnet GEMM kernels read them with
+    // the splice as input segments (clamped like the feature input)
+    iv_.norm = (float*)DevAlloc(sizeof(float) * (size_t)S * ring_ * D);
+    float* ivx = (float*)DevAlloc(sizeof(float) * (size_t)S * ring_ * 2 * DL);
     iv_.in_base = ring_ptrs[plan_.input_node];
     iv_.in_mask = ring_ - 1;
     iv_.slots = S;
+    // frame records of one step: per stream at most the chunks' new frames
+    max_iv_frames_ = S * (jobs_per_slot_ * fpc + plan_.right_context + 8);
+    max_iv_rows_ = (max_iv_frames_ / kIvFrameBlock + 2 * S) * kIvFrameBlock;
+    iv_.frames = (IvFrame*)DevAlloc(sizeof(IvFrame) * (size_t)max_iv_rows_);
+    float* xraw = (float*)DevAlloc(sizeof(float) * (size_t)max_iv_rows_ * DL);
+    d_iv_ll_ = (float*)DevAlloc(sizeof(float) * (size_t)max_iv_rows_ * G);
+    iv_.xraw = xraw;
+    iv_.snap = (double*)DevAlloc(sizeof(double) * (size_t)S * jobs_per_slot_ * (QS + Si));
+    iv_.snap_nfr = (double*)DevAlloc(sizeof(double) * (size_t)S * jobs_per_slot_);
+    iv_.chv = (double*)DevAlloc(sizeof(double) * (size_t)max_iv_rows_);
     d_ivec_ = (float*)DevAlloc(sizeof(float) * (size_t)S * jobs_per_slot_ * Si);
     HIPCHECK(hipMemset(d_ivec_, 0, sizeof(float) * (size_t)S * jobs_per_slot_ * Si));
     iv_.ivec = d_ivec_;
+    // GEMM ops over blocks of kIvFrameBlock frames (DevJob: slot, first frame,
+    // splice clamp), canonical order as oracle.c canon_dot
+    std::vector<int> pat(kIvFrameBlock);
+    for (int i = 0; i < kIvFrameBlock; i++) pat[i] = i;
+    const int* d_pat = Upload(pat);
+    std::vector<float> wl((size_t)DL * K), bl(DL, 0.0f);
+    for (int r = 0; r < DL; r++) {
+      for (int j = 0; j < K; j++) wl[(size_t)r * K + j] = iv.lda.row(r)[j];
+      if (iv.lda.cols == K + 1) bl[r] = iv.lda.row(r)[K];
+    }
+    auto base_op = [&](int N, int Kk, const std::vector<float>& W) {
+      NnetOpArgs o;
+      memset(&o, 0, sizeof(o));
+      o.N = N;
+      o.K = Kk;
+      o.P = kIvFrameBlock;
+      o.pattern = d_pat;
+      o.W = Upload(W);
+      o.rings = rings_;
+      o.kslices = GemmKSlices(Kk);
+      o.out_node = -1;
+      return o;
+    };
+    auto splice = [&](NnetOpArgs& o, const float* ring) {
+      o.nsegs = ctx;
+      for (int c = 0; c < ctx; c++) o.segs[c] = DevSeg{ring, D, 1, c - iv.left, c * D, D, 0};
+    };
+    // (0) normalized frames -> [x | x*x] ring: LDA rows twice, squared right half
+    {
+      std::vector<float> w2(wl);
+      w2.insert(w2.end(), wl.begin(), wl.end());
+      std::vector<float> b2(bl);
+      b2.insert(b2.end(), bl.begin(), bl.end());
+      NnetOpArgs o = base_op(2 * DL, K, w2);
+      splice(o, iv_.norm);
+      o.nstages = 2;
+      o.stages[0] = DevStage{nullptr, Upload(b2), nullptr, 0, 0, 0, 0, 0, 0, 1.0f};
+      o.stages[1] = DevStage{nullptr, nullptr, nullptr, 5, 0, 0, 0, DL, 0, 1.0f};
+      o.out_node = 0;
+      o.out_base = ivx;
+      o.out_ldim = 2 * DL;
+      iv_ops_.push_back(o);
+    }
+    // (1) raw frames -> x_raw rows
+    {
+      NnetOpArgs o = base_op(DL, K, wl);
+      splice(o, iv_.in_base);
+      o.nstages = 1;
+      o.stages[0] = DevStage{nullptr, Upload(bl), nullptr, 0, 0, 0, 0, 0, 0, 1.0f};
+      o.llh = xraw;
+      iv_ops_.push_back(o);
+    }
+    // (2) UBM log-likelihoods: [means_invvars | -0.5 inv_vars] . [x | x*x] + gconst
+    {
+      std::vector<float> wu((size_t)G * 2 * DL);
+      for (int g = 0; g < G; g++)
+        for (int e = 0; e < DL; e++) {
+          wu[(size_t)g * 2 * DL + e] = iv.means_invvars[(size_t)g * DL + e];
+          wu[(size_t)g * 2 * DL + DL + e] = -0.5f * iv.inv_vars[(size_t)g * DL + e];
+        }
+      NnetOpArgs o = base_op(G, 2 * DL, wu);
+      o.nsegs = 1;
+      o.segs[0] = DevSeg{ivx, 2 * DL, 0, 0, 0, 2 * DL, 0};
+      o.nstages = 1;
+      o.stages[0] = DevStage{nullptr, Upload(iv.gconsts), nullptr, 0, 0, 0, 0, 0, 0, 1.0f};
+      o.llh = d_iv_ll_;
+      iv_ops_.push_back(o);
+    }
+    for (auto& o : iv_ops_) {
+      int bk = 64;
+      for (int i = 0; i < o.nsegs; i++)
+        while (bk > 8 && (o.segs[i].col0 % bk || o.segs[i].dim % bk)) bk >>= 1;
+      for (int i = 0; i < o.nsegs; i++)
+        if (o.segs[i].col0 % 8 || o.segs[i].dim % 8)
+          VAMD_ERR("i-vector feature dims must be multiples of 8 for the GEMM kernels");
+      if (o.kslices != 1 && !GemmStreamable(o)) VAMD_ERR("i-vector GEMM shape unsupported");
+      iv_op_bk_.push_back(bk);
+    }
   } else if (m.use_ivector) {
     VAMD_WARN("ivector/ extractor present but the nnet has no i-vector input: not used");
   }
@@ -466,7 +554,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
                  2 * Align256(sizeof(SampleJob) * S) + Align256(sizeof(ResampleJob) * S) +
                  Align256(sizeof(MfccJob) * S) +
                  Align256(sizeof(DevJob) * max_jobs_) + Align256(sizeof(DecJob) * S) +
-                 Align256(sizeof(IvStreamJob) * S) + Align256(sizeof(IvReq) * max_jobs_) + 1024;
+                 Align256(sizeof(IvStreamJob) * S) + Align256(sizeof(IvReq) * max_jobs_) +
+                 2 * Align256(sizeof(IvFrameBlock) * ((size_t)max_iv_frames_ / kIvFrameBlock + 2 * S)) + 1024;
   // two halves: a pipelined decoder batch keeps its jobs while the next step stages
   HIPCHECK(hipHostMalloc((void**)&h_stage_, 2 * stage_bytes_, hipHostMallocDefault));
   d_stage_ = (char*)DevAlloc(2 * stage_bytes_);
@@ -534,6 +623,7 @@ void Engine::ResetPipeline(int slot) {
   h.raw_pushed = 0;
   h.res_flushed = false;
   h.iv_reset = true;
+  h.iv_norm_done = h.iv_norm_to = h.iv_stats_done = 0;
 }
 
 void Engine::ResetDecoder(int slot) {
@@ -631,6 +721,9 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
   st_dec_.clear();
   st_iv_jobs_.clear();
   st_iv_reqs_.clear();
+  st_iv_blocks_.clear();
+  st_iv_devjobs_.clear();
+  st_iv_frames_ = 0;
   const int fpc = plan_.fpc, opc = plan_.opc, fss = plan_.fss, R = plan_.right_context;
   int stats_rows = 0;
   bool any = false;
@@ -736,8 +829,23 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
         // the chunk's i-vector: at its last input frame incl. right context,
         // clamped to the utterance (DecodableNnetLoopedOnline); priming
         // jobs (same step, just before) share chunk 0's
-        const int job = (int)st_jobs_.size();
-        st_iv_reqs_.push_back(IvReq{std::min((c + 1) * fpc + R, T) - 1, c == 0 ? jobs0 : job, job + 1, 0});
+        const int job = (int)st_jobs_.size(), f = std::min((c + 1) * fpc + R, T) - 1;
+        IvReq r{f, c == 0 ? jobs0 : job, job + 1, st_iv_frames_, st_iv_frames_, 0, 0, 0};
+        if (f >= h.iv_stats_done) {  // new frames: records, then CG (else reuse)
+          const int ivjob = (int)st_iv_jobs_.size();
+          for (int t0 = h.iv_stats_done; t0 <= f; t0 += kIvFrameBlock) {
+            const int nf = std::min(kIvFrameBlock, f + 1 - t0);
+            // frame records are indexed by GEMM row: kIvFrameBlock per block,
+            // rows past the block's frames are empty records (no posteriors)
+            st_iv_blocks_.push_back(IvFrameBlock{ivjob, t0, nf, st_iv_frames_});
+            st_iv_devjobs_.push_back(DevJob{s, t0, T - 1, 0});
+            st_iv_frames_ += kIvFrameBlock;
+          }
+          r.row_to = st_iv_frames_;
+          h.iv_stats_done = f + 1;
+          h.iv_norm_to = std::max(h.iv_norm_to, std::min(f + iv_.m.right, T - 1) + 1);
+        }
+        st_iv_reqs_.push_back(r);
       }
       if (c >= 0) {
         if (first_real < 0) first_real = (int)st_jobs_.size();
@@ -751,7 +859,8 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
     }
     if ((int)st_iv_reqs_.size() > req0) {
       st_iv_jobs_.push_back(IvStreamJob{s, req0, (int)st_iv_reqs_.size() - req0, h.iv_reset ? 1 : 0, T,
-                                        0, 0, 0});
+                                        h.iv_norm_done, h.iv_norm_to, 0});
+      h.iv_norm_done = h.iv_norm_to;
       h.iv_reset = false;
     }
     h.out_ready += dec_frames;
@@ -847,6 +956,8 @@ void Engine::RunStep(bool allow_pipeline) {
   size_t o_dj = put(st_jobs_.data(), sizeof(DevJob) * st_jobs_.size());
   size_t o_ivj = put(st_iv_jobs_.data(), sizeof(IvStreamJob) * st_iv_jobs_.size());
   size_t o_ivr = put(st_iv_reqs_.data(), sizeof(IvReq) * st_iv_reqs_.size());
+  size_t o_ivb = put(st_iv_blocks_.data(), sizeof(IvFrameBlock) * st_iv_blocks_.size());
+  size_t o_ivd = put(st_iv_devjobs_.data(), sizeof(DevJob) * st_iv_devjobs_.size());
   DecBatch cur;
   cur.jobs = st_dec_;
   cur.o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
@@ -873,8 +984,18 @@ void Engine::RunStep(bool allow_pipeline) {
     IvArgs ia = iv_;
     ia.jobs = (const IvStreamJob*)(dsg + o_ivj);
     ia.reqs = (const IvReq*)(dsg + o_ivr);
-    LaunchIvector(ia, (int)st_iv_jobs_.size(), stream_);
-    launches++;
+    ia.blocks = (const IvFrameBlock*)(dsg + o_ivb);
+    const int rows = (int)st_iv_blocks_.size() * kIvFrameBlock;
+    if (rows > max_iv_rows_) VAMD_ERR("i-vector frame records overflow");
+    LaunchIvectorCmvn(ia, (int)st_iv_jobs_.size(), stream_);
+    for (size_t i = 0; i < iv_ops_.size() && rows > 0; i++) {
+      NnetOpArgs o = iv_ops_[i];
+      o.M = rows;
+      o.jobs = (const DevJob*)(dsg + o_ivd);
+      LaunchNnetGemm(o, iv_op_bk_[i], stream_);
+    }
+    LaunchIvectorStats(ia, d_iv_ll_, rows, (int)st_iv_jobs_.size(), stream_);
+    launches += 4 + (rows > 0 ? 4 : 0);
   }
   if (tk) HIPCHECK(hipEventRecord(ev_[2], stream_));
   const int l_front = launches;
@@ -1068,6 +1189,9 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     st_dec_.clear();
     st_iv_jobs_.clear();
     st_iv_reqs_.clear();
+    st_iv_blocks_.clear();
+    st_iv_devjobs_.clear();
+    st_iv_frames_ = 0;
     h.stats.clear();
     const bool rs = first && (reset || h.need_reset);
     st_dec_.push_back(DecJob{slot, 0, n, rs ? 1 : 0, 0, 0, 0, 0});

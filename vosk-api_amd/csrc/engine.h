@@ -167,6 +167,8 @@ class Engine {
     long long raw_pushed = 0;  // raw (input-rate) samples pushed to the raw ring
     bool res_flushed = false;  // resampler flushed at end of input
     bool iv_reset = true;      // i-vector state restarts at the next request
+    int iv_norm_done = 0, iv_norm_to = 0;  // frames CMVN-normalized (after this step)
+    int iv_stats_done = 0;     // frames accumulated into the i-vector statistics
     std::vector<float> ivecs;  // collect_llh: per-chunk i-vectors
   };
   struct DecBatch {  // one decoder launch's jobs, staged in one staging half
@@ -237,10 +239,17 @@ class Engine {
   std::vector<DecJob> st_dec_;
   std::vector<IvStreamJob> st_iv_jobs_;
   std::vector<IvReq> st_iv_reqs_;
+  std::vector<IvFrameBlock> st_iv_blocks_;
+  std::vector<DevJob> st_iv_devjobs_;  // GEMM rows of the blocks
+  int st_iv_frames_ = 0, max_iv_frames_ = 0;
   // i-vector extraction (nnet with a per-chunk i-vector input)
   bool use_iv_ = false;
   IvArgs iv_{};
   float* d_ivec_ = nullptr;  // [max jobs][ivector dim], row per chunk job of a step
+  float* d_iv_ll_ = nullptr; // [GEMM rows][num_gauss] UBM log-likelihoods
+  std::vector<NnetOpArgs> iv_ops_;  // LDA (normalized -> [x | x*x]), LDA (raw), UBM
+  std::vector<int> iv_op_bk_;
+  int max_iv_rows_ = 0;
   int max_jobs_ = 0, max_dec_frames_ = 0;
 
   void* DevAlloc(size_t bytes);

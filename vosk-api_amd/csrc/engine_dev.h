@@ -107,17 +107,14 @@ struct DecSlot {
 
 // ---- online i-vector extraction (kernels.hip ivector_kernel)
 constexpr int kIvMaxS = 100, kIvMaxD = 64, kIvMaxK = 320, kIvMaxG = 512, kIvMaxQ = 20 * 256;
-constexpr int kIvHist = 1024, kIvNorm = 256;
+constexpr int kIvHist = 1024;
+constexpr int kIvFrameBlock = 8;  // frames per ivector_frame_kernel workgroup
 struct IvectorDev {
   int feat_dim, left, right, lda_dim, lda_cols, num_gauss, ivec_dim, cmn_window;
   int global_frames, num_gselect, num_cg_iters, pad;
   float min_post, posterior_scale, log_min_post, pad2;
   double prior_offset, max_count;
-  const float* lda;            // [lda_dim][lda_cols]
   const double* cmvn;          // [2][feat_dim + 1]
-  const float* gconsts;        // [G]
-  const float* means_invvars;  // [G][lda_dim]
-  const float* inv_vars;       // [G][lda_dim]
   const double* sigma_inv_m;   // [G][lda_dim][S]
   const double* U;             // [G][S(S+1)/2]
 };
@@ -126,25 +123,44 @@ struct IvState {  // per stream, persistent across steps (reset with the pipelin
   double nfr;           // posterior-weighted frame count
   double lin[kIvMaxS];  // linear term (incl. prior)
   double cur[kIvMaxS];  // current i-vector (CG warm start)
-  int norm_done, stats_done, pad0, pad1;
 };
-struct IvStreamJob {  // one workgroup: the requests of one stream in this step
-  int slot, req0, nreq, reset, t_ready, pad0, pad1, pad2;
+struct IvStreamJob {  // one stream's i-vector work in this step
+  int slot, req0, nreq, reset;
+  int t_ready;             // MFCC frames available (splice clamp)
+  int norm_from, norm_to;  // frames to CMVN-normalize
+  int pad;
 };
-struct IvReq {  // i-vector at `frame` -> rows [job_lo, job_hi) of the per-job buffer
-  int frame, job_lo, job_hi, pad;
+struct IvReq {  // i-vector at `frame` -> rows [job_lo, job_hi) of the per-job buffer,
+                // after accumulating frame records [row_from, row_to)
+  int frame, job_lo, job_hi, row_from, row_to, pad0, pad1, pad2;
+};
+struct IvFrameBlock {  // ivector_frame_kernel workgroup: frames t0.. (nf) of a job's stream
+  int job, t0, nf, row;
+};
+struct IvFrame {  // per-frame result: selected Gaussians and posteriors
+  int nsel;
+  int sel[5];
+  float post[5];
+  int xrow;  // row of the frame in the step's LDA / UBM GEMM outputs
 };
 struct IvArgs {
   IvectorDev m;
   IvState* state;     // [slots]
   double* quad;       // [slots][S(S+1)/2]
+  double* qfull;      // [slots][S][S] the same, unpacked for the CG mat-vec (S > 48)
   float* hist;        // [slots][kIvHist][feat_dim] raw features (CMVN window)
-  float* norm;        // [slots][kIvNorm][feat_dim] CMVN-normalized features
+  float* norm;        // [ring][slots][feat_dim] CMVN-normalized features (MFCC ring layout)
   const float* in_base;  // MFCC input ring [ring][slots][feat_dim]
   int in_mask, slots;
+  IvFrame* frames;    // [max frames per step]
+  const float* xraw;  // [GEMM rows][lda_dim] LDA projection of the raw features
+  double* snap;       // [max requests per step][S(S+1)/2 + S] terms at each request
+  double* snap_nfr;   // [max requests per step] frame count at each request
+  double* chv;        // [max frames per step] prior-scale change at each frame
   float* ivec;        // [jobs][S] per chunk job, prior offset removed
   const IvStreamJob* jobs;
   const IvReq* reqs;
+  const IvFrameBlock* blocks;
 };
 
 struct DecJob {

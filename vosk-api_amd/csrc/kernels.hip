@@ -270,6 +270,7 @@ __device__ __forceinline__ float apply_stages(const NnetOpArgs& a, float x, int 
         x = st.scaled ? (st.c * z) + x : z + x;
         break;
       }
+      case 5: x = col >= st.src_col ? x * x : x; break;       // square (i-vector UBM input)
       default: x = x * st.c; break;                            // scale
     }
   }
@@ -335,6 +336,11 @@ __device__ __forceinline__ void epilogue_16(const NnetOpArgs& a, float (&v)[16],
       } else {
 #pragma unroll
         for (int j = 0; j < 16; j++) v[j] = z[j] + v[j];
+      }
+    } else if (kind == 5) {
+      if (col >= st.src_col) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = v[j] * v[j];
       }
     } else {
 #pragma unroll
@@ -673,15 +679,20 @@ void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s) {
 }
 
 // ===========================================================================
-// Online i-vector extraction: Kaldi OnlineIvectorFeature semantics (online
-// CMVN -> splice -> LDA -> diagonal-UBM top-N posteriors -> stats -> CG),
-// operation for operation as the sequential restatement in oracle/oracle.c
-// orc_ivector_extract (double stats, fixed summation orders), so the result
-// is bit-identical.  One 256-thread workgroup per stream; the per-stream state
-// (CMVN window sums, linear / quadratic terms, current i-vector) persists in
-// HBM across steps.  Small LDS footprint (~25 KB) so it co-resides with the
-// pipelined decoder.
-constexpr int IV_FB = 4;  // frames per stats sub-batch
+// Online i-vector extraction: Kaldi OnlineIvectorFeature semantics, operation
+// for operation as the restatement in oracle/oracle.c orc_ivector_extract
+// (double statistics, fixed summation orders), so the result is
+// bit-identical.  Per step:
+//   ivector_cmvn_kernel   one wave per stream: online CMVN of the new frames
+//                         (running double sums, sequential in time) into a
+//                         ring laid out like the MFCC ring
+//   3 GEMM launches       (engine.cc, the nnet GEMM kernels) over blocks of
+//                         frames: LDA of the spliced normalized frames -> [x |
+//                         x*x], LDA of the raw frames, UBM log-likelihoods
+//   ivector_top_kernel    one wave per frame: 5-best Gaussians, posteriors
+//   ivector_acc_kernel    Kaldi's per-frame OnlineIvectorEstimationStats
+//                         updates, XCD-partitioned, frames in order
+//   ivector_cg_kernel     one workgroup per stream: warm-started CG per request
 
 __device__ float dev_expf(float x) {  // oracle.c orc_expf
   if (x < -87.0f) return 0.0f;
@@ -699,292 +710,453 @@ __device__ float dev_expf(float x) {  // oracle.c orc_expf
   return ldexpf(p, (int)k);
 }
 
-struct IvShared {
-  float xs[2][IV_FB][kIvMaxK];  // spliced frames: CMVN-normalized / raw
-  float xl[2][IV_FB][kIvMaxD];  // their LDA projections
-  float ll[IV_FB][kIvMaxG];     // UBM log-likelihoods
-  int sel[IV_FB][8];
-  float post[IV_FB][8];
-  int nsel[IV_FB];
-  double cg[5][kIvMaxS];        // CG: x (= current i-vector), p, r, Ap, b
-  double sc[4];
+__device__ __forceinline__ const float* iv_raw(const IvArgs& a, int slot, int u) {
+  return a.in_base + ((size_t)(u & a.in_mask) * a.slots + slot) * a.m.feat_dim;
+}
+
+__global__ __launch_bounds__(64) void ivector_cmvn_kernel(IvArgs a) {
+  const IvStreamJob J = a.jobs[blockIdx.x];
+  const IvectorDev& m = a.m;
+  const int d = threadIdx.x, D = m.feat_dim, W = m.cmn_window, slot = J.slot;
+  if (d >= D) return;
+  IvState* st = a.state + slot;
+  float* hist = a.hist + (size_t)slot * kIvHist * D;
+  float* norm = a.norm;  // ring layout [ring][slots][feat_dim], like the MFCC ring
+  double csum = J.reset ? 0.0 : st->sum[d];
+  const double gcount = m.cmvn[D], gmean = m.cmvn[d];
+  // blocks of 16 frames, all loads first (cmn_window >= 16: no frame leaving
+  // the window is stored in the same block)
+  for (int u0 = J.norm_from; u0 < J.norm_to; u0 += 16) {
+    float xn[16], xo[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int u = u0 + k;
+      xn[k] = u < J.norm_to ? iv_raw(a, slot, u)[d] : 0.0f;
+      xo[k] = (u < J.norm_to && u - W >= 0) ? hist[(size_t)((u - W) % kIvHist) * D + d] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int u = u0 + k;
+      if (u >= J.norm_to) break;
+      const float x = xn[k];
+      csum = csum + (double)x;
+      hist[(size_t)(u % kIvHist) * D + d] = x;
+      if (u - W >= 0) csum = csum - (double)xo[k];
+      double cnt = (double)min(u + 1, W), stv = csum;
+      if (cnt < W) {
+        double cgf = W - cnt;
+        if (cgf > m.global_frames) cgf = m.global_frames;
+        const double scl = cgf / gcount;
+        stv = stv + scl * gmean;
+        cnt = cnt + scl * gcount;
+      }
+      const float alpha = (float)(-1.0 / cnt);
+      const float off = (float)((double)alpha * stv);
+      norm[((size_t)(u & a.in_mask) * a.slots + slot) * D + d] = x + off;
+    }
+  }
+  st->sum[d] = csum;
+}
+
+// Max of a 64-bit key over the wave: DPP butterflies inside each 16-lane row
+// (quad_perm 1,0,3,2 / 2,3,0,1, half-row and row mirrors), then the four
+// row results combined through readlane.
+__device__ __forceinline__ unsigned long long iv_dpp_step(unsigned long long v, int ctrl_id) {
+  int lo = (int)(unsigned)v, hi = (int)(unsigned)(v >> 32), lo2, hi2;
+  switch (ctrl_id) {
+    case 0:
+      lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0xB1, 0xF, 0xF, false);
+      hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0xB1, 0xF, 0xF, false);
+      break;
+    case 1:
+      lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x4E, 0xF, 0xF, false);
+      hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x4E, 0xF, 0xF, false);
+      break;
+    case 2:
+      lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x141, 0xF, 0xF, false);
+      hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x141, 0xF, 0xF, false);
+      break;
+    default:
+      lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x140, 0xF, 0xF, false);
+      hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x140, 0xF, 0xF, false);
+      break;
+  }
+  const unsigned long long w = ((unsigned long long)(unsigned)hi2 << 32) | (unsigned)lo2;
+  return w > v ? w : v;
+}
+__device__ __forceinline__ unsigned long long iv_wave_max_u64(unsigned long long v) {
+  v = iv_dpp_step(v, 0);
+  v = iv_dpp_step(v, 1);
+  v = iv_dpp_step(v, 2);
+  v = iv_dpp_step(v, 3);
+  unsigned long long r = 0;
+#pragma unroll
+  for (int row = 0; row < 4; row++) {
+    const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)v, row * 16);
+    const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(v >> 32), row * 16);
+    const unsigned long long x = ((unsigned long long)hi << 32) | lo;
+    r = x > r ? x : r;
+  }
+  return r;
+}
+
+// 5-best Gaussians (descending, ties to the lower index) and posteriors of
+// each frame: one wave per frame over the UBM GEMM's log-likelihood row.
+__global__ __launch_bounds__(256) void ivector_top_kernel(IvArgs a, const float* ll, int M) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= M) return;
+  const IvFrameBlock B = a.blocks[r / kIvFrameBlock];
+  const int k0 = r % kIvFrameBlock;
+  if (k0 >= B.nf) {  // padding row of the block: an empty record
+    if (lane == 0) a.frames[r].nsel = 0;
+    return;
+  }
+  const IvectorDev& m = a.m;
+  const int G = m.num_gauss;
+  const float* row = ll + (size_t)r * G;
+  unsigned long long key[kIvMaxG / 64];
+#pragma unroll
+  for (int i = 0; i < kIvMaxG / 64; i++) {
+    const int g = lane + 64 * i;
+    float v = g < G ? row[g] : 0.0f;
+    v = v == 0.0f ? 0.0f : v;  // -0 ties with +0 as in a float comparison
+    key[i] = g < G ? ((unsigned long long)ford(v) << 32) | (0xFFFFFFFFu - (unsigned)g) : 0ull;
+  }
+  int chosen[5];
+  float val[5];
+  unsigned used = 0;
+  const int ng = min(m.num_gselect, G);
+  for (int kk = 0; kk < ng; kk++) {
+    unsigned long long b = 0;
+#pragma unroll
+    for (int i = 0; i < kIvMaxG / 64; i++)
+      if (!((used >> i) & 1) && key[i] > b) b = key[i];
+    b = iv_wave_max_u64(b);
+    const int g = (int)(0xFFFFFFFFu - (unsigned)b);
+    chosen[kk] = g;
+    val[kk] = row[g];
+    if ((g & 63) == lane) used |= 1u << (g >> 6);
+  }
+  if (lane == 0) {
+    int ns = ng;
+    while (ns > 1 && val[ns - 1] < val[0] + m.log_min_post) ns--;
+    float e[5], tot = 0.0f;
+    for (int k = 0; k < ns; k++) {
+      e[k] = dev_expf(val[k] - val[0]);
+      tot = tot + e[k];
+    }
+    IvFrame& F = a.frames[r];
+    F.nsel = ns;
+    F.xrow = r;
+    for (int k = 0; k < ns; k++) {
+      F.sel[k] = chosen[k];
+      F.post[k] = (e[k] / tot) * (m.posterior_scale * 1.0f);
+    }
+  }
+}
+
+__device__ __forceinline__ int iv_tri_row(int e) {  // packed lower-triangle row of entry e
+  int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+  while ((i + 1) * (i + 2) / 2 <= e) i++;
+  while (i * (i + 1) / 2 > e) i--;
+  return i;
+}
+
+constexpr int kIvCgLds = 48;  // S up to this: the CG matrix lives in LDS
+
+// Kaldi's per-frame statistics update.  Eight workgroups per stream, one per
+// XCD (blockIdx % 8 share an XCD): part p owns a contiguous eighth of the
+// packed quadratic term and of the linear-term columns, so each
+// XCD's L2 holds only its slice of U and SigmaInvM.  Each entry replays the
+// stream's frames in order (exactly the oracle's per-entry chains); a
+// snapshot of the terms is taken at every request for the CG kernel.
+// Posterior-weighted frame count and Kaldi's max-count prior rescaling per
+// frame: a short sequential scan per stream (one lane each), so the
+// accumulation kernel needs no divisions.  ch[row] = change of the prior
+// scale at that frame (0 while the count is below max-count).
+__global__ __launch_bounds__(64) void ivector_nfr_kernel(IvArgs a, int njobs) {
+  const int jb = blockIdx.x * 64 + threadIdx.x;
+  if (jb >= njobs) return;
+  const IvStreamJob J = a.jobs[jb];
+  const double mc = a.m.max_count;
+  IvState* st = a.state + J.slot;
+  double nfr = J.reset ? 0.0 : st->nfr;
+  for (int q = 0; q < J.nreq; q++) {
+    const IvReq R = a.reqs[J.req0 + q];
+    for (int r = R.row_from; r < R.row_to; r++) {
+      const IvFrame F = a.frames[r];
+      double tw = 0.0;
+      for (int k = 0; k < F.nsel; k++) {
+        const double w = (double)F.post[k];
+        if (w != 0.0) tw = tw + w;
+      }
+      double ch = 0.0;
+      const double newn = nfr + tw;
+      if (mc > 0.0 && (nfr > mc || newn > mc)) {  // else both scales are exactly 1
+        const double oldp = (nfr > mc ? nfr : mc) / mc;
+        const double newp = (newn > mc ? newn : mc) / mc;
+        ch = newp - oldp;
+      }
+      a.chv[r] = ch;
+      nfr = newn;
+    }
+    a.snap_nfr[J.req0 + q] = nfr;
+  }
+  st->nfr = nfr;
+}
+
+constexpr int kIvAccChunk = 32;  // frame records staged in LDS at a time
+constexpr int kIvAccFrames = 8;  // frames per projection sub-block
+struct IvAccShared {
+  double w[kIvAccChunk][5];
+  double ch[kIvAccChunk];
+  int sel[kIvAccChunk][5];
+  int ns[kIvAccChunk];
+  float xr[kIvAccChunk][kIvMaxD];
+  double proj[kIvAccFrames][5][(kIvMaxS + 7) / 8];
 };
 
-__device__ void iv_matvec(const double* Q, int S, const double* v, double* y) {
-  const int i = threadIdx.x;
-  if (i < S) {
-    double acc = 0.0;
-    for (int j = 0; j < S; j++) {
-      const int r = i > j ? i : j, c = i > j ? j : i;
-      acc = acc + Q[(size_t)r * (r + 1) / 2 + c] * v[j];
-    }
-    y[i] = acc;
+template <int NQP>  // packed quad entries per thread: ceil(ceil(QS / 8) / 256)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ivector_acc_kernel(IvArgs a) {
+  __shared__ IvAccShared sh;
+  const int part = blockIdx.x & 7, jb = blockIdx.x >> 3, tid = threadIdx.x;
+  const IvStreamJob J = a.jobs[jb];
+  const IvectorDev& m = a.m;
+  const int S = m.ivec_dim, DL = m.lda_dim, QS = S * (S + 1) / 2, NE = QS + S;
+  const int qchunk = (QS + 7) / 8, q0 = part * qchunk, q1 = min(QS, q0 + qchunk);
+  const int cw = (S + 7) / 8, c0 = min(S, part * cw), ncol = min(S, c0 + cw) - c0;  // columns [c0, c0+ncol)
+  IvState* st = a.state + J.slot;
+  double* quad = a.quad + (size_t)J.slot * QS;
+  const double po = m.prior_offset;
+  double qe[NQP];
+  bool qd[NQP];
+#pragma unroll
+  for (int j = 0; j < NQP; j++) {
+    const int e = q0 + tid + 256 * j, i = iv_tri_row(e);
+    qd[j] = e == i * (i + 1) / 2 + i;
+    qe[j] = e < q1 ? (J.reset ? (qd[j] ? 1.0 : 0.0) : quad[e]) : 0.0;
   }
+  const int col = c0 + tid;  // lin column owned by threads tid < ncol
+  double lin = 0.0;
+  if (tid < ncol) lin = J.reset ? (col == 0 ? po : 0.0) : st->lin[col];
+  for (int q = 0; q < J.nreq; q++) {
+    const IvReq R = a.reqs[J.req0 + q];
+    for (int c0r = R.row_from; c0r < R.row_to; c0r += kIvAccChunk) {
+      const int nc = min(kIvAccChunk, R.row_to - c0r);
+      // stage the chunk's records (one round of independent loads)
+      __syncthreads();
+      for (int i = tid; i < nc * 5; i += 256) {
+        const int f = i / 5, k = i % 5;
+        const IvFrame& F = a.frames[c0r + f];
+        const int ns = F.nsel;
+        if (k == 0) {
+          sh.ns[f] = ns;
+          sh.ch[f] = a.chv[c0r + f];
+        }
+        sh.w[f][k] = k < ns ? (double)F.post[k] : 0.0;
+        sh.sel[f][k] = k < ns ? F.sel[k] : 0;
+      }
+      for (int i = tid; i < nc * DL; i += 256)
+        sh.xr[i / DL][i % DL] = a.xraw[(size_t)(c0r + i / DL) * DL + i % DL];
+      __syncthreads();
+      for (int b0 = 0; b0 < nc; b0 += kIvAccFrames) {
+        const int nb = min(kIvAccFrames, nc - b0);
+        if (b0 > 0) __syncthreads();  // proj of the previous sub-block consumed
+        // SigmaInvM_g^T x_raw for this part's columns, every (frame, Gaussian)
+        for (int i = tid; i < nb * 5 * ncol; i += 256) {
+          const int c = i % ncol, k = (i / ncol) % 5, f = b0 + i / (5 * ncol);
+          if (k < sh.ns[f] && sh.w[f][k] != 0.0) {
+            const double* sm = m.sigma_inv_m + (size_t)sh.sel[f][k] * DL * S + c0 + c;
+            const float* xr = sh.xr[f];
+            double acc = 0.0;
+            for (int d0 = 0; d0 < DL; d0 += 20) {  // batches of 20 loads in flight
+              double sv[20];
+#pragma unroll
+              for (int u = 0; u < 20; u++) sv[u] = d0 + u < DL ? sm[(size_t)(d0 + u) * S] : 0.0;
+#pragma unroll
+              for (int u = 0; u < 20; u++) {
+                if (d0 + u >= DL) break;
+                acc = fma(sv[u], (double)xr[d0 + u], acc);
+              }
+            }
+            sh.proj[f - b0][k][c] = acc;
+          }
+        }
+        // quadratic entries: U loads of 4 frames at a time, then the chains
+        for (int f0 = 0; f0 < nb; f0 += 4) {
+          double uv[4][5][NQP];
+#pragma unroll
+          for (int f2 = 0; f2 < 4; f2++)
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+#pragma unroll
+              for (int j = 0; j < NQP; j++) {
+                const int f = b0 + f0 + f2;
+                uv[f2][k][j] = (f0 + f2 < nb && k < sh.ns[f] && q0 + tid + 256 * j < q1)
+                                   ? m.U[(size_t)sh.sel[f][k] * QS + q0 + tid + 256 * j] : 0.0;
+              }
+#pragma unroll
+          for (int f2 = 0; f2 < 4; f2++) {
+            const int f = b0 + f0 + f2;
+            if (f0 + f2 >= nb) break;
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+              if (k >= sh.ns[f]) break;
+              const double w = sh.w[f][k];
+              if (w == 0.0) continue;
+#pragma unroll
+              for (int j = 0; j < NQP; j++)
+                if (q0 + tid + 256 * j < q1) qe[j] = qe[j] + w * uv[f2][k][j];
+            }
+            const double ch = sh.ch[f];
+            if (ch != 0.0) {
+#pragma unroll
+              for (int j = 0; j < NQP; j++)
+                if (qd[j] && q0 + tid + 256 * j < q1) qe[j] += ch;
+            }
+          }
+        }
+        __syncthreads();
+        if (tid < ncol) {
+          for (int f = b0; f < b0 + nb; f++) {
+            for (int k = 0; k < sh.ns[f]; k++) {
+              const double w = sh.w[f][k];
+              if (w == 0.0) continue;
+              lin = lin + w * sh.proj[f - b0][k][tid];
+            }
+            if (sh.ch[f] != 0.0 && col == 0) lin = lin + po * sh.ch[f];
+          }
+        }
+      }
+    }
+    if (R.row_to > R.row_from) {
+      double* sn = a.snap + (size_t)(J.req0 + q) * NE;
+#pragma unroll
+      for (int j = 0; j < NQP; j++)
+        if (q0 + tid + 256 * j < q1) sn[q0 + tid + 256 * j] = qe[j];
+      if (tid < ncol) sn[QS + col] = lin;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NQP; j++)
+    if (q0 + tid + 256 * j < q1) quad[q0 + tid + 256 * j] = qe[j];
+  if (tid < ncol) st->lin[col] = lin;
 }
 
 __device__ double iv_dot(const double* x, const double* y, int n) {
   double s = 0.0;
+#pragma unroll 8
   for (int i = 0; i < n; i++) s = s + x[i] * y[i];
   return s;
 }
 
-__global__ __launch_bounds__(256) void ivector_kernel(IvArgs a) {
-  __shared__ IvShared sh;
-  const IvStreamJob J = a.jobs[blockIdx.x];
-  const IvectorDev& m = a.m;
-  const int tid = threadIdx.x, slot = J.slot;
-  const int D = m.feat_dim, DL = m.lda_dim, S = m.ivec_dim, G = m.num_gauss;
-  const int QS = S * (S + 1) / 2, K = (m.left + m.right + 1) * D, W = m.cmn_window;
-  IvState* st = a.state + slot;
-  double* quad = a.quad + (size_t)slot * QS;
-  float* hist = a.hist + (size_t)slot * kIvHist * D;
-  float* norm = a.norm + (size_t)slot * kIvNorm * D;
-  auto raw = [&](int u) { return a.in_base + ((size_t)(u & a.in_mask) * a.slots + slot) * D; };
-  const double po = m.prior_offset, mc = m.max_count;
-
-  // ---- state -> registers / LDS (reset: prior-only statistics)
-  double csum = 0.0, lin = 0.0, nfr = 0.0;
-  double qe[kIvMaxQ / 256];
-  bool qdiag[kIvMaxQ / 256];
-#pragma unroll
-  for (int j = 0; j < kIvMaxQ / 256; j++) {
-    const int e = tid + 256 * j;
-    int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-    while ((i + 1) * (i + 2) / 2 <= e) i++;
-    while (i * (i + 1) / 2 > e) i--;
-    qdiag[j] = e == i * (i + 1) / 2 + i;
-    qe[j] = e < QS ? (J.reset ? (qdiag[j] ? 1.0 : 0.0) : quad[e]) : 0.0;
-  }
-  int norm_done = 0, stats_done = 0;
-  if (J.reset) {
-    if (tid < S) lin = tid == 0 ? po : 0.0;
-    if (tid < S) sh.cg[0][tid] = tid == 0 ? po : 0.0;
-  } else {
-    if (tid < D) csum = st->sum[tid];
-    if (tid < S) lin = st->lin[tid];
-    if (tid < S) sh.cg[0][tid] = st->cur[tid];
-    nfr = st->nfr;
-    norm_done = st->norm_done;
-    stats_done = st->stats_done;
-  }
-  __syncthreads();
-
-  for (int q = 0; q < J.nreq; q++) {
-    const IvReq R = a.reqs[J.req0 + q];
-    const int f = R.frame;
-    if (f >= stats_done) {
-      // 1. online CMVN through the splice's right context of frame f
-      const int nend = min(f + m.right, J.t_ready - 1) + 1;
-      if (tid < D) {
-        const double gcount = m.cmvn[D];
-        for (int u = norm_done; u < nend; u++) {
-          const float x = raw(u)[tid];
-          csum = csum + (double)x;
-          hist[(size_t)(u % kIvHist) * D + tid] = x;
-          if (u - W >= 0) csum = csum - (double)hist[(size_t)((u - W) % kIvHist) * D + tid];
-          double cnt = (double)min(u + 1, W), stv = csum;
-          if (cnt < W) {
-            double cgf = W - cnt;
-            if (cgf > m.global_frames) cgf = m.global_frames;
-            const double scl = cgf / gcount;
-            stv = stv + scl * m.cmvn[tid];
-            cnt = cnt + scl * gcount;
-          }
-          const float alpha = (float)(-1.0 / cnt);
-          const float off = (float)((double)alpha * stv);
-          norm[(size_t)(u % kIvNorm) * D + tid] = x + off;
-        }
-      }
-      if (nend > norm_done) norm_done = nend;
-      __syncthreads();
-      // 2. statistics of frames [stats_done, f], IV_FB frames at a time
-      for (int t0 = stats_done; t0 <= f; t0 += IV_FB) {
-        const int nf = min(IV_FB, f + 1 - t0);
-        for (int i = tid; i < nf * K; i += 256) {
-          const int fr = i / K, j = i - fr * K, c = j / D, d = j - c * D;
-          int u = t0 + fr - m.left + c;
-          u = max(u, 0);
-          u = min(u, J.t_ready - 1);
-          sh.xs[0][fr][j] = norm[(size_t)(u % kIvNorm) * D + d];
-          sh.xs[1][fr][j] = raw(u)[d];
-        }
-        __syncthreads();
-        for (int i = tid; i < 2 * nf * DL; i += 256) {
-          const int w = i / (nf * DL), r = i - w * nf * DL, fr = r / DL, row = r - fr * DL;
-          const float* lw = m.lda + (size_t)row * m.lda_cols;
-          const float* x = sh.xs[w][fr];
-          float acc = 0.0f;
-          for (int j = 0; j < K; j++) acc = fmaf(lw[j], x[j], acc);
-          if (m.lda_cols == K + 1) acc = acc + lw[K];
-          sh.xl[w][fr][row] = acc;
-        }
-        __syncthreads();
-        for (int i = tid; i < nf * G; i += 256) {
-          const int fr = i / G, g = i - fr * G;
-          const float* mi = m.means_invvars + (size_t)g * DL;
-          const float* iv = m.inv_vars + (size_t)g * DL;
-          const float* x = sh.xl[0][fr];
-          float d1 = 0.0f, d2 = 0.0f;
-          for (int d = 0; d < DL; d++) d1 = fmaf(mi[d], x[d], d1);
-          for (int d = 0; d < DL; d++) d2 = fmaf(iv[d], x[d] * x[d], d2);
-          sh.ll[fr][g] = (m.gconsts[g] + d1) + (-0.5f * d2);
-        }
-        __syncthreads();
-        // top-N Gaussians of a frame (descending, ties to the lower index): one wave
-        {
-          const int wv = tid >> 6, lane = tid & 63;
-          if (wv < nf) {
-            const float* ll = sh.ll[wv];
-            int chosen[8];
-            int ns = 0;
-            for (int k = 0; k < m.num_gselect && k < G; k++) {
-              float bv = 0.0f;
-              int bi = -1;
-              for (int g = lane; g < G; g += 64) {
-                bool used = false;
-                for (int j = 0; j < ns; j++) used |= chosen[j] == g;
-                if (used) continue;
-                if (bi < 0 || ll[g] > bv) { bv = ll[g]; bi = g; }
-              }
-              for (int o = 32; o > 0; o >>= 1) {
-                const float ov = __shfl_xor(bv, o);
-                const int oi = __shfl_xor(bi, o);
-                if (oi >= 0 && (bi < 0 || ov > bv || (ov == bv && oi < bi))) { bv = ov; bi = oi; }
-              }
-              chosen[ns++] = bi;
-            }
-            if (lane == 0) {
-              while (ns > 1 && ll[chosen[ns - 1]] < ll[chosen[0]] + m.log_min_post) ns--;
-              float e[8], tot = 0.0f;
-              for (int k = 0; k < ns; k++) {
-                e[k] = dev_expf(ll[chosen[k]] - ll[chosen[0]]);
-                tot = tot + e[k];
-              }
-              for (int k = 0; k < ns; k++) {
-                sh.sel[wv][k] = chosen[k];
-                sh.post[wv][k] = (e[k] / tot) * (m.posterior_scale * 1.0f);
-              }
-              sh.nsel[wv] = ns;
-            }
-          }
-        }
-        __syncthreads();
-        // accumulate: each thread owns lin[tid] and the packed quad entries tid + 256 j
-        for (int fr = 0; fr < nf; fr++) {
-          const int ns = sh.nsel[fr];
-          double tw = 0.0;
-          for (int k = 0; k < ns; k++) {
-            const double w = (double)sh.post[fr][k];
-            if (w == 0.0) continue;
-            const int g = sh.sel[fr][k];
-            if (tid < S) {
-              const double* sm = m.sigma_inv_m + (size_t)g * DL * S + tid;
-              const float* xr = sh.xl[1][fr];
-              double acc = 0.0;
-              for (int d = 0; d < DL; d++) acc = fma(sm[(size_t)d * S], (double)xr[d], acc);
-              lin = lin + w * acc;
-            }
-            const double* u = m.U + (size_t)g * QS;
-#pragma unroll
-            for (int j = 0; j < kIvMaxQ / 256; j++) {
-              const int e = tid + 256 * j;
-              if (e < QS) qe[j] = qe[j] + w * u[e];
-            }
-            tw = tw + w;
-          }
-          if (mc > 0.0) {
-            const double oldp = (nfr > mc ? nfr : mc) / mc, newn = nfr + tw;
-            const double newp = (newn > mc ? newn : mc) / mc, ch = newp - oldp;
-            if (ch != 0.0) {
-              if (tid == 0) lin = lin + po * ch;
-#pragma unroll
-              for (int j = 0; j < kIvMaxQ / 256; j++)
-                if (qdiag[j] && tid + 256 * j < QS) qe[j] += ch;
-            }
-          }
-          nfr = nfr + tw;
-        }
-        __syncthreads();
-      }
-      stats_done = f + 1;
-      // 3. conjugate gradient from the previous i-vector (Kaldi LinearCgd)
-      if (nfr > 0.0) {
-#pragma unroll
-        for (int j = 0; j < kIvMaxQ / 256; j++)
-          if (tid + 256 * j < QS) quad[tid + 256 * j] = qe[j];
-        double *X = sh.cg[0], *P = sh.cg[1], *Rr = sh.cg[2], *AP = sh.cg[3], *B = sh.cg[4];
-        if (tid < S) B[tid] = lin;
-        __syncthreads();
-        iv_matvec(quad, S, X, AP);
-        __syncthreads();
-        if (tid < S) {
-          P[tid] = B[tid] - AP[tid];
-          Rr[tid] = -P[tid];
-        }
-        __syncthreads();
-        if (tid == 0) sh.sc[0] = iv_dot(Rr, Rr, S);
-        __syncthreads();
-        double rcur = sh.sc[0], rrec = rcur;
-        for (int k = 0; k < S + 5 && k != m.num_cg_iters; k++) {
-          iv_matvec(quad, S, P, AP);
-          __syncthreads();
-          if (tid == 0) sh.sc[1] = -iv_dot(P, Rr, S) / iv_dot(P, AP, S);
-          __syncthreads();
-          const double alpha = sh.sc[1];
-          if (tid < S) {
-            X[tid] = X[tid] + alpha * P[tid];
-            Rr[tid] = Rr[tid] + alpha * AP[tid];
-          }
-          __syncthreads();
-          if (tid == 0) sh.sc[2] = iv_dot(Rr, Rr, S);
-          __syncthreads();
-          double rnext = sh.sc[2];
-          if (rnext < 1e-4 * rrec || rnext > 1e4 * rrec) {
-            iv_matvec(quad, S, X, AP);
-            __syncthreads();
-            if (tid < S) Rr[tid] = AP[tid] - B[tid];
-            __syncthreads();
-            if (tid == 0) sh.sc[3] = iv_dot(Rr, Rr, S);
-            __syncthreads();
-            rnext = sh.sc[3];
-            rrec = rnext;
-          }
-          if (rnext <= 2.2250738585072014e-308) break;
-          const double beta = rnext / rcur;
-          if (tid < S) P[tid] = beta * P[tid] - Rr[tid];
-          __syncthreads();
-          rcur = rnext;
-        }
-        __syncthreads();
-      }
-    }
-    // i-vector rows of the request's chunk jobs (prior offset removed)
-    for (int i = tid; i < (R.job_hi - R.job_lo) * S; i += 256) {
-      const int r = R.job_lo + i / S, s = i % S;
-      float v = (float)sh.cg[0][s];
-      if (s == 0) v = v - (float)po;
-      a.ivec[(size_t)r * S + s] = v;
-    }
-  }
-  // ---- registers / LDS -> state
-  if (tid < D) st->sum[tid] = csum;
-  if (tid < S) {
-    st->lin[tid] = lin;
-    st->cur[tid] = sh.cg[0][tid];
-  }
-#pragma unroll
-  for (int j = 0; j < kIvMaxQ / 256; j++)
-    if (tid + 256 * j < QS) quad[tid + 256 * j] = qe[j];
-  if (tid == 0) {
-    st->nfr = nfr;
-    st->norm_done = norm_done;
-    st->stats_done = stats_done;
+// y = Q v over the full symmetric matrix (row j read as column: lanes coalesced)
+__device__ void iv_matvec(const double* Qf, int S, const double* v, double* y) {
+  const int i = threadIdx.x;
+  if (i < S) {
+    double acc = 0.0;
+#pragma unroll 8
+    for (int j = 0; j < S; j++) acc = acc + Qf[(size_t)j * S + i] * v[j];
+    y[i] = acc;
   }
 }
 
-void LaunchIvector(const IvArgs& a, int njobs, hipStream_t s) {
+struct IvCgShared {
+  double cg[5][kIvMaxS];  // x (= current i-vector), p, r, Ap, b
+  double sc[4];
+  double q[kIvCgLds * kIvCgLds];
+};
+
+// Warm-started conjugate gradient (Kaldi LinearCgd) per request, in order.
+__global__ __launch_bounds__(128) void ivector_cg_kernel(IvArgs a) {
+  __shared__ IvCgShared sh;
+  const IvStreamJob J = a.jobs[blockIdx.x];
+  const IvectorDev& m = a.m;
+  const int tid = threadIdx.x, S = m.ivec_dim, QS = S * (S + 1) / 2, NE = QS + S;
+  IvState* st = a.state + J.slot;
+  double* qfull = S <= kIvCgLds ? sh.q : a.qfull + (size_t)J.slot * S * S;
+  const double po = m.prior_offset;
+  double *X = sh.cg[0], *P = sh.cg[1], *Rr = sh.cg[2], *AP = sh.cg[3], *Bv = sh.cg[4];
+  if (tid < S) X[tid] = J.reset ? (tid == 0 ? po : 0.0) : st->cur[tid];
+  for (int q = 0; q < J.nreq; q++) {
+    const IvReq R = a.reqs[J.req0 + q];
+    if (R.row_to > R.row_from && a.snap_nfr[J.req0 + q] > 0.0) {
+      const double* sn = a.snap + (size_t)(J.req0 + q) * NE;
+      __syncthreads();
+      for (int e = tid; e < QS; e += 128) {
+        const int r = iv_tri_row(e), c = e - r * (r + 1) / 2;
+        const double v = sn[e];
+        qfull[(size_t)r * S + c] = v;
+        qfull[(size_t)c * S + r] = v;
+      }
+      if (tid < S) Bv[tid] = sn[QS + tid];
+      __syncthreads();
+      iv_matvec(qfull, S, X, AP);
+      __syncthreads();
+      if (tid < S) {
+        P[tid] = Bv[tid] - AP[tid];
+        Rr[tid] = -P[tid];
+      }
+      __syncthreads();
+      if (tid == 0) sh.sc[0] = iv_dot(Rr, Rr, S);
+      __syncthreads();
+      double rcur = sh.sc[0], rrec = rcur;
+      for (int k = 0; k < S + 5 && k != m.num_cg_iters; k++) {
+        iv_matvec(qfull, S, P, AP);
+        __syncthreads();
+        if (tid == 0) sh.sc[1] = -iv_dot(P, Rr, S) / iv_dot(P, AP, S);
+        __syncthreads();
+        const double alpha = sh.sc[1];
+        if (tid < S) {
+          X[tid] = X[tid] + alpha * P[tid];
+          Rr[tid] = Rr[tid] + alpha * AP[tid];
+        }
+        __syncthreads();
+        if (tid == 0) sh.sc[2] = iv_dot(Rr, Rr, S);
+        __syncthreads();
+        double rnext = sh.sc[2];
+        if (rnext < 1e-4 * rrec || rnext > 1e4 * rrec) {
+          iv_matvec(qfull, S, X, AP);
+          __syncthreads();
+          if (tid < S) Rr[tid] = AP[tid] - Bv[tid];
+          __syncthreads();
+          if (tid == 0) sh.sc[3] = iv_dot(Rr, Rr, S);
+          __syncthreads();
+          rnext = sh.sc[3];
+          rrec = rnext;
+        }
+        if (rnext <= 2.2250738585072014e-308) break;
+        const double beta = rnext / rcur;
+        if (tid < S) P[tid] = beta * P[tid] - Rr[tid];
+        __syncthreads();
+        rcur = rnext;
+      }
+    }
+    __syncthreads();
+    // i-vector rows of the request's chunk jobs (prior offset removed)
+    for (int i = tid; i < (R.job_hi - R.job_lo) * S; i += 128) {
+      const int r = R.job_lo + i / S, c = i % S;
+      float v = (float)X[c];
+      if (c == 0) v = v - (float)po;
+      a.ivec[(size_t)r * S + c] = v;
+    }
+  }
+  if (tid < S) st->cur[tid] = X[tid];
+}
+
+void LaunchIvectorCmvn(const IvArgs& a, int njobs, hipStream_t s) {
+  if (njobs > 0) hipLaunchKernelGGL(ivector_cmvn_kernel, dim3(njobs), dim3(64), 0, s, a);
+}
+
+void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, hipStream_t s) {
   if (njobs <= 0) return;
-  hipLaunchKernelGGL(ivector_kernel, dim3(njobs), dim3(256), 0, s, a);
+  if (rows > 0) hipLaunchKernelGGL(ivector_top_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, a, ll, rows);
+  hipLaunchKernelGGL(ivector_nfr_kernel, dim3((njobs + 63) / 64), dim3(64), 0, s, a, njobs);
+  const int S = a.m.ivec_dim, nqp = ((S * (S + 1) / 2 + 7) / 8 + 255) / 256;
+  if (nqp <= 1) hipLaunchKernelGGL(ivector_acc_kernel<1>, dim3(njobs * 8), dim3(256), 0, s, a);
+  else if (nqp == 2) hipLaunchKernelGGL(ivector_acc_kernel<2>, dim3(njobs * 8), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(ivector_acc_kernel<3>, dim3(njobs * 8), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(ivector_cg_kernel, dim3(njobs), dim3(128), 0, s, a);
 }
 
 // ===========================================================================
