@@ -137,6 +137,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   HIPCHECK(hipSetDevice(cfg_.device));
   HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIPCHECK(hipStreamCreateWithFlags(&dstream_, hipStreamNonBlocking));
+  HIPCHECK(hipStreamCreateWithFlags(&fstream_, hipStreamNonBlocking));
   const ModelData& m = *md_;
   const int fss = m.dcb.frame_subsampling_factor;
   int fpc = cfg_.frames_per_chunk;
@@ -233,8 +234,9 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   jobs_per_slot_ = plan_.priming_chunks + 2;
   const int step_frames = cfg_.max_step_samples / o.WindowShift() + 2;
   ring_ = std::max(512, plan_.RingFrames(jobs_per_slot_));
+  // the pipelined front end runs one step ahead of the nnet
   ring_ = std::max(ring_, Pow2AtLeast((long long)jobs_per_slot_ * fpc + plan_.left_context +
-                                      plan_.right_context + step_frames + fpc + 16));
+                                      plan_.right_context + 2 * step_frames + fpc + 16));
   sample_ring_ = Pow2AtLeast((long long)cfg_.max_step_samples + 2 * L + o.WindowShift() + 64);
   const int S = cfg_.max_slots;
   std::vector<float*> ring_ptrs(plan_.nodes.size());
@@ -310,9 +312,11 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     iv_.snap = (double*)DevAlloc(sizeof(double) * (size_t)S * jobs_per_slot_ * (QS + Si));
     iv_.snap_nfr = (double*)DevAlloc(sizeof(double) * (size_t)S * jobs_per_slot_);
     iv_.chv = (double*)DevAlloc(sizeof(double) * (size_t)max_iv_rows_);
-    d_ivec_ = (float*)DevAlloc(sizeof(float) * (size_t)S * jobs_per_slot_ * Si);
-    HIPCHECK(hipMemset(d_ivec_, 0, sizeof(float) * (size_t)S * jobs_per_slot_ * Si));
-    iv_.ivec = d_ivec_;
+    for (int i = 0; i < 2; i++) {
+      d_ivec_buf_[i] = (float*)DevAlloc(sizeof(float) * (size_t)S * jobs_per_slot_ * Si);
+      HIPCHECK(hipMemset(d_ivec_buf_[i], 0, sizeof(float) * (size_t)S * jobs_per_slot_ * Si));
+    }
+    iv_.ivec = d_ivec_buf_[0];
     // GEMM ops over blocks of kIvFrameBlock frames (DevJob: slot, first frame,
     // splice clamp), canonical order as oracle.c canon_dot
     std::vector<int> pat(kIvFrameBlock);
@@ -440,8 +444,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
         a.parts[i] = DevPart{gp.col0, gp.dim, ni, (int)gp.prog.size()};
         for (auto& g : gp.prog) {
           if (ni >= kMaxInstr) VAMD_ERR("descriptor program too long in op " << op.name);
-          if (g.op == GInstr::PUSH_JOB)  // the step's per-job i-vector rows
-            a.instr[ni++] = DevInstr{d_ivec_, g.op, plan_.ivector_dim, 0, 0, g.src_col, g.c};
+          if (g.op == GInstr::PUSH_JOB)  // the step's per-job i-vector rows (buffer set per step)
+            a.instr[ni++] = DevInstr{d_ivec_buf_[0], g.op, plan_.ivector_dim, 0, 0, g.src_col, g.c};
           else
             a.instr[ni++] = DevInstr{g.op == GInstr::PUSH ? ring_ptrs[g.node] : nullptr, g.op,
                                      g.op == GInstr::PUSH ? ring_dims[g.node] : 0,
@@ -556,9 +560,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
                  Align256(sizeof(DevJob) * max_jobs_) + Align256(sizeof(DecJob) * S) +
                  Align256(sizeof(IvStreamJob) * S) + Align256(sizeof(IvReq) * max_jobs_) +
                  2 * Align256(sizeof(IvFrameBlock) * ((size_t)max_iv_frames_ / kIvFrameBlock + 2 * S)) + 1024;
-  // two halves: a pipelined decoder batch keeps its jobs while the next step stages
-  HIPCHECK(hipHostMalloc((void**)&h_stage_, 2 * stage_bytes_, hipHostMallocDefault));
-  d_stage_ = (char*)DevAlloc(2 * stage_bytes_);
+  // three buffers: the pipelined nnet and decoder passes keep their jobs
+  // while the next step stages
+  HIPCHECK(hipHostMalloc((void**)&h_stage_, 3 * stage_bytes_, hipHostMallocDefault));
+  d_stage_ = (char*)DevAlloc(3 * stage_bytes_);
   HIPCHECK(hipHostMalloc((void**)&h_slots_, sizeof(DecSlot) * S, hipHostMallocDefault));
   HIPCHECK(hipHostMalloc((void**)&h_stats_, sizeof(FrameStat) * max_dec_frames_, hipHostMallocDefault));
   for (auto& ev : ev_) HIPCHECK(hipEventCreate(&ev));
@@ -572,6 +577,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
 Engine::~Engine() {
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (dstream_) (void)hipStreamSynchronize(dstream_);
+  if (fstream_) (void)hipStreamSynchronize(fstream_);
   for (auto& ev : ev_)
     if (ev) (void)hipEventDestroy(ev);
   for (auto& h : slots_)
@@ -582,6 +588,7 @@ Engine::~Engine() {
   if (h_stats_) (void)hipHostFree(h_stats_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (dstream_) (void)hipStreamDestroy(dstream_);
+  if (fstream_) (void)hipStreamDestroy(fstream_);
 }
 
 int Engine::AllocSlot() {
@@ -883,8 +890,8 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
 void Engine::LaunchDecodeBatch(const DecBatch& b, hipStream_t s) {
   if (b.jobs.empty()) return;
   DecArgs d = dec_;
-  d.jobs = (const DecJob*)(d_stage_ + (size_t)b.half * stage_bytes_ + b.o_ej);
-  d.llh = d_llh_buf_[b.half];
+  d.jobs = (const DecJob*)(d_stage_ + (size_t)b.buf * stage_bytes_ + b.o_ej);
+  d.llh = d_llh_buf_[b.llh];
   LaunchDecode(d, (int)b.jobs.size(), s);
   HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(),
                           hipMemcpyDeviceToHost, s));
@@ -910,7 +917,7 @@ void Engine::FinishDecodeBatch(const DecBatch& b) {
     if (cfg_.collect_llh && j.nframes) {
       size_t n = (size_t)j.nframes * plan_.out_dim, o = h.llh.size();
       h.llh.resize(o + n);
-      HIPCHECK(hipMemcpy(h.llh.data() + o, d_llh_buf_[b.half] + (size_t)j.llh_row0 * plan_.out_dim,
+      HIPCHECK(hipMemcpy(h.llh.data() + o, d_llh_buf_[b.llh] + (size_t)j.llh_row0 * plan_.out_dim,
                          sizeof(float) * n, hipMemcpyDeviceToHost));
     }
     if (cfg_.collect_stats) {
@@ -927,15 +934,36 @@ void Engine::FinishDecodeBatch(const DecBatch& b) {
   }
 }
 
-// One step: stage inputs (one pinned H2D copy), samples -> MFCC -> nnet ops on
-// the main stream; the decoder runs this step's LLH in order (no pipeline) or
-// the previous step's LLH concurrently on the decoder stream (pipeline).
+void Engine::LaunchNnet(const NnetBatch& b, hipStream_t s) {
+  if (b.njobs == 0) return;
+  const DevJob* dj = (const DevJob*)(d_stage_ + (size_t)b.buf * stage_bytes_ + b.o_dj);
+  for (size_t i = 0; i < plan_.ops.size(); i++) {
+    NnetOpArgs a = op_args_[i];
+    a.M = b.njobs * a.P;
+    a.jobs = dj;
+    a.llh = d_llh_buf_[b.par];
+    if (plan_.ops[i].kind == Op::GEMM) {
+      LaunchNnetGemm(a, op_bk_[i], s);
+    } else {
+      for (int k = 0; k < a.nparts; k++)
+        for (int j = a.parts[k].instr0; j < a.parts[k].instr0 + a.parts[k].ninstr; j++)
+          if (a.instr[j].op == GInstr::PUSH_JOB) a.instr[j].base = d_ivec_buf_[b.par];
+      LaunchNnetGather(a, s);
+    }
+  }
+  counters_.launches += (long long)plan_.ops.size();
+}
+
+// One engine step.  Front end (staging copy, samples, MFCC, i-vectors) of the
+// step just built, the nnet of the previous step and the decoder of the one
+// before run concurrently on three streams (pipeline), or all three stages of
+// this step in order on the main stream.
 void Engine::RunStep(bool allow_pipeline) {
   const bool pipe = cfg_.pipeline && allow_pipeline;
   if (!pipe) FlushLocked();
-  const int hf = half_;
-  char* hs = h_stage_ + (size_t)hf * stage_bytes_;
-  char* dsg = d_stage_ + (size_t)hf * stage_bytes_;
+  const int buf = (int)(seq_ % 3), par = (int)(seq_ % 2);
+  char* hs = h_stage_ + (size_t)buf * stage_bytes_;
+  char* dsg = d_stage_ + (size_t)buf * stage_bytes_;
   size_t off = 0;
   auto put = [&](const void* src, size_t bytes) {
     size_t o = off;
@@ -953,105 +981,104 @@ void Engine::RunStep(bool allow_pipeline) {
   size_t o_rj = put(st_raw_.data(), sizeof(SampleJob) * st_raw_.size());
   size_t o_resj = put(st_res_.data(), sizeof(ResampleJob) * st_res_.size());
   size_t o_mj = put(st_mfcc_.data(), sizeof(MfccJob) * st_mfcc_.size());
-  size_t o_dj = put(st_jobs_.data(), sizeof(DevJob) * st_jobs_.size());
+  NnetBatch cur;
+  cur.njobs = (int)st_jobs_.size();
+  cur.o_dj = put(st_jobs_.data(), sizeof(DevJob) * st_jobs_.size());
+  cur.buf = buf;
+  cur.par = par;
   size_t o_ivj = put(st_iv_jobs_.data(), sizeof(IvStreamJob) * st_iv_jobs_.size());
   size_t o_ivr = put(st_iv_reqs_.data(), sizeof(IvReq) * st_iv_reqs_.size());
   size_t o_ivb = put(st_iv_blocks_.data(), sizeof(IvFrameBlock) * st_iv_blocks_.size());
   size_t o_ivd = put(st_iv_devjobs_.data(), sizeof(DevJob) * st_iv_devjobs_.size());
-  DecBatch cur;
-  cur.jobs = st_dec_;
-  cur.o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
-  cur.half = hf;
-  for (auto& j : st_dec_) cur.expect.push_back(slots_[j.slot].decoded_at_build);
+  cur.dec.jobs = st_dec_;
+  cur.dec.o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
+  cur.dec.buf = buf;
+  cur.dec.llh = par;
+  for (auto& j : st_dec_) cur.dec.expect.push_back(slots_[j.slot].decoded_at_build);
   if (off > stage_bytes_) VAMD_ERR("step staging overflow");
+
   const bool tk = cfg_.time_kernels;
-  if (tk) HIPCHECK(hipEventRecord(ev_[0], stream_));
-  HIPCHECK(hipMemcpyAsync(dsg, hs, off, hipMemcpyHostToDevice, stream_));
-  int launches = 0;
-  if (tk) HIPCHECK(hipEventRecord(ev_[1], stream_));
-  LaunchAppendSamples((const SampleJob*)(dsg + o_rj), (int)st_raw_.size(), d_raw_, raw_ring_,
-                      stream_);
+  hipStream_t fs = pipe ? fstream_ : stream_, ns = stream_, ds = pipe ? dstream_ : stream_;
+  if (tk) HIPCHECK(hipEventRecord(ev_[0], fs));
+  HIPCHECK(hipMemcpyAsync(dsg, hs, off, hipMemcpyHostToDevice, fs));
+  // ---- front end of this step
+  int lf = 0;
+  if (tk) HIPCHECK(hipEventRecord(ev_[1], fs));
+  LaunchAppendSamples((const SampleJob*)(dsg + o_rj), (int)st_raw_.size(), d_raw_, raw_ring_, fs);
   LaunchResample((const ResampleJob*)(dsg + o_resj), (int)st_res_.size(), d_res_tables_, d_raw_,
-                 raw_ring_, d_samples_, sample_ring_, stream_);
-  launches += !st_raw_.empty() + !st_res_.empty();
+                 raw_ring_, d_samples_, sample_ring_, fs);
+  lf += !st_raw_.empty() + !st_res_.empty();
   LaunchAppendSamples((const SampleJob*)(dsg + o_sj), (int)st_samples_.size(), d_samples_,
-                      sample_ring_, stream_);
-  launches += !st_samples_.empty();
-  LaunchMfcc(mfcc_, (const MfccJob*)(dsg + o_mj), (int)st_mfcc_.size(), st_mfcc_total_,
-             d_samples_, sample_ring_, rings_, stream_);
-  launches += st_mfcc_total_ > 0;
+                      sample_ring_, fs);
+  lf += !st_samples_.empty();
+  LaunchMfcc(mfcc_, (const MfccJob*)(dsg + o_mj), (int)st_mfcc_.size(), st_mfcc_total_, d_samples_,
+             sample_ring_, rings_, fs);
+  lf += st_mfcc_total_ > 0;
   if (!st_iv_jobs_.empty()) {
     IvArgs ia = iv_;
     ia.jobs = (const IvStreamJob*)(dsg + o_ivj);
     ia.reqs = (const IvReq*)(dsg + o_ivr);
     ia.blocks = (const IvFrameBlock*)(dsg + o_ivb);
+    ia.ivec = d_ivec_buf_[par];
     const int rows = (int)st_iv_blocks_.size() * kIvFrameBlock;
     if (rows > max_iv_rows_) VAMD_ERR("i-vector frame records overflow");
-    LaunchIvectorCmvn(ia, (int)st_iv_jobs_.size(), stream_);
+    LaunchIvectorCmvn(ia, (int)st_iv_jobs_.size(), fs);
     for (size_t i = 0; i < iv_ops_.size() && rows > 0; i++) {
       NnetOpArgs o = iv_ops_[i];
       o.M = rows;
       o.jobs = (const DevJob*)(dsg + o_ivd);
-      LaunchNnetGemm(o, iv_op_bk_[i], stream_);
+      LaunchNnetGemm(o, iv_op_bk_[i], fs);
     }
-    LaunchIvectorStats(ia, d_iv_ll_, rows, (int)st_iv_jobs_.size(), stream_);
-    launches += 4 + (rows > 0 ? 4 : 0);
+    LaunchIvectorStats(ia, d_iv_ll_, rows, (int)st_iv_jobs_.size(), fs);
+    lf += 4 + (rows > 0 ? 4 : 0);
   }
-  if (tk) HIPCHECK(hipEventRecord(ev_[2], stream_));
-  const int l_front = launches;
-  if (!st_jobs_.empty()) {
-    const DevJob* dj = (const DevJob*)(dsg + o_dj);
-    for (size_t i = 0; i < plan_.ops.size(); i++) {
-      NnetOpArgs a = op_args_[i];
-      a.M = (int)st_jobs_.size() * a.P;
-      a.jobs = dj;
-      a.llh = d_llh_buf_[hf];
-      if (plan_.ops[i].kind == Op::GEMM) LaunchNnetGemm(a, op_bk_[i], stream_);
-      else LaunchNnetGather(a, stream_);
-      launches++;
-    }
-  }
-  if (tk) HIPCHECK(hipEventRecord(ev_[3], stream_));
-  const int l_nnet = launches - l_front;
-  // decoder: this step's batch in order, or the previous one beside the nnet
-  const DecBatch* db = nullptr;
-  hipStream_t dst = stream_;
-  if (!pipe) {
-    if (!cur.jobs.empty()) db = &cur;
-  } else if (pend_active_) {
-    db = &pend_;
-    dst = dstream_;
-    if (tk) HIPCHECK(hipStreamWaitEvent(dstream_, ev_[0], 0));
-  }
-  if (tk) HIPCHECK(hipEventRecord(ev_[5], dst));
-  if (db) LaunchDecodeBatch(*db, dst);
-  if (tk) HIPCHECK(hipEventRecord(ev_[6], dst));
-  if (tk) HIPCHECK(hipEventRecord(ev_[4], stream_));
-  HIPCHECK(hipGetLastError());
-  HIPCHECK(hipStreamSynchronize(stream_));
-  if (pipe) HIPCHECK(hipStreamSynchronize(dstream_));
+  if (tk) HIPCHECK(hipEventRecord(ev_[2], fs));
+  // ---- nnet: this step's (in order) or the previous step's (pipeline)
+  const NnetBatch* nb = pipe ? (pendn_active_ ? &pendn_ : nullptr) : &cur;
   if (tk) {
-    float a = 0, b = 0, c = 0, t = 0, t2 = 0;
+    if (pipe) HIPCHECK(hipStreamWaitEvent(ns, ev_[0], 0));
+    HIPCHECK(hipEventRecord(ev_[3], ns));
+  }
+  if (nb) LaunchNnet(*nb, ns);
+  if (tk) HIPCHECK(hipEventRecord(ev_[4], ns));
+  // ---- decoder: this step's (in order) or the one before the previous (pipeline)
+  const DecBatch* db = pipe ? (pend_active_ ? &pend_ : nullptr) : &cur.dec;
+  if (tk) {
+    if (pipe) HIPCHECK(hipStreamWaitEvent(ds, ev_[0], 0));
+    HIPCHECK(hipEventRecord(ev_[5], ds));
+  }
+  if (db) LaunchDecodeBatch(*db, ds);
+  if (tk) HIPCHECK(hipEventRecord(ev_[6], ds));
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(ns));
+  if (pipe) {
+    HIPCHECK(hipStreamSynchronize(fs));
+    HIPCHECK(hipStreamSynchronize(ds));
+  }
+  if (tk) {
+    float a = 0, b = 0, c = 0, t1 = 0, t2 = 0, t3 = 0;
     HIPCHECK(hipEventElapsedTime(&a, ev_[1], ev_[2]));
-    HIPCHECK(hipEventElapsedTime(&b, ev_[2], ev_[3]));
+    HIPCHECK(hipEventElapsedTime(&b, ev_[3], ev_[4]));
     HIPCHECK(hipEventElapsedTime(&c, ev_[5], ev_[6]));
-    HIPCHECK(hipEventElapsedTime(&t, ev_[0], ev_[4]));
-    HIPCHECK(hipEventElapsedTime(&t2, ev_[0], ev_[6]));
-    times_.ms[0] += a; times_.ms[1] += b; times_.ms[2] += c; times_.ms[3] += std::max(t, t2);
-    times_.launches[0] += l_front;
-    times_.launches[1] += l_nnet;
-    times_.launches[2] += db ? 1 : 0;
+    HIPCHECK(hipEventElapsedTime(&t1, ev_[0], ev_[2]));
+    HIPCHECK(hipEventElapsedTime(&t2, ev_[0], ev_[4]));
+    HIPCHECK(hipEventElapsedTime(&t3, ev_[0], ev_[6]));
+    times_.ms[0] += a; times_.ms[1] += b; times_.ms[2] += c;
+    times_.ms[3] += std::max(t1, std::max(t2, t3));
+    times_.launches[0] += lf;
+    times_.launches[1] += nb && nb->njobs ? (long long)plan_.ops.size() : 0;
+    times_.launches[2] += db && !db->jobs.empty() ? 1 : 0;
     times_.launches[3] += 1;
   }
   counters_.steps++;
-  counters_.launches += launches;
+  counters_.launches += lf;
   counters_.frames_mfcc += st_mfcc_total_;
   counters_.chunk_jobs += st_jobs_.size();
   if (db) FinishDecodeBatch(*db);
   if (cfg_.collect_llh && !st_iv_reqs_.empty()) {
     const int Si = plan_.ivector_dim;
     std::vector<float> rows((size_t)st_jobs_.size() * Si);
-    HIPCHECK(hipMemcpy(rows.data(), d_ivec_, sizeof(float) * rows.size(), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(rows.data(), d_ivec_buf_[par], sizeof(float) * rows.size(), hipMemcpyDeviceToHost));
     for (const IvStreamJob& j : st_iv_jobs_)
       for (int q = 0; q < j.nreq; q++) {
         const IvReq& r = st_iv_reqs_[j.req0 + q];
@@ -1059,10 +1086,12 @@ void Engine::RunStep(bool allow_pipeline) {
         slots_[j.slot].ivecs.insert(slots_[j.slot].ivecs.end(), v, v + Si);
       }
   }
-  half_ ^= 1;
+  seq_++;
   if (pipe) {
-    pend_active_ = !cur.jobs.empty();
-    if (pend_active_) pend_ = std::move(cur);
+    pend_active_ = pendn_active_ && !pendn_.dec.jobs.empty();
+    if (pend_active_) pend_ = std::move(pendn_.dec);
+    pendn_active_ = cur.njobs > 0 || !cur.dec.jobs.empty();
+    if (pendn_active_) pendn_ = std::move(cur);
   }
 }
 
@@ -1077,20 +1106,37 @@ void Engine::Flush() {
   FlushLocked();
 }
 
+// One pipeline-tail pass: the pending nnet beside the pending decoder, or the
+// last decoder alone.
+void Engine::DrainOnce() {
+  if (pendn_active_) {
+    LaunchNnet(pendn_, stream_);
+    if (pend_active_) LaunchDecodeBatch(pend_, dstream_);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(stream_));
+    HIPCHECK(hipStreamSynchronize(dstream_));
+    if (pend_active_) FinishDecodeBatch(pend_);
+    pendn_active_ = false;
+    pend_active_ = !pendn_.dec.jobs.empty();
+    if (pend_active_) pend_ = std::move(pendn_.dec);
+  } else if (pend_active_) {
+    pend_active_ = false;
+    LaunchDecodeBatch(pend_, dstream_);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(dstream_));
+    FinishDecodeBatch(pend_);
+  }
+}
+
 void Engine::FlushLocked() {
-  if (!pend_active_) return;
-  pend_active_ = false;
-  LaunchDecodeBatch(pend_, dstream_);
-  HIPCHECK(hipGetLastError());
-  HIPCHECK(hipStreamSynchronize(dstream_));
-  FinishDecodeBatch(pend_);
+  while (pendn_active_ || pend_active_) DrainOnce();
 }
 
 bool Engine::Step(const std::vector<int>& slots) {
   std::lock_guard<std::mutex> lk(mu_);
   if (!BuildStep(slots)) {
-    if (!pend_active_) return false;
-    FlushLocked();  // pipeline tail: only the pending decoder batch is left
+    if (!pendn_active_ && !pend_active_) return false;
+    DrainOnce();  // pipeline tail: only pending nnet / decoder passes are left
     return true;
   }
   RunStep();
@@ -1175,7 +1221,7 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
   while (first || done < nframes) {
     const int n = std::min(nframes - done, max_dec_frames_);
     if (n > 0)
-      HIPCHECK(hipMemcpyAsync(d_llh_, llh + (size_t)done * P, sizeof(float) * n * P,
+      HIPCHECK(hipMemcpyAsync(d_llh_buf_[seq_ % 2], llh + (size_t)done * P, sizeof(float) * n * P,
                               hipMemcpyHostToDevice, stream_));
     st_samples_.clear();
     st_sample_src_.clear();

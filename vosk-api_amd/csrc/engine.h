@@ -55,10 +55,11 @@ struct EngineConfig {
   bool collect_stats = false;
   bool collect_llh = false;  // tests: keep a host copy of every decoded LLH row
   bool time_kernels = false; // HIP-event timing of each stage on the engine stream
-  // Two-stream pipeline: step i runs samples+MFCC+nnet of step i on the main
-  // stream while the decoder consumes step i-1's log-likelihoods on a second
-  // stream (double-buffered LLH + staging).  Decoder results lag one step;
-  // every call that reads or resets decoder state drains the pipeline first.
+  // Three-stage pipeline over three HIP streams: one engine step runs the
+  // front end (samples, MFCC, i-vectors) of step s, the nnet of step s-1 and
+  // the decoder of step s-2 concurrently (staging triple-buffered, LLH and
+  // per-job i-vectors double-buffered).  Results lag two steps; every call
+  // that reads or resets decoder state drains the pipeline first.
   bool pipeline = false;
 };
 
@@ -171,16 +172,26 @@ class Engine {
     int iv_stats_done = 0;     // frames accumulated into the i-vector statistics
     std::vector<float> ivecs;  // collect_llh: per-chunk i-vectors
   };
-  struct DecBatch {  // one decoder launch's jobs, staged in one staging half
+  struct DecBatch {  // one decoder launch's jobs, staged in one staging buffer
     std::vector<DecJob> jobs;
     std::vector<int> expect;  // decoded-frame count each job's slot must reach
     size_t o_ej = 0;
-    int half = 0;
+    int buf = 0;  // staging buffer of the jobs
+    int llh = 0;  // LLH buffer the nnet wrote
+  };
+  struct NnetBatch {  // one nnet pass: chunk jobs staged in one staging buffer
+    int njobs = 0;
+    size_t o_dj = 0;
+    int buf = 0;
+    int par = 0;  // LLH / i-vector buffer
+    DecBatch dec;
   };
   bool BuildStep(const std::vector<int>& slots);
   void RunStep(bool allow_pipeline = true);
+  void LaunchNnet(const NnetBatch& b, hipStream_t s);
   void LaunchDecodeBatch(const DecBatch& b, hipStream_t s);
   void FinishDecodeBatch(const DecBatch& b);
+  void DrainOnce();  // pipeline tail: the pending nnet and decoder passes
   void FlushLocked();
   int NumFramesFor(long long samples) const;
 
@@ -190,14 +201,16 @@ class Engine {
   std::mutex mu_;
   hipStream_t stream_ = nullptr;
   hipStream_t dstream_ = nullptr;  // decoder stream (pipeline mode)
+  hipStream_t fstream_ = nullptr;  // front-end stream (pipeline mode)
   int ring_ = 0, sample_ring_ = 0, jobs_per_slot_ = 0;
   std::vector<SlotHost> slots_;
   EngineCounters counters_;
   StageTimes times_;
   hipEvent_t ev_[7] = {};
-  int half_ = 0;            // staging + LLH half of the step being built
-  bool pend_active_ = false;
-  DecBatch pend_;           // pipeline mode: decoder batch waiting for the next step
+  long long seq_ = 0;       // steps run: staging buffer seq % 3, LLH / i-vector buffer seq % 2
+  bool pendn_active_ = false, pend_active_ = false;
+  NnetBatch pendn_;         // pipeline mode: front end done, nnet waiting
+  DecBatch pend_;           // pipeline mode: nnet done, decoder waiting
 
   // device: model
   MfccDev mfcc_{};
@@ -245,7 +258,7 @@ class Engine {
   // i-vector extraction (nnet with a per-chunk i-vector input)
   bool use_iv_ = false;
   IvArgs iv_{};
-  float* d_ivec_ = nullptr;  // [max jobs][ivector dim], row per chunk job of a step
+  float* d_ivec_buf_[2] = {nullptr, nullptr};  // [max jobs][ivector dim] per chunk job of a step
   float* d_iv_ll_ = nullptr; // [GEMM rows][num_gauss] UBM log-likelihoods
   std::vector<NnetOpArgs> iv_ops_;  // LDA (normalized -> [x | x*x]), LDA (raw), UBM
   std::vector<int> iv_op_bk_;
