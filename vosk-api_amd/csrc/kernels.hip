@@ -913,18 +913,18 @@ struct IvAccShared {
   int sel[kIvAccChunk][5];
   int ns[kIvAccChunk];
   float xr[kIvAccChunk][kIvMaxD];
-  double proj[kIvAccFrames][5][(kIvMaxS + 7) / 8];
+  double proj[kIvAccFrames][5][(kIvMaxS + 3) / 4];
 };
 
-template <int NQP>  // packed quad entries per thread: ceil(ceil(QS / 8) / 256)
+template <int NQP, int NP>  // NP parts; packed quad entries per thread: ceil(ceil(QS / NP) / 256)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ivector_acc_kernel(IvArgs a) {
   __shared__ IvAccShared sh;
-  const int part = blockIdx.x & 7, jb = blockIdx.x >> 3, tid = threadIdx.x;
+  const int part = blockIdx.x % NP, jb = blockIdx.x / NP, tid = threadIdx.x;
   const IvStreamJob J = a.jobs[jb];
   const IvectorDev& m = a.m;
   const int S = m.ivec_dim, DL = m.lda_dim, QS = S * (S + 1) / 2, NE = QS + S;
-  const int qchunk = (QS + 7) / 8, q0 = part * qchunk, q1 = min(QS, q0 + qchunk);
-  const int cw = (S + 7) / 8, c0 = min(S, part * cw), ncol = min(S, c0 + cw) - c0;  // columns [c0, c0+ncol)
+  const int qchunk = (QS + NP - 1) / NP, q0 = part * qchunk, q1 = min(QS, q0 + qchunk);
+  const int cw = (S + NP - 1) / NP, c0 = min(S, part * cw), ncol = min(S, c0 + cw) - c0;  // columns [c0, c0+ncol)
   IvState* st = a.state + J.slot;
   double* quad = a.quad + (size_t)J.slot * QS;
   const double po = m.prior_offset;
@@ -1152,10 +1152,20 @@ void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, h
   if (njobs <= 0) return;
   if (rows > 0) hipLaunchKernelGGL(ivector_top_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, a, ll, rows);
   hipLaunchKernelGGL(ivector_nfr_kernel, dim3((njobs + 63) / 64), dim3(64), 0, s, a, njobs);
-  const int S = a.m.ivec_dim, nqp = ((S * (S + 1) / 2 + 7) / 8 + 255) / 256;
-  if (nqp <= 1) hipLaunchKernelGGL(ivector_acc_kernel<1>, dim3(njobs * 8), dim3(256), 0, s, a);
-  else if (nqp == 2) hipLaunchKernelGGL(ivector_acc_kernel<2>, dim3(njobs * 8), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(ivector_acc_kernel<3>, dim3(njobs * 8), dim3(256), 0, s, a);
+  // parts: blocks b and b + 8 share an XCD, so part = b % NP keeps each XCD's
+  // L2 on 1/NP of U and SigmaInvM
+  static const int np = getenv("VOSK_AMD_IV_PARTS") ? atoi(getenv("VOSK_AMD_IV_PARTS")) : 4;
+  const int S = a.m.ivec_dim, QS = S * (S + 1) / 2;
+  if (np == 8) {
+    const int nqp = ((QS + 7) / 8 + 255) / 256;
+    if (nqp <= 1) hipLaunchKernelGGL((ivector_acc_kernel<1, 8>), dim3(njobs * 8), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((ivector_acc_kernel<3, 8>), dim3(njobs * 8), dim3(256), 0, s, a);
+  } else {
+    const int nqp = ((QS + 3) / 4 + 255) / 256;
+    if (nqp <= 1) hipLaunchKernelGGL((ivector_acc_kernel<1, 4>), dim3(njobs * 4), dim3(256), 0, s, a);
+    else if (nqp <= 3) hipLaunchKernelGGL((ivector_acc_kernel<3, 4>), dim3(njobs * 4), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((ivector_acc_kernel<5, 4>), dim3(njobs * 4), dim3(256), 0, s, a);
+  }
   hipLaunchKernelGGL(ivector_cg_kernel, dim3(njobs), dim3(128), 0, s, a);
 }
 
