@@ -66,6 +66,37 @@ float orc_expf(float x) {
   return ldexpf(p, (int)k);
 }
 
+/* ---- online CMVN (Kaldi feat/online-feature.cc OnlineCmvn::GetFrame with
+   global stats only: ComputeStatsForFrame's running window sums, then
+   SmoothOnlineCmvnStats and ApplyCmvn without variance normalization) ---- */
+void orc_online_cmvn(const double* gstats, int D, int window, int global_frames,
+                     const float* feats, int T, float* out) {
+  double sum[256] = {0}, n = 0.0;
+  const double gcount = gstats[D];
+  for (int t = 0; t < T; t++) {
+    for (int d = 0; d < D; d++) sum[d] = sum[d] + (double)feats[(size_t)t * D + d];
+    n = n + 1.0;
+    if (t - window >= 0) {
+      for (int d = 0; d < D; d++) sum[d] = sum[d] - (double)feats[(size_t)(t - window) * D + d];
+      n = n - 1.0;
+    }
+    double st[256], cnt = n;
+    for (int d = 0; d < D; d++) st[d] = sum[d];
+    if (cnt < window) {
+      double cg = window - cnt;
+      if (cg > global_frames) cg = global_frames;
+      const double sc = cg / gcount;
+      for (int d = 0; d < D; d++) st[d] = st[d] + sc * gstats[d];
+      cnt = cnt + sc * gcount;
+    }
+    const float alpha = (float)(-1.0 / cnt);
+    for (int d = 0; d < D; d++) {
+      const float off = (float)((double)alpha * st[d]);
+      out[(size_t)t * D + d] = feats[(size_t)t * D + d] + off;
+    }
+  }
+}
+
 /* ---- online i-vector extraction ----------------------------------------- */
 /* one row of an affine map in the canonical order (see the nnet affine
    case in orc_nnet_forward): fmaf chains from 0 over orc_kslices(K) slices,
@@ -176,32 +207,7 @@ int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, c
   }
   /* online CMVN (window cmn_window, smoothed with global_frames of global stats) */
   float* norm = (float*)malloc(sizeof(float) * (size_t)(T > 0 ? T : 1) * D);
-  {
-    double sum[64] = {0}, n = 0.0;
-    const double gcount = m->cmvn[D];
-    for (int t = 0; t < T; t++) {
-      for (int d = 0; d < D; d++) sum[d] = sum[d] + (double)feats[(size_t)t * D + d];
-      n = n + 1.0;
-      if (t - m->cmn_window >= 0) {
-        for (int d = 0; d < D; d++) sum[d] = sum[d] - (double)feats[(size_t)(t - m->cmn_window) * D + d];
-        n = n - 1.0;
-      }
-      double st[64], cnt = n;
-      for (int d = 0; d < D; d++) st[d] = sum[d];
-      if (cnt < m->cmn_window) {
-        double cg = m->cmn_window - cnt;
-        if (cg > m->global_frames) cg = m->global_frames;
-        const double sc = cg / gcount;
-        for (int d = 0; d < D; d++) st[d] = st[d] + sc * m->cmvn[d];
-        cnt = cnt + sc * gcount;
-      }
-      const float alpha = (float)(-1.0 / cnt);
-      for (int d = 0; d < D; d++) {
-        const float off = (float)((double)alpha * st[d]);
-        norm[(size_t)t * D + d] = feats[(size_t)t * D + d] + off;
-      }
-    }
-  }
+  orc_online_cmvn(m->cmvn, D, m->cmn_window, m->global_frames, feats, T, norm);
   double lin[128] = {0}, cur[128] = {0};
   double* quad = (double*)calloc(QS, sizeof(double));
   lin[0] = m->prior_offset;
@@ -363,6 +369,10 @@ float orc_logf(float x) {
 
 static float mel_scale(float f) { return 1127.0f * logf(1.0f + f / 700.0f); }
 
+int orc_feat_dim(const orc_mfcc_opts* o) {
+  return o->fbank ? o->num_bins + (o->use_energy ? 1 : 0) : o->num_ceps;
+}
+
 int orc_mfcc(const orc_mfcc_opts* o, const float* wave, long n, float* out) {
   const int L = frame_length(o), S = frame_shift(o), N = padded_length(o);
   const int nf = orc_mfcc_num_frames(o, n);
@@ -483,10 +493,22 @@ int orc_mfcc(const orc_mfcc_opts* o, const float* wave, long n, float* out) {
       if (first[b] >= 0)
         for (int i = first[b]; i <= last[b]; i++) {
           float p = re[i] * re[i] + im[i] * im[i];
+          if (o->fbank && !o->use_power) p = sqrtf(p);
           e = fmaf(melw[(size_t)b * nfft + i], p, e);
         }
+      if (o->fbank && !o->use_log_fbank) {
+        mel[b] = e;
+        continue;
+      }
       if (e < 1.1920929e-07f) e = 1.1920929e-07f;
       mel[b] = orc_logf(e);
+    }
+    if (o->fbank) {  /* FbankComputer::Compute: [log energy,] log mel energies */
+      const int off = o->use_energy ? 1 : 0;
+      float* o_row = out + (size_t)f * (nb + off);
+      for (int b = 0; b < nb; b++) o_row[off + b] = mel[b];
+      if (o->use_energy) o_row[0] = log_energy;
+      continue;
     }
     float* o_row = out + (size_t)f * nc;
     for (int k = 0; k < nc; k++) {

@@ -31,7 +31,20 @@ typedef struct {
   int num_bins, num_ceps, use_energy, remove_dc_offset;
   int window_type; /* 0 povey, 1 hamming, 2 hanning, 3 rectangular, 4 blackman */
   int round_to_power_of_two;
+  /* fbank front end (Kaldi feat/feature-fbank.cc, src/model.cc:222-225):
+     log mel energies, log energy first when use_energy */
+  int fbank, use_log_fbank, use_power;
 } orc_mfcc_opts;
+
+/* feature dimension of the front end: num_ceps (MFCC) or num_bins (+1) (fbank) */
+int orc_feat_dim(const orc_mfcc_opts* o);
+/* Kaldi OnlineCmvn with global stats only (mean normalization; the running
+   window sums in double, SmoothOnlineCmvnStats, ApplyCmvn), as the
+   reference's feature pipeline applies it with am/global_cmvn.stats
+   (src/model.cc:265-269) and as the i-vector extractor's CMVN does.
+   gstats: [2][D+1] (row 0 sums and count).  out may equal nothing of feats. */
+void orc_online_cmvn(const double* gstats, int D, int window, int global_frames,
+                     const float* feats, int T, float* out);
 
 /* Windowed-sinc resampling (Kaldi feat/resample.cc LinearResample, as the
    reference uses it: src/batch_recognizer.cc:27-29, filter cutoff
@@ -43,7 +56,7 @@ long orc_resample_num_outputs(int rate_in, int rate_out, long n);
 long orc_resample(int rate_in, int rate_out, const float* x, long n, float* out, long cap);
 
 int orc_mfcc_num_frames(const orc_mfcc_opts* o, long num_samples);
-/* wave: float samples (int16 range).  out: [frames][num_ceps]. returns frames */
+/* wave: float samples (int16 range).  out: [frames][orc_feat_dim]. returns frames */
 int orc_mfcc(const orc_mfcc_opts* o, const float* wave, long num_samples, float* out);
 int orc_kslices(int K);
 float orc_logf(float x);

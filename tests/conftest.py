@@ -96,3 +96,13 @@ def has_gpu():
         return engine.device_count() > 0
     except Exception:
         return False
+
+
+@pytest.fixture(scope="session", params=[("fbank", True), ("mfcc", True)],
+                ids=["fbank_cmvn", "mfcc_cmvn"])
+def synth_model_frontend(request):
+    """Small models with the other front ends of src/model.cc:218-269: a log
+    fbank front end and/or global CMVN on the nnet input (am/global_cmvn.stats)."""
+    fe, cmvn = request.param
+    return _make(f"synth_{fe}{'_cmvn' if cmvn else ''}", seed=5, vocab=500, num_pdfs=300,
+                 frontend=fe, global_cmvn=cmvn)

@@ -29,6 +29,10 @@ def load_lib():
     lib = C.CDLL(LIB_PATH)
     lib.orc_mfcc.restype = C.c_int
     lib.orc_mfcc_num_frames.restype = C.c_int
+    lib.orc_feat_dim.restype = C.c_int
+    lib.orc_online_cmvn.restype = None
+    lib.orc_online_cmvn.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                    C.c_void_p]
     lib.orc_logf.restype = C.c_float
     lib.orc_logf.argtypes = [C.c_float]
     lib.orc_nnet_forward.restype = C.c_int
@@ -72,23 +76,36 @@ class OrcMfccOpts(C.Structure):
                 ("cepstral_lifter", C.c_float), ("blackman_coeff", C.c_float),
                 ("num_bins", C.c_int), ("num_ceps", C.c_int), ("use_energy", C.c_int),
                 ("remove_dc_offset", C.c_int), ("window_type", C.c_int),
-                ("round_to_power_of_two", C.c_int)]
+                ("round_to_power_of_two", C.c_int), ("fbank", C.c_int),
+                ("use_log_fbank", C.c_int), ("use_power", C.c_int)]
 
 
-def mfcc_opts(conf: dict) -> OrcMfccOpts:
-    o = nk.MfccOpts(conf)
+def mfcc_opts(conf: dict, fbank: bool = False) -> OrcMfccOpts:
+    o = nk.MfccOpts(conf, fbank)
     wt = {"povey": 0, "hamming": 1, "hanning": 2, "rectangular": 3, "blackman": 4}[o.window_type]
     return OrcMfccOpts(o.samp_freq, o.frame_shift_ms, o.frame_length_ms, o.preemph,
                        o.low_freq, o.high_freq, o.cepstral_lifter, o.blackman_coeff,
                        o.num_bins, o.num_ceps, int(o.use_energy), int(o.remove_dc), wt,
-                       int(o.round_pow2))
+                       int(o.round_pow2), int(fbank), int(o.use_log_fbank), int(o.use_power))
 
 
-def mfcc(wave, conf: dict) -> np.ndarray:
-    o = mfcc_opts(conf)
+def online_cmvn(feats, gstats, window=600, global_frames=200) -> np.ndarray:
+    """C oracle's Kaldi OnlineCmvn (global stats, mean normalization)."""
+    f = np.ascontiguousarray(feats, np.float32)
+    g = np.ascontiguousarray(gstats, np.float64)
+    out = np.zeros_like(f)
+    if f.shape[0]:
+        lib().orc_online_cmvn(g.ctypes.data, f.shape[1], window, global_frames, f.ctypes.data,
+                              f.shape[0], out.ctypes.data)
+    return out
+
+
+def mfcc(wave, conf: dict, fbank: bool = False) -> np.ndarray:
+    """The model's front end: MFCC, or log fbank with fbank=True."""
+    o = mfcc_opts(conf, fbank)
     w = np.ascontiguousarray(wave, np.float32)
     n = lib().orc_mfcc_num_frames(C.byref(o), C.c_long(len(w)))
-    out = np.zeros((max(n, 0), o.num_ceps), np.float32)
+    out = np.zeros((max(n, 0), lib().orc_feat_dim(C.byref(o))), np.float32)
     if n > 0:
         lib().orc_mfcc(C.byref(o), w.ctypes.data_as(C.c_void_p), C.c_long(len(w)),
                        out.ctypes.data_as(C.c_void_p))
@@ -466,7 +483,14 @@ class OracleModel:
 
     def __init__(self, model_dir: str, fpc=None):
         self.dir = model_dir
-        self.mfcc_conf = kf.parse_conf(os.path.join(model_dir, "conf", "mfcc.conf"))
+        # front end (src/model.cc:218-228): mfcc.conf, else fbank.conf;
+        # am/global_cmvn.stats adds online CMVN on the nnet input (:265-269)
+        mconf = os.path.join(model_dir, "conf", "mfcc.conf")
+        self.fbank = not os.path.exists(mconf)
+        self.mfcc_conf = kf.parse_conf(mconf if not self.fbank else
+                                       os.path.join(model_dir, "conf", "fbank.conf"))
+        cpath = os.path.join(model_dir, "am", "global_cmvn.stats")
+        self.global_cmvn = kf.read_matrix_file(cpath) if os.path.exists(cpath) else None
         self.model_conf = kf.parse_conf(os.path.join(model_dir, "conf", "model.conf"))
         self.tm, self.nn = kf.read_final_mdl(os.path.join(model_dir, "am", "final.mdl"))
         self.fst = kf.read_fst(os.path.join(model_dir, "graph", "HCLG.fst"))
@@ -523,15 +547,21 @@ class OracleModel:
         return np.minimum(c, max(nch - 1, 0)).astype(np.int32), t0
 
     def features(self, wave):
-        return mfcc(wave, self.mfcc_conf)
+        """Raw front-end features (the i-vector extractor's input)."""
+        return mfcc(wave, self.mfcc_conf, self.fbank)
+
+    def nnet_features(self, feats):
+        """The nnet's input: the features, CMVN-normalized with global stats."""
+        return feats if self.global_cmvn is None else online_cmvn(feats, self.global_cmvn)
 
     def loglikes(self, wave):
         return self.loglikes_feats(self.features(wave))
 
-    def loglikes_feats(self, feats):
+    def loglikes_feats(self, raw):
+        feats = self.nnet_features(raw)
         if self.ivector is None or feats.shape[0] == 0:
             return self.net.forward(feats)
-        iv = self.ivectors(feats)
+        iv = self.ivectors(raw)
         ivt, t0 = self._ivec_of_time(feats.shape[0], len(iv))
         return self.net.forward(feats, iv, ivt, t0)
 

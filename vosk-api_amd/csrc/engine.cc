@@ -35,7 +35,7 @@ float MelScale(float f) { return 1127.0f * logf(1.0f + f / 700.0f); }
 // ---------------------------------------------------------------------------
 void ModelData::Load(const std::string& path) {
   dir = path;
-  std::string mdl, hclg, words_txt, wb, mfcc_conf, conf_file;
+  std::string mdl, hclg, words_txt, wb, mfcc_conf, fbank_conf, cmvn_stats, pitch_conf, conf_file;
   if (FileExists(path + "/am/final.mdl") && FileExists(path + "/conf/model.conf")) {
     // V2 layout (src/model.cc:180-207)
     ApplyModelOptions(ReadConfigFile(path + "/conf/model.conf"), &dec, &dcb, &endpoint);
@@ -44,6 +44,9 @@ void ModelData::Load(const std::string& path) {
     words_txt = path + "/graph/words.txt";
     wb = path + "/graph/phones/word_boundary.int";
     mfcc_conf = path + "/conf/mfcc.conf";
+    fbank_conf = path + "/conf/fbank.conf";
+    cmvn_stats = path + "/am/global_cmvn.stats";
+    pitch_conf = path + "/conf/pitch.conf";
   } else if (FileExists(path + "/final.mdl") && FileExists(path + "/mfcc.conf")) {
     // V1 layout: hard-coded options (src/model.cc:132-158)
     std::map<std::string, std::string> kv = {
@@ -59,26 +62,45 @@ void ModelData::Load(const std::string& path) {
     words_txt = path + "/words.txt";
     wb = path + "/word_boundary.int";
     mfcc_conf = path + "/mfcc.conf";
+    fbank_conf = path + "/fbank.conf";
+    cmvn_stats = path + "/global_cmvn.stats";
+    pitch_conf = path + "/pitch.conf";
   } else {
     VAMD_ERR("Folder '" << path << "' does not contain model files. Make sure you specified "
                            "the model path properly in Model constructor.");
   }
   VAMD_LOG("Decoding params beam=" << dec.beam << " max-active=" << dec.max_active
                                    << " lattice-beam=" << dec.lattice_beam);
-  if (!FileExists(mfcc_conf)) VAMD_ERR("Failed to find feature config file (only MFCC front-ends are supported)");
-  mfcc.Apply(ReadConfigFile(mfcc_conf));
+  // front end (src/model.cc:218-228): mfcc.conf, else fbank.conf
+  if (FileExists(mfcc_conf)) {
+    mfcc.Apply(ReadConfigFile(mfcc_conf));
+  } else if (FileExists(fbank_conf)) {
+    mfcc.SetFbankDefaults();
+    mfcc.Apply(ReadConfigFile(fbank_conf));
+  } else {
+    VAMD_ERR("Failed to find feature config file");
+  }
   mfcc.allow_downsample = true;
   ReadFinalMdl(mdl, &tm, &nnet);
   if (FileExists(path + "/ivector/final.ie")) {
     VAMD_LOG("Loading i-vector extractor from " << path << "/ivector/final.ie");
     ReadIvectorModel(path + "/ivector", &ivec);
     use_ivector = true;
-    if (ivec.feat_dim != mfcc.num_ceps)
-      VAMD_ERR("i-vector extractor expects " << ivec.feat_dim << "-dim features, MFCC gives "
-                                             << mfcc.num_ceps);
+    if (ivec.feat_dim != mfcc.FeatDim())
+      VAMD_ERR("i-vector extractor expects " << ivec.feat_dim << "-dim features, the front end gives "
+                                             << mfcc.FeatDim());
   }
-  if (FileExists(path + "/am/global_cmvn.stats") || FileExists(path + "/conf/pitch.conf"))
-    VAMD_ERR("global CMVN / pitch front-ends are not supported yet");
+  if (FileExists(cmvn_stats)) {
+    VAMD_LOG("Reading CMVN stats from " << cmvn_stats);
+    int rows = 0, cols = 0;
+    global_cmvn = ReadKaldiMatrixFile(cmvn_stats, &rows, &cols);
+    if (rows != 2 || cols != mfcc.FeatDim() + 1)
+      VAMD_ERR("global_cmvn.stats must be 2 x " << mfcc.FeatDim() + 1);
+    if (!(global_cmvn[cols - 1] > 0.0)) VAMD_ERR("global_cmvn.stats has no frames");
+    use_cmvn = true;
+  }
+  if (FileExists(pitch_conf))
+    VAMD_ERR("pitch front-ends (" << pitch_conf << ") are not supported yet");
   if (!FileExists(hclg))
     VAMD_ERR("no static " << hclg << " (lookahead HCLr.fst+Gr.fst graphs need the host expansion "
                                      "of SURVEY.md 8f-2, not implemented yet)");
@@ -156,8 +178,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   const int L = o.WindowSize(), N = o.PaddedWindowSize();
   if (N > 512 || (N & (N - 1))) VAMD_ERR("FFT size " << N << " unsupported (power of two <= 512)");
   if (o.num_bins > 64 || o.num_ceps > 64) VAMD_ERR("num-mel-bins / num-ceps must be <= 64");
-  if (plan_.input_dim != o.num_ceps)
-    VAMD_ERR("nnet input dim " << plan_.input_dim << " != num-ceps " << o.num_ceps);
+  if (plan_.input_dim != o.FeatDim())
+    VAMD_ERR("nnet input dim " << plan_.input_dim << " != feature dim " << o.FeatDim());
   {
     std::vector<float> win(L);
     double a = 2.0 * M_PI / (L - 1);
@@ -228,6 +250,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     mfcc_.lifter = Upload(lift);
     mfcc_.twr = Upload(twr);
     mfcc_.twi = Upload(twi);
+    mfcc_.fbank = o.fbank ? 1 : 0;
+    mfcc_.use_log_fbank = o.use_log_fbank ? 1 : 0;
+    mfcc_.use_power = o.use_power ? 1 : 0;
+    mfcc_.feat_dim = o.FeatDim();
   }
 
   // ---- rings
@@ -255,6 +281,20 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   rings_.ring = ring_;
   rings_.slots = S;
   rings_.input_node = plan_.input_node;
+  // features: MFCC/fbank straight into the nnet input ring, or (global CMVN)
+  // into a raw ring that the CMVN kernel normalizes into the input ring
+  const int FD = o.FeatDim();
+  float* feat_src = ring_ptrs[plan_.input_node];
+  if (m.use_cmvn) {
+    feat_src = (float*)DevAlloc(sizeof(float) * (size_t)S * ring_ * FD);
+    HIPCHECK(hipMemset(feat_src, 0, sizeof(float) * (size_t)S * ring_ * FD));
+    if (FD > kCmvnMaxD) VAMD_ERR("CMVN feature dim must be <= " << kCmvnMaxD);
+    ncmvn_ = CmvnDev{FD, 600, 200, 0, Upload(m.global_cmvn),
+                     (double*)DevAlloc(sizeof(double) * (size_t)S * FD),
+                     (float*)DevAlloc(sizeof(float) * (size_t)S * kCmvnHist * FD),
+                     feat_src, ring_ptrs[plan_.input_node], ring_ - 1, S};
+  }
+  mfcc_.out = feat_src;
   d_samples_ = (float*)DevAlloc(sizeof(float) * (size_t)S * sample_ring_);
   // raw input ring for resampled streams: up to 6x the model rate per step
   raw_ring_ = Pow2AtLeast((long long)cfg_.max_step_samples * 6 + 8192);
@@ -273,7 +313,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     if (iv.feat_dim != plan_.input_dim) VAMD_ERR("i-vector feature dim != nnet input dim");
     if (Si > kIvMaxS || QS > kIvMaxQ || iv.feat_dim > kIvMaxD || iv.lda_dim > kIvMaxD ||
         (iv.left + iv.right + 1) * iv.feat_dim > kIvMaxK || iv.num_gauss > kIvMaxG ||
-        iv.num_gselect > 5 || iv.num_gselect < 1 || iv.cmn_window >= kIvHist || iv.cmn_window < 16 ||
+        iv.num_gselect > 5 || iv.num_gselect < 1 || iv.cmn_window >= kCmvnHist || iv.cmn_window < 16 ||
         iv.left < 0 || iv.right < 0)
       VAMD_ERR("i-vector extractor dimensions exceed the kernel limits");
     IvectorDev& d = iv_.m;
@@ -293,13 +333,17 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     HIPCHECK(hipMemset(iv_.state, 0, sizeof(IvState) * S));
     iv_.quad = (double*)DevAlloc(sizeof(double) * (size_t)S * QS);
     iv_.qfull = (double*)DevAlloc(sizeof(double) * (size_t)S * Si * Si);
-    iv_.hist = (float*)DevAlloc(sizeof(float) * (size_t)S * kIvHist * D);
+    if (D > kCmvnMaxD) VAMD_ERR("i-vector feature dim must be <= " << kCmvnMaxD);
     // CMVN-normalized features and the UBM input [x | x*x] live in rings laid
     // out like the activation rings, so the nnet GEMM kernels read them with
     // the splice as input segments (clamped like the feature input)
     iv_.norm = (float*)DevAlloc(sizeof(float) * (size_t)S * ring_ * D);
     float* ivx = (float*)DevAlloc(sizeof(float) * (size_t)S * ring_ * 2 * DL);
-    iv_.in_base = ring_ptrs[plan_.input_node];
+    iv_.in_base = feat_src;  // the raw front-end features (before any global CMVN)
+    ivcmvn_ = CmvnDev{D, iv.cmn_window, iv.global_frames, 0, Upload(iv.cmvn),
+                      (double*)DevAlloc(sizeof(double) * (size_t)S * D),
+                      (float*)DevAlloc(sizeof(float) * (size_t)S * kCmvnHist * D),
+                      feat_src, iv_.norm, ring_ - 1, S};
     iv_.in_mask = ring_ - 1;
     iv_.slots = S;
     // frame records of one step: per stream at most the chunks' new frames
@@ -559,6 +603,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
                  Align256(sizeof(MfccJob) * S) +
                  Align256(sizeof(DevJob) * max_jobs_) + Align256(sizeof(DecJob) * S) +
                  Align256(sizeof(IvStreamJob) * S) + Align256(sizeof(IvReq) * max_jobs_) +
+                 2 * Align256(sizeof(CmvnJob) * S) +
                  2 * Align256(sizeof(IvFrameBlock) * ((size_t)max_iv_frames_ / kIvFrameBlock + 2 * S)) + 1024;
   // three buffers: the pipelined nnet and decoder passes keep their jobs
   // while the next step stages
@@ -630,6 +675,7 @@ void Engine::ResetPipeline(int slot) {
   h.raw_pushed = 0;
   h.res_flushed = false;
   h.iv_reset = true;
+  h.cmvn_reset = true;
   h.iv_norm_done = h.iv_norm_to = h.iv_stats_done = 0;
 }
 
@@ -730,6 +776,8 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
   st_iv_reqs_.clear();
   st_iv_blocks_.clear();
   st_iv_devjobs_.clear();
+  st_ncmvn_.clear();
+  st_ivcmvn_.clear();
   st_iv_frames_ = 0;
   const int fpc = plan_.fpc, opc = plan_.opc, fss = plan_.fss, R = plan_.right_context;
   int stats_rows = 0;
@@ -811,6 +859,10 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
     int nf_total = NumFramesFor(h.samples);
     if (nf_total > h.frames) {
       st_mfcc_.push_back(MfccJob{s, h.frames, nf_total - h.frames, st_mfcc_total_});
+      if (md_->use_cmvn) {
+        st_ncmvn_.push_back(CmvnJob{s, h.frames, nf_total, h.cmvn_reset ? 1 : 0});
+        h.cmvn_reset = false;
+      }
       st_mfcc_total_ += nf_total - h.frames;
       h.frames = nf_total;
       any = true;
@@ -866,7 +918,8 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
     }
     if ((int)st_iv_reqs_.size() > req0) {
       st_iv_jobs_.push_back(IvStreamJob{s, req0, (int)st_iv_reqs_.size() - req0, h.iv_reset ? 1 : 0, T,
-                                        h.iv_norm_done, h.iv_norm_to, 0});
+                                        0, 0, 0});
+      st_ivcmvn_.push_back(CmvnJob{s, h.iv_norm_done, h.iv_norm_to, h.iv_reset ? 1 : 0});
       h.iv_norm_done = h.iv_norm_to;
       h.iv_reset = false;
     }
@@ -990,6 +1043,8 @@ void Engine::RunStep(bool allow_pipeline) {
   size_t o_ivr = put(st_iv_reqs_.data(), sizeof(IvReq) * st_iv_reqs_.size());
   size_t o_ivb = put(st_iv_blocks_.data(), sizeof(IvFrameBlock) * st_iv_blocks_.size());
   size_t o_ivd = put(st_iv_devjobs_.data(), sizeof(DevJob) * st_iv_devjobs_.size());
+  size_t o_ncm = put(st_ncmvn_.data(), sizeof(CmvnJob) * st_ncmvn_.size());
+  size_t o_icm = put(st_ivcmvn_.data(), sizeof(CmvnJob) * st_ivcmvn_.size());
   cur.dec.jobs = st_dec_;
   cur.dec.o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
   cur.dec.buf = buf;
@@ -1014,6 +1069,10 @@ void Engine::RunStep(bool allow_pipeline) {
   LaunchMfcc(mfcc_, (const MfccJob*)(dsg + o_mj), (int)st_mfcc_.size(), st_mfcc_total_, d_samples_,
              sample_ring_, rings_, fs);
   lf += st_mfcc_total_ > 0;
+  if (!st_ncmvn_.empty()) {
+    LaunchCmvn(ncmvn_, (const CmvnJob*)(dsg + o_ncm), (int)st_ncmvn_.size(), fs);
+    lf++;
+  }
   if (!st_iv_jobs_.empty()) {
     IvArgs ia = iv_;
     ia.jobs = (const IvStreamJob*)(dsg + o_ivj);
@@ -1022,7 +1081,7 @@ void Engine::RunStep(bool allow_pipeline) {
     ia.ivec = d_ivec_buf_[par];
     const int rows = (int)st_iv_blocks_.size() * kIvFrameBlock;
     if (rows > max_iv_rows_) VAMD_ERR("i-vector frame records overflow");
-    LaunchIvectorCmvn(ia, (int)st_iv_jobs_.size(), fs);
+    LaunchCmvn(ivcmvn_, (const CmvnJob*)(dsg + o_icm), (int)st_ivcmvn_.size(), fs);
     for (size_t i = 0; i < iv_ops_.size() && rows > 0; i++) {
       NnetOpArgs o = iv_ops_[i];
       o.M = rows;
@@ -1237,6 +1296,8 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     st_iv_reqs_.clear();
     st_iv_blocks_.clear();
     st_iv_devjobs_.clear();
+    st_ncmvn_.clear();
+    st_ivcmvn_.clear();
     st_iv_frames_ = 0;
     h.stats.clear();
     const bool rs = first && (reset || h.need_reset);

@@ -40,6 +40,10 @@ struct ModelData {
   bool has_word_boundary = false;
   bool use_ivector = false;            // ivector/final.ie present (src/model.cc:247)
   IvectorModel ivec;
+  // global_cmvn.stats present (src/model.cc:265-269): online CMVN (window 600,
+  // 200 global frames, mean only) on the nnet input features
+  bool use_cmvn = false;
+  std::vector<double> global_cmvn;     // [2][feat_dim + 1]
   // Loads a V2 (am/, conf/, graph/) or V1 (flat) layout (src/model.cc:106-128).
   void Load(const std::string& dir);
   void LoadBatchLayout(const std::string& dir);  // src/batch_model.cc:23-54
@@ -168,6 +172,7 @@ class Engine {
     long long raw_pushed = 0;  // raw (input-rate) samples pushed to the raw ring
     bool res_flushed = false;  // resampler flushed at end of input
     bool iv_reset = true;      // i-vector state restarts at the next request
+    bool cmvn_reset = true;    // nnet-input CMVN restarts at the next frames
     int iv_norm_done = 0, iv_norm_to = 0;  // frames CMVN-normalized (after this step)
     int iv_stats_done = 0;     // frames accumulated into the i-vector statistics
     std::vector<float> ivecs;  // collect_llh: per-chunk i-vectors
@@ -254,6 +259,8 @@ class Engine {
   std::vector<IvReq> st_iv_reqs_;
   std::vector<IvFrameBlock> st_iv_blocks_;
   std::vector<DevJob> st_iv_devjobs_;  // GEMM rows of the blocks
+  std::vector<CmvnJob> st_ncmvn_, st_ivcmvn_;  // nnet-input / i-vector CMVN
+  CmvnDev ncmvn_{}, ivcmvn_{};
   int st_iv_frames_ = 0, max_iv_frames_ = 0;
   // i-vector extraction (nnet with a per-chunk i-vector input)
   bool use_iv_ = false;

@@ -67,7 +67,25 @@ struct MfccDev {
   const float* lifter;   // [num_ceps]
   const float* twr;      // [padded/2]
   const float* twi;      // [padded/2]
+  int fbank, use_log_fbank, use_power, feat_dim;
+  float* out;            // feature ring [ring][slots][feat_dim]
 };
+
+// online CMVN (Kaldi OnlineCmvn, global stats, mean only): running window
+// sums per stream, sequential in time; in/out rings [ring][slots][D]
+struct CmvnDev {
+  int D, window, global_frames, pad;
+  const double* gstats;  // [2][D + 1]
+  double* sums;          // [slots][D] window sums (persistent)
+  float* hist;           // [slots][kCmvnHist][D] raw frames (the window's tail)
+  const float* in_base;
+  float* out_base;
+  int mask, slots;
+};
+struct CmvnJob {  // normalize frames [from, to) of a stream
+  int slot, from, to, reset;
+};
+constexpr int kCmvnHist = 1024, kCmvnMaxD = 128;
 
 struct MfccJob {  // frames [first, first+count) of one slot; rows [row0, row0+count)
   int slot, first, count, row0;
@@ -107,7 +125,6 @@ struct DecSlot {
 
 // ---- online i-vector extraction (kernels.hip ivector_kernel)
 constexpr int kIvMaxS = 100, kIvMaxD = 64, kIvMaxK = 320, kIvMaxG = 512, kIvMaxQ = 20 * 256;
-constexpr int kIvHist = 1024;
 constexpr int kIvFrameBlock = 8;  // frames per ivector_frame_kernel workgroup
 struct IvectorDev {
   int feat_dim, left, right, lda_dim, lda_cols, num_gauss, ivec_dim, cmn_window;
@@ -119,7 +136,6 @@ struct IvectorDev {
   const double* U;             // [G][S(S+1)/2]
 };
 struct IvState {  // per stream, persistent across steps (reset with the pipeline)
-  double sum[kIvMaxD];  // CMVN window sums
   double nfr;           // posterior-weighted frame count
   double lin[kIvMaxS];  // linear term (incl. prior)
   double cur[kIvMaxS];  // current i-vector (CG warm start)
@@ -127,8 +143,7 @@ struct IvState {  // per stream, persistent across steps (reset with the pipelin
 struct IvStreamJob {  // one stream's i-vector work in this step
   int slot, req0, nreq, reset;
   int t_ready;             // MFCC frames available (splice clamp)
-  int norm_from, norm_to;  // frames to CMVN-normalize
-  int pad;
+  int pad0, pad1, pad2;
 };
 struct IvReq {  // i-vector at `frame` -> rows [job_lo, job_hi) of the per-job buffer,
                 // after accumulating frame records [row_from, row_to)
@@ -148,7 +163,6 @@ struct IvArgs {
   IvState* state;     // [slots]
   double* quad;       // [slots][S(S+1)/2]
   double* qfull;      // [slots][S][S] the same, unpacked for the CG mat-vec (S > 48)
-  float* hist;        // [slots][kIvHist][feat_dim] raw features (CMVN window)
   float* norm;        // [ring][slots][feat_dim] CMVN-normalized features (MFCC ring layout)
   const float* in_base;  // MFCC input ring [ring][slots][feat_dim]
   int in_mask, slots;

@@ -23,7 +23,7 @@ extern int g_gemm_variant;  // dev override: 1/2 streaming NB=natural/1, 3 LDS (
 void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s);
 // i-vector extraction: online CMVN per stream (before the LDA / UBM GEMMs),
 // then per-frame 5-best posteriors, statistics and CG per stream (after them)
-void LaunchIvectorCmvn(const IvArgs& a, int njobs, hipStream_t s);
+void LaunchCmvn(const CmvnDev& c, const CmvnJob* jobs, int njobs, hipStream_t s);
 void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, hipStream_t s);
 void LdsHashSelfTest(int n, int blocks, int* out);  // dev (tools/gemm_bench)
 int DecoderLdsFrameTokens();  // default LDS frame-construction threshold

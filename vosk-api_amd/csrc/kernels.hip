@@ -218,21 +218,27 @@ __global__ __launch_bounds__(256) void mfcc_kernel(MfccDev m, const MfccJob* job
     if (f0 >= 0)
       for (int i = f0; i <= f1; i++) {
         float pw = re[i] * re[i] + im[i] * im[i];
+        if (m.fbank && !m.use_power) pw = sqrtf(pw);
         e = __builtin_fmaf(wrow[i], pw, e);
       }
-    if (e < 1.1920929e-07f) e = 1.1920929e-07f;
-    MEL[w][lane] = dev_logf(e);
+    if (!(m.fbank && !m.use_log_fbank)) {
+      if (e < 1.1920929e-07f) e = 1.1920929e-07f;
+      e = dev_logf(e);
+    }
+    MEL[w][lane] = e;
   }
   __syncthreads();
-  if (valid && lane < m.num_ceps) {
+  float* dst = m.out + ((size_t)(frame & rings.mask) * rings.slots + slot) * m.feat_dim;
+  if (m.fbank) {  // [log energy,] log mel energies
+    const int off = m.use_energy ? 1 : 0;
+    if (valid && lane < m.num_bins) dst[off + lane] = MEL[w][lane];
+    if (valid && m.use_energy && lane == 0) dst[0] = SC[w][1];
+  } else if (valid && lane < m.num_ceps) {
     float c = 0.0f;
     const float* drow = m.dct + (size_t)lane * m.num_bins;
     for (int j = 0; j < m.num_bins; j++) c = __builtin_fmaf(drow[j], MEL[w][j], c);
     float out = c * m.lifter[lane];
     if (m.use_energy && lane == 0) out = SC[w][1];
-    const int in = rings.input_node;
-    float* dst = rings.base[in] +
-                 ((size_t)(frame & rings.mask) * rings.slots + slot) * rings.dim[in];
     dst[lane] = out;
   }
 }
@@ -683,7 +689,7 @@ void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s) {
 // for operation as the restatement in oracle/oracle.c orc_ivector_extract
 // (double statistics, fixed summation orders), so the result is
 // bit-identical.  Per step:
-//   ivector_cmvn_kernel   one wave per stream: online CMVN of the new frames
+//   cmvn_kernel           per stream: online CMVN of the new frames
 //                         (running double sums, sequential in time) into a
 //                         ring laid out like the MFCC ring
 //   3 GEMM launches       (engine.cc, the nnet GEMM kernels) over blocks of
@@ -714,48 +720,51 @@ __device__ __forceinline__ const float* iv_raw(const IvArgs& a, int slot, int u)
   return a.in_base + ((size_t)(u & a.in_mask) * a.slots + slot) * a.m.feat_dim;
 }
 
-__global__ __launch_bounds__(64) void ivector_cmvn_kernel(IvArgs a) {
-  const IvStreamJob J = a.jobs[blockIdx.x];
-  const IvectorDev& m = a.m;
-  const int d = threadIdx.x, D = m.feat_dim, W = m.cmn_window, slot = J.slot;
+// Online CMVN with global stats (Kaldi OnlineCmvn::GetFrame: the window sums
+// of ComputeStatsForFrame, SmoothOnlineCmvnStats, ApplyCmvn without variance
+// normalization), as oracle.c orc_online_cmvn: one lane per dimension walks
+// the stream's new frames in order.  Used on the nnet input (global_cmvn.stats)
+// and inside the i-vector extractor.
+__global__ __launch_bounds__(128) void cmvn_kernel(CmvnDev c, const CmvnJob* jobs) {
+  const CmvnJob J = jobs[blockIdx.x];
+  const int d = threadIdx.x, D = c.D, W = c.window, slot = J.slot;
   if (d >= D) return;
-  IvState* st = a.state + slot;
-  float* hist = a.hist + (size_t)slot * kIvHist * D;
-  float* norm = a.norm;  // ring layout [ring][slots][feat_dim], like the MFCC ring
-  double csum = J.reset ? 0.0 : st->sum[d];
-  const double gcount = m.cmvn[D], gmean = m.cmvn[d];
-  // blocks of 16 frames, all loads first (cmn_window >= 16: no frame leaving
-  // the window is stored in the same block)
-  for (int u0 = J.norm_from; u0 < J.norm_to; u0 += 16) {
+  float* hist = c.hist + (size_t)slot * kCmvnHist * D;
+  double csum = J.reset ? 0.0 : c.sums[(size_t)slot * D + d];
+  const double gcount = c.gstats[D], gmean = c.gstats[d];
+  auto in_row = [&](int u) { return c.in_base + ((size_t)(u & c.mask) * c.slots + slot) * D; };
+  // blocks of 16 frames, all loads first (window >= 16: no frame leaving the
+  // window is stored in the same block)
+  for (int u0 = J.from; u0 < J.to; u0 += 16) {
     float xn[16], xo[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       const int u = u0 + k;
-      xn[k] = u < J.norm_to ? iv_raw(a, slot, u)[d] : 0.0f;
-      xo[k] = (u < J.norm_to && u - W >= 0) ? hist[(size_t)((u - W) % kIvHist) * D + d] : 0.0f;
+      xn[k] = u < J.to ? in_row(u)[d] : 0.0f;
+      xo[k] = (u < J.to && u - W >= 0) ? hist[(size_t)((u - W) % kCmvnHist) * D + d] : 0.0f;
     }
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       const int u = u0 + k;
-      if (u >= J.norm_to) break;
+      if (u >= J.to) break;
       const float x = xn[k];
       csum = csum + (double)x;
-      hist[(size_t)(u % kIvHist) * D + d] = x;
+      hist[(size_t)(u % kCmvnHist) * D + d] = x;
       if (u - W >= 0) csum = csum - (double)xo[k];
       double cnt = (double)min(u + 1, W), stv = csum;
       if (cnt < W) {
         double cgf = W - cnt;
-        if (cgf > m.global_frames) cgf = m.global_frames;
+        if (cgf > c.global_frames) cgf = c.global_frames;
         const double scl = cgf / gcount;
         stv = stv + scl * gmean;
         cnt = cnt + scl * gcount;
       }
       const float alpha = (float)(-1.0 / cnt);
       const float off = (float)((double)alpha * stv);
-      norm[((size_t)(u & a.in_mask) * a.slots + slot) * D + d] = x + off;
+      c.out_base[((size_t)(u & c.mask) * c.slots + slot) * D + d] = x + off;
     }
   }
-  st->sum[d] = csum;
+  c.sums[(size_t)slot * D + d] = csum;
 }
 
 // Max of a 64-bit key over the wave: DPP butterflies inside each 16-lane row
@@ -1144,8 +1153,8 @@ __global__ __launch_bounds__(128) void ivector_cg_kernel(IvArgs a) {
   if (tid < S) st->cur[tid] = X[tid];
 }
 
-void LaunchIvectorCmvn(const IvArgs& a, int njobs, hipStream_t s) {
-  if (njobs > 0) hipLaunchKernelGGL(ivector_cmvn_kernel, dim3(njobs), dim3(64), 0, s, a);
+void LaunchCmvn(const CmvnDev& c, const CmvnJob* jobs, int njobs, hipStream_t s) {
+  if (njobs > 0) hipLaunchKernelGGL(cmvn_kernel, dim3(njobs), dim3(128), 0, s, c, jobs);
 }
 
 void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, hipStream_t s) {

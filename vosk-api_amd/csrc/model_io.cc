@@ -82,7 +82,9 @@ void MfccOptions::Apply(const std::map<std::string, std::string>& kv) {
     else if (k == "cepstral-lifter") cepstral_lifter = std::stof(v);
     else if (k == "allow-downsample") allow_downsample = ParseBool(v);
     else if (k == "allow-upsample") allow_upsample = ParseBool(v);
-    else VAMD_WARN("ignoring unsupported mfcc option --" << k);
+    else if (k == "use-log-fbank") use_log_fbank = ParseBool(v);
+    else if (k == "use-power") use_power = ParseBool(v);
+    else VAMD_WARN("ignoring unsupported feature option --" << k);
   }
 }
 
@@ -800,6 +802,14 @@ void ReadSymbolTable(const std::string& path, SymbolTable* t) {
 // ---------------------------------------------------------------------------
 // i-vector extractor directory (src/model.cc:247-263 file set)
 // ---------------------------------------------------------------------------
+std::vector<double> ReadKaldiMatrixFile(const std::string& path, int* rows, int* cols) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) VAMD_ERR("cannot open " << path);
+  std::string d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  KReader r(d);
+  return r.Mat64(rows, cols);
+}
+
 void ReadIvectorModel(const std::string& dir, IvectorModel* m) {
   auto slurp = [](const std::string& path) {
     std::ifstream f(path, std::ios::binary);

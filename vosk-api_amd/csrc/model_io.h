@@ -40,6 +40,11 @@ struct MfccOptions {
   bool use_energy = true, raw_energy = true, htk_compat = false;
   float energy_floor = 0.f, low_freq = 20.f, high_freq = 0.f, cepstral_lifter = 22.f;
   bool allow_downsample = false, allow_upsample = false;
+  // fbank front end (feat/feature-fbank.h; src/model.cc:222-225): log mel
+  // energies (+ log energy first), no DCT
+  bool fbank = false, use_log_fbank = true, use_power = true;
+  int FeatDim() const { return fbank ? num_bins + (use_energy ? 1 : 0) : num_ceps; }
+  void SetFbankDefaults() { fbank = true; use_energy = false; }
   int WindowShift() const { return (int)(samp_freq * 0.001f * frame_shift_ms); }
   int WindowSize() const { return (int)(samp_freq * 0.001f * frame_length_ms); }
   int PaddedWindowSize() const {
@@ -194,5 +199,7 @@ struct IvectorModel {
   std::vector<double> U;                   // derived [G][S(S+1)/2]
 };
 void ReadIvectorModel(const std::string& dir, IvectorModel* m);
+// A Kaldi binary Matrix<float|double> file (e.g. global_cmvn.stats) as doubles.
+std::vector<double> ReadKaldiMatrixFile(const std::string& path, int* rows, int* cols);
 
 }  // namespace vamd

@@ -23,8 +23,14 @@ import numpy as np
 # MFCC
 # ----------------------------------------------------------------------------
 class MfccOpts:
-    def __init__(self, conf: dict | None = None):
+    """MfccOptions, or FbankOptions with fbank=True (feat/feature-fbank.h:
+    use-energy defaults to false, log mel energies, power spectrum)."""
+
+    def __init__(self, conf: dict | None = None, fbank: bool = False):
         c = conf or {}
+        self.fbank = fbank
+        self.use_log_fbank = c.get("use-log-fbank", "true") == "true"
+        self.use_power = c.get("use-power", "true") == "true"
         self.samp_freq = float(c.get("sample-frequency", 16000))
         self.frame_shift_ms = float(c.get("frame-shift", 10))
         self.frame_length_ms = float(c.get("frame-length", 25))
@@ -37,10 +43,14 @@ class MfccOpts:
         self.snip_edges = c.get("snip-edges", "true") == "true"
         self.num_bins = int(c.get("num-mel-bins", 23))
         self.num_ceps = int(c.get("num-ceps", 13))
-        self.use_energy = c.get("use-energy", "true") == "true"
+        self.use_energy = c.get("use-energy", "false" if fbank else "true") == "true"
         self.low_freq = float(c.get("low-freq", 20))
         self.high_freq = float(c.get("high-freq", 0))
         self.cepstral_lifter = float(c.get("cepstral-lifter", 22))
+
+    @property
+    def feat_dim(self):
+        return self.num_bins + int(self.use_energy) if self.fbank else self.num_ceps
 
     @property
     def shift(self):
@@ -115,6 +125,60 @@ def lifter(o: MfccOpts):
     q = o.cepstral_lifter
     i = np.arange(o.num_ceps, dtype=np.float64)
     return 1.0 + 0.5 * q * np.sin(math.pi * i / q) if q != 0 else np.ones(o.num_ceps)
+
+
+def online_cmvn(feats, gstats, window=600, global_frames=200):
+    """Kaldi OnlineCmvn (mean only) with global stats [2][D+1]: sliding
+    window sums smoothed with up to global_frames of the global mean."""
+    feats = np.asarray(feats, np.float64)
+    T, D = feats.shape
+    g = np.asarray(gstats, np.float64)
+    out = np.zeros_like(feats)
+    for t in range(T):
+        lo = max(0, t + 1 - window)
+        st = feats[lo:t + 1].sum(0)
+        cnt = float(t + 1 - lo)
+        if cnt < window:
+            sc = min(window - cnt, global_frames) / g[0, D]
+            st = st + sc * g[0, :D]
+            cnt = cnt + sc * g[0, D]
+        out[t] = feats[t] - st / cnt
+    return out
+
+
+def features(wave, o: MfccOpts):
+    """The front end the options describe: MFCC or (log) fbank."""
+    return fbank(wave, o) if o.fbank else mfcc(wave, o)
+
+
+def fbank(wave, o: MfccOpts):
+    """FbankComputer::Compute: [log raw energy,] log mel energies."""
+    wave = np.asarray(wave, np.float64)
+    nf = num_frames(len(wave), o)
+    win = window_fn(o)
+    W = mel_banks(o)
+    off = int(o.use_energy)
+    out = np.zeros((nf, o.num_bins + off))
+    for f in range(nf):
+        x = wave[f * o.shift: f * o.shift + o.length].copy()
+        if o.remove_dc:
+            x -= x.mean()
+        energy = max(float(np.dot(x, x)), np.finfo(np.float32).eps)
+        if o.preemph != 0:
+            x[1:] = x[1:] - o.preemph * x[:-1]
+            x[0] -= o.preemph * x[0]
+        x *= win
+        X = np.fft.rfft(x, o.padded)
+        p = (X.real ** 2 + X.imag ** 2)[: o.padded // 2]
+        if not o.use_power:
+            p = np.sqrt(p)
+        e = W @ p
+        if o.use_log_fbank:
+            e = np.log(np.maximum(e, np.finfo(np.float32).eps))
+        out[f, off:] = e
+        if o.use_energy:
+            out[f, 0] = math.log(energy)
+    return out
 
 
 def mfcc(wave, o: MfccOpts):
