@@ -27,6 +27,15 @@ const char *vamd_json_words(const char *list_key, const char *text_key, int n,
                             const char *const *words, const double *start, const double *end,
                             const double *conf);
 
+/* host-only: the recognizer's silence weighting (silence.h) over a sequence
+ * of calls; call c passes the best-path traceback (per decoded frame: tid and
+ * source token) in [trace_off[c], trace_off[c+1]) and receives its (feature
+ * frame, delta weight) list in [out_off[c], out_off[c+1]).  Returns the total. */
+int vamd_silence_weighting_run(int ncalls, const int *num_frames_ready, const int *first_decoder_frame,
+                               const int *trace_off, const int *tids, const int *toks,
+                               const unsigned char *tid_is_silence, int num_tids, float silence_weight,
+                               int fss, int *out_off, int *out_frame, float *out_w, int cap);
+
 const char *vamd_last_error(void);
 int vamd_device_count(void);
 
@@ -67,6 +76,11 @@ long long vamd_stream_llh(VamdEngine *e, int stream, float *out, long long cap);
  * copies up to cap floats, returns the count; ivector dim 0 = no i-vector input */
 long long vamd_stream_ivectors(VamdEngine *e, int stream, float *out, long long cap);
 int vamd_engine_ivector_dim(VamdEngine *e);
+/* silence weighting of the i-vector statistics (the reference Recognizer's
+ * UpdateSilenceWeights, src/recognizer.cc:226-237): call after accepting
+ * samples and before advancing; first_decoder_frame = feature frame of the
+ * decoder segment's frame 0.  Returns 1 if active for the model, 0 if not. */
+int vamd_stream_update_silence_weights(VamdEngine *e, int stream, int first_decoder_frame);
 /* per-frame stats of the last advance (flag 1): 8 floats per frame
  * {ntok_in, ntok_out, arcs_emit, arcs_eps, best, cutoff, next_cutoff, adaptive_beam} */
 int vamd_stream_stats(VamdEngine *e, int stream, float *out, int cap_frames);

@@ -180,10 +180,104 @@ static void iv_cgd(const double* Q, const double* b, int S, int max_iters, doubl
   }
 }
 
-int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, const int* requests,
-                        const int* t_ready, int nreq, float* out) {
+/* one frame's record (OnlineIvectorFeature::UpdateStatsForFrames): LDA of
+   the CMVN-normalized splice, diagonal-UBM log-likelihoods, num_gselect best
+   Gaussians (descending, ties by lower index) pruned by min_post, their
+   posteriors before any frame weight, and the LDA of the raw splice */
+typedef struct {
+  int ns, sel[16];
+  float post[16];
+  float xr[256];
+} iv_rec;
+
+static void iv_record(const orc_ivector_model* m, const float* norm, const float* feats, int t,
+                      int t_ready, const float* wubm, float* ll, iv_rec* R) {
+  const int DL = m->lda_rows, G = m->num_gauss;
+  const float log_min_post = (float)log((double)m->min_post);
+  float xn[256], xq[512];
+  iv_lda(m, norm, t, t_ready, xn);
+  for (int d = 0; d < DL; d++) {
+    xq[d] = xn[d];
+    xq[DL + d] = xn[d] * xn[d];
+  }
+  for (int g = 0; g < G; g++) ll[g] = canon_dot(wubm + (size_t)g * 2 * DL, xq, 2 * DL) + m->gconsts[g];
+  int ns = 0;
+  for (int k = 0; k < m->num_gselect && k < G; k++) {
+    int b = -1;
+    for (int g = 0; g < G; g++) {
+      int used = 0;
+      for (int j = 0; j < ns; j++) used |= R->sel[j] == g;
+      if (used) continue;
+      if (b < 0 || ll[g] > ll[b]) b = g;
+    }
+    R->sel[ns++] = b;
+  }
+  while (ns > 1 && ll[R->sel[ns - 1]] < ll[R->sel[0]] + log_min_post) ns--;
+  float e[16], tot = 0.0f;
+  for (int k = 0; k < ns; k++) {
+    e[k] = orc_expf(ll[R->sel[k]] - ll[R->sel[0]]);
+    tot = tot + e[k];
+  }
+  for (int k = 0; k < ns; k++) R->post[k] = e[k] / tot;
+  R->ns = ns;
+  iv_lda(m, feats, t, t_ready, R->xr);
+}
+
+/* per-frame OnlineIvectorEstimationStats::AccStats with the frame weight
+   folded into the posteriors as Kaldi does (post * (posterior_scale * w),
+   in float; negative weights undo earlier contributions), then the
+   max-count prior rescaling */
+typedef struct {
+  double lin[128], cur[128];
+  double* quad;
+  double nfr;
+} iv_stats;
+
+static void iv_accumulate(const orc_ivector_model* m, const double* SIM, const double* U,
+                          const iv_rec* R, float w, iv_stats* st) {
+  const int DL = m->lda_rows, S = m->ivec_dim, QS = S * (S + 1) / 2;
+  double tw = 0.0;
+  for (int k = 0; k < R->ns; k++) {
+    const float post = R->post[k] * (m->posterior_scale * w);
+    const double wd = (double)post;
+    if (wd == 0.0) continue;
+    const double* sm = SIM + (size_t)R->sel[k] * DL * S;
+    for (int s2 = 0; s2 < S; s2++) {
+      double a = 0.0;
+      for (int d = 0; d < DL; d++) a = fma(sm[(size_t)d * S + s2], (double)R->xr[d], a);
+      st->lin[s2] = st->lin[s2] + wd * a;
+    }
+    const double* u = U + (size_t)R->sel[k] * QS;
+    for (int i = 0; i < QS; i++) st->quad[i] = st->quad[i] + wd * u[i];
+    tw = tw + wd;
+  }
+  if (m->max_count > 0.0) {
+    const double mc = m->max_count, nfr = st->nfr;
+    const double oldp = (nfr > mc ? nfr : mc) / mc, newn = nfr + tw;
+    const double newp = (newn > mc ? newn : mc) / mc, ch = newp - oldp;
+    if (ch != 0.0) {
+      st->lin[0] = st->lin[0] + m->prior_offset * ch;
+      for (int i = 0; i < S; i++) st->quad[(size_t)i * (i + 1) / 2 + i] += ch;
+    }
+  }
+  st->nfr = st->nfr + tw;
+}
+
+/* Requests in order; request q = the i-vector at frame requests[q] with
+   t_ready[q] feature frames available.  A request past the frames already
+   accumulated first computes the records of the new frames, then applies
+   either every new frame with weight 1 (ent_off == NULL: no silence
+   weighting, OnlineIvectorFeature::UpdateStatsUntilFrame) or the entries
+   [ent_off[q], ent_off[q+1]) (frame, delta weight) in the given order
+   (UpdateStatsUntilFrameWeighted: the queued delta weights of frames <= the
+   request, popped in (frame, weight) order), then the warm-started CG
+   (IvectorEstimationStats::GetIvector; no net frames -> the prior). */
+int orc_ivector_extract_w(const orc_ivector_model* m, const float* feats, int T, const int* requests,
+                          const int* t_ready, int nreq, const int* ent_off, const int* ent_frame,
+                          const float* ent_w, float* out) {
   const int D = m->feat_dim, DL = m->lda_rows, S = m->ivec_dim, G = m->num_gauss;
   const int QS = S * (S + 1) / 2;
+  if (DL > 256 || S > 128 || m->num_gselect > 16) return -1;
   /* derived extractor terms (IvectorExtractor::ComputeDerivedVars) */
   double* SIM = (double*)malloc(sizeof(double) * (size_t)G * DL * S);
   double* U = (double*)malloc(sizeof(double) * (size_t)G * QS);
@@ -208,16 +302,15 @@ int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, c
   /* online CMVN (window cmn_window, smoothed with global_frames of global stats) */
   float* norm = (float*)malloc(sizeof(float) * (size_t)(T > 0 ? T : 1) * D);
   orc_online_cmvn(m->cmvn, D, m->cmn_window, m->global_frames, feats, T, norm);
-  double lin[128] = {0}, cur[128] = {0};
-  double* quad = (double*)calloc(QS, sizeof(double));
-  lin[0] = m->prior_offset;
-  for (int i = 0; i < S; i++) quad[(size_t)i * (i + 1) / 2 + i] = 1.0;
-  cur[0] = m->prior_offset;
-  double nfr = 0.0;
+  iv_stats st;
+  memset(&st, 0, sizeof(st));
+  st.quad = (double*)calloc(QS, sizeof(double));
+  st.lin[0] = m->prior_offset;
+  for (int i = 0; i < S; i++) st.quad[(size_t)i * (i + 1) / 2 + i] = 1.0;
+  st.cur[0] = m->prior_offset;
   int done = 0;
-  const float log_min_post = (float)log((double)m->min_post);
   float* ll = (float*)malloc(sizeof(float) * G);
-  float xn[256], xr[256], xq[512];
+  iv_rec* recs = (iv_rec*)malloc(sizeof(iv_rec) * (size_t)(T > 0 ? T : 1));
   /* UBM log-likelihoods as one affine row per Gaussian over [x | x*x]:
      [means_invvars | -0.5 inv_vars] (the -0.5 scaling is exact), gconst last */
   float* wubm = (float*)malloc(sizeof(float) * (size_t)G * 2 * DL);
@@ -226,71 +319,39 @@ int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, c
       wubm[(size_t)g * 2 * DL + d] = m->means_invvars[(size_t)g * DL + d];
       wubm[(size_t)g * 2 * DL + DL + d] = -0.5f * m->inv_vars[(size_t)g * DL + d];
     }
+  int rc = 0;
   for (int q = 0; q < nreq; q++) {
     const int f = requests[q];
     if (f >= done) {
-      for (int t = done; t <= f; t++) {
-        iv_lda(m, norm, t, t_ready[q], xn);
-        for (int d = 0; d < DL; d++) {
-          xq[d] = xn[d];
-          xq[DL + d] = xn[d] * xn[d];
+      if (f >= T) { rc = -2; break; }
+      for (int t = done; t <= f; t++) iv_record(m, norm, feats, t, t_ready[q], wubm, ll, &recs[t]);
+      if (!ent_off) {
+        for (int t = done; t <= f; t++) iv_accumulate(m, SIM, U, &recs[t], 1.0f, &st);
+      } else {
+        for (int i = ent_off[q]; i < ent_off[q + 1]; i++) {
+          if (ent_frame[i] < 0 || ent_frame[i] > f) { rc = -3; break; }
+          iv_accumulate(m, SIM, U, &recs[ent_frame[i]], ent_w[i], &st);
         }
-        for (int g = 0; g < G; g++)
-          ll[g] = canon_dot(wubm + (size_t)g * 2 * DL, xq, 2 * DL) + m->gconsts[g];
-        /* num_gselect best, descending, ties by lower index */
-        int sel[16];
-        int ns = 0;
-        for (int k = 0; k < m->num_gselect && k < G; k++) {
-          int b = -1;
-          for (int g = 0; g < G; g++) {
-            int used = 0;
-            for (int j = 0; j < ns; j++) used |= sel[j] == g;
-            if (used) continue;
-            if (b < 0 || ll[g] > ll[b]) b = g;
-          }
-          sel[ns++] = b;
-        }
-        while (ns > 1 && ll[sel[ns - 1]] < ll[sel[0]] + log_min_post) ns--;
-        float e[16], tot = 0.0f;
-        for (int k = 0; k < ns; k++) {
-          e[k] = orc_expf(ll[sel[k]] - ll[sel[0]]);
-          tot = tot + e[k];
-        }
-        iv_lda(m, feats, t, t_ready[q], xr);
-        double tw = 0.0;
-        for (int k = 0; k < ns; k++) {
-          const float post = (e[k] / tot) * (m->posterior_scale * 1.0f);
-          const double w = (double)post;
-          if (w == 0.0) continue;
-          const double* sm = SIM + (size_t)sel[k] * DL * S;
-          for (int s2 = 0; s2 < S; s2++) {
-            double a = 0.0;
-            for (int d = 0; d < DL; d++) a = fma(sm[(size_t)d * S + s2], (double)xr[d], a);
-            lin[s2] = lin[s2] + w * a;
-          }
-          const double* u = U + (size_t)sel[k] * QS;
-          for (int i = 0; i < QS; i++) quad[i] = quad[i] + w * u[i];
-          tw = tw + w;
-        }
-        if (m->max_count > 0.0) {
-          const double mc = m->max_count;
-          const double oldp = (nfr > mc ? nfr : mc) / mc, newn = nfr + tw;
-          const double newp = (newn > mc ? newn : mc) / mc, ch = newp - oldp;
-          if (ch != 0.0) {
-            lin[0] = lin[0] + m->prior_offset * ch;
-            for (int i = 0; i < S; i++) quad[(size_t)i * (i + 1) / 2 + i] += ch;
-          }
-        }
-        nfr = nfr + tw;
+        if (rc) break;
       }
       done = f + 1;
-      if (nfr > 0.0) iv_cgd(quad, lin, S, m->num_cg_iters, cur);
+      if (st.nfr > 0.0) {
+        iv_cgd(st.quad, st.lin, S, m->num_cg_iters, st.cur);
+      } else {
+        for (int i = 0; i < S; i++) st.cur[i] = 0.0;
+        st.cur[0] = m->prior_offset;
+      }
     }
-    for (int i = 0; i < S; i++) out[(size_t)q * S + i] = (float)cur[i];
+    for (int i = 0; i < S; i++) out[(size_t)q * S + i] = (float)st.cur[i];
     out[(size_t)q * S] = out[(size_t)q * S] - (float)m->prior_offset;
   }
-  free(SIM); free(U); free(norm); free(quad); free(ll); free(wubm);
-  return 0;
+  free(SIM); free(U); free(norm); free(st.quad); free(ll); free(wubm); free(recs);
+  return rc;
+}
+
+int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, const int* requests,
+                        const int* t_ready, int nreq, float* out) {
+  return orc_ivector_extract_w(m, feats, T, requests, t_ready, nreq, NULL, NULL, NULL, out);
 }
 
 /* ---- resampling (Kaldi LinearResample, feat/resample.cc) ---------------- */

@@ -116,6 +116,11 @@ typedef struct {
    with the prior offset removed from dimension 0.  Returns 0. */
 int orc_ivector_extract(const orc_ivector_model* m, const float* feats, int T, const int* requests,
                         const int* t_ready, int nreq, float* out);
+/* the same with silence weighting: request q applies the (frame, delta
+   weight) entries [ent_off[q], ent_off[q+1]) instead of its new frames */
+int orc_ivector_extract_w(const orc_ivector_model* m, const float* feats, int T, const int* requests,
+                          const int* t_ready, int nreq, const int* ent_off, const int* ent_frame,
+                          const float* ent_w, float* out);
 
 /* ---------------- token-passing decoder (Kaldi decoder/lattice-faster-decoder.cc) */
 typedef struct {

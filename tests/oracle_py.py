@@ -9,6 +9,7 @@ cpu_baseline leg.
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 import subprocess
 import sys
@@ -44,6 +45,9 @@ def load_lib():
     lib.orc_ivector_extract.restype = C.c_int
     lib.orc_ivector_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                         C.c_int, C.c_void_p]
+    lib.orc_ivector_extract_w.restype = C.c_int
+    lib.orc_ivector_extract_w.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                          C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.orc_expf.restype = C.c_float
     lib.orc_expf.argtypes = [C.c_float]
     return lib
@@ -98,6 +102,40 @@ def online_cmvn(feats, gstats, window=600, global_frames=200) -> np.ndarray:
         lib().orc_online_cmvn(g.ctypes.data, f.shape[1], window, global_frames, f.ctypes.data,
                               f.shape[0], out.ctypes.data)
     return out
+
+
+def recognizer_pieces(n, chunk, rate):
+    """Sample counts the reference Recognizer processes per decoding advance
+    when fed `chunk` samples per AcceptWaveform call: 0.2 s steps inside each
+    call (src/recognizer.cc:305-311)."""
+    step = int(rate * 0.2)
+    out = []
+    for i in range(0, n, chunk):
+        m = min(chunk, n - i)
+        out += [min(step, m - j) for j in range(0, m, step)]
+    return out
+
+
+def resample_num_outputs(rate_in, rate_out, n, flush):
+    """Kaldi LinearResample::GetNumOutputSamples (feat/resample.cc [K]):
+    without flush, outputs whose filter window reaches past the input wait."""
+    tick = rate_in * rate_out // math.gcd(rate_in, rate_out)
+    interval = n * (tick // rate_in)
+    if not flush:
+        cutoff = 0.5 * min(rate_in, rate_out)
+        interval -= int(math.floor(6 / (2.0 * cutoff) * tick))
+    if interval <= 0:
+        return 0
+    tpo = tick // rate_out
+    last = interval // tpo
+    if last * tpo == interval:
+        last -= 1
+    return last + 1
+
+
+def mfcc_num_frames(num_samples, conf: dict, fbank: bool = False) -> int:
+    o = mfcc_opts(conf, fbank)
+    return int(lib().orc_mfcc_num_frames(C.byref(o), C.c_long(num_samples)))
 
 
 def mfcc(wave, conf: dict, fbank: bool = False) -> np.ndarray:
@@ -161,6 +199,84 @@ class OracleIvector:
         out = np.zeros((len(req), self.dim), np.float32)
         lib().orc_ivector_extract(C.byref(self.m), feats.ctypes.data, T, req.ctypes.data,
                                   tr.ctypes.data, len(req), out.ctypes.data)
+        return out
+
+
+    def extract_weighted(self, feats, requests, entries):
+        """Silence-weighted extraction: entries[q] = the (frame, delta weight)
+        list request q applies, in order (empty for requests that reuse the
+        current i-vector)."""
+        feats = np.ascontiguousarray(feats, np.float32)
+        T = feats.shape[0]
+        req = np.ascontiguousarray(requests, np.int32)
+        tr = np.full(len(req), T, np.int32)
+        off = np.zeros(len(req) + 1, np.int32)
+        off[1:] = np.cumsum([len(e) for e in entries])
+        fr = np.ascontiguousarray([f for e in entries for f, _ in e] or [0], np.int32)
+        w = np.ascontiguousarray([x for e in entries for _, x in e] or [0], np.float32)
+        out = np.zeros((len(req), self.dim), np.float32)
+        rc = lib().orc_ivector_extract_w(C.byref(self.m), feats.ctypes.data, T, req.ctypes.data,
+                                         tr.ctypes.data, len(req), off.ctypes.data, fr.ctypes.data,
+                                         w.ctypes.data, out.ctypes.data)
+        assert rc == 0, rc
+        return out
+
+
+class SilenceWeighting:
+    """Restatement of Kaldi's OnlineSilenceWeighting (online2/online-ivector-
+    feature.cc [K]; not vendored in the reference) as the reference's
+    Recognizer drives it: silence weight 1e-3 and the endpoint silence phones
+    (src/model.cc:230-231), ComputeCurrentTraceback + GetDeltaWeights before
+    every decoding advance (src/recognizer.cc:226-237), a new object per
+    decoder segment (src/recognizer.cc:188-191).  max_state_duration is
+    unset in the reference (no duration rule)."""
+
+    def __init__(self, is_silence_tid, silence_weight=1e-3, fss=3):
+        self.is_sil = is_silence_tid
+        self.sw = np.float32(silence_weight)
+        self.fss = fss
+        self.info = []  # [token, tid, current_weight]
+
+    def compute_current_traceback(self, tids, toks):
+        n, prev = len(tids), len(self.info)
+        if prev < n:
+            self.info += [[-1, -1, np.float32(0)] for _ in range(n - prev)]
+        if prev > n and self.info[n][1] != -1:
+            raise RuntimeError("number of frames decoded decreased")
+        for fr in range(n - 1, -1, -1):
+            if self.info[fr][0] == toks[fr]:
+                break  # unchanged from here back
+            self.info[fr][0] = toks[fr]
+            self.info[fr][1] = tids[fr]
+
+    def get_delta_weights(self, num_frames_ready, first_decoder_frame):
+        fs = self.fss
+        ndec = (num_frames_ready - first_decoder_frame + fs - 1) // fs
+        prev = len(self.info)
+        if len(self.info) < ndec:
+            self.info += [[-1, -1, np.float32(0)] for _ in range(ndec - len(self.info))]
+        begin = max(0, prev - 100)
+        nout = len(self.info) - begin
+        out = []
+        if nout <= 0:
+            return out
+        fw = [np.float32(1.0)] * nout
+        if self.info[begin][1] == -1:
+            w = self.sw if begin == 0 else self.info[begin - 1][2]
+            fw = [w] * nout
+        else:
+            for o in range(nout):
+                tid = self.info[begin + o][1]
+                if tid == -1:
+                    fw[o] = fw[o - 1]
+                elif self.is_sil(tid):
+                    fw[o] = self.sw
+        for o in range(nout):
+            fi = self.info[begin + o]
+            diff = np.float32(fw[o] - fi[2])
+            fi[2] = fw[o]
+            if diff != 0 or o + 1 == nout:
+                out += [(first_decoder_frame + (begin + o) * fs + i, diff) for i in range(fs)]
         return out
 
 
@@ -568,6 +684,80 @@ class OracleModel:
     def decode_llh(self, llh, use_final=True):
         return self.graph.decode(llh, self.beam, self.max_active, self.min_active,
                                  self.beam_delta, use_final)
+
+    def online(self, wave, chunk=None, rate=16000, silence_weighting=True):
+        """The single-stream Recognizer's online flow (src/recognizer.cc:297-
+        323, FinalResult :818-830) with the engine's chunk schedule: per
+        piece, features of all samples so far, UpdateSilenceWeights from the
+        best path of the frames decoded so far, then every chunk that became
+        ready (its i-vector request applies the queued delta weights of
+        frames <= the request).  Returns per-chunk i-vectors, the LLH rows,
+        and the final decode."""
+        assert self.ivector is not None
+        wave = np.asarray(wave, np.float32)
+        model_rate = int(float(self.mfcc_conf.get("sample-frequency", 16000)))
+        feats_all = self.features(wave if rate == model_rate else resample(wave, rate, model_rate))
+        fss, fpc, R = self.fss, self.fpc, self.right_context
+        right = self.ivector.m.right
+        opc = fpc // fss
+        tm, g = self.tm, self.graph
+        sil = set(int(p) for p in str(self.model_conf.get("endpoint.silence-phones", "")).replace(",", ":").split(":") if p)
+        sw = SilenceWeighting(lambda tid: int(tm.tid2phone[tid]) in sil, 1e-3, fss)
+        active = silence_weighting and bool(sil)
+        pending, weighted = [], False
+        reqs, ents = [], []
+        c, done, dec = 0, 0, 0
+        ivecs = np.zeros((0, self.ivector.dim), np.float32)
+        llh = np.zeros((0, self.net.out_dim), np.float32)
+        pieces, n = [], 0
+        for k in recognizer_pieces(len(wave), chunk or len(wave), rate):
+            n += k
+            pieces.append((n, False))
+        pieces.append((len(wave), True))
+        for n, fin in pieces:
+            n_out = n if rate == model_rate else resample_num_outputs(rate, model_rate, n, fin)
+            T = mfcc_num_frames(n_out, self.mfcc_conf, self.fbank)
+            ready = T if fin else max(0, T - right)
+            if active and ready > 0 and (weighted or done == 0):
+                tids, toks = [], []
+                if dec > 0:
+                    r = self.decode_llh(llh[:dec], use_final=False)
+                    for a in r["path"]:
+                        if g.ilabel[a] != 0:
+                            tids.append(int(g.ilabel[a]))
+                            toks.append(int(np.searchsorted(g.arc_begin, a, side="right") - 1))
+                sw.compute_current_traceback(tids, toks)
+                pending += sw.get_delta_weights(ready, 0)
+                weighted = True
+            need_out = -(-T // fss) if fin else 0
+            new = False
+            while True:
+                ok = (T > 0 and c * opc < need_out) if fin else T >= (c + 1) * fpc + R + right
+                if not ok:
+                    break
+                f = min((c + 1) * fpc + R, T) - 1
+                e = []
+                if f >= done and weighted:
+                    pending.sort()
+                    e = [x for x in pending if x[0] <= f]
+                    pending = [x for x in pending if x[0] > f]
+                reqs.append(f)
+                ents.append(e)
+                done = max(done, f + 1)
+                dec += min(opc, need_out - c * opc) if fin else opc
+                c += 1
+                new = True
+            if new:
+                feats = feats_all[:T]
+                if weighted:
+                    ivecs = self.ivector.extract_weighted(feats, reqs, ents)
+                else:
+                    ivecs = self.ivector.extract(feats, reqs)
+                nf = self.nnet_features(feats)
+                ivt, t0 = self._ivec_of_time(T, len(ivecs))
+                llh = self.net.forward(nf, ivecs, ivt, t0)[:dec]
+        r = self.decode_llh(llh)
+        return dict(ivectors=ivecs, llh=llh, decode=r, requests=reqs, entries=ents)
 
     def recognize(self, wave):
         r = self.decode_llh(self.loglikes(wave))

@@ -26,9 +26,13 @@ def _pcm(x):
 
 
 def test_kaldi_recognizer_matches_oracle(vosk_mod, synth_model_noep, test_wave):
-    """test_simple.py pattern: 4000-frame chunks, partial results, final result."""
+    """test_simple.py pattern: 4000-frame chunks, partial results, final result.
+    The reference Recognizer silence-weights its i-vector statistics from the
+    decoder's best path (src/recognizer.cc:226-237): the oracle replays the
+    same online flow."""
     oracle = oracle_py.OracleModel(synth_model_noep)
-    ref = oracle.recognize(test_wave)
+    ref = oracle.online(test_wave, chunk=4000)["decode"]
+    ref["text"] = " ".join(oracle.words[w] for w in ref["words"])
     m = vosk_mod.Model(synth_model_noep)
     rec = vosk_mod.KaldiRecognizer(m, 16000)
     rec.SetWords(True)
@@ -51,7 +55,8 @@ def test_kaldi_recognizer_matches_oracle(vosk_mod, synth_model_noep, test_wave):
     assert rec.AcceptWaveform(data[:16000]) == 0
     assert isinstance(json.loads(rec.PartialResult())["partial"], str)
     final2 = json.loads(rec.FinalResult())
-    assert final2["text"] == oracle.recognize(test_wave[:8000])["text"]
+    ref2 = oracle.online(test_wave[:8000], chunk=8000)["decode"]
+    assert final2["text"] == " ".join(oracle.words[w] for w in ref2["words"])
 
 
 def test_accept_waveform_variants_agree(vosk_mod, synth_model_noep, test_wave):

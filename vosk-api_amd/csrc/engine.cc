@@ -349,13 +349,20 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     // frame records of one step: per stream at most the chunks' new frames
     max_iv_frames_ = S * (jobs_per_slot_ * fpc + plan_.right_context + 8);
     max_iv_rows_ = (max_iv_frames_ / kIvFrameBlock + 2 * S) * kIvFrameBlock;
-    iv_.frames = (IvFrame*)DevAlloc(sizeof(IvFrame) * (size_t)max_iv_rows_);
-    float* xraw = (float*)DevAlloc(sizeof(float) * (size_t)max_iv_rows_ * DL);
+    // silence-weighted entries (single-stream recognizers) get rows after the
+    // GEMM rows; their frames' records come from the per-stream history ring
+    max_iv_ents_ = std::max(16384, 4 * max_iv_frames_);
+    const size_t all_rows = (size_t)max_iv_rows_ + max_iv_ents_;
+    iv_.frames = (IvFrame*)DevAlloc(sizeof(IvFrame) * all_rows);
+    float* xraw = (float*)DevAlloc(sizeof(float) * all_rows * DL);
     d_iv_ll_ = (float*)DevAlloc(sizeof(float) * (size_t)max_iv_rows_ * G);
     iv_.xraw = xraw;
     iv_.snap = (double*)DevAlloc(sizeof(double) * (size_t)S * jobs_per_slot_ * (QS + Si));
     iv_.snap_nfr = (double*)DevAlloc(sizeof(double) * (size_t)S * jobs_per_slot_);
-    iv_.chv = (double*)DevAlloc(sizeof(double) * (size_t)max_iv_rows_);
+    iv_.chv = (double*)DevAlloc(sizeof(double) * all_rows);
+    iv_.ring = (IvFrame*)DevAlloc(sizeof(IvFrame) * (size_t)S * kIvRing);
+    iv_.ring_x = (float*)DevAlloc(sizeof(float) * (size_t)S * kIvRing * DL);
+    iv_.ent_row0 = max_iv_rows_;
     for (int i = 0; i < 2; i++) {
       d_ivec_buf_[i] = (float*)DevAlloc(sizeof(float) * (size_t)S * jobs_per_slot_ * Si);
       HIPCHECK(hipMemset(d_ivec_buf_[i], 0, sizeof(float) * (size_t)S * jobs_per_slot_ * Si));
@@ -604,7 +611,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
                  Align256(sizeof(DevJob) * max_jobs_) + Align256(sizeof(DecJob) * S) +
                  Align256(sizeof(IvStreamJob) * S) + Align256(sizeof(IvReq) * max_jobs_) +
                  2 * Align256(sizeof(CmvnJob) * S) +
-                 2 * Align256(sizeof(IvFrameBlock) * ((size_t)max_iv_frames_ / kIvFrameBlock + 2 * S)) + 1024;
+                 2 * Align256(sizeof(IvFrameBlock) * ((size_t)max_iv_frames_ / kIvFrameBlock + 2 * S)) +
+                 Align256(sizeof(IvEntry) * (size_t)max_iv_ents_) + 1024;
   // three buffers: the pipelined nnet and decoder passes keep their jobs
   // while the next step stages
   HIPCHECK(hipHostMalloc((void**)&h_stage_, 3 * stage_bytes_, hipHostMallocDefault));
@@ -677,6 +685,9 @@ void Engine::ResetPipeline(int slot) {
   h.iv_reset = true;
   h.cmvn_reset = true;
   h.iv_norm_done = h.iv_norm_to = h.iv_stats_done = 0;
+  h.iv_weighted = false;
+  h.iv_pending.clear();
+  h.sw.Reset();
 }
 
 void Engine::ResetDecoder(int slot) {
@@ -685,6 +696,7 @@ void Engine::ResetDecoder(int slot) {
   SlotHost& h = slots_.at(slot);
   h.decoded = 0;
   h.need_reset = true;
+  h.sw.Reset();  // a new OnlineSilenceWeighting per decoder segment (src/recognizer.cc:190-191)
 }
 
 void Engine::AcceptSamples(int slot, const float* x, int n) {
@@ -779,6 +791,7 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
   st_ncmvn_.clear();
   st_ivcmvn_.clear();
   st_iv_frames_ = 0;
+  st_iv_ents_.clear();
   const int fpc = plan_.fpc, opc = plan_.opc, fss = plan_.fss, R = plan_.right_context;
   int stats_rows = 0;
   bool any = false;
@@ -891,16 +904,35 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
         const int job = (int)st_jobs_.size(), f = std::min((c + 1) * fpc + R, T) - 1;
         IvReq r{f, c == 0 ? jobs0 : job, job + 1, st_iv_frames_, st_iv_frames_, 0, 0, 0};
         if (f >= h.iv_stats_done) {  // new frames: records, then CG (else reuse)
+          r.upd = 1;
           const int ivjob = (int)st_iv_jobs_.size();
+          const int ring = h.iv_weighted ? s * kIvRing : -1;
           for (int t0 = h.iv_stats_done; t0 <= f; t0 += kIvFrameBlock) {
             const int nf = std::min(kIvFrameBlock, f + 1 - t0);
             // frame records are indexed by GEMM row: kIvFrameBlock per block,
             // rows past the block's frames are empty records (no posteriors)
-            st_iv_blocks_.push_back(IvFrameBlock{ivjob, t0, nf, st_iv_frames_});
+            st_iv_blocks_.push_back(IvFrameBlock{ivjob, t0, nf, st_iv_frames_, ring, 0, 0, 0});
             st_iv_devjobs_.push_back(DevJob{s, t0, T - 1, 0});
             st_iv_frames_ += kIvFrameBlock;
           }
           r.row_to = st_iv_frames_;
+          if (h.iv_weighted) {
+            // OnlineIvectorFeature::UpdateStatsUntilFrameWeighted: the queued
+            // delta weights of frames <= f, popped in (frame, weight) order
+            auto& q = h.iv_pending;
+            std::stable_sort(q.begin(), q.end());
+            size_t n = 0;
+            while (n < q.size() && q[n].first <= f) n++;
+            r.row_from = max_iv_rows_ + (int)st_iv_ents_.size();
+            for (size_t i = 0; i < n; i++) {
+              const int t = q[i].first;
+              if (t <= f - kIvRing) VAMD_ERR("silence weight for frame " << t << " left the history ring");
+              st_iv_ents_.push_back(IvEntry{s * kIvRing + t % kIvRing, q[i].second});
+            }
+            q.erase(q.begin(), q.begin() + n);
+            r.row_to = max_iv_rows_ + (int)st_iv_ents_.size();
+            if ((int)st_iv_ents_.size() > max_iv_ents_) VAMD_ERR("silence-weighted i-vector entries overflow");
+          }
           h.iv_stats_done = f + 1;
           h.iv_norm_to = std::max(h.iv_norm_to, std::min(f + iv_.m.right, T - 1) + 1);
         }
@@ -1045,6 +1077,7 @@ void Engine::RunStep(bool allow_pipeline) {
   size_t o_ivd = put(st_iv_devjobs_.data(), sizeof(DevJob) * st_iv_devjobs_.size());
   size_t o_ncm = put(st_ncmvn_.data(), sizeof(CmvnJob) * st_ncmvn_.size());
   size_t o_icm = put(st_ivcmvn_.data(), sizeof(CmvnJob) * st_ivcmvn_.size());
+  size_t o_ive = put(st_iv_ents_.data(), sizeof(IvEntry) * st_iv_ents_.size());
   cur.dec.jobs = st_dec_;
   cur.dec.o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
   cur.dec.buf = buf;
@@ -1079,6 +1112,8 @@ void Engine::RunStep(bool allow_pipeline) {
     ia.reqs = (const IvReq*)(dsg + o_ivr);
     ia.blocks = (const IvFrameBlock*)(dsg + o_ivb);
     ia.ivec = d_ivec_buf_[par];
+    ia.ents = (const IvEntry*)(dsg + o_ive);
+    ia.nents = (int)st_iv_ents_.size();
     const int rows = (int)st_iv_blocks_.size() * kIvFrameBlock;
     if (rows > max_iv_rows_) VAMD_ERR("i-vector frame records overflow");
     LaunchCmvn(ivcmvn_, (const CmvnJob*)(dsg + o_icm), (int)st_ivcmvn_.size(), fs);
@@ -1268,6 +1303,62 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
     return;
   }
   VAMD_ERR("traceback path buffer could not be sized");
+}
+
+int Engine::IvectorFramesReady(int slot) const {
+  const SlotHost& h = slots_.at(slot);
+  long long remaining = (long long)(h.pending.size() - h.pending_pos);
+  if (h.resident) remaining += h.resident_n - h.resident_pos;
+  const bool fin = h.finished || (h.resident && h.resident_finish);
+  long long samples;
+  if (h.rate != 0) {
+    const ResampleTable& T = res_tables_[h.table];
+    samples = T.NumOutputSamples(h.raw_pushed + remaining, fin);
+  } else {
+    samples = h.samples + remaining;
+  }
+  const int frames = NumFramesFor(samples);
+  if (fin) return frames;
+  return std::max(0, frames - (use_iv_ ? iv_.m.right : 0));
+}
+
+void Engine::UpdateSilenceWeights(int slot, int first_decoder_frame) {
+  if (!SilenceWeightingActive()) return;
+  int ready;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    const SlotHost& h = slots_.at(slot);
+    // statistics already accumulated without weights stay unweighted
+    if (!h.iv_weighted && h.iv_stats_done > 0) return;
+    ready = IvectorFramesReady(slot);
+  }
+  if (ready <= 0) return;
+  const Graph& g = md_->graph;
+  std::vector<int> tid, tok;
+  if (NumFramesDecoded(slot) > 0) {
+    std::vector<PathResult> pr;
+    BestPaths({slot}, false, &pr);
+    for (int a : pr[0].arcs) {
+      if (g.ilabel[a] == 0) continue;
+      // source state of the arc: the token it leaves (unique per frame and state)
+      const int src = (int)(std::upper_bound(g.arc_begin.begin(), g.arc_begin.end(), (int64_t)a) -
+                            g.arc_begin.begin()) - 1;
+      tid.push_back(g.ilabel[a]);
+      tok.push_back(src);
+    }
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  SlotHost& h = slots_.at(slot);
+  const ModelData& m = *md_;
+  auto is_sil = [&m](int t) {
+    const int ph = m.tm.tid2phone[t];
+    return ph < (int)m.phone_is_silence.size() && m.phone_is_silence[ph] != 0;
+  };
+  std::vector<std::pair<int, float>> d;
+  h.sw.ComputeCurrentTraceback(tid, tok);
+  h.sw.GetDeltaWeights(ready, first_decoder_frame, is_sil, &d);
+  h.iv_pending.insert(h.iv_pending.end(), d.begin(), d.end());
+  h.iv_weighted = true;
 }
 
 void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset) {

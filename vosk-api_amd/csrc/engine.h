@@ -22,6 +22,7 @@
 #include "model_io.h"
 #include "nnet_plan.h"
 #include "resample.h"
+#include "silence.h"
 
 namespace vamd {
 
@@ -144,6 +145,18 @@ class Engine {
   const std::vector<float>& ChunkIvectors(int slot) const { return slots_.at(slot).ivecs; }
   int IvectorDim() const { return use_iv_ ? plan_.ivector_dim : 0; }
   void DecodeExternal(int slot, const float* llh, int nframes, bool reset);
+  // Silence weighting of the i-vector statistics (Recognizer::UpdateSilenceWeights,
+  // src/recognizer.cc:226-237): traceback of the stream's best path, weight
+  // changes for the feature frames ready once the accepted samples are
+  // consumed, queued for the stream's next i-vector requests.  No-op without
+  // an i-vector extractor or silence phones.  first_decoder_frame = feature
+  // frame of the decoder segment's frame 0 (frame_offset * 3).
+  void UpdateSilenceWeights(int slot, int first_decoder_frame);
+  bool SilenceWeightingActive() const { return use_iv_ && !md_->endpoint.silence_phones.empty(); }
+  // i-vector feature frames ready once the accepted samples are consumed
+  // (OnlineNnet2FeaturePipeline::NumFramesReady: the splice's right context
+  // waits for more frames until input is finished)
+  int IvectorFramesReady(int slot) const;
   // VOSK_AMD_DEC_PROFILE=1: summed s_memtime clocks per decoder phase
   // [cutoff, seed, expand, compact, eps, commit, -, frames]
   void DecoderPhaseClocks(long long* out8);
@@ -176,6 +189,11 @@ class Engine {
     int iv_norm_done = 0, iv_norm_to = 0;  // frames CMVN-normalized (after this step)
     int iv_stats_done = 0;     // frames accumulated into the i-vector statistics
     std::vector<float> ivecs;  // collect_llh: per-chunk i-vectors
+    // silence weighting: the decoder segment's weighting state and the
+    // stream's queue of (feature frame, delta weight) not yet applied
+    bool iv_weighted = false;
+    std::vector<std::pair<int, float>> iv_pending;
+    SilenceWeighting sw;
   };
   struct DecBatch {  // one decoder launch's jobs, staged in one staging buffer
     std::vector<DecJob> jobs;
@@ -269,7 +287,8 @@ class Engine {
   float* d_iv_ll_ = nullptr; // [GEMM rows][num_gauss] UBM log-likelihoods
   std::vector<NnetOpArgs> iv_ops_;  // LDA (normalized -> [x | x*x]), LDA (raw), UBM
   std::vector<int> iv_op_bk_;
-  int max_iv_rows_ = 0;
+  int max_iv_rows_ = 0, max_iv_ents_ = 0;
+  std::vector<IvEntry> st_iv_ents_;  // silence-weighted entries of this step
   int max_jobs_ = 0, max_dec_frames_ = 0;
 
   void* DevAlloc(size_t bytes);

@@ -146,12 +146,24 @@ struct IvStreamJob {  // one stream's i-vector work in this step
   int pad0, pad1, pad2;
 };
 struct IvReq {  // i-vector at `frame` -> rows [job_lo, job_hi) of the per-job buffer,
-                // after accumulating frame records [row_from, row_to)
-  int frame, job_lo, job_hi, row_from, row_to, pad0, pad1, pad2;
+                // after accumulating frame records [row_from, row_to); upd = the
+                // statistics advance to `frame` here (else the current i-vector
+                // is reused, OnlineIvectorFeature::GetFrame with no new frames)
+  int frame, job_lo, job_hi, row_from, row_to, upd, pad1, pad2;
 };
-struct IvFrameBlock {  // ivector_frame_kernel workgroup: frames t0.. (nf) of a job's stream
-  int job, t0, nf, row;
+struct IvFrameBlock {  // ivector_top_kernel rows: frames t0.. (nf) of a job's stream;
+                       // ring >= 0: also keep the records in the stream's history
+                       // ring (silence-weighted streams re-weight past frames)
+  int job, t0, nf, row, ring, pad0, pad1, pad2;
 };
+// silence weighting (src/recognizer.cc:226-237): one (frame, delta weight)
+// entry of the stream's Kaldi delta-weight queue, applied in (frame, weight)
+// order; rec = the frame's record in the history ring [slot * kIvRing + t % kIvRing]
+struct IvEntry {
+  int rec;
+  float w;
+};
+constexpr int kIvRing = 1024;  // history ring frames per stream (>= 3 x 100 re-weighted + chunk)
 struct IvFrame {  // per-frame result: selected Gaussians and posteriors
   int nsel;
   int sel[5];
@@ -167,7 +179,7 @@ struct IvArgs {
   const float* in_base;  // MFCC input ring [ring][slots][feat_dim]
   int in_mask, slots;
   IvFrame* frames;    // [max frames per step]
-  const float* xraw;  // [GEMM rows][lda_dim] LDA projection of the raw features
+  float* xraw;        // [GEMM rows + entry rows][lda_dim] LDA projection of the raw features
   double* snap;       // [max requests per step][S(S+1)/2 + S] terms at each request
   double* snap_nfr;   // [max requests per step] frame count at each request
   double* chv;        // [max frames per step] prior-scale change at each frame
@@ -175,6 +187,10 @@ struct IvArgs {
   const IvStreamJob* jobs;
   const IvReq* reqs;
   const IvFrameBlock* blocks;
+  IvFrame* ring;        // [slots][kIvRing] records, posteriors unscaled (e/tot)
+  float* ring_x;        // [slots][kIvRing][lda_dim]
+  const IvEntry* ents;  // this step's weighted entries -> rows ent_row0 + i
+  int ent_row0, nents;
 };
 
 struct DecJob {

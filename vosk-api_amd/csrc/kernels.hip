@@ -861,7 +861,42 @@ __global__ __launch_bounds__(256) void ivector_top_kernel(IvArgs a, const float*
       F.sel[k] = chosen[k];
       F.post[k] = (e[k] / tot) * (m.posterior_scale * 1.0f);
     }
+    if (B.ring >= 0) {  // history record: posteriors before the frame weight
+      IvFrame& H = a.ring[B.ring + (B.t0 + k0) % kIvRing];
+      H.nsel = ns;
+      H.xrow = B.t0 + k0;
+      for (int k = 0; k < ns; k++) {
+        H.sel[k] = chosen[k];
+        H.post[k] = e[k] / tot;
+      }
+    }
   }
+  if (B.ring >= 0 && lane < m.lda_dim)
+    a.ring_x[(size_t)(B.ring + (B.t0 + k0) % kIvRing) * m.lda_dim + lane] = a.xraw[(size_t)r * m.lda_dim + lane];
+}
+
+// Silence-weighted entries (OnlineIvectorFeature::UpdateStatsForFrames with
+// delta weights): the record of each entry's frame from the history ring,
+// posteriors scaled by posterior_scale * weight as Kaldi does
+// (`posterior[j].second *= info_.posterior_scale * weight`), into the rows
+// the statistics kernels read.  One wave per entry.
+__global__ __launch_bounds__(256) void ivector_entry_kernel(IvArgs a) {
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (e >= a.nents) return;
+  const IvEntry E = a.ents[e];
+  const int row = a.ent_row0 + e, DL = a.m.lda_dim;
+  if (lane == 0) {
+    const IvFrame H = a.ring[E.rec];
+    IvFrame F;
+    F.nsel = H.nsel;
+    F.xrow = row;
+    for (int k = 0; k < 5; k++) {
+      F.sel[k] = k < H.nsel ? H.sel[k] : 0;
+      F.post[k] = k < H.nsel ? H.post[k] * (a.m.posterior_scale * E.w) : 0.0f;
+    }
+    a.frames[row] = F;
+  }
+  if (lane < DL) a.xraw[(size_t)row * DL + lane] = a.ring_x[(size_t)E.rec * DL + lane];
 }
 
 __device__ __forceinline__ int iv_tri_row(int e) {  // packed lower-triangle row of entry e
@@ -1038,7 +1073,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
         }
       }
     }
-    if (R.row_to > R.row_from) {
+    if (R.upd) {
       double* sn = a.snap + (size_t)(J.req0 + q) * NE;
 #pragma unroll
       for (int j = 0; j < NQP; j++)
@@ -1089,7 +1124,10 @@ __global__ __launch_bounds__(128) void ivector_cg_kernel(IvArgs a) {
   if (tid < S) X[tid] = J.reset ? (tid == 0 ? po : 0.0) : st->cur[tid];
   for (int q = 0; q < J.nreq; q++) {
     const IvReq R = a.reqs[J.req0 + q];
-    if (R.row_to > R.row_from && a.snap_nfr[J.req0 + q] > 0.0) {
+    if (R.upd && !(a.snap_nfr[J.req0 + q] > 0.0)) {
+      // IvectorEstimationStats::GetIvector with no (net) frames: the default
+      if (tid < S) X[tid] = tid == 0 ? po : 0.0;
+    } else if (R.upd) {
       const double* sn = a.snap + (size_t)(J.req0 + q) * NE;
       __syncthreads();
       for (int e = tid; e < QS; e += 128) {
@@ -1160,6 +1198,7 @@ void LaunchCmvn(const CmvnDev& c, const CmvnJob* jobs, int njobs, hipStream_t s)
 void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, hipStream_t s) {
   if (njobs <= 0) return;
   if (rows > 0) hipLaunchKernelGGL(ivector_top_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, a, ll, rows);
+  if (a.nents > 0) hipLaunchKernelGGL(ivector_entry_kernel, dim3((a.nents + 3) / 4), dim3(256), 0, s, a);
   hipLaunchKernelGGL(ivector_nfr_kernel, dim3((njobs + 63) / 64), dim3(64), 0, s, a, njobs);
   // parts: blocks b and b + 8 share an XCD, so part = b % NP keeps each XCD's
   // L2 on 1/NP of U and SigmaInvM

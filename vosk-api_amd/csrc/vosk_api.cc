@@ -265,6 +265,33 @@ const char* vamd_plan_describe(const char* model_dir, int fpc) {
   API_CATCH(nullptr)
 }
 
+int vamd_silence_weighting_run(int ncalls, const int* num_frames_ready, const int* first_decoder_frame,
+                               const int* trace_off, const int* tids, const int* toks,
+                               const unsigned char* tid_is_silence, int num_tids, float silence_weight,
+                               int fss, int* out_off, int* out_frame, float* out_w, int cap) {
+  API_TRY
+  SilenceWeighting sw(silence_weight, fss);
+  auto is_sil = [&](int t) { return t >= 0 && t < num_tids && tid_is_silence[t] != 0; };
+  int n = 0;
+  out_off[0] = 0;
+  std::vector<std::pair<int, float>> d;
+  for (int c = 0; c < ncalls; c++) {
+    std::vector<int> ti(tids + trace_off[c], tids + trace_off[c + 1]);
+    std::vector<int> to(toks + trace_off[c], toks + trace_off[c + 1]);
+    sw.ComputeCurrentTraceback(ti, to);
+    sw.GetDeltaWeights(num_frames_ready[c], first_decoder_frame[c], is_sil, &d);
+    for (auto& x : d) {
+      if (n >= cap) VAMD_ERR("output capacity");
+      out_frame[n] = x.first;
+      out_w[n] = x.second;
+      n++;
+    }
+    out_off[c + 1] = n;
+  }
+  return n;
+  API_CATCH(-1)
+}
+
 int vamd_plan_info(const char* model_dir, int fpc, int* o, double* flops) {
   API_TRY
   ModelData md;
@@ -392,6 +419,13 @@ long long vamd_stream_ivectors(VamdEngine* e, int s, float* out, long long cap) 
   long long n = std::min<long long>(cap, (long long)v.size());
   if (out && n > 0) memcpy(out, v.data(), sizeof(float) * n);
   return (long long)v.size();
+  API_CATCH(-1)
+}
+
+int vamd_stream_update_silence_weights(VamdEngine* e, int s, int first_decoder_frame) {
+  API_TRY
+  e->eng->UpdateSilenceWeights(s, first_decoder_frame);
+  return e->eng->SilenceWeightingActive() ? 1 : 0;
   API_CATCH(-1)
 }
 

@@ -164,6 +164,7 @@ bool Recognizer::AcceptWaveform(std::vector<float>& w) {  // src/recognizer.cc:2
   for (size_t i = 0; i < w.size(); i += step) {
     const int n = (int)std::min<size_t>(step, w.size() - i);
     engine_->AcceptSamples(slot_, w.data() + i, n);
+    engine_->UpdateSilenceWeights(slot_, frame_offset_ * 3);  // src/recognizer.cc:309
     engine_->Advance({slot_});
   }
   samples_processed_ += w.size();
@@ -272,6 +273,7 @@ const char* Recognizer::Result() {  // src/recognizer.cc:808-816
 const char* Recognizer::FinalResult() {  // src/recognizer.cc:818-844
   if (state_ != RECOGNIZER_RUNNING) return StoreEmptyReturn();
   engine_->InputFinished(slot_);
+  engine_->UpdateSilenceWeights(slot_, frame_offset_ * 3);  // src/recognizer.cc:825
   engine_->Advance({slot_});
   state_ = RECOGNIZER_FINALIZED;
   GetResult();

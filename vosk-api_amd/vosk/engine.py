@@ -34,6 +34,9 @@ _SIGS = {
     "vamd_stream_llh": (C.c_longlong, [_vp, C.c_int, _vp, C.c_longlong]),
     "vamd_stream_ivectors": (C.c_longlong, [_vp, C.c_int, _vp, C.c_longlong]),
     "vamd_engine_ivector_dim": (C.c_int, [_vp]),
+    "vamd_stream_update_silence_weights": (C.c_int, [_vp, C.c_int, C.c_int]),
+    "vamd_silence_weighting_run": (C.c_int, [C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
+                                             C.c_float, C.c_int, _vp, _vp, _vp, C.c_int]),
     "vamd_stream_stats": (C.c_int, [_vp, C.c_int, _vp, C.c_int]),
     "vamd_stream_decode_llh": (C.c_int, [_vp, C.c_int, _vp, C.c_int, C.c_int]),
     "vamd_stream_best_path": (C.c_int, [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _vp]),
@@ -63,6 +66,29 @@ def _chk(r):
     if r is None or (isinstance(r, int) and r < 0):
         raise RuntimeError("libvosk engine error: " + _err())
     return r
+
+
+def silence_weighting_run(calls, tid_is_silence, silence_weight=1e-3, fss=3):
+    """Host-only: the recognizer's silence weighting over a call sequence.
+    calls: [(num_frames_ready, first_decoder_frame, tids, toks)]; returns the
+    (frame, delta weight) list of each call."""
+    n = len(calls)
+    ready = np.array([c[0] for c in calls] or [0], np.int32)
+    first = np.array([c[1] for c in calls] or [0], np.int32)
+    off = np.zeros(n + 1, np.int32)
+    off[1:] = np.cumsum([len(c[2]) for c in calls])
+    tids = np.array([t for c in calls for t in c[2]] or [0], np.int32)
+    toks = np.array([t for c in calls for t in c[3]] or [0], np.int32)
+    sil = np.ascontiguousarray(tid_is_silence, np.uint8)
+    cap = 1 << 20
+    oo = np.zeros(n + 1, np.int32)
+    of = np.zeros(cap, np.int32)
+    ow = np.zeros(cap, np.float32)
+    _chk(_c.vamd_silence_weighting_run(n, ready.ctypes.data, first.ctypes.data, off.ctypes.data,
+                                       tids.ctypes.data, toks.ctypes.data, sil.ctypes.data, len(sil),
+                                       silence_weight, fss, oo.ctypes.data, of.ctypes.data,
+                                       ow.ctypes.data, cap))
+    return [list(zip(of[oo[i]:oo[i + 1]].tolist(), ow[oo[i]:oo[i + 1]].tolist())) for i in range(n)]
 
 
 def plan_describe(model_dir, frames_per_chunk=0):
@@ -163,6 +189,11 @@ class Engine:
         out = np.zeros(n, np.float32)
         _c.vamd_stream_ivectors(self.h, s, out.ctypes.data, n)
         return out.reshape(-1, dim) if dim else out.reshape(0, 0)
+
+    def update_silence_weights(self, s, first_decoder_frame=0):
+        """Silence-weight the stream's i-vector statistics from its current
+        best path (Recognizer::UpdateSilenceWeights); True if active."""
+        return bool(_chk(_c.vamd_stream_update_silence_weights(self.h, s, first_decoder_frame)))
 
     def stats(self, s, cap=100000):
         out = np.zeros((cap, 8), np.float32)
