@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="decoder in order after the nnet (default: decoder of step i-1 "
                          "concurrently with the nnet of step i on a second HIP stream)")
+    ap.add_argument("--no-lattice", action="store_true",
+                    help="decoder without lattice links (default: Kaldi forward links kept in "
+                         "HBM per stream, as the reference's batch decoder produces lattices)")
     ap.add_argument("--cpu-streams", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=300.0)
     args = ap.parse_args()
@@ -129,7 +132,7 @@ def main():
     S = args.streams
     pipe = not args.no_pipeline
     e = ve.Engine(model, frames_per_chunk=51, max_streams=S, stats=True, time_kernels=True,
-                  pipeline=pipe)
+                  pipeline=pipe, lattice=not args.no_lattice)
     chunk = e.fpc * 160
     e.set_step_samples(chunk)
     base = load_wave()

@@ -43,7 +43,8 @@ int vamd_device_count(void);
  * flags: 1 = collect per-frame decoder stats, 2 = keep decoded LLH rows,
  *        4 = HIP-event timing of each stage on the engine's stream,
  *        8 = two-stream pipeline (decoder of step i-1 beside the nnet of step
- *            i; decoder results lag one step, vamd_engine_flush drains). */
+ *            i; decoder results lag one step, vamd_engine_flush drains),
+ *       16 = lattice generation (vamd_stream_lattice). */
 VamdEngine *vamd_engine_new(const char *model_dir, int frames_per_chunk, int max_streams,
                             int flags);
 void vamd_engine_free(VamdEngine *e);
@@ -76,6 +77,14 @@ long long vamd_stream_llh(VamdEngine *e, int stream, float *out, long long cap);
  * copies up to cap floats, returns the count; ivector dim 0 = no i-vector input */
 long long vamd_stream_ivectors(VamdEngine *e, int stream, float *out, long long cap);
 int vamd_engine_ivector_dim(VamdEngine *e);
+/* state-level lattice of a stream's decoder segment (engine flag 16): call
+ * with frame_begin == NULL to build it and get sizes4 = [frames, tokens,
+ * links, final costs | overflow << 30], then again with arrays of those sizes
+ * ([frames + 2], [tokens] x2, [links] x5, [final costs]) to copy it out.
+ * Link acoustic costs have the frame's cost offset removed (Kaldi GetRawLattice). */
+int vamd_stream_lattice(VamdEngine *e, int stream, int use_final, int *sizes4, int *frame_begin,
+                        int *tok_state, float *tok_cost, int *link_src, int *link_dst, int *link_arc,
+                        float *link_graph, float *link_ac, float *final_cost);
 /* silence weighting of the i-vector statistics (the reference Recognizer's
  * UpdateSilenceWeights, src/recognizer.cc:226-237): call after accepting
  * samples and before advancing; first_decoder_frame = feature frame of the

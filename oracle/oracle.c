@@ -905,6 +905,38 @@ static void commit_frame(dstate* d, int base, int* cur_state, float* cur_cost, i
   for (int i = 0; i < d->ntoks; i++) d->key[d->toks[i]] = EMPTY_KEY;
 }
 
+static void lat_link(orc_dec_result* r, int k, int src, int arc, float ac) {
+  if (!r->lat_frame_begin) return;
+  if (r->lat_nlink < r->lat_link_cap) {
+    r->lat_link_frame[r->lat_nlink] = k;
+    r->lat_link_src[r->lat_nlink] = src;
+    r->lat_link_arc[r->lat_nlink] = arc;
+    r->lat_link_ac[r->lat_nlink] = ac;
+  }
+  r->lat_nlink++;
+}
+
+/* the committed frame k: its tokens, then its epsilon links (Kaldi keeps,
+   per token, the epsilon links of its final cost: tokens are re-expanded
+   when improved, ProcessNonemitting) */
+static void lat_frame(const orc_graph* g, orc_dec_result* r, int k, const int* st, const float* co,
+                      int n, float cutoff, float cost_offset) {
+  if (!r->lat_frame_begin) return;
+  r->lat_frame_begin[k] = r->lat_ntok;
+  r->lat_cost_offset[k] = cost_offset;
+  for (int i = 0; i < n; i++) {
+    if (r->lat_ntok < r->lat_tok_cap) {
+      r->lat_tok_state[r->lat_ntok] = st[i];
+      r->lat_tok_cost[r->lat_ntok] = co[i];
+    }
+    r->lat_ntok++;
+  }
+  r->lat_frame_begin[k + 1] = r->lat_ntok;
+  for (int i = 0; i < n; i++)
+    for (int64_t a = g->eps_begin[st[i]]; a < g->arc_begin[st[i] + 1]; a++)
+      if (co[i] + g->weight[a] < cutoff) lat_link(r, k, st[i], (int)a, 0.0f);
+}
+
 int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const orc_dec_opts* o,
                int use_final, orc_dec_result* r) {
   const int S = g->num_states;
@@ -932,6 +964,8 @@ int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const or
   eps_closure(g, &d, 0, o->beam);
   int ncur = d.ntoks;
   commit_frame(&d, 0, cur_state, cur_cost, cur_idx);
+  if (r->lat_frame_begin) { r->lat_ntok = 0; r->lat_nlink = 0; }
+  lat_frame(g, r, 0, cur_state, cur_cost, ncur, o->beam, 0.0f);
   if (r->ntok) r->ntok[0] = ncur;
   if (r->best) {
     float b = INFINITY;
@@ -999,7 +1033,10 @@ int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const or
       for (int64_t a = g->arc_begin[s]; a < g->eps_begin[s]; a++) {
         float ac = cost_offset - L[g->tid2pdf[g->ilabel[a]]];
         float tot = (cur_cost[i] + ac) + g->weight[a];
-        if (tot < next_cutoff) relax(&d, g->nextstate[a], tot, (int)a, cur_idx[i]);
+        if (tot < next_cutoff) {
+          relax(&d, g->nextstate[a], tot, (int)a, cur_idx[i]);
+          lat_link(r, f + 1, s, (int)a, ac);
+        }
       }
     }
     int base = d.narena;
@@ -1007,6 +1044,7 @@ int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const or
     eps_closure(g, &d, base, next_cutoff);
     ncur = d.ntoks;
     commit_frame(&d, base, cur_state, cur_cost, cur_idx);
+    lat_frame(g, r, f + 1, cur_state, cur_cost, ncur, next_cutoff, cost_offset);
     offsets_sum += cost_offset;
     if (r->ntok) r->ntok[f + 1] = ncur;
     if (r->cutoff) r->cutoff[f] = cutoff;

@@ -149,6 +149,17 @@ typedef struct {
   float best_tot;     /* raw tot_cost of the chosen end token            */
   int end_state;
   float final_relative_cost;
+  /* optional raw lattice (LatticeFasterDecoder tokens and forward links, in
+     the order-independent formulation): frame index k = 0 for the initial
+     closure, f + 1 after frame f.  Tokens of frame k are
+     [lat_frame_begin[k], lat_frame_begin[k+1]) with (state, cost); links
+     (frame k of their destination, source state, arc, acoustic cost incl.
+     the frame's cost offset; 0 for epsilon links). NULL = not wanted. */
+  int* lat_frame_begin;  /* [F + 2] */
+  int* lat_tok_state; float* lat_tok_cost; int lat_tok_cap, lat_ntok;
+  int* lat_link_frame; int* lat_link_src; int* lat_link_arc; float* lat_link_ac;
+  int lat_link_cap, lat_nlink;
+  float* lat_cost_offset; /* [F + 1] cost offset of the links into frame k */
 } orc_dec_result;
 
 int orc_decode(const orc_graph* g, const float* llh, int num_frames, int llh_stride,

@@ -539,7 +539,12 @@ class OrcDecResult(C.Structure):
                 ("next_cutoff", C.c_void_p), ("arcs_emit", C.c_void_p), ("path", C.c_void_p),
                 ("path_cap", C.c_int), ("path_len", C.c_int), ("best_cost", C.c_double),
                 ("best_tot", C.c_float), ("end_state", C.c_int),
-                ("final_relative_cost", C.c_float)]
+                ("final_relative_cost", C.c_float),
+                ("lat_frame_begin", C.c_void_p), ("lat_tok_state", C.c_void_p),
+                ("lat_tok_cost", C.c_void_p), ("lat_tok_cap", C.c_int), ("lat_ntok", C.c_int),
+                ("lat_link_frame", C.c_void_p), ("lat_link_src", C.c_void_p),
+                ("lat_link_arc", C.c_void_p), ("lat_link_ac", C.c_void_p),
+                ("lat_link_cap", C.c_int), ("lat_nlink", C.c_int), ("lat_cost_offset", C.c_void_p)]
 
 
 class OracleGraph:
@@ -567,7 +572,7 @@ class OracleGraph:
                           self.final.ctypes.data, self.tid2pdf.ctypes.data)
 
     def decode(self, llh: np.ndarray, beam=13.0, max_active=7000, min_active=200,
-               beam_delta=0.5, use_final=True):
+               beam_delta=0.5, use_final=True, lattice=False):
         llh = np.ascontiguousarray(llh, np.float32)
         F = llh.shape[0]
         ntok = np.zeros(F + 1, np.int32)
@@ -579,16 +584,38 @@ class OracleGraph:
         path = np.zeros(cap, np.int32)
         res = OrcDecResult(ntok.ctypes.data, best.ctypes.data, cut.ctypes.data, ncut.ctypes.data,
                            ex.ctypes.data, path.ctypes.data, cap, 0, 0.0, 0.0, -1, 0.0)
+        if lattice:
+            tcap, lcap = 4000 * (F + 1) + 4096, 16000 * (F + 1) + 16384
+            lat = dict(frame_begin=np.zeros(F + 2, np.int32), tok_state=np.zeros(tcap, np.int32),
+                       tok_cost=np.zeros(tcap, np.float32), link_frame=np.zeros(lcap, np.int32),
+                       link_src=np.zeros(lcap, np.int32), link_arc=np.zeros(lcap, np.int32),
+                       link_ac=np.zeros(lcap, np.float32), cost_offset=np.zeros(F + 1, np.float32))
+            res.lat_frame_begin = lat["frame_begin"].ctypes.data
+            res.lat_tok_state, res.lat_tok_cost = lat["tok_state"].ctypes.data, lat["tok_cost"].ctypes.data
+            res.lat_tok_cap = tcap
+            res.lat_link_frame, res.lat_link_src = lat["link_frame"].ctypes.data, lat["link_src"].ctypes.data
+            res.lat_link_arc, res.lat_link_ac = lat["link_arc"].ctypes.data, lat["link_ac"].ctypes.data
+            res.lat_link_cap = lcap
+            res.lat_cost_offset = lat["cost_offset"].ctypes.data
         o = OrcDecOpts(beam, beam_delta, max_active, min_active)
         rc = lib().orc_decode(C.byref(self.g), llh.ctypes.data_as(C.c_void_p), C.c_int(F),
                               C.c_int(llh.shape[1]), C.byref(o), C.c_int(int(use_final)),
                               C.byref(res))
         p = path[:res.path_len].copy()
         words = [int(self.olabel[a]) for a in p if self.olabel[a] != 0]
-        return dict(rc=rc, ntok=ntok, best=best, cutoff=cut[:F], next_cutoff=ncut[:F],
-                    arcs_emit=ex[:F], path=p, words=words, best_cost=res.best_cost,
-                    best_tot=res.best_tot, end_state=res.end_state,
-                    final_relative_cost=res.final_relative_cost)
+        out = dict(rc=rc, ntok=ntok, best=best, cutoff=cut[:F], next_cutoff=ncut[:F],
+                   arcs_emit=ex[:F], path=p, words=words, best_cost=res.best_cost,
+                   best_tot=res.best_tot, end_state=res.end_state,
+                   final_relative_cost=res.final_relative_cost)
+        if lattice:
+            assert res.lat_ntok <= res.lat_tok_cap and res.lat_nlink <= res.lat_link_cap
+            nt, nl = res.lat_ntok, res.lat_nlink
+            out["lattice"] = dict(
+                frame_begin=lat["frame_begin"], tok_state=lat["tok_state"][:nt],
+                tok_cost=lat["tok_cost"][:nt], link_frame=lat["link_frame"][:nl],
+                link_src=lat["link_src"][:nl], link_arc=lat["link_arc"][:nl],
+                link_ac=lat["link_ac"][:nl], cost_offset=lat["cost_offset"])
+        return out
 
 
 class OracleModel:

@@ -591,6 +591,14 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   dec_.lds_frame_tokens = DecoderLdsFrameTokens();
   if (const char* lt = getenv("VOSK_AMD_LDS_FRAME_TOKENS")) dec_.lds_frame_tokens = atoi(lt);
   dec_.arena_cap = cfg_.arena_tokens;
+  dec_.links = nullptr;
+  dec_.lat_frames = nullptr;
+  dec_.link_cap = cfg_.lattice_links;
+  dec_.lat_frame_cap = cfg_.lattice_frames;
+  if (cfg_.lattice) {
+    dec_.links = (int4*)DevAlloc(sizeof(int4) * (size_t)S * cfg_.lattice_links);
+    dec_.lat_frames = (LatFrame*)DevAlloc(sizeof(LatFrame) * (size_t)S * cfg_.lattice_frames);
+  }
   d_slots_ = (DecSlot*)DevAlloc(sizeof(DecSlot) * S);
   HIPCHECK(hipMemset(d_slots_, 0, sizeof(DecSlot) * S));
   dec_.slots = d_slots_;
@@ -1303,6 +1311,31 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
     return;
   }
   VAMD_ERR("traceback path buffer could not be sized");
+}
+
+void Engine::GetRawLattice(int slot, bool use_final, RawLattice* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  FlushLocked();
+  *out = RawLattice();
+  if (!dec_.links) return;
+  DecSlot st;
+  HIPCHECK(hipMemcpy(&st, d_slots_ + slot, sizeof(DecSlot), hipMemcpyDeviceToHost));
+  if (slots_.at(slot).decoded == 0 && st.frames == 0 && st.arena_used == 0) return;
+  const int nf = std::min(st.frames + 1, dec_.lat_frame_cap);
+  std::vector<LatFrame> frames(nf);
+  std::vector<int2> arena(st.arena_used);
+  const long long nl = std::min(st.links_used, dec_.link_cap);
+  std::vector<int4> links(nl);
+  HIPCHECK(hipMemcpy(frames.data(), dec_.lat_frames + (size_t)slot * dec_.lat_frame_cap,
+                     sizeof(LatFrame) * nf, hipMemcpyDeviceToHost));
+  if (!arena.empty())
+    HIPCHECK(hipMemcpy(arena.data(), dec_.arena + (size_t)slot * dec_.arena_cap, sizeof(int2) * arena.size(),
+                       hipMemcpyDeviceToHost));
+  if (nl > 0)
+    HIPCHECK(hipMemcpy(links.data(), dec_.links + (size_t)slot * dec_.link_cap, sizeof(int4) * nl,
+                       hipMemcpyDeviceToHost));
+  BuildRawLattice(md_->graph, md_->graph.start, frames, arena, links, use_final, out);
+  if (st.lat_ovf || st.frames + 1 > dec_.lat_frame_cap || st.err) out->overflow = true;
 }
 
 int Engine::IvectorFramesReady(int slot) const {

@@ -22,6 +22,7 @@
 #include "model_io.h"
 #include "nnet_plan.h"
 #include "resample.h"
+#include "lattice.h"
 #include "silence.h"
 
 namespace vamd {
@@ -66,6 +67,11 @@ struct EngineConfig {
   // per-job i-vectors double-buffered).  Results lag two steps; every call
   // that reads or resets decoder state drains the pipeline first.
   bool pipeline = false;
+  // Lattice generation: the decoder keeps Kaldi's forward links in HBM per
+  // stream (engine_dev.h LatFrame); GetRawLattice reads the segment's.
+  bool lattice = false;
+  long long lattice_links = 1 << 22;  // link arena per stream (16 B each)
+  int lattice_frames = 1 << 14;       // frames per decoder segment with a lattice
 };
 
 // HIP-event times accumulated on the engine stream (time_kernels).
@@ -145,6 +151,9 @@ class Engine {
   const std::vector<float>& ChunkIvectors(int slot) const { return slots_.at(slot).ivecs; }
   int IvectorDim() const { return use_iv_ ? plan_.ivector_dim : 0; }
   void DecodeExternal(int slot, const float* llh, int nframes, bool reset);
+  // Canonical state-level lattice of the stream's decoder segment (empty
+  // without EngineConfig::lattice); use_final: final costs if any token is final.
+  void GetRawLattice(int slot, bool use_final, RawLattice* out);
   // Silence weighting of the i-vector statistics (Recognizer::UpdateSilenceWeights,
   // src/recognizer.cc:226-237): traceback of the stream's best path, weight
   // changes for the feature frames ready once the accepted samples are

@@ -118,9 +118,26 @@ struct DecSlot {
   int parity;       // which posmap half holds the current frame
   int stamp;        // epsilon-closure round stamp
   int err;          // bit 0: token list overflow, bit 1: arena overflow, bit 2: no tokens
-  int pad;
+  int lat_ovf;      // lattice: 1 = link arena or frame table overflowed (results fall back to 1-best)
   double offset_sum;
   unsigned long long best_key;  // min over current tokens of (ordered cost << 32 | state)
+  long long links_used;         // lattice links written since the reset
+};
+
+// ---- lattice (LatticeFasterDecoder forward links, kept in HBM per stream).
+// A raw link {src, arc, acoustic cost, tot}: emitting links carry the arena
+// index of their source token (the destination is the next frame's token of
+// arcs[arc].nextstate), epsilon links src = -1 (source and destination are
+// tokens of the same frame: the arc's source and next state; relaxations
+// with a stale source cost repeat the link, the host keeps one per arc).
+// Links whose tot is not below the frame's final cutoff are dropped by the
+// host (the kernel writes every relaxation below the seed bound).
+struct LatFrame {   // per decoded frame (index 0 = InitDecoding's closure)
+  int tok_base, ntok;      // arena slots [tok_base, tok_base + ntok) (dead slots: prev == -2)
+  long long link_begin, link_end;
+  float cutoff;            // tokens and links of this frame are below it
+  float cost_offset;       // cost offset of the emitting links INTO this frame
+  int pad0, pad1;
 };
 
 // ---- online i-vector extraction (kernels.hip ivector_kernel)
@@ -228,6 +245,10 @@ struct DecArgs {
   int max_tok;
   int lds_frame_tokens;   // frames with more current tokens use the global maps
   long long arena_cap;
+  int4* links;            // [slots][link_cap] raw lattice links (nullptr: no lattice)
+  LatFrame* lat_frames;   // [slots][lat_frame_cap]
+  long long link_cap;
+  int lat_frame_cap;
 };
 
 struct TraceArgs {

@@ -1241,11 +1241,12 @@ struct DecShared {
   int scan[DT + 1];   // exclusive prefix sums of the chunk's degrees
   int abeg[DT];       // first arc per chunk token
   float tcost[DT];    // cost per chunk token
+  int tsrc[DT];       // arena index per chunk token (lattice links)
   unsigned hist[256];
   unsigned long long red_u[DW];
   float red_f[DW];
   int red_i[DW];
-  int n_new, n_next, n_front0, total, sel_k, ovf;
+  int n_new, n_next, n_front0, total, sel_k, ovf, n_links, lat_ovf;
   unsigned sel_prefix, sel_mask;
   float seed;
   int bad;
@@ -1396,6 +1397,25 @@ struct DecPtrs {
   int2* arena;
 };
 
+// Lattice link of a relaxation (see LatFrame in engine_dev.h): one LDS
+// counter bump per wave (ballot / popcount), then a 16-byte store into the
+// stream's link arena after the links of the previous frames.
+__device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long long used, int slot,
+                                          int src, int arc, float ac, float tot) {
+  const unsigned long long m = __ballot(1);
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(&sh.n_links, __popcll(m));
+  base = __shfl(base, leader, 64);
+  const int off = __popcll(m & ((1ull << lane) - 1ull));
+  const long long pos = used + base + off;
+  if (pos < a.link_cap)
+    a.links[(long long)slot * a.link_cap + pos] = make_int4(src, arc, __float_as_int(ac), __float_as_int(tot));
+  else
+    sh.lat_ovf = 1;
+}
+
 // relax dest with (tot, arc); appends a newly created token to the frame
 // list.  Returns 1 if improved, 2 if created (created implies improved).
 __device__ __forceinline__ int relax(const DecArgs& a, DecShared& sh, const DecPtrs& p, int dest,
@@ -1425,7 +1445,7 @@ __device__ __forceinline__ void push_front(const DecArgs& a, DecShared& sh, int*
 // ProcessNonemitting: epsilon closure in rounds over frontiers that only
 // hold states with epsilon arcs (round 0: created by the emitting pass).
 __device__ void eps_closure(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st, float cutoff,
-                            int nfront, int* arcs_eps) {
+                            int nfront, int* arcs_eps, int slot) {
   int* front = p.fa;
   int* next = p.fb;
   int examined = 0;
@@ -1459,9 +1479,12 @@ __device__ void eps_closure(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot
         const int arc = sh.abeg[j] + (it - sh.scan[j]);
         const int4 A = a.arcs[arc];
         const float tot = sh.tcost[j] + __int_as_float(A.y);
-        if (tot < cutoff && relax(a, sh, p, A.x, tot, arc) && ((unsigned)A.w & kDestEps) &&
-            atomicExch(&p.stamp[A.x], stamp) != stamp)
-          push_front(a, sh, next, &sh.n_next, A.x);
+        if (tot < cutoff) {
+          if (a.links) emit_link(a, sh, st.links_used, slot, -1, arc, 0.0f, tot);
+          if (relax(a, sh, p, A.x, tot, arc) && ((unsigned)A.w & kDestEps) &&
+              atomicExch(&p.stamp[A.x], stamp) != stamp)
+            push_front(a, sh, next, &sh.n_next, A.x);
+        }
       }
       __syncthreads();
     }
@@ -1509,6 +1532,8 @@ __device__ void commit(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st,
       }
       const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)s;
       bk = tk < bk ? tk : bk;
+    } else if (ok) {
+      p.arena[base + j] = make_int2(-2, -1);  // dead list entry (lattice readers skip it)
     }
     AG_ST(&p.key[s], kEmpty);
   }
@@ -1605,11 +1630,13 @@ __device__ __forceinline__ int lds_find(const FrameLds& t, int s) {
 
 __device__ float expand_emitting_lds(const DecArgs& a, DecShared& sh, const FrameLds& t,
                                      const TokView& tv, int ntok, float cutoff, float cost_offset,
-                                     const float* Lp, int mode, float bound, int* examined) {
+                                     const float* Lp, int mode, float bound, int* examined,
+                                     const DecPtrs& p, const DecSlot& st, int slot) {
   float m = __int_as_float(0x7f800000);
+  const bool lat = a.links != nullptr && mode == 1;
   for (int c0 = 0; c0 < ntok; c0 += DT) {
     const int i = c0 + threadIdx.x;
-    int deg = 0, ab = 0;
+    int deg = 0, ab = 0, src = 0;
     float c = 0.0f;
     if (i < ntok) {
       c = tv.c(i);
@@ -1617,11 +1644,13 @@ __device__ float expand_emitting_lds(const DecArgs& a, DecShared& sh, const Fram
         const int4 si = a.sinfo[tv.s(i)];
         ab = si.x;
         deg = si.y - si.x;
+        if (lat) src = st.cur_base + AG_LD(&p.cp[i]);
       }
     }
     block_scan(sh, deg);
     sh.abeg[threadIdx.x] = ab;
     sh.tcost[threadIdx.x] = c;
+    sh.tsrc[threadIdx.x] = src;
     __syncthreads();
     const int total = sh.total;
     *examined += total;
@@ -1633,6 +1662,7 @@ __device__ float expand_emitting_lds(const DecArgs& a, DecShared& sh, const Fram
       const float tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
       m = fminf(m, tot);
       if (mode == 1 && tot < bound) {
+        if (lat) emit_link(a, sh, st.links_used, slot, sh.tsrc[j], arc, ac, tot);
         const int r = relax_lds(sh, t, A.x, tot, arc);
         if (r >= 0 && (r & 3) == 2 && ((unsigned)A.w & kDestEps)) {
           const int q = atomicAdd(&sh.n_front0, 1);
@@ -1647,7 +1677,7 @@ __device__ float expand_emitting_lds(const DecArgs& a, DecShared& sh, const Fram
 }
 
 __device__ void eps_closure_lds(const DecArgs& a, DecShared& sh, const FrameLds& t, float cutoff,
-                                int nfront, int* arcs_eps) {
+                                int nfront, int* arcs_eps, const DecSlot& st, int slot) {
   unsigned short* front = t.fa;
   unsigned short* next = t.fb;
   int examined = 0, round = 0;
@@ -1681,6 +1711,7 @@ __device__ void eps_closure_lds(const DecArgs& a, DecShared& sh, const FrameLds&
         const int4 A = a.arcs[arc];
         const float tot = sh.tcost[j] + __int_as_float(A.y);
         if (tot < cutoff) {
+          if (a.links) emit_link(a, sh, st.links_used, slot, -1, arc, 0.0f, tot);
           const int r = relax_lds(sh, t, A.x, tot, arc);
           if (r >= 0 && (r & 3) && ((unsigned)A.w & kDestEps) &&
               atomicExch(&t.hst[r >> 2], round) != round) {
@@ -1741,6 +1772,8 @@ __device__ void commit_lds(const DecArgs& a, DecShared& sh, DecPtrs& p, const Fr
       }
       const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)s;
       bk = tk < bk ? tk : bk;
+    } else if (ok) {
+      p.arena[base + j] = make_int2(-2, -1);  // dead list entry (lattice readers skip it)
     }
   }
   bk = block_min_u64(sh, bk);  // ends with a barrier: the table is no longer read
@@ -1806,11 +1839,12 @@ void LdsHashSelfTest(int n, int blocks, int* out) {
 // mode 0 = minimum only, 1 = relax below `bound` (+ minimum)
 __device__ float expand_emitting(const DecArgs& a, DecShared& sh, DecPtrs& p, const TokView& tv,
                                  int ntok, float cutoff, float cost_offset, const float* Lp,
-                                 int mode, float bound, int* examined) {
+                                 int mode, float bound, int* examined, const DecSlot& st, int slot) {
   float m = __int_as_float(0x7f800000);
+  const bool lat = a.links != nullptr && mode == 1;
   for (int c0 = 0; c0 < ntok; c0 += DT) {
     const int i = c0 + threadIdx.x;
-    int deg = 0, ab = 0;
+    int deg = 0, ab = 0, src = 0;
     float c = 0.0f;
     if (i < ntok) {
       c = tv.c(i);
@@ -1818,11 +1852,13 @@ __device__ float expand_emitting(const DecArgs& a, DecShared& sh, DecPtrs& p, co
         const int4 si = a.sinfo[tv.s(i)];
         ab = si.x;
         deg = si.y - si.x;
+        if (lat) src = st.cur_base + AG_LD(&p.cp[i]);
       }
     }
     block_scan(sh, deg);
     sh.abeg[threadIdx.x] = ab;
     sh.tcost[threadIdx.x] = c;
+    sh.tsrc[threadIdx.x] = src;
     __syncthreads();
     const int total = sh.total;
     *examined += total;
@@ -1834,6 +1870,7 @@ __device__ float expand_emitting(const DecArgs& a, DecShared& sh, DecPtrs& p, co
       const float tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
       m = fminf(m, tot);
       if (mode == 1 && tot < bound) {
+        if (lat) emit_link(a, sh, st.links_used, slot, sh.tsrc[j], arc, ac, tot);
         if (relax(a, sh, p, A.x, tot, arc) == 2 && ((unsigned)A.w & kDestEps))
           push_front(a, sh, p.fa, &sh.n_front0, A.x);
       }
@@ -1841,6 +1878,28 @@ __device__ float expand_emitting(const DecArgs& a, DecShared& sh, DecPtrs& p, co
     __syncthreads();
   }
   return block_min_f(sh, m);
+}
+
+// after a commit (all threads, past its barriers): the frame's lattice
+// record; every thread advances its copy of links_used identically
+__device__ void lat_frame_done(const DecArgs& a, DecShared& sh, DecSlot& st, int slot, int index,
+                               float cutoff, float cost_offset) {
+  const int nl = sh.n_links;
+  if (threadIdx.x == 0) {
+    if (index < a.lat_frame_cap) {
+      LatFrame F;
+      F.tok_base = st.cur_base;
+      F.ntok = st.arena_used - st.cur_base;
+      F.link_begin = st.links_used;
+      F.link_end = st.links_used + nl;
+      F.cutoff = cutoff;
+      F.cost_offset = cost_offset;
+      F.pad0 = F.pad1 = 0;
+      a.lat_frames[(long long)slot * a.lat_frame_cap + index] = F;
+    }
+  }
+  if (index >= a.lat_frame_cap || sh.lat_ovf) st.lat_ovf = 1;
+  st.links_used += nl;
 }
 
 template <bool PROF>
@@ -1874,7 +1933,11 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   p.fa = a.front_a + (long long)slot * a.max_tok;
   p.fb = a.front_b + (long long)slot * a.max_tok;
   p.arena = a.arena + (long long)slot * a.arena_cap;
-  if (threadIdx.x == 0) sh.bad = 0;
+  if (threadIdx.x == 0) {
+    sh.bad = 0;
+    sh.n_links = 0;
+    sh.lat_ovf = 0;
+  }
   int arcs_eps = 0;
   bool lds = false;
   // optional phase clocks (diagnostics): thread 0 stamps s_memtime
@@ -1895,6 +1958,8 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     st.frames = 0;
     st.offset_sum = 0.0;
     st.err = 0;
+    st.links_used = 0;
+    st.lat_ovf = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
       sh.n_new = 1;
@@ -1904,9 +1969,10 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       AG_ST(&p.fa[0], a.start_state);
     }
     __syncthreads();
-    eps_closure(a, sh, p, st, a.beam, 1, &arcs_eps);
+    eps_closure(a, sh, p, st, a.beam, 1, &arcs_eps, slot);
     float b;
     commit(a, sh, p, st, TS, TC, &lds, a.beam, &b);
+    if (a.links) lat_frame_done(a, sh, st, slot, 0, a.beam, 0.0f);
   } else if (st.ntok > 0 && st.ntok <= kTokLds) {
     for (int i = threadIdx.x; i < st.ntok; i += DT) {
       TS[i] = AG_LD(&p.cs[i]);
@@ -1983,6 +2049,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
         sh.n_new = 0;
         sh.n_front0 = 0;
         sh.ovf = 0;
+        sh.n_links = 0;
       }
     }
     __syncthreads();
@@ -2002,21 +2069,22 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     if (try_lds) {
       if (seed != __int_as_float(0x7f800000)) {
         const float m = expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
-                                            &examined);
+                                            &examined, p, st, slot);
         next_cutoff = seed;
         if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
       } else {
         const float m = expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
-                                            &examined);
+                                            &examined, p, st, slot);
         next_cutoff = seed;
         if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
         int dummy = 0;
-        expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy);
+        expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy, p, st,
+                            slot);
       }
       __syncthreads();
       DEC_PHASE(2);
       if (prof) pacc[3] += sh.n_new;  // tokens created by the emitting pass
-      if (!sh.ovf) eps_closure_lds(a, sh, t, next_cutoff, sh.n_front0, &arcs_eps);
+      if (!sh.ovf) eps_closure_lds(a, sh, t, next_cutoff, sh.n_front0, &arcs_eps, st, slot);
       __syncthreads();
       DEC_PHASE(4);
     }
@@ -2033,6 +2101,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
         if (threadIdx.x == 0) {
           sh.n_new = 0;
           sh.n_front0 = 0;
+          sh.n_links = 0;  // the LDS attempt's links are rewritten
         }
         __syncthreads();
       }
@@ -2040,25 +2109,26 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       arcs_eps = 0;
       if (seed != __int_as_float(0x7f800000)) {
         const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
-                                        &examined);
+                                        &examined, st, slot);
         next_cutoff = seed;
         if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
       } else {
         const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
-                                        &examined);
+                                        &examined, st, slot);
         next_cutoff = seed;
         if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
         int dummy = 0;
-        expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy);
+        expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy, st, slot);
       }
       __syncthreads();
       DEC_PHASE(2);
-      eps_closure(a, sh, p, st, next_cutoff, sh.n_front0, &arcs_eps);
+      eps_closure(a, sh, p, st, next_cutoff, sh.n_front0, &arcs_eps, slot);
       DEC_PHASE(4);
       commit(a, sh, p, st, TS, TC, &lds, next_cutoff, &new_best);
     }
     DEC_PHASE(5);
     if (prof) pacc[7]++;
+    if (a.links) lat_frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset);
     st.offset_sum += (double)cost_offset;
     st.frames++;
     if (threadIdx.x == 0 && a.stats) {

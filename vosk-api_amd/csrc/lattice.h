@@ -1,0 +1,110 @@
+// Lattices of the decoder's segment (host side).
+//
+// The decode kernel keeps Kaldi's forward links (LatticeFasterDecoder /
+// LatticeIncrementalDecoder [K]; the reference builds its results from the
+// decoder's lattice, src/recognizer.cc:669-729 GetResult -> MbrResult /
+// NbestResult / NlsmlResult, and src/batch_recognizer.cc:43-107) in HBM per
+// stream: raw relaxations, LatFrame records and the token arena
+// (engine_dev.h).  RawLattice is the canonical state-level lattice built from
+// them (GetRawLattice): tokens per frame, deduplicated links below each
+// frame's cutoff, graph / acoustic costs, final costs.  The word-level steps
+// (lattice-beam pruning, determinization, MBR) live in lattice.cc.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "engine_dev.h"
+
+namespace vamd {
+
+struct Graph;
+struct TransitionTables;
+
+struct RawLattice {
+  int num_frames = 0;                // decoded frames; token frames are 0..num_frames
+  std::vector<int> frame_begin;      // [num_frames + 2] tokens of frame k: [frame_begin[k], frame_begin[k+1])
+  std::vector<int> tok_state;
+  std::vector<float> tok_cost;       // decoder tot_cost (with the frames' cost offsets)
+  struct Link {
+    int src, dst;                    // token ids
+    int arc;                         // graph arc (ilabel = transition-id or 0, olabel = word or 0)
+    float graph_cost;                // arc weight
+    float acoustic_cost;             // decoder's ac cost minus the frame's cost offset (0 for epsilon)
+  };
+  std::vector<Link> links;           // sorted by (destination frame, src, arc)
+  std::vector<float> final_cost;     // per token of the last frame (+inf: not final); empty = all final with 0
+  bool overflow = false;             // link arena / frame table overflowed: incomplete
+};
+
+// Canonical lattice from the device records of one stream: frames [0, F]
+// (LatFrame), the token arena and the raw links.  Dead arena entries
+// (prev == -2) are skipped; emitting links whose tot is not below their
+// frame's cutoff are dropped; epsilon links are deduplicated per arc and kept
+// when (final source cost + weight) is below the cutoff.  use_final: final
+// costs of the last frame's tokens if any token is final (Kaldi GetRawLattice
+// with use_final_probs).
+void BuildRawLattice(const Graph& g, int start_state, const std::vector<LatFrame>& frames,
+                     const std::vector<int2>& arena, const std::vector<int4>& links,
+                     bool use_final, RawLattice* out);
+
+// ---- word level (lattice.cc)
+
+// A word lattice after determinization: states topologically sorted (0 =
+// start), every arc one word (0 = epsilon word), weight = (graph, acoustic)
+// pair, and the transition-ids of the frames the arc spans.
+struct WordLattice {
+  struct Arc {
+    int word, next;
+    float graph, acoustic;
+    std::vector<int> tids;
+  };
+  std::vector<std::vector<Arc>> arcs;
+  std::vector<float> final_graph, final_acoustic;  // +inf graph: not final
+  std::vector<std::vector<int>> final_tids;
+  int NumStates() const { return (int)arcs.size(); }
+};
+
+struct LatticeOptions {
+  float lattice_beam = 6.0f;
+  int max_states = 100000;  // determinization guard (falls back to the best path)
+};
+
+// Lattice-beam pruning of the raw lattice (PruneForwardLinks /
+// PruneForwardLinksFinal semantics: keep links and tokens whose best path
+// through them is within lattice_beam of the best complete path).
+void PruneRawLattice(RawLattice* lat, float lattice_beam);
+
+// Word-level determinization (DeterminizeLatticePruned [K]): one path per
+// word sequence, the best alignment, strings output as their common prefix.
+// Returns false if the guard tripped.
+bool DeterminizeToWords(const RawLattice& lat, const Graph& g, const LatticeOptions& opt,
+                        WordLattice* out);
+
+// Scale the graph part of every weight (fst::GraphLatticeScale, src/recognizer.cc:718)
+void ScaleGraph(WordLattice* lat, float scale);
+
+// Minimum Bayes risk decoding (Kaldi lat/sausages.cc MinimumBayesRisk [K]):
+// one-best words, their confidences (posteriors in the aligned bins) and
+// times (frames, from the bin averages).
+struct MbrResult {
+  std::vector<int> words;
+  std::vector<float> conf;
+  std::vector<std::pair<float, float>> times;
+};
+void MinimumBayesRisk(const WordLattice& lat, MbrResult* out);
+
+// n-best distinct word sequences (fst::ShortestPath on the determinized
+// lattice, src/recognizer.cc:484-607): words, per-word frame spans, total
+// cost split into (graph, acoustic).
+struct NbestPath {
+  std::vector<int> words;
+  std::vector<std::pair<int, int>> spans;  // [begin, end) frames of each word
+  float graph = 0, acoustic = 0;
+};
+void NbestPaths(const WordLattice& lat, int n, std::vector<NbestPath>* out);
+
+}  // namespace vamd

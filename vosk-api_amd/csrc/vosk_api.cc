@@ -207,6 +207,7 @@ struct VamdEngine {
   std::shared_ptr<ModelData> md;
   std::unique_ptr<Engine> eng;
   std::string desc;
+  RawLattice lat;  // last lattice read by vamd_stream_lattice
 };
 
 const char* vamd_last_error(void) { return g_last_error.c_str(); }
@@ -229,6 +230,7 @@ VamdEngine* vamd_engine_new(const char* model_dir, int fpc, int max_streams, int
   cfg.collect_llh = (flags & 2) != 0;
   cfg.time_kernels = (flags & 4) != 0;
   cfg.pipeline = (flags & 8) != 0;
+  cfg.lattice = (flags & 16) != 0;
   const char* d = getenv("VOSK_AMD_DEVICE");
   cfg.device = d ? atoi(d) : 0;
   const char* at = getenv("VOSK_AMD_ARENA_TOKENS");
@@ -426,6 +428,33 @@ int vamd_stream_update_silence_weights(VamdEngine* e, int s, int first_decoder_f
   API_TRY
   e->eng->UpdateSilenceWeights(s, first_decoder_frame);
   return e->eng->SilenceWeightingActive() ? 1 : 0;
+  API_CATCH(-1)
+}
+
+int vamd_stream_lattice(VamdEngine* e, int s, int use_final, int* sizes4, int* frame_begin,
+                        int* tok_state, float* tok_cost, int* link_src, int* link_dst, int* link_arc,
+                        float* link_graph, float* link_ac, float* final_cost) {
+  API_TRY
+  RawLattice& L = e->lat;
+  if (!frame_begin) e->eng->GetRawLattice(s, use_final != 0, &L);
+  sizes4[0] = L.num_frames;
+  sizes4[1] = (int)L.tok_state.size();
+  sizes4[2] = (int)L.links.size();
+  sizes4[3] = (int)L.final_cost.size() | (L.overflow ? (1 << 30) : 0);
+  if (frame_begin) {
+    std::copy(L.frame_begin.begin(), L.frame_begin.end(), frame_begin);
+    std::copy(L.tok_state.begin(), L.tok_state.end(), tok_state);
+    std::copy(L.tok_cost.begin(), L.tok_cost.end(), tok_cost);
+    for (size_t i = 0; i < L.links.size(); i++) {
+      link_src[i] = L.links[i].src;
+      link_dst[i] = L.links[i].dst;
+      link_arc[i] = L.links[i].arc;
+      link_graph[i] = L.links[i].graph_cost;
+      link_ac[i] = L.links[i].acoustic_cost;
+    }
+    std::copy(L.final_cost.begin(), L.final_cost.end(), final_cost);
+  }
+  return 0;
   API_CATCH(-1)
 }
 

@@ -35,6 +35,8 @@ _SIGS = {
     "vamd_stream_ivectors": (C.c_longlong, [_vp, C.c_int, _vp, C.c_longlong]),
     "vamd_engine_ivector_dim": (C.c_int, [_vp]),
     "vamd_stream_update_silence_weights": (C.c_int, [_vp, C.c_int, C.c_int]),
+    "vamd_stream_lattice": (C.c_int, [_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                      _vp, _vp, _vp]),
     "vamd_silence_weighting_run": (C.c_int, [C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
                                              C.c_float, C.c_int, _vp, _vp, _vp, C.c_int]),
     "vamd_stream_stats": (C.c_int, [_vp, C.c_int, _vp, C.c_int]),
@@ -115,9 +117,9 @@ def device_count():
 
 class Engine:
     def __init__(self, model_dir, frames_per_chunk=0, max_streams=8, stats=False, keep_llh=False,
-                 time_kernels=False, pipeline=False):
+                 time_kernels=False, pipeline=False, lattice=False):
         flags = ((1 if stats else 0) | (2 if keep_llh else 0) | (4 if time_kernels else 0)
-                 | (8 if pipeline else 0))
+                 | (8 if pipeline else 0) | (16 if lattice else 0))
         h = _c.vamd_engine_new(str(model_dir).encode(), frames_per_chunk, max_streams, flags)
         if not h:
             raise RuntimeError("vamd_engine_new failed: " + _err())
@@ -189,6 +191,26 @@ class Engine:
         out = np.zeros(n, np.float32)
         _c.vamd_stream_ivectors(self.h, s, out.ctypes.data, n)
         return out.reshape(-1, dim) if dim else out.reshape(0, 0)
+
+    def lattice(self, s, use_final=True):
+        """State-level lattice of the stream's decoder segment (engine built
+        with lattice=True): dict of numpy arrays."""
+        sz = np.zeros(4, np.int32)
+        _chk(_c.vamd_stream_lattice(self.h, s, 1 if use_final else 0, sz.ctypes.data, *([None] * 9)))
+        F, nt, nl = int(sz[0]), int(sz[1]), int(sz[2])
+        nfc, ovf = int(sz[3]) & ((1 << 30) - 1), bool(int(sz[3]) >> 30)
+        out = dict(frame_begin=np.zeros(F + 2, np.int32), tok_state=np.zeros(nt, np.int32),
+                   tok_cost=np.zeros(nt, np.float32), link_src=np.zeros(nl, np.int32),
+                   link_dst=np.zeros(nl, np.int32), link_arc=np.zeros(nl, np.int32),
+                   link_graph=np.zeros(nl, np.float32), link_ac=np.zeros(nl, np.float32),
+                   final_cost=np.zeros(nfc, np.float32))
+        keys = ("frame_begin", "tok_state", "tok_cost", "link_src", "link_dst", "link_arc",
+                "link_graph", "link_ac", "final_cost")
+        _chk(_c.vamd_stream_lattice(self.h, s, 1 if use_final else 0, sz.ctypes.data,
+                                    *[out[k].ctypes.data for k in keys]))
+        out["num_frames"] = F
+        out["overflow"] = ovf
+        return out
 
     def update_silence_weights(self, s, first_decoder_frame=0):
         """Silence-weight the stream's i-vector statistics from its current
