@@ -36,6 +36,18 @@ int vamd_silence_weighting_run(int ncalls, const int *num_frames_ready, const in
                                const unsigned char *tid_is_silence, int num_tids, float silence_weight,
                                int fss, int *out_off, int *out_frame, float *out_w, int cap);
 
+/* host-only: the result pipeline over a state-level lattice (the arrays of
+ * vamd_stream_lattice; arc_ilabel / arc_olabel index the graph's arcs):
+ * lattice-beam pruning, word determinization, graph scaling, MBR and n-best.
+ * Returns JSON {pruned_tokens, pruned_links, det_ok, det_states, det_arcs,
+ * mbr: {words, conf, times}, nbest: [{words, spans, graph, acoustic}]}. */
+const char *vamd_lattice_words_json(int num_frames, const int *frame_begin, const int *tok_state,
+                                    const float *tok_cost, const int *link_src, const int *link_dst,
+                                    const int *link_arc, const float *link_graph, const float *link_ac,
+                                    int nlink, const float *final_cost, int nfinal, const int *arc_ilabel,
+                                    const int *arc_olabel, int narcs, float lattice_beam, float graph_scale,
+                                    int nbest);
+
 const char *vamd_last_error(void);
 int vamd_device_count(void);
 

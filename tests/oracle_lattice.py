@@ -1,0 +1,495 @@
+"""Oracle restatement of the result pipeline over a state-level lattice
+(test infrastructure).
+
+The reference builds every result from the decoder's lattice
+(src/recognizer.cc:669-729 GetResult: GraphLatticeScale(0.9) then MbrResult
+:429-482 / NbestResult :526-607 / NlsmlResult :609-667; the batch path
+src/batch_recognizer.cc:43-107).  The algorithms are Kaldi's [K], absent from
+the reference tree: lattice-beam pruning (LatticeFasterDecoder
+PruneForwardLinks / PruneForwardLinksFinal), word-level lattice
+determinization (DeterminizeLatticePruned: one path per word sequence, its
+best alignment, residual strings, subsets equal within kDelta = 1/1024),
+MinimumBayesRisk (lat/sausages.cc, Xu et al. 2011: edit-distance forward
+pass, backward gamma accumulation, iterated hypothesis) and n-best shortest
+paths.  Parity with Kaldi is unpinned (no Kaldi here, no reference vectors
+for confidences); this restatement pins libvosk.so's C++ (csrc/lattice.cc)
+to the same algorithm.  Word alignment (WordAlignLattice) is not restated:
+both sides use the unaligned lattice (the reference's CopyLatticeForMbr path).
+"""
+import math
+
+import numpy as np
+
+F32 = np.float32
+INF = float("inf")
+
+
+def raw_from_oracle(r, graph, use_final=True):
+    """Oracle decode(lattice=True) -> the arrays of vamd_stream_lattice."""
+    L = r["lattice"]
+    fb = L["frame_begin"]
+    F = len(fb) - 2
+    ids = {}
+    for k in range(F + 1):
+        for t in range(fb[k], fb[k + 1]):
+            ids[(k, int(L["tok_state"][t]))] = t
+    src, dst, arc, gc, ac = [], [], [], [], []
+    per_frame = [[] for _ in range(F + 1)]
+    for k, s, a, x in zip(L["link_frame"], L["link_src"], L["link_arc"], L["link_ac"]):
+        emit = graph.ilabel[a] != 0
+        sid = ids[(int(k) - 1 if emit else int(k), int(s))]
+        did = ids[(int(k), int(graph.nextstate[a]))]
+        acx = F32(F32(x) - F32(L["cost_offset"][k])) if emit else F32(0)
+        per_frame[int(k)].append((sid, int(a), did, F32(graph.weight[a]), acx))
+    for k in range(F + 1):
+        for sid, a, did, g, x in sorted(per_frame[k], key=lambda z: (z[0], z[1])):
+            src.append(sid)
+            dst.append(did)
+            arc.append(a)
+            gc.append(g)
+            ac.append(x)
+    last = L["tok_state"][fb[F]:fb[F + 1]]
+    fin = graph.final[last].astype(np.float32)
+    final = fin if (use_final and np.isfinite(fin).any()) else np.zeros(0, np.float32)
+    return dict(num_frames=F, frame_begin=np.asarray(fb, np.int32),
+                tok_state=np.asarray(L["tok_state"], np.int32), tok_cost=np.asarray(L["tok_cost"], np.float32),
+                link_src=np.asarray(src, np.int32), link_dst=np.asarray(dst, np.int32),
+                link_arc=np.asarray(arc, np.int32), link_graph=np.asarray(gc, np.float32),
+                link_ac=np.asarray(ac, np.float32), final_cost=final)
+
+
+# ---------------------------------------------------------------- pruning
+def prune(L, beam):
+    F = L["num_frames"]
+    fb = L["frame_begin"]
+    N = len(L["tok_state"])
+    frame = np.zeros(N, np.int64)
+    for k in range(F + 1):
+        frame[fb[k]:fb[k + 1]] = k
+    links = list(zip(L["link_src"].tolist(), L["link_dst"].tolist(), L["link_arc"].tolist(),
+                     L["link_graph"], L["link_ac"]))
+    by_frame = [[] for _ in range(F + 1)]
+    for i, l in enumerate(links):
+        by_frame[frame[l[1]]].append(i)
+    cost = [float(F32(l[3]) + F32(l[4])) for l in links]
+    alpha = [INF] * N
+    beta = [INF] * N
+    for t in range(fb[0], fb[1]):
+        if L["tok_cost"][t] == 0.0:
+            alpha[t] = 0.0
+            break
+    for k in range(F + 1):
+        for i in by_frame[k]:
+            s, d = links[i][0], links[i][1]
+            if frame[s] != k:
+                alpha[d] = min(alpha[d], alpha[s] + cost[i])
+        ch = True
+        while ch:
+            ch = False
+            for i in by_frame[k]:
+                s, d = links[i][0], links[i][1]
+                if frame[s] == k and alpha[s] + cost[i] < alpha[d]:
+                    alpha[d] = alpha[s] + cost[i]
+                    ch = True
+    best = INF
+    fin = L["final_cost"]
+    for t in range(fb[F], fb[F + 1]):
+        fc = 0.0 if len(fin) == 0 else float(fin[t - fb[F]])
+        beta[t] = fc
+        best = min(best, alpha[t] + fc)
+    for k in range(F, -1, -1):
+        ch = True
+        while ch:
+            ch = False
+            for i in by_frame[k]:
+                s, d = links[i][0], links[i][1]
+                if frame[s] == k and cost[i] + beta[d] < beta[s]:
+                    beta[s] = cost[i] + beta[d]
+                    ch = True
+        for i in by_frame[k]:
+            s, d = links[i][0], links[i][1]
+            if frame[s] != k:
+                beta[s] = min(beta[s], cost[i] + beta[d])
+    remap = [-1] * N
+    out_state, out_cost, nfb = [], [], [0] * (F + 2)
+    for k in range(F + 1):
+        nfb[k] = len(out_state)
+        for t in range(fb[k], fb[k + 1]):
+            if not (alpha[t] + beta[t] - best <= beam):
+                continue
+            remap[t] = len(out_state)
+            out_state.append(int(L["tok_state"][t]))
+            out_cost.append(L["tok_cost"][t])
+        nfb[k + 1] = len(out_state)
+    ls, ld, la, lg, lx = [], [], [], [], []
+    for i, (s, d, a, g, x) in enumerate(links):
+        if remap[s] < 0 or remap[d] < 0:
+            continue
+        if not (alpha[s] + cost[i] + beta[d] - best <= beam):
+            continue
+        ls.append(remap[s]); ld.append(remap[d]); la.append(a); lg.append(g); lx.append(x)
+    nfin = [fin[t - fb[F]] for t in range(fb[F], fb[F + 1]) if remap[t] >= 0] if len(fin) else []
+    return dict(num_frames=F, frame_begin=np.asarray(nfb, np.int32), tok_state=np.asarray(out_state, np.int32),
+                tok_cost=np.asarray(out_cost, np.float32), link_src=np.asarray(ls, np.int32),
+                link_dst=np.asarray(ld, np.int32), link_arc=np.asarray(la, np.int32),
+                link_graph=np.asarray(lg, np.float32), link_ac=np.asarray(lx, np.float32),
+                final_cost=np.asarray(nfin, np.float32))
+
+
+# ---------------------------------------------------------- determinization
+def _cmp(x, y):  # Kaldi LatticeWeight Compare: 1 if x is better
+    fx, fy = F32(x[0] + x[1]), F32(y[0] + y[1])
+    if fx < fy:
+        return 1
+    if fx > fy:
+        return -1
+    if x[0] < y[0]:
+        return 1
+    if x[0] > y[0]:
+        return -1
+    if x[1] < y[1]:
+        return 1
+    if x[1] > y[1]:
+        return -1
+    return 0
+
+
+def _better(e, f):  # (weight, string) order
+    c = _cmp(e[1], f[1])
+    if c != 0:
+        return c > 0
+    if len(e[2]) != len(f[2]):
+        return len(e[2]) < len(f[2])
+    return e[2] < f[2]
+
+
+def determinize(L, ilabel, olabel):
+    """-> (arcs per state [(word, next, g, a, tids)], finals [(g, a, tids) | None]),
+    states topologically sorted as the C++ does."""
+    N = len(L["tok_state"])
+    F = L["num_frames"]
+    fb = L["frame_begin"]
+    if N == 0:
+        return [], []
+    outl = [[] for _ in range(N)]
+    links = list(zip(L["link_src"].tolist(), L["link_dst"].tolist(), L["link_arc"].tolist(),
+                     L["link_graph"], L["link_ac"]))
+    for i, l in enumerate(links):
+        outl[l[0]].append(i)
+    fin = [INF] * N
+    for t in range(fb[F], fb[F + 1]):
+        fin[t] = F32(0) if len(L["final_cost"]) == 0 else L["final_cost"][t - fb[F]]
+    start = next((t for t in range(fb[0], fb[1]) if L["tok_cost"][t] == 0.0), -1)
+    if start < 0:
+        return [], []
+
+    def times(w, g, a):
+        return (F32(w[0] + F32(g)), F32(w[1] + F32(a)))
+
+    def closure(sub):
+        at = {e[0]: i for i, e in enumerate(sub)}
+        work = list(range(len(sub)))
+        while work:
+            i = work.pop()
+            e = sub[i]
+            for li in outl[e[0]]:
+                s, d, a, g, x = links[li]
+                if olabel[a] != 0:
+                    continue
+                n = (d, times(e[1], g, x), e[2] + ((int(ilabel[a]),) if ilabel[a] != 0 else ()))
+                if d not in at:
+                    at[d] = len(sub)
+                    work.append(len(sub))
+                    sub.append(n)
+                elif _better(n, sub[at[d]]):
+                    sub[at[d]] = n
+                    work.append(at[d])
+        sub.sort(key=lambda e: e[0])
+        return sub
+
+    def normalize(sub):
+        tot = sub[0][1]
+        for e in sub:
+            if _cmp(e[1], tot) > 0:
+                tot = e[1]
+        n = len(sub[0][2])
+        for e in sub:
+            j = 0
+            while j < n and j < len(e[2]) and e[2][j] == sub[0][2][j]:
+                j += 1
+            n = j
+        prefix = list(sub[0][2][:n])
+        out = [(e[0], (F32(e[1][0] - tot[0]), F32(e[1][1] - tot[1])), e[2][n:]) for e in sub]
+        return out, tot, prefix
+
+    delta = 1.0 / 1024.0
+    index, subsets = {}, []
+
+    def find_or_add(sub):
+        key = tuple((e[0], e[2]) for e in sub)
+        for sid in index.get(key, []):
+            o = subsets[sid]
+            if all(abs(float(o[i][1][0]) - float(sub[i][1][0])) <= delta and
+                   abs(float(o[i][1][1]) - float(sub[i][1][1])) <= delta for i in range(len(o))):
+                return sid, False
+        sid = len(subsets)
+        subsets.append(sub)
+        index.setdefault(key, []).append(sid)
+        return sid, True
+
+    s0 = closure([(start, (F32(0), F32(0)), ())])
+    find_or_add(s0)
+    arcs = [[]]
+    queue = [0]
+    qi = 0
+    while qi < len(queue):
+        sid = queue[qi]
+        qi += 1
+        by_word = {}
+        for e in subsets[sid]:
+            for li in outl[e[0]]:
+                s, d, a, g, x = links[li]
+                w = int(olabel[a])
+                if w == 0:
+                    continue
+                n = (d, times(e[1], g, x), e[2] + ((int(ilabel[a]),) if ilabel[a] != 0 else ()))
+                v = by_word.setdefault(w, [])
+                for j, y in enumerate(v):
+                    if y[0] == d:
+                        if _better(n, y):
+                            v[j] = n
+                        break
+                else:
+                    v.append(n)
+        for w in sorted(by_word):
+            sub = closure(by_word[w])
+            sub, tot, prefix = normalize(sub)
+            dst, added = find_or_add(sub)
+            if added:
+                queue.append(dst)
+                arcs.append([])
+            arcs[sid].append((w, dst, tot[0], tot[1], prefix))
+    S = len(subsets)
+    finals = [None] * S
+    for s in range(S):
+        best = None
+        for e in subsets[s]:
+            if fin[e[0]] == INF:
+                continue
+            c = (e[0], (F32(e[1][0] + F32(fin[e[0]])), e[1][1]), e[2])
+            if best is None or _better(c, best):
+                best = c
+        if best is not None:
+            finals[s] = (best[1][0], best[1][1], list(best[2]))
+    # topological order: DFS stack as the C++ (arcs pushed in reverse)
+    indeg = [0] * S
+    for s in range(S):
+        for a in arcs[s]:
+            indeg[a[1]] += 1
+    order, st = [], [0]
+    while st:
+        s = st.pop()
+        order.append(s)
+        for a in reversed(arcs[s]):
+            indeg[a[1]] -= 1
+            if indeg[a[1]] == 0:
+                st.append(a[1])
+    pos = {s: i for i, s in enumerate(order)}
+    W = [[] for _ in range(S)]
+    Fi = [None] * S
+    for s in range(S):
+        W[pos[s]] = [(w, pos[d], g, a, p) for (w, d, g, a, p) in arcs[s]]
+        Fi[pos[s]] = finals[s]
+    return W, Fi
+
+
+def scale_graph(W, Fi, scale):
+    W = [[(w, d, F32(F32(g) * F32(scale)), a, p) for (w, d, g, a, p) in v] for v in W]
+    Fi = [None if f is None else (F32(F32(f[0]) * F32(scale)), f[1], f[2]) for f in Fi]
+    return W, Fi
+
+
+# -------------------------------------------------------------------- MBR
+def _logadd(x, y):
+    if x < y:
+        diff = x - y
+        x = y
+    else:
+        diff = y - x
+    if diff >= math.log(np.finfo(np.float64).eps):
+        return x + math.log1p(math.exp(diff))
+    return x
+
+
+def mbr(W, Fi):
+    S = len(W)
+    if S == 0:
+        return dict(words=[], conf=[], times=[])
+    N = S + 1
+    arcs, pre = [], [[] for _ in range(N + 1)]
+
+    def add(s, e, w, ll):
+        pre[e].append(len(arcs))
+        arcs.append((w, s, e, ll))
+    t = [-1] * (S + 1)
+    t[0] = 0
+    for s in range(S):
+        for (w, d, g, a, p) in W[s]:
+            add(s + 1, d + 1, w, -float(F32(F32(g) + F32(a))))
+            t[d] = t[s] + len(p)
+        if Fi[s] is not None:
+            add(s + 1, N, 0, -float(F32(F32(Fi[s][0]) + F32(Fi[s][1]))))
+            t[S] = t[s] + len(Fi[s][2])
+    st = [0] * (N + 1)
+    for s in range(S + 1):
+        st[s + 1] = max(0, t[s])
+    best = [-INF] * (N + 1)
+    frm = [-1] * (N + 1)
+    best[1] = 0.0
+    for n in range(2, N + 1):
+        for ai in pre[n]:
+            w, s, e, ll = arcs[ai]
+            v = best[s] + ll
+            if v > best[n]:
+                best[n] = v
+                frm[n] = ai
+    R = []
+    n = N
+    while n > 1 and frm[n] >= 0:
+        if arcs[frm[n]][0] != 0:
+            R.append(arcs[frm[n]][0])
+        n = arcs[frm[n]][1]
+    R.reverse()
+
+    def l(a, b, pen=False):
+        return 0.0 if a == b else (1.0 + 1.0e-05 if pen else 1.0)
+
+    result = None
+    for it in range(1000):
+        R = [0] + [x for w in R if w != 0 for x in (w, 0)]
+        Q = len(R)
+        alpha = [0.0] * (N + 1)
+        ad = [[0.0] * (Q + 1) for _ in range(N + 1)]
+        bd = [[0.0] * (Q + 1) for _ in range(N + 1)]
+        ada = [0.0] * (Q + 1)
+        alpha[1] = 0.0
+        ad[1][0] = 0.0
+        for q in range(1, Q + 1):
+            ad[1][q] = ad[1][q - 1] + l(0, R[q - 1])
+        for n in range(2, N + 1):
+            an = -INF
+            for ai in pre[n]:
+                an = _logadd(an, alpha[arcs[ai][1]] + arcs[ai][3])
+            alpha[n] = an
+            for ai in pre[n]:
+                w, s, e, ll = arcs[ai]
+                for q in range(Q + 1):
+                    if q == 0:
+                        ada[q] = ad[s][q] + l(w, 0, True)
+                    else:
+                        rq = R[q - 1]  # substitution, insertion, deletion (within the arc)
+                        ada[q] = min(ad[s][q - 1] + l(w, rq), ad[s][q] + l(w, 0, True), ada[q - 1] + l(0, rq))
+                    ad[n][q] += math.exp(alpha[s] + ll - alpha[n]) * ada[q]
+        gamma = [dict() for _ in range(Q + 1)]
+        tau_b, tau_e = [0.0] * (Q + 1), [0.0] * (Q + 1)
+        b_arc = [0] * (Q + 1)
+        bd[N][Q] = 1.0
+        for n in range(N, 1, -1):
+            for ai in pre[n]:
+                w, s, e, ll = arcs[ai]
+                ada[0] = ad[s][0] + l(w, 0, True)
+                for q in range(1, Q + 1):
+                    rq = R[q - 1]
+                    a1, a2, a3 = ad[s][q - 1] + l(w, rq), ad[s][q] + l(w, 0, True), ada[q - 1] + l(0, rq)
+                    if a1 <= a2:
+                        b_arc[q], ada[q] = (1, a1) if a1 <= a3 else (3, a3)
+                    else:
+                        b_arc[q], ada[q] = (2, a2) if a2 <= a3 else (3, a3)
+                bda = [0.0] * (Q + 1)
+                post = math.exp(alpha[s] + ll - alpha[n])
+                for q in range(Q, 0, -1):
+                    bda[q] += post * bd[n][q]
+                    if b_arc[q] == 1:
+                        bd[s][q - 1] += bda[q]
+                        gamma[q][w] = gamma[q].get(w, 0.0) + bda[q]
+                        tau_b[q] += st[s] * bda[q]
+                        tau_e[q] += st[n] * bda[q]
+                    elif b_arc[q] == 2:
+                        bd[s][q] += bda[q]
+                    else:
+                        bda[q - 1] += bda[q]
+                        gamma[q][0] = gamma[q].get(0, 0.0) + bda[q]
+                        tau_b[q] += st[s] * bda[q]
+                        tau_e[q] += st[n] * bda[q]
+                bda[0] += post * bd[n][0]
+                bd[s][0] += bda[0]
+        bda = [0.0] * (Q + 1)
+        for q in range(Q, 0, -1):
+            bda[q] += bd[1][q]
+            bda[q - 1] += bda[q]
+            gamma[q][0] = gamma[q].get(0, 0.0) + bda[q]
+            tau_b[q] += st[1] * bda[q]
+            tau_e[q] += st[1] * bda[q]
+        g_ = []
+        for q in range(1, Q + 1):
+            v = sorted(((k, float(F32(x))) for k, x in gamma[q].items()), key=lambda z: z[0])
+            v = sorted(v, key=lambda z: -z[1])  # stable: ties keep word order
+            g_.append(v)
+        times = [(float(F32(tau_b[q])), float(F32(tau_e[q]))) for q in range(1, Q + 1)]
+        dq = 0.0
+        result = dict(words=[], conf=[], times=[])
+        for q in range(Q):
+            g = g_[q]
+            old = 0.0
+            new = g[0][1] if g else 0.0
+            for k, x in g:
+                if k == R[q]:
+                    old = x
+            dq += old - new
+            if g:
+                R[q] = g[0][0]
+            if R[q] != 0:
+                conf = 0.0
+                for k, x in g:
+                    if k == R[q]:
+                        conf = x
+                result["words"].append(R[q])
+                result["conf"].append(conf)
+                result["times"].append(times[q])
+        if dq == 0.0 or it > 100:
+            break
+    return result
+
+
+def nbest(W, Fi, n):
+    S = len(W)
+    if S == 0 or n <= 0:
+        return []
+    best = [None] * S
+    for s in range(S - 1, -1, -1):
+        c = []
+        if Fi[s] is not None:
+            c.append((F32(Fi[s][0]), F32(Fi[s][1]), -1, 0))
+        for i, (w, d, g, a, p) in enumerate(W[s]):
+            for k, (bg, ba, _, _) in enumerate(best[d]):
+                c.append((F32(F32(g) + bg), F32(F32(a) + ba), i, k))
+        import functools
+        c.sort(key=functools.cmp_to_key(lambda x, y: -_cmp((x[0], x[1]), (y[0], y[1]))))
+        best[s] = c[:n]
+    out = []
+    for k in range(len(best[0])):
+        g, a = best[0][k][0], best[0][k][1]
+        words, spans = [], []
+        s, rank, t = 0, k, 0
+        while True:
+            _, _, ai, r = best[s][rank]
+            if ai < 0:
+                break
+            w, d, _, _, p = W[s][ai]
+            if w != 0:
+                words.append(w)
+                spans.append((t, t + len(p)))
+            t += len(p)
+            s, rank = d, r
+        out.append(dict(words=words, spans=spans, graph=float(g), acoustic=float(a)))
+    return out

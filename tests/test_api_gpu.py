@@ -25,6 +25,28 @@ def _pcm(x):
     return np.asarray(x, np.float32).astype("<i2").tobytes()
 
 
+def _oracle_mbr(oracle, wave, chunk):
+    import oracle_lattice as OL
+    llh = oracle.online(wave, chunk=chunk)["llh"]
+    r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
+                            True, lattice=True)
+    L = OL.raw_from_oracle(r, oracle.graph, True)
+    W, Fi = OL.determinize(OL.prune(L, 6.0), oracle.graph.ilabel, oracle.graph.olabel)
+    W, Fi = OL.scale_graph(W, Fi, 0.9)
+    return OL.mbr(W, Fi)
+
+
+def _oracle_mbr_text(oracle, wave):
+    import oracle_lattice as OL
+    llh = oracle.loglikes(wave)
+    r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
+                            True, lattice=True)
+    W, Fi = OL.determinize(OL.prune(OL.raw_from_oracle(r, oracle.graph, True), 6.0),
+                           oracle.graph.ilabel, oracle.graph.olabel)
+    mb = OL.mbr(*OL.scale_graph(W, Fi, 0.9))
+    return " ".join(oracle.words[w] for w in mb["words"])
+
+
 def test_kaldi_recognizer_matches_oracle(vosk_mod, synth_model_noep, test_wave):
     """test_simple.py pattern: 4000-frame chunks, partial results, final result.
     The reference Recognizer silence-weights its i-vector statistics from the
@@ -45,11 +67,16 @@ def test_kaldi_recognizer_matches_oracle(vosk_mod, synth_model_noep, test_wave):
         assert "partial" in p
         partials.append(p["partial"])
     final = json.loads(rec.FinalResult())
-    assert final["text"] == ref["text"]
-    assert [w["word"] for w in final.get("result", [])] == ref["text"].split()
-    for w in final.get("result", []):
+    # the result is the MBR decoding of the segment's lattice (graph scale
+    # 0.9, src/recognizer.cc:429-482,718): words, confidences, times
+    mb = _oracle_mbr(oracle, test_wave, 4000)
+    assert final["text"] == " ".join(oracle.words[w] for w in mb["words"])
+    assert [w["word"] for w in final.get("result", [])] == final["text"].split()
+    for w, c, (tb, te) in zip(final.get("result", []), mb["conf"], mb["times"]):
+        assert w["conf"] == pytest.approx(c, abs=1e-5)
+        assert w["start"] == pytest.approx(tb * 0.03, abs=1e-5)
+        assert w["end"] == pytest.approx(te * 0.03, abs=1e-5)
         assert 0.0 <= w["start"] <= w["end"] <= len(test_wave) / 16000 + 0.1
-        assert w["conf"] == 1.0
     assert any(partials)  # partial hypotheses appear while streaming
     # next AcceptWaveform after FinalResult starts a fresh utterance
     assert rec.AcceptWaveform(data[:16000]) == 0
@@ -142,4 +169,40 @@ def test_batch_recognizer_matches_oracle(vosk_mod, synth_model_noep, test_wave, 
         if res:
             texts[i] = (texts[i] + " " + json.loads(res)["text"]).strip()
         assert recs[i].GetPendingChunks() == 0
-        assert texts[i] == oracle.recognize(waves[i])["text"], i
+        # PushLattice: the MBR words of the stream's lattice (batch_recognizer.cc:43-107)
+        assert texts[i] == _oracle_mbr_text(oracle, waves[i]), i
+
+
+def test_alternatives_and_nlsml_from_lattice(vosk_mod, synth_model_noep, test_wave):
+    """SetMaxAlternatives: the n-best word sequences of the segment's lattice
+    with likelihood -(graph + acoustic) (NbestResult, src/recognizer.cc:526-
+    607); NLSML carries the same texts and likelihoods (:609-667)."""
+    import oracle_lattice as OL
+    oracle = oracle_py.OracleModel(synth_model_noep)
+    x = test_wave[:16000 * 5]
+    llh = oracle.online(x, chunk=4000)["llh"]
+    r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
+                            True, lattice=True)
+    W, Fi = OL.determinize(OL.prune(OL.raw_from_oracle(r, oracle.graph, True), 6.0),
+                           oracle.graph.ilabel, oracle.graph.olabel)
+    nb = OL.nbest(*OL.scale_graph(W, Fi, 0.9), 3)
+    m = vosk_mod.Model(synth_model_noep)
+    outs = {}
+    for nlsml in (False, True):
+        rec = vosk_mod.KaldiRecognizer(m, 16000)
+        rec.SetMaxAlternatives(3)
+        rec.SetWords(True)
+        rec.SetNLSML(nlsml)
+        data = _pcm(x)
+        for i in range(0, len(data), 8000):
+            rec.AcceptWaveform(data[i:i + 8000])
+        outs[nlsml] = rec.FinalResult()
+    alts = json.loads(outs[False])["alternatives"]
+    assert [a["text"] for a in alts] == [" ".join(oracle.words[w] for w in p["words"]) for p in nb]
+    for a, p in zip(alts, nb):
+        assert a["confidence"] == pytest.approx(-(p["graph"] + p["acoustic"]), abs=1e-2)
+        assert [w["word"] for w in a.get("result", [])] == a["text"].split()
+    assert outs[True].startswith('<?xml version="1.0"?>\n<result grammar="default">\n')
+    assert outs[True].count("<interpretation") == len(alts)
+    for a in alts:
+        assert "<instance>" + a["text"] + "</instance>" in outs[True]

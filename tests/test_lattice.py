@@ -1,0 +1,85 @@
+"""Result pipeline over lattices (host code of libvosk.so, csrc/lattice.cc)
+against its oracle restatement (tests/oracle_lattice.py): lattice-beam
+pruning, word-level determinization, graph scaling, Kaldi MBR (words,
+confidences, times) and n-best, on the oracle decoder's lattices of the
+synthetic models.  CPU only (host-only ABI, no GPU)."""
+import numpy as np
+import pytest
+
+import oracle_lattice as OL
+import oracle_py
+
+
+def _lattice(model, wave, use_final=True):
+    o = oracle_py.OracleModel(model)
+    llh = o.loglikes(wave)
+    r = o.graph.decode(llh, o.beam, o.max_active, o.min_active, o.beam_delta, use_final, lattice=True)
+    return o, r, OL.raw_from_oracle(r, o.graph, use_final)
+
+
+def _python(o, L, beam=6.0, scale=0.9, n=5):
+    P = OL.prune(L, beam)
+    W, Fi = OL.determinize(P, o.graph.ilabel, o.graph.olabel)
+    if scale != 1.0:
+        W, Fi = OL.scale_graph(W, Fi, scale)
+    return P, W, OL.mbr(W, Fi), OL.nbest(W, Fi, n)
+
+
+@pytest.mark.parametrize("secs,use_final", [(1.5, True), (4, True), (8.3, True), (5, False)])
+def test_cpp_pipeline_matches_restatement(synth_model, test_wave, secs, use_final):
+    from vosk import engine
+    o, r, L = _lattice(synth_model, test_wave[:int(16000 * secs)], use_final)
+    scale = 0.9 if use_final else 1.0
+    got = engine.lattice_words(L, o.graph.ilabel, o.graph.olabel, 6.0, scale, 5)
+    P, W, mb, nb = _python(o, L, 6.0, scale, 5)
+    assert got["pruned_tokens"] == len(P["tok_state"])
+    assert got["pruned_links"] == len(P["link_src"])
+    assert got["det_ok"] == 1
+    assert got["det_states"] == len(W)
+    assert got["det_arcs"] == sum(len(v) for v in W)
+    assert got["mbr"]["words"] == mb["words"]
+    np.testing.assert_allclose(got["mbr"]["conf"], mb["conf"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(np.reshape(got["mbr"]["times"], (-1, 2)),
+                               np.reshape(mb["times"], (-1, 2)), rtol=0, atol=1e-4)
+    assert [x["words"] for x in got["nbest"]] == [x["words"] for x in nb]
+    assert [x["spans"] for x in got["nbest"]] == [[list(s) for s in x["spans"]] for x in nb]
+    np.testing.assert_allclose([x["graph"] + x["acoustic"] for x in got["nbest"]],
+                               [x["graph"] + x["acoustic"] for x in nb], rtol=0, atol=1e-3)
+    # sanity of the semantics: confidences are posteriors, n-best is sorted
+    # and distinct, the best path is the first alternative
+    assert all(0.0 <= c <= 1.0 + 1e-6 for c in got["mbr"]["conf"])
+    costs = [x["graph"] + x["acoustic"] for x in got["nbest"]]
+    assert costs == sorted(costs)
+    assert len({tuple(x["words"]) for x in got["nbest"]}) == len(got["nbest"])
+    if use_final:
+        assert got["nbest"][0]["words"] == r["words"]
+
+
+def test_pruning_keeps_best_path_and_shrinks(synth_model, test_wave):
+    o, r, L = _lattice(synth_model, test_wave[:16000 * 3])
+    P = OL.prune(L, 6.0)
+    assert 0 < len(P["tok_state"]) < len(L["tok_state"])
+    # every best-path arc survives the beam
+    arcs = set(P["link_arc"].tolist())
+    assert all(a in arcs for a in r["path"])
+    # a zero beam keeps only best-path ties
+    P0 = OL.prune(L, 0.0)
+    assert len(P0["link_src"]) <= len(r["path"]) + 4
+
+
+def test_mbr_confidences_on_a_two_word_choice():
+    """Hand-made lattice: one frame, two competing words with costs 0 and
+    ln(3): posteriors 0.75 / 0.25, MBR picks the likelier word."""
+    import math
+    L = dict(num_frames=1, frame_begin=np.array([0, 1, 3], np.int32), tok_state=np.array([0, 1, 2], np.int32),
+             tok_cost=np.array([0, 0, 1], np.float32), link_src=np.array([0, 0], np.int32),
+             link_dst=np.array([1, 2], np.int32), link_arc=np.array([0, 1], np.int32),
+             link_graph=np.array([0.0, math.log(3.0)], np.float32), link_ac=np.zeros(2, np.float32),
+             final_cost=np.zeros(0, np.float32))
+    ilabel, olabel = np.array([5, 6], np.int32), np.array([11, 12], np.int32)
+    from vosk import engine
+    got = engine.lattice_words(L, ilabel, olabel, 6.0, 1.0, 3)
+    assert got["mbr"]["words"] == [11]
+    assert got["mbr"]["conf"][0] == pytest.approx(0.75, abs=1e-6)
+    assert got["mbr"]["times"] == [[0, 1]]
+    assert [x["words"] for x in got["nbest"]] == [[11], [12]]

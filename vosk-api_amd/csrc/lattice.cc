@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <limits>
+#include <map>
 #include <unordered_map>
 
 #include "common.h"
@@ -113,6 +114,611 @@ void BuildRawLattice(const Graph& g, int start_state, const std::vector<LatFrame
       any |= c != kInf;
     }
     if (any) L.final_cost = fc;
+  }
+}
+
+}  // namespace vamd
+
+// ===========================================================================
+// word level
+// ===========================================================================
+namespace vamd {
+
+namespace {
+
+// Kaldi LatticeWeight order: smaller total cost is better; ties by graph cost
+struct LW {
+  float g = 0.0f, a = 0.0f;
+};
+inline int CompareLW(const LW& x, const LW& y) {  // 1: x better, -1: y better
+  const float fx = x.g + x.a, fy = y.g + y.a;
+  if (fx < fy) return 1;
+  if (fx > fy) return -1;
+  if (x.g < y.g) return 1;
+  if (x.g > y.g) return -1;
+  if (x.a < y.a) return 1;
+  if (x.a > y.a) return -1;
+  return 0;
+}
+inline LW Times(const LW& x, const LW& y) { return LW{x.g + y.g, x.a + y.a}; }
+inline LW Divide(const LW& x, const LW& y) { return LW{x.g - y.g, x.a - y.a}; }
+
+struct Elem {
+  int tok;
+  LW w;
+  std::vector<int> str;
+};
+// (weight, string) order of Kaldi's determinizer when one state is reached twice
+inline bool ElemBetter(const Elem& x, const Elem& y) {
+  const int c = CompareLW(x.w, y.w);
+  if (c != 0) return c > 0;
+  if (x.str.size() != y.str.size()) return x.str.size() < y.str.size();
+  return x.str < y.str;
+}
+
+}  // namespace
+
+void PruneRawLattice(RawLattice* lat, float beam) {
+  RawLattice& L = *lat;
+  const int N = (int)L.tok_state.size(), F = L.num_frames;
+  if (N == 0) return;
+  std::vector<int> frame(N);
+  for (int k = 0; k <= F; k++)
+    for (int t = L.frame_begin[k]; t < L.frame_begin[k + 1]; t++) frame[t] = k;
+  // links grouped by destination frame (BuildRawLattice order)
+  std::vector<int> lb(F + 2, 0);
+  for (auto& l : L.links) lb[frame[l.dst] + 1]++;
+  for (int k = 0; k <= F; k++) lb[k + 1] += lb[k];
+  auto cost = [](const RawLattice::Link& l) { return l.graph_cost + l.acoustic_cost; };
+  std::vector<double> alpha(N, INFINITY), beta(N, INFINITY);
+  for (int t = L.frame_begin[0]; t < L.frame_begin[1]; t++)
+    if (L.tok_cost[t] == 0.0f && L.tok_state[t] >= 0) { alpha[t] = 0.0; break; }
+  for (int k = 0; k <= F; k++) {
+    // emitting links (from frame k-1) first, then epsilon links to a fixpoint
+    for (int i = lb[k]; i < lb[k + 1]; i++) {
+      const auto& l = L.links[i];
+      if (frame[l.src] != k) alpha[l.dst] = std::min(alpha[l.dst], alpha[l.src] + cost(l));
+    }
+    for (bool ch = true; ch;) {
+      ch = false;
+      for (int i = lb[k]; i < lb[k + 1]; i++) {
+        const auto& l = L.links[i];
+        if (frame[l.src] == k && alpha[l.src] + cost(l) < alpha[l.dst]) {
+          alpha[l.dst] = alpha[l.src] + cost(l);
+          ch = true;
+        }
+      }
+    }
+  }
+  double best = INFINITY;
+  for (int t = L.frame_begin[F]; t < L.frame_begin[F + 1]; t++) {
+    const double fc = L.final_cost.empty() ? 0.0 : (double)L.final_cost[t - L.frame_begin[F]];
+    beta[t] = fc;
+    best = std::min(best, alpha[t] + fc);
+  }
+  for (int k = F; k >= 0; k--) {
+    for (bool ch = true; ch;) {
+      ch = false;
+      for (int i = lb[k]; i < lb[k + 1]; i++) {
+        const auto& l = L.links[i];
+        if (frame[l.src] == k && cost(l) + beta[l.dst] < beta[l.src]) {
+          beta[l.src] = cost(l) + beta[l.dst];
+          ch = true;
+        }
+      }
+    }
+    for (int i = lb[k]; i < lb[k + 1]; i++) {
+      const auto& l = L.links[i];
+      if (frame[l.src] != k) beta[l.src] = std::min(beta[l.src], cost(l) + beta[l.dst]);
+    }
+  }
+  // keep what lies on a path within the beam of the best one
+  std::vector<int> remap(N, -1);
+  RawLattice out;
+  out.num_frames = F;
+  out.frame_begin.assign(F + 2, 0);
+  out.overflow = L.overflow;
+  for (int k = 0; k <= F; k++) {
+    out.frame_begin[k] = (int)out.tok_state.size();
+    for (int t = L.frame_begin[k]; t < L.frame_begin[k + 1]; t++) {
+      if (!(alpha[t] + beta[t] - best <= beam)) continue;
+      remap[t] = (int)out.tok_state.size();
+      out.tok_state.push_back(L.tok_state[t]);
+      out.tok_cost.push_back(L.tok_cost[t]);
+    }
+    out.frame_begin[k + 1] = (int)out.tok_state.size();
+  }
+  for (auto& l : L.links) {
+    if (remap[l.src] < 0 || remap[l.dst] < 0) continue;
+    if (!(alpha[l.src] + cost(l) + beta[l.dst] - best <= beam)) continue;
+    RawLattice::Link m = l;
+    m.src = remap[l.src];
+    m.dst = remap[l.dst];
+    out.links.push_back(m);
+  }
+  if (!L.final_cost.empty())
+    for (int t = L.frame_begin[F]; t < L.frame_begin[F + 1]; t++)
+      if (remap[t] >= 0) out.final_cost.push_back(L.final_cost[t - L.frame_begin[F]]);
+  L = std::move(out);
+}
+
+bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOptions& opt, WordLattice* out) {
+  WordLattice& W = *out;
+  W = WordLattice();
+  const int N = (int)L.tok_state.size(), F = L.num_frames;
+  if (N == 0) return true;
+  std::vector<std::vector<int>> outl(N);
+  for (int i = 0; i < (int)L.links.size(); i++) outl[L.links[i].src].push_back(i);
+  std::vector<float> fin(N, INFINITY);
+  for (int t = L.frame_begin[F]; t < L.frame_begin[F + 1]; t++)
+    fin[t] = L.final_cost.empty() ? 0.0f : L.final_cost[t - L.frame_begin[F]];
+  int start = -1;
+  for (int t = L.frame_begin[0]; t < L.frame_begin[1]; t++)
+    if (L.tok_cost[t] == 0.0f) { start = t; break; }
+  if (start < 0) return true;
+
+  // closure over word-epsilon links (emitting arcs without a word label too):
+  // for each token the best (weight, string) reaching it
+  auto closure = [&](std::vector<Elem>* sub) {
+    std::unordered_map<int, int> at;
+    std::vector<int> work;
+    for (int i = 0; i < (int)sub->size(); i++) {
+      at[(*sub)[i].tok] = i;
+      work.push_back(i);
+    }
+    while (!work.empty()) {
+      const int i = work.back();
+      work.pop_back();
+      const Elem e = (*sub)[i];
+      for (int li : outl[e.tok]) {
+        const auto& l = L.links[li];
+        if (g.olabel[l.arc] != 0) continue;
+        Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}), e.str};
+        if (g.ilabel[l.arc] != 0) n.str.push_back(g.ilabel[l.arc]);
+        auto it = at.find(n.tok);
+        if (it == at.end()) {
+          at[n.tok] = (int)sub->size();
+          work.push_back((int)sub->size());
+          sub->push_back(std::move(n));
+        } else if (ElemBetter(n, (*sub)[it->second])) {
+          (*sub)[it->second] = std::move(n);
+          work.push_back(it->second);
+        }
+      }
+    }
+    std::sort(sub->begin(), sub->end(), [](const Elem& x, const Elem& y) { return x.tok < y.tok; });
+  };
+  // normalization: the best weight and the common string prefix move to the arc
+  auto normalize = [](std::vector<Elem>* sub, LW* tot, std::vector<int>* prefix) {
+    *tot = (*sub)[0].w;
+    for (auto& e : *sub)
+      if (CompareLW(e.w, *tot) > 0) *tot = e.w;
+    size_t n = (*sub)[0].str.size();
+    for (auto& e : *sub) {
+      size_t j = 0;
+      while (j < n && j < e.str.size() && e.str[j] == (*sub)[0].str[j]) j++;
+      n = j;
+    }
+    prefix->assign((*sub)[0].str.begin(), (*sub)[0].str.begin() + n);
+    for (auto& e : *sub) {
+      e.w = Divide(e.w, *tot);
+      e.str.erase(e.str.begin(), e.str.begin() + n);
+    }
+  };
+  // subsets are equal with the same tokens and strings and weights within
+  // delta (Kaldi's determinizer, delta = kDelta = 1/1024)
+  const float delta = 1.0f / 1024.0f;
+  std::unordered_map<std::string, std::vector<int>> index;
+  std::vector<std::vector<Elem>> subsets;
+  auto key_of = [](const std::vector<Elem>& sub) {
+    std::string k;
+    for (auto& e : sub) {
+      k.append((const char*)&e.tok, sizeof(int));
+      const int n = (int)e.str.size();
+      k.append((const char*)&n, sizeof(int));
+      k.append((const char*)e.str.data(), sizeof(int) * n);
+    }
+    return k;
+  };
+  auto find_or_add = [&](std::vector<Elem>&& sub, bool* added) {
+    const std::string k = key_of(sub);
+    auto& cand = index[k];
+    for (int id : cand) {
+      const auto& o = subsets[id];
+      bool eq = true;
+      for (size_t i = 0; i < o.size() && eq; i++)
+        eq = std::fabs(o[i].w.g - sub[i].w.g) <= delta && std::fabs(o[i].w.a - sub[i].w.a) <= delta;
+      if (eq) {
+        *added = false;
+        return id;
+      }
+    }
+    const int id = (int)subsets.size();
+    subsets.push_back(std::move(sub));
+    cand.push_back(id);
+    *added = true;
+    return id;
+  };
+  // start state: the closure of the start token, not normalized (its weight
+  // and string stay on the first arcs / final weight)
+  std::vector<Elem> s0{Elem{start, LW{}, {}}};
+  closure(&s0);
+  bool added;
+  find_or_add(std::move(s0), &added);
+  std::vector<std::vector<WordLattice::Arc>> arcs(1);
+  std::vector<int> queue{0};
+  for (size_t qi = 0; qi < queue.size(); qi++) {
+    const int sid = queue[qi];
+    // transitions per word label, in label order
+    std::map<int, std::vector<Elem>> by_word;
+    {
+      const std::vector<Elem>& sub = subsets[sid];
+      for (const Elem& e : sub)
+        for (int li : outl[e.tok]) {
+          const auto& l = L.links[li];
+          const int w = g.olabel[l.arc];
+          if (w == 0) continue;
+          Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}), e.str};
+          if (g.ilabel[l.arc] != 0) n.str.push_back(g.ilabel[l.arc]);
+          auto& v = by_word[w];
+          bool merged = false;
+          for (auto& x : v)
+            if (x.tok == n.tok) {
+              if (ElemBetter(n, x)) x = n;
+              merged = true;
+              break;
+            }
+          if (!merged) v.push_back(std::move(n));
+        }
+    }
+    for (auto& kv : by_word) {
+      std::vector<Elem> sub = std::move(kv.second);
+      closure(&sub);
+      LW tot;
+      std::vector<int> prefix;
+      normalize(&sub, &tot, &prefix);
+      const int dst = find_or_add(std::move(sub), &added);
+      if (added) {
+        if ((int)subsets.size() > opt.max_states) return false;
+        queue.push_back(dst);
+        arcs.emplace_back();
+      }
+      arcs[sid].push_back(WordLattice::Arc{kv.first, dst, tot.g, tot.a, std::move(prefix)});
+    }
+  }
+  const int S = (int)subsets.size();
+  std::vector<LW> fw(S);
+  std::vector<std::vector<int>> fs(S);
+  std::vector<char> isf(S, 0);
+  for (int s = 0; s < S; s++) {
+    const Elem* best = nullptr;
+    Elem tmp;
+    for (const Elem& e : subsets[s]) {
+      if (fin[e.tok] == INFINITY) continue;
+      Elem c{e.tok, Times(e.w, LW{fin[e.tok], 0.0f}), e.str};
+      if (!best || ElemBetter(c, *best)) {
+        tmp = c;
+        best = &tmp;
+      }
+    }
+    if (best) {
+      isf[s] = 1;
+      fw[s] = tmp.w;
+      fs[s] = tmp.str;
+    }
+  }
+  // topological order (the lattice is acyclic), start state first
+  std::vector<int> indeg(S, 0), order;
+  for (int s = 0; s < S; s++)
+    for (auto& a : arcs[s]) indeg[a.next]++;
+  std::vector<int> st{0};
+  while (!st.empty()) {
+    const int s = st.back();
+    st.pop_back();
+    order.push_back(s);
+    for (auto it = arcs[s].rbegin(); it != arcs[s].rend(); ++it)
+      if (--indeg[it->next] == 0) st.push_back(it->next);
+  }
+  if ((int)order.size() != S) VAMD_ERR("lattice determinization produced a cycle");
+  std::vector<int> pos(S);
+  for (int i = 0; i < S; i++) pos[order[i]] = i;
+  W.arcs.resize(S);
+  W.final_graph.assign(S, INFINITY);
+  W.final_acoustic.assign(S, 0.0f);
+  W.final_tids.resize(S);
+  for (int s = 0; s < S; s++) {
+    const int p = pos[s];
+    for (auto& a : arcs[s]) {
+      WordLattice::Arc b = a;
+      b.next = pos[a.next];
+      W.arcs[p].push_back(std::move(b));
+    }
+    if (isf[s]) {
+      W.final_graph[p] = fw[s].g;
+      W.final_acoustic[p] = fw[s].a;
+      W.final_tids[p] = fs[s];
+    }
+  }
+  return true;
+}
+
+void ScaleGraph(WordLattice* lat, float scale) {
+  for (auto& v : lat->arcs)
+    for (auto& a : v) a.graph *= scale;
+  for (auto& f : lat->final_graph)
+    if (f != INFINITY) f *= scale;
+}
+
+namespace {
+
+// Kaldi LogAdd (base/kaldi-math.h)
+inline double LogAdd(double x, double y) {
+  double diff;
+  if (x < y) {
+    diff = x - y;
+    x = y;
+  } else {
+    diff = y - x;
+  }
+  static const double kMinLogDiff = std::log(std::numeric_limits<double>::epsilon());
+  if (diff >= kMinLogDiff) return x + std::log1p(std::exp(diff));
+  return x;
+}
+
+struct MbrArc {
+  int word, start, end;
+  double loglike;
+};
+
+class Mbr {
+ public:
+  explicit Mbr(const WordLattice& W) {
+    // CreateSuperFinal: final weights become epsilon arcs into one new final
+    // state (numbered last: the lattice stays topologically sorted)
+    const int S = W.NumStates();
+    N_ = S + 1;
+    pre_.assign(N_ + 1, {});
+    times_st_.assign(N_ + 1, 0);
+    std::vector<int> t(S + 1, -1);
+    t[0] = 0;
+    for (int s = 0; s < S; s++) {
+      for (const auto& a : W.arcs[s]) {
+        add(s + 1, a.next + 1, a.word, -(double)(a.graph + a.acoustic));
+        t[a.next] = t[s] + (int)a.tids.size();
+      }
+      if (W.final_graph[s] != INFINITY) {
+        add(s + 1, N_, 0, -(double)(W.final_graph[s] + W.final_acoustic[s]));
+        t[S] = t[s] + (int)W.final_tids[s].size();
+      }
+    }
+    for (int s = 0; s <= S; s++) times_st_[s + 1] = std::max(0, t[s]);
+    // initial hypothesis: the best path's words
+    std::vector<double> best(N_ + 1, -INFINITY);
+    std::vector<int> from(N_ + 1, -1);
+    best[1] = 0.0;
+    for (int n = 2; n <= N_; n++)
+      for (int ai : pre_[n]) {
+        const MbrArc& a = arcs_[ai];
+        const double v = best[a.start] + a.loglike;
+        if (v > best[n]) {
+          best[n] = v;
+          from[n] = ai;
+        }
+      }
+    for (int n = N_; n > 1 && from[n] >= 0; n = arcs_[from[n]].start)
+      if (arcs_[from[n]].word != 0) R_.push_back(arcs_[from[n]].word);
+    std::reverse(R_.begin(), R_.end());
+    Decode();
+  }
+  MbrResult result;
+
+ private:
+  void add(int s, int e, int w, double ll) {
+    pre_[e].push_back((int)arcs_.size());
+    arcs_.push_back(MbrArc{w, s, e, ll});
+  }
+  static double l(int a, int b, bool penalize = false) {
+    return a == b ? 0.0 : (penalize ? 1.0 + 1.0e-05 : 1.0);
+  }
+  int r(int q) const { return R_[q - 1]; }
+  void NormalizeEps() {
+    std::vector<int> x{0};
+    for (int w : R_)
+      if (w != 0) {
+        x.push_back(w);
+        x.push_back(0);
+      }
+    R_ = x;
+  }
+  double EditDistance(int N, int Q, std::vector<double>& alpha, std::vector<std::vector<double>>& ad,
+                      std::vector<double>& ada) {
+    alpha[1] = 0.0;
+    ad[1][0] = 0.0;
+    for (int q = 1; q <= Q; q++) ad[1][q] = ad[1][q - 1] + l(0, r(q));
+    for (int n = 2; n <= N; n++) {
+      double an = -INFINITY;
+      for (int ai : pre_[n]) an = LogAdd(an, alpha[arcs_[ai].start] + arcs_[ai].loglike);
+      alpha[n] = an;
+      for (int ai : pre_[n]) {
+        const MbrArc& a = arcs_[ai];
+        for (int q = 0; q <= Q; q++) {
+          if (q == 0) {
+            ada[q] = ad[a.start][q] + l(a.word, 0, true);
+          } else {
+            // substitution, insertion of the arc's word, deletion of r_q
+            const int rq = r(q);
+            const double a1 = ad[a.start][q - 1] + l(a.word, rq), a2 = ad[a.start][q] + l(a.word, 0, true),
+                         a3 = ada[q - 1] + l(0, rq);
+            ada[q] = std::min(a1, std::min(a2, a3));
+          }
+          ad[n][q] += std::exp(alpha[a.start] + a.loglike - alpha[n]) * ada[q];
+        }
+      }
+    }
+    return ad[N][Q];
+  }
+  void AccStats() {
+    const int N = N_, Q = (int)R_.size();
+    std::vector<double> alpha(N + 1, 0.0), ada(Q + 1, 0.0), bda(Q + 1, 0.0);
+    std::vector<std::vector<double>> ad(N + 1, std::vector<double>(Q + 1, 0.0)),
+        bd(N + 1, std::vector<double>(Q + 1, 0.0));
+    std::vector<char> b_arc(Q + 1, 0);
+    std::vector<std::map<int, double>> gamma(Q + 1);
+    std::vector<double> tau_b(Q + 1, 0.0), tau_e(Q + 1, 0.0);
+    EditDistance(N, Q, alpha, ad, ada);
+    bd[N][Q] = 1.0;
+    for (int n = N; n >= 2; n--) {
+      for (int ai : pre_[n]) {
+        const MbrArc& a = arcs_[ai];
+        const int sa = a.start, wa = a.word;
+        ada[0] = ad[sa][0] + l(wa, 0, true);
+        for (int q = 1; q <= Q; q++) {
+          const int rq = r(q);
+          const double a1 = ad[sa][q - 1] + l(wa, rq), a2 = ad[sa][q] + l(wa, 0, true),
+                       a3 = ada[q - 1] + l(0, rq);
+          if (a1 <= a2) {
+            if (a1 <= a3) { b_arc[q] = 1; ada[q] = a1; }
+            else { b_arc[q] = 3; ada[q] = a3; }
+          } else {
+            if (a2 <= a3) { b_arc[q] = 2; ada[q] = a2; }
+            else { b_arc[q] = 3; ada[q] = a3; }
+          }
+        }
+        std::fill(bda.begin(), bda.end(), 0.0);
+        const double post = std::exp(alpha[sa] + a.loglike - alpha[n]);
+        for (int q = Q; q >= 1; q--) {
+          bda[q] += post * bd[n][q];
+          switch (b_arc[q]) {
+            case 1:  // the arc's word in bin q
+              bd[sa][q - 1] += bda[q];
+              gamma[q][wa] += bda[q];
+              tau_b[q] += times_st_[sa] * bda[q];
+              tau_e[q] += times_st_[n] * bda[q];
+              break;
+            case 2:
+              bd[sa][q] += bda[q];
+              break;
+            default:  // epsilon in bin q, within the arc
+              bda[q - 1] += bda[q];
+              gamma[q][0] += bda[q];
+              tau_b[q] += times_st_[sa] * bda[q];
+              tau_e[q] += times_st_[n] * bda[q];
+              break;
+          }
+        }
+        bda[0] += post * bd[n][0];
+        bd[sa][0] += bda[0];
+      }
+    }
+    std::fill(bda.begin(), bda.end(), 0.0);
+    for (int q = Q; q >= 1; q--) {
+      bda[q] += bd[1][q];
+      bda[q - 1] += bda[q];
+      gamma[q][0] += bda[q];
+      tau_b[q] += times_st_[1] * bda[q];
+      tau_e[q] += times_st_[1] * bda[q];
+    }
+    gamma_.assign(Q, {});
+    times_.assign(Q, {});
+    for (int q = 1; q <= Q; q++) {
+      for (auto& kv : gamma[q]) gamma_[q - 1].push_back({kv.first, (float)kv.second});
+      std::stable_sort(gamma_[q - 1].begin(), gamma_[q - 1].end(),
+                       [](const std::pair<int, float>& x, const std::pair<int, float>& y) {
+                         return x.second > y.second;
+                       });
+      times_[q - 1] = {(float)tau_b[q], (float)tau_e[q]};
+    }
+  }
+  void Decode() {
+    for (int iter = 0;; iter++) {
+      NormalizeEps();
+      AccStats();
+      double dq = 0.0;
+      result = MbrResult();
+      for (size_t q = 0; q < R_.size(); q++) {
+        const auto& g = gamma_[q];
+        double old_g = 0.0;
+        const double new_g = g.empty() ? 0.0 : g[0].second;
+        for (auto& x : g)
+          if (x.first == R_[q]) old_g = x.second;
+        dq += old_g - new_g;
+        if (!g.empty()) R_[q] = g[0].first;
+        if (R_[q] != 0) {
+          float conf = 0.0f;
+          for (auto& x : g)
+            if (x.first == R_[q]) conf = x.second;
+          result.words.push_back(R_[q]);
+          result.conf.push_back(conf);
+          result.times.push_back(times_[q]);
+        }
+      }
+      if (dq == 0.0 || iter > 100) break;
+    }
+  }
+  int N_ = 0;
+  std::vector<MbrArc> arcs_;
+  std::vector<std::vector<int>> pre_;
+  std::vector<int> times_st_;
+  std::vector<int> R_;
+  std::vector<std::vector<std::pair<int, float>>> gamma_;
+  std::vector<std::pair<float, float>> times_;
+};
+
+}  // namespace
+
+void MinimumBayesRisk(const WordLattice& lat, MbrResult* out) {
+  *out = MbrResult();
+  if (lat.NumStates() == 0) return;
+  Mbr m(lat);
+  *out = m.result;
+}
+
+void NbestPaths(const WordLattice& W, int n, std::vector<NbestPath>* out) {
+  out->clear();
+  const int S = W.NumStates();
+  if (S == 0 || n <= 0) return;
+  // k best completions per state (the lattice is determinized: distinct
+  // paths are distinct word sequences), backwards in topological order
+  struct Cand {
+    float g, a;
+    int arc;   // index into W.arcs[s], -1 = final
+    int rank;  // rank of the continuation at the arc's next state
+  };
+  auto better = [](const Cand& x, const Cand& y) {
+    return CompareLW(LW{x.g, x.a}, LW{y.g, y.a}) > 0;
+  };
+  std::vector<std::vector<Cand>> best(S);
+  for (int s = S - 1; s >= 0; s--) {
+    std::vector<Cand> c;
+    if (W.final_graph[s] != INFINITY) c.push_back(Cand{W.final_graph[s], W.final_acoustic[s], -1, 0});
+    for (int i = 0; i < (int)W.arcs[s].size(); i++) {
+      const auto& a = W.arcs[s][i];
+      for (int k = 0; k < (int)best[a.next].size(); k++)
+        c.push_back(Cand{a.graph + best[a.next][k].g, a.acoustic + best[a.next][k].a, i, k});
+    }
+    std::stable_sort(c.begin(), c.end(), better);
+    if ((int)c.size() > n) c.resize(n);
+    best[s] = std::move(c);
+  }
+  for (int k = 0; k < (int)best[0].size(); k++) {
+    NbestPath p;
+    p.graph = best[0][k].g;
+    p.acoustic = best[0][k].a;
+    int s = 0, rank = k, t = 0;
+    while (true) {
+      const Cand& c = best[s][rank];
+      if (c.arc < 0) break;
+      const auto& a = W.arcs[s][c.arc];
+      const int len = (int)a.tids.size();
+      if (a.word != 0) {
+        p.words.push_back(a.word);
+        p.spans.push_back({t, t + len});
+      }
+      t += len;
+      s = a.next;
+      rank = c.rank;
+    }
+    out->push_back(std::move(p));
   }
 }
 

@@ -10,6 +10,7 @@
 // frame's cutoff, graph / acoustic costs, final costs.  The word-level steps
 // (lattice-beam pruning, determinization, MBR) live in lattice.cc.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <utility>
@@ -38,6 +39,9 @@ struct RawLattice {
   std::vector<Link> links;           // sorted by (destination frame, src, arc)
   std::vector<float> final_cost;     // per token of the last frame (+inf: not final); empty = all final with 0
   bool overflow = false;             // link arena / frame table overflowed: incomplete
+  int FrameOf(int tok) const {
+    return (int)(std::upper_bound(frame_begin.begin(), frame_begin.end(), tok) - frame_begin.begin()) - 1;
+  }
 };
 
 // Canonical lattice from the device records of one stream: frames [0, F]

@@ -294,6 +294,65 @@ int vamd_silence_weighting_run(int ncalls, const int* num_frames_ready, const in
   API_CATCH(-1)
 }
 
+const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, const int* tok_state,
+                                    const float* tok_cost, const int* link_src, const int* link_dst,
+                                    const int* link_arc, const float* link_graph, const float* link_ac,
+                                    int nlink, const float* final_cost, int nfinal, const int* arc_ilabel,
+                                    const int* arc_olabel, int narcs, float lattice_beam, float graph_scale,
+                                    int nbest) {
+  static thread_local std::string out;
+  API_TRY
+  RawLattice L;
+  L.num_frames = num_frames;
+  L.frame_begin.assign(frame_begin, frame_begin + num_frames + 2);
+  const int ntok = L.frame_begin.back();
+  L.tok_state.assign(tok_state, tok_state + ntok);
+  L.tok_cost.assign(tok_cost, tok_cost + ntok);
+  for (int i = 0; i < nlink; i++)
+    L.links.push_back(RawLattice::Link{link_src[i], link_dst[i], link_arc[i], link_graph[i], link_ac[i]});
+  L.final_cost.assign(final_cost, final_cost + nfinal);
+  Graph g;
+  g.ilabel.assign(arc_ilabel, arc_ilabel + narcs);
+  g.olabel.assign(arc_olabel, arc_olabel + narcs);
+  PruneRawLattice(&L, lattice_beam);
+  std::ostringstream os;
+  os.precision(9);
+  os << "{\"pruned_tokens\": " << L.tok_state.size() << ", \"pruned_links\": " << L.links.size();
+  WordLattice wl;
+  LatticeOptions opt;
+  opt.lattice_beam = lattice_beam;
+  const bool ok = DeterminizeToWords(L, g, opt, &wl);
+  os << ", \"det_ok\": " << (ok ? 1 : 0) << ", \"det_states\": " << wl.NumStates();
+  int det_arcs = 0;
+  for (auto& v : wl.arcs) det_arcs += (int)v.size();
+  os << ", \"det_arcs\": " << det_arcs;
+  if (graph_scale != 1.0f) ScaleGraph(&wl, graph_scale);
+  MbrResult r;
+  MinimumBayesRisk(wl, &r);
+  os << ", \"mbr\": {\"words\": [";
+  for (size_t i = 0; i < r.words.size(); i++) os << (i ? ", " : "") << r.words[i];
+  os << "], \"conf\": [";
+  for (size_t i = 0; i < r.conf.size(); i++) os << (i ? ", " : "") << r.conf[i];
+  os << "], \"times\": [";
+  for (size_t i = 0; i < r.times.size(); i++)
+    os << (i ? ", " : "") << "[" << r.times[i].first << ", " << r.times[i].second << "]";
+  os << "]}, \"nbest\": [";
+  std::vector<NbestPath> nb;
+  NbestPaths(wl, nbest, &nb);
+  for (size_t k = 0; k < nb.size(); k++) {
+    os << (k ? ", " : "") << "{\"words\": [";
+    for (size_t i = 0; i < nb[k].words.size(); i++) os << (i ? ", " : "") << nb[k].words[i];
+    os << "], \"spans\": [";
+    for (size_t i = 0; i < nb[k].spans.size(); i++)
+      os << (i ? ", " : "") << "[" << nb[k].spans[i].first << ", " << nb[k].spans[i].second << "]";
+    os << "], \"graph\": " << nb[k].graph << ", \"acoustic\": " << nb[k].acoustic << "}";
+  }
+  os << "]}";
+  out = os.str();
+  return out.c_str();
+  API_CATCH(nullptr)
+}
+
 int vamd_plan_info(const char* model_dir, int fpc, int* o, double* flops) {
   API_TRY
   ModelData md;

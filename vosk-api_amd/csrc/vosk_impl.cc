@@ -93,6 +93,7 @@ Engine* Model::StreamEngine() {
     cfg.max_slots = EnvInt("VOSK_AMD_MAX_STREAMS", 64);
     cfg.device = DeviceFromEnv();
     cfg.max_step_samples = 4096;
+    cfg.lattice = true;  // results come from the segment's lattice (MBR)
     engine_.reset(new Engine(md_, cfg));
   }
   return engine_.get();
@@ -182,6 +183,44 @@ bool Recognizer::EndpointDetected() {
                            pr[0].final_relative_cost);
 }
 
+// ---------------------------------------------------------------------------
+// lattice -> words (src/recognizer.cc:422-482 MbrResult, :669-729 GetResult)
+// ---------------------------------------------------------------------------
+// The decoder segment's lattice (kept on the GPU), pruned at the lattice beam
+// and determinized on words; false if unavailable (no lattice engine,
+// overflow, determinization guard).
+static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use_final, WordLattice* wl) {
+  RawLattice raw;
+  e->GetRawLattice(slot, use_final, &raw);
+  if (raw.overflow || raw.tok_state.empty()) return false;
+  PruneRawLattice(&raw, m.dec.lattice_beam);
+  LatticeOptions opt;
+  opt.lattice_beam = m.dec.lattice_beam;
+  if (!DeterminizeToWords(raw, m.graph, opt, wl) || wl->NumStates() == 0) return false;
+  return true;
+}
+
+// MBR words, confidences and frame times of the segment; graph_scale as the
+// reference applies to final results (GraphLatticeScale(0.9), :718), 1 for
+// partial results.  Without a lattice: the best path, confidence 1.
+static MbrResult SegmentMbr(Engine* e, int slot, const ModelData& m, bool use_final, float graph_scale) {
+  MbrResult r;
+  WordLattice wl;
+  if (SegmentWordLattice(e, slot, m, use_final, &wl)) {
+    if (graph_scale != 1.0f) ScaleGraph(&wl, graph_scale);
+    MinimumBayesRisk(wl, &r);
+    return r;
+  }
+  std::vector<PathResult> pr;
+  e->BestPaths({slot}, use_final, &pr);
+  for (const WordSeg& w : PathWords(m, pr[0].arcs)) {
+    r.words.push_back(w.word);
+    r.conf.push_back(1.0f);
+    r.times.push_back({(float)w.start, (float)w.end});
+  }
+  return r;
+}
+
 std::string Recognizer::WordsText(const std::vector<WordSeg>& w) const {
   std::ostringstream text;
   for (size_t i = 0; i < w.size(); i++) {
@@ -191,50 +230,77 @@ std::string Recognizer::WordsText(const std::vector<WordSeg>& w) const {
   return text.str();
 }
 
-const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729 (1-best form)
+const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
   if (engine_->NumFramesDecoded(slot_) == 0) return StoreEmptyReturn();
-  std::vector<PathResult> pr;
-  engine_->BestPaths({slot_}, true, &pr);
   const ModelData& m = *model_->data();
-  std::vector<WordSeg> w = PathWords(m, pr[0].arcs);
+  const double t0 = samples_round_start_ / sample_frequency_;
   const double shift = 0.01 * m.dcb.frame_subsampling_factor;
-  if (max_alternatives_ > 0 && !nlsml_) {
-    Json obj, entry;
-    for (auto& ws : w) {
-      if (words_) {
-        Json word;
-        word["word"] = Json::Str(m.words.Find(ws.word));
-        word["start"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.start) * shift);
-        word["end"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.end) * shift);
-        entry["result"].Append(word);
-      }
+  auto wtext = [&](const std::vector<int>& words) {
+    std::ostringstream text;
+    for (size_t i = 0; i < words.size(); i++) text << (i ? " " : "") << m.words.Find(words[i]);
+    return text.str();
+  };
+  if (max_alternatives_ == 0) {  // MbrResult, :429-482
+    const MbrResult r = SegmentMbr(engine_, slot_, m, true, 0.9f);
+    Json obj;
+    for (size_t i = 0; i < r.words.size(); i++) {
+      if (!words_) continue;
+      Json word;
+      word["word"] = Json::Str(m.words.Find(r.words[i]));
+      word["start"] = Json::Float(t0 + (frame_offset_ + r.times[i].first) * shift);
+      word["end"] = Json::Float(t0 + (frame_offset_ + r.times[i].second) * shift);
+      word["conf"] = Json::Float(r.conf[i]);
+      obj["result"].Append(word);
     }
-    entry["text"] = Json::Str(WordsText(w));
-    entry["confidence"] = Json::Float(-pr[0].cost);
-    obj["alternatives"].Append(entry);
+    obj["text"] = Json::Str(wtext(r.words));
     return StoreReturn(obj.Dump());
   }
-  if (max_alternatives_ > 0 && nlsml_) {
+  // n-best (NbestResult :526-607 / NlsmlResult :609-667): the shortest
+  // paths of the graph-scaled word lattice, likelihood = -(graph + acoustic)
+  std::vector<NbestPath> nb;
+  WordLattice wl;
+  if (SegmentWordLattice(engine_, slot_, m, true, &wl)) {
+    ScaleGraph(&wl, 0.9f);
+    NbestPaths(wl, max_alternatives_, &nb);
+  } else {
+    std::vector<PathResult> pr;
+    engine_->BestPaths({slot_}, true, &pr);
+    NbestPath p;
+    for (const WordSeg& w : PathWords(m, pr[0].arcs)) {
+      p.words.push_back(w.word);
+      p.spans.push_back({w.start, w.end});
+    }
+    p.graph = (float)pr[0].cost;
+    nb.push_back(p);
+  }
+  if (nlsml_) {
     std::stringstream ss;
     ss << "<?xml version=\"1.0\"?>\n<result grammar=\"default\">\n";
-    ss << "<interpretation grammar=\"default\" confidence=\"" << (float)(-pr[0].cost) << "\">\n";
-    ss << "<input mode=\"speech\">" << WordsText(w) << "</input>\n";
-    ss << "<instance>" << WordsText(w) << "</instance>\n";
-    ss << "</interpretation>\n</result>\n";
+    for (const NbestPath& p : nb) {
+      const std::string text = wtext(p.words);
+      ss << "<interpretation grammar=\"default\" confidence=\"" << -(p.graph + p.acoustic) << "\">\n";
+      ss << "<input mode=\"speech\">" << text << "</input>\n";
+      ss << "<instance>" << text << "</instance>\n";
+      ss << "</interpretation>\n";
+    }
+    ss << "</result>\n";
     return StoreReturn(ss.str());
   }
   Json obj;
-  for (auto& ws : w) {
-    if (words_) {
+  for (const NbestPath& p : nb) {
+    Json entry;
+    for (size_t i = 0; i < p.words.size(); i++) {
+      if (!words_) continue;
       Json word;
-      word["word"] = Json::Str(m.words.Find(ws.word));
-      word["start"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.start) * shift);
-      word["end"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.end) * shift);
-      word["conf"] = Json::Float(1.0);
-      obj["result"].Append(word);
+      word["word"] = Json::Str(m.words.Find(p.words[i]));
+      word["start"] = Json::Float(t0 + (frame_offset_ + p.spans[i].first) * shift);
+      word["end"] = Json::Float(t0 + (frame_offset_ + p.spans[i].second) * shift);
+      entry["result"].Append(word);
     }
+    entry["text"] = Json::Str(wtext(p.words));
+    entry["confidence"] = Json::Float(-(p.graph + p.acoustic));
+    obj["alternatives"].Append(entry);
   }
-  obj["text"] = Json::Str(WordsText(w));
   return StoreReturn(obj.Dump());
 }
 
@@ -245,21 +311,26 @@ const char* Recognizer::PartialResult() {  // src/recognizer.cc:732-806
     res["partial"] = Json::Str("");
     return StoreReturn(res.Dump());
   }
+  const ModelData& m = *model_->data();
+  if (partial_words_) {  // MBR over the partial lattice, no final costs, no graph scale (:740-780)
+    const MbrResult r = SegmentMbr(engine_, slot_, m, false, 1.0f);
+    const double shift = 0.01 * m.dcb.frame_subsampling_factor;
+    std::ostringstream text;
+    for (size_t i = 0; i < r.words.size(); i++) {
+      Json word;
+      word["word"] = Json::Str(m.words.Find(r.words[i]));
+      word["start"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + r.times[i].first) * shift);
+      word["end"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + r.times[i].second) * shift);
+      word["conf"] = Json::Float(r.conf[i]);
+      res["partial_result"].Append(word);
+      text << (i ? " " : "") << m.words.Find(r.words[i]);
+    }
+    res["partial"] = Json::Str(text.str());
+    return StoreReturn(res.Dump());
+  }
   std::vector<PathResult> pr;
   engine_->BestPaths({slot_}, false, &pr);
-  const ModelData& m = *model_->data();
   std::vector<WordSeg> w = PathWords(m, pr[0].arcs);
-  if (partial_words_) {
-    const double shift = 0.01 * m.dcb.frame_subsampling_factor;
-    for (auto& ws : w) {
-      Json word;
-      word["word"] = Json::Str(m.words.Find(ws.word));
-      word["start"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.start) * shift);
-      word["end"] = Json::Float(samples_round_start_ / sample_frequency_ + (frame_offset_ + ws.end) * shift);
-      word["conf"] = Json::Float(1.0);
-      res["partial_result"].Append(word);
-    }
-  }
   res["partial"] = Json::Str(WordsText(w));
   return StoreReturn(res.Dump());
 }
@@ -314,6 +385,7 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
   cfg.device = DeviceFromEnv();
   cfg.max_step_samples = cfg.frames_per_chunk * md_->mfcc.WindowShift() + 512;
   cfg.arena_tokens = EnvInt("VOSK_AMD_ARENA_TOKENS", 1 << 22);
+  cfg.lattice = true;  // PushLattice: MBR over each segment's lattice (batch_recognizer.cc:43-107)
   engine_.reset(new Engine(md_, cfg));
   samples_per_chunk_ = cfg.frames_per_chunk * md_->mfcc.WindowShift();
   worker_ = std::thread([this] { Worker(); });
@@ -403,9 +475,7 @@ void BatchModel::Worker() {
         const int s = r->slot();
         const int frames = engine_->NumFramesDecoded(s);
         if (c.last) {
-          std::vector<PathResult> fr;
-          if (frames > 0) engine_->BestPaths({s}, true, &fr);
-          r->PushResult(frames > 0 ? PathWords(m, fr[0].arcs) : std::vector<WordSeg>(),
+          r->PushResult(frames > 0 ? SegmentMbr(engine_.get(), s, m, true, 0.9f) : MbrResult(),
                         r->segment_offset_);
           if (frames > 0) k++;
           continue;
@@ -414,9 +484,7 @@ void BatchModel::Worker() {
         const PathResult& p = nofinal[k++];
         if (EndpointRulesFire(m.endpoint, frames, TrailingSilenceFrames(m, p.arcs), shift,
                               p.final_relative_cost)) {
-          std::vector<PathResult> fr;
-          engine_->BestPaths({s}, true, &fr);
-          r->PushResult(PathWords(m, fr[0].arcs), r->segment_offset_);
+          r->PushResult(SegmentMbr(engine_.get(), s, m, true, 0.9f), r->segment_offset_);
           r->segment_offset_ += frames * shift;
           engine_->ResetDecoder(s);
         }
@@ -470,30 +538,33 @@ void BatchRecognizer::FinishStream() {  // batch_recognizer.cc:37-41
   buffer_.clear();
 }
 
-void BatchRecognizer::PushResult(const std::vector<WordSeg>& words, double offset) {
-  // batch_recognizer.cc:43-107 (1-best form; MBR confidences are a next row)
+void BatchRecognizer::PushResult(const MbrResult& r, double offset) {
+  // batch_recognizer.cc:43-107 (PushLattice: MBR words, confidences, rounded frame times)
   const ModelData& m = model_->data();
   std::string out;
   std::stringstream text;
-  for (size_t i = 0; i < words.size(); i++) {
+  for (size_t i = 0; i < r.words.size(); i++) {
     if (i) text << " ";
-    text << m.words.Find(words[i].word);
+    text << m.words.Find(r.words[i]);
   }
   if (nlsml_) {
+    float confidence = 0.0f;
+    for (float c : r.conf) confidence += c;
+    confidence /= (float)r.words.size();  // NaN for an empty result, as the reference
     std::stringstream ss;
     ss << "<?xml version=\"1.0\"?>\n<result grammar=\"default\">\n";
-    ss << "<interpretation grammar=\"default\" confidence=\"" << (words.empty() ? 0.0f : 1.0f)
+    ss << "<interpretation grammar=\"default\" confidence=\"" << confidence
        << "\">\n<input mode=\"speech\">" << text.str() << "</input>\n<instance>" << text.str()
        << "</instance>\n</interpretation>\n</result>\n";
     out = ss.str();
   } else {
     Json obj;
-    for (auto& w : words) {
+    for (size_t i = 0; i < r.words.size(); i++) {
       Json word;
-      word["word"] = Json::Str(m.words.Find(w.word));
-      word["start"] = Json::Float(std::round((double)w.start) * 0.03 + offset);
-      word["end"] = Json::Float(std::round((double)w.end) * 0.03 + offset);
-      word["conf"] = Json::Float(1.0);
+      word["word"] = Json::Str(m.words.Find(r.words[i]));
+      word["start"] = Json::Float(std::round((double)r.times[i].first) * 0.03 + offset);
+      word["end"] = Json::Float(std::round((double)r.times[i].second) * 0.03 + offset);
+      word["conf"] = Json::Float(r.conf[i]);
       obj["result"].Append(word);
     }
     obj["text"] = Json::Str(text.str());

@@ -135,7 +135,7 @@ class BatchRecognizer {
 
   // called from the batch worker
   int slot() const { return slot_; }
-  void PushResult(const std::vector<WordSeg>& words, double offset_s);
+  void PushResult(const MbrResult& r, double offset_s);
   double segment_offset_ = 0;  // seconds at the start of the current segment
   int frames_before_segment_ = 0;
 

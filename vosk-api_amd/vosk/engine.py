@@ -37,6 +37,9 @@ _SIGS = {
     "vamd_stream_update_silence_weights": (C.c_int, [_vp, C.c_int, C.c_int]),
     "vamd_stream_lattice": (C.c_int, [_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                       _vp, _vp, _vp]),
+    "vamd_lattice_words_json": (C.c_char_p, [C.c_int] + [_vp] * 8 + [C.c_int, _vp, C.c_int, _vp, _vp,
+                                                                   C.c_int, C.c_float, C.c_float,
+                                                                   C.c_int]),
     "vamd_silence_weighting_run": (C.c_int, [C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
                                              C.c_float, C.c_int, _vp, _vp, _vp, C.c_int]),
     "vamd_stream_stats": (C.c_int, [_vp, C.c_int, _vp, C.c_int]),
@@ -68,6 +71,28 @@ def _chk(r):
     if r is None or (isinstance(r, int) and r < 0):
         raise RuntimeError("libvosk engine error: " + _err())
     return r
+
+
+def lattice_words(L, arc_ilabel, arc_olabel, lattice_beam=6.0, graph_scale=0.9, nbest=5):
+    """Host-only: the result pipeline (prune, determinize, scale, MBR,
+    n-best) over a lattice in the vamd_stream_lattice array form."""
+    import json
+    il = np.ascontiguousarray(arc_ilabel, np.int32)
+    ol = np.ascontiguousarray(arc_olabel, np.int32)
+    a = {k: np.ascontiguousarray(L[k]) for k in ("frame_begin", "tok_state", "tok_cost", "link_src",
+                                                 "link_dst", "link_arc", "link_graph", "link_ac",
+                                                 "final_cost")}
+    fc = a["final_cost"] if len(a["final_cost"]) else np.zeros(1, np.float32)
+    r = _c.vamd_lattice_words_json(int(L["num_frames"]), a["frame_begin"].ctypes.data,
+                                   a["tok_state"].ctypes.data, a["tok_cost"].ctypes.data,
+                                   a["link_src"].ctypes.data, a["link_dst"].ctypes.data,
+                                   a["link_arc"].ctypes.data, a["link_graph"].ctypes.data,
+                                   a["link_ac"].ctypes.data, len(a["link_src"]), fc.ctypes.data,
+                                   len(L["final_cost"]), il.ctypes.data, ol.ctypes.data, len(il),
+                                   lattice_beam, graph_scale, nbest)
+    if r is None:
+        raise RuntimeError("vamd_lattice_words_json failed: " + _err())
+    return json.loads(r.decode())
 
 
 def silence_weighting_run(calls, tid_is_silence, silence_weight=1e-3, fss=3):
