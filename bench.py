@@ -52,7 +52,7 @@ def stream_audio(base, i, n):
 
 def bench_model(rank, dist):
     import make_synth_model
-    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", "bench_v2")
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", "bench_v3")
     if rank == 0 and not os.path.exists(os.path.join(cache, "README")):
         make_synth_model.make_model(cache, seed=11, vocab=20000, num_pdfs=2000)
     if dist is not None:

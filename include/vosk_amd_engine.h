@@ -38,7 +38,9 @@ int vamd_silence_weighting_run(int ncalls, const int *num_frames_ready, const in
 
 /* host-only: the result pipeline over a state-level lattice (the arrays of
  * vamd_stream_lattice; arc_ilabel / arc_olabel index the graph's arcs):
- * lattice-beam pruning, word determinization, graph scaling, MBR and n-best.
+ * lattice-beam pruning, word determinization, graph scaling, word alignment
+ * (when ntids > 0: per transition-id phone boundary type, IsFinal, IsSelfLoop),
+ * MBR and n-best.
  * Returns JSON {pruned_tokens, pruned_links, det_ok, det_states, det_arcs,
  * mbr: {words, conf, times}, nbest: [{words, spans, graph, acoustic}]}. */
 const char *vamd_lattice_words_json(int num_frames, const int *frame_begin, const int *tok_state,
@@ -46,7 +48,8 @@ const char *vamd_lattice_words_json(int num_frames, const int *frame_begin, cons
                                     const int *link_arc, const float *link_graph, const float *link_ac,
                                     int nlink, const float *final_cost, int nfinal, const int *arc_ilabel,
                                     const int *arc_olabel, int narcs, float lattice_beam, float graph_scale,
-                                    int nbest);
+                                    int nbest, const signed char *tid_type, const signed char *tid_final,
+                                    const signed char *tid_loop, int ntids);
 
 const char *vamd_last_error(void);
 int vamd_device_count(void);

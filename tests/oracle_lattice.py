@@ -493,3 +493,194 @@ def nbest(W, Fi, n):
             s, rank = d, r
         out.append(dict(words=words, spans=spans, graph=float(g), acoustic=float(a)))
     return out
+
+
+# ---------------------------------------------------------------- alignment
+def align_tables(tm, boundary_file):
+    """Per transition-id (phone boundary type, IsFinal, IsSelfLoop) from the
+    transition model and word_boundary.int (1 nonword .. 5 singleton)."""
+    names = {"nonword": 1, "begin": 2, "end": 3, "internal": 4, "singleton": 5}
+    ptype = {}
+    with open(boundary_file) as f:
+        for line in f:
+            p, t = line.split()
+            ptype[int(p)] = names[t]
+    ty = np.array([ptype.get(int(p), 0) for p in tm.tid2phone], np.int8)
+    ty[0] = 0
+    return ty, np.asarray(tm.tid_is_final, np.int8), np.asarray(tm.tid_is_selfloop, np.int8)
+
+
+def _phone_end(fin, loop, t, i):
+    n = len(t)
+    while i < n and not fin[t[i]]:
+        i += 1
+    if i == n:
+        return -1
+    i += 1
+    while i < n and loop[t[i]]:
+        i += 1
+    return -1 if i == n else i
+
+
+def _try_output(ty, fin, loop, t, w):
+    if not t:
+        return -1, 0
+    k = ty[t[0]]
+    if k == 1:
+        return _phone_end(fin, loop, t, 0), 0
+    if not w:
+        return -1, 0
+    if k == 5:
+        return _phone_end(fin, loop, t, 0), w[0]
+    if k == 2:
+        i = 0
+        while i < len(t) and ty[t[i]] != 3:
+            i += 1
+        if i == len(t):
+            return -1, 0
+        return _phone_end(fin, loop, t, i), w[0]
+    return -1, 0
+
+
+def word_align(W, Fi, tables):
+    """LatticeWordAligner restated as the C++ (csrc/lattice.cc) does it."""
+    ty, fin, loop = tables
+    S = len(W)
+    if S == 0:
+        return [], []
+    nodes, index, eps, outs, isfin, queue = [], {}, [], [], [], []
+
+    def get(n):
+        k = (n[0], tuple(n[1]), tuple(n[2]))
+        if k in index:
+            return index[k]
+        index[k] = len(nodes)
+        nodes.append(n)
+        eps.append([])
+        outs.append([])
+        isfin.append(False)
+        queue.append(len(nodes) - 1)
+        return len(nodes) - 1
+
+    get((0, [], []))
+    qi = 0
+    while qi < len(queue):
+        i = queue[qi]
+        qi += 1
+        s, t, w = nodes[i]
+        k, lab = _try_output(ty, fin, loop, t, w)
+        if k >= 0:
+            to = get((s, t[k:], w[1:] if lab != 0 else w))
+            outs[i].append((to, lab, list(t[:k])))
+            continue
+        if s < 0:
+            if not t and not w:
+                isfin[i] = True
+                continue
+            lab, nw = 0, w
+            if not (t and ty[t[0]] == 1) and w:
+                lab, nw = w[0], w[1:]
+            to = get((-1, [], nw))
+            outs[i].append((to, lab, list(t)))
+            continue
+        if Fi[s] is not None:
+            to = get((-1, t + list(Fi[s][2]), w))
+            eps[i].append((to, (F32(Fi[s][0]), F32(Fi[s][1]))))
+        for (word, d, g, a, p) in W[s]:
+            to = get((d, t + list(p), w + ([word] if word != 0 else [])))
+            eps[i].append((to, (F32(g), F32(a))))
+    N = len(nodes)
+    arcs = [[] for _ in range(N)]
+    fw, isf = [None] * N, [False] * N
+    for x in range(N):
+        # DFS postorder of the epsilon graph from x, reversed = topological
+        mark, topo, stk = {x: 1}, [], [[x, 0]]
+        while stk:
+            u, j = stk[-1]
+            if j < len(eps[u]):
+                stk[-1][1] += 1
+                v = eps[u][j][0]
+                if v not in mark:
+                    mark[v] = 1
+                    stk.append([v, 0])
+            else:
+                topo.append(u)
+                stk.pop()
+        topo.reverse()
+        clo = {x: (F32(0), F32(0))}
+        for u in topo:
+            for v, wt in eps[u]:
+                cand = (F32(clo[u][0] + wt[0]), F32(clo[u][1] + wt[1]))
+                if v not in clo or _cmp(cand, clo[v]) > 0:
+                    clo[v] = cand
+        for u in topo:
+            cw = clo[u]
+            for (to, lab, tids) in outs[u]:
+                arcs[x].append((lab, to, cw[0], cw[1], tids))
+            if isfin[u] and (not isf[x] or _cmp(cw, fw[x]) > 0):
+                isf[x] = True
+                fw[x] = cw
+    reach = [False] * N
+    reach[0] = True
+    st = [0]
+    while st:
+        u = st.pop()
+        for a in arcs[u]:
+            if not reach[a[1]]:
+                reach[a[1]] = True
+                st.append(a[1])
+    rev = [[] for _ in range(N)]
+    for u in range(N):
+        for a in arcs[u]:
+            rev[a[1]].append(u)
+    co = [False] * N
+    st = [u for u in range(N) if isf[u] and reach[u]]
+    for u in st:
+        co[u] = True
+    while st:
+        u = st.pop()
+        for p in rev[u]:
+            if not co[p] and reach[p]:
+                co[p] = True
+                st.append(p)
+    if not co[0]:
+        return [], []
+    indeg = [0] * N
+    for u in range(N):
+        if co[u]:
+            for a in arcs[u]:
+                if co[a[1]]:
+                    indeg[a[1]] += 1
+    order, st = [], [0]
+    while st:
+        u = st.pop()
+        order.append(u)
+        for a in reversed(arcs[u]):
+            if co[a[1]]:
+                indeg[a[1]] -= 1
+                if indeg[a[1]] == 0:
+                    st.append(a[1])
+    pos = {u: i for i, u in enumerate(order)}
+    A = [[(lab, pos[to], g, a, tids) for (lab, to, g, a, tids) in arcs[u] if co[to]] for u in order]
+    F = [None if not isf[u] else (fw[u][0], fw[u][1], []) for u in order]
+    return A, F
+
+
+def results(oracle, llh, use_final=True, graph_scale=0.9, nbest_n=0):
+    """The reference's result chain over the oracle decoder's lattice of
+    `llh`: prune, determinize, graph scale, word alignment (when the model has
+    word_boundary.int), then MBR (and n-best)."""
+    import os
+    r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
+                            use_final, lattice=True)
+    W, Fi = determinize(prune(raw_from_oracle(r, oracle.graph, use_final), 6.0),
+                        oracle.graph.ilabel, oracle.graph.olabel)
+    if graph_scale != 1.0:
+        W, Fi = scale_graph(W, Fi, graph_scale)
+    wb = os.path.join(oracle.dir, "graph", "phones", "word_boundary.int")
+    if os.path.exists(wb):
+        W, Fi = word_align(W, Fi, align_tables(oracle.tm, wb))
+    out = dict(mbr=mbr(W, Fi))
+    if nbest_n:
+        out["nbest"] = nbest(W, Fi, nbest_n)
+    return out

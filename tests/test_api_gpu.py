@@ -27,23 +27,12 @@ def _pcm(x):
 
 def _oracle_mbr(oracle, wave, chunk):
     import oracle_lattice as OL
-    llh = oracle.online(wave, chunk=chunk)["llh"]
-    r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
-                            True, lattice=True)
-    L = OL.raw_from_oracle(r, oracle.graph, True)
-    W, Fi = OL.determinize(OL.prune(L, 6.0), oracle.graph.ilabel, oracle.graph.olabel)
-    W, Fi = OL.scale_graph(W, Fi, 0.9)
-    return OL.mbr(W, Fi)
+    return OL.results(oracle, oracle.online(wave, chunk=chunk)["llh"])["mbr"]
 
 
 def _oracle_mbr_text(oracle, wave):
     import oracle_lattice as OL
-    llh = oracle.loglikes(wave)
-    r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
-                            True, lattice=True)
-    W, Fi = OL.determinize(OL.prune(OL.raw_from_oracle(r, oracle.graph, True), 6.0),
-                           oracle.graph.ilabel, oracle.graph.olabel)
-    mb = OL.mbr(*OL.scale_graph(W, Fi, 0.9))
+    mb = OL.results(oracle, oracle.loglikes(wave))["mbr"]
     return " ".join(oracle.words[w] for w in mb["words"])
 
 
@@ -180,12 +169,7 @@ def test_alternatives_and_nlsml_from_lattice(vosk_mod, synth_model_noep, test_wa
     import oracle_lattice as OL
     oracle = oracle_py.OracleModel(synth_model_noep)
     x = test_wave[:16000 * 5]
-    llh = oracle.online(x, chunk=4000)["llh"]
-    r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
-                            True, lattice=True)
-    W, Fi = OL.determinize(OL.prune(OL.raw_from_oracle(r, oracle.graph, True), 6.0),
-                           oracle.graph.ilabel, oracle.graph.olabel)
-    nb = OL.nbest(*OL.scale_graph(W, Fi, 0.9), 3)
+    nb = OL.results(oracle, oracle.online(x, chunk=4000)["llh"], nbest_n=3)["nbest"]
     m = vosk_mod.Model(synth_model_noep)
     outs = {}
     for nlsml in (False, True):

@@ -1,8 +1,9 @@
 """Result pipeline over lattices (host code of libvosk.so, csrc/lattice.cc)
 against its oracle restatement (tests/oracle_lattice.py): lattice-beam
-pruning, word-level determinization, graph scaling, Kaldi MBR (words,
-confidences, times) and n-best, on the oracle decoder's lattices of the
-synthetic models.  CPU only (host-only ABI, no GPU)."""
+pruning, word-level determinization, graph scaling, word alignment, Kaldi MBR
+(words, confidences, times) and n-best, on the oracle decoder's lattices of
+the synthetic models.  CPU only (host-only ABI, no GPU)."""
+import os
 import numpy as np
 import pytest
 
@@ -51,8 +52,9 @@ def test_cpp_pipeline_matches_restatement(synth_model, test_wave, secs, use_fina
     costs = [x["graph"] + x["acoustic"] for x in got["nbest"]]
     assert costs == sorted(costs)
     assert len({tuple(x["words"]) for x in got["nbest"]}) == len(got["nbest"])
-    if use_final:
-        assert got["nbest"][0]["words"] == r["words"]
+    # without the graph scale the first alternative is the decoder's best path
+    unscaled = engine.lattice_words(L, o.graph.ilabel, o.graph.olabel, 6.0, 1.0, 1)
+    assert unscaled["nbest"][0]["words"] == r["words"]
 
 
 def test_pruning_keeps_best_path_and_shrinks(synth_model, test_wave):
@@ -83,3 +85,44 @@ def test_mbr_confidences_on_a_two_word_choice():
     assert got["mbr"]["conf"][0] == pytest.approx(0.75, abs=1e-6)
     assert got["mbr"]["times"] == [[0, 1]]
     assert [x["words"] for x in got["nbest"]] == [[11], [12]]
+
+
+def _tables(o):
+    return OL.align_tables(o.tm, os.path.join(o.dir, "graph", "phones", "word_boundary.int"))
+
+
+@pytest.mark.parametrize("secs", [2, 4, 8.3])
+def test_word_alignment_matches_restatement(synth_model, test_wave, secs):
+    from vosk import engine
+    o, r, L = _lattice(synth_model, test_wave[:int(16000 * secs)])
+    tables = _tables(o)
+    got = engine.lattice_words(L, o.graph.ilabel, o.graph.olabel, 6.0, 0.9, 4, align=tables)
+    W, Fi = OL.scale_graph(*OL.determinize(OL.prune(L, 6.0), o.graph.ilabel, o.graph.olabel), 0.9)
+    A, AF = OL.word_align(W, Fi, tables)
+    assert got["align_ok"] == 1
+    assert got["align_states"] == len(A) and got["align_arcs"] == sum(len(v) for v in A)
+    mb, nb = OL.mbr(A, AF), OL.nbest(A, AF, 4)
+    assert got["mbr"]["words"] == mb["words"]
+    np.testing.assert_allclose(got["mbr"]["conf"], mb["conf"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(np.reshape(got["mbr"]["times"], (-1, 2)),
+                               np.reshape(mb["times"], (-1, 2)), rtol=0, atol=1e-4)
+    assert [x["words"] for x in got["nbest"]] == [x["words"] for x in nb]
+    assert [x["spans"] for x in got["nbest"]] == [[list(s) for s in x["spans"]] for x in nb]
+    # alignment keeps every path and its cost
+    nb0 = OL.nbest(W, Fi, 4)
+    assert [x["words"] for x in nb0] == [x["words"] for x in nb]
+    np.testing.assert_allclose([x["graph"] + x["acoustic"] for x in nb0],
+                               [x["graph"] + x["acoustic"] for x in nb], rtol=0, atol=1e-2)
+    # every aligned word arc spans whole phones from a begin (or singleton)
+    # phone to an end (or singleton) phone; silence arcs hold non-word phones
+    ty, fin, loop = tables
+    for arcs in A:
+        for (w, d, g, a, tids) in arcs:
+            if not tids:
+                continue
+            if w == 0:
+                assert all(ty[t] == 1 for t in tids) or d == len(A) - 1
+            else:
+                assert ty[tids[0]] in (2, 5)
+                ends = [t for t in tids if ty[t] in (3, 5) and fin[t]]
+                assert ends or d == len(A) - 1

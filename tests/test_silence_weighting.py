@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import oracle_py
+from conftest import perturbed_stream
 
 
 def _run_py(calls, sil, sw=1e-3, fss=3):
@@ -110,7 +111,7 @@ def test_silence_weighting_reweights_past_frames(synth_model, test_wave):
     negative deltas: the GPU test over it exercises the history ring, not only
     new frames."""
     o = oracle_py.OracleModel(synth_model)
-    ref = o.online(test_wave, chunk=4000)
+    ref = o.online(perturbed_stream(test_wave, 1, seconds=10.0), chunk=4000)
     prev, back = -1, 0
     for q, ents in zip(ref["requests"], ref["entries"]):
         back += sum(1 for f, _ in ents if f <= prev)

@@ -29,9 +29,13 @@ def _run_engine(model, wave, chunk, rate=16000):
     return e, s
 
 
-@pytest.mark.parametrize("secs,chunk", [(4, 4000), (None, 4000), (None, 16000)])
+@pytest.mark.parametrize("secs,chunk", [(4, 4000), (None, 4000), (None, 16000), ("p1", 4000)])
 def test_silence_weighted_stream_matches_oracle(synth_model, test_wave, secs, chunk):
-    x = test_wave if secs is None else test_wave[:16000 * secs]
+    """("p1": a 10 s perturbed stream whose traceback changes re-weight past
+    frames with negative deltas.)"""
+    from conftest import perturbed_stream
+    x = (test_wave if secs is None else perturbed_stream(test_wave, 1, seconds=10.0) if secs == "p1"
+         else test_wave[:16000 * secs])
     o = oracle_py.OracleModel(synth_model)
     ref = o.online(x, chunk=chunk)
     e, s = _run_engine(synth_model, x, chunk)

@@ -2,6 +2,7 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <fstream>
 #include <climits>
 #include <cmath>
 #include <cstdlib>
@@ -115,6 +116,22 @@ void ModelData::Load(const std::string& path) {
   has_word_boundary = FileExists(wb);
   int max_phone = 0;
   for (int p : tm.tid2phone) max_phone = std::max(max_phone, p);
+  if (has_word_boundary) {
+    phone_boundary.assign(max_phone + 1, 0);
+    std::ifstream in(wb);
+    int ph;
+    std::string type;
+    static const char* kTypes[] = {"", "nonword", "begin", "end", "internal", "singleton"};
+    while (in >> ph >> type) {
+      int t = 0;
+      for (int i = 1; i <= 5; i++)
+        if (type == kTypes[i]) t = i;
+      if (t == 0) VAMD_ERR("bad phone type '" << type << "' in " << wb);
+      if (ph >= 0 && ph <= max_phone) phone_boundary[ph] = (char)t;
+    }
+    tid_boundary.assign(tm.tid2phone.size(), 0);
+    for (size_t t = 1; t < tm.tid2phone.size(); t++) tid_boundary[t] = phone_boundary[tm.tid2phone[t]];
+  }
   phone_is_silence.assign(max_phone + 1, 0);
   for (int p : endpoint.silence_phones)
     if (p >= 0 && p <= max_phone) phone_is_silence[p] = 1;

@@ -40,6 +40,10 @@ struct ModelData {
   SymbolTable words;
   std::vector<char> phone_is_silence;  // indexed by phone id
   bool has_word_boundary = false;
+  // word_boundary.int (WordBoundaryInfo): per phone 1 nonword, 2 begin,
+  // 3 end, 4 internal, 5 singleton (0 = unlisted)
+  std::vector<char> phone_boundary;
+  std::vector<char> tid_boundary;  // the same per transition-id (word alignment)
   bool use_ivector = false;            // ivector/final.ie present (src/model.cc:247)
   IvectorModel ivec;
   // global_cmvn.stats present (src/model.cc:265-269): online CMVN (window 600,

@@ -723,3 +723,267 @@ void NbestPaths(const WordLattice& W, int n, std::vector<NbestPath>* out) {
 }
 
 }  // namespace vamd
+
+// ===========================================================================
+// word alignment
+// ===========================================================================
+namespace vamd {
+
+namespace {
+
+struct AlignCtx {
+  const std::vector<char>& type;  // per tid: boundary type of its phone
+  const std::vector<char>& fin;   // per tid: IsFinal
+  const std::vector<char>& loop;  // per tid: IsSelfLoop
+  int Type(int tid) const { return tid < (int)type.size() ? type[tid] : 0; }
+};
+
+// index just past the phone that starts at i (its final transition-id and,
+// with reorder, the self-loops after it); -1 if the phone is not known to be
+// complete within t
+int PhoneEnd(const AlignCtx& c, const std::vector<int>& t, size_t i) {
+  const size_t len = t.size();
+  for (; i < len; i++)
+    if (c.fin[t[i]]) break;
+  if (i == len) return -1;
+  i++;
+  while (i < len && c.loop[t[i]]) i++;
+  if (i == len) return -1;
+  return (int)i;
+}
+
+// LatticeWordAligner::ComputationState::OutputArc: silence phone, one-phone
+// word, normal word; returns the number of transition-ids consumed and the
+// label (0 for silence), or -1 if nothing can be output yet
+int TryOutput(const AlignCtx& c, const std::vector<int>& t, const std::vector<int>& words, int* label) {
+  if (t.empty()) return -1;
+  const int ty = c.Type(t[0]);
+  if (ty == 1) {  // nonword
+    *label = 0;
+    return PhoneEnd(c, t, 0);
+  }
+  if (words.empty()) return -1;
+  if (ty == 5) {  // begin-and-end
+    *label = words[0];
+    return PhoneEnd(c, t, 0);
+  }
+  if (ty == 2) {  // begin: up to the end phone's end
+    size_t i = 0;
+    while (i < t.size() && c.Type(t[i]) != 3) i++;
+    if (i == t.size()) return -1;
+    *label = words[0];
+    return PhoneEnd(c, t, i);
+  }
+  return -1;
+}
+
+struct ANode {
+  int in;                  // input (word lattice) state, -1 = past a final flush
+  std::vector<int> t, w;   // pending transition-ids and word labels
+};
+
+}  // namespace
+
+bool WordAlignLattice(const WordLattice& W, const std::vector<char>& type, const std::vector<char>& fin,
+                      const std::vector<char>& loop, int max_states, WordLattice* out) {
+  *out = WordLattice();
+  const int S = W.NumStates();
+  if (S == 0) return true;
+  const AlignCtx c{type, fin, loop};
+  std::vector<ANode> nodes;
+  std::unordered_map<std::string, int> index;
+  // node edges: epsilon advances (weight) and output arcs (label, tids)
+  struct Eps { int to; LW w; };
+  struct Out { int to, label; std::vector<int> tids; };
+  std::vector<std::vector<Eps>> eps;
+  std::vector<std::vector<Out>> outs;
+  std::vector<char> is_final;
+  auto key_of = [](const ANode& n) {
+    std::string k((const char*)&n.in, sizeof(int));
+    const int a = (int)n.t.size(), b = (int)n.w.size();
+    k.append((const char*)&a, sizeof(int));
+    k.append((const char*)n.t.data(), sizeof(int) * a);
+    k.append((const char*)&b, sizeof(int));
+    k.append((const char*)n.w.data(), sizeof(int) * b);
+    return k;
+  };
+  std::vector<int> queue;
+  auto get = [&](ANode&& n) {
+    const std::string k = key_of(n);
+    auto it = index.find(k);
+    if (it != index.end()) return it->second;
+    const int id = (int)nodes.size();
+    index[k] = id;
+    nodes.push_back(std::move(n));
+    eps.emplace_back();
+    outs.emplace_back();
+    is_final.push_back(0);
+    queue.push_back(id);
+    return id;
+  };
+  get(ANode{0, {}, {}});
+  for (size_t qi = 0; qi < queue.size(); qi++) {
+    if ((int)nodes.size() > max_states) return false;
+    const int id = queue[qi];
+    const ANode n = nodes[id];
+    int label = 0;
+    const int k = TryOutput(c, n.t, n.w, &label);
+    if (k >= 0) {  // something pending goes out first (no advancing)
+      ANode m{n.in, std::vector<int>(n.t.begin() + k, n.t.end()), n.w};
+      if (label != 0) m.w.erase(m.w.begin());
+      std::vector<int> tids(n.t.begin(), n.t.begin() + k);
+      const int to = get(std::move(m));
+      outs[id].push_back(Out{to, label, std::move(tids)});
+      continue;
+    }
+    if (n.in < 0) {  // past the input's final weight: flush (OutputArcForce)
+      if (n.t.empty() && n.w.empty()) {
+        is_final[id] = 1;
+        continue;
+      }
+      // a leading non-word phone: everything pending goes out as silence
+      // (word labels follow with empty strings); else a partial word with
+      // the first pending label (partial_word_label 0 if none)
+      ANode m{-1, {}, n.w};
+      int lab = 0;
+      if (!(!n.t.empty() && c.Type(n.t[0]) == 1) && !m.w.empty()) {
+        lab = m.w[0];
+        m.w.erase(m.w.begin());
+      }
+      const int to = get(std::move(m));
+      outs[id].push_back(Out{to, lab, n.t});
+      continue;
+    }
+    // the input state's final weight (CreateSuperFinal: an epsilon arc with
+    // the final string into a super-final input state)
+    if (W.final_graph[n.in] != INFINITY) {
+      ANode m{-1, n.t, n.w};
+      m.t.insert(m.t.end(), W.final_tids[n.in].begin(), W.final_tids[n.in].end());
+      const int to = get(std::move(m));
+      eps[id].push_back(Eps{to, LW{W.final_graph[n.in], W.final_acoustic[n.in]}});
+    }
+    for (const auto& a : W.arcs[n.in]) {
+      ANode m{a.next, n.t, n.w};
+      m.t.insert(m.t.end(), a.tids.begin(), a.tids.end());
+      if (a.word != 0) m.w.push_back(a.word);
+      const int to = get(std::move(m));
+      eps[id].push_back(Eps{to, LW{a.graph, a.acoustic}});
+    }
+  }
+  // RmEpsilon: each node's output arcs and finality through its epsilon
+  // closure (best weight per reached node, Kaldi LatticeWeight order)
+  const int N = (int)nodes.size();
+  std::vector<std::vector<WordLattice::Arc>> arcs(N);
+  std::vector<LW> fw(N);
+  std::vector<char> isf(N, 0);
+  for (int x = 0; x < N; x++) {
+    std::unordered_map<int, LW> clo;
+    std::vector<int> order, st{x};
+    clo[x] = LW{};
+    // the epsilon graph is acyclic: relax in DFS discovery order, then
+    // settle in topological order
+    std::vector<int> topo;
+    {
+      std::unordered_map<int, int> mark;  // 1 = visiting, 2 = done
+      std::vector<std::pair<int, size_t>> stk{{x, 0}};
+      mark[x] = 1;
+      while (!stk.empty()) {
+        auto& [u, i] = stk.back();
+        if (i < eps[u].size()) {
+          const int v = eps[u][i++].to;
+          if (!mark.count(v)) {
+            mark[v] = 1;
+            stk.push_back({v, 0});
+          }
+        } else {
+          mark[u] = 2;
+          topo.push_back(u);
+          stk.pop_back();
+        }
+      }
+      std::reverse(topo.begin(), topo.end());
+    }
+    for (int u : topo)
+      for (const Eps& e : eps[u]) {
+        const LW cand = Times(clo[u], e.w);
+        auto it = clo.find(e.to);
+        if (it == clo.end() || CompareLW(cand, it->second) > 0) clo[e.to] = cand;
+      }
+    for (int u : topo) {
+      const LW cw = clo[u];
+      for (const Out& o : outs[u]) arcs[x].push_back(WordLattice::Arc{o.label, o.to, cw.g, cw.a, o.tids});
+      if (is_final[u] && (!isf[x] || CompareLW(cw, fw[x]) > 0)) {
+        isf[x] = 1;
+        fw[x] = cw;
+      }
+    }
+  }
+  // connect: states reachable by output arcs from the start and co-reachable
+  std::vector<char> reach(N, 0), coreach(N, 0);
+  std::vector<int> st{0};
+  reach[0] = 1;
+  while (!st.empty()) {
+    const int u = st.back();
+    st.pop_back();
+    for (auto& a : arcs[u])
+      if (!reach[a.next]) {
+        reach[a.next] = 1;
+        st.push_back(a.next);
+      }
+  }
+  std::vector<std::vector<int>> rev(N);
+  for (int u = 0; u < N; u++)
+    for (auto& a : arcs[u]) rev[a.next].push_back(u);
+  for (int u = 0; u < N; u++)
+    if (isf[u] && reach[u]) {
+      coreach[u] = 1;
+      st.push_back(u);
+    }
+  while (!st.empty()) {
+    const int u = st.back();
+    st.pop_back();
+    for (int p : rev[u])
+      if (!coreach[p] && reach[p]) {
+        coreach[p] = 1;
+        st.push_back(p);
+      }
+  }
+  if (!coreach[0]) return true;  // nothing complete: empty lattice
+  // topological renumbering (output arcs only; acyclic), start first
+  std::vector<int> indeg(N, 0), order;
+  for (int u = 0; u < N; u++)
+    if (coreach[u])
+      for (auto& a : arcs[u])
+        if (coreach[a.next]) indeg[a.next]++;
+  st.assign(1, 0);
+  while (!st.empty()) {
+    const int u = st.back();
+    st.pop_back();
+    order.push_back(u);
+    for (auto it = arcs[u].rbegin(); it != arcs[u].rend(); ++it)
+      if (coreach[it->next] && --indeg[it->next] == 0) st.push_back(it->next);
+  }
+  std::vector<int> pos(N, -1);
+  for (size_t i = 0; i < order.size(); i++) pos[order[i]] = (int)i;
+  const int M = (int)order.size();
+  out->arcs.resize(M);
+  out->final_graph.assign(M, INFINITY);
+  out->final_acoustic.assign(M, 0.0f);
+  out->final_tids.resize(M);
+  for (int i = 0; i < M; i++) {
+    const int u = order[i];
+    for (auto& a : arcs[u])
+      if (coreach[a.next]) {
+        WordLattice::Arc b = a;
+        b.next = pos[a.next];
+        out->arcs[i].push_back(std::move(b));
+      }
+    if (isf[u]) {
+      out->final_graph[i] = fw[u].g;
+      out->final_acoustic[i] = fw[u].a;
+    }
+  }
+  return true;
+}
+
+}  // namespace vamd

@@ -88,6 +88,19 @@ void PruneRawLattice(RawLattice* lat, float lattice_beam);
 bool DeterminizeToWords(const RawLattice& lat, const Graph& g, const LatticeOptions& opt,
                         WordLattice* out);
 
+// Word alignment (Kaldi lat/word-align-lattice.cc WordAlignLattice [K], with
+// WordBoundaryInfo from word_boundary.int and reorder = true; the reference
+// aligns before MBR and n-best, src/recognizer.cc:433-434,555-558,
+// src/batch_recognizer.cc:48): every output arc spans exactly one word (begin
+// .. end phone, or a singleton phone) or one non-word phone (word 0), the
+// word label moved onto its phones.  Per-state pending transition-ids and
+// word labels (the aligner's computation state), advance weights on epsilon
+// transitions removed at the end (RmEpsilon).  phone_type per phone: 1
+// nonword, 2 begin, 3 end, 4 internal, 5 singleton.  False if the guard trips.
+bool WordAlignLattice(const WordLattice& in, const std::vector<char>& tid2phone_type,
+                      const std::vector<char>& tid2final, const std::vector<char>& tid2selfloop,
+                      int max_states, WordLattice* out);
+
 // Scale the graph part of every weight (fst::GraphLatticeScale, src/recognizer.cc:718)
 void ScaleGraph(WordLattice* lat, float scale);
 

@@ -586,6 +586,8 @@ void ReadFinalMdl(const std::string& path, TransitionModel* tm, Nnet* nnet) {
   int n_tuples = r.I32();
   tm->tid2pdf.assign(1, -1);
   tm->tid2phone.assign(1, 0);
+  tm->tid2selfloop.assign(1, 0);
+  tm->tid2final.assign(1, 0);
   int max_pdf = -1;
   for (int i = 0; i < n_tuples; i++) {
     int phone = r.I32(), hmm_state = r.I32(), fpdf = r.I32();
@@ -598,6 +600,8 @@ void ReadFinalMdl(const std::string& path, TransitionModel* tm, Nnet* nnet) {
       int pdf = self_loop ? spdf : fpdf;
       tm->tid2pdf.push_back(pdf);
       tm->tid2phone.push_back(phone);
+      tm->tid2selfloop.push_back(self_loop ? 1 : 0);
+      tm->tid2final.push_back(dst == (int)entries[phone2idx[phone]].size() - 1 ? 1 : 0);
       max_pdf = std::max(max_pdf, pdf);
     }
   }

@@ -93,6 +93,8 @@ void ApplyModelOptions(const std::map<std::string, std::string>& kv, DecoderOpti
 struct TransitionModel {
   std::vector<int> tid2pdf;    // index 0 unused
   std::vector<int> tid2phone;  // index 0 unused
+  std::vector<char> tid2selfloop;  // transition back to its own HMM state (index 0 unused)
+  std::vector<char> tid2final;     // transition into the HMM's final state (IsFinal)
   int num_pdfs = 0;
   int NumTransitionIds() const { return (int)tid2pdf.size() - 1; }
 };

@@ -299,7 +299,8 @@ const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, cons
                                     const int* link_arc, const float* link_graph, const float* link_ac,
                                     int nlink, const float* final_cost, int nfinal, const int* arc_ilabel,
                                     const int* arc_olabel, int narcs, float lattice_beam, float graph_scale,
-                                    int nbest) {
+                                    int nbest, const signed char* tid_type, const signed char* tid_final,
+                                    const signed char* tid_loop, int ntids) {
   static thread_local std::string out;
   API_TRY
   RawLattice L;
@@ -327,6 +328,17 @@ const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, cons
   for (auto& v : wl.arcs) det_arcs += (int)v.size();
   os << ", \"det_arcs\": " << det_arcs;
   if (graph_scale != 1.0f) ScaleGraph(&wl, graph_scale);
+  if (ntids > 0) {
+    std::vector<char> ty(tid_type, tid_type + ntids), fi(tid_final, tid_final + ntids),
+        lo(tid_loop, tid_loop + ntids);
+    WordLattice al;
+    const bool aok = WordAlignLattice(wl, ty, fi, lo, 1000000, &al);
+    int aarcs = 0;
+    for (auto& v : al.arcs) aarcs += (int)v.size();
+    os << ", \"align_ok\": " << (aok ? 1 : 0) << ", \"align_states\": " << al.NumStates()
+       << ", \"align_arcs\": " << aarcs;
+    wl = std::move(al);
+  }
   MbrResult r;
   MinimumBayesRisk(wl, &r);
   os << ", \"mbr\": {\"words\": [";

@@ -189,7 +189,10 @@ bool Recognizer::EndpointDetected() {
 // The decoder segment's lattice (kept on the GPU), pruned at the lattice beam
 // and determinized on words; false if unavailable (no lattice engine,
 // overflow, determinization guard).
-static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use_final, WordLattice* wl) {
+// Then the graph scale, and word alignment when the model has
+// word_boundary.int (WordAlignLattice, :433-434; CopyLatticeForMbr otherwise).
+static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use_final, float graph_scale,
+                               WordLattice* wl) {
   RawLattice raw;
   e->GetRawLattice(slot, use_final, &raw);
   if (raw.overflow || raw.tok_state.empty()) return false;
@@ -197,6 +200,16 @@ static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use
   LatticeOptions opt;
   opt.lattice_beam = m.dec.lattice_beam;
   if (!DeterminizeToWords(raw, m.graph, opt, wl) || wl->NumStates() == 0) return false;
+  if (graph_scale != 1.0f) ScaleGraph(wl, graph_scale);
+  if (m.has_word_boundary) {
+    WordLattice al;
+    if (!WordAlignLattice(*wl, m.tid_boundary, m.tm.tid2final, m.tm.tid2selfloop, opt.max_states, &al) ||
+        al.NumStates() == 0) {
+      VAMD_WARN("word alignment failed; using the unaligned lattice");
+      return true;
+    }
+    *wl = std::move(al);
+  }
   return true;
 }
 
@@ -206,8 +219,7 @@ static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use
 static MbrResult SegmentMbr(Engine* e, int slot, const ModelData& m, bool use_final, float graph_scale) {
   MbrResult r;
   WordLattice wl;
-  if (SegmentWordLattice(e, slot, m, use_final, &wl)) {
-    if (graph_scale != 1.0f) ScaleGraph(&wl, graph_scale);
+  if (SegmentWordLattice(e, slot, m, use_final, graph_scale, &wl)) {
     MinimumBayesRisk(wl, &r);
     return r;
   }
@@ -259,8 +271,7 @@ const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
   // paths of the graph-scaled word lattice, likelihood = -(graph + acoustic)
   std::vector<NbestPath> nb;
   WordLattice wl;
-  if (SegmentWordLattice(engine_, slot_, m, true, &wl)) {
-    ScaleGraph(&wl, 0.9f);
+  if (SegmentWordLattice(engine_, slot_, m, true, 0.9f, &wl)) {
     NbestPaths(wl, max_alternatives_, &nb);
   } else {
     std::vector<PathResult> pr;

@@ -287,6 +287,7 @@ class TransitionModel:
     tid2pdf: np.ndarray = field(default=None)
     tid2phone: np.ndarray = field(default=None)
     tid_is_selfloop: np.ndarray = field(default=None)
+    tid_is_final: np.ndarray = field(default=None)  # into the HMM's final state (IsFinal)
     tuple_first_tid: np.ndarray = field(default=None)
 
     def derive(self):
@@ -297,18 +298,22 @@ class TransitionModel:
         pdf = [0]
         phone = [0]
         sl = [0]
+        fin = [0]
         first = []
         for (ph, hs, fpdf, spdf) in self.tuples:
             first.append(len(pdf))
-            st = self.topo.entries[self.topo.phone2idx[ph]][hs]
+            entry = self.topo.entries[self.topo.phone2idx[ph]]
+            st = entry[hs]
             for (dst, _p) in st.transitions:
                 is_sl = dst == hs
                 pdf.append(spdf if is_sl else fpdf)
                 phone.append(ph)
                 sl.append(1 if is_sl else 0)
+                fin.append(1 if dst == len(entry) - 1 else 0)
         self.tid2pdf = np.array(pdf, np.int32)
         self.tid2phone = np.array(phone, np.int32)
         self.tid_is_selfloop = np.array(sl, np.int32)
+        self.tid_is_final = np.array(fin, np.int32)
         self.tuple_first_tid = np.array(first, np.int32)
         return self
 

@@ -115,13 +115,21 @@ def build_transition_model(rng, num_phones, num_pdfs):
     return tm, tids
 
 
-def build_graph(rng, tids, num_phones, vocab):
-    """Lexicon prefix tree + unigram loop.  Returns kf.Fst and words list."""
+def position_phone(base, pos, n, num_base):
+    """Word-position-dependent phone (Kaldi _B/_E/_I/_S): base phones
+    2..num_base map to 2 + 4*(base-2) + {0 begin, 1 end, 2 internal, 3 singleton}."""
+    k = 3 if n == 1 else (0 if pos == 0 else (1 if pos == n - 1 else 2))
+    return 2 + 4 * (base - 2) + k
+
+
+def build_graph(rng, tids, num_base, vocab):
+    """Lexicon prefix tree over word-position-dependent phones + unigram
+    loop.  Returns kf.Fst and words list (prons in base phones)."""
     words = []
     seen = set()
     while len(words) < vocab:
-        n = int(rng.integers(2, 8))
-        pron = tuple(int(p) for p in rng.integers(2, num_phones + 1, size=n))
+        n = int(rng.integers(1, 8))
+        pron = tuple(int(p) for p in rng.integers(2, num_base + 1, size=n))
         if pron in seen:
             continue
         seen.add(pron)
@@ -156,7 +164,8 @@ def build_graph(rng, tids, num_phones, vocab):
     for wi, pron in enumerate(words):
         node = LOOP
         prev = 0
-        for ph in pron:
+        for j, bph in enumerate(pron):
+            ph = position_phone(bph, j, len(pron), num_base)
             key = (node, ph)
             if key not in children:
                 child = new_state()
@@ -401,7 +410,9 @@ def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_st
         f.write(MODEL_CONF)
     mo = nk.MfccOpts(kf.parse_conf(conf_path), fbank=fb)
 
-    tm, tids = build_transition_model(rng, num_phones, num_pdfs)
+    # silence + 4 word-position variants of each of the other base phones
+    num_pos_phones = 1 + 4 * (num_phones - 1)
+    tm, tids = build_transition_model(rng, num_pos_phones, num_pdfs)
     fst, words = build_graph(rng, tids, num_phones, vocab)
     nn = build_nnet(rng, num_pdfs, mo, ivector_dim)
     feats = nk.features(load_test_wav(), mo)
@@ -428,11 +439,11 @@ def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_st
         f.write(f"#0 {len(words) + 1}\n<s> {len(words) + 2}\n</s> {len(words) + 3}\n")
     with open(os.path.join(out_dir, "graph", "phones", "word_boundary.int"), "w") as f:
         f.write("1 nonword\n")
-        for p in range(2, num_phones + 1):
-            f.write(f"{p} internal\n")
+        for p in range(2, num_pos_phones + 1):
+            f.write(f"{p} {('begin', 'end', 'internal', 'singleton')[(p - 2) % 4]}\n")
     with open(os.path.join(out_dir, "README"), "w") as f:
         f.write(f"synthetic vosk-api_amd model seed={seed} vocab={vocab} pdfs={num_pdfs} "
-                f"phones={num_phones} ivector_dim={ivector_dim} frontend={frontend} "
+                f"phones={num_pos_phones} ivector_dim={ivector_dim} frontend={frontend} "
                 f"global_cmvn={int(global_cmvn)} states={fst.num_states} "
                 f"arcs={fst.num_arcs}\n")
     return out_dir

@@ -39,7 +39,7 @@ _SIGS = {
                                       _vp, _vp, _vp]),
     "vamd_lattice_words_json": (C.c_char_p, [C.c_int] + [_vp] * 8 + [C.c_int, _vp, C.c_int, _vp, _vp,
                                                                    C.c_int, C.c_float, C.c_float,
-                                                                   C.c_int]),
+                                                                   C.c_int, _vp, _vp, _vp, C.c_int]),
     "vamd_silence_weighting_run": (C.c_int, [C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
                                              C.c_float, C.c_int, _vp, _vp, _vp, C.c_int]),
     "vamd_stream_stats": (C.c_int, [_vp, C.c_int, _vp, C.c_int]),
@@ -73,9 +73,11 @@ def _chk(r):
     return r
 
 
-def lattice_words(L, arc_ilabel, arc_olabel, lattice_beam=6.0, graph_scale=0.9, nbest=5):
+def lattice_words(L, arc_ilabel, arc_olabel, lattice_beam=6.0, graph_scale=0.9, nbest=5, align=None):
     """Host-only: the result pipeline (prune, determinize, scale, MBR,
-    n-best) over a lattice in the vamd_stream_lattice array form."""
+    n-best) over a lattice in the vamd_stream_lattice array form; align =
+    (tid phone-boundary type, tid IsFinal, tid IsSelfLoop) arrays to word-align
+    before MBR / n-best."""
     import json
     il = np.ascontiguousarray(arc_ilabel, np.int32)
     ol = np.ascontiguousarray(arc_olabel, np.int32)
@@ -83,13 +85,16 @@ def lattice_words(L, arc_ilabel, arc_olabel, lattice_beam=6.0, graph_scale=0.9, 
                                                  "link_dst", "link_arc", "link_graph", "link_ac",
                                                  "final_cost")}
     fc = a["final_cost"] if len(a["final_cost"]) else np.zeros(1, np.float32)
+    al = [np.ascontiguousarray(x, np.int8) for x in align] if align is not None else None
     r = _c.vamd_lattice_words_json(int(L["num_frames"]), a["frame_begin"].ctypes.data,
                                    a["tok_state"].ctypes.data, a["tok_cost"].ctypes.data,
                                    a["link_src"].ctypes.data, a["link_dst"].ctypes.data,
                                    a["link_arc"].ctypes.data, a["link_graph"].ctypes.data,
                                    a["link_ac"].ctypes.data, len(a["link_src"]), fc.ctypes.data,
                                    len(L["final_cost"]), il.ctypes.data, ol.ctypes.data, len(il),
-                                   lattice_beam, graph_scale, nbest)
+                                   lattice_beam, graph_scale, nbest,
+                                   *(([x.ctypes.data for x in al] + [len(al[0])]) if al is not None
+                                     else [None, None, None, 0]))
     if r is None:
         raise RuntimeError("vamd_lattice_words_json failed: " + _err())
     return json.loads(r.decode())
