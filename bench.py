@@ -173,9 +173,11 @@ def main():
     tot = e.decoder_totals()
     errs = sum(1 for s in streams if e.error(s))
     # decoder roofline: algorithmic bytes per launch:
-    # 16*T_in + 16*E + 8*E + 16*T_new + 20*L, L = T_new backpointer links
+    # 16*T_in + 16*E + 8*E + 16*T_new + 20*L, L = T_new backpointer links,
+    # plus 16 B per lattice link record kept in HBM
     E = tot["arcs_emit"] + tot["arcs_eps"]
-    dec_bytes = 16 * tot["tok_in"] + 24 * E + 16 * tot["tok_out"] + 20 * tot["tok_out"]
+    dec_bytes = (16 * tot["tok_in"] + 24 * E + 16 * tot["tok_out"] + 20 * tot["tok_out"]
+                 + 16 * tot.get("links", 0))
     dec_ms, dec_n = st["decode"]
     nnet_ms, nnet_n = st["nnet"]
     front_ms, front_n = st["front"]
@@ -241,6 +243,7 @@ def main():
             "decoder": {"frames": tot["frames"],
                         "tokens_per_frame": round(tot["tok_out"] / max(tot["frames"], 1), 1),
                         "arcs_per_frame": round(E / max(tot["frames"], 1), 1),
+                        "lattice_links_per_frame": round(tot.get("links", 0) / max(tot["frames"], 1), 1),
                         "stream_errors": errs},
             "cpu_baseline": cpu,
         }

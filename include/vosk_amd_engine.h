@@ -124,8 +124,9 @@ int vamd_engine_set_step_samples(VamdEngine *e, int n);
  * [samples+MFCC, nnet ops, decoder, whole step]; reset=1 clears them */
 int vamd_engine_stage_times(VamdEngine *e, double *ms4, long long *launches4, int reset);
 /* decoder work since the last stage-time reset (flag 1): [frames, tokens in,
- * tokens out, emitting arcs examined, epsilon arcs examined] */
-int vamd_engine_decoder_totals(VamdEngine *e, long long *out5);
+ * tokens out, emitting arcs examined, epsilon arcs examined, lattice links
+ * written] */
+int vamd_engine_decoder_totals(VamdEngine *e, long long *out6);
 /* decoder phase clocks (env VOSK_AMD_DEC_PROFILE=1), summed over streams:
  * [cutoff, seed, expand, compact, eps-closure, commit, 0, frames] */
 int vamd_engine_decoder_phases(VamdEngine *e, long long *out8);

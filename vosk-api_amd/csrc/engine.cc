@@ -1040,6 +1040,10 @@ void Engine::FinishDecodeBatch(const DecBatch& b) {
         times_.dec[3] += fs.arcs_emit;
         times_.dec[4] += fs.arcs_eps;
       }
+      // links written by this launch (the counter restarts with the decoder)
+      const long long lu = ds.links_used;
+      times_.dec[5] += lu >= h.links_seen ? lu - h.links_seen : lu;
+      h.links_seen = lu;
     }
   }
 }

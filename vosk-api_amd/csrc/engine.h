@@ -84,7 +84,7 @@ struct StageTimes {
   long long launches[4] = {0, 0, 0, 0};
   // decoder work totals (collect_stats): frames, tokens in, tokens out,
   // emitting arcs examined, epsilon arcs examined
-  long long dec[5] = {0, 0, 0, 0, 0};
+  long long dec[6] = {0, 0, 0, 0, 0, 0};  // [5] lattice links written
 };
 
 struct PathResult {
@@ -202,6 +202,7 @@ class Engine {
     int iv_norm_done = 0, iv_norm_to = 0;  // frames CMVN-normalized (after this step)
     int iv_stats_done = 0;     // frames accumulated into the i-vector statistics
     std::vector<float> ivecs;  // collect_llh: per-chunk i-vectors
+    long long links_seen = 0;  // lattice links counted so far (stage totals)
     // silence weighting: the decoder segment's weighting state and the
     // stream's queue of (feature frame, delta weight) not yet applied
     bool iv_weighted = false;

@@ -603,10 +603,10 @@ int vamd_engine_stage_times(VamdEngine* e, double* ms4, long long* launches4, in
   API_CATCH(-1)
 }
 
-int vamd_engine_decoder_totals(VamdEngine* e, long long* o5) {
+int vamd_engine_decoder_totals(VamdEngine* e, long long* o6) {
   API_TRY
   const StageTimes& t = e->eng->stage_times();
-  for (int i = 0; i < 5; i++) o5[i] = t.dec[i];
+  for (int i = 0; i < 6; i++) o6[i] = t.dec[i];
   return 0;
   API_CATCH(-1)
 }

@@ -286,9 +286,9 @@ class Engine:
         return {n: (float(m), int(l)) for n, m, l in zip(names, ms, ln)}
 
     def decoder_totals(self):
-        out = np.zeros(5, np.int64)
+        out = np.zeros(6, np.int64)
         _chk(_c.vamd_engine_decoder_totals(self.h, out.ctypes.data))
-        return dict(zip(("frames", "tok_in", "tok_out", "arcs_emit", "arcs_eps"), out.tolist()))
+        return dict(zip(("frames", "tok_in", "tok_out", "arcs_emit", "arcs_eps", "links"), out.tolist()))
 
     def decoder_phases(self):
         out = np.zeros(8, np.int64)
