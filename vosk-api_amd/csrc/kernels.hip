@@ -1981,14 +1981,38 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     lds = true;
   }
 
+  // log-likelihood rows staged in LDS: row f+1 is loaded into registers
+  // while frame f is processed and written to L once frame f's emitting
+  // expansion no longer reads it (just before its commit)
+  constexpr int kLlhRegs = kLlhLds / DT;
+  const bool stage_llh = a.P <= kLlhLds;
+  float nxt[kLlhRegs];
+  if (stage_llh && job.nframes > 0) {
+    const float* llh0 = a.llh + (size_t)job.llh_row0 * a.P;
+    for (int i = threadIdx.x; i < a.P; i += DT) L[i] = llh0[i];
+  }
   for (int f = 0; f < job.nframes; f++) {
     if (st.ntok == 0 || st.err) break;
     const float* llh = a.llh + (size_t)(job.llh_row0 + f) * a.P;
-    const float* Lp = llh;
-    if (a.P <= kLlhLds) {
-      for (int i = threadIdx.x; i < a.P; i += DT) L[i] = llh[i];
-      Lp = L;
+    const float* Lp = stage_llh ? L : llh;
+    const bool pf = stage_llh && f + 1 < job.nframes;
+    if (pf) {
+      const float* nrow = llh + a.P;
+#pragma unroll
+      for (int r = 0; r < kLlhRegs; r++) {
+        const int i = threadIdx.x + r * DT;
+        nxt[r] = i < a.P ? nrow[i] : 0.0f;
+      }
     }
+    auto store_next = [&]() {
+      if (pf) {
+#pragma unroll
+        for (int r = 0; r < kLlhRegs; r++) {
+          const int i = threadIdx.x + r * DT;
+          if (i < a.P) L[i] = nxt[r];
+        }
+      }
+    };
     const int ntok = st.ntok;
     const TokView tv{p.cs, p.cc, TS, TC, lds};
     // ---- GetCutoff (best token: min (cost, state), kept by the previous commit)
@@ -2089,6 +2113,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       DEC_PHASE(4);
     }
     if (try_lds && !sh.ovf) {
+      store_next();  // L is not read again in this frame (barrier inside the commit)
       commit_lds(a, sh, p, t, st, TS, TC, &lds, next_cutoff, &new_best);
     } else {
       // ---- global maps: a single emitting pass relaxing below the seed
@@ -2124,6 +2149,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       DEC_PHASE(2);
       eps_closure(a, sh, p, st, next_cutoff, sh.n_front0, &arcs_eps, slot);
       DEC_PHASE(4);
+      store_next();
       commit(a, sh, p, st, TS, TC, &lds, next_cutoff, &new_best);
     }
     DEC_PHASE(5);
