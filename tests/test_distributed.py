@@ -78,3 +78,54 @@ def test_two_rank_sharding_matches_single_process(synth_model):
     for sid in range(4):
         ref = m.recognize(perturbed_stream(base, sid, seconds=1.5))["path"].tolist()
         assert merged[sid] == ref
+
+
+# ---- admission-time sharding (vosk/shard.py): one int32 all-gather per epoch
+def test_plan_admission_prefers_free_capacity():
+    from vosk.shard import plan_admission
+    plan, head = plan_admission([2, 5, 0, 5], 10, 100)
+    assert head == 22
+    assert [len(p) for p in plan] == [2, 5, 0, 5]
+    assert sorted(q for p in plan for q in p) == list(range(10, 22))
+    plan, head = plan_admission([3, 3], 0, 4)  # queue shorter than capacity
+    assert head == 4 and sorted(plan[0] + plan[1]) == [0, 1, 2, 3]
+
+
+def _admission_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vosk.shard import AdmissionController
+    U, S = 40, 4
+    ctl = AdmissionController(dist, U)
+    free, active, got = S, {}, []
+    step = 0
+    while True:
+        for u in ctl.admit(free):
+            free -= 1
+            # rank 0 drains streams 3x faster than rank 1
+            active[u] = (1 + u % 3) * (1 if rank == 0 else 3)
+            got.append(u)
+        done = ctl.gather([len(active), int(ctl.exhausted)])
+        if all(a == 0 and x == 1 for a, x in done):
+            break
+        for u in list(active):
+            active[u] -= 1
+            if active[u] == 0:
+                del active[u]
+                free += 1
+        step += 1
+        assert step < 10000
+    out[rank] = got
+    dist.destroy_process_group()
+
+
+def test_admission_controller_gloo_world2():
+    """Every utterance is admitted exactly once, both ranks stop together,
+    and the faster rank takes more of the queue."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    mp.spawn(_admission_worker, args=(2, port, out), nprocs=2, join=True)
+    a, b = out[0], out[1]
+    assert sorted(a + b) == list(range(40))
+    assert len(a) > len(b)
