@@ -110,6 +110,8 @@ def main():
                          "resident; dynamic: a node-wide queue of variable-length utterances "
                          "admitted per epoch to the GPUs with the most free slots (one int32 "
                          "all-gather per epoch, vosk/shard.py)")
+    ap.add_argument("--no-single-stream", action="store_true",
+                    help="skip the single-stream accept_waveform latency measurement")
     ap.add_argument("--cpu-streams", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=300.0)
     args = ap.parse_args()
@@ -210,6 +212,13 @@ def main():
                      "achieved": round(nnet_tflops, 4), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": nnet_tflops / FP32_PEAK_TFLOPS}
 
+    # single-stream latency (BASELINE config 2): wall time of one
+    # vosk_recognizer_accept_waveform call on a 0.25 s (8000-byte) chunk
+    # through the public API, test_simple.py's feeding pattern, 30 s of audio
+    single = None
+    if rank == 0 and world == 1 and not args.no_single_stream:
+        single = single_stream_latency(model, base)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         workers = min(16, os.cpu_count() or 1)
@@ -253,6 +262,7 @@ def main():
                         "lattice_links_per_frame": round(tot.get("links", 0) / max(tot["frames"], 1), 1),
                         "stream_errors": errs},
             "cpu_baseline": cpu,
+            "single_stream": single,
         }
         if os.environ.get("VOSK_AMD_DEC_PROFILE"):
             out["decoder_phase_clocks_per_frame"] = {
@@ -263,6 +273,39 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def single_stream_latency(model, base, seconds=30.0, chunk_bytes=8000):
+    """One KaldiRecognizer (silence-weighted i-vectors, lattice results)
+    fed 8000-byte chunks; p50/p90/p99 of the accept_waveform wall time, the
+    stream's real-time factor, and a final result call's time."""
+    import vosk
+    x = stream_audio(base, 777, int(seconds * SR))
+    data = np.clip(x, -32768, 32767).astype("<i2").tobytes()
+    m = vosk.Model(model)
+    rec = vosk.KaldiRecognizer(m, SR)
+    rec.SetWords(True)
+    for i in range(0, 16000 * 2, chunk_bytes):  # warm up (first kernels, allocations)
+        rec.AcceptWaveform(data[i:i + chunk_bytes])
+    rec.FinalResult()
+    lat = []
+    t0 = time.perf_counter()
+    for i in range(0, len(data), chunk_bytes):
+        ts = time.perf_counter()
+        if rec.AcceptWaveform(data[i:i + chunk_bytes]):
+            rec.Result()
+        lat.append(time.perf_counter() - ts)
+    tf = time.perf_counter()
+    rec.FinalResult()
+    t1 = time.perf_counter()
+    lat = np.array(lat) * 1e3
+    return {"p50_accept_ms": round(float(np.percentile(lat, 50)), 3),
+            "p90_accept_ms": round(float(np.percentile(lat, 90)), 3),
+            "p99_accept_ms": round(float(np.percentile(lat, 99)), 3),
+            "final_result_ms": round((t1 - tf) * 1e3, 3),
+            "xrt": round(seconds / (t1 - t0), 2),
+            "chunk": "8000 B (0.25 s) per accept_waveform, test_simple.py pattern, 30 s stream; "
+                     "results (MBR over the GPU lattice) included when an endpoint fires"}
 
 
 def run_dynamic(args, model, dist, rank, world, local_rank):
