@@ -67,10 +67,23 @@ def test_real_model_transcripts(gold, test_wave):
     import vosk
     m = vosk.Model(os.environ["VOSK_TEST_MODEL"])
     rec = vosk.KaldiRecognizer(m, 16000)
-    texts = []
+    rec.SetWords(True)
+    rec.SetPartialWords(True)
+    texts, words = [], []
     data = test_wave.astype("<i2").tobytes()
     for i in range(44, len(data), 8000):
         if rec.AcceptWaveform(data[i:i + 8000]):
-            texts.append(json.loads(rec.Result())["text"])
-    texts.append(json.loads(rec.FinalResult())["text"])
+            r = json.loads(rec.Result())
+            texts.append(r["text"])
+            words += r.get("result", [])
+    r = json.loads(rec.FinalResult())
+    texts.append(r["text"])
+    words += r.get("result", [])
     assert " ".join(t for t in texts if t) == "one zero zero zero one nah no to i know zero one eight zero three"
+    # MBR confidences and aligned word times of the notebook (dither differs:
+    # the notebook ran with Kaldi's default dither, so tolerances, not bytes)
+    ref = [w for o in gold["runs"][0]["outputs"] if "result" in o for w in o["result"]]
+    assert [w["word"] for w in words] == [w["word"] for w in ref]
+    for w, g in zip(words, ref):
+        assert abs(w["conf"] - g["conf"]) < 0.1
+        assert abs(w["start"] - g["start"]) < 0.061 and abs(w["end"] - g["end"]) < 0.061
