@@ -223,33 +223,59 @@ static void iv_record(const orc_ivector_model* m, const float* norm, const float
   iv_lda(m, feats, t, t_ready, R->xr);
 }
 
-/* per-frame OnlineIvectorEstimationStats::AccStats with the frame weight
-   folded into the posteriors as Kaldi does (post * (posterior_scale * w),
-   in float; negative weights undo earlier contributions), then the
-   max-count prior rescaling */
+/* One statistics batch (OnlineIvectorFeature::UpdateStatsForFrames ->
+   OnlineIvectorEstimationStats::AccStats over a matrix of frames [K]): the
+   frame weight folded into the posteriors as Kaldi does (post *
+   (posterior_scale * w), in float; zero-weight frames dropped; negative
+   weights undo earlier contributions), zeroth and first order statistics
+   aggregated per Gaussian (gamma_g, X_g = sum post * x, in frame order),
+   then per Gaussian in ascending index: linear += SigmaInvM_g^T X_g,
+   quadratic += gamma_g U_g; the batch weight (sum of gamma_g, ascending g)
+   updates the frame count and Kaldi's max-count prior rescaling once. */
 typedef struct {
   double lin[128], cur[128];
   double* quad;
   double nfr;
+  double* gamma;   /* [G] scratch */
+  double* X;       /* [G][DL] scratch */
+  char* used;      /* [G] */
 } iv_stats;
 
-static void iv_accumulate(const orc_ivector_model* m, const double* SIM, const double* U,
-                          const iv_rec* R, float w, iv_stats* st) {
-  const int DL = m->lda_rows, S = m->ivec_dim, QS = S * (S + 1) / 2;
+static void iv_accumulate_batch(const orc_ivector_model* m, const double* SIM, const double* U,
+                                const iv_rec* const* recs, const float* ws, int n, iv_stats* st) {
+  const int DL = m->lda_rows, S = m->ivec_dim, QS = S * (S + 1) / 2, G = m->num_gauss;
+  memset(st->used, 0, G);
+  for (int i = 0; i < n; i++) {
+    const iv_rec* R = recs[i];
+    const float w = ws[i];
+    if (w == 0.0f) continue;
+    for (int k = 0; k < R->ns; k++) {
+      const double p = (double)(R->post[k] * (m->posterior_scale * w));
+      if (p == 0.0) continue;
+      const int g = R->sel[k];
+      if (!st->used[g]) {
+        st->used[g] = 1;
+        st->gamma[g] = 0.0;
+        for (int d = 0; d < DL; d++) st->X[(size_t)g * DL + d] = 0.0;
+      }
+      st->gamma[g] = st->gamma[g] + p;
+      for (int d = 0; d < DL; d++)
+        st->X[(size_t)g * DL + d] = st->X[(size_t)g * DL + d] + p * (double)R->xr[d];
+    }
+  }
   double tw = 0.0;
-  for (int k = 0; k < R->ns; k++) {
-    const float post = R->post[k] * (m->posterior_scale * w);
-    const double wd = (double)post;
-    if (wd == 0.0) continue;
-    const double* sm = SIM + (size_t)R->sel[k] * DL * S;
+  for (int g = 0; g < G; g++) {
+    if (!st->used[g]) continue;
+    const double* sm = SIM + (size_t)g * DL * S;
+    const double* x = st->X + (size_t)g * DL;
     for (int s2 = 0; s2 < S; s2++) {
       double a = 0.0;
-      for (int d = 0; d < DL; d++) a = fma(sm[(size_t)d * S + s2], (double)R->xr[d], a);
-      st->lin[s2] = st->lin[s2] + wd * a;
+      for (int d = 0; d < DL; d++) a = fma(sm[(size_t)d * S + s2], x[d], a);
+      st->lin[s2] = st->lin[s2] + a;
     }
-    const double* u = U + (size_t)R->sel[k] * QS;
-    for (int i = 0; i < QS; i++) st->quad[i] = st->quad[i] + wd * u[i];
-    tw = tw + wd;
+    const double* u = U + (size_t)g * QS;
+    for (int i = 0; i < QS; i++) st->quad[i] = st->quad[i] + st->gamma[g] * u[i];
+    tw = tw + st->gamma[g];
   }
   if (m->max_count > 0.0) {
     const double mc = m->max_count, nfr = st->nfr;
@@ -305,6 +331,12 @@ int orc_ivector_extract_w(const orc_ivector_model* m, const float* feats, int T,
   iv_stats st;
   memset(&st, 0, sizeof(st));
   st.quad = (double*)calloc(QS, sizeof(double));
+  st.gamma = (double*)calloc(G, sizeof(double));
+  st.X = (double*)calloc((size_t)G * DL, sizeof(double));
+  st.used = (char*)calloc(G, 1);
+  const int bcap = (T > 0 ? T : 1) + (ent_off ? ent_off[nreq] : 0) + 8;
+  const iv_rec** brec = (const iv_rec**)malloc(sizeof(iv_rec*) * (size_t)bcap);
+  float* bw = (float*)malloc(sizeof(float) * (size_t)bcap);
   st.lin[0] = m->prior_offset;
   for (int i = 0; i < S; i++) st.quad[(size_t)i * (i + 1) / 2 + i] = 1.0;
   st.cur[0] = m->prior_offset;
@@ -325,12 +357,25 @@ int orc_ivector_extract_w(const orc_ivector_model* m, const float* feats, int T,
     if (f >= done) {
       if (f >= T) { rc = -2; break; }
       for (int t = done; t <= f; t++) iv_record(m, norm, feats, t, t_ready[q], wubm, ll, &recs[t]);
-      if (!ent_off) {
-        for (int t = done; t <= f; t++) iv_accumulate(m, SIM, U, &recs[t], 1.0f, &st);
-      } else {
-        for (int i = ent_off[q]; i < ent_off[q + 1]; i++) {
-          if (ent_frame[i] < 0 || ent_frame[i] > f) { rc = -3; break; }
-          iv_accumulate(m, SIM, U, &recs[ent_frame[i]], ent_w[i], &st);
+      if (!ent_off) {  /* one batch: the new frames with weight 1 */
+        for (int t = done; t <= f; t++) {
+          brec[t - done] = &recs[t];
+          bw[t - done] = 1.0f;
+        }
+        iv_accumulate_batch(m, SIM, U, brec, bw, f + 1 - done, &st);
+      } else {  /* batches as popped: entries with frame <= done, then one per frame */
+        int i = ent_off[q];
+        while (i < ent_off[q + 1]) {
+          const int key = ent_frame[i] > done ? ent_frame[i] : done;
+          int nb = 0;
+          while (i < ent_off[q + 1] && (ent_frame[i] > done ? ent_frame[i] : done) == key) {
+            if (ent_frame[i] < 0 || ent_frame[i] > f || nb >= bcap) { rc = -3; break; }
+            brec[nb] = &recs[ent_frame[i]];
+            bw[nb++] = ent_w[i];
+            i++;
+          }
+          if (rc) break;
+          iv_accumulate_batch(m, SIM, U, brec, bw, nb, &st);
         }
         if (rc) break;
       }
@@ -346,6 +391,7 @@ int orc_ivector_extract_w(const orc_ivector_model* m, const float* feats, int T,
     out[(size_t)q * S] = out[(size_t)q * S] - (float)m->prior_offset;
   }
   free(SIM); free(U); free(norm); free(st.quad); free(ll); free(wubm); free(recs);
+  free(st.gamma); free(st.X); free(st.used); free(brec); free(bw);
   return rc;
 }
 

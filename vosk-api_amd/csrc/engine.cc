@@ -376,7 +376,6 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     iv_.xraw = xraw;
     iv_.snap = (double*)DevAlloc(sizeof(double) * (size_t)S * jobs_per_slot_ * (QS + Si));
     iv_.snap_nfr = (double*)DevAlloc(sizeof(double) * (size_t)S * jobs_per_slot_);
-    iv_.chv = (double*)DevAlloc(sizeof(double) * all_rows);
     iv_.ring = (IvFrame*)DevAlloc(sizeof(IvFrame) * (size_t)S * kIvRing);
     iv_.ring_x = (float*)DevAlloc(sizeof(float) * (size_t)S * kIvRing * DL);
     iv_.ent_row0 = max_iv_rows_;
@@ -637,7 +636,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
                  Align256(sizeof(IvStreamJob) * S) + Align256(sizeof(IvReq) * max_jobs_) +
                  2 * Align256(sizeof(CmvnJob) * S) +
                  2 * Align256(sizeof(IvFrameBlock) * ((size_t)max_iv_frames_ / kIvFrameBlock + 2 * S)) +
-                 Align256(sizeof(IvEntry) * (size_t)max_iv_ents_) + 1024;
+                 Align256(sizeof(IvEntry) * (size_t)max_iv_ents_) +
+                 Align256(sizeof(IvBatch) * ((size_t)max_jobs_ + max_iv_ents_)) + 1024;
   // three buffers: the pipelined nnet and decoder passes keep their jobs
   // while the next step stages
   HIPCHECK(hipHostMalloc((void**)&h_stage_, 3 * stage_bytes_, hipHostMallocDefault));
@@ -817,6 +817,7 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
   st_ivcmvn_.clear();
   st_iv_frames_ = 0;
   st_iv_ents_.clear();
+  st_iv_batches_.clear();
   const int fpc = plan_.fpc, opc = plan_.opc, fss = plan_.fss, R = plan_.right_context;
   int stats_rows = 0;
   bool any = false;
@@ -941,23 +942,43 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
             st_iv_frames_ += kIvFrameBlock;
           }
           r.row_to = st_iv_frames_;
-          if (h.iv_weighted) {
+          r.batch0 = (int)st_iv_batches_.size();
+          if (!h.iv_weighted) {
+            // UpdateStatsUntilFrame: the new frames form one batch
+            st_iv_batches_.push_back(IvBatch{r.row_from, r.row_to});
+          } else {
             // OnlineIvectorFeature::UpdateStatsUntilFrameWeighted: the queued
-            // delta weights of frames <= f, popped in (frame, weight) order
+            // delta weights of frames <= f, popped in (frame, weight) order;
+            // one UpdateStatsForFrames batch at the first new frame (every
+            // entry of a frame <= it), then one per later frame
             auto& q = h.iv_pending;
             std::stable_sort(q.begin(), q.end());
             size_t n = 0;
             while (n < q.size() && q[n].first <= f) n++;
+            const int done = h.iv_stats_done;
             r.row_from = max_iv_rows_ + (int)st_iv_ents_.size();
+            int key = -1;
             for (size_t i = 0; i < n; i++) {
               const int t = q[i].first;
               if (t <= f - kIvRing) VAMD_ERR("silence weight for frame " << t << " left the history ring");
+              const int row = max_iv_rows_ + (int)st_iv_ents_.size();
+              const int k = std::max(t, done);
+              if (k != key) {
+                st_iv_batches_.push_back(IvBatch{row, row});
+                key = k;
+              }
+              st_iv_batches_.back().row_to = row + 1;
               st_iv_ents_.push_back(IvEntry{s * kIvRing + t % kIvRing, q[i].second});
             }
             q.erase(q.begin(), q.begin() + n);
             r.row_to = max_iv_rows_ + (int)st_iv_ents_.size();
             if ((int)st_iv_ents_.size() > max_iv_ents_) VAMD_ERR("silence-weighted i-vector entries overflow");
           }
+          r.nbatch = (int)st_iv_batches_.size() - r.batch0;
+          for (int b = r.batch0; b < (int)st_iv_batches_.size(); b++)
+            if (st_iv_batches_[b].row_to - st_iv_batches_[b].row_from > kIvBatchRows)
+              VAMD_ERR("i-vector statistics batch of " << st_iv_batches_[b].row_to - st_iv_batches_[b].row_from
+                                                        << " frames exceeds " << kIvBatchRows);
           h.iv_stats_done = f + 1;
           h.iv_norm_to = std::max(h.iv_norm_to, std::min(f + iv_.m.right, T - 1) + 1);
         }
@@ -1107,6 +1128,7 @@ void Engine::RunStep(bool allow_pipeline) {
   size_t o_ncm = put(st_ncmvn_.data(), sizeof(CmvnJob) * st_ncmvn_.size());
   size_t o_icm = put(st_ivcmvn_.data(), sizeof(CmvnJob) * st_ivcmvn_.size());
   size_t o_ive = put(st_iv_ents_.data(), sizeof(IvEntry) * st_iv_ents_.size());
+  size_t o_ivbt = put(st_iv_batches_.data(), sizeof(IvBatch) * st_iv_batches_.size());
   cur.dec.jobs = st_dec_;
   cur.dec.o_ej = put(st_dec_.data(), sizeof(DecJob) * st_dec_.size());
   cur.dec.buf = buf;
@@ -1143,6 +1165,7 @@ void Engine::RunStep(bool allow_pipeline) {
     ia.ivec = d_ivec_buf_[par];
     ia.ents = (const IvEntry*)(dsg + o_ive);
     ia.nents = (int)st_iv_ents_.size();
+    ia.batches = (const IvBatch*)(dsg + o_ivbt);
     const int rows = (int)st_iv_blocks_.size() * kIvFrameBlock;
     if (rows > max_iv_rows_) VAMD_ERR("i-vector frame records overflow");
     LaunchCmvn(ivcmvn_, (const CmvnJob*)(dsg + o_icm), (int)st_ivcmvn_.size(), fs);
@@ -1441,6 +1464,8 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     st_iv_reqs_.clear();
     st_iv_blocks_.clear();
     st_iv_devjobs_.clear();
+    st_iv_batches_.clear();
+    st_iv_ents_.clear();
     st_ncmvn_.clear();
     st_ivcmvn_.clear();
     st_iv_frames_ = 0;

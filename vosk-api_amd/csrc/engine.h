@@ -303,6 +303,7 @@ class Engine {
   std::vector<int> iv_op_bk_;
   int max_iv_rows_ = 0, max_iv_ents_ = 0;
   std::vector<IvEntry> st_iv_ents_;  // silence-weighted entries of this step
+  std::vector<IvBatch> st_iv_batches_;  // statistics batches of this step's requests
   int max_jobs_ = 0, max_dec_frames_ = 0;
 
   void* DevAlloc(size_t bytes);

@@ -163,11 +163,18 @@ struct IvStreamJob {  // one stream's i-vector work in this step
   int pad0, pad1, pad2;
 };
 struct IvReq {  // i-vector at `frame` -> rows [job_lo, job_hi) of the per-job buffer,
-                // after accumulating frame records [row_from, row_to); upd = the
+                // after accumulating frame records [row_from, row_to) in the
+                // statistics batches [batch0, batch0 + nbatch); upd = the
                 // statistics advance to `frame` here (else the current i-vector
                 // is reused, OnlineIvectorFeature::GetFrame with no new frames)
-  int frame, job_lo, job_hi, row_from, row_to, upd, pad1, pad2;
+  int frame, job_lo, job_hi, row_from, row_to, upd, batch0, nbatch;
 };
+// one UpdateStatsForFrames call: frame records [row_from, row_to) aggregated
+// per Gaussian (OnlineIvectorEstimationStats::AccStats over a matrix)
+struct IvBatch {
+  int row_from, row_to;
+};
+constexpr int kIvBatchRows = 512;  // frame records per statistics batch (host-checked)
 struct IvFrameBlock {  // ivector_top_kernel rows: frames t0.. (nf) of a job's stream;
                        // ring >= 0: also keep the records in the stream's history
                        // ring (silence-weighted streams re-weight past frames)
@@ -199,7 +206,7 @@ struct IvArgs {
   float* xraw;        // [GEMM rows + entry rows][lda_dim] LDA projection of the raw features
   double* snap;       // [max requests per step][S(S+1)/2 + S] terms at each request
   double* snap_nfr;   // [max requests per step] frame count at each request
-  double* chv;        // [max frames per step] prior-scale change at each frame
+
   float* ivec;        // [jobs][S] per chunk job, prior offset removed
   const IvStreamJob* jobs;
   const IvReq* reqs;
@@ -208,6 +215,7 @@ struct IvArgs {
   float* ring_x;        // [slots][kIvRing][lda_dim]
   const IvEntry* ents;  // this step's weighted entries -> rows ent_row0 + i
   int ent_row0, nents;
+  const IvBatch* batches;
 };
 
 struct DecJob {

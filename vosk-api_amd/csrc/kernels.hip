@@ -908,70 +908,47 @@ __device__ __forceinline__ int iv_tri_row(int e) {  // packed lower-triangle row
 
 constexpr int kIvCgLds = 48;  // S up to this: the CG matrix lives in LDS
 
-// Kaldi's per-frame statistics update.  Eight workgroups per stream, one per
-// XCD (blockIdx % 8 share an XCD): part p owns a contiguous eighth of the
-// packed quadratic term and of the linear-term columns, so each
-// XCD's L2 holds only its slice of U and SigmaInvM.  Each entry replays the
-// stream's frames in order (exactly the oracle's per-entry chains); a
-// snapshot of the terms is taken at every request for the CG kernel.
-// Posterior-weighted frame count and Kaldi's max-count prior rescaling per
-// frame: a short sequential scan per stream (one lane each), so the
-// accumulation kernel needs no divisions.  ch[row] = change of the prior
-// scale at that frame (0 while the count is below max-count).
-__global__ __launch_bounds__(64) void ivector_nfr_kernel(IvArgs a, int njobs) {
-  const int jb = blockIdx.x * 64 + threadIdx.x;
-  if (jb >= njobs) return;
-  const IvStreamJob J = a.jobs[jb];
-  const double mc = a.m.max_count;
-  IvState* st = a.state + J.slot;
-  double nfr = J.reset ? 0.0 : st->nfr;
-  for (int q = 0; q < J.nreq; q++) {
-    const IvReq R = a.reqs[J.req0 + q];
-    for (int r = R.row_from; r < R.row_to; r++) {
-      const IvFrame F = a.frames[r];
-      double tw = 0.0;
-      for (int k = 0; k < F.nsel; k++) {
-        const double w = (double)F.post[k];
-        if (w != 0.0) tw = tw + w;
-      }
-      double ch = 0.0;
-      const double newn = nfr + tw;
-      if (mc > 0.0 && (nfr > mc || newn > mc)) {  // else both scales are exactly 1
-        const double oldp = (nfr > mc ? nfr : mc) / mc;
-        const double newp = (newn > mc ? newn : mc) / mc;
-        ch = newp - oldp;
-      }
-      a.chv[r] = ch;
-      nfr = newn;
-    }
-    a.snap_nfr[J.req0 + q] = nfr;
-  }
-  st->nfr = nfr;
-}
-
-constexpr int kIvAccChunk = 32;  // frame records staged in LDS at a time
-constexpr int kIvAccFrames = 8;  // frames per projection sub-block
+// i-vector statistics, batched as Kaldi's OnlineIvectorFeature::
+// UpdateStatsForFrames -> OnlineIvectorEstimationStats::AccStats over a
+// matrix of frames: per batch, zeroth / first order statistics per Gaussian
+// (gamma_g, X_g = sum post * x in frame order), then per Gaussian in
+// ascending index linear += SigmaInvM_g^T X_g and quadratic += gamma_g U_g,
+// then the frame count and the max-count prior rescaling once per batch
+// (oracle.c iv_accumulate_batch restates it).  NP workgroups per stream: part
+// p owns a contiguous 1/NP of the packed quadratic term and of the linear
+// columns (blocks b and b + 8 share an XCD, so each XCD's L2 holds only its
+// slice of U and SigmaInvM); the per-Gaussian aggregation is recomputed by
+// every part (identical).  A snapshot of the terms is taken at every request
+// for the CG kernel.
+constexpr int kIvGroup = 8;  // Gaussians whose X_g are held in LDS at a time
 struct IvAccShared {
-  double w[kIvAccChunk][5];
-  double ch[kIvAccChunk];
-  int sel[kIvAccChunk][5];
-  int ns[kIvAccChunk];
-  float xr[kIvAccChunk][kIvMaxD];
-  double proj[kIvAccFrames][5][(kIvMaxS + 3) / 4];
+  unsigned short sel[kIvBatchRows][5];
+  float post[kIvBatchRows][5];
+  unsigned char ns[kIvBatchRows];
+  int cnt[kIvMaxG], off[kIvMaxG], run[kIvMaxG];
+  unsigned short dlist[kIvMaxG];
+  unsigned short occ[kIvBatchRows * 5];  // row * 5 + k, grouped by Gaussian, rows ascending
+  int ndist;
+  int wsum[4];
+  double X[kIvGroup][kIvMaxD];
+  double gam[kIvGroup];
+  double proj[kIvGroup][(kIvMaxS + 3) / 4];
+  double tw;
 };
 
 template <int NQP, int NP>  // NP parts; packed quad entries per thread: ceil(ceil(QS / NP) / 256)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void ivector_acc_kernel(IvArgs a) {
   __shared__ IvAccShared sh;
   const int part = blockIdx.x % NP, jb = blockIdx.x / NP, tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
   const IvStreamJob J = a.jobs[jb];
   const IvectorDev& m = a.m;
-  const int S = m.ivec_dim, DL = m.lda_dim, QS = S * (S + 1) / 2, NE = QS + S;
+  const int S = m.ivec_dim, DL = m.lda_dim, QS = S * (S + 1) / 2, NE = QS + S, G = m.num_gauss;
   const int qchunk = (QS + NP - 1) / NP, q0 = part * qchunk, q1 = min(QS, q0 + qchunk);
   const int cw = (S + NP - 1) / NP, c0 = min(S, part * cw), ncol = min(S, c0 + cw) - c0;  // columns [c0, c0+ncol)
   IvState* st = a.state + J.slot;
   double* quad = a.quad + (size_t)J.slot * QS;
-  const double po = m.prior_offset;
+  const double po = m.prior_offset, mc = m.max_count;
   double qe[NQP];
   bool qd[NQP];
 #pragma unroll
@@ -983,95 +960,161 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
   const int col = c0 + tid;  // lin column owned by threads tid < ncol
   double lin = 0.0;
   if (tid < ncol) lin = J.reset ? (col == 0 ? po : 0.0) : st->lin[col];
+  double nfr = J.reset ? 0.0 : st->nfr;
   for (int q = 0; q < J.nreq; q++) {
     const IvReq R = a.reqs[J.req0 + q];
-    for (int c0r = R.row_from; c0r < R.row_to; c0r += kIvAccChunk) {
-      const int nc = min(kIvAccChunk, R.row_to - c0r);
-      // stage the chunk's records (one round of independent loads)
-      __syncthreads();
-      for (int i = tid; i < nc * 5; i += 256) {
-        const int f = i / 5, k = i % 5;
-        const IvFrame& F = a.frames[c0r + f];
-        const int ns = F.nsel;
-        if (k == 0) {
-          sh.ns[f] = ns;
-          sh.ch[f] = a.chv[c0r + f];
+    for (int bi = 0; bi < R.nbatch; bi++) {
+      const IvBatch B = a.batches[R.batch0 + bi];
+      const int n = B.row_to - B.row_from;
+      __syncthreads();  // previous batch done with the shared arrays
+      for (int i = tid; i < n; i += 256) {
+        const IvFrame F = a.frames[B.row_from + i];
+        sh.ns[i] = (unsigned char)F.nsel;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+          sh.sel[i][k] = (unsigned short)(k < F.nsel ? F.sel[k] : 0);
+          sh.post[i][k] = k < F.nsel ? F.post[k] : 0.0f;
         }
-        sh.w[f][k] = k < ns ? (double)F.post[k] : 0.0;
-        sh.sel[f][k] = k < ns ? F.sel[k] : 0;
       }
-      for (int i = tid; i < nc * DL; i += 256)
-        sh.xr[i / DL][i % DL] = a.xraw[(size_t)(c0r + i / DL) * DL + i % DL];
+      for (int g = tid; g < G; g += 256) {
+        sh.cnt[g] = 0;
+        sh.run[g] = 0;
+      }
       __syncthreads();
-      for (int b0 = 0; b0 < nc; b0 += kIvAccFrames) {
-        const int nb = min(kIvAccFrames, nc - b0);
-        if (b0 > 0) __syncthreads();  // proj of the previous sub-block consumed
-        // SigmaInvM_g^T x_raw for this part's columns, every (frame, Gaussian)
-        for (int i = tid; i < nb * 5 * ncol; i += 256) {
-          const int c = i % ncol, k = (i / ncol) % 5, f = b0 + i / (5 * ncol);
-          if (k < sh.ns[f] && sh.w[f][k] != 0.0) {
-            const double* sm = m.sigma_inv_m + (size_t)sh.sel[f][k] * DL * S + c0 + c;
-            const float* xr = sh.xr[f];
-            double acc = 0.0;
-            for (int d0 = 0; d0 < DL; d0 += 20) {  // batches of 20 loads in flight
-              double sv[20];
-#pragma unroll
-              for (int u = 0; u < 20; u++) sv[u] = d0 + u < DL ? sm[(size_t)(d0 + u) * S] : 0.0;
-#pragma unroll
-              for (int u = 0; u < 20; u++) {
-                if (d0 + u >= DL) break;
-                acc = fma(sv[u], (double)xr[d0 + u], acc);
-              }
-            }
-            sh.proj[f - b0][k][c] = acc;
+      // per-Gaussian occurrence counts (zero posteriors contribute nothing)
+      for (int i = tid; i < n * 5; i += 256) {
+        const int r = i / 5, k = i - r * 5;
+        if (k < sh.ns[r] && sh.post[r][k] != 0.0f) atomicAdd(&sh.cnt[sh.sel[r][k]], 1);
+      }
+      __syncthreads();
+      // exclusive scan of the counts (two per thread, G <= 512) and the
+      // ascending list of Gaussians present
+      {
+        const int g0 = 2 * tid;
+        const int c_a = g0 < G ? sh.cnt[g0] : 0, c_b = g0 + 1 < G ? sh.cnt[g0 + 1] : 0;
+        int v = c_a + c_b, d_v = (c_a > 0) + (c_b > 0);
+        int incl = v, dincl = d_v;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int u = __shfl_up(incl, o, 64), du = __shfl_up(dincl, o, 64);
+          if (lane >= o) {
+            incl += u;
+            dincl += du;
           }
         }
-        // quadratic entries: U loads of 4 frames at a time, then the chains
-        for (int f0 = 0; f0 < nb; f0 += 4) {
-          double uv[4][5][NQP];
-#pragma unroll
-          for (int f2 = 0; f2 < 4; f2++)
+        if (lane == 63) sh.wsum[wv] = (incl & 0xffff) | (dincl << 16);
+        __syncthreads();
+        int base = 0, dbase = 0;
+        for (int w = 0; w < wv; w++) {
+          base += sh.wsum[w] & 0xffff;
+          dbase += sh.wsum[w] >> 16;
+        }
+        const int ex = base + incl - v, dex = dbase + dincl - d_v;
+        if (g0 < G) {
+          sh.off[g0] = ex;
+          if (c_a > 0) sh.dlist[dex] = (unsigned short)g0;
+        }
+        if (g0 + 1 < G) {
+          sh.off[g0 + 1] = ex + c_a;
+          if (c_b > 0) sh.dlist[dex + (c_a > 0)] = (unsigned short)(g0 + 1);
+        }
+        if (tid == 255) sh.ndist = dbase + dincl;
+      }
+      __syncthreads();
+      // occurrence lists in row order: one thread per Gaussian present scans
+      // the batch's (row, k) pairs in order (uniform LDS reads broadcast)
+      {
+        const int nd0 = sh.ndist;
+        for (int di = tid; di < nd0 + 255 - (nd0 + 255) % 256; di += 256) {
+          const int g = di < nd0 ? sh.dlist[di] : -1;
+          int c = 0;
+          const int o0 = g >= 0 ? sh.off[g] : 0;
+          for (int r = 0; r < n; r++) {
+            const int nsr = sh.ns[r];
 #pragma unroll
             for (int k = 0; k < 5; k++)
-#pragma unroll
-              for (int j = 0; j < NQP; j++) {
-                const int f = b0 + f0 + f2;
-                uv[f2][k][j] = (f0 + f2 < nb && k < sh.ns[f] && q0 + tid + 256 * j < q1)
-                                   ? m.U[(size_t)sh.sel[f][k] * QS + q0 + tid + 256 * j] : 0.0;
-              }
-#pragma unroll
-          for (int f2 = 0; f2 < 4; f2++) {
-            const int f = b0 + f0 + f2;
-            if (f0 + f2 >= nb) break;
-#pragma unroll
-            for (int k = 0; k < 5; k++) {
-              if (k >= sh.ns[f]) break;
-              const double w = sh.w[f][k];
-              if (w == 0.0) continue;
-#pragma unroll
-              for (int j = 0; j < NQP; j++)
-                if (q0 + tid + 256 * j < q1) qe[j] = qe[j] + w * uv[f2][k][j];
-            }
-            const double ch = sh.ch[f];
-            if (ch != 0.0) {
-#pragma unroll
-              for (int j = 0; j < NQP; j++)
-                if (qd[j] && q0 + tid + 256 * j < q1) qe[j] += ch;
-            }
-          }
-        }
-        __syncthreads();
-        if (tid < ncol) {
-          for (int f = b0; f < b0 + nb; f++) {
-            for (int k = 0; k < sh.ns[f]; k++) {
-              const double w = sh.w[f][k];
-              if (w == 0.0) continue;
-              lin = lin + w * sh.proj[f - b0][k][tid];
-            }
-            if (sh.ch[f] != 0.0 && col == 0) lin = lin + po * sh.ch[f];
+              if (k < nsr && sh.sel[r][k] == g && sh.post[r][k] != 0.0f) sh.occ[o0 + c++] = (unsigned short)(r * 5 + k);
           }
         }
       }
+      if (tid == 0) sh.tw = 0.0;
+      __syncthreads();
+      const int nd = sh.ndist;
+      for (int gb = 0; gb < nd; gb += kIvGroup) {
+        const int ng = min(kIvGroup, nd - gb);
+        // X_g and gamma_g of the group, each summed over its rows in order
+        for (int i = tid; i < ng * (DL + 1); i += 256) {
+          const int gi = i / (DL + 1), d = i - gi * (DL + 1);
+          const int g = sh.dlist[gb + gi], o0 = sh.off[g], oc = sh.cnt[g];
+          double acc = 0.0;
+          for (int ob = 0; ob < oc; ob += 8) {  // batches of 8 row loads in flight
+            float xv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              xv[u] = 1.0f;
+              if (ob + u < oc && d < DL) {
+                const int r = sh.occ[o0 + ob + u] / 5;
+                xv[u] = a.xraw[(size_t)(B.row_from + r) * DL + d];
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              if (ob + u >= oc) break;
+              const int rk = sh.occ[o0 + ob + u], r = rk / 5, k = rk - r * 5;
+              const double p = (double)sh.post[r][k];
+              acc = d < DL ? acc + p * (double)xv[u] : acc + p;
+            }
+          }
+          if (d < DL) sh.X[gi][d] = acc;
+          else sh.gam[gi] = acc;
+        }
+        __syncthreads();
+        for (int gi = 0; gi < ng; gi++) {
+          const int g = sh.dlist[gb + gi];
+          const double gm = sh.gam[gi];
+          const double* U = m.U + (size_t)g * QS;
+#pragma unroll
+          for (int j = 0; j < NQP; j++)
+            if (q0 + tid + 256 * j < q1) qe[j] = qe[j] + gm * U[q0 + tid + 256 * j];
+        }
+        // SigmaInvM_g^T X_g for every (Gaussian, column) of the group in
+        // parallel, then each column adds them in Gaussian order
+        for (int i = tid; i < ng * ncol; i += 256) {
+          const int gi = i / ncol, c = i - gi * ncol;
+          const double* sm = m.sigma_inv_m + (size_t)sh.dlist[gb + gi] * DL * S + c0 + c;
+          double acc = 0.0;
+          for (int d0 = 0; d0 < DL; d0 += 20) {  // batches of 20 loads in flight
+            double sv[20];
+#pragma unroll
+            for (int u = 0; u < 20; u++) sv[u] = d0 + u < DL ? sm[(size_t)(d0 + u) * S] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 20; u++) {
+              if (d0 + u >= DL) break;
+              acc = fma(sv[u], sh.X[gi][d0 + u], acc);
+            }
+          }
+          sh.proj[gi][c] = acc;
+        }
+        __syncthreads();
+        if (tid < ncol)
+          for (int gi = 0; gi < ng; gi++) lin = lin + sh.proj[gi][tid];
+        if (tid == 0)
+          for (int gi = 0; gi < ng; gi++) sh.tw = sh.tw + sh.gam[gi];
+        __syncthreads();  // the group's X / gamma / projections are consumed
+      }
+      // frame count and Kaldi's max-count prior rescaling, once per batch
+      const double tw = sh.tw, newn = nfr + tw;
+      if (mc > 0.0 && (nfr > mc || newn > mc)) {  // else both scales are exactly 1
+        const double oldp = (nfr > mc ? nfr : mc) / mc;
+        const double newp = (newn > mc ? newn : mc) / mc;
+        const double ch = newp - oldp;
+        if (ch != 0.0) {
+#pragma unroll
+          for (int j = 0; j < NQP; j++)
+            if (qd[j] && q0 + tid + 256 * j < q1) qe[j] += ch;
+          if (tid < ncol && col == 0) lin = lin + po * ch;
+        }
+      }
+      nfr = newn;
     }
     if (R.upd) {
       double* sn = a.snap + (size_t)(J.req0 + q) * NE;
@@ -1080,11 +1123,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void i
         if (q0 + tid + 256 * j < q1) sn[q0 + tid + 256 * j] = qe[j];
       if (tid < ncol) sn[QS + col] = lin;
     }
+    if (part == 0 && tid == 0) a.snap_nfr[J.req0 + q] = nfr;
   }
 #pragma unroll
   for (int j = 0; j < NQP; j++)
     if (q0 + tid + 256 * j < q1) quad[q0 + tid + 256 * j] = qe[j];
   if (tid < ncol) st->lin[col] = lin;
+  if (part == 0 && tid == 0) st->nfr = nfr;
 }
 
 __device__ double iv_dot(const double* x, const double* y, int n) {
@@ -1199,7 +1244,6 @@ void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, h
   if (njobs <= 0) return;
   if (rows > 0) hipLaunchKernelGGL(ivector_top_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, a, ll, rows);
   if (a.nents > 0) hipLaunchKernelGGL(ivector_entry_kernel, dim3((a.nents + 3) / 4), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(ivector_nfr_kernel, dim3((njobs + 63) / 64), dim3(64), 0, s, a, njobs);
   // parts: blocks b and b + 8 share an XCD, so part = b % NP keeps each XCD's
   // L2 on 1/NP of U and SigmaInvM
   static const int np = getenv("VOSK_AMD_IV_PARTS") ? atoi(getenv("VOSK_AMD_IV_PARTS")) : 4;
