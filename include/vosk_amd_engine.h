@@ -36,6 +36,19 @@ int vamd_silence_weighting_run(int ncalls, const int *num_frames_ready, const in
                                const unsigned char *tid_is_silence, int num_tids, float silence_weight,
                                int fss, int *out_off, int *out_frame, float *out_w, int cap);
 
+/* host-only: the decode graph of a model directory as the engine uploads it
+ * (graph/HCLG.fst as stored, or graph/HCLr.fst o graph/Gr.fst expanded by
+ * graph_compose.h), or with grammar != NULL the grammar recognizer's runtime
+ * graph (HCLr o the phrase-list bigram).  NULL on error.  vamd_graph_dims
+ * returns the state count (start state and arc count through the pointers);
+ * vamd_graph_copy fills final costs [S], arc offsets [S+1] (emitting arcs
+ * first per state) and the arcs [A]. */
+void *vamd_graph_new(const char *model_dir, const char *grammar);
+int vamd_graph_dims(void *graph, int *start, long long *num_arcs);
+int vamd_graph_copy(void *graph, float *final_cost, long long *arc_begin, int *ilabel, int *olabel,
+                    float *weight, int *nextstate);
+void vamd_graph_free(void *graph);
+
 /* host-only: the result pipeline over a state-level lattice (the arrays of
  * vamd_stream_lattice; arc_ilabel / arc_olabel index the graph's arcs):
  * lattice-beam pruning, word determinization, graph scaling, word alignment

@@ -21,13 +21,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
 
 
-def _make(name, **kw):
+def _make(name, post=None, **kw):
     import make_synth_model as msm
     path = os.path.join(MODEL_CACHE, f"{name}_{SYNTH_VERSION}")
     if not os.path.exists(os.path.join(path, "README")):
         tmp = path + f".tmp{os.getpid()}"
         shutil.rmtree(tmp, ignore_errors=True)
         msm.make_model(tmp, **kw)
+        if post is not None:
+            post(tmp)
         shutil.rmtree(path, ignore_errors=True)
         os.rename(tmp, path)
     return path
@@ -69,6 +71,17 @@ def synth_model_wide(synth_model):
         shutil.rmtree(path, ignore_errors=True)
         os.rename(tmp, path)
     return path
+
+
+@pytest.fixture(scope="session")
+def synth_lookahead():
+    """Lookahead model (graph/HCLr.fst + graph/Gr.fst + disambig_tid.int, no
+    HCLG), endpointing disabled (one segment per stream)."""
+    def noep(d):
+        with open(os.path.join(d, "conf", "model.conf"), "a") as f:
+            for r in range(1, 6):
+                f.write(f"--endpoint.rule{r}.min-utterance-length=1e9\n")
+    return _make("synth_la", post=noep, seed=11, vocab=300, num_pdfs=2000, graph="lookahead")
 
 
 @pytest.fixture(scope="session")

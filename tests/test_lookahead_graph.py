@@ -1,0 +1,186 @@
+"""Lookahead graphs and runtime grammars on the host (CPU).
+
+* the ngram (LOUDS) reader against hand-built n-gram models (the explicit
+  destinations are the longest existing history, the backoff arc goes to
+  the history without its oldest word);
+* the static expansion of HCLr o Gr in libvosk.so (graph_compose.cc, through
+  the host-only ``vamd_graph_*`` ABI) against the unpruned restatement in
+  tests/oracle_graph.py, array for array, for the model graph and for
+  grammar graphs;
+* LanguageModelEstimator known answers (src/language_model.cc) and the
+  grammar JSON handling (src/recognizer.cc:60-92).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import kaldi_formats as kf
+import oracle_graph as OG
+
+LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "vosk-api_amd", "vosk", "libvosk.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    lib = C.CDLL(LIB)
+    lib.vamd_graph_new.restype = C.c_void_p
+    lib.vamd_graph_new.argtypes = [C.c_char_p, C.c_char_p]
+    lib.vamd_graph_dims.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]
+    lib.vamd_graph_copy.argtypes = [C.c_void_p] + [C.c_void_p] * 6
+    lib.vamd_graph_free.argtypes = [C.c_void_p]
+    lib.vosk_set_log_level(-2)
+    return lib
+
+
+def _cgraph(lib, model, grammar=None):
+    h = lib.vamd_graph_new(model.encode(), grammar.encode() if grammar is not None else None)
+    if not h:
+        return None
+    st, na = C.c_int(), C.c_longlong()
+    S = lib.vamd_graph_dims(h, C.byref(st), C.byref(na))
+    A = na.value
+    out = kf.Fst(st.value, np.zeros(S, np.float32), np.zeros(S + 1, np.int64), np.zeros(A, np.int32),
+                 np.zeros(A, np.int32), np.zeros(A, np.float32), np.zeros(A, np.int32))
+    lib.vamd_graph_copy(h, out.final.ctypes.data, out.row.ctypes.data, out.ilabel.ctypes.data,
+                        out.olabel.ctypes.data, out.weight.ctypes.data, out.nextstate.ctypes.data)
+    lib.vamd_graph_free(h)
+    return out
+
+
+def _assert_same_fst(a, b):
+    assert a.start == b.start
+    np.testing.assert_array_equal(a.row, b.row)
+    np.testing.assert_array_equal(a.ilabel, b.ilabel)
+    np.testing.assert_array_equal(a.olabel, b.olabel)
+    np.testing.assert_array_equal(a.nextstate, b.nextstate)
+    np.testing.assert_array_equal(a.weight.view(np.int32), b.weight.view(np.int32))
+    np.testing.assert_array_equal(a.final.view(np.int32), b.final.view(np.int32))
+
+
+def _toy_lm():
+    # histories most recent word first; () root, (0,) sentence start
+    return {
+        (): {"fut": {1: 2.0, 2: 2.5, 3: 3.0, 4: 3.5}, "final": 1.5},
+        (0,): {"fut": {1: 0.5, 3: 1.25}, "backoff": 0.75, "final": None},
+        (1,): {"fut": {2: 0.25, 4: 1.0}, "backoff": 0.5, "final": 2.0},
+        (2,): {"fut": {3: 0.125}, "backoff": 0.625, "final": None},
+        (1, 0): {"fut": {2: 0.0625}, "backoff": 0.375, "final": None},
+        (2, 1): {"fut": {1: 0.3, 4: 0.2}, "backoff": 0.1, "final": 0.9},
+    }
+
+
+def test_ngram_fst_semantics(tmp_path):
+    lm = _toy_lm()
+    path = str(tmp_path / "Gr.fst")
+    kf.write_ngram_fst(path, lm)
+    f = kf.read_fst(path)
+    # level order of the reversed-history trie: (), then children by label
+    order = [(), (0,), (1,), (2,), (1, 0), (2, 1)]
+    assert f.num_states == len(order) and f.start == 1
+    for s, h in enumerate(order):
+        arcs = [(int(f.ilabel[a]), int(f.olabel[a]), float(f.weight[a]), order[int(f.nextstate[a])])
+                for a in range(int(f.row[s]), int(f.row[s + 1]))]
+        want = []
+        if h:
+            want.append((0, 0, float(np.float32(lm[h]["backoff"])), h[:-1]))
+        for w, c in sorted(lm[h]["fut"].items()):
+            nh = (w,) + h
+            while nh not in lm:  # longest existing history
+                nh = nh[:-1]
+            want.append((w, w, float(np.float32(c)), nh))
+        assert arcs == want, h
+        fc = lm[h]["final"]
+        assert (f.final[s] == np.float32(fc)) if fc is not None else np.isinf(f.final[s])
+
+
+def test_lookahead_file_roundtrip(tmp_path):
+    f = kf.Fst(0, np.array([0.0, np.inf], np.float32), np.array([0, 2, 3], np.int64),
+               np.array([5, 0, 7], np.int32), np.array([0, 3, 4], np.int32),
+               np.array([0.5, 1.0, 0.25], np.float32), np.array([1, 0, 0], np.int32))
+    path = str(tmp_path / "HCLr.fst")
+    kf.write_lookahead_fst(path, f)
+    g = kf.read_fst(path)
+    _assert_same_fst(f, g)
+
+
+def test_lookahead_graph_matches_restatement(lib, synth_lookahead):
+    c = _cgraph(lib, synth_lookahead)
+    assert c is not None
+    p = OG.model_graph(synth_lookahead)
+    _assert_same_fst(c, p)
+    # every disambiguation id became epsilon; ilabels are transition-ids
+    dis = [int(x) for x in open(os.path.join(synth_lookahead, "graph", "disambig_tid.int")).read().split()]
+    assert not np.isin(c.ilabel, dis).any()
+    hcl = kf.read_fst(os.path.join(synth_lookahead, "graph", "HCLr.fst"))
+    assert np.isin(hcl.ilabel, dis).any()
+    # every state is useful (trimmed), emitting arcs first per state
+    for s in range(c.num_states):
+        il = c.ilabel[c.row[s]:c.row[s + 1]]
+        assert not np.any((il[:-1] == 0) & (il[1:] != 0))
+
+
+@pytest.mark.parametrize("grammar", [
+    '["w00001 w00002", "w00003 w00005 w00007", "w00002"]',
+    '["w00010", "w00010 w00011 w00010", "nonexistent w00012", "[unk]"]',
+    ' [ "w00004\\tw00005" , "w00006  w00007"] ',
+])
+def test_grammar_graph_matches_restatement(lib, synth_lookahead, grammar):
+    c = _cgraph(lib, synth_lookahead, grammar)
+    assert c is not None
+    _assert_same_fst(c, OG.model_graph(synth_lookahead, grammar))
+    # the grammar's words (and only those) appear on output labels
+    words = {v: k for k, v in kf.read_symbol_table(os.path.join(synth_lookahead, "graph", "words.txt")).items()}
+    sents = OG.parse_grammar(grammar, words)
+    assert set(int(x) for x in c.olabel if x) == set(w for s in sents for w in s)
+
+
+@pytest.mark.parametrize("grammar", ['{"a": 1}', "[1, 2]", "[]", "not json", '["unterminated'])
+def test_bad_grammar_is_an_error(lib, synth_lookahead, grammar):
+    assert _cgraph(lib, synth_lookahead, grammar) is None
+    with pytest.raises(ValueError):
+        OG.parse_grammar(grammar, {})
+
+
+def test_grammar_on_hclg_model_is_an_error_here(lib, synth_model):
+    # the recognizer falls back to the static graph with a warning; the
+    # diagnostic graph builder reports it
+    assert _cgraph(lib, synth_model, '["w00001"]') is None
+
+
+def test_grammar_lm_known_answer():
+    g = OG.estimate_grammar_lm([[1, 2], [1]], order=2, discount=0.5)
+    L = lambda x: float(-OG.logf(np.float32(x)))  # noqa: E731
+    assert g.start == 0 and g.num_states == 3
+    arcs = [[(int(g.ilabel[a]), float(g.weight[a]), int(g.nextstate[a]))
+             for a in range(int(g.row[s]), int(g.row[s + 1]))] for s in range(3)]
+    # root: counts {</s>: 2, 1: 2, 2: 1} of 5 (own + children's)
+    assert arcs[0] == [(1, L(0.2), 1), (2, L(0.1), 2)]
+    assert g.final[0] == np.float32(L(0.2))
+    # history (1): {</s>: 1, 2: 1}; backoff -log(0.5)
+    assert arcs[1] == [(0, L(0.5), 0), (2, L(0.25), 2)]
+    assert g.final[1] == np.float32(L(0.25))
+    assert arcs[2] == [(0, L(0.5), 0)]
+    assert g.final[2] == np.float32(L(0.5))
+
+
+def test_grammar_parse_escapes():
+    words = {"a": 1, "b/c": 2, 'q"x': 3, "\\u00e9": 4}
+    # JSON::ToString re-escapes the parsed string (src/json.h:295-298): "\/"
+    # becomes "/", but a parsed quote is looked up as \" and is not found
+    assert OG.parse_grammar('["a b\\/c", "q\\"x", "a"]', words) == [[1, 2], [], [1]]
+    # json.h keeps \\u escapes as text, and ToString re-escapes the backslash
+    assert OG.parse_grammar('["\\u00e9 a"]', words) == [[1]]
+
+
+def test_truncated_graph_files_fail_cleanly(lib, synth_lookahead, tmp_path):
+    import shutil
+    d = str(tmp_path / "m")
+    shutil.copytree(synth_lookahead, d)
+    gr = os.path.join(d, "graph", "Gr.fst")
+    data = open(gr, "rb").read()
+    open(gr, "wb").write(data[:len(data) // 2])
+    assert _cgraph(lib, d) is None
+    os.remove(gr)
+    assert _cgraph(lib, d) is None  # neither HCLG nor HCLr + Gr

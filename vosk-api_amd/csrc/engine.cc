@@ -1,5 +1,6 @@
 // GPU engine (see engine.h).
 #include "engine.h"
+#include "graph_compose.h"
 
 #include <algorithm>
 #include <fstream>
@@ -36,12 +37,15 @@ float MelScale(float f) { return 1127.0f * logf(1.0f + f / 700.0f); }
 // ---------------------------------------------------------------------------
 void ModelData::Load(const std::string& path) {
   dir = path;
-  std::string mdl, hclg, words_txt, wb, mfcc_conf, fbank_conf, cmvn_stats, pitch_conf, conf_file;
+  std::string mdl, hclg, hcl, gr, disambig_int, words_txt, wb, mfcc_conf, fbank_conf, cmvn_stats, pitch_conf, conf_file;
   if (FileExists(path + "/am/final.mdl") && FileExists(path + "/conf/model.conf")) {
     // V2 layout (src/model.cc:180-207)
     ApplyModelOptions(ReadConfigFile(path + "/conf/model.conf"), &dec, &dcb, &endpoint);
     mdl = path + "/am/final.mdl";
     hclg = path + "/graph/HCLG.fst";
+    hcl = path + "/graph/HCLr.fst";
+    gr = path + "/graph/Gr.fst";
+    disambig_int = path + "/graph/disambig_tid.int";
     words_txt = path + "/graph/words.txt";
     wb = path + "/graph/phones/word_boundary.int";
     mfcc_conf = path + "/conf/mfcc.conf";
@@ -60,6 +64,9 @@ void ModelData::Load(const std::string& path) {
     ApplyModelOptions(kv, &dec, &dcb, &endpoint);
     mdl = path + "/final.mdl";
     hclg = path + "/HCLG.fst";
+    hcl = path + "/HCLr.fst";
+    gr = path + "/Gr.fst";
+    disambig_int = path + "/disambig_tid.int";
     words_txt = path + "/words.txt";
     wb = path + "/word_boundary.int";
     mfcc_conf = path + "/mfcc.conf";
@@ -102,11 +109,29 @@ void ModelData::Load(const std::string& path) {
   }
   if (FileExists(pitch_conf))
     VAMD_ERR("pitch front-ends (" << pitch_conf << ") are not supported yet");
-  if (!FileExists(hclg))
-    VAMD_ERR("no static " << hclg << " (lookahead HCLr.fst+Gr.fst graphs need the host expansion "
-                                     "of SURVEY.md 8f-2, not implemented yet)");
-  VAMD_LOG("Loading HCLG from " << hclg);
-  ReadFstGraph(hclg, &graph);
+  if (FileExists(hclg)) {
+    VAMD_LOG("Loading HCLG from " << hclg);
+    ReadFstGraph(hclg, &graph);
+  } else if (FileExists(hcl) && FileExists(gr)) {
+    // src/model.cc:281-285 + src/recognizer.cc:31-37: HCLr o Gr, expanded
+    // once into a static graph (graph_compose.h)
+    VAMD_LOG("Loading HCL and G from " << hcl << " " << gr);
+    auto h = std::make_shared<HostFst>();
+    ReadFst(hcl, h.get());
+    HostFst g, composed;
+    ReadFst(gr, &g);
+    {
+      std::ifstream in(disambig_int);
+      if (!in) VAMD_ERR("cannot open " << disambig_int);
+      int d;
+      while (in >> d) disambig.push_back(d);
+    }
+    ComposeLookahead(*h, g, disambig, &composed);
+    ToGraph(composed, &graph, hcl + " o " + gr);
+    lookahead_hcl = h;
+  } else {
+    VAMD_ERR("Can't create decoding graph: neither " << hclg << " nor " << hcl << " + " << gr);
+  }
   if (!graph.osyms.empty()) {
     for (auto& [id, sym] : graph.osyms) { words.id2sym[id] = sym; words.sym2id[sym] = id; }
   } else {

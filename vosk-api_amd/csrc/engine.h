@@ -37,6 +37,11 @@ struct ModelData {
   TransitionModel tm;
   Nnet nnet;
   Graph graph;
+  // Lookahead models (graph/HCLr.fst + graph/Gr.fst, src/model.cc:282-285):
+  // the HCLr FST and disambiguation transition-ids, kept for the grammar
+  // recognizers' runtime graphs (graph_compose.h); null for HCLG models.
+  std::shared_ptr<const HostFst> lookahead_hcl;
+  std::vector<int> disambig;
   SymbolTable words;
   std::vector<char> phone_is_silence;  // indexed by phone id
   bool has_word_boundary = false;

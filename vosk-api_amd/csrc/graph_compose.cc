@@ -1,0 +1,522 @@
+// Static composition of lookahead graph pairs and runtime grammars
+// (graph_compose.h).
+#include "graph_compose.h"
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <functional>
+#include <sstream>
+#include <limits>
+#include <map>
+#include <utility>
+
+#include "common.h"
+
+namespace vamd {
+namespace {
+
+using Intervals = std::vector<std::pair<int, int>>;  // sorted, disjoint, non-adjacent [lo, hi]
+
+void Coalesce(Intervals* v) {
+  if (v->empty()) return;
+  std::sort(v->begin(), v->end());
+  size_t o = 0;
+  for (size_t i = 1; i < v->size(); i++) {
+    auto& b = (*v)[o];
+    const auto& c = (*v)[i];
+    if ((long long)c.first <= (long long)b.second + 1) {
+      b.second = std::max(b.second, c.second);
+    } else {
+      (*v)[++o] = c;
+    }
+  }
+  v->resize(o + 1);
+}
+
+// Output labels reachable from each state of `a` through output-epsilon arcs
+// (the label of the first non-epsilon output arc on such a path), and whether
+// a final state is reachable that way: per strongly connected component of
+// the output-epsilon subgraph (Tarjan, iterative; components complete sinks
+// first, so successors are done before their predecessors).
+struct Reach {
+  std::vector<int> comp;               // per state
+  std::vector<Intervals> labels;       // per component
+  std::vector<char> final;             // per component
+};
+
+void ComputeReach(const HostFst& a, Reach* r) {
+  const int S = a.NumStates();
+  std::vector<int> idx(S, -1), low(S, 0);
+  std::vector<char> onst(S, 0);
+  std::vector<int> st;
+  struct Frame { int v; int64_t arc; };
+  std::vector<Frame> cs;
+  r->comp.assign(S, -1);
+  int counter = 0, ncomp = 0;
+  for (int root = 0; root < S; root++) {
+    if (idx[root] >= 0) continue;
+    idx[root] = low[root] = counter++;
+    st.push_back(root);
+    onst[root] = 1;
+    cs.push_back({root, a.row[root]});
+    while (!cs.empty()) {
+      Frame& fr = cs.back();
+      const int v = fr.v;
+      if (fr.arc < a.row[v + 1]) {
+        const int64_t e = fr.arc++;
+        if (a.olabel[e] != 0) continue;
+        const int w = a.nextstate[e];
+        if (idx[w] < 0) {
+          idx[w] = low[w] = counter++;
+          st.push_back(w);
+          onst[w] = 1;
+          cs.push_back({w, a.row[w]});
+        } else if (onst[w]) {
+          low[v] = std::min(low[v], idx[w]);
+        }
+      } else {
+        if (low[v] == idx[v]) {
+          while (true) {
+            const int x = st.back();
+            st.pop_back();
+            onst[x] = 0;
+            r->comp[x] = ncomp;
+            if (x == v) break;
+          }
+          ncomp++;
+        }
+        cs.pop_back();
+        if (!cs.empty()) low[cs.back().v] = std::min(low[cs.back().v], low[v]);
+      }
+    }
+  }
+  // members of each component
+  std::vector<int> cbeg(ncomp + 1, 0), members(S);
+  for (int s = 0; s < S; s++) cbeg[r->comp[s] + 1]++;
+  for (int c = 0; c < ncomp; c++) cbeg[c + 1] += cbeg[c];
+  {
+    std::vector<int> fill(cbeg.begin(), cbeg.end() - 1);
+    for (int s = 0; s < S; s++) members[fill[r->comp[s]]++] = s;
+  }
+  r->labels.assign(ncomp, Intervals());
+  r->final.assign(ncomp, 0);
+  for (int c = 0; c < ncomp; c++) {
+    Intervals acc;
+    char fin = 0;
+    for (int m = cbeg[c]; m < cbeg[c + 1]; m++) {
+      const int v = members[m];
+      if (std::isfinite(a.final_cost[v])) fin = 1;
+      for (int64_t e = a.row[v]; e < a.row[v + 1]; e++) {
+        if (a.olabel[e] != 0) {
+          acc.push_back({a.olabel[e], a.olabel[e]});
+        } else {
+          const int d = r->comp[a.nextstate[e]];
+          if (d == c) continue;
+          fin |= r->final[d];
+          acc.insert(acc.end(), r->labels[d].begin(), r->labels[d].end());
+        }
+      }
+    }
+    Coalesce(&acc);
+    r->labels[c] = std::move(acc);
+    r->final[c] = fin;
+  }
+}
+
+// composed state -> id (open addressing; key = q1 << 33 | q2 << 1 | filter)
+struct StateTable {
+  std::vector<uint64_t> keys;
+  std::vector<int> vals;
+  size_t count = 0;
+  static uint64_t Mix(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+  }
+  StateTable() { keys.assign(1 << 16, ~0ull); vals.assign(1 << 16, -1); }
+  void Grow() {
+    std::vector<uint64_t> ok;
+    std::vector<int> ov;
+    ok.swap(keys);
+    ov.swap(vals);
+    keys.assign(ok.size() * 2, ~0ull);
+    vals.assign(ok.size() * 2, -1);
+    const uint64_t mask = keys.size() - 1;
+    for (size_t i = 0; i < ok.size(); i++) {
+      if (ok[i] == ~0ull) continue;
+      uint64_t h = Mix(ok[i]) & mask;
+      while (keys[h] != ~0ull) h = (h + 1) & mask;
+      keys[h] = ok[i];
+      vals[h] = ov[i];
+    }
+  }
+  // returns the id; *added when new (id = next_id)
+  int FindOrAdd(uint64_t key, int next_id, bool* added) {
+    if ((count + 1) * 2 > keys.size()) Grow();
+    const uint64_t mask = keys.size() - 1;
+    uint64_t h = Mix(key) & mask;
+    while (keys[h] != ~0ull) {
+      if (keys[h] == key) { *added = false; return vals[h]; }
+      h = (h + 1) & mask;
+    }
+    keys[h] = key;
+    vals[h] = next_id;
+    count++;
+    *added = true;
+    return next_id;
+  }
+};
+
+// Trim to the states that reach a final state and renumber breadth-first from
+// the start over each state's emitting arcs, then its epsilon-input arcs.
+void ConnectCanonical(const HostFst& in, HostFst* out) {
+  const int S = in.NumStates();
+  const int64_t A = in.NumArcs();
+  std::vector<int64_t> rbeg(S + 1, 0);
+  for (int64_t e = 0; e < A; e++) rbeg[in.nextstate[e] + 1]++;
+  for (int s = 0; s < S; s++) rbeg[s + 1] += rbeg[s];
+  std::vector<int> rsrc(A);
+  {
+    std::vector<int64_t> fill(rbeg.begin(), rbeg.end() - 1);
+    for (int s = 0; s < S; s++)
+      for (int64_t e = in.row[s]; e < in.row[s + 1]; e++) rsrc[fill[in.nextstate[e]]++] = s;
+  }
+  std::vector<char> coacc(S, 0);
+  std::vector<int> q;
+  for (int s = 0; s < S; s++)
+    if (std::isfinite(in.final_cost[s])) { coacc[s] = 1; q.push_back(s); }
+  for (size_t i = 0; i < q.size(); i++)
+    for (int64_t k = rbeg[q[i]]; k < rbeg[q[i] + 1]; k++)
+      if (!coacc[rsrc[k]]) { coacc[rsrc[k]] = 1; q.push_back(rsrc[k]); }
+  if (in.start < 0 || !coacc[in.start]) VAMD_ERR("the composed decoding graph is empty (no path reaches a final state)");
+  std::vector<int> nid(S, -1);
+  std::vector<int> order;
+  order.push_back(in.start);
+  nid[in.start] = 0;
+  *out = HostFst();
+  out->osyms = in.osyms;
+  out->start = 0;
+  out->row.push_back(0);
+  for (size_t i = 0; i < order.size(); i++) {
+    const int s = order[i];
+    out->final_cost.push_back(in.final_cost[s]);
+    for (int pass = 0; pass < 2; pass++) {
+      for (int64_t e = in.row[s]; e < in.row[s + 1]; e++) {
+        if ((in.ilabel[e] == 0) != (pass == 1)) continue;
+        const int d = in.nextstate[e];
+        if (!coacc[d]) continue;
+        if (nid[d] < 0) { nid[d] = (int)order.size(); order.push_back(d); }
+        out->ilabel.push_back(in.ilabel[e]);
+        out->olabel.push_back(in.olabel[e]);
+        out->weight.push_back(in.weight[e]);
+        out->nextstate.push_back(nid[d]);
+      }
+    }
+    out->row.push_back((int64_t)out->ilabel.size());
+  }
+}
+
+}  // namespace
+
+void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>& disambig,
+                      HostFst* out) {
+  if (a.NumStates() == 0 || b.NumStates() == 0) VAMD_ERR("cannot compose an empty FST");
+  if ((uint64_t)a.NumStates() >= (1ull << 31) || (uint64_t)b.NumStates() >= (1ull << 31))
+    VAMD_ERR("graph too large to compose");
+  int max_il = 0;
+  for (int l : a.ilabel) max_il = std::max(max_il, l);
+  std::vector<char> is_disambig(max_il + 1, 0);
+  for (int d : disambig)
+    if (d > 0 && d <= max_il) is_disambig[d] = 1;
+  Reach reach;
+  ComputeReach(a, &reach);
+  // grammar side: per state the epsilon arcs in order and the non-epsilon
+  // arcs sorted by input label (stable)
+  const int SB = b.NumStates();
+  std::vector<int64_t> bsorted(b.NumArcs());
+  std::vector<int64_t> beps_end(SB);  // arcs [row[s], beps_end[s]) of bsorted are epsilon
+  std::vector<int> bword(b.NumArcs());
+  std::vector<char> b_has_eps(SB), b_alleps(SB);
+  for (int s = 0; s < SB; s++) {
+    int64_t o = b.row[s];
+    for (int64_t e = b.row[s]; e < b.row[s + 1]; e++)
+      if (b.ilabel[e] == 0) bsorted[o++] = e;
+    beps_end[s] = o;
+    for (int64_t e = b.row[s]; e < b.row[s + 1]; e++)
+      if (b.ilabel[e] != 0) bsorted[o++] = e;
+    std::stable_sort(bsorted.begin() + beps_end[s], bsorted.begin() + b.row[s + 1],
+                     [&](int64_t x, int64_t y) { return b.ilabel[x] < b.ilabel[y]; });
+    for (int64_t k = b.row[s]; k < b.row[s + 1]; k++) bword[k] = b.ilabel[bsorted[k]];
+    b_has_eps[s] = beps_end[s] > b.row[s];
+    b_alleps[s] = beps_end[s] == b.row[s + 1] && !std::isfinite(b.final_cost[s]);
+  }
+  // can a path from HCL state p (grammar state q, no further grammar epsilon
+  // moves) match a word q accepts, or end in a final state?
+  auto useful = [&](int p, int q) {
+    const int c = reach.comp[p];
+    if (reach.final[c] && std::isfinite(b.final_cost[q])) return true;
+    const Intervals& iv = reach.labels[c];
+    const int* wb = bword.data() + beps_end[q];
+    const int* we = bword.data() + b.row[q + 1];
+    if (iv.empty() || wb == we) return false;
+    if ((int64_t)iv.size() <= (int64_t)(we - wb)) {
+      for (const auto& r : iv) {
+        const int* it = std::lower_bound(wb, we, r.first);
+        if (it != we && *it <= r.second) return true;
+      }
+    } else {
+      for (const int* w = wb; w < we; w++) {
+        auto it = std::upper_bound(iv.begin(), iv.end(), std::make_pair(*w, std::numeric_limits<int>::max()));
+        if (it != iv.begin() && std::prev(it)->second >= *w) return true;
+      }
+    }
+    return false;
+  };
+
+  HostFst c;
+  c.osyms = b.osyms;
+  StateTable table;
+  std::vector<uint64_t> keys;
+  auto key_of = [](int q1, int q2, int fs) {
+    return ((uint64_t)q1 << 33) | ((uint64_t)(uint32_t)q2 << 1) | (uint64_t)fs;
+  };
+  auto id_of = [&](int q1, int q2, int fs) {
+    const uint64_t k = key_of(q1, q2, fs);
+    bool added = false;
+    const int id = table.FindOrAdd(k, (int)keys.size(), &added);
+    if (added) {
+      if (keys.size() >= (size_t)std::numeric_limits<int>::max() - 1) VAMD_ERR("composed graph too large");
+      keys.push_back(k);
+    }
+    return id;
+  };
+  c.start = id_of(a.start, b.start, 0);
+  c.row.push_back(0);
+  for (size_t s = 0; s < keys.size(); s++) {
+    const int q1 = (int)(keys[s] >> 33), q2 = (int)((keys[s] >> 1) & 0xffffffffu), fs = (int)(keys[s] & 1);
+    const float fa = a.final_cost[q1], fb = b.final_cost[q2];
+    c.final_cost.push_back(std::isfinite(fa) && std::isfinite(fb) ? fa + fb
+                                                                   : std::numeric_limits<float>::infinity());
+    auto push = [&](int il, int ol, float w, int dst) {
+      c.ilabel.push_back(il); c.olabel.push_back(ol); c.weight.push_back(w); c.nextstate.push_back(dst);
+    };
+    if (fs == 0)  // the grammar moves alone on its epsilon (backoff) arcs
+      for (int64_t k = b.row[q2]; k < beps_end[q2]; k++) {
+        const int64_t e = bsorted[k];
+        push(0, b.olabel[e], b.weight[e], id_of(q1, b.nextstate[e], 0));
+      }
+    for (int64_t e = a.row[q1]; e < a.row[q1 + 1]; e++) {
+      const int il = (a.ilabel[e] > 0 && a.ilabel[e] <= max_il && is_disambig[a.ilabel[e]]) ? 0 : a.ilabel[e];
+      const int p = a.nextstate[e];
+      if (a.olabel[e] == 0) {  // HCL moves alone
+        if (b_alleps[q2] || !useful(p, q2)) continue;
+        push(il, 0, a.weight[e], id_of(p, q2, b_has_eps[q2] ? 1 : 0));
+      } else {  // matched word
+        const int* wb = bword.data() + beps_end[q2];
+        const int* we = bword.data() + b.row[q2 + 1];
+        const int* lo = std::lower_bound(wb, we, a.olabel[e]);
+        for (const int* it = lo; it != we && *it == a.olabel[e]; it++) {
+          const int64_t g = bsorted[it - bword.data()];
+          push(il, b.olabel[g], a.weight[e] + b.weight[g], id_of(p, b.nextstate[g], 0));
+        }
+      }
+    }
+    c.row.push_back((int64_t)c.ilabel.size());
+  }
+  VAMD_LOG("Composed lookahead graph: " << c.NumStates() << " states, " << c.NumArcs() << " arcs expanded");
+  ConnectCanonical(c, out);
+  VAMD_LOG("Static decoding graph: " << out->NumStates() << " states, " << out->NumArcs() << " arcs");
+}
+
+void EstimateGrammarLm(const std::vector<std::vector<int>>& sentences, int order, float discount,
+                       HostFst* out) {
+  if (order < 2) VAMD_ERR("--ngram-order must be >= 2");
+  struct LmState {
+    std::vector<int> history;
+    std::map<int, int> counts;
+    int tot = 0, backoff = -1, fst_state = -1;
+  };
+  std::vector<LmState> st;
+  std::map<std::vector<int>, int> index;
+  int num_active = 0;
+  std::function<int(const std::vector<int>&)> find_or_create = [&](const std::vector<int>& h) {
+    auto it = index.find(h);
+    if (it != index.end()) return it->second;
+    const int ans = (int)st.size();
+    st.emplace_back();
+    st.back().history = h;
+    index[h] = ans;
+    if (!h.empty()) {
+      const int b = find_or_create(std::vector<int>(h.begin() + 1, h.end()));
+      st[ans].backoff = b;
+    }
+    return ans;
+  };
+  auto add_count = [](LmState& s, int w, int n) {
+    s.counts[w] += n;
+    s.tot += n;
+  };
+  auto increment = [&](const std::vector<int>& h, int w) {
+    const int l = find_or_create(h);
+    if (st[l].tot == 0) num_active++;
+    add_count(st[l], w, 1);
+  };
+  for (const auto& sent : sentences) {  // AddCounts
+    std::vector<int> h;
+    for (int w : sent) {
+      if (w == 0) VAMD_ERR("word id 0 in a grammar sentence");
+      increment(h, w);
+      h.push_back(w);
+      if ((int)h.size() >= order) h.erase(h.begin());
+    }
+    increment(h, 0);
+  }
+  if (st.empty()) VAMD_ERR("empty grammar");
+  const int nst = (int)st.size();
+  for (int l = 0; l < nst; l++)  // SetParentCounts
+    for (int p = st[l].backoff; p != -1; p = st[p].backoff) {
+      const std::map<int, int> counts = st[l].counts;
+      for (const auto& [w, n] : counts) add_count(st[p], w, n);
+    }
+  int nfst = 0;  // AssignFstStates
+  for (int l = 0; l < nst; l++)
+    if (st[l].tot != 0) st[l].fst_state = nfst++;
+  if (nfst != num_active) VAMD_ERR("grammar LM estimation: inconsistent state counts");
+  auto find_nonzero = [&](std::vector<int> h) {
+    while (true) {
+      auto it = index.find(h);
+      if (it == index.end() || st[it->second].tot == 0) {
+        if (h.empty()) VAMD_ERR("grammar LM: no state for a history");
+        h.erase(h.begin());
+      } else {
+        return it->second;
+      }
+    }
+  };
+  std::vector<std::vector<std::pair<int, std::pair<float, int>>>> arcs(nfst);  // (label, (cost, dst))
+  *out = HostFst();
+  out->final_cost.assign(nfst, std::numeric_limits<float>::infinity());
+  out->start = st[find_nonzero({})].fst_state;
+  for (int l = 0; l < nst; l++) {
+    const LmState& s = st[l];
+    if (s.fst_state < 0) continue;
+    for (const auto& [w, n] : s.counts) {
+      const float p = (float)n * discount / (float)s.tot;
+      const float logprob = std::log(p);
+      if (w == 0) {
+        out->final_cost[s.fst_state] = -logprob;
+      } else {
+        std::vector<int> next = s.history;
+        next.push_back(w);
+        const int d = st[find_nonzero(next)].fst_state;
+        arcs[s.fst_state].push_back({w, {-logprob, d}});
+      }
+    }
+    if (s.backoff >= 0)
+      arcs[s.fst_state].push_back({0, {-std::log(1.0f - discount), st[s.backoff].fst_state}});
+  }
+  out->row.push_back(0);
+  for (int s = 0; s < nfst; s++) {
+    std::sort(arcs[s].begin(), arcs[s].end(),
+              [](const auto& x, const auto& y) { return x.first < y.first; });
+    for (const auto& a : arcs[s]) {
+      out->ilabel.push_back(a.first);
+      out->olabel.push_back(a.first);
+      out->weight.push_back(a.second.first);
+      out->nextstate.push_back(a.second.second);
+    }
+    out->row.push_back((int64_t)out->ilabel.size());
+  }
+}
+
+namespace {
+// json.h parse_string / json_escape (src/json.h:34-48,519-555): a grammar
+// phrase is the parsed string re-escaped, as JSON::ToString returns it.
+std::string JsonEscape(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\b': o += "\\b"; break;
+      case '\f': o += "\\f"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      default: o += c;
+    }
+  }
+  return o;
+}
+}  // namespace
+
+std::vector<std::vector<int>> ParseGrammarJson(const std::string& js, const SymbolTable& words) {
+  size_t p = 0;
+  auto ws = [&]() { while (p < js.size() && (js[p] == ' ' || js[p] == '\t' || js[p] == '\n' || js[p] == '\r')) p++; };
+  ws();
+  if (p >= js.size() || js[p] != '[') VAMD_ERR("Expecting array of strings, got: '" << js << "'");
+  p++;
+  std::vector<std::string> phrases;
+  ws();
+  if (p < js.size() && js[p] == ']') {
+    p++;
+  } else {
+    while (true) {
+      ws();
+      if (p >= js.size() || js[p] != '"') VAMD_ERR("Expecting array of strings, got: '" << js << "'");
+      std::string val;
+      for (p++; p < js.size() && js[p] != '"'; p++) {
+        if (js[p] != '\\') { val += js[p]; continue; }
+        if (++p >= js.size()) break;
+        switch (js[p]) {
+          case '"': val += '"'; break;
+          case '\\': val += '\\'; break;
+          case '/': val += '/'; break;
+          case 'b': val += '\b'; break;
+          case 'f': val += '\f'; break;
+          case 'n': val += '\n'; break;
+          case 'r': val += '\r'; break;
+          case 't': val += '\t'; break;
+          case 'u':
+            val += "\\u";
+            for (int i = 1; i <= 4; i++) {
+              const char c = p + i < js.size() ? js[p + i] : 0;
+              if (!isxdigit((unsigned char)c)) VAMD_ERR("bad unicode escape in grammar");
+              val += c;
+            }
+            p += 4;
+            break;
+          default: val += '\\';
+        }
+      }
+      if (p >= js.size()) VAMD_ERR("unterminated string in grammar");
+      p++;
+      phrases.push_back(JsonEscape(val));
+      ws();
+      if (p < js.size() && js[p] == ',') { p++; continue; }
+      if (p < js.size() && js[p] == ']') { p++; break; }
+      VAMD_ERR("Expecting array of strings, got: '" << js << "'");
+    }
+  }
+  if (phrases.empty()) VAMD_ERR("Expecting array of strings, got: '" << js << "'");
+  std::vector<std::vector<int>> out;
+  for (const auto& line : phrases) {
+    std::vector<int> sent;
+    std::string tok;
+    std::istringstream ss(line);
+    while (std::getline(ss, tok, ' ')) {
+      const int id = words.Find(tok);
+      if (id < 0) {
+        VAMD_WARN("Ignoring word missing in vocabulary: '" << tok << "'");
+      } else {
+        sent.push_back(id);
+      }
+    }
+    out.push_back(std::move(sent));
+  }
+  return out;
+}
+
+}  // namespace vamd

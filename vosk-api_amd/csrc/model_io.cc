@@ -7,6 +7,7 @@
 #include <atomic>
 #include <cmath>
 #include <iterator>
+#include <limits>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -708,85 +709,215 @@ void ReadSymtab(BReader& r, std::map<int, std::string>* out) {
 }
 }  // namespace
 
-void ReadFstGraph(const std::string& path, Graph* g) {
+namespace {
+constexpr int32_t kAddOnMagic = 446681434;
+
+// LOUDS n-gram FST body (OpenFST extensions/ngram NGramFstImpl::Init layout):
+// uint64 num_states, num_futures, num_final; context bitmap (2n+1 bits),
+// future bitmap (num_futures+n+1 bits), final bitmap (n bits), each in 64-bit
+// words with bit i at word i/64, position i%64; int32 context words [n+1],
+// future words [num_futures]; padding to 4 bytes; float backoff [n+1], final
+// costs [num_final], future costs [num_futures+1].
+void ParseNgramBody(BReader& r, HostFst* f, const std::string& path) {
+  const uint64_t n = r.Get<uint64_t>(), nfut = r.Get<uint64_t>(), nfin = r.Get<uint64_t>();
+  if (n < 2 || n > (1ull << 31) || nfut > (1ull << 34) || nfin > n) VAMD_ERR("malformed ngram FST " << path);
+  auto words64 = [](uint64_t bits) { return (bits + 63) / 64; };
+  const uint64_t cbits = 2 * n + 1, fbits = nfut + n + 1;
+  std::vector<uint64_t> ctx(words64(cbits)), fut(words64(fbits)), fin(words64(n));
+  for (auto& v : ctx) v = r.Get<uint64_t>();
+  for (auto& v : fut) v = r.Get<uint64_t>();
+  for (auto& v : fin) v = r.Get<uint64_t>();
+  std::vector<int32_t> cwords(n + 1), fwords(nfut);
+  for (auto& v : cwords) v = r.Get<int32_t>();
+  for (auto& v : fwords) v = r.Get<int32_t>();
+  std::vector<float> backoff(n + 1), finals(nfin), fprob(nfut + 1);
+  for (auto& v : backoff) v = r.Get<float>();
+  for (auto& v : finals) v = r.Get<float>();
+  for (auto& v : fprob) v = r.Get<float>();
+  auto bit = [](const std::vector<uint64_t>& b, uint64_t i) { return (b[i >> 6] >> (i & 63)) & 1; };
+  // context tree (LOUDS with super-root "10"): node ids in level order; the
+  // degree sequence of node k (1^d 0) follows the super-root's
+  if (!(bit(ctx, 0) == 1 && bit(ctx, 1) == 0)) VAMD_ERR("malformed ngram FST context " << path);
+  std::vector<int> parent(n, -1), first_child(n, 0), num_children(n, 0);
+  {
+    uint64_t pos = 2, next = 1;
+    for (uint64_t k = 0; k < n; k++) {
+      first_child[k] = (int)next;
+      while (pos < cbits && bit(ctx, pos)) {
+        if (next >= n) VAMD_ERR("malformed ngram FST context " << path);
+        parent[next++] = (int)k;
+        num_children[k]++;
+        pos++;
+      }
+      if (pos >= cbits) VAMD_ERR("malformed ngram FST context " << path);
+      pos++;  // the 0 that ends node k's degree sequence
+    }
+    if (next != n || num_children[0] == 0)
+      VAMD_ERR("malformed ngram FST context " << path);
+  }
+  // futures: a leading 0, then 1^k 0 per state
+  std::vector<int64_t> fut_begin(n + 1, 0);
+  {
+    if (bit(fut, 0) != 0) VAMD_ERR("malformed ngram FST futures " << path);
+    uint64_t pos = 1, ones = 0;
+    for (uint64_t s = 0; s < n; s++) {
+      fut_begin[s] = (int64_t)ones;
+      while (pos < fbits && bit(fut, pos)) { ones++; pos++; }
+      if (pos >= fbits) VAMD_ERR("malformed ngram FST futures " << path);
+      pos++;
+    }
+    fut_begin[n] = (int64_t)ones;
+    if (ones != nfut) VAMD_ERR("malformed ngram FST futures " << path);
+  }
+  // child of node k labelled w (children are sorted by label), or -1
+  auto child = [&](int k, int w) {
+    const int32_t* b = cwords.data() + first_child[k];
+    const int32_t* e = b + num_children[k];
+    const int32_t* it = std::lower_bound(b, e, w);
+    return (it == e || *it != w) ? -1 : first_child[k] + (int)(it - b);
+  };
+  std::vector<int> ctx_words;  // labels from the state's node up to the root
+  f->start = 1;
+  f->final_cost.assign(n, std::numeric_limits<float>::infinity());
+  f->row.assign(n + 1, 0);
+  f->ilabel.clear(); f->olabel.clear(); f->weight.clear(); f->nextstate.clear();
+  uint64_t nf = 0;
+  for (uint64_t s = 0; s < n; s++) {
+    f->row[s] = (int64_t)f->ilabel.size();
+    if (bit(fin, s)) f->final_cost[s] = finals[nf++];
+    if (s != 0) {  // backoff: the parent context (oldest word dropped)
+      f->ilabel.push_back(0); f->olabel.push_back(0);
+      f->weight.push_back(backoff[s]); f->nextstate.push_back(parent[s]);
+    }
+    ctx_words.clear();
+    for (int k = (int)s; k != 0; k = parent[k]) ctx_words.push_back(cwords[k]);
+    for (int64_t i = fut_begin[s]; i < fut_begin[s + 1]; i++) {
+      const int w = fwords[i];
+      // NGramFstImpl::Transition: the root's child w, then down the
+      // state's context from its most recent word while children exist
+      int node = child(0, w);
+      if (node < 0) {
+        node = 0;
+      } else {
+        for (int j = (int)ctx_words.size() - 1; j >= 0 && num_children[node] > 0; j--) {
+          const int c = child(node, ctx_words[j]);
+          if (c < 0) break;
+          node = c;
+        }
+      }
+      f->ilabel.push_back(w); f->olabel.push_back(w);
+      f->weight.push_back(fprob[i]); f->nextstate.push_back(node);
+    }
+  }
+  f->row[n] = (int64_t)f->ilabel.size();
+  if (nf != nfin) VAMD_ERR("malformed ngram FST finals " << path);
+}
+
+void ParseFst(BReader& r, HostFst* f, const std::string& path, int depth) {
+  if (r.Get<int32_t>() != kFstMagic) VAMD_ERR(path << " is not an OpenFST binary file");
+  std::string ftype = r.Str(), atype = r.Str();
+  if (atype != "standard") VAMD_ERR("unsupported arc type " << atype << " in " << path);
+  r.Get<int32_t>();  // version
+  int32_t flags = r.Get<int32_t>();
+  r.Get<uint64_t>();  // properties
+  int64_t start = r.Get<int64_t>(), ns = r.Get<int64_t>(), na = r.Get<int64_t>();
+  if (flags & 1) ReadSymtab(r, nullptr);
+  if (flags & 2) ReadSymtab(r, &f->osyms);
+  f->ilabel.clear(); f->olabel.clear(); f->weight.clear(); f->nextstate.clear();
+  f->final_cost.clear(); f->row.clear();
+  if (ftype == "const") {
+    if (ns < 0 || na < 0) VAMD_ERR("bad const FST header in " << path);
+    if (flags & 4) r.p = (r.p + 15) / 16 * 16;
+    f->final_cost.resize(ns);
+    f->row.resize(ns + 1);
+    for (int64_t s = 0; s < ns; s++) {
+      f->final_cost[s] = r.Get<float>();
+      f->row[s] = r.Get<uint32_t>();
+      r.Get<uint32_t>();
+      r.Get<uint32_t>();
+      r.Get<uint32_t>();
+    }
+    f->row[ns] = na;
+    if (flags & 4) r.p = (r.p + 15) / 16 * 16;
+    f->ilabel.resize(na); f->olabel.resize(na); f->weight.resize(na); f->nextstate.resize(na);
+    for (int64_t a = 0; a < na; a++) {
+      f->ilabel[a] = r.Get<int32_t>();
+      f->olabel[a] = r.Get<int32_t>();
+      f->weight[a] = r.Get<float>();
+      f->nextstate[a] = r.Get<int32_t>();
+    }
+    f->start = (int)start;
+  } else if (ftype == "vector") {
+    f->row.push_back(0);
+    for (int64_t s = 0; ns < 0 ? r.p < r.d.size() : s < ns; s++) {
+      f->final_cost.push_back(r.Get<float>());
+      int64_t n = r.Get<int64_t>();
+      for (int64_t a = 0; a < n; a++) {
+        f->ilabel.push_back(r.Get<int32_t>());
+        f->olabel.push_back(r.Get<int32_t>());
+        f->weight.push_back(r.Get<float>());
+        f->nextstate.push_back(r.Get<int32_t>());
+      }
+      f->row.push_back((int64_t)f->ilabel.size());
+    }
+    f->start = (int)start;
+  } else if (ftype == "ngram") {
+    ParseNgramBody(r, f, path);
+  } else if (ftype == "olabel_lookahead" && depth == 0) {
+    if (r.Get<int32_t>() != kAddOnMagic) VAMD_ERR("bad add-on header in " << path);
+    std::map<int, std::string> outer = std::move(f->osyms);
+    ParseFst(r, f, path, depth + 1);  // the contained FST; the add-on data is not needed
+    if (f->osyms.empty()) f->osyms = std::move(outer);
+  } else {
+    VAMD_ERR("unsupported FST type '" << ftype << "' in " << path);
+  }
+  const int64_t S = f->NumStates();
+  if (S > 0 && (f->start < 0 || f->start >= S)) VAMD_ERR("bad start state in " << path);
+  for (int64_t a = 0; a < f->NumArcs(); a++)
+    if (f->nextstate[a] < 0 || f->nextstate[a] >= S) VAMD_ERR("arc to invalid state in " << path);
+}
+}  // namespace
+
+void ReadFst(const std::string& path, HostFst* f) {
   BReader r;
   {
     std::ifstream in(path, std::ios::binary);
     if (!in) VAMD_ERR("cannot open " << path);
     r.d.assign((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
   }
-  if (r.Get<int32_t>() != kFstMagic) VAMD_ERR(path << " is not an OpenFST binary file");
-  std::string ftype = r.Str(), atype = r.Str();
-  if (atype != "standard") VAMD_ERR("unsupported arc type " << atype);
-  r.Get<int32_t>();  // version
-  int32_t flags = r.Get<int32_t>();
-  r.Get<uint64_t>();  // properties
-  int64_t start = r.Get<int64_t>(), ns = r.Get<int64_t>(), na = r.Get<int64_t>();
-  if (flags & 1) ReadSymtab(r, nullptr);
-  if (flags & 2) ReadSymtab(r, &g->osyms);
-  std::vector<float> final_cost;
-  std::vector<int64_t> row;
-  std::vector<int> il, ol, nx;
-  std::vector<float> w;
-  if (ftype == "const") {
-    if (flags & 4) r.p = (r.p + 15) / 16 * 16;
-    final_cost.resize(ns);
-    row.resize(ns + 1);
-    for (int64_t s = 0; s < ns; s++) {
-      final_cost[s] = r.Get<float>();
-      row[s] = r.Get<uint32_t>();
-      r.Get<uint32_t>();
-      r.Get<uint32_t>();
-      r.Get<uint32_t>();
-    }
-    row[ns] = na;
-    if (flags & 4) r.p = (r.p + 15) / 16 * 16;
-    il.resize(na); ol.resize(na); w.resize(na); nx.resize(na);
-    for (int64_t a = 0; a < na; a++) {
-      il[a] = r.Get<int32_t>();
-      ol[a] = r.Get<int32_t>();
-      w[a] = r.Get<float>();
-      nx[a] = r.Get<int32_t>();
-    }
-  } else if (ftype == "vector") {
-    row.push_back(0);
-    for (int64_t s = 0; ns < 0 ? r.p < r.d.size() : s < ns; s++) {
-      final_cost.push_back(r.Get<float>());
-      int64_t n = r.Get<int64_t>();
-      for (int64_t a = 0; a < n; a++) {
-        il.push_back(r.Get<int32_t>());
-        ol.push_back(r.Get<int32_t>());
-        w.push_back(r.Get<float>());
-        nx.push_back(r.Get<int32_t>());
-      }
-      row.push_back((int64_t)il.size());
-    }
-  } else {
-    VAMD_ERR("unsupported FST type '" << ftype << "' (lookahead/ngram graphs need the host "
-                                         "expansion of SURVEY.md 8f-2)");
-  }
-  // reorder per state: emitting arcs first (stable), then epsilon-input arcs
-  int64_t S = (int64_t)final_cost.size(), A = (int64_t)il.size();
-  g->start = (int)start;
-  g->final_cost = final_cost;
+  *f = HostFst();
+  ParseFst(r, f, path, 0);
+}
+
+void ToGraph(const HostFst& f, Graph* g, const std::string& what) {
+  const int64_t S = f.NumStates(), A = f.NumArcs();
+  if (S == 0) VAMD_ERR(what << " has no states");
+  g->start = f.start;
+  g->final_cost = f.final_cost;
+  g->osyms = f.osyms;
   g->arc_begin.assign(S + 1, 0);
   g->eps_begin.assign(S, 0);
   g->ilabel.resize(A); g->olabel.resize(A); g->weight.resize(A); g->nextstate.resize(A);
   int64_t o = 0;
-  for (int64_t s = 0; s < S; s++) {
+  for (int64_t s = 0; s < S; s++) {  // emitting arcs first (stable), then epsilon-input arcs
     g->arc_begin[s] = o;
     for (int pass = 0; pass < 2; pass++) {
       if (pass == 1) g->eps_begin[s] = o;
-      for (int64_t a = row[s]; a < row[s + 1]; a++) {
-        bool eps = il[a] == 0;
-        if (eps != (pass == 1)) continue;
-        if (nx[a] < 0 || nx[a] >= S) VAMD_ERR("arc to invalid state in " << path);
-        g->ilabel[o] = il[a]; g->olabel[o] = ol[a]; g->weight[o] = w[a]; g->nextstate[o] = nx[a];
+      for (int64_t a = f.row[s]; a < f.row[s + 1]; a++) {
+        if ((f.ilabel[a] == 0) != (pass == 1)) continue;
+        g->ilabel[o] = f.ilabel[a]; g->olabel[o] = f.olabel[a];
+        g->weight[o] = f.weight[a]; g->nextstate[o] = f.nextstate[a];
         ++o;
       }
     }
   }
   g->arc_begin[S] = o;
+}
+
+void ReadFstGraph(const std::string& path, Graph* g) {
+  HostFst f;
+  ReadFst(path, &f);
+  ToGraph(f, g, path);
 }
 
 void ReadSymbolTable(const std::string& path, SymbolTable* t) {

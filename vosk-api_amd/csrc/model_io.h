@@ -165,6 +165,36 @@ struct Graph {
 
 void ReadFstGraph(const std::string& path, Graph* g);
 
+// A StdArc FST on the host in file order (CSR): what ReadFst returns for any
+// of the graph files a model directory holds, and what the composition of a
+// lookahead graph pair produces (graph_compose.h).
+struct HostFst {
+  int start = -1;
+  std::vector<float> final_cost;  // +inf = not final
+  std::vector<int64_t> row;       // arcs of state s: [row[s], row[s+1])
+  std::vector<int> ilabel, olabel, nextstate;
+  std::vector<float> weight;
+  std::map<int, std::string> osyms;  // output symbols from the header, if present
+  int NumStates() const { return (int)final_cost.size(); }
+  int64_t NumArcs() const { return (int64_t)ilabel.size(); }
+};
+
+// OpenFST binary reader for the FST types Vosk models ship
+// (src/model.cc:27-32 registers them; :278-285 reads them):
+//  * "const" / "vector" StdArc FSTs (HCLG.fst);
+//  * "olabel_lookahead" (HCLr.fst): an add-on FST (outer header, add-on magic
+//    446681434, the contained const FST with its own header, then the
+//    label-reachability data).  Only the contained FST is used: composition
+//    computes the reachable output labels itself (graph_compose.cc);
+//  * "ngram" (Gr.fst): OpenFST's LOUDS-encoded backoff n-gram acceptor
+//    (extensions/ngram/ngram-fst.h), expanded to explicit arcs: per state the
+//    backoff epsilon arc first (all states but the unigram root 0), then one
+//    arc per future word, whose destination is the longest context of the
+//    reversed-history trie (NGramFstImpl::Transition); start state 1.
+void ReadFst(const std::string& path, HostFst* f);
+// CSR decode graph from a host FST: emitting arcs first per state (stable).
+void ToGraph(const HostFst& f, Graph* g, const std::string& what);
+
 struct SymbolTable {
   std::unordered_map<int, std::string> id2sym;
   std::unordered_map<std::string, int> sym2id;

@@ -12,6 +12,7 @@
 #include <string>
 
 #include "common.h"
+#include "graph_compose.h"
 #include "vosk_impl.h"
 #include "../../include/vosk_api.h"
 #include "../../include/vosk_amd_engine.h"
@@ -85,9 +86,7 @@ VoskRecognizer* vosk_recognizer_new_spk(VoskModel* model, float sample_rate, Vos
 
 VoskRecognizer* vosk_recognizer_new_grm(VoskModel* model, float sample_rate, const char* grammar) {
   API_TRY
-  VAMD_WARN("Runtime graphs are not supported by this model build; decoding with the static graph");
-  (void)grammar;
-  return (VoskRecognizer*)new Recognizer((Model*)model, sample_rate);
+  return (VoskRecognizer*)new Recognizer((Model*)model, sample_rate, grammar ? grammar : "");
   API_CATCH(nullptr)
 }
 
@@ -266,6 +265,43 @@ const char* vamd_plan_describe(const char* model_dir, int fpc) {
   return out.c_str();
   API_CATCH(nullptr)
 }
+
+void* vamd_graph_new(const char* model_dir, const char* grammar) {
+  API_TRY
+  auto md = std::make_unique<ModelData>();
+  md->Load(model_dir);
+  if (grammar) {
+    if (!md->lookahead_hcl) VAMD_ERR("Runtime graphs are not supported by this model");
+    HostFst g, composed;
+    EstimateGrammarLm(ParseGrammarJson(grammar, md->words), 2, 0.5f, &g);
+    ComposeLookahead(*md->lookahead_hcl, g, md->disambig, &composed);
+    md->graph = Graph();
+    ToGraph(composed, &md->graph, "grammar graph");
+  }
+  return (void*)new Graph(std::move(md->graph));
+  API_CATCH(nullptr)
+}
+
+int vamd_graph_dims(void* graph, int* start, long long* num_arcs) {
+  const Graph* g = (const Graph*)graph;
+  *start = g->start;
+  *num_arcs = (long long)g->NumArcs();
+  return g->NumStates();
+}
+
+int vamd_graph_copy(void* graph, float* final_cost, long long* arc_begin, int* ilabel, int* olabel,
+                    float* weight, int* nextstate) {
+  const Graph* g = (const Graph*)graph;
+  std::copy(g->final_cost.begin(), g->final_cost.end(), final_cost);
+  std::copy(g->arc_begin.begin(), g->arc_begin.end(), arc_begin);
+  std::copy(g->ilabel.begin(), g->ilabel.end(), ilabel);
+  std::copy(g->olabel.begin(), g->olabel.end(), olabel);
+  std::copy(g->weight.begin(), g->weight.end(), weight);
+  std::copy(g->nextstate.begin(), g->nextstate.end(), nextstate);
+  return g->NumStates();
+}
+
+void vamd_graph_free(void* graph) { delete (Graph*)graph; }
 
 int vamd_silence_weighting_run(int ncalls, const int* num_frames_ready, const int* first_decoder_frame,
                                const int* trace_off, const int* tids, const int* toks,

@@ -1,5 +1,6 @@
 // Vosk object layer (see vosk_impl.h).
 #include "vosk_impl.h"
+#include "graph_compose.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -87,6 +88,35 @@ int Model::FindWord(const std::string& w) const { return md_->words.Find(w); }
 
 Engine* Model::StreamEngine() {
   std::lock_guard<std::mutex> lk(mu_);
+  return StreamEngineLocked();
+}
+
+Engine* Model::GrammarEngine(const std::string& grammar) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!md_->lookahead_hcl) {
+    VAMD_WARN("Runtime graphs are not supported by this model");
+    return StreamEngineLocked();
+  }
+  auto it = grammar_engines_.find(grammar);
+  if (it != grammar_engines_.end()) return it->second.get();
+  HostFst g, composed;
+  EstimateGrammarLm(ParseGrammarJson(grammar, md_->words), 2, 0.5f, &g);
+  ComposeLookahead(*md_->lookahead_hcl, g, md_->disambig, &composed);
+  auto md = std::make_shared<ModelData>(*md_);
+  md->graph = Graph();
+  ToGraph(composed, &md->graph, "grammar graph");
+  EngineConfig cfg;
+  cfg.frames_per_chunk = md->dcb.frames_per_chunk;
+  cfg.max_slots = EnvInt("VOSK_AMD_GRAMMAR_STREAMS", 8);
+  cfg.device = DeviceFromEnv();
+  cfg.max_step_samples = 4096;
+  cfg.lattice = true;
+  Engine* e = new Engine(md, cfg);
+  grammar_engines_[grammar].reset(e);
+  return e;
+}
+
+Engine* Model::StreamEngineLocked() {
   if (!engine_) {
     EngineConfig cfg;
     cfg.frames_per_chunk = md_->dcb.frames_per_chunk;
@@ -111,9 +141,12 @@ static int InputRate(float sr) {
   return r;
 }
 
-Recognizer::Recognizer(Model* model, float sr) : model_(model), sample_frequency_(sr) {
+Recognizer::Recognizer(Model* model, float sr) : Recognizer(model, sr, nullptr) {}
+
+Recognizer::Recognizer(Model* model, float sr, const char* grammar)
+    : model_(model), sample_frequency_(sr) {
   const int rate = InputRate(sr);
-  engine_ = model->StreamEngine();
+  engine_ = grammar ? model->GrammarEngine(grammar) : model->StreamEngine();
   slot_ = engine_->AllocSlot();
   try {
     engine_->SetSampleRate(slot_, rate);
@@ -177,7 +210,7 @@ bool Recognizer::EndpointDetected() {
   if (frames == 0) return false;
   std::vector<PathResult> pr;
   engine_->BestPaths({slot_}, false, &pr);
-  const ModelData& m = *model_->data();
+  const ModelData& m = engine_->model();
   const float shift = 0.01f * m.dcb.frame_subsampling_factor;
   return EndpointRulesFire(m.endpoint, frames, TrailingSilenceFrames(m, pr[0].arcs), shift,
                            pr[0].final_relative_cost);
@@ -244,7 +277,7 @@ std::string Recognizer::WordsText(const std::vector<WordSeg>& w) const {
 
 const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
   if (engine_->NumFramesDecoded(slot_) == 0) return StoreEmptyReturn();
-  const ModelData& m = *model_->data();
+  const ModelData& m = engine_->model();
   const double t0 = samples_round_start_ / sample_frequency_;
   const double shift = 0.01 * m.dcb.frame_subsampling_factor;
   auto wtext = [&](const std::vector<int>& words) {
@@ -322,7 +355,7 @@ const char* Recognizer::PartialResult() {  // src/recognizer.cc:732-806
     res["partial"] = Json::Str("");
     return StoreReturn(res.Dump());
   }
-  const ModelData& m = *model_->data();
+  const ModelData& m = engine_->model();
   if (partial_words_) {  // MBR over the partial lattice, no final costs, no graph scale (:740-780)
     const MbrResult r = SegmentMbr(engine_, slot_, m, false, 1.0f);
     const double shift = 0.01 * m.dcb.frame_subsampling_factor;

@@ -42,12 +42,19 @@ class Model {
   const std::shared_ptr<ModelData>& data() const { return md_; }
   // Engine shared by this model's streaming recognizers (created lazily).
   Engine* StreamEngine();
+  // Engine of the grammar recognizers with this phrase list (JSON array of
+  // strings, src/recognizer.cc:49-108): the runtime graph HCLr o G(grammar),
+  // one engine per distinct grammar, created on first use.  Models without
+  // HCLr.fst warn and return the static-graph engine, as the reference does.
+  Engine* GrammarEngine(const std::string& grammar);
 
  private:
   ~Model() = default;
   std::shared_ptr<ModelData> md_;
   std::unique_ptr<Engine> engine_;
+  std::map<std::string, std::unique_ptr<Engine>> grammar_engines_;
   std::mutex mu_;
+  Engine* StreamEngineLocked();
   std::atomic<int> ref_{1};
 };
 
@@ -57,6 +64,7 @@ enum RecognizerState { RECOGNIZER_INITIALIZED, RECOGNIZER_RUNNING, RECOGNIZER_EN
 class Recognizer {
  public:
   Recognizer(Model* model, float sample_frequency);
+  Recognizer(Model* model, float sample_frequency, const char* grammar);
   ~Recognizer();
   void SetMaxAlternatives(int n) { max_alternatives_ = n; }
   void SetWords(bool w) { words_ = w; }

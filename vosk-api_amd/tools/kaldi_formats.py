@@ -31,6 +31,7 @@ Reference call sites that read these files: ``src/model.cc:233-243`` (final.mdl)
 """
 from __future__ import annotations
 
+import os
 import struct
 from dataclasses import dataclass, field
 
@@ -652,6 +653,170 @@ def write_vector_fst(path: str, f: Fst):
         fh.write(bytes(buf))
 
 
+ADDON_MAGIC = 446681434
+
+
+def _fst_header(ftype, start, ns, na, version=2, flags=0):
+    return (struct.pack("<i", FST_MAGIC) + _wstr(ftype) + _wstr("standard")
+            + struct.pack("<i", version) + struct.pack("<i", flags) + struct.pack("<Q", 0)
+            + struct.pack("<q", start) + struct.pack("<q", ns) + struct.pack("<q", na))
+
+
+def write_lookahead_fst(path: str, f: Fst):
+    """OpenFST "olabel_lookahead" add-on FST: outer header, add-on magic, the
+    contained const FST (aligned, its own header), then the add-on flag.  The
+    synthetic files carry no label-reachability data (flag 0); readers here
+    compute reachability themselves."""
+    inner_path = path + ".inner.tmp"
+    write_const_fst(inner_path, f, aligned=False)
+    inner = open(inner_path, "rb").read()
+    os.remove(inner_path)
+    buf = bytearray(_fst_header("olabel_lookahead", -1, 0, 0, version=1))
+    buf += struct.pack("<i", ADDON_MAGIC)
+    buf += inner
+    buf += b"\0"  # have_addon = false
+    with open(path, "wb") as fh:
+        fh.write(bytes(buf))
+
+
+def write_ngram_fst(path: str, lm: dict):
+    """OpenFST "ngram" (LOUDS) backoff n-gram acceptor.  lm maps a history,
+    most recent word first (a tuple; () = the unigram root, (0,) = sentence
+    start), to {"fut": {word: cost}, "backoff": cost (not for the root),
+    "final": cost or None}.  Every history's parent (oldest word dropped)
+    must exist, and (0,) must exist (it becomes the start state 1)."""
+    kids = {}
+    for h in lm:
+        if h:
+            if h[:-1] not in lm:
+                raise ValueError(f"history {h} has no parent")
+            kids.setdefault(h[:-1], []).append(h)
+    if (0,) not in lm:
+        raise ValueError("no sentence-start history (0,)")
+    order = [()]
+    i = 0
+    while i < len(order):
+        order.extend(sorted(kids.get(order[i], []), key=lambda x: x[-1]))
+        i += 1
+    n = len(order)
+    ctx = [1, 0]
+    for h in order:
+        ctx += [1] * len(kids.get(h, [])) + [0]
+    fut = [0]
+    fwords, fprobs, finals, finbits = [], [], [], []
+    for h in order:
+        f = sorted(lm[h]["fut"].items())
+        fut += [1] * len(f) + [0]
+        fwords += [w for w, _ in f]
+        fprobs += [c for _, c in f]
+        fc = lm[h].get("final")
+        finbits.append(1 if fc is not None else 0)
+        if fc is not None:
+            finals.append(fc)
+
+    def pack(bits):
+        words = np.zeros((len(bits) + 63) // 64, np.uint64)
+        for j, b in enumerate(bits):
+            if b:
+                words[j >> 6] |= np.uint64(1) << np.uint64(j & 63)
+        return words.tobytes()
+
+    cwords = [0] + [h[-1] for h in order[1:]] + [0]
+    backoff = [0.0] + [lm[h].get("backoff", 0.0) for h in order[1:]] + [0.0]
+    data = struct.pack("<QQQ", n, len(fwords), len(finals))
+    data += pack(ctx) + pack(fut) + pack(finbits)
+    data += np.array(cwords, "<i4").tobytes() + np.array(fwords, "<i4").tobytes()
+    while len(data) % 4:
+        data += b"\0"
+    data += np.array(backoff, "<f4").tobytes() + np.array(finals, "<f4").tobytes()
+    data += np.array(fprobs + [0.0], "<f4").tobytes()
+    with open(path, "wb") as fh:
+        fh.write(_fst_header("ngram", 1, n, -1, version=4) + data)
+
+
+def _read_ngram_body(d, p):
+    """Mirror of the C++ reader (model_io.cc ParseNgramBody): explicit arcs,
+    backoff arc first for every state but the root, then the futures with
+    NGramFstImpl::Transition destinations."""
+    n, nfut, nfin = struct.unpack_from("<QQQ", d, p)
+    p += 24
+
+    def bits(nbits):
+        nonlocal p
+        nw = (nbits + 63) // 64
+        w = np.frombuffer(d, "<u8", nw, p)
+        p += 8 * nw
+        return np.unpackbits(w.view(np.uint8), bitorder="little")[:nbits]
+
+    ctx, fut, fin = bits(2 * n + 1), bits(nfut + n + 1), bits(n)
+    cwords = np.frombuffer(d, "<i4", n + 1, p); p += 4 * (n + 1)
+    fwords = np.frombuffer(d, "<i4", nfut, p); p += 4 * nfut
+    # (OpenFST pads the weights to 4 bytes relative to the data block, whose
+    # preceding fields are all multiples of 4 bytes: no padding)
+    backoff = np.frombuffer(d, "<f4", n + 1, p); p += 4 * (n + 1)
+    finals = np.frombuffer(d, "<f4", nfin, p); p += 4 * nfin
+    fprob = np.frombuffer(d, "<f4", nfut + 1, p); p += 4 * (nfut + 1)
+    assert ctx[0] == 1 and ctx[1] == 0
+    parent = [-1] * n
+    first, nch = [0] * n, [0] * n
+    pos, nxt = 2, 1
+    for k in range(n):
+        first[k] = nxt
+        while ctx[pos]:
+            parent[nxt] = k
+            nxt += 1
+            nch[k] += 1
+            pos += 1
+        pos += 1
+    assert nxt == n
+    fbeg = [0] * (n + 1)
+    pos, ones = 1, 0
+    for s in range(n):
+        fbeg[s] = ones
+        while fut[pos]:
+            ones += 1
+            pos += 1
+        pos += 1
+    fbeg[n] = ones
+
+    def child(k, w):
+        lo, hi = first[k], first[k] + nch[k]
+        j = lo + int(np.searchsorted(cwords[lo:hi], w))
+        return j if j < hi and cwords[j] == w else -1
+
+    final = np.full(n, np.inf, np.float32)
+    rows, il, ol, wt, nx = [0], [], [], [], []
+    nf = 0
+    for s in range(n):
+        if fin[s]:
+            final[s] = finals[nf]
+            nf += 1
+        if s != 0:
+            il.append(0); ol.append(0); wt.append(backoff[s]); nx.append(parent[s])
+        ctxw = []
+        k = s
+        while k != 0:
+            ctxw.append(int(cwords[k]))
+            k = parent[k]
+        for i in range(fbeg[s], fbeg[s + 1]):
+            w = int(fwords[i])
+            node = child(0, w)
+            if node < 0:
+                node = 0
+            else:
+                for j in range(len(ctxw) - 1, -1, -1):
+                    if nch[node] == 0:
+                        break
+                    c = child(node, ctxw[j])
+                    if c < 0:
+                        break
+                    node = c
+            il.append(w); ol.append(w); wt.append(fprob[i]); nx.append(node)
+        rows.append(len(il))
+    return Fst(1, final, np.array(rows, np.int64), np.array(il, np.int32), np.array(ol, np.int32),
+               np.array(wt, np.float32), np.array(nx, np.int32)), p
+
+
 def _rstr(d, p):
     n = struct.unpack_from("<i", d, p)[0]
     return d[p + 4:p + 4 + n].decode(), p + 4 + n
@@ -676,7 +841,10 @@ def _read_symtab(d, p):
 
 def read_fst(path: str) -> Fst:
     d = open(path, "rb").read()
-    p = 0
+    return _parse_fst(d, 0, 0)
+
+
+def _parse_fst(d, p, depth):
     magic = struct.unpack_from("<i", d, p)[0]
     if magic != FST_MAGIC:
         raise ValueError("not an OpenFST binary file")
@@ -727,6 +895,17 @@ def read_fst(path: str) -> Fst:
         a = np.concatenate(arcl) if arcl else np.zeros(0, dtype=[("i", "<i4"), ("o", "<i4"), ("w", "<f4"), ("n", "<i4")])
         return Fst(int(start), np.array(finals, np.float32), np.array(rows, np.int64),
                    a["i"].copy(), a["o"].copy(), a["w"].copy(), a["n"].copy(), isyms, osyms)
+    if ftype == "ngram":
+        f, p = _read_ngram_body(d, p)
+        f.isyms, f.osyms = isyms, osyms
+        return f
+    if ftype == "olabel_lookahead" and depth == 0:
+        if struct.unpack_from("<i", d, p)[0] != ADDON_MAGIC:
+            raise ValueError("bad add-on header")
+        f = _parse_fst(d, p + 4, 1)
+        if f.osyms is None:
+            f.osyms = osyms
+        return f
     raise ValueError(f"unsupported fst type {ftype}")
 
 

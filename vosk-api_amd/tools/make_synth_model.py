@@ -193,6 +193,97 @@ def build_graph(rng, tids, num_base, vocab):
     return f, words
 
 
+def build_lookahead_graph(rng, tids, num_base, vocab, num_tids):
+    """Lookahead graph pair (src/model.cc:281-285): an HCLr
+    transducer (the lexicon prefix tree over the chain HMMs with optional
+    silence, every word's output label on the arc back to the word-start
+    state; one word in 25 is a homophone of an earlier word, told apart by a
+    disambiguation transition-id on its word-end arc) and a backoff trigram
+    LM in the ngram trie form (write_ngram_fst).  Returns (hclr Fst, lm
+    dict, words, disambig ids)."""
+    words = []
+    seen = {}
+    while len(words) < vocab:
+        if len(words) >= 25 and len(words) % 25 == 0:
+            pron = words[int(rng.integers(len(words)))]
+            if seen[pron] >= 3:
+                continue
+        else:
+            n = int(rng.integers(1, 6))
+            pron = tuple(int(p) for p in rng.integers(2, num_base + 1, size=n))
+            if pron in seen:
+                continue
+        seen[pron] = seen.get(pron, -1) + 1
+        words.append(pron)
+    disambig = [num_tids + 1, num_tids + 2, num_tids + 3]
+    arcs = []
+    LOOP = 0
+    n_states = [1]
+
+    def new_state():
+        n_states[0] += 1
+        return n_states[0] - 1
+
+    sil_f, sil_s = tids(0, 1)
+    s_sil = new_state()
+    arcs.append((LOOP, sil_f, 0, 0.7, s_sil))
+    arcs.append((s_sil, sil_s, 0, 0.0, s_sil))
+    arcs.append((s_sil, 0, 0, 0.0, LOOP))
+    children = {}
+    ends = []
+    for wi, pron in enumerate(words):
+        node, prev = LOOP, 0
+        for j, bph in enumerate(pron):
+            ph = position_phone(bph, j, len(pron), num_base)
+            key = (node, ph)
+            if key not in children:
+                child = new_state()
+                children[key] = child
+                f, sl = tids(prev, ph)
+                arcs.append((node, f, 0, 0.0, child))
+                arcs.append((child, sl, 0, 0.0, child))
+            node = children[key]
+            prev = ph
+        ends.append(node)
+    homophone = {}
+    for wi, node in enumerate(ends):
+        k = homophone.get(node, 0)
+        homophone[node] = k + 1
+        arcs.append((node, disambig[k - 1] if k else 0, wi + 1, 0.0, LOOP))
+    S = n_states[0]
+    arcs.sort(key=lambda a: a[0])
+    row = np.zeros(S + 1, np.int64)
+    np.add.at(row, np.array([a[0] for a in arcs], np.int64) + 1, 1)
+    row = np.cumsum(row)
+    final = np.full(S, np.inf, np.float32)
+    final[LOOP] = 0.0
+    hclr = kf.Fst(LOOP, final, row,
+                  np.array([a[1] for a in arcs], np.int32), np.array([a[2] for a in arcs], np.int32),
+                  np.array([a[3] for a in arcs], np.float32), np.array([a[4] for a in arcs], np.int32))
+    # backoff trigram: unigram root over the vocabulary, sentence start,
+    # bigram histories, trigram histories under some of them
+    V = len(words)
+    ranks = rng.permutation(V) + 1
+    p = 1.0 / ranks
+    p /= p.sum()
+    uni = -np.log(p)
+
+    def fut(nw):
+        ws = rng.choice(V, size=min(nw, V), replace=False) + 1
+        return {int(w): float(uni[w - 1] * rng.uniform(0.3, 0.9)) for w in ws}
+
+    lm = {(): {"fut": {w + 1: float(uni[w]) for w in range(V)}, "final": 4.0},
+          (0,): {"fut": fut(30), "backoff": 0.6, "final": None}}
+    big = [int(w) for w in rng.choice(V, size=min(40, V), replace=False) + 1]
+    for h in big:
+        lm[(h,)] = {"fut": fut(12), "backoff": float(rng.uniform(0.3, 1.5)),
+                    "final": float(rng.uniform(1.0, 4.0)) if rng.random() < 0.4 else None}
+    for h in big[:12]:
+        for u in [0] + [int(x) for x in rng.choice(big, size=2, replace=False)]:
+            lm[(h, u)] = {"fut": fut(6), "backoff": float(rng.uniform(0.2, 1.0)), "final": None}
+    return hclr, lm, words, disambig
+
+
 # ----------------------------------------------------------------------------
 # nnet3
 # ----------------------------------------------------------------------------
@@ -395,9 +486,11 @@ def calibrate(nn, feats, llh_std, ivec=None):
 
 
 def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_std=3.0,
-               ivector_dim=40, frontend="mfcc", global_cmvn=False):
+               ivector_dim=40, frontend="mfcc", global_cmvn=False, graph="hclg"):
     """frontend: "mfcc" (conf/mfcc.conf) or "fbank" (conf/fbank.conf);
-    global_cmvn: write am/global_cmvn.stats (online CMVN on the nnet input)."""
+    global_cmvn: write am/global_cmvn.stats (online CMVN on the nnet input);
+    graph: "hclg" (graph/HCLG.fst) or "lookahead" (graph/HCLr.fst +
+    graph/Gr.fst + graph/disambig_tid.int, no HCLG)."""
     rng = np.random.default_rng(seed)
     os.makedirs(os.path.join(out_dir, "am"), exist_ok=True)
     os.makedirs(os.path.join(out_dir, "conf"), exist_ok=True)
@@ -413,7 +506,10 @@ def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_st
     # silence + 4 word-position variants of each of the other base phones
     num_pos_phones = 1 + 4 * (num_phones - 1)
     tm, tids = build_transition_model(rng, num_pos_phones, num_pdfs)
-    fst, words = build_graph(rng, tids, num_phones, vocab)
+    if graph == "lookahead":
+        fst, lm, words, disambig = build_lookahead_graph(rng, tids, num_phones, vocab, tm.num_tids)
+    else:
+        fst, words = build_graph(rng, tids, num_phones, vocab)
     nn = build_nnet(rng, num_pdfs, mo, ivector_dim)
     feats = nk.features(load_test_wav(), mo)
     nnet_feats = feats
@@ -431,7 +527,13 @@ def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_st
         ivec = im.extract(feats, [feats.shape[0] - 1])[-1]
     calibrate(nn, nnet_feats, llh_std, ivec)
     kf.write_final_mdl(os.path.join(out_dir, "am", "final.mdl"), tm, nn)
-    kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), fst)
+    if graph == "lookahead":
+        kf.write_lookahead_fst(os.path.join(out_dir, "graph", "HCLr.fst"), fst)
+        kf.write_ngram_fst(os.path.join(out_dir, "graph", "Gr.fst"), lm)
+        with open(os.path.join(out_dir, "graph", "disambig_tid.int"), "w") as f:
+            f.write("".join(f"{d}\n" for d in disambig))
+    else:
+        kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), fst)
     with open(os.path.join(out_dir, "graph", "words.txt"), "w") as f:
         f.write("<eps> 0\n")
         for i, _ in enumerate(words):
@@ -444,7 +546,7 @@ def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_st
     with open(os.path.join(out_dir, "README"), "w") as f:
         f.write(f"synthetic vosk-api_amd model seed={seed} vocab={vocab} pdfs={num_pdfs} "
                 f"phones={num_pos_phones} ivector_dim={ivector_dim} frontend={frontend} "
-                f"global_cmvn={int(global_cmvn)} states={fst.num_states} "
+                f"global_cmvn={int(global_cmvn)} graph={graph} states={fst.num_states} "
                 f"arcs={fst.num_arcs}\n")
     return out_dir
 
@@ -455,8 +557,9 @@ def main():
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--vocab", type=int, default=3000)
     ap.add_argument("--pdfs", type=int, default=2000)
+    ap.add_argument("--graph", choices=("hclg", "lookahead"), default="hclg")
     a = ap.parse_args()
-    make_model(a.out, a.seed, a.vocab, a.pdfs)
+    make_model(a.out, a.seed, a.vocab, a.pdfs, graph=a.graph)
     print(open(os.path.join(a.out, "README")).read().strip())
 
 
