@@ -34,6 +34,11 @@ static int padded_length(const orc_mfcc_opts* o) {
 
 int orc_mfcc_num_frames(const orc_mfcc_opts* o, long n) {
   int L = frame_length(o), S = frame_shift(o);
+  if (!o->snip_edges) { /* FeatureWindow NumFrames(flush=false), snip_edges=false */
+    long nf = (n + S / 2) / S, end = (nf - 1) * S + S / 2 - L / 2 + L;
+    while (nf > 0 && end > n) { nf--; end -= S; }
+    return (int)nf;
+  }
   if (n < L) return 0;
   return (int)(1 + (n - L) / S);
 }
@@ -553,8 +558,13 @@ int orc_mfcc(const orc_mfcc_opts* o, const float* wave, long n, float* out) {
   float* mel = (float*)malloc(sizeof(float) * nb);
 
   for (int f = 0; f < nf; f++) {
-    const float* src = wave + (long)f * S;
-    for (int i = 0; i < L; i++) x[i] = src[i];
+    const long s0 = (long)f * S + (o->snip_edges ? 0 : S / 2 - L / 2);
+    for (int i = 0; i < L; i++) {
+      long k = s0 + i;
+      if (k < 0) k = -k - 1; /* ExtractWindow reflection */
+      if (k >= n) k = 2 * n - 1 - k;
+      x[i] = wave[k];
+    }
     if (o->remove_dc_offset) {
       float sum = 0.0f;
       for (int i = 0; i < L; i++) sum = sum + x[i];
@@ -1142,4 +1152,84 @@ int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const or
   free(d.key); free(d.prevtok); free(d.pos); free(d.inq); free(d.toks); free(d.arena);
   free(cur_state); free(cur_cost); free(cur_idx); free(tmp);
   return end >= 0 ? 0 : -1;
+}
+
+/* ===================================================================== */
+/* Speaker x-vectors (src/recognizer.cc:356-419, Kaldi                    */
+/* feat/feature-functions.cc SlidingWindowCmnInternal,                    */
+/* nnet3/nnet-general-component.cc Statistics{Extraction,Pooling}).       */
+/* ===================================================================== */
+void orc_sliding_cmn(const float* feats, int T, int D, int window, float* out) {
+  for (int d = 0; d < D; d++) {
+    double sum = 0.0;
+    int last_start = -1, last_end = -1;
+    for (int t = 0; t < T; t++) {
+      int ws = t - window / 2, we = ws + window;
+      if (ws < 0) { we -= ws; ws = 0; }
+      if (we > T) { ws -= we - T; we = T; if (ws < 0) ws = 0; }
+      if (last_start < 0) {
+        for (int u = ws; u < we; u++) sum = sum + (double)feats[(size_t)u * D + d];
+      } else {
+        if (ws > last_start) sum = sum - (double)feats[(size_t)last_start * D + d];
+        if (we > last_end) sum = sum + (double)feats[(size_t)last_end * D + d];
+      }
+      last_start = ws;
+      last_end = we;
+      const double alpha = -1.0 / (double)(we - ws);
+      out[(size_t)t * D + d] = (float)((double)feats[(size_t)t * D + d] + alpha * sum);
+    }
+  }
+}
+
+int orc_xvector_tail(const orc_xvec* x, const float* rows, int ld, int r0, int r1, float* out) {
+  const int D = x->stats_dim, n = r1 - r0 + 1;
+  if (n <= 0) return -1;
+  int maxd = x->nlog + 2 * D;
+  for (int i = 0; i < x->nops; i++) if (x->out_dim[i] > maxd) maxd = x->out_dim[i];
+  float* a = (float*)calloc((size_t)maxd, sizeof(float));
+  float* b = (float*)calloc((size_t)maxd, sizeof(float));
+  for (int k = 0; k < x->nlog; k++) a[k] = (float)log((double)n);
+  for (int d = 0; d < D; d++) {
+    double s = 0.0, s2 = 0.0;
+    for (int t = 0; t < n; t++) {
+      const double v = (double)rows[(size_t)(r0 + t) * ld + d];
+      s = s + v;
+      s2 = s2 + v * v;
+    }
+    const double mean = s / (double)n;
+    a[x->nlog + d] = (float)mean;
+    if (x->stddevs) {
+      double var = s2 / (double)n - mean * mean;
+      if (var < (double)x->var_floor) var = (double)x->var_floor;
+      a[x->nlog + D + d] = (float)sqrt(var);
+    }
+  }
+  for (int i = 0; i < x->nops; i++) {
+    const int K = x->in_dim[i], N = x->out_dim[i];
+    const float* W = x->params + x->w_off[i];
+    const float* B = x->b_off[i] >= 0 ? x->params + x->b_off[i] : NULL;
+    for (int o = 0; o < N; o++) {
+      if (x->kind[i] == 1) {
+        const float v = canon_dot(W + (size_t)o * K, a, K);
+        b[o] = B ? v + B[o] : v;
+      } else if (x->kind[i] == 2) {
+        b[o] = a[o] < 0.0f ? 0.0f : a[o];
+      } else {
+        b[o] = a[o] * W[o] + B[o];
+      }
+    }
+    float* t = a; a = b; b = t;
+  }
+  const int E = x->embed_dim, R = x->out_dim_final;
+  float* xc = (float*)malloc(sizeof(float) * E);
+  for (int e = 0; e < E; e++) xc[e] = a[e] - x->mean[e];
+  for (int r = 0; r < R; r++) out[r] = canon_dot(x->transform + (size_t)r * E, xc, E);
+  float ss = 0.0f;
+  for (int r = 0; r < R; r++) ss = ss + out[r] * out[r];
+  const float norm = sqrtf(ss);
+  const float ratio = (float)((double)norm / sqrt((double)R));
+  const float scale = (float)(1.0 / (double)ratio);
+  for (int r = 0; r < R; r++) out[r] = out[r] * scale;
+  free(a); free(b); free(xc);
+  return 0;
 }

@@ -34,6 +34,10 @@ typedef struct {
   /* fbank front end (Kaldi feat/feature-fbank.cc, src/model.cc:222-225):
      log mel energies, log energy first when use_energy */
   int fbank, use_log_fbank, use_power;
+  /* snip_edges = 0 (the speaker front end, Kaldi FeatureWindow): frame t
+     starts at t*shift + shift/2 - length/2, samples before 0 are reflected,
+     and the online (not flushed) frame count applies */
+  int snip_edges;
 } orc_mfcc_opts;
 
 /* feature dimension of the front end: num_ceps (MFCC) or num_bins (+1) (fbank) */
@@ -82,6 +86,30 @@ typedef struct {
 
 /* out: [ceil(T/fss)][dim(output)] */
 int orc_nnet_forward(const orc_net* net, const float* feats, int T, float* out);
+
+/* ---------------- speaker x-vectors (src/recognizer.cc:356-419) -------------
+   Sliding-window CMN (Kaldi SlidingWindowCmn, centered, means only, in
+   double: out = x + (-1 / frames) * window sum), then -- after the
+   frame-level nnet (orc_nnet_forward up to the statistics input) --
+   orc_xvector_tail: statistics pooling over rows [r0, r1] (double sums in row
+   order; [log count x nlog], mean, stddev = sqrt(max(floor, E[x^2] -
+   mean^2))), the head ops (1 affine W [out][in] + b in the canonical order,
+   2 ReLU, 3 x * scale + offset), x - mean, transform rows (canonical order),
+   and the scale to norm sqrt(R) (sequential float sum of squares; ratio and
+   1/ratio through double).  Shared bit-for-bit with kernels.hip xvec_*. */
+void orc_sliding_cmn(const float* feats, int T, int D, int window, float* out);
+typedef struct {
+  int stats_dim, nlog, stddevs;
+  float var_floor;
+  int nops;
+  const int* kind; const int* in_dim; const int* out_dim;
+  const int64_t* w_off; const int64_t* b_off;  /* into params; b_off -1: no bias */
+  const float* params;
+  int embed_dim, out_dim_final;
+  const float* mean;       /* [embed_dim] */
+  const float* transform;  /* [out_dim_final][embed_dim] */
+} orc_xvec;
+int orc_xvector_tail(const orc_xvec* x, const float* rows, int ld, int r0, int r1, float* out);
 
 /* ---------------- online i-vector extraction ----------------------------------
    Kaldi online2/online-ivector-feature.cc (OnlineIvectorFeature with

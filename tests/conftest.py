@@ -85,6 +85,21 @@ def synth_lookahead():
 
 
 @pytest.fixture(scope="session")
+def synth_spk():
+    """Synthetic x-vector speaker model (mfcc.conf, final.ext.raw, mean.vec,
+    transform.mat)."""
+    import make_synth_model as msm
+    path = os.path.join(MODEL_CACHE, f"synth_spk_{SYNTH_VERSION}")
+    if not os.path.exists(os.path.join(path, "README")):
+        tmp = path + f".tmp{os.getpid()}"
+        shutil.rmtree(tmp, ignore_errors=True)
+        msm.make_spk_model(tmp)
+        shutil.rmtree(path, ignore_errors=True)
+        os.rename(tmp, path)
+    return path
+
+
+@pytest.fixture(scope="session")
 def test_wave():
     w = wave.open(os.path.join(REPO, "tests", "golden", "test.wav"), "rb")
     return np.frombuffer(w.readframes(w.getnframes()), "<i2").astype(np.float32)

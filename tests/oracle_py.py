@@ -81,7 +81,7 @@ class OrcMfccOpts(C.Structure):
                 ("num_bins", C.c_int), ("num_ceps", C.c_int), ("use_energy", C.c_int),
                 ("remove_dc_offset", C.c_int), ("window_type", C.c_int),
                 ("round_to_power_of_two", C.c_int), ("fbank", C.c_int),
-                ("use_log_fbank", C.c_int), ("use_power", C.c_int)]
+                ("use_log_fbank", C.c_int), ("use_power", C.c_int), ("snip_edges", C.c_int)]
 
 
 def mfcc_opts(conf: dict, fbank: bool = False) -> OrcMfccOpts:
@@ -90,7 +90,8 @@ def mfcc_opts(conf: dict, fbank: bool = False) -> OrcMfccOpts:
     return OrcMfccOpts(o.samp_freq, o.frame_shift_ms, o.frame_length_ms, o.preemph,
                        o.low_freq, o.high_freq, o.cepstral_lifter, o.blackman_coeff,
                        o.num_bins, o.num_ceps, int(o.use_energy), int(o.remove_dc), wt,
-                       int(o.round_pow2), int(fbank), int(o.use_log_fbank), int(o.use_power))
+                       int(o.round_pow2), int(fbank), int(o.use_log_fbank), int(o.use_power),
+                       int(o.snip_edges))
 
 
 def online_cmvn(feats, gstats, window=600, global_frames=200) -> np.ndarray:

@@ -194,6 +194,87 @@ int Engine::NumFramesFor(long long samples) const {
   return (int)(1 + (samples - L) / S);
 }
 
+// MFCC / fbank tables (float arithmetic as Kaldi MelBanks /
+// FeatureWindowFunction / ComputeDctMatrix) for mfcc_kernel.  snip_edges
+// false (the speaker front end) starts frame t at t*shift + shift/2 -
+// length/2 and reflects samples before the start (Kaldi ExtractWindow).
+MfccTables BuildMfccTables(const MfccOptions& o) {
+  MfccTables t;
+  if (o.htk_compat) VAMD_ERR("htk-compat is not supported");
+  const int L = o.WindowSize(), N = o.PaddedWindowSize();
+  if (N > 512 || (N & (N - 1))) VAMD_ERR("FFT size " << N << " unsupported (power of two <= 512)");
+  if (o.num_bins > 64 || o.num_ceps > 64) VAMD_ERR("num-mel-bins / num-ceps must be <= 64");
+  std::vector<float> win(L);
+  double a = 2.0 * M_PI / (L - 1);
+  for (int i = 0; i < L; i++) {
+    double c = cos(a * i), w;
+    if (o.window_type == "povey") w = pow(0.5 - 0.5 * c, 0.85);
+    else if (o.window_type == "hamming") w = 0.54 - 0.46 * c;
+    else if (o.window_type == "hanning") w = 0.5 - 0.5 * c;
+    else if (o.window_type == "rectangular") w = 1.0;
+    else if (o.window_type == "blackman")
+      w = o.blackman_coeff - 0.5 * c + (0.5 - o.blackman_coeff) * cos(2 * a * i);
+    else VAMD_ERR("unsupported window type " << o.window_type);
+    win[i] = (float)w;
+  }
+  const int nfft = N / 2, nb = o.num_bins, nc = o.num_ceps;
+  std::vector<float> melw((size_t)nb * nfft, 0.0f);
+  std::vector<int> first(nb, -1), last(nb, -1);
+  float nyq = 0.5f * o.samp_freq;
+  float hi = o.high_freq > 0.0f ? o.high_freq : nyq + o.high_freq;
+  float width = o.samp_freq / (float)N;
+  float ml = MelScale(o.low_freq), mh = MelScale(hi);
+  float delta = (mh - ml) / (float)(nb + 1);
+  for (int b = 0; b < nb; b++) {
+    float left = ml + (float)b * delta, center = ml + (float)(b + 1) * delta,
+          right = ml + (float)(b + 2) * delta;
+    for (int i = 0; i < nfft; i++) {
+      float mel = MelScale(width * (float)i);
+      if (mel > left && mel < right) {
+        float w = mel <= center ? (mel - left) / (center - left) : (right - mel) / (right - center);
+        melw[(size_t)b * nfft + i] = w;
+        if (first[b] < 0) first[b] = i;
+        last[b] = i;
+      }
+    }
+  }
+  std::vector<float> dct((size_t)nc * nb);
+  float norm0 = (float)sqrt(1.0 / (double)nb), norm = (float)sqrt(2.0 / (double)nb);
+  for (int j = 0; j < nb; j++) dct[j] = norm0;
+  for (int k = 1; k < nc; k++)
+    for (int j = 0; j < nb; j++) dct[(size_t)k * nb + j] = (float)((double)norm * cos(M_PI / nb * (j + 0.5) * k));
+  std::vector<float> lift(nc);
+  for (int i = 0; i < nc; i++) {
+    double q = o.cepstral_lifter;
+    lift[i] = q != 0.0 ? (float)(1.0 + 0.5 * q * sin(M_PI * i / q)) : 1.0f;
+  }
+  std::vector<float> twr(N / 2), twi(N / 2);
+  for (int k = 0; k < N / 2; k++) {
+    twr[k] = (float)cos(2.0 * M_PI * k / N);
+    twi[k] = (float)(-sin(2.0 * M_PI * k / N));
+  }
+  int log2n = 0;
+  while ((1 << log2n) < N) log2n++;
+  t.dev.frame_length = L;
+  t.dev.frame_shift = o.WindowShift();
+  t.dev.first_offset = o.snip_edges ? 0 : o.WindowShift() / 2 - L / 2;
+  t.dev.padded = N;
+  t.dev.log2n = log2n;
+  t.dev.num_bins = nb;
+  t.dev.num_ceps = nc;
+  t.dev.nfft = nfft;
+  t.dev.use_energy = o.use_energy ? 1 : 0;
+  t.dev.remove_dc = o.remove_dc_offset ? 1 : 0;
+  t.dev.preemph = o.preemph_coeff;
+  t.dev.fbank = o.fbank ? 1 : 0;
+  t.dev.use_log_fbank = o.use_log_fbank ? 1 : 0;
+  t.dev.use_power = o.use_power ? 1 : 0;
+  t.dev.feat_dim = o.FeatDim();
+  t.win = std::move(win); t.melw = std::move(melw); t.first = std::move(first); t.last = std::move(last);
+  t.dct = std::move(dct); t.lift = std::move(lift); t.twr = std::move(twr); t.twi = std::move(twi);
+  return t;
+}
+
 Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : md_(md), cfg_(cfg) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -217,85 +298,20 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   if (o.dither != 0.0f)
     VAMD_WARN("dither=" << o.dither << " ignored: the pipeline is deterministic (dither 0)");
   if (o.htk_compat || !o.snip_edges) VAMD_ERR("htk-compat / snip-edges=false are not supported");
-  const int L = o.WindowSize(), N = o.PaddedWindowSize();
-  if (N > 512 || (N & (N - 1))) VAMD_ERR("FFT size " << N << " unsupported (power of two <= 512)");
-  if (o.num_bins > 64 || o.num_ceps > 64) VAMD_ERR("num-mel-bins / num-ceps must be <= 64");
+  const int L = o.WindowSize();
   if (plan_.input_dim != o.FeatDim())
     VAMD_ERR("nnet input dim " << plan_.input_dim << " != feature dim " << o.FeatDim());
   {
-    std::vector<float> win(L);
-    double a = 2.0 * M_PI / (L - 1);
-    for (int i = 0; i < L; i++) {
-      double c = cos(a * i), w;
-      if (o.window_type == "povey") w = pow(0.5 - 0.5 * c, 0.85);
-      else if (o.window_type == "hamming") w = 0.54 - 0.46 * c;
-      else if (o.window_type == "hanning") w = 0.5 - 0.5 * c;
-      else if (o.window_type == "rectangular") w = 1.0;
-      else if (o.window_type == "blackman")
-        w = o.blackman_coeff - 0.5 * c + (0.5 - o.blackman_coeff) * cos(2 * a * i);
-      else VAMD_ERR("unsupported window type " << o.window_type);
-      win[i] = (float)w;
-    }
-    const int nfft = N / 2, nb = o.num_bins, nc = o.num_ceps;
-    std::vector<float> melw((size_t)nb * nfft, 0.0f);
-    std::vector<int> first(nb, -1), last(nb, -1);
-    float nyq = 0.5f * o.samp_freq;
-    float hi = o.high_freq > 0.0f ? o.high_freq : nyq + o.high_freq;
-    float width = o.samp_freq / (float)N;
-    float ml = MelScale(o.low_freq), mh = MelScale(hi);
-    float delta = (mh - ml) / (float)(nb + 1);
-    for (int b = 0; b < nb; b++) {
-      float left = ml + (float)b * delta, center = ml + (float)(b + 1) * delta,
-            right = ml + (float)(b + 2) * delta;
-      for (int i = 0; i < nfft; i++) {
-        float mel = MelScale(width * (float)i);
-        if (mel > left && mel < right) {
-          float w = mel <= center ? (mel - left) / (center - left) : (right - mel) / (right - center);
-          melw[(size_t)b * nfft + i] = w;
-          if (first[b] < 0) first[b] = i;
-          last[b] = i;
-        }
-      }
-    }
-    std::vector<float> dct((size_t)nc * nb);
-    float norm0 = (float)sqrt(1.0 / (double)nb), norm = (float)sqrt(2.0 / (double)nb);
-    for (int j = 0; j < nb; j++) dct[j] = norm0;
-    for (int k = 1; k < nc; k++)
-      for (int j = 0; j < nb; j++) dct[(size_t)k * nb + j] = (float)((double)norm * cos(M_PI / nb * (j + 0.5) * k));
-    std::vector<float> lift(nc);
-    for (int i = 0; i < nc; i++) {
-      double q = o.cepstral_lifter;
-      lift[i] = q != 0.0 ? (float)(1.0 + 0.5 * q * sin(M_PI * i / q)) : 1.0f;
-    }
-    std::vector<float> twr(N / 2), twi(N / 2);
-    for (int k = 0; k < N / 2; k++) {
-      twr[k] = (float)cos(2.0 * M_PI * k / N);
-      twi[k] = (float)(-sin(2.0 * M_PI * k / N));
-    }
-    int log2n = 0;
-    while ((1 << log2n) < N) log2n++;
-    mfcc_.frame_length = L;
-    mfcc_.frame_shift = o.WindowShift();
-    mfcc_.padded = N;
-    mfcc_.log2n = log2n;
-    mfcc_.num_bins = nb;
-    mfcc_.num_ceps = nc;
-    mfcc_.nfft = nfft;
-    mfcc_.use_energy = o.use_energy ? 1 : 0;
-    mfcc_.remove_dc = o.remove_dc_offset ? 1 : 0;
-    mfcc_.preemph = o.preemph_coeff;
-    mfcc_.window = Upload(win);
-    mfcc_.melw = Upload(melw);
-    mfcc_.mel_first = Upload(first);
-    mfcc_.mel_last = Upload(last);
-    mfcc_.dct = Upload(dct);
-    mfcc_.lifter = Upload(lift);
-    mfcc_.twr = Upload(twr);
-    mfcc_.twi = Upload(twi);
-    mfcc_.fbank = o.fbank ? 1 : 0;
-    mfcc_.use_log_fbank = o.use_log_fbank ? 1 : 0;
-    mfcc_.use_power = o.use_power ? 1 : 0;
-    mfcc_.feat_dim = o.FeatDim();
+    MfccTables t = BuildMfccTables(o);
+    mfcc_ = t.dev;
+    mfcc_.window = Upload(t.win);
+    mfcc_.melw = Upload(t.melw);
+    mfcc_.mel_first = Upload(t.first);
+    mfcc_.mel_last = Upload(t.last);
+    mfcc_.dct = Upload(t.dct);
+    mfcc_.lifter = Upload(t.lift);
+    mfcc_.twr = Upload(t.twr);
+    mfcc_.twi = Upload(t.twi);
   }
 
   // ---- rings

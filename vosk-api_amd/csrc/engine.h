@@ -60,6 +60,14 @@ struct ModelData {
   void LoadBatchLayout(const std::string& dir);  // src/batch_model.cc:23-54
 };
 
+// host tables of the MFCC / fbank front end (mfcc_kernel); pointers in dev unset
+struct MfccTables {
+  MfccDev dev{};
+  std::vector<float> win, melw, dct, lift, twr, twi;
+  std::vector<int> first, last;
+};
+MfccTables BuildMfccTables(const MfccOptions& o);
+
 struct EngineConfig {
   int frames_per_chunk = 21;
   int max_slots = 64;

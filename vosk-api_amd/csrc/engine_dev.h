@@ -68,6 +68,8 @@ struct MfccDev {
   const float* twr;      // [padded/2]
   const float* twi;      // [padded/2]
   int fbank, use_log_fbank, use_power, feat_dim;
+  int first_offset;      // frame t starts at t*frame_shift + first_offset (snip-edges=false:
+                         // shift/2 - length/2; samples before 0 are reflected)
   float* out;            // feature ring [ring][slots][feat_dim]
 };
 

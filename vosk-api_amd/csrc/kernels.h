@@ -29,6 +29,16 @@ void LdsHashSelfTest(int n, int blocks, int* out);  // dev (tools/gemm_bench)
 int DecoderLdsFrameTokens();  // default LDS frame-construction threshold
 void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s);
 void LaunchTraceback(const TraceArgs& a, int n, hipStream_t s);
+// speaker x-vectors (xvector.h): selection + sliding CMN, statistics
+// pooling, head ops, whitening
+void LaunchXvecCmn(const float* feats, int feat_mask, int D, const int* rows, int n, int window,
+                   float* out, int out_mask, int out_dim, hipStream_t s);
+void LaunchXvecPool(const float* rows, int ld, int r0, int n, int D, int nlog, int stddevs,
+                    float var_floor, float* out, hipStream_t s);
+void LaunchXvecAffine(const float* W, const float* b, const float* x, int K, int N, int kind,
+                      float* y, hipStream_t s);
+void LaunchXvecFinish(const float* x, const float* mean, int E, const float* T, int R, float* out,
+                      hipStream_t s);
 void LaunchInitKeys(unsigned long long* key, int* stamp, long long n_states_total, hipStream_t s);
 
 }  // namespace vamd

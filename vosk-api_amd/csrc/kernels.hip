@@ -153,9 +153,12 @@ __global__ __launch_bounds__(256) void mfcc_kernel(MfccDev m, const MfccJob* job
   float* re = RE[w];
   float* im = IM[w];
   const float* src = ring + (size_t)slot * ring_len;
-  const long long s0 = (long long)frame * m.frame_shift;
-  for (int i = lane; i < L; i += 64)
-    x[i] = valid ? src[(s0 + i) & (ring_len - 1)] : 0.0f;
+  const long long s0 = (long long)frame * m.frame_shift + m.first_offset;
+  for (int i = lane; i < L; i += 64) {
+    long long k = s0 + i;
+    if (k < 0) k = -k - 1;  // Kaldi ExtractWindow reflection (snip-edges=false)
+    x[i] = valid ? src[k & (ring_len - 1)] : 0.0f;
+  }
   __syncthreads();
   if (lane == 0) {
     float c = 0.0f;
@@ -2317,6 +2320,150 @@ void LaunchInitKeys(unsigned long long* key, int* stamp, long long n, hipStream_
   long long blocks = (n + 255) / 256;
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(init_keys_kernel, dim3((unsigned)blocks), dim3(256), 0, s, key, stamp, n);
+}
+
+// ===========================================================================
+// speaker x-vectors (xvector.h)
+// ===========================================================================
+// Kaldi SlidingWindowCmn (feat/feature-functions.cc SlidingWindowCmnInternal
+// [K]) with the reference's options (centered 300-frame window, means only,
+// src/recognizer.cc:393-397), in double, over the selected frames: one lane
+// per feature dim walks the frames with the running window sum; out = x +
+// (-1 / frames) * sum.  Columns past D (input padding) are zero.
+__global__ void xvec_cmn_kernel(const float* feats, int feat_mask, int D, const int* rows, int n,
+                                int window, float* out, int out_mask, int out_dim) {
+  const int d = threadIdx.x;
+  if (d >= out_dim) return;
+  if (d >= D) {
+    for (int t = 0; t < n; t++) out[(size_t)(t & out_mask) * out_dim + d] = 0.0f;
+    return;
+  }
+  double sum = 0.0;
+  int last_start = -1, last_end = -1;
+  for (int t = 0; t < n; t++) {
+    int ws = t - window / 2, we = ws + window;
+    if (ws < 0) { we -= ws; ws = 0; }
+    if (we > n) {
+      ws -= we - n;
+      we = n;
+      if (ws < 0) ws = 0;
+    }
+    if (last_start < 0) {
+      for (int u = ws; u < we; u++) sum = sum + (double)feats[(size_t)(rows[u] & feat_mask) * D + d];
+    } else {
+      if (ws > last_start) sum = sum - (double)feats[(size_t)(rows[last_start] & feat_mask) * D + d];
+      if (we > last_end) sum = sum + (double)feats[(size_t)(rows[last_end] & feat_mask) * D + d];
+    }
+    last_start = ws;
+    last_end = we;
+    const double alpha = -1.0 / (double)(we - ws);
+    const double x = (double)feats[(size_t)(rows[t] & feat_mask) * D + d];
+    out[(size_t)(t & out_mask) * out_dim + d] = (float)(x + alpha * sum);
+  }
+}
+
+// statistics extraction + pooling (StatisticsExtractionComponent /
+// StatisticsPoolingComponent, nnet3/nnet-general-component.cc [K]) of rows
+// [r0, r0 + n): [log count x nlog], mean, stddev = sqrt(max(floor, E[x^2] -
+// mean^2)); double sums in row order
+__global__ void xvec_pool_kernel(const float* rows, int ld, int r0, int n, int D, int nlog,
+                                 int stddevs, float var_floor, float* out) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d < nlog) out[d] = (float)log((double)n);
+  if (d >= D) return;
+  double s = 0.0, s2 = 0.0;
+  for (int t = 0; t < n; t++) {
+    const double x = (double)rows[(size_t)(r0 + t) * ld + d];
+    s = s + x;
+    s2 = s2 + x * x;
+  }
+  const double mean = s / (double)n;
+  out[nlog + d] = (float)mean;
+  if (stddevs) {
+    double var = s2 / (double)n - mean * mean;
+    if (var < (double)var_floor) var = (double)var_floor;
+    out[nlog + D + d] = (float)sqrt(var);
+  }
+}
+
+// one row of an affine map in the GEMM kernels' canonical order (nnet_plan.h
+// GemmKSlices; groups of eight walked 0,4,1,5,2,6,3,7), oracle canon_dot
+__device__ float xvec_canon_dot(const float* w, const float* x, int K) {
+  const int ns = (K >= 512 && K % 256 == 0) ? K / 256 : 1, kw = K / ns;  // GemmKSlices
+  float a = 0.0f;
+  for (int z = 0; z < ns; z++) {
+    float p = 0.0f;
+    const int ke = (z + 1) * kw;
+    for (int kg = z * kw; kg < ke; kg += 8)
+      for (int i = 0; i < 8 && kg + i < ke; i++) {
+        const int k = kg + 8 <= ke ? kg + ((i & 1) << 2) + (i >> 1) : kg + i;
+        p = __builtin_fmaf(x[k], w[k], p);
+      }
+    a = z == 0 ? p : a + p;
+  }
+  return a;
+}
+
+// head op of the pooled statistics: 1 affine (+ bias when b), 2 ReLU,
+// 3 x * scale + offset
+__global__ void xvec_affine_kernel(const float* W, const float* b, const float* x, int K, int N,
+                                   int kind, float* y) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  if (kind == 1) {
+    const float a = xvec_canon_dot(W + (size_t)n * K, x, K);
+    y[n] = b ? a + b[n] : a;
+  } else if (kind == 2) {
+    y[n] = x[n] < 0.0f ? 0.0f : x[n];
+  } else {
+    y[n] = x[n] * W[n] + b[n];
+  }
+}
+
+// whitening and length normalisation (src/recognizer.cc:406-416): x - mean,
+// transform rows (canonical order), norm = sqrt of the sequential float sum
+// of squares, ratio = norm / sqrt(R) and scale 1/ratio rounded through double
+__global__ __launch_bounds__(256) void xvec_finish_kernel(const float* x, const float* mean, int E,
+                                                          const float* T, int R, float* out) {
+  __shared__ float xc[1024];
+  __shared__ float scale;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) xc[e] = x[e] - mean[e];
+  __syncthreads();
+  for (int r = threadIdx.x; r < R; r += blockDim.x) out[r] = xvec_canon_dot(T + (size_t)r * E, xc, E);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float ss = 0.0f;
+    for (int r = 0; r < R; r++) ss = ss + out[r] * out[r];
+    const float norm = sqrtf(ss);
+    const float ratio = (float)((double)norm / sqrt((double)R));
+    scale = (float)(1.0 / (double)ratio);
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < R; r += blockDim.x) out[r] = out[r] * scale;
+}
+
+void LaunchXvecCmn(const float* feats, int feat_mask, int D, const int* rows, int n, int window,
+                   float* out, int out_mask, int out_dim, hipStream_t s) {
+  hipLaunchKernelGGL(xvec_cmn_kernel, dim3(1), dim3((out_dim + 63) / 64 * 64), 0, s, feats,
+                     feat_mask, D, rows, n, window, out, out_mask, out_dim);
+}
+
+void LaunchXvecPool(const float* rows, int ld, int r0, int n, int D, int nlog, int stddevs,
+                    float var_floor, float* out, hipStream_t s) {
+  const int threads = D > nlog ? D : nlog;
+  hipLaunchKernelGGL(xvec_pool_kernel, dim3((threads + 255) / 256), dim3(256), 0, s, rows, ld, r0,
+                     n, D, nlog, stddevs, var_floor, out);
+}
+
+void LaunchXvecAffine(const float* W, const float* b, const float* x, int K, int N, int kind,
+                      float* y, hipStream_t s) {
+  hipLaunchKernelGGL(xvec_affine_kernel, dim3((N + 255) / 256), dim3(256), 0, s, W, b, x, K, N,
+                     kind, y);
+}
+
+void LaunchXvecFinish(const float* x, const float* mean, int E, const float* T, int R, float* out,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(xvec_finish_kernel, dim3(1), dim3(256), 0, s, x, mean, E, T, R, out);
 }
 
 }  // namespace vamd

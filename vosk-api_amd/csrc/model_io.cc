@@ -338,6 +338,11 @@ const std::map<std::string, FieldKind>& FieldKinds() {
       {"<Dim>", FK_I}, {"<BlockDim>", FK_I}, {"<InputDim>", FK_I}, {"<OutputDim>", FK_I},
       {"<RankIn>", FK_I}, {"<RankOut>", FK_I}, {"<UpdatePeriod>", FK_I}, {"<TimePeriod>", FK_I},
       {"<TimeMaskMaxFrames>", FK_I},
+      // StatisticsExtractionComponent / StatisticsPoolingComponent (x-vector
+      // nnets, nnet3/nnet-general-component.cc [K]; "Varinance" is Kaldi's spelling)
+      {"<InputPeriod>", FK_I}, {"<OutputPeriod>", FK_I}, {"<IncludeVarinance>", FK_B},
+      {"<LeftContext>", FK_I}, {"<RightContext>", FK_I}, {"<NumLogCountFeatures>", FK_I},
+      {"<OutputStddevs>", FK_B}, {"<VarianceFloor>", FK_F},
       {"<IsGradient>", FK_B}, {"<TestMode>", FK_B}, {"<UseNaturalGradient>", FK_B},
       {"<Continuous>", FK_B},
       {"<BiasParams>", FK_V}, {"<StatsMean>", FK_V}, {"<StatsVar>", FK_V}, {"<ValueAvg>", FK_V},
@@ -512,6 +517,14 @@ const NnetNode& Nnet::Node(const std::string& n) const {
 }
 
 static int ComponentOutputDim(const Component& c) {
+  if (c.type == "StatisticsExtractionComponent") {  // [count, sum x (, sum x^2)]
+    const int d = c.i.at("InputDim");
+    return 1 + d * (c.b.count("IncludeVarinance") && c.b.at("IncludeVarinance") ? 2 : 1);
+  }
+  if (c.type == "StatisticsPoolingComponent") {  // [log-counts, mean (, stddev)]
+    const int n = c.i.count("NumLogCountFeatures") ? c.i.at("NumLogCountFeatures") : 0;
+    return c.i.at("InputDim") - 1 + n;
+  }
   auto m = c.m.find("LinearParams");
   if (m != c.m.end()) return m->second.rows;
   m = c.m.find("Params");
@@ -550,6 +563,8 @@ int Nnet::DescDim(const Desc& d) const {
     default: return DescDim(d.args[0]);
   }
 }
+
+void ParseNnet3(KReader& r, size_t size, Nnet* nnet);
 
 void ReadFinalMdl(const std::string& path, TransitionModel* tm, Nnet* nnet) {
   std::ifstream in(path, std::ios::binary);
@@ -612,8 +627,36 @@ void ReadFinalMdl(const std::string& path, TransitionModel* tm, Nnet* nnet) {
   r.Expect("</LogProbs>");
   r.Expect("</TransitionModel>");
   tm->num_pdfs = max_pdf + 1;
+  ParseNnet3(r, data.size(), nnet);
+}
 
-  // ---- nnet3 (nnet3/nnet-nnet.cc, nnet3/am-nnet-simple.cc [K])
+void ReadNnetRaw(const std::string& path, Nnet* nnet) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) VAMD_ERR("cannot open " << path);
+  std::string data((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+  KReader r(data);
+  ParseNnet3(r, data.size(), nnet);
+}
+
+std::vector<float> ReadKaldiVectorFloat(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) VAMD_ERR("cannot open " << path);
+  std::string d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  KReader r(d);
+  return r.Vector();
+}
+
+Matrix ReadKaldiMatrixFloat(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) VAMD_ERR("cannot open " << path);
+  std::string d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  KReader r(d);
+  return r.Mat();
+}
+
+// nnet3 (nnet3/nnet-nnet.cc, nnet3/am-nnet-simple.cc [K]): config lines,
+// components, then AmNnetSimple's context / priors when present
+void ParseNnet3(KReader& r, size_t size, Nnet* nnet) {
   r.Expect("<Nnet3>");
   r.Line();  // remainder of the token's line
   nnet->nodes.clear();
@@ -654,12 +697,12 @@ void ReadFinalMdl(const std::string& path, TransitionModel* tm, Nnet* nnet) {
     nnet->components[name] = ReadComponent(r);
   }
   r.Expect("</Nnet3>");
-  if (r.p < data.size() && r.PeekToken() == "<LeftContext>") {
+  if (r.p < size && r.PeekToken() == "<LeftContext>") {
     r.Expect("<LeftContext>");
     nnet->left_context = r.I32();
     r.Expect("<RightContext>");
     nnet->right_context = r.I32();
-    if (r.p < data.size() && r.PeekToken() == "<Priors>") {
+    if (r.p < size && r.PeekToken() == "<Priors>") {
       r.Expect("<Priors>");
       std::vector<float> pri = r.Vector();
       if (!pri.empty()) VAMD_WARN("non-empty priors ignored (chain models have none)");

@@ -145,6 +145,12 @@ struct Nnet {
 };
 
 void ReadFinalMdl(const std::string& path, TransitionModel* tm, Nnet* nnet);
+// a raw nnet3 object (Nnet::Write: "<Nnet3>" ... "</Nnet3>"), e.g. the speaker
+// model's final.ext.raw (src/spk_model.cc:23)
+void ReadNnetRaw(const std::string& path, Nnet* nnet);
+// Kaldi binary vector / matrix objects as float (mean.vec, transform.mat)
+std::vector<float> ReadKaldiVectorFloat(const std::string& path);
+Matrix ReadKaldiMatrixFloat(const std::string& path);
 
 // ---------------------------------------------------------------------------
 // Decode graph (StdArc FST) in CSR form, emitting arcs first per state.

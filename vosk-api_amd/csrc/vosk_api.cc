@@ -63,13 +63,16 @@ int vosk_model_find_word(VoskModel* model, const char* word) {
   API_CATCH(-1)
 }
 
-VoskSpkModel* vosk_spk_model_new(const char* model_path) {
-  g_last_error = "speaker (x-vector) models are not supported by this build";
-  VAMD_WARN(g_last_error << " (" << (model_path ? model_path : "") << ")");
-  return nullptr;
+VoskSpkModel* vosk_spk_model_new(const char* model_path) {  // src/vosk_api.cc:52-59
+  API_TRY
+  return (VoskSpkModel*)new SpkModel(model_path ? model_path : "");
+  API_CATCH(nullptr)
 }
 
-void vosk_spk_model_free(VoskSpkModel*) {}
+void vosk_spk_model_free(VoskSpkModel* model) {
+  if (model == nullptr) return;
+  ((SpkModel*)model)->Unref();
+}
 
 VoskRecognizer* vosk_recognizer_new(VoskModel* model, float sample_rate) {
   API_TRY
@@ -79,8 +82,7 @@ VoskRecognizer* vosk_recognizer_new(VoskModel* model, float sample_rate) {
 
 VoskRecognizer* vosk_recognizer_new_spk(VoskModel* model, float sample_rate, VoskSpkModel* spk) {
   API_TRY
-  if (spk) VAMD_WARN("speaker model ignored (x-vector path not implemented)");
-  return (VoskRecognizer*)new Recognizer((Model*)model, sample_rate);
+  return (VoskRecognizer*)new Recognizer((Model*)model, sample_rate, (SpkModel*)spk);
   API_CATCH(nullptr)
 }
 
@@ -92,6 +94,22 @@ VoskRecognizer* vosk_recognizer_new_grm(VoskModel* model, float sample_rate, con
 
 void vosk_recognizer_set_spk_model(VoskRecognizer* recognizer, VoskSpkModel* spk_model) {
   if (recognizer == nullptr || spk_model == nullptr) return;
+  API_TRY
+  ((Recognizer*)recognizer)->SetSpkModel((SpkModel*)spk_model);
+  API_CATCH_VOID
+}
+
+int vamd_spk_extract(VoskSpkModel* spk, const float* samples, long long n, int first_frame,
+                     const signed char* keep, int nkeep, float* out, int cap, int* num_frames) {
+  API_TRY
+  std::vector<char> k(keep, keep + nkeep);
+  std::vector<float> xv;
+  SpkExtractor* ex = ((SpkModel*)spk)->Extractor();
+  if (!ex->Extract(samples, n, first_frame, k, &xv, num_frames)) return 0;
+  if ((int)xv.size() > cap) VAMD_ERR("output capacity");
+  std::copy(xv.begin(), xv.end(), out);
+  return (int)xv.size();
+  API_CATCH(-1)
 }
 
 void vosk_recognizer_set_max_alternatives(VoskRecognizer* r, int n) {

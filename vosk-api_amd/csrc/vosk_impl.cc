@@ -141,7 +141,7 @@ static int InputRate(float sr) {
   return r;
 }
 
-Recognizer::Recognizer(Model* model, float sr) : Recognizer(model, sr, nullptr) {}
+Recognizer::Recognizer(Model* model, float sr) : Recognizer(model, sr, (const char*)nullptr) {}
 
 Recognizer::Recognizer(Model* model, float sr, const char* grammar)
     : model_(model), sample_frequency_(sr) {
@@ -157,9 +157,65 @@ Recognizer::Recognizer(Model* model, float sr, const char* grammar)
   model_->Ref();
 }
 
+Recognizer::Recognizer(Model* model, float sr, SpkModel* spk) : Recognizer(model, sr, (const char*)nullptr) {
+  if (spk) {
+    spk_ = spk;
+    spk_->Ref();
+  }
+}
+
+void Recognizer::SetSpkModel(SpkModel* spk) {
+  if (state_ == RECOGNIZER_RUNNING) {
+    VAMD_WARN("Can't add speaker model to already running recognizer");
+    return;
+  }
+  spk->Ref();
+  if (spk_) spk_->Unref();
+  spk_ = spk;
+  spk_samples_.clear();
+}
+
 Recognizer::~Recognizer() {
   engine_->FreeSlot(slot_);
+  if (spk_) spk_->Unref();
   model_->Unref();
+}
+
+SpkModel::SpkModel(const std::string& dir) : md_(std::make_shared<SpkModelData>()) {
+  md_->Load(dir);
+}
+
+SpkExtractor* SpkModel::Extractor() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!ex_) ex_.reset(new SpkExtractor(md_, DeviceFromEnv()));
+  return ex_.get();
+}
+
+bool Recognizer::GetSpkVector(std::vector<float>* xvec, int* num_frames) {
+  const ModelData& m = engine_->model();
+  *num_frames = 0;
+  // OnlineSilenceWeighting::Active() with the reference's configuration
+  // (silence weight 1e-3, the endpoint silence phones; src/model.cc:230-231)
+  std::vector<char> keep;
+  if (!m.endpoint.silence_phones.empty() && engine_->NumFramesDecoded(slot_) > 0) {
+    std::vector<PathResult> pr;
+    engine_->BestPaths({slot_}, true, &pr);
+    for (int a : pr[0].arcs) {
+      const int il = m.graph.ilabel[a];
+      if (il == 0) continue;
+      const int ph = m.tm.tid2phone[il];
+      keep.push_back(ph < (int)m.phone_is_silence.size() && m.phone_is_silence[ph] ? 0 : 1);
+    }
+  }
+  if (std::lround(sample_frequency_) != std::lround(spk_->data().mfcc.samp_freq)) {
+    if (!spk_rate_warned_)
+      VAMD_WARN("speaker vectors need input at the speaker model's rate ("
+                << spk_->data().mfcc.samp_freq << " Hz); not computed");
+    spk_rate_warned_ = true;
+    return false;
+  }
+  return spk_->Extractor()->Extract(spk_samples_.data(), (long long)spk_samples_.size(),
+                                    frame_offset_ * 3, keep, xvec, num_frames);
 }
 
 void Recognizer::CleanUp() {  // src/recognizer.cc:188-224
@@ -169,6 +225,7 @@ void Recognizer::CleanUp() {  // src/recognizer.cc:188-224
     samples_processed_ = 0;
     frame_offset_ = 0;
     engine_->ResetPipeline(slot_);
+    spk_samples_.clear();  // a new speaker front end (src/recognizer.cc:217-220)
   } else {
     engine_->ResetDecoder(slot_);
   }
@@ -202,6 +259,7 @@ bool Recognizer::AcceptWaveform(std::vector<float>& w) {  // src/recognizer.cc:2
     engine_->Advance({slot_});
   }
   samples_processed_ += w.size();
+  if (spk_) spk_samples_.insert(spk_samples_.end(), w.begin(), w.end());  // src/recognizer.cc:314-316
   return EndpointDetected();
 }
 
@@ -298,6 +356,14 @@ const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
       obj["result"].Append(word);
     }
     obj["text"] = Json::Str(wtext(r.words));
+    if (spk_) {  // :470-479
+      std::vector<float> xv;
+      int nspk = 0;
+      if (GetSpkVector(&xv, &nspk)) {
+        for (float v : xv) obj["spk"].Append(Json::Float(v));
+        obj["spk_frames"] = Json::Int(nspk);
+      }
+    }
     return StoreReturn(obj.Dump());
   }
   // n-best (NbestResult :526-607 / NlsmlResult :609-667): the shortest

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "xvector.h"
 #include "json_out.h"
 
 namespace vamd {
@@ -58,6 +59,26 @@ class Model {
   std::atomic<int> ref_{1};
 };
 
+// Speaker model (src/spk_model.cc): refcounted like Model; the GPU x-vector
+// extractor is created on first use on the recognizers' device.
+class SpkModel {
+ public:
+  explicit SpkModel(const std::string& dir);
+  void Ref() { ref_.fetch_add(1); }
+  void Unref() {
+    if (ref_.fetch_sub(1) == 1) delete this;
+  }
+  const SpkModelData& data() const { return *md_; }
+  SpkExtractor* Extractor();
+
+ private:
+  ~SpkModel() = default;
+  std::shared_ptr<SpkModelData> md_;
+  std::unique_ptr<SpkExtractor> ex_;
+  std::mutex mu_;
+  std::atomic<int> ref_{1};
+};
+
 enum RecognizerState { RECOGNIZER_INITIALIZED, RECOGNIZER_RUNNING, RECOGNIZER_ENDPOINT,
                        RECOGNIZER_FINALIZED };
 
@@ -65,6 +86,9 @@ class Recognizer {
  public:
   Recognizer(Model* model, float sample_frequency);
   Recognizer(Model* model, float sample_frequency, const char* grammar);
+  Recognizer(Model* model, float sample_frequency, SpkModel* spk);
+  // src/recognizer.cc:259-268 (refused while an utterance is running)
+  void SetSpkModel(SpkModel* spk);
   ~Recognizer();
   void SetMaxAlternatives(int n) { max_alternatives_ = n; }
   void SetWords(bool w) { words_ = w; }
@@ -86,6 +110,9 @@ class Recognizer {
   const char* StoreEmptyReturn();
   const char* StoreReturn(const std::string& s);
   std::string WordsText(const std::vector<WordSeg>& w) const;
+  // GetSpkVector (src/recognizer.cc:356-419): the segment's non-silence
+  // frames on the best path -> x-vector on the GPU
+  bool GetSpkVector(std::vector<float>* xvec, int* num_frames);
 
   Model* model_;
   Engine* engine_;
@@ -99,6 +126,9 @@ class Recognizer {
   bool finalized_decoder_ = false;
   std::string last_result_;
   std::vector<float> resample_buf_;
+  SpkModel* spk_ = nullptr;
+  std::vector<float> spk_samples_;  // the speaker front end's input since its last reset
+  bool spk_rate_warned_ = false;
 };
 
 class BatchRecognizer;

@@ -423,6 +423,10 @@ FIELD_KIND = {
     "<Dim>": "i", "<BlockDim>": "i", "<InputDim>": "i", "<OutputDim>": "i",
     "<RankIn>": "i", "<RankOut>": "i", "<UpdatePeriod>": "i", "<TimePeriod>": "i",
     "<TimeMaskMaxFrames>": "i",
+    # statistics extraction / pooling (x-vector nnets; Kaldi spells "Varinance")
+    "<InputPeriod>": "i", "<OutputPeriod>": "i", "<IncludeVarinance>": "b",
+    "<LeftContext>": "i", "<RightContext>": "i", "<NumLogCountFeatures>": "i",
+    "<OutputStddevs>": "b", "<VarianceFloor>": "f",
     # bools
     "<IsGradient>": "b", "<TestMode>": "b", "<UseNaturalGradient>": "b",
     "<Continuous>": "b",
@@ -550,6 +554,41 @@ def read_nnet3_am(r: KaldiReader) -> Nnet3:
         if r.p < len(r.d) and r.peek_token() == "<Priors>":
             r.expect("<Priors>"); pri = r.vector()
     return Nnet3(lines, comps, order, lc, rc, pri)
+
+
+def write_nnet3_raw(path: str, nn: Nnet3):
+    """Nnet::Write (binary): config lines, components, </Nnet3> -- a raw
+    nnet such as a speaker model's final.ext.raw."""
+    w = KaldiWriter()
+    w.token("<Nnet3>")
+    w.raw(b"\n")
+    for ln in nn.config_lines:
+        w.raw(ln.encode() + b"\n")
+    w.raw(b"\n")
+    w.token("<NumComponents>")
+    w.i32(len(nn.component_order))
+    for name in nn.component_order:
+        ctype, fields = nn.components[name]
+        w.token("<ComponentName>")
+        w.token(name)
+        write_component(w, ctype, fields)
+    w.token("</Nnet3>")
+    with open(path, "wb") as f:
+        f.write(w.bytes())
+
+
+def read_nnet3_raw(path: str) -> Nnet3:
+    return read_nnet3_am(KaldiReader(open(path, "rb").read()))
+
+
+def write_vector_file(path: str, v):
+    w = KaldiWriter()
+    w.fvector(v)
+    open(path, "wb").write(w.bytes())
+
+
+def read_vector_file(path: str) -> np.ndarray:
+    return np.asarray(KaldiReader(open(path, "rb").read()).vector(), np.float32)
 
 
 def write_final_mdl(path: str, tm: TransitionModel, nn: Nnet3):

@@ -551,6 +551,69 @@ def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_st
     return out_dir
 
 
+SPK_MFCC_CONF = """--sample-frequency=16000
+--frame-length=25 # the default is 25
+--low-freq=20 # the default.
+--high-freq=7600 # the default is zero meaning use the Nyquist (8k in this case).
+--num-mel-bins=30
+--num-ceps=30
+--snip-edges=false
+--dither=0
+"""
+
+
+def make_spk_model(out_dir, seed=5, hidden=128, stats_dim=192, embed=128, out=64):
+    """Synthetic speaker model (the reference reads
+    mfcc.conf, final.ext.raw, mean.vec and transform.mat,
+    src/spk_model.cc:17-32): a Kaldi x-vector topology (TDNN layers with
+    splicing, statistics extraction + mean/stddev pooling over the whole
+    input, the embedding affine) with seeded random weights."""
+    rng = np.random.default_rng(seed)
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, "mfcc.conf"), "w") as f:
+        f.write(SPK_MFCC_CONF)
+    D = 30
+    lines = [f"input-node name=input dim={D}"]
+    comps, order = {}, []
+
+    def add(name, comp, inp):
+        lines.append(f"component-node name={name} component={name} input={inp}")
+        comps[name] = comp
+        order.append(name)
+
+    def layer(i, din, dout, splice, src):
+        terms = [src if o == 0 else f"Offset({src}, {o})" for o in splice]
+        inp = terms[0] if len(terms) == 1 else "Append(" + ", ".join(terms) + ")"
+        add(f"tdnn{i}.affine", nat_affine(rng, din * len(splice), dout), inp)
+        add(f"tdnn{i}.relu", relu(dout), f"tdnn{i}.affine")
+        add(f"tdnn{i}.batchnorm", batchnorm(dout), f"tdnn{i}.relu")
+        return f"tdnn{i}.batchnorm"
+
+    x = layer(1, D, hidden, [-2, -1, 0, 1, 2], "input")
+    x = layer(2, hidden, hidden, [-2, 0, 2], x)
+    x = layer(3, hidden, hidden, [-3, 0, 3], x)
+    x = layer(4, hidden, hidden, [0], x)
+    x = layer(5, hidden, stats_dim, [0], x)
+    add("stats-extraction-0-10000", ("StatisticsExtractionComponent", [
+        ("<InputDim>", stats_dim), ("<InputPeriod>", 1), ("<OutputPeriod>", 1),
+        ("<IncludeVarinance>", True)]), x)
+    add("stats-pooling-0-10000", ("StatisticsPoolingComponent", [
+        ("<InputDim>", 1 + 2 * stats_dim), ("<InputPeriod>", 1), ("<LeftContext>", 0),
+        ("<RightContext>", 10000), ("<NumLogCountFeatures>", 0), ("<OutputStddevs>", True),
+        ("<VarianceFloor>", 1e-10)]), "stats-extraction-0-10000")
+    add("tdnn6.affine", nat_affine(rng, 2 * stats_dim, embed, gain=1.0), "Round(stats-pooling-0-10000, 1)")
+    lines.append("output-node name=output input=tdnn6.affine objective=linear")
+    kf.write_nnet3_raw(os.path.join(out_dir, "final.ext.raw"), kf.Nnet3(lines, comps, order))
+    kf.write_vector_file(os.path.join(out_dir, "mean.vec"),
+                         (rng.standard_normal(embed) * 0.1).astype(np.float32))
+    kf.write_matrix_file(os.path.join(out_dir, "transform.mat"),
+                         (rng.standard_normal((out, embed)) / math.sqrt(embed)).astype(np.float32))
+    with open(os.path.join(out_dir, "README"), "w") as f:
+        f.write(f"synthetic vosk-api_amd speaker model seed={seed} stats={stats_dim} "
+                f"embed={embed} out={out}\n")
+    return out_dir
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
