@@ -923,7 +923,7 @@ constexpr int kIvCgLds = 48;  // S up to this: the CG matrix lives in LDS
 // slice of U and SigmaInvM); the per-Gaussian aggregation is recomputed by
 // every part (identical).  A snapshot of the terms is taken at every request
 // for the CG kernel.
-constexpr int kIvGroup = 8;  // Gaussians whose X_g are held in LDS at a time
+constexpr int kIvGroup = 16;  // Gaussians whose X_g are held in LDS at a time
 struct IvAccShared {
   unsigned short sel[kIvBatchRows][5];
   float post[kIvBatchRows][5];
