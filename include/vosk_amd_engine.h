@@ -51,10 +51,11 @@ void vamd_graph_free(void *graph);
 
 /* speaker x-vector of a sample sequence (the GPU path GetSpkVector uses,
  * xvector.h): samples at the speaker MFCC rate since the speaker front end
- * started, the segment's frames from first_frame, frame i used iff
+ * started (at `rate`, resampled to the speaker model's rate on the GPU), the
+ * segment's frames from first_frame, frame i used iff
  * keep[(i - first_frame) / 3].  Returns the vector length (0: fewer than 50
  * frames selected; -1: error); *num_frames = the selected frame count. */
-int vamd_spk_extract(VoskSpkModel *spk, const float *samples, long long n, int first_frame,
+int vamd_spk_extract(VoskSpkModel *spk, const float *samples, long long n, int rate, int first_frame,
                      const signed char *keep, int nkeep, float *out, int cap, int *num_frames);
 
 /* host-only: the result pipeline over a state-level lattice (the arrays of

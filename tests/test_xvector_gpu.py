@@ -33,16 +33,16 @@ def spk_oracle(synth_spk):
     return OX.OracleSpk(synth_spk)
 
 
-def _extract(vosk_mod, spk, wave, first, keep):
+def _extract(vosk_mod, spk, wave, first, keep, rate=16000):
     so = C.CDLL(os.path.join(os.path.dirname(vosk_mod.__file__), "libvosk.so"))
     so.vamd_spk_extract.restype = C.c_int
-    so.vamd_spk_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_int, C.c_void_p, C.c_int,
-                                    C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    so.vamd_spk_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_void_p,
+                                    C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     w = np.ascontiguousarray(wave, np.float32)
     k = np.ascontiguousarray(keep, np.int8)
     out = np.zeros(1024, np.float32)
     nf = C.c_int(0)
-    r = so.vamd_spk_extract(spk._handle, w.ctypes.data, len(w), first, k.ctypes.data, len(k),
+    r = so.vamd_spk_extract(spk._handle, w.ctypes.data, len(w), rate, first, k.ctypes.data, len(k),
                             out.ctypes.data, len(out), C.byref(nf))
     assert r >= 0
     return (out[:r].copy() if r > 0 else None), nf.value
@@ -66,6 +66,19 @@ def test_xvector_matches_oracle(vosk_mod, synth_spk, spk_oracle, test_wave, case
     if ref is None:
         assert got is None
         return
+    np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("rate", [8000, 44100])
+def test_xvector_other_sample_rates(vosk_mod, synth_spk, spk_oracle, test_wave, rate):
+    """Input at another rate goes through the GPU resampler first (Kaldi
+    LinearResample, not flushed, as the online speaker front end)."""
+    spk = vosk_mod.SpkModel(synth_spk)
+    wave = oracle_py.resample(test_wave, 16000, rate)
+    got, n = _extract(vosk_mod, spk, wave, 0, [1] * 10000, rate=rate)
+    x16 = oracle_py.resample(wave, rate, 16000)[:oracle_py.resample_num_outputs(rate, 16000, len(wave), False)]
+    ref, nr = spk_oracle.xvector(x16, 0, [1] * 10000)
+    assert n == nr
     np.testing.assert_array_equal(got, ref)
 
 

@@ -99,13 +99,13 @@ void vosk_recognizer_set_spk_model(VoskRecognizer* recognizer, VoskSpkModel* spk
   API_CATCH_VOID
 }
 
-int vamd_spk_extract(VoskSpkModel* spk, const float* samples, long long n, int first_frame,
+int vamd_spk_extract(VoskSpkModel* spk, const float* samples, long long n, int rate, int first_frame,
                      const signed char* keep, int nkeep, float* out, int cap, int* num_frames) {
   API_TRY
   std::vector<char> k(keep, keep + nkeep);
   std::vector<float> xv;
   SpkExtractor* ex = ((SpkModel*)spk)->Extractor();
-  if (!ex->Extract(samples, n, first_frame, k, &xv, num_frames)) return 0;
+  if (!ex->Extract(samples, n, rate, first_frame, k, &xv, num_frames)) return 0;
   if ((int)xv.size() > cap) VAMD_ERR("output capacity");
   std::copy(xv.begin(), xv.end(), out);
   return (int)xv.size();

@@ -207,15 +207,9 @@ bool Recognizer::GetSpkVector(std::vector<float>* xvec, int* num_frames) {
       keep.push_back(ph < (int)m.phone_is_silence.size() && m.phone_is_silence[ph] ? 0 : 1);
     }
   }
-  if (std::lround(sample_frequency_) != std::lround(spk_->data().mfcc.samp_freq)) {
-    if (!spk_rate_warned_)
-      VAMD_WARN("speaker vectors need input at the speaker model's rate ("
-                << spk_->data().mfcc.samp_freq << " Hz); not computed");
-    spk_rate_warned_ = true;
-    return false;
-  }
   return spk_->Extractor()->Extract(spk_samples_.data(), (long long)spk_samples_.size(),
-                                    frame_offset_ * 3, keep, xvec, num_frames);
+                                    (int)std::lround(sample_frequency_), frame_offset_ * 3, keep,
+                                    xvec, num_frames);
 }
 
 void Recognizer::CleanUp() {  // src/recognizer.cc:188-224

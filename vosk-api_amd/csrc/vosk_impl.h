@@ -128,7 +128,6 @@ class Recognizer {
   std::vector<float> resample_buf_;
   SpkModel* spk_ = nullptr;
   std::vector<float> spk_samples_;  // the speaker front end's input since its last reset
-  bool spk_rate_warned_ = false;
 };
 
 class BatchRecognizer;

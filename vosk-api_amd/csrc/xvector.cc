@@ -389,11 +389,29 @@ void SpkExtractor::Reserve(long long samples, int frames, int sel) {
   }
 }
 
-bool SpkExtractor::Extract(const float* samples, long long n, int first_frame,
+bool SpkExtractor::Extract(const float* samples, long long n_in, int rate, int first_frame,
                            const std::vector<char>& keep, std::vector<float>* xvec, int* num_frames) {
   std::lock_guard<std::mutex> lk(mu_);
   XV_HIPCHECK(hipSetDevice(device_));
   const NnetPlan& plan = net_.frames;
+  const int spk_rate = (int)std::lround(md_->mfcc.samp_freq);
+  long long n = n_in;
+  if (rate != spk_rate) {
+    if (rate <= 0) VAMD_ERR("bad sample rate " << rate);
+    if (table_rate_ != rate) {
+      table_ = BuildResampleTable(rate, spk_rate);
+      ResampleDev td{};
+      td.first = Upload(table_.first);
+      td.ntaps = Upload(table_.ntaps);
+      td.w = Upload(table_.w);
+      td.in_unit = table_.in_unit;
+      td.out_unit = table_.out_unit;
+      td.taps = table_.taps;
+      d_table_ = Upload(std::vector<ResampleDev>{td});
+      table_rate_ = rate;
+    }
+    n = table_.NumOutputSamples(n_in, false);
+  }
   const int nfr = SpkNumFrames(md_->mfcc, n);
   std::vector<int> rows;
   for (int i = std::max(0, first_frame); i < nfr; i++) {
@@ -409,7 +427,31 @@ bool SpkExtractor::Extract(const float* samples, long long n, int first_frame,
   const int r_lo = std::max(plan.left_context, -net_.pool_left);
   const int r_hi = std::min(sel - 1 - plan.right_context, net_.pool_right);
   if (r_lo > r_hi) return false;
-  XV_HIPCHECK(hipMemcpyAsync(d_wave_, samples, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+  if (rate == spk_rate) {
+    XV_HIPCHECK(hipMemcpyAsync(d_wave_, samples, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+  } else {
+    if (n_in + 1 > raw_cap_) {
+      long long c = 1024;
+      while (c < n_in + 1) c <<= 1;
+      DevFree(d_raw_);
+      d_raw_ = (float*)DevAlloc(sizeof(float) * c);
+      raw_cap_ = c;
+    }
+    XV_HIPCHECK(hipMemcpyAsync(d_raw_, samples, sizeof(float) * n_in, hipMemcpyHostToDevice, stream_));
+    const int per = 4096;
+    const int nj = (int)((n + per - 1) / per);
+    if (nj > rjobs_cap_) {
+      DevFree(d_rjobs_);
+      d_rjobs_ = (ResampleJob*)DevAlloc(sizeof(ResampleJob) * nj);
+      rjobs_cap_ = nj;
+    }
+    std::vector<ResampleJob> rj(nj);
+    for (int j = 0; j < nj; j++)
+      rj[j] = ResampleJob{0, j * per, (int)std::min<long long>(per, n - (long long)j * per), 0,
+                          (long long)j * per, n_in};
+    XV_HIPCHECK(hipMemcpyAsync(d_rjobs_, rj.data(), sizeof(ResampleJob) * nj, hipMemcpyHostToDevice, stream_));
+    LaunchResample(d_rjobs_, nj, d_table_, d_raw_, (int)raw_cap_, d_wave_, (int)wave_cap_, stream_);
+  }
   MfccJob mj{0, 0, nfr, 0};
   XV_HIPCHECK(hipMemcpyAsync(d_mjob_, &mj, sizeof(mj), hipMemcpyHostToDevice, stream_));
   MfccDev m = mfcc_;

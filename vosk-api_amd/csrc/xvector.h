@@ -25,6 +25,7 @@
 #include "engine_dev.h"
 #include "model_io.h"
 #include "nnet_plan.h"
+#include "resample.h"
 
 namespace vamd {
 
@@ -69,8 +70,10 @@ class SpkExtractor {
   // MFCC rate; the segment's frames start at first_frame; frame i is used iff
   // keep[(i - first_frame) / 3].  Returns false (and *num_frames) when fewer
   // than 50 frames are selected (src/recognizer.cc:354,386-389).
-  bool Extract(const float* samples, long long n, int first_frame, const std::vector<char>& keep,
-               std::vector<float>* xvec, int* num_frames);
+  // Input at another rate is resampled first (Kaldi LinearResample, cutoff
+  // min(rates)/2, 6 zeros, not flushed: the online feature's resampler).
+  bool Extract(const float* samples, long long n, int rate, int first_frame,
+               const std::vector<char>& keep, std::vector<float>* xvec, int* num_frames);
   int OutputDim() const { return md_->transform.rows; }
   const XvectorNet& net() const { return net_; }
 
@@ -97,6 +100,12 @@ class SpkExtractor {
   long long wave_cap_ = 0;
   int frame_cap_ = 0, sel_cap_ = 0, ring_ = 0;
   float* d_wave_ = nullptr;
+  float* d_raw_ = nullptr;       // input before resampling
+  long long raw_cap_ = 0;
+  int table_rate_ = 0;           // rate of the cached resampling table
+  ResampleDev* d_table_ = nullptr;
+  ResampleJob* d_rjobs_ = nullptr;
+  int rjobs_cap_ = 0;
   float* d_feats_ = nullptr;     // [frame ring][1][feat_dim]
   int feat_ring_ = 0;
   int* d_rows_ = nullptr;        // selected frame indices
@@ -113,6 +122,7 @@ class SpkExtractor {
   float* d_transform_ = nullptr;
   float* d_xvec_ = nullptr;
   int head_max_ = 0;
+  ResampleTable table_;
   std::mutex mu_;
 };
 
