@@ -58,6 +58,12 @@ void vamd_graph_free(void *graph);
 int vamd_spk_extract(VoskSpkModel *spk, const float *samples, long long n, int rate, int first_frame,
                      const signed char *keep, int nkeep, float *out, int cap, int *num_frames);
 
+/* host-only: LM rescoring (rescore.h) applied by vamd_lattice_words_json
+ * after determinization (both paths NULL: off); vamd_carpa_logprob is a
+ * ConstArpa n-gram lookup (natural log, history oldest word first). */
+int vamd_lattice_set_rescore(const char *g_fst, const char *g_carpa);
+float vamd_carpa_logprob(const char *g_carpa, int word, const int *hist, int nhist);
+
 /* host-only: the result pipeline over a state-level lattice (the arrays of
  * vamd_stream_lattice; arc_ilabel / arc_olabel index the graph's arcs):
  * lattice-beam pruning, word determinization, graph scaling, word alignment

@@ -85,6 +85,21 @@ def synth_lookahead():
 
 
 @pytest.fixture(scope="session")
+def synth_model_rescore(synth_model_noep):
+    """synth_model_noep + rescore/G.fst and rescore/G.carpa."""
+    import make_synth_model as msm
+    path = os.path.join(MODEL_CACHE, f"synth_rescore_{SYNTH_VERSION}")
+    if not os.path.exists(os.path.join(path, "README")):
+        tmp = path + f".tmp{os.getpid()}"
+        shutil.rmtree(tmp, ignore_errors=True)
+        shutil.copytree(synth_model_noep, tmp)
+        msm.add_rescore(tmp)
+        shutil.rmtree(path, ignore_errors=True)
+        os.rename(tmp, path)
+    return path
+
+
+@pytest.fixture(scope="session")
 def synth_spk():
     """Synthetic x-vector speaker model (mfcc.conf, final.ext.raw, mean.vec,
     transform.mat)."""

@@ -666,7 +666,7 @@ def word_align(W, Fi, tables):
     return A, F
 
 
-def results(oracle, llh, use_final=True, graph_scale=0.9, nbest_n=0):
+def results(oracle, llh, use_final=True, graph_scale=0.9, nbest_n=0, rescore=None):
     """The reference's result chain over the oracle decoder's lattice of
     `llh`: prune, determinize, graph scale, word alignment (when the model has
     word_boundary.int), then MBR (and n-best)."""
@@ -675,6 +675,10 @@ def results(oracle, llh, use_final=True, graph_scale=0.9, nbest_n=0):
                             use_final, lattice=True)
     W, Fi = determinize(prune(raw_from_oracle(r, oracle.graph, use_final), 6.0),
                         oracle.graph.ilabel, oracle.graph.olabel)
+    if rescore is not None:  # (W, Fi) -> rescored (W, Fi) or None (unchanged)
+        rr = rescore(W, Fi)
+        if rr is not None:
+            W, Fi = rr
     if graph_scale != 1.0:
         W, Fi = scale_graph(W, Fi, graph_scale)
     wb = os.path.join(oracle.dir, "graph", "phones", "word_boundary.int")

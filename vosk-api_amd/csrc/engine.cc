@@ -138,6 +138,15 @@ void ModelData::Load(const std::string& path) {
     VAMD_LOG("Loading words from " << words_txt);
     ReadSymbolTable(words_txt, &words);
   }
+  if (FileExists(path + "/rescore/G.carpa")) {
+    VAMD_LOG("Loading subtract G.fst model from " << path << "/rescore/G.fst");
+    VAMD_LOG("Loading CARPA model from " << path << "/rescore/G.carpa");
+    auto r = std::make_shared<RescoreLm>();
+    r->Load(path + "/rescore/G.fst", path + "/rescore/G.carpa");
+    rescore = r;
+  }
+  if (FileExists(path + "/rnnlm/final.raw"))
+    VAMD_WARN("RNNLM rescoring (rnnlm/) is not supported; final results use the ConstArpa rescoring only");
   has_word_boundary = FileExists(wb);
   int max_phone = 0;
   for (int p : tm.tid2phone) max_phone = std::max(max_phone, p);

@@ -23,6 +23,7 @@
 #include "nnet_plan.h"
 #include "resample.h"
 #include "lattice.h"
+#include "rescore.h"
 #include "silence.h"
 
 namespace vamd {
@@ -42,6 +43,9 @@ struct ModelData {
   // recognizers' runtime graphs (graph_compose.h); null for HCLG models.
   std::shared_ptr<const HostFst> lookahead_hcl;
   std::vector<int> disambig;
+  // rescore/G.fst + rescore/G.carpa (src/model.cc:308-314): LM rescoring of
+  // final results (rescore.h); null without them
+  std::shared_ptr<const RescoreLm> rescore;
   SymbolTable words;
   std::vector<char> phone_is_silence;  // indexed by phone id
   bool has_word_boundary = false;

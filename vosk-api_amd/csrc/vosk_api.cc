@@ -6,6 +6,7 @@
 // (the GPU path is the only path).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <sstream>
@@ -348,6 +349,33 @@ int vamd_silence_weighting_run(int ncalls, const int* num_frames_ready, const in
   API_CATCH(-1)
 }
 
+static std::shared_ptr<RescoreLm> g_host_rescore;  // vamd_lattice_set_rescore (tests)
+
+int vamd_lattice_set_rescore(const char* g_fst, const char* g_carpa) {
+  API_TRY
+  if (!g_fst || !g_carpa) {
+    g_host_rescore.reset();
+    return 0;
+  }
+  auto r = std::make_shared<RescoreLm>();
+  r->Load(g_fst, g_carpa);
+  g_host_rescore = r;
+  return 0;
+  API_CATCH(-1)
+}
+
+float vamd_carpa_logprob(const char* g_carpa, int word, const int* hist, int nhist) {
+  static std::string loaded;
+  static ConstArpaLm lm;
+  API_TRY
+  if (loaded != g_carpa) {
+    lm.Read(g_carpa);
+    loaded = g_carpa;
+  }
+  return lm.NgramLogprob(word, std::vector<int>(hist, hist + nhist));
+  API_CATCH(NAN)
+}
+
 const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, const int* tok_state,
                                     const float* tok_cost, const int* link_src, const int* link_dst,
                                     const int* link_arc, const float* link_graph, const float* link_ac,
@@ -381,6 +409,15 @@ const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, cons
   int det_arcs = 0;
   for (auto& v : wl.arcs) det_arcs += (int)v.size();
   os << ", \"det_arcs\": " << det_arcs;
+  if (g_host_rescore) {
+    WordLattice r;
+    const bool rok = RescoreLattice(wl, *g_host_rescore, opt, &r);
+    if (rok) wl = std::move(r);
+    int rarcs = 0;
+    for (auto& v : wl.arcs) rarcs += (int)v.size();
+    os << ", \"rescored\": " << (rok ? 1 : 0) << ", \"rescored_states\": " << wl.NumStates()
+       << ", \"rescored_arcs\": " << rarcs;
+  }
   if (graph_scale != 1.0f) ScaleGraph(&wl, graph_scale);
   if (ntids > 0) {
     std::vector<char> ty(tid_type, tid_type + ntids), fi(tid_final, tid_final + ntids),

@@ -277,7 +277,7 @@ bool Recognizer::EndpointDetected() {
 // Then the graph scale, and word alignment when the model has
 // word_boundary.int (WordAlignLattice, :433-434; CopyLatticeForMbr otherwise).
 static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use_final, float graph_scale,
-                               WordLattice* wl) {
+                               WordLattice* wl, bool rescore = false) {
   RawLattice raw;
   e->GetRawLattice(slot, use_final, &raw);
   if (raw.overflow || raw.tok_state.empty()) return false;
@@ -285,6 +285,10 @@ static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use
   LatticeOptions opt;
   opt.lattice_beam = m.dec.lattice_beam;
   if (!DeterminizeToWords(raw, m.graph, opt, wl) || wl->NumStates() == 0) return false;
+  if (rescore && m.rescore) {  // src/recognizer.cc:680-711
+    WordLattice r;
+    if (RescoreLattice(*wl, *m.rescore, opt, &r)) *wl = std::move(r);
+  }
   if (graph_scale != 1.0f) ScaleGraph(wl, graph_scale);
   if (m.has_word_boundary) {
     WordLattice al;
@@ -301,10 +305,11 @@ static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use
 // MBR words, confidences and frame times of the segment; graph_scale as the
 // reference applies to final results (GraphLatticeScale(0.9), :718), 1 for
 // partial results.  Without a lattice: the best path, confidence 1.
-static MbrResult SegmentMbr(Engine* e, int slot, const ModelData& m, bool use_final, float graph_scale) {
+static MbrResult SegmentMbr(Engine* e, int slot, const ModelData& m, bool use_final, float graph_scale,
+                            bool rescore = false) {
   MbrResult r;
   WordLattice wl;
-  if (SegmentWordLattice(e, slot, m, use_final, graph_scale, &wl)) {
+  if (SegmentWordLattice(e, slot, m, use_final, graph_scale, &wl, rescore)) {
     MinimumBayesRisk(wl, &r);
     return r;
   }
@@ -338,7 +343,7 @@ const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
     return text.str();
   };
   if (max_alternatives_ == 0) {  // MbrResult, :429-482
-    const MbrResult r = SegmentMbr(engine_, slot_, m, true, 0.9f);
+    const MbrResult r = SegmentMbr(engine_, slot_, m, true, 0.9f, true);
     Json obj;
     for (size_t i = 0; i < r.words.size(); i++) {
       if (!words_) continue;
@@ -364,7 +369,7 @@ const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
   // paths of the graph-scaled word lattice, likelihood = -(graph + acoustic)
   std::vector<NbestPath> nb;
   WordLattice wl;
-  if (SegmentWordLattice(engine_, slot_, m, true, 0.9f, &wl)) {
+  if (SegmentWordLattice(engine_, slot_, m, true, 0.9f, &wl, true)) {
     NbestPaths(wl, max_alternatives_, &nb);
   } else {
     std::vector<PathResult> pr;

@@ -1064,3 +1064,79 @@ def write_matrix_file(path: str, m, double=False):
 
 def read_matrix_file(path: str) -> np.ndarray:
     return KaldiReader(open(path, "rb").read()).matrix64()
+
+
+# ----------------------------------------------------------------------------
+# Kaldi ConstArpaLm (lm/const-arpa-lm.{h,cc}) binary object, as read by
+# vosk-api_amd/csrc/rescore.cc
+# ----------------------------------------------------------------------------
+def write_const_arpa(path: str, ngrams: dict, bos: int, eos: int, unk: int, order: int):
+    """ngrams: {(w1, ..., wn): (logprob, backoff_logprob)} natural log, every
+    prefix of an n-gram present.  States: one per n-gram that is a unigram or
+    a history of a longer n-gram: [logprob][backoff][num children]
+    [(word, child info)...] with children sorted by word; child info = 2 *
+    (child offset - parent offset) + 1 for children with a state, else the
+    child's logprob bits with the lowest bit cleared.  A 3-int dummy state
+    at offset 0 keeps offset 0 free for "no unigram state"."""
+    kids = {}
+    for ng in ngrams:
+        if len(ng) > 1:
+            kids.setdefault(ng[:-1], []).append(ng)
+    has_state = {ng for ng in ngrams if len(ng) == 1 or ng in kids}
+    order_states = sorted((ng for ng in has_state if len(ng) == 1))
+    frontier = list(order_states)
+    while frontier:
+        nxt = []
+        for h in frontier:
+            for c in sorted(kids.get(h, []), key=lambda x: x[-1]):
+                if c in has_state:
+                    nxt.append(c)
+        order_states += nxt
+        frontier = nxt
+    pos, p = {}, 3
+    for st in order_states:
+        pos[st] = p
+        p += 3 + 2 * len(kids.get(st, []))
+    arr = np.zeros(p, np.int32)
+
+    def fbits(x):
+        return int(np.array([x], np.float32).view(np.int32)[0])
+
+    for st in order_states:
+        q = pos[st]
+        lp, bo = ngrams[st]
+        ch = sorted(kids.get(st, []), key=lambda x: x[-1])
+        arr[q], arr[q + 1], arr[q + 2] = fbits(lp), fbits(bo), len(ch)
+        for i, c in enumerate(ch):
+            arr[q + 3 + 2 * i] = c[-1]
+            if c in has_state:
+                arr[q + 4 + 2 * i] = 2 * (pos[c] - q) + 1
+            else:
+                arr[q + 4 + 2 * i] = fbits(ngrams[c][0]) & ~1
+    num_words = max(w for ng in ngrams for w in ng) + 1
+    uni = [pos.get((w,), 0) for w in range(num_words)]
+    b = bytearray(b"\0B")
+
+    def tok(t):
+        b.extend(t.encode() + b" ")
+
+    def i32(v):
+        b.extend(b"\x04" + struct.pack("<i", v))
+
+    def i64(v):
+        b.extend(b"\x08" + struct.pack("<q", v))
+
+    tok("<ConstArpaLm>"); tok("<LmInfo>")
+    i32(bos); i32(eos); i32(unk); i32(order)
+    tok("</LmInfo>"); tok("<LmStates>")
+    i64(len(arr))
+    b.extend(arr.tobytes())
+    tok("</LmStates>"); tok("<LmUnigram>")
+    i32(num_words)
+    for u in uni:
+        i64(u)
+    tok("</LmUnigram>"); tok("<LmOverflow>")
+    i32(0)
+    tok("</LmOverflow>"); tok("</ConstArpaLm>")
+    with open(path, "wb") as f:
+        f.write(bytes(b))

@@ -614,6 +614,61 @@ def make_spk_model(out_dir, seed=5, hidden=128, stats_dim=192, embed=128, out=64
     return out_dir
 
 
+def add_rescore(model_dir, seed=3):
+    """rescore/G.fst (the LM to subtract: a backoff bigram acceptor whose
+    backoff arcs carry #0 on the input, as Kaldi's G.fst) and rescore/G.carpa
+    (a ConstArpa trigram over the model's words with <s> / </s>),
+    src/model.cc:308-314."""
+    rng = np.random.default_rng(seed)
+    words = kf.read_symbol_table(os.path.join(model_dir, "graph", "words.txt"))
+    sym = {v: k for k, v in words.items()}
+    vocab = sorted(i for i, w in words.items() if w.startswith("w"))
+    disamb, bos, eos = sym["#0"], sym["<s>"], sym["</s>"]
+    os.makedirs(os.path.join(model_dir, "rescore"), exist_ok=True)
+    # G.fst: state 0 = unigram; bigram states for some words
+    big = [int(w) for w in rng.choice(vocab, size=min(60, len(vocab)), replace=False)]
+    bstate = {w: i + 1 for i, w in enumerate(big)}
+    arcs = []
+    uni = {w: float(rng.uniform(4.0, 10.0)) for w in vocab}
+    for w in vocab:
+        arcs.append((0, w, w, uni[w], bstate.get(w, 0)))
+    for w, s in bstate.items():
+        for v in rng.choice(vocab, size=12, replace=False):
+            v = int(v)
+            arcs.append((s, v, v, float(uni[v] * rng.uniform(0.3, 0.9)), bstate.get(v, 0)))
+        arcs.append((s, disamb, 0, float(rng.uniform(0.3, 1.5)), 0))
+    S = 1 + len(big)
+    arcs.sort(key=lambda a: (a[0], a[1]))
+    row = np.zeros(S + 1, np.int64)
+    np.add.at(row, np.array([a[0] for a in arcs]) + 1, 1)
+    final = np.full(S, np.inf, np.float32)
+    final[0] = 3.0
+    for s in range(1, S):
+        if rng.random() < 0.3:
+            final[s] = float(rng.uniform(1.0, 4.0))
+    g = kf.Fst(0, final, np.cumsum(row), np.array([a[1] for a in arcs], np.int32),
+               np.array([a[2] for a in arcs], np.int32), np.array([a[3] for a in arcs], np.float32),
+               np.array([a[4] for a in arcs], np.int32))
+    kf.write_vector_fst(os.path.join(model_dir, "rescore", "G.fst"), g)
+    # ConstArpa trigram (natural-log probabilities, backoffs)
+    ng = {(bos,): (-99.0, float(-rng.uniform(0.1, 1.0))), (eos,): (-3.0, 0.0)}
+    for w in vocab:
+        ng[(w,)] = (-uni[w], float(-rng.uniform(0.1, 1.0)))
+    hist1 = [bos] + [int(w) for w in rng.choice(vocab, size=min(80, len(vocab)), replace=False)]
+    for h in hist1:
+        for v in list(rng.choice(vocab, size=10, replace=False)) + [eos]:
+            ng[(h, int(v))] = (float(-rng.uniform(0.5, 6.0)), float(-rng.uniform(0.05, 0.8)))
+    pairs = [k for k in ng if len(k) == 2 and k[1] != eos]
+    for k in pairs[: len(pairs) // 3]:
+        for v in rng.choice(vocab, size=4, replace=False):
+            ng[k + (int(v),)] = (float(-rng.uniform(0.2, 3.0)), 0.0)
+    # an n-gram that extends to no longer n-gram backs off with weight 1 (log 0)
+    ctx = {k[:-1] for k in ng if len(k) > 1}
+    ng = {k: (v[0], v[1] if (k in ctx or len(k) == 1) else 0.0) for k, v in ng.items()}
+    kf.write_const_arpa(os.path.join(model_dir, "rescore", "G.carpa"), ng, bos, eos, -1, 3)
+    return ng
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")

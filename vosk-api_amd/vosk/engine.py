@@ -53,6 +53,8 @@ _SIGS = {
     "vamd_engine_decoder_phases": (C.c_int, [_vp, _vp]),
     "vamd_engine_set_step_samples": (C.c_int, [_vp, C.c_int]),
     "vamd_engine_stage_times": (C.c_int, [_vp, _vp, _vp, C.c_int]),
+    "vamd_lattice_set_rescore": (C.c_int, [C.c_char_p, C.c_char_p]),
+    "vamd_carpa_logprob": (C.c_float, [C.c_char_p, C.c_int, _vp, C.c_int]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(_c, _name)
@@ -304,3 +306,17 @@ class Engine:
         _chk(_c.vamd_engine_counters(self.h, out.ctypes.data))
         return dict(zip(("steps", "launches", "mfcc_frames", "chunk_jobs", "frames_decoded"),
                         out.tolist()))
+
+
+def set_rescore(g_fst=None, g_carpa=None):
+    """Host-only: LM rescoring (rescore.h) inside lattice_words (None: off)."""
+    r = _c.vamd_lattice_set_rescore(g_fst.encode() if g_fst else None,
+                                    g_carpa.encode() if g_carpa else None)
+    if r != 0:
+        raise RuntimeError("vamd_lattice_set_rescore failed: " + _err())
+
+
+def carpa_logprob(g_carpa, word, hist):
+    """Host-only: ConstArpa n-gram log probability (natural log)."""
+    h = np.ascontiguousarray(list(hist) or [0], np.int32)
+    return float(_c.vamd_carpa_logprob(g_carpa.encode(), int(word), h.ctypes.data, len(hist)))
