@@ -3,12 +3,14 @@
 #include "graph_compose.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cctype>
 #include <cmath>
 #include <functional>
 #include <sstream>
 #include <limits>
 #include <map>
+#include <memory>
 #include <utility>
 
 #include "common.h"
@@ -230,8 +232,10 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
   std::vector<char> is_disambig(max_il + 1, 0);
   for (int d : disambig)
     if (d > 0 && d <= max_il) is_disambig[d] = 1;
+  auto t0 = std::chrono::steady_clock::now();
   Reach reach;
   ComputeReach(a, &reach);
+  auto t1 = std::chrono::steady_clock::now();
   // grammar side: per state the epsilon arcs in order and the non-epsilon
   // arcs sorted by input label (stable)
   const int SB = b.NumStates();
@@ -275,6 +279,55 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
     return false;
   };
 
+  // Wide HCL states (the word-start states: one output-epsilon arc per first
+  // phone) are checked per grammar word instead of per arc: the label line is
+  // cut into segments, each listing the arcs whose reachable labels cover it,
+  // and each word of the grammar state marks the arcs of its segment.
+  struct ArcIndex {
+    std::vector<int> seg_lo;      // segment starts (ascending); segment k = [seg_lo[k], seg_lo[k+1])
+    std::vector<int> seg_begin;   // [nseg + 1] into arcs
+    std::vector<int> arcs;        // local arc indices covering each segment
+    std::vector<int> final_arcs;  // arcs that reach a final state
+  };
+  constexpr int kWide = 16;
+  std::vector<std::unique_ptr<ArcIndex>> arc_index(a.NumStates());
+  auto index_of = [&](int q1) -> const ArcIndex* {
+    const int64_t b0 = a.row[q1], n = a.row[q1 + 1] - b0;
+    if (n < kWide) return nullptr;
+    if (arc_index[q1]) return arc_index[q1].get();
+    auto ix = std::make_unique<ArcIndex>();
+    std::vector<std::pair<long long, int>> ev;  // (position, +arc+1 / -(arc+1))
+    for (int64_t e = b0; e < b0 + n; e++) {
+      if (a.olabel[e] != 0) continue;
+      const int c = reach.comp[a.nextstate[e]];
+      if (reach.final[c]) ix->final_arcs.push_back((int)(e - b0));
+      for (const auto& r : reach.labels[c]) {
+        ev.push_back({r.first, (int)(e - b0) + 1});
+        ev.push_back({(long long)r.second + 1, -((int)(e - b0) + 1)});
+      }
+    }
+    std::sort(ev.begin(), ev.end());
+    std::vector<int> active;
+    size_t i = 0;
+    while (i < ev.size()) {
+      const long long x = ev[i].first;
+      for (; i < ev.size() && ev[i].first == x; i++) {
+        const int v = ev[i].second;
+        if (v > 0) active.push_back(v - 1);
+        else active.erase(std::find(active.begin(), active.end(), -v - 1));
+      }
+      ix->seg_lo.push_back((int)std::min<long long>(x, std::numeric_limits<int>::max()));
+      ix->seg_begin.push_back((int)ix->arcs.size());
+      std::vector<int> sorted_active(active);
+      std::sort(sorted_active.begin(), sorted_active.end());
+      ix->arcs.insert(ix->arcs.end(), sorted_active.begin(), sorted_active.end());
+    }
+    ix->seg_begin.push_back((int)ix->arcs.size());
+    arc_index[q1] = std::move(ix);
+    return arc_index[q1].get();
+  };
+  std::vector<char> mark;
+
   HostFst c;
   c.osyms = b.osyms;
   StateTable table;
@@ -307,11 +360,25 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
         const int64_t e = bsorted[k];
         push(0, b.olabel[e], b.weight[e], id_of(q1, b.nextstate[e], 0));
       }
+    const ArcIndex* ix = b_alleps[q2] ? nullptr : index_of(q1);
+    if (ix) {  // mark the useful output-epsilon arcs of a wide HCL state
+      mark.assign(a.row[q1 + 1] - a.row[q1], 0);
+      if (std::isfinite(b.final_cost[q2]))
+        for (int k : ix->final_arcs) mark[k] = 1;
+      for (int64_t k = beps_end[q2]; k < b.row[q2 + 1]; k++) {
+        const int w = bword[k];
+        auto it = std::upper_bound(ix->seg_lo.begin(), ix->seg_lo.end(), w);
+        if (it == ix->seg_lo.begin()) continue;
+        const size_t sg = (size_t)(it - ix->seg_lo.begin()) - 1;
+        for (int j = ix->seg_begin[sg]; j < ix->seg_begin[sg + 1]; j++) mark[ix->arcs[j]] = 1;
+      }
+    }
     for (int64_t e = a.row[q1]; e < a.row[q1 + 1]; e++) {
       const int il = (a.ilabel[e] > 0 && a.ilabel[e] <= max_il && is_disambig[a.ilabel[e]]) ? 0 : a.ilabel[e];
       const int p = a.nextstate[e];
       if (a.olabel[e] == 0) {  // HCL moves alone
-        if (b_alleps[q2] || !useful(p, q2)) continue;
+        if (b_alleps[q2]) continue;
+        if (ix ? !mark[e - a.row[q1]] : !useful(p, q2)) continue;
         push(il, 0, a.weight[e], id_of(p, q2, b_has_eps[q2] ? 1 : 0));
       } else {  // matched word
         const int* wb = bword.data() + beps_end[q2];
@@ -326,7 +393,10 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
     c.row.push_back((int64_t)c.ilabel.size());
   }
   VAMD_LOG("Composed lookahead graph: " << c.NumStates() << " states, " << c.NumArcs() << " arcs expanded");
+  auto t2 = std::chrono::steady_clock::now();
   ConnectCanonical(c, out);
+  auto t3 = std::chrono::steady_clock::now();
+  VAMD_LOG_VERBOSE("compose timing: reach " << std::chrono::duration<double>(t1 - t0).count() << " s, expand " << std::chrono::duration<double>(t2 - t1).count() << " s, connect " << std::chrono::duration<double>(t3 - t2).count() << " s");
   VAMD_LOG("Static decoding graph: " << out->NumStates() << " states, " << out->NumArcs() << " arcs");
 }
 

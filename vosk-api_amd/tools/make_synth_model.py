@@ -193,7 +193,7 @@ def build_graph(rng, tids, num_base, vocab):
     return f, words
 
 
-def build_lookahead_graph(rng, tids, num_base, vocab, num_tids):
+def build_lookahead_graph(rng, tids, num_base, vocab, num_tids, n_big=40, fut_big=12, n_tri=12):
     """Lookahead graph pair (src/model.cc:281-285): an HCLr
     transducer (the lexicon prefix tree over the chain HMMs with optional
     silence, every word's output label on the arc back to the word-start
@@ -274,11 +274,11 @@ def build_lookahead_graph(rng, tids, num_base, vocab, num_tids):
 
     lm = {(): {"fut": {w + 1: float(uni[w]) for w in range(V)}, "final": 4.0},
           (0,): {"fut": fut(30), "backoff": 0.6, "final": None}}
-    big = [int(w) for w in rng.choice(V, size=min(40, V), replace=False) + 1]
+    big = [int(w) for w in rng.choice(V, size=min(n_big, V), replace=False) + 1]
     for h in big:
-        lm[(h,)] = {"fut": fut(12), "backoff": float(rng.uniform(0.3, 1.5)),
+        lm[(h,)] = {"fut": fut(fut_big), "backoff": float(rng.uniform(0.3, 1.5)),
                     "final": float(rng.uniform(1.0, 4.0)) if rng.random() < 0.4 else None}
-    for h in big[:12]:
+    for h in big[:n_tri]:
         for u in [0] + [int(x) for x in rng.choice(big, size=2, replace=False)]:
             lm[(h, u)] = {"fut": fut(6), "backoff": float(rng.uniform(0.2, 1.0)), "final": None}
     return hclr, lm, words, disambig
