@@ -1249,12 +1249,19 @@ void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, h
   if (a.nents > 0) hipLaunchKernelGGL(ivector_entry_kernel, dim3((a.nents + 3) / 4), dim3(256), 0, s, a);
   // parts: blocks b and b + 8 share an XCD, so part = b % NP keeps each XCD's
   // L2 on 1/NP of U and SigmaInvM
-  static const int np = getenv("VOSK_AMD_IV_PARTS") ? atoi(getenv("VOSK_AMD_IV_PARTS")) : 4;
+  // (VOSK_AMD_IV_PARTS: 2, 4 or 8; the per-part linear-term columns must fit
+  // IvAccShared::proj, ceil(S / parts) <= 25)
+  static const int np_env = getenv("VOSK_AMD_IV_PARTS") ? atoi(getenv("VOSK_AMD_IV_PARTS")) : 4;
   const int S = a.m.ivec_dim, QS = S * (S + 1) / 2;
+  const int np = (np_env == 8 || (np_env == 2 && (S + 1) / 2 <= (kIvMaxS + 3) / 4)) ? np_env : 4;
   if (np == 8) {
     const int nqp = ((QS + 7) / 8 + 255) / 256;
     if (nqp <= 1) hipLaunchKernelGGL((ivector_acc_kernel<1, 8>), dim3(njobs * 8), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((ivector_acc_kernel<3, 8>), dim3(njobs * 8), dim3(256), 0, s, a);
+  } else if (np == 2) {
+    const int nqp = ((QS + 1) / 2 + 255) / 256;
+    if (nqp <= 3) hipLaunchKernelGGL((ivector_acc_kernel<3, 2>), dim3(njobs * 2), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((ivector_acc_kernel<5, 2>), dim3(njobs * 2), dim3(256), 0, s, a);
   } else {
     const int nqp = ((QS + 3) / 4 + 255) / 256;
     if (nqp <= 1) hipLaunchKernelGGL((ivector_acc_kernel<1, 4>), dim3(njobs * 4), dim3(256), 0, s, a);
