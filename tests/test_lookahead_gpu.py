@@ -114,3 +114,43 @@ def test_grammar_on_hclg_model_uses_static_graph(vosk_mod, synth_model_noep, tes
     a = _final_text(vosk_mod, m, test_wave[:48000], '["w00001"]')
     b = _final_text(vosk_mod, m, test_wave[:48000])
     assert a == b
+
+
+def test_batch_recognizer_on_a_lookahead_model(vosk_mod, synth_lookahead, la_oracle, test_wave, monkeypatch):
+    """BASELINE config 3 names vosk-model-small-en-us, which ships HCLr.fst +
+    Gr.fst: the reference's CUDA batch path needs an HCLG; here the
+    BatchModel decodes on the expanded graph.  Final texts == the oracle's
+    MBR words on that graph (test_gpu_batch.py pattern)."""
+    import oracle_lattice as OL
+    monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_lookahead)
+    oracle = oracle_py.OracleModel(la_oracle.dir, fpc=51)
+    vosk_mod.GpuInit()
+    model = vosk_mod.BatchModel()
+    n = 4
+    waves = [perturbed_stream(test_wave, i, seconds=2.5 + 0.5 * i) for i in range(n)]
+    recs = [vosk_mod.BatchRecognizer(model, 16000) for _ in range(n)]
+    datas = [_pcm(w) for w in waves]
+    pos, texts, ended = [0] * n, [""] * n, set()
+    while len(ended) < n:
+        for i in range(n):
+            if i in ended:
+                continue
+            chunk = datas[i][pos[i]:pos[i] + 8000]
+            pos[i] += 8000
+            if not chunk:
+                recs[i].FinishStream()
+                ended.add(i)
+                continue
+            recs[i].AcceptWaveform(chunk)
+        model.Wait()
+        for i in range(n):
+            res = recs[i].Result()
+            if res:
+                texts[i] = (texts[i] + " " + json.loads(res)["text"]).strip()
+    model.Wait()
+    for i in range(n):
+        res = recs[i].Result()
+        if res:
+            texts[i] = (texts[i] + " " + json.loads(res)["text"]).strip()
+        mb = OL.results(oracle, oracle.loglikes(waves[i]))["mbr"]
+        assert texts[i] == " ".join(oracle.words[w] for w in mb["words"]), i
