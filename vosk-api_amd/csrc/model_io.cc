@@ -335,6 +335,10 @@ const std::map<std::string, FieldKind>& FieldKinds() {
       {"<SelfRepairLowerThreshold>", FK_F}, {"<SelfRepairUpperThreshold>", FK_F},
       {"<SelfRepairScale>", FK_F}, {"<ZeroedProportion>", FK_F}, {"<Scale>", FK_F},
       {"<BiasStddev>", FK_F}, {"<ParamStddev>", FK_F},
+      // NonlinearComponent self-repair statistics (doubles in newer Kaldi)
+      // and ScaleAndOffsetComponent's natural-gradient rank
+      {"<NumDimsSelfRepaired>", FK_F}, {"<NumDimsProcessed>", FK_F}, {"<SelfRepairTarget>", FK_F},
+      {"<Rank>", FK_I},
       {"<Dim>", FK_I}, {"<BlockDim>", FK_I}, {"<InputDim>", FK_I}, {"<OutputDim>", FK_I},
       {"<RankIn>", FK_I}, {"<RankOut>", FK_I}, {"<UpdatePeriod>", FK_I}, {"<TimePeriod>", FK_I},
       {"<TimeMaskMaxFrames>", FK_I},

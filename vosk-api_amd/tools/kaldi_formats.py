@@ -419,6 +419,8 @@ FIELD_KIND = {
     "<SelfRepairLowerThreshold>": "f", "<SelfRepairUpperThreshold>": "f",
     "<SelfRepairScale>": "f", "<ZeroedProportion>": "f", "<Scale>": "f",
     "<BiasStddev>": "f", "<ParamStddev>": "f",
+    "<NumDimsSelfRepaired>": "f", "<NumDimsProcessed>": "f", "<SelfRepairTarget>": "f",
+    "<Rank>": "i",
     # ints
     "<Dim>": "i", "<BlockDim>": "i", "<InputDim>": "i", "<OutputDim>": "i",
     "<RankIn>": "i", "<RankOut>": "i", "<UpdatePeriod>": "i", "<TimePeriod>": "i",
