@@ -81,18 +81,19 @@ def test_ivectors_bit_exact(synth_model, test_wave, fpc, chunk):
     np.testing.assert_array_equal(got, ref)
 
 
-# decoder frame construction: LDS table (default), global maps only, and
-# always-LDS (large frames overflow the table and are rebuilt on the global maps)
-FRAME_PATHS = {"default": None, "global": "0", "lds_then_rebuild": "1000000000"}
+# decoder frame construction: LDS table with HBM overflow (default), every
+# state in the HBM tables, and a 2-slot LDS probe limit (states split between
+# LDS and HBM in every frame)
+FRAME_PATHS = {"default": None, "hbm": "0", "mixed": "2"}
 
 
 @pytest.fixture(params=sorted(FRAME_PATHS))
 def frame_path(request, monkeypatch):
     v = FRAME_PATHS[request.param]
     if v is None:
-        monkeypatch.delenv("VOSK_AMD_LDS_FRAME_TOKENS", raising=False)
+        monkeypatch.delenv("VOSK_AMD_DEC_LDS_PROBE", raising=False)
     else:
-        monkeypatch.setenv("VOSK_AMD_LDS_FRAME_TOKENS", v)
+        monkeypatch.setenv("VOSK_AMD_DEC_LDS_PROBE", v)
     return request.param
 
 
@@ -114,8 +115,8 @@ def test_decoder_from_oracle_llh(synth_model, oracle, test_wave, frame_path):
 
 
 def test_decoder_wide_beam_all_paths(synth_model_wide, test_wave, frame_path):
-    """Thousands of tokens per frame: LDS table overflow / global rebuild and
-    the predictive global path give the oracle's best path and statistics."""
+    """Thousands of tokens per frame (more than the LDS table holds): the HBM
+    overflow tables give the oracle's best path and statistics."""
     import oracle_py
     ow = oracle_py.OracleModel(synth_model_wide)
     llh = ow.loglikes(test_wave[:64000])

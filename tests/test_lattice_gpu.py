@@ -2,8 +2,8 @@
 stream) rebuilt into the state-level lattice must equal the oracle's
 (LatticeFasterDecoder tokens and links, order-independent formulation) for
 every frame: the same tokens with the same costs, the same links with the
-same graph and acoustic costs.  Exercises the LDS frame table, the global
-maps and the overflow rebuild, and a wide-beam model."""
+same graph and acoustic costs.  Exercises the LDS frame table, the HBM
+overflow tables and a mix of both in every frame, and a wide-beam model."""
 import numpy as np
 import pytest
 
@@ -12,16 +12,16 @@ from lattice_util import canon_engine, canon_oracle
 
 pytestmark = pytest.mark.gpu
 
-FRAME_PATHS = {"default": None, "global": "0", "lds_then_rebuild": "1000000000"}
+FRAME_PATHS = {"default": None, "hbm": "0", "mixed": "2"}
 
 
 @pytest.fixture(params=sorted(FRAME_PATHS))
 def frame_path(request, monkeypatch):
     v = FRAME_PATHS[request.param]
     if v is None:
-        monkeypatch.delenv("VOSK_AMD_LDS_FRAME_TOKENS", raising=False)
+        monkeypatch.delenv("VOSK_AMD_DEC_LDS_PROBE", raising=False)
     else:
-        monkeypatch.setenv("VOSK_AMD_LDS_FRAME_TOKENS", v)
+        monkeypatch.setenv("VOSK_AMD_DEC_LDS_PROBE", v)
     return request.param
 
 

@@ -1,0 +1,1110 @@
+// Token passing on MI355X (gfx950): Kaldi LatticeFasterDecoder's per-frame
+// GetCutoff / ProcessEmitting / ProcessNonemitting over a CSR graph in HBM,
+// with Kaldi's forward links kept per stream for lattices, the best-path
+// traceback, and the periodic lattice pruning that keeps every stream's
+// arenas bounded (PruneActiveTokens).  Reference call sites:
+// src/recognizer.cc:39-43 (decoder), :318 (endpoint), :790 (best path);
+// src/batch_model.cc:78-80 (batch options).
+//
+// Per-stream state is bounded by the token counts, never by the graph size:
+// the frame under construction lives in an LDS open-addressing table (4096
+// slots); a state whose first kMaxProbe LDS slots are taken by other states
+// lives in a per-stream HBM hash table instead (two of them, ping-pong: the
+// current frame's HBM-resident tokens stay findable while the next frame is
+// built).  Placement is deterministic within a frame -- LDS slots are only
+// ever claimed, never released, during a frame, so every thread that relaxes
+// a state finds it in the same place -- and the table a state lands in has no
+// effect on any cost, key or backpointer, so results are those of the
+// order-independent formulation restated in oracle/oracle.c.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dev_util.h"
+#include "engine_dev.h"
+#include "kernels.h"
+
+namespace vamd {
+
+#ifndef VAMD_DEC_THREADS
+#define VAMD_DEC_THREADS 512
+#endif
+constexpr int DT = VAMD_DEC_THREADS;  // threads per decoder workgroup
+constexpr int DW = DT / 64;           // waves
+constexpr int kLlhLds = 4096;         // log-likelihood row staged in LDS up to this size
+constexpr int kTokLds = 1024;         // current-frame tokens cached in LDS up to this count
+constexpr int kHashCap = 4096;        // LDS frame table slots (power of two)
+constexpr int kHashBits = 12;
+constexpr int kMaxProbe = 32;         // default LDS probe limit (DecArgs::lds_probe); states past it live in HBM
+constexpr int kFrontLds = 2048;       // epsilon frontier entries in LDS (more spill to HBM)
+constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
+constexpr unsigned kDestEps = 0x80000000u;  // arcs[].w: nextstate has epsilon arcs
+
+struct DecShared {
+  int scan[DT + 1];   // exclusive prefix sums of the chunk's degrees
+  int abeg[DT];       // first arc per chunk token
+  float tcost[DT];    // cost per chunk token
+  int tsrc[DT];       // arena index per chunk token (lattice links)
+  unsigned hist[256];
+  unsigned long long red_u[DW];
+  float red_f[DW];
+  int red_i[DW];
+  int n_new_l, n_new_g, n_next, n_front, n_fnext, total, sel_k, n_links, lat_ovf, n_eps;
+  unsigned sel_prefix, sel_mask;
+  float seed;
+  int bad;
+};
+
+__device__ __forceinline__ float wave_min_f(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float block_min_f(DecShared& sh, float v) {
+  v = wave_min_f(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh.red_f[w] = v;
+  __syncthreads();
+  float r = sh.red_f[0];
+  for (int i = 1; i < DW; i++) r = fminf(r, sh.red_f[i]);
+  return r;
+}
+
+__device__ __forceinline__ unsigned long long block_min_u64(DecShared& sh, unsigned long long v) {
+  v = wave_min_u64(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh.red_u[w] = v;
+  __syncthreads();
+  unsigned long long r = sh.red_u[0];
+  for (int i = 1; i < DW; i++) r = sh.red_u[i] < r ? sh.red_u[i] : r;
+  return r;
+}
+
+__device__ __forceinline__ unsigned long long block_sum_u64(DecShared& sh, unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh.red_u[w] = v;
+  __syncthreads();
+  unsigned long long r = 0;
+  for (int i = 0; i < DW; i++) r += sh.red_u[i];
+  return r;
+}
+
+// exclusive scan of deg over the block; writes sh.scan[0..DT], sh.total
+__device__ __forceinline__ void block_scan(DecShared& sh, int deg) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int v = deg;
+  for (int o = 1; o < 64; o <<= 1) {
+    int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  __syncthreads();
+  if (lane == 63) sh.red_i[w] = v;
+  __syncthreads();
+  int off = 0;
+  for (int i = 0; i < w; i++) off += sh.red_i[i];
+  sh.scan[threadIdx.x] = off + v - deg;
+  if (threadIdx.x == DT - 1) {
+    sh.scan[DT] = off + v;
+    sh.total = off + v;
+  }
+  __syncthreads();
+}
+
+// token index j within the chunk that owns item `it` (largest j: scan[j] <= it)
+__device__ __forceinline__ int owner(const DecShared& sh, int it) {
+  int lo = 0, hi = DT - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (sh.scan[mid] <= it) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// current-frame tokens: LDS cache when they fit, else global (agent loads)
+struct TokView {
+  int* gs;
+  float* gc;
+  const int* ls;
+  const float* lc;
+  bool lds;
+  __device__ __forceinline__ int s(int i) const { return lds ? ls[i] : AG_LD(&gs[i]); }
+  __device__ __forceinline__ float c(int i) const { return lds ? lc[i] : AG_LD(&gc[i]); }
+};
+
+// exact k-th smallest (0-based) of the token costs by 4-pass 8-bit radix select
+__device__ __forceinline__ float kth_smallest(DecShared& sh, const TokView& tv, int n, int k) {
+  if (threadIdx.x == 0) {
+    sh.sel_prefix = 0;
+    sh.sel_mask = 0;
+    sh.sel_k = k;
+  }
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 256; i += DT) sh.hist[i] = 0;
+    __syncthreads();
+    const unsigned prefix = sh.sel_prefix, mask = sh.sel_mask;
+    for (int i = threadIdx.x; i < n; i += DT) {
+      const unsigned u = ford(tv.c(i));
+      if ((u & mask) == prefix) atomicAdd(&sh.hist[(u >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // wave 0: prefix over the 256 buckets (4 per lane)
+      const int l = threadIdx.x;
+      const int h0 = sh.hist[4 * l], h1 = sh.hist[4 * l + 1], h2 = sh.hist[4 * l + 2],
+                h3 = sh.hist[4 * l + 3];
+      const int tot = h0 + h1 + h2 + h3;
+      int incl = tot;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o, 64);
+        if (l >= o) incl += u;
+      }
+      const int excl = incl - tot;
+      const int kk = sh.sel_k;
+      if (kk >= excl && kk < incl) {  // exactly one lane holds the bucket
+        int r = kk - excl, b = 4 * l;
+        if (r >= h0) { r -= h0; b++;
+          if (r >= h1) { r -= h1; b++;
+            if (r >= h2) { r -= h2; b++; } } }
+        sh.sel_k = r;
+        sh.sel_prefix = prefix | ((unsigned)b << shift);
+        sh.sel_mask = mask | (255u << shift);
+      }
+    }
+  }
+  __syncthreads();
+  return funord(sh.sel_prefix);
+}
+
+// ---------------------------------------------------------------------------
+// frame tables
+// ---------------------------------------------------------------------------
+// LDS: the frame under construction (state, (cost, arc) key, list position,
+// epsilon round stamp, list of slots) and the previous frame's (state, list
+// position) pairs, double-buffered by swapping the pointers at each commit.
+struct FrameLds {
+  int* hs;                  // [kHashCap] state, -1 = empty
+  unsigned short* hp;       // [kHashCap] position in the frame's list
+  const int* ps;            // previous frame: state per slot
+  const unsigned short* pp; // previous frame: list position per slot
+  unsigned long long* hk;   // [kHashCap] (ordered cost << 32 | arc), kEmpty
+  int* hst;                 // [kHashCap] epsilon round stamp
+  unsigned short* nl;       // [kHashCap] list -> slot
+  int* fr0;                 // [kFrontLds] epsilon frontiers (tagged slots)
+  int* fr1;
+};
+
+// HBM: one of the stream's two overflow tables
+struct HbmTab {
+  int* state;               // [H] -1 = empty
+  unsigned long long* key;  // [H]
+  int* pos;                 // [H] creation index (list position - the frame's LDS count)
+  int* stamp;               // [H]
+  int* list;                // [max_tok] slots in creation order
+};
+
+__device__ __forceinline__ unsigned lds_hash(int s) {
+  return ((unsigned)s * 2654435761u) >> (32 - kHashBits);
+}
+// independent of lds_hash, so states crowded in LDS spread out in HBM
+__device__ __forceinline__ unsigned hbm_hash(int s, int bits) {
+  unsigned x = (unsigned)s * 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x >> (32 - bits);
+}
+
+// DecSlot's per-table list counts, selected without indexing (an indexed
+// array in a register struct would be placed in scratch)
+__device__ __forceinline__ int tab_n(const DecSlot& st, int t) { return t ? st.tab_n1 : st.tab_n0; }
+__device__ __forceinline__ void set_tab_n(DecSlot& st, int t, int v) {
+  if (t) st.tab_n1 = v;
+  else st.tab_n0 = v;
+}
+
+struct DecPtrs {
+  int* cs;     // current tokens: state
+  float* cc;   //                 cost
+  int* cp;     //                 list position (arena index = cur_base + cp)
+  int4* arena; // {prev, arc, cost bits, state} per token of the segment
+  int* fg0;    // HBM frontier spill [max_tok]
+  int* fg1;
+  int slot;
+};
+
+// HBM table t (0 or 1) of a stream: plain address arithmetic (no indexed
+// struct arrays, which would live in scratch)
+__device__ __forceinline__ HbmTab hbm_tab(const DecArgs& a, int slot, int t) {
+  const long long H = 1ll << a.hbits;
+  const long long o = ((long long)slot * 2 + t) * H;
+  HbmTab r;
+  r.state = a.ht_state + o;
+  r.key = a.ht_key + o;
+  r.pos = a.ht_pos + o;
+  r.stamp = a.ht_stamp + o;
+  r.list = a.ht_list + ((long long)slot * 2 + t) * a.max_tok;
+  return r;
+}
+
+// result of a relaxation: slot >= 0 LDS slot, < 0 ~(HBM slot);
+// flags 2 created, 1 improved, 0 not improved, -1 no room (sh.bad set)
+struct Relax {
+  int slot, flags;
+};
+
+__device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                       const HbmTab& T, int dest, float tot, int arc) {
+  const unsigned long long k = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
+  unsigned h = lds_hash(dest);
+  for (int probe = 0; probe < a.lds_probe; probe++) {
+    int cur = __hip_atomic_load(&t.hs[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cur == -1) {
+      cur = atomicCAS(&t.hs[h], -1, dest);
+      if (cur == -1) {
+        const int pos = atomicAdd(&sh.n_new_l, 1);  // < kHashCap: one per claimed slot
+        t.nl[pos] = (unsigned short)h;
+        t.hp[h] = (unsigned short)pos;
+        atomicMin(&t.hk[h], k);
+        return Relax{(int)h, 2};
+      }
+    }
+    if (cur == dest) {
+      const unsigned long long old = atomicMin(&t.hk[h], k);
+      return Relax{(int)h, k < old ? 1 : 0};
+    }
+    h = (h + 1) & (kHashCap - 1);
+  }
+  const unsigned hm = (1u << a.hbits) - 1u;
+  unsigned g = hbm_hash(dest, a.hbits);
+  for (int probe = 0; probe < a.hprobe; probe++) {
+    int cur = AG_LD(&T.state[g]);
+    if (cur == -1) {
+      cur = atomicCAS(&T.state[g], -1, dest);
+      if (cur == -1) {
+        const int pos = atomicAdd(&sh.n_new_g, 1);
+        if (pos < a.max_tok) {
+          AG_ST(&T.list[pos], (int)g);
+          AG_ST(&T.pos[g], pos);
+        } else {
+          sh.bad |= 1;
+        }
+        atomicMin(&T.key[g], k);
+        return Relax{~(int)g, 2};
+      }
+    }
+    if (cur == dest) {
+      const unsigned long long old = atomicMin(&T.key[g], k);
+      return Relax{~(int)g, k < old ? 1 : 0};
+    }
+    g = (g + 1) & hm;
+  }
+  sh.bad |= 1;
+  return Relax{0, -1};
+}
+
+__device__ __forceinline__ unsigned long long slot_key(const FrameLds& t, const HbmTab& T, int v) {
+  return v >= 0 ? t.hk[v] : AG_LD(&T.key[~v]);
+}
+__device__ __forceinline__ int slot_state(const FrameLds& t, const HbmTab& T, int v) {
+  return v >= 0 ? t.hs[v] : AG_LD(&T.state[~v]);
+}
+
+// list position of state s in the frame under construction (nl_n = its LDS count)
+__device__ __forceinline__ int frame_pos(const DecArgs& a, const FrameLds& t, const HbmTab& T, int nl_n, int s) {
+  unsigned h = lds_hash(s);
+  for (int probe = 0; probe < a.lds_probe; probe++) {
+    const int c = t.hs[h];
+    if (c == s) return t.hp[h];
+    if (c == -1) break;
+    h = (h + 1) & (kHashCap - 1);
+  }
+  const unsigned hm = (1u << a.hbits) - 1u;
+  unsigned g = hbm_hash(s, a.hbits);
+  for (int probe = 0; probe < a.hprobe; probe++) {
+    const int c = AG_LD(&T.state[g]);
+    if (c == s) return nl_n + AG_LD(&T.pos[g]);
+    if (c == -1) break;
+    g = (g + 1) & hm;
+  }
+  return -1;
+}
+
+// list position of state s in the current (committed) frame: the previous
+// LDS table, else the HBM table of the current frame (cur_tab)
+__device__ __forceinline__ int prev_pos(const DecArgs& a, const FrameLds& t, const DecPtrs& p, const DecSlot& st,
+                        int s) {
+  unsigned h = lds_hash(s);
+  for (int probe = 0; probe < a.lds_probe; probe++) {
+    const int c = t.ps[h];
+    if (c == s) return t.pp[h];
+    if (c == -1) break;
+    h = (h + 1) & (kHashCap - 1);
+  }
+  if (st.cur_tab < 0) return -1;
+  const HbmTab T = hbm_tab(a, p.slot, st.cur_tab);
+  const unsigned hm = (1u << a.hbits) - 1u;
+  unsigned g = hbm_hash(s, a.hbits);
+  for (int probe = 0; probe < a.hprobe; probe++) {
+    const int c = AG_LD(&T.state[g]);
+    if (c == s) return st.cur_nl + AG_LD(&T.pos[g]);
+    if (c == -1) break;
+    g = (g + 1) & hm;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void push_front(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                           const DecPtrs& p, int b, int* count, int v) {
+  const int q = atomicAdd(count, 1);
+  if (q < kFrontLds) (b ? t.fr1 : t.fr0)[q] = v;
+  else if (q - kFrontLds < a.max_tok) AG_ST(&(b ? p.fg1 : p.fg0)[q - kFrontLds], v);
+  else sh.bad |= 1;
+}
+__device__ __forceinline__ int get_front(const FrameLds& t, const DecPtrs& p, int b, int i) {
+  return i < kFrontLds ? (b ? t.fr1 : t.fr0)[i] : AG_LD(&(b ? p.fg1 : p.fg0)[i - kFrontLds]);
+}
+
+// ---------------------------------------------------------------------------
+// lattice links.  During the emitting pass every relaxation below the bound
+// appends {src arena index, tot bits, arc, acoustic cost bits} to the
+// stream's link arena; the commit keeps those below the frame's final cutoff
+// with tot replaced by the destination's arena index, then appends the
+// frame's epsilon links from the final token costs (one per arc, Kaldi
+// re-expands a token whenever it improves: ProcessNonemitting).  A committed
+// link is {src arena index, dst arena index, arc, acoustic cost bits}.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long long used, int slot,
+                                          int4 rec) {
+  const unsigned long long m = __ballot(1);
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(&sh.n_links, __popcll(m));
+  base = __shfl(base, leader, 64);
+  const int off = __popcll(m & ((1ull << lane) - 1ull));
+  const long long pos = used + base + off;
+  if (pos < a.link_cap) a.links[(long long)slot * a.link_cap + pos] = rec;
+  else sh.lat_ovf = 1;
+}
+
+// one emitting expansion pass over the current tokens (ProcessEmitting):
+// mode 0 = minimum only, 1 = relax below `bound` (+ minimum)
+__device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                 const HbmTab& T, const DecPtrs& p, const TokView& tv, int ntok,
+                                 float cutoff, float cost_offset, const float* Lp, int mode,
+                                 float bound, int* examined, const DecSlot& st, int slot) {
+  float m = __int_as_float(0x7f800000);
+  const bool lat = a.links != nullptr && mode == 1;
+  for (int c0 = 0; c0 < ntok; c0 += DT) {
+    const int i = c0 + threadIdx.x;
+    int deg = 0, ab = 0, src = 0;
+    float c = 0.0f;
+    if (i < ntok) {
+      c = tv.c(i);
+      if (c <= cutoff) {
+        const int4 si = a.sinfo[tv.s(i)];
+        ab = si.x;
+        deg = si.y - si.x;
+        if (lat) src = st.cur_base + AG_LD(&p.cp[i]);
+      }
+    }
+    block_scan(sh, deg);
+    sh.abeg[threadIdx.x] = ab;
+    sh.tcost[threadIdx.x] = c;
+    sh.tsrc[threadIdx.x] = src;
+    __syncthreads();
+    const int total = sh.total;
+    *examined += total;
+    for (int it = threadIdx.x; it < total; it += DT) {
+      const int j = owner(sh, it);
+      const int arc = sh.abeg[j] + (it - sh.scan[j]);
+      const int4 A = a.arcs[arc];
+      const float ac = cost_offset - Lp[A.z];
+      const float tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
+      m = fminf(m, tot);
+      if (mode == 1 && tot < bound) {
+        if (lat)
+          emit_link(a, sh, st.links_used, slot,
+                    make_int4(sh.tsrc[j], __float_as_int(tot), arc, __float_as_int(ac)));
+        const Relax r = relax(a, sh, t, T, A.x, tot, arc);
+        if (r.flags == 2 && ((unsigned)A.w & kDestEps))
+          push_front(a, sh, t, p, 0, &sh.n_front, r.slot);
+      }
+    }
+    __syncthreads();
+  }
+  return block_min_f(sh, m);
+}
+
+// ProcessNonemitting: epsilon closure in rounds over frontiers that only
+// hold states with epsilon arcs (round 0: created by the emitting pass);
+// a state improved in a round is expanded again in the next one.
+__device__ __forceinline__ void eps_closure(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
+                            const DecPtrs& p, DecSlot& st, float cutoff, int nfront, int* arcs_eps) {
+  int b = 0;
+  int examined = 0;
+  const int cap = kFrontLds + a.max_tok;
+  nfront = nfront < cap ? nfront : cap;
+  while (nfront > 0) {
+    st.stamp++;
+    const int stamp = st.stamp;
+    __syncthreads();
+    if (threadIdx.x == 0) sh.n_fnext = 0;
+    for (int c0 = 0; c0 < nfront; c0 += DT) {
+      const int i = c0 + threadIdx.x;
+      int deg = 0, ab = 0;
+      float c = 0.0f;
+      if (i < nfront) {
+        const int v = get_front(t, p, b, i);
+        c = funord((uint32_t)(slot_key(t, T, v) >> 32));
+        if (c < cutoff) {  // created tokens are < cutoff; dead ones are not
+          const int4 si = a.sinfo[slot_state(t, T, v)];
+          ab = si.y;
+          deg = si.z - si.y;
+        }
+      }
+      block_scan(sh, deg);
+      sh.abeg[threadIdx.x] = ab;
+      sh.tcost[threadIdx.x] = c;
+      __syncthreads();
+      const int total = sh.total;
+      examined += total;
+      for (int it = threadIdx.x; it < total; it += DT) {
+        const int j = owner(sh, it);
+        const int arc = sh.abeg[j] + (it - sh.scan[j]);
+        const int4 A = a.arcs[arc];
+        const float tot = sh.tcost[j] + __int_as_float(A.y);
+        if (tot < cutoff) {
+          const Relax r = relax(a, sh, t, T, A.x, tot, arc);
+          if (r.flags > 0 && ((unsigned)A.w & kDestEps)) {
+            const int old = r.slot >= 0 ? atomicExch(&t.hst[r.slot], stamp)
+                                        : atomicExch(&T.stamp[~r.slot], stamp);
+            if (old != stamp) push_front(a, sh, t, p, b ^ 1, &sh.n_fnext, r.slot);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    nfront = sh.n_fnext < cap ? sh.n_fnext : cap;
+    b ^= 1;
+  }
+  *arcs_eps += examined;
+}
+
+__device__ __forceinline__ void lds_clear_build(const FrameLds& t) {
+  for (int h = threadIdx.x; h < kHashCap; h += DT) {
+    t.hs[h] = -1;
+    t.hk[h] = kEmpty;
+    t.hst[h] = 0;
+  }
+}
+
+// clears the listed entries of an HBM table
+__device__ __forceinline__ void hbm_clear_listed(const HbmTab& T, int n) {
+  for (int j = threadIdx.x; j < n; j += DT) {
+    const int g = AG_LD(&T.list[j]);
+    AG_ST(&T.state[g], -1);
+    AG_ST(&T.key[g], kEmpty);
+  }
+}
+__device__ __forceinline__ void hbm_clear_all(const DecArgs& a, const HbmTab& T) {
+  const int H = 1 << a.hbits;
+  for (int g = threadIdx.x; g < H; g += DT) {
+    AG_ST(&T.state[g], -1);
+    AG_ST(&T.key[g], kEmpty);
+    AG_ST(&T.stamp[g], -1);
+  }
+}
+
+// Lattice side of a commit (all threads; the frame tables are still intact):
+// keep this frame's emitting records below the cutoff, resolved to arena
+// indices (chunked in-place compaction: writes never pass the chunk being
+// read), then the epsilon links of the committed tokens.  Returns the
+// frame's link count.
+__device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
+                            const DecPtrs& p, const DecSlot& st, const int* TS, const float* TC,
+                            int slot, int base, int nl_n, int live, float cutoff) {
+  int4* L = a.links + (long long)slot * a.link_cap;
+  const long long lb = st.links_used;
+  long long nrec = sh.n_links;
+  if (lb + nrec > a.link_cap) nrec = a.link_cap - lb > 0 ? a.link_cap - lb : 0;
+  int out = 0;
+  for (long long c0 = 0; c0 < nrec; c0 += DT) {
+    const long long i = c0 + threadIdx.x;
+    int keep = 0;
+    int4 r = make_int4(0, 0, 0, 0);
+    if (i < nrec) {
+      r = L[lb + i];
+      if (__int_as_float(r.y) < cutoff) {
+        const int d = frame_pos(a, t, T, nl_n, a.arcs[r.z].x);
+        if (d >= 0) {
+          r.y = base + d;
+          keep = 1;
+        }
+      }
+    }
+    block_scan(sh, keep);
+    if (keep) L[lb + out + sh.scan[threadIdx.x]] = r;
+    out += sh.total;
+    __syncthreads();
+  }
+  // epsilon links of the committed tokens, at their final costs
+  if (threadIdx.x == 0) sh.n_eps = 0;
+  for (int c0 = 0; c0 < live; c0 += DT) {
+    const int q = c0 + threadIdx.x;
+    int deg = 0, ab = 0, src = 0;
+    float c = 0.0f;
+    if (q < live) {
+      const int s = q < kTokLds ? TS[q] : AG_LD(&p.cs[q]);
+      c = q < kTokLds ? TC[q] : AG_LD(&p.cc[q]);
+      const int4 si = a.sinfo[s];
+      ab = si.y;
+      deg = si.z - si.y;
+      src = base + AG_LD(&p.cp[q]);
+    }
+    block_scan(sh, deg);
+    sh.abeg[threadIdx.x] = ab;
+    sh.tcost[threadIdx.x] = c;
+    sh.tsrc[threadIdx.x] = src;
+    __syncthreads();
+    const int total = sh.total;
+    for (int it = threadIdx.x; it < total; it += DT) {
+      const int j = owner(sh, it);
+      const int arc = sh.abeg[j] + (it - sh.scan[j]);
+      const int4 A = a.arcs[arc];
+      const float tot = sh.tcost[j] + __int_as_float(A.y);
+      if (tot < cutoff) {
+        const int d = frame_pos(a, t, T, nl_n, A.x);
+        const unsigned long long m = __ballot(1);
+        const int lane = threadIdx.x & 63;
+        const int leader = __ffsll((long long)m) - 1;
+        int w0 = 0;
+        if (lane == leader) w0 = atomicAdd(&sh.n_eps, __popcll(m));
+        w0 = __shfl(w0, leader, 64);
+        const long long pos = lb + out + w0 + __popcll(m & ((1ull << lane) - 1ull));
+        if (pos < a.link_cap && d >= 0) L[pos] = make_int4(sh.tsrc[j], base + d, arc, 0);
+        else sh.lat_ovf = 1;
+      }
+    }
+    __syncthreads();
+  }
+  const int n = out + sh.n_eps;
+  if (nrec < sh.n_links || lb + n > a.link_cap) sh.lat_ovf = 1;
+  return lb + n > a.link_cap ? (int)(a.link_cap - lb) : n;
+}
+
+// Move the frame under construction into the arena + current token arrays
+// (global, and the LDS cache when it fits).  List entries whose cost is not
+// below `cutoff` (dead: created by the single emitting pass above the final
+// next_cutoff) keep an arena slot marked dead.  Then the previous frame's
+// HBM table is cleared and the LDS tables swap roles.
+__device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds& t, DecPtrs& p, DecSlot& st,
+                       int* TS, float* TC, bool* lds, float cutoff, float* best_out, int slot,
+                       int y, int* nlinks) {
+  __syncthreads();
+  const HbmTab T = hbm_tab(a, slot, y);
+  const int nl_n = sh.n_new_l;
+  const int ng = sh.n_new_g < a.max_tok ? sh.n_new_g : a.max_tok;
+  const int n = nl_n + ng;
+  const int base = st.arena_used;
+  const bool ok = (long long)base + n <= a.arena_cap;
+  if (threadIdx.x == 0) sh.n_next = 0;
+  __syncthreads();
+  unsigned long long bk = kEmpty;
+  for (int j = threadIdx.x; j < n; j += DT) {
+    int s;
+    unsigned long long k;
+    if (j < nl_n) {
+      const int h = t.nl[j];
+      s = t.hs[h];
+      k = t.hk[h];
+    } else {
+      const int g = AG_LD(&T.list[j - nl_n]);
+      s = AG_LD(&T.state[g]);
+      k = AG_LD(&T.key[g]);
+    }
+    const int arc = (int)(unsigned)(k & 0xffffffffu);
+    const float cost = funord((uint32_t)(k >> 32));
+    if (ok && cost < cutoff) {
+      int prev = -1;
+      if (arc >= 0) {
+        const int4 A = a.arcs[arc];
+        const int src = (int)((unsigned)A.w & 0x7fffffffu);
+        if (A.z >= 0) {
+          const int pp = prev_pos(a, t, p, st, src);
+          prev = pp >= 0 ? st.cur_base + pp : -1;
+        } else {
+          const int fp = frame_pos(a, t, T, nl_n, src);
+          prev = fp >= 0 ? base + fp : -1;
+        }
+        if (prev < 0) sh.bad |= 8;  // a source the tables cannot place (never expected)
+      }
+      p.arena[base + j] = make_int4(prev, arc, __float_as_int(cost), s);
+      const int q = atomicAdd(&sh.n_next, 1);
+      AG_ST(&p.cs[q], s);
+      AG_ST(&p.cc[q], cost);
+      AG_ST(&p.cp[q], j);
+      if (q < kTokLds) {
+        TS[q] = s;
+        TC[q] = cost;
+      }
+      const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)s;
+      bk = tk < bk ? tk : bk;
+    } else if (ok) {
+      p.arena[base + j] = make_int4(-2, -1, __float_as_int(cost), s);  // dead list entry
+    }
+  }
+  bk = block_min_u64(sh, bk);  // ends with a barrier
+  if (!ok) sh.bad |= 2;
+  const int live = sh.n_next;
+  *nlinks = (a.links && ok) ? commit_links(a, sh, t, T, p, st, TS, TC, slot, base, nl_n, live, cutoff)
+                            : 0;
+  // the previous frame's HBM table has served its lookups
+  if (st.cur_tab >= 0) hbm_clear_listed(hbm_tab(a, slot, st.cur_tab), tab_n(st, st.cur_tab));
+  __syncthreads();
+  // swap: the frame just built becomes the previous frame
+  int* ohs = const_cast<int*>(t.ps);
+  unsigned short* ohp = const_cast<unsigned short*>(t.pp);
+  t.ps = t.hs;
+  t.pp = t.hp;
+  t.hs = ohs;
+  t.hp = ohp;
+  lds_clear_build(t);
+  __syncthreads();
+  if (st.cur_tab >= 0) set_tab_n(st, st.cur_tab, 0);
+  if (ok) {
+    st.cur_base = base;
+    st.arena_used = base + n;
+    st.ntok = live;
+  } else {
+    st.ntok = 0;
+  }
+  st.cur_tab = ng > 0 ? y : -1;
+  if (ng > 0) set_tab_n(st, y, ng);
+  st.cur_nl = nl_n;
+  *lds = live <= kTokLds;
+  st.best_key = bk;  // GetCutoff's best token of the next frame
+  *best_out = funord((uint32_t)(bk >> 32));
+}
+
+// End of a launch: the LDS-resident tokens of the current frame move into its
+// HBM table so that the next launch (whose LDS starts empty) finds them.
+__device__ __forceinline__ void flush_prev(const DecArgs& a, DecShared& sh, const FrameLds& t, DecPtrs& p,
+                           DecSlot& st) {
+  __syncthreads();
+  if (st.cur_nl == 0) return;
+  const int y = st.cur_tab >= 0 ? st.cur_tab : 0;
+  const HbmTab T = hbm_tab(a, p.slot, y);
+  if (threadIdx.x == 0) sh.n_new_g = st.cur_tab >= 0 ? tab_n(st, y) : 0;
+  __syncthreads();
+  const unsigned hm = (1u << a.hbits) - 1u;
+  for (int h = threadIdx.x; h < kHashCap; h += DT) {
+    const int s = t.ps[h];
+    if (s < 0) continue;
+    unsigned g = hbm_hash(s, a.hbits);
+    bool done = false;
+    for (int probe = 0; probe < a.hprobe && !done; probe++) {
+      if (atomicCAS(&T.state[g], -1, s) == -1) {
+        const int q = atomicAdd(&sh.n_new_g, 1);
+        if (q < a.max_tok) AG_ST(&T.list[q], (int)g);
+        else sh.bad |= 1;
+        AG_ST(&T.pos[g], (int)t.pp[h] - st.cur_nl);  // cur_nl + pos = the LDS position
+        done = true;
+      } else {
+        g = (g + 1) & hm;
+      }
+    }
+    if (!done) sh.bad |= 1;
+  }
+  __syncthreads();
+  st.cur_tab = y;
+  set_tab_n(st, y, sh.n_new_g < a.max_tok ? sh.n_new_g : a.max_tok);
+}
+
+// after a commit (all threads, past its barriers): the frame's lattice
+// record; every thread advances its copy of links_used identically
+__device__ __forceinline__ void lat_frame_done(const DecArgs& a, DecShared& sh, DecSlot& st, int slot, int index,
+                               float cutoff, float cost_offset, int nl) {
+  if (threadIdx.x == 0 && index < a.lat_frame_cap) {
+    LatFrame F;
+    F.tok_base = st.cur_base;
+    F.ntok = st.arena_used - st.cur_base;
+    F.link_begin = st.links_used;
+    F.link_end = st.links_used + nl;
+    F.cutoff = cutoff;
+    F.cost_offset = cost_offset;
+    F.pad0 = F.pad1 = 0;
+    a.lat_frames[(long long)slot * a.lat_frame_cap + index] = F;
+  }
+  if (index >= a.lat_frame_cap || sh.lat_ovf) st.lat_ovf = 1;
+  st.links_used += nl;
+}
+
+template <bool PROF>
+__global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
+  __shared__ DecShared sh;
+  __shared__ float L[kLlhLds];
+  __shared__ int TS[kTokLds];
+  __shared__ float TC[kTokLds];
+  __shared__ int t_hs[2][kHashCap];
+  __shared__ unsigned short t_hp[2][kHashCap];
+  __shared__ unsigned long long t_hk[kHashCap];
+  __shared__ int t_hst[kHashCap];
+  __shared__ unsigned short t_nl[kHashCap];
+  __shared__ int t_fr[2][kFrontLds];
+  FrameLds t;
+  t.hs = t_hs[0];
+  t.hp = t_hp[0];
+  t.ps = t_hs[1];
+  t.pp = t_hp[1];
+  t.hk = t_hk;
+  t.hst = t_hst;
+  t.nl = t_nl;
+  t.fr0 = t_fr[0];
+  t.fr1 = t_fr[1];
+  lds_clear_build(t);
+  for (int h = threadIdx.x; h < kHashCap; h += DT) t_hs[1][h] = -1;
+  const DecJob job = a.jobs[blockIdx.x];
+  const int slot = job.slot;
+  DecSlot st = a.slots[slot];
+  DecPtrs p;
+  p.cs = a.cur_state + (long long)slot * a.max_tok;
+  p.cc = a.cur_cost + (long long)slot * a.max_tok;
+  p.cp = a.cur_pos + (long long)slot * a.max_tok;
+  p.arena = a.arena + (long long)slot * a.arena_cap;
+  p.fg0 = a.front_g + ((long long)slot * 2) * a.max_tok;
+  p.fg1 = p.fg0 + a.max_tok;
+  p.slot = slot;
+  if (threadIdx.x == 0) {
+    sh.bad = 0;
+    sh.n_links = 0;
+    sh.lat_ovf = 0;
+  }
+  int arcs_eps = 0;
+  bool lds = false;
+  // optional phase clocks (diagnostics): thread 0 stamps s_memtime
+  const bool prof = PROF && threadIdx.x == 0;
+  long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tstamp = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
+#define DEC_PHASE(i)                                                     \
+  if (prof) {                                                            \
+    const long long _t = (long long)__builtin_amdgcn_s_memtime();        \
+    pacc[i] += _t - tstamp;                                              \
+    tstamp = _t;                                                         \
+  }
+
+  if (job.reset) {  // InitDecoding: start token, closure with cutoff = beam
+    __syncthreads();
+    if (st.err) {  // an overflow may have left unlisted entries: clear everything
+      hbm_clear_all(a, hbm_tab(a, slot, 0));
+      hbm_clear_all(a, hbm_tab(a, slot, 1));
+    } else if (st.cur_tab >= 0) {
+      hbm_clear_listed(hbm_tab(a, slot, st.cur_tab), tab_n(st, st.cur_tab));
+    }
+    st.ntok = 0;
+    st.cur_base = 0;
+    st.arena_used = 0;
+    st.frames = 0;
+    st.offset_sum = 0.0;
+    st.err = 0;
+    st.links_used = 0;
+    st.lat_ovf = 0;
+    st.cur_tab = -1;
+    st.tab_n0 = st.tab_n1 = 0;
+    st.cur_nl = 0;
+    st.seg_base = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      sh.n_new_l = 0;
+      sh.n_new_g = 0;
+      sh.n_front = 0;
+      sh.n_links = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const Relax r = relax(a, sh, t, hbm_tab(a, slot, 0), a.start_state, 0.0f, -1);
+      t.fr0[0] = r.slot;
+      sh.n_front = 1;
+    }
+    eps_closure(a, sh, t, hbm_tab(a, slot, 0), p, st, a.beam, 1, &arcs_eps);
+    float b;
+    int nl = 0;
+    commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, 0, &nl);
+    if (a.links) lat_frame_done(a, sh, st, slot, 0, a.beam, 0.0f, nl);
+  } else if (st.ntok > 0 && st.ntok <= kTokLds) {
+    for (int i = threadIdx.x; i < st.ntok; i += DT) {
+      TS[i] = AG_LD(&p.cs[i]);
+      TC[i] = AG_LD(&p.cc[i]);
+    }
+    lds = true;
+  }
+
+  // log-likelihood rows staged in LDS: row f+1 is loaded into registers
+  // while frame f is processed and written to L once frame f's emitting
+  // expansion no longer reads it (just before its commit)
+  constexpr int kLlhRegs = kLlhLds / DT;
+  const bool stage_llh = a.P <= kLlhLds;
+  float nxt[kLlhRegs];
+  if (stage_llh && job.nframes > 0) {
+    const float* llh0 = a.llh + (size_t)job.llh_row0 * a.P;
+    for (int i = threadIdx.x; i < a.P; i += DT) L[i] = llh0[i];
+  }
+  for (int f = 0; f < job.nframes; f++) {
+    if (st.ntok == 0 || st.err) break;
+    const float* llh = a.llh + (size_t)(job.llh_row0 + f) * a.P;
+    const float* Lp = stage_llh ? L : llh;
+    const bool pf = stage_llh && f + 1 < job.nframes;
+    if (pf) {
+      const float* nrow = llh + a.P;
+#pragma unroll
+      for (int r = 0; r < kLlhRegs; r++) {
+        const int i = threadIdx.x + r * DT;
+        nxt[r] = i < a.P ? nrow[i] : 0.0f;
+      }
+    }
+    const int ntok = st.ntok;
+    const TokView tv{p.cs, p.cc, TS, TC, lds};
+    // ---- GetCutoff (best token: min (cost, state), kept by the previous commit)
+    const unsigned long long bk = st.best_key;
+    const float best = funord((uint32_t)(bk >> 32));
+    const int best_state = (int)(unsigned)(bk & 0xffffffffu);
+    const float beam_cutoff = best + a.beam;
+    float max_cut = __int_as_float(0x7f800000), min_cut = __int_as_float(0x7f800000);
+    float adaptive, cutoff;
+    // The k-th smallest cost is only needed when it can change the outcome:
+    // max_cut < beam_cutoff  <=>  more than max_active costs are < beam_cutoff,
+    // min_cut > beam_cutoff  <=>  at most min_active costs are <= beam_cutoff.
+    bool need_max = ntok > a.max_active, need_min = ntok > a.min_active && a.min_active > 0;
+    if (need_max || need_min) {
+      unsigned long long cnt = 0;  // (# cost < beam_cutoff) << 32 | # cost <= beam_cutoff
+      for (int i = threadIdx.x; i < ntok; i += DT) {
+        const float c = tv.c(i);
+        cnt += ((unsigned long long)(c < beam_cutoff) << 32) | (unsigned)(c <= beam_cutoff);
+      }
+      cnt = block_sum_u64(sh, cnt);
+      const int n_lt = (int)(cnt >> 32), n_le = (int)(unsigned)(cnt & 0xffffffffu);
+      need_max = need_max && n_lt > a.max_active;
+      need_min = need_min && n_le <= a.min_active;
+    } else {
+      __syncthreads();  // the LLH row staged above is read by wave 0 below
+    }
+    if (need_max) max_cut = kth_smallest(sh, tv, ntok, a.max_active);
+    if (max_cut < beam_cutoff) {
+      adaptive = max_cut - best + a.beam_delta;
+      cutoff = max_cut;
+    } else {
+      if (ntok > a.min_active)
+        min_cut = a.min_active == 0 ? best
+                  : need_min ? kth_smallest(sh, tv, ntok, a.min_active)
+                             : beam_cutoff;  // proven <= beam_cutoff: the exact value is unused
+      if (min_cut > beam_cutoff) {
+        adaptive = min_cut - best + a.beam_delta;
+        cutoff = min_cut;
+      } else {
+        adaptive = a.beam;
+        cutoff = beam_cutoff;
+      }
+    }
+    const float cost_offset = -best;
+    DEC_PHASE(0);
+    // ---- ProcessEmitting: Kaldi's seed from the best token's arcs (wave 0)
+    if (threadIdx.x < 64) {
+      float sd = __int_as_float(0x7f800000);
+      const int4 si = a.sinfo[best_state];
+      for (int arc = si.x + (int)threadIdx.x; arc < si.y; arc += 64) {
+        const int4 A = a.arcs[arc];
+        const float nw = ((__int_as_float(A.y) + cost_offset) - Lp[A.z]) + best;
+        sd = fminf(sd, nw + adaptive);
+      }
+      sd = wave_min_f(sd);
+      if (threadIdx.x == 0) {
+        sh.seed = sd;
+        sh.n_new_l = 0;
+        sh.n_new_g = 0;
+        sh.n_front = 0;
+        sh.n_links = 0;
+      }
+    }
+    __syncthreads();
+    DEC_PHASE(1);
+    const float seed = sh.seed;
+    int examined = 0;
+    float next_cutoff, new_best;
+    // one emitting pass relaxing below the seed bound (a superset), then the
+    // epsilon closure; tokens whose best cost is not below the final
+    // next_cutoff stay as dead list entries (never expanded: cost >= cutoff)
+    // and are dropped at commit -- exactly the tokens a relax-below-
+    // next_cutoff pass creates, with the same keys.  Without a finite seed
+    // the exact two-pass form runs.
+    const int y = st.cur_tab == 0 ? 1 : 0;  // HBM table of the frame under construction
+    const HbmTab T = hbm_tab(a, slot, y);
+    if (seed != __int_as_float(0x7f800000)) {
+      const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
+                                      &examined, st, slot);
+      next_cutoff = seed;
+      if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
+    } else {
+      const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
+                                      &examined, st, slot);
+      next_cutoff = seed;
+      if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
+      int dummy = 0;
+      expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy, st,
+                      slot);
+    }
+    __syncthreads();
+    DEC_PHASE(2);
+    if (prof) pacc[3] += sh.n_new_l + sh.n_new_g;  // tokens created by the emitting pass
+    if (prof) pacc[6] += sh.n_new_g;               // of them in the HBM table
+    eps_closure(a, sh, t, T, p, st, next_cutoff, sh.n_front, &arcs_eps);
+    __syncthreads();
+    DEC_PHASE(4);
+    if (pf) {  // L is not read again in this frame
+#pragma unroll
+      for (int r = 0; r < kLlhRegs; r++) {
+        const int i = threadIdx.x + r * DT;
+        if (i < a.P) L[i] = nxt[r];
+      }
+    }
+    int nl = 0;
+    commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, y, &nl);
+    DEC_PHASE(5);
+    if (prof) pacc[7]++;
+    if (a.links) lat_frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset, nl);
+    st.offset_sum += (double)cost_offset;
+    st.frames++;
+    if (threadIdx.x == 0 && a.stats) {
+      FrameStat fs;
+      fs.ntok_in = ntok;
+      fs.ntok_out = st.ntok;
+      fs.arcs_emit = examined;
+      fs.arcs_eps = arcs_eps;
+      fs.best = new_best;
+      fs.cutoff = cutoff;
+      fs.next_cutoff = next_cutoff;
+      fs.adaptive_beam = adaptive;
+      a.stats[job.stats_row0 + f] = fs;
+    }
+    arcs_eps = 0;
+    __syncthreads();
+    if (sh.bad) st.err |= sh.bad;
+  }
+  __syncthreads();
+  if (sh.bad) st.err |= sh.bad;
+  if (st.ntok == 0 && !st.err) st.err |= 4;
+  if (!st.err) flush_prev(a, sh, t, p, st);
+  __syncthreads();
+  if (sh.bad) st.err |= sh.bad;
+  if (threadIdx.x == 0) a.slots[slot] = st;
+  if (prof)
+    for (int i = 0; i < 8; i++) a.prof[slot * 8 + i] += pacc[i];
+#undef DEC_PHASE
+}
+
+int DecoderLdsProbe() { return kMaxProbe; }
+
+void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s) {
+  if (njobs <= 0) return;
+  if (a.prof) hipLaunchKernelGGL(decode_kernel<true>, dim3(njobs), dim3(DT), 0, s, a);
+  else hipLaunchKernelGGL(decode_kernel<false>, dim3(njobs), dim3(DT), 0, s, a);
+}
+
+// ---------------------------------------------------------------------------
+// traceback: best end token (with final costs if any is final), then walk
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void traceback_kernel(TraceArgs a) {
+  __shared__ unsigned long long red[4];
+  __shared__ float redf[4][2];
+  __shared__ int endpos;
+  const int slot = a.req_slot[blockIdx.x];
+  const DecSlot st = a.slots[slot];
+  const int* cs = a.cur_state + (long long)slot * a.max_tok;
+  const float* cc = a.cur_cost + (long long)slot * a.max_tok;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float bn = __int_as_float(0x7f800000), bf = __int_as_float(0x7f800000);
+  for (int i = threadIdx.x; i < st.ntok; i += 256) {
+    const float c = cc[i];
+    bn = fminf(bn, c);
+    const float fc = __int_as_float(a.sinfo[cs[i]].w);
+    if (fc != __int_as_float(0x7f800000)) bf = fminf(bf, c + fc);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    bn = fminf(bn, __shfl_xor(bn, o, 64));
+    bf = fminf(bf, __shfl_xor(bf, o, 64));
+  }
+  if (lane == 0) { redf[w][0] = bn; redf[w][1] = bf; }
+  __syncthreads();
+  bn = fminf(fminf(redf[0][0], redf[1][0]), fminf(redf[2][0], redf[3][0]));
+  bf = fminf(fminf(redf[0][1], redf[1][1]), fminf(redf[2][1], redf[3][1]));
+  const bool any_final = bf != __int_as_float(0x7f800000);
+  const bool use_f = a.use_final && any_final;
+  unsigned long long bk = kEmpty;
+  for (int i = threadIdx.x; i < st.ntok; i += 256) {
+    float c = cc[i];
+    if (use_f) c = c + __int_as_float(a.sinfo[cs[i]].w);
+    const unsigned long long k = ((unsigned long long)ford(c) << 32) | (unsigned)cs[i];
+    bk = k < bk ? k : bk;
+  }
+  bk = wave_min_u64(bk);
+  if (lane == 0) red[w] = bk;
+  if (threadIdx.x == 0) endpos = -1;
+  __syncthreads();
+  bk = red[0];
+  for (int i = 1; i < 4; i++) bk = red[i] < bk ? red[i] : bk;
+  for (int i = threadIdx.x; i < st.ntok; i += 256)
+    if (cs[i] == (int)(unsigned)(bk & 0xffffffffu)) endpos = i;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int n = 0;
+    int* out = a.path + (long long)blockIdx.x * a.path_cap;
+    if (endpos >= 0) {
+      const int4* arena = a.arena + (long long)slot * a.arena_cap;
+      int k = st.cur_base + a.cur_pos[(long long)slot * a.max_tok + endpos];
+      while (k >= 0) {
+        const int4 e = arena[k];
+        if (e.y < 0) break;
+        if (n < a.path_cap) out[n] = e.y;
+        n++;
+        k = e.x;
+      }
+    }
+    a.path_len[blockIdx.x] = n;
+    a.end_cost[blockIdx.x] = endpos >= 0 ? funord((uint32_t)(bk >> 32)) : __int_as_float(0x7f800000);
+    a.final_rel[blockIdx.x] = any_final ? bf - bn : __int_as_float(0x7f800000);
+    a.end_state[blockIdx.x] = endpos >= 0 ? (int)(unsigned)(bk & 0xffffffffu) : -1;
+  }
+}
+
+void LaunchTraceback(const TraceArgs& a, int n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(traceback_kernel, dim3(n), dim3(256), 0, s, a);
+}
+
+// HBM frame tables at engine construction: all slots empty
+__global__ void init_tables_kernel(int* state, unsigned long long* key, int* stamp, long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    state[i] = -1;
+    key[i] = kEmpty;
+    stamp[i] = -1;
+  }
+}
+
+void LaunchInitTables(int* state, unsigned long long* key, int* stamp, long long n, hipStream_t s) {
+  if (n <= 0) return;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(init_tables_kernel, dim3((unsigned)blocks), dim3(256), 0, s, state, key, stamp, n);
+}
+
+}  // namespace vamd

@@ -640,22 +640,30 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   dec_.min_active = m.dec.min_active;
   dec_.P = plan_.out_dim;
   dec_.llh = d_llh_;
-  dec_.key = (unsigned long long*)DevAlloc(sizeof(unsigned long long) * S * NS);
-  dec_.posmap = (int*)DevAlloc(sizeof(int) * 2 * S * NS);
-  dec_.stamp = (int*)DevAlloc(sizeof(int) * S * NS);
+  // bounded per-stream decoder state (decoder.hip): two HBM frame tables of
+  // H >= 2 * max_tokens slots for the states a frame's LDS table cannot hold
   const long long MT = cfg_.max_tokens;
+  int hbits = 10;
+  while ((1ll << hbits) < 2 * MT) hbits++;
+  const long long H = 1ll << hbits;
+  dec_.hbits = hbits;
+  dec_.hprobe = 256;
+  dec_.ht_state = (int*)DevAlloc(sizeof(int) * 2 * S * H);
+  dec_.ht_key = (unsigned long long*)DevAlloc(sizeof(unsigned long long) * 2 * S * H);
+  dec_.ht_pos = (int*)DevAlloc(sizeof(int) * 2 * S * H);
+  dec_.ht_stamp = (int*)DevAlloc(sizeof(int) * 2 * S * H);
+  dec_.ht_list = (int*)DevAlloc(sizeof(int) * 2 * S * MT);
+  dec_.front_g = (int*)DevAlloc(sizeof(int) * 2 * S * MT);
   dec_.cur_state = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.cur_cost = (float*)DevAlloc(sizeof(float) * S * MT);
   dec_.cur_pos = (int*)DevAlloc(sizeof(int) * S * MT);
-  dec_.new_list = (int*)DevAlloc(sizeof(int) * S * MT);
-  dec_.front_a = (int*)DevAlloc(sizeof(int) * S * MT);
-  dec_.front_b = (int*)DevAlloc(sizeof(int) * S * MT);
-  dec_.arena = (int2*)DevAlloc(sizeof(int2) * S * cfg_.arena_tokens);
+  dec_.arena = (int4*)DevAlloc(sizeof(int4) * S * cfg_.arena_tokens);
   dec_.max_tok = (int)MT;
-  // LDS frame construction threshold (kernels.hip kLdsFrameTokens); tests
-  // force either path with VOSK_AMD_LDS_FRAME_TOKENS (0 = always global)
-  dec_.lds_frame_tokens = DecoderLdsFrameTokens();
-  if (const char* lt = getenv("VOSK_AMD_LDS_FRAME_TOKENS")) dec_.lds_frame_tokens = atoi(lt);
+  // LDS probe limit of the frame table (decoder.hip); tests force the HBM
+  // tables with VOSK_AMD_DEC_LDS_PROBE (0 = every state in HBM)
+  dec_.lds_probe = DecoderLdsProbe();
+  if (const char* lp = getenv("VOSK_AMD_DEC_LDS_PROBE")) dec_.lds_probe = atoi(lp);
+  dec_.lattice_beam = m.dec.lattice_beam;
   dec_.arena_cap = cfg_.arena_tokens;
   dec_.links = nullptr;
   dec_.lat_frames = nullptr;
@@ -675,8 +683,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     dec_.prof = (long long*)DevAlloc(sizeof(long long) * 8 * S);
     HIPCHECK(hipMemset(dec_.prof, 0, sizeof(long long) * 8 * S));
   }
-  LaunchInitKeys(dec_.key, dec_.stamp, S * NS, stream_);
-  HIPCHECK(hipMemsetAsync(dec_.posmap, 0, sizeof(int) * 2 * S * NS, stream_));
+  LaunchInitTables(dec_.ht_state, dec_.ht_key, dec_.ht_stamp, 2 * S * H, stream_);
 
   // ---- staging
   stage_bytes_ = Align256(sizeof(float) * (size_t)S * cfg_.max_step_samples) +
@@ -1417,13 +1424,13 @@ void Engine::GetRawLattice(int slot, bool use_final, RawLattice* out) {
   if (slots_.at(slot).decoded == 0 && st.frames == 0 && st.arena_used == 0) return;
   const int nf = std::min(st.frames + 1, dec_.lat_frame_cap);
   std::vector<LatFrame> frames(nf);
-  std::vector<int2> arena(st.arena_used);
+  std::vector<int4> arena(st.arena_used);
   const long long nl = std::min(st.links_used, dec_.link_cap);
   std::vector<int4> links(nl);
   HIPCHECK(hipMemcpy(frames.data(), dec_.lat_frames + (size_t)slot * dec_.lat_frame_cap,
                      sizeof(LatFrame) * nf, hipMemcpyDeviceToHost));
   if (!arena.empty())
-    HIPCHECK(hipMemcpy(arena.data(), dec_.arena + (size_t)slot * dec_.arena_cap, sizeof(int2) * arena.size(),
+    HIPCHECK(hipMemcpy(arena.data(), dec_.arena + (size_t)slot * dec_.arena_cap, sizeof(int4) * arena.size(),
                        hipMemcpyDeviceToHost));
   if (nl > 0)
     HIPCHECK(hipMemcpy(links.data(), dec_.links + (size_t)slot * dec_.link_cap, sizeof(int4) * nl,

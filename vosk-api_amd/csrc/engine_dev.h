@@ -117,23 +117,29 @@ struct DecSlot {
   int cur_base;     // arena index of the current frame's first token
   int arena_used;
   int frames;       // frames decoded since the last reset
-  int parity;       // which posmap half holds the current frame
-  int stamp;        // epsilon-closure round stamp
-  int err;          // bit 0: token list overflow, bit 1: arena overflow, bit 2: no tokens
+  int cur_tab;      // HBM frame table holding the current frame's HBM-resident tokens (-1 none)
+  int stamp;        // epsilon-closure round stamp (monotonic)
+  int err;          // bit 0: token list / table overflow, bit 1: arena overflow, bit 2: no tokens,
+                    // bit 3: unplaceable backpointer source
   int lat_ovf;      // lattice: 1 = link arena or frame table overflowed (results fall back to 1-best)
   double offset_sum;
   unsigned long long best_key;  // min over current tokens of (ordered cost << 32 | state)
-  long long links_used;         // lattice links written since the reset
+  long long links_used;         // lattice links in the stream's link arena
+  int tab_n0, tab_n1;  // entries listed per HBM table (cleared by list)
+  int cur_nl;       // LDS-resident tokens of the current frame (their list positions come first)
+  int seg_base;     // lattice: LatFrame index of the segment's first kept frame (pruning)
+  int prune_from;   // lattice: first frame the next pruning pass revisits
+  int pad0;
 };
 
 // ---- lattice (LatticeFasterDecoder forward links, kept in HBM per stream).
-// A raw link {src, arc, acoustic cost, tot}: emitting links carry the arena
-// index of their source token (the destination is the next frame's token of
-// arcs[arc].nextstate), epsilon links src = -1 (source and destination are
-// tokens of the same frame: the arc's source and next state; relaxations
-// with a stale source cost repeat the link, the host keeps one per arc).
-// Links whose tot is not below the frame's final cutoff are dropped by the
-// host (the kernel writes every relaxation below the seed bound).
+// A link {src arena index, dst arena index, arc, acoustic cost bits}: an
+// emitting link goes from a token of frame k-1 to one of frame k, an epsilon
+// link (arcs[arc] has no pdf) joins two tokens of frame k.  The frame's
+// links are exactly Kaldi's: emitting links below the frame's final cutoff,
+// epsilon links once per arc at the final source cost (decoder.hip
+// commit_links).  Their total cost is recomputed from the source token's
+// cost: (cost + ac) + weight (emitting), cost + weight (epsilon).
 struct LatFrame {   // per decoded frame (index 0 = InitDecoding's closure)
   int tok_base, ntok;      // arena slots [tok_base, tok_base + ntok) (dead slots: prev == -2)
   long long link_begin, link_end;
@@ -240,30 +246,34 @@ struct DecArgs {
   int P;
   const float* llh;
   const DecJob* jobs;
-  unsigned long long* key;  // [slots][S]
-  int* posmap;              // [slots][2][S]
-  int* stamp;               // [slots][S]
+  // per stream, two HBM frame tables of H = 1 << hbits slots (decoder.hip):
+  // states that do not fit the LDS table of the frame under construction
+  int* ht_state;            // [slots][2][H]
+  unsigned long long* ht_key;  // [slots][2][H]
+  int* ht_pos;              // [slots][2][H]
+  int* ht_stamp;            // [slots][2][H]
+  int* ht_list;             // [slots][2][max_tok]
+  int hbits, hprobe;
+  int* front_g;             // [slots][2][max_tok] epsilon frontier spill
   int* cur_state;           // [slots][max_tok]
   float* cur_cost;          // [slots][max_tok]
   int* cur_pos;             // [slots][max_tok] list position (arena offset from cur_base)
-  int* new_list;            // [slots][max_tok]
-  int* front_a;             // [slots][max_tok]
-  int* front_b;             // [slots][max_tok]
-  int2* arena;              // [slots][arena_cap]
+  int4* arena;              // [slots][arena_cap] {prev, arc, cost bits, state}
   DecSlot* slots;
   FrameStat* stats;
   int max_tok;
-  int lds_frame_tokens;   // frames with more current tokens use the global maps
+  int lds_probe;          // LDS probe limit (states past it live in HBM); tests: 0 = all HBM
   long long arena_cap;
-  int4* links;            // [slots][link_cap] raw lattice links (nullptr: no lattice)
+  int4* links;            // [slots][link_cap] lattice links (nullptr: no lattice)
   LatFrame* lat_frames;   // [slots][lat_frame_cap]
   long long link_cap;
   int lat_frame_cap;
+  float lattice_beam;     // pruning (PruneActiveTokens)
 };
 
 struct TraceArgs {
   const int4* sinfo;
-  const int2* arena;
+  const int4* arena;
   const int* cur_state;
   const float* cur_cost;
   const int* cur_pos;

@@ -25,8 +25,8 @@ void LaunchNnetGather(const NnetOpArgs& a, hipStream_t s);
 // then per-frame 5-best posteriors, statistics and CG per stream (after them)
 void LaunchCmvn(const CmvnDev& c, const CmvnJob* jobs, int njobs, hipStream_t s);
 void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, hipStream_t s);
-void LdsHashSelfTest(int n, int blocks, int* out);  // dev (tools/gemm_bench)
-int DecoderLdsFrameTokens();  // default LDS frame-construction threshold
+// token passing (decoder.hip)
+int DecoderLdsProbe();  // default LDS probe limit of the frame table
 void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s);
 void LaunchTraceback(const TraceArgs& a, int n, hipStream_t s);
 // speaker x-vectors (xvector.h): selection + sliding CMN, statistics
@@ -39,6 +39,6 @@ void LaunchXvecAffine(const float* W, const float* b, const float* x, int K, int
                       float* y, hipStream_t s);
 void LaunchXvecFinish(const float* x, const float* mean, int E, const float* T, int R, float* out,
                       hipStream_t s);
-void LaunchInitKeys(unsigned long long* key, int* stamp, long long n_states_total, hipStream_t s);
+void LaunchInitTables(int* state, unsigned long long* key, int* stamp, long long n, hipStream_t s);
 
 }  // namespace vamd

@@ -27,6 +27,7 @@
 
 #include <cstdint>
 
+#include "dev_util.h"
 #include "engine_dev.h"
 #include "kernels.h"
 
@@ -34,17 +35,6 @@ namespace vamd {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-#define AG_LD(p) __hip_atomic_load((p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-#define AG_ST(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-
-__device__ __forceinline__ uint32_t ford(float f) {
-  uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float funord(uint32_t k) {
-  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
-  return __uint_as_float(u);
-}
 
 // natural log; identical operation sequence to orc_logf (oracle/oracle.c)
 __device__ __forceinline__ float dev_logf(float x) {
@@ -1269,1064 +1259,6 @@ void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, h
     else hipLaunchKernelGGL((ivector_acc_kernel<5, 4>), dim3(njobs * 4), dim3(256), 0, s, a);
   }
   hipLaunchKernelGGL(ivector_cg_kernel, dim3(njobs), dim3(128), 0, s, a);
-}
-
-// ===========================================================================
-// token passing
-// ===========================================================================
-#ifndef VAMD_DEC_THREADS
-#define VAMD_DEC_THREADS 512
-#endif
-constexpr int DT = VAMD_DEC_THREADS;  // threads per decoder workgroup
-constexpr int DW = DT / 64;      // waves
-constexpr int kLlhLds = 4096;    // log-likelihood row staged in LDS up to this size
-constexpr int kTokLds = 1024;    // current-frame tokens cached in LDS up to this count
-// LDS frame construction: open-addressing table of the frame being built
-constexpr int kHashCap = 4096;   // slots (power of two)
-constexpr int kHashBits = 12;
-constexpr int kNewLds = 3072;    // tokens a frame may create in LDS mode (load <= 0.75)
-constexpr int kFrontLds = 2048;  // epsilon frontier capacity in LDS mode
-constexpr int kMaxProbe = 64;    // longer probe sequences count as overflow
-constexpr int kLdsFrameTokens = 1000;  // frames with more current tokens skip the LDS table
-constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
-constexpr unsigned kDestEps = 0x80000000u;  // arcs[].w: nextstate has epsilon arcs
-
-struct DecShared {
-  int scan[DT + 1];   // exclusive prefix sums of the chunk's degrees
-  int abeg[DT];       // first arc per chunk token
-  float tcost[DT];    // cost per chunk token
-  int tsrc[DT];       // arena index per chunk token (lattice links)
-  unsigned hist[256];
-  unsigned long long red_u[DW];
-  float red_f[DW];
-  int red_i[DW];
-  int n_new, n_next, n_front0, total, sel_k, ovf, n_links, lat_ovf;
-  unsigned sel_prefix, sel_mask;
-  float seed;
-  int bad;
-};
-
-__device__ __forceinline__ float wave_min_f(float v) {
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    unsigned long long w = __shfl_xor(v, o, 64);
-    v = w < v ? w : v;
-  }
-  return v;
-}
-
-__device__ float block_min_f(DecShared& sh, float v) {
-  v = wave_min_f(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) sh.red_f[w] = v;
-  __syncthreads();
-  float r = sh.red_f[0];
-  for (int i = 1; i < DW; i++) r = fminf(r, sh.red_f[i]);
-  return r;
-}
-
-__device__ unsigned long long block_min_u64(DecShared& sh, unsigned long long v) {
-  v = wave_min_u64(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) sh.red_u[w] = v;
-  __syncthreads();
-  unsigned long long r = sh.red_u[0];
-  for (int i = 1; i < DW; i++) r = sh.red_u[i] < r ? sh.red_u[i] : r;
-  return r;
-}
-
-__device__ unsigned long long block_sum_u64(DecShared& sh, unsigned long long v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) sh.red_u[w] = v;
-  __syncthreads();
-  unsigned long long r = 0;
-  for (int i = 0; i < DW; i++) r += sh.red_u[i];
-  return r;
-}
-
-// exclusive scan of deg over the block; writes sh.scan[0..DT], sh.total
-__device__ void block_scan(DecShared& sh, int deg) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int v = deg;
-  for (int o = 1; o < 64; o <<= 1) {
-    int u = __shfl_up(v, o, 64);
-    if (lane >= o) v += u;
-  }
-  __syncthreads();
-  if (lane == 63) sh.red_i[w] = v;
-  __syncthreads();
-  int off = 0;
-  for (int i = 0; i < w; i++) off += sh.red_i[i];
-  sh.scan[threadIdx.x] = off + v - deg;
-  if (threadIdx.x == DT - 1) {
-    sh.scan[DT] = off + v;
-    sh.total = off + v;
-  }
-  __syncthreads();
-}
-
-// token index j within the chunk that owns item `it` (largest j: scan[j] <= it)
-__device__ __forceinline__ int owner(const DecShared& sh, int it) {
-  int lo = 0, hi = DT - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (sh.scan[mid] <= it) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
-// current-frame tokens: LDS cache when they fit, else global (agent loads)
-struct TokView {
-  int* gs;
-  float* gc;
-  const int* ls;
-  const float* lc;
-  bool lds;
-  __device__ __forceinline__ int s(int i) const { return lds ? ls[i] : AG_LD(&gs[i]); }
-  __device__ __forceinline__ float c(int i) const { return lds ? lc[i] : AG_LD(&gc[i]); }
-};
-
-// exact k-th smallest (0-based) of the token costs by 4-pass 8-bit radix select
-__device__ float kth_smallest(DecShared& sh, const TokView& tv, int n, int k) {
-  if (threadIdx.x == 0) {
-    sh.sel_prefix = 0;
-    sh.sel_mask = 0;
-    sh.sel_k = k;
-  }
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < 256; i += DT) sh.hist[i] = 0;
-    __syncthreads();
-    const unsigned prefix = sh.sel_prefix, mask = sh.sel_mask;
-    for (int i = threadIdx.x; i < n; i += DT) {
-      const unsigned u = ford(tv.c(i));
-      if ((u & mask) == prefix) atomicAdd(&sh.hist[(u >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {  // wave 0: prefix over the 256 buckets (4 per lane)
-      const int l = threadIdx.x;
-      const int h0 = sh.hist[4 * l], h1 = sh.hist[4 * l + 1], h2 = sh.hist[4 * l + 2],
-                h3 = sh.hist[4 * l + 3];
-      const int tot = h0 + h1 + h2 + h3;
-      int incl = tot;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(incl, o, 64);
-        if (l >= o) incl += u;
-      }
-      const int excl = incl - tot;
-      const int kk = sh.sel_k;
-      if (kk >= excl && kk < incl) {  // exactly one lane holds the bucket
-        int r = kk - excl, b = 4 * l;
-        if (r >= h0) { r -= h0; b++;
-          if (r >= h1) { r -= h1; b++;
-            if (r >= h2) { r -= h2; b++; } } }
-        sh.sel_k = r;
-        sh.sel_prefix = prefix | ((unsigned)b << shift);
-        sh.sel_mask = mask | (255u << shift);
-      }
-    }
-  }
-  __syncthreads();
-  return funord(sh.sel_prefix);
-}
-
-struct DecPtrs {
-  unsigned long long* key;
-  int* pos_cur;
-  int* pos_new;
-  int* stamp;
-  int* cs;
-  float* cc;
-  int* cp;   // list position of each current token (arena index = cur_base + cp)
-  int* nl;   // tokens of the frame under construction
-  int* fa;   // epsilon frontiers / compaction scratch
-  int* fb;
-  int2* arena;
-};
-
-// Lattice link of a relaxation (see LatFrame in engine_dev.h): one LDS
-// counter bump per wave (ballot / popcount), then a 16-byte store into the
-// stream's link arena after the links of the previous frames.
-__device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long long used, int slot,
-                                          int src, int arc, float ac, float tot) {
-  const unsigned long long m = __ballot(1);
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)m) - 1;
-  int base = 0;
-  if (lane == leader) base = atomicAdd(&sh.n_links, __popcll(m));
-  base = __shfl(base, leader, 64);
-  const int off = __popcll(m & ((1ull << lane) - 1ull));
-  const long long pos = used + base + off;
-  if (pos < a.link_cap)
-    a.links[(long long)slot * a.link_cap + pos] = make_int4(src, arc, __float_as_int(ac), __float_as_int(tot));
-  else
-    sh.lat_ovf = 1;
-}
-
-// relax dest with (tot, arc); appends a newly created token to the frame
-// list.  Returns 1 if improved, 2 if created (created implies improved).
-__device__ __forceinline__ int relax(const DecArgs& a, DecShared& sh, const DecPtrs& p, int dest,
-                                     float tot, int arc) {
-  const unsigned long long k = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
-  const unsigned long long old = atomicMin(&p.key[dest], k);
-  if (old == kEmpty) {
-    const int pos = atomicAdd(&sh.n_new, 1);
-    if (pos < a.max_tok) {
-      AG_ST(&p.nl[pos], dest);
-      AG_ST(&p.pos_new[dest], pos);
-    } else {
-      sh.bad |= 1;
-    }
-    return 2;
-  }
-  return k < old ? 1 : 0;
-}
-
-__device__ __forceinline__ void push_front(const DecArgs& a, DecShared& sh, int* list, int* count,
-                                           int s) {
-  const int q = atomicAdd(count, 1);
-  if (q < a.max_tok) AG_ST(&list[q], s);
-  else sh.bad |= 1;
-}
-
-// ProcessNonemitting: epsilon closure in rounds over frontiers that only
-// hold states with epsilon arcs (round 0: created by the emitting pass).
-__device__ void eps_closure(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st, float cutoff,
-                            int nfront, int* arcs_eps, int slot) {
-  int* front = p.fa;
-  int* next = p.fb;
-  int examined = 0;
-  nfront = nfront < a.max_tok ? nfront : a.max_tok;
-  while (nfront > 0) {
-    st.stamp++;
-    const int stamp = st.stamp;
-    __syncthreads();
-    if (threadIdx.x == 0) sh.n_next = 0;
-    for (int c0 = 0; c0 < nfront; c0 += DT) {
-      const int i = c0 + threadIdx.x;
-      int deg = 0, ab = 0;
-      float c = 0.0f;
-      if (i < nfront) {
-        const int s = AG_LD(&front[i]);
-        c = funord((uint32_t)(AG_LD(&p.key[s]) >> 32));
-        if (c < cutoff) {  // created tokens are < cutoff; dead ones are not
-          const int4 si = a.sinfo[s];
-          ab = si.y;
-          deg = si.z - si.y;
-        }
-      }
-      block_scan(sh, deg);
-      sh.abeg[threadIdx.x] = ab;
-      sh.tcost[threadIdx.x] = c;
-      __syncthreads();
-      const int total = sh.total;
-      examined += total;
-      for (int it = threadIdx.x; it < total; it += DT) {
-        const int j = owner(sh, it);
-        const int arc = sh.abeg[j] + (it - sh.scan[j]);
-        const int4 A = a.arcs[arc];
-        const float tot = sh.tcost[j] + __int_as_float(A.y);
-        if (tot < cutoff) {
-          if (a.links) emit_link(a, sh, st.links_used, slot, -1, arc, 0.0f, tot);
-          if (relax(a, sh, p, A.x, tot, arc) && ((unsigned)A.w & kDestEps) &&
-              atomicExch(&p.stamp[A.x], stamp) != stamp)
-            push_front(a, sh, next, &sh.n_next, A.x);
-        }
-      }
-      __syncthreads();
-    }
-    nfront = sh.n_next < a.max_tok ? sh.n_next : a.max_tok;
-    int* t = front;
-    front = next;
-    next = t;
-  }
-  *arcs_eps += examined;
-}
-
-// Move the frame under construction into the arena + current token arrays
-// (global, and the LDS cache when it fits); reset its keys.  List entries
-// whose cost is not below `cutoff` (dead: created by the single emitting
-// pass above the final next_cutoff) keep their arena slot unused.
-__device__ void commit(const DecArgs& a, DecShared& sh, DecPtrs& p, DecSlot& st, int* TS, float* TC,
-                       bool* lds, float cutoff, float* best_out) {
-  __syncthreads();
-  const int n = sh.n_new < a.max_tok ? sh.n_new : a.max_tok;
-  const int base = st.arena_used;
-  const bool ok = (long long)base + n <= a.arena_cap;
-  if (threadIdx.x == 0) sh.n_next = 0;
-  __syncthreads();
-  unsigned long long bk = kEmpty;
-  for (int j = threadIdx.x; j < n; j += DT) {
-    const int s = AG_LD(&p.nl[j]);
-    const unsigned long long k = AG_LD(&p.key[s]);
-    const int arc = (int)(unsigned)(k & 0xffffffffu);
-    const float cost = funord((uint32_t)(k >> 32));
-    if (ok && cost < cutoff) {
-      int prev = -1;
-      if (arc >= 0) {
-        const int4 A = a.arcs[arc];
-        const int src = (int)((unsigned)A.w & 0x7fffffffu);
-        prev = A.z >= 0 ? st.cur_base + AG_LD(&p.pos_cur[src]) : base + AG_LD(&p.pos_new[src]);
-      }
-      p.arena[base + j] = make_int2(prev, arc);
-      const int q = atomicAdd(&sh.n_next, 1);
-      AG_ST(&p.cs[q], s);
-      AG_ST(&p.cc[q], cost);
-      AG_ST(&p.cp[q], j);
-      if (q < kTokLds) {
-        TS[q] = s;
-        TC[q] = cost;
-      }
-      const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)s;
-      bk = tk < bk ? tk : bk;
-    } else if (ok) {
-      p.arena[base + j] = make_int2(-2, -1);  // dead list entry (lattice readers skip it)
-    }
-    AG_ST(&p.key[s], kEmpty);
-  }
-  bk = block_min_u64(sh, bk);
-  if (!ok) sh.bad |= 2;
-  __syncthreads();
-  const int live = sh.n_next;
-  if (ok) {
-    st.cur_base = base;
-    st.arena_used = base + n;
-    st.ntok = live;
-  } else {
-    st.ntok = 0;
-  }
-  *lds = live <= kTokLds;
-  int* t = p.pos_cur;
-  p.pos_cur = p.pos_new;
-  p.pos_new = t;
-  st.parity ^= 1;
-  st.best_key = bk;  // GetCutoff's best token of the next frame
-  *best_out = funord((uint32_t)(bk >> 32));
-}
-
-// ---- LDS frame construction.  The frame being built lives in an LDS hash
-// table (state, (cost, arc) key, list position, epsilon-round stamp) with
-// LDS token list and frontiers; global memory is only written by the commit
-// (arena, current-token arrays, position map).  A frame that overflows the
-// table, the list or a frontier sets sh.ovf before anything global changed and
-// is re-run on the global-map path (same semantics, same results).
-struct FrameLds {
-  int* hs;                  // [kHashCap] state, -1 = empty
-  unsigned long long* hk;   // [kHashCap] (ordered cost << 32 | arc), kEmpty
-  unsigned short* hp;       // [kHashCap] position in the frame's list
-  int* hst;                 // [kHashCap] epsilon round stamp
-  unsigned short* nl;       // [kNewLds] list -> slot
-  unsigned short* fa;       // [kFrontLds] frontier slots
-  unsigned short* fb;
-};
-
-__device__ __forceinline__ unsigned hash_slot(int s) {
-  return ((unsigned)s * 2654435761u) >> (32 - kHashBits);
-}
-
-__device__ void lds_clear(const FrameLds& t) {
-  for (int h = threadIdx.x; h < kHashCap; h += DT) {
-    t.hs[h] = -1;
-    t.hk[h] = kEmpty;
-    t.hst[h] = 0;
-  }
-}
-
-// relax into the LDS table: returns (slot << 2) | 2 if created, | 1 if
-// improved, | 0 otherwise; -1 on overflow (sh.ovf set)
-__device__ __forceinline__ int relax_lds(DecShared& sh, const FrameLds& t, int dest, float tot,
-                                         int arc) {
-  if (__hip_atomic_load(&sh.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return -1;
-  const unsigned long long k = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
-  unsigned h = hash_slot(dest);
-  for (int probe = 0; probe < kMaxProbe; probe++) {
-    int cur = __hip_atomic_load(&t.hs[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (cur == -1) {
-      cur = atomicCAS(&t.hs[h], -1, dest);
-      if (cur == -1) {
-        const int pos = atomicAdd(&sh.n_new, 1);
-        if (pos < kNewLds) {
-          t.nl[pos] = (unsigned short)h;
-          t.hp[h] = (unsigned short)pos;
-        } else {
-          sh.ovf |= 1;
-        }
-        atomicMin(&t.hk[h], k);
-        return (int)(h << 2) | 2;
-      }
-    }
-    if (cur == dest) {
-      const unsigned long long old = atomicMin(&t.hk[h], k);
-      return (int)(h << 2) | (k < old ? 1 : 0);
-    }
-    h = (h + 1) & (kHashCap - 1);
-  }
-  sh.ovf |= 2;
-  return -1;
-}
-
-__device__ __forceinline__ int lds_find(const FrameLds& t, int s) {
-  unsigned h = hash_slot(s);
-  for (int probe = 0; probe < kMaxProbe; probe++) {
-    if (t.hs[h] == s) return (int)h;
-    if (t.hs[h] == -1) return -1;
-    h = (h + 1) & (kHashCap - 1);
-  }
-  return -1;
-}
-
-__device__ float expand_emitting_lds(const DecArgs& a, DecShared& sh, const FrameLds& t,
-                                     const TokView& tv, int ntok, float cutoff, float cost_offset,
-                                     const float* Lp, int mode, float bound, int* examined,
-                                     const DecPtrs& p, const DecSlot& st, int slot) {
-  float m = __int_as_float(0x7f800000);
-  const bool lat = a.links != nullptr && mode == 1;
-  for (int c0 = 0; c0 < ntok; c0 += DT) {
-    const int i = c0 + threadIdx.x;
-    int deg = 0, ab = 0, src = 0;
-    float c = 0.0f;
-    if (i < ntok) {
-      c = tv.c(i);
-      if (c <= cutoff) {
-        const int4 si = a.sinfo[tv.s(i)];
-        ab = si.x;
-        deg = si.y - si.x;
-        if (lat) src = st.cur_base + AG_LD(&p.cp[i]);
-      }
-    }
-    block_scan(sh, deg);
-    sh.abeg[threadIdx.x] = ab;
-    sh.tcost[threadIdx.x] = c;
-    sh.tsrc[threadIdx.x] = src;
-    __syncthreads();
-    const int total = sh.total;
-    *examined += total;
-    for (int it = threadIdx.x; it < total; it += DT) {
-      const int j = owner(sh, it);
-      const int arc = sh.abeg[j] + (it - sh.scan[j]);
-      const int4 A = a.arcs[arc];
-      const float ac = cost_offset - Lp[A.z];
-      const float tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
-      m = fminf(m, tot);
-      if (mode == 1 && tot < bound) {
-        if (lat) emit_link(a, sh, st.links_used, slot, sh.tsrc[j], arc, ac, tot);
-        const int r = relax_lds(sh, t, A.x, tot, arc);
-        if (r >= 0 && (r & 3) == 2 && ((unsigned)A.w & kDestEps)) {
-          const int q = atomicAdd(&sh.n_front0, 1);
-          if (q < kFrontLds) t.fa[q] = (unsigned short)(r >> 2);
-          else sh.ovf |= 4;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  return block_min_f(sh, m);
-}
-
-__device__ void eps_closure_lds(const DecArgs& a, DecShared& sh, const FrameLds& t, float cutoff,
-                                int nfront, int* arcs_eps, const DecSlot& st, int slot) {
-  unsigned short* front = t.fa;
-  unsigned short* next = t.fb;
-  int examined = 0, round = 0;
-  nfront = nfront < kFrontLds ? nfront : kFrontLds;
-  while (nfront > 0) {
-    round++;
-    __syncthreads();
-    if (threadIdx.x == 0) sh.n_next = 0;
-    for (int c0 = 0; c0 < nfront; c0 += DT) {
-      const int i = c0 + threadIdx.x;
-      int deg = 0, ab = 0;
-      float c = 0.0f;
-      if (i < nfront) {
-        const int h = front[i];
-        c = funord((uint32_t)(t.hk[h] >> 32));
-        if (c < cutoff) {  // created tokens are < cutoff; dead ones are not
-          const int4 si = a.sinfo[t.hs[h]];
-          ab = si.y;
-          deg = si.z - si.y;
-        }
-      }
-      block_scan(sh, deg);
-      sh.abeg[threadIdx.x] = ab;
-      sh.tcost[threadIdx.x] = c;
-      __syncthreads();
-      const int total = sh.total;
-      examined += total;
-      for (int it = threadIdx.x; it < total; it += DT) {
-        const int j = owner(sh, it);
-        const int arc = sh.abeg[j] + (it - sh.scan[j]);
-        const int4 A = a.arcs[arc];
-        const float tot = sh.tcost[j] + __int_as_float(A.y);
-        if (tot < cutoff) {
-          if (a.links) emit_link(a, sh, st.links_used, slot, -1, arc, 0.0f, tot);
-          const int r = relax_lds(sh, t, A.x, tot, arc);
-          if (r >= 0 && (r & 3) && ((unsigned)A.w & kDestEps) &&
-              atomicExch(&t.hst[r >> 2], round) != round) {
-            const int q = atomicAdd(&sh.n_next, 1);
-            if (q < kFrontLds) next[q] = (unsigned short)(r >> 2);
-            else sh.ovf |= 8;
-          }
-        }
-      }
-      __syncthreads();
-    }
-    nfront = sh.n_next < kFrontLds ? sh.n_next : kFrontLds;
-    unsigned short* tmp = front;
-    front = next;
-    next = tmp;
-  }
-  *arcs_eps += examined;
-}
-
-// commit of an LDS-built frame (see commit()); clears the table afterwards
-__device__ void commit_lds(const DecArgs& a, DecShared& sh, DecPtrs& p, const FrameLds& t,
-                           DecSlot& st, int* TS, float* TC, bool* lds, float cutoff,
-                           float* best_out) {
-  __syncthreads();
-  const int n = sh.n_new < kNewLds ? sh.n_new : kNewLds;
-  const int base = st.arena_used;
-  const bool ok = (long long)base + n <= a.arena_cap;
-  if (threadIdx.x == 0) sh.n_next = 0;
-  __syncthreads();
-  unsigned long long bk = kEmpty;
-  for (int j = threadIdx.x; j < n; j += DT) {
-    const int h = t.nl[j];
-    const int s = t.hs[h];
-    const unsigned long long k = t.hk[h];
-    const int arc = (int)(unsigned)(k & 0xffffffffu);
-    const float cost = funord((uint32_t)(k >> 32));
-    if (ok && cost < cutoff) {
-      int prev = -1;
-      if (arc >= 0) {
-        const int4 A = a.arcs[arc];
-        const int src = (int)((unsigned)A.w & 0x7fffffffu);
-        if (A.z >= 0) {
-          prev = st.cur_base + AG_LD(&p.pos_cur[src]);
-        } else {
-          const int hsrc = lds_find(t, src);
-          prev = base + (hsrc >= 0 ? t.hp[hsrc] : 0);
-        }
-      }
-      p.arena[base + j] = make_int2(prev, arc);
-      const int q = atomicAdd(&sh.n_next, 1);
-      AG_ST(&p.cs[q], s);
-      AG_ST(&p.cc[q], cost);
-      AG_ST(&p.cp[q], j);
-      AG_ST(&p.pos_new[s], j);
-      if (q < kTokLds) {
-        TS[q] = s;
-        TC[q] = cost;
-      }
-      const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)s;
-      bk = tk < bk ? tk : bk;
-    } else if (ok) {
-      p.arena[base + j] = make_int2(-2, -1);  // dead list entry (lattice readers skip it)
-    }
-  }
-  bk = block_min_u64(sh, bk);  // ends with a barrier: the table is no longer read
-  if (!ok) sh.bad |= 2;
-  lds_clear(t);
-  __syncthreads();
-  const int live = sh.n_next;
-  if (ok) {
-    st.cur_base = base;
-    st.arena_used = base + n;
-    st.ntok = live;
-  } else {
-    st.ntok = 0;
-  }
-  *lds = live <= kTokLds;
-  int* tp = p.pos_cur;
-  p.pos_cur = p.pos_new;
-  p.pos_new = tp;
-  st.parity ^= 1;
-  st.best_key = bk;
-  *best_out = funord((uint32_t)(bk >> 32));
-}
-
-// dev self-test of the LDS frame table (tools/gemm_bench): each block inserts
-// `n` random states (each relaxed 3 times) and reports overflow bits and the
-// number of distinct states the table holds
-__global__ __launch_bounds__(DT) void lds_hash_selftest_kernel(int n, int seed, int* out) {
-  __shared__ DecShared sh;
-  __shared__ int t_hs[kHashCap];
-  __shared__ unsigned long long t_hk[kHashCap];
-  __shared__ unsigned short t_hp[kHashCap];
-  __shared__ int t_hst[kHashCap];
-  __shared__ unsigned short t_nl[kNewLds];
-  __shared__ unsigned short t_fa[kFrontLds];
-  __shared__ unsigned short t_fb[kFrontLds];
-  const FrameLds t{t_hs, t_hk, t_hp, t_hst, t_nl, t_fa, t_fb};
-  lds_clear(t);
-  if (threadIdx.x == 0) {
-    sh.n_new = 0;
-    sh.ovf = 0;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 3 * n; i += DT) {
-    const int k = i % n;
-    const unsigned st = ((unsigned)(k + 1) * 2246822519u + (unsigned)seed * 3266489917u) % 55000u;
-    relax_lds(sh, t, (int)st, (float)(i & 7), i);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int used = 0;
-    for (int h = 0; h < kHashCap; h++) used += t.hs[h] != -1;
-    out[blockIdx.x * 3 + 0] = sh.ovf;
-    out[blockIdx.x * 3 + 1] = sh.n_new;
-    out[blockIdx.x * 3 + 2] = used;
-  }
-}
-
-void LdsHashSelfTest(int n, int blocks, int* out) {
-  hipLaunchKernelGGL(lds_hash_selftest_kernel, dim3(blocks), dim3(DT), 0, 0, n, 7, out);
-}
-
-// one emitting expansion pass over the current tokens (ProcessEmitting):
-// mode 0 = minimum only, 1 = relax below `bound` (+ minimum)
-__device__ float expand_emitting(const DecArgs& a, DecShared& sh, DecPtrs& p, const TokView& tv,
-                                 int ntok, float cutoff, float cost_offset, const float* Lp,
-                                 int mode, float bound, int* examined, const DecSlot& st, int slot) {
-  float m = __int_as_float(0x7f800000);
-  const bool lat = a.links != nullptr && mode == 1;
-  for (int c0 = 0; c0 < ntok; c0 += DT) {
-    const int i = c0 + threadIdx.x;
-    int deg = 0, ab = 0, src = 0;
-    float c = 0.0f;
-    if (i < ntok) {
-      c = tv.c(i);
-      if (c <= cutoff) {
-        const int4 si = a.sinfo[tv.s(i)];
-        ab = si.x;
-        deg = si.y - si.x;
-        if (lat) src = st.cur_base + AG_LD(&p.cp[i]);
-      }
-    }
-    block_scan(sh, deg);
-    sh.abeg[threadIdx.x] = ab;
-    sh.tcost[threadIdx.x] = c;
-    sh.tsrc[threadIdx.x] = src;
-    __syncthreads();
-    const int total = sh.total;
-    *examined += total;
-    for (int it = threadIdx.x; it < total; it += DT) {
-      const int j = owner(sh, it);
-      const int arc = sh.abeg[j] + (it - sh.scan[j]);
-      const int4 A = a.arcs[arc];
-      const float ac = cost_offset - Lp[A.z];
-      const float tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
-      m = fminf(m, tot);
-      if (mode == 1 && tot < bound) {
-        if (lat) emit_link(a, sh, st.links_used, slot, sh.tsrc[j], arc, ac, tot);
-        if (relax(a, sh, p, A.x, tot, arc) == 2 && ((unsigned)A.w & kDestEps))
-          push_front(a, sh, p.fa, &sh.n_front0, A.x);
-      }
-    }
-    __syncthreads();
-  }
-  return block_min_f(sh, m);
-}
-
-// after a commit (all threads, past its barriers): the frame's lattice
-// record; every thread advances its copy of links_used identically
-__device__ void lat_frame_done(const DecArgs& a, DecShared& sh, DecSlot& st, int slot, int index,
-                               float cutoff, float cost_offset) {
-  const int nl = sh.n_links;
-  if (threadIdx.x == 0) {
-    if (index < a.lat_frame_cap) {
-      LatFrame F;
-      F.tok_base = st.cur_base;
-      F.ntok = st.arena_used - st.cur_base;
-      F.link_begin = st.links_used;
-      F.link_end = st.links_used + nl;
-      F.cutoff = cutoff;
-      F.cost_offset = cost_offset;
-      F.pad0 = F.pad1 = 0;
-      a.lat_frames[(long long)slot * a.lat_frame_cap + index] = F;
-    }
-  }
-  if (index >= a.lat_frame_cap || sh.lat_ovf) st.lat_ovf = 1;
-  st.links_used += nl;
-}
-
-template <bool PROF>
-__global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
-  __shared__ DecShared sh;
-  __shared__ float L[kLlhLds];
-  __shared__ int TS[kTokLds];
-  __shared__ float TC[kTokLds];
-  __shared__ int t_hs[kHashCap];
-  __shared__ unsigned long long t_hk[kHashCap];
-  __shared__ unsigned short t_hp[kHashCap];
-  __shared__ int t_hst[kHashCap];
-  __shared__ unsigned short t_nl[kNewLds];
-  __shared__ unsigned short t_fa[kFrontLds];
-  __shared__ unsigned short t_fb[kFrontLds];
-  const FrameLds t{t_hs, t_hk, t_hp, t_hst, t_nl, t_fa, t_fb};
-  lds_clear(t);
-  const DecJob job = a.jobs[blockIdx.x];
-  const int slot = job.slot;
-  const long long S = a.num_states;
-  DecSlot st = a.slots[slot];
-  DecPtrs p;
-  p.key = a.key + slot * S;
-  p.pos_cur = a.posmap + slot * 2 * S + st.parity * S;
-  p.pos_new = a.posmap + slot * 2 * S + (st.parity ^ 1) * S;
-  p.stamp = a.stamp + slot * S;
-  p.cs = a.cur_state + (long long)slot * a.max_tok;
-  p.cc = a.cur_cost + (long long)slot * a.max_tok;
-  p.cp = a.cur_pos + (long long)slot * a.max_tok;
-  p.nl = a.new_list + (long long)slot * a.max_tok;
-  p.fa = a.front_a + (long long)slot * a.max_tok;
-  p.fb = a.front_b + (long long)slot * a.max_tok;
-  p.arena = a.arena + (long long)slot * a.arena_cap;
-  if (threadIdx.x == 0) {
-    sh.bad = 0;
-    sh.n_links = 0;
-    sh.lat_ovf = 0;
-  }
-  int arcs_eps = 0;
-  bool lds = false;
-  // optional phase clocks (diagnostics): thread 0 stamps s_memtime
-  const bool prof = PROF && threadIdx.x == 0;
-  long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long tstamp = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
-#define DEC_PHASE(i)                                                     \
-  if (prof) {                                                            \
-    const long long _t = (long long)__builtin_amdgcn_s_memtime();        \
-    pacc[i] += _t - tstamp;                                              \
-    tstamp = _t;                                                         \
-  }
-
-  if (job.reset) {  // InitDecoding: start token, closure with cutoff = beam
-    st.ntok = 0;
-    st.cur_base = 0;
-    st.arena_used = 0;
-    st.frames = 0;
-    st.offset_sum = 0.0;
-    st.err = 0;
-    st.links_used = 0;
-    st.lat_ovf = 0;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      sh.n_new = 1;
-      AG_ST(&p.key[a.start_state], ((unsigned long long)ford(0.0f) << 32) | 0xffffffffu);
-      AG_ST(&p.nl[0], a.start_state);
-      AG_ST(&p.pos_new[a.start_state], 0);
-      AG_ST(&p.fa[0], a.start_state);
-    }
-    __syncthreads();
-    eps_closure(a, sh, p, st, a.beam, 1, &arcs_eps, slot);
-    float b;
-    commit(a, sh, p, st, TS, TC, &lds, a.beam, &b);
-    if (a.links) lat_frame_done(a, sh, st, slot, 0, a.beam, 0.0f);
-  } else if (st.ntok > 0 && st.ntok <= kTokLds) {
-    for (int i = threadIdx.x; i < st.ntok; i += DT) {
-      TS[i] = AG_LD(&p.cs[i]);
-      TC[i] = AG_LD(&p.cc[i]);
-    }
-    lds = true;
-  }
-
-  // log-likelihood rows staged in LDS: row f+1 is loaded into registers
-  // while frame f is processed and written to L once frame f's emitting
-  // expansion no longer reads it (just before its commit)
-  constexpr int kLlhRegs = kLlhLds / DT;
-  const bool stage_llh = a.P <= kLlhLds;
-  float nxt[kLlhRegs];
-  if (stage_llh && job.nframes > 0) {
-    const float* llh0 = a.llh + (size_t)job.llh_row0 * a.P;
-    for (int i = threadIdx.x; i < a.P; i += DT) L[i] = llh0[i];
-  }
-  for (int f = 0; f < job.nframes; f++) {
-    if (st.ntok == 0 || st.err) break;
-    const float* llh = a.llh + (size_t)(job.llh_row0 + f) * a.P;
-    const float* Lp = stage_llh ? L : llh;
-    const bool pf = stage_llh && f + 1 < job.nframes;
-    if (pf) {
-      const float* nrow = llh + a.P;
-#pragma unroll
-      for (int r = 0; r < kLlhRegs; r++) {
-        const int i = threadIdx.x + r * DT;
-        nxt[r] = i < a.P ? nrow[i] : 0.0f;
-      }
-    }
-    auto store_next = [&]() {
-      if (pf) {
-#pragma unroll
-        for (int r = 0; r < kLlhRegs; r++) {
-          const int i = threadIdx.x + r * DT;
-          if (i < a.P) L[i] = nxt[r];
-        }
-      }
-    };
-    const int ntok = st.ntok;
-    const TokView tv{p.cs, p.cc, TS, TC, lds};
-    // ---- GetCutoff (best token: min (cost, state), kept by the previous commit)
-    const unsigned long long bk = st.best_key;
-    const float best = funord((uint32_t)(bk >> 32));
-    const int best_state = (int)(unsigned)(bk & 0xffffffffu);
-    const float beam_cutoff = best + a.beam;
-    float max_cut = __int_as_float(0x7f800000), min_cut = __int_as_float(0x7f800000);
-    float adaptive, cutoff;
-    // The k-th smallest cost is only needed when it can change the outcome:
-    // max_cut < beam_cutoff  <=>  more than max_active costs are < beam_cutoff,
-    // min_cut > beam_cutoff  <=>  at most min_active costs are <= beam_cutoff.
-    bool need_max = ntok > a.max_active, need_min = ntok > a.min_active && a.min_active > 0;
-    if (need_max || need_min) {
-      unsigned long long cnt = 0;  // (# cost < beam_cutoff) << 32 | # cost <= beam_cutoff
-      for (int i = threadIdx.x; i < ntok; i += DT) {
-        const float c = tv.c(i);
-        cnt += ((unsigned long long)(c < beam_cutoff) << 32) | (unsigned)(c <= beam_cutoff);
-      }
-      cnt = block_sum_u64(sh, cnt);
-      const int n_lt = (int)(cnt >> 32), n_le = (int)(unsigned)(cnt & 0xffffffffu);
-      need_max = need_max && n_lt > a.max_active;
-      need_min = need_min && n_le <= a.min_active;
-    } else {
-      __syncthreads();  // the LLH row staged above is read by wave 0 below
-    }
-    if (need_max) max_cut = kth_smallest(sh, tv, ntok, a.max_active);
-    if (max_cut < beam_cutoff) {
-      adaptive = max_cut - best + a.beam_delta;
-      cutoff = max_cut;
-    } else {
-      if (ntok > a.min_active)
-        min_cut = a.min_active == 0 ? best
-                  : need_min ? kth_smallest(sh, tv, ntok, a.min_active)
-                             : beam_cutoff;  // proven <= beam_cutoff: the exact value is unused
-      if (min_cut > beam_cutoff) {
-        adaptive = min_cut - best + a.beam_delta;
-        cutoff = min_cut;
-      } else {
-        adaptive = a.beam;
-        cutoff = beam_cutoff;
-      }
-    }
-    const float cost_offset = -best;
-    DEC_PHASE(0);
-    // ---- ProcessEmitting: Kaldi's seed from the best token's arcs (wave 0)
-    if (threadIdx.x < 64) {
-      float sd = __int_as_float(0x7f800000);
-      const int4 si = a.sinfo[best_state];
-      for (int arc = si.x + (int)threadIdx.x; arc < si.y; arc += 64) {
-        const int4 A = a.arcs[arc];
-        const float nw = ((__int_as_float(A.y) + cost_offset) - Lp[A.z]) + best;
-        sd = fminf(sd, nw + adaptive);
-      }
-      sd = wave_min_f(sd);
-      if (threadIdx.x == 0) {
-        sh.seed = sd;
-        sh.n_new = 0;
-        sh.n_front0 = 0;
-        sh.ovf = 0;
-        sh.n_links = 0;
-      }
-    }
-    __syncthreads();
-    DEC_PHASE(1);
-    const float seed = sh.seed;
-    int examined = 0;
-    float next_cutoff, new_best;
-    // ---- frame construction in LDS: one emitting pass relaxing below the
-    // seed bound (a superset), then the epsilon closure; tokens whose best
-    // cost is not below the final next_cutoff stay as dead list entries
-    // (never expanded: cost >= cutoff) and are dropped at commit -- exactly
-    // the tokens a relax-below-next_cutoff pass creates, with the same keys.
-    // Frames predicted too large for the LDS table (many current tokens) go
-    // straight to the global maps; a frame that overflows anyway is rebuilt
-    // there (nothing global was written).
-    const bool try_lds = ntok <= a.lds_frame_tokens;
-    if (try_lds) {
-      if (seed != __int_as_float(0x7f800000)) {
-        const float m = expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
-                                            &examined, p, st, slot);
-        next_cutoff = seed;
-        if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
-      } else {
-        const float m = expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
-                                            &examined, p, st, slot);
-        next_cutoff = seed;
-        if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
-        int dummy = 0;
-        expand_emitting_lds(a, sh, t, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy, p, st,
-                            slot);
-      }
-      __syncthreads();
-      DEC_PHASE(2);
-      if (prof) pacc[3] += sh.n_new;  // tokens created by the emitting pass
-      if (!sh.ovf) eps_closure_lds(a, sh, t, next_cutoff, sh.n_front0, &arcs_eps, st, slot);
-      __syncthreads();
-      DEC_PHASE(4);
-    }
-    if (try_lds && !sh.ovf) {
-      store_next();  // L is not read again in this frame (barrier inside the commit)
-      commit_lds(a, sh, p, t, st, TS, TC, &lds, next_cutoff, &new_best);
-    } else {
-      // ---- global maps: a single emitting pass relaxing below the seed
-      // bound when it is finite (dead entries dropped at commit), else the
-      // exact two-pass form
-      if (prof) pacc[6]++;
-      if (try_lds) {
-        lds_clear(t);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          sh.n_new = 0;
-          sh.n_front0 = 0;
-          sh.n_links = 0;  // the LDS attempt's links are rewritten
-        }
-        __syncthreads();
-      }
-      examined = 0;
-      arcs_eps = 0;
-      if (seed != __int_as_float(0x7f800000)) {
-        const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
-                                        &examined, st, slot);
-        next_cutoff = seed;
-        if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
-      } else {
-        const float m = expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
-                                        &examined, st, slot);
-        next_cutoff = seed;
-        if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
-        int dummy = 0;
-        expand_emitting(a, sh, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy, st, slot);
-      }
-      __syncthreads();
-      DEC_PHASE(2);
-      eps_closure(a, sh, p, st, next_cutoff, sh.n_front0, &arcs_eps, slot);
-      DEC_PHASE(4);
-      store_next();
-      commit(a, sh, p, st, TS, TC, &lds, next_cutoff, &new_best);
-    }
-    DEC_PHASE(5);
-    if (prof) pacc[7]++;
-    if (a.links) lat_frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset);
-    st.offset_sum += (double)cost_offset;
-    st.frames++;
-    if (threadIdx.x == 0 && a.stats) {
-      FrameStat fs;
-      fs.ntok_in = ntok;
-      fs.ntok_out = st.ntok;
-      fs.arcs_emit = examined;
-      fs.arcs_eps = arcs_eps;
-      fs.best = new_best;
-      fs.cutoff = cutoff;
-      fs.next_cutoff = next_cutoff;
-      fs.adaptive_beam = adaptive;
-      a.stats[job.stats_row0 + f] = fs;
-    }
-    arcs_eps = 0;
-    __syncthreads();
-    if (sh.bad) st.err |= sh.bad;
-  }
-  __syncthreads();
-  if (sh.bad) st.err |= sh.bad;
-  if (st.ntok == 0 && !st.err) st.err |= 4;
-  if (threadIdx.x == 0) a.slots[slot] = st;
-  if (prof)
-    for (int i = 0; i < 8; i++) a.prof[slot * 8 + i] += pacc[i];
-#undef DEC_PHASE
-}
-
-int DecoderLdsFrameTokens() { return kLdsFrameTokens; }
-
-void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s) {
-  if (njobs <= 0) return;
-  if (a.prof) hipLaunchKernelGGL(decode_kernel<true>, dim3(njobs), dim3(DT), 0, s, a);
-  else hipLaunchKernelGGL(decode_kernel<false>, dim3(njobs), dim3(DT), 0, s, a);
-}
-
-// ---------------------------------------------------------------------------
-// traceback: best end token (with final costs if any is final), then walk
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void traceback_kernel(TraceArgs a) {
-  __shared__ unsigned long long red[4];
-  __shared__ float redf[4][2];
-  __shared__ int endpos;
-  const int slot = a.req_slot[blockIdx.x];
-  const DecSlot st = a.slots[slot];
-  const int* cs = a.cur_state + (long long)slot * a.max_tok;
-  const float* cc = a.cur_cost + (long long)slot * a.max_tok;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float bn = __int_as_float(0x7f800000), bf = __int_as_float(0x7f800000);
-  for (int i = threadIdx.x; i < st.ntok; i += 256) {
-    const float c = cc[i];
-    bn = fminf(bn, c);
-    const float fc = __int_as_float(a.sinfo[cs[i]].w);
-    if (fc != __int_as_float(0x7f800000)) bf = fminf(bf, c + fc);
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    bn = fminf(bn, __shfl_xor(bn, o, 64));
-    bf = fminf(bf, __shfl_xor(bf, o, 64));
-  }
-  if (lane == 0) { redf[w][0] = bn; redf[w][1] = bf; }
-  __syncthreads();
-  bn = fminf(fminf(redf[0][0], redf[1][0]), fminf(redf[2][0], redf[3][0]));
-  bf = fminf(fminf(redf[0][1], redf[1][1]), fminf(redf[2][1], redf[3][1]));
-  const bool any_final = bf != __int_as_float(0x7f800000);
-  const bool use_f = a.use_final && any_final;
-  unsigned long long bk = kEmpty;
-  for (int i = threadIdx.x; i < st.ntok; i += 256) {
-    float c = cc[i];
-    if (use_f) c = c + __int_as_float(a.sinfo[cs[i]].w);
-    const unsigned long long k = ((unsigned long long)ford(c) << 32) | (unsigned)cs[i];
-    bk = k < bk ? k : bk;
-  }
-  bk = wave_min_u64(bk);
-  if (lane == 0) red[w] = bk;
-  if (threadIdx.x == 0) endpos = -1;
-  __syncthreads();
-  bk = red[0];
-  for (int i = 1; i < 4; i++) bk = red[i] < bk ? red[i] : bk;
-  for (int i = threadIdx.x; i < st.ntok; i += 256)
-    if (cs[i] == (int)(unsigned)(bk & 0xffffffffu)) endpos = i;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int n = 0;
-    int* out = a.path + (long long)blockIdx.x * a.path_cap;
-    if (endpos >= 0) {
-      const int2* arena = a.arena + (long long)slot * a.arena_cap;
-      int k = st.cur_base + a.cur_pos[(long long)slot * a.max_tok + endpos];
-      while (k >= 0) {
-        const int2 e = arena[k];
-        if (e.y < 0) break;
-        if (n < a.path_cap) out[n] = e.y;
-        n++;
-        k = e.x;
-      }
-    }
-    a.path_len[blockIdx.x] = n;
-    a.end_cost[blockIdx.x] = endpos >= 0 ? funord((uint32_t)(bk >> 32)) : __int_as_float(0x7f800000);
-    a.final_rel[blockIdx.x] = any_final ? bf - bn : __int_as_float(0x7f800000);
-    a.end_state[blockIdx.x] = endpos >= 0 ? (int)(unsigned)(bk & 0xffffffffu) : -1;
-  }
-}
-
-void LaunchTraceback(const TraceArgs& a, int n, hipStream_t s) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(traceback_kernel, dim3(n), dim3(256), 0, s, a);
-}
-
-__global__ void init_keys_kernel(unsigned long long* key, int* stamp, long long n) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    key[i] = kEmpty;
-    stamp[i] = -1;
-  }
-}
-
-void LaunchInitKeys(unsigned long long* key, int* stamp, long long n, hipStream_t s) {
-  if (n <= 0) return;
-  long long blocks = (n + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(init_keys_kernel, dim3((unsigned)blocks), dim3(256), 0, s, key, stamp, n);
 }
 
 // ===========================================================================

@@ -45,14 +45,14 @@ struct RawLattice {
 };
 
 // Canonical lattice from the device records of one stream: frames [0, F]
-// (LatFrame), the token arena and the raw links.  Dead arena entries
-// (prev == -2) are skipped; emitting links whose tot is not below their
-// frame's cutoff are dropped; epsilon links are deduplicated per arc and kept
-// when (final source cost + weight) is below the cutoff.  use_final: final
-// costs of the last frame's tokens if any token is final (Kaldi GetRawLattice
-// with use_final_probs).
+// (LatFrame), the token arena {prev, arc, cost, state} and the frames'
+// links {src, dst arena index, arc, acoustic cost} (engine_dev.h; the
+// decoder already keeps exactly Kaldi's links).  Dead arena entries
+// (prev == -2) are skipped; links are sorted by (source, arc) per frame.
+// use_final: final costs of the last frame's tokens if any token is final
+// (Kaldi GetRawLattice with use_final_probs).
 void BuildRawLattice(const Graph& g, int start_state, const std::vector<LatFrame>& frames,
-                     const std::vector<int2>& arena, const std::vector<int4>& links,
+                     const std::vector<int4>& arena, const std::vector<int4>& links,
                      bool use_final, RawLattice* out);
 
 // ---- word level (lattice.cc)

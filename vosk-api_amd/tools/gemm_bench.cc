@@ -79,28 +79,7 @@ static void PeakTest() {
   }
 }
 
-static void HashTest() {
-  int* d;
-  CK(hipMalloc(&d, sizeof(int) * 3 * 64));
-  for (int n : {300, 600, 1000, 1400}) {
-    LdsHashSelfTest(n, 64, d);
-    std::vector<int> h(3 * 64);
-    CK(hipMemcpy(h.data(), d, sizeof(int) * h.size(), hipMemcpyDeviceToHost));
-    int ovf = 0, mx = 0;
-    for (int b = 0; b < 64; b++) {
-      ovf += h[3 * b] != 0;
-      mx = std::max(mx, h[3 * b + 2]);
-    }
-    printf("lds hash n=%d: blocks with overflow %d/64, first block ovf=%d n_new=%d used=%d\n", n, ovf,
-           h[0], h[1], h[2]);
-  }
-}
-
 int main(int argc, char** argv) {
-  if (getenv("GB_HASH")) {
-    HashTest();
-    return 0;
-  }
   PeakTest();
   const int reps = argc > 1 ? atoi(argv[1]) : 50;
   const int S = 256, R = 512;

@@ -193,6 +193,121 @@ def build_graph(rng, tids, num_base, vocab):
     return f, words
 
 
+def build_bigram_graph(rng, tids, num_base, vocab, num_hist=1000, fut=400):
+    """Bigram HCLG at the scale of a large model's static graph (BASELINE
+    config 4: vosk-model-en-us-0.22's HCLG, src/batch_model.cc:51-54): the
+    unigram state owns a lexicon prefix tree over the whole vocabulary, and
+    each of `num_hist` bigram histories owns its own prefix tree over `fut`
+    successor words (as a determinized/minimized HCLG keeps one word-prefix
+    copy per LM state), a backoff epsilon arc to the unigram state and a final
+    cost.  A word end goes to the word's bigram history when it has one, else
+    to the unigram state.  Built vectorized (numpy) so multi-million-state
+    graphs take seconds.  Returns (kf.Fst, words)."""
+    words, seen = [], set()
+    while len(words) < vocab:
+        n = int(rng.integers(1, 8))
+        pron = tuple(int(p) for p in rng.integers(2, num_base + 1, size=n))
+        if pron in seen:
+            continue
+        seen.add(pron)
+        words.append(pron)
+    V = len(words)
+    ranks = rng.permutation(V) + 1
+    p = 1.0 / ranks
+    p /= p.sum()
+    uni = -np.log(p)
+    # full prefix trie over position-dependent phones; node 0 = root
+    parent, phone, prevph = [0], [0], [0]
+    children = {}
+    paths, ends = [], np.zeros(V, np.int64)
+    for wi, pron in enumerate(words):
+        node, prev, path = 0, 0, []
+        for j, bph in enumerate(pron):
+            ph = position_phone(bph, j, len(pron), num_base)
+            key = (node, ph)
+            if key not in children:
+                children[key] = len(parent)
+                parent.append(node)
+                phone.append(ph)
+                prevph.append(prev)
+            node = children[key]
+            prev = ph
+            path.append(node)
+        paths.append(path)
+        ends[wi] = node
+    parent, phone, prevph = (np.array(x, np.int64) for x in (parent, phone, prevph))
+    num_pp = int(phone.max()) + 1
+    tidf = np.zeros((num_pp, num_pp), np.int64)
+    tids_ = np.zeros((num_pp, num_pp), np.int64)
+    for l in range(num_pp):
+        for c in range(1, num_pp):
+            try:
+                tidf[l, c], tids_[l, c] = tids(l, c)
+            except KeyError:
+                pass
+    wn_ptr = np.zeros(V + 1, np.int64)
+    wn_ptr[1:] = np.cumsum([len(x) for x in paths])
+    wn_idx = np.array([n for x in paths for n in x], np.int64)
+    hist_words = rng.choice(V, size=min(num_hist, V), replace=False)
+    dest = np.zeros(V, np.int64)  # unigram state 0 unless the word is a history
+
+    src_l, il_l, ol_l, w_l, dst_l = [], [], [], [], []
+
+    def add(s, i, o, w, d):
+        s, i, o, w, d = np.broadcast_arrays(np.atleast_1d(np.asarray(s, np.int64)),
+                                            np.asarray(i, np.int64), np.asarray(o, np.int64),
+                                            np.asarray(w, np.float64), np.asarray(d, np.int64))
+        for l, x in zip((src_l, il_l, ol_l, w_l, dst_l), (s, i, o, w, d)):
+            l.append(x.ravel())
+
+    def tree(root, wsel, costs, next_state):
+        """prefix tree of the words wsel hanging off `root`; states from next_state"""
+        st = wn_ptr[wsel]
+        ln = wn_ptr[wsel + 1] - st
+        rep = np.repeat(st - np.concatenate([[0], np.cumsum(ln)[:-1]]), ln) + np.arange(ln.sum())
+        nodes = np.unique(wn_idx[rep])
+        sid = next_state + np.arange(len(nodes))
+        par = parent[nodes]
+        psid = np.where(par == 0, root, next_state + np.searchsorted(nodes, par))
+        add(psid, tidf[prevph[nodes], phone[nodes]], 0, 0.0, sid)       # enter the phone
+        add(sid, tids_[prevph[nodes], phone[nodes]], 0, 0.0, sid)       # self-loop
+        end_sid = next_state + np.searchsorted(nodes, ends[wsel])
+        return nodes, end_sid, next_state + len(nodes)
+
+    n = 1
+    s_sil = n
+    n += 1
+    sil_f, sil_s = tids(0, 1)
+    add([0, s_sil, s_sil], [sil_f, sil_s, 0], 0, [0.7, 0.0, 0.0], [s_sil, s_sil, 0])
+    hist_state = n + np.arange(len(hist_words))
+    n += len(hist_words)
+    dest[hist_words] = hist_state
+    allw = np.arange(V)
+    _, end_u, n = tree(0, allw, uni, n)
+    add(end_u, 0, allw + 1, uni, dest[allw])
+    final_h = np.full(len(hist_words), np.inf)
+    for k, h in enumerate(hist_words):
+        wsel = np.sort(rng.choice(V, size=min(fut, V), replace=False))
+        cost = uni[wsel] * rng.uniform(0.3, 0.9, size=len(wsel))
+        _, end_h, n = tree(hist_state[k], wsel, cost, n)
+        add(end_h, 0, wsel + 1, cost, dest[wsel])
+        add(hist_state[k], 0, 0, float(rng.uniform(0.3, 1.5)), 0)        # backoff
+        if rng.random() < 0.4:
+            final_h[k] = float(rng.uniform(1.0, 4.0))
+    src, il, ol, wt, dst = (np.concatenate(l) for l in (src_l, il_l, ol_l, w_l, dst_l))
+    order = np.lexsort((il == 0, src))  # per state: emitting first (stable)
+    src, il, ol, wt, dst = src[order], il[order], ol[order], wt[order], dst[order]
+    row = np.zeros(n + 1, np.int64)
+    np.add.at(row, src + 1, 1)
+    row = np.cumsum(row)
+    final = np.full(n, np.inf, np.float32)
+    final[0] = 0.0
+    final[hist_state] = final_h
+    f = kf.Fst(0, final, row, il.astype(np.int32), ol.astype(np.int32), wt.astype(np.float32),
+               dst.astype(np.int32))
+    return f, words
+
+
 def build_lookahead_graph(rng, tids, num_base, vocab, num_tids, n_big=40, fut_big=12, n_tri=12):
     """Lookahead graph pair (src/model.cc:281-285): an HCLr
     transducer (the lexicon prefix tree over the chain HMMs with optional
@@ -486,11 +601,16 @@ def calibrate(nn, feats, llh_std, ivec=None):
 
 
 def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_std=3.0,
-               ivector_dim=40, frontend="mfcc", global_cmvn=False, graph="hclg"):
+               ivector_dim=40, frontend="mfcc", global_cmvn=False, graph="hclg", graph_opts=None,
+               model_conf=None):
     """frontend: "mfcc" (conf/mfcc.conf) or "fbank" (conf/fbank.conf);
     global_cmvn: write am/global_cmvn.stats (online CMVN on the nnet input);
-    graph: "hclg" (graph/HCLG.fst) or "lookahead" (graph/HCLr.fst +
-    graph/Gr.fst + graph/disambig_tid.int, no HCLG)."""
+    graph: "hclg" (graph/HCLG.fst, unigram lexicon tree), "bigram"
+    (graph/HCLG.fst, build_bigram_graph: the multi-million-state static graph
+    of a large model) or "lookahead" (graph/HCLr.fst + graph/Gr.fst +
+    graph/disambig_tid.int, no HCLG); graph_opts: keyword arguments of the
+    graph builder; model_conf: conf/model.conf text (default MODEL_CONF)."""
+    graph_opts = graph_opts or {}
     rng = np.random.default_rng(seed)
     os.makedirs(os.path.join(out_dir, "am"), exist_ok=True)
     os.makedirs(os.path.join(out_dir, "conf"), exist_ok=True)
@@ -500,14 +620,17 @@ def make_model(out_dir, seed=7, vocab=3000, num_pdfs=2000, num_phones=40, llh_st
     with open(conf_path, "w") as f:
         f.write(FBANK_CONF if fb else MFCC_CONF)
     with open(os.path.join(out_dir, "conf", "model.conf"), "w") as f:
-        f.write(MODEL_CONF)
+        f.write(model_conf or MODEL_CONF)
     mo = nk.MfccOpts(kf.parse_conf(conf_path), fbank=fb)
 
     # silence + 4 word-position variants of each of the other base phones
     num_pos_phones = 1 + 4 * (num_phones - 1)
     tm, tids = build_transition_model(rng, num_pos_phones, num_pdfs)
     if graph == "lookahead":
-        fst, lm, words, disambig = build_lookahead_graph(rng, tids, num_phones, vocab, tm.num_tids)
+        fst, lm, words, disambig = build_lookahead_graph(rng, tids, num_phones, vocab, tm.num_tids,
+                                                         **graph_opts)
+    elif graph == "bigram":
+        fst, words = build_bigram_graph(rng, tids, num_phones, vocab, **graph_opts)
     else:
         fst, words = build_graph(rng, tids, num_phones, vocab)
     nn = build_nnet(rng, num_pdfs, mo, ivector_dim)
@@ -669,15 +792,45 @@ def add_rescore(model_dir, seed=3):
     return ng
 
 
+# Named models for the large-graph tests and the benchmark.  llh_std 1.5
+# gives the realistic active-token regime (hundreds to ~20 k tokens per frame
+# at beam 13, max-active 7000 engaged in some frames) that the reference's
+# batch decoder settings target (src/batch_model.cc:78-80).
+PRESETS = {
+    # BASELINE config 4's per-GPU share: a multi-million-state static HCLG
+    "bigram_2m": dict(seed=21, vocab=20000, num_pdfs=2000, llh_std=1.5, graph="bigram",
+                      graph_opts=dict(num_hist=2000, fut=300)),
+    # vosk-model-small-en-us scale (BASELINE config 3): 20 k-word HCLr + a
+    # ~29 k-history trigram Gr, expanded at load to ~1.9 M states
+    "la_small_en_us": dict(seed=11, vocab=20000, num_pdfs=2000, llh_std=1.5, graph="lookahead",
+                           graph_opts=dict(n_big=20000, fut_big=24, n_tri=3000)),
+}
+
+
+def make_preset(name, out_dir):
+    return make_model(out_dir, **PRESETS[name])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--vocab", type=int, default=3000)
     ap.add_argument("--pdfs", type=int, default=2000)
-    ap.add_argument("--graph", choices=("hclg", "lookahead"), default="hclg")
+    ap.add_argument("--graph", choices=("hclg", "bigram", "lookahead"), default="hclg")
+    ap.add_argument("--num-hist", type=int, default=None, help="bigram: LM histories")
+    ap.add_argument("--fut", type=int, default=None, help="bigram: successor words per history")
+    ap.add_argument("--llh-std", type=float, default=3.0,
+                    help="output log-likelihood spread the nnet is calibrated to (smaller: "
+                         "flatter scores, more active tokens)")
+    ap.add_argument("--preset", choices=sorted(PRESETS), default=None,
+                    help="a named model of models_for_bench(); overrides the other options")
     a = ap.parse_args()
-    make_model(a.out, a.seed, a.vocab, a.pdfs, graph=a.graph)
+    if a.preset:
+        make_preset(a.preset, a.out)
+    else:
+        go = {k: v for k, v in (("num_hist", a.num_hist), ("fut", a.fut)) if v is not None}
+        make_model(a.out, a.seed, a.vocab, a.pdfs, llh_std=a.llh_std, graph=a.graph, graph_opts=go)
     print(open(os.path.join(a.out, "README")).read().strip())
 
 
