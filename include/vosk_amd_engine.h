@@ -112,6 +112,9 @@ int vamd_stream_accept(VamdEngine *e, int stream, const float *samples, int n, i
 int vamd_engine_advance(VamdEngine *e, const int *streams, int n);
 int vamd_stream_frames_decoded(VamdEngine *e, int stream);
 int vamd_stream_error(VamdEngine *e, int stream);
+/* device decoder state: {tokens, arena tokens used, frames, lattice links
+   used, err, lattice overflow, prune_from, last pruned frame} */
+int vamd_stream_decoder_state(VamdEngine *e, int stream, long long *out8);
 /* feature rows [first, first+n) from the device ring, n*dim floats */
 int vamd_stream_features(VamdEngine *e, int stream, int first, int n, float *out);
 /* decoded log-likelihood rows (flag 2): copies up to cap floats, returns count */
@@ -158,6 +161,8 @@ int vamd_engine_decoder_totals(VamdEngine *e, long long *out6);
 /* decoder phase clocks (env VOSK_AMD_DEC_PROFILE=1), summed over streams:
  * [cutoff, seed, expand, compact, eps-closure, commit, 0, frames] */
 int vamd_engine_decoder_phases(VamdEngine *e, long long *out8);
+/* the same per stream slot: out[max_streams][8] */
+int vamd_engine_decoder_phases_per_stream(VamdEngine *e, long long *out);
 /* engine counters: [steps, launches, mfcc frames, chunk jobs, frames decoded] */
 int vamd_engine_counters(VamdEngine *e, long long *out5);
 

@@ -114,6 +114,25 @@ def synth_spk():
     return path
 
 
+def _make_preset(name):
+    import make_synth_model as msm
+    return _make(name, **msm.PRESETS[name])
+
+
+@pytest.fixture(scope="session")
+def synth_bigram_2m():
+    """BASELINE config 4's per-GPU share: a 2.4 M-state static HCLG (bigram
+    LM over 20 k words), flat scores (max-active 7000 engaged)."""
+    return _make_preset("bigram_2m")
+
+
+@pytest.fixture(scope="session")
+def synth_la_small_en_us():
+    """vosk-model-small-en-us scale lookahead model (20 k-word HCLr + a
+    29 k-history trigram Gr; ~1.9 M states once expanded at load)."""
+    return _make_preset("la_small_en_us")
+
+
 @pytest.fixture(scope="session")
 def test_wave():
     w = wave.open(os.path.join(REPO, "tests", "golden", "test.wav"), "rb")

@@ -1,0 +1,135 @@
+"""Large decoding graphs at batch scale (BASELINE configs 3 and 4; SURVEY.md
+A10/A11): 64 streams decoded together through the pipelined engine with
+lattices (and PruneActiveTokens) on
+
+* a 2.4 M-state static HCLG (config 4's per-GPU share of a large model), and
+* the ~1.9 M-state static expansion of a vosk-model-small-en-us-scale
+  lookahead model (config 3's model),
+
+both with flat enough scores that max-active 7000 engages (the oracle sees
+frames with far more than 7000 tokens).  Every stream's best path equals the
+C oracle's on the same graph.  A 60 s stream without an endpoint keeps a
+bounded arena and never sets an error.
+"""
+import multiprocessing as mp
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+import kaldi_formats as kf
+import oracle_py
+from conftest import perturbed_stream
+
+pytestmark = pytest.mark.gpu
+
+NSTREAMS = 64
+SECS = 5.0
+_ORC = {}
+
+
+def _orc_job(i):
+    r = _ORC["o"].recognize(_ORC["waves"][i])
+    return r["path"], int(r["ntok"].max())
+
+
+def _oracle_paths(oracle_dir, waves):
+    o = oracle_py.OracleModel(oracle_dir, fpc=51)  # the engine's chunking (i-vector per chunk)
+    _ORC.update(o=o, waves=waves)
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    with mp.get_context("fork").Pool(workers) as pool:
+        res = pool.map(_orc_job, range(len(waves)))
+    _ORC.clear()
+    return res, o.max_active
+
+
+def _expanded_model(model_dir, out_dir):
+    """A copy of a lookahead model whose graph/HCLG.fst is libvosk's own
+    static expansion of HCLr o Gr (vamd_graph_*; the expansion itself is
+    checked against the Python restatement in test_lookahead_graph.py): the
+    oracle decodes the graph the engine decodes."""
+    import ctypes as C
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "vosk-api_amd", "vosk",
+                              "libvosk.so"))
+    lib.vamd_graph_new.restype = C.c_void_p
+    lib.vamd_graph_new.argtypes = [C.c_char_p, C.c_char_p]
+    lib.vamd_graph_dims.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]
+    lib.vamd_graph_copy.argtypes = [C.c_void_p] + [C.c_void_p] * 6
+    lib.vamd_graph_free.argtypes = [C.c_void_p]
+    h = lib.vamd_graph_new(model_dir.encode(), None)
+    assert h
+    st, na = C.c_int(), C.c_longlong()
+    S = lib.vamd_graph_dims(h, C.byref(st), C.byref(na))
+    A = na.value
+    g = kf.Fst(st.value, np.zeros(S, np.float32), np.zeros(S + 1, np.int64), np.zeros(A, np.int32),
+               np.zeros(A, np.int32), np.zeros(A, np.float32), np.zeros(A, np.int32))
+    lib.vamd_graph_copy(h, g.final.ctypes.data, g.row.ctypes.data, g.ilabel.ctypes.data,
+                        g.olabel.ctypes.data, g.weight.ctypes.data, g.nextstate.ctypes.data)
+    lib.vamd_graph_free(h)
+    if os.path.exists(out_dir):
+        shutil.rmtree(out_dir)
+    shutil.copytree(model_dir, out_dir, ignore=shutil.ignore_patterns("HCLr.fst", "Gr.fst", "disambig_tid.int"))
+    kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), g)
+    return out_dir, S
+
+
+def _batch_decode(model_dir, test_wave):
+    from vosk import engine
+    waves = [perturbed_stream(test_wave, 100 + i, seconds=SECS + 0.05 * i) for i in range(NSTREAMS)]
+    e = engine.Engine(model_dir, frames_per_chunk=51, max_streams=NSTREAMS, pipeline=True, lattice=True)
+    e.set_step_samples(51 * 160)
+    ss = [e.new_stream() for _ in range(NSTREAMS)]
+    for s, w in zip(ss, waves):
+        e.preload(s, w, finished=True)
+    steps = 0
+    while e.step(ss):
+        steps += 1
+        assert steps < 2000
+    out = []
+    for s in ss:
+        st = e.decoder_state(s)
+        assert st["err"] == 0 and st["lat_ovf"] == 0, st
+        assert st["last_prune"] > 0
+        out.append(e.best_path(s, use_final=True)[0])
+    e.close()
+    return waves, out
+
+
+def test_static_hclg_2m_states_64_streams(synth_bigram_2m, test_wave):
+    waves, paths = _batch_decode(synth_bigram_2m, test_wave)
+    ref, max_active = _oracle_paths(synth_bigram_2m, waves)
+    for k in range(NSTREAMS):
+        np.testing.assert_array_equal(paths[k], ref[k][0], err_msg=f"stream {k}")
+    assert max(r[1] for r in ref) > max_active  # max-active engaged
+
+
+def test_lookahead_expansion_64_streams(synth_la_small_en_us, test_wave, tmp_path):
+    odir, S = _expanded_model(synth_la_small_en_us, str(tmp_path / "la_hclg"))
+    assert S > 1_000_000
+    waves, paths = _batch_decode(synth_la_small_en_us, test_wave)
+    ref, max_active = _oracle_paths(odir, waves)
+    for k in range(NSTREAMS):
+        np.testing.assert_array_equal(paths[k], ref[k][0], err_msg=f"stream {k}")
+    assert max(r[1] for r in ref) > max_active
+
+
+def test_60s_stream_without_endpoint_stays_bounded(synth_bigram_2m, test_wave):
+    """One decoder segment of 60 s (2000 frames, thousands of tokens per
+    frame): pruning keeps the arena and link arena small and nothing
+    overflows; the best path equals the oracle's."""
+    from vosk import engine
+    w = perturbed_stream(test_wave, 4242, seconds=60.0)
+    e = engine.Engine(synth_bigram_2m, frames_per_chunk=51, max_streams=2, lattice=True)
+    s = e.new_stream()
+    e.preload(s, w, finished=True)
+    while e.step([s]):
+        pass
+    st = e.decoder_state(s)
+    assert st["err"] == 0 and st["lat_ovf"] == 0, st
+    assert st["frames"] >= 1990
+    # ~2000 frames of several thousand tokens each without pruning
+    assert st["arena_used"] < 1_000_000 and st["links_used"] < 2_000_000, st
+    o = oracle_py.OracleModel(synth_bigram_2m, fpc=51)
+    r = o.recognize(w)
+    np.testing.assert_array_equal(e.best_path(s, use_final=True)[0], r["path"])

@@ -15,6 +15,14 @@ pytestmark = pytest.mark.gpu
 FRAME_PATHS = {"default": None, "hbm": "0", "mixed": "2"}
 
 
+@pytest.fixture(autouse=True)
+def no_pruning(monkeypatch):
+    """Frame-by-frame raw lattices are compared: PruneActiveTokens off (its
+    effect, nothing after the lattice-beam prune, is tested in
+    test_decoder_prune_gpu.py)."""
+    monkeypatch.setenv("VOSK_AMD_DEC_PRUNE", "0")
+
+
 @pytest.fixture(params=sorted(FRAME_PATHS))
 def frame_path(request, monkeypatch):
     v = FRAME_PATHS[request.param]

@@ -1,21 +1,27 @@
 // Token passing on MI355X (gfx950): Kaldi LatticeFasterDecoder's per-frame
 // GetCutoff / ProcessEmitting / ProcessNonemitting over a CSR graph in HBM,
 // with Kaldi's forward links kept per stream for lattices, the best-path
-// traceback, and the periodic lattice pruning that keeps every stream's
-// arenas bounded (PruneActiveTokens).  Reference call sites:
-// src/recognizer.cc:39-43 (decoder), :318 (endpoint), :790 (best path);
-// src/batch_model.cc:78-80 (batch options).
+// traceback, and the periodic pruning that keeps every stream's arenas
+// bounded (PruneActiveTokens).  Reference call sites: src/recognizer.cc:39-43
+// (decoder), :318 (endpoint), :790 (best path); src/batch_model.cc:78-80
+// (batch options).
 //
 // Per-stream state is bounded by the token counts, never by the graph size:
 // the frame under construction lives in an LDS open-addressing table (4096
 // slots); a state whose first kMaxProbe LDS slots are taken by other states
-// lives in a per-stream HBM hash table instead (two of them, ping-pong: the
-// current frame's HBM-resident tokens stay findable while the next frame is
-// built).  Placement is deterministic within a frame -- LDS slots are only
-// ever claimed, never released, during a frame, so every thread that relaxes
-// a state finds it in the same place -- and the table a state lands in has no
-// effect on any cost, key or backpointer, so results are those of the
-// order-independent formulation restated in oracle/oracle.c.
+// lives in the stream's HBM hash table instead.  Placement is deterministic
+// within a frame -- slots are only ever claimed, never released, while a
+// frame is built -- so a relaxation's slot stays valid until the commit, and
+// the table a state lands in has no effect on any cost, key or backpointer:
+// results are those of the order-independent formulation restated in
+// oracle/oracle.c.
+//
+// Backpointers are resolved while relaxing: a relaxation whose (cost, arc)
+// key is still its slot's minimum after the pass's next barrier writes its
+// source (the arena index of an emitting source, the frame-table slot of an
+// epsilon source) into the slot.  A later pass can only lower the key, and a
+// later winner writes after that barrier, so the last write is the final
+// winner's.  The commit therefore never reloads an arc or looks a source up.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -37,14 +43,25 @@ constexpr int kHashCap = 4096;        // LDS frame table slots (power of two)
 constexpr int kHashBits = 12;
 constexpr int kMaxProbe = 32;         // default LDS probe limit (DecArgs::lds_probe); states past it live in HBM
 constexpr int kFrontLds = 2048;       // epsilon frontier entries in LDS (more spill to HBM)
+constexpr int kUnroll = 4;            // (token, arc) items in flight per thread in the emitting pass
 constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
 constexpr unsigned kDestEps = 0x80000000u;  // arcs[].w: nextstate has epsilon arcs
+// backpointer of a frame-table slot: an emitting source's arena index (>= 0),
+// or kBpEps | the epsilon source's slot (kBpHbm: an HBM-table slot)
+constexpr int kBpEps = (int)0x80000000u;
+constexpr int kBpHbm = 0x40000000;
+constexpr unsigned short kPosEps = 0x8000;  // LDS list position flag: the state has epsilon arcs
+constexpr int kHPosEps = 0x40000000;        // the same flag in an HBM table position
+// pruning: links / tokens are dropped only beyond lattice_beam + this margin,
+// so float rounding never drops what the host's exact (double) lattice-beam
+// prune keeps (the pruned lattice is unchanged)
+constexpr float kPruneMargin = 0.5f;
 
 struct DecShared {
   int scan[DT + 1];   // exclusive prefix sums of the chunk's degrees
   int abeg[DT];       // first arc per chunk token
   float tcost[DT];    // cost per chunk token
-  int tsrc[DT];       // arena index per chunk token (lattice links)
+  int tsrc[DT];       // source per chunk token (arena index / epsilon slot code)
   unsigned hist[256];
   unsigned long long red_u[DW];
   float red_f[DW];
@@ -52,7 +69,9 @@ struct DecShared {
   int n_new_l, n_new_g, n_next, n_front, n_fnext, total, sel_k, n_links, lat_ovf, n_eps;
   unsigned sel_prefix, sel_mask;
   float seed;
-  int bad;
+  int bad, flag;
+  LatFrame fr;        // pruning: the frame record being processed (broadcast)
+  LatFrame fr1;
 };
 
 __device__ __forceinline__ float wave_min_f(float v) {
@@ -187,29 +206,25 @@ __device__ __forceinline__ float kth_smallest(DecShared& sh, const TokView& tv, 
 }
 
 // ---------------------------------------------------------------------------
-// frame tables
+// frame table: LDS slots first, the stream's HBM table for the rest
 // ---------------------------------------------------------------------------
-// LDS: the frame under construction (state, (cost, arc) key, list position,
-// epsilon round stamp, list of slots) and the previous frame's (state, list
-// position) pairs, double-buffered by swapping the pointers at each commit.
 struct FrameLds {
   int* hs;                  // [kHashCap] state, -1 = empty
-  unsigned short* hp;       // [kHashCap] position in the frame's list
-  const int* ps;            // previous frame: state per slot
-  const unsigned short* pp; // previous frame: list position per slot
   unsigned long long* hk;   // [kHashCap] (ordered cost << 32 | arc), kEmpty
+  int* hb;                  // [kHashCap] backpointer (kBpEps encoding)
+  unsigned short* hp;       // [kHashCap] list position | kPosEps
   int* hst;                 // [kHashCap] epsilon round stamp
   unsigned short* nl;       // [kHashCap] list -> slot
-  int* fr0;                 // [kFrontLds] epsilon frontiers (tagged slots)
+  int* fr0;                 // [kFrontLds] epsilon frontiers (slot codes)
   int* fr1;
 };
 
-// HBM: one of the stream's two overflow tables
 struct HbmTab {
   int* state;               // [H] -1 = empty
   unsigned long long* key;  // [H]
-  int* pos;                 // [H] creation index (list position - the frame's LDS count)
+  int* pos;                 // [H] creation index | kHPosEps
   int* stamp;               // [H]
+  int* bp;                  // [H]
   int* list;                // [max_tok] slots in creation order
 };
 
@@ -225,14 +240,6 @@ __device__ __forceinline__ unsigned hbm_hash(int s, int bits) {
   return x >> (32 - bits);
 }
 
-// DecSlot's per-table list counts, selected without indexing (an indexed
-// array in a register struct would be placed in scratch)
-__device__ __forceinline__ int tab_n(const DecSlot& st, int t) { return t ? st.tab_n1 : st.tab_n0; }
-__device__ __forceinline__ void set_tab_n(DecSlot& st, int t, int v) {
-  if (t) st.tab_n1 = v;
-  else st.tab_n0 = v;
-}
-
 struct DecPtrs {
   int* cs;     // current tokens: state
   float* cc;   //                 cost
@@ -243,17 +250,15 @@ struct DecPtrs {
   int slot;
 };
 
-// HBM table t (0 or 1) of a stream: plain address arithmetic (no indexed
-// struct arrays, which would live in scratch)
-__device__ __forceinline__ HbmTab hbm_tab(const DecArgs& a, int slot, int t) {
-  const long long H = 1ll << a.hbits;
-  const long long o = ((long long)slot * 2 + t) * H;
+__device__ __forceinline__ HbmTab hbm_tab(const DecArgs& a, int slot) {
+  const long long o = (long long)slot << a.hbits;
   HbmTab r;
   r.state = a.ht_state + o;
   r.key = a.ht_key + o;
   r.pos = a.ht_pos + o;
   r.stamp = a.ht_stamp + o;
-  r.list = a.ht_list + ((long long)slot * 2 + t) * a.max_tok;
+  r.bp = a.ht_bp + o;
+  r.list = a.ht_list + (long long)slot * a.max_tok;
   return r;
 }
 
@@ -264,7 +269,7 @@ struct Relax {
 };
 
 __device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const FrameLds& t,
-                                       const HbmTab& T, int dest, float tot, int arc) {
+                                       const HbmTab& T, int dest, float tot, int arc, bool eps) {
   const unsigned long long k = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
   unsigned h = lds_hash(dest);
   for (int probe = 0; probe < a.lds_probe; probe++) {
@@ -274,7 +279,7 @@ __device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const Fr
       if (cur == -1) {
         const int pos = atomicAdd(&sh.n_new_l, 1);  // < kHashCap: one per claimed slot
         t.nl[pos] = (unsigned short)h;
-        t.hp[h] = (unsigned short)pos;
+        t.hp[h] = (unsigned short)(pos | (eps ? kPosEps : 0));
         atomicMin(&t.hk[h], k);
         return Relax{(int)h, 2};
       }
@@ -295,7 +300,7 @@ __device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const Fr
         const int pos = atomicAdd(&sh.n_new_g, 1);
         if (pos < a.max_tok) {
           AG_ST(&T.list[pos], (int)g);
-          AG_ST(&T.pos[g], pos);
+          AG_ST(&T.pos[g], pos | (eps ? kHPosEps : 0));
         } else {
           sh.bad |= 1;
         }
@@ -319,13 +324,27 @@ __device__ __forceinline__ unsigned long long slot_key(const FrameLds& t, const 
 __device__ __forceinline__ int slot_state(const FrameLds& t, const HbmTab& T, int v) {
   return v >= 0 ? t.hs[v] : AG_LD(&T.state[~v]);
 }
+__device__ __forceinline__ void set_bp(const FrameLds& t, const HbmTab& T, int v, int bp) {
+  if (v >= 0) t.hb[v] = bp;
+  else AG_ST(&T.bp[~v], bp);
+}
+// list position of a slot of the frame under construction (nl_n = its LDS count)
+__device__ __forceinline__ int slot_pos(const FrameLds& t, const HbmTab& T, int nl_n, int v) {
+  return v >= 0 ? (int)(t.hp[v] & 0x7fff) : nl_n + (AG_LD(&T.pos[~v]) & (kHPosEps - 1));
+}
+// the epsilon-source slot code of a relaxation from slot v
+__device__ __forceinline__ int eps_bp(int v) { return kBpEps | (v >= 0 ? v : (kBpHbm | ~v)); }
+__device__ __forceinline__ int bp_slot(int bp) {
+  const int c = bp & ~kBpEps;
+  return (c & kBpHbm) ? ~(c & (kBpHbm - 1)) : c;
+}
 
-// list position of state s in the frame under construction (nl_n = its LDS count)
+// list position of state s in the frame under construction (eps links at commit)
 __device__ __forceinline__ int frame_pos(const DecArgs& a, const FrameLds& t, const HbmTab& T, int nl_n, int s) {
   unsigned h = lds_hash(s);
   for (int probe = 0; probe < a.lds_probe; probe++) {
     const int c = t.hs[h];
-    if (c == s) return t.hp[h];
+    if (c == s) return t.hp[h] & 0x7fff;
     if (c == -1) break;
     h = (h + 1) & (kHashCap - 1);
   }
@@ -333,31 +352,7 @@ __device__ __forceinline__ int frame_pos(const DecArgs& a, const FrameLds& t, co
   unsigned g = hbm_hash(s, a.hbits);
   for (int probe = 0; probe < a.hprobe; probe++) {
     const int c = AG_LD(&T.state[g]);
-    if (c == s) return nl_n + AG_LD(&T.pos[g]);
-    if (c == -1) break;
-    g = (g + 1) & hm;
-  }
-  return -1;
-}
-
-// list position of state s in the current (committed) frame: the previous
-// LDS table, else the HBM table of the current frame (cur_tab)
-__device__ __forceinline__ int prev_pos(const DecArgs& a, const FrameLds& t, const DecPtrs& p, const DecSlot& st,
-                        int s) {
-  unsigned h = lds_hash(s);
-  for (int probe = 0; probe < a.lds_probe; probe++) {
-    const int c = t.ps[h];
-    if (c == s) return t.pp[h];
-    if (c == -1) break;
-    h = (h + 1) & (kHashCap - 1);
-  }
-  if (st.cur_tab < 0) return -1;
-  const HbmTab T = hbm_tab(a, p.slot, st.cur_tab);
-  const unsigned hm = (1u << a.hbits) - 1u;
-  unsigned g = hbm_hash(s, a.hbits);
-  for (int probe = 0; probe < a.hprobe; probe++) {
-    const int c = AG_LD(&T.state[g]);
-    if (c == s) return st.cur_nl + AG_LD(&T.pos[g]);
+    if (c == s) return nl_n + (AG_LD(&T.pos[g]) & (kHPosEps - 1));
     if (c == -1) break;
     g = (g + 1) & hm;
   }
@@ -378,14 +373,15 @@ __device__ __forceinline__ int get_front(const FrameLds& t, const DecPtrs& p, in
 // ---------------------------------------------------------------------------
 // lattice links.  During the emitting pass every relaxation below the bound
 // appends {src arena index, tot bits, arc, acoustic cost bits} to the
-// stream's link arena; the commit keeps those below the frame's final cutoff
-// with tot replaced by the destination's arena index, then appends the
-// frame's epsilon links from the final token costs (one per arc, Kaldi
-// re-expands a token whenever it improves: ProcessNonemitting).  A committed
-// link is {src arena index, dst arena index, arc, acoustic cost bits}.
+// stream's link arena and its destination slot to link_dst; the commit keeps
+// those below the frame's final cutoff with tot replaced by the destination's
+// arena index, then appends the frame's epsilon links from the final token
+// costs (one per arc, Kaldi re-expands a token whenever it improves:
+// ProcessNonemitting).  A committed link is {src arena index, dst arena
+// index, arc, acoustic cost bits}.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long long used, int slot,
-                                          int4 rec) {
+                                          int4 rec, int dslot) {
   const unsigned long long m = __ballot(1);
   const int lane = threadIdx.x & 63;
   const int leader = __ffsll((long long)m) - 1;
@@ -394,12 +390,19 @@ __device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long 
   base = __shfl(base, leader, 64);
   const int off = __popcll(m & ((1ull << lane) - 1ull));
   const long long pos = used + base + off;
-  if (pos < a.link_cap) a.links[(long long)slot * a.link_cap + pos] = rec;
-  else sh.lat_ovf = 1;
+  if (pos < a.link_cap) {
+    a.links[(long long)slot * a.link_cap + pos] = rec;
+    a.link_dst[(long long)slot * a.link_cap + pos] = dslot;
+  } else {
+    sh.lat_ovf = 1;
+  }
 }
 
 // one emitting expansion pass over the current tokens (ProcessEmitting):
-// mode 0 = minimum only, 1 = relax below `bound` (+ minimum)
+// mode 0 = minimum only, 1 = relax below `bound` (+ minimum).  Items are
+// processed kUnroll per thread at a time (arc loads in flight together),
+// each sub-round closed by a barrier after which the sub-round's winners
+// write their backpointers.
 __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh, const FrameLds& t,
                                  const HbmTab& T, const DecPtrs& p, const TokView& tv, int ntok,
                                  float cutoff, float cost_offset, const float* Lp, int mode,
@@ -416,7 +419,7 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
         const int4 si = a.sinfo[tv.s(i)];
         ab = si.x;
         deg = si.y - si.x;
-        if (lat) src = st.cur_base + AG_LD(&p.cp[i]);
+        if (mode == 1) src = st.cur_base + AG_LD(&p.cp[i]);
       }
     }
     block_scan(sh, deg);
@@ -426,20 +429,48 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
     __syncthreads();
     const int total = sh.total;
     *examined += total;
-    for (int it = threadIdx.x; it < total; it += DT) {
-      const int j = owner(sh, it);
-      const int arc = sh.abeg[j] + (it - sh.scan[j]);
-      const int4 A = a.arcs[arc];
-      const float ac = cost_offset - Lp[A.z];
-      const float tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
-      m = fminf(m, tot);
-      if (mode == 1 && tot < bound) {
-        if (lat)
-          emit_link(a, sh, st.links_used, slot,
-                    make_int4(sh.tsrc[j], __float_as_int(tot), arc, __float_as_int(ac)));
-        const Relax r = relax(a, sh, t, T, A.x, tot, arc);
-        if (r.flags == 2 && ((unsigned)A.w & kDestEps))
-          push_front(a, sh, t, p, 0, &sh.n_front, r.slot);
+    for (int sb = 0; sb < total; sb += DT * kUnroll) {
+      int4 A[kUnroll];
+      int jv[kUnroll], arcv[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        const int it = sb + u * DT + (int)threadIdx.x;
+        jv[u] = -1;
+        if (it < total) {
+          const int j = owner(sh, it);
+          jv[u] = j;
+          arcv[u] = sh.abeg[j] + (it - sh.scan[j]);
+          A[u] = a.arcs[arcv[u]];
+        }
+      }
+      int sv[kUnroll];
+      unsigned long long kv[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        sv[u] = 0x7fffffff;
+        if (jv[u] < 0) continue;
+        const int j = jv[u];
+        const float ac = cost_offset - Lp[A[u].z];
+        const float tot = (sh.tcost[j] + ac) + __int_as_float(A[u].y);
+        m = fminf(m, tot);
+        if (mode == 1 && tot < bound) {
+          const bool de = ((unsigned)A[u].w & kDestEps) != 0;
+          const Relax r = relax(a, sh, t, T, A[u].x, tot, arcv[u], de);
+          if (r.flags > 0) {
+            sv[u] = r.slot;
+            kv[u] = ((unsigned long long)ford(tot) << 32) | (unsigned)arcv[u];
+          }
+          if (lat)
+            emit_link(a, sh, st.links_used, slot,
+                      make_int4(sh.tsrc[j], __float_as_int(tot), arcv[u], __float_as_int(ac)), r.slot);
+          if (r.flags == 2 && de) push_front(a, sh, t, p, 0, &sh.n_front, r.slot);
+        }
+      }
+      if (mode == 1) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++)
+          if (sv[u] != 0x7fffffff && slot_key(t, T, sv[u]) == kv[u]) set_bp(t, T, sv[u], sh.tsrc[jv[u]]);
       }
     }
     __syncthreads();
@@ -463,10 +494,10 @@ __device__ __forceinline__ void eps_closure(const DecArgs& a, DecShared& sh, con
     if (threadIdx.x == 0) sh.n_fnext = 0;
     for (int c0 = 0; c0 < nfront; c0 += DT) {
       const int i = c0 + threadIdx.x;
-      int deg = 0, ab = 0;
+      int deg = 0, ab = 0, v = 0;
       float c = 0.0f;
       if (i < nfront) {
-        const int v = get_front(t, p, b, i);
+        v = get_front(t, p, b, i);
         c = funord((uint32_t)(slot_key(t, T, v) >> 32));
         if (c < cutoff) {  // created tokens are < cutoff; dead ones are not
           const int4 si = a.sinfo[slot_state(t, T, v)];
@@ -477,22 +508,35 @@ __device__ __forceinline__ void eps_closure(const DecArgs& a, DecShared& sh, con
       block_scan(sh, deg);
       sh.abeg[threadIdx.x] = ab;
       sh.tcost[threadIdx.x] = c;
+      sh.tsrc[threadIdx.x] = eps_bp(v);
       __syncthreads();
       const int total = sh.total;
       examined += total;
-      for (int it = threadIdx.x; it < total; it += DT) {
-        const int j = owner(sh, it);
-        const int arc = sh.abeg[j] + (it - sh.scan[j]);
-        const int4 A = a.arcs[arc];
-        const float tot = sh.tcost[j] + __int_as_float(A.y);
-        if (tot < cutoff) {
-          const Relax r = relax(a, sh, t, T, A.x, tot, arc);
-          if (r.flags > 0 && ((unsigned)A.w & kDestEps)) {
-            const int old = r.slot >= 0 ? atomicExch(&t.hst[r.slot], stamp)
-                                        : atomicExch(&T.stamp[~r.slot], stamp);
-            if (old != stamp) push_front(a, sh, t, p, b ^ 1, &sh.n_fnext, r.slot);
+      for (int sb = 0; sb < total; sb += DT) {
+        const int it = sb + threadIdx.x;
+        int sv = 0x7fffffff, j = 0;
+        unsigned long long kk = 0;
+        if (it < total) {
+          j = owner(sh, it);
+          const int arc = sh.abeg[j] + (it - sh.scan[j]);
+          const int4 A = a.arcs[arc];
+          const float tot = sh.tcost[j] + __int_as_float(A.y);
+          if (tot < cutoff) {
+            const bool de = ((unsigned)A.w & kDestEps) != 0;
+            const Relax r = relax(a, sh, t, T, A.x, tot, arc, de);
+            if (r.flags > 0) {
+              sv = r.slot;
+              kk = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
+              if (de) {
+                const int old = r.slot >= 0 ? atomicExch(&t.hst[r.slot], stamp)
+                                            : atomicExch(&T.stamp[~r.slot], stamp);
+                if (old != stamp) push_front(a, sh, t, p, b ^ 1, &sh.n_fnext, r.slot);
+              }
+            }
           }
         }
+        __syncthreads();
+        if (sv != 0x7fffffff && slot_key(t, T, sv) == kk) set_bp(t, T, sv, sh.tsrc[j]);
       }
       __syncthreads();
     }
@@ -510,7 +554,7 @@ __device__ __forceinline__ void lds_clear_build(const FrameLds& t) {
   }
 }
 
-// clears the listed entries of an HBM table
+// clears the listed entries of the HBM table
 __device__ __forceinline__ void hbm_clear_listed(const HbmTab& T, int n) {
   for (int j = threadIdx.x; j < n; j += DT) {
     const int g = AG_LD(&T.list[j]);
@@ -529,13 +573,15 @@ __device__ __forceinline__ void hbm_clear_all(const DecArgs& a, const HbmTab& T)
 
 // Lattice side of a commit (all threads; the frame tables are still intact):
 // keep this frame's emitting records below the cutoff, resolved to arena
-// indices (chunked in-place compaction: writes never pass the chunk being
-// read), then the epsilon links of the committed tokens.  Returns the
-// frame's link count.
+// indices through their destination slots (chunked in-place compaction:
+// writes never pass the chunk being read), then the epsilon links of the
+// committed tokens that have epsilon arcs (listed by the commit in the
+// frontier arrays, neps of them).  Returns the frame's link count.
 __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
-                            const DecPtrs& p, const DecSlot& st, const int* TS, const float* TC,
-                            int slot, int base, int nl_n, int live, float cutoff) {
+                            const DecPtrs& p, const DecSlot& st, int slot, int base, int nl_n,
+                            int neps, float cutoff) {
   int4* L = a.links + (long long)slot * a.link_cap;
+  const int* LD = a.link_dst + (long long)slot * a.link_cap;
   const long long lb = st.links_used;
   long long nrec = sh.n_links;
   if (lb + nrec > a.link_cap) nrec = a.link_cap - lb > 0 ? a.link_cap - lb : 0;
@@ -547,11 +593,8 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
     if (i < nrec) {
       r = L[lb + i];
       if (__int_as_float(r.y) < cutoff) {
-        const int d = frame_pos(a, t, T, nl_n, a.arcs[r.z].x);
-        if (d >= 0) {
-          r.y = base + d;
-          keep = 1;
-        }
+        r.y = base + slot_pos(t, T, nl_n, LD[lb + i]);
+        keep = 1;
       }
     }
     block_scan(sh, keep);
@@ -561,17 +604,18 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
   }
   // epsilon links of the committed tokens, at their final costs
   if (threadIdx.x == 0) sh.n_eps = 0;
-  for (int c0 = 0; c0 < live; c0 += DT) {
+  for (int c0 = 0; c0 < neps; c0 += DT) {
     const int q = c0 + threadIdx.x;
     int deg = 0, ab = 0, src = 0;
     float c = 0.0f;
-    if (q < live) {
-      const int s = q < kTokLds ? TS[q] : AG_LD(&p.cs[q]);
-      c = q < kTokLds ? TC[q] : AG_LD(&p.cc[q]);
+    if (q < neps) {
+      const int v = get_front(t, p, 0, q);
+      const int s = slot_state(t, T, v);
+      c = funord((uint32_t)(slot_key(t, T, v) >> 32));
       const int4 si = a.sinfo[s];
       ab = si.y;
       deg = si.z - si.y;
-      src = base + AG_LD(&p.cp[q]);
+      src = base + slot_pos(t, T, nl_n, v);
     }
     block_scan(sh, deg);
     sh.abeg[threadIdx.x] = ab;
@@ -607,50 +651,48 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
 // Move the frame under construction into the arena + current token arrays
 // (global, and the LDS cache when it fits).  List entries whose cost is not
 // below `cutoff` (dead: created by the single emitting pass above the final
-// next_cutoff) keep an arena slot marked dead.  Then the previous frame's
-// HBM table is cleared and the LDS tables swap roles.
+// next_cutoff) keep an arena slot marked dead.  Then both tables are cleared.
 __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds& t, DecPtrs& p, DecSlot& st,
                        int* TS, float* TC, bool* lds, float cutoff, float* best_out, int slot,
-                       int y, int* nlinks) {
+                       int* nlinks) {
   __syncthreads();
-  const HbmTab T = hbm_tab(a, slot, y);
+  const HbmTab T = hbm_tab(a, slot);
   const int nl_n = sh.n_new_l;
   const int ng = sh.n_new_g < a.max_tok ? sh.n_new_g : a.max_tok;
   const int n = nl_n + ng;
   const int base = st.arena_used;
   const bool ok = (long long)base + n <= a.arena_cap;
-  if (threadIdx.x == 0) sh.n_next = 0;
+  const bool lat = a.links != nullptr;
+  if (threadIdx.x == 0) {
+    sh.n_next = 0;
+    sh.n_front = 0;
+  }
   __syncthreads();
   unsigned long long bk = kEmpty;
   for (int j = threadIdx.x; j < n; j += DT) {
-    int s;
+    int s, bp, v;
     unsigned long long k;
+    bool has_eps;
     if (j < nl_n) {
-      const int h = t.nl[j];
-      s = t.hs[h];
-      k = t.hk[h];
+      v = t.nl[j];
+      s = t.hs[v];
+      k = t.hk[v];
+      bp = t.hb[v];
+      has_eps = (t.hp[v] & kPosEps) != 0;
     } else {
       const int g = AG_LD(&T.list[j - nl_n]);
+      v = ~g;
       s = AG_LD(&T.state[g]);
       k = AG_LD(&T.key[g]);
+      bp = AG_LD(&T.bp[g]);
+      has_eps = (AG_LD(&T.pos[g]) & kHPosEps) != 0;
     }
     const int arc = (int)(unsigned)(k & 0xffffffffu);
     const float cost = funord((uint32_t)(k >> 32));
     if (ok && cost < cutoff) {
       int prev = -1;
-      if (arc >= 0) {
-        const int4 A = a.arcs[arc];
-        const int src = (int)((unsigned)A.w & 0x7fffffffu);
-        if (A.z >= 0) {
-          const int pp = prev_pos(a, t, p, st, src);
-          prev = pp >= 0 ? st.cur_base + pp : -1;
-        } else {
-          const int fp = frame_pos(a, t, T, nl_n, src);
-          prev = fp >= 0 ? base + fp : -1;
-        }
-        if (prev < 0) sh.bad |= 8;  // a source the tables cannot place (never expected)
-      }
-      p.arena[base + j] = make_int4(prev, arc, __float_as_int(cost), s);
+      if (arc >= 0) prev = (bp & kBpEps) ? base + slot_pos(t, T, nl_n, bp_slot(bp)) : bp;
+      ag_st4(&p.arena[base + j], make_int4(prev, arc, __float_as_int(cost), s));
       const int q = atomicAdd(&sh.n_next, 1);
       AG_ST(&p.cs[q], s);
       AG_ST(&p.cc[q], cost);
@@ -659,30 +701,22 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
         TS[q] = s;
         TC[q] = cost;
       }
+      if (lat && has_eps) push_front(a, sh, t, p, 0, &sh.n_front, v);
       const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)s;
       bk = tk < bk ? tk : bk;
     } else if (ok) {
-      p.arena[base + j] = make_int4(-2, -1, __float_as_int(cost), s);  // dead list entry
+      ag_st4(&p.arena[base + j], make_int4(-2, -1, __float_as_int(cost), s));  // dead list entry
     }
   }
   bk = block_min_u64(sh, bk);  // ends with a barrier
   if (!ok) sh.bad |= 2;
   const int live = sh.n_next;
-  *nlinks = (a.links && ok) ? commit_links(a, sh, t, T, p, st, TS, TC, slot, base, nl_n, live, cutoff)
-                            : 0;
-  // the previous frame's HBM table has served its lookups
-  if (st.cur_tab >= 0) hbm_clear_listed(hbm_tab(a, slot, st.cur_tab), tab_n(st, st.cur_tab));
+  const int neps = sh.n_front < kFrontLds + a.max_tok ? sh.n_front : kFrontLds + a.max_tok;
+  *nlinks = (lat && ok) ? commit_links(a, sh, t, T, p, st, slot, base, nl_n, neps, cutoff) : 0;
   __syncthreads();
-  // swap: the frame just built becomes the previous frame
-  int* ohs = const_cast<int*>(t.ps);
-  unsigned short* ohp = const_cast<unsigned short*>(t.pp);
-  t.ps = t.hs;
-  t.pp = t.hp;
-  t.hs = ohs;
-  t.hp = ohp;
+  hbm_clear_listed(T, ng);
   lds_clear_build(t);
   __syncthreads();
-  if (st.cur_tab >= 0) set_tab_n(st, st.cur_tab, 0);
   if (ok) {
     st.cur_base = base;
     st.arena_used = base + n;
@@ -690,52 +724,15 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   } else {
     st.ntok = 0;
   }
-  st.cur_tab = ng > 0 ? y : -1;
-  if (ng > 0) set_tab_n(st, y, ng);
-  st.cur_nl = nl_n;
   *lds = live <= kTokLds;
   st.best_key = bk;  // GetCutoff's best token of the next frame
   *best_out = funord((uint32_t)(bk >> 32));
 }
 
-// End of a launch: the LDS-resident tokens of the current frame move into its
-// HBM table so that the next launch (whose LDS starts empty) finds them.
-__device__ __forceinline__ void flush_prev(const DecArgs& a, DecShared& sh, const FrameLds& t, DecPtrs& p,
-                           DecSlot& st) {
-  __syncthreads();
-  if (st.cur_nl == 0) return;
-  const int y = st.cur_tab >= 0 ? st.cur_tab : 0;
-  const HbmTab T = hbm_tab(a, p.slot, y);
-  if (threadIdx.x == 0) sh.n_new_g = st.cur_tab >= 0 ? tab_n(st, y) : 0;
-  __syncthreads();
-  const unsigned hm = (1u << a.hbits) - 1u;
-  for (int h = threadIdx.x; h < kHashCap; h += DT) {
-    const int s = t.ps[h];
-    if (s < 0) continue;
-    unsigned g = hbm_hash(s, a.hbits);
-    bool done = false;
-    for (int probe = 0; probe < a.hprobe && !done; probe++) {
-      if (atomicCAS(&T.state[g], -1, s) == -1) {
-        const int q = atomicAdd(&sh.n_new_g, 1);
-        if (q < a.max_tok) AG_ST(&T.list[q], (int)g);
-        else sh.bad |= 1;
-        AG_ST(&T.pos[g], (int)t.pp[h] - st.cur_nl);  // cur_nl + pos = the LDS position
-        done = true;
-      } else {
-        g = (g + 1) & hm;
-      }
-    }
-    if (!done) sh.bad |= 1;
-  }
-  __syncthreads();
-  st.cur_tab = y;
-  set_tab_n(st, y, sh.n_new_g < a.max_tok ? sh.n_new_g : a.max_tok);
-}
-
-// after a commit (all threads, past its barriers): the frame's lattice
-// record; every thread advances its copy of links_used identically
-__device__ __forceinline__ void lat_frame_done(const DecArgs& a, DecShared& sh, DecSlot& st, int slot, int index,
-                               float cutoff, float cost_offset, int nl) {
+// after a commit (all threads, past its barriers): the frame's record; every
+// thread advances its copy of links_used identically
+__device__ __forceinline__ void frame_done(const DecArgs& a, DecShared& sh, DecSlot& st, int slot, int index,
+                                           float cutoff, float cost_offset, int nl) {
   if (threadIdx.x == 0 && index < a.lat_frame_cap) {
     LatFrame F;
     F.tok_base = st.cur_base;
@@ -744,11 +741,228 @@ __device__ __forceinline__ void lat_frame_done(const DecArgs& a, DecShared& sh, 
     F.link_end = st.links_used + nl;
     F.cutoff = cutoff;
     F.cost_offset = cost_offset;
-    F.pad0 = F.pad1 = 0;
+    F.new_base = F.new_ntok = 0;
     a.lat_frames[(long long)slot * a.lat_frame_cap + index] = F;
   }
   if (index >= a.lat_frame_cap || sh.lat_ovf) st.lat_ovf = 1;
   st.links_used += nl;
+}
+
+// ---------------------------------------------------------------------------
+// PruneActiveTokens (Kaldi LatticeFasterDecoder, every prune_interval
+// frames): extra costs backwards from the frontier (whose tokens have extra
+// cost 0), links whose extra cost exceeds the beam dropped, tokens with no
+// surviving link dropped, and the stream's arena and link arena compacted
+// in place.  Extra costs only grow as the frontier advances, so a link
+// dropped here is one the final lattice-beam prune drops too: the pruned
+// lattice is unchanged.  Frames below prune_from keep their
+// last extra costs; the backward walk stops at the first such frame whose
+// costs did not change.  Without a lattice (no links) the same compaction
+// keeps the tokens on the backpointer chains of the frontier's tokens.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float tok_cost(const int4* AR, int t) { return __int_as_float(AG_LD(&AR[t].z)); }
+__device__ __forceinline__ void atomic_min_pos(float* p, float v) {  // v >= 0
+  atomicMin(reinterpret_cast<int*>(p), __float_as_int(v));
+}
+
+__device__ __forceinline__ void load_frame(const DecArgs& a, DecShared& sh, const LatFrame* LF, int k, int k1) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sh.fr = LF[k];
+    if (k1 >= 0) sh.fr1 = LF[k1];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, DecSlot& st, const DecPtrs& p, int slot) {
+  const int F = st.frames;
+  if (F <= 0 || F >= a.lat_frame_cap || st.err) return;
+  LatFrame* LF = a.lat_frames + (long long)slot * a.lat_frame_cap;
+  float* X = a.extra + (long long)slot * a.arena_cap;
+  int* R = a.remap + (long long)slot * a.arena_cap;
+  int4* AR = p.arena;
+  const bool lat = a.links != nullptr && !st.lat_ovf;
+  int4* LK = a.links ? a.links + (long long)slot * a.link_cap : nullptr;
+  const float beamp = a.lattice_beam + kPruneMargin;
+  const float kInf = __int_as_float(0x7f800000);
+  const int pf = st.prune_from;
+  load_frame(a, sh, LF, F, -1);
+  const int tbF = sh.fr.tok_base, endF = sh.fr.tok_base + sh.fr.ntok;
+  for (int t = tbF + threadIdx.x; t < endF; t += DT) AG_ST(&X[t], 0.0f);
+  int kmin = F;
+  for (int k = F - 1; k >= 0; k--) {
+    load_frame(a, sh, LF, k, k + 1);
+    const int tb = sh.fr.tok_base, te = sh.fr.tok_base + sh.fr.ntok;
+    for (int t = tb + threadIdx.x; t < te; t += DT) {
+      if (k < pf) AG_ST(&R[t], __float_as_int(AG_LD(&X[t])));  // old extra cost
+      AG_ST(&X[t], kInf);
+    }
+    __syncthreads();
+    if (lat) {
+      // emitting out-links of frame k (stored with frame k + 1: sources below its tokens)
+      const int tb1 = sh.fr1.tok_base;
+      for (long long i = sh.fr1.link_begin + threadIdx.x; i < sh.fr1.link_end; i += DT) {
+        const int4 r = LK[i];
+        if (r.x >= tb1) continue;
+        const float d = ((tok_cost(AR, r.x) + __int_as_float(r.w)) + __int_as_float(a.arcs[r.z].y)) -
+                        tok_cost(AR, r.y);
+        const float le = AG_LD(&X[r.y]) + d;
+        if (le <= beamp) atomic_min_pos(&X[r.x], fmaxf(le, 0.0f));
+      }
+      // epsilon links within frame k, to a fixpoint
+      while (true) {
+        __syncthreads();
+        if (threadIdx.x == 0) sh.flag = 0;
+        __syncthreads();
+        for (long long i = sh.fr.link_begin + threadIdx.x; i < sh.fr.link_end; i += DT) {
+          const int4 r = LK[i];
+          if (r.x < tb) continue;
+          const float d = (tok_cost(AR, r.x) + __int_as_float(a.arcs[r.z].y)) - tok_cost(AR, r.y);
+          const float le = fmaxf(AG_LD(&X[r.y]) + d, 0.0f);
+          if (le <= beamp && le < AG_LD(&X[r.x])) {
+            atomic_min_pos(&X[r.x], le);
+            sh.flag = 1;
+          }
+        }
+        __syncthreads();
+        if (!sh.flag) break;
+      }
+    } else {
+      // backpointer chains: frame k + 1's kept tokens keep their frame-k sources
+      for (int t = sh.fr1.tok_base + threadIdx.x; t < sh.fr1.tok_base + sh.fr1.ntok; t += DT) {
+        if (AG_LD(&X[t]) != 0.0f) continue;
+        const int pv = AG_LD(&AR[t].x);
+        if (pv >= tb && pv < te) AG_ST(&X[pv], 0.0f);
+      }
+      while (true) {  // epsilon backpointers inside frame k
+        __syncthreads();
+        if (threadIdx.x == 0) sh.flag = 0;
+        __syncthreads();
+        for (int t = tb + threadIdx.x; t < te; t += DT) {
+          if (AG_LD(&X[t]) != 0.0f) continue;
+          const int pv = AG_LD(&AR[t].x);
+          if (pv >= tb && pv < te && AG_LD(&X[pv]) != 0.0f) {
+            AG_ST(&X[pv], 0.0f);
+            sh.flag = 1;
+          }
+        }
+        __syncthreads();
+        if (!sh.flag) break;
+      }
+    }
+    kmin = k;
+    if (k < pf) {  // unchanged extra costs: the frames below are unchanged too
+      int ch = 0;
+      for (int t = tb + threadIdx.x; t < te; t += DT)
+        ch |= AG_LD(&X[t]) != __int_as_float(AG_LD(&R[t]));
+      __syncthreads();
+      if (threadIdx.x == 0) sh.flag = 0;
+      __syncthreads();
+      if (ch) sh.flag = 1;
+      __syncthreads();
+      if (!sh.flag) break;
+    }
+  }
+  // ---- token remap over the window [wb, arena_used): frame by frame
+  load_frame(a, sh, LF, kmin, -1);
+  const int wb = sh.fr.tok_base;
+  int out = wb;
+  for (int k = kmin; k <= F; k++) {
+    load_frame(a, sh, LF, k, -1);
+    const int tb = sh.fr.tok_base, te = sh.fr.tok_base + sh.fr.ntok;
+    const int nb = out;
+    for (int c0 = tb; c0 < te; c0 += DT) {
+      const int t = c0 + threadIdx.x;
+      int keep = 0;
+      if (t < te) keep = (k == F) || AG_LD(&X[t]) <= beamp;
+      block_scan(sh, keep);
+      if (t < te) AG_ST(&R[t - wb], keep ? out + sh.scan[threadIdx.x] : -1);
+      out += sh.total;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      LF[k].new_base = nb;
+      LF[k].new_ntok = out - nb;
+    }
+  }
+  const int new_end = out;
+  // ---- links (before the tokens move: extra costs and costs by old index)
+  long long lout = 0;
+  if (a.links) {
+    load_frame(a, sh, LF, kmin, -1);
+    lout = sh.fr.link_begin;
+    for (int k = kmin; k <= F; k++) {
+      load_frame(a, sh, LF, k, -1);
+      const long long nb = lout;
+      for (long long c0 = sh.fr.link_begin; c0 < sh.fr.link_end; c0 += DT) {
+        const long long i = c0 + threadIdx.x;
+        int keep = 0;
+        int4 r = make_int4(0, 0, 0, 0);
+        if (i < sh.fr.link_end) {
+          r = LK[i];
+          const int rs = r.x >= wb ? AG_LD(&R[r.x - wb]) : r.x;
+          const int rd = r.y >= wb ? AG_LD(&R[r.y - wb]) : r.y;
+          if (rs >= 0 && rd >= 0) {
+            if (!lat || (k == F && r.x >= tbF)) {
+              keep = 1;  // the frontier's epsilon links (or no pruning state)
+            } else {
+              const bool eps = r.x >= sh.fr.tok_base;
+              const float w = __int_as_float(a.arcs[r.z].y);
+              const float d = eps ? (tok_cost(AR, r.x) + w) - tok_cost(AR, r.y)
+                                  : ((tok_cost(AR, r.x) + __int_as_float(r.w)) + w) - tok_cost(AR, r.y);
+              keep = AG_LD(&X[r.y]) + d <= beamp;
+            }
+            r.x = rs;
+            r.y = rd;
+          }
+        }
+        block_scan(sh, keep);  // every thread has read its record: writes may follow
+        if (keep) LK[lout + sh.scan[threadIdx.x]] = r;
+        lout += sh.total;
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) {
+        LF[k].link_begin = nb;
+        LF[k].link_end = lout;
+      }
+    }
+  }
+  // ---- move the kept tokens (and their extra costs) down, in order
+  for (int c0 = wb; c0 < st.arena_used; c0 += DT) {
+    const int t = c0 + threadIdx.x;
+    int nt = -1;
+    int4 rec = make_int4(0, 0, 0, 0);
+    float x = 0.0f;
+    if (t < st.arena_used) {
+      nt = AG_LD(&R[t - wb]);
+      if (nt >= 0) {
+        rec = ag_ld4(&AR[t]);
+        x = AG_LD(&X[t]);
+        if (rec.x >= wb) {
+          const int np = AG_LD(&R[rec.x - wb]);
+          if (np < 0) sh.bad |= 16;
+          rec.x = np;
+        }
+      }
+    }
+    __syncthreads();
+    if (nt >= 0) {
+      ag_st4(&AR[nt], rec);
+      AG_ST(&X[nt], x);
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  for (int k = kmin + threadIdx.x; k <= F; k += DT) {
+    LF[k].tok_base = LF[k].new_base;
+    LF[k].ntok = LF[k].new_ntok;
+  }
+  __syncthreads();
+  st.cur_base = new_end - (endF - tbF);
+  st.arena_used = new_end;
+  if (a.links) st.links_used = lout;
+  st.prune_from = F;
+  st.last_prune = F;
 }
 
 template <bool PROF>
@@ -757,24 +971,23 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   __shared__ float L[kLlhLds];
   __shared__ int TS[kTokLds];
   __shared__ float TC[kTokLds];
-  __shared__ int t_hs[2][kHashCap];
-  __shared__ unsigned short t_hp[2][kHashCap];
+  __shared__ int t_hs[kHashCap];
   __shared__ unsigned long long t_hk[kHashCap];
+  __shared__ int t_hb[kHashCap];
+  __shared__ unsigned short t_hp[kHashCap];
   __shared__ int t_hst[kHashCap];
   __shared__ unsigned short t_nl[kHashCap];
   __shared__ int t_fr[2][kFrontLds];
   FrameLds t;
-  t.hs = t_hs[0];
-  t.hp = t_hp[0];
-  t.ps = t_hs[1];
-  t.pp = t_hp[1];
+  t.hs = t_hs;
   t.hk = t_hk;
+  t.hb = t_hb;
+  t.hp = t_hp;
   t.hst = t_hst;
   t.nl = t_nl;
   t.fr0 = t_fr[0];
   t.fr1 = t_fr[1];
   lds_clear_build(t);
-  for (int h = threadIdx.x; h < kHashCap; h += DT) t_hs[1][h] = -1;
   const DecJob job = a.jobs[blockIdx.x];
   const int slot = job.slot;
   DecSlot st = a.slots[slot];
@@ -786,6 +999,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   p.fg0 = a.front_g + ((long long)slot * 2) * a.max_tok;
   p.fg1 = p.fg0 + a.max_tok;
   p.slot = slot;
+  const HbmTab T = hbm_tab(a, slot);
   if (threadIdx.x == 0) {
     sh.bad = 0;
     sh.n_links = 0;
@@ -806,12 +1020,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
 
   if (job.reset) {  // InitDecoding: start token, closure with cutoff = beam
     __syncthreads();
-    if (st.err) {  // an overflow may have left unlisted entries: clear everything
-      hbm_clear_all(a, hbm_tab(a, slot, 0));
-      hbm_clear_all(a, hbm_tab(a, slot, 1));
-    } else if (st.cur_tab >= 0) {
-      hbm_clear_listed(hbm_tab(a, slot, st.cur_tab), tab_n(st, st.cur_tab));
-    }
+    if (st.err) hbm_clear_all(a, T);  // an overflow may have left unlisted entries
     st.ntok = 0;
     st.cur_base = 0;
     st.arena_used = 0;
@@ -820,10 +1029,8 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     st.err = 0;
     st.links_used = 0;
     st.lat_ovf = 0;
-    st.cur_tab = -1;
-    st.tab_n0 = st.tab_n1 = 0;
-    st.cur_nl = 0;
-    st.seg_base = 0;
+    st.prune_from = 0;
+    st.last_prune = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
       sh.n_new_l = 0;
@@ -833,15 +1040,16 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      const Relax r = relax(a, sh, t, hbm_tab(a, slot, 0), a.start_state, 0.0f, -1);
+      const Relax r = relax(a, sh, t, T, a.start_state, 0.0f, -1,
+                            ((unsigned)a.sinfo[a.start_state].z - (unsigned)a.sinfo[a.start_state].y) != 0);
       t.fr0[0] = r.slot;
       sh.n_front = 1;
     }
-    eps_closure(a, sh, t, hbm_tab(a, slot, 0), p, st, a.beam, 1, &arcs_eps);
+    eps_closure(a, sh, t, T, p, st, a.beam, 1, &arcs_eps);
     float b;
     int nl = 0;
-    commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, 0, &nl);
-    if (a.links) lat_frame_done(a, sh, st, slot, 0, a.beam, 0.0f, nl);
+    commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, &nl);
+    frame_done(a, sh, st, slot, 0, a.beam, 0.0f, nl);
   } else if (st.ntok > 0 && st.ntok <= kTokLds) {
     for (int i = threadIdx.x; i < st.ntok; i += DT) {
       TS[i] = AG_LD(&p.cs[i]);
@@ -947,8 +1155,6 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     // and are dropped at commit -- exactly the tokens a relax-below-
     // next_cutoff pass creates, with the same keys.  Without a finite seed
     // the exact two-pass form runs.
-    const int y = st.cur_tab == 0 ? 1 : 0;  // HBM table of the frame under construction
-    const HbmTab T = hbm_tab(a, slot, y);
     if (seed != __int_as_float(0x7f800000)) {
       const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
                                       &examined, st, slot);
@@ -965,8 +1171,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     }
     __syncthreads();
     DEC_PHASE(2);
-    if (prof) pacc[3] += sh.n_new_l + sh.n_new_g;  // tokens created by the emitting pass
-    if (prof) pacc[6] += sh.n_new_g;               // of them in the HBM table
+    if (prof) pacc[3] += sh.n_new_g;  // tokens the emitting pass created in the HBM table
     eps_closure(a, sh, t, T, p, st, next_cutoff, sh.n_front, &arcs_eps);
     __syncthreads();
     DEC_PHASE(4);
@@ -978,10 +1183,10 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       }
     }
     int nl = 0;
-    commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, y, &nl);
+    commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, &nl);
     DEC_PHASE(5);
     if (prof) pacc[7]++;
-    if (a.links) lat_frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset, nl);
+    frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset, nl);
     st.offset_sum += (double)cost_offset;
     st.frames++;
     if (threadIdx.x == 0 && a.stats) {
@@ -1003,9 +1208,13 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   __syncthreads();
   if (sh.bad) st.err |= sh.bad;
   if (st.ntok == 0 && !st.err) st.err |= 4;
-  if (!st.err) flush_prev(a, sh, t, p, st);
-  __syncthreads();
-  if (sh.bad) st.err |= sh.bad;
+  // PruneActiveTokens every prune_interval frames (at the end of a launch)
+  if (a.prune_interval > 0 && !st.err && st.frames - st.last_prune >= a.prune_interval) {
+    prune_segment(a, sh, st, p, slot);
+    __syncthreads();
+    if (sh.bad) st.err |= sh.bad;
+  }
+  DEC_PHASE(6);
   if (threadIdx.x == 0) a.slots[slot] = st;
   if (prof)
     for (int i = 0; i < 8; i++) a.prof[slot * 8 + i] += pacc[i];

@@ -640,7 +640,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   dec_.min_active = m.dec.min_active;
   dec_.P = plan_.out_dim;
   dec_.llh = d_llh_;
-  // bounded per-stream decoder state (decoder.hip): two HBM frame tables of
+  // bounded per-stream decoder state (decoder.hip): one HBM frame table of
   // H >= 2 * max_tokens slots for the states a frame's LDS table cannot hold
   const long long MT = cfg_.max_tokens;
   int hbits = 10;
@@ -648,30 +648,40 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   const long long H = 1ll << hbits;
   dec_.hbits = hbits;
   dec_.hprobe = 256;
-  dec_.ht_state = (int*)DevAlloc(sizeof(int) * 2 * S * H);
-  dec_.ht_key = (unsigned long long*)DevAlloc(sizeof(unsigned long long) * 2 * S * H);
-  dec_.ht_pos = (int*)DevAlloc(sizeof(int) * 2 * S * H);
-  dec_.ht_stamp = (int*)DevAlloc(sizeof(int) * 2 * S * H);
-  dec_.ht_list = (int*)DevAlloc(sizeof(int) * 2 * S * MT);
+  dec_.ht_state = (int*)DevAlloc(sizeof(int) * S * H);
+  dec_.ht_key = (unsigned long long*)DevAlloc(sizeof(unsigned long long) * S * H);
+  dec_.ht_pos = (int*)DevAlloc(sizeof(int) * S * H);
+  dec_.ht_stamp = (int*)DevAlloc(sizeof(int) * S * H);
+  dec_.ht_bp = (int*)DevAlloc(sizeof(int) * S * H);
+  dec_.ht_list = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.front_g = (int*)DevAlloc(sizeof(int) * 2 * S * MT);
   dec_.cur_state = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.cur_cost = (float*)DevAlloc(sizeof(float) * S * MT);
   dec_.cur_pos = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.arena = (int4*)DevAlloc(sizeof(int4) * S * cfg_.arena_tokens);
+  // PruneActiveTokens state: extra cost per arena token + compaction scratch
+  dec_.extra = (float*)DevAlloc(sizeof(float) * S * cfg_.arena_tokens);
+  dec_.remap = (int*)DevAlloc(sizeof(int) * S * cfg_.arena_tokens);
   dec_.max_tok = (int)MT;
   // LDS probe limit of the frame table (decoder.hip); tests force the HBM
   // tables with VOSK_AMD_DEC_LDS_PROBE (0 = every state in HBM)
   dec_.lds_probe = DecoderLdsProbe();
   if (const char* lp = getenv("VOSK_AMD_DEC_LDS_PROBE")) dec_.lds_probe = atoi(lp);
   dec_.lattice_beam = m.dec.lattice_beam;
+  // Kaldi prunes every prune_interval (25) frames; VOSK_AMD_DEC_PRUNE=0 turns
+  // pruning off (tests that compare the raw per-frame lattice with the oracle)
+  dec_.prune_interval = m.dec.prune_interval;
+  if (const char* pe = getenv("VOSK_AMD_DEC_PRUNE")) dec_.prune_interval = atoi(pe) ? m.dec.prune_interval : 0;
   dec_.arena_cap = cfg_.arena_tokens;
   dec_.links = nullptr;
-  dec_.lat_frames = nullptr;
+  dec_.link_dst = nullptr;
   dec_.link_cap = cfg_.lattice_links;
   dec_.lat_frame_cap = cfg_.lattice_frames;
+  // frame records are kept with or without a lattice (pruning walks them)
+  dec_.lat_frames = (LatFrame*)DevAlloc(sizeof(LatFrame) * (size_t)S * cfg_.lattice_frames);
   if (cfg_.lattice) {
     dec_.links = (int4*)DevAlloc(sizeof(int4) * (size_t)S * cfg_.lattice_links);
-    dec_.lat_frames = (LatFrame*)DevAlloc(sizeof(LatFrame) * (size_t)S * cfg_.lattice_frames);
+    dec_.link_dst = (int*)DevAlloc(sizeof(int) * (size_t)S * cfg_.lattice_links);
   }
   d_slots_ = (DecSlot*)DevAlloc(sizeof(DecSlot) * S);
   HIPCHECK(hipMemset(d_slots_, 0, sizeof(DecSlot) * S));
@@ -683,7 +693,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     dec_.prof = (long long*)DevAlloc(sizeof(long long) * 8 * S);
     HIPCHECK(hipMemset(dec_.prof, 0, sizeof(long long) * 8 * S));
   }
-  LaunchInitTables(dec_.ht_state, dec_.ht_key, dec_.ht_stamp, 2 * S * H, stream_);
+  LaunchInitTables(dec_.ht_state, dec_.ht_key, dec_.ht_stamp, S * H, stream_);
 
   // ---- staging
   stage_bytes_ = Align256(sizeof(float) * (size_t)S * cfg_.max_step_samples) +
@@ -853,6 +863,22 @@ int Engine::PendingSamples(int slot) const {
   return (int)(h.pending.size() - h.pending_pos);
 }
 int Engine::DecoderError(int slot) const { return slots_.at(slot).err; }
+
+void Engine::DecoderState(int slot, long long* o8) {
+  std::lock_guard<std::mutex> lk(mu_);
+  FlushLocked();
+  slots_.at(slot);
+  DecSlot st;
+  HIPCHECK(hipMemcpy(&st, d_slots_ + slot, sizeof(DecSlot), hipMemcpyDeviceToHost));
+  o8[0] = st.ntok;
+  o8[1] = st.arena_used;
+  o8[2] = st.frames;
+  o8[3] = st.links_used;
+  o8[4] = st.err;
+  o8[5] = st.lat_ovf;
+  o8[6] = st.prune_from;
+  o8[7] = st.last_prune;
+}
 const std::vector<FrameStat>& Engine::LastStats(int slot) const { return slots_.at(slot).stats; }
 
 bool Engine::BuildStep(const std::vector<int>& slots) {
@@ -1539,7 +1565,7 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
   }
 }
 
-void Engine::DecoderPhaseClocks(long long* out8) {
+void Engine::DecoderPhaseClocks(long long* out8, long long* per_slot) {
   std::lock_guard<std::mutex> lk(mu_);
   FlushLocked();
   for (int i = 0; i < 8; i++) out8[i] = 0;
@@ -1548,6 +1574,7 @@ void Engine::DecoderPhaseClocks(long long* out8) {
   HIPCHECK(hipMemcpy(h.data(), dec_.prof, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
   for (size_t s = 0; s < slots_.size(); s++)
     for (int i = 0; i < 8; i++) out8[i] += h[s * 8 + i];
+  if (per_slot) std::copy(h.begin(), h.end(), per_slot);
 }
 
 void Engine::DebugFeatures(int slot, int first, int n, std::vector<float>* out) {

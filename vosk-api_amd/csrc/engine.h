@@ -159,6 +159,9 @@ class Engine {
   bool InputIsFinished(int slot) const;
   int PendingSamples(int slot) const;
   int DecoderError(int slot) const;
+  // device decoder state of a stream: {tokens, arena tokens used, frames,
+  // lattice links used, err, lattice overflow, prune_from, last prune frame}
+  void DecoderState(int slot, long long* out8);
   // Best path of the current utterance (batched over slots).
   void BestPaths(const std::vector<int>& slots, bool use_final, std::vector<PathResult>* out);
   // Optional per-frame decoder statistics of the last Advance (collect_stats).
@@ -188,8 +191,9 @@ class Engine {
   // waits for more frames until input is finished)
   int IvectorFramesReady(int slot) const;
   // VOSK_AMD_DEC_PROFILE=1: summed s_memtime clocks per decoder phase
-  // [cutoff, seed, expand, compact, eps, commit, -, frames]
-  void DecoderPhaseClocks(long long* out8);
+  // [cutoff, seed, expand, tokens created in the HBM table, eps, commit,
+  // prune, frames]; per_slot (optional): the same per slot [max_slots][8]
+  void DecoderPhaseClocks(long long* out8, long long* per_slot = nullptr);
 
  private:
   struct SlotHost {

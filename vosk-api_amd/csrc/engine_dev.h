@@ -117,18 +117,15 @@ struct DecSlot {
   int cur_base;     // arena index of the current frame's first token
   int arena_used;
   int frames;       // frames decoded since the last reset
-  int cur_tab;      // HBM frame table holding the current frame's HBM-resident tokens (-1 none)
-  int stamp;        // epsilon-closure round stamp (monotonic)
+  int stamp;        // epsilon-closure round stamp (monotonic; HBM table stamps)
   int err;          // bit 0: token list / table overflow, bit 1: arena overflow, bit 2: no tokens,
-                    // bit 3: unplaceable backpointer source
+                    // bit 3: unplaceable backpointer source, bit 4: pruning lost a backpointer
   int lat_ovf;      // lattice: 1 = link arena or frame table overflowed (results fall back to 1-best)
+  int prune_from;   // first LatFrame whose extra costs were never computed (PruneActiveTokens)
   double offset_sum;
   unsigned long long best_key;  // min over current tokens of (ordered cost << 32 | state)
   long long links_used;         // lattice links in the stream's link arena
-  int tab_n0, tab_n1;  // entries listed per HBM table (cleared by list)
-  int cur_nl;       // LDS-resident tokens of the current frame (their list positions come first)
-  int seg_base;     // lattice: LatFrame index of the segment's first kept frame (pruning)
-  int prune_from;   // lattice: first frame the next pruning pass revisits
+  int last_prune;   // frames decoded at the last pruning pass
   int pad0;
 };
 
@@ -145,7 +142,7 @@ struct LatFrame {   // per decoded frame (index 0 = InitDecoding's closure)
   long long link_begin, link_end;
   float cutoff;            // tokens and links of this frame are below it
   float cost_offset;       // cost offset of the emitting links INTO this frame
-  int pad0, pad1;
+  int new_base, new_ntok;  // pruning scratch (compacted token range)
 };
 
 // ---- online i-vector extraction (kernels.hip ivector_kernel)
@@ -246,13 +243,14 @@ struct DecArgs {
   int P;
   const float* llh;
   const DecJob* jobs;
-  // per stream, two HBM frame tables of H = 1 << hbits slots (decoder.hip):
+  // per stream, one HBM frame table of H = 1 << hbits slots (decoder.hip):
   // states that do not fit the LDS table of the frame under construction
-  int* ht_state;            // [slots][2][H]
-  unsigned long long* ht_key;  // [slots][2][H]
-  int* ht_pos;              // [slots][2][H]
-  int* ht_stamp;            // [slots][2][H]
-  int* ht_list;             // [slots][2][max_tok]
+  int* ht_state;            // [slots][H]
+  unsigned long long* ht_key;  // [slots][H]
+  int* ht_pos;              // [slots][H] creation index | has-epsilon-arcs << 30
+  int* ht_stamp;            // [slots][H]
+  int* ht_bp;               // [slots][H] backpointer (decoder.hip kBpEps encoding)
+  int* ht_list;             // [slots][max_tok]
   int hbits, hprobe;
   int* front_g;             // [slots][2][max_tok] epsilon frontier spill
   int* cur_state;           // [slots][max_tok]
@@ -265,10 +263,14 @@ struct DecArgs {
   int lds_probe;          // LDS probe limit (states past it live in HBM); tests: 0 = all HBM
   long long arena_cap;
   int4* links;            // [slots][link_cap] lattice links (nullptr: no lattice)
-  LatFrame* lat_frames;   // [slots][lat_frame_cap]
+  int* link_dst;          // [slots][link_cap] destination frame-table slot of a raw link
+  LatFrame* lat_frames;   // [slots][lat_frame_cap] (always kept: pruning walks the frames)
   long long link_cap;
   int lat_frame_cap;
   float lattice_beam;     // pruning (PruneActiveTokens)
+  int prune_interval;     // frames between pruning passes (0 = never)
+  float* extra;           // [slots][arena_cap] Kaldi extra_cost per token (pruning)
+  int* remap;             // [slots][arena_cap] pruning scratch (old -> new arena index)
 };
 
 struct TraceArgs {

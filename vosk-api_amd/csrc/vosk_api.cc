@@ -559,6 +559,13 @@ int vamd_stream_error(VamdEngine* e, int s) {
   API_CATCH(-1)
 }
 
+int vamd_stream_decoder_state(VamdEngine* e, int s, long long* out8) {
+  API_TRY
+  e->eng->DecoderState(s, out8);
+  return 0;
+  API_CATCH(-1)
+}
+
 int vamd_stream_features(VamdEngine* e, int s, int first, int n, float* out) {
   API_TRY
   std::vector<float> v;
@@ -705,6 +712,14 @@ int vamd_engine_decoder_totals(VamdEngine* e, long long* o6) {
 int vamd_engine_decoder_phases(VamdEngine* e, long long* o8) {
   API_TRY
   e->eng->DecoderPhaseClocks(o8);
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_engine_decoder_phases_per_stream(VamdEngine* e, long long* o) {
+  API_TRY
+  long long tot[8];
+  e->eng->DecoderPhaseClocks(tot, o);
   return 0;
   API_CATCH(-1)
 }

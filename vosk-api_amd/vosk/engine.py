@@ -30,6 +30,7 @@ _SIGS = {
     "vamd_engine_advance": (C.c_int, [_vp, _vp, C.c_int]),
     "vamd_stream_frames_decoded": (C.c_int, [_vp, C.c_int]),
     "vamd_stream_error": (C.c_int, [_vp, C.c_int]),
+    "vamd_stream_decoder_state": (C.c_int, [_vp, C.c_int, _vp]),
     "vamd_stream_features": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, _vp]),
     "vamd_stream_llh": (C.c_longlong, [_vp, C.c_int, _vp, C.c_longlong]),
     "vamd_stream_ivectors": (C.c_longlong, [_vp, C.c_int, _vp, C.c_longlong]),
@@ -51,6 +52,7 @@ _SIGS = {
     "vamd_engine_flush": (C.c_int, [_vp]),
     "vamd_engine_decoder_totals": (C.c_int, [_vp, _vp]),
     "vamd_engine_decoder_phases": (C.c_int, [_vp, _vp]),
+    "vamd_engine_decoder_phases_per_stream": (C.c_int, [_vp, _vp]),
     "vamd_engine_set_step_samples": (C.c_int, [_vp, C.c_int]),
     "vamd_engine_stage_times": (C.c_int, [_vp, _vp, _vp, C.c_int]),
     "vamd_lattice_set_rescore": (C.c_int, [C.c_char_p, C.c_char_p]),
@@ -156,6 +158,7 @@ class Engine:
         if not h:
             raise RuntimeError("vamd_engine_new failed: " + _err())
         self.h = h
+        self.max_streams = max_streams
         info = np.zeros(8, np.int32)
         fl = C.c_double(0)
         _chk(_c.vamd_engine_info(h, info.ctypes.data, C.addressof(fl)))
@@ -202,6 +205,12 @@ class Engine:
 
     def error(self, s):
         return _chk(_c.vamd_stream_error(self.h, s))
+
+    def decoder_state(self, s):
+        out = np.zeros(8, np.int64)
+        _chk(_c.vamd_stream_decoder_state(self.h, s, out.ctypes.data))
+        return dict(zip(("ntok", "arena_used", "frames", "links_used", "err", "lat_ovf",
+                         "prune_from", "last_prune"), out.tolist()))
 
     def features(self, s, first, n, dim):
         out = np.zeros((n, dim), np.float32)
@@ -295,11 +304,18 @@ class Engine:
     def decoder_phases(self):
         out = np.zeros(8, np.int64)
         _chk(_c.vamd_engine_decoder_phases(self.h, out.ctypes.data))
-        # clocks per phase; slot 3 sums the tokens the emitting pass created,
-        # slot 6 counts frames rebuilt on the global maps after an LDS overflow
-        names = ("cutoff", "seed", "expand", "created", "eps", "commit", "lds_fallback_frames",
-                 "frames")
-        return dict(zip(names, out.tolist()))
+        # clocks per phase; slot 3 sums the tokens the emitting pass created
+        # in the HBM table (past the LDS table's probe limit), slot 6 the
+        # clocks of the pruning passes
+        return dict(zip(self.PHASES, out.tolist()))
+
+    PHASES = ("cutoff", "seed", "expand", "hbm_created", "eps", "commit", "prune", "frames")
+
+    def decoder_phases_per_stream(self):
+        """[max_streams, 8] int64: decoder_phases() per stream slot."""
+        out = np.zeros((self.max_streams, 8), np.int64)
+        _chk(_c.vamd_engine_decoder_phases_per_stream(self.h, out.ctypes.data))
+        return out
 
     def counters(self):
         out = np.zeros(5, np.int64)
