@@ -265,9 +265,16 @@ def main():
             "single_stream": single,
         }
         if os.environ.get("VOSK_AMD_DEC_PROFILE"):
+            ph = e.decoder_phases()
             out["decoder_phase_clocks_per_frame"] = {
-                k: round(v / max(e.decoder_phases()["frames"], 1), 1)
-                for k, v in e.decoder_phases().items() if k != "frames"}
+                k: round(v / max(ph["frames"], 1), 1) for k, v in ph.items() if k != "frames"}
+            # per-stream spread: the slowest stream sets each launch's time
+            per = e.decoder_phases_per_stream()[:S]
+            clk = per[:, [0, 1, 2, 4, 5, 6]].sum(1).astype(np.float64)
+            out["decoder_stream_clocks"] = {
+                "mean": round(float(clk.mean()), 1), "p50": round(float(np.percentile(clk, 50)), 1),
+                "p90": round(float(np.percentile(clk, 90)), 1), "max": round(float(clk.max()), 1),
+                "max_over_mean": round(float(clk.max() / max(clk.mean(), 1.0)), 3)}
         print(json.dumps(out), flush=True)
     e.close()
     if dist is not None:

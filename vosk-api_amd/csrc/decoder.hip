@@ -69,7 +69,9 @@ struct DecShared {
   int n_new_l, n_new_g, n_next, n_front, n_fnext, total, sel_k, n_links, lat_ovf, n_eps;
   unsigned sel_prefix, sel_mask;
   float seed;
-  int bad, flag;
+  int bad, flag, kk;
+  int fl[3];                  // FixRound flags
+  unsigned char kbits[DT];    // pruning: per-thread keep bits of the chunk
   LatFrame fr;        // pruning: the frame record being processed (broadcast)
   LatFrame fr1;
 };
@@ -339,12 +341,14 @@ __device__ __forceinline__ int bp_slot(int bp) {
   return (c & kBpHbm) ? ~(c & (kBpHbm - 1)) : c;
 }
 
-// list position of state s in the frame under construction (eps links at commit)
-__device__ __forceinline__ int frame_pos(const DecArgs& a, const FrameLds& t, const HbmTab& T, int nl_n, int s) {
+// slot of state s in the frame under construction (eps links at commit);
+// kNoSlot if absent
+constexpr int kNoSlot = 0x7fffffff;
+__device__ __forceinline__ int frame_slot(const DecArgs& a, const FrameLds& t, const HbmTab& T, int s) {
   unsigned h = lds_hash(s);
   for (int probe = 0; probe < a.lds_probe; probe++) {
     const int c = t.hs[h];
-    if (c == s) return t.hp[h] & 0x7fff;
+    if (c == s) return (int)h;
     if (c == -1) break;
     h = (h + 1) & (kHashCap - 1);
   }
@@ -352,11 +356,11 @@ __device__ __forceinline__ int frame_pos(const DecArgs& a, const FrameLds& t, co
   unsigned g = hbm_hash(s, a.hbits);
   for (int probe = 0; probe < a.hprobe; probe++) {
     const int c = AG_LD(&T.state[g]);
-    if (c == s) return nl_n + (AG_LD(&T.pos[g]) & (kHPosEps - 1));
+    if (c == s) return ~(int)g;
     if (c == -1) break;
     g = (g + 1) & hm;
   }
-  return -1;
+  return kNoSlot;
 }
 
 __device__ __forceinline__ void push_front(const DecArgs& a, DecShared& sh, const FrameLds& t,
@@ -576,12 +580,15 @@ __device__ __forceinline__ void hbm_clear_all(const DecArgs& a, const HbmTab& T)
 // indices through their destination slots (chunked in-place compaction:
 // writes never pass the chunk being read), then the epsilon links of the
 // committed tokens that have epsilon arcs (listed by the commit in the
-// frontier arrays, neps of them).  Returns the frame's link count.
+// frontier arrays, neps of them).  Every kept link's cost above its
+// destination's, tot - cost(dst) >= 0 (the link's extra cost over the
+// destination for PruneActiveTokens), replaces its destination slot in
+// link_dst.  Returns the frame's link count.
 __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
                             const DecPtrs& p, const DecSlot& st, int slot, int base, int nl_n,
                             int neps, float cutoff) {
   int4* L = a.links + (long long)slot * a.link_cap;
-  const int* LD = a.link_dst + (long long)slot * a.link_cap;
+  int* LD = a.link_dst + (long long)slot * a.link_cap;
   const long long lb = st.links_used;
   long long nrec = sh.n_links;
   if (lb + nrec > a.link_cap) nrec = a.link_cap - lb > 0 ? a.link_cap - lb : 0;
@@ -590,15 +597,22 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
     const long long i = c0 + threadIdx.x;
     int keep = 0;
     int4 r = make_int4(0, 0, 0, 0);
+    float d = 0.0f;
     if (i < nrec) {
       r = L[lb + i];
-      if (__int_as_float(r.y) < cutoff) {
-        r.y = base + slot_pos(t, T, nl_n, LD[lb + i]);
+      const float tot = __int_as_float(r.y);
+      if (tot < cutoff) {
+        const int v = LD[lb + i];
+        r.y = base + slot_pos(t, T, nl_n, v);
+        d = tot - funord((uint32_t)(slot_key(t, T, v) >> 32));
         keep = 1;
       }
     }
     block_scan(sh, keep);
-    if (keep) L[lb + out + sh.scan[threadIdx.x]] = r;
+    if (keep) {
+      L[lb + out + sh.scan[threadIdx.x]] = r;
+      LD[lb + out + sh.scan[threadIdx.x]] = __float_as_int(d);
+    }
     out += sh.total;
     __syncthreads();
   }
@@ -629,7 +643,7 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
       const int4 A = a.arcs[arc];
       const float tot = sh.tcost[j] + __int_as_float(A.y);
       if (tot < cutoff) {
-        const int d = frame_pos(a, t, T, nl_n, A.x);
+        const int v = frame_slot(a, t, T, A.x);
         const unsigned long long m = __ballot(1);
         const int lane = threadIdx.x & 63;
         const int leader = __ffsll((long long)m) - 1;
@@ -637,8 +651,12 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
         if (lane == leader) w0 = atomicAdd(&sh.n_eps, __popcll(m));
         w0 = __shfl(w0, leader, 64);
         const long long pos = lb + out + w0 + __popcll(m & ((1ull << lane) - 1ull));
-        if (pos < a.link_cap && d >= 0) L[pos] = make_int4(sh.tsrc[j], base + d, arc, 0);
-        else sh.lat_ovf = 1;
+        if (pos < a.link_cap && v != kNoSlot) {
+          L[pos] = make_int4(sh.tsrc[j], base + slot_pos(t, T, nl_n, v), arc, 0);
+          LD[pos] = __float_as_int(tot - funord((uint32_t)(slot_key(t, T, v) >> 32)));
+        } else {
+          sh.lat_ovf = 1;
+        }
       }
     }
     __syncthreads();
@@ -759,17 +777,58 @@ __device__ __forceinline__ void frame_done(const DecArgs& a, DecShared& sh, DecS
 // last extra costs; the backward walk stops at the first such frame whose
 // costs did not change.  Without a lattice (no links) the same compaction
 // keeps the tokens on the backpointer chains of the frontier's tokens.
+//
+// A link's extra cost is X[dst] + d with d = tot - cost(dst) >= 0 stored at
+// commit (link_dst), so the backward pass reads only the destination's
+// extra cost.  The compaction passes run over the whole window at once,
+// four items per thread.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float tok_cost(const int4* AR, int t) { return __int_as_float(AG_LD(&AR[t].z)); }
+constexpr int kDropped = (int)0x80000000u;  // remap entry flag: token dropped (low bits: kept before it)
+constexpr int kPI = 4;                      // items per thread in the compaction passes
+
 __device__ __forceinline__ void atomic_min_pos(float* p, float v) {  // v >= 0
   atomicMin(reinterpret_cast<int*>(p), __float_as_int(v));
 }
 
-__device__ __forceinline__ void load_frame(const DecArgs& a, DecShared& sh, const LatFrame* LF, int k, int k1) {
+__device__ __forceinline__ void load_frame(DecShared& sh, const LatFrame* LF, int k, int k1) {
   __syncthreads();
   if (threadIdx.x == 0) {
     sh.fr = LF[k];
     if (k1 >= 0) sh.fr1 = LF[k1];
+  }
+  __syncthreads();
+}
+
+// block-wide "did any thread set its flag" loop helper: three rotating LDS
+// flags, one barrier per round
+struct FixRound {
+  int it = 0;
+  __device__ __forceinline__ void begin(DecShared& sh) {
+    if (threadIdx.x == 0) sh.fl[(it + 1) % 3] = 0;
+  }
+  __device__ __forceinline__ void mark(DecShared& sh) { sh.fl[it % 3] = 1; }
+  __device__ __forceinline__ bool end(DecShared& sh) {  // true: another round
+    __syncthreads();
+    const bool again = sh.fl[it % 3] != 0;
+    it++;
+    return again;
+  }
+};
+
+// development: structural invariants of frames kmin..F (links of frame k:
+// destination in frame k, source in frame k-1 or k); tag = call site
+__device__ void prune_check(const DecArgs& a, const LatFrame* LF, const int4* LK, int kmin, int F, int slot,
+                            int tag, bool use_new) {
+  for (int k = kmin; k <= F; k++) {
+    const int tb = use_new ? LF[k].new_base : LF[k].tok_base;
+    const int te = tb + (use_new ? LF[k].new_ntok : LF[k].ntok);
+    const int tp = k > 0 ? (use_new && k > kmin ? LF[k - 1].new_base : LF[k - 1].tok_base) : tb;
+    for (long long i = LF[k].link_begin + threadIdx.x; i < LF[k].link_end; i += DT) {
+      const int4 r = LK[i];
+      if (r.y < tb || r.y >= te || r.x < tp || r.x >= te)
+        printf("prune_check tag %d slot %d frame %d kmin %d F %d link %lld src %d dst %d frame [%d,%d) prev %d\n",
+               tag, slot, k, kmin, F, i, r.x, r.y, tb, te, tp);
+    }
   }
   __syncthreads();
 }
@@ -783,50 +842,47 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
   int4* AR = p.arena;
   const bool lat = a.links != nullptr && !st.lat_ovf;
   int4* LK = a.links ? a.links + (long long)slot * a.link_cap : nullptr;
+  int* LDd = a.links ? a.link_dst + (long long)slot * a.link_cap : nullptr;  // d bits of committed links
   const float beamp = a.lattice_beam + kPruneMargin;
   const float kInf = __int_as_float(0x7f800000);
   const int pf = st.prune_from;
-  load_frame(a, sh, LF, F, -1);
+  load_frame(sh, LF, F, -1);
   const int tbF = sh.fr.tok_base, endF = sh.fr.tok_base + sh.fr.ntok;
   for (int t = tbF + threadIdx.x; t < endF; t += DT) AG_ST(&X[t], 0.0f);
   int kmin = F;
   for (int k = F - 1; k >= 0; k--) {
-    load_frame(a, sh, LF, k, k + 1);
+    load_frame(sh, LF, k, k + 1);
     const int tb = sh.fr.tok_base, te = sh.fr.tok_base + sh.fr.ntok;
     for (int t = tb + threadIdx.x; t < te; t += DT) {
       if (k < pf) AG_ST(&R[t], __float_as_int(AG_LD(&X[t])));  // old extra cost
       AG_ST(&X[t], kInf);
     }
+    if (threadIdx.x == 0) sh.fl[0] = 0;
     __syncthreads();
+    FixRound fx;
     if (lat) {
       // emitting out-links of frame k (stored with frame k + 1: sources below its tokens)
       const int tb1 = sh.fr1.tok_base;
       for (long long i = sh.fr1.link_begin + threadIdx.x; i < sh.fr1.link_end; i += DT) {
-        const int4 r = LK[i];
-        if (r.x >= tb1) continue;
-        const float d = ((tok_cost(AR, r.x) + __int_as_float(r.w)) + __int_as_float(a.arcs[r.z].y)) -
-                        tok_cost(AR, r.y);
-        const float le = AG_LD(&X[r.y]) + d;
-        if (le <= beamp) atomic_min_pos(&X[r.x], fmaxf(le, 0.0f));
+        const int src = LK[i].x;
+        if (src >= tb1) continue;
+        const float le = AG_LD(&X[LK[i].y]) + __int_as_float(LDd[i]);
+        if (le <= beamp) atomic_min_pos(&X[src], le);
       }
+      __syncthreads();
       // epsilon links within frame k, to a fixpoint
-      while (true) {
-        __syncthreads();
-        if (threadIdx.x == 0) sh.flag = 0;
-        __syncthreads();
+      do {
+        fx.begin(sh);
         for (long long i = sh.fr.link_begin + threadIdx.x; i < sh.fr.link_end; i += DT) {
-          const int4 r = LK[i];
-          if (r.x < tb) continue;
-          const float d = (tok_cost(AR, r.x) + __int_as_float(a.arcs[r.z].y)) - tok_cost(AR, r.y);
-          const float le = fmaxf(AG_LD(&X[r.y]) + d, 0.0f);
-          if (le <= beamp && le < AG_LD(&X[r.x])) {
-            atomic_min_pos(&X[r.x], le);
-            sh.flag = 1;
+          const int src = LK[i].x;
+          if (src < tb) continue;
+          const float le = AG_LD(&X[LK[i].y]) + __int_as_float(LDd[i]);
+          if (le <= beamp && le < AG_LD(&X[src])) {
+            atomic_min_pos(&X[src], le);
+            fx.mark(sh);
           }
         }
-        __syncthreads();
-        if (!sh.flag) break;
-      }
+      } while (fx.end(sh));
     } else {
       // backpointer chains: frame k + 1's kept tokens keep their frame-k sources
       for (int t = sh.fr1.tok_base + threadIdx.x; t < sh.fr1.tok_base + sh.fr1.ntok; t += DT) {
@@ -834,130 +890,180 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
         const int pv = AG_LD(&AR[t].x);
         if (pv >= tb && pv < te) AG_ST(&X[pv], 0.0f);
       }
-      while (true) {  // epsilon backpointers inside frame k
-        __syncthreads();
-        if (threadIdx.x == 0) sh.flag = 0;
-        __syncthreads();
+      __syncthreads();
+      do {  // epsilon backpointers inside frame k
+        fx.begin(sh);
         for (int t = tb + threadIdx.x; t < te; t += DT) {
           if (AG_LD(&X[t]) != 0.0f) continue;
           const int pv = AG_LD(&AR[t].x);
           if (pv >= tb && pv < te && AG_LD(&X[pv]) != 0.0f) {
             AG_ST(&X[pv], 0.0f);
-            sh.flag = 1;
+            fx.mark(sh);
           }
         }
-        __syncthreads();
-        if (!sh.flag) break;
-      }
+      } while (fx.end(sh));
     }
     kmin = k;
     if (k < pf) {  // unchanged extra costs: the frames below are unchanged too
-      int ch = 0;
+      if (threadIdx.x == 0) sh.fl[0] = 0;
+      __syncthreads();
       for (int t = tb + threadIdx.x; t < te; t += DT)
-        ch |= AG_LD(&X[t]) != __int_as_float(AG_LD(&R[t]));
+        if (AG_LD(&X[t]) != __int_as_float(AG_LD(&R[t]))) sh.fl[0] = 1;
       __syncthreads();
-      if (threadIdx.x == 0) sh.flag = 0;
-      __syncthreads();
-      if (ch) sh.flag = 1;
-      __syncthreads();
-      if (!sh.flag) break;
+      if (!sh.fl[0]) break;
     }
   }
-  // ---- token remap over the window [wb, arena_used): frame by frame
-  load_frame(a, sh, LF, kmin, -1);
+  if (a.debug && a.links) prune_check(a, LF, LK, kmin, F, slot, 1, false);
+  // ---- token remap over the window [wb, arena_used): R[t - wb] = number of
+  // kept tokens before t (kDropped: t itself is dropped)
+  load_frame(sh, LF, kmin, -1);
   const int wb = sh.fr.tok_base;
+  const long long lw = sh.fr.link_begin;
+  const int end = st.arena_used;
   int out = wb;
-  for (int k = kmin; k <= F; k++) {
-    load_frame(a, sh, LF, k, -1);
-    const int tb = sh.fr.tok_base, te = sh.fr.tok_base + sh.fr.ntok;
-    const int nb = out;
-    for (int c0 = tb; c0 < te; c0 += DT) {
-      const int t = c0 + threadIdx.x;
-      int keep = 0;
-      if (t < te) keep = (k == F) || AG_LD(&X[t]) <= beamp;
-      block_scan(sh, keep);
-      if (t < te) AG_ST(&R[t - wb], keep ? out + sh.scan[threadIdx.x] : -1);
-      out += sh.total;
-      __syncthreads();
+  for (int c0 = wb; c0 < end; c0 += kPI * DT) {
+    const int t0 = c0 + kPI * (int)threadIdx.x;
+    int kb = 0, cnt = 0;
+#pragma unroll
+    for (int u = 0; u < kPI; u++) {
+      const int t = t0 + u;
+      const int k = t < end && (t >= tbF || AG_LD(&X[t]) <= beamp);
+      kb |= k << u;
+      cnt += k;
     }
-    if (threadIdx.x == 0) {
-      LF[k].new_base = nb;
-      LF[k].new_ntok = out - nb;
+    block_scan(sh, cnt);
+    int pre = out + sh.scan[threadIdx.x];
+#pragma unroll
+    for (int u = 0; u < kPI; u++) {
+      const int t = t0 + u;
+      if (t < end) AG_ST(&R[t - wb], ((kb >> u) & 1) ? pre : (pre | kDropped));
+      pre += (kb >> u) & 1;
     }
+    out += sh.total;
+    __syncthreads();
   }
   const int new_end = out;
-  // ---- links (before the tokens move: extra costs and costs by old index)
-  long long lout = 0;
-  if (a.links) {
-    load_frame(a, sh, LF, kmin, -1);
-    lout = sh.fr.link_begin;
-    for (int k = kmin; k <= F; k++) {
-      load_frame(a, sh, LF, k, -1);
-      const long long nb = lout;
-      for (long long c0 = sh.fr.link_begin; c0 < sh.fr.link_end; c0 += DT) {
-        const long long i = c0 + threadIdx.x;
-        int keep = 0;
-        int4 r = make_int4(0, 0, 0, 0);
-        if (i < sh.fr.link_end) {
-          r = LK[i];
-          const int rs = r.x >= wb ? AG_LD(&R[r.x - wb]) : r.x;
-          const int rd = r.y >= wb ? AG_LD(&R[r.y - wb]) : r.y;
-          if (rs >= 0 && rd >= 0) {
-            if (!lat || (k == F && r.x >= tbF)) {
-              keep = 1;  // the frontier's epsilon links (or no pruning state)
-            } else {
-              const bool eps = r.x >= sh.fr.tok_base;
-              const float w = __int_as_float(a.arcs[r.z].y);
-              const float d = eps ? (tok_cost(AR, r.x) + w) - tok_cost(AR, r.y)
-                                  : ((tok_cost(AR, r.x) + __int_as_float(r.w)) + w) - tok_cost(AR, r.y);
-              keep = AG_LD(&X[r.y]) + d <= beamp;
-            }
-            r.x = rs;
-            r.y = rd;
-          }
-        }
-        block_scan(sh, keep);  // every thread has read its record: writes may follow
-        if (keep) LK[lout + sh.scan[threadIdx.x]] = r;
-        lout += sh.total;
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) {
-        LF[k].link_begin = nb;
-        LF[k].link_end = lout;
-      }
-    }
-  }
-  // ---- move the kept tokens (and their extra costs) down, in order
-  for (int c0 = wb; c0 < st.arena_used; c0 += DT) {
-    const int t = c0 + threadIdx.x;
-    int nt = -1;
-    int4 rec = make_int4(0, 0, 0, 0);
-    float x = 0.0f;
-    if (t < st.arena_used) {
-      nt = AG_LD(&R[t - wb]);
-      if (nt >= 0) {
-        rec = ag_ld4(&AR[t]);
-        x = AG_LD(&X[t]);
-        if (rec.x >= wb) {
-          const int np = AG_LD(&R[rec.x - wb]);
-          if (np < 0) sh.bad |= 16;
-          rec.x = np;
-        }
-      }
-    }
-    __syncthreads();
-    if (nt >= 0) {
-      ag_st4(&AR[nt], rec);
-      AG_ST(&X[nt], x);
-    }
-    __syncthreads();
+  for (int k = kmin + threadIdx.x; k <= F; k += DT) {
+    const int tbk = LF[k].tok_base;
+    LF[k].new_base = tbk < end ? (AG_LD(&R[tbk - wb]) & ~kDropped) : new_end;
   }
   __syncthreads();
+  for (int k = kmin + threadIdx.x; k <= F; k += DT)
+    LF[k].new_ntok = (k < F ? LF[k + 1].new_base : new_end) - LF[k].new_base;
+  // ---- links (before the tokens move: extra costs by old index), whole
+  // window; wave 0 moves the frame boundaries that fall in each chunk
+  long long lout = lw;
+  if (a.links) {
+    const long long lend = st.links_used;
+    if (threadIdx.x == 0) sh.kk = kmin;
+    __syncthreads();
+    for (long long c0 = lw; c0 < lend; c0 += kPI * DT) {
+      const long long i0 = c0 + kPI * (long long)threadIdx.x;
+      int4 r[kPI];
+      int dv[kPI];
+      int kb = 0, cnt = 0;
+#pragma unroll
+      for (int u = 0; u < kPI; u++) {
+        const long long i = i0 + u;
+        int k = 0;
+        if (i < lend) {
+          r[u] = LK[i];
+          dv[u] = LDd[i];
+          const int rs = r[u].x >= wb ? AG_LD(&R[r[u].x - wb]) : r[u].x;
+          const int rd = r[u].y >= wb ? AG_LD(&R[r[u].y - wb]) : r[u].y;
+          if (((rs | rd) & kDropped) == 0) {
+            k = !lat || AG_LD(&X[r[u].y]) + __int_as_float(dv[u]) <= beamp;
+            r[u].x = rs;
+            r[u].y = rd;
+          }
+        }
+        kb |= k << u;
+        cnt += k;
+      }
+      sh.kbits[threadIdx.x] = (unsigned char)kb;
+      block_scan(sh, cnt);  // every thread has read its links: writes may follow
+      int pre = sh.scan[threadIdx.x];
+#pragma unroll
+      for (int u = 0; u < kPI; u++) {
+        if ((kb >> u) & 1) {
+          LK[lout + pre] = r[u];
+          LDd[lout + pre] = dv[u];
+        }
+        pre += (kb >> u) & 1;
+      }
+      if (threadIdx.x < 64) {  // frame boundaries inside this chunk
+        const long long cend = c0 + kPI * DT;
+        int kk = sh.kk;  // wave-uniform; sh.kk is only written back for the next chunk
+        while (true) {
+          const int k = kk + (int)threadIdx.x;
+          long long olb = 0;
+          bool in = false;
+          if (k <= F) {
+            olb = LF[k].link_begin;
+            in = olb < cend;
+          }
+          const unsigned long long m = __ballot(in);
+          if (in) {
+            const int q = (int)(olb - c0), th = q / kPI, w = q % kPI;
+            const int before = __popc((unsigned)sh.kbits[th] & ((1u << w) - 1u));
+            LF[k].link_begin = lout + sh.scan[th] + before;
+          }
+          const int nin = __popcll(m);
+          kk += nin;
+          if (nin < 64) break;
+        }
+        if (threadIdx.x == 0) sh.kk = kk;
+      }
+      lout += sh.total;
+      __syncthreads();
+    }
+    // boundaries at or past the end of the links
+    for (int k = sh.kk + threadIdx.x; k <= F; k += DT) LF[k].link_begin = lout;
+    __syncthreads();
+    for (int k = kmin + threadIdx.x; k <= F; k += DT) LF[k].link_end = k < F ? LF[k + 1].link_begin : lout;
+  }
+  // ---- move the kept tokens (and their extra costs) down, in order
+  for (int c0 = wb; c0 < end; c0 += kPI * DT) {
+    const int t0 = c0 + kPI * (int)threadIdx.x;
+    int nt[kPI];
+    int4 rec[kPI];
+    float x[kPI];
+#pragma unroll
+    for (int u = 0; u < kPI; u++) {
+      const int t = t0 + u;
+      nt[u] = -1;
+      if (t < end) {
+        const int rv = AG_LD(&R[t - wb]);
+        if ((rv & kDropped) == 0) {
+          nt[u] = rv;
+          rec[u] = ag_ld4(&AR[t]);
+          x[u] = AG_LD(&X[t]);
+          if (rec[u].x >= wb) {
+            const int np = AG_LD(&R[rec[u].x - wb]);
+            if (np & kDropped) sh.bad |= 16;
+            rec[u].x = np & ~kDropped;
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPI; u++)
+      if (nt[u] >= 0) {
+        ag_st4(&AR[nt[u]], rec[u]);
+        AG_ST(&X[nt[u]], x[u]);
+      }
+    __syncthreads();
+  }
   for (int k = kmin + threadIdx.x; k <= F; k += DT) {
     LF[k].tok_base = LF[k].new_base;
     LF[k].ntok = LF[k].new_ntok;
   }
   __syncthreads();
+  if (a.debug && a.links) prune_check(a, LF, LK, kmin, F, slot, 2, false);
+  if (a.debug && threadIdx.x == 0)
+    printf("prune slot %d F %d pf %d kmin %d wb %d end %d new_end %d links %lld -> %lld\n", slot, F, pf, kmin,
+           wb, end, new_end, lw, lout);
   st.cur_base = new_end - (endF - tbF);
   st.arena_used = new_end;
   if (a.links) st.links_used = lout;
