@@ -82,9 +82,9 @@ def test_ivectors_bit_exact(synth_model, test_wave, fpc, chunk):
 
 
 # decoder frame construction: LDS table with HBM overflow (default), every
-# state in the HBM tables, and a 2-slot LDS probe limit (states split between
+# state in the HBM tables, and one LDS bucket per state (states split between
 # LDS and HBM in every frame)
-FRAME_PATHS = {"default": None, "hbm": "0", "mixed": "2"}
+FRAME_PATHS = {"default": None, "hbm": "0", "mixed": "1"}
 
 
 @pytest.fixture(params=sorted(FRAME_PATHS))

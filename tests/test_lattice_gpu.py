@@ -12,7 +12,7 @@ from lattice_util import canon_engine, canon_oracle
 
 pytestmark = pytest.mark.gpu
 
-FRAME_PATHS = {"default": None, "hbm": "0", "mixed": "2"}
+FRAME_PATHS = {"default": None, "hbm": "0", "mixed": "1"}
 
 
 @pytest.fixture(autouse=True)

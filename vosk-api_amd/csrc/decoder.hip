@@ -7,8 +7,8 @@
 // (batch options).
 //
 // Per-stream state is bounded by the token counts, never by the graph size:
-// the frame under construction lives in an LDS open-addressing table (4096
-// slots); a state whose first kMaxProbe LDS slots are taken by other states
+// the frame under construction lives in an LDS table (4096 slots, two-choice
+// buckets of four); a state whose two buckets are taken by other states
 // lives in the stream's HBM hash table instead.  Placement is deterministic
 // within a frame -- slots are only ever claimed, never released, while a
 // frame is built -- so a relaxation's slot stays valid until the commit, and
@@ -41,7 +41,7 @@ constexpr int kLlhLds = 4096;         // log-likelihood row staged in LDS up to 
 constexpr int kTokLds = 1024;         // current-frame tokens cached in LDS up to this count
 constexpr int kHashCap = 4096;        // LDS frame table slots (power of two)
 constexpr int kHashBits = 12;
-constexpr int kMaxProbe = 32;         // default LDS probe limit (DecArgs::lds_probe); states past it live in HBM
+constexpr int kMaxProbe = 2;          // LDS buckets a state may use (DecArgs::lds_probe: 0 all HBM, 1 one bucket)
 constexpr int kFrontLds = 2048;       // epsilon frontier entries in LDS (more spill to HBM)
 constexpr int kUnroll = 4;            // (token, arc) items in flight per thread in the emitting pass
 constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
@@ -74,6 +74,29 @@ struct DecShared {
   unsigned char kbits[DT];    // pruning: per-thread keep bits of the chunk
   LatFrame fr;        // pruning: the frame record being processed (broadcast)
   LatFrame fr1;
+};
+
+// optional phase clocks (VOSK_AMD_DEC_PROFILE): thread 0 stamps s_memtime
+// at phase ends; slots as vosk/engine.py Engine.PHASES
+struct Prof {
+  bool on;
+  long long t;
+  long long acc[kDecProf];
+  __device__ __forceinline__ void init(bool o) {
+    on = o;
+    for (int i = 0; i < kDecProf; i++) acc[i] = 0;
+    t = on ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  }
+  __device__ __forceinline__ void mark(int i) {
+    if (on) {
+      const long long n = (long long)__builtin_amdgcn_s_memtime();
+      acc[i] += n - t;
+      t = n;
+    }
+  }
+  __device__ __forceinline__ void count(int i, long long v) {
+    if (on) acc[i] += v;
+  }
 };
 
 __device__ __forceinline__ float wave_min_f(float v) {
@@ -230,8 +253,20 @@ struct HbmTab {
   int* list;                // [max_tok] slots in creation order
 };
 
-__device__ __forceinline__ unsigned lds_hash(int s) {
-  return ((unsigned)s * 2654435761u) >> (32 - kHashBits);
+// LDS frame table: kHashCap / 4 buckets of four slots; a state lives in the
+// first empty slot of its first bucket, else of its second bucket, else in
+// the HBM table (two-choice bucketed hashing: at most eight slots looked at)
+constexpr int kBucketBits = kHashBits - 2;
+__device__ __forceinline__ unsigned bucket1(int s) {
+  return ((unsigned)s * 2654435761u) >> (32 - kBucketBits);
+}
+__device__ __forceinline__ unsigned bucket2(int s, unsigned b1) {
+  unsigned x = (unsigned)s * 0x85ebca6bu;
+  x ^= x >> 15;
+  x *= 0x27d4eb2du;
+  x ^= x >> 13;
+  const unsigned b = x >> (32 - kBucketBits);
+  return b == b1 ? b ^ 1u : b;
 }
 // independent of lds_hash, so states crowded in LDS spread out in HBM
 __device__ __forceinline__ unsigned hbm_hash(int s, int bits) {
@@ -273,24 +308,35 @@ struct Relax {
 __device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const FrameLds& t,
                                        const HbmTab& T, int dest, float tot, int arc, bool eps) {
   const unsigned long long k = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
-  unsigned h = lds_hash(dest);
-  for (int probe = 0; probe < a.lds_probe; probe++) {
-    int cur = __hip_atomic_load(&t.hs[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (cur == -1) {
-      cur = atomicCAS(&t.hs[h], -1, dest);
-      if (cur == -1) {
-        const int pos = atomicAdd(&sh.n_new_l, 1);  // < kHashCap: one per claimed slot
-        t.nl[pos] = (unsigned short)h;
-        t.hp[h] = (unsigned short)(pos | (eps ? kPosEps : 0));
-        atomicMin(&t.hk[h], k);
-        return Relax{(int)h, 2};
+  const int nbk = a.lds_probe < 2 ? a.lds_probe : 2;
+  const unsigned b1 = bucket1(dest);
+  for (int nb = 0; nb < nbk; nb++) {
+    const int h0 = 4 * (int)(nb ? bucket2(dest, b1) : b1);
+    while (true) {  // buckets fill left to right: claim the first empty slot
+      int e = -1, f = -1;
+#pragma unroll
+      for (int i = 3; i >= 0; i--) {
+        const int c = __hip_atomic_load(&t.hs[h0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (c == dest) f = i;
+        if (c == -1) e = i;
       }
-    }
-    if (cur == dest) {
+      int h = h0 + f;
+      if (f < 0) {
+        if (e < 0) break;  // full: the second bucket, then HBM
+        h = h0 + e;
+        const int cur = atomicCAS(&t.hs[h], -1, dest);
+        if (cur == -1) {
+          const int pos = atomicAdd(&sh.n_new_l, 1);  // < kHashCap: one per claimed slot
+          t.nl[pos] = (unsigned short)h;
+          t.hp[h] = (unsigned short)(pos | (eps ? kPosEps : 0));
+          atomicMin(&t.hk[h], k);
+          return Relax{h, 2};
+        }
+        if (cur != dest) continue;  // another state took it: look again
+      }
       const unsigned long long old = atomicMin(&t.hk[h], k);
-      return Relax{(int)h, k < old ? 1 : 0};
+      return Relax{h, k < old ? 1 : 0};
     }
-    h = (h + 1) & (kHashCap - 1);
   }
   const unsigned hm = (1u << a.hbits) - 1u;
   unsigned g = hbm_hash(dest, a.hbits);
@@ -345,12 +391,15 @@ __device__ __forceinline__ int bp_slot(int bp) {
 // kNoSlot if absent
 constexpr int kNoSlot = 0x7fffffff;
 __device__ __forceinline__ int frame_slot(const DecArgs& a, const FrameLds& t, const HbmTab& T, int s) {
-  unsigned h = lds_hash(s);
-  for (int probe = 0; probe < a.lds_probe; probe++) {
-    const int c = t.hs[h];
-    if (c == s) return (int)h;
-    if (c == -1) break;
-    h = (h + 1) & (kHashCap - 1);
+  const int nbk = a.lds_probe < 2 ? a.lds_probe : 2;
+  const unsigned b1 = bucket1(s);
+  for (int nb = 0; nb < nbk; nb++) {
+    const int h0 = 4 * (int)(nb ? bucket2(s, b1) : b1);
+    for (int i = 0; i < 4; i++) {
+      const int c = t.hs[h0 + i];
+      if (c == s) return h0 + i;
+      if (c == -1) return kNoSlot;  // the state would be here
+    }
   }
   const unsigned hm = (1u << a.hbits) - 1u;
   unsigned g = hbm_hash(s, a.hbits);
@@ -410,7 +459,7 @@ __device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long 
 __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh, const FrameLds& t,
                                  const HbmTab& T, const DecPtrs& p, const TokView& tv, int ntok,
                                  float cutoff, float cost_offset, const float* Lp, int mode,
-                                 float bound, int* examined, const DecSlot& st, int slot) {
+                                 float bound, int* examined, const DecSlot& st, int slot, Prof& pr) {
   float m = __int_as_float(0x7f800000);
   const bool lat = a.links != nullptr && mode == 1;
   for (int c0 = 0; c0 < ntok; c0 += DT) {
@@ -431,6 +480,8 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
     sh.tcost[threadIdx.x] = c;
     sh.tsrc[threadIdx.x] = src;
     __syncthreads();
+    pr.mark(2);
+    pr.count(14, 1);
     const int total = sh.total;
     *examined += total;
     for (int sb = 0; sb < total; sb += DT * kUnroll) {
@@ -470,14 +521,17 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
           if (r.flags == 2 && de) push_front(a, sh, t, p, 0, &sh.n_front, r.slot);
         }
       }
+      pr.mark(3);
       if (mode == 1) {
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kUnroll; u++)
           if (sv[u] != 0x7fffffff && slot_key(t, T, sv[u]) == kv[u]) set_bp(t, T, sv[u], sh.tsrc[jv[u]]);
+        pr.mark(4);
       }
     }
     __syncthreads();
+    pr.mark(2);
   }
   return block_min_f(sh, m);
 }
@@ -486,12 +540,14 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
 // hold states with epsilon arcs (round 0: created by the emitting pass);
 // a state improved in a round is expanded again in the next one.
 __device__ __forceinline__ void eps_closure(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
-                            const DecPtrs& p, DecSlot& st, float cutoff, int nfront, int* arcs_eps) {
+                            const DecPtrs& p, DecSlot& st, float cutoff, int nfront, int* arcs_eps,
+                            Prof& pr) {
   int b = 0;
   int examined = 0;
   const int cap = kFrontLds + a.max_tok;
   nfront = nfront < cap ? nfront : cap;
   while (nfront > 0) {
+    pr.count(13, 1);
     st.stamp++;
     const int stamp = st.stamp;
     __syncthreads();
@@ -586,7 +642,7 @@ __device__ __forceinline__ void hbm_clear_all(const DecArgs& a, const HbmTab& T)
 // link_dst.  Returns the frame's link count.
 __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
                             const DecPtrs& p, const DecSlot& st, int slot, int base, int nl_n,
-                            int neps, float cutoff) {
+                            int neps, float cutoff, Prof& pr) {
   int4* L = a.links + (long long)slot * a.link_cap;
   int* LD = a.link_dst + (long long)slot * a.link_cap;
   const long long lb = st.links_used;
@@ -616,6 +672,7 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
     out += sh.total;
     __syncthreads();
   }
+  pr.mark(7);
   // epsilon links of the committed tokens, at their final costs
   if (threadIdx.x == 0) sh.n_eps = 0;
   for (int c0 = 0; c0 < neps; c0 += DT) {
@@ -661,6 +718,7 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
     }
     __syncthreads();
   }
+  pr.mark(8);
   const int n = out + sh.n_eps;
   if (nrec < sh.n_links || lb + n > a.link_cap) sh.lat_ovf = 1;
   return lb + n > a.link_cap ? (int)(a.link_cap - lb) : n;
@@ -672,7 +730,7 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
 // next_cutoff) keep an arena slot marked dead.  Then both tables are cleared.
 __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds& t, DecPtrs& p, DecSlot& st,
                        int* TS, float* TC, bool* lds, float cutoff, float* best_out, int slot,
-                       int* nlinks) {
+                       int* nlinks, Prof& pr) {
   __syncthreads();
   const HbmTab T = hbm_tab(a, slot);
   const int nl_n = sh.n_new_l;
@@ -727,14 +785,17 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
     }
   }
   bk = block_min_u64(sh, bk);  // ends with a barrier
+  pr.mark(6);
+  pr.count(12, n);
   if (!ok) sh.bad |= 2;
   const int live = sh.n_next;
   const int neps = sh.n_front < kFrontLds + a.max_tok ? sh.n_front : kFrontLds + a.max_tok;
-  *nlinks = (lat && ok) ? commit_links(a, sh, t, T, p, st, slot, base, nl_n, neps, cutoff) : 0;
+  *nlinks = (lat && ok) ? commit_links(a, sh, t, T, p, st, slot, base, nl_n, neps, cutoff, pr) : 0;
   __syncthreads();
   hbm_clear_listed(T, ng);
   lds_clear_build(t);
   __syncthreads();
+  pr.mark(9);
   if (ok) {
     st.cur_base = base;
     st.arena_used = base + n;
@@ -1113,16 +1174,8 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   }
   int arcs_eps = 0;
   bool lds = false;
-  // optional phase clocks (diagnostics): thread 0 stamps s_memtime
-  const bool prof = PROF && threadIdx.x == 0;
-  long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long tstamp = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
-#define DEC_PHASE(i)                                                     \
-  if (prof) {                                                            \
-    const long long _t = (long long)__builtin_amdgcn_s_memtime();        \
-    pacc[i] += _t - tstamp;                                              \
-    tstamp = _t;                                                         \
-  }
+  Prof pr;
+  pr.init(PROF && threadIdx.x == 0);
 
   if (job.reset) {  // InitDecoding: start token, closure with cutoff = beam
     __syncthreads();
@@ -1151,10 +1204,10 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       t.fr0[0] = r.slot;
       sh.n_front = 1;
     }
-    eps_closure(a, sh, t, T, p, st, a.beam, 1, &arcs_eps);
+    eps_closure(a, sh, t, T, p, st, a.beam, 1, &arcs_eps, pr);
     float b;
     int nl = 0;
-    commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, &nl);
+    commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, &nl, pr);
     frame_done(a, sh, st, slot, 0, a.beam, 0.0f, nl);
   } else if (st.ntok > 0 && st.ntok <= kTokLds) {
     for (int i = threadIdx.x; i < st.ntok; i += DT) {
@@ -1231,7 +1284,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       }
     }
     const float cost_offset = -best;
-    DEC_PHASE(0);
+    pr.mark(0);
     // ---- ProcessEmitting: Kaldi's seed from the best token's arcs (wave 0)
     if (threadIdx.x < 64) {
       float sd = __int_as_float(0x7f800000);
@@ -1251,7 +1304,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       }
     }
     __syncthreads();
-    DEC_PHASE(1);
+    pr.mark(1);
     const float seed = sh.seed;
     int examined = 0;
     float next_cutoff, new_best;
@@ -1263,24 +1316,24 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     // the exact two-pass form runs.
     if (seed != __int_as_float(0x7f800000)) {
       const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
-                                      &examined, st, slot);
+                                      &examined, st, slot, pr);
       next_cutoff = seed;
       if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
     } else {
       const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
-                                      &examined, st, slot);
+                                      &examined, st, slot, pr);
       next_cutoff = seed;
       if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
       int dummy = 0;
       expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy, st,
-                      slot);
+                      slot, pr);
     }
     __syncthreads();
-    DEC_PHASE(2);
-    if (prof) pacc[3] += sh.n_new_g;  // tokens the emitting pass created in the HBM table
-    eps_closure(a, sh, t, T, p, st, next_cutoff, sh.n_front, &arcs_eps);
+    pr.mark(2);
+    pr.count(11, sh.n_new_g);  // tokens the emitting pass created in the HBM table
+    eps_closure(a, sh, t, T, p, st, next_cutoff, sh.n_front, &arcs_eps, pr);
     __syncthreads();
-    DEC_PHASE(4);
+    pr.mark(5);
     if (pf) {  // L is not read again in this frame
 #pragma unroll
       for (int r = 0; r < kLlhRegs; r++) {
@@ -1289,9 +1342,8 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       }
     }
     int nl = 0;
-    commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, &nl);
-    DEC_PHASE(5);
-    if (prof) pacc[7]++;
+    commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, &nl, pr);
+    pr.count(15, 1);
     frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset, nl);
     st.offset_sum += (double)cost_offset;
     st.frames++;
@@ -1320,11 +1372,10 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     __syncthreads();
     if (sh.bad) st.err |= sh.bad;
   }
-  DEC_PHASE(6);
+  pr.mark(10);
   if (threadIdx.x == 0) a.slots[slot] = st;
-  if (prof)
-    for (int i = 0; i < 8; i++) a.prof[slot * 8 + i] += pacc[i];
-#undef DEC_PHASE
+  if (pr.on)
+    for (int i = 0; i < kDecProf; i++) a.prof[slot * kDecProf + i] += pr.acc[i];
 }
 
 int DecoderLdsProbe() { return kMaxProbe; }

@@ -691,8 +691,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   dec_.stats = cfg_.collect_stats ? d_stats_ : nullptr;
   dec_.prof = nullptr;
   if (getenv("VOSK_AMD_DEC_PROFILE")) {
-    dec_.prof = (long long*)DevAlloc(sizeof(long long) * 8 * S);
-    HIPCHECK(hipMemset(dec_.prof, 0, sizeof(long long) * 8 * S));
+    dec_.prof = (long long*)DevAlloc(sizeof(long long) * kDecProf * S);
+    HIPCHECK(hipMemset(dec_.prof, 0, sizeof(long long) * kDecProf * S));
   }
   LaunchInitTables(dec_.ht_state, dec_.ht_key, dec_.ht_stamp, S * H, stream_);
 
@@ -1566,15 +1566,15 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
   }
 }
 
-void Engine::DecoderPhaseClocks(long long* out8, long long* per_slot) {
+void Engine::DecoderPhaseClocks(long long* out, long long* per_slot) {
   std::lock_guard<std::mutex> lk(mu_);
   FlushLocked();
-  for (int i = 0; i < 8; i++) out8[i] = 0;
-  if (!dec_.prof) return;
-  std::vector<long long> h((size_t)8 * slots_.size());
-  HIPCHECK(hipMemcpy(h.data(), dec_.prof, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
+  for (int i = 0; i < kDecProf; i++) out[i] = 0;
+  std::vector<long long> h((size_t)kDecProf * slots_.size(), 0);
+  if (dec_.prof)
+    HIPCHECK(hipMemcpy(h.data(), dec_.prof, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
   for (size_t s = 0; s < slots_.size(); s++)
-    for (int i = 0; i < 8; i++) out8[i] += h[s * 8 + i];
+    for (int i = 0; i < kDecProf; i++) out[i] += h[s * kDecProf + i];
   if (per_slot) std::copy(h.begin(), h.end(), per_slot);
 }
 

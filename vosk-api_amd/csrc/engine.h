@@ -190,10 +190,10 @@ class Engine {
   // (OnlineNnet2FeaturePipeline::NumFramesReady: the splice's right context
   // waits for more frames until input is finished)
   int IvectorFramesReady(int slot) const;
-  // VOSK_AMD_DEC_PROFILE=1: summed s_memtime clocks per decoder phase
-  // [cutoff, seed, expand, tokens created in the HBM table, eps, commit,
-  // prune, frames]; per_slot (optional): the same per slot [max_slots][8]
-  void DecoderPhaseClocks(long long* out8, long long* per_slot = nullptr);
+  // VOSK_AMD_DEC_PROFILE=1: summed s_memtime clocks per decoder phase and
+  // event counts, kDecProf values (decoder.hip Prof); per_slot (optional):
+  // the same per slot [max_slots][kDecProf]
+  void DecoderPhaseClocks(long long* out, long long* per_slot = nullptr);
 
  private:
   struct SlotHost {

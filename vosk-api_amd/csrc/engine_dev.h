@@ -232,8 +232,9 @@ struct FrameStat {
   float best, cutoff, next_cutoff, adaptive_beam;
 };
 
+constexpr int kDecProf = 16;  // decoder phase-clock slots per stream (decoder.hip Prof)
 struct DecArgs {
-  long long* prof;       // optional per-slot phase clocks [slots][8] (diagnostics)
+  long long* prof;       // optional per-slot phase clocks [slots][kDecProf] (diagnostics)
   const int4* sinfo;     // per state {arc_begin, eps_begin, arc_end, final cost bits}
   const int4* arcs;      // per arc {nextstate, weight bits, pdf (-1 eps),
                          //          source state | (nextstate has eps arcs) << 31}

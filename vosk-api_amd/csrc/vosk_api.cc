@@ -718,7 +718,7 @@ int vamd_engine_decoder_phases(VamdEngine* e, long long* o8) {
 
 int vamd_engine_decoder_phases_per_stream(VamdEngine* e, long long* o) {
   API_TRY
-  long long tot[8];
+  long long tot[kDecProf];
   e->eng->DecoderPhaseClocks(tot, o);
   return 0;
   API_CATCH(-1)

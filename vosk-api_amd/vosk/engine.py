@@ -302,18 +302,19 @@ class Engine:
         return dict(zip(("frames", "tok_in", "tok_out", "arcs_emit", "arcs_eps", "links"), out.tolist()))
 
     def decoder_phases(self):
-        out = np.zeros(8, np.int64)
+        out = np.zeros(16, np.int64)
         _chk(_c.vamd_engine_decoder_phases(self.h, out.ctypes.data))
-        # clocks per phase; slot 3 sums the tokens the emitting pass created
-        # in the HBM table (past the LDS table's probe limit), slot 6 the
-        # clocks of the pruning passes
         return dict(zip(self.PHASES, out.tolist()))
 
-    PHASES = ("cutoff", "seed", "expand", "hbm_created", "eps", "commit", "prune", "frames")
+    # decoder.hip Prof: s_memtime clocks per phase (slots 0-10), then counts
+    PHASES = ("cutoff", "seed", "exp_tokens", "exp_items", "exp_winners", "eps", "commit_toks",
+              "commit_links", "commit_eps_links", "commit_clear", "prune", "n_hbm_created",
+              "n_created", "n_eps_rounds", "n_chunks", "frames")
+    PHASE_CLOCKS = PHASES[:11]
 
     def decoder_phases_per_stream(self):
-        """[max_streams, 8] int64: decoder_phases() per stream slot."""
-        out = np.zeros((self.max_streams, 8), np.int64)
+        """[max_streams, 16] int64: decoder_phases() per stream slot."""
+        out = np.zeros((self.max_streams, 16), np.int64)
         _chk(_c.vamd_engine_decoder_phases_per_stream(self.h, out.ctypes.data))
         return out
 
