@@ -45,6 +45,7 @@ constexpr int kMaxProbe = 2;          // LDS buckets a state may use (DecArgs::l
 constexpr int kFrontLds = 2048;       // epsilon frontier entries in LDS (more spill to HBM)
 constexpr int kUnroll = 4;            // (token, arc) items in flight per thread in the emitting pass
 constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
+constexpr int kNoSlot = 0x7fffffff;   // no frame-table slot
 constexpr unsigned kDestEps = 0x80000000u;  // arcs[].w: nextstate has epsilon arcs
 // backpointer of a frame-table slot: an emitting source's arena index (>= 0),
 // or kBpEps | the epsilon source's slot (kBpHbm: an HBM-table slot)
@@ -305,9 +306,26 @@ struct Relax {
   int slot, flags;
 };
 
-__device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const FrameLds& t,
-                                       const HbmTab& T, int dest, float tot, int arc, bool eps) {
-  const unsigned long long k = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
+// a new HBM-table entry at slot g: listed, key by atomic min (a concurrent
+// relaxation of the same state may already have lowered it)
+__device__ __forceinline__ void hbm_created(const DecArgs& a, DecShared& sh, const HbmTab& T, unsigned g,
+                                            unsigned long long k, bool eps) {
+  const int pos = atomicAdd(&sh.n_new_g, 1);
+  if (pos < a.max_tok) {
+    AG_ST(&T.list[pos], (int)g);
+    AG_ST(&T.pos[g], pos | (eps ? kHPosEps : 0));
+  } else {
+    sh.bad |= 1;
+  }
+  __hip_atomic_fetch_min(&T.key[g], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// LDS part of a relaxation (key k); slot kNoSlot: both buckets are full.
+// Without NEED_OLD the key is lowered without waiting for the old value and
+// an existing state reports flags 1.
+template <bool NEED_OLD>
+__device__ __forceinline__ Relax relax_lds(const DecArgs& a, DecShared& sh, const FrameLds& t, int dest,
+                                           unsigned long long k, bool eps) {
   const int nbk = a.lds_probe < 2 ? a.lds_probe : 2;
   const unsigned b1 = bucket1(dest);
   for (int nb = 0; nb < nbk; nb++) {
@@ -329,32 +347,34 @@ __device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const Fr
           const int pos = atomicAdd(&sh.n_new_l, 1);  // < kHashCap: one per claimed slot
           t.nl[pos] = (unsigned short)h;
           t.hp[h] = (unsigned short)(pos | (eps ? kPosEps : 0));
-          atomicMin(&t.hk[h], k);
+          __hip_atomic_fetch_min(&t.hk[h], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           return Relax{h, 2};
         }
         if (cur != dest) continue;  // another state took it: look again
       }
-      const unsigned long long old = atomicMin(&t.hk[h], k);
-      return Relax{h, k < old ? 1 : 0};
+      if (NEED_OLD) {
+        const unsigned long long old = atomicMin(&t.hk[h], k);
+        return Relax{h, k < old ? 1 : 0};
+      }
+      __hip_atomic_fetch_min(&t.hk[h], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return Relax{h, 1};
     }
   }
+  return Relax{kNoSlot, 0};
+}
+
+__device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                       const HbmTab& T, int dest, float tot, int arc, bool eps) {
+  const unsigned long long k = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
+  const Relax rl = relax_lds<true>(a, sh, t, dest, k, eps);
+  if (rl.slot != kNoSlot) return rl;
   const unsigned hm = (1u << a.hbits) - 1u;
   unsigned g = hbm_hash(dest, a.hbits);
   for (int probe = 0; probe < a.hprobe; probe++) {
-    int cur = AG_LD(&T.state[g]);
+    const int cur = atomicCAS(&T.state[g], -1, dest);  // one round trip per probe
     if (cur == -1) {
-      cur = atomicCAS(&T.state[g], -1, dest);
-      if (cur == -1) {
-        const int pos = atomicAdd(&sh.n_new_g, 1);
-        if (pos < a.max_tok) {
-          AG_ST(&T.list[pos], (int)g);
-          AG_ST(&T.pos[g], pos | (eps ? kHPosEps : 0));
-        } else {
-          sh.bad |= 1;
-        }
-        atomicMin(&T.key[g], k);
-        return Relax{~(int)g, 2};
-      }
+      hbm_created(a, sh, T, g, k, eps);
+      return Relax{~(int)g, 2};
     }
     if (cur == dest) {
       const unsigned long long old = atomicMin(&T.key[g], k);
@@ -364,6 +384,63 @@ __device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const Fr
   }
   sh.bad |= 1;
   return Relax{0, -1};
+}
+
+// The emitting pass's relaxations, kUnroll per thread: the LDS buckets
+// first, then the HBM probes of all items that need them in flight together
+// (one CAS per probe); keys by atomic min without waiting for the result
+// (the winners are found after the sub-round's barrier).  Output per item:
+// slot (kNoSlot: no relaxation) and created.
+__device__ __forceinline__ void relax_batch(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
+                                            const int* dest, const unsigned long long* key, const bool* eps,
+                                            const bool* want, int* slot_out, bool* created) {
+  bool pend[kUnroll];
+  unsigned g[kUnroll];
+  bool any = false;
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++) {
+    slot_out[u] = kNoSlot;
+    created[u] = false;
+    pend[u] = false;
+    if (!want[u]) continue;
+    const Relax r = relax_lds<false>(a, sh, t, dest[u], key[u], eps[u]);
+    if (r.slot != kNoSlot) {
+      slot_out[u] = r.slot;
+      created[u] = r.flags == 2;
+    } else {
+      pend[u] = true;
+      g[u] = hbm_hash(dest[u], a.hbits);
+      any = true;
+    }
+  }
+  const unsigned hm = (1u << a.hbits) - 1u;
+  for (int probe = 0; any && probe < a.hprobe; probe++) {
+    int cur[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++)
+      if (pend[u]) cur[u] = atomicCAS(&T.state[g[u]], -1, dest[u]);
+    any = false;
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++) {
+      if (!pend[u]) continue;
+      if (cur[u] == -1) {
+        hbm_created(a, sh, T, g[u], key[u], eps[u]);
+        slot_out[u] = ~(int)g[u];
+        created[u] = true;
+        pend[u] = false;
+      } else if (cur[u] == dest[u]) {
+        __hip_atomic_fetch_min(&T.key[g[u]], key[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        slot_out[u] = ~(int)g[u];
+        pend[u] = false;
+      } else {
+        g[u] = (g[u] + 1) & hm;
+        any = true;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kUnroll; u++)
+    if (pend[u]) sh.bad |= 1;
 }
 
 __device__ __forceinline__ unsigned long long slot_key(const FrameLds& t, const HbmTab& T, int v) {
@@ -389,7 +466,6 @@ __device__ __forceinline__ int bp_slot(int bp) {
 
 // slot of state s in the frame under construction (eps links at commit);
 // kNoSlot if absent
-constexpr int kNoSlot = 0x7fffffff;
 __device__ __forceinline__ int frame_slot(const DecArgs& a, const FrameLds& t, const HbmTab& T, int s) {
   const int nbk = a.lds_probe < 2 ? a.lds_probe : 2;
   const unsigned b1 = bucket1(s);
@@ -498,27 +574,33 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
           A[u] = a.arcs[arcv[u]];
         }
       }
-      int sv[kUnroll];
+      int sv[kUnroll], dst[kUnroll];
       unsigned long long kv[kUnroll];
+      float acv[kUnroll], totv[kUnroll];
+      bool want[kUnroll], de[kUnroll], cr[kUnroll];
 #pragma unroll
       for (int u = 0; u < kUnroll; u++) {
-        sv[u] = 0x7fffffff;
+        want[u] = false;
         if (jv[u] < 0) continue;
         const int j = jv[u];
-        const float ac = cost_offset - Lp[A[u].z];
-        const float tot = (sh.tcost[j] + ac) + __int_as_float(A[u].y);
-        m = fminf(m, tot);
-        if (mode == 1 && tot < bound) {
-          const bool de = ((unsigned)A[u].w & kDestEps) != 0;
-          const Relax r = relax(a, sh, t, T, A[u].x, tot, arcv[u], de);
-          if (r.flags > 0) {
-            sv[u] = r.slot;
-            kv[u] = ((unsigned long long)ford(tot) << 32) | (unsigned)arcv[u];
-          }
+        acv[u] = cost_offset - Lp[A[u].z];
+        totv[u] = (sh.tcost[j] + acv[u]) + __int_as_float(A[u].y);
+        m = fminf(m, totv[u]);
+        want[u] = mode == 1 && totv[u] < bound;
+        dst[u] = A[u].x;
+        de[u] = ((unsigned)A[u].w & kDestEps) != 0;
+        kv[u] = ((unsigned long long)ford(totv[u]) << 32) | (unsigned)arcv[u];
+      }
+      if (mode == 1) {
+        relax_batch(a, sh, t, T, dst, kv, de, want, sv, cr);
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+          if (!want[u]) continue;
           if (lat)
             emit_link(a, sh, st.links_used, slot,
-                      make_int4(sh.tsrc[j], __float_as_int(tot), arcv[u], __float_as_int(ac)), r.slot);
-          if (r.flags == 2 && de) push_front(a, sh, t, p, 0, &sh.n_front, r.slot);
+                      make_int4(sh.tsrc[jv[u]], __float_as_int(totv[u]), arcv[u], __float_as_int(acv[u])),
+                      sv[u]);
+          if (cr[u] && de[u]) push_front(a, sh, t, p, 0, &sh.n_front, sv[u]);
         }
       }
       pr.mark(3);
@@ -526,7 +608,8 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kUnroll; u++)
-          if (sv[u] != 0x7fffffff && slot_key(t, T, sv[u]) == kv[u]) set_bp(t, T, sv[u], sh.tsrc[jv[u]]);
+          if (want[u] && sv[u] != kNoSlot && slot_key(t, T, sv[u]) == kv[u])
+            set_bp(t, T, sv[u], sh.tsrc[jv[u]]);
         pr.mark(4);
       }
     }
@@ -657,8 +740,8 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
     if (i < nrec) {
       r = L[lb + i];
       const float tot = __int_as_float(r.y);
-      if (tot < cutoff) {
-        const int v = LD[lb + i];
+      const int v = LD[lb + i];
+      if (tot < cutoff && v != kNoSlot) {  // (kNoSlot: a failed relaxation, the frame is in error)
         r.y = base + slot_pos(t, T, nl_n, v);
         d = tot - funord((uint32_t)(slot_key(t, T, v) >> 32));
         keep = 1;
