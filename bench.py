@@ -272,7 +272,7 @@ def main():
                 sum(ph[k] for k in e.PHASE_CLOCKS) / max(ph["frames"], 1), 1)
             # per-stream spread: the slowest stream sets each launch's time
             per = e.decoder_phases_per_stream()[:S]
-            clk = per[:, :len(e.PHASE_CLOCKS)].sum(1).astype(np.float64)
+            clk = per[:, e.PHASE_CLOCK_IDX].sum(1).astype(np.float64)
             out["decoder_stream_clocks"] = {
                 "mean": round(float(clk.mean()), 1), "p50": round(float(np.percentile(clk, 50)), 1),
                 "p90": round(float(np.percentile(clk, 90)), 1), "max": round(float(clk.max()), 1),

@@ -160,8 +160,8 @@ int vamd_engine_stage_times(VamdEngine *e, double *ms4, long long *launches4, in
 int vamd_engine_decoder_totals(VamdEngine *e, long long *out6);
 /* decoder phase clocks (env VOSK_AMD_DEC_PROFILE=1), summed over streams:
  * [cutoff, seed, expand, compact, eps-closure, commit, 0, frames] */
-int vamd_engine_decoder_phases(VamdEngine *e, long long *out16);
-/* the same per stream slot: out[max_streams][16] */
+int vamd_engine_decoder_phases(VamdEngine *e, long long *out24);
+/* the same per stream slot: out[max_streams][24] */
 int vamd_engine_decoder_phases_per_stream(VamdEngine *e, long long *out);
 /* engine counters: [steps, launches, mfcc frames, chunk jobs, frames decoded] */
 int vamd_engine_counters(VamdEngine *e, long long *out5);

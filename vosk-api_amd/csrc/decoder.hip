@@ -71,7 +71,7 @@ struct DecShared {
   unsigned sel_prefix, sel_mask;
   float seed;
   int bad, flag, kk;
-  int fl[3];                  // FixRound flags
+  int fl[8];                  // FixRound flags (two sets of three) + change flags
   unsigned char kbits[DT];    // pruning: per-thread keep bits of the chunk
   LatFrame fr;        // pruning: the frame record being processed (broadcast)
   LatFrame fr1;
@@ -947,13 +947,14 @@ __device__ __forceinline__ void load_frame(DecShared& sh, const LatFrame* LF, in
 // flags, one barrier per round
 struct FixRound {
   int it = 0;
+  int base = 0;  // flag set (alternate sets in consecutive loops need no barrier between them)
   __device__ __forceinline__ void begin(DecShared& sh) {
-    if (threadIdx.x == 0) sh.fl[(it + 1) % 3] = 0;
+    if (threadIdx.x == 0) sh.fl[base + (it + 1) % 3] = 0;
   }
-  __device__ __forceinline__ void mark(DecShared& sh) { sh.fl[it % 3] = 1; }
+  __device__ __forceinline__ void mark(DecShared& sh) { sh.fl[base + it % 3] = 1; }
   __device__ __forceinline__ bool end(DecShared& sh) {  // true: another round
     __syncthreads();
-    const bool again = sh.fl[it % 3] != 0;
+    const bool again = sh.fl[base + it % 3] != 0;
     it++;
     return again;
   }
@@ -977,7 +978,8 @@ __device__ void prune_check(const DecArgs& a, const LatFrame* LF, const int4* LK
   __syncthreads();
 }
 
-__device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, DecSlot& st, const DecPtrs& p, int slot) {
+__device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, DecSlot& st, const DecPtrs& p, int slot,
+                                              Prof& pr) {
   const int F = st.frames;
   if (F <= 0 || F >= a.lat_frame_cap || st.err) return;
   LatFrame* LF = a.lat_frames + (long long)slot * a.lat_frame_cap;
@@ -994,20 +996,32 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
   const int tbF = sh.fr.tok_base, endF = sh.fr.tok_base + sh.fr.ntok;
   for (int t = tbF + threadIdx.x; t < endF; t += DT) AG_ST(&X[t], 0.0f);
   int kmin = F;
-  for (int k = F - 1; k >= 0; k--) {
-    load_frame(sh, LF, k, k + 1);
-    const int tb = sh.fr.tok_base, te = sh.fr.tok_base + sh.fr.ntok;
+  // Frames below prune_from are revisited at most prune_interval deep: a
+  // frame past that keeps the extra costs of its last walk, which are never
+  // above the current ones (safe, it is only pruned less).
+  const int kstop = pf - a.prune_interval > 0 ? pf - a.prune_interval : 0;
+  for (int k = F - 1; k >= kstop; k--) {
+    // frame records read by every thread (nothing writes them during this walk)
+    const LatFrame fk = LF[k], fk1 = LF[k + 1];
+    const int tb = fk.tok_base, te = fk.tok_base + fk.ntok;
     for (int t = tb + threadIdx.x; t < te; t += DT) {
       if (k < pf) AG_ST(&R[t], __float_as_int(AG_LD(&X[t])));  // old extra cost
       AG_ST(&X[t], kInf);
     }
-    if (threadIdx.x == 0) sh.fl[0] = 0;
-    __syncthreads();
+    // flags of this frame: the other set than frame k + 1's (whose last
+    // readers may still be reading), reset before this barrier
     FixRound fx;
+    fx.base = 3 * (k & 1);
+    const int cf = 6 + (k & 1);
+    if (threadIdx.x == 0) {
+      sh.fl[fx.base] = 0;
+      sh.fl[cf] = 0;
+    }
+    __syncthreads();
     if (lat) {
       // emitting out-links of frame k (stored with frame k + 1: sources below its tokens)
-      const int tb1 = sh.fr1.tok_base;
-      for (long long i = sh.fr1.link_begin + threadIdx.x; i < sh.fr1.link_end; i += DT) {
+      const int tb1 = fk1.tok_base;
+      for (long long i = fk1.link_begin + threadIdx.x; i < fk1.link_end; i += DT) {
         const int src = LK[i].x;
         if (src >= tb1) continue;
         const float le = AG_LD(&X[LK[i].y]) + __int_as_float(LDd[i]);
@@ -1017,7 +1031,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
       // epsilon links within frame k, to a fixpoint
       do {
         fx.begin(sh);
-        for (long long i = sh.fr.link_begin + threadIdx.x; i < sh.fr.link_end; i += DT) {
+        for (long long i = fk.link_begin + threadIdx.x; i < fk.link_end; i += DT) {
           const int src = LK[i].x;
           if (src < tb) continue;
           const float le = AG_LD(&X[LK[i].y]) + __int_as_float(LDd[i]);
@@ -1029,7 +1043,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
       } while (fx.end(sh));
     } else {
       // backpointer chains: frame k + 1's kept tokens keep their frame-k sources
-      for (int t = sh.fr1.tok_base + threadIdx.x; t < sh.fr1.tok_base + sh.fr1.ntok; t += DT) {
+      for (int t = fk1.tok_base + threadIdx.x; t < fk1.tok_base + fk1.ntok; t += DT) {
         if (AG_LD(&X[t]) != 0.0f) continue;
         const int pv = AG_LD(&AR[t].x);
         if (pv >= tb && pv < te) AG_ST(&X[pv], 0.0f);
@@ -1048,15 +1062,21 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
       } while (fx.end(sh));
     }
     kmin = k;
-    if (k < pf) {  // unchanged extra costs: the frames below are unchanged too
-      if (threadIdx.x == 0) sh.fl[0] = 0;
-      __syncthreads();
+    if (k < pf) {
+      // Kaldi's delta (lattice_beam * prune_scale 0.1): when no extra cost of
+      // this frame moved by more than it, the frames below keep theirs.  A
+      // kept extra cost is never above the current one (they only grow), so
+      // it prunes less, never more.  Backpointer marks compare exactly.
+      const float delta = lat ? a.lattice_beam * 0.1f : 0.0f;
       for (int t = tb + threadIdx.x; t < te; t += DT)
-        if (AG_LD(&X[t]) != __int_as_float(AG_LD(&R[t]))) sh.fl[0] = 1;
+        if (fabsf(AG_LD(&X[t]) - __int_as_float(AG_LD(&R[t]))) > delta) sh.fl[cf] = 1;
       __syncthreads();
-      if (!sh.fl[0]) break;
+      if (!sh.fl[cf]) break;
     }
   }
+  pr.mark(16);
+  pr.count(20, F - kmin);
+  pr.count(21, 1);
   if (a.debug && a.links) prune_check(a, LF, LK, kmin, F, slot, 1, false);
   // ---- token remap over the window [wb, arena_used): R[t - wb] = number of
   // kept tokens before t (kDropped: t itself is dropped)
@@ -1094,6 +1114,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
   __syncthreads();
   for (int k = kmin + threadIdx.x; k <= F; k += DT)
     LF[k].new_ntok = (k < F ? LF[k + 1].new_base : new_end) - LF[k].new_base;
+  pr.mark(17);
   // ---- links (before the tokens move: extra costs by old index), whole
   // window; wave 0 moves the frame boundaries that fall in each chunk
   long long lout = lw;
@@ -1166,6 +1187,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
     __syncthreads();
     for (int k = kmin + threadIdx.x; k <= F; k += DT) LF[k].link_end = k < F ? LF[k + 1].link_begin : lout;
   }
+  pr.mark(18);
   // ---- move the kept tokens (and their extra costs) down, in order
   for (int c0 = wb; c0 < end; c0 += kPI * DT) {
     const int t0 = c0 + kPI * (int)threadIdx.x;
@@ -1204,6 +1226,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
     LF[k].ntok = LF[k].new_ntok;
   }
   __syncthreads();
+  pr.mark(19);
   if (a.debug && a.links) prune_check(a, LF, LK, kmin, F, slot, 2, false);
   if (a.debug && threadIdx.x == 0)
     printf("prune slot %d F %d pf %d kmin %d wb %d end %d new_end %d links %lld -> %lld\n", slot, F, pf, kmin,
@@ -1451,7 +1474,8 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   if (st.ntok == 0 && !st.err) st.err |= 4;
   // PruneActiveTokens every prune_interval frames (at the end of a launch)
   if (a.prune_interval > 0 && !st.err && st.frames - st.last_prune >= a.prune_interval) {
-    prune_segment(a, sh, st, p, slot);
+    pr.mark(10);
+    prune_segment(a, sh, st, p, slot, pr);
     __syncthreads();
     if (sh.bad) st.err |= sh.bad;
   }

@@ -302,19 +302,21 @@ class Engine:
         return dict(zip(("frames", "tok_in", "tok_out", "arcs_emit", "arcs_eps", "links"), out.tolist()))
 
     def decoder_phases(self):
-        out = np.zeros(16, np.int64)
+        out = np.zeros(len(self.PHASES), np.int64)
         _chk(_c.vamd_engine_decoder_phases(self.h, out.ctypes.data))
         return dict(zip(self.PHASES, out.tolist()))
 
     # decoder.hip Prof: s_memtime clocks per phase (slots 0-10), then counts
     PHASES = ("cutoff", "seed", "exp_tokens", "exp_items", "exp_winners", "eps", "commit_toks",
               "commit_links", "commit_eps_links", "commit_clear", "prune", "n_hbm_created",
-              "n_created", "n_eps_rounds", "n_chunks", "frames")
-    PHASE_CLOCKS = PHASES[:11]
+              "n_created", "n_eps_rounds", "n_chunks", "frames", "prune_walk", "prune_remap",
+              "prune_links", "prune_move", "n_prune_frames", "n_prunes", "-", "-")
+    PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19]  # the clock slots (the rest count)
+    PHASE_CLOCKS = PHASES[:11] + PHASES[16:20]
 
     def decoder_phases_per_stream(self):
-        """[max_streams, 16] int64: decoder_phases() per stream slot."""
-        out = np.zeros((self.max_streams, 16), np.int64)
+        """[max_streams, len(PHASES)] int64: decoder_phases() per stream slot."""
+        out = np.zeros((self.max_streams, len(self.PHASES)), np.int64)
         _chk(_c.vamd_engine_decoder_phases_per_stream(self.h, out.ctypes.data))
         return out
 
