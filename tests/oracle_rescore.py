@@ -60,7 +60,7 @@ class ConstArpa:
         return F32(np.array([i], np.int32).view(np.float32)[0])
 
     def _ustate(self, w):
-        if w < 0 or w >= len(self.uni) or self.uni[w] == 0:
+        if w < 0 or w >= len(self.uni) or self.uni[w] < 0:  # -1 = no state (Kaldi)
             return None
         return self.uni[w]
 

@@ -84,3 +84,47 @@ def test_rescoring_matches_restatement(synth_model_rescore, test_wave, secs):
     # (checked on the first alternative against the unrescored n-best)
     plain = engine.lattice_words(L, o.graph.ilabel, o.graph.olabel, 6.0, 1.0, 50)
     assert got["nbest"][0]["words"] in [x["words"] for x in plain["nbest"]] or len(plain["nbest"]) == 50
+
+
+def test_const_arpa_kaldi_layout(tmp_path):
+    """Hand-built bytes in Kaldi's ConstArpaLm::Write layout (not through
+    kaldi_formats.write_const_arpa): the first state at offset 0 and -1 for
+    words without a unigram state (<eps> here, as in every real G.carpa)."""
+    import struct
+    from vosk import engine
+    f = lambda x: struct.unpack("<i", struct.pack("<f", x))[0]  # noqa: E731
+    leaf = lambda x: f(x) & ~1  # noqa: E731
+    lp = {1: -99.0, 2: -1.5, 3: -2.25, 4: -3.5}     # <s> </s> a b
+    bo = {1: -0.5, 2: 0.0, 3: -0.75, 4: -1.25}
+    lp_ab, lp_sa, bo_sa, lp_sab = -0.625, -1.125, -0.375, -0.3125
+    st = [f(lp[1]), f(bo[1]), 1, 3, 2 * (16 - 0) + 1,     # 0: <s> -> (<s> a)
+          f(lp[2]), f(bo[2]), 0,                          # 5: </s>
+          f(lp[3]), f(bo[3]), 1, 4, leaf(lp_ab),          # 8: a -> leaf (a b)
+          f(lp[4]), f(bo[4]), 0,                          # 13: b
+          f(lp_sa), f(bo_sa), 1, 4, leaf(lp_sab)]         # 16: <s> a -> leaf (<s> a b)
+    uni = [-1, 0, 5, 8, 13]
+    b = bytearray(b"\0B")
+    tok = lambda t: b.extend(t.encode() + b" ")  # noqa: E731
+    i32 = lambda v: b.extend(b"\x04" + struct.pack("<i", v))  # noqa: E731
+    i64 = lambda v: b.extend(b"\x08" + struct.pack("<q", v))  # noqa: E731
+    tok("<ConstArpaLm>"); tok("<LmInfo>"); i32(1); i32(2); i32(-1); i32(3); tok("</LmInfo>")
+    tok("<LmStates>"); i64(len(st)); b.extend(struct.pack(f"<{len(st)}i", *st)); tok("</LmStates>")
+    tok("<LmUnigram>"); i32(len(uni))
+    for u in uni:
+        i64(u)
+    tok("</LmUnigram>"); tok("<LmOverflow>"); i32(0); tok("</LmOverflow>"); tok("</ConstArpaLm>")
+    path = str(tmp_path / "G.carpa")
+    open(path, "wb").write(bytes(b))
+    F = np.float32
+    unleaf = lambda x: F(struct.unpack("<f", struct.pack("<i", leaf(x)))[0])  # noqa: E731
+    want = {(4, (1, 3)): unleaf(lp_sab),             # trigram leaf under the offset-0 root
+            (4, (3,)): unleaf(lp_ab),
+            (3, (1,)): F(lp_sa),                       # offset-0 state's child
+            (3, (4,)): F(bo[4]) + F(lp[3]),            # backoff
+            (4, (1,)): F(bo[1]) + F(lp[4]),            # offset-0 state backs off
+            (3, (4, 4)): F(bo[4]) + F(lp[3]),          # missing history state
+            (2, ()): F(lp[2]), (1, ()): F(lp[1])}
+    lm = ORS.ConstArpa(path)
+    for (w, h), v in want.items():
+        assert lm.logprob(w, list(h)) == v, (w, h)
+        assert np.float32(engine.carpa_logprob(path, w, list(h))) == v, (w, h)

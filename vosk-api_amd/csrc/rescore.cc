@@ -89,8 +89,11 @@ void ConstArpaLm::Read(const std::string& path) {
   const int64_t nw = r.Int();
   if (nw < 0 || nw > (int64_t)1 << 31) VAMD_ERR("bad LmUnigram size in " << path);
   unigram_.resize(nw);
+  // Kaldi's ConstArpaLm::Write stores -1 for a word without a unigram state
+  // (<eps>, disambiguation symbols); offset 0 is an ordinary state
   for (auto& u : unigram_) {
     u = r.Int();
+    if (u == -1) continue;
     if (u < 0 || u + 3 > n) VAMD_ERR("bad unigram offset in " << path);
   }
   r.Expect("</LmUnigram>");
@@ -100,6 +103,7 @@ void ConstArpaLm::Read(const std::string& path) {
   overflow_.resize(no);
   for (auto& o : overflow_) {
     o = r.Int();
+    if (o == -1) continue;
     if (o < 0 || o + 3 > n) VAMD_ERR("bad overflow offset in " << path);
   }
   r.Expect("</LmOverflow>");
@@ -108,7 +112,7 @@ void ConstArpaLm::Read(const std::string& path) {
 }
 
 const int32_t* ConstArpaLm::UnigramState(int w) const {
-  if (w < 0 || w >= (int)unigram_.size() || unigram_[w] == 0) return nullptr;
+  if (w < 0 || w >= (int)unigram_.size() || unigram_[w] < 0) return nullptr;
   return states_.data() + unigram_[w];
 }
 
@@ -139,7 +143,8 @@ void ConstArpaLm::Decode(int32_t info, const int32_t* parent, const int32_t** ch
   if (off > 0) {
     *child = parent + off;
   } else {
-    if (-off >= (int32_t)overflow_.size()) VAMD_ERR("ConstArpaLm overflow index out of range");
+    if (-off >= (int32_t)overflow_.size() || overflow_[-off] < 0)
+      VAMD_ERR("ConstArpaLm overflow index out of range");
     *child = states_.data() + overflow_[-off];
   }
   *logprob = AsFloat(**child);

@@ -1078,8 +1078,9 @@ def write_const_arpa(path: str, ngrams: dict, bos: int, eos: int, unk: int, orde
     a history of a longer n-gram: [logprob][backoff][num children]
     [(word, child info)...] with children sorted by word; child info = 2 *
     (child offset - parent offset) + 1 for children with a state, else the
-    child's logprob bits with the lowest bit cleared.  A 3-int dummy state
-    at offset 0 keeps offset 0 free for "no unigram state"."""
+    child's logprob bits with the lowest bit cleared.  Words without a
+    unigram state get offset -1 (Kaldi's ConstArpaLm::Write); the first
+    state sits at offset 0."""
     kids = {}
     for ng in ngrams:
         if len(ng) > 1:
@@ -1095,7 +1096,7 @@ def write_const_arpa(path: str, ngrams: dict, bos: int, eos: int, unk: int, orde
                     nxt.append(c)
         order_states += nxt
         frontier = nxt
-    pos, p = {}, 3
+    pos, p = {}, 0
     for st in order_states:
         pos[st] = p
         p += 3 + 2 * len(kids.get(st, []))
@@ -1116,7 +1117,7 @@ def write_const_arpa(path: str, ngrams: dict, bos: int, eos: int, unk: int, orde
             else:
                 arr[q + 4 + 2 * i] = fbits(ngrams[c][0]) & ~1
     num_words = max(w for ng in ngrams for w in ng) + 1
-    uni = [pos.get((w,), 0) for w in range(num_words)]
+    uni = [pos.get((w,), -1) for w in range(num_words)]
     b = bytearray(b"\0B")
 
     def tok(t):
