@@ -1,20 +1,28 @@
 #!/usr/bin/env python3
-"""Aggregate real-time factor of the Vosk hot path on MI355X.
+"""Aggregate real-time factor of the Vosk batch path on MI355X.
 
-Workload (BASELINE.json configs[2], the largest single-GPU configuration):
-BatchRecognizer-style decoding of 256 concurrent synthetic 16 kHz streams per
-GPU through libvosk.so's GPU engine -- MFCC -> looped TDNN-F nnet3 (fp32 MFMA)
--> token-passing beam search (beam 13, max-active 7000) -- with the
-frames_per_chunk = 51 chunking of src/batch_model.cc:84-88.  A "step" is one
-engine pass that advances every stream by one 8160-sample chunk (0.51 s of
-audio); stream audio is resident in HBM before the timed region (per-step
-PCIe traffic is excluded; see DESIGN.md for the host-fed rate).
+Headline workload (BASELINE.json configs[2], the largest single-GPU
+configuration): the reference's own GPU batch harness,
+python/example/test_gpu_batch.py:25-59, through the public API -- 256
+BatchRecognizers per GPU fed 8000-byte s16le chunks from host memory, one
+feeding round over every stream, BatchModel.Wait(), Result() of every stream
+-- on 60 s streams.  libvosk.so's BatchModel runs one GPU lane per process
+here (VOSK_AMD_DEVICE = LOCAL_RANK): MFCC + online i-vectors -> looped TDNN-F
+nnet3 (fp32 MFMA) -> token passing (beam 13, max-active 7000) with lattices
+-> endpointing -> lattice MBR results on host worker threads.  A "step" is
+one feeding round (0.25 s of audio per stream); the timed region also covers
+FinishStream, the last Wait and the final results.
 
-Model: no Vosk model is available offline, so a seeded synthetic model with
-the reference recipe's TDNN-F topology (training/local/chain/run_tdnn.sh:
-98-129, random-init weights, BatchNorm calibrated on test.wav) and a 20k-word
-lexicon-tree HCLG is generated in the real Kaldi/OpenFST formats.  Streams
-are test.wav tiled, shifted, gained and noised per BASELINE.md.
+Model: no Vosk model is available offline, so a seeded synthetic model in
+the real Kaldi/OpenFST formats stands in for vosk-model-small-en-us: the
+recipe's TDNN-F topology (training/local/chain/run_tdnn.sh:98-129, random-init
+weights, BatchNorm calibrated on test.wav) with a 20 k-word lookahead graph
+(HCLr + a ~29 k-history trigram Gr, expanded at load to ~1.9 M states).
+Streams are test.wav tiled, shifted, gained and noised per BASELINE.md.
+
+Secondary keys: "engine_only" (the GPU engine stepped directly on
+HBM-resident audio, no host feeding or result production), the single-stream
+KaldiRecognizer latency (config 2) and the CPU baseline.
 
 Multi-GPU: one process per GPU (torchrun); streams are sharded by rank with
 no data-path collective ("scaling": "weak"); a barrier brackets the timed
@@ -38,6 +46,9 @@ for _p in (PKG, os.path.join(PKG, "tools"), os.path.join(REPO, "tests")):
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3   # dense fp32 MFMA peak (MI355X_MICROARCH.md)
 SR = 16000
+FEED_BYTES = 8000          # test_gpu_batch.py:33 reads 8000 bytes per stream per round
+METRIC = "aggregate real-time factor (xRT) + p50 per-chunk latency, vosk-model-small-en-us"
+PMC_PROFILE = os.path.join(REPO, "profiles", "r02_decode_pmc.json")
 
 
 def load_wave():
@@ -50,21 +61,50 @@ def stream_audio(base, i, n):
     return perturbed_stream(base, i, seconds=n / SR)
 
 
-def bench_model(rank, dist):
+def pcm(x):
+    return np.clip(np.asarray(x, np.float32), -32768, 32767).astype("<i2").tobytes()
+
+
+def bench_model(rank, dist, preset):
     import make_synth_model
-    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", "bench_v3")
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", f"bench_{preset}_v3")
     if rank == 0 and not os.path.exists(os.path.join(cache, "README")):
-        make_synth_model.make_model(cache, seed=11, vocab=20000, num_pdfs=2000)
+        tmp = cache + f".tmp{os.getpid()}"
+        make_synth_model.make_preset(preset, tmp)
+        os.rename(tmp, cache)
     if dist is not None:
         dist.barrier()
     return cache
 
 
+def cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return os.cpu_count() or 1, model
+
+
+def cpu_workers():
+    """Host cores this process may use: its affinity set, capped by the
+    box's CPU share when the environment states one (OMP_NUM_THREADS)."""
+    n = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
 def cpu_baseline(model, base, streams, seconds, workers):
-    """Oracle (single-threaded C restatement) timed on host cores: one stream
-    per worker process at a time (the transcribe_scp.py Pool pattern)."""
+    """Oracle (single-threaded C restatement: MFCC, i-vectors, nnet3, token
+    passing) timed on host cores: one stream per worker process at a time
+    (the transcribe_scp.py Pool pattern)."""
     import multiprocessing as mp
-    jobs = [(model, i, seconds) for i in range(streams)]
+    jobs = [(i, seconds) for i in range(streams)]
     ctx = mp.get_context("fork")
     with ctx.Pool(workers, initializer=_cpu_init, initargs=(model,)) as pool:
         t0 = time.time()
@@ -79,47 +119,81 @@ _ORC = {}
 
 def _cpu_init(model):
     import oracle_py
-    _ORC["m"] = oracle_py.OracleModel(model, fpc=51)  # the engine's chunking (i-vector per chunk)
+    _ORC["m"] = oracle_py.OracleModel(model, fpc=51)  # the batch chunking (i-vector per chunk)
     _ORC["base"] = load_wave()
 
 
 def _cpu_job(args):
-    model, i, seconds = args
+    i, seconds = args
     x = stream_audio(_ORC["base"], 10_000 + i, int(seconds * SR))
     t = time.time()
     _ORC["m"].recognize(x)
     return len(x) / SR, time.time() - t
 
 
+def oracle_model_dir(model):
+    """The oracle reads graph/HCLG.fst: for a lookahead model, a copy with
+    libvosk's static expansion of HCLr o Gr (the graph the GPU decodes)."""
+    if os.path.exists(os.path.join(model, "graph", "HCLG.fst")):
+        return model
+    import oracle_graph as OG
+    out = model.rstrip("/") + "_oracle_hclg"
+    if not os.path.exists(os.path.join(out, "graph", "HCLG.fst")):
+        OG.expanded_hclg_model(model, out + ".tmp")
+        os.rename(out + ".tmp", out)
+    return out
+
+
+def decoder_roofline(dec_ms, dec_launches, tot, kernel):
+    """HBM roofline of the decoder launches: algorithmic bytes (SURVEY.md 8d,
+    16*T_in + 24*E + 16*T_new + 20*L_bp + 16 per lattice link) per launch over
+    the HIP-event launch time on the decoder's stream."""
+    E = tot["arcs_emit"] + tot["arcs_eps"]
+    alg = 16 * tot["tok_in"] + 24 * E + 16 * tot["tok_out"] + 20 * tot["tok_out"] + 16 * tot.get("links", 0)
+    n = max(dec_launches, 1)
+    launch_ms = dec_ms / n
+    gbs = (alg / n) / (launch_ms * 1e-3) / 1e9 if dec_ms > 0 else 0.0
+    traffic, source = None, None
+    if os.path.exists(PMC_PROFILE):
+        try:
+            traffic = json.load(open(PMC_PROFILE)).get("hbm_bytes_per_launch")
+            source = os.path.relpath(PMC_PROFILE, REPO) + " (rocprofv3 FETCH_SIZE+WRITE_SIZE passes)"
+        except Exception:
+            traffic = None
+    return {"bound": "hbm", "kernel": kernel, "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": source,
+            "avg_launch_ms": round(launch_ms, 4), "launches": dec_launches,
+            "alg_bytes_per_launch": alg / n}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed feeding rounds (0.25 s per stream each); default: the rest of "
+                         "--stream-seconds after the warmup")
+    ap.add_argument("--warmup", type=int, default=8, help="untimed feeding rounds")
+    ap.add_argument("--stream-seconds", type=float, default=60.0)
     ap.add_argument("--streams", type=int, default=256, help="streams per GPU")
-    ap.add_argument("--model", default=None)
+    ap.add_argument("--preset", default="la_small_en_us", help="synthetic model preset")
+    ap.add_argument("--model", default=None, help="model directory (overrides --preset)")
+    ap.add_argument("--workload", choices=("api", "engine", "dynamic"), default="api",
+                    help="api (default, the headline): test_gpu_batch.py through vosk_batch_*; "
+                         "engine: the GPU engine stepped on HBM-resident audio; dynamic: "
+                         "variable-length utterances admitted per epoch across ranks")
+    ap.add_argument("--engine-steps", type=int, default=20)
+    ap.add_argument("--no-engine-line", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="decoder in order after the nnet (default: decoder of step i-1 "
-                         "concurrently with the nnet of step i on a second HIP stream)")
-    ap.add_argument("--no-lattice", action="store_true",
-                    help="decoder without lattice links (default: Kaldi forward links kept in "
-                         "HBM per stream, as the reference's batch decoder produces lattices)")
-    ap.add_argument("--workload", choices=("static", "dynamic"), default="static",
-                    help="static (default, the headline): S equal-length streams per GPU, HBM "
-                         "resident; dynamic: a node-wide queue of variable-length utterances "
-                         "admitted per epoch to the GPUs with the most free slots (one int32 "
-                         "all-gather per epoch, vosk/shard.py)")
-    ap.add_argument("--no-single-stream", action="store_true",
-                    help="skip the single-stream accept_waveform latency measurement")
-    ap.add_argument("--cpu-streams", type=int, default=64)
-    ap.add_argument("--cpu-seconds", type=float, default=300.0)
+    ap.add_argument("--no-single-stream", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--no-lattice", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline: seconds per stream")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
-    os.environ["VOSK_AMD_DEVICE"] = str(local_rank)
+    os.environ["VOSK_AMD_DEVICE"] = str(local_rank)  # one BatchModel lane (GPU) per rank
     dist = None
     if world > 1:
         import torch
@@ -130,158 +204,240 @@ def main():
         tdist.init_process_group(backend=backend)
         dist = tdist
 
-    model = args.model or bench_model(rank, dist)
+    model = args.model or bench_model(rank, dist, args.preset)
     import vosk
     from vosk import engine as ve
     vosk.SetLogLevel(-1)
     if ve.device_count() == 0:
         raise SystemExit("bench.py: no HIP device visible")
-    S = args.streams
     if args.workload == "dynamic":
-        return run_dynamic(args, model, dist, rank, world, local_rank)
+        return run_dynamic(args, model, dist, rank, world)
+    base = load_wave()
+    if args.workload == "engine":
+        out = run_engine(args, model, dist, rank, world, base, args.steps or 40)
+    else:
+        out = run_api(args, model, dist, rank, world, base)
+        if not args.no_engine_line:
+            eng = run_engine(args, model, dist, rank, world, base, args.engine_steps)
+            if eng is not None:
+                out["engine_only"] = {k: eng[k] for k in ("value", "unit", "ms_per_step", "steps",
+                                                          "stages_ms_per_step", "roofline",
+                                                          "roofline_nnet", "decoder", "config")}
+    if rank == 0 and world == 1:
+        if not args.no_single_stream:
+            out["single_stream"] = single_stream_latency(model, base)
+        if not args.no_cpu_baseline:
+            nproc, cpu_model = cpu_info()
+            workers = cpu_workers()
+            odir = oracle_model_dir(model)
+            v, a, w = cpu_baseline(odir, base, workers, args.cpu_seconds, workers)
+            out["cpu_baseline"] = {
+                "value": round(v, 3), "unit": "xRT", "cores": workers, "kind": "port",
+                "nproc": nproc, "cpu_model": cpu_model,
+                "sample": f"{workers} synthetic streams x {args.cpu_seconds:.0f} s through the C oracle "
+                          f"(MFCC + i-vectors + nnet3 + token passing on the same graph, no lattice "
+                          f"results), one stream per worker process, {workers} processes "
+                          f"(affinity/OMP share of {nproc} CPUs), {a:.0f} s audio in {w:.1f} s wall"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _max_over_ranks(dist, elapsed):
+    if dist is None:
+        return elapsed
+    import torch
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def run_api(args, model, dist, rank, world, base):
+    """test_gpu_batch.py:25-59 on S streams per GPU: feed 8000 bytes to every
+    stream, Wait(), Result() of every stream; FinishStream at the end."""
+    import vosk
+    from vosk import engine as ve
+    S = args.streams
+    W = args.warmup
+    K = args.steps if args.steps is not None else max(1, int(round(args.stream_seconds * SR * 2 / FEED_BYTES)) - W)
+    rounds = W + K
+    os.environ["VOSK_BATCH_MODEL_DIR"] = model
+    os.environ["VOSK_AMD_BATCH_TIMING"] = "1"   # HIP-event stage times on the lane's streams
+    os.environ["VOSK_AMD_BATCH_STATS"] = "1"    # decoder work counters (roofline bytes)
+    if args.no_pipeline:
+        os.environ["VOSK_AMD_BATCH_PIPELINE"] = "0"
+    datas = [pcm(stream_audio(base, rank * S + i, rounds * FEED_BYTES // 2)) for i in range(S)]
+    vosk.GpuInit()
+    bm = vosk.BatchModel()
+    recs = [vosk.BatchRecognizer(bm, SR) for _ in range(S)]
+    texts = [""] * S
+    nres = [0]
+
+    def collect():
+        for i in range(S):
+            res = recs[i].Result()
+            if res:
+                texts[i] = texts[i] + " " + json.loads(res)["text"]
+                nres[0] += 1
+
+    def feed_round(k):
+        o = k * FEED_BYTES
+        for i in range(S):
+            recs[i].AcceptWaveform(datas[i][o:o + FEED_BYTES])
+        bm.Wait()
+        collect()
+
+    for k in range(W):
+        feed_round(k)
+    for lane in range(ve.batch_lanes(bm)):
+        ve.batch_lane_stats(bm, lane, reset=True)
+    if dist is not None:
+        dist.barrier()
+    spc = 8160 * 2  # bytes per 51-frame chunk (samples_per_chunk, batch_model.cc:84-88)
+    lat = []
+    t0 = time.perf_counter()
+    for k in range(W, rounds):
+        ts = time.perf_counter()
+        feed_round(k)
+        # rounds that complete a chunk: Push -> results of the round available
+        if ((k + 1) * FEED_BYTES) // spc > (k * FEED_BYTES) // spc:
+            lat.append(time.perf_counter() - ts)
+    tf = time.perf_counter()
+    for r in recs:
+        r.FinishStream()
+    bm.Wait()
+    collect()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    elapsed = _max_over_ranks(dist, t1 - t0)
+    audio_s = K * FEED_BYTES / 2 / SR * S * world
+    st = ve.batch_lane_stats(bm, 0)
+    nonempty = sum(1 for t in texts if t.strip())
+    words = sum(len(t.split()) for t in texts)
+    del recs
+    del bm
+    if rank != 0:
+        return None
+    dec_ms, dec_n = st["stages"]["decode"]
+    nnet_ms, nnet_n = st["stages"]["nnet"]
+    front_ms, _ = st["stages"]["front"]
+    step_ms, steps = st["stages"]["step"]
+    tot = st["decoder"]
+    info = ve.plan_info(model, 51)
+    opc = 51 // 3
+    nnet_flops = tot["frames"] / opc * info["flops_per_chunk"]
+    nnet_tflops = nnet_flops / (nnet_ms * 1e-3) / 1e12 if nnet_ms else 0.0
+    lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
+    return {
+        "metric": METRIC, "value": round(audio_s / elapsed, 2), "unit": "xRT", "n_gpus": world,
+        "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic: test.wav tiled/shifted/gain/noise per BASELINE.md, s16le host buffers; "
+                "seeded random-init synthetic model (recipe TDNN-F topology, 20k-word lookahead "
+                "HCLr + trigram Gr expanded to a static graph)",
+        "config": {"workload": "config3: test_gpu_batch.py loop through vosk_batch_* (BatchModel + "
+                               "BatchRecognizer, 8000-byte feeds, Wait, Result per round), "
+                               f"{S} streams/GPU x {rounds * FEED_BYTES / 2 / SR:.0f} s, 1xMI355X per rank",
+                   "model": os.path.basename(model.rstrip("/")), "streams_per_gpu": S,
+                   "global_streams": S * world, "feed_bytes": FEED_BYTES, "chunk_samples": 8160,
+                   "frames_per_chunk": 51, "beam": 13.0, "max_active": 7000, "lattice_beam": 6.0,
+                   "parallelism": f"dp{world}",
+                   "pipeline": "lane thread: front(s) || nnet(s-1) || decoder(s-2) on 3 HIP streams "
+                               "while chunks are queued; a round with nothing behind it runs its "
+                               "stages in order; MBR results on host worker threads"},
+        "step": "one feeding round: 8000 bytes to every stream, Wait(), Result() of every stream",
+        "timed_region": "rounds W..W+K, then FinishStream + Wait + final results",
+        "p50_chunk_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),
+        "p90_chunk_latency_ms": round(float(np.percentile(lat_ms, 90)), 3),
+        "p99_chunk_latency_ms": round(float(np.percentile(lat_ms, 99)), 3),
+        "latency_definition": "wall time of a feeding round that completes a chunk: AcceptWaveform "
+                              "(Push) of every stream -> Wait() -> results collected",
+        "finish_ms": round((t1 - tf) * 1e3, 3),
+        "roofline": decoder_roofline(dec_ms, dec_n, tot, "decode_kernel"),
+        "roofline_nnet": {"bound": "mfma", "kernel": "nnet GEMM launches", "achieved": round(nnet_tflops, 4),
+                          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": nnet_tflops / FP32_PEAK_TFLOPS},
+        "gpu_ms_per_step": {"front": round(front_ms / K, 4), "nnet": round(nnet_ms / K, 4),
+                            "decode": round(dec_ms / K, 4), "engine_steps": steps},
+        "decoder": {"frames": tot["frames"],
+                    "tokens_per_frame": round(tot["tok_out"] / max(tot["frames"], 1), 1),
+                    "arcs_per_frame": round((tot["arcs_emit"] + tot["arcs_eps"]) / max(tot["frames"], 1), 1),
+                    "lattice_links_per_frame": round(tot["links"] / max(tot["frames"], 1), 1)},
+        "results": {"streams_with_text": nonempty, "words": words, "result_messages": nres[0]},
+    }
+
+
+def run_engine(args, model, dist, rank, world, base, steps):
+    """The GPU engine stepped directly: every step advances all S streams by
+    one 8160-sample chunk of HBM-resident audio (no host feeding, no result
+    production)."""
+    from vosk import engine as ve
+    S = args.streams
     pipe = not args.no_pipeline
+    warm = 5
     e = ve.Engine(model, frames_per_chunk=51, max_streams=S, stats=True, time_kernels=True,
                   pipeline=pipe, lattice=not args.no_lattice)
     chunk = e.fpc * 160
     e.set_step_samples(chunk)
-    base = load_wave()
-    total_steps = args.warmup + args.steps + 2
+    total_steps = warm + steps + 2
     streams = []
     for i in range(S):
         s = e.new_stream()
         e.preload(s, stream_audio(base, rank * S + i, total_steps * chunk), finished=False)
         streams.append(s)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    for _ in range(args.warmup):
+    for _ in range(warm):
         e.step(streams)
     e.stage_times(reset=True)
-    lat = []
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ts = time.perf_counter()
-        e.step(streams)  # synchronises the engine stream before returning
-        lat.append(time.perf_counter() - ts)
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
     if dist is not None:
-        import torch
-        dev = "cuda" if torch.cuda.is_available() else "cpu"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    audio_s = args.steps * S * chunk / SR * world
-    xrt = audio_s / elapsed
-
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        e.step(streams)
+    elapsed = _max_over_ranks(dist, time.perf_counter() - t0)
     st = e.stage_times()
     tot = e.decoder_totals()
     errs = sum(1 for s in streams if e.error(s))
-    # decoder roofline: algorithmic bytes per launch:
-    # 16*T_in + 16*E + 8*E + 16*T_new + 20*L, L = T_new backpointer links,
-    # plus 16 B per lattice link record kept in HBM
-    E = tot["arcs_emit"] + tot["arcs_eps"]
-    dec_bytes = (16 * tot["tok_in"] + 24 * E + 16 * tot["tok_out"] + 20 * tot["tok_out"]
-                 + 16 * tot.get("links", 0))
-    dec_ms, dec_n = st["decode"]
-    nnet_ms, nnet_n = st["nnet"]
-    front_ms, front_n = st["front"]
-    dec_launch_ms = dec_ms / max(dec_n, 1)
-    dec_gbs = (dec_bytes / max(dec_n, 1)) / (dec_launch_ms * 1e-3) / 1e9 if dec_n else 0.0
-    nnet_flops = e.flops_per_chunk * S * args.steps
-    nnet_tflops = nnet_flops / (nnet_ms * 1e-3) / 1e12 if nnet_ms else 0.0
-    # dominant kernel (rocprofv3 --stats: decode_kernel, one launch per step,
-    # the largest share of GPU time): HBM roofline on algorithmic bytes, with
-    # the measured HBM traffic per launch from the committed PMC summary
-    traffic = None
-    pmc_path = os.path.join(REPO, "profiles", "r01_decode_pmc.json")
-    if os.path.exists(pmc_path):
-        try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    roofline = {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(dec_gbs, 3),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dec_gbs / HBM_PEAK_GBS,
-                "traffic": traffic, "avg_launch_ms": round(dec_launch_ms, 4),
-                "alg_bytes_per_launch": dec_bytes / max(dec_n, 1)}
-    roofline_nnet = {"bound": "mfma", "kernel": "nnet GEMM launches (29 per step)",
-                     "achieved": round(nnet_tflops, 4), "peak": FP32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": nnet_tflops / FP32_PEAK_TFLOPS}
-
-    # single-stream latency (BASELINE config 2): wall time of one
-    # vosk_recognizer_accept_waveform call on a 0.25 s (8000-byte) chunk
-    # through the public API, test_simple.py's feeding pattern, 30 s of audio
-    single = None
-    if rank == 0 and world == 1 and not args.no_single_stream:
-        single = single_stream_latency(model, base)
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = min(16, os.cpu_count() or 1)
-        v, a, w = cpu_baseline(model, base, args.cpu_streams, args.cpu_seconds, workers)
-        cpu = {"value": round(v, 3), "unit": "xRT", "cores": workers, "kind": "port",
-               "sample": f"{args.cpu_streams} synthetic streams x {args.cpu_seconds:.0f} s through "
-                         f"the C oracle (MFCC + nnet3 + token passing), {workers} worker processes, "
-                         f"{a:.0f} s audio in {w:.1f} s wall"}
-
-    if rank == 0:
-        lat_ms = np.array(lat) * 1e3
-        if pipe:  # a chunk's nnet runs in one step, its decoding in the next
-            lat_ms = lat_ms[1:] + lat_ms[:-1]
-        out = {
-            "metric": "aggregate real-time factor (xRT) + p50 per-chunk latency, vosk-model-small-en-us",
-            "value": round(xrt, 2), "unit": "xRT", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic: test.wav tiled/shifted/gain/noise per BASELINE.md; seeded "
-                    "random-init synthetic model (recipe TDNN-F topology, 20k-word HCLG)",
-            "config": {"workload": "config3: BatchRecognizer-equivalent, 256 streams/GPU, "
-                                   "GPU MFCC + nnet3 + WFST beam search, 1xMI355X per rank",
-                       "streams_per_gpu": S, "global_streams": S * world,
-                       "chunk_samples": chunk, "frames_per_chunk": e.fpc,
-                       "beam": 13.0, "max_active": 7000, "parallelism": f"dp{world}",
-                       "pipeline": "decoder(step i-1) || mfcc+nnet(step i), 2 HIP streams"
-                                   if pipe else "in-order"},
-            "p50_chunk_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),
-            "p90_chunk_latency_ms": round(float(np.percentile(lat_ms, 90)), 3),
-            "p99_chunk_latency_ms": round(float(np.percentile(lat_ms, 99)), 3),
-            "roofline": roofline,
-            "roofline_nnet": roofline_nnet,
-            "stages_ms_per_step": {"front": round(front_ms / args.steps, 4),
-                                   "nnet": round(nnet_ms / args.steps, 4),
-                                   "decode": round(dec_ms / args.steps, 4),
-                                   "gpu_step": round(st["step"][0] / args.steps, 4)},
-            "nnet_tflops": round(nnet_tflops, 4),
-            "decoder": {"frames": tot["frames"],
-                        "tokens_per_frame": round(tot["tok_out"] / max(tot["frames"], 1), 1),
-                        "arcs_per_frame": round(E / max(tot["frames"], 1), 1),
-                        "lattice_links_per_frame": round(tot.get("links", 0) / max(tot["frames"], 1), 1),
-                        "stream_errors": errs},
-            "cpu_baseline": cpu,
-            "single_stream": single,
-        }
-        if os.environ.get("VOSK_AMD_DEC_PROFILE"):
-            ph = e.decoder_phases()
-            out["decoder_phase_clocks_per_frame"] = {
-                k: round(v / max(ph["frames"], 1), 1) for k, v in ph.items() if k != "frames"}
-            out["decoder_phase_clocks_per_frame"]["total"] = round(
-                sum(ph[k] for k in e.PHASE_CLOCKS) / max(ph["frames"], 1), 1)
-            # per-stream spread: the slowest stream sets each launch's time
-            per = e.decoder_phases_per_stream()[:S]
-            clk = per[:, e.PHASE_CLOCK_IDX].sum(1).astype(np.float64)
-            out["decoder_stream_clocks"] = {
-                "mean": round(float(clk.mean()), 1), "p50": round(float(np.percentile(clk, 50)), 1),
-                "p90": round(float(np.percentile(clk, 90)), 1), "max": round(float(clk.max()), 1),
-                "max_over_mean": round(float(clk.max() / max(clk.mean(), 1.0)), 3)}
-        print(json.dumps(out), flush=True)
+    flops = e.flops_per_chunk
+    phases = None
+    if os.environ.get("VOSK_AMD_DEC_PROFILE"):
+        ph = e.decoder_phases()
+        phases = {k: round(v / max(ph["frames"], 1), 1) for k, v in ph.items() if k != "frames"}
+        per = e.decoder_phases_per_stream()[:S]
+        clk = per[:, e.PHASE_CLOCK_IDX].sum(1).astype(np.float64)
+        phases["stream_clock_max_over_mean"] = round(float(clk.max() / max(clk.mean(), 1.0)), 3)
     e.close()
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    if rank != 0:
+        return None
+    dec_ms, dec_n = st["decode"]
+    nnet_ms, _ = st["nnet"]
+    front_ms, _ = st["front"]
+    nnet_tflops = flops * S * steps / (nnet_ms * 1e-3) / 1e12 if nnet_ms else 0.0
+    out = {
+        "metric": METRIC, "value": round(steps * S * chunk / SR * world / elapsed, 2), "unit": "xRT",
+        "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (HBM-resident audio), seeded random-init synthetic model",
+        "config": {"workload": "engine: GPU engine steps over HBM-resident audio (no host feeding, "
+                               "no result production)", "streams_per_gpu": S, "chunk_samples": chunk,
+                   "pipeline": "front(s) || nnet(s-1) || decoder(s-2), 3 HIP streams" if pipe else "in-order"},
+        "roofline": decoder_roofline(dec_ms, dec_n, tot, "decode_kernel"),
+        "roofline_nnet": {"bound": "mfma", "kernel": "nnet GEMM launches", "achieved": round(nnet_tflops, 4),
+                          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": nnet_tflops / FP32_PEAK_TFLOPS},
+        "stages_ms_per_step": {"front": round(front_ms / steps, 4), "nnet": round(nnet_ms / steps, 4),
+                               "decode": round(dec_ms / steps, 4),
+                               "gpu_step": round(st["step"][0] / steps, 4)},
+        "decoder": {"frames": tot["frames"],
+                    "tokens_per_frame": round(tot["tok_out"] / max(tot["frames"], 1), 1),
+                    "arcs_per_frame": round((tot["arcs_emit"] + tot["arcs_eps"]) / max(tot["frames"], 1), 1),
+                    "lattice_links_per_frame": round(tot.get("links", 0) / max(tot["frames"], 1), 1),
+                    "stream_errors": errs},
+    }
+    if phases is not None:
+        out["decoder_phase_clocks_per_frame"] = phases
+    return out
 
 
 def single_stream_latency(model, base, seconds=30.0, chunk_bytes=8000):
@@ -289,8 +445,7 @@ def single_stream_latency(model, base, seconds=30.0, chunk_bytes=8000):
     fed 8000-byte chunks; p50/p90/p99 of the accept_waveform wall time, the
     stream's real-time factor, and a final result call's time."""
     import vosk
-    x = stream_audio(base, 777, int(seconds * SR))
-    data = np.clip(x, -32768, 32767).astype("<i2").tobytes()
+    data = pcm(stream_audio(base, 777, int(seconds * SR)))
     m = vosk.Model(model)
     rec = vosk.KaldiRecognizer(m, SR)
     rec.SetWords(True)
@@ -317,15 +472,14 @@ def single_stream_latency(model, base, seconds=30.0, chunk_bytes=8000):
                      "results (MBR over the GPU lattice) included when an endpoint fires"}
 
 
-def run_dynamic(args, model, dist, rank, world, local_rank):
+def run_dynamic(args, model, dist, rank, world):
     """Variable-length utterances (5-60 s, seeded) from one node-wide queue
     (3 x streams x GPUs of them), admitted every 4 steps to the ranks with the
     most free slots; a finished stream frees its slot.  Samples are uploaded
     when a stream is admitted (inside the timed region: this mode measures
     the admission path, not the headline)."""
-    import vosk
     from vosk import engine as ve
-    from vosk.shard import AdmissionController
+    from shard import AdmissionController
     S = args.streams
     e = ve.Engine(model, frames_per_chunk=51, max_streams=S, stats=True, lattice=not args.no_lattice)
     chunk = e.fpc * 160
@@ -339,16 +493,7 @@ def run_dynamic(args, model, dist, rank, world, local_rank):
         import torch
         dev = "cuda" if torch.cuda.is_available() else "cpu"
     ctl = AdmissionController(dist, U, device=dev)
-    # the utterances' samples exist before the timed region (host memory);
-    # admission uploads them to the stream's HBM buffer
-    wav = {}
-
-    def utt(u):
-        if u not in wav:
-            wav[u] = stream_audio(base, 50_000 + u, int(lens[u]))
-        return wav[u]
-    for u in range(U):
-        utt(u)
+    wav = {u: stream_audio(base, 50_000 + u, int(lens[u])) for u in range(U)}
     free = [e.new_stream() for _ in range(S)]
     active = {}  # slot -> (utterance, expected decoder frames)
     audio = 0.0
@@ -361,7 +506,7 @@ def run_dynamic(args, model, dist, rank, world, local_rank):
             for u in ctl.admit(len(free)):
                 s = free.pop()
                 e.reset(s)
-                x = utt(u)
+                x = wav[u]
                 e.preload(s, x, finished=True)
                 frames = 1 + (len(x) - 400) // 160 if len(x) >= 400 else 0
                 active[s] = (u, (frames + 2) // 3)
@@ -382,11 +527,10 @@ def run_dynamic(args, model, dist, rank, world, local_rank):
     tot_audio = audio
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed, audio], dtype=torch.float64, device=dev)
-        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        elapsed = _max_over_ranks(dist, elapsed)
         a = torch.tensor([audio], dtype=torch.float64, device=dev)
         dist.all_reduce(a, op=dist.ReduceOp.SUM)
-        elapsed, tot_audio = float(t[0].item()), float(a.item())
+        tot_audio = float(a.item())
     if rank == 0:
         print(json.dumps({
             "metric": "aggregate real-time factor (xRT), dynamic admission",

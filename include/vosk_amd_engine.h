@@ -166,6 +166,24 @@ int vamd_engine_decoder_phases_per_stream(VamdEngine *e, long long *out);
 /* engine counters: [steps, launches, mfcc frames, chunk jobs, frames decoded] */
 int vamd_engine_counters(VamdEngine *e, long long *out5);
 
+/* ---- batch path diagnostics (the VoskBatchModel of vosk_api.h) ---- */
+struct VoskBatchModel;
+/* GPU lanes of a batch model (one engine + batcher thread per GPU) */
+int vamd_batch_lanes(struct VoskBatchModel *m);
+/* one lane: load3 = {device, streams, pending chunks}; with env
+ * VOSK_AMD_BATCH_TIMING=1 / VOSK_AMD_BATCH_STATS=1 at model creation also the
+ * lane engine's stage times (as vamd_engine_stage_times) and decoder totals
+ * (as vamd_engine_decoder_totals); reset=1 clears them.  Call while the lane
+ * is quiescent (after vosk_batch_model_wait). */
+int vamd_batch_lane_stats(struct VoskBatchModel *m, int lane, int *load3, double *ms4,
+                          long long *launches4, long long *dec6, int reset);
+/* stream -> lane index it was admitted to */
+int vamd_batch_recognizer_lane(struct VoskBatchRecognizer *r);
+/* admission policy (host only, no GPU): replays `n` admissions against lanes
+ * whose pending-chunk loads drain at the given per-admission rates; writes
+ * the lane of each admission to out[n] */
+int vamd_admission_replay(int lanes, const int *drain_per_step, int n, const int *chunks, int *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,28 @@ def synth_model_noep(synth_model):
     return path
 
 
+# endpoint rules that fire on the synthetic model (its best paths carry
+# almost no silence-phone frames): rule 1 on the final relative cost alone
+# (data-dependent positions), rule 5 after 4 s
+EP_RULES = ("--endpoint.rule1.min-trailing-silence=0\n--endpoint.rule1.max-relative-cost=12\n"
+            "--endpoint.rule5.min-utterance-length=4\n")
+
+
+@pytest.fixture(scope="session")
+def synth_model_ep(synth_model):
+    """synth_model with endpoint rules that fire every few seconds."""
+    path = os.path.join(MODEL_CACHE, f"synth_ep_{SYNTH_VERSION}")
+    if not os.path.exists(os.path.join(path, "README")):
+        tmp = path + f".tmp{os.getpid()}"
+        shutil.rmtree(tmp, ignore_errors=True)
+        shutil.copytree(synth_model, tmp)
+        with open(os.path.join(tmp, "conf", "model.conf"), "a") as f:
+            f.write(EP_RULES)
+        shutil.rmtree(path, ignore_errors=True)
+        os.rename(tmp, path)
+    return path
+
+
 @pytest.fixture(scope="session")
 def synth_model_wide(synth_model):
     """Same model with a wide beam (30) and max-active 20000: frames with

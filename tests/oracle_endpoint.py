@@ -1,0 +1,100 @@
+"""CPU restatement of endpointing and of the batch path's segmentation
+(TEST INFRASTRUCTURE ONLY).
+
+Endpoint rules: Kaldi OnlineEndpointConfig / EndpointDetected
+(online2/online-endpoint.{h,cc} [K], not vendored in the reference) as the
+reference calls it, src/recognizer.cc:318 (rules from model.conf, V1
+defaults src/model.cc:142-145); float32 arithmetic like the C++ restatement
+(vosk-api_amd/csrc/vosk_impl.cc EndpointRulesFire).
+
+Batch segmentation: BatchRecognizer (src/batch_recognizer.cc:115-181) pushes
+8160-sample chunks, the GPU pipeline decodes each chunk's ready frames and,
+with reset_on_endpoint (src/batch_model.cc:72), ends the decoder segment when
+the rules fire after a chunk; the final chunk (FinishStream) ends the last
+segment.  The chunk schedule mirrors the engine's (DecodableNnetLoopedOnline
+readiness: a chunk waits for the nnet's right context and the i-vector
+splice's).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+F32 = np.float32
+INF = F32(np.inf)
+
+# (must_contain_nonsilence, min_trailing_silence, max_relative_cost, min_utterance_length)
+DEFAULT_RULES = [(False, 5.0, np.inf, 0.0), (True, 0.5, 2.0, 0.0), (True, 1.0, 8.0, 0.0),
+                 (True, 2.0, np.inf, 0.0), (False, 0.0, np.inf, 20.0)]
+_FIELDS = ("must-contain-nonsilence", "min-trailing-silence", "max-relative-cost",
+           "min-utterance-length")
+
+
+def endpoint_config(model_conf: dict):
+    """(rules as float32 tuples, silence phone set) from conf/model.conf."""
+    rules = [list(r) for r in DEFAULT_RULES]
+    for k, v in model_conf.items():
+        if not k.startswith("endpoint.rule"):
+            continue
+        r = int(k[len("endpoint.rule")]) - 1
+        f = _FIELDS.index(k[len("endpoint.ruleN."):])
+        rules[r][f] = str(v).lower() in ("true", "1") if f == 0 else float(v)
+    sil = set(int(p) for p in str(model_conf.get("endpoint.silence-phones", "")).replace(",", ":").split(":") if p)
+    return [(bool(a), F32(b), F32(c), F32(d)) for a, b, c, d in rules], sil
+
+
+def trailing_silence(path, ilabel, tid2phone, sil):
+    """TrailingSilenceLength over the best path's emitting arcs."""
+    n = 0
+    for a in reversed(list(path)):
+        il = int(ilabel[a])
+        if il == 0:
+            continue
+        if int(tid2phone[il]) in sil:
+            n += 1
+        else:
+            break
+    return n
+
+
+def rules_fire(rules, frames, trailing_sil, shift, final_relative_cost):
+    utt = F32(frames) * F32(shift)
+    s = F32(trailing_sil) * F32(shift)
+    for must, min_sil, max_rel, min_len in rules:
+        if ((utt > s) or not must) and s >= min_sil and F32(final_relative_cost) <= max_rel and utt >= min_len:
+            return True
+    return False
+
+
+def batch_segments(oracle, wave, llh, right_context, priming, spc=8160):
+    """Decoder segments [(first frame, end frame)] of one BatchRecognizer
+    stream fed `wave` and finished; llh = the stream's log-likelihood rows
+    (whole-stream, the batch chunking)."""
+    from oracle_py import mfcc_num_frames
+    rules, sil = endpoint_config(oracle.model_conf)
+    shift = F32(F32(0.01) * F32(oracle.fss))
+    min_len = min(r[3] for r in rules)
+    fpc, fss = oracle.fpc, oracle.fss
+    opc = fpc // fss
+    ivr = oracle.ivector.m.right if oracle.ivector is not None else 0
+    N = len(wave)
+    g = oracle.graph
+    c, out_ready, seg0, segs = -priming, 0, 0, []
+    for k in range(N // spc):
+        T = mfcc_num_frames((k + 1) * spc, oracle.mfcc_conf, oracle.fbank)
+        njobs = 0
+        while njobs < priming + 2 and T >= (max(c, 0) + 1) * fpc + right_context + ivr:
+            if c >= 0:
+                out_ready += opc
+            c += 1
+            njobs += 1
+        frames = out_ready - seg0
+        if frames <= 0 or F32(frames) * shift < min_len:
+            continue
+        r = oracle.decode_llh(llh[seg0:out_ready], use_final=False)
+        ts = trailing_silence(r["path"], g.ilabel, oracle.tm.tid2phone, sil)
+        if rules_fire(rules, frames, ts, shift, r["final_relative_cost"]):
+            segs.append((seg0, out_ready))
+            seg0 = out_ready
+    T = mfcc_num_frames(N, oracle.mfcc_conf, oracle.fbank)
+    segs.append((seg0, -(-T // fss)))
+    return segs

@@ -316,3 +316,34 @@ def write_hclg_model(src_dir, out_dir, grammar=None):
     shutil.copytree(src_dir, out_dir, ignore=shutil.ignore_patterns("HCLr.fst", "Gr.fst", "disambig_tid.int"))
     kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), model_graph(src_dir, grammar))
     return out_dir
+
+
+def expanded_hclg_model(model_dir, out_dir):
+    """A copy of a lookahead model whose graph/HCLG.fst is libvosk's own
+    static expansion of HCLr o Gr (vamd_graph_*; the expansion itself is
+    checked against the Python restatement in test_lookahead_graph.py): the
+    oracle decodes the graph the engine decodes.  Returns (dir, states)."""
+    import ctypes as C
+    import shutil
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "vosk-api_amd", "vosk",
+                              "libvosk.so"))
+    lib.vamd_graph_new.restype = C.c_void_p
+    lib.vamd_graph_new.argtypes = [C.c_char_p, C.c_char_p]
+    lib.vamd_graph_dims.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]
+    lib.vamd_graph_copy.argtypes = [C.c_void_p] + [C.c_void_p] * 6
+    lib.vamd_graph_free.argtypes = [C.c_void_p]
+    h = lib.vamd_graph_new(model_dir.encode(), None)
+    assert h
+    st, na = C.c_int(), C.c_longlong()
+    S = lib.vamd_graph_dims(h, C.byref(st), C.byref(na))
+    A = na.value
+    g = kf.Fst(st.value, np.zeros(S, np.float32), np.zeros(S + 1, np.int64), np.zeros(A, np.int32),
+               np.zeros(A, np.int32), np.zeros(A, np.float32), np.zeros(A, np.int32))
+    lib.vamd_graph_copy(h, g.final.ctypes.data, g.row.ctypes.data, g.ilabel.ctypes.data,
+                        g.olabel.ctypes.data, g.weight.ctypes.data, g.nextstate.ctypes.data)
+    lib.vamd_graph_free(h)
+    if os.path.exists(out_dir):
+        shutil.rmtree(out_dir)
+    shutil.copytree(model_dir, out_dir, ignore=shutil.ignore_patterns("HCLr.fst", "Gr.fst", "disambig_tid.int"))
+    kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), g)
+    return out_dir, S

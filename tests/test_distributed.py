@@ -82,7 +82,7 @@ def test_two_rank_sharding_matches_single_process(synth_model):
 
 # ---- admission-time sharding (vosk/shard.py): one int32 all-gather per epoch
 def test_plan_admission_prefers_free_capacity():
-    from vosk.shard import plan_admission
+    from shard import plan_admission
     plan, head = plan_admission([2, 5, 0, 5], 10, 100)
     assert head == 22
     assert [len(p) for p in plan] == [2, 5, 0, 5]
@@ -94,7 +94,7 @@ def test_plan_admission_prefers_free_capacity():
 def _admission_worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from vosk.shard import AdmissionController
+    from shard import AdmissionController
     U, S = 40, 4
     ctl = AdmissionController(dist, U)
     free, active, got = S, {}, []
@@ -129,3 +129,21 @@ def test_admission_controller_gloo_world2():
     a, b = out[0], out[1]
     assert sorted(a + b) == list(range(40))
     assert len(a) > len(b)
+
+
+def test_library_admission_exactly_once_over_two_lanes():
+    """The batch path's in-library admission (BatchModel::Admit's PickLane,
+    replayed host-only over 2 virtual GPU lanes): every stream is admitted to
+    exactly one lane, loads stay balanced, and a lane that drains faster takes
+    more streams."""
+    from vosk import engine
+    rng = np.random.default_rng(5)
+    chunks = rng.integers(10, 120, size=400)
+    even = engine.admission_replay([40, 40], chunks)
+    assert len(even) == len(chunks) and set(even.tolist()) <= {0, 1}
+    assert abs(int((even == 0).sum()) - int((even == 1).sum())) <= 20
+    fast = engine.admission_replay([60, 20], chunks)
+    assert len(fast) == len(chunks)
+    assert (fast == 0).sum() > 1.5 * (fast == 1).sum()
+    # equal loads: fewest streams, then the lower index
+    assert engine.admission_replay([0, 0], [5, 5, 5, 5]).tolist() == [0, 1, 0, 1]

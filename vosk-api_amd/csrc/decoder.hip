@@ -1541,7 +1541,19 @@ __global__ __launch_bounds__(256) void traceback_kernel(TraceArgs a) {
   if (threadIdx.x == 0) {
     int n = 0;
     int* out = a.path + (long long)blockIdx.x * a.path_cap;
-    if (endpos >= 0) {
+    if (endpos >= 0 && a.arc_sil) {
+      // OnlineEndpoint TrailingSilenceLength: silence frames back from the best token
+      const int4* arena = a.arena + (long long)slot * a.arena_cap;
+      int k = st.cur_base + a.cur_pos[(long long)slot * a.max_tok + endpos];
+      while (k >= 0) {
+        const int4 e = arena[k];
+        if (e.y < 0) break;
+        const int c = a.arc_sil[e.y];
+        if (c == 2) break;
+        n += c;
+        k = e.x;
+      }
+    } else if (endpos >= 0) {
       const int4* arena = a.arena + (long long)slot * a.arena_cap;
       int k = st.cur_base + a.cur_pos[(long long)slot * a.max_tok + endpos];
       while (k >= 0) {

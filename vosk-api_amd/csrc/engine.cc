@@ -1,5 +1,7 @@
 // GPU engine (see engine.h).
 #include "engine.h"
+
+#include <sstream>
 #include "graph_compose.h"
 
 #include <algorithm>
@@ -19,6 +21,9 @@
     if (_e != hipSuccess) VAMD_ERR("HIP error " << hipGetErrorString(_e) << " at " \
                                                 << __FILE__ << ":" << __LINE__);     \
   } while (0)
+// HIP's current device is per host thread: every entry point that touches the
+// device selects the engine's (BatchModel lanes drive one engine per GPU)
+#define DEVICE_GUARD() HIPCHECK(hipSetDevice(cfg_.device))
 
 namespace vamd {
 
@@ -621,6 +626,17 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
       }
     d_sinfo_ = Upload(sinfo);
     d_arcs_ = Upload(arcs);
+    // endpoint probes: per arc epsilon / silence-phone / other (ProbeEndpoints)
+    if (!m.phone_is_silence.empty()) {
+      std::vector<unsigned char> cls(g.NumArcs());
+      for (int64_t a = 0; a < g.NumArcs(); a++) {
+        const int il = g.ilabel[a];
+        if (il == 0) { cls[a] = 0; continue; }
+        const int ph = m.tm.tid2phone[il];
+        cls[a] = ph < (int)m.phone_is_silence.size() && m.phone_is_silence[ph] ? 1 : 2;
+      }
+      d_arc_sil_ = Upload(cls);
+    }
   }
 
   // ---- decoder state
@@ -721,6 +737,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
 }
 
 Engine::~Engine() {
+  (void)hipSetDevice(cfg_.device);
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (dstream_) (void)hipStreamSynchronize(dstream_);
   if (fstream_) (void)hipStreamSynchronize(fstream_);
@@ -732,6 +749,7 @@ Engine::~Engine() {
   if (h_stage_) (void)hipHostFree(h_stage_);
   if (h_slots_) (void)hipHostFree(h_slots_);
   if (h_stats_) (void)hipHostFree(h_stats_);
+  if (h_probe_) (void)hipHostFree(h_probe_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (dstream_) (void)hipStreamDestroy(dstream_);
   if (fstream_) (void)hipStreamDestroy(fstream_);
@@ -751,13 +769,15 @@ int Engine::AllocSlot() {
 
 void Engine::FreeSlot(int slot) {
   std::lock_guard<std::mutex> lk(mu_);
-  FlushLocked();
+  DEVICE_GUARD();
+  if (SlotInFlight(slot)) FlushLocked();
   slots_.at(slot).used = false;
 }
 
 void Engine::ResetPipeline(int slot) {
   std::lock_guard<std::mutex> lk(mu_);
-  FlushLocked();
+  DEVICE_GUARD();
+  if (SlotInFlight(slot)) FlushLocked();
   SlotHost& h = slots_.at(slot);
   h.pending.clear();
   h.pending_pos = 0;
@@ -785,7 +805,8 @@ void Engine::ResetPipeline(int slot) {
 
 void Engine::ResetDecoder(int slot) {
   std::lock_guard<std::mutex> lk(mu_);
-  FlushLocked();
+  DEVICE_GUARD();
+  if (SlotInFlight(slot)) FlushLocked();
   SlotHost& h = slots_.at(slot);
   h.decoded = 0;
   h.need_reset = true;
@@ -805,6 +826,7 @@ void Engine::AcceptSamples(int slot, const float* x, int n) {
 
 void Engine::SetSampleRate(int slot, int rate) {
   std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
   SlotHost& h = slots_.at(slot);
   if (h.samples > 0 || h.raw_pushed > 0) VAMD_ERR("SetSampleRate after samples were accepted");
   const int model_rate = (int)std::lround(md_->mfcc.samp_freq);
@@ -840,6 +862,7 @@ void Engine::SetSampleRate(int slot, int rate) {
 
 void Engine::PreloadSamples(int slot, const float* x, long long n, bool finished) {
   std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
   SlotHost& h = slots_.at(slot);
   if (h.resident && h.resident_pos < h.resident_n) VAMD_ERR("previous preloaded audio not consumed");
   if (h.resident) (void)hipFree(h.resident);
@@ -867,6 +890,7 @@ int Engine::DecoderError(int slot) const { return slots_.at(slot).err; }
 
 void Engine::DecoderState(int slot, long long* o8) {
   std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
   FlushLocked();
   slots_.at(slot);
   DecSlot st;
@@ -1089,7 +1113,7 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
     if (dec_frames > 0 || h.need_reset) {
       if (dec_frames > 0 || h.samples > 0 || fin) {
         st_dec_.push_back(DecJob{s, first_real < 0 ? 0 : first_real * opc, dec_frames,
-                                 h.need_reset ? 1 : 0, stats_rows, 0, 0, 0});
+                                 h.need_reset ? 1 : 0, stats_rows, fin ? 1 : 0, 0, 0});
         stats_rows += dec_frames;
         if (h.need_reset) h.decoded = 0;
         h.need_reset = false;
@@ -1127,6 +1151,8 @@ void Engine::FinishDecodeBatch(const DecBatch& b) {
       VAMD_WARN("decoder frame count mismatch on slot " << j.slot << ": " << ds.frames << " vs "
                                                          << b.expect[i]);
     h.err = ds.err;
+    h.dev_frames = ds.frames;
+    if (cfg_.track_decoded) decoded_.push_back(DecodedJob{j.slot, j.pad0 != 0});
     if (ds.err) VAMD_WARN("decoder error flags " << ds.err << " on stream slot " << j.slot);
     counters_.frames_decoded += j.nframes;
     if (cfg_.collect_llh && j.nframes) {
@@ -1327,12 +1353,14 @@ void Engine::RunStep(bool allow_pipeline) {
 
 void Engine::Advance(const std::vector<int>& slots) {
   std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
   while (BuildStep(slots)) RunStep();
   FlushLocked();
 }
 
 void Engine::Flush() {
   std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
   FlushLocked();
 }
 
@@ -1362,25 +1390,29 @@ void Engine::FlushLocked() {
   while (pendn_active_ || pend_active_) DrainOnce();
 }
 
-bool Engine::Step(const std::vector<int>& slots) {
+bool Engine::Step(const std::vector<int>& slots, bool allow_pipeline) {
   std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
   if (!BuildStep(slots)) {
     if (!pendn_active_ && !pend_active_) return false;
     DrainOnce();  // pipeline tail: only pending nnet / decoder passes are left
     return true;
   }
-  RunStep();
+  RunStep(allow_pipeline);
   return true;
 }
 
 void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
-                       std::vector<PathResult>* out) {
+                       std::vector<PathResult>* out, bool drain) {
   std::lock_guard<std::mutex> lk(mu_);
-  FlushLocked();
+  DEVICE_GUARD();
+  if (drain) FlushLocked();
   out->assign(slots.size(), PathResult());
   if (slots.empty()) return;
+  // frames decoded on the device (equal to the host count once drained)
+  auto frames_of = [&](int s) { return drain ? slots_.at(s).decoded : slots_.at(s).dev_frames; };
   int maxf = 0;
-  for (int s : slots) maxf = std::max(maxf, slots_.at(s).decoded);
+  for (int s : slots) maxf = std::max(maxf, frames_of(s));
   int cap = 4 * maxf + 64;
   const int n = (int)slots.size();
   for (int attempt = 0; attempt < 3; attempt++) {
@@ -1396,6 +1428,7 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
     size_t o_st = o_rel + Align256(sizeof(int) * n);
     HIPCHECK(hipMemcpyAsync(d + o_req, slots.data(), sizeof(int) * n, hipMemcpyHostToDevice, stream_));
     TraceArgs t;
+    t.arc_sil = nullptr;
     t.sinfo = d_sinfo_;
     t.arena = dec_.arena;
     t.cur_state = dec_.cur_state;
@@ -1434,7 +1467,7 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
       r.final_relative_cost = ((float*)(h.data() + o_rel))[i];
       r.end_state = ((int*)(h.data() + o_st))[i];
       r.cost = (double)r.end_cost - h_slots_[slots[i]].offset_sum;
-      if (slots_.at(slots[i]).decoded == 0) r.arcs.clear();
+      if (frames_of(slots[i]) == 0) r.arcs.clear();
     }
     return;
   }
@@ -1442,28 +1475,170 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
 }
 
 void Engine::GetRawLattice(int slot, bool use_final, RawLattice* out) {
-  std::lock_guard<std::mutex> lk(mu_);
-  FlushLocked();
+  SegmentLattice sl;
+  CopySegmentLattice(slot, &sl, true);
   *out = RawLattice();
+  if (sl.frames.empty()) return;
+  BuildRawLattice(md_->graph, md_->graph.start, sl.frames, sl.arena, sl.links, use_final, out);
+  if (sl.overflow) out->overflow = true;
+}
+
+void Engine::CopySegmentLattice(int slot, SegmentLattice* out, bool drain) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
+  if (drain) FlushLocked();
+  *out = SegmentLattice();
   if (!dec_.links) return;
   DecSlot st;
   HIPCHECK(hipMemcpy(&st, d_slots_ + slot, sizeof(DecSlot), hipMemcpyDeviceToHost));
-  if (slots_.at(slot).decoded == 0 && st.frames == 0 && st.arena_used == 0) return;
+  const int host_frames = drain ? slots_.at(slot).decoded : slots_.at(slot).dev_frames;
+  if (host_frames == 0 && st.frames == 0 && st.arena_used == 0) return;
   const int nf = std::min(st.frames + 1, dec_.lat_frame_cap);
-  std::vector<LatFrame> frames(nf);
-  std::vector<int4> arena(st.arena_used);
+  out->frames.resize(nf);
+  out->arena.resize(st.arena_used);
   const long long nl = std::min(st.links_used, dec_.link_cap);
-  std::vector<int4> links(nl);
-  HIPCHECK(hipMemcpy(frames.data(), dec_.lat_frames + (size_t)slot * dec_.lat_frame_cap,
+  out->links.resize(nl);
+  HIPCHECK(hipMemcpy(out->frames.data(), dec_.lat_frames + (size_t)slot * dec_.lat_frame_cap,
                      sizeof(LatFrame) * nf, hipMemcpyDeviceToHost));
-  if (!arena.empty())
-    HIPCHECK(hipMemcpy(arena.data(), dec_.arena + (size_t)slot * dec_.arena_cap, sizeof(int4) * arena.size(),
-                       hipMemcpyDeviceToHost));
+  if (!out->arena.empty())
+    HIPCHECK(hipMemcpy(out->arena.data(), dec_.arena + (size_t)slot * dec_.arena_cap,
+                       sizeof(int4) * out->arena.size(), hipMemcpyDeviceToHost));
   if (nl > 0)
-    HIPCHECK(hipMemcpy(links.data(), dec_.links + (size_t)slot * dec_.link_cap, sizeof(int4) * nl,
+    HIPCHECK(hipMemcpy(out->links.data(), dec_.links + (size_t)slot * dec_.link_cap, sizeof(int4) * nl,
                        hipMemcpyDeviceToHost));
-  BuildRawLattice(md_->graph, md_->graph.start, frames, arena, links, use_final, out);
-  if (st.lat_ovf || st.frames + 1 > dec_.lat_frame_cap || st.err) out->overflow = true;
+  out->overflow = st.lat_ovf || st.frames + 1 > dec_.lat_frame_cap || st.err;
+}
+
+void Engine::TakeDecoded(std::vector<DecodedJob>* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  out->swap(decoded_);
+  decoded_.clear();
+}
+
+void Engine::ProbeEndpoints(const std::vector<int>& slots, std::vector<EndpointProbe>* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
+  const int n = (int)slots.size();
+  out->assign(n, EndpointProbe());
+  if (n == 0) return;
+  if (!d_arc_sil_) VAMD_ERR("endpoint probe without silence phones");
+  const int S = (int)slots_.size();
+  if (!d_probe_) {  // [req][len][final_rel][end_cost][end_state], S entries each
+    d_probe_ = (int*)DevAlloc(sizeof(int) * 5 * S);
+    HIPCHECK(hipHostMalloc((void**)&h_probe_, sizeof(int) * 5 * S, hipHostMallocDefault));
+  }
+  if (n > S) VAMD_ERR("endpoint probe over more streams than slots");
+  memcpy(h_probe_, slots.data(), sizeof(int) * n);
+  HIPCHECK(hipMemcpyAsync(d_probe_, h_probe_, sizeof(int) * n, hipMemcpyHostToDevice, stream_));
+  TraceArgs t;
+  memset(&t, 0, sizeof(t));
+  t.arc_sil = d_arc_sil_;
+  t.sinfo = d_sinfo_;
+  t.arena = dec_.arena;
+  t.cur_state = dec_.cur_state;
+  t.cur_cost = dec_.cur_cost;
+  t.cur_pos = dec_.cur_pos;
+  t.slots = d_slots_;
+  t.req_slot = d_probe_;
+  t.use_final = 0;
+  t.max_tok = dec_.max_tok;
+  t.arena_cap = dec_.arena_cap;
+  t.path_len = d_probe_ + S;
+  t.final_rel = (float*)(d_probe_ + 2 * S);
+  t.end_cost = (float*)(d_probe_ + 3 * S);
+  t.end_state = d_probe_ + 4 * S;
+  LaunchTraceback(t, n, stream_);
+  HIPCHECK(hipMemcpyAsync(h_probe_ + S, d_probe_ + S, sizeof(int) * 2 * S, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  for (int i = 0; i < n; i++) {
+    EndpointProbe& p = (*out)[i];
+    p.frames = slots_.at(slots[i]).dev_frames;
+    p.trailing_sil = h_probe_[S + i];
+    memcpy(&p.final_relative_cost, h_probe_ + 2 * S + i, 4);
+  }
+}
+
+bool Engine::SlotInFlight(int slot) const {
+  auto has = [slot](const DecBatch& b) {
+    for (const DecJob& j : b.jobs)
+      if (j.slot == slot) return true;
+    return false;
+  };
+  return (pend_active_ && has(pend_)) || (pendn_active_ && has(pendn_.dec));
+}
+
+// Whether BuildStep would stage any work for the stream (its predicates).
+bool Engine::HasRunnableWork(const SlotHost& h) const {
+  if (!h.used) return false;
+  if (h.pending_pos < h.pending.size()) return true;
+  if (h.resident && h.resident_pos < h.resident_n) return true;
+  if (h.rate != 0) {
+    const ResampleTable& T = res_tables_[h.table];
+    if (T.NumOutputSamples(h.raw_pushed, h.finished && !h.res_flushed) > h.samples) return true;
+    if (h.finished && !h.res_flushed) return true;
+  }
+  if (NumFramesFor(h.samples) > h.frames) return true;
+  const bool fin = h.finished && h.pending_pos == h.pending.size() &&
+                   (!h.resident || h.resident_pos == h.resident_n) && (h.rate == 0 || h.res_flushed);
+  const int T = h.frames, c = h.next_chunk;
+  bool ready;
+  if (fin) ready = T > 0 && (c < 0 || c * plan_.opc < (T + plan_.fss - 1) / plan_.fss);
+  else ready = T >= (std::max(c, 0) + 1) * plan_.fpc + plan_.right_context + (use_iv_ ? iv_.m.right : 0);
+  if (ready) return true;
+  // a pending decoder reset alone waits for the stream's next frames (it is
+  // folded into that job) unless the input has ended
+  return h.need_reset && fin && h.samples > 0;
+}
+
+std::string Engine::DescribeSlot(int slot) const {
+  const SlotHost& h = slots_.at(slot);
+  std::ostringstream o;
+  o << "slot " << slot << " used=" << h.used << " pending=" << h.pending.size() - h.pending_pos
+    << " samples=" << h.samples << " frames=" << h.frames << " next_chunk=" << h.next_chunk
+    << " out_ready=" << h.out_ready << " decoded=" << h.decoded << " dev=" << h.dev_frames
+    << " finished=" << h.finished << " need_reset=" << h.need_reset << " rate=" << h.rate
+    << " inflight=" << SlotInFlight(slot) << " runnable=" << HasRunnableWork(h)
+    << " nf(samples)=" << NumFramesFor(h.samples);
+  return o.str();
+}
+
+bool Engine::StreamIdle(int slot) const {
+  std::lock_guard<std::mutex> lk(const_cast<std::mutex&>(mu_));
+  return !SlotInFlight(slot) && !HasRunnableWork(slots_.at(slot));
+}
+
+void Engine::ResetDecoderAtNextJob(int slot) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
+  SlotHost& h = slots_.at(slot);
+  h.sw.Reset();
+  h.dev_frames = 0;
+  // the earliest staged decoder job of the stream: pend_ launches next
+  DecBatch* order[2] = {pend_active_ ? &pend_ : nullptr, pendn_active_ ? &pendn_.dec : nullptr};
+  for (int b = 0; b < 2; b++) {
+    if (!order[b]) continue;
+    DecBatch& db = *order[b];
+    for (size_t i = 0; i < db.jobs.size(); i++) {
+      if (db.jobs[i].slot != slot) continue;
+      db.jobs[i].reset = 1;
+      DecJob* d = (DecJob*)(d_stage_ + (size_t)db.buf * stage_bytes_ + db.o_ej) + i;
+      HIPCHECK(hipMemcpy(d, &db.jobs[i], sizeof(DecJob), hipMemcpyHostToDevice));
+      // frame counts of the new segment: this job's, then the later staged one's
+      int n = db.jobs[i].nframes;
+      db.expect[i] = n;
+      if (b == 0 && order[1])
+        for (size_t k = 0; k < order[1]->jobs.size(); k++)
+          if (order[1]->jobs[k].slot == slot) {
+            n += order[1]->jobs[k].nframes;
+            order[1]->expect[k] = n;
+          }
+      h.decoded = n;
+      h.decoded_at_build = n;
+      return;
+    }
+  }
+  h.decoded = 0;
+  h.need_reset = true;
 }
 
 int Engine::IvectorFramesReady(int slot) const {
@@ -1524,6 +1699,7 @@ void Engine::UpdateSilenceWeights(int slot, int first_decoder_frame) {
 
 void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset) {
   std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
   FlushLocked();
   SlotHost& h = slots_.at(slot);
   const int P = plan_.out_dim;
@@ -1568,6 +1744,7 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
 
 void Engine::DecoderPhaseClocks(long long* out, long long* per_slot) {
   std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
   FlushLocked();
   for (int i = 0; i < kDecProf; i++) out[i] = 0;
   std::vector<long long> h((size_t)kDecProf * slots_.size(), 0);
@@ -1580,6 +1757,7 @@ void Engine::DecoderPhaseClocks(long long* out, long long* per_slot) {
 
 void Engine::DebugFeatures(int slot, int first, int n, std::vector<float>* out) {
   std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
   const int dim = plan_.input_dim;
   std::vector<float> ring((size_t)ring_ * dim);
   float* base = nullptr;

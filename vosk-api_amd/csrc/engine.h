@@ -93,6 +93,7 @@ struct EngineConfig {
   bool lattice = false;
   long long lattice_links = 1 << 22;  // link arena per stream (16 B each)
   int lattice_frames = 1 << 14;       // frames per decoder segment with a lattice
+  bool track_decoded = false;  // record completed decoder jobs for TakeDecoded
 };
 
 // HIP-event times accumulated on the engine stream (time_kernels).
@@ -110,6 +111,21 @@ struct PathResult {
   double cost = 0;        // offset-corrected path cost
   float final_relative_cost = 0;
   int end_state = -1;
+};
+
+// A decoder segment's lattice records copied from HBM (GetRawLattice input;
+// BuildRawLattice turns them into the canonical state-level lattice).
+struct SegmentLattice {
+  std::vector<LatFrame> frames;
+  std::vector<int4> arena, links;
+  bool overflow = false;  // link arena / frame table overflow or decoder error
+};
+
+// Endpoint inputs of a stream (OnlineEndpoint [K]): decoder-segment frames,
+// trailing silence frames on the best path, final relative cost.
+struct EndpointProbe {
+  int frames = 0, trailing_sil = 0;
+  float final_relative_cost = 0;
 };
 
 struct EngineCounters {
@@ -144,7 +160,9 @@ class Engine {
   // (no host->device copy inside the steps).  finished: end of input after it.
   void PreloadSamples(int slot, const float* x, long long n, bool finished);
   // Exactly one batched step over the given streams; returns false if idle.
-  bool Step(const std::vector<int>& slots);
+  // allow_pipeline=false (pipeline mode): this step's three stages run in
+  // order after any pending pipeline stages (a batch with nothing behind it).
+  bool Step(const std::vector<int>& slots, bool allow_pipeline = true);
   void SetStepSamples(int n) { cfg_.max_step_samples = n; }
   const StageTimes& stage_times() const { return times_; }
   void ResetStageTimes() { times_ = StageTimes(); }
@@ -162,8 +180,11 @@ class Engine {
   // device decoder state of a stream: {tokens, arena tokens used, frames,
   // lattice links used, err, lattice overflow, prune_from, last prune frame}
   void DecoderState(int slot, long long* out8);
-  // Best path of the current utterance (batched over slots).
-  void BestPaths(const std::vector<int>& slots, bool use_final, std::vector<PathResult>* out);
+  // Best path of the current utterance (batched over slots).  drain=false
+  // (pipeline mode, between steps): the state as of the last completed
+  // decoder job, without running the jobs still in the pipeline.
+  void BestPaths(const std::vector<int>& slots, bool use_final, std::vector<PathResult>* out,
+                 bool drain = true);
   // Optional per-frame decoder statistics of the last Advance (collect_stats).
   const std::vector<FrameStat>& LastStats(int slot) const;
   const EngineCounters& counters() const { return counters_; }
@@ -178,6 +199,34 @@ class Engine {
   // Canonical state-level lattice of the stream's decoder segment (empty
   // without EngineConfig::lattice); use_final: final costs if any token is final.
   void GetRawLattice(int slot, bool use_final, RawLattice* out);
+  // The segment's lattice records (drain as BestPaths); empty without a lattice.
+  void CopySegmentLattice(int slot, SegmentLattice* out, bool drain = true);
+
+  // ---- asynchronous driving (BatchModel lanes: one thread steps the engine,
+  // results are produced between steps without draining the pipeline)
+  // Decoder jobs completed since the last call, in completion order;
+  // input_ended: the job was built after the stream's input had ended (its
+  // last frames; no endpoint check applies to it).
+  struct DecodedJob {
+    int slot;
+    bool input_ended;
+  };
+  void TakeDecoded(std::vector<DecodedJob>* out);
+  // Frames of the current decoder segment already decoded on the device.
+  int DeviceFramesDecoded(int slot) const { return slots_.at(slot).dev_frames; }
+  // Nothing of the stream is in the pipeline and nothing is runnable.
+  bool StreamIdle(int slot) const;
+  std::string DescribeSlot(int slot) const;  // development tracing
+  bool PipelineBusy() const { return pendn_active_ || pend_active_; }
+  // Ends the decoder segment after the frames decoded on the device so far:
+  // the stream's next decoder job not yet launched restarts the decoder (a
+  // job already staged in the pipeline gets its reset flag patched in HBM),
+  // so the segment boundary is the same as with an in-order ResetDecoder.
+  void ResetDecoderAtNextJob(int slot);
+  // Endpoint inputs of the streams as of their last completed decoder job
+  // (no drain): a traceback that stops at the first non-silence frame.
+  // Requires silence phones (model endpoint configuration).
+  void ProbeEndpoints(const std::vector<int>& slots, std::vector<EndpointProbe>* out);
   // Silence weighting of the i-vector statistics (Recognizer::UpdateSilenceWeights,
   // src/recognizer.cc:226-237): traceback of the stream's best path, weight
   // changes for the feature frames ready once the accepted samples are
@@ -206,6 +255,7 @@ class Engine {
     int out_ready = 0;       // output frames computed
     int decoded = 0;         // frames decoded since the decoder reset (incl. a pending batch)
     int decoded_at_build = 0;
+    int dev_frames = 0;      // frames of the decoder segment decoded on the device
     bool finished = false;
     bool need_reset = true;
     int err = 0;
@@ -230,6 +280,8 @@ class Engine {
     std::vector<std::pair<int, float>> iv_pending;
     SilenceWeighting sw;
   };
+  bool HasRunnableWork(const SlotHost& h) const;
+  bool SlotInFlight(int slot) const;
   struct DecBatch {  // one decoder launch's jobs, staged in one staging buffer
     std::vector<DecJob> jobs;
     std::vector<int> expect;  // decoded-frame count each job's slot must reach
@@ -269,6 +321,7 @@ class Engine {
   bool pendn_active_ = false, pend_active_ = false;
   NnetBatch pendn_;         // pipeline mode: front end done, nnet waiting
   DecBatch pend_;           // pipeline mode: nnet done, decoder waiting
+  std::vector<DecodedJob> decoded_;  // completed decoder jobs (TakeDecoded)
 
   // device: model
   MfccDev mfcc_{};
@@ -280,6 +333,9 @@ class Engine {
   RingSet rings_{};
   int4* d_sinfo_ = nullptr;
   int4* d_arcs_ = nullptr;
+  unsigned char* d_arc_sil_ = nullptr;  // per arc: 0 epsilon, 1 silence phone, 2 other
+  int* d_probe_ = nullptr;              // ProbeEndpoints buffers
+  int* h_probe_ = nullptr;
   // device: per-stream state
   float* d_samples_ = nullptr;
   float* d_raw_ = nullptr;  // [slots][raw_ring_] input-rate samples of resampled streams

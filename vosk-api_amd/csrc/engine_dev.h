@@ -224,7 +224,9 @@ struct IvArgs {
 };
 
 struct DecJob {
-  int slot, llh_row0, nframes, reset, stats_row0, pad0, pad1, pad2;
+  int slot, llh_row0, nframes, reset, stats_row0;
+  int pad0;  // host bookkeeping: 1 = built after the stream's input ended (not read by the kernel)
+  int pad1, pad2;
 };
 
 struct FrameStat {
@@ -292,6 +294,10 @@ struct TraceArgs {
   float* end_cost;       // [n] (with final cost if used)
   float* final_rel;      // [n] final relative cost
   int* end_state;        // [n]
+  // endpoint probe (optional): per arc 0 = epsilon, 1 = silence-phone
+  // emitting, 2 = other emitting; the walk stops at the first 2 and path_len
+  // counts the trailing silence frames (no path is written)
+  const unsigned char* arc_sil;
 };
 
 }  // namespace vamd

@@ -176,7 +176,9 @@ VoskBatchModel* vosk_batch_model_new() {
   API_CATCH(nullptr)
 }
 
-void vosk_batch_model_free(VoskBatchModel* model) { delete (BatchModel*)model; }
+void vosk_batch_model_free(VoskBatchModel* model) {
+  if (model) ((BatchModel*)model)->Unref();
+}
 
 void vosk_batch_model_wait(VoskBatchModel* model) {
   API_TRY
@@ -720,6 +722,56 @@ int vamd_engine_decoder_phases_per_stream(VamdEngine* e, long long* o) {
   API_TRY
   long long tot[kDecProf];
   e->eng->DecoderPhaseClocks(tot, o);
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_batch_lanes(VoskBatchModel* m) {
+  API_TRY
+  return ((BatchModel*)m)->num_lanes();
+  API_CATCH(-1)
+}
+
+int vamd_batch_lane_stats(VoskBatchModel* m, int lane, int* load3, double* ms4, long long* launches4,
+                          long long* dec6, int reset) {
+  API_TRY
+  BatchModel* bm = (BatchModel*)m;
+  const auto loads = bm->LaneLoads();
+  if (lane < 0 || lane >= (int)loads.size()) VAMD_ERR("bad lane " << lane);
+  if (load3)
+    for (int i = 0; i < 3; i++) load3[i] = loads[lane][i];
+  Engine* e = bm->lane_engine(lane);
+  const StageTimes& t = e->stage_times();
+  for (int i = 0; i < 4; i++) {
+    if (ms4) ms4[i] = t.ms[i];
+    if (launches4) launches4[i] = t.launches[i];
+  }
+  if (dec6)
+    for (int i = 0; i < 6; i++) dec6[i] = t.dec[i];
+  if (reset) e->ResetStageTimes();
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_batch_recognizer_lane(VoskBatchRecognizer* r) {
+  API_TRY
+  return ((BatchRecognizer*)r)->lane();
+  API_CATCH(-1)
+}
+
+int vamd_admission_replay(int lanes, const int* drain, int n, const int* chunks, int* out) {
+  API_TRY
+  if (lanes <= 0 || n < 0) VAMD_ERR("bad admission replay arguments");
+  // each admission adds the stream's chunks to its lane; between admissions
+  // every lane processes drain[lane] pending chunks
+  std::vector<std::array<int, 2>> loads(lanes, {0, 0});
+  for (int k = 0; k < n; k++) {
+    const int l = PickLane(loads);
+    out[k] = l;
+    loads[l][0] += chunks[k];
+    loads[l][1] += 1;
+    for (int i = 0; i < lanes; i++) loads[i][0] = std::max(0, loads[i][0] - drain[i]);
+  }
   return 0;
   API_CATCH(-1)
 }

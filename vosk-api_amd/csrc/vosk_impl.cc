@@ -2,7 +2,10 @@
 #include "vosk_impl.h"
 #include "graph_compose.h"
 
+#include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <sstream>
 
@@ -271,15 +274,12 @@ bool Recognizer::EndpointDetected() {
 // ---------------------------------------------------------------------------
 // lattice -> words (src/recognizer.cc:422-482 MbrResult, :669-729 GetResult)
 // ---------------------------------------------------------------------------
-// The decoder segment's lattice (kept on the GPU), pruned at the lattice beam
-// and determinized on words; false if unavailable (no lattice engine,
-// overflow, determinization guard).
-// Then the graph scale, and word alignment when the model has
-// word_boundary.int (WordAlignLattice, :433-434; CopyLatticeForMbr otherwise).
-static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use_final, float graph_scale,
-                               WordLattice* wl, bool rescore = false) {
-  RawLattice raw;
-  e->GetRawLattice(slot, use_final, &raw);
+// A decoder segment's raw lattice pruned at the lattice beam and determinized
+// on words; false if unusable (overflow, determinization guard).  Then the
+// graph scale, and word alignment when the model has word_boundary.int
+// (WordAlignLattice, src/recognizer.cc:433-434; CopyLatticeForMbr otherwise).
+static bool WordLatticeFromRaw(RawLattice& raw, const ModelData& m, float graph_scale, WordLattice* wl,
+                               bool rescore) {
   if (raw.overflow || raw.tok_state.empty()) return false;
   PruneRawLattice(&raw, m.dec.lattice_beam);
   LatticeOptions opt;
@@ -302,9 +302,28 @@ static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use
   return true;
 }
 
+// The decoder segment's lattice (kept on the GPU) as a word lattice.
+static bool SegmentWordLattice(Engine* e, int slot, const ModelData& m, bool use_final, float graph_scale,
+                               WordLattice* wl, bool rescore = false) {
+  RawLattice raw;
+  e->GetRawLattice(slot, use_final, &raw);
+  return WordLatticeFromRaw(raw, m, graph_scale, wl, rescore);
+}
+
+// Without a usable lattice: the best path's words, confidence 1.
+static MbrResult PathMbr(const ModelData& m, const std::vector<int>& arcs) {
+  MbrResult r;
+  for (const WordSeg& w : PathWords(m, arcs)) {
+    r.words.push_back(w.word);
+    r.conf.push_back(1.0f);
+    r.times.push_back({(float)w.start, (float)w.end});
+  }
+  return r;
+}
+
 // MBR words, confidences and frame times of the segment; graph_scale as the
 // reference applies to final results (GraphLatticeScale(0.9), :718), 1 for
-// partial results.  Without a lattice: the best path, confidence 1.
+// partial results.
 static MbrResult SegmentMbr(Engine* e, int slot, const ModelData& m, bool use_final, float graph_scale,
                             bool rescore = false) {
   MbrResult r;
@@ -315,12 +334,7 @@ static MbrResult SegmentMbr(Engine* e, int slot, const ModelData& m, bool use_fi
   }
   std::vector<PathResult> pr;
   e->BestPaths({slot}, use_final, &pr);
-  for (const WordSeg& w : PathWords(m, pr[0].arcs)) {
-    r.words.push_back(w.word);
-    r.conf.push_back(1.0f);
-    r.times.push_back({(float)w.start, (float)w.end});
-  }
-  return r;
+  return PathMbr(m, pr[0].arcs);
 }
 
 std::string Recognizer::WordsText(const std::vector<WordSeg>& w) const {
@@ -480,8 +494,86 @@ const char* Recognizer::StoreReturn(const std::string& s) {
 }
 
 // ---------------------------------------------------------------------------
+// WorkerPool
+// ---------------------------------------------------------------------------
+WorkerPool::WorkerPool(int n) {
+  for (int i = 0; i < std::max(1, n); i++) threads_.emplace_back([this] { Run(); });
+}
+
+WorkerPool::~WorkerPool() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+void WorkerPool::Submit(std::function<void()> task) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    tasks_.push_back(std::move(task));
+  }
+  cv_.notify_one();
+}
+
+void WorkerPool::WaitIdle() {
+  std::unique_lock<std::mutex> lk(mu_);
+  idle_cv_.wait(lk, [&] { return tasks_.empty() && busy_ == 0; });
+}
+
+void WorkerPool::Run() {
+  while (true) {
+    std::function<void()> t;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !tasks_.empty(); });
+      if (tasks_.empty()) return;  // stop_
+      t = std::move(tasks_.front());
+      tasks_.pop_front();
+      busy_++;
+    }
+    t();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      busy_--;
+    }
+    idle_cv_.notify_all();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // BatchModel / BatchRecognizer (src/batch_model.cc, src/batch_recognizer.cc)
 // ---------------------------------------------------------------------------
+struct BatchModel::Lane {
+  int index = 0, device = 0;
+  std::unique_ptr<Engine> engine;
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  std::vector<BatchRecognizer*> recs;     // admitted streams
+  std::vector<BatchRecognizer*> by_slot;  // engine slot -> stream
+  int queued = 0;   // chunks queued, not yet handed to the engine
+  int streams_queued = 0;  // streams with a queued chunk
+  int handed = 0;   // chunks handed to the engine, work not finished
+  int busy = 0;     // streams with work in the engine
+  int tasks = 0;    // results in production
+  bool stop = false;
+  std::thread thread;
+};
+
+// GPUs of the batch path: VOSK_AMD_DEVICE / LOCAL_RANK pin one (one process
+// per GPU deployments); otherwise every visible device (VOSK_AMD_BATCH_GPUS caps).
+static std::vector<int> BatchDevices() {
+  if (getenv("VOSK_AMD_DEVICE") || getenv("LOCAL_RANK")) return {DeviceFromEnv()};
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    VAMD_ERR("no HIP device available: the MI355X batch path requires a GPU");
+  const int cap = EnvInt("VOSK_AMD_BATCH_GPUS", n);
+  std::vector<int> d;
+  for (int i = 0; i < std::min(n, std::max(cap, 1)); i++) d.push_back(i);
+  return d;
+}
+
 BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>()) {
   md_->LoadBatchLayout(dir);
   EngineConfig cfg;
@@ -490,144 +582,364 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
   NnetPlan probe = BuildNnetPlan(nn, 51, md_->dcb.frame_subsampling_factor, md_->dcb.acoustic_scale);
   int rc = probe.right_context;
   cfg.frames_per_chunk = std::max(51, rc + 3 - rc % 3);
-  cfg.max_slots = EnvInt("VOSK_AMD_BATCH_SLOTS", 256);
-  cfg.device = DeviceFromEnv();
+  // channels per GPU: the reference's num_channels = 600 (batch_model.cc:71)
+  cfg.max_slots = EnvInt("VOSK_AMD_BATCH_SLOTS", 600);
   cfg.max_step_samples = cfg.frames_per_chunk * md_->mfcc.WindowShift() + 512;
   cfg.arena_tokens = EnvInt("VOSK_AMD_ARENA_TOKENS", 1 << 22);
   cfg.lattice = true;  // PushLattice: MBR over each segment's lattice (batch_recognizer.cc:43-107)
-  engine_.reset(new Engine(md_, cfg));
+  cfg.pipeline = EnvInt("VOSK_AMD_BATCH_PIPELINE", 1) != 0;
+  cfg.track_decoded = true;
+  cfg.time_kernels = EnvInt("VOSK_AMD_BATCH_TIMING", 0) != 0;
+  cfg.collect_stats = EnvInt("VOSK_AMD_BATCH_STATS", 0) != 0;
   samples_per_chunk_ = cfg.frames_per_chunk * md_->mfcc.WindowShift();
-  worker_ = std::thread([this] { Worker(); });
+  const std::vector<int> devs = BatchDevices();
+  for (size_t i = 0; i < devs.size(); i++) {
+    auto L = std::make_unique<Lane>();
+    L->index = (int)i;
+    L->device = devs[i];
+    EngineConfig c = cfg;
+    c.device = devs[i];
+    L->engine.reset(new Engine(md_, c));
+    L->by_slot.assign(c.max_slots, nullptr);
+    lanes_.push_back(std::move(L));
+  }
+  // result workers: VOSK_AMD_RESULT_THREADS, default one per host core up to
+  // 16 per GPU (num_worker_threads = -1: all cores)
+  int hc = (int)std::thread::hardware_concurrency();
+  int nt = EnvInt("VOSK_AMD_RESULT_THREADS", std::max(2, std::min(hc > 0 ? hc : 8, 16 * (int)lanes_.size())));
+  pool_.reset(new WorkerPool(nt));
+  for (auto& L : lanes_) {
+    Lane* l = L.get();
+    l->thread = std::thread([this, l] { LaneLoop(l); });
+  }
+  VAMD_LOG("batch model: " << lanes_.size() << " GPU lane(s), " << cfg.max_slots << " channels each, "
+                           << pool_->size() << " result workers");
 }
 
 BatchModel::~BatchModel() {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    stop_ = true;
+  for (auto& L : lanes_) {
+    {
+      std::lock_guard<std::mutex> lk(L->mu);
+      L->stop = true;
+    }
+    L->cv.notify_all();
   }
-  cv_.notify_all();
-  if (worker_.joinable()) worker_.join();
+  for (auto& L : lanes_)
+    if (L->thread.joinable()) L->thread.join();
+  pool_.reset();
 }
 
-void BatchModel::Register(BatchRecognizer* r) {
-  std::lock_guard<std::mutex> lk(mu_);
-  queues_[r];
+int PickLane(const std::vector<std::array<int, 2>>& loads) {
+  int best = -1;
+  for (int i = 0; i < (int)loads.size(); i++)
+    if (best < 0 || loads[i] < loads[best]) best = i;
+  return best;
 }
 
-void BatchModel::Unregister(BatchRecognizer* r) {
-  std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [&] { return queues_[r].empty() && in_flight_ == 0; });
-  queues_.erase(r);
+Engine* BatchModel::LaneEngine(int i) { return lanes_.at(i)->engine.get(); }
+
+int BatchModel::LaneOf(const BatchRecognizer* r) const { return r->lane_; }
+
+void BatchModel::Admit(BatchRecognizer* r, int rate) {
+  std::lock_guard<std::mutex> g(admit_mu_);
+  std::vector<std::array<int, 2>> loads;
+  for (auto& L : lanes_) {
+    std::lock_guard<std::mutex> lk(L->mu);
+    loads.push_back({L->queued + L->handed, (int)L->recs.size()});
+  }
+  // PickLane's order; a lane whose channels are all in use is skipped
+  std::vector<int> tried(lanes_.size(), 0);
+  for (size_t k = 0; k < lanes_.size(); k++) {
+    std::vector<std::array<int, 2>> avail;
+    std::vector<int> idx;
+    for (size_t i = 0; i < lanes_.size(); i++)
+      if (!tried[i]) { avail.push_back(loads[i]); idx.push_back((int)i); }
+    const int li = idx[PickLane(avail)];
+    tried[li] = 1;
+    Lane* L = lanes_[li].get();
+    int slot;
+    try {
+      slot = L->engine->AllocSlot();
+    } catch (const std::exception&) {
+      continue;  // this GPU's channels are all in use
+    }
+    try {
+      L->engine->ResetPipeline(slot);
+      L->engine->SetSampleRate(slot, rate);
+    } catch (...) {
+      L->engine->FreeSlot(slot);
+      throw;
+    }
+    std::lock_guard<std::mutex> lk(L->mu);
+    r->lane_ = L->index;
+    r->slot_ = slot;
+    L->recs.push_back(r);
+    L->by_slot[slot] = r;
+    return;
+  }
+  VAMD_ERR("all batch channels of the " << lanes_.size() << " GPU lane(s) are in use");
+}
+
+void BatchModel::Release(BatchRecognizer* r) {
+  Lane* L = lanes_.at(r->lane_).get();
+  {
+    std::unique_lock<std::mutex> lk(L->mu);
+    L->done_cv.wait(lk, [&] { return r->queue_.empty() && !r->busy_ && r->tasks_ == 0; });
+    L->recs.erase(std::remove(L->recs.begin(), L->recs.end(), r), L->recs.end());
+    L->by_slot[r->slot_] = nullptr;
+  }
+  L->engine->FreeSlot(r->slot_);
 }
 
 void BatchModel::Push(BatchRecognizer* r, std::vector<float>&& chunk, bool last) {
+  Lane* L = lanes_.at(r->lane_).get();
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    queues_[r].push_back(Chunk{std::move(chunk), last});
+    std::lock_guard<std::mutex> lk(L->mu);
+    if (r->queue_.empty()) L->streams_queued++;
+    r->queue_.push_back(BatchRecognizer::Chunk{std::move(chunk), last});
+    L->queued++;
   }
-  cv_.notify_all();
+  L->cv.notify_one();
 }
 
 int BatchModel::PendingChunks(const BatchRecognizer* r) {
-  std::lock_guard<std::mutex> lk(mu_);
-  auto it = queues_.find(const_cast<BatchRecognizer*>(r));
-  return it == queues_.end() ? 0 : (int)it->second.size();
+  Lane* L = lanes_.at(r->lane_).get();
+  std::lock_guard<std::mutex> lk(L->mu);
+  return (int)r->queue_.size() + r->handed_;
+}
+
+std::vector<std::array<int, 3>> BatchModel::LaneLoads() {
+  std::vector<std::array<int, 3>> out;
+  for (auto& L : lanes_) {
+    std::lock_guard<std::mutex> lk(L->mu);
+    out.push_back({L->device, (int)L->recs.size(), L->queued + L->handed});
+  }
+  return out;
 }
 
 void BatchModel::WaitForCompletion() {  // src/batch_model.cc:118-121
-  std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [&] {
-    if (in_flight_) return false;
-    for (auto& q : queues_)
-      if (!q.second.empty()) return false;
-    return true;
+  for (auto& L : lanes_) {
+    std::unique_lock<std::mutex> lk(L->mu);
+    L->done_cv.wait(lk, [&] { return L->queued == 0 && L->busy == 0 && L->tasks == 0; });
+  }
+}
+
+void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, const PathResult* best) {
+  Engine* e = L->engine.get();
+  const float shift = 0.01f * md_->dcb.frame_subsampling_factor;
+  const int frames = e->DeviceFramesDecoded(r->slot_);
+  auto sl = std::make_shared<SegmentLattice>();
+  if (frames > 0) e->CopySegmentLattice(r->slot_, sl.get(), false);
+  const double offset = r->segment_offset_;
+  r->segment_offset_ = final_segment ? 0.0 : r->segment_offset_ + frames * shift;
+  const uint64_t seq = r->next_seq_++;
+  std::vector<int> path = best ? best->arcs : std::vector<int>();
+  {
+    std::lock_guard<std::mutex> lk(L->mu);
+    r->tasks_++;
+    L->tasks++;
+  }
+  pool_->Submit([this, L, r, sl, seq, offset, frames, path]() {
+    const ModelData& m = *md_;
+    MbrResult res;
+    try {
+      if (frames > 0) {
+        RawLattice raw;
+        if (!sl->frames.empty())
+          BuildRawLattice(m.graph, m.graph.start, sl->frames, sl->arena, sl->links, true, &raw);
+        raw.overflow = raw.overflow || sl->overflow;
+        WordLattice wl;
+        if (WordLatticeFromRaw(raw, m, 0.9f, &wl, false)) MinimumBayesRisk(wl, &res);
+        else res = PathMbr(m, path);
+      }
+    } catch (const std::exception& ex) {
+      VAMD_WARN("batch result failed: " << ex.what());
+      res = MbrResult();
+    }
+    r->PublishResult(seq, r->FormatResult(res, offset));
+    {
+      std::lock_guard<std::mutex> lk(L->mu);
+      r->tasks_--;
+      L->tasks--;
+    }
+    L->done_cv.notify_all();
   });
 }
 
-void BatchModel::Worker() {
+void BatchModel::LaneLoop(Lane* L) {
+  Engine* e = L->engine.get();
+  (void)hipSetDevice(L->device);
   const ModelData& m = *md_;
   const float shift = 0.01f * m.dcb.frame_subsampling_factor;
+  // no endpoint rule fires before its minimum utterance length
+  float min_len = 1e30f;
+  for (const EndpointRule& rule : m.endpoint.rule) min_len = std::min(min_len, rule.min_utterance_length);
+  std::vector<BatchRecognizer*> active;  // streams with work in the engine
+  std::vector<Engine::DecodedJob> decoded;
+  std::vector<int> slots, probe;
+  std::vector<BatchRecognizer*> probe_r, ends, retire, finals;
+  std::vector<EndpointProbe> pr;
+  std::vector<PathResult> best;
+  bool pipelined = false;
+  const bool trace = EnvInt("VOSK_AMD_BATCH_TRACE", 0) != 0;  // development: one line per lane step
+  long long iter = 0;
   while (true) {
-    std::vector<std::pair<BatchRecognizer*, Chunk>> batch;
+    std::vector<std::pair<BatchRecognizer*, BatchRecognizer::Chunk>> batch;
     {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] {
-        if (stop_) return true;
-        for (auto& q : queues_)
-          if (!q.second.empty()) return true;
-        return false;
-      });
-      if (stop_) return;
-      for (auto& q : queues_)
-        if (!q.second.empty()) {
-          batch.emplace_back(q.first, std::move(q.second.front()));
-          q.second.pop_front();
+      std::unique_lock<std::mutex> lk(L->mu);
+      L->cv.wait(lk, [&] { return L->stop || L->queued > 0 || !active.empty(); });
+      if (L->stop) return;
+      // dynamic batching (CudaOnlinePipelineDynamicBatcher, batch_model.cc:94-96):
+      // with the GPU idle, wait briefly for the other streams' chunks of this
+      // feeding round (until every stream has one, no push for 250 us, or 2 ms)
+      if (L->queued > 0 && !e->PipelineBusy()) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (L->streams_queued < (int)L->recs.size() && !L->stop) {
+          const int before = L->queued;
+          L->cv.wait_for(lk, std::chrono::microseconds(250));
+          if (L->queued == before || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
         }
-      in_flight_ = 1;
+      }
+      for (BatchRecognizer* r : L->recs) {  // one chunk per stream per step
+        if (r->queue_.empty()) continue;
+        batch.emplace_back(r, std::move(r->queue_.front()));
+        r->queue_.pop_front();
+        L->queued--;
+        if (r->queue_.empty()) L->streams_queued--;
+        r->handed_++;
+        L->handed++;
+        if (!r->busy_) {
+          r->busy_ = true;
+          L->busy++;
+          active.push_back(r);
+        }
+      }
+      // pipeline the stages while a backlog keeps them fed; a batch with
+      // nothing queued behind it runs its stages in order (one sync, not three)
+      pipelined = L->queued > 0 || e->PipelineBusy();
     }
+    bool failed = false;
+    const bool tr = trace && (++iter < 300 || iter % 20000 == 0);
+    if (tr)
+      fprintf(stderr, "[lane %d] batch=%zu active=%zu queued=%d busy=%d tasks=%d pipelined=%d pipe_busy=%d\n",
+              L->index, batch.size(), active.size(), L->queued, L->busy, L->tasks, (int)pipelined,
+              (int)e->PipelineBusy());
     try {
-      std::vector<int> slots;
       for (auto& [r, c] : batch) {
-        if (!c.data.empty()) engine_->AcceptSamples(r->slot(), c.data.data(), (int)c.data.size());
-        if (c.last) engine_->InputFinished(r->slot());
-        slots.push_back(r->slot());
-      }
-      engine_->Advance(slots);
-      // endpoint (reset_on_endpoint, batch_model.cc:72) and end-of-stream results
-      std::vector<int> tb;
-      for (auto& [r, c] : batch)
-        if (engine_->NumFramesDecoded(r->slot()) > 0) tb.push_back(r->slot());
-      std::vector<PathResult> nofinal, withfinal;
-      engine_->BestPaths(tb, false, &nofinal);
-      size_t k = 0;
-      for (auto& [r, c] : batch) {
-        const int s = r->slot();
-        const int frames = engine_->NumFramesDecoded(s);
+        if (!c.data.empty()) e->AcceptSamples(r->slot_, c.data.data(), (int)c.data.size());
         if (c.last) {
-          r->PushResult(frames > 0 ? SegmentMbr(engine_.get(), s, m, true, 0.9f) : MbrResult(),
-                        r->segment_offset_);
-          if (frames > 0) k++;
-          continue;
-        }
-        if (frames == 0) continue;
-        const PathResult& p = nofinal[k++];
-        if (EndpointRulesFire(m.endpoint, frames, TrailingSilenceFrames(m, p.arcs), shift,
-                              p.final_relative_cost)) {
-          r->PushResult(SegmentMbr(engine_.get(), s, m, true, 0.9f), r->segment_offset_);
-          r->segment_offset_ += frames * shift;
-          engine_->ResetDecoder(s);
+          e->InputFinished(r->slot_);
+          r->finishing_ = true;
         }
       }
-    } catch (const std::exception& e) {
-      VAMD_WARN("batch step failed: " << e.what());
+      slots.clear();
+      for (BatchRecognizer* r : active) slots.push_back(r->slot_);
+      e->Step(slots, pipelined);
+      // reset_on_endpoint (batch_model.cc:72): streams whose decoder job just
+      // completed, checked on the device state without draining the pipeline
+      e->TakeDecoded(&decoded);
+      probe.clear();
+      probe_r.clear();
+      for (const Engine::DecodedJob& dj : decoded) {
+        const int s = dj.slot;
+        BatchRecognizer* r = L->by_slot[s];
+        // the last frames of a stream: its final segment ends when it is idle
+        if (!r || dj.input_ended) continue;
+        const int frames = e->DeviceFramesDecoded(s);
+        if (frames <= 0 || frames * shift < min_len) continue;
+        probe.push_back(s);
+        probe_r.push_back(r);
+      }
+      if (!probe.empty()) {
+        e->ProbeEndpoints(probe, &pr);
+        ends.clear();
+        std::vector<int> end_slots;
+        for (size_t i = 0; i < probe.size(); i++)
+          if (EndpointRulesFire(m.endpoint, pr[i].frames, pr[i].trailing_sil, shift, pr[i].final_relative_cost)) {
+            ends.push_back(probe_r[i]);
+            end_slots.push_back(probe[i]);
+          }
+        if (!ends.empty()) {
+          e->BestPaths(end_slots, true, &best, false);  // fallback words if a lattice is unusable
+          for (size_t i = 0; i < ends.size(); i++) {
+            EmitSegment(L, ends[i], false, &best[i]);
+            e->ResetDecoderAtNextJob(ends[i]->slot_);
+          }
+        }
+      }
+    } catch (const std::exception& ex) {
+      VAMD_WARN("batch step failed on GPU " << L->device << ": " << ex.what());
+      failed = true;
     }
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      in_flight_ = 0;
+    // streams with nothing left in the engine: their chunks are done; a
+    // finishing stream's final segment ends here (FinishStream)
+    retire.clear();
+    finals.clear();
+    for (BatchRecognizer* r : active) {
+      bool idle = failed;
+      if (!idle) {
+        try {
+          idle = e->StreamIdle(r->slot_);
+        } catch (const std::exception&) {
+          idle = true;
+        }
+      }
+      if (!idle) continue;
+      retire.push_back(r);
+      if (r->finishing_) finals.push_back(r);
     }
-    done_cv_.notify_all();
+    if (!finals.empty()) {
+      try {
+        slots.clear();
+        for (BatchRecognizer* r : finals) slots.push_back(r->slot_);
+        e->BestPaths(slots, true, &best, false);
+        for (size_t i = 0; i < finals.size(); i++) {
+          EmitSegment(L, finals[i], true, &best[i]);
+          e->ResetPipeline(finals[i]->slot_);  // a later AcceptWaveform starts a new utterance
+        }
+      } catch (const std::exception& ex) {
+        // every finished stream still gets a (empty) final result
+        VAMD_WARN("batch final results failed on GPU " << L->device << ": " << ex.what());
+        for (BatchRecognizer* r : finals) r->PublishResult(r->next_seq_++, r->FormatResult(MbrResult(), 0.0));
+      }
+    }
+    if (tr) {
+      fprintf(stderr, "[lane %d] decoded=%zu probed=%zu retire=%zu finals=%zu failed=%d\n", L->index,
+              decoded.size(), probe.size(), retire.size(), finals.size(), (int)failed);
+      for (BatchRecognizer* r : active)
+        if (std::find(retire.begin(), retire.end(), r) == retire.end()) {
+          fprintf(stderr, "  busy: %s finishing=%d\n", e->DescribeSlot(r->slot_).c_str(), (int)r->finishing_);
+          break;
+        }
+    }
+    if (!retire.empty()) {
+      {
+        std::lock_guard<std::mutex> lk(L->mu);
+        for (BatchRecognizer* r : retire) {
+          r->busy_ = false;
+          r->finishing_ = false;
+          L->busy--;
+          L->handed -= r->handed_;
+          r->handed_ = 0;
+          active.erase(std::find(active.begin(), active.end(), r));
+        }
+      }
+      L->done_cv.notify_all();
+    }
   }
 }
 
 BatchRecognizer::BatchRecognizer(BatchModel* model, float sr) : model_(model), sample_frequency_(sr) {
   // the reference resamples each call independently (flush per call,
   // src/batch_recognizer.cc:27-29,157-158); here the stream is resampled
-  // continuously (no discontinuity at call boundaries)
-  const int rate = InputRate(sr);
-  slot_ = model_->engine()->AllocSlot();
-  model_->engine()->ResetPipeline(slot_);
-  try {
-    model_->engine()->SetSampleRate(slot_, rate);
-  } catch (...) {
-    model_->engine()->FreeSlot(slot_);
-    throw;
-  }
-  model_->Register(this);
+  // continuously on the GPU (no discontinuity at call boundaries)
+  model_->Admit(this, InputRate(sr));
+  model_->Ref();
 }
 
 BatchRecognizer::~BatchRecognizer() {
-  model_->Unregister(this);
-  model_->engine()->FreeSlot(slot_);
+  model_->Release(this);
+  model_->Unref();
 }
 
 void BatchRecognizer::AcceptWaveform(const char* data, int len) {  // batch_recognizer.cc:115-181
@@ -647,10 +959,9 @@ void BatchRecognizer::FinishStream() {  // batch_recognizer.cc:37-41
   buffer_.clear();
 }
 
-void BatchRecognizer::PushResult(const MbrResult& r, double offset) {
+std::string BatchRecognizer::FormatResult(const MbrResult& r, double offset) const {
   // batch_recognizer.cc:43-107 (PushLattice: MBR words, confidences, rounded frame times)
   const ModelData& m = model_->data();
-  std::string out;
   std::stringstream text;
   for (size_t i = 0; i < r.words.size(); i++) {
     if (i) text << " ";
@@ -665,22 +976,29 @@ void BatchRecognizer::PushResult(const MbrResult& r, double offset) {
     ss << "<interpretation grammar=\"default\" confidence=\"" << confidence
        << "\">\n<input mode=\"speech\">" << text.str() << "</input>\n<instance>" << text.str()
        << "</instance>\n</interpretation>\n</result>\n";
-    out = ss.str();
-  } else {
-    Json obj;
-    for (size_t i = 0; i < r.words.size(); i++) {
-      Json word;
-      word["word"] = Json::Str(m.words.Find(r.words[i]));
-      word["start"] = Json::Float(std::round((double)r.times[i].first) * 0.03 + offset);
-      word["end"] = Json::Float(std::round((double)r.times[i].second) * 0.03 + offset);
-      word["conf"] = Json::Float(r.conf[i]);
-      obj["result"].Append(word);
-    }
-    obj["text"] = Json::Str(text.str());
-    out = obj.Dump();
+    return ss.str();
   }
+  Json obj;
+  for (size_t i = 0; i < r.words.size(); i++) {
+    Json word;
+    word["word"] = Json::Str(m.words.Find(r.words[i]));
+    word["start"] = Json::Float(std::round((double)r.times[i].first) * 0.03 + offset);
+    word["end"] = Json::Float(std::round((double)r.times[i].second) * 0.03 + offset);
+    word["conf"] = Json::Float(r.conf[i]);
+    obj["result"].Append(word);
+  }
+  obj["text"] = Json::Str(text.str());
+  return obj.Dump();
+}
+
+void BatchRecognizer::PublishResult(uint64_t seq, std::string&& json) {
   std::lock_guard<std::mutex> lk(rmu_);
-  results_.push_back(out);
+  reorder_[seq] = std::move(json);
+  for (auto it = reorder_.find(publish_seq_); it != reorder_.end(); it = reorder_.find(publish_seq_)) {
+    results_.push_back(std::move(it->second));
+    reorder_.erase(it);
+    publish_seq_++;
+  }
 }
 
 const char* BatchRecognizer::FrontResult() {

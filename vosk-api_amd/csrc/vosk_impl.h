@@ -4,7 +4,9 @@
 // src/batch_recognizer.h:28-53) and their state machines.
 #pragma once
 
+#include <array>
 #include <atomic>
+#include <functional>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -132,31 +134,82 @@ class Recognizer {
 
 class BatchRecognizer;
 
+// Admission policy of the batch path: the lane with the
+// fewest pending chunks, then the fewest streams, then the lowest index.
+// loads[i] = {pending chunks, streams}.
+int PickLane(const std::vector<std::array<int, 2>>& loads);
+
+// Host threads for the batch path's result production: segment lattice ->
+// word lattice -> MBR -> JSON, off the GPU lanes' critical path (the
+// reference runs lattice post-processing on num_worker_threads=-1 worker
+// threads, src/batch_model.cc:69, callback src/batch_recognizer.cc:138-149).
+class WorkerPool {
+ public:
+  explicit WorkerPool(int threads);
+  ~WorkerPool();
+  void Submit(std::function<void()> task);
+  void WaitIdle();
+  int size() const { return (int)threads_.size(); }
+
+ private:
+  void Run();
+  std::mutex mu_;
+  std::condition_variable cv_, idle_cv_;
+  std::deque<std::function<void()>> tasks_;
+  int busy_ = 0;
+  bool stop_ = false;
+  std::vector<std::thread> threads_;
+};
+
+// The batch path (src/batch_model.cc:23-121): one model, one GPU engine and
+// one batcher thread ("lane") per visible MI355X.  A BatchRecognizer is
+// admitted once, to the lane with the fewest pending chunks (then the fewest
+// streams), and stays there (independent streams, no data-path
+// collective).  Each lane thread steps its engine's three-stage pipeline over
+// every stream with queued chunks (one chunk per stream per step), checks
+// endpoints on the decoder state between steps without draining the
+// pipeline (reset_on_endpoint, src/batch_model.cc:72: the segment ends after
+// the frames decoded so far, exactly as an in-order reset), and hands each
+// finished segment's lattice to the result workers.
 class BatchModel {
  public:
   explicit BatchModel(const std::string& dir = "model");
-  ~BatchModel();
-  void WaitForCompletion();
-  Engine* engine() { return engine_.get(); }
+  // Refcounted like Model: vosk_batch_model_free drops the caller's
+  // reference, every BatchRecognizer holds one, so recognizers freed after
+  // their model (any binding's garbage-collection order) stay valid.
+  void Ref() { ref_.fetch_add(1); }
+  void Unref() {
+    if (ref_.fetch_sub(1) == 1) delete this;
+  }
+  void WaitForCompletion();  // src/batch_model.cc:118-121
   const ModelData& data() const { return *md_; }
   int samples_per_chunk() const { return samples_per_chunk_; }
-  void Register(BatchRecognizer* r);
-  void Unregister(BatchRecognizer* r);
+  int num_lanes() const { return (int)lanes_.size(); }
+  // Admission: picks the lane, allocates the stream slot on its engine.
+  void Admit(BatchRecognizer* r, int rate);
+  // Waits until the stream has no queued work and no result in production.
+  void Release(BatchRecognizer* r);
   void Push(BatchRecognizer* r, std::vector<float>&& chunk, bool last);
   int PendingChunks(const BatchRecognizer* r);
+  // per lane: {device, streams, pending chunks}
+  std::vector<std::array<int, 3>> LaneLoads();
+  Engine* lane_engine(int i) { return LaneEngine(i); }
+  int LaneOf(const BatchRecognizer* r) const;
 
  private:
-  void Worker();
+  struct Lane;
+  Engine* LaneEngine(int i);
+  void LaneLoop(Lane* L);
+  // A segment of stream r ends (endpoint or end of stream): lattice records
+  // copied from HBM now, MBR and JSON on the result workers.
+  void EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, const PathResult* best);
   std::shared_ptr<ModelData> md_;
-  std::unique_ptr<Engine> engine_;
   int samples_per_chunk_ = 0;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  struct Chunk { std::vector<float> data; bool last; };
-  std::map<BatchRecognizer*, std::deque<Chunk>> queues_;
-  int in_flight_ = 0;
-  bool stop_ = false;
-  std::thread worker_;
+  std::vector<std::unique_ptr<Lane>> lanes_;
+  std::unique_ptr<WorkerPool> pool_;
+  std::mutex admit_mu_;
+  std::atomic<int> ref_{1};
+  ~BatchModel();
 };
 
 class BatchRecognizer {
@@ -169,20 +222,36 @@ class BatchRecognizer {
   const char* FrontResult();
   void Pop();
   int GetNumPendingChunks() { return model_->PendingChunks(this); }
-
-  // called from the batch worker
-  int slot() const { return slot_; }
-  void PushResult(const MbrResult& r, double offset_s);
-  double segment_offset_ = 0;  // seconds at the start of the current segment
-  int frames_before_segment_ = 0;
+  int lane() const { return lane_; }
 
  private:
+  friend class BatchModel;
+  struct Chunk {
+    std::vector<float> data;
+    bool last;
+  };
+  // results are produced out of order by the worker pool and published in
+  // segment order
+  void PublishResult(uint64_t seq, std::string&& json);
+  std::string FormatResult(const MbrResult& r, double offset_s) const;  // PushLattice
+
   BatchModel* model_;
-  int slot_;
   float sample_frequency_;
   bool nlsml_ = false;
   std::vector<float> buffer_;
+  // lane state (guarded by the lane's mutex)
+  int lane_ = -1, slot_ = -1;
+  std::deque<Chunk> queue_;
+  int handed_ = 0;          // chunks given to the engine whose work is not finished
+  bool busy_ = false;       // has work in the engine
+  bool finishing_ = false;  // last chunk handed: final result when the stream is idle
+  int tasks_ = 0;           // results in production on the worker pool
+  double segment_offset_ = 0;  // seconds at the start of the current segment
+  uint64_t next_seq_ = 0;
+  // results
   std::mutex rmu_;
+  uint64_t publish_seq_ = 0;
+  std::map<uint64_t, std::string> reorder_;
   std::deque<std::string> results_;
   std::string front_;
 };

@@ -57,6 +57,10 @@ _SIGS = {
     "vamd_engine_stage_times": (C.c_int, [_vp, _vp, _vp, C.c_int]),
     "vamd_lattice_set_rescore": (C.c_int, [C.c_char_p, C.c_char_p]),
     "vamd_carpa_logprob": (C.c_float, [C.c_char_p, C.c_int, _vp, C.c_int]),
+    "vamd_batch_lanes": (C.c_int, [_vp]),
+    "vamd_batch_lane_stats": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, C.c_int]),
+    "vamd_batch_recognizer_lane": (C.c_int, [_vp]),
+    "vamd_admission_replay": (C.c_int, [C.c_int, _vp, C.c_int, _vp, _vp]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(_c, _name)
@@ -75,6 +79,42 @@ def _chk(r):
     if r is None or (isinstance(r, int) and r < 0):
         raise RuntimeError("libvosk engine error: " + _err())
     return r
+
+
+def admission_replay(drain_per_step, chunks):
+    """Host-only: the batch path's admission policy (BatchModel::Admit,
+    PickLane) replayed over len(chunks) admissions against lanes draining
+    drain_per_step[i] pending chunks between admissions; returns the lane of
+    each admission."""
+    d = np.ascontiguousarray(drain_per_step, np.int32)
+    c = np.ascontiguousarray(chunks, np.int32)
+    out = np.zeros(len(c), np.int32)
+    _chk(_c.vamd_admission_replay(len(d), d.ctypes.data, len(c), c.ctypes.data, out.ctypes.data))
+    return out
+
+
+def batch_lanes(model):
+    """Number of GPU lanes of a vosk.BatchModel."""
+    return _chk(_c.vamd_batch_lanes(model._handle))
+
+
+def batch_lane_stats(model, lane, reset=False):
+    """{device, streams, pending, stage ms / launches, decoder totals} of one lane."""
+    ld = np.zeros(3, np.int32)
+    ms = np.zeros(4, np.float64)
+    ln = np.zeros(4, np.int64)
+    dec = np.zeros(6, np.int64)
+    _chk(_c.vamd_batch_lane_stats(model._handle, lane, ld.ctypes.data, ms.ctypes.data, ln.ctypes.data,
+                                  dec.ctypes.data, 1 if reset else 0))
+    names = ("front", "nnet", "decode", "step")
+    return {"device": int(ld[0]), "streams": int(ld[1]), "pending": int(ld[2]),
+            "stages": {k: (float(ms[i]), int(ln[i])) for i, k in enumerate(names)},
+            "decoder": dict(zip(("frames", "tok_in", "tok_out", "arcs_emit", "arcs_eps", "links"),
+                                (int(x) for x in dec)))}
+
+
+def batch_recognizer_lane(rec):
+    return _chk(_c.vamd_batch_recognizer_lane(rec._handle))
 
 
 def lattice_words(L, arc_ilabel, arc_olabel, lattice_beam=6.0, graph_scale=0.9, nbest=5, align=None):
