@@ -1155,6 +1155,301 @@ int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const or
 }
 
 /* ===================================================================== */
+/* Kaldi-sequential token passing (TEST INFRASTRUCTURE: quantifies the    */
+/* order-independent formulation above against the decoder as Kaldi runs  */
+/* it).  Restates LatticeFasterDecoderTpl (decoder/lattice-faster-        */
+/* decoder.cc [K], shared by the LatticeIncrementalDecoder the reference  */
+/* uses, src/recognizer.cc:39-43) operation for operation:                */
+/*  - toks_ is a HashList<StateId, Token*> (util/hash-list-inl.h): its    */
+/*    list order is by bucket (state % hash_size) in order of the bucket's */
+/*    first occupancy, then insertion order within a bucket; hash_size    */
+/*    starts at 1000 and grows to tok_cnt * hash_ratio (PossiblyResizeHash)*/
+/*  - GetCutoff: the first minimum in list order is best_elem; nth_element */
+/*    for max_active / min_active                                          */
+/*  - ProcessEmitting: seed from best_elem's arcs, then every token in    */
+/*    list order with cost <= cutoff, its emitting arcs in graph order,   */
+/*    skipping tot >= next_cutoff and tightening next_cutoff as it goes   */
+/*    (FindOrAddToken keeps the minimum)                                  */
+/*  - ProcessNonemitting: queue = list order of states with epsilon arcs, */
+/*    LIFO (pop_back), cost >= cutoff skipped, improved states re-queued  */
+/* Backpointers: the (source token, arc) of a token's last improvement.  */
+/* ===================================================================== */
+typedef struct {
+  int* where;       /* per state: element index in the frame being built, -1 */
+  int* st; float* cost; int* bp; int* arc; int* bucket; int n, cap;
+  int* bucket_rank; /* per bucket: first-occupancy rank in this frame, -1 */
+  int nranks;
+  size_t hash_size, bucket_cap;
+} khash;
+
+static void kh_reserve(khash* h, int n) {
+  if (n <= h->cap) return;
+  while (h->cap < n) h->cap *= 2;
+  h->st = (int*)realloc(h->st, sizeof(int) * h->cap);
+  h->cost = (float*)realloc(h->cost, sizeof(float) * h->cap);
+  h->bp = (int*)realloc(h->bp, sizeof(int) * h->cap);
+  h->arc = (int*)realloc(h->arc, sizeof(int) * h->cap);
+  h->bucket = (int*)realloc(h->bucket, sizeof(int) * h->cap);
+}
+
+static void kh_set_size(khash* h, size_t size) {  /* HashList::SetSize (list empty) */
+  h->hash_size = size;
+  if (size > h->bucket_cap) {
+    h->bucket_rank = (int*)realloc(h->bucket_rank, sizeof(int) * size);
+    for (size_t b = h->bucket_cap; b < size; b++) h->bucket_rank[b] = -1;
+    h->bucket_cap = size;
+  }
+}
+
+static void kh_clear(khash* h) {
+  for (int i = 0; i < h->n; i++) { h->where[h->st[i]] = -1; h->bucket_rank[h->bucket[i]] = -1; }
+  h->n = 0;
+  h->nranks = 0;
+}
+
+/* FindOrAddToken: returns the element; *changed = created or improved */
+static int kh_find_or_add(khash* h, int s, float tot, int bp, int arc, int* changed) {
+  int e = h->where[s];
+  if (e < 0) {
+    kh_reserve(h, h->n + 1);
+    e = h->n++;
+    h->where[s] = e;
+    h->st[e] = s; h->cost[e] = tot; h->bp[e] = bp; h->arc[e] = arc;
+    int b = (int)((size_t)s % h->hash_size);
+    h->bucket[e] = b;
+    if (h->bucket_rank[b] < 0) h->bucket_rank[b] = h->nranks++;
+    *changed = 1;
+    return e;
+  }
+  if (h->cost[e] > tot) { h->cost[e] = tot; h->bp[e] = bp; h->arc[e] = arc; *changed = 1; }
+  else *changed = 0;
+  return e;
+}
+
+/* list order: elements by their bucket's first-occupancy rank, then insertion */
+static void kh_order(const khash* h, int* order, int* cnt) {
+  for (int r = 0; r <= h->nranks; r++) cnt[r] = 0;
+  for (int i = 0; i < h->n; i++) cnt[h->bucket_rank[h->bucket[i]] + 1]++;
+  for (int r = 0; r < h->nranks; r++) cnt[r + 1] += cnt[r];
+  for (int i = 0; i < h->n; i++) order[cnt[h->bucket_rank[h->bucket[i]]]++] = i;
+}
+
+static int cmp_float_nth(const void* a, const void* b) { return cmp_float(a, b); }
+
+int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, const orc_dec_opts* o,
+                     int use_final, orc_dec_result* r) {
+  const int S = g->num_states;
+  khash h;
+  memset(&h, 0, sizeof(h));
+  h.where = (int*)malloc(sizeof(int) * S);
+  for (int s = 0; s < S; s++) h.where[s] = -1;
+  h.cap = 1024;
+  h.st = (int*)malloc(sizeof(int) * h.cap); h.cost = (float*)malloc(sizeof(float) * h.cap);
+  h.bp = (int*)malloc(sizeof(int) * h.cap); h.arc = (int*)malloc(sizeof(int) * h.cap);
+  h.bucket = (int*)malloc(sizeof(int) * h.cap);
+  kh_set_size(&h, 1000);  /* the decoder's constructor: toks_.SetSize(1000) */
+  /* arena of committed tokens: backpointer (arena index) and arc */
+  int acap = 1 << 16, narena = 0;
+  int* a_prev = (int*)malloc(sizeof(int) * acap);
+  int* a_arc = (int*)malloc(sizeof(int) * acap);
+  int* cur_state = NULL; float* cur_cost = NULL; int* cur_idx = NULL; int ccap = 0, ncur = 0;
+  int* order = NULL; int* cnt = NULL; int ocap = 0;
+  float* tmp = NULL; int tcap = 0;
+  int* queue = NULL; int qcap = 0;
+  double offsets_sum = 0.0;
+  const float hash_ratio = 2.0f;
+
+#define ENSURE(ptr, capv, need, type) do { if ((need) > (capv)) { capv = (need) * 2; ptr = (type*)realloc(ptr, sizeof(type) * (capv)); } } while (0)
+  /* commit the frame being built: list order becomes the current token order */
+#define COMMIT_FRAME() do {                                                        \
+    int n_ = h.n;                                                                  \
+    if (n_ + 1 > ocap) { ocap = 2 * (n_ + 1); order = (int*)realloc(order, sizeof(int) * ocap); } \
+    cnt = (int*)realloc(cnt, sizeof(int) * (h.nranks + 2));                        \
+    kh_order(&h, order, cnt);                                                      \
+    if (n_ > ccap) { ccap = 2 * n_; cur_state = (int*)realloc(cur_state, sizeof(int) * ccap); \
+      cur_cost = (float*)realloc(cur_cost, sizeof(float) * ccap); cur_idx = (int*)realloc(cur_idx, sizeof(int) * ccap); } \
+    for (int q_ = 0; q_ < n_; q_++) {                                              \
+      const int e_ = order[q_];                                                    \
+      if (narena == acap) { acap *= 2; a_prev = (int*)realloc(a_prev, sizeof(int) * acap); a_arc = (int*)realloc(a_arc, sizeof(int) * acap); } \
+      a_prev[narena] = h.bp[e_]; a_arc[narena] = h.arc[e_];                        \
+      cur_state[q_] = h.st[e_]; cur_cost[q_] = h.cost[e_]; cur_idx[q_] = narena++; \
+    }                                                                              \
+    ncur = n_;                                                                     \
+    kh_clear(&h);                                                                  \
+  } while (0)
+
+  /* ProcessNonemitting over the frame being built (elements in list order) */
+#define NONEMITTING(cutoff_) do {                                                  \
+    int n0_ = h.n;                                                                 \
+    if (n0_ + 1 > ocap) { ocap = 2 * (n0_ + 1); order = (int*)realloc(order, sizeof(int) * ocap); } \
+    cnt = (int*)realloc(cnt, sizeof(int) * (h.nranks + 2));                        \
+    kh_order(&h, order, cnt);                                                      \
+    int qn_ = 0;                                                                   \
+    for (int q_ = 0; q_ < n0_; q_++) {                                             \
+      const int s_ = h.st[order[q_]];                                              \
+      if (g->eps_begin[s_] < g->arc_begin[s_ + 1]) { ENSURE(queue, qcap, qn_ + 1, int); queue[qn_++] = s_; } \
+    }                                                                              \
+    while (qn_ > 0) {                                                              \
+      const int s_ = queue[--qn_];                                                 \
+      const int e_ = h.where[s_];                                                  \
+      const float cc_ = h.cost[e_];                                                \
+      if (cc_ >= (cutoff_)) continue;                                              \
+      const int src_ = -2 - e_; /* source: element e_ of this frame (resolved at commit) */ \
+      for (int64_t a_ = g->eps_begin[s_]; a_ < g->arc_begin[s_ + 1]; a_++) {       \
+        const float tot_ = cc_ + g->weight[a_];                                    \
+        if (tot_ < (cutoff_)) {                                                    \
+          int ch_;                                                                 \
+          const int d_ = g->nextstate[a_];                                         \
+          kh_find_or_add(&h, d_, tot_, src_, (int)a_, &ch_);                       \
+          if (ch_ && g->eps_begin[d_] < g->arc_begin[d_ + 1]) { ENSURE(queue, qcap, qn_ + 1, int); queue[qn_++] = d_; } \
+        }                                                                          \
+      }                                                                            \
+    }                                                                              \
+  } while (0)
+
+  /* epsilon sources inside the frame being built are recorded as -2 - element;
+     resolved to arena indices at commit (the element's arena slot) */
+#define RESOLVE_EPS_BP(base_) do {                                                 \
+    for (int q_ = 0; q_ < ncur; q_++) {                                            \
+      const int ai_ = cur_idx[q_];                                                 \
+      if (a_prev[ai_] <= -2) a_prev[ai_] = (base_) + elem_pos[-2 - a_prev[ai_]];   \
+    }                                                                              \
+  } while (0)
+
+  int* elem_pos = NULL; int epcap = 0;
+  /* InitDecoding */
+  {
+    int ch;
+    kh_find_or_add(&h, g->start, 0.0f, -1, -1, &ch);
+    NONEMITTING(o->beam);
+    ENSURE(elem_pos, epcap, h.n + 1, int);
+    int n_ = h.n;
+    { /* element -> position in list order */
+      int* ord = (int*)malloc(sizeof(int) * (n_ + 1)); int* c2 = (int*)malloc(sizeof(int) * (h.nranks + 2));
+      kh_order(&h, ord, c2);
+      for (int q = 0; q < n_; q++) elem_pos[ord[q]] = q;
+      free(ord); free(c2);
+    }
+    int base = narena;
+    COMMIT_FRAME();
+    RESOLVE_EPS_BP(base);
+  }
+  if (r->ntok) r->ntok[0] = ncur;
+  if (r->best) { float b = INFINITY; for (int i = 0; i < ncur; i++) if (cur_cost[i] < b) b = cur_cost[i]; r->best[0] = b; }
+
+  for (int f = 0; f < F; f++) {
+    const float* L = llh + (size_t)f * stride;
+    if (ncur == 0) break;
+    /* ---- GetCutoff: best_elem = first minimum in list order */
+    float best = INFINITY; int best_i = -1;
+    for (int i = 0; i < ncur; i++) if (cur_cost[i] < best) { best = cur_cost[i]; best_i = i; }
+    float beam_cutoff = best + o->beam, adaptive, cutoff;
+    float max_cut = INFINITY, min_cut = INFINITY;
+    ENSURE(tmp, tcap, ncur + 1, float);
+    memcpy(tmp, cur_cost, sizeof(float) * ncur);
+    if (ncur > o->max_active) { qsort(tmp, ncur, sizeof(float), cmp_float_nth); max_cut = tmp[o->max_active]; }
+    if (max_cut < beam_cutoff) { adaptive = max_cut - best + o->beam_delta; cutoff = max_cut; }
+    else {
+      if (ncur > o->min_active) {
+        if (o->min_active == 0) min_cut = best;
+        else {
+          if (!(ncur > o->max_active)) qsort(tmp, ncur, sizeof(float), cmp_float_nth);
+          min_cut = tmp[o->min_active];
+        }
+      }
+      if (min_cut > beam_cutoff) { adaptive = min_cut - best + o->beam_delta; cutoff = min_cut; }
+      else { adaptive = o->beam; cutoff = beam_cutoff; }
+    }
+    /* PossiblyResizeHash(tok_cnt) on the emptied hash */
+    {
+      size_t nsz = (size_t)((float)ncur * hash_ratio);
+      if (nsz > h.hash_size) kh_set_size(&h, nsz);
+    }
+    /* ---- ProcessEmitting */
+    float next_cutoff = INFINITY;
+    float cost_offset = -best;
+    {
+      int s = cur_state[best_i];
+      for (int64_t a = g->arc_begin[s]; a < g->eps_begin[s]; a++) {
+        float nw = ((g->weight[a] + cost_offset) - L[g->tid2pdf[g->ilabel[a]]]) + best;
+        if (nw + adaptive < next_cutoff) next_cutoff = nw + adaptive;
+      }
+    }
+    int64_t examined = 0;
+    for (int i = 0; i < ncur; i++) {
+      if (!(cur_cost[i] <= cutoff)) continue;
+      int s = cur_state[i];
+      for (int64_t a = g->arc_begin[s]; a < g->eps_begin[s]; a++) {
+        float ac = cost_offset - L[g->tid2pdf[g->ilabel[a]]];
+        float tot = (cur_cost[i] + ac) + g->weight[a];
+        examined++;
+        if (tot >= next_cutoff) continue;
+        if (tot + adaptive < next_cutoff) next_cutoff = tot + adaptive;
+        int ch;
+        kh_find_or_add(&h, g->nextstate[a], tot, cur_idx[i], (int)a, &ch);
+      }
+    }
+    /* ---- ProcessNonemitting(next_cutoff) */
+    NONEMITTING(next_cutoff);
+    ENSURE(elem_pos, epcap, h.n + 1, int);
+    {
+      int n_ = h.n;
+      int* ord = (int*)malloc(sizeof(int) * (n_ + 1)); int* c2 = (int*)malloc(sizeof(int) * (h.nranks + 2));
+      kh_order(&h, ord, c2);
+      for (int q = 0; q < n_; q++) elem_pos[ord[q]] = q;
+      free(ord); free(c2);
+    }
+    int base = narena;
+    COMMIT_FRAME();
+    RESOLVE_EPS_BP(base);
+    offsets_sum += cost_offset;
+    if (r->ntok) r->ntok[f + 1] = ncur;
+    if (r->cutoff) r->cutoff[f] = cutoff;
+    if (r->next_cutoff) r->next_cutoff[f] = next_cutoff;
+    if (r->arcs_emit) r->arcs_emit[f] = examined;
+    if (r->best) { float b = INFINITY; for (int i = 0; i < ncur; i++) if (cur_cost[i] < b) b = cur_cost[i]; r->best[f + 1] = b; }
+  }
+#undef ENSURE
+#undef COMMIT_FRAME
+#undef NONEMITTING
+#undef RESOLVE_EPS_BP
+
+  /* best path end: with final costs if any token is final (first minimum in list order) */
+  int end = -1;
+  float end_cost = INFINITY, best_nofinal = INFINITY, best_final = INFINITY;
+  for (int i = 0; i < ncur; i++) {
+    float c = cur_cost[i];
+    if (c < best_nofinal) best_nofinal = c;
+    float fc = g->final_cost[cur_state[i]];
+    if (fc != INFINITY && c + fc < best_final) best_final = c + fc;
+  }
+  int any_final = best_final != INFINITY;
+  for (int i = 0; i < ncur; i++) {
+    float c = (use_final && any_final) ? cur_cost[i] + g->final_cost[cur_state[i]] : cur_cost[i];
+    if (c < end_cost) { end_cost = c; end = i; }
+  }
+  r->final_relative_cost = any_final ? best_final - best_nofinal : INFINITY;
+  r->path_len = 0;
+  if (end >= 0) {
+    r->end_state = cur_state[end];
+    r->best_tot = end_cost;
+    r->best_cost = (double)end_cost - offsets_sum;
+    int n = 0;
+    for (int k = cur_idx[end]; k >= 0 && a_arc[k] >= 0; k = a_prev[k]) n++;
+    r->path_len = n;
+    int k = cur_idx[end];
+    for (int j = n - 1; j >= 0; j--) {
+      if (j < r->path_cap) r->path[j] = a_arc[k];
+      k = a_prev[k];
+    }
+  }
+  free(h.where); free(h.st); free(h.cost); free(h.bp); free(h.arc); free(h.bucket); free(h.bucket_rank);
+  free(a_prev); free(a_arc); free(cur_state); free(cur_cost); free(cur_idx); free(order); free(cnt);
+  free(tmp); free(queue); free(elem_pos);
+  return end >= 0 ? 0 : -1;
+}
+
+/* ===================================================================== */
 /* Speaker x-vectors (src/recognizer.cc:356-419, Kaldi                    */
 /* feat/feature-functions.cc SlidingWindowCmnInternal,                    */
 /* nnet3/nnet-general-component.cc Statistics{Extraction,Pooling}).       */

@@ -192,6 +192,12 @@ typedef struct {
 
 int orc_decode(const orc_graph* g, const float* llh, int num_frames, int llh_stride,
                const orc_dec_opts* o, int use_final, orc_dec_result* r);
+/* Kaldi-sequential token passing (LatticeFasterDecoderTpl with its HashList
+   iteration order, running emitting cutoff and LIFO epsilon queue): the
+   tolerance reference of the order-independent form.  Fills ntok, best,
+   cutoff, next_cutoff, arcs_emit and the best path (no lattice). */
+int orc_decode_kaldi(const orc_graph* g, const float* llh, int num_frames, int llh_stride,
+                     const orc_dec_opts* o, int use_final, orc_dec_result* r);
 
 #ifdef __cplusplus
 }

@@ -573,7 +573,11 @@ class OracleGraph:
                           self.final.ctypes.data, self.tid2pdf.ctypes.data)
 
     def decode(self, llh: np.ndarray, beam=13.0, max_active=7000, min_active=200,
-               beam_delta=0.5, use_final=True, lattice=False):
+               beam_delta=0.5, use_final=True, lattice=False, kaldi=False):
+        """kaldi=True: the Kaldi-sequential restatement (orc_decode_kaldi:
+        HashList order, running emitting cutoff, LIFO epsilon queue; no
+        lattice) instead of the order-independent form the GPU computes."""
+        assert not (kaldi and lattice)
         llh = np.ascontiguousarray(llh, np.float32)
         F = llh.shape[0]
         ntok = np.zeros(F + 1, np.int32)
@@ -599,7 +603,8 @@ class OracleGraph:
             res.lat_link_cap = lcap
             res.lat_cost_offset = lat["cost_offset"].ctypes.data
         o = OrcDecOpts(beam, beam_delta, max_active, min_active)
-        rc = lib().orc_decode(C.byref(self.g), llh.ctypes.data_as(C.c_void_p), C.c_int(F),
+        fn = lib().orc_decode_kaldi if kaldi else lib().orc_decode
+        rc = fn(C.byref(self.g), llh.ctypes.data_as(C.c_void_p), C.c_int(F),
                               C.c_int(llh.shape[1]), C.byref(o), C.c_int(int(use_final)),
                               C.byref(res))
         p = path[:res.path_len].copy()

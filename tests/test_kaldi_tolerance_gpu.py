@@ -1,0 +1,38 @@
+"""The GPU decoder's 1-best against the Kaldi-sequential restatement of the
+reference decoder (oracle.c orc_decode_kaldi) on the GPU's own
+log-likelihoods: the stated tolerance of DESIGN.md section 5 (>= 65 %
+identical 1-best, <= 10 % WER between the forms, best-path cost within 5 %;
+identical 1-best when no active-token limit applies)."""
+import numpy as np
+import pytest
+
+from conftest import perturbed_stream
+import oracle_py
+from test_kaldi_seq import N, SECS, _ed
+
+pytestmark = pytest.mark.gpu
+
+
+def test_gpu_one_best_within_stated_tolerance(synth_model, test_wave):
+    from vosk import engine
+    o = oracle_py.OracleModel(synth_model, fpc=51)
+    e = engine.Engine(synth_model, frames_per_chunk=51, max_streams=N, keep_llh=True)
+    waves = [perturbed_stream(test_wave, 7000 + i, seconds=SECS) for i in range(N)]
+    ss = [e.new_stream() for _ in range(N)]
+    for s, w in zip(ss, waves):
+        e.accept(s, w, finished=True)
+    e.advance(ss)
+    same = errs = words = 0
+    rel = []
+    for s in ss:
+        arcs, cost, _ = e.best_path(s, use_final=True)
+        gw = [int(o.graph.olabel[a]) for a in arcs if o.graph.olabel[a] != 0]
+        k = o.graph.decode(e.llh(s), o.beam, o.max_active, o.min_active, o.beam_delta, True, kaldi=True)
+        same += gw == k["words"]
+        errs += _ed(k["words"], gw)
+        words += len(k["words"])
+        rel.append(abs(cost - k["best_cost"]) / abs(k["best_cost"]))
+    e.close()
+    assert same / N >= 0.65, same
+    assert errs / words <= 0.10, (errs, words)
+    assert max(rel) <= 0.05, max(rel)

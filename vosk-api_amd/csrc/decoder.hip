@@ -996,10 +996,10 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
   const int tbF = sh.fr.tok_base, endF = sh.fr.tok_base + sh.fr.ntok;
   for (int t = tbF + threadIdx.x; t < endF; t += DT) AG_ST(&X[t], 0.0f);
   int kmin = F;
-  // Frames below prune_from are revisited at most prune_interval deep: a
+  // Frames below prune_from are revisited at most prune_revisit deep: a
   // frame past that keeps the extra costs of its last walk, which are never
   // above the current ones (safe, it is only pruned less).
-  const int kstop = pf - a.prune_interval > 0 ? pf - a.prune_interval : 0;
+  const int kstop = pf - a.prune_revisit > 0 ? pf - a.prune_revisit : 0;
   for (int k = F - 1; k >= kstop; k--) {
     // frame records read by every thread (nothing writes them during this walk)
     const LatFrame fk = LF[k], fk1 = LF[k + 1];

@@ -688,6 +688,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   // pruning off (tests that compare the raw per-frame lattice with the oracle)
   dec_.prune_interval = m.dec.prune_interval;
   if (const char* pe = getenv("VOSK_AMD_DEC_PRUNE")) dec_.prune_interval = atoi(pe) ? m.dec.prune_interval : 0;
+  // re-walk depth below the last pruned frame (Kaldi walks until the extra
+  // costs settle; a shallower re-walk only prunes less, the final lattice-beam
+  // prune is exact either way)
+  dec_.prune_revisit = getenv("VOSK_AMD_DEC_PRUNE_REVISIT") ? atoi(getenv("VOSK_AMD_DEC_PRUNE_REVISIT")) : 5;
   dec_.debug = getenv("VOSK_AMD_DEC_DEBUG") ? atoi(getenv("VOSK_AMD_DEC_DEBUG")) : 0;
   dec_.arena_cap = cfg_.arena_tokens;
   dec_.links = nullptr;

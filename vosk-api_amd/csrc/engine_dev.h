@@ -272,6 +272,7 @@ struct DecArgs {
   int lat_frame_cap;
   float lattice_beam;     // pruning (PruneActiveTokens)
   int prune_interval;     // frames between pruning passes (0 = never)
+  int prune_revisit;      // frames below the last pruned frame a pass may re-walk
   int debug;              // VOSK_AMD_DEC_DEBUG: invariant checks with printf (development)
   float* extra;           // [slots][arena_cap] Kaldi extra_cost per token (pruning)
   int* remap;             // [slots][arena_cap] pruning scratch (old -> new arena index)
