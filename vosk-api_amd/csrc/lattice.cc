@@ -1,9 +1,13 @@
 #include "lattice.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <limits>
 #include <map>
+#include <queue>
 #include <unordered_map>
 
 #include "common.h"
@@ -105,17 +109,91 @@ inline int CompareLW(const LW& x, const LW& y) {  // 1: x better, -1: y better
 inline LW Times(const LW& x, const LW& y) { return LW{x.g + y.g, x.a + y.a}; }
 inline LW Divide(const LW& x, const LW& y) { return LW{x.g - y.g, x.a - y.a}; }
 
+// Transition-id strings of the determinizer as nodes of one trie (Kaldi's
+// LatticeDeterminizer keeps a StringRepository for the same reason): a string
+// is a node (the path from the root), appending a label is one hash lookup.
+// The elements of a subset share a base node (the prefixes already moved to
+// arcs); an element's residual string is the path base -> node, compared by
+// length and a polynomial hash mod 2^61 - 1, so removing a common prefix is
+// a change of base (a lowest common ancestor by jump pointers), not a copy.
+struct StrRepo {
+  static constexpr uint64_t kMod = (1ull << 61) - 1, kBase = 1000003ull;
+  static constexpr int kLevels = 20;  // strings up to 2^20 labels
+  std::vector<int> parent{-1}, label{0}, len{0};
+  std::vector<uint64_t> hash{0}, pw{1};
+  std::vector<int> up[kLevels];
+  std::unordered_map<uint64_t, int> succ;
+  StrRepo() {
+    for (int k = 0; k < kLevels; k++) up[k].push_back(0);
+  }
+  static uint64_t MulMod(uint64_t x, uint64_t y) {
+    const unsigned __int128 p = (unsigned __int128)x * y;
+    uint64_t r = (uint64_t)(p & kMod) + (uint64_t)(p >> 61);
+    return r >= kMod ? r - kMod : r;
+  }
+  int Succ(int id, int lab) {
+    const uint64_t k = ((uint64_t)(uint32_t)id << 32) | (uint32_t)lab;
+    auto it = succ.find(k);
+    if (it != succ.end()) return it->second;
+    const int n = (int)parent.size();
+    parent.push_back(id);
+    label.push_back(lab);
+    len.push_back(len[id] + 1);
+    uint64_t h = MulMod(hash[id], kBase) + (uint64_t)(uint32_t)lab + 1;
+    hash.push_back(h >= kMod ? h - kMod : h);
+    if ((int)pw.size() <= len[n]) pw.push_back(MulMod(pw.back(), kBase));
+    up[0].push_back(id);
+    for (int j = 1; j < kLevels; j++) up[j].push_back(up[j - 1][up[j - 1][n]]);
+    succ.emplace(k, n);
+    return n;
+  }
+  int Ancestor(int id, int depth) const {  // the prefix of id with `depth` labels
+    int d = len[id] - depth;
+    for (int j = 0; d; j++, d >>= 1)
+      if (d & 1) id = up[j][id];
+    return id;
+  }
+  int Lca(int a, int b) const {  // longest common prefix of two strings
+    if (len[a] > len[b]) a = Ancestor(a, len[b]);
+    else if (len[b] > len[a]) b = Ancestor(b, len[a]);
+    if (a == b) return a;
+    for (int j = kLevels - 1; j >= 0; j--)
+      if (up[j][a] != up[j][b]) {
+        a = up[j][a];
+        b = up[j][b];
+      }
+    return parent[a];
+  }
+  // residual string base -> id (base a prefix of id): length and hash
+  int ResLen(int id, int base) const { return len[id] - len[base]; }
+  uint64_t ResHash(int id, int base) const {
+    const uint64_t sub = MulMod(hash[base], pw[len[id] - len[base]]);
+    return hash[id] >= sub ? hash[id] - sub : hash[id] + kMod - sub;
+  }
+  void Get(int id, int base, std::vector<int>* out) const {
+    out->resize(len[id] - len[base]);
+    for (int i = (int)out->size() - 1; i >= 0; i--, id = parent[id]) (*out)[i] = label[id];
+  }
+  bool Less(int a, int b, int base) const {  // residuals: shorter first, then lexicographic
+    if (len[a] != len[b]) return len[a] < len[b];
+    if (a == b) return false;
+    std::vector<int> x, y;
+    Get(a, base, &x);
+    Get(b, base, &y);
+    return x < y;
+  }
+};
+
 struct Elem {
   int tok;
   LW w;
-  std::vector<int> str;
+  int str;  // StrRepo node; the residual string is base -> str
 };
 // (weight, string) order of Kaldi's determinizer when one state is reached twice
-inline bool ElemBetter(const Elem& x, const Elem& y) {
+inline bool ElemBetter(const StrRepo& R, int base, const Elem& x, const Elem& y) {
   const int c = CompareLW(x.w, y.w);
   if (c != 0) return c > 0;
-  if (x.str.size() != y.str.size()) return x.str.size() < y.str.size();
-  return x.str < y.str;
+  return R.Less(x.str, y.str, base);
 }
 
 }  // namespace
@@ -219,71 +297,84 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     if (L.tok_cost[t] == 0.0f) { start = t; break; }
   if (start < 0) return true;
 
+  StrRepo R;
+  long long dbg_ext = 0;
+  double dt_clo = 0, dt_norm = 0, dt_bw = 0, dt_find = 0;
+  using dclk = std::chrono::steady_clock;
+  auto dms = [](dclk::time_point a) { return std::chrono::duration<double, std::milli>(dclk::now() - a).count(); };
   // closure over word-epsilon links (emitting arcs without a word label too):
   // for each token the best (weight, string) reaching it
-  auto closure = [&](std::vector<Elem>* sub) {
+  // frame of every token: the closure visits tokens frame by frame (links go
+  // from frame k to k + 1, or within frame k), so a token is expanded once its
+  // frame's predecessors are final -- not once per improvement along every
+  // path (the same fixpoint: the best (weight, string) per token)
+  std::vector<int> tframe(N);
+  for (int k = 0; k <= F; k++)
+    for (int t = L.frame_begin[k]; t < L.frame_begin[k + 1]; t++) tframe[t] = k;
+  auto closure = [&](std::vector<Elem>* sub, int base) {
     std::unordered_map<int, int> at;
-    std::vector<int> work;
+    std::priority_queue<std::pair<int, int>, std::vector<std::pair<int, int>>, std::greater<std::pair<int, int>>>
+        work;  // (frame, element), earliest frame first
     for (int i = 0; i < (int)sub->size(); i++) {
       at[(*sub)[i].tok] = i;
-      work.push_back(i);
+      work.push({tframe[(*sub)[i].tok], i});
     }
     while (!work.empty()) {
-      const int i = work.back();
-      work.pop_back();
+      const int i = work.top().second;
+      work.pop();
       const Elem e = (*sub)[i];
+      dbg_ext++;
       for (int li : outl[e.tok]) {
         const auto& l = L.links[li];
         if (g.olabel[l.arc] != 0) continue;
-        Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}), e.str};
-        if (g.ilabel[l.arc] != 0) n.str.push_back(g.ilabel[l.arc]);
+        Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}),
+               g.ilabel[l.arc] != 0 ? R.Succ(e.str, g.ilabel[l.arc]) : e.str};
         auto it = at.find(n.tok);
         if (it == at.end()) {
           at[n.tok] = (int)sub->size();
-          work.push_back((int)sub->size());
-          sub->push_back(std::move(n));
-        } else if (ElemBetter(n, (*sub)[it->second])) {
-          (*sub)[it->second] = std::move(n);
-          work.push_back(it->second);
+          work.push({tframe[n.tok], (int)sub->size()});
+          sub->push_back(n);
+        } else if (ElemBetter(R, base, n, (*sub)[it->second])) {
+          (*sub)[it->second] = n;
+          work.push({tframe[n.tok], it->second});
         }
       }
     }
     std::sort(sub->begin(), sub->end(), [](const Elem& x, const Elem& y) { return x.tok < y.tok; });
   };
-  // normalization: the best weight and the common string prefix move to the arc
-  auto normalize = [](std::vector<Elem>* sub, LW* tot, std::vector<int>* prefix) {
+  // normalization: the best weight and the common string prefix move to the
+  // arc (the prefix = base -> lowest common ancestor, the subset's new base)
+  auto normalize = [&](std::vector<Elem>* sub, int base, LW* tot, std::vector<int>* prefix) {
     *tot = (*sub)[0].w;
-    for (auto& e : *sub)
+    int common = (*sub)[0].str;
+    for (auto& e : *sub) {
       if (CompareLW(e.w, *tot) > 0) *tot = e.w;
-    size_t n = (*sub)[0].str.size();
-    for (auto& e : *sub) {
-      size_t j = 0;
-      while (j < n && j < e.str.size() && e.str[j] == (*sub)[0].str[j]) j++;
-      n = j;
+      common = R.Lca(common, e.str);
     }
-    prefix->assign((*sub)[0].str.begin(), (*sub)[0].str.begin() + n);
-    for (auto& e : *sub) {
-      e.w = Divide(e.w, *tot);
-      e.str.erase(e.str.begin(), e.str.begin() + n);
-    }
+    R.Get(common, base, prefix);
+    for (auto& e : *sub) e.w = Divide(e.w, *tot);
+    return common;
   };
   // subsets are equal with the same tokens and strings and weights within
   // delta (Kaldi's determinizer, delta = kDelta = 1/1024)
   const float delta = 1.0f / 1024.0f;
   std::unordered_map<std::string, std::vector<int>> index;
   std::vector<std::vector<Elem>> subsets;
-  auto key_of = [](const std::vector<Elem>& sub) {
+  std::vector<int> bases;  // per subset: the base node of its residual strings
+  auto key_of = [&](const std::vector<Elem>& sub, int base) {
     std::string k;
+    k.reserve(sub.size() * 16);
     for (auto& e : sub) {
+      const int n = R.ResLen(e.str, base);
+      const uint64_t h = R.ResHash(e.str, base);
       k.append((const char*)&e.tok, sizeof(int));
-      const int n = (int)e.str.size();
       k.append((const char*)&n, sizeof(int));
-      k.append((const char*)e.str.data(), sizeof(int) * n);
+      k.append((const char*)&h, sizeof(h));
     }
     return k;
   };
-  auto find_or_add = [&](std::vector<Elem>&& sub, bool* added) {
-    const std::string k = key_of(sub);
+  auto find_or_add = [&](std::vector<Elem>&& sub, int base, bool* added) {
+    const std::string k = key_of(sub, base);
     auto& cand = index[k];
     for (int id : cand) {
       const auto& o = subsets[id];
@@ -297,20 +388,22 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     }
     const int id = (int)subsets.size();
     subsets.push_back(std::move(sub));
+    bases.push_back(base);
     cand.push_back(id);
     *added = true;
     return id;
   };
   // start state: the closure of the start token, not normalized (its weight
   // and string stay on the first arcs / final weight)
-  std::vector<Elem> s0{Elem{start, LW{}, {}}};
-  closure(&s0);
+  std::vector<Elem> s0{Elem{start, LW{}, 0}};
+  closure(&s0, 0);
   bool added;
-  find_or_add(std::move(s0), &added);
+  find_or_add(std::move(s0), 0, &added);
   std::vector<std::vector<WordLattice::Arc>> arcs(1);
   std::vector<int> queue{0};
   for (size_t qi = 0; qi < queue.size(); qi++) {
     const int sid = queue[qi];
+    const int sbase = bases[sid];
     // transitions per word label, in label order
     std::map<int, std::vector<Elem>> by_word;
     {
@@ -320,26 +413,32 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
           const auto& l = L.links[li];
           const int w = g.olabel[l.arc];
           if (w == 0) continue;
-          Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}), e.str};
-          if (g.ilabel[l.arc] != 0) n.str.push_back(g.ilabel[l.arc]);
+          Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}),
+                 g.ilabel[l.arc] != 0 ? R.Succ(e.str, g.ilabel[l.arc]) : e.str};
           auto& v = by_word[w];
           bool merged = false;
           for (auto& x : v)
             if (x.tok == n.tok) {
-              if (ElemBetter(n, x)) x = n;
+              if (ElemBetter(R, sbase, n, x)) x = n;
               merged = true;
               break;
             }
-          if (!merged) v.push_back(std::move(n));
+          if (!merged) v.push_back(n);
         }
     }
     for (auto& kv : by_word) {
       std::vector<Elem> sub = std::move(kv.second);
-      closure(&sub);
+      auto t0 = dclk::now();
+      closure(&sub, sbase);
+      dt_clo += dms(t0);
       LW tot;
       std::vector<int> prefix;
-      normalize(&sub, &tot, &prefix);
-      const int dst = find_or_add(std::move(sub), &added);
+      t0 = dclk::now();
+      const int nbase = normalize(&sub, sbase, &tot, &prefix);
+      dt_norm += dms(t0);
+      t0 = dclk::now();
+      const int dst = find_or_add(std::move(sub), nbase, &added);
+      dt_find += dms(t0);
       if (added) {
         if ((int)subsets.size() > opt.max_states) return false;
         queue.push_back(dst);
@@ -349,24 +448,30 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     }
   }
   const int S = (int)subsets.size();
+  if (getenv("VOSK_AMD_DET_DEBUG")) {
+    long long el = 0;
+    for (auto& x : subsets) el += (long long)x.size();
+    fprintf(stderr, "det: tokens %d links %zu subsets %d elems %lld expansions %lld strings %zu clo %.2f norm %.2f find %.2f\n",
+            N, L.links.size(), S, el, dbg_ext, R.parent.size(), dt_clo, dt_norm, dt_find);
+  }
   std::vector<LW> fw(S);
   std::vector<std::vector<int>> fs(S);
   std::vector<char> isf(S, 0);
   for (int s = 0; s < S; s++) {
-    const Elem* best = nullptr;
-    Elem tmp;
+    bool have = false;
+    Elem best{0, LW{}, 0};
     for (const Elem& e : subsets[s]) {
       if (fin[e.tok] == INFINITY) continue;
       Elem c{e.tok, Times(e.w, LW{fin[e.tok], 0.0f}), e.str};
-      if (!best || ElemBetter(c, *best)) {
-        tmp = c;
-        best = &tmp;
+      if (!have || ElemBetter(R, bases[s], c, best)) {
+        best = c;
+        have = true;
       }
     }
-    if (best) {
+    if (have) {
       isf[s] = 1;
-      fw[s] = tmp.w;
-      fs[s] = tmp.str;
+      fw[s] = best.w;
+      R.Get(best.str, bases[s], &fs[s]);
     }
   }
   // topological order (the lattice is acyclic), start state first

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <sstream>
@@ -399,7 +400,11 @@ const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, cons
   Graph g;
   g.ilabel.assign(arc_ilabel, arc_ilabel + narcs);
   g.olabel.assign(arc_olabel, arc_olabel + narcs);
+  using clk = std::chrono::steady_clock;
+  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const auto t0 = clk::now();
   PruneRawLattice(&L, lattice_beam);
+  const auto t1 = clk::now();
   std::ostringstream os;
   os.precision(9);
   os << "{\"pruned_tokens\": " << L.tok_state.size() << ", \"pruned_links\": " << L.links.size();
@@ -407,6 +412,7 @@ const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, cons
   LatticeOptions opt;
   opt.lattice_beam = lattice_beam;
   const bool ok = DeterminizeToWords(L, g, opt, &wl);
+  const auto t2 = clk::now();
   os << ", \"det_ok\": " << (ok ? 1 : 0) << ", \"det_states\": " << wl.NumStates();
   int det_arcs = 0;
   for (auto& v : wl.arcs) det_arcs += (int)v.size();
@@ -432,8 +438,12 @@ const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, cons
        << ", \"align_arcs\": " << aarcs;
     wl = std::move(al);
   }
+  const auto t3 = clk::now();
   MbrResult r;
   MinimumBayesRisk(wl, &r);
+  const auto t4 = clk::now();
+  os << ", \"ms\": {\"prune\": " << ms(t0, t1) << ", \"determinize\": " << ms(t1, t2)
+     << ", \"scale_align\": " << ms(t2, t3) << ", \"mbr\": " << ms(t3, t4) << "}";
   os << ", \"mbr\": {\"words\": [";
   for (size_t i = 0; i < r.words.size(); i++) os << (i ? ", " : "") << r.words[i];
   os << "], \"conf\": [";
