@@ -316,6 +316,7 @@ def run_api(args, model, dist, rank, world, base):
     elapsed = _max_over_ranks(dist, t1 - t0)
     audio_s = K * FEED_BYTES / 2 / SR * S * world
     st = ve.batch_lane_stats(bm, 0)
+    rprof = ve.batch_result_profile(bm)
     nonempty = sum(1 for t in texts if t.strip())
     words = sum(len(t.split()) for t in texts)
     del recs
@@ -367,6 +368,7 @@ def run_api(args, model, dist, rank, world, base):
                     "arcs_per_frame": round((tot["arcs_emit"] + tot["arcs_eps"]) / max(tot["frames"], 1), 1),
                     "lattice_links_per_frame": round(tot["links"] / max(tot["frames"], 1), 1)},
         "results": {"streams_with_text": nonempty, "words": words, "result_messages": nres[0]},
+        "result_production": {k: round(v, 2) for k, v in rprof.items()},
     }
 
 

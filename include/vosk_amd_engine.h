@@ -177,6 +177,10 @@ int vamd_batch_lanes(struct VoskBatchModel *m);
  * is quiescent (after vosk_batch_model_wait). */
 int vamd_batch_lane_stats(struct VoskBatchModel *m, int lane, int *load3, double *ms4,
                           long long *launches4, long long *dec6, int reset);
+/* result production totals: {segments, lattice links copied, ms copying
+ * (lane threads), ms building raw lattices, ms prune + determinize + align,
+ * ms MBR, ms formatting} */
+int vamd_batch_result_profile(struct VoskBatchModel *m, double *out7);
 /* stream -> lane index it was admitted to */
 int vamd_batch_recognizer_lane(struct VoskBatchRecognizer *r);
 /* admission policy (host only, no GPU): replays `n` admissions against lanes

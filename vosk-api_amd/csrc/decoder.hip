@@ -605,6 +605,10 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
       }
       pr.mark(3);
       if (mode == 1) {
+        // the relaxations' key minima are issued without waiting for them
+        // (no-return atomics): complete them before the barrier, so every
+        // winner check below reads keys that include its own relaxation
+        __threadfence();
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kUnroll; u++)
@@ -678,6 +682,7 @@ __device__ __forceinline__ void eps_closure(const DecArgs& a, DecShared& sh, con
             }
           }
         }
+        __threadfence();  // a created HBM entry's key minimum is a no-return atomic (hbm_created)
         __syncthreads();
         if (sv != 0x7fffffff && slot_key(t, T, sv) == kk) set_bp(t, T, sv, sh.tsrc[j]);
       }
@@ -850,7 +855,20 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
     const float cost = funord((uint32_t)(k >> 32));
     if (ok && cost < cutoff) {
       int prev = -1;
-      if (arc >= 0) prev = (bp & kBpEps) ? base + slot_pos(t, T, nl_n, bp_slot(bp)) : bp;
+      if (arc >= 0) {
+        if (bp & kBpEps) {
+          const int sv = bp_slot(bp);
+          // a source slot outside both tables can only be a backpointer that
+          // was never written: flagged, never dereferenced
+          if (sv >= kHashCap || (sv < 0 && ~sv >= (1 << a.hbits))) {
+            sh.bad |= 8;
+          } else {
+            prev = base + slot_pos(t, T, nl_n, sv);
+          }
+        } else {
+          prev = bp;
+        }
+      }
       ag_st4(&p.arena[base + j], make_int4(prev, arc, __float_as_int(cost), s));
       const int q = atomicAdd(&sh.n_next, 1);
       AG_ST(&p.cs[q], s);

@@ -669,6 +669,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   dec_.ht_pos = (int*)DevAlloc(sizeof(int) * S * H);
   dec_.ht_stamp = (int*)DevAlloc(sizeof(int) * S * H);
   dec_.ht_bp = (int*)DevAlloc(sizeof(int) * S * H);
+  // backpointers and positions are written before they are read in a frame;
+  // zeroed so that a slot never holds another engine's data
+  HIPCHECK(hipMemset(dec_.ht_pos, 0, sizeof(int) * S * H));
+  HIPCHECK(hipMemset(dec_.ht_bp, 0, sizeof(int) * S * H));
   dec_.ht_list = (int*)DevAlloc(sizeof(int) * S * MT);
   dec_.front_g = (int*)DevAlloc(sizeof(int) * 2 * S * MT);
   dec_.cur_state = (int*)DevAlloc(sizeof(int) * S * MT);

@@ -763,6 +763,13 @@ int vamd_batch_lane_stats(VoskBatchModel* m, int lane, int* load3, double* ms4, 
   API_CATCH(-1)
 }
 
+int vamd_batch_result_profile(VoskBatchModel* m, double* out7) {
+  API_TRY
+  ((BatchModel*)m)->ResultProfile(out7);
+  return 0;
+  API_CATCH(-1)
+}
+
 int vamd_batch_recognizer_lane(VoskBatchRecognizer* r) {
   API_TRY
   return ((BatchRecognizer*)r)->lane();

@@ -638,6 +638,12 @@ int PickLane(const std::vector<std::array<int, 2>>& loads) {
 
 Engine* BatchModel::LaneEngine(int i) { return lanes_.at(i)->engine.get(); }
 
+void BatchModel::ResultProfile(double* out) const {
+  out[0] = (double)prof_[0];
+  out[1] = (double)prof_[1];
+  for (int i = 2; i < 7; i++) out[i] = prof_[i] * 1e-6;
+}
+
 int BatchModel::LaneOf(const BatchRecognizer* r) const { return r->lane_; }
 
 void BatchModel::Admit(BatchRecognizer* r, int rate) {
@@ -728,8 +734,16 @@ void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, co
   Engine* e = L->engine.get();
   const float shift = 0.01f * md_->dcb.frame_subsampling_factor;
   const int frames = e->DeviceFramesDecoded(r->slot_);
+  using clk = std::chrono::steady_clock;
+  auto ns = [](clk::time_point a, clk::time_point b) {
+    return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+  };
   auto sl = std::make_shared<SegmentLattice>();
+  const auto tc = clk::now();
   if (frames > 0) e->CopySegmentLattice(r->slot_, sl.get(), false);
+  prof_[0]++;
+  prof_[1] += (long long)sl->links.size();
+  prof_[2] += ns(tc, clk::now());
   const double offset = r->segment_offset_;
   r->segment_offset_ = final_segment ? 0.0 : r->segment_offset_ + frames * shift;
   const uint64_t seq = r->next_seq_++;
@@ -739,24 +753,34 @@ void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, co
     r->tasks_++;
     L->tasks++;
   }
-  pool_->Submit([this, L, r, sl, seq, offset, frames, path]() {
+  pool_->Submit([this, L, r, sl, seq, offset, frames, path, ns]() {
     const ModelData& m = *md_;
     MbrResult res;
     try {
       if (frames > 0) {
         RawLattice raw;
+        const auto t0 = clk::now();
         if (!sl->frames.empty())
           BuildRawLattice(m.graph, m.graph.start, sl->frames, sl->arena, sl->links, true, &raw);
         raw.overflow = raw.overflow || sl->overflow;
+        const auto t1 = clk::now();
         WordLattice wl;
-        if (WordLatticeFromRaw(raw, m, 0.9f, &wl, false)) MinimumBayesRisk(wl, &res);
+        const bool ok = WordLatticeFromRaw(raw, m, 0.9f, &wl, false);
+        const auto t2 = clk::now();
+        if (ok) MinimumBayesRisk(wl, &res);
         else res = PathMbr(m, path);
+        prof_[3] += ns(t0, t1);
+        prof_[4] += ns(t1, t2);
+        prof_[5] += ns(t2, clk::now());
       }
     } catch (const std::exception& ex) {
       VAMD_WARN("batch result failed: " << ex.what());
       res = MbrResult();
     }
-    r->PublishResult(seq, r->FormatResult(res, offset));
+    const auto tf = clk::now();
+    std::string js = r->FormatResult(res, offset);
+    prof_[6] += ns(tf, clk::now());
+    r->PublishResult(seq, std::move(js));
     {
       std::lock_guard<std::mutex> lk(L->mu);
       r->tasks_--;

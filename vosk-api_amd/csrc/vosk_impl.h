@@ -194,6 +194,10 @@ class BatchModel {
   // per lane: {device, streams, pending chunks}
   std::vector<std::array<int, 3>> LaneLoads();
   Engine* lane_engine(int i) { return LaneEngine(i); }
+  // result production totals: {segments, lattice links copied, ms copying
+  // (lane thread), ms building raw lattices, ms prune + determinize + align,
+  // ms MBR, ms formatting}
+  void ResultProfile(double* out7) const;
   int LaneOf(const BatchRecognizer* r) const;
 
  private:
@@ -209,6 +213,7 @@ class BatchModel {
   std::unique_ptr<WorkerPool> pool_;
   std::mutex admit_mu_;
   std::atomic<int> ref_{1};
+  std::atomic<long long> prof_[7] = {};  // ResultProfile (ns except counts)
   ~BatchModel();
 };
 

@@ -60,6 +60,7 @@ _SIGS = {
     "vamd_batch_lanes": (C.c_int, [_vp]),
     "vamd_batch_lane_stats": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, C.c_int]),
     "vamd_batch_recognizer_lane": (C.c_int, [_vp]),
+    "vamd_batch_result_profile": (C.c_int, [_vp, _vp]),
     "vamd_admission_replay": (C.c_int, [C.c_int, _vp, C.c_int, _vp, _vp]),
 }
 for _name, (_res, _args) in _SIGS.items():
@@ -111,6 +112,15 @@ def batch_lane_stats(model, lane, reset=False):
             "stages": {k: (float(ms[i]), int(ln[i])) for i, k in enumerate(names)},
             "decoder": dict(zip(("frames", "tok_in", "tok_out", "arcs_emit", "arcs_eps", "links"),
                                 (int(x) for x in dec)))}
+
+
+def batch_result_profile(model):
+    """Result production totals of a vosk.BatchModel (segments, links copied,
+    ms copy / build / prune+determinize+align / MBR / format)."""
+    o = np.zeros(7, np.float64)
+    _chk(_c.vamd_batch_result_profile(model._handle, o.ctypes.data))
+    return dict(zip(("segments", "links_copied", "copy_ms", "build_ms", "det_ms", "mbr_ms", "format_ms"),
+                    (float(x) for x in o)))
 
 
 def batch_recognizer_lane(rec):
