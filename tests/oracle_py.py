@@ -718,14 +718,23 @@ class OracleModel:
         return self.graph.decode(llh, self.beam, self.max_active, self.min_active,
                                  self.beam_delta, use_final)
 
-    def online(self, wave, chunk=None, rate=16000, silence_weighting=True):
+    def online(self, wave, chunk=None, rate=16000, silence_weighting=True, endpoints=False):
         """The single-stream Recognizer's online flow (src/recognizer.cc:297-
         323, FinalResult :818-830) with the engine's chunk schedule: per
         piece, features of all samples so far, UpdateSilenceWeights from the
         best path of the frames decoded so far, then every chunk that became
         ready (its i-vector request applies the queued delta weights of
         frames <= the request).  Returns per-chunk i-vectors, the LLH rows,
-        and the final decode."""
+        and the final decode.
+
+        endpoints=True: after every AcceptWaveform call of `chunk` samples the
+        endpoint rules run on the decoder segment (EndpointDetected,
+        :318; tests/oracle_endpoint.py); when they fire the caller takes
+        Result() and the next call starts with CleanUp (:188-224): the
+        decoder restarts at the frames decoded so far and the silence
+        weighting restarts with first decoder frame = frame offset * 3
+        (features and i-vector statistics continue).  Adds "segments":
+        [(first frame, end frame)] with the last one ended by FinalResult."""
         assert self.ivector is not None
         wave = np.asarray(wave, np.float32)
         model_rate = int(float(self.mfcc_conf.get("sample-frequency", 16000)))
@@ -740,57 +749,77 @@ class OracleModel:
         pending, weighted = [], False
         reqs, ents = [], []
         c, done, dec = 0, 0, 0
+        seg0, segs, reset_next = 0, [], False
+        if endpoints:
+            import oracle_endpoint as OE
+            rules, _ = OE.endpoint_config(self.model_conf)
+            shift = np.float32(np.float32(0.01) * np.float32(fss))
         ivecs = np.zeros((0, self.ivector.dim), np.float32)
         llh = np.zeros((0, self.net.out_dim), np.float32)
-        pieces, n = [], 0
-        for k in recognizer_pieces(len(wave), chunk or len(wave), rate):
-            n += k
-            pieces.append((n, False))
-        pieces.append((len(wave), True))
-        for n, fin in pieces:
-            n_out = n if rate == model_rate else resample_num_outputs(rate, model_rate, n, fin)
-            T = mfcc_num_frames(n_out, self.mfcc_conf, self.fbank)
-            ready = T if fin else max(0, T - right)
-            if active and ready > 0 and (weighted or done == 0):
-                tids, toks = [], []
-                if dec > 0:
-                    r = self.decode_llh(llh[:dec], use_final=False)
-                    for a in r["path"]:
-                        if g.ilabel[a] != 0:
-                            tids.append(int(g.ilabel[a]))
-                            toks.append(int(np.searchsorted(g.arc_begin, a, side="right") - 1))
-                sw.compute_current_traceback(tids, toks)
-                pending += sw.get_delta_weights(ready, 0)
-                weighted = True
-            need_out = -(-T // fss) if fin else 0
-            new = False
-            while True:
-                ok = (T > 0 and c * opc < need_out) if fin else T >= (c + 1) * fpc + R + right
-                if not ok:
-                    break
-                f = min((c + 1) * fpc + R, T) - 1
-                e = []
-                if f >= done and weighted:
-                    pending.sort()
-                    e = [x for x in pending if x[0] <= f]
-                    pending = [x for x in pending if x[0] > f]
-                reqs.append(f)
-                ents.append(e)
-                done = max(done, f + 1)
-                dec += min(opc, need_out - c * opc) if fin else opc
-                c += 1
-                new = True
-            if new:
-                feats = feats_all[:T]
-                if weighted:
-                    ivecs = self.ivector.extract_weighted(feats, reqs, ents)
-                else:
-                    ivecs = self.ivector.extract(feats, reqs)
-                nf = self.nnet_features(feats)
-                ivt, t0 = self._ivec_of_time(T, len(ivecs))
-                llh = self.net.forward(nf, ivecs, ivt, t0)[:dec]
-        r = self.decode_llh(llh)
-        return dict(ivectors=ivecs, llh=llh, decode=r, requests=reqs, entries=ents)
+        calls, n = [], 0
+        step = int(rate * 0.2)
+        ch = chunk or len(wave)
+        for i in range(0, len(wave), ch):
+            m = min(ch, len(wave) - i)
+            calls.append([n + j + min(step, m - j) for j in range(0, m, step)])
+            n += m
+        calls.append(None)  # FinalResult
+        for call in calls:
+            if call is not None and reset_next:  # CleanUp: InitDecoding, new OnlineSilenceWeighting
+                seg0, reset_next = dec, False
+                sw = SilenceWeighting(lambda tid: int(tm.tid2phone[tid]) in sil, 1e-3, fss)
+            for n, fin in ([(x, False) for x in call] if call is not None else [(len(wave), True)]):
+                n_out = n if rate == model_rate else resample_num_outputs(rate, model_rate, n, fin)
+                T = mfcc_num_frames(n_out, self.mfcc_conf, self.fbank)
+                ready = T if fin else max(0, T - right)
+                if active and ready > 0 and (weighted or done == 0):
+                    tids, toks = [], []
+                    if dec > seg0:
+                        r = self.decode_llh(llh[seg0:dec], use_final=False)
+                        for a in r["path"]:
+                            if g.ilabel[a] != 0:
+                                tids.append(int(g.ilabel[a]))
+                                toks.append(int(np.searchsorted(g.arc_begin, a, side="right") - 1))
+                    sw.compute_current_traceback(tids, toks)
+                    pending += sw.get_delta_weights(ready, seg0 * fss)
+                    weighted = True
+                need_out = -(-T // fss) if fin else 0
+                new = False
+                while True:
+                    ok = (T > 0 and c * opc < need_out) if fin else T >= (c + 1) * fpc + R + right
+                    if not ok:
+                        break
+                    f = min((c + 1) * fpc + R, T) - 1
+                    e = []
+                    if f >= done and weighted:
+                        pending.sort()
+                        e = [x for x in pending if x[0] <= f]
+                        pending = [x for x in pending if x[0] > f]
+                    reqs.append(f)
+                    ents.append(e)
+                    done = max(done, f + 1)
+                    dec += min(opc, need_out - c * opc) if fin else opc
+                    c += 1
+                    new = True
+                if new:
+                    feats = feats_all[:T]
+                    if weighted:
+                        ivecs = self.ivector.extract_weighted(feats, reqs, ents)
+                    else:
+                        ivecs = self.ivector.extract(feats, reqs)
+                    nf = self.nnet_features(feats)
+                    ivt, t0 = self._ivec_of_time(T, len(ivecs))
+                    llh = self.net.forward(nf, ivecs, ivt, t0)[:dec]
+            if endpoints and call is not None and dec > seg0:
+                r = self.decode_llh(llh[seg0:dec], use_final=False)
+                ts = OE.trailing_silence(r["path"], g.ilabel, tm.tid2phone, sil)
+                if OE.rules_fire(rules, dec - seg0, ts, shift, r["final_relative_cost"]):
+                    segs.append((seg0, dec))
+                    reset_next = True
+        if endpoints:
+            segs.append((seg0, dec))
+        r = self.decode_llh(llh[seg0:]) if endpoints else self.decode_llh(llh)
+        return dict(ivectors=ivecs, llh=llh, decode=r, requests=reqs, entries=ents, segments=segs)
 
     def recognize(self, wave):
         r = self.decode_llh(self.loglikes(wave))

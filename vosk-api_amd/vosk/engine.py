@@ -127,7 +127,8 @@ def batch_recognizer_lane(rec):
     return _chk(_c.vamd_batch_recognizer_lane(rec._handle))
 
 
-def lattice_words(L, arc_ilabel, arc_olabel, lattice_beam=6.0, graph_scale=0.9, nbest=5, align=None):
+def lattice_words(L, arc_ilabel, arc_olabel, lattice_beam=6.0, graph_scale=0.9, nbest=5, align=None,
+                  timings=False):
     """Host-only: the result pipeline (prune, determinize, scale, MBR,
     n-best) over a lattice in the vamd_stream_lattice array form; align =
     (tid phone-boundary type, tid IsFinal, tid IsSelfLoop) arrays to word-align
@@ -151,7 +152,10 @@ def lattice_words(L, arc_ilabel, arc_olabel, lattice_beam=6.0, graph_scale=0.9, 
                                      else [None, None, None, 0]))
     if r is None:
         raise RuntimeError("vamd_lattice_words_json failed: " + _err())
-    return json.loads(r.decode())
+    d = json.loads(r.decode())
+    if not timings:
+        d.pop("ms", None)  # host stage times (vary run to run)
+    return d
 
 
 def silence_weighting_run(calls, tid_is_silence, silence_weight=1e-3, fss=3):
