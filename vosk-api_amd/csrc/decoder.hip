@@ -100,6 +100,10 @@ struct Prof {
   }
 };
 
+// s_waitcnt vmcnt(0): every vector memory operation of this wave, no-return
+// atomics included, has completed (gfx9 encoding: expcnt 7, lgkmcnt 15)
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 __device__ __forceinline__ float wave_min_f(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
   return v;
@@ -606,9 +610,10 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
       pr.mark(3);
       if (mode == 1) {
         // the relaxations' key minima are issued without waiting for them
-        // (no-return atomics): complete them before the barrier, so every
-        // winner check below reads keys that include its own relaxation
-        __threadfence();
+        // (no-return atomics): wait for their completion (vmcnt, no cache
+        // maintenance) before the barrier, so every winner check below reads
+        // keys that include its own relaxation
+        vm_drain();
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kUnroll; u++)
@@ -682,7 +687,7 @@ __device__ __forceinline__ void eps_closure(const DecArgs& a, DecShared& sh, con
             }
           }
         }
-        __threadfence();  // a created HBM entry's key minimum is a no-return atomic (hbm_created)
+        vm_drain();  // a created HBM entry's key minimum is a no-return atomic (hbm_created)
         __syncthreads();
         if (sv != 0x7fffffff && slot_key(t, T, sv) == kk) set_bp(t, T, sv, sh.tsrc[j]);
       }
