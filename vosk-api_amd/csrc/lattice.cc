@@ -118,13 +118,33 @@ inline LW Divide(const LW& x, const LW& y) { return LW{x.g - y.g, x.a - y.a}; }
 // a change of base (a lowest common ancestor by jump pointers), not a copy.
 struct StrRepo {
   static constexpr uint64_t kMod = (1ull << 61) - 1, kBase = 1000003ull;
-  static constexpr int kLevels = 20;  // strings up to 2^20 labels
-  std::vector<int> parent{-1}, label{0}, len{0};
+  // jump[]: skew-binary jump pointers (one per node, O(log depth) ancestor
+  // and common-prefix queries)
+  std::vector<int> parent{-1}, label{0}, len{0}, jump{0};
   std::vector<uint64_t> hash{0}, pw{1};
-  std::vector<int> up[kLevels];
-  std::unordered_map<uint64_t, int> succ;
-  StrRepo() {
-    for (int k = 0; k < kLevels; k++) up[k].push_back(0);
+  // (node, label) -> successor node: open addressing, linear probing
+  std::vector<uint64_t> skey = std::vector<uint64_t>(1024, ~0ull);
+  std::vector<int> sval = std::vector<int>(1024, -1);
+  size_t sused = 0;
+  static size_t Mix(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    return (size_t)k;
+  }
+  void Grow() {
+    std::vector<uint64_t> ok(skey.size() * 2, ~0ull);
+    std::vector<int> ov(skey.size() * 2, -1);
+    ok.swap(skey);
+    ov.swap(sval);
+    const size_t m = skey.size() - 1;
+    for (size_t i = 0; i < ok.size(); i++)
+      if (ok[i] != ~0ull) {
+        size_t h = Mix(ok[i]) & m;
+        while (skey[h] != ~0ull) h = (h + 1) & m;
+        skey[h] = ok[i];
+        sval[h] = ov[i];
+      }
   }
   static uint64_t MulMod(uint64_t x, uint64_t y) {
     const unsigned __int128 p = (unsigned __int128)x * y;
@@ -133,36 +153,42 @@ struct StrRepo {
   }
   int Succ(int id, int lab) {
     const uint64_t k = ((uint64_t)(uint32_t)id << 32) | (uint32_t)lab;
-    auto it = succ.find(k);
-    if (it != succ.end()) return it->second;
+    size_t m = skey.size() - 1, q = Mix(k) & m;
+    while (skey[q] != ~0ull) {
+      if (skey[q] == k) return sval[q];
+      q = (q + 1) & m;
+    }
     const int n = (int)parent.size();
+    skey[q] = k;
+    sval[q] = n;
+    if (2 * ++sused > skey.size()) Grow();
     parent.push_back(id);
     label.push_back(lab);
     len.push_back(len[id] + 1);
     uint64_t h = MulMod(hash[id], kBase) + (uint64_t)(uint32_t)lab + 1;
     hash.push_back(h >= kMod ? h - kMod : h);
     if ((int)pw.size() <= len[n]) pw.push_back(MulMod(pw.back(), kBase));
-    up[0].push_back(id);
-    for (int j = 1; j < kLevels; j++) up[j].push_back(up[j - 1][up[j - 1][n]]);
-    succ.emplace(k, n);
+    const int j1 = jump[id], j2 = jump[j1];
+    jump.push_back(id != 0 && len[id] - len[j1] == len[j1] - len[j2] ? j2 : id);
     return n;
   }
   int Ancestor(int id, int depth) const {  // the prefix of id with `depth` labels
-    int d = len[id] - depth;
-    for (int j = 0; d; j++, d >>= 1)
-      if (d & 1) id = up[j][id];
+    while (len[id] > depth) id = len[jump[id]] >= depth ? jump[id] : parent[id];
     return id;
   }
   int Lca(int a, int b) const {  // longest common prefix of two strings
     if (len[a] > len[b]) a = Ancestor(a, len[b]);
     else if (len[b] > len[a]) b = Ancestor(b, len[a]);
-    if (a == b) return a;
-    for (int j = kLevels - 1; j >= 0; j--)
-      if (up[j][a] != up[j][b]) {
-        a = up[j][a];
-        b = up[j][b];
+    while (a != b) {  // equal depths: the jump structure is the same on both sides
+      if (jump[a] != jump[b]) {
+        a = jump[a];
+        b = jump[b];
+      } else {
+        a = parent[a];
+        b = parent[b];
       }
-    return parent[a];
+    }
+    return a;
   }
   // residual string base -> id (base a prefix of id): length and hash
   int ResLen(int id, int base) const { return len[id] - len[base]; }
@@ -289,6 +315,13 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
   if (N == 0) return true;
   std::vector<std::vector<int>> outl(N);
   for (int i = 0; i < (int)L.links.size(); i++) outl[L.links[i].src].push_back(i);
+  // the labels of every link, gathered once (the graph's label arrays are
+  // large: random reads of them in every closure miss the caches)
+  std::vector<int> lin(L.links.size()), lout(L.links.size());
+  for (size_t i = 0; i < L.links.size(); i++) {
+    lin[i] = g.ilabel[L.links[i].arc];
+    lout[i] = g.olabel[L.links[i].arc];
+  }
   std::vector<float> fin(N, INFINITY);
   for (int t = L.frame_begin[F]; t < L.frame_begin[F + 1]; t++)
     fin[t] = L.final_cost.empty() ? 0.0f : L.final_cost[t - L.frame_begin[F]];
@@ -311,12 +344,27 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
   std::vector<int> tframe(N);
   for (int k = 0; k <= F; k++)
     for (int t = L.frame_begin[k]; t < L.frame_begin[k + 1]; t++) tframe[t] = k;
+  std::vector<int> at_pos(N, -1);  // closure scratch: token -> element (reset after each closure)
   auto closure = [&](std::vector<Elem>* sub, int base) {
-    std::unordered_map<int, int> at;
+    struct AtMap {
+      std::vector<int>& pos;
+      std::vector<int> touched;
+      struct It {
+        int second;
+      };
+      int find_idx(int t) const { return pos[t]; }
+      void set(int t, int i) {
+        if (pos[t] < 0) touched.push_back(t);
+        pos[t] = i;
+      }
+      ~AtMap() {
+        for (int t : touched) pos[t] = -1;
+      }
+    } at{at_pos, {}};
     std::priority_queue<std::pair<int, int>, std::vector<std::pair<int, int>>, std::greater<std::pair<int, int>>>
         work;  // (frame, element), earliest frame first
     for (int i = 0; i < (int)sub->size(); i++) {
-      at[(*sub)[i].tok] = i;
+      at.set((*sub)[i].tok, i);
       work.push({tframe[(*sub)[i].tok], i});
     }
     while (!work.empty()) {
@@ -326,17 +374,17 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
       dbg_ext++;
       for (int li : outl[e.tok]) {
         const auto& l = L.links[li];
-        if (g.olabel[l.arc] != 0) continue;
+        if (lout[li] != 0) continue;
         Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}),
-               g.ilabel[l.arc] != 0 ? R.Succ(e.str, g.ilabel[l.arc]) : e.str};
-        auto it = at.find(n.tok);
-        if (it == at.end()) {
-          at[n.tok] = (int)sub->size();
+               lin[li] != 0 ? R.Succ(e.str, lin[li]) : e.str};
+        const int ei = at.find_idx(n.tok);
+        if (ei < 0) {
+          at.set(n.tok, (int)sub->size());
           work.push({tframe[n.tok], (int)sub->size()});
           sub->push_back(n);
-        } else if (ElemBetter(R, base, n, (*sub)[it->second])) {
-          (*sub)[it->second] = n;
-          work.push({tframe[n.tok], it->second});
+        } else if (ElemBetter(R, base, n, (*sub)[ei])) {
+          (*sub)[ei] = n;
+          work.push({tframe[n.tok], ei});
         }
       }
     }
@@ -411,10 +459,10 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
       for (const Elem& e : sub)
         for (int li : outl[e.tok]) {
           const auto& l = L.links[li];
-          const int w = g.olabel[l.arc];
+          const int w = lout[li];
           if (w == 0) continue;
           Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}),
-                 g.ilabel[l.arc] != 0 ? R.Succ(e.str, g.ilabel[l.arc]) : e.str};
+                 lin[li] != 0 ? R.Succ(e.str, lin[li]) : e.str};
           auto& v = by_word[w];
           bool merged = false;
           for (auto& x : v)
