@@ -226,6 +226,7 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_single_stream:
             out["single_stream"] = single_stream_latency(model, base)
+            out["concurrent_recognizers"] = concurrent_recognizers(model, base)
         if not args.no_cpu_baseline:
             nproc, cpu_model = cpu_info()
             workers = cpu_workers()
@@ -472,6 +473,49 @@ def single_stream_latency(model, base, seconds=30.0, chunk_bytes=8000):
             "xrt": round(seconds / (t1 - t0), 2),
             "chunk": "8000 B (0.25 s) per accept_waveform, test_simple.py pattern, 30 s stream; "
                      "results (MBR over the GPU lattice) included when an endpoint fires"}
+
+
+def concurrent_recognizers(model, base, threads=32, seconds=20.0, chunk_bytes=8000):
+    """`threads` KaldiRecognizers, one per Python thread (vosk-server's
+    shape), each fed 8000-byte chunks of its own stream; their engine calls
+    are coalesced into shared GPU steps (Engine::AdvanceCoalesced).  Reports
+    the aggregate xRT and the per-call latency percentiles."""
+    import threading
+    import vosk
+    datas = [pcm(stream_audio(base, 900 + i, int(seconds * SR))) for i in range(threads)]
+    m = vosk.Model(model)
+    recs = [vosk.KaldiRecognizer(m, SR) for _ in range(threads)]
+    for r in recs:  # warm up every slot
+        r.AcceptWaveform(datas[0][:chunk_bytes])
+        r.FinalResult()
+    lats = [[] for _ in range(threads)]
+    go = threading.Barrier(threads + 1)
+
+    def work(i):
+        rec, d, lat = recs[i], datas[i], lats[i]
+        go.wait()
+        for o in range(0, len(d), chunk_bytes):
+            ts = time.perf_counter()
+            if rec.AcceptWaveform(d[o:o + chunk_bytes]):
+                rec.Result()
+            lat.append(time.perf_counter() - ts)
+        rec.FinalResult()
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in th:
+        t.start()
+    go.wait()
+    t0 = time.perf_counter()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    lat = np.concatenate([np.array(x) for x in lats]) * 1e3
+    del recs
+    return {"threads": threads, "xrt": round(threads * seconds / el, 2),
+            "p50_accept_ms": round(float(np.percentile(lat, 50)), 3),
+            "p99_accept_ms": round(float(np.percentile(lat, 99)), 3),
+            "workload": f"{threads} KaldiRecognizers on {threads} threads, {seconds:.0f} s streams, "
+                        "8000-byte accept_waveform calls, Result on endpoints, FinalResult"}
 
 
 def run_dynamic(args, model, dist, rank, world):

@@ -1,0 +1,77 @@
+"""Concurrent KaldiRecognizers (one per thread, the reference's usual server
+shape: vosk-server runs one recognizer per connection on a thread pool,
+src/recognizer.cc:297-323 per call).  Their AcceptWaveform/FinalResult calls
+are coalesced into shared batched engine steps (Engine::AdvanceCoalesced);
+every stream's results must equal those of the same stream decoded alone.
+The second case caps the stream engine at 4 slots so the recognizers spread
+over several engines (Model::AllocStreamSlot)."""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import perturbed_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _pcm(x):
+    return np.asarray(x, np.float32).astype("<i2").tobytes()
+
+
+def _run(rec, data, out, key):
+    res = []
+    for i in range(0, len(data), 8000):
+        if rec.AcceptWaveform(data[i:i + 8000]):
+            res.append(json.loads(rec.Result()))
+    res.append(json.loads(rec.FinalResult()))
+    out[key] = res
+
+
+@pytest.mark.parametrize("max_streams", [None, 4])
+def test_concurrent_recognizers_match_sequential(synth_model_ep, test_wave, max_streams, monkeypatch):
+    import vosk
+    vosk.SetLogLevel(-1)
+    if max_streams:
+        monkeypatch.setenv("VOSK_AMD_MAX_STREAMS", str(max_streams))
+    waves = [_pcm(perturbed_stream(test_wave, 40 + i, seconds=8.0)) for i in range(10)]
+    m = vosk.Model(synth_model_ep)
+
+    alone = {}
+    for i, d in enumerate(waves):
+        rec = vosk.KaldiRecognizer(m, 16000)
+        rec.SetWords(True)
+        _run(rec, d, alone, i)
+        del rec
+
+    recs = []
+    for _ in waves:
+        r = vosk.KaldiRecognizer(m, 16000)
+        r.SetWords(True)
+        recs.append(r)
+    together, errs = {}, []
+
+    def work(i):
+        try:
+            _run(recs[i], waves[i], together, i)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(waves))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th)
+    assert not errs, errs
+    for i in range(len(waves)):
+        assert len(together[i]) == len(alone[i]) >= 2
+        for a, b in zip(alone[i], together[i]):
+            assert a["text"] == b["text"]
+            wa, wb = a.get("result", []), b.get("result", [])
+            assert [w["word"] for w in wa] == [w["word"] for w in wb]
+            for x, y in zip(wa, wb):
+                assert x["start"] == y["start"] and x["end"] == y["end"]
+                assert x["conf"] == pytest.approx(y["conf"], abs=1e-5)

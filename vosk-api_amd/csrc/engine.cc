@@ -763,7 +763,7 @@ Engine::~Engine() {
   if (fstream_) (void)hipStreamDestroy(fstream_);
 }
 
-int Engine::AllocSlot() {
+int Engine::TryAllocSlot() {
   std::lock_guard<std::mutex> lk(mu_);
   for (size_t i = 0; i < slots_.size(); i++)
     if (!slots_[i].used) {
@@ -772,7 +772,13 @@ int Engine::AllocSlot() {
       slots_[i].next_chunk = -plan_.priming_chunks;
       return (int)i;
     }
-  VAMD_ERR("all " << slots_.size() << " stream slots of the engine are in use");
+  return -1;
+}
+
+int Engine::AllocSlot() {
+  const int s = TryAllocSlot();
+  if (s < 0) VAMD_ERR("all " << slots_.size() << " stream slots of the engine are in use");
+  return s;
 }
 
 void Engine::FreeSlot(int slot) {
@@ -1667,42 +1673,55 @@ int Engine::IvectorFramesReady(int slot) const {
 }
 
 void Engine::UpdateSilenceWeights(int slot, int first_decoder_frame) {
+  UpdateSilenceWeights(std::vector<int>{slot}, std::vector<int>{first_decoder_frame});
+}
+
+void Engine::UpdateSilenceWeights(const std::vector<int>& slots, const std::vector<int>& first_decoder_frame) {
   if (!SilenceWeightingActive()) return;
-  int ready;
+  const size_t n = slots.size();
+  std::vector<int> ready(n, 0), with_path;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    const SlotHost& h = slots_.at(slot);
-    // statistics already accumulated without weights stay unweighted
-    if (!h.iv_weighted && h.iv_stats_done > 0) return;
-    ready = IvectorFramesReady(slot);
-  }
-  if (ready <= 0) return;
-  const Graph& g = md_->graph;
-  std::vector<int> tid, tok;
-  if (NumFramesDecoded(slot) > 0) {
-    std::vector<PathResult> pr;
-    BestPaths({slot}, false, &pr);
-    for (int a : pr[0].arcs) {
-      if (g.ilabel[a] == 0) continue;
-      // source state of the arc: the token it leaves (unique per frame and state)
-      const int src = (int)(std::upper_bound(g.arc_begin.begin(), g.arc_begin.end(), (int64_t)a) -
-                            g.arc_begin.begin()) - 1;
-      tid.push_back(g.ilabel[a]);
-      tok.push_back(src);
+    for (size_t i = 0; i < n; i++) {
+      const SlotHost& h = slots_.at(slots[i]);
+      // statistics already accumulated without weights stay unweighted
+      if (!h.iv_weighted && h.iv_stats_done > 0) continue;
+      ready[i] = IvectorFramesReady(slots[i]);
+      if (ready[i] > 0 && h.decoded > 0) with_path.push_back(slots[i]);
     }
   }
-  std::lock_guard<std::mutex> lk(mu_);
-  SlotHost& h = slots_.at(slot);
+  if (with_path.empty() && std::all_of(ready.begin(), ready.end(), [](int r) { return r <= 0; })) return;
+  std::vector<PathResult> pr;
+  if (!with_path.empty()) BestPaths(with_path, false, &pr);  // one traceback launch for all
+  const Graph& g = md_->graph;
   const ModelData& m = *md_;
   auto is_sil = [&m](int t) {
     const int ph = m.tm.tid2phone[t];
     return ph < (int)m.phone_is_silence.size() && m.phone_is_silence[ph] != 0;
   };
-  std::vector<std::pair<int, float>> d;
-  h.sw.ComputeCurrentTraceback(tid, tok);
-  h.sw.GetDeltaWeights(ready, first_decoder_frame, is_sil, &d);
-  h.iv_pending.insert(h.iv_pending.end(), d.begin(), d.end());
-  h.iv_weighted = true;
+  std::lock_guard<std::mutex> lk(mu_);
+  size_t k = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (ready[i] <= 0) continue;
+    std::vector<int> tid, tok;
+    if (k < with_path.size() && with_path[k] == slots[i]) {
+      for (int a : pr[k].arcs) {
+        if (g.ilabel[a] == 0) continue;
+        // source state of the arc: the token it leaves (unique per frame and state)
+        const int src = (int)(std::upper_bound(g.arc_begin.begin(), g.arc_begin.end(), (int64_t)a) -
+                              g.arc_begin.begin()) - 1;
+        tid.push_back(g.ilabel[a]);
+        tok.push_back(src);
+      }
+      k++;
+    }
+    SlotHost& h = slots_.at(slots[i]);
+    std::vector<std::pair<int, float>> d;
+    h.sw.ComputeCurrentTraceback(tid, tok);
+    h.sw.GetDeltaWeights(ready[i], first_decoder_frame[i], is_sil, &d);
+    h.iv_pending.insert(h.iv_pending.end(), d.begin(), d.end());
+    h.iv_weighted = true;
+  }
 }
 
 void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset) {

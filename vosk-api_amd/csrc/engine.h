@@ -12,7 +12,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdint>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -134,6 +136,67 @@ struct EngineCounters {
 
 constexpr int kMaxResampleTables = 32;  // distinct input sample rates per engine
 
+// Group commit of per-stream requests: callers on different threads (one
+// stream each) are served together by one batched call made by whichever
+// caller leads; each Run returns once a batch that started after its call
+// has served its stream (the batch's exception, if any, is rethrown in every
+// caller it served).
+class SlotGroupCommit {
+ public:
+  void Resize(int slots) {
+    req_.assign(slots, 0);
+    done_.assign(slots, 0);
+    err_.assign(slots, nullptr);
+  }
+  template <class BatchFn>
+  void Run(int slot, BatchFn&& fn) {
+    std::unique_lock<std::mutex> lk(mu_);
+    const long long ticket = ++req_.at(slot);
+    pending_.push_back(slot);
+    while (done_[slot] < ticket) {
+      if (leader_) {
+        cv_.wait(lk);
+        continue;
+      }
+      leader_ = true;  // lead batches until this caller's stream is served
+      while (done_[slot] < ticket && !pending_.empty()) {
+        std::vector<int> batch;
+        batch.swap(pending_);
+        std::vector<long long> tick;
+        for (int s : batch) tick.push_back(req_[s]);
+        lk.unlock();
+        std::exception_ptr e;
+        try {
+          fn(batch);
+        } catch (...) {
+          e = std::current_exception();
+        }
+        lk.lock();
+        for (size_t i = 0; i < batch.size(); i++) {
+          done_[batch[i]] = std::max(done_[batch[i]], tick[i]);
+          err_[batch[i]] = e;
+        }
+        cv_.notify_all();
+      }
+      leader_ = false;
+      cv_.notify_all();  // a waiting caller with a pending stream leads next
+    }
+    if (err_[slot]) {
+      std::exception_ptr e = err_[slot];
+      err_[slot] = nullptr;
+      std::rethrow_exception(e);
+    }
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<long long> req_, done_;  // per stream: request / served tickets
+  std::vector<std::exception_ptr> err_;
+  std::vector<int> pending_;
+  bool leader_ = false;
+};
+
 class Engine {
  public:
   Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg);
@@ -147,6 +210,7 @@ class Engine {
   std::mutex& mutex() { return mu_; }
 
   int AllocSlot();
+  int TryAllocSlot();  // -1 when every slot is in use
   void FreeSlot(int slot);
   // New utterance: features restart at sample 0, decoder restarts.
   void ResetPipeline(int slot);
@@ -234,6 +298,8 @@ class Engine {
   // an i-vector extractor or silence phones.  first_decoder_frame = feature
   // frame of the decoder segment's frame 0 (frame_offset * 3).
   void UpdateSilenceWeights(int slot, int first_decoder_frame);
+  // The same for several streams with one batched traceback.
+  void UpdateSilenceWeights(const std::vector<int>& slots, const std::vector<int>& first_decoder_frame);
   bool SilenceWeightingActive() const { return use_iv_ && !md_->endpoint.silence_phones.empty(); }
   // i-vector feature frames ready once the accepted samples are consumed
   // (OnlineNnet2FeaturePipeline::NumFramesReady: the splice's right context

@@ -89,16 +89,32 @@ Model::Model(const std::string& path) : md_(std::make_shared<ModelData>()) { md_
 
 int Model::FindWord(const std::string& w) const { return md_->words.Find(w); }
 
-Engine* Model::StreamEngine() {
-  std::lock_guard<std::mutex> lk(mu_);
-  return StreamEngineLocked();
+RecognizerGroup::RecognizerGroup(Engine* e) : engine(e), by_slot(e->config().max_slots, nullptr) {
+  gc.Resize(e->config().max_slots);
 }
 
-Engine* Model::GrammarEngine(const std::string& grammar) {
+RecognizerGroup* Model::AllocStreamSlot(int* slot) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& g : engines_) {
+    *slot = g->engine->TryAllocSlot();
+    if (*slot >= 0) return g.get();
+  }
+  EngineConfig cfg;
+  cfg.frames_per_chunk = md_->dcb.frames_per_chunk;
+  cfg.max_slots = EnvInt("VOSK_AMD_MAX_STREAMS", 64);
+  cfg.device = DeviceFromEnv();
+  cfg.max_step_samples = 4096;
+  cfg.lattice = true;  // results come from the segment's lattice (MBR)
+  engines_.emplace_back(new RecognizerGroup(new Engine(md_, cfg)));
+  *slot = engines_.back()->engine->AllocSlot();
+  return engines_.back().get();
+}
+
+RecognizerGroup* Model::GrammarEngine(const std::string& grammar) {
   std::lock_guard<std::mutex> lk(mu_);
   if (!md_->lookahead_hcl) {
     VAMD_WARN("Runtime graphs are not supported by this model");
-    return StreamEngineLocked();
+    return nullptr;
   }
   auto it = grammar_engines_.find(grammar);
   if (it != grammar_engines_.end()) return it->second.get();
@@ -114,22 +130,59 @@ Engine* Model::GrammarEngine(const std::string& grammar) {
   cfg.device = DeviceFromEnv();
   cfg.max_step_samples = 4096;
   cfg.lattice = true;
-  Engine* e = new Engine(md, cfg);
-  grammar_engines_[grammar].reset(e);
-  return e;
+  RecognizerGroup* grp = new RecognizerGroup(new Engine(md, cfg));
+  grammar_engines_[grammar].reset(grp);
+  return grp;
 }
 
-Engine* Model::StreamEngineLocked() {
-  if (!engine_) {
-    EngineConfig cfg;
-    cfg.frames_per_chunk = md_->dcb.frames_per_chunk;
-    cfg.max_slots = EnvInt("VOSK_AMD_MAX_STREAMS", 64);
-    cfg.device = DeviceFromEnv();
-    cfg.max_step_samples = 4096;
-    cfg.lattice = true;  // results come from the segment's lattice (MBR)
-    engine_.reset(new Engine(md_, cfg));
+void RecognizerGroup::Serve(const std::vector<int>& slots) {
+  std::vector<Recognizer*> rs;
+  for (int s : slots) rs.push_back(by_slot.at(s));
+  // pieces of 0.2 s as the reference's AcceptWaveform loop (src/recognizer.cc:305-311)
+  std::vector<int> step(rs.size());
+  size_t pieces = 1;
+  for (size_t i = 0; i < rs.size(); i++) {
+    step[i] = (int)(rs[i]->sample_frequency_ * 0.2f);
+    const size_t n = rs[i]->req_wave_ ? rs[i]->req_wave_->size() : 0;
+    pieces = std::max(pieces, (n + step[i] - 1) / step[i]);
   }
-  return engine_.get();
+  for (size_t p = 0; p < pieces; p++) {
+    std::vector<int> sl, first;
+    for (size_t i = 0; i < rs.size(); i++) {
+      Recognizer* r = rs[i];
+      const size_t n = r->req_wave_ ? r->req_wave_->size() : 0;
+      const size_t o = p * step[i];
+      if (o < n) {
+        engine->AcceptSamples(r->slot_, r->req_wave_->data() + o, (int)std::min<size_t>(step[i], n - o));
+      } else if (!(r->req_final_ && p == 0)) {
+        continue;  // a FinalResult request runs in the first piece only
+      }
+      sl.push_back(r->slot_);
+      first.push_back(r->frame_offset_ * 3);  // src/recognizer.cc:309, :825
+    }
+    if (sl.empty()) continue;
+    engine->UpdateSilenceWeights(sl, first);
+    engine->Advance(sl);
+  }
+  // EndpointDetected (src/recognizer.cc:318) of the AcceptWaveform requests
+  std::vector<int> ep;
+  std::vector<Recognizer*> er;
+  for (Recognizer* r : rs) {
+    r->req_endpoint_ = false;
+    if (!r->req_final_ && engine->NumFramesDecoded(r->slot_) > 0) {
+      ep.push_back(r->slot_);
+      er.push_back(r);
+    }
+  }
+  if (ep.empty()) return;
+  std::vector<PathResult> pr;
+  engine->BestPaths(ep, false, &pr);
+  const ModelData& m = engine->model();
+  const float shift = 0.01f * m.dcb.frame_subsampling_factor;
+  for (size_t i = 0; i < ep.size(); i++)
+    er[i]->req_endpoint_ = EndpointRulesFire(m.endpoint, engine->NumFramesDecoded(ep[i]),
+                                             TrailingSilenceFrames(m, pr[i].arcs), shift,
+                                             pr[i].final_relative_cost);
 }
 
 // ---------------------------------------------------------------------------
@@ -149,8 +202,11 @@ Recognizer::Recognizer(Model* model, float sr) : Recognizer(model, sr, (const ch
 Recognizer::Recognizer(Model* model, float sr, const char* grammar)
     : model_(model), sample_frequency_(sr) {
   const int rate = InputRate(sr);
-  engine_ = grammar ? model->GrammarEngine(grammar) : model->StreamEngine();
-  slot_ = engine_->AllocSlot();
+  group_ = grammar ? model->GrammarEngine(grammar) : nullptr;
+  if (group_) slot_ = group_->engine->AllocSlot();
+  else group_ = model->AllocStreamSlot(&slot_);
+  engine_ = group_->engine.get();
+  group_->by_slot.at(slot_) = this;
   try {
     engine_->SetSampleRate(slot_, rate);
   } catch (...) {
@@ -179,6 +235,7 @@ void Recognizer::SetSpkModel(SpkModel* spk) {
 }
 
 Recognizer::~Recognizer() {
+  group_->by_slot.at(slot_) = nullptr;
   engine_->FreeSlot(slot_);
   if (spk_) spk_->Unref();
   model_->Unref();
@@ -248,27 +305,18 @@ bool Recognizer::AcceptWaveform(const float* data, int len) {
 bool Recognizer::AcceptWaveform(std::vector<float>& w) {  // src/recognizer.cc:297-323
   if (!(state_ == RECOGNIZER_RUNNING || state_ == RECOGNIZER_INITIALIZED)) CleanUp();
   state_ = RECOGNIZER_RUNNING;
-  const int step = (int)(sample_frequency_ * 0.2f);
-  for (size_t i = 0; i < w.size(); i += step) {
-    const int n = (int)std::min<size_t>(step, w.size() - i);
-    engine_->AcceptSamples(slot_, w.data() + i, n);
-    engine_->UpdateSilenceWeights(slot_, frame_offset_ * 3);  // src/recognizer.cc:309
-    engine_->Advance({slot_});
-  }
+  const bool endpoint = Submit(&w, false);  // pieces, silence weights, decoding, endpoint
   samples_processed_ += w.size();
   if (spk_) spk_samples_.insert(spk_samples_.end(), w.begin(), w.end());  // src/recognizer.cc:314-316
-  return EndpointDetected();
+  return endpoint;
 }
 
-bool Recognizer::EndpointDetected() {
-  const int frames = engine_->NumFramesDecoded(slot_);
-  if (frames == 0) return false;
-  std::vector<PathResult> pr;
-  engine_->BestPaths({slot_}, false, &pr);
-  const ModelData& m = engine_->model();
-  const float shift = 0.01f * m.dcb.frame_subsampling_factor;
-  return EndpointRulesFire(m.endpoint, frames, TrailingSilenceFrames(m, pr[0].arcs), shift,
-                           pr[0].final_relative_cost);
+bool Recognizer::Submit(const std::vector<float>* wave, bool final) {
+  req_wave_ = wave;
+  req_final_ = final;
+  group_->gc.Run(slot_, [this](const std::vector<int>& slots) { group_->Serve(slots); });
+  req_wave_ = nullptr;
+  return req_endpoint_;
 }
 
 // ---------------------------------------------------------------------------
@@ -467,8 +515,7 @@ const char* Recognizer::Result() {  // src/recognizer.cc:808-816
 const char* Recognizer::FinalResult() {  // src/recognizer.cc:818-844
   if (state_ != RECOGNIZER_RUNNING) return StoreEmptyReturn();
   engine_->InputFinished(slot_);
-  engine_->UpdateSilenceWeights(slot_, frame_offset_ * 3);  // src/recognizer.cc:825
-  engine_->Advance({slot_});
+  Submit(nullptr, true);  // UpdateSilenceWeights + AdvanceDecoding (src/recognizer.cc:825-826)
   state_ = RECOGNIZER_FINALIZED;
   GetResult();
   return last_result_.c_str();

@@ -34,6 +34,22 @@ int TrailingSilenceFrames(const ModelData& m, const std::vector<int>& arcs);
 bool EndpointRulesFire(const EndpointConfig& c, int frames_decoded, int trailing_sil,
                        float frame_shift_s, float final_relative_cost);
 
+class Recognizer;
+
+// The streaming recognizers on one engine.  Applications run one recognizer
+// per connection thread (vosk-server); their AcceptWaveform / FinalResult
+// calls arriving together are served by one batched pass (group commit):
+// per 0.2-s piece one UpdateSilenceWeights traceback launch and one Advance
+// over all their streams, then one endpoint traceback launch, where each
+// call alone would run its own.  Per-stream results are unchanged.
+struct RecognizerGroup {
+  explicit RecognizerGroup(Engine* e);
+  std::unique_ptr<Engine> engine;
+  SlotGroupCommit gc;
+  std::vector<Recognizer*> by_slot;
+  void Serve(const std::vector<int>& slots);  // the leader's batched pass
+};
+
 class Model {
  public:
   explicit Model(const std::string& path);
@@ -43,21 +59,22 @@ class Model {
   }
   int FindWord(const std::string& w) const;
   const std::shared_ptr<ModelData>& data() const { return md_; }
-  // Engine shared by this model's streaming recognizers (created lazily).
-  Engine* StreamEngine();
+  // A free stream slot on one of the model's stream engines (created
+  // lazily; a new engine of VOSK_AMD_MAX_STREAMS slots when all are full).
+  RecognizerGroup* AllocStreamSlot(int* slot);
   // Engine of the grammar recognizers with this phrase list (JSON array of
   // strings, src/recognizer.cc:49-108): the runtime graph HCLr o G(grammar),
   // one engine per distinct grammar, created on first use.  Models without
-  // HCLr.fst warn and return the static-graph engine, as the reference does.
-  Engine* GrammarEngine(const std::string& grammar);
+  // HCLr.fst warn and return null (the caller takes a static-graph stream
+  // slot, as the reference falls back to its static graph).
+  RecognizerGroup* GrammarEngine(const std::string& grammar);
 
  private:
   ~Model() = default;
   std::shared_ptr<ModelData> md_;
-  std::unique_ptr<Engine> engine_;
-  std::map<std::string, std::unique_ptr<Engine>> grammar_engines_;
+  std::vector<std::unique_ptr<RecognizerGroup>> engines_;  // stream engines
+  std::map<std::string, std::unique_ptr<RecognizerGroup>> grammar_engines_;
   std::mutex mu_;
-  Engine* StreamEngineLocked();
   std::atomic<int> ref_{1};
 };
 
@@ -107,7 +124,6 @@ class Recognizer {
  private:
   bool AcceptWaveform(std::vector<float>& wave);
   void CleanUp();
-  bool EndpointDetected();
   const char* GetResult();
   const char* StoreEmptyReturn();
   const char* StoreReturn(const std::string& s);
@@ -116,9 +132,17 @@ class Recognizer {
   // frames on the best path -> x-vector on the GPU
   bool GetSpkVector(std::vector<float>* xvec, int* num_frames);
 
+  friend struct RecognizerGroup;
+  // AcceptWaveform / FinalResult through the group's batched pass
+  bool Submit(const std::vector<float>* wave, bool final);
+
   Model* model_;
+  RecognizerGroup* group_ = nullptr;
   Engine* engine_;
   int slot_;
+  // the request the group's batched pass serves (Submit)
+  const std::vector<float>* req_wave_ = nullptr;
+  bool req_final_ = false, req_endpoint_ = false;
   float sample_frequency_;
   int max_alternatives_ = 0;
   bool words_ = false, partial_words_ = false, nlsml_ = false;
