@@ -284,20 +284,33 @@ def run_api(args, model, dist, rank, world, base):
                 texts[i] = texts[i] + " " + json.loads(res)["text"]
                 nres[0] += 1
 
+    parts = {True: np.zeros(3), False: np.zeros(3)}  # chunk round? -> feed, wait, collect seconds
+    nparts = {True: 0, False: 0}
+    spc = 8160 * 2  # bytes per 51-frame chunk (samples_per_chunk, batch_model.cc:84-88)
+
     def feed_round(k):
         o = k * FEED_BYTES
+        t0 = time.perf_counter()
         for i in range(S):
             recs[i].AcceptWaveform(datas[i][o:o + FEED_BYTES])
+        t1 = time.perf_counter()
         bm.Wait()
+        t2 = time.perf_counter()
         collect()
+        t3 = time.perf_counter()
+        kind = ((k + 1) * FEED_BYTES) // spc > (k * FEED_BYTES) // spc
+        parts[kind] += (t1 - t0, t2 - t1, t3 - t2)
+        nparts[kind] += 1
 
     for k in range(W):
         feed_round(k)
+    for kind in parts:
+        parts[kind][:] = 0
+        nparts[kind] = 0
     for lane in range(ve.batch_lanes(bm)):
         ve.batch_lane_stats(bm, lane, reset=True)
     if dist is not None:
         dist.barrier()
-    spc = 8160 * 2  # bytes per 51-frame chunk (samples_per_chunk, batch_model.cc:84-88)
     lat = []
     t0 = time.perf_counter()
     for k in range(W, rounds):
@@ -359,6 +372,10 @@ def run_api(args, model, dist, rank, world, base):
         "latency_definition": "wall time of a feeding round that completes a chunk: AcceptWaveform "
                               "(Push) of every stream -> Wait() -> results collected",
         "finish_ms": round((t1 - tf) * 1e3, 3),
+        "round_parts_ms": {("chunk_rounds" if kind else "other_rounds"): {
+            "rounds": nparts[kind], **{n: round(float(v) / max(nparts[kind], 1) * 1e3, 3)
+                                       for n, v in zip(("feed", "wait", "collect"), parts[kind])}}
+            for kind in (True, False)},
         "roofline": decoder_roofline(dec_ms, dec_n, tot, "decode_kernel"),
         "roofline_nnet": {"bound": "mfma", "kernel": "nnet GEMM launches", "achieved": round(nnet_tflops, 4),
                           "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": nnet_tflops / FP32_PEAK_TFLOPS},

@@ -43,6 +43,10 @@ constexpr int kHashCap = 4096;        // LDS frame table slots (power of two)
 constexpr int kHashBits = 12;
 constexpr int kMaxProbe = 2;          // LDS buckets a state may use (DecArgs::lds_probe: 0 all HBM, 1 one bucket)
 constexpr int kFrontLds = 2048;       // epsilon frontier entries in LDS (more spill to HBM)
+// emitting-pass backpointers resolved at commit from the frame's link
+// records (no per-sub-round winner barrier) while the link arena has at
+// least this much room left; otherwise the sub-round winner checks run
+constexpr long long kDeferHeadroom = 1 << 20;
 constexpr int kUnroll = 4;            // (token, arc) items in flight per thread in the emitting pass
 constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
 constexpr int kNoSlot = 0x7fffffff;   // no frame-table slot
@@ -514,7 +518,7 @@ __device__ __forceinline__ int get_front(const FrameLds& t, const DecPtrs& p, in
 // index, arc, acoustic cost bits}.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long long used, int slot,
-                                          int4 rec, int dslot) {
+                                          int4 rec, int dslot, bool defer) {
   const unsigned long long m = __ballot(1);
   const int lane = threadIdx.x & 63;
   const int leader = __ffsll((long long)m) - 1;
@@ -528,6 +532,7 @@ __device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long 
     a.link_dst[(long long)slot * a.link_cap + pos] = dslot;
   } else {
     sh.lat_ovf = 1;
+    if (defer) sh.bad |= 32;  // the record held a backpointer candidate (deferred winners)
   }
 }
 
@@ -539,9 +544,13 @@ __device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long 
 __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh, const FrameLds& t,
                                  const HbmTab& T, const DecPtrs& p, const TokView& tv, int ntok,
                                  float cutoff, float cost_offset, const float* Lp, int mode,
-                                 float bound, int* examined, const DecSlot& st, int slot, Prof& pr) {
+                                 float bound, int* examined, const DecSlot& st, int slot, bool defer,
+                                 Prof& pr) {
   float m = __int_as_float(0x7f800000);
+  // defer: every relaxation leaves a link record and the winners are
+  // resolved from the records at commit (commit_emit_links)
   const bool lat = a.links != nullptr && mode == 1;
+  defer = defer && lat;
   for (int c0 = 0; c0 < ntok; c0 += DT) {
     const int i = c0 + threadIdx.x;
     int deg = 0, ab = 0, src = 0;
@@ -603,12 +612,12 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
           if (lat)
             emit_link(a, sh, st.links_used, slot,
                       make_int4(sh.tsrc[jv[u]], __float_as_int(totv[u]), arcv[u], __float_as_int(acv[u])),
-                      sv[u]);
+                      sv[u], defer);
           if (cr[u] && de[u]) push_front(a, sh, t, p, 0, &sh.n_front, sv[u]);
         }
       }
       pr.mark(3);
-      if (mode == 1) {
+      if (mode == 1 && !defer) {
         // the relaxations' key minima are issued without waiting for them
         // (no-return atomics): wait for their completion (vmcnt, no cache
         // maintenance) before the barrier, so every winner check below reads
@@ -622,6 +631,9 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
         pr.mark(4);
       }
     }
+    // deferred: the keys' no-return minima complete before the chunk's
+    // barrier (the epsilon closure and the commit read them)
+    if (defer) vm_drain();
     __syncthreads();
     pr.mark(2);
   }
@@ -724,36 +736,52 @@ __device__ __forceinline__ void hbm_clear_all(const DecArgs& a, const HbmTab& T)
   }
 }
 
-// Lattice side of a commit (all threads; the frame tables are still intact):
-// keep this frame's emitting records below the cutoff, resolved to arena
-// indices through their destination slots (chunked in-place compaction:
-// writes never pass the chunk being read), then the epsilon links of the
-// committed tokens that have epsilon arcs (listed by the commit in the
-// frontier arrays, neps of them).  Every kept link's cost above its
-// destination's, tot - cost(dst) >= 0 (the link's extra cost over the
-// destination for PruneActiveTokens), replaces its destination slot in
-// link_dst.  Returns the frame's link count.
-__device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
-                            const DecPtrs& p, const DecSlot& st, int slot, int base, int nl_n,
-                            int neps, float cutoff, Prof& pr) {
+// Lattice side of a commit (all threads; the frame tables are still intact).
+// commit_emit_links: keep this frame's emitting records below the cutoff,
+// resolved to arena indices through their destination slots (chunked
+// in-place compaction: writes never pass the chunk being read); with
+// deferred winners a kept record whose (cost, arc) key is its destination's
+// final key writes its source as the destination's backpointer (exactly one
+// relaxation per surviving slot holds the final key: emitting arcs are
+// relaxed once per frame, and a slot an epsilon arc improved holds an
+// epsilon key).  commit_eps_links: the epsilon links of the committed tokens
+// that have epsilon arcs (listed by the commit in the frontier arrays, neps
+// of them).  Every kept link's cost above its destination's, tot - cost(dst)
+// >= 0 (the link's extra cost over the destination for PruneActiveTokens),
+// replaces its destination slot in link_dst.
+__device__ __forceinline__ int commit_emit_links(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                                 const HbmTab& T, const DecSlot& st, int slot, int base,
+                                                 int nl_n, float cutoff, bool defer) {
   int4* L = a.links + (long long)slot * a.link_cap;
   int* LD = a.link_dst + (long long)slot * a.link_cap;
   const long long lb = st.links_used;
   long long nrec = sh.n_links;
   if (lb + nrec > a.link_cap) nrec = a.link_cap - lb > 0 ? a.link_cap - lb : 0;
   int out = 0;
+  // records of the next chunk are loaded while this one is compacted
+  int4 rn = make_int4(0, 0, 0, 0);
+  int vn = kNoSlot;
+  if (threadIdx.x < nrec) {
+    rn = L[lb + threadIdx.x];
+    vn = LD[lb + threadIdx.x];
+  }
   for (long long c0 = 0; c0 < nrec; c0 += DT) {
     const long long i = c0 + threadIdx.x;
     int keep = 0;
-    int4 r = make_int4(0, 0, 0, 0);
+    int4 r = rn;
+    const int v = vn;
+    if (i + DT < nrec) {
+      rn = L[lb + i + DT];
+      vn = LD[lb + i + DT];
+    }
     float d = 0.0f;
     if (i < nrec) {
-      r = L[lb + i];
       const float tot = __int_as_float(r.y);
-      const int v = LD[lb + i];
       if (tot < cutoff && v != kNoSlot) {  // (kNoSlot: a failed relaxation, the frame is in error)
+        const unsigned long long key = slot_key(t, T, v);
+        if (defer && key == (((unsigned long long)ford(tot) << 32) | (unsigned)r.z)) set_bp(t, T, v, r.x);
         r.y = base + slot_pos(t, T, nl_n, v);
-        d = tot - funord((uint32_t)(slot_key(t, T, v) >> 32));
+        d = tot - funord((uint32_t)(key >> 32));
         keep = 1;
       }
     }
@@ -765,7 +793,17 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
     out += sh.total;
     __syncthreads();
   }
-  pr.mark(7);
+  if (defer) vm_drain();  // HBM backpointers visible to the token commit after its barrier
+  return out;
+}
+
+__device__ __forceinline__ int commit_eps_links(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                                const HbmTab& T, const DecPtrs& p, const DecSlot& st,
+                                                int slot, int base, int nl_n, int neps, int out,
+                                                float cutoff) {
+  int4* L = a.links + (long long)slot * a.link_cap;
+  int* LD = a.link_dst + (long long)slot * a.link_cap;
+  const long long lb = st.links_used;
   // epsilon links of the committed tokens, at their final costs
   if (threadIdx.x == 0) sh.n_eps = 0;
   for (int c0 = 0; c0 < neps; c0 += DT) {
@@ -811,9 +849,9 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
     }
     __syncthreads();
   }
-  pr.mark(8);
+  const long long nrec = sh.n_links;
   const int n = out + sh.n_eps;
-  if (nrec < sh.n_links || lb + n > a.link_cap) sh.lat_ovf = 1;
+  if (lb + nrec > a.link_cap || lb + n > a.link_cap) sh.lat_ovf = 1;
   return lb + n > a.link_cap ? (int)(a.link_cap - lb) : n;
 }
 
@@ -823,7 +861,7 @@ __device__ __forceinline__ int commit_links(const DecArgs& a, DecShared& sh, con
 // next_cutoff) keep an arena slot marked dead.  Then both tables are cleared.
 __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds& t, DecPtrs& p, DecSlot& st,
                        int* TS, float* TC, bool* lds, float cutoff, float* best_out, int slot,
-                       int* nlinks, Prof& pr) {
+                       int* nlinks, bool defer, Prof& pr) {
   __syncthreads();
   const HbmTab T = hbm_tab(a, slot);
   const int nl_n = sh.n_new_l;
@@ -832,6 +870,10 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   const int base = st.arena_used;
   const bool ok = (long long)base + n <= a.arena_cap;
   const bool lat = a.links != nullptr;
+  // the emitting records first: with deferred winners they set the
+  // backpointers the token commit below reads
+  const int n_emit = (lat && ok) ? commit_emit_links(a, sh, t, T, st, slot, base, nl_n, cutoff, defer) : 0;
+  pr.mark(7);
   if (threadIdx.x == 0) {
     sh.n_next = 0;
     sh.n_front = 0;
@@ -896,7 +938,8 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   if (!ok) sh.bad |= 2;
   const int live = sh.n_next;
   const int neps = sh.n_front < kFrontLds + a.max_tok ? sh.n_front : kFrontLds + a.max_tok;
-  *nlinks = (lat && ok) ? commit_links(a, sh, t, T, p, st, slot, base, nl_n, neps, cutoff, pr) : 0;
+  *nlinks = (lat && ok) ? commit_eps_links(a, sh, t, T, p, st, slot, base, nl_n, neps, n_emit, cutoff) : 0;
+  pr.mark(8);
   __syncthreads();
   hbm_clear_listed(T, ng);
   lds_clear_build(t);
@@ -1336,7 +1379,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     eps_closure(a, sh, t, T, p, st, a.beam, 1, &arcs_eps, pr);
     float b;
     int nl = 0;
-    commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, &nl, pr);
+    commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, &nl, false, pr);
     frame_done(a, sh, st, slot, 0, a.beam, 0.0f, nl);
   } else if (st.ntok > 0 && st.ntok <= kTokLds) {
     for (int i = threadIdx.x; i < st.ntok; i += DT) {
@@ -1436,6 +1479,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     pr.mark(1);
     const float seed = sh.seed;
     int examined = 0;
+    const bool defer = a.links != nullptr && a.link_cap - st.links_used >= kDeferHeadroom;
     float next_cutoff, new_best;
     // one emitting pass relaxing below the seed bound (a superset), then the
     // epsilon closure; tokens whose best cost is not below the final
@@ -1445,17 +1489,17 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     // the exact two-pass form runs.
     if (seed != __int_as_float(0x7f800000)) {
       const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
-                                      &examined, st, slot, pr);
+                                      &examined, st, slot, defer, pr);
       next_cutoff = seed;
       if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
     } else {
       const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
-                                      &examined, st, slot, pr);
+                                      &examined, st, slot, false, pr);
       next_cutoff = seed;
       if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
       int dummy = 0;
       expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy, st,
-                      slot, pr);
+                      slot, defer, pr);
     }
     __syncthreads();
     pr.mark(2);
@@ -1471,7 +1515,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       }
     }
     int nl = 0;
-    commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, &nl, pr);
+    commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, &nl, defer, pr);
     pr.count(15, 1);
     frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset, nl);
     st.offset_sum += (double)cost_offset;

@@ -119,7 +119,8 @@ struct DecSlot {
   int frames;       // frames decoded since the last reset
   int stamp;        // epsilon-closure round stamp (monotonic; HBM table stamps)
   int err;          // bit 0: token list / table overflow, bit 1: arena overflow, bit 2: no tokens,
-                    // bit 3: unplaceable backpointer source, bit 4: pruning lost a backpointer
+                    // bit 3: unplaceable backpointer source, bit 4: pruning lost a backpointer,
+                    // bit 5: a link record with a backpointer candidate did not fit (deferred winners)
   int lat_ovf;      // lattice: 1 = link arena or frame table overflowed (results fall back to 1-best)
   int prune_from;   // first LatFrame whose extra costs were never computed (PruneActiveTokens)
   double offset_sum;
