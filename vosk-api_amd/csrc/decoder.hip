@@ -47,7 +47,10 @@ constexpr int kFrontLds = 2048;       // epsilon frontier entries in LDS (more s
 // records (no per-sub-round winner barrier) while the link arena has at
 // least this much room left; otherwise the sub-round winner checks run
 constexpr long long kDeferHeadroom = 1 << 20;
-constexpr int kUnroll = 4;            // (token, arc) items in flight per thread in the emitting pass
+#ifndef VAMD_DEC_UNROLL
+#define VAMD_DEC_UNROLL 4
+#endif
+constexpr int kUnroll = VAMD_DEC_UNROLL;            // (token, arc) items in flight per thread in the emitting pass
 constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
 constexpr int kNoSlot = 0x7fffffff;   // no frame-table slot
 constexpr unsigned kDestEps = 0x80000000u;  // arcs[].w: nextstate has epsilon arcs
@@ -604,8 +607,10 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
         de[u] = ((unsigned)A[u].w & kDestEps) != 0;
         kv[u] = ((unsigned long long)ford(totv[u]) << 32) | (unsigned)arcv[u];
       }
+      pr.mark(3);
       if (mode == 1) {
         relax_batch(a, sh, t, T, dst, kv, de, want, sv, cr);
+        pr.mark(22);
 #pragma unroll
         for (int u = 0; u < kUnroll; u++) {
           if (!want[u]) continue;
@@ -616,7 +621,7 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
           if (cr[u] && de[u]) push_front(a, sh, t, p, 0, &sh.n_front, sv[u]);
         }
       }
-      pr.mark(3);
+      pr.mark(23);
       if (mode == 1 && !defer) {
         // the relaxations' key minima are issued without waiting for them
         // (no-return atomics): wait for their completion (vmcnt, no cache
@@ -880,24 +885,41 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   }
   __syncthreads();
   unsigned long long bk = kEmpty;
-  for (int j = threadIdx.x; j < n; j += DT) {
-    int s, bp, v;
-    unsigned long long k;
-    bool has_eps;
+  for (int j0 = threadIdx.x; j0 < n; j0 += 2 * DT) {
+   // two entries per thread: the HBM entries' dependent loads in flight together
+   int sq[2], bpq[2], vq[2];
+   unsigned long long kq[2];
+   bool eq[2];
+#pragma unroll
+   for (int q = 0; q < 2; q++) {
+    const int j = j0 + q * DT;
+    vq[q] = j < nl_n ? (int)t.nl[j] : j < n ? ~AG_LD(&T.list[j - nl_n]) : 0;
+   }
+#pragma unroll
+   for (int q = 0; q < 2; q++) {
+    const int j = j0 + q * DT;
+    if (j >= n) continue;
+    const int v = vq[q];
     if (j < nl_n) {
-      v = t.nl[j];
-      s = t.hs[v];
-      k = t.hk[v];
-      bp = t.hb[v];
-      has_eps = (t.hp[v] & kPosEps) != 0;
+      sq[q] = t.hs[v];
+      kq[q] = t.hk[v];
+      bpq[q] = t.hb[v];
+      eq[q] = (t.hp[v] & kPosEps) != 0;
     } else {
-      const int g = AG_LD(&T.list[j - nl_n]);
-      v = ~g;
-      s = AG_LD(&T.state[g]);
-      k = AG_LD(&T.key[g]);
-      bp = AG_LD(&T.bp[g]);
-      has_eps = (AG_LD(&T.pos[g]) & kHPosEps) != 0;
+      const int g = ~v;
+      sq[q] = AG_LD(&T.state[g]);
+      kq[q] = AG_LD(&T.key[g]);
+      bpq[q] = AG_LD(&T.bp[g]);
+      eq[q] = (AG_LD(&T.pos[g]) & kHPosEps) != 0;
     }
+   }
+#pragma unroll
+   for (int q = 0; q < 2; q++) {
+    const int j = j0 + q * DT;
+    if (j >= n) continue;
+    const int s = sq[q], bp = bpq[q], v = vq[q];
+    const unsigned long long k = kq[q];
+    const bool has_eps = eq[q];
     const int arc = (int)(unsigned)(k & 0xffffffffu);
     const float cost = funord((uint32_t)(k >> 32));
     if (ok && cost < cutoff) {
@@ -931,6 +953,7 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
     } else if (ok) {
       ag_st4(&p.arena[base + j], make_int4(-2, -1, __float_as_int(cost), s));  // dead list entry
     }
+   }
   }
   bk = block_min_u64(sh, bk);  // ends with a barrier
   pr.mark(6);

@@ -364,9 +364,9 @@ class Engine:
     PHASES = ("cutoff", "seed", "exp_tokens", "exp_items", "exp_winners", "eps", "commit_toks",
               "commit_links", "commit_eps_links", "commit_clear", "prune", "n_hbm_created",
               "n_created", "n_eps_rounds", "n_chunks", "frames", "prune_walk", "prune_remap",
-              "prune_links", "prune_move", "n_prune_frames", "n_prunes", "-", "-")
-    PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19]  # the clock slots (the rest count)
-    PHASE_CLOCKS = PHASES[:11] + PHASES[16:20]
+              "prune_links", "prune_move", "n_prune_frames", "n_prunes", "exp_relax", "exp_links")
+    PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19, 22, 23]  # the clock slots (the rest count)
+    PHASE_CLOCKS = PHASES[:11] + PHASES[16:20] + PHASES[22:24]
 
     def decoder_phases_per_stream(self):
         """[max_streams, len(PHASES)] int64: decoder_phases() per stream slot."""
