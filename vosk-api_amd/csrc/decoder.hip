@@ -77,6 +77,7 @@ struct DecShared {
   int n_new_l, n_new_g, n_next, n_front, n_fnext, total, sel_k, n_links, lat_ovf, n_eps;
   unsigned sel_prefix, sel_mask;
   float seed;
+  unsigned run_bound;  // emitting pass: running next_cutoff bound (ordered float bits)
   int bad, flag, kk;
   int fl[8];                  // FixRound flags (two sets of three) + change flags
   unsigned char kbits[DT];    // pruning: per-thread keep bits of the chunk
@@ -547,9 +548,14 @@ __device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long 
 __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh, const FrameLds& t,
                                  const HbmTab& T, const DecPtrs& p, const TokView& tv, int ntok,
                                  float cutoff, float cost_offset, const float* Lp, int mode,
-                                 float bound, int* examined, const DecSlot& st, int slot, bool defer,
-                                 Prof& pr) {
+                                 float bound, float adaptive, int* examined, const DecSlot& st, int slot,
+                                 bool defer, Prof& pr) {
   float m = __int_as_float(0x7f800000);
+  // Running bound (Kaldi's running next_cutoff): min(bound, tot + adaptive)
+  // over the relaxations seen so far.  It never falls below the pass's final
+  // next_cutoff (min over all of tot + adaptive), so a relaxation at or
+  // above it could only create an entry the commit drops as dead.
+  if (threadIdx.x == 0) sh.run_bound = ford(bound);
   // defer: every relaxation leaves a link record and the winners are
   // resolved from the records at commit (commit_emit_links)
   const bool lat = a.links != nullptr && mode == 1;
@@ -594,6 +600,10 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
       unsigned long long kv[kUnroll];
       float acv[kUnroll], totv[kUnroll];
       bool want[kUnroll], de[kUnroll], cr[kUnroll];
+      const float rb = mode == 1 ? funord(__hip_atomic_load(&sh.run_bound, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_WORKGROUP))
+                                 : bound;
+      float wm = __int_as_float(0x7f800000);
 #pragma unroll
       for (int u = 0; u < kUnroll; u++) {
         want[u] = false;
@@ -602,13 +612,16 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
         acv[u] = cost_offset - Lp[A[u].z];
         totv[u] = (sh.tcost[j] + acv[u]) + __int_as_float(A[u].y);
         m = fminf(m, totv[u]);
-        want[u] = mode == 1 && totv[u] < bound;
+        wm = fminf(wm, totv[u]);
+        want[u] = mode == 1 && totv[u] < rb;
         dst[u] = A[u].x;
         de[u] = ((unsigned)A[u].w & kDestEps) != 0;
         kv[u] = ((unsigned long long)ford(totv[u]) << 32) | (unsigned)arcv[u];
       }
       pr.mark(3);
       if (mode == 1) {
+        wm = wave_min_f(wm);
+        if ((threadIdx.x & 63) == 0 && wm + adaptive < rb) atomicMin(&sh.run_bound, ford(wm + adaptive));
         relax_batch(a, sh, t, T, dst, kv, de, want, sv, cr);
         pr.mark(22);
 #pragma unroll
@@ -1511,17 +1524,17 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     // next_cutoff pass creates, with the same keys.  Without a finite seed
     // the exact two-pass form runs.
     if (seed != __int_as_float(0x7f800000)) {
-      const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed,
+      const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed, adaptive,
                                       &examined, st, slot, defer, pr);
       next_cutoff = seed;
       if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
     } else {
-      const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f,
+      const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 0, 0.0f, adaptive,
                                       &examined, st, slot, false, pr);
       next_cutoff = seed;
       if (m + adaptive < next_cutoff) next_cutoff = m + adaptive;
       int dummy = 0;
-      expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, &dummy, st,
+      expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, adaptive, &dummy, st,
                       slot, defer, pr);
     }
     __syncthreads();
