@@ -560,17 +560,26 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
   // resolved from the records at commit (commit_emit_links)
   const bool lat = a.links != nullptr && mode == 1;
   defer = defer && lat;
+  // the next chunk's token (cost, state, list position) is loaded while
+  // this chunk's arcs are processed
+  float cn = 0.0f;
+  int sn = 0, pn = 0;
+  if ((int)threadIdx.x < ntok) {
+    cn = tv.c(threadIdx.x);
+    sn = tv.s(threadIdx.x);
+    if (mode == 1) pn = AG_LD(&p.cp[threadIdx.x]);
+  }
   for (int c0 = 0; c0 < ntok; c0 += DT) {
     const int i = c0 + threadIdx.x;
     int deg = 0, ab = 0, src = 0;
     float c = 0.0f;
     if (i < ntok) {
-      c = tv.c(i);
+      c = cn;
       if (c <= cutoff) {
-        const int4 si = a.sinfo[tv.s(i)];
+        const int4 si = a.sinfo[sn];
         ab = si.x;
         deg = si.y - si.x;
-        if (mode == 1) src = st.cur_base + AG_LD(&p.cp[i]);
+        if (mode == 1) src = st.cur_base + pn;
       }
     }
     block_scan(sh, deg);
@@ -578,6 +587,11 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
     sh.tcost[threadIdx.x] = c;
     sh.tsrc[threadIdx.x] = src;
     __syncthreads();
+    if (i + DT < ntok) {
+      cn = tv.c(i + DT);
+      sn = tv.s(i + DT);
+      if (mode == 1) pn = AG_LD(&p.cp[i + DT]);
+    }
     pr.mark(2);
     pr.count(14, 1);
     const int total = sh.total;
