@@ -967,9 +967,13 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
       }
       ag_st4(&p.arena[base + j], make_int4(prev, arc, __float_as_int(cost), s));
       const int q = atomicAdd(&sh.n_next, 1);
-      AG_ST(&p.cs[q], s);
-      AG_ST(&p.cc[q], cost);
-      AG_ST(&p.cp[q], j);
+      if (q < a.max_tok) {  // the current-token arrays hold max_tok entries
+        AG_ST(&p.cs[q], s);
+        AG_ST(&p.cc[q], cost);
+        AG_ST(&p.cp[q], j);
+      } else {
+        sh.bad |= 1;
+      }
       if (q < kTokLds) {
         TS[q] = s;
         TC[q] = cost;
@@ -986,7 +990,7 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   pr.mark(6);
   pr.count(12, n);
   if (!ok) sh.bad |= 2;
-  const int live = sh.n_next;
+  const int live = sh.n_next < a.max_tok ? sh.n_next : a.max_tok;
   const int neps = sh.n_front < kFrontLds + a.max_tok ? sh.n_front : kFrontLds + a.max_tok;
   *nlinks = (lat && ok) ? commit_eps_links(a, sh, t, T, p, st, slot, base, nl_n, neps, n_emit, cutoff) : 0;
   pr.mark(8);

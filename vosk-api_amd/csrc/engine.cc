@@ -658,6 +658,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   dec_.llh = d_llh_;
   // bounded per-stream decoder state (decoder.hip): one HBM frame table of
   // H >= 2 * max_tokens slots for the states a frame's LDS table cannot hold
+  if (const char* mt = getenv("VOSK_AMD_DEC_MAX_TOKENS")) cfg_.max_tokens = std::max(64, atoi(mt));  // tests
   const long long MT = cfg_.max_tokens;
   int hbits = 10;
   while ((1ll << hbits) < 2 * MT) hbits++;
