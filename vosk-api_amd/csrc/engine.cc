@@ -722,6 +722,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   LaunchInitTables(dec_.ht_state, dec_.ht_key, dec_.ht_stamp, S * H, stream_);
 
   // ---- staging
+  stage_sample_cap_ = (size_t)S * cfg_.max_step_samples;
   stage_bytes_ = Align256(sizeof(float) * (size_t)S * cfg_.max_step_samples) +
                  2 * Align256(sizeof(SampleJob) * S) + Align256(sizeof(ResampleJob) * S) +
                  Align256(sizeof(MfccJob) * S) +
@@ -839,6 +840,24 @@ void Engine::AcceptSamples(int slot, const float* x, int n) {
   h.pending.insert(h.pending.end(), x, x + n);
 }
 
+void Engine::AcceptSamples(int slot, std::vector<float>&& x) {
+  std::lock_guard<std::mutex> lk(mu_);
+  SlotHost& h = slots_.at(slot);
+  if (h.finished) VAMD_ERR("AcceptSamples after InputFinished");
+  if (h.pending_pos == h.pending.size()) {
+    h.pending.swap(x);
+    h.pending_pos = 0;
+  } else {
+    h.pending.insert(h.pending.end(), x.begin(), x.end());
+  }
+}
+
+void Engine::StageSamples(const float* x, size_t n) {
+  if (st_sample_n_ + n > stage_sample_cap_) VAMD_ERR("step staging overflow (samples)");
+  memcpy(st_sample_data_ + st_sample_n_, x, sizeof(float) * n);
+  st_sample_n_ += n;
+}
+
 void Engine::SetSampleRate(int slot, int rate) {
   std::lock_guard<std::mutex> lk(mu_);
   DEVICE_GUARD();
@@ -924,7 +943,8 @@ const std::vector<FrameStat>& Engine::LastStats(int slot) const { return slots_.
 bool Engine::BuildStep(const std::vector<int>& slots) {
   st_samples_.clear();
   st_sample_src_.clear();
-  st_sample_data_.clear();
+  st_sample_data_ = (float*)(h_stage_ + (size_t)(seq_ % 3) * stage_bytes_);  // RunStep's buffer
+  st_sample_n_ = 0;
   st_raw_.clear();
   st_raw_src_.clear();
   st_res_.clear();
@@ -957,8 +977,7 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
                                        : (long long)(h.pending.size() - h.pending_pos);
       long long n = std::min<long long>(avail, max_raw_step_);
       if (!from_res)  // host-fed samples share the step's staging buffer
-        n = std::min<long long>(n, (long long)slots_.size() * cfg_.max_step_samples -
-                                       (long long)st_sample_data_.size());
+        n = std::min<long long>(n, (long long)stage_sample_cap_ - (long long)st_sample_n_);
       if (n < 0) n = 0;
       auto ends_after = [&](long long nn) {
         return nn == avail && (from_res ? h.resident_finish : h.finished);
@@ -980,9 +999,8 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
           if (h.resident_pos == h.resident_n && h.resident_finish) h.finished = true;
         } else {
           st_raw_.push_back(SampleJob{s, pos, (int)n, 0, nullptr});
-          st_raw_src_.push_back((int)st_sample_data_.size());
-          st_sample_data_.insert(st_sample_data_.end(), h.pending.begin() + h.pending_pos,
-                                 h.pending.begin() + h.pending_pos + n);
+          st_raw_src_.push_back((int)st_sample_n_);
+          StageSamples(h.pending.data() + h.pending_pos, (size_t)n);
           h.pending_pos += n;
         }
         h.raw_pushed += n;
@@ -1009,9 +1027,8 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
       int n = std::min(avail, cfg_.max_step_samples);
       if (n > 0) {
         st_samples_.push_back(SampleJob{s, (int)(h.samples & (sample_ring_ - 1)), n, 0, nullptr});
-        st_sample_src_.push_back((int)st_sample_data_.size());
-        st_sample_data_.insert(st_sample_data_.end(), h.pending.begin() + h.pending_pos,
-                               h.pending.begin() + h.pending_pos + n);
+        st_sample_src_.push_back((int)st_sample_n_);
+        StageSamples(h.pending.data() + h.pending_pos, (size_t)n);
         h.pending_pos += n;
         h.samples += n;
         any = true;
@@ -1231,7 +1248,10 @@ void Engine::RunStep(bool allow_pipeline) {
     off += Align256(bytes);
     return o;
   };
-  size_t o_data = put(st_sample_data_.data(), sizeof(float) * st_sample_data_.size());
+  // the samples are already in place (BuildStep wrote them into this buffer)
+  if (st_sample_n_ > 0 && (char*)st_sample_data_ != hs) VAMD_ERR("staging buffer mismatch");
+  const size_t o_data = 0;
+  off = Align256(sizeof(float) * st_sample_n_);
   for (size_t i = 0; i < st_samples_.size(); i++)
     if (st_sample_src_[i] >= 0)
       st_samples_[i].src = (const float*)(dsg + o_data) + st_sample_src_[i];
@@ -1740,7 +1760,7 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
                               hipMemcpyHostToDevice, stream_));
     st_samples_.clear();
     st_sample_src_.clear();
-    st_sample_data_.clear();
+    st_sample_n_ = 0;
     st_raw_.clear();
     st_raw_src_.clear();
     st_res_.clear();

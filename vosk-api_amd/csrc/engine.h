@@ -220,6 +220,9 @@ class Engine {
   // resampled on the GPU (resample.h).  Set before the stream's first samples.
   void SetSampleRate(int slot, int rate);
   void AcceptSamples(int slot, const float* x, int n);
+  // The same, taking the buffer (no copy when the stream's pending samples
+  // are all consumed, the batch lane's usual case)
+  void AcceptSamples(int slot, std::vector<float>&& x);
   // Uploads a stream's whole audio into HBM; later steps read it from there
   // (no host->device copy inside the steps).  finished: end of input after it.
   void PreloadSamples(int slot, const float* x, long long n, bool finished);
@@ -425,7 +428,11 @@ class Engine {
   std::vector<int> st_raw_src_;
   std::vector<ResampleJob> st_res_;
   std::vector<int> st_sample_src_;  // offset into st_sample_data_, -1 = resident
-  std::vector<float> st_sample_data_;
+  // host-fed samples of the step being built, written straight into the
+  // step's pinned staging buffer (its first region)
+  float* st_sample_data_ = nullptr;
+  size_t st_sample_n_ = 0, stage_sample_cap_ = 0;
+  void StageSamples(const float* x, size_t n);
   std::vector<MfccJob> st_mfcc_;
   int st_mfcc_total_ = 0;
   std::vector<DevJob> st_jobs_;

@@ -897,7 +897,7 @@ void BatchModel::LaneLoop(Lane* L) {
               (int)e->PipelineBusy());
     try {
       for (auto& [r, c] : batch) {
-        if (!c.data.empty()) e->AcceptSamples(r->slot_, c.data.data(), (int)c.data.size());
+        if (!c.data.empty()) e->AcceptSamples(r->slot_, std::move(c.data));
         if (c.last) {
           e->InputFinished(r->slot_);
           r->finishing_ = true;
