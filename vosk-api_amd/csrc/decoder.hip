@@ -199,8 +199,27 @@ struct TokView {
   __device__ __forceinline__ float c(int i) const { return lds ? lc[i] : AG_LD(&gc[i]); }
 };
 
-// exact k-th smallest (0-based) of the token costs by 4-pass 8-bit radix select
-__device__ __forceinline__ float kth_smallest(DecShared& sh, const TokView& tv, int n, int k) {
+// token costs held in registers for GetCutoff when the frame has at most
+// DT * kCutRegs tokens (element r of a thread: token threadIdx.x + r * DT);
+// loaded once, with all loads in flight together, for the count and every
+// radix pass
+constexpr int kCutRegs = 8;
+struct CostRegs {
+  float c[kCutRegs];
+  __device__ __forceinline__ void load(const TokView& tv, int n, int base = 0) {
+#pragma unroll
+    for (int r = 0; r < kCutRegs; r++) {
+      const int i = base + (int)threadIdx.x + r * DT;
+      c[r] = i < n ? tv.c(i) : 0.0f;
+    }
+  }
+};
+
+// exact k-th smallest (0-based) of the token costs by 4-pass 8-bit radix
+// select; the costs come from registers (cr) or from the token view
+template <bool REGS>
+__device__ __forceinline__ float kth_smallest(DecShared& sh, const TokView& tv, const CostRegs& cr, int n,
+                                              int k) {
   if (threadIdx.x == 0) {
     sh.sel_prefix = 0;
     sh.sel_mask = 0;
@@ -211,9 +230,23 @@ __device__ __forceinline__ float kth_smallest(DecShared& sh, const TokView& tv, 
     for (int i = threadIdx.x; i < 256; i += DT) sh.hist[i] = 0;
     __syncthreads();
     const unsigned prefix = sh.sel_prefix, mask = sh.sel_mask;
-    for (int i = threadIdx.x; i < n; i += DT) {
-      const unsigned u = ford(tv.c(i));
-      if ((u & mask) == prefix) atomicAdd(&sh.hist[(u >> shift) & 255u], 1u);
+    if (REGS) {
+#pragma unroll
+      for (int r = 0; r < kCutRegs; r++) {
+        const unsigned u = ford(cr.c[r]);
+        if ((int)threadIdx.x + r * DT < n && (u & mask) == prefix) atomicAdd(&sh.hist[(u >> shift) & 255u], 1u);
+      }
+    } else {  // blocks of DT * kCutRegs costs, each block's loads in flight together
+      for (int b0 = 0; b0 < n; b0 += DT * kCutRegs) {
+        CostRegs blk;
+        blk.load(tv, n, b0);
+#pragma unroll
+        for (int r = 0; r < kCutRegs; r++) {
+          const unsigned u = ford(blk.c[r]);
+          if (b0 + (int)threadIdx.x + r * DT < n && (u & mask) == prefix)
+            atomicAdd(&sh.hist[(u >> shift) & 255u], 1u);
+        }
+      }
     }
     __syncthreads();
     if (threadIdx.x < 64) {  // wave 0: prefix over the 256 buckets (4 per lane)
@@ -1479,11 +1512,29 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     // max_cut < beam_cutoff  <=>  more than max_active costs are < beam_cutoff,
     // min_cut > beam_cutoff  <=>  at most min_active costs are <= beam_cutoff.
     bool need_max = ntok > a.max_active, need_min = ntok > a.min_active && a.min_active > 0;
+    const bool regs = ntok <= DT * kCutRegs;
+    CostRegs cr;
     if (need_max || need_min) {
       unsigned long long cnt = 0;  // (# cost < beam_cutoff) << 32 | # cost <= beam_cutoff
-      for (int i = threadIdx.x; i < ntok; i += DT) {
-        const float c = tv.c(i);
-        cnt += ((unsigned long long)(c < beam_cutoff) << 32) | (unsigned)(c <= beam_cutoff);
+      if (regs) {
+        cr.load(tv, ntok);
+#pragma unroll
+        for (int r = 0; r < kCutRegs; r++) {
+          const float c = cr.c[r];
+          if ((int)threadIdx.x + r * DT < ntok)
+            cnt += ((unsigned long long)(c < beam_cutoff) << 32) | (unsigned)(c <= beam_cutoff);
+        }
+      } else {
+        for (int b0 = 0; b0 < ntok; b0 += DT * kCutRegs) {
+          CostRegs blk;
+          blk.load(tv, ntok, b0);
+#pragma unroll
+          for (int r = 0; r < kCutRegs; r++) {
+            const float c = blk.c[r];
+            if (b0 + (int)threadIdx.x + r * DT < ntok)
+              cnt += ((unsigned long long)(c < beam_cutoff) << 32) | (unsigned)(c <= beam_cutoff);
+          }
+        }
       }
       cnt = block_sum_u64(sh, cnt);
       const int n_lt = (int)(cnt >> 32), n_le = (int)(unsigned)(cnt & 0xffffffffu);
@@ -1492,14 +1543,17 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     } else {
       __syncthreads();  // the LLH row staged above is read by wave 0 below
     }
-    if (need_max) max_cut = kth_smallest(sh, tv, ntok, a.max_active);
+    auto kth = [&](int k) {
+      return regs ? kth_smallest<true>(sh, tv, cr, ntok, k) : kth_smallest<false>(sh, tv, cr, ntok, k);
+    };
+    if (need_max) max_cut = kth(a.max_active);
     if (max_cut < beam_cutoff) {
       adaptive = max_cut - best + a.beam_delta;
       cutoff = max_cut;
     } else {
       if (ntok > a.min_active)
         min_cut = a.min_active == 0 ? best
-                  : need_min ? kth_smallest(sh, tv, ntok, a.min_active)
+                  : need_min ? kth(a.min_active)
                              : beam_cutoff;  // proven <= beam_cutoff: the exact value is unused
       if (min_cut > beam_cutoff) {
         adaptive = min_cut - best + a.beam_delta;
