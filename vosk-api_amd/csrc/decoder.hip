@@ -33,7 +33,7 @@
 namespace vamd {
 
 #ifndef VAMD_DEC_THREADS
-#define VAMD_DEC_THREADS 512
+#define VAMD_DEC_THREADS 1024
 #endif
 constexpr int DT = VAMD_DEC_THREADS;  // threads per decoder workgroup
 constexpr int DW = DT / 64;           // waves
@@ -48,7 +48,7 @@ constexpr int kFrontLds = 2048;       // epsilon frontier entries in LDS (more s
 // least this much room left; otherwise the sub-round winner checks run
 constexpr long long kDeferHeadroom = 1 << 20;
 #ifndef VAMD_DEC_UNROLL
-#define VAMD_DEC_UNROLL 4
+#define VAMD_DEC_UNROLL (2048 / VAMD_DEC_THREADS)
 #endif
 constexpr int kUnroll = VAMD_DEC_UNROLL;            // (token, arc) items in flight per thread in the emitting pass
 constexpr unsigned long long kEmpty = 0xffffffffffffffffull;
@@ -203,7 +203,7 @@ struct TokView {
 // DT * kCutRegs tokens (element r of a thread: token threadIdx.x + r * DT);
 // loaded once, with all loads in flight together, for the count and every
 // radix pass
-constexpr int kCutRegs = 8;
+constexpr int kCutRegs = 4096 / DT;
 struct CostRegs {
   float c[kCutRegs];
   __device__ __forceinline__ void load(const TokView& tv, int n, int base = 0) {
@@ -871,6 +871,7 @@ __device__ __forceinline__ int commit_eps_links(const DecArgs& a, DecShared& sh,
   const long long lb = st.links_used;
   // epsilon links of the committed tokens, at their final costs
   if (threadIdx.x == 0) sh.n_eps = 0;
+  __syncthreads();  // every thread reads n_eps below, also when neps == 0
   for (int c0 = 0; c0 < neps; c0 += DT) {
     const int q = c0 + threadIdx.x;
     int deg = 0, ab = 0, src = 0;
@@ -908,7 +909,7 @@ __device__ __forceinline__ int commit_eps_links(const DecArgs& a, DecShared& sh,
           L[pos] = make_int4(sh.tsrc[j], base + slot_pos(t, T, nl_n, v), arc, 0);
           LD[pos] = __float_as_int(tot - funord((uint32_t)(slot_key(t, T, v) >> 32)));
         } else {
-          sh.lat_ovf = 1;
+          atomicOr(&sh.lat_ovf, v == kNoSlot ? 2 : 1);  // 2: an epsilon link's destination is not in the frame
         }
       }
     }
@@ -1059,7 +1060,8 @@ __device__ __forceinline__ void frame_done(const DecArgs& a, DecShared& sh, DecS
     F.new_base = F.new_ntok = 0;
     a.lat_frames[(long long)slot * a.lat_frame_cap + index] = F;
   }
-  if (index >= a.lat_frame_cap || sh.lat_ovf) st.lat_ovf = 1;
+  // bits: 1 link arena full, 2 epsilon-link destination missing, 4 frame table full
+  st.lat_ovf |= sh.lat_ovf | (index >= a.lat_frame_cap ? 4 : 0);
   st.links_used += nl;
 }
 
