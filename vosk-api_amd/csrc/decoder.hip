@@ -1469,6 +1469,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     float b;
     int nl = 0;
     commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, &nl, false, pr);
+    st.commit_cutoff = a.beam;
     frame_done(a, sh, st, slot, 0, a.beam, 0.0f, nl);
   } else if (st.ntok > 0 && st.ntok <= kTokLds) {
     for (int i = threadIdx.x; i < st.ntok; i += DT) {
@@ -1516,7 +1517,10 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     bool need_max = ntok > a.max_active, need_min = ntok > a.min_active && a.min_active > 0;
     const bool regs = ntok <= DT * kCutRegs;
     CostRegs cr;
-    if (need_max || need_min) {
+    // every token's cost is below the last commit's cutoff: when that is at
+    // most beam_cutoff, all ntok are < (and <=) beam_cutoff without counting
+    const bool all_in = st.commit_cutoff <= beam_cutoff;
+    if ((need_max || need_min) && !all_in) {
       unsigned long long cnt = 0;  // (# cost < beam_cutoff) << 32 | # cost <= beam_cutoff
       if (regs) {
         cr.load(tv, ntok);
@@ -1545,6 +1549,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     } else {
       __syncthreads();  // the LLH row staged above is read by wave 0 below
     }
+    if (all_in) need_min = false;  // n_le = ntok > min_active (need_max stays ntok > max_active)
     auto kth = [&](int k) {
       return regs ? kth_smallest<true>(sh, tv, cr, ntok, k) : kth_smallest<false>(sh, tv, cr, ntok, k);
     };
@@ -1626,6 +1631,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     }
     int nl = 0;
     commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, &nl, defer, pr);
+    st.commit_cutoff = next_cutoff;
     pr.count(15, 1);
     frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset, nl);
     st.offset_sum += (double)cost_offset;

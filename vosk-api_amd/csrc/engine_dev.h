@@ -121,13 +121,14 @@ struct DecSlot {
   int err;          // bit 0: token list / table overflow, bit 1: arena overflow, bit 2: no tokens,
                     // bit 3: unplaceable backpointer source, bit 4: pruning lost a backpointer,
                     // bit 5: a link record with a backpointer candidate did not fit (deferred winners)
-  int lat_ovf;      // lattice: 1 = link arena or frame table overflowed (results fall back to 1-best)
+  int lat_ovf;      // lattice overflow (results fall back to 1-best): bit 0 link arena, bit 1 an
+                    // epsilon link's destination missing, bit 2 frame-record table
   int prune_from;   // first LatFrame whose extra costs were never computed (PruneActiveTokens)
   double offset_sum;
   unsigned long long best_key;  // min over current tokens of (ordered cost << 32 | state)
   long long links_used;         // lattice links in the stream's link arena
   int last_prune;   // frames decoded at the last pruning pass
-  int pad0;
+  float commit_cutoff;  // cutoff of the last commit: every current token's cost is below it
 };
 
 // ---- lattice (LatticeFasterDecoder forward links, kept in HBM per stream).
