@@ -751,6 +751,7 @@ void BatchModel::Push(BatchRecognizer* r, std::vector<float>&& chunk, bool last)
     if (r->queue_.empty()) L->streams_queued++;
     r->queue_.push_back(BatchRecognizer::Chunk{std::move(chunk), last});
     L->queued++;
+    r->ended_ = last;  // a chunk after FinishStream starts a new utterance
   }
   L->cv.notify_one();
 }
@@ -770,10 +771,21 @@ std::vector<std::array<int, 3>> BatchModel::LaneLoads() {
   return out;
 }
 
-void BatchModel::WaitForCompletion() {  // src/batch_model.cc:118-121
+// src/batch_model.cc:118-121.  Every pushed chunk has been decoded; the
+// results of finished streams (FinishStream) are published.  An endpoint
+// segment of a stream still running may still be in production on the
+// worker pool and arrives with a later Result(), as the reference's
+// lattice callbacks run asynchronously on its worker threads
+// (batch_model.cc:69, batch_recognizer.cc:138-149).
+void BatchModel::WaitForCompletion() {
   for (auto& L : lanes_) {
     std::unique_lock<std::mutex> lk(L->mu);
-    L->done_cv.wait(lk, [&] { return L->queued == 0 && L->busy == 0 && L->tasks == 0; });
+    L->done_cv.wait(lk, [&] {
+      if (L->queued != 0 || L->busy != 0) return false;
+      for (const BatchRecognizer* r : L->recs)
+        if (r->ended_ && r->tasks_ > 0) return false;
+      return true;
+    });
   }
 }
 

@@ -275,6 +275,7 @@ class BatchRecognizer {
   bool busy_ = false;       // has work in the engine
   bool finishing_ = false;  // last chunk handed: final result when the stream is idle
   int tasks_ = 0;           // results in production on the worker pool
+  bool ended_ = false;      // FinishStream pushed: Wait() also covers its results in production
   double segment_offset_ = 0;  // seconds at the start of the current segment
   uint64_t next_seq_ = 0;
   // results
