@@ -144,6 +144,10 @@ int vamd_stream_decode_llh(VamdEngine *e, int stream, const float *llh, int nfra
 /* best path: arc indices into the graph (emitting-first CSR order) */
 int vamd_stream_best_path(VamdEngine *e, int stream, int use_final, int *arcs, int cap,
                           double *cost, float *final_relative_cost);
+/* The same path from the segment's lattice records copied to the host
+ * (final costs used when any token is final): the batch path's fallback
+ * words when a segment's lattice is unusable.  Returns the arc count. */
+int vamd_stream_segment_best_path(VamdEngine *e, int stream, int *arcs, int cap);
 /* upload a stream's whole audio into HBM (read by later steps, no per-step
  * host->device copy); finished=1 marks end of input after it */
 int vamd_stream_preload(VamdEngine *e, int stream, const float *samples, long long n, int finished);
@@ -180,7 +184,7 @@ int vamd_batch_lane_stats(struct VoskBatchModel *m, int lane, int *load3, double
 /* result production totals: {segments, lattice links copied, ms copying
  * (lane threads), ms building raw lattices, ms prune + determinize + align,
  * ms MBR, ms formatting} */
-int vamd_batch_result_profile(struct VoskBatchModel *m, double *out7);
+int vamd_batch_result_profile(struct VoskBatchModel *m, double *out13);
 /* stream -> lane index it was admitted to */
 int vamd_batch_recognizer_lane(struct VoskBatchRecognizer *r);
 /* admission policy (host only, no GPU): replays `n` admissions against lanes

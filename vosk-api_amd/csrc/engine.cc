@@ -760,6 +760,8 @@ Engine::~Engine() {
   if (h_slots_) (void)hipHostFree(h_slots_);
   if (h_stats_) (void)hipHostFree(h_stats_);
   if (h_probe_) (void)hipHostFree(h_probe_);
+  if (h_lat_stage_) (void)hipHostFree(h_lat_stage_);
+  if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (dstream_) (void)hipStreamDestroy(dstream_);
   if (fstream_) (void)hipStreamDestroy(fstream_);
@@ -1519,29 +1521,76 @@ void Engine::GetRawLattice(int slot, bool use_final, RawLattice* out) {
 }
 
 void Engine::CopySegmentLattice(int slot, SegmentLattice* out, bool drain) {
+  CopySegmentLattices({slot}, {out}, drain);
+}
+
+// The segments' records go through one pinned staging buffer on a copy
+// stream of their own (not queued behind the pipeline's kernels): one read
+// of the decoder states, then all frames / arena / link copies in flight
+// together, one synchronization.
+void Engine::CopySegmentLattices(const std::vector<int>& slots, const std::vector<SegmentLattice*>& outs,
+                                 bool drain) {
   std::lock_guard<std::mutex> lk(mu_);
   DEVICE_GUARD();
   if (drain) FlushLocked();
-  *out = SegmentLattice();
-  if (!dec_.links) return;
-  DecSlot st;
-  HIPCHECK(hipMemcpy(&st, d_slots_ + slot, sizeof(DecSlot), hipMemcpyDeviceToHost));
-  const int host_frames = drain ? slots_.at(slot).decoded : slots_.at(slot).dev_frames;
-  if (host_frames == 0 && st.frames == 0 && st.arena_used == 0) return;
-  const int nf = std::min(st.frames + 1, dec_.lat_frame_cap);
-  out->frames.resize(nf);
-  out->arena.resize(st.arena_used);
-  const long long nl = std::min(st.links_used, dec_.link_cap);
-  out->links.resize(nl);
-  HIPCHECK(hipMemcpy(out->frames.data(), dec_.lat_frames + (size_t)slot * dec_.lat_frame_cap,
-                     sizeof(LatFrame) * nf, hipMemcpyDeviceToHost));
-  if (!out->arena.empty())
-    HIPCHECK(hipMemcpy(out->arena.data(), dec_.arena + (size_t)slot * dec_.arena_cap,
-                       sizeof(int4) * out->arena.size(), hipMemcpyDeviceToHost));
-  if (nl > 0)
-    HIPCHECK(hipMemcpy(out->links.data(), dec_.links + (size_t)slot * dec_.link_cap, sizeof(int4) * nl,
-                       hipMemcpyDeviceToHost));
-  out->overflow = st.lat_ovf || st.frames + 1 > dec_.lat_frame_cap || st.err;
+  for (SegmentLattice* o : outs) {  // (recycled buffers keep their capacity)
+    o->frames.clear();
+    o->arena.clear();
+    o->links.clear();
+    o->overflow = false;
+  }
+  if (!dec_.links || slots.empty()) return;
+  if (!copy_stream_) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+  HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(), hipMemcpyDeviceToHost,
+                          copy_stream_));
+  HIPCHECK(hipStreamSynchronize(copy_stream_));
+  struct Part { size_t f, a, l; int nf = 0; int na = 0; long long nl = 0; };
+  std::vector<Part> parts(slots.size());
+  size_t bytes = 0;
+  auto take = [&](size_t n) { const size_t o = bytes; bytes += Align256(n); return o; };
+  for (size_t i = 0; i < slots.size(); i++) {
+    const DecSlot& st = h_slots_[slots[i]];
+    const int host_frames = drain ? slots_.at(slots[i]).decoded : slots_.at(slots[i]).dev_frames;
+    if (host_frames == 0 && st.frames == 0 && st.arena_used == 0) continue;
+    Part& q = parts[i];
+    q.nf = std::min(st.frames + 1, dec_.lat_frame_cap);
+    q.na = st.arena_used;
+    q.nl = std::min(st.links_used, dec_.link_cap);
+    q.f = take(sizeof(LatFrame) * q.nf);
+    q.a = take(sizeof(int4) * q.na);
+    q.l = take(sizeof(int4) * q.nl);
+    outs[i]->overflow = st.lat_ovf || st.frames + 1 > dec_.lat_frame_cap || st.err;
+  }
+  if (bytes > lat_stage_bytes_) {
+    if (h_lat_stage_) HIPCHECK(hipHostFree(h_lat_stage_));
+    h_lat_stage_ = nullptr;
+    lat_stage_bytes_ = std::max(bytes, lat_stage_bytes_ * 2);
+    HIPCHECK(hipHostMalloc((void**)&h_lat_stage_, lat_stage_bytes_, hipHostMallocDefault));
+  }
+  for (size_t i = 0; i < slots.size(); i++) {
+    const Part& q = parts[i];
+    const size_t s = (size_t)slots[i];
+    if (q.nf > 0)
+      HIPCHECK(hipMemcpyAsync(h_lat_stage_ + q.f, dec_.lat_frames + s * dec_.lat_frame_cap,
+                              sizeof(LatFrame) * q.nf, hipMemcpyDeviceToHost, copy_stream_));
+    if (q.na > 0)
+      HIPCHECK(hipMemcpyAsync(h_lat_stage_ + q.a, dec_.arena + s * dec_.arena_cap, sizeof(int4) * q.na,
+                              hipMemcpyDeviceToHost, copy_stream_));
+    if (q.nl > 0)
+      HIPCHECK(hipMemcpyAsync(h_lat_stage_ + q.l, dec_.links + s * dec_.link_cap, sizeof(int4) * q.nl,
+                              hipMemcpyDeviceToHost, copy_stream_));
+  }
+  HIPCHECK(hipStreamSynchronize(copy_stream_));
+  for (size_t i = 0; i < slots.size(); i++) {
+    const Part& q = parts[i];
+    SegmentLattice* o = outs[i];
+    const LatFrame* F = (const LatFrame*)(h_lat_stage_ + q.f);
+    const int4* A = (const int4*)(h_lat_stage_ + q.a);
+    const int4* L = (const int4*)(h_lat_stage_ + q.l);
+    o->frames.assign(F, F + q.nf);
+    o->arena.assign(A, A + q.na);
+    o->links.assign(L, L + q.nl);
+  }
 }
 
 void Engine::TakeDecoded(std::vector<DecodedJob>* out) {

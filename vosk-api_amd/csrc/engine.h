@@ -268,6 +268,9 @@ class Engine {
   void GetRawLattice(int slot, bool use_final, RawLattice* out);
   // The segment's lattice records (drain as BestPaths); empty without a lattice.
   void CopySegmentLattice(int slot, SegmentLattice* out, bool drain = true);
+  // The same for several streams with the copies batched.
+  void CopySegmentLattices(const std::vector<int>& slots, const std::vector<SegmentLattice*>& outs,
+                           bool drain = true);
 
   // ---- asynchronous driving (BatchModel lanes: one thread steps the engine,
   // results are produced between steps without draining the pipeline)
@@ -405,6 +408,9 @@ class Engine {
   unsigned char* d_arc_sil_ = nullptr;  // per arc: 0 epsilon, 1 silence phone, 2 other
   int* d_probe_ = nullptr;              // ProbeEndpoints buffers
   int* h_probe_ = nullptr;
+  hipStream_t copy_stream_ = nullptr;  // segment lattice copies
+  char* h_lat_stage_ = nullptr;        // pinned staging of segment lattice copies
+  size_t lat_stage_bytes_ = 0;
   // device: per-stream state
   float* d_samples_ = nullptr;
   float* d_raw_ = nullptr;  // [slots][raw_ring_] input-rate samples of resampled streams

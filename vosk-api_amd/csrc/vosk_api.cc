@@ -680,6 +680,16 @@ int vamd_stream_best_path(VamdEngine* e, int s, int use_final, int* arcs, int ca
   API_CATCH(-1)
 }
 
+int vamd_stream_segment_best_path(VamdEngine* e, int s, int* arcs, int cap) {
+  API_TRY
+  SegmentLattice sl;
+  e->eng->CopySegmentLattice(s, &sl, true);
+  const std::vector<int> p = SegmentBestPath(e->eng->model().graph, sl);
+  for (int i = 0; i < (int)p.size() && i < cap; i++) arcs[i] = p[i];
+  return (int)p.size();
+  API_CATCH(-1)
+}
+
 int vamd_stream_preload(VamdEngine* e, int s, const float* x, long long n, int finished) {
   API_TRY
   e->eng->PreloadSamples(s, x, n, finished != 0);
@@ -763,9 +773,9 @@ int vamd_batch_lane_stats(VoskBatchModel* m, int lane, int* load3, double* ms4, 
   API_CATCH(-1)
 }
 
-int vamd_batch_result_profile(VoskBatchModel* m, double* out7) {
+int vamd_batch_result_profile(VoskBatchModel* m, double* out13) {
   API_TRY
-  ((BatchModel*)m)->ResultProfile(out7);
+  ((BatchModel*)m)->ResultProfile(out13);
   return 0;
   API_CATCH(-1)
 }

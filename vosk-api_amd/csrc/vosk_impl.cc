@@ -2,11 +2,14 @@
 #include "vosk_impl.h"
 #include "graph_compose.h"
 
+#include <sched.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <sstream>
 
 #include "common.h"
@@ -369,6 +372,55 @@ static MbrResult PathMbr(const ModelData& m, const std::vector<int>& arcs) {
   return r;
 }
 
+// Best path of a segment from its copied records, for a segment whose
+// lattice is unusable: the traceback kernel's rule (decoder.hip
+// traceback_kernel) on the host — the last frame's live token with the
+// smallest (cost, plus the final cost if any token is final; state), then its
+// backpointers.
+static float BitsToFloat(int b) {
+  float f;
+  std::memcpy(&f, &b, 4);
+  return f;
+}
+static uint32_t OrderedBits(float f) {  // dev_util.h ford
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+std::vector<int> SegmentBestPath(const Graph& g, const SegmentLattice& sl) {
+  std::vector<int> arcs;
+  if (sl.frames.empty()) return arcs;
+  const LatFrame& F = sl.frames.back();
+  const long long n = (long long)sl.arena.size();
+  if (F.tok_base < 0 || (long long)F.tok_base + F.ntok > n) return arcs;
+  const float inf = std::numeric_limits<float>::infinity();
+  float bf = inf;
+  for (int i = F.tok_base; i < F.tok_base + F.ntok; i++) {
+    const int4& e = sl.arena[i];
+    if (e.x == -2 || e.w < 0 || e.w >= g.NumStates()) continue;  // dead entry
+    if (std::isfinite(g.final_cost[e.w])) bf = std::min(bf, BitsToFloat(e.z) + g.final_cost[e.w]);
+  }
+  const bool use_f = bf != inf;
+  unsigned long long bk = ~0ull;
+  long long end = -1;
+  for (int i = F.tok_base; i < F.tok_base + F.ntok; i++) {
+    const int4& e = sl.arena[i];
+    if (e.x == -2 || e.w < 0 || e.w >= g.NumStates()) continue;
+    const float c = use_f ? BitsToFloat(e.z) + g.final_cost[e.w] : BitsToFloat(e.z);
+    const unsigned long long k = ((unsigned long long)OrderedBits(c) << 32) | (unsigned)e.w;
+    if (k < bk) { bk = k; end = i; }
+  }
+  for (long long k = end; k >= 0 && k < n && (long long)arcs.size() <= n;) {
+    const int4& e = sl.arena[k];
+    if (e.y < 0) break;
+    arcs.push_back(e.y);
+    k = e.x;
+  }
+  std::reverse(arcs.begin(), arcs.end());
+  return arcs;
+}
+
 // MBR words, confidences and frame times of the segment; graph_scale as the
 // reference applies to final results (GraphLatticeScale(0.9), :718), 1 for
 // partial results.
@@ -650,10 +702,21 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
     L->by_slot.assign(c.max_slots, nullptr);
     lanes_.push_back(std::move(L));
   }
-  // result workers: VOSK_AMD_RESULT_THREADS, default one per host core up to
-  // 16 per GPU (num_worker_threads = -1: all cores)
+  // result workers: VOSK_AMD_RESULT_THREADS, default half the host cores
+  // this process may use (affinity, capped by OMP_NUM_THREADS when set; at
+  // most 16 per GPU) (reference: num_worker_threads = -1, all cores)
   int hc = (int)std::thread::hardware_concurrency();
-  int nt = EnvInt("VOSK_AMD_RESULT_THREADS", std::max(2, std::min(hc > 0 ? hc : 8, 16 * (int)lanes_.size())));
+  {
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0) hc = CPU_COUNT(&cs);
+    const int omp = EnvInt("OMP_NUM_THREADS", 0);
+    if (omp > 0) hc = std::min(hc, omp);
+  }
+  // half of them: the feeding thread, the lanes and the HIP runtime keep
+  // theirs (more workers only contend: 8 vs 14 of 16 cores measured equal
+  // or better on the 60-s bench)
+  const int cores = std::min(hc > 0 ? hc : 8, 16 * (int)lanes_.size());
+  int nt = EnvInt("VOSK_AMD_RESULT_THREADS", std::max(2, cores / 2));
   pool_.reset(new WorkerPool(nt));
   for (auto& L : lanes_) {
     Lane* l = L.get();
@@ -688,7 +751,9 @@ Engine* BatchModel::LaneEngine(int i) { return lanes_.at(i)->engine.get(); }
 void BatchModel::ResultProfile(double* out) const {
   out[0] = (double)prof_[0];
   out[1] = (double)prof_[1];
-  for (int i = 2; i < 7; i++) out[i] = prof_[i] * 1e-6;
+  for (int i = 2; i < 11; i++) out[i] = prof_[i] * 1e-6;
+  out[11] = (double)prof_[11];
+  out[12] = prof_[12] * 1e-6;
 }
 
 int BatchModel::LaneOf(const BatchRecognizer* r) const { return r->lane_; }
@@ -789,30 +854,67 @@ void BatchModel::WaitForCompletion() {
   }
 }
 
-void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, const PathResult* best) {
+std::shared_ptr<SegmentLattice> BatchModel::TakeSegmentBuffer() {
+  std::lock_guard<std::mutex> lk(sl_mu_);
+  if (sl_pool_.empty()) return std::make_shared<SegmentLattice>();
+  auto sl = std::move(sl_pool_.back());
+  sl_pool_.pop_back();
+  return sl;
+}
+
+void BatchModel::ReturnSegmentBuffer(std::shared_ptr<SegmentLattice> sl) {
+  std::lock_guard<std::mutex> lk(sl_mu_);
+  if (sl_pool_.size() < 64) sl_pool_.push_back(std::move(sl));
+}
+
+void BatchModel::EmitSegments(Lane* L, const std::vector<BatchRecognizer*>& rs, bool final_segment) {
   Engine* e = L->engine.get();
-  const float shift = 0.01f * md_->dcb.frame_subsampling_factor;
-  const int frames = e->DeviceFramesDecoded(r->slot_);
   using clk = std::chrono::steady_clock;
   auto ns = [](clk::time_point a, clk::time_point b) {
     return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
   };
-  auto sl = std::make_shared<SegmentLattice>();
+  // the segments' lattice records, copied together
+  std::vector<std::shared_ptr<SegmentLattice>> sls(rs.size());
+  std::vector<int> frames(rs.size()), cslots;
+  std::vector<SegmentLattice*> couts;
+  for (size_t i = 0; i < rs.size(); i++) {
+    sls[i] = TakeSegmentBuffer();
+    sls[i]->frames.clear();
+    sls[i]->arena.clear();
+    sls[i]->links.clear();
+    sls[i]->overflow = false;
+    frames[i] = e->DeviceFramesDecoded(rs[i]->slot_);
+    if (frames[i] > 0) {
+      cslots.push_back(rs[i]->slot_);
+      couts.push_back(sls[i].get());
+    }
+  }
   const auto tc = clk::now();
-  if (frames > 0) e->CopySegmentLattice(r->slot_, sl.get(), false);
-  prof_[0]++;
-  prof_[1] += (long long)sl->links.size();
+  if (!cslots.empty()) e->CopySegmentLattices(cslots, couts, false);
   prof_[2] += ns(tc, clk::now());
+  for (size_t i = 0; i < rs.size(); i++) {
+    prof_[0]++;
+    prof_[1] += (long long)sls[i]->links.size();
+    EmitSegment(L, rs[i], final_segment, sls[i], frames[i]);
+  }
+}
+
+void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment,
+                             std::shared_ptr<SegmentLattice> sl, int frames) {
+  const float shift = 0.01f * md_->dcb.frame_subsampling_factor;
+  using clk = std::chrono::steady_clock;
+  auto ns = [](clk::time_point a, clk::time_point b) {
+    return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+  };
   const double offset = r->segment_offset_;
   r->segment_offset_ = final_segment ? 0.0 : r->segment_offset_ + frames * shift;
   const uint64_t seq = r->next_seq_++;
-  std::vector<int> path = best ? best->arcs : std::vector<int>();
   {
     std::lock_guard<std::mutex> lk(L->mu);
     r->tasks_++;
     L->tasks++;
   }
-  pool_->Submit([this, L, r, sl, seq, offset, frames, path, ns]() {
+  pool_->Submit([this, L, r, sl, seq, offset, frames, ns]() {
     const ModelData& m = *md_;
     MbrResult res;
     try {
@@ -827,7 +929,7 @@ void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, co
         const bool ok = WordLatticeFromRaw(raw, m, 0.9f, &wl, false);
         const auto t2 = clk::now();
         if (ok) MinimumBayesRisk(wl, &res);
-        else res = PathMbr(m, path);
+        else res = PathMbr(m, SegmentBestPath(m.graph, *sl));  // lattice unusable: 1-best words
         prof_[3] += ns(t0, t1);
         prof_[4] += ns(t1, t2);
         prof_[5] += ns(t2, clk::now());
@@ -836,6 +938,7 @@ void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, co
       VAMD_WARN("batch result failed: " << ex.what());
       res = MbrResult();
     }
+    ReturnSegmentBuffer(sl);
     const auto tf = clk::now();
     std::string js = r->FormatResult(res, offset);
     prof_[6] += ns(tf, clk::now());
@@ -862,25 +965,30 @@ void BatchModel::LaneLoop(Lane* L) {
   std::vector<int> slots, probe;
   std::vector<BatchRecognizer*> probe_r, ends, retire, finals;
   std::vector<EndpointProbe> pr;
-  std::vector<PathResult> best;
   bool pipelined = false;
   const bool trace = EnvInt("VOSK_AMD_BATCH_TRACE", 0) != 0;  // development: one line per lane step
   long long iter = 0;
+  using clk = std::chrono::steady_clock;
+  auto ns = [](clk::time_point a, clk::time_point b) {
+    return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+  };
   while (true) {
     std::vector<std::pair<BatchRecognizer*, BatchRecognizer::Chunk>> batch;
+    clk::time_point tw;
     {
       std::unique_lock<std::mutex> lk(L->mu);
       L->cv.wait(lk, [&] { return L->stop || L->queued > 0 || !active.empty(); });
       if (L->stop) return;
+      tw = clk::now();
       // dynamic batching (CudaOnlinePipelineDynamicBatcher, batch_model.cc:94-96):
       // with the GPU idle, wait briefly for the other streams' chunks of this
-      // feeding round (until every stream has one, no push for 250 us, or 2 ms)
+      // feeding round (until every stream has one, no push for 1 ms, or 4 ms)
       if (L->queued > 0 && !e->PipelineBusy()) {
         const auto t0 = std::chrono::steady_clock::now();
         while (L->streams_queued < (int)L->recs.size() && !L->stop) {
           const int before = L->queued;
-          L->cv.wait_for(lk, std::chrono::microseconds(250));
-          if (L->queued == before || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+          L->cv.wait_for(lk, std::chrono::microseconds(1000));
+          if (L->queued == before || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(4)) break;
         }
       }
       for (BatchRecognizer* r : L->recs) {  // one chunk per stream per step
@@ -901,6 +1009,9 @@ void BatchModel::LaneLoop(Lane* L) {
       // nothing queued behind it runs its stages in order (one sync, not three)
       pipelined = L->queued > 0 || e->PipelineBusy();
     }
+    const auto ts = clk::now();
+    prof_[7] += ns(tw, ts);
+    prof_[11]++;
     bool failed = false;
     const bool tr = trace && (++iter < 300 || iter % 20000 == 0);
     if (tr)
@@ -918,6 +1029,8 @@ void BatchModel::LaneLoop(Lane* L) {
       slots.clear();
       for (BatchRecognizer* r : active) slots.push_back(r->slot_);
       e->Step(slots, pipelined);
+      prof_[8] += ns(ts, clk::now());
+      const auto tp = clk::now();
       // reset_on_endpoint (batch_model.cc:72): streams whose decoder job just
       // completed, checked on the device state without draining the pipeline
       e->TakeDecoded(&decoded);
@@ -934,7 +1047,9 @@ void BatchModel::LaneLoop(Lane* L) {
         probe_r.push_back(r);
       }
       if (!probe.empty()) {
+        const auto tq = clk::now();
         e->ProbeEndpoints(probe, &pr);
+        prof_[12] += ns(tq, clk::now());
         ends.clear();
         std::vector<int> end_slots;
         for (size_t i = 0; i < probe.size(); i++)
@@ -943,17 +1058,16 @@ void BatchModel::LaneLoop(Lane* L) {
             end_slots.push_back(probe[i]);
           }
         if (!ends.empty()) {
-          e->BestPaths(end_slots, true, &best, false);  // fallback words if a lattice is unusable
-          for (size_t i = 0; i < ends.size(); i++) {
-            EmitSegment(L, ends[i], false, &best[i]);
-            e->ResetDecoderAtNextJob(ends[i]->slot_);
-          }
+          EmitSegments(L, ends, false);
+          for (BatchRecognizer* r : ends) e->ResetDecoderAtNextJob(r->slot_);
         }
       }
+      prof_[9] += ns(tp, clk::now());
     } catch (const std::exception& ex) {
       VAMD_WARN("batch step failed on GPU " << L->device << ": " << ex.what());
       failed = true;
     }
+    const auto tr0 = clk::now();
     // streams with nothing left in the engine: their chunks are done; a
     // finishing stream's final segment ends here (FinishStream)
     retire.clear();
@@ -975,11 +1089,8 @@ void BatchModel::LaneLoop(Lane* L) {
       try {
         slots.clear();
         for (BatchRecognizer* r : finals) slots.push_back(r->slot_);
-        e->BestPaths(slots, true, &best, false);
-        for (size_t i = 0; i < finals.size(); i++) {
-          EmitSegment(L, finals[i], true, &best[i]);
-          e->ResetPipeline(finals[i]->slot_);  // a later AcceptWaveform starts a new utterance
-        }
+        EmitSegments(L, finals, true);
+        for (BatchRecognizer* r : finals) e->ResetPipeline(r->slot_);  // a later AcceptWaveform: new utterance
       } catch (const std::exception& ex) {
         // every finished stream still gets a (empty) final result
         VAMD_WARN("batch final results failed on GPU " << L->device << ": " << ex.what());
@@ -995,6 +1106,7 @@ void BatchModel::LaneLoop(Lane* L) {
           break;
         }
     }
+    prof_[10] += ns(tr0, clk::now());
     if (!retire.empty()) {
       {
         std::lock_guard<std::mutex> lk(L->mu);

@@ -30,6 +30,9 @@ struct WordSeg {
 };
 std::vector<WordSeg> PathWords(const ModelData& m, const std::vector<int>& arcs);
 int TrailingSilenceFrames(const ModelData& m, const std::vector<int>& arcs);
+// Best path (arc indices) of a segment from its copied lattice records, by the
+// traceback kernel's rule (the batch path's fallback words).
+std::vector<int> SegmentBestPath(const Graph& g, const SegmentLattice& sl);
 // OnlineEndpointConfig rules (Kaldi online2/online-endpoint.cc [K]).
 bool EndpointRulesFire(const EndpointConfig& c, int frames_decoded, int trailing_sil,
                        float frame_shift_s, float final_relative_cost);
@@ -228,16 +231,27 @@ class BatchModel {
   struct Lane;
   Engine* LaneEngine(int i);
   void LaneLoop(Lane* L);
-  // A segment of stream r ends (endpoint or end of stream): lattice records
-  // copied from HBM now, MBR and JSON on the result workers.
-  void EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, const PathResult* best);
+  // Segments of streams rs end (endpoint or end of stream): their lattice
+  // records copied from HBM now (batched), MBR and JSON on the result workers.
+  void EmitSegments(Lane* L, const std::vector<BatchRecognizer*>& rs, bool final_segment);
+  void EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, std::shared_ptr<SegmentLattice> sl,
+                   int frames);
   std::shared_ptr<ModelData> md_;
   int samples_per_chunk_ = 0;
   std::vector<std::unique_ptr<Lane>> lanes_;
   std::unique_ptr<WorkerPool> pool_;
   std::mutex admit_mu_;
   std::atomic<int> ref_{1};
-  std::atomic<long long> prof_[7] = {};  // ResultProfile (ns except counts)
+  // segment lattice buffers recycled between segments (their vectors keep
+  // their capacity: no fresh allocation and page faults per copy)
+  std::shared_ptr<SegmentLattice> TakeSegmentBuffer();
+  void ReturnSegmentBuffer(std::shared_ptr<SegmentLattice> sl);
+  std::mutex sl_mu_;
+  std::vector<std::shared_ptr<SegmentLattice>> sl_pool_;
+  // ResultProfile (ns except counts): segments, links, copy, build, det, MBR,
+  // format; lane loop: dynamic batching wait, step, endpoints, finals, steps;
+  // endpoint probe launches (within endpoints)
+  std::atomic<long long> prof_[13] = {};
   ~BatchModel();
 };
 

@@ -48,6 +48,7 @@ _SIGS = {
     "vamd_stream_best_path": (C.c_int, [_vp, C.c_int, C.c_int, _vp, C.c_int, _vp, _vp]),
     "vamd_engine_counters": (C.c_int, [_vp, _vp]),
     "vamd_stream_preload": (C.c_int, [_vp, C.c_int, _vp, C.c_longlong, C.c_int]),
+    "vamd_stream_segment_best_path": (C.c_int, [_vp, C.c_int, _vp, C.c_int]),
     "vamd_engine_step": (C.c_int, [_vp, _vp, C.c_int]),
     "vamd_engine_flush": (C.c_int, [_vp]),
     "vamd_engine_decoder_totals": (C.c_int, [_vp, _vp]),
@@ -116,11 +117,15 @@ def batch_lane_stats(model, lane, reset=False):
 
 def batch_result_profile(model):
     """Result production totals of a vosk.BatchModel (segments, links copied,
-    ms copy / build / prune+determinize+align / MBR / format)."""
-    o = np.zeros(7, np.float64)
+    ms copy / build / prune+determinize+align / MBR / format) and the lane
+    loops' host time (ms in the dynamic batching wait, the engine step,
+    endpoint checks + segment hand-off, finals + retiring; lane iterations;
+    the endpoint probe launches within the endpoint checks)."""
+    o = np.zeros(13, np.float64)
     _chk(_c.vamd_batch_result_profile(model._handle, o.ctypes.data))
-    return dict(zip(("segments", "links_copied", "copy_ms", "build_ms", "det_ms", "mbr_ms", "format_ms"),
-                    (float(x) for x in o)))
+    return dict(zip(("segments", "links_copied", "copy_ms", "build_ms", "det_ms", "mbr_ms", "format_ms",
+                     "lane_batch_wait_ms", "lane_step_ms", "lane_endpoint_ms", "lane_finals_ms",
+                     "lane_iterations", "lane_probe_ms"), (float(x) for x in o)))
 
 
 def batch_recognizer_lane(rec):
@@ -328,6 +333,13 @@ class Engine:
         n = _chk(_c.vamd_stream_best_path(self.h, s, 1 if use_final else 0, arcs.ctypes.data,
                                            cap, C.addressof(cost), C.addressof(frel)))
         return arcs[:n].copy(), cost.value, frel.value
+
+    def segment_best_path(self, s, cap=1 << 20):
+        """Best path from the segment's lattice records on the host (final
+        costs if any token is final): the batch path's fallback words."""
+        arcs = np.zeros(cap, np.int32)
+        n = _chk(_c.vamd_stream_segment_best_path(self.h, s, arcs.ctypes.data, cap))
+        return arcs[:n].copy()
 
     def preload(self, s, samples, finished=True):
         x = np.ascontiguousarray(samples, np.float32)
