@@ -1541,9 +1541,12 @@ void Engine::CopySegmentLattices(const std::vector<int>& slots, const std::vecto
   }
   if (!dec_.links || slots.empty()) return;
   if (!copy_stream_) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
   HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(), hipMemcpyDeviceToHost,
                           copy_stream_));
   HIPCHECK(hipStreamSynchronize(copy_stream_));
+  const auto t1 = clk::now();
   struct Part { size_t f, a, l; int nf = 0; int na = 0; long long nl = 0; };
   std::vector<Part> parts(slots.size());
   size_t bytes = 0;
@@ -1581,6 +1584,7 @@ void Engine::CopySegmentLattices(const std::vector<int>& slots, const std::vecto
                               hipMemcpyDeviceToHost, copy_stream_));
   }
   HIPCHECK(hipStreamSynchronize(copy_stream_));
+  const auto t2 = clk::now();
   for (size_t i = 0; i < slots.size(); i++) {
     const Part& q = parts[i];
     SegmentLattice* o = outs[i];
@@ -1591,6 +1595,16 @@ void Engine::CopySegmentLattices(const std::vector<int>& slots, const std::vecto
     o->arena.assign(A, A + q.na);
     o->links.assign(L, L + q.nl);
   }
+  auto us = [](clk::time_point a, clk::time_point b) {
+    return (long long)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+  };
+  copy_us_[0] += us(t0, t1);
+  copy_us_[1] += us(t1, t2);
+  copy_us_[2] += us(t2, clk::now());
+  copy_us_[3] += (long long)bytes;
+  if (getenv("VOSK_AMD_COPY_DEBUG") && ++copy_calls_ % 20 == 0)
+    fprintf(stderr, "segment copies: %lld calls, states %lld us, records %lld us, host %lld us, %lld MB\n",
+            copy_calls_, copy_us_[0], copy_us_[1], copy_us_[2], copy_us_[3] >> 20);
 }
 
 void Engine::TakeDecoded(std::vector<DecodedJob>* out) {
