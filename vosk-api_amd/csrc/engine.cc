@@ -760,7 +760,9 @@ Engine::~Engine() {
   if (h_slots_) (void)hipHostFree(h_slots_);
   if (h_stats_) (void)hipHostFree(h_stats_);
   if (h_probe_) (void)hipHostFree(h_probe_);
+  if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
   if (h_lat_stage_) (void)hipHostFree(h_lat_stage_);
+  if (h_copy_slots_) (void)hipHostFree(h_copy_slots_);
   if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (dstream_) (void)hipStreamDestroy(dstream_);
@@ -1543,7 +1545,9 @@ void Engine::CopySegmentLattices(const std::vector<int>& slots, const std::vecto
   if (!copy_stream_) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
-  HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(), hipMemcpyDeviceToHost,
+  if (!h_copy_slots_)  // own snapshot: h_slots_ may be the target of a decoder batch's read-back
+    HIPCHECK(hipHostMalloc((void**)&h_copy_slots_, sizeof(DecSlot) * slots_.size(), hipHostMallocDefault));
+  HIPCHECK(hipMemcpyAsync(h_copy_slots_, d_slots_, sizeof(DecSlot) * slots_.size(), hipMemcpyDeviceToHost,
                           copy_stream_));
   HIPCHECK(hipStreamSynchronize(copy_stream_));
   const auto t1 = clk::now();
@@ -1552,7 +1556,7 @@ void Engine::CopySegmentLattices(const std::vector<int>& slots, const std::vecto
   size_t bytes = 0;
   auto take = [&](size_t n) { const size_t o = bytes; bytes += Align256(n); return o; };
   for (size_t i = 0; i < slots.size(); i++) {
-    const DecSlot& st = h_slots_[slots[i]];
+    const DecSlot& st = h_copy_slots_[slots[i]];
     const int host_frames = drain ? slots_.at(slots[i]).decoded : slots_.at(slots[i]).dev_frames;
     if (host_frames == 0 && st.frames == 0 && st.arena_used == 0) continue;
     Part& q = parts[i];

@@ -411,6 +411,7 @@ class Engine {
   hipStream_t copy_stream_ = nullptr;  // segment lattice copies
   char* h_lat_stage_ = nullptr;        // pinned staging of segment lattice copies
   size_t lat_stage_bytes_ = 0;
+  DecSlot* h_copy_slots_ = nullptr;  // decoder-state snapshot of the segment copies
   long long copy_us_[4] = {0, 0, 0, 0}, copy_calls_ = 0;  // development (VOSK_AMD_COPY_DEBUG)
   // device: per-stream state
   float* d_samples_ = nullptr;
