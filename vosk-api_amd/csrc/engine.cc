@@ -763,6 +763,7 @@ Engine::~Engine() {
   if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
   if (h_lat_stage_) (void)hipHostFree(h_lat_stage_);
   if (h_copy_slots_) (void)hipHostFree(h_copy_slots_);
+  if (copy_ev_) (void)hipEventDestroy(copy_ev_);
   if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (dstream_) (void)hipStreamDestroy(dstream_);
@@ -1167,6 +1168,10 @@ void Engine::LaunchDecodeBatch(const DecBatch& b, hipStream_t s) {
   DecArgs d = dec_;
   d.jobs = (const DecJob*)(d_stage_ + (size_t)b.buf * stage_bytes_ + b.o_ej);
   d.llh = d_llh_buf_[b.llh];
+  if (copy_pending_) {  // segment records still being copied (StartSegmentCopies)
+    HIPCHECK(hipStreamWaitEvent(s, copy_ev_, 0));
+    copy_pending_ = false;
+  }
   LaunchDecode(d, (int)b.jobs.size(), s);
   HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(),
                           hipMemcpyDeviceToHost, s));
@@ -1609,6 +1614,104 @@ void Engine::CopySegmentLattices(const std::vector<int>& slots, const std::vecto
   if (getenv("VOSK_AMD_COPY_DEBUG") && ++copy_calls_ % 20 == 0)
     fprintf(stderr, "segment copies: %lld calls, states %lld us, records %lld us, host %lld us, %lld MB\n",
             copy_calls_, copy_us_[0], copy_us_[1], copy_us_[2], copy_us_[3] >> 20);
+}
+
+PinnedPool::~PinnedPool() {
+  for (auto& b : free_) (void)hipHostFree(b.second);
+}
+
+char* PinnedPool::Take(size_t bytes, size_t* cap) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    size_t best = free_.size();
+    for (size_t i = 0; i < free_.size(); i++)
+      if (free_[i].first >= bytes && (best == free_.size() || free_[i].first < free_[best].first)) best = i;
+    if (best < free_.size()) {
+      char* p = free_[best].second;
+      *cap = free_[best].first;
+      free_.erase(free_.begin() + best);
+      return p;
+    }
+  }
+  *cap = std::max<size_t>(Align256(bytes), 1 << 20);
+  char* p = nullptr;
+  HIPCHECK(hipHostMalloc((void**)&p, *cap, hipHostMallocDefault));
+  return p;
+}
+
+void PinnedPool::Give(char* p, size_t cap) {
+  std::lock_guard<std::mutex> lk(mu_);
+  free_.push_back({cap, p});
+}
+
+void SegmentCopy::Finish(SegmentLattice* out) {
+  out->frames.clear();
+  out->arena.clear();
+  out->links.clear();
+  out->overflow = overflow;
+  if (!block) return;
+  (void)hipSetDevice(device);
+  HIPCHECK(hipEventSynchronize(done));
+  (void)hipEventDestroy(done);
+  done = nullptr;
+  const LatFrame* F = (const LatFrame*)(block + f);
+  const int4* A = (const int4*)(block + a);
+  const int4* L = (const int4*)(block + l);
+  out->frames.assign(F, F + nf);
+  out->arena.assign(A, A + na);
+  out->links.assign(L, L + nl);
+  pool->Give(block, cap);
+  block = nullptr;
+}
+
+void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::shared_ptr<SegmentCopy>>* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
+  out->clear();
+  for (size_t i = 0; i < slots.size(); i++) out->push_back(std::make_shared<SegmentCopy>());
+  if (!dec_.links || slots.empty()) return;
+  if (!copy_stream_) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+  if (!copy_ev_) HIPCHECK(hipEventCreateWithFlags(&copy_ev_, hipEventDisableTiming));
+  if (!h_copy_slots_)  // own snapshot: h_slots_ may be the target of a decoder batch's read-back
+    HIPCHECK(hipHostMalloc((void**)&h_copy_slots_, sizeof(DecSlot) * slots_.size(), hipHostMallocDefault));
+  HIPCHECK(hipMemcpyAsync(h_copy_slots_, d_slots_, sizeof(DecSlot) * slots_.size(), hipMemcpyDeviceToHost,
+                          copy_stream_));
+  HIPCHECK(hipStreamSynchronize(copy_stream_));
+  for (size_t i = 0; i < slots.size(); i++) {
+    const DecSlot& st = h_copy_slots_[slots[i]];
+    SegmentCopy& c = *(*out)[i];
+    if (slots_.at(slots[i]).dev_frames == 0 && st.frames == 0 && st.arena_used == 0) continue;
+    c.nf = std::min(st.frames + 1, dec_.lat_frame_cap);
+    c.na = st.arena_used;
+    c.nl = std::min(st.links_used, dec_.link_cap);
+    c.overflow = st.lat_ovf || st.frames + 1 > dec_.lat_frame_cap || st.err;
+    size_t bytes = 0;
+    c.f = bytes;
+    bytes += Align256(sizeof(LatFrame) * c.nf);
+    c.a = bytes;
+    bytes += Align256(sizeof(int4) * c.na);
+    c.l = bytes;
+    bytes += Align256(sizeof(int4) * c.nl);
+    c.pool = pinned_;
+    c.device = cfg_.device;
+    c.block = pinned_->Take(bytes, &c.cap);
+    const size_t s = (size_t)slots[i];
+    if (c.nf > 0)
+      HIPCHECK(hipMemcpyAsync(c.block + c.f, dec_.lat_frames + s * dec_.lat_frame_cap, sizeof(LatFrame) * c.nf,
+                              hipMemcpyDeviceToHost, copy_stream_));
+    if (c.na > 0)
+      HIPCHECK(hipMemcpyAsync(c.block + c.a, dec_.arena + s * dec_.arena_cap, sizeof(int4) * c.na,
+                              hipMemcpyDeviceToHost, copy_stream_));
+    if (c.nl > 0)
+      HIPCHECK(hipMemcpyAsync(c.block + c.l, dec_.links + s * dec_.link_cap, sizeof(int4) * c.nl,
+                              hipMemcpyDeviceToHost, copy_stream_));
+    HIPCHECK(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
+    HIPCHECK(hipEventRecord(c.done, copy_stream_));
+  }
+  // the stream's next decoder launch (which may reset and overwrite these
+  // records) waits for the copies on the device
+  HIPCHECK(hipEventRecord(copy_ev_, copy_stream_));
+  copy_pending_ = true;
 }
 
 void Engine::TakeDecoded(std::vector<DecodedJob>* out) {

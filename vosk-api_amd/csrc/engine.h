@@ -125,6 +125,34 @@ struct SegmentLattice {
 
 // Endpoint inputs of a stream (OnlineEndpoint [K]): decoder-segment frames,
 // trailing silence frames on the best path, final relative cost.
+// Pinned host blocks for asynchronous segment copies, shared by an engine
+// and the copies in flight (thread-safe; blocks are reused by size).
+class PinnedPool {
+ public:
+  ~PinnedPool();
+  char* Take(size_t bytes, size_t* cap);
+  void Give(char* p, size_t cap);
+
+ private:
+  std::mutex mu_;
+  std::vector<std::pair<size_t, char*>> free_;
+};
+
+// A segment's records being copied to the host (StartSegmentCopies): the
+// consumer calls Finish, which waits for the copy and fills the lattice.
+struct SegmentCopy {
+  std::shared_ptr<PinnedPool> pool;
+  char* block = nullptr;
+  size_t cap = 0;
+  hipEvent_t done = nullptr;
+  int device = 0;
+  size_t f = 0, a = 0, l = 0;
+  int nf = 0, na = 0;
+  long long nl = 0;
+  bool overflow = false;
+  void Finish(SegmentLattice* out);  // once, from any thread
+};
+
 struct EndpointProbe {
   int frames = 0, trailing_sil = 0;
   float final_relative_cost = 0;
@@ -271,6 +299,10 @@ class Engine {
   // The same for several streams with the copies batched.
   void CopySegmentLattices(const std::vector<int>& slots, const std::vector<SegmentLattice*>& outs,
                            bool drain = true);
+  // The same, asynchronously (pipeline state as of the last completed decoder
+  // job): the copies run on the copy stream, the next decoder launch waits for
+  // them on the device, and each SegmentCopy is finished by its consumer.
+  void StartSegmentCopies(const std::vector<int>& slots, std::vector<std::shared_ptr<SegmentCopy>>* out);
 
   // ---- asynchronous driving (BatchModel lanes: one thread steps the engine,
   // results are produced between steps without draining the pipeline)
@@ -411,8 +443,11 @@ class Engine {
   hipStream_t copy_stream_ = nullptr;  // segment lattice copies
   char* h_lat_stage_ = nullptr;        // pinned staging of segment lattice copies
   size_t lat_stage_bytes_ = 0;
-  DecSlot* h_copy_slots_ = nullptr;  // decoder-state snapshot of the segment copies
   long long copy_us_[4] = {0, 0, 0, 0}, copy_calls_ = 0;  // development (VOSK_AMD_COPY_DEBUG)
+  std::shared_ptr<PinnedPool> pinned_ = std::make_shared<PinnedPool>();
+  DecSlot* h_copy_slots_ = nullptr;  // decoder-state snapshot of the segment copies
+  hipEvent_t copy_ev_ = nullptr;  // last asynchronous segment copy (decoder launches wait for it)
+  bool copy_pending_ = false;
   // device: per-stream state
   float* d_samples_ = nullptr;
   float* d_raw_ = nullptr;  // [slots][raw_ring_] input-rate samples of resampled streams

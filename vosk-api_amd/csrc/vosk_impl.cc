@@ -873,34 +873,32 @@ void BatchModel::EmitSegments(Lane* L, const std::vector<BatchRecognizer*>& rs, 
   auto ns = [](clk::time_point a, clk::time_point b) {
     return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
   };
-  // the segments' lattice records, copied together
-  std::vector<std::shared_ptr<SegmentLattice>> sls(rs.size());
+  // the segments' lattice records: copies started together (asynchronous,
+  // finished by the result workers; the stream's next decoder launch waits
+  // for them on the device)
   std::vector<int> frames(rs.size()), cslots;
-  std::vector<SegmentLattice*> couts;
+  std::vector<size_t> ci;
   for (size_t i = 0; i < rs.size(); i++) {
-    sls[i] = TakeSegmentBuffer();
-    sls[i]->frames.clear();
-    sls[i]->arena.clear();
-    sls[i]->links.clear();
-    sls[i]->overflow = false;
     frames[i] = e->DeviceFramesDecoded(rs[i]->slot_);
     if (frames[i] > 0) {
       cslots.push_back(rs[i]->slot_);
-      couts.push_back(sls[i].get());
+      ci.push_back(i);
     }
   }
+  std::vector<std::shared_ptr<SegmentCopy>> started, copies(rs.size());
   const auto tc = clk::now();
-  if (!cslots.empty()) e->CopySegmentLattices(cslots, couts, false);
+  if (!cslots.empty()) e->StartSegmentCopies(cslots, &started);
+  for (size_t k = 0; k < ci.size(); k++) copies[ci[k]] = started[k];
   prof_[2] += ns(tc, clk::now());
   for (size_t i = 0; i < rs.size(); i++) {
     prof_[0]++;
-    prof_[1] += (long long)sls[i]->links.size();
-    EmitSegment(L, rs[i], final_segment, sls[i], frames[i]);
+    if (copies[i]) prof_[1] += copies[i]->nl;
+    EmitSegment(L, rs[i], final_segment, copies[i], frames[i]);
   }
 }
 
 void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment,
-                             std::shared_ptr<SegmentLattice> sl, int frames) {
+                             std::shared_ptr<SegmentCopy> copy, int frames) {
   const float shift = 0.01f * md_->dcb.frame_subsampling_factor;
   using clk = std::chrono::steady_clock;
   auto ns = [](clk::time_point a, clk::time_point b) {
@@ -914,10 +912,15 @@ void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment,
     r->tasks_++;
     L->tasks++;
   }
-  pool_->Submit([this, L, r, sl, seq, offset, frames, ns]() {
+  pool_->Submit([this, L, r, copy, seq, offset, frames, ns]() {
     const ModelData& m = *md_;
     MbrResult res;
+    std::shared_ptr<SegmentLattice> sl = TakeSegmentBuffer();
     try {
+      const auto tw = clk::now();
+      if (copy) copy->Finish(sl.get());
+      else *sl = SegmentLattice();
+      prof_[2] += ns(tw, clk::now());
       if (frames > 0) {
         RawLattice raw;
         const auto t0 = clk::now();

@@ -234,7 +234,7 @@ class BatchModel {
   // Segments of streams rs end (endpoint or end of stream): their lattice
   // records copied from HBM now (batched), MBR and JSON on the result workers.
   void EmitSegments(Lane* L, const std::vector<BatchRecognizer*>& rs, bool final_segment);
-  void EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, std::shared_ptr<SegmentLattice> sl,
+  void EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment, std::shared_ptr<SegmentCopy> copy,
                    int frames);
   std::shared_ptr<ModelData> md_;
   int samples_per_chunk_ = 0;
