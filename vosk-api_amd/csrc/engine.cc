@@ -1705,7 +1705,7 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
     if (c.nl > 0)
       HIPCHECK(hipMemcpyAsync(c.block + c.l, dec_.links + s * dec_.link_cap, sizeof(int4) * c.nl,
                               hipMemcpyDeviceToHost, copy_stream_));
-    HIPCHECK(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&c.done, hipEventDisableTiming | hipEventBlockingSync));  // a waiting worker sleeps, not spins
     HIPCHECK(hipEventRecord(c.done, copy_stream_));
   }
   // the stream's next decoder launch (which may reset and overwrite these

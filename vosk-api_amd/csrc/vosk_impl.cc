@@ -653,6 +653,7 @@ struct BatchModel::Lane {
   std::vector<BatchRecognizer*> by_slot;  // engine slot -> stream
   int queued = 0;   // chunks queued, not yet handed to the engine
   int streams_queued = 0;  // streams with a queued chunk
+  int last_batch = 0;      // streams in the last step's batch (dynamic batching)
   int handed = 0;   // chunks handed to the engine, work not finished
   int busy = 0;     // streams with work in the engine
   int tasks = 0;    // results in production
@@ -984,14 +985,23 @@ void BatchModel::LaneLoop(Lane* L) {
       if (L->stop) return;
       tw = clk::now();
       // dynamic batching (CudaOnlinePipelineDynamicBatcher, batch_model.cc:94-96):
-      // with the GPU idle, wait briefly for the other streams' chunks of this
-      // feeding round (until every stream has one, no push for 1 ms, or 4 ms)
+      // with the GPU idle, wait for the other streams' chunks of this feeding
+      // round: until every stream has one, or as many streams as the last
+      // batch had (up to 12 ms), else until no push for 2.5 ms.  A round
+      // split in two costs a second step as long as its slowest stream, far
+      // more than the feeding thread's pauses this waits out.
       if (L->queued > 0 && !e->PipelineBusy()) {
         const auto t0 = std::chrono::steady_clock::now();
+        const int expect = std::min((int)L->recs.size(), L->last_batch);
         while (L->streams_queued < (int)L->recs.size() && !L->stop) {
+          if (expect > 0 && L->streams_queued >= expect) break;
           const int before = L->queued;
-          L->cv.wait_for(lk, std::chrono::microseconds(1000));
-          if (L->queued == before || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(4)) break;
+          L->cv.wait_for(lk, std::chrono::microseconds(2500));
+          const auto waited = std::chrono::steady_clock::now() - t0;
+          if (waited > std::chrono::milliseconds(12)) break;
+          if (L->queued == before && (expect == 0 || waited > std::chrono::milliseconds(2))) {
+            if (expect == 0 || L->streams_queued * 2 >= expect) break;  // a straggler: go on
+          }
         }
       }
       for (BatchRecognizer* r : L->recs) {  // one chunk per stream per step
@@ -1008,6 +1018,7 @@ void BatchModel::LaneLoop(Lane* L) {
           active.push_back(r);
         }
       }
+      L->last_batch = (int)batch.size();
       // pipeline the stages while a backlog keeps them fed; a batch with
       // nothing queued behind it runs its stages in order (one sync, not three)
       pipelined = L->queued > 0 || e->PipelineBusy();
