@@ -48,7 +48,7 @@ constexpr int kFrontLds = 2048;       // epsilon frontier entries in LDS (more s
 // least this much room left; otherwise the sub-round winner checks run
 constexpr long long kDeferHeadroom = 1 << 20;
 #ifndef VAMD_DEC_UNROLL
-#define VAMD_DEC_UNROLL (2048 / VAMD_DEC_THREADS)
+#define VAMD_DEC_UNROLL (1024 / VAMD_DEC_THREADS)
 #endif
 constexpr int kUnroll = VAMD_DEC_UNROLL;            // (token, arc) items in flight per thread in the emitting pass
 constexpr unsigned long long kEmpty = 0xffffffffffffffffull;

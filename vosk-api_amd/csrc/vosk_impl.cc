@@ -178,10 +178,21 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
     }
   }
   if (ep.empty()) return;
-  std::vector<PathResult> pr;
-  engine->BestPaths(ep, false, &pr);
   const ModelData& m = engine->model();
   const float shift = 0.01f * m.dcb.frame_subsampling_factor;
+  if (!m.phone_is_silence.empty()) {  // (the engine's per-arc silence classes exist)
+    // the endpoint probe: trailing silence and final relative cost from the
+    // traceback kernel, without copying the paths (same walk as
+    // TrailingSilenceFrames over the best path)
+    std::vector<EndpointProbe> pr;
+    engine->ProbeEndpoints(ep, &pr);
+    for (size_t i = 0; i < ep.size(); i++)
+      er[i]->req_endpoint_ = EndpointRulesFire(m.endpoint, engine->NumFramesDecoded(ep[i]), pr[i].trailing_sil,
+                                               shift, pr[i].final_relative_cost);
+    return;
+  }
+  std::vector<PathResult> pr;
+  engine->BestPaths(ep, false, &pr);
   for (size_t i = 0; i < ep.size(); i++)
     er[i]->req_endpoint_ = EndpointRulesFire(m.endpoint, engine->NumFramesDecoded(ep[i]),
                                              TrailingSilenceFrames(m, pr[i].arcs), shift,
