@@ -22,7 +22,11 @@ Streams are test.wav tiled, shifted, gained and noised per BASELINE.md.
 
 Secondary keys: "engine_only" (the GPU engine stepped directly on
 HBM-resident audio, no host feeding or result production), the single-stream
-KaldiRecognizer latency (config 2) and the CPU baseline.
+KaldiRecognizer latency (config 2), 32 KaldiRecognizers on 32 threads
+("concurrent_recognizers": their calls share batched engine passes),
+"round_parts_ms" (feed / Wait / collect per round), "result_production"
+(lattice copy / build / determinize / MBR totals and the lane's host time)
+and the CPU baseline.
 
 Multi-GPU: one process per GPU (torchrun); streams are sharded by rank with
 no data-path collective ("scaling": "weak"); a barrier brackets the timed
