@@ -163,9 +163,13 @@ int vamd_engine_stage_times(VamdEngine *e, double *ms4, long long *launches4, in
  * written] */
 int vamd_engine_decoder_totals(VamdEngine *e, long long *out6);
 /* decoder phase clocks (env VOSK_AMD_DEC_PROFILE=1), summed over streams:
- * [cutoff, seed, expand, compact, eps-closure, commit, 0, frames] */
-int vamd_engine_decoder_phases(VamdEngine *e, long long *out24);
-/* the same per stream slot: out[max_streams][24] */
+ * the first eight of the decoder's counters [cutoff, seed, exp_tokens,
+ * exp_items, exp_winners, eps, commit_toks, commit_links] (s_memtime clocks;
+ * the full list is vosk/engine.py Engine.PHASES) */
+int vamd_engine_decoder_phases(VamdEngine *e, long long *out8);
+/* all decoder phase counters: writes min(cap, N) values, returns N (24) */
+int vamd_engine_decoder_phases_n(VamdEngine *e, long long *out, int cap);
+/* the N counters per stream slot: out[max_streams][N] */
 int vamd_engine_decoder_phases_per_stream(VamdEngine *e, long long *out);
 /* engine counters: [steps, launches, mfcc frames, chunk jobs, frames decoded] */
 int vamd_engine_counters(VamdEngine *e, long long *out5);
@@ -185,6 +189,14 @@ int vamd_batch_lane_stats(struct VoskBatchModel *m, int lane, int *load3, double
  * (lane threads), ms building raw lattices, ms prune + determinize + align,
  * ms MBR, ms formatting} */
 int vamd_batch_result_profile(struct VoskBatchModel *m, double *out13);
+/* dynamic batching: {lane steps, bounded waits that expired (a feeding
+ * round split in two steps), waits ended by a vosk_batch_model_wait caller
+ * before the round was complete} */
+int vamd_batch_batching_counters(struct VoskBatchModel *m, long long *out3);
+/* the lane's dynamic batching rule (host only, no GPU): 1 if a step would
+ * still wait for streams of the feeding round, given each stream's chunks
+ * pushed, chunks handed to the engine and input-ended flag */
+int vamd_feeding_round_incomplete(int n, const long long *pushed, const long long *taken, const int *ended);
 /* stream -> lane index it was admitted to */
 int vamd_batch_recognizer_lane(struct VoskBatchRecognizer *r);
 /* admission policy (host only, no GPU): replays `n` admissions against lanes

@@ -1,0 +1,113 @@
+"""The batch lane's dynamic batching rule (CudaOnlinePipelineDynamicBatcher,
+src/batch_model.cc:94-96; BatchModel::LaneLoop): a step waits, bounded, for
+the rest of the feeding round by chunk sequence -- every running stream that
+pushed chunk n-1 must have pushed chunk n, n being the furthest queued chunk.
+
+The CPU tests drive the rule through the host-only ABI entry; the GPU test
+feeds BatchRecognizers the test_gpu_batch.py way with one feeding pause
+longer than the bounded wait and checks that only that round is split."""
+import time
+
+import numpy as np
+import pytest
+
+from conftest import perturbed_stream
+
+
+def _inc(pushed, taken, ended=None):
+    from vosk import engine
+    return engine.feeding_round_incomplete(pushed, taken, ended or [0] * len(pushed))
+
+
+def test_nothing_queued_is_complete():
+    assert not _inc([0, 0, 0], [0, 0, 0])
+    assert not _inc([4, 4], [4, 4])
+
+
+def test_waits_for_streams_of_the_round():
+    # streams 0, 1 pushed their first chunk; 2, 3 have not yet
+    assert _inc([1, 1, 0, 0], [0, 0, 0, 0])
+    assert not _inc([1, 1, 1, 1], [0, 0, 0, 0])
+
+
+def test_split_round_does_not_perpetuate():
+    # round 2 split by a pause: streams 0, 1 were stepped, 2, 3 are queued.
+    # The second half goes at once (0 and 1 already handed chunk 2) ...
+    assert not _inc([2, 2, 2, 2], [2, 2, 1, 1])
+    # ... and round 3 waits for every stream again, not for half of them
+    assert _inc([3, 3, 2, 2], [2, 2, 2, 2])
+    assert not _inc([3, 3, 3, 3], [2, 2, 2, 2])
+
+
+def test_ended_and_lagging_streams_are_not_waited_for():
+    # stream 2 finished its input (FinishStream) at chunk 1
+    assert not _inc([2, 2, 1], [1, 1, 1], [0, 0, 1])
+    # stream 2 is far behind the round (paused without FinishStream)
+    assert not _inc([6, 6, 2], [5, 5, 2])
+    # a stream with more than one chunk queued offers its oldest
+    assert _inc([3, 2, 1], [1, 1, 1])
+
+
+N = 24
+ROUNDS = 16
+
+
+@pytest.mark.gpu
+def test_feeding_pause_splits_one_round_only(synth_model_noep, test_wave, monkeypatch):
+    import vosk
+    from vosk import engine
+    vosk.SetLogLevel(-1)
+    monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_model_noep)
+    model = vosk.BatchModel()
+    recs = [vosk.BatchRecognizer(model, 16000) for _ in range(N)]
+    data = [np.clip(perturbed_stream(test_wave, 40 + i, seconds=ROUNDS * 0.25 + 1), -32768, 32767)
+            .astype("<i2").tobytes() for i in range(N)]
+    pause_round = 8  # a round in which every stream pushes a chunk (8160-sample chunks, 4000-sample feeds)
+    steps = []
+    for r in range(ROUNDS):
+        before = engine.batch_batching_counters(model)["steps"]
+        for i in range(N):
+            recs[i].AcceptWaveform(data[i][r * 8000:(r + 1) * 8000])
+            if r == pause_round and i == N // 2:
+                time.sleep(0.010)  # longer than the bounded wait's 4 ms without a push
+        model.Wait()
+        steps.append(engine.batch_batching_counters(model)["steps"] - before)
+        for rec in recs:
+            while rec.Result():
+                pass
+    c = engine.batch_batching_counters(model)
+    chunk_rounds = [r for r in range(ROUNDS) if ((r + 1) * 4000) // 8160 > (r * 4000) // 8160]
+    assert pause_round in chunk_rounds
+    # every chunk round but the paused one is one step; the paused one is two
+    for r in chunk_rounds:
+        assert steps[r] == (2 if r == pause_round else 1), (r, steps)
+    assert c["split_rounds"] == 1, c
+    for rec in recs:
+        rec.FinishStream()
+    model.Wait()
+    del recs
+
+
+@pytest.mark.gpu
+def test_free_right_after_finish_stream(synth_model_noep, test_wave, monkeypatch):
+    """BatchRecognizers freed straight after FinishStream, with no Wait():
+    the free waits for the stream's queued chunks and its final result in
+    production on the worker pool (BatchModel::Release), so no worker touches
+    a freed recognizer.  Repeated over several generations of streams on one
+    model, with the model freed before its last recognizers."""
+    import gc
+    import vosk
+    vosk.SetLogLevel(-1)
+    monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_model_noep)
+    model = vosk.BatchModel()
+    for gen in range(3):
+        recs = [vosk.BatchRecognizer(model, 16000) for _ in range(8)]
+        for i, rec in enumerate(recs):
+            x = perturbed_stream(test_wave, 70 + 8 * gen + i, seconds=2.0 + 0.3 * i)
+            rec.AcceptWaveform(np.clip(x, -32768, 32767).astype("<i2").tobytes())
+            rec.FinishStream()
+        if gen == 2:
+            del model  # the recognizers keep the (refcounted) batch model alive
+            gc.collect()
+        del recs
+        gc.collect()

@@ -1644,24 +1644,31 @@ void PinnedPool::Give(char* p, size_t cap) {
   free_.push_back({cap, p});
 }
 
+CopyBatch::~CopyBatch() {
+  if (done) {
+    (void)hipSetDevice(device);
+    (void)hipEventSynchronize(done);  // never recycle a block a copy still writes
+    (void)hipEventDestroy(done);
+  }
+  if (block) pool->Give(block, cap);
+}
+
 void SegmentCopy::Finish(SegmentLattice* out) {
   out->frames.clear();
   out->arena.clear();
   out->links.clear();
   out->overflow = overflow;
-  if (!block) return;
-  (void)hipSetDevice(device);
-  HIPCHECK(hipEventSynchronize(done));
-  (void)hipEventDestroy(done);
-  done = nullptr;
+  if (!batch) return;
+  (void)hipSetDevice(batch->device);
+  HIPCHECK(hipEventSynchronize(batch->done));
+  const char* block = batch->block;
   const LatFrame* F = (const LatFrame*)(block + f);
   const int4* A = (const int4*)(block + a);
   const int4* L = (const int4*)(block + l);
   out->frames.assign(F, F + nf);
   out->arena.assign(A, A + na);
   out->links.assign(L, L + nl);
-  pool->Give(block, cap);
-  block = nullptr;
+  batch.reset();  // the last segment of the call returns the block
 }
 
 void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::shared_ptr<SegmentCopy>>* out) {
@@ -1677,6 +1684,9 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
   HIPCHECK(hipMemcpyAsync(h_copy_slots_, d_slots_, sizeof(DecSlot) * slots_.size(), hipMemcpyDeviceToHost,
                           copy_stream_));
   HIPCHECK(hipStreamSynchronize(copy_stream_));
+  // one pinned block and one completion event for all of the call's segments
+  size_t bytes = 0;
+  std::vector<int> copied;
   for (size_t i = 0; i < slots.size(); i++) {
     const DecSlot& st = h_copy_slots_[slots[i]];
     SegmentCopy& c = *(*out)[i];
@@ -1685,28 +1695,36 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
     c.na = st.arena_used;
     c.nl = std::min(st.links_used, dec_.link_cap);
     c.overflow = st.lat_ovf || st.frames + 1 > dec_.lat_frame_cap || st.err;
-    size_t bytes = 0;
     c.f = bytes;
     bytes += Align256(sizeof(LatFrame) * c.nf);
     c.a = bytes;
     bytes += Align256(sizeof(int4) * c.na);
     c.l = bytes;
     bytes += Align256(sizeof(int4) * c.nl);
-    c.pool = pinned_;
-    c.device = cfg_.device;
-    c.block = pinned_->Take(bytes, &c.cap);
-    const size_t s = (size_t)slots[i];
-    if (c.nf > 0)
-      HIPCHECK(hipMemcpyAsync(c.block + c.f, dec_.lat_frames + s * dec_.lat_frame_cap, sizeof(LatFrame) * c.nf,
-                              hipMemcpyDeviceToHost, copy_stream_));
-    if (c.na > 0)
-      HIPCHECK(hipMemcpyAsync(c.block + c.a, dec_.arena + s * dec_.arena_cap, sizeof(int4) * c.na,
-                              hipMemcpyDeviceToHost, copy_stream_));
-    if (c.nl > 0)
-      HIPCHECK(hipMemcpyAsync(c.block + c.l, dec_.links + s * dec_.link_cap, sizeof(int4) * c.nl,
-                              hipMemcpyDeviceToHost, copy_stream_));
-    HIPCHECK(hipEventCreateWithFlags(&c.done, hipEventDisableTiming | hipEventBlockingSync));  // a waiting worker sleeps, not spins
-    HIPCHECK(hipEventRecord(c.done, copy_stream_));
+    copied.push_back((int)i);
+  }
+  if (!copied.empty()) {
+    auto cb = std::make_shared<CopyBatch>();
+    cb->pool = pinned_;
+    cb->device = cfg_.device;
+    cb->block = pinned_->Take(bytes, &cb->cap);
+    for (int i : copied) {
+      SegmentCopy& c = *(*out)[i];
+      c.batch = cb;
+      const size_t s = (size_t)slots[i];
+      if (c.nf > 0)
+        HIPCHECK(hipMemcpyAsync(cb->block + c.f, dec_.lat_frames + s * dec_.lat_frame_cap,
+                                sizeof(LatFrame) * c.nf, hipMemcpyDeviceToHost, copy_stream_));
+      if (c.na > 0)
+        HIPCHECK(hipMemcpyAsync(cb->block + c.a, dec_.arena + s * dec_.arena_cap, sizeof(int4) * c.na,
+                                hipMemcpyDeviceToHost, copy_stream_));
+      if (c.nl > 0)
+        HIPCHECK(hipMemcpyAsync(cb->block + c.l, dec_.links + s * dec_.link_cap, sizeof(int4) * c.nl,
+                                hipMemcpyDeviceToHost, copy_stream_));
+    }
+    // a waiting worker sleeps, not spins
+    HIPCHECK(hipEventCreateWithFlags(&cb->done, hipEventDisableTiming | hipEventBlockingSync));
+    HIPCHECK(hipEventRecord(cb->done, copy_stream_));
   }
   // the stream's next decoder launch (which may reset and overwrite these
   // records) waits for the copies on the device

@@ -138,14 +138,23 @@ class PinnedPool {
   std::vector<std::pair<size_t, char*>> free_;
 };
 
-// A segment's records being copied to the host (StartSegmentCopies): the
-// consumer calls Finish, which waits for the copy and fills the lattice.
-struct SegmentCopy {
+// One StartSegmentCopies call's pinned block and completion event, shared by
+// the call's segments: the block goes back to the pool and the event is
+// destroyed when the last segment has been finished (one host allocation and
+// one event per call, not per segment).
+struct CopyBatch {
   std::shared_ptr<PinnedPool> pool;
   char* block = nullptr;
   size_t cap = 0;
   hipEvent_t done = nullptr;
   int device = 0;
+  ~CopyBatch();
+};
+
+// A segment's records being copied to the host (StartSegmentCopies): the
+// consumer calls Finish, which waits for the copy and fills the lattice.
+struct SegmentCopy {
+  std::shared_ptr<CopyBatch> batch;
   size_t f = 0, a = 0, l = 0;
   int nf = 0, na = 0;
   long long nl = 0;

@@ -733,8 +733,20 @@ int vamd_engine_decoder_totals(VamdEngine* e, long long* o6) {
 
 int vamd_engine_decoder_phases(VamdEngine* e, long long* o8) {
   API_TRY
-  e->eng->DecoderPhaseClocks(o8);
+  long long all[kDecProf];
+  e->eng->DecoderPhaseClocks(all);
+  for (int i = 0; i < 8; i++) o8[i] = all[i];  // the base ABI's eight slots
   return 0;
+  API_CATCH(-1)
+}
+
+int vamd_engine_decoder_phases_n(VamdEngine* e, long long* out, int cap) {
+  API_TRY
+  long long all[kDecProf];
+  e->eng->DecoderPhaseClocks(all);
+  const int n = std::min(cap, (int)kDecProf);
+  for (int i = 0; i < n; i++) out[i] = all[i];
+  return kDecProf;
   API_CATCH(-1)
 }
 
@@ -777,6 +789,22 @@ int vamd_batch_result_profile(VoskBatchModel* m, double* out13) {
   API_TRY
   ((BatchModel*)m)->ResultProfile(out13);
   return 0;
+  API_CATCH(-1)
+}
+
+int vamd_batch_batching_counters(VoskBatchModel* m, long long* out3) {
+  API_TRY
+  ((BatchModel*)m)->BatchingCounters(out3);
+  return 0;
+  API_CATCH(-1)
+}
+
+int vamd_feeding_round_incomplete(int n, const long long* pushed, const long long* taken, const int* ended) {
+  API_TRY
+  if (n < 0) VAMD_ERR("bad stream count");
+  std::vector<std::array<long long, 3>> s(n);
+  for (int i = 0; i < n; i++) s[i] = {pushed[i], taken[i], ended[i] ? 1LL : 0LL};
+  return FeedingRoundIncomplete(s) ? 1 : 0;
   API_CATCH(-1)
 }
 

@@ -664,8 +664,8 @@ struct BatchModel::Lane {
   std::vector<BatchRecognizer*> by_slot;  // engine slot -> stream
   int queued = 0;   // chunks queued, not yet handed to the engine
   int streams_queued = 0;  // streams with a queued chunk
-  int last_batch = 0;      // streams in the last step's batch (dynamic batching)
-  int handed = 0;   // chunks handed to the engine, work not finished
+  int waiters = 0;         // threads in WaitForCompletion: their feeding round is complete
+  int handed = 0;  // chunks handed to the engine, work not finished
   int busy = 0;     // streams with work in the engine
   int tasks = 0;    // results in production
   bool stop = false;
@@ -770,6 +770,28 @@ void BatchModel::ResultProfile(double* out) const {
 
 int BatchModel::LaneOf(const BatchRecognizer* r) const { return r->lane_; }
 
+void BatchModel::BatchingCounters(long long* out) const {
+  for (int i = 0; i < 3; i++) out[i] = batching_[i];
+}
+
+bool FeedingRoundIncomplete(const std::vector<std::array<long long, 3>>& s) {
+  long long n = 0;
+  for (const auto& x : s)
+    if (x[0] > x[1]) n = std::max(n, x[1] + 1);
+  if (n == 0) return false;
+  for (const auto& x : s)
+    if (!x[2] && x[0] == x[1] && x[0] == n - 1) return true;
+  return false;
+}
+
+// FeedingRoundIncomplete over a lane's streams (under the lane's mutex)
+bool BatchModel::RoundIncomplete(const std::vector<BatchRecognizer*>& recs) {
+  std::vector<std::array<long long, 3>> s;
+  s.reserve(recs.size());
+  for (const BatchRecognizer* r : recs) s.push_back({r->pushed_, r->taken_, r->ended_ ? 1LL : 0LL});
+  return FeedingRoundIncomplete(s);
+}
+
 void BatchModel::Admit(BatchRecognizer* r, int rate) {
   std::lock_guard<std::mutex> g(admit_mu_);
   std::vector<std::array<int, 2>> loads;
@@ -827,6 +849,7 @@ void BatchModel::Push(BatchRecognizer* r, std::vector<float>&& chunk, bool last)
     std::lock_guard<std::mutex> lk(L->mu);
     if (r->queue_.empty()) L->streams_queued++;
     r->queue_.push_back(BatchRecognizer::Chunk{std::move(chunk), last});
+    r->pushed_++;
     L->queued++;
     r->ended_ = last;  // a chunk after FinishStream starts a new utterance
   }
@@ -855,6 +878,24 @@ std::vector<std::array<int, 3>> BatchModel::LaneLoads() {
 // lattice callbacks run asynchronously on its worker threads
 // (batch_model.cc:69, batch_recognizer.cc:138-149).
 void BatchModel::WaitForCompletion() {
+  // the caller's feeding round is complete: every lane's dynamic batching
+  // stops waiting for more of it
+  for (auto& L : lanes_) {
+    {
+      std::lock_guard<std::mutex> lk(L->mu);
+      L->waiters++;
+    }
+    L->cv.notify_all();
+  }
+  struct Leave {
+    std::vector<std::unique_ptr<Lane>>& lanes;
+    ~Leave() {
+      for (auto& L : lanes) {
+        std::lock_guard<std::mutex> lk(L->mu);
+        L->waiters--;
+      }
+    }
+  } leave{lanes_};
   for (auto& L : lanes_) {
     std::unique_lock<std::mutex> lk(L->mu);
     L->done_cv.wait(lk, [&] {
@@ -996,24 +1037,29 @@ void BatchModel::LaneLoop(Lane* L) {
       if (L->stop) return;
       tw = clk::now();
       // dynamic batching (CudaOnlinePipelineDynamicBatcher, batch_model.cc:94-96):
-      // with the GPU idle, wait for the other streams' chunks of this feeding
-      // round: until every stream has one, or as many streams as the last
-      // batch had (up to 12 ms), else until no push for 2.5 ms.  A round
-      // split in two costs a second step as long as its slowest stream, far
-      // more than the feeding thread's pauses this waits out.
+      // with the GPU idle, wait for the rest of this feeding round, i.e. by
+      // chunk sequence: the round's chunk number n is the furthest queued
+      // chunk, and every running stream that has pushed chunk n-1 is waited
+      // for until it has pushed chunk n.  The wait ends early when a thread
+      // calls Wait() (its feeding round is complete) and is bounded (12 ms,
+      // or no push for 4 ms).  A round split by a feeding pause costs a
+      // second step as long as its slowest stream; the next round is whole
+      // again, since the rule looks at sequence numbers, not at the last
+      // batch's size.
       if (L->queued > 0 && !e->PipelineBusy()) {
-        const auto t0 = std::chrono::steady_clock::now();
-        const int expect = std::min((int)L->recs.size(), L->last_batch);
-        while (L->streams_queued < (int)L->recs.size() && !L->stop) {
-          if (expect > 0 && L->streams_queued >= expect) break;
+        const auto t0 = clk::now();
+        auto last_push = t0;
+        while (!L->stop && L->waiters == 0 && RoundIncomplete(L->recs)) {
           const int before = L->queued;
-          L->cv.wait_for(lk, std::chrono::microseconds(2500));
-          const auto waited = std::chrono::steady_clock::now() - t0;
-          if (waited > std::chrono::milliseconds(12)) break;
-          if (L->queued == before && (expect == 0 || waited > std::chrono::milliseconds(2))) {
-            if (expect == 0 || L->streams_queued * 2 >= expect) break;  // a straggler: go on
+          L->cv.wait_for(lk, std::chrono::microseconds(1000));
+          const auto now = clk::now();
+          if (L->queued != before) last_push = now;
+          if (now - t0 > std::chrono::milliseconds(12) || now - last_push > std::chrono::milliseconds(4)) {
+            batching_[1]++;  // bounded wait expired: the round is split
+            break;
           }
         }
+        if (L->waiters > 0 && RoundIncomplete(L->recs)) batching_[2]++;
       }
       for (BatchRecognizer* r : L->recs) {  // one chunk per stream per step
         if (r->queue_.empty()) continue;
@@ -1022,6 +1068,7 @@ void BatchModel::LaneLoop(Lane* L) {
         L->queued--;
         if (r->queue_.empty()) L->streams_queued--;
         r->handed_++;
+        r->taken_++;
         L->handed++;
         if (!r->busy_) {
           r->busy_ = true;
@@ -1029,7 +1076,6 @@ void BatchModel::LaneLoop(Lane* L) {
           active.push_back(r);
         }
       }
-      L->last_batch = (int)batch.size();
       // pipeline the stages while a backlog keeps them fed; a batch with
       // nothing queued behind it runs its stages in order (one sync, not three)
       pipelined = L->queued > 0 || e->PipelineBusy();
@@ -1037,6 +1083,7 @@ void BatchModel::LaneLoop(Lane* L) {
     const auto ts = clk::now();
     prof_[7] += ns(tw, ts);
     prof_[11]++;
+    batching_[0]++;
     bool failed = false;
     const bool tr = trace && (++iter < 300 || iter % 20000 == 0);
     if (tr)

@@ -166,6 +166,13 @@ class BatchRecognizer;
 // loads[i] = {pending chunks, streams}.
 int PickLane(const std::vector<std::array<int, 2>>& loads);
 
+// Dynamic batching rule of a lane: per stream {chunks
+// pushed, chunks handed to the engine, input ended}.  The feeding round's
+// chunk number n is the furthest queued chunk (a stream with a queued chunk
+// offers chunk handed+1); the round is incomplete while a running stream that
+// pushed chunk n-1 has not pushed chunk n.
+bool FeedingRoundIncomplete(const std::vector<std::array<long long, 3>>& streams);
+
 // Host threads for the batch path's result production: segment lattice ->
 // word lattice -> MBR -> JSON, off the GPU lanes' critical path (the
 // reference runs lattice post-processing on num_worker_threads=-1 worker
@@ -226,11 +233,13 @@ class BatchModel {
   // ms MBR, ms formatting}
   void ResultProfile(double* out7) const;
   int LaneOf(const BatchRecognizer* r) const;
+  void BatchingCounters(long long* out3) const;
 
  private:
   struct Lane;
   Engine* LaneEngine(int i);
   void LaneLoop(Lane* L);
+  static bool RoundIncomplete(const std::vector<BatchRecognizer*>& recs);
   // Segments of streams rs end (endpoint or end of stream): their lattice
   // records copied from HBM now (batched), MBR and JSON on the result workers.
   void EmitSegments(Lane* L, const std::vector<BatchRecognizer*>& rs, bool final_segment);
@@ -252,6 +261,9 @@ class BatchModel {
   // format; lane loop: dynamic batching wait, step, endpoints, finals, steps;
   // endpoint probe launches (within endpoints)
   std::atomic<long long> prof_[13] = {};
+  // dynamic batching: {steps, bounded waits that expired (split rounds),
+  // waits ended by a Wait() caller}
+  std::atomic<long long> batching_[3] = {};
   ~BatchModel();
 };
 
@@ -286,6 +298,8 @@ class BatchRecognizer {
   int lane_ = -1, slot_ = -1;
   std::deque<Chunk> queue_;
   int handed_ = 0;          // chunks given to the engine whose work is not finished
+  long long pushed_ = 0;    // chunks pushed since admission (the stream's chunk sequence)
+  long long taken_ = 0;     // chunks handed to the engine since admission
   bool busy_ = false;       // has work in the engine
   bool finishing_ = false;  // last chunk handed: final result when the stream is idle
   int tasks_ = 0;           // results in production on the worker pool

@@ -53,6 +53,9 @@ _SIGS = {
     "vamd_engine_flush": (C.c_int, [_vp]),
     "vamd_engine_decoder_totals": (C.c_int, [_vp, _vp]),
     "vamd_engine_decoder_phases": (C.c_int, [_vp, _vp]),
+    "vamd_engine_decoder_phases_n": (C.c_int, [_vp, _vp, C.c_int]),
+    "vamd_batch_batching_counters": (C.c_int, [_vp, _vp]),
+    "vamd_feeding_round_incomplete": (C.c_int, [C.c_int, _vp, _vp, _vp]),
     "vamd_engine_decoder_phases_per_stream": (C.c_int, [_vp, _vp]),
     "vamd_engine_set_step_samples": (C.c_int, [_vp, C.c_int]),
     "vamd_engine_stage_times": (C.c_int, [_vp, _vp, _vp, C.c_int]),
@@ -93,6 +96,22 @@ def admission_replay(drain_per_step, chunks):
     out = np.zeros(len(c), np.int32)
     _chk(_c.vamd_admission_replay(len(d), d.ctypes.data, len(c), c.ctypes.data, out.ctypes.data))
     return out
+
+
+def feeding_round_incomplete(pushed, taken, ended):
+    """Host-only: the lane's dynamic batching rule (FeedingRoundIncomplete):
+    True while a step would still wait for streams of the feeding round."""
+    p = np.ascontiguousarray(pushed, np.int64)
+    t = np.ascontiguousarray(taken, np.int64)
+    e = np.ascontiguousarray(ended, np.int32)
+    return bool(_chk(_c.vamd_feeding_round_incomplete(len(p), p.ctypes.data, t.ctypes.data, e.ctypes.data)))
+
+
+def batch_batching_counters(model):
+    """{steps, split_rounds, released_by_wait} of a vosk.BatchModel's lanes."""
+    o = np.zeros(3, np.int64)
+    _chk(_c.vamd_batch_batching_counters(model._handle, o.ctypes.data))
+    return dict(zip(("steps", "split_rounds", "released_by_wait"), (int(x) for x in o)))
 
 
 def batch_lanes(model):
@@ -369,7 +388,9 @@ class Engine:
 
     def decoder_phases(self):
         out = np.zeros(len(self.PHASES), np.int64)
-        _chk(_c.vamd_engine_decoder_phases(self.h, out.ctypes.data))
+        n = _c.vamd_engine_decoder_phases_n(self.h, out.ctypes.data, len(out))
+        if n != len(out):
+            raise RuntimeError(f"decoder phase counters: library has {n}, binding expects {len(out)}")
         return dict(zip(self.PHASES, out.tolist()))
 
     # decoder.hip Prof: s_memtime clocks per phase (slots 0-10), then counts
