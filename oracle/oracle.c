@@ -1236,6 +1236,16 @@ static void kh_order(const khash* h, int* order, int* cnt) {
 
 static int cmp_float_nth(const void* a, const void* b) { return cmp_float(a, b); }
 
+/* work counters of orc_decode_kaldi (diagnostics: how much of a frame is
+   the sequential epsilon queue): frames, emitting items examined, emitting
+   relaxations accepted, tokens created by the emitting pass, epsilon-queue
+   pops, pops skipped (cost >= cutoff), epsilon relaxations below the cutoff,
+   tokens created by the epsilon pass, re-queued improvements */
+static long long g_kstats[9];
+void orc_kaldi_stats(long long* out, int reset) {
+  for (int i = 0; i < 9; i++) { out[i] = g_kstats[i]; if (reset) g_kstats[i] = 0; }
+}
+
 int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, const orc_dec_opts* o,
                      int use_final, orc_dec_result* r) {
   const int S = g->num_states;
@@ -1293,14 +1303,19 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
       const int s_ = queue[--qn_];                                                 \
       const int e_ = h.where[s_];                                                  \
       const float cc_ = h.cost[e_];                                                \
-      if (cc_ >= (cutoff_)) continue;                                              \
+      g_kstats[4]++;                                                               \
+      if (cc_ >= (cutoff_)) { g_kstats[5]++; continue; }                           \
       const int src_ = -2 - e_; /* source: element e_ of this frame (resolved at commit) */ \
       for (int64_t a_ = g->eps_begin[s_]; a_ < g->arc_begin[s_ + 1]; a_++) {       \
         const float tot_ = cc_ + g->weight[a_];                                    \
         if (tot_ < (cutoff_)) {                                                    \
           int ch_;                                                                 \
           const int d_ = g->nextstate[a_];                                         \
+          const int nb_ = h.n;                                                     \
           kh_find_or_add(&h, d_, tot_, src_, (int)a_, &ch_);                       \
+          g_kstats[6]++;                                                           \
+          if (h.n > nb_) g_kstats[7]++;                                            \
+          else if (ch_) g_kstats[8]++;                                             \
           if (ch_ && g->eps_begin[d_] < g->arc_begin[d_ + 1]) { ENSURE(queue, qcap, qn_ + 1, int); queue[qn_++] = d_; } \
         }                                                                          \
       }                                                                            \
@@ -1386,7 +1401,10 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
         if (tot >= next_cutoff) continue;
         if (tot + adaptive < next_cutoff) next_cutoff = tot + adaptive;
         int ch;
+        const int nb = h.n;
         kh_find_or_add(&h, g->nextstate[a], tot, cur_idx[i], (int)a, &ch);
+        g_kstats[2]++;
+        if (h.n > nb) g_kstats[3]++;
       }
     }
     /* ---- ProcessNonemitting(next_cutoff) */
@@ -1407,6 +1425,8 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
     if (r->cutoff) r->cutoff[f] = cutoff;
     if (r->next_cutoff) r->next_cutoff[f] = next_cutoff;
     if (r->arcs_emit) r->arcs_emit[f] = examined;
+    g_kstats[0]++;
+    g_kstats[1] += examined;
     if (r->best) { float b = INFINITY; for (int i = 0; i < ncur; i++) if (cur_cost[i] < b) b = cur_cost[i]; r->best[f + 1] = b; }
   }
 #undef ENSURE

@@ -70,8 +70,10 @@ def test_real_model_transcripts(gold, test_wave):
     rec.SetWords(True)
     rec.SetPartialWords(True)
     texts, words = [], []
+    # test_wave holds the samples after the RIFF header (wave.readframes), so
+    # 4000-frame reads are 8000-byte slices from byte 0 (vosk.ipynb's loop)
     data = test_wave.astype("<i2").tobytes()
-    for i in range(44, len(data), 8000):
+    for i in range(0, len(data), 8000):
         if rec.AcceptWaveform(data[i:i + 8000]):
             r = json.loads(rec.Result())
             texts.append(r["text"])
