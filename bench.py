@@ -192,12 +192,22 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-lattice", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline: seconds per stream")
+    ap.add_argument("--lanes", default=None,
+                    help="in-library lanes mode (one process, no torchrun): the BatchModel runs one lane "
+                         "per listed device (VOSK_AMD_BATCH_DEVICES, e.g. 0,1,2,3,4,5,6,7 or 0,0), "
+                         "--streams per lane, admission by the library's PickLane")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
-    os.environ["VOSK_AMD_DEVICE"] = str(local_rank)  # one BatchModel lane (GPU) per rank
+    if args.lanes:
+        if world > 1:
+            raise SystemExit("bench.py --lanes runs as one process (the library drives every lane)")
+        os.environ["VOSK_AMD_BATCH_DEVICES"] = args.lanes
+        os.environ.pop("VOSK_AMD_DEVICE", None)
+    else:
+        os.environ["VOSK_AMD_DEVICE"] = str(local_rank)  # one BatchModel lane (GPU) per rank
     dist = None
     if world > 1:
         import torch
@@ -265,7 +275,8 @@ def run_api(args, model, dist, rank, world, base):
     stream, Wait(), Result() of every stream; FinishStream at the end."""
     import vosk
     from vosk import engine as ve
-    S = args.streams
+    lanes = [int(x) for x in args.lanes.split(",") if x] if args.lanes else [0]
+    S = args.streams * len(lanes)
     W = args.warmup
     K = args.steps if args.steps is not None else max(1, int(round(args.stream_seconds * SR * 2 / FEED_BYTES)) - W)
     rounds = W + K
@@ -333,6 +344,8 @@ def run_api(args, model, dist, rank, world, base):
         dist.barrier()
     elapsed = _max_over_ranks(dist, t1 - t0)
     audio_s = K * FEED_BYTES / 2 / SR * S * world
+    nl = ve.batch_lanes(bm)
+    lane_streams = [sum(1 for r in recs if ve.batch_recognizer_lane(r) == li) for li in range(nl)]
     st = ve.batch_lane_stats(bm, 0)
     rprof = ve.batch_result_profile(bm)
     nonempty = sum(1 for t in texts if t.strip())
@@ -352,7 +365,8 @@ def run_api(args, model, dist, rank, world, base):
     nnet_tflops = nnet_flops / (nnet_ms * 1e-3) / 1e12 if nnet_ms else 0.0
     lat_ms = np.array(lat) * 1e3 if lat else np.zeros(1)
     return {
-        "metric": METRIC, "value": round(audio_s / elapsed, 2), "unit": "xRT", "n_gpus": world,
+        "metric": METRIC, "value": round(audio_s / elapsed, 2), "unit": "xRT",
+        "n_gpus": len(set(lanes)) if args.lanes else world,
         "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic: test.wav tiled/shifted/gain/noise per BASELINE.md, s16le host buffers; "
@@ -360,11 +374,14 @@ def run_api(args, model, dist, rank, world, base):
                 "HCLr + trigram Gr expanded to a static graph)",
         "config": {"workload": "config3: test_gpu_batch.py loop through vosk_batch_* (BatchModel + "
                                "BatchRecognizer, 8000-byte feeds, Wait, Result per round), "
-                               f"{S} streams/GPU x {rounds * FEED_BYTES / 2 / SR:.0f} s, 1xMI355X per rank",
-                   "model": os.path.basename(model.rstrip("/")), "streams_per_gpu": S,
+                               f"{args.streams} streams/lane x {rounds * FEED_BYTES / 2 / SR:.0f} s, "
+                               + (f"one process, in-library lanes on devices {args.lanes}" if args.lanes
+                                  else "1xMI355X per rank"),
+                   "model": os.path.basename(model.rstrip("/")), "streams_per_gpu": args.streams,
                    "global_streams": S * world, "feed_bytes": FEED_BYTES, "chunk_samples": 8160,
                    "frames_per_chunk": 51, "beam": 13.0, "max_active": 7000, "lattice_beam": 6.0,
-                   "parallelism": f"dp{world}",
+                   "parallelism": f"lanes{len(lanes)}" if args.lanes else f"dp{world}",
+                   "lane_streams": lane_streams,
                    "pipeline": "lane thread: front(s) || nnet(s-1) || decoder(s-2) on 3 HIP streams "
                                "while chunks are queued; a round with nothing behind it runs its "
                                "stages in order; MBR results on host worker threads"},

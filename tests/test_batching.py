@@ -111,3 +111,60 @@ def test_free_right_after_finish_stream(synth_model_noep, test_wave, monkeypatch
             gc.collect()
         del recs
         gc.collect()
+
+
+def _decode_batch(vosk, waves, pattern):
+    model = vosk.BatchModel()
+    recs = [vosk.BatchRecognizer(model, 16000) for _ in waves]
+    datas = [np.clip(w, -32768, 32767).astype("<i2").tobytes() for w in waves]
+    out = [[] for _ in waves]
+
+    def collect():
+        for i, r in enumerate(recs):
+            while True:
+                res = r.Result()
+                if not res:
+                    break
+                out[i].append(res)
+
+    n = max(len(d) for d in datas)
+    for o in range(0, n, 8000):
+        for i, r in enumerate(recs):
+            if o < len(datas[i]):
+                r.AcceptWaveform(datas[i][o:o + 8000])
+        if pattern == "wait_per_round":
+            model.Wait()
+            collect()
+    for r in recs:
+        r.FinishStream()
+    model.Wait()
+    collect()
+    from vosk import engine
+    lanes = [engine.batch_recognizer_lane(r) for r in recs]
+    nl = engine.batch_lanes(model)
+    del recs
+    del model
+    return out, lanes, nl
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", ["wait_per_round", "queued_upfront"])
+def test_two_lanes_on_one_device_equal_one_lane(synth_model_ep, test_wave, monkeypatch, pattern):
+    """The in-library multi-GPU path (BatchModel lanes, admission by
+    PickLane; src/batch_model.cc:23-100) on the one GPU available: two lanes
+    on device 0 (VOSK_AMD_BATCH_DEVICES=0,0) give every stream the same result
+    messages as one lane, and both lanes take streams."""
+    import vosk
+    vosk.SetLogLevel(-1)
+    monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_model_ep)
+    monkeypatch.delenv("VOSK_AMD_DEVICE", raising=False)
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
+    waves = [perturbed_stream(test_wave, 300 + i, seconds=5.0 + 0.9 * i) for i in range(10)]
+    monkeypatch.setenv("VOSK_AMD_BATCH_DEVICES", "0")
+    one, lanes1, n1 = _decode_batch(vosk, waves, pattern)
+    monkeypatch.setenv("VOSK_AMD_BATCH_DEVICES", "0,0")
+    two, lanes2, n2 = _decode_batch(vosk, waves, pattern)
+    assert (n1, n2) == (1, 2)
+    assert set(lanes1) == {0} and set(lanes2) == {0, 1}, lanes2
+    assert all(len(r) >= 1 for r in one)
+    assert one == two

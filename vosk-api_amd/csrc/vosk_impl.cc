@@ -672,13 +672,28 @@ struct BatchModel::Lane {
   std::thread thread;
 };
 
-// GPUs of the batch path: VOSK_AMD_DEVICE / LOCAL_RANK pin one (one process
-// per GPU deployments); otherwise every visible device (VOSK_AMD_BATCH_GPUS caps).
+// GPUs of the batch path: VOSK_AMD_BATCH_DEVICES lists the lanes' devices
+// explicitly (repeats allowed: "0,0" runs two lanes on device 0);
+// VOSK_AMD_DEVICE / LOCAL_RANK pin one (one process per GPU deployments);
+// otherwise every visible device (VOSK_AMD_BATCH_GPUS caps).
 static std::vector<int> BatchDevices() {
-  if (getenv("VOSK_AMD_DEVICE") || getenv("LOCAL_RANK")) return {DeviceFromEnv()};
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
     VAMD_ERR("no HIP device available: the MI355X batch path requires a GPU");
+  if (const char* list = getenv("VOSK_AMD_BATCH_DEVICES")) {
+    std::vector<int> d;
+    std::stringstream ss(list);
+    std::string item;
+    while (std::getline(ss, item, ',')) {
+      if (item.empty()) continue;
+      const int dev = atoi(item.c_str());
+      if (dev < 0 || dev >= n) VAMD_ERR("VOSK_AMD_BATCH_DEVICES: device " << dev << " of " << n);
+      d.push_back(dev);
+    }
+    if (d.empty()) VAMD_ERR("VOSK_AMD_BATCH_DEVICES lists no device");
+    return d;
+  }
+  if (getenv("VOSK_AMD_DEVICE") || getenv("LOCAL_RANK")) return {DeviceFromEnv()};
   const int cap = EnvInt("VOSK_AMD_BATCH_GPUS", n);
   std::vector<int> d;
   for (int i = 0; i < std::min(n, std::max(cap, 1)); i++) d.push_back(i);
