@@ -1155,24 +1155,30 @@ int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const or
 }
 
 /* ===================================================================== */
-/* Kaldi-sequential token passing (TEST INFRASTRUCTURE: quantifies the    */
-/* order-independent formulation above against the decoder as Kaldi runs  */
-/* it).  Restates LatticeFasterDecoderTpl (decoder/lattice-faster-        */
-/* decoder.cc [K], shared by the LatticeIncrementalDecoder the reference  */
-/* uses, src/recognizer.cc:39-43) operation for operation:                */
-/*  - toks_ is a HashList<StateId, Token*> (util/hash-list-inl.h): its    */
-/*    list order is by bucket (state % hash_size) in order of the bucket's */
-/*    first occupancy, then insertion order within a bucket; hash_size    */
-/*    starts at 1000 and grows to tok_cnt * hash_ratio (PossiblyResizeHash)*/
+/* Kaldi-sequential token passing: the decoder as Kaldi runs it           */
+/* (decoder/lattice-faster-decoder.cc [K], LatticeFasterDecoderTpl, whose  */
+/* search the LatticeIncrementalDecoder of the reference shares,          */
+/* src/recognizer.cc:39-43), which the GPU decoder reproduces by default  */
+/* (DESIGN.md §4).  TEST INFRASTRUCTURE.  Operation for operation:         */
+/*  - toks_ is a HashList<StateId, Token*> (util/hash-list-inl.h): list    */
+/*    order by bucket (state % hash_size) in order of the bucket's first   */
+/*    occupancy, then insertion order within a bucket; hash_size is 1000   */
+/*    for a new decoder (kept across InitDecoding: opts.hash_size in,      */
+/*    result.hash_size out) and grows to tok_cnt * hash_ratio (2) at each  */
+/*    ProcessEmitting (PossiblyResizeHash)                                 */
 /*  - GetCutoff: the first minimum in list order is best_elem; nth_element */
 /*    for max_active / min_active                                          */
-/*  - ProcessEmitting: seed from best_elem's arcs, then every token in    */
-/*    list order with cost <= cutoff, its emitting arcs in graph order,   */
-/*    skipping tot >= next_cutoff and tightening next_cutoff as it goes   */
-/*    (FindOrAddToken keeps the minimum)                                  */
-/*  - ProcessNonemitting: queue = list order of states with epsilon arcs, */
-/*    LIFO (pop_back), cost >= cutoff skipped, improved states re-queued  */
-/* Backpointers: the (source token, arc) of a token's last improvement.  */
+/*  - ProcessEmitting: seed next_cutoff from best_elem's arcs, then every  */
+/*    token in list order with cost <= cutoff, its emitting arcs in graph  */
+/*    order: skip tot >= next_cutoff, tighten next_cutoff to tot +         */
+/*    adaptive_beam; every accepted relaxation is a forward link and       */
+/*    FindOrAddToken keeps the minimum cost                                */
+/*  - ProcessNonemitting: queue = list order of tokens with epsilon arcs,  */
+/*    LIFO (pop_back), cost >= cutoff skipped, a token's forward links     */
+/*    replaced at each expansion, created / cheaper tokens re-queued       */
+/* Backpointer of a token (this restatement's 1-best; Kaldi reads the     */
+/* best path from the lattice): the (source, arc) of its minimum          */
+/* (cost, arc) relaxation, the GPU key minimum's tie rule.                */
 /* ===================================================================== */
 typedef struct {
   int* where;       /* per state: element index in the frame being built, -1 */
@@ -1207,7 +1213,8 @@ static void kh_clear(khash* h) {
   h->nranks = 0;
 }
 
-/* FindOrAddToken: returns the element; *changed = created or improved */
+/* FindOrAddToken: *changed = created or a strictly lower cost (Kaldi's
+   test); the backpointer follows the minimum (cost, arc) */
 static int kh_find_or_add(khash* h, int s, float tot, int bp, int arc, int* changed) {
   int e = h->where[s];
   if (e < 0) {
@@ -1221,8 +1228,12 @@ static int kh_find_or_add(khash* h, int s, float tot, int bp, int arc, int* chan
     *changed = 1;
     return e;
   }
-  if (h->cost[e] > tot) { h->cost[e] = tot; h->bp[e] = bp; h->arc[e] = arc; *changed = 1; }
-  else *changed = 0;
+  *changed = 0;
+  if (tot < h->cost[e]) {
+    h->cost[e] = tot; h->bp[e] = bp; h->arc[e] = arc; *changed = 1;
+  } else if (tot == h->cost[e] && (unsigned)arc < (unsigned)h->arc[e]) {
+    h->bp[e] = bp; h->arc[e] = arc;
+  }
   return e;
 }
 
@@ -1234,8 +1245,6 @@ static void kh_order(const khash* h, int* order, int* cnt) {
   for (int i = 0; i < h->n; i++) order[cnt[h->bucket_rank[h->bucket[i]]]++] = i;
 }
 
-static int cmp_float_nth(const void* a, const void* b) { return cmp_float(a, b); }
-
 /* work counters of orc_decode_kaldi (diagnostics: how much of a frame is
    the sequential epsilon queue): frames, emitting items examined, emitting
    relaxations accepted, tokens created by the emitting pass, epsilon-queue
@@ -1246,129 +1255,172 @@ void orc_kaldi_stats(long long* out, int reset) {
   for (int i = 0; i < 9; i++) { out[i] = g_kstats[i]; if (reset) g_kstats[i] = 0; }
 }
 
+typedef struct {
+  khash h;
+  int* order; int* cnt; int ocap, ccap;
+  int* queue; int qcap;
+  int* elem_pos;     /* element -> list position (frame being committed) */
+  int* a_prev; int* a_arc; int narena, acap;  /* committed tokens: backpointer, arc */
+  int* cur_state; float* cur_cost; int* cur_idx; int ncur, cur_cap;
+} kdec;
+
+static void kd_list_order(kdec* d) {
+  khash* h = &d->h;
+  if (h->n + 1 > d->ocap) { d->ocap = 2 * (h->n + 1); d->order = (int*)realloc(d->order, sizeof(int) * d->ocap); }
+  if (h->nranks + 2 > d->ccap) { d->ccap = 2 * (h->nranks + 2); d->cnt = (int*)realloc(d->cnt, sizeof(int) * d->ccap); }
+  kh_order(h, d->order, d->cnt);
+}
+
+/* ProcessNonemitting over the frame being built */
+static void kd_nonemitting(const orc_graph* g, kdec* d, float cutoff) {
+  khash* h = &d->h;
+  kd_list_order(d);
+  int qn = 0;
+  for (int q = 0; q < h->n; q++) {
+    const int s = h->st[d->order[q]];
+    if (g->eps_begin[s] < g->arc_begin[s + 1]) {
+      if (qn + 1 > d->qcap) { d->qcap = 2 * (qn + 1); d->queue = (int*)realloc(d->queue, sizeof(int) * d->qcap); }
+      d->queue[qn++] = s;
+    }
+  }
+  while (qn > 0) {
+    const int s = d->queue[--qn];
+    const int e = h->where[s];
+    const float cc = h->cost[e];
+    g_kstats[4]++;
+    if (cc >= cutoff) { g_kstats[5]++; continue; }
+    const int src = -2 - e;  /* element e of this frame (resolved at commit) */
+    for (int64_t a = g->eps_begin[s]; a < g->arc_begin[s + 1]; a++) {
+      const float tot = cc + g->weight[a];
+      if (tot < cutoff) {
+        int ch;
+        const int dst = g->nextstate[a];
+        const int nb = h->n;
+        kh_find_or_add(h, dst, tot, src, (int)a, &ch);
+        g_kstats[6]++;
+        if (h->n > nb) g_kstats[7]++;
+        else if (ch) g_kstats[8]++;
+        if (ch && g->eps_begin[dst] < g->arc_begin[dst + 1]) {
+          if (qn + 1 > d->qcap) { d->qcap = 2 * (qn + 1); d->queue = (int*)realloc(d->queue, sizeof(int) * d->qcap); }
+          d->queue[qn++] = dst;
+        }
+      }
+    }
+  }
+}
+
+/* commit the frame being built (list order becomes the current token order);
+   its tokens and epsilon links go to the lattice output as frame k */
+static void kd_commit(const orc_graph* g, kdec* d, orc_dec_result* r, int k, float cutoff, float cost_offset) {
+  khash* h = &d->h;
+  const int n = h->n;
+  kd_list_order(d);
+  d->elem_pos = (int*)realloc(d->elem_pos, sizeof(int) * (n + 1));
+  for (int q = 0; q < n; q++) d->elem_pos[d->order[q]] = q;
+  if (n > d->cur_cap) {
+    d->cur_cap = 2 * n;
+    d->cur_state = (int*)realloc(d->cur_state, sizeof(int) * d->cur_cap);
+    d->cur_cost = (float*)realloc(d->cur_cost, sizeof(float) * d->cur_cap);
+    d->cur_idx = (int*)realloc(d->cur_idx, sizeof(int) * d->cur_cap);
+  }
+  const int base = d->narena;
+  if (d->narena + n > d->acap) {
+    while (d->narena + n > d->acap) d->acap *= 2;
+    d->a_prev = (int*)realloc(d->a_prev, sizeof(int) * d->acap);
+    d->a_arc = (int*)realloc(d->a_arc, sizeof(int) * d->acap);
+  }
+  for (int q = 0; q < n; q++) {
+    const int e = d->order[q];
+    int bp = h->bp[e];
+    if (bp <= -2) bp = base + d->elem_pos[-2 - bp];  /* epsilon source in this frame */
+    d->a_prev[base + q] = bp;
+    d->a_arc[base + q] = h->arc[e];
+    d->cur_state[q] = h->st[e];
+    d->cur_cost[q] = h->cost[e];
+    d->cur_idx[q] = base + q;
+  }
+  d->narena += n;
+  d->ncur = n;
+  kh_clear(h);
+  if (!r->lat_frame_begin) return;
+  r->lat_frame_begin[k] = r->lat_ntok;
+  r->lat_cost_offset[k] = cost_offset;
+  for (int i = 0; i < n; i++) {
+    if (r->lat_ntok < r->lat_tok_cap) {
+      r->lat_tok_state[r->lat_ntok] = d->cur_state[i];
+      r->lat_tok_cost[r->lat_ntok] = d->cur_cost[i];
+    }
+    r->lat_ntok++;
+  }
+  r->lat_frame_begin[k + 1] = r->lat_ntok;
+  /* a token's epsilon links are those of its last expansion: its final cost,
+     when below the cutoff (ProcessNonemitting never expands the others) */
+  for (int i = 0; i < n; i++) {
+    const float c = d->cur_cost[i];
+    if (c >= cutoff) continue;
+    const int s = d->cur_state[i];
+    for (int64_t a = g->eps_begin[s]; a < g->arc_begin[s + 1]; a++)
+      if (c + g->weight[a] < cutoff) lat_link(r, k, s, (int)a, 0.0f);
+  }
+}
+
 int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, const orc_dec_opts* o,
                      int use_final, orc_dec_result* r) {
   const int S = g->num_states;
-  khash h;
-  memset(&h, 0, sizeof(h));
-  h.where = (int*)malloc(sizeof(int) * S);
-  for (int s = 0; s < S; s++) h.where[s] = -1;
-  h.cap = 1024;
-  h.st = (int*)malloc(sizeof(int) * h.cap); h.cost = (float*)malloc(sizeof(float) * h.cap);
-  h.bp = (int*)malloc(sizeof(int) * h.cap); h.arc = (int*)malloc(sizeof(int) * h.cap);
-  h.bucket = (int*)malloc(sizeof(int) * h.cap);
-  kh_set_size(&h, 1000);  /* the decoder's constructor: toks_.SetSize(1000) */
-  /* arena of committed tokens: backpointer (arena index) and arc */
-  int acap = 1 << 16, narena = 0;
-  int* a_prev = (int*)malloc(sizeof(int) * acap);
-  int* a_arc = (int*)malloc(sizeof(int) * acap);
-  int* cur_state = NULL; float* cur_cost = NULL; int* cur_idx = NULL; int ccap = 0, ncur = 0;
-  int* order = NULL; int* cnt = NULL; int ocap = 0;
-  float* tmp = NULL; int tcap = 0;
-  int* queue = NULL; int qcap = 0;
+  kdec d;
+  memset(&d, 0, sizeof(d));
+  khash* h = &d.h;
+  h->where = (int*)malloc(sizeof(int) * S);
+  for (int s = 0; s < S; s++) h->where[s] = -1;
+  h->cap = 1024;
+  h->st = (int*)malloc(sizeof(int) * h->cap); h->cost = (float*)malloc(sizeof(float) * h->cap);
+  h->bp = (int*)malloc(sizeof(int) * h->cap); h->arc = (int*)malloc(sizeof(int) * h->cap);
+  h->bucket = (int*)malloc(sizeof(int) * h->cap);
+  /* a new decoder's toks_.SetSize(1000), or the size the decoder had (InitDecoding keeps it) */
+  kh_set_size(h, o->hash_size > 0 ? (size_t)o->hash_size : 1000);
+  d.acap = 1 << 16;
+  d.a_prev = (int*)malloc(sizeof(int) * d.acap);
+  d.a_arc = (int*)malloc(sizeof(int) * d.acap);
+  float* tmp = NULL;
+  int tcap = 0;
   double offsets_sum = 0.0;
   const float hash_ratio = 2.0f;
+  if (r->lat_frame_begin) { r->lat_ntok = 0; r->lat_nlink = 0; }
 
-#define ENSURE(ptr, capv, need, type) do { if ((need) > (capv)) { capv = (need) * 2; ptr = (type*)realloc(ptr, sizeof(type) * (capv)); } } while (0)
-  /* commit the frame being built: list order becomes the current token order */
-#define COMMIT_FRAME() do {                                                        \
-    int n_ = h.n;                                                                  \
-    if (n_ + 1 > ocap) { ocap = 2 * (n_ + 1); order = (int*)realloc(order, sizeof(int) * ocap); } \
-    cnt = (int*)realloc(cnt, sizeof(int) * (h.nranks + 2));                        \
-    kh_order(&h, order, cnt);                                                      \
-    if (n_ > ccap) { ccap = 2 * n_; cur_state = (int*)realloc(cur_state, sizeof(int) * ccap); \
-      cur_cost = (float*)realloc(cur_cost, sizeof(float) * ccap); cur_idx = (int*)realloc(cur_idx, sizeof(int) * ccap); } \
-    for (int q_ = 0; q_ < n_; q_++) {                                              \
-      const int e_ = order[q_];                                                    \
-      if (narena == acap) { acap *= 2; a_prev = (int*)realloc(a_prev, sizeof(int) * acap); a_arc = (int*)realloc(a_arc, sizeof(int) * acap); } \
-      a_prev[narena] = h.bp[e_]; a_arc[narena] = h.arc[e_];                        \
-      cur_state[q_] = h.st[e_]; cur_cost[q_] = h.cost[e_]; cur_idx[q_] = narena++; \
-    }                                                                              \
-    ncur = n_;                                                                     \
-    kh_clear(&h);                                                                  \
-  } while (0)
-
-  /* ProcessNonemitting over the frame being built (elements in list order) */
-#define NONEMITTING(cutoff_) do {                                                  \
-    int n0_ = h.n;                                                                 \
-    if (n0_ + 1 > ocap) { ocap = 2 * (n0_ + 1); order = (int*)realloc(order, sizeof(int) * ocap); } \
-    cnt = (int*)realloc(cnt, sizeof(int) * (h.nranks + 2));                        \
-    kh_order(&h, order, cnt);                                                      \
-    int qn_ = 0;                                                                   \
-    for (int q_ = 0; q_ < n0_; q_++) {                                             \
-      const int s_ = h.st[order[q_]];                                              \
-      if (g->eps_begin[s_] < g->arc_begin[s_ + 1]) { ENSURE(queue, qcap, qn_ + 1, int); queue[qn_++] = s_; } \
-    }                                                                              \
-    while (qn_ > 0) {                                                              \
-      const int s_ = queue[--qn_];                                                 \
-      const int e_ = h.where[s_];                                                  \
-      const float cc_ = h.cost[e_];                                                \
-      g_kstats[4]++;                                                               \
-      if (cc_ >= (cutoff_)) { g_kstats[5]++; continue; }                           \
-      const int src_ = -2 - e_; /* source: element e_ of this frame (resolved at commit) */ \
-      for (int64_t a_ = g->eps_begin[s_]; a_ < g->arc_begin[s_ + 1]; a_++) {       \
-        const float tot_ = cc_ + g->weight[a_];                                    \
-        if (tot_ < (cutoff_)) {                                                    \
-          int ch_;                                                                 \
-          const int d_ = g->nextstate[a_];                                         \
-          const int nb_ = h.n;                                                     \
-          kh_find_or_add(&h, d_, tot_, src_, (int)a_, &ch_);                       \
-          g_kstats[6]++;                                                           \
-          if (h.n > nb_) g_kstats[7]++;                                            \
-          else if (ch_) g_kstats[8]++;                                             \
-          if (ch_ && g->eps_begin[d_] < g->arc_begin[d_ + 1]) { ENSURE(queue, qcap, qn_ + 1, int); queue[qn_++] = d_; } \
-        }                                                                          \
-      }                                                                            \
-    }                                                                              \
-  } while (0)
-
-  /* epsilon sources inside the frame being built are recorded as -2 - element;
-     resolved to arena indices at commit (the element's arena slot) */
-#define RESOLVE_EPS_BP(base_) do {                                                 \
-    for (int q_ = 0; q_ < ncur; q_++) {                                            \
-      const int ai_ = cur_idx[q_];                                                 \
-      if (a_prev[ai_] <= -2) a_prev[ai_] = (base_) + elem_pos[-2 - a_prev[ai_]];   \
-    }                                                                              \
-  } while (0)
-
-  int* elem_pos = NULL; int epcap = 0;
-  /* InitDecoding */
+  /* InitDecoding: start token, ProcessNonemitting(beam) */
   {
     int ch;
-    kh_find_or_add(&h, g->start, 0.0f, -1, -1, &ch);
-    NONEMITTING(o->beam);
-    ENSURE(elem_pos, epcap, h.n + 1, int);
-    int n_ = h.n;
-    { /* element -> position in list order */
-      int* ord = (int*)malloc(sizeof(int) * (n_ + 1)); int* c2 = (int*)malloc(sizeof(int) * (h.nranks + 2));
-      kh_order(&h, ord, c2);
-      for (int q = 0; q < n_; q++) elem_pos[ord[q]] = q;
-      free(ord); free(c2);
-    }
-    int base = narena;
-    COMMIT_FRAME();
-    RESOLVE_EPS_BP(base);
+    kh_find_or_add(h, g->start, 0.0f, -1, -1, &ch);
+    kd_nonemitting(g, &d, o->beam);
+    kd_commit(g, &d, r, 0, o->beam, 0.0f);
   }
-  if (r->ntok) r->ntok[0] = ncur;
-  if (r->best) { float b = INFINITY; for (int i = 0; i < ncur; i++) if (cur_cost[i] < b) b = cur_cost[i]; r->best[0] = b; }
+  if (r->ntok) r->ntok[0] = d.ncur;
+  if (r->best) { float b = INFINITY; for (int i = 0; i < d.ncur; i++) if (d.cur_cost[i] < b) b = d.cur_cost[i]; r->best[0] = b; }
 
   for (int f = 0; f < F; f++) {
     const float* L = llh + (size_t)f * stride;
+    const int ncur = d.ncur;
     if (ncur == 0) break;
+    const float* cur_cost = d.cur_cost;
+    const int* cur_state = d.cur_state;
     /* ---- GetCutoff: best_elem = first minimum in list order */
-    float best = INFINITY; int best_i = -1;
+    float best = INFINITY;
+    int best_i = -1;
     for (int i = 0; i < ncur; i++) if (cur_cost[i] < best) { best = cur_cost[i]; best_i = i; }
     float beam_cutoff = best + o->beam, adaptive, cutoff;
     float max_cut = INFINITY, min_cut = INFINITY;
-    ENSURE(tmp, tcap, ncur + 1, float);
+    if (ncur + 1 > tcap) { tcap = 2 * (ncur + 1); tmp = (float*)realloc(tmp, sizeof(float) * tcap); }
     memcpy(tmp, cur_cost, sizeof(float) * ncur);
-    if (ncur > o->max_active) { qsort(tmp, ncur, sizeof(float), cmp_float_nth); max_cut = tmp[o->max_active]; }
-    if (max_cut < beam_cutoff) { adaptive = max_cut - best + o->beam_delta; cutoff = max_cut; }
-    else {
+    int sorted = 0;
+    if (ncur > o->max_active) { qsort(tmp, ncur, sizeof(float), cmp_float); sorted = 1; max_cut = tmp[o->max_active]; }
+    if (max_cut < beam_cutoff) {
+      adaptive = max_cut - best + o->beam_delta;
+      cutoff = max_cut;
+    } else {
       if (ncur > o->min_active) {
         if (o->min_active == 0) min_cut = best;
         else {
-          if (!(ncur > o->max_active)) qsort(tmp, ncur, sizeof(float), cmp_float_nth);
+          if (!sorted) qsort(tmp, ncur, sizeof(float), cmp_float);
           min_cut = tmp[o->min_active];
         }
       }
@@ -1378,94 +1430,83 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
     /* PossiblyResizeHash(tok_cnt) on the emptied hash */
     {
       size_t nsz = (size_t)((float)ncur * hash_ratio);
-      if (nsz > h.hash_size) kh_set_size(&h, nsz);
+      if (nsz > h->hash_size) kh_set_size(h, nsz);
     }
     /* ---- ProcessEmitting */
     float next_cutoff = INFINITY;
-    float cost_offset = -best;
+    const float cost_offset = -best;
     {
-      int s = cur_state[best_i];
+      const int s = cur_state[best_i];
       for (int64_t a = g->arc_begin[s]; a < g->eps_begin[s]; a++) {
-        float nw = ((g->weight[a] + cost_offset) - L[g->tid2pdf[g->ilabel[a]]]) + best;
+        const float nw = ((g->weight[a] + cost_offset) - L[g->tid2pdf[g->ilabel[a]]]) + best;
         if (nw + adaptive < next_cutoff) next_cutoff = nw + adaptive;
       }
     }
     int64_t examined = 0;
     for (int i = 0; i < ncur; i++) {
       if (!(cur_cost[i] <= cutoff)) continue;
-      int s = cur_state[i];
+      const int s = cur_state[i];
       for (int64_t a = g->arc_begin[s]; a < g->eps_begin[s]; a++) {
-        float ac = cost_offset - L[g->tid2pdf[g->ilabel[a]]];
-        float tot = (cur_cost[i] + ac) + g->weight[a];
+        const float ac = cost_offset - L[g->tid2pdf[g->ilabel[a]]];
+        const float tot = (cur_cost[i] + ac) + g->weight[a];
         examined++;
         if (tot >= next_cutoff) continue;
         if (tot + adaptive < next_cutoff) next_cutoff = tot + adaptive;
         int ch;
-        const int nb = h.n;
-        kh_find_or_add(&h, g->nextstate[a], tot, cur_idx[i], (int)a, &ch);
+        const int nb = h->n;
+        kh_find_or_add(h, g->nextstate[a], tot, d.cur_idx[i], (int)a, &ch);
         g_kstats[2]++;
-        if (h.n > nb) g_kstats[3]++;
+        if (h->n > nb) g_kstats[3]++;
+        lat_link(r, f + 1, s, (int)a, ac);
       }
     }
     /* ---- ProcessNonemitting(next_cutoff) */
-    NONEMITTING(next_cutoff);
-    ENSURE(elem_pos, epcap, h.n + 1, int);
-    {
-      int n_ = h.n;
-      int* ord = (int*)malloc(sizeof(int) * (n_ + 1)); int* c2 = (int*)malloc(sizeof(int) * (h.nranks + 2));
-      kh_order(&h, ord, c2);
-      for (int q = 0; q < n_; q++) elem_pos[ord[q]] = q;
-      free(ord); free(c2);
-    }
-    int base = narena;
-    COMMIT_FRAME();
-    RESOLVE_EPS_BP(base);
+    kd_nonemitting(g, &d, next_cutoff);
+    kd_commit(g, &d, r, f + 1, next_cutoff, cost_offset);
     offsets_sum += cost_offset;
-    if (r->ntok) r->ntok[f + 1] = ncur;
+    g_kstats[0]++;
+    g_kstats[1] += examined;
+    if (r->ntok) r->ntok[f + 1] = d.ncur;
     if (r->cutoff) r->cutoff[f] = cutoff;
     if (r->next_cutoff) r->next_cutoff[f] = next_cutoff;
     if (r->arcs_emit) r->arcs_emit[f] = examined;
-    g_kstats[0]++;
-    g_kstats[1] += examined;
-    if (r->best) { float b = INFINITY; for (int i = 0; i < ncur; i++) if (cur_cost[i] < b) b = cur_cost[i]; r->best[f + 1] = b; }
+    if (r->best) { float b = INFINITY; for (int i = 0; i < d.ncur; i++) if (d.cur_cost[i] < b) b = d.cur_cost[i]; r->best[f + 1] = b; }
   }
-#undef ENSURE
-#undef COMMIT_FRAME
-#undef NONEMITTING
-#undef RESOLVE_EPS_BP
+  r->hash_size = (int)h->hash_size;
 
   /* best path end: with final costs if any token is final (first minimum in list order) */
+  const int ncur = d.ncur;
   int end = -1;
   float end_cost = INFINITY, best_nofinal = INFINITY, best_final = INFINITY;
   for (int i = 0; i < ncur; i++) {
-    float c = cur_cost[i];
+    const float c = d.cur_cost[i];
     if (c < best_nofinal) best_nofinal = c;
-    float fc = g->final_cost[cur_state[i]];
+    const float fc = g->final_cost[d.cur_state[i]];
     if (fc != INFINITY && c + fc < best_final) best_final = c + fc;
   }
-  int any_final = best_final != INFINITY;
+  const int any_final = best_final != INFINITY;
   for (int i = 0; i < ncur; i++) {
-    float c = (use_final && any_final) ? cur_cost[i] + g->final_cost[cur_state[i]] : cur_cost[i];
+    const float c = (use_final && any_final) ? d.cur_cost[i] + g->final_cost[d.cur_state[i]] : d.cur_cost[i];
     if (c < end_cost) { end_cost = c; end = i; }
   }
   r->final_relative_cost = any_final ? best_final - best_nofinal : INFINITY;
   r->path_len = 0;
   if (end >= 0) {
-    r->end_state = cur_state[end];
+    r->end_state = d.cur_state[end];
     r->best_tot = end_cost;
     r->best_cost = (double)end_cost - offsets_sum;
     int n = 0;
-    for (int k = cur_idx[end]; k >= 0 && a_arc[k] >= 0; k = a_prev[k]) n++;
+    for (int k = d.cur_idx[end]; k >= 0 && d.a_arc[k] >= 0; k = d.a_prev[k]) n++;
     r->path_len = n;
-    int k = cur_idx[end];
+    int k = d.cur_idx[end];
     for (int j = n - 1; j >= 0; j--) {
-      if (j < r->path_cap) r->path[j] = a_arc[k];
-      k = a_prev[k];
+      if (j < r->path_cap) r->path[j] = d.a_arc[k];
+      k = d.a_prev[k];
     }
   }
-  free(h.where); free(h.st); free(h.cost); free(h.bp); free(h.arc); free(h.bucket); free(h.bucket_rank);
-  free(a_prev); free(a_arc); free(cur_state); free(cur_cost); free(cur_idx); free(order); free(cnt);
-  free(tmp); free(queue); free(elem_pos);
+  free(h->where); free(h->st); free(h->cost); free(h->bp); free(h->arc); free(h->bucket); free(h->bucket_rank);
+  free(d.a_prev); free(d.a_arc); free(d.cur_state); free(d.cur_cost); free(d.cur_idx); free(d.order);
+  free(d.cnt); free(d.queue); free(d.elem_pos); free(tmp);
   return end >= 0 ? 0 : -1;
 }
 

@@ -154,6 +154,7 @@ int orc_ivector_extract_w(const orc_ivector_model* m, const float* feats, int T,
 typedef struct {
   float beam, beam_delta;
   int max_active, min_active;
+  int hash_size;  /* orc_decode_kaldi: the HashList size at the start (0: a new decoder's 1000) */
 } orc_dec_opts;
 
 typedef struct {
@@ -188,14 +189,15 @@ typedef struct {
   int* lat_link_frame; int* lat_link_src; int* lat_link_arc; float* lat_link_ac;
   int lat_link_cap, lat_nlink;
   float* lat_cost_offset; /* [F + 1] cost offset of the links into frame k */
+  int hash_size;          /* orc_decode_kaldi: the HashList size at the end */
 } orc_dec_result;
 
 int orc_decode(const orc_graph* g, const float* llh, int num_frames, int llh_stride,
                const orc_dec_opts* o, int use_final, orc_dec_result* r);
 /* Kaldi-sequential token passing (LatticeFasterDecoderTpl with its HashList
-   iteration order, running emitting cutoff and LIFO epsilon queue): the
-   tolerance reference of the order-independent form.  Fills ntok, best,
-   cutoff, next_cutoff, arcs_emit and the best path (no lattice). */
+   iteration order, running emitting cutoff and LIFO epsilon queue), the GPU
+   decoder's default semantics.  Fills everything orc_decode does (lattice
+   included) and the HashList size at the end. */
 int orc_decode_kaldi(const orc_graph* g, const float* llh, int num_frames, int llh_stride,
                      const orc_dec_opts* o, int use_final, orc_dec_result* r);
 

@@ -530,9 +530,17 @@ class OrcGraph(C.Structure):
                 ("tid2pdf", C.c_void_p)]
 
 
+def decoder_order():
+    """The token-passing semantics the GPU decoder runs (VOSK_AMD_DEC_ORDER,
+    as the engine reads it): "kaldi" (default, LatticeFasterDecoder's
+    sequential order) or "parallel" (the order-independent form)."""
+    v = os.environ.get("VOSK_AMD_DEC_ORDER", "kaldi").strip().lower()
+    return "parallel" if v in ("parallel", "0", "order-independent") else "kaldi"
+
+
 class OrcDecOpts(C.Structure):
     _fields_ = [("beam", C.c_float), ("beam_delta", C.c_float), ("max_active", C.c_int),
-                ("min_active", C.c_int)]
+                ("min_active", C.c_int), ("hash_size", C.c_int)]
 
 
 class OrcDecResult(C.Structure):
@@ -545,7 +553,8 @@ class OrcDecResult(C.Structure):
                 ("lat_tok_cost", C.c_void_p), ("lat_tok_cap", C.c_int), ("lat_ntok", C.c_int),
                 ("lat_link_frame", C.c_void_p), ("lat_link_src", C.c_void_p),
                 ("lat_link_arc", C.c_void_p), ("lat_link_ac", C.c_void_p),
-                ("lat_link_cap", C.c_int), ("lat_nlink", C.c_int), ("lat_cost_offset", C.c_void_p)]
+                ("lat_link_cap", C.c_int), ("lat_nlink", C.c_int), ("lat_cost_offset", C.c_void_p),
+                ("hash_size", C.c_int)]
 
 
 class OracleGraph:
@@ -573,11 +582,15 @@ class OracleGraph:
                           self.final.ctypes.data, self.tid2pdf.ctypes.data)
 
     def decode(self, llh: np.ndarray, beam=13.0, max_active=7000, min_active=200,
-               beam_delta=0.5, use_final=True, lattice=False, kaldi=False):
+               beam_delta=0.5, use_final=True, lattice=False, kaldi=None, hash_size=0):
         """kaldi=True: the Kaldi-sequential restatement (orc_decode_kaldi:
-        HashList order, running emitting cutoff, LIFO epsilon queue; no
-        lattice) instead of the order-independent form the GPU computes."""
-        assert not (kaldi and lattice)
+        HashList order, running emitting cutoff, LIFO epsilon queue), the
+        GPU decoder's default; False: the order-independent form (the GPU's
+        VOSK_AMD_DEC_ORDER=parallel mode); None: as the environment selects
+        (decoder_order()).  hash_size: the Kaldi HashList size the decoder
+        starts with (0: a new decoder); out["hash_size"] is its size at the end."""
+        if kaldi is None:
+            kaldi = decoder_order() == "kaldi"
         llh = np.ascontiguousarray(llh, np.float32)
         F = llh.shape[0]
         ntok = np.zeros(F + 1, np.int32)
@@ -602,7 +615,7 @@ class OracleGraph:
             res.lat_link_arc, res.lat_link_ac = lat["link_arc"].ctypes.data, lat["link_ac"].ctypes.data
             res.lat_link_cap = lcap
             res.lat_cost_offset = lat["cost_offset"].ctypes.data
-        o = OrcDecOpts(beam, beam_delta, max_active, min_active)
+        o = OrcDecOpts(beam, beam_delta, max_active, min_active, int(hash_size))
         fn = lib().orc_decode_kaldi if kaldi else lib().orc_decode
         rc = fn(C.byref(self.g), llh.ctypes.data_as(C.c_void_p), C.c_int(F),
                               C.c_int(llh.shape[1]), C.byref(o), C.c_int(int(use_final)),
@@ -612,7 +625,7 @@ class OracleGraph:
         out = dict(rc=rc, ntok=ntok, best=best, cutoff=cut[:F], next_cutoff=ncut[:F],
                    arcs_emit=ex[:F], path=p, words=words, best_cost=res.best_cost,
                    best_tot=res.best_tot, end_state=res.end_state,
-                   final_relative_cost=res.final_relative_cost)
+                   final_relative_cost=res.final_relative_cost, hash_size=res.hash_size)
         if lattice:
             assert res.lat_ntok <= res.lat_tok_cap and res.lat_nlink <= res.lat_link_cap
             nt, nl = res.lat_ntok, res.lat_nlink
@@ -714,9 +727,9 @@ class OracleModel:
         ivt, t0 = self._ivec_of_time(feats.shape[0], len(iv))
         return self.net.forward(feats, iv, ivt, t0)
 
-    def decode_llh(self, llh, use_final=True):
+    def decode_llh(self, llh, use_final=True, hash_size=0):
         return self.graph.decode(llh, self.beam, self.max_active, self.min_active,
-                                 self.beam_delta, use_final)
+                                 self.beam_delta, use_final, hash_size=hash_size)
 
     def online(self, wave, chunk=None, rate=16000, silence_weighting=True, endpoints=False):
         """The single-stream Recognizer's online flow (src/recognizer.cc:297-
@@ -750,6 +763,9 @@ class OracleModel:
         reqs, ents = [], []
         c, done, dec = 0, 0, 0
         seg0, segs, reset_next = 0, [], False
+        # Kaldi order: InitDecoding keeps the decoder's HashList size, so a
+        # segment starts with the size the previous one grew to
+        hs_seg, hs_last, seg_hash = 0, 0, []
         if endpoints:
             import oracle_endpoint as OE
             rules, _ = OE.endpoint_config(self.model_conf)
@@ -767,6 +783,7 @@ class OracleModel:
         for call in calls:
             if call is not None and reset_next:  # CleanUp: InitDecoding, new OnlineSilenceWeighting
                 seg0, reset_next = dec, False
+                hs_seg = hs_last
                 sw = SilenceWeighting(lambda tid: int(tm.tid2phone[tid]) in sil, 1e-3, fss)
             for n, fin in ([(x, False) for x in call] if call is not None else [(len(wave), True)]):
                 n_out = n if rate == model_rate else resample_num_outputs(rate, model_rate, n, fin)
@@ -775,7 +792,7 @@ class OracleModel:
                 if active and ready > 0 and (weighted or done == 0):
                     tids, toks = [], []
                     if dec > seg0:
-                        r = self.decode_llh(llh[seg0:dec], use_final=False)
+                        r = self.decode_llh(llh[seg0:dec], use_final=False, hash_size=hs_seg)
                         for a in r["path"]:
                             if g.ilabel[a] != 0:
                                 tids.append(int(g.ilabel[a]))
@@ -811,15 +828,19 @@ class OracleModel:
                     ivt, t0 = self._ivec_of_time(T, len(ivecs))
                     llh = self.net.forward(nf, ivecs, ivt, t0)[:dec]
             if endpoints and call is not None and dec > seg0:
-                r = self.decode_llh(llh[seg0:dec], use_final=False)
+                r = self.decode_llh(llh[seg0:dec], use_final=False, hash_size=hs_seg)
+                hs_last = r["hash_size"]
                 ts = OE.trailing_silence(r["path"], g.ilabel, tm.tid2phone, sil)
                 if OE.rules_fire(rules, dec - seg0, ts, shift, r["final_relative_cost"]):
                     segs.append((seg0, dec))
+                    seg_hash.append(hs_seg)
                     reset_next = True
         if endpoints:
             segs.append((seg0, dec))
-        r = self.decode_llh(llh[seg0:]) if endpoints else self.decode_llh(llh)
-        return dict(ivectors=ivecs, llh=llh, decode=r, requests=reqs, entries=ents, segments=segs)
+            seg_hash.append(hs_seg)
+        r = self.decode_llh(llh[seg0:], hash_size=hs_seg) if endpoints else self.decode_llh(llh)
+        return dict(ivectors=ivecs, llh=llh, decode=r, requests=reqs, entries=ents, segments=segs,
+                    segment_hash_sizes=seg_hash)
 
     def recognize(self, wave):
         r = self.decode_llh(self.loglikes(wave))

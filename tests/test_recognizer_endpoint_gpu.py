@@ -32,8 +32,8 @@ def test_recognizer_endpoint_segments_match_oracle(synth_model_ep, test_wave, se
     segs = on["segments"]
     assert len(segs) >= 3  # the rules fire
     exp = []
-    for s0, s1 in segs:
-        mb = OL.results(o, on["llh"][s0:s1])["mbr"]
+    for (s0, s1), hs in zip(segs, on["segment_hash_sizes"]):
+        mb = OL.results(o, on["llh"][s0:s1], hash_size=hs)["mbr"]
         exp.append((" ".join(o.words[w] for w in mb["words"]),
                     [((s0 + a) * 0.03, (s0 + b) * 0.03) for a, b in mb["times"]]))
     m = vosk.Model(synth_model_ep)

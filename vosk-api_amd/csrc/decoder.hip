@@ -83,6 +83,12 @@ struct DecShared {
   unsigned char kbits[DT];    // pruning: per-thread keep bits of the chunk
   LatFrame fr;        // pruning: the frame record being processed (broadcast)
   LatFrame fr1;
+  // Kaldi order: emitting pass running cutoff (prefix minimum, two sets for
+  // alternating sub-rounds), creator-rank scan, epsilon queue bookkeeping
+  float kmin_w[2][DW];
+  float kcar[2];
+  int ksum_w[2][DW];
+  int kn0, kne;
 };
 
 // optional phase clocks (VOSK_AMD_DEC_PROFILE): thread 0 stamps s_memtime
@@ -498,8 +504,11 @@ __device__ __forceinline__ void set_bp(const FrameLds& t, const HbmTab& T, int v
   if (v >= 0) t.hb[v] = bp;
   else AG_ST(&T.bp[~v], bp);
 }
-// list position of a slot of the frame under construction (nl_n = its LDS count)
-__device__ __forceinline__ int slot_pos(const FrameLds& t, const HbmTab& T, int nl_n, int v) {
+// position of a slot of the frame under construction in the committed frame
+// (arena offset): its creation index (nl_n = the LDS count), or in Kaldi
+// order its list position (kaldi_positions, kept in the slot's hst / stamp)
+__device__ __forceinline__ int slot_pos(const DecArgs& a, const FrameLds& t, const HbmTab& T, int nl_n, int v) {
+  if (a.kaldi) return v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
   return v >= 0 ? (int)(t.hp[v] & 0x7fff) : nl_n + (AG_LD(&T.pos[~v]) & (kHPosEps - 1));
 }
 // the epsilon-source slot code of a relaxation from slot v
@@ -776,20 +785,26 @@ __device__ __forceinline__ void eps_closure(const DecArgs& a, DecShared& sh, con
   *arcs_eps += examined;
 }
 
+// hst / stamp: the epsilon round stamp of the order-independent closure, or
+// in Kaldi order the creation index, then the list position; kNoStamp when
+// the entry is free
+constexpr int kNoStamp = 0x7fffffff;
+
 __device__ __forceinline__ void lds_clear_build(const FrameLds& t) {
   for (int h = threadIdx.x; h < kHashCap; h += DT) {
     t.hs[h] = -1;
     t.hk[h] = kEmpty;
-    t.hst[h] = 0;
+    t.hst[h] = kNoStamp;
   }
 }
 
 // clears the listed entries of the HBM table
-__device__ __forceinline__ void hbm_clear_listed(const HbmTab& T, int n) {
+__device__ __forceinline__ void hbm_clear_listed(const DecArgs& a, const HbmTab& T, int n) {
   for (int j = threadIdx.x; j < n; j += DT) {
     const int g = AG_LD(&T.list[j]);
     AG_ST(&T.state[g], -1);
     AG_ST(&T.key[g], kEmpty);
+    if (a.kaldi) AG_ST(&T.stamp[g], kNoStamp);
   }
 }
 __device__ __forceinline__ void hbm_clear_all(const DecArgs& a, const HbmTab& T) {
@@ -797,7 +812,418 @@ __device__ __forceinline__ void hbm_clear_all(const DecArgs& a, const HbmTab& T)
   for (int g = threadIdx.x; g < H; g += DT) {
     AG_ST(&T.state[g], -1);
     AG_ST(&T.key[g], kEmpty);
-    AG_ST(&T.stamp[g], -1);
+    AG_ST(&T.stamp[g], kNoStamp);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kaldi order (DecArgs::kaldi, the default).  Kaldi's
+// ProcessEmitting walks the frame's tokens in HashList order and tightens
+// next_cutoff as it goes, so which relaxations create tokens depends on that
+// order.  Here:
+//  - the current-token arrays are kept in HashList order (kaldi_positions:
+//    buckets state % khash in order of first occupancy, then creation);
+//  - the emitting pass enumerates the (token, arc) items in that order and
+//    accepts item i iff tot_i < min(seed, min_{j<i} tot_j + adaptive_beam),
+//    a block prefix minimum carried across sub-rounds (a rejected item never
+//    lowers it: tot_j >= the running cutoff and adaptive_beam > 0);
+//  - a token's creation index is the rank of its first accepted relaxation
+//    (ranked densely per sub-round), then its order of creation in the
+//    epsilon queue;
+//  - ProcessNonemitting runs as Kaldi's LIFO queue on one thread, seeded in
+//    list order with the tokens that can relax an epsilon arc below the
+//    cutoff (another token does nothing when Kaldi pops it; if its cost later
+//    falls it is pushed again, as in Kaldi);
+//  - a token's cost is the minimum over its accepted relaxations and its
+//    backpointer the minimum (cost, arc) one; every token Kaldi creates is
+//    kept, every accepted emitting relaxation is a lattice link.
+// ---------------------------------------------------------------------------
+
+// exclusive running minimum over the block in thread order, seeded with
+// sh.kcar[par]; leaves the running minimum after the block in sh.kcar[par ^ 1]
+__device__ __forceinline__ float kaldi_excl_min(DecShared& sh, float v, int par) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const float u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl = fminf(incl, u);
+  }
+  float excl = __shfl_up(incl, 1, 64);
+  if (lane == 0) excl = __int_as_float(0x7f800000);
+  if (lane == 63) sh.kmin_w[par][w] = incl;
+  __syncthreads();
+  float pre = sh.kcar[par];
+  for (int i = 0; i < w; i++) pre = fminf(pre, sh.kmin_w[par][i]);
+  if (threadIdx.x == DT - 1) sh.kcar[par ^ 1] = fminf(pre, incl);
+  return fminf(pre, excl);
+}
+
+// exclusive prefix sum over the block in thread order; *total = the block's sum
+__device__ __forceinline__ int kaldi_excl_sum(DecShared& sh, int v, int par, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) sh.ksum_w[par][w] = incl;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int i = 0; i < DW; i++) {
+    const int x = sh.ksum_w[par][i];
+    off += i < w ? x : 0;
+    tot += x;
+  }
+  *total = tot;
+  return off + incl - v;
+}
+
+// ProcessEmitting in list order (see above); returns next_cutoff.  The
+// created tokens get creation indices [0, *ncreated) (kord: index -> slot).
+__device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                                       const HbmTab& T, const DecPtrs& p, const TokView& tv,
+                                                       int ntok, float cutoff, float cost_offset, const float* Lp,
+                                                       float seed, float adaptive, int* examined, const DecSlot& st,
+                                                       int slot, int* ncreated, Prof& pr) {
+  const bool lat = a.links != nullptr;
+  int* KO = a.kord + (long long)slot * a.kord_cap;
+  if (threadIdx.x == 0) sh.kcar[0] = seed;  // read after the next barrier
+  int par = 0, ibase = 0, nc = 0;
+  float cn = 0.0f;
+  int sn = 0, pn = 0;
+  if ((int)threadIdx.x < ntok) {
+    cn = tv.c(threadIdx.x);
+    sn = tv.s(threadIdx.x);
+    pn = AG_LD(&p.cp[threadIdx.x]);
+  }
+  for (int c0 = 0; c0 < ntok; c0 += DT) {
+    const int i = c0 + threadIdx.x;
+    int deg = 0, ab = 0, src = 0;
+    float c = 0.0f;
+    if (i < ntok) {
+      c = cn;
+      if (c <= cutoff) {
+        const int4 si = a.sinfo[sn];
+        ab = si.x;
+        deg = si.y - si.x;
+        src = st.cur_base + pn;
+      }
+    }
+    block_scan(sh, deg);
+    sh.abeg[threadIdx.x] = ab;
+    sh.tcost[threadIdx.x] = c;
+    sh.tsrc[threadIdx.x] = src;
+    __syncthreads();
+    if (i + DT < ntok) {
+      cn = tv.c(i + DT);
+      sn = tv.s(i + DT);
+      pn = AG_LD(&p.cp[i + DT]);
+    }
+    pr.mark(2);
+    pr.count(14, 1);
+    const int total = sh.total;
+    *examined += total;
+    for (int sb = 0; sb < total; sb += DT) {
+      const int it = sb + (int)threadIdx.x;
+      const bool valid = it < total;
+      int j = 0, arc = 0;
+      int4 A = make_int4(0, 0, 0, 0);
+      float ac = 0.0f, tot = __int_as_float(0x7f800000);
+      if (valid) {
+        j = owner(sh, it);
+        arc = sh.abeg[j] + (it - sh.scan[j]);
+        A = a.arcs[arc];
+        ac = cost_offset - Lp[A.z];
+        tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
+      }
+      pr.mark(3);
+      const float run = kaldi_excl_min(sh, valid ? tot + adaptive : __int_as_float(0x7f800000), par);
+      const bool want = valid && tot < run;
+      const int item = ibase + it;
+      const unsigned long long kv = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
+      int sv = kNoSlot;
+      if (want) {
+        const bool de = ((unsigned)A.w & kDestEps) != 0;
+        const Relax r = relax(a, sh, t, T, A.x, tot, arc, de);
+        if (r.flags >= 0) {
+          sv = r.slot;
+          if (sv >= 0) atomicMin(&t.hst[sv], item);
+          else __hip_atomic_fetch_min(&T.stamp[~sv], item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lat)
+          emit_link(a, sh, st.links_used, slot, make_int4(sh.tsrc[j], __float_as_int(tot), arc, __float_as_int(ac)),
+                    sv, false);
+      }
+      pr.mark(22);
+      vm_drain();  // the relaxations' atomics (keys, creation indices) are complete at the barrier
+      __syncthreads();
+      // each slot's winner writes its backpointer; its creator (the slot's
+      // first accepted relaxation) takes the next creation index
+      int cf = 0;
+      if (sv != kNoSlot) {
+        if (slot_key(t, T, sv) == kv) set_bp(t, T, sv, sh.tsrc[j]);
+        cf = (sv >= 0 ? t.hst[sv] : AG_LD(&T.stamp[~sv])) == item;
+      }
+      int ncr;
+      const int rk = nc + kaldi_excl_sum(sh, cf, par, &ncr);
+      if (cf) {
+        if (rk < a.kord_cap) {
+          if (sv >= 0) t.hst[sv] = rk;
+          else AG_ST(&T.stamp[~sv], rk);
+          AG_ST(&KO[rk], sv);
+        } else {
+          sh.bad |= 1;
+        }
+      }
+      vm_drain();
+      nc += ncr;
+      par ^= 1;
+      pr.mark(4);
+    }
+    ibase += total;
+    __syncthreads();
+    pr.mark(2);
+  }
+  __syncthreads();
+  *ncreated = nc < a.kord_cap ? nc : a.kord_cap;
+  return sh.kcar[par];
+}
+
+// find-or-add of one epsilon relaxation by a single thread (the queue):
+// the slot, the key it had (kEmpty if created) and whether it was created;
+// the key becomes the minimum
+struct KRelax {
+  int slot;
+  bool created;
+  unsigned long long old;
+};
+__device__ __forceinline__ KRelax kaldi_find_or_add(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                                    const HbmTab& T, int dest, unsigned long long k, bool eps) {
+  const int nbk = a.lds_probe < 2 ? a.lds_probe : 2;
+  const unsigned b1 = bucket1(dest);
+  for (int nb = 0; nb < nbk; nb++) {
+    const int h0 = 4 * (int)(nb ? bucket2(dest, b1) : b1);
+    for (int i = 0; i < 4; i++) {
+      const int h = h0 + i;
+      const int c = t.hs[h];
+      if (c == dest) {
+        const unsigned long long old = t.hk[h];
+        if (k < old) t.hk[h] = k;
+        return KRelax{h, false, old};
+      }
+      if (c == -1) {  // buckets fill left to right
+        t.hs[h] = dest;
+        const int pos = sh.n_new_l++;
+        t.nl[pos] = (unsigned short)h;
+        t.hp[h] = (unsigned short)(pos | (eps ? kPosEps : 0));
+        t.hk[h] = k;
+        return KRelax{h, true, kEmpty};
+      }
+    }
+  }
+  const unsigned hm = (1u << a.hbits) - 1u;
+  unsigned g = hbm_hash(dest, a.hbits);
+  for (int probe = 0; probe < a.hprobe; probe++) {
+    const int c = AG_LD(&T.state[g]);
+    if (c == dest) {
+      const unsigned long long old = AG_LD(&T.key[g]);
+      if (k < old) AG_ST(&T.key[g], k);
+      return KRelax{~(int)g, false, old};
+    }
+    if (c == -1) {
+      AG_ST(&T.state[g], dest);
+      const int pos = sh.n_new_g++;
+      if (pos < a.max_tok) {
+        AG_ST(&T.list[pos], (int)g);
+        AG_ST(&T.pos[g], pos | (eps ? kHPosEps : 0));
+      } else {
+        sh.bad |= 1;
+      }
+      AG_ST(&T.key[g], k);
+      return KRelax{~(int)g, true, kEmpty};
+    }
+    g = (g + 1) & hm;
+  }
+  sh.bad |= 1;
+  return KRelax{kNoSlot, false, 0};
+}
+
+// ProcessNonemitting in Kaldi order over the frame under construction, whose
+// tokens have creation indices [0, nc) (bucket state % khash); returns the
+// token count after the epsilon queue.  stk: LDS part of the queue.
+__device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                                 const HbmTab& T, const DecPtrs& p, int* stk, int slot, int khash,
+                                                 float cutoff, int nc, int* arcs_eps, Prof& pr) {
+  int* KO = a.kord + (long long)slot * a.kord_cap;
+  int* KB = a.kbkt + (long long)slot * a.kord_cap;
+  int* KS = a.kstk + (long long)slot * a.kord_cap;
+  int* BF = a.kb_first + (long long)slot * a.kb_cap;
+  int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
+  int* BM = a.kb_memb + (long long)slot * a.kb_cap * 4;
+  constexpr int kKeyLds = kFrontLds;  // queue keys in LDS over both frontier arrays
+  unsigned long long* KV = reinterpret_cast<unsigned long long*>(t.fr0);
+  unsigned long long* KVg = reinterpret_cast<unsigned long long*>(p.fg0);  // [max_tok] past the LDS part
+  // the buckets of the emitting pass's tokens
+  for (int c = threadIdx.x; c < nc; c += DT) {
+    const int v = AG_LD(&KO[c]);
+    const int b = (int)((unsigned)slot_state(t, T, v) % (unsigned)khash);
+    AG_ST(&KB[c], b);
+    __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (m < 4) AG_ST(&BM[4 * b + m], c);
+  }
+  if (threadIdx.x == 0) sh.kn0 = 0;
+  vm_drain();
+  __syncthreads();
+  // Kaldi's initial queue, restricted to the tokens that can relax an
+  // epsilon arc below the cutoff, keyed by list order (bucket's first
+  // creation index, creation index)
+  for (int c = threadIdx.x; c < nc; c += DT) {
+    const int v = AG_LD(&KO[c]);
+    const bool eps = v >= 0 ? (t.hp[v] & kPosEps) != 0 : (AG_LD(&T.pos[~v]) & kHPosEps) != 0;
+    if (!eps) continue;
+    const float cost = funord((uint32_t)(slot_key(t, T, v) >> 32));
+    if (!(cost < cutoff)) continue;
+    const int4 si = a.sinfo[slot_state(t, T, v)];
+    bool prod = false;
+    for (int arc = si.y; arc < si.z && !prod; arc++) prod = cost + __int_as_float(a.arcs[arc].y) < cutoff;
+    if (!prod) continue;
+    const int q = atomicAdd(&sh.kn0, 1);
+    const unsigned long long key =
+        ((unsigned long long)(unsigned)AG_LD(&BF[AG_LD(&KB[c])]) << 32) | (unsigned)c;
+    if (q < kKeyLds) KV[q] = key;
+    else if (q - kKeyLds < a.max_tok) AG_ST(&KVg[q - kKeyLds], key);
+    else sh.bad |= 1;
+  }
+  vm_drain();
+  __syncthreads();
+  int n0 = sh.kn0;
+  n0 = n0 < kKeyLds + a.max_tok ? n0 : kKeyLds + a.max_tok;
+  // list order: rank by counting (the queue holds few tokens)
+  for (int i = threadIdx.x; i < n0; i += DT) {
+    const unsigned long long ki = i < kKeyLds ? KV[i] : AG_LD(&KVg[i - kKeyLds]);
+    int r = 0;
+    for (int j = 0; j < n0; j++) r += (j < kKeyLds ? KV[j] : AG_LD(&KVg[j - kKeyLds])) < ki;
+    const int v = AG_LD(&KO[(int)(unsigned)(ki & 0xffffffffu)]);
+    if (r < kTokLds) stk[r] = v;
+    else if (r - kTokLds < a.kord_cap) AG_ST(&KS[r - kTokLds], v);
+  }
+  vm_drain();
+  __syncthreads();
+  pr.mark(5);
+  // the LIFO queue (pop_back), one thread
+  if (threadIdx.x == 0) {
+    int sp = n0, ne = nc, ex = 0;
+    bool ok = true;
+    while (sp > 0 && ok) {
+      --sp;
+      const int v = sp < kTokLds ? stk[sp] : AG_LD(&KS[sp - kTokLds]);
+      const float cst = funord((uint32_t)(slot_key(t, T, v) >> 32));
+      if (!(cst < cutoff)) continue;
+      const int4 si = a.sinfo[slot_state(t, T, v)];
+      for (int arc = si.y; arc < si.z; arc++) {
+        const int4 A = a.arcs[arc];
+        ex++;
+        const float tot = cst + __int_as_float(A.y);
+        if (!(tot < cutoff)) continue;
+        const bool de = ((unsigned)A.w & kDestEps) != 0;
+        const unsigned long long kk = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
+        const KRelax r = kaldi_find_or_add(a, sh, t, T, A.x, kk, de);
+        if (r.slot == kNoSlot || ne >= a.kord_cap) {
+          sh.bad |= 1;
+          ok = false;
+          break;
+        }
+        if (kk < r.old) set_bp(t, T, r.slot, eps_bp(v));
+        if (r.created) {
+          const int c = ne++;
+          if (r.slot >= 0) t.hst[r.slot] = c;
+          else AG_ST(&T.stamp[~r.slot], c);
+          AG_ST(&KO[c], r.slot);
+          const int b = (int)((unsigned)A.x % (unsigned)khash);
+          AG_ST(&KB[c], b);
+          if (AG_LD(&BF[b]) > c) AG_ST(&BF[b], c);
+          const int m = AG_LD(&BC[b]);
+          AG_ST(&BC[b], m + 1);
+          if (m < 4) AG_ST(&BM[4 * b + m], c);
+        }
+        if (de && (r.created || tot < funord((uint32_t)(r.old >> 32)))) {  // FindOrAddToken's changed
+          if (sp < kTokLds) stk[sp] = r.slot;
+          else if (sp - kTokLds < a.kord_cap) AG_ST(&KS[sp - kTokLds], r.slot);
+          else {
+            sh.bad |= 1;
+            ok = false;
+            break;
+          }
+          sp++;
+        }
+      }
+    }
+    sh.kne = ne;
+    *arcs_eps += ex;
+  }
+  vm_drain();
+  __syncthreads();
+  return sh.kne;
+}
+
+// List positions of the frame's n tokens (HashList order: buckets by their
+// first creation index, then creation index), written to each slot's hst /
+// stamp (slot_pos).  Bucket starts: a scan over the creation order in which
+// each bucket's first token contributes the bucket's size.
+__device__ __forceinline__ void kaldi_positions(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
+                                                int slot, int n) {
+  const int* KO = a.kord + (long long)slot * a.kord_cap;
+  const int* KB = a.kbkt + (long long)slot * a.kord_cap;
+  int* BF = a.kb_first + (long long)slot * a.kb_cap;
+  int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
+  int* BS = a.kb_start + (long long)slot * a.kb_cap;
+  int* BM = a.kb_memb + (long long)slot * a.kb_cap * 4;
+  int run = 0, par = 0;
+  for (int c0 = 0; c0 < n; c0 += DT) {
+    const int c = c0 + threadIdx.x;
+    int b = 0, sz = 0;
+    bool lead = false;
+    if (c < n) {
+      b = AG_LD(&KB[c]);
+      lead = AG_LD(&BF[b]) == c;
+      if (lead) sz = AG_LD(&BC[b]);
+    }
+    int tot;
+    const int ex = run + kaldi_excl_sum(sh, sz, par, &tot);
+    if (lead) AG_ST(&BS[b], ex);
+    run += tot;
+    par ^= 1;
+  }
+  vm_drain();
+  __syncthreads();
+  for (int c = threadIdx.x; c < n; c += DT) {
+    const int b = AG_LD(&KB[c]);
+    const int cnt = AG_LD(&BC[b]);
+    int rk = 0;
+    if (cnt <= 4) {
+      for (int i = 0; i < cnt; i++) rk += AG_LD(&BM[4 * b + i]) < c;
+    } else {  // a crowded bucket: count its tokens created before
+      for (int c2 = 0; c2 < c; c2++) rk += AG_LD(&KB[c2]) == b;
+    }
+    const int pos = AG_LD(&BS[b]) + rk;
+    const int v = AG_LD(&KO[c]);
+    if (v >= 0) t.hst[v] = pos;
+    else AG_ST(&T.stamp[~v], pos);
+  }
+  vm_drain();
+  __syncthreads();
+}
+
+// the buckets the frame used, emptied for the next one
+__device__ __forceinline__ void kaldi_clear_buckets(const DecArgs& a, int slot, int n) {
+  const int* KB = a.kbkt + (long long)slot * a.kord_cap;
+  int* BF = a.kb_first + (long long)slot * a.kb_cap;
+  int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
+  for (int c = threadIdx.x; c < n; c += DT) {
+    const int b = AG_LD(&KB[c]);
+    AG_ST(&BF[b], kNoStamp);
+    AG_ST(&BC[b], 0);
   }
 }
 
@@ -845,7 +1271,7 @@ __device__ __forceinline__ int commit_emit_links(const DecArgs& a, DecShared& sh
       if (tot < cutoff && v != kNoSlot) {  // (kNoSlot: a failed relaxation, the frame is in error)
         const unsigned long long key = slot_key(t, T, v);
         if (defer && key == (((unsigned long long)ford(tot) << 32) | (unsigned)r.z)) set_bp(t, T, v, r.x);
-        r.y = base + slot_pos(t, T, nl_n, v);
+        r.y = base + slot_pos(a, t, T, nl_n, v);
         d = tot - funord((uint32_t)(key >> 32));
         keep = 1;
       }
@@ -883,7 +1309,7 @@ __device__ __forceinline__ int commit_eps_links(const DecArgs& a, DecShared& sh,
       const int4 si = a.sinfo[s];
       ab = si.y;
       deg = si.z - si.y;
-      src = base + slot_pos(t, T, nl_n, v);
+      src = base + slot_pos(a, t, T, nl_n, v);
     }
     block_scan(sh, deg);
     sh.abeg[threadIdx.x] = ab;
@@ -906,7 +1332,7 @@ __device__ __forceinline__ int commit_eps_links(const DecArgs& a, DecShared& sh,
         w0 = __shfl(w0, leader, 64);
         const long long pos = lb + out + w0 + __popcll(m & ((1ull << lane) - 1ull));
         if (pos < a.link_cap && v != kNoSlot) {
-          L[pos] = make_int4(sh.tsrc[j], base + slot_pos(t, T, nl_n, v), arc, 0);
+          L[pos] = make_int4(sh.tsrc[j], base + slot_pos(a, t, T, nl_n, v), arc, 0);
           LD[pos] = __float_as_int(tot - funord((uint32_t)(slot_key(t, T, v) >> 32)));
         } else {
           atomicOr(&sh.lat_ovf, v == kNoSlot ? 2 : 1);  // 2: an epsilon link's destination is not in the frame
@@ -936,9 +1362,14 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   const int base = st.arena_used;
   const bool ok = (long long)base + n <= a.arena_cap;
   const bool lat = a.links != nullptr;
+  // Kaldi order: the tokens' list positions (slot_pos) first
+  if (a.kaldi) kaldi_positions(a, sh, t, T, slot, n);
   // the emitting records first: with deferred winners they set the
-  // backpointers the token commit below reads
-  const int n_emit = (lat && ok) ? commit_emit_links(a, sh, t, T, st, slot, base, nl_n, cutoff, defer) : 0;
+  // backpointers the token commit below reads (Kaldi order: every record is
+  // an accepted relaxation, kept)
+  const int n_emit = (lat && ok) ? commit_emit_links(a, sh, t, T, st, slot, base, nl_n,
+                                                     a.kaldi ? __int_as_float(0x7f800000) : cutoff, defer)
+                                 : 0;
   pr.mark(7);
   if (threadIdx.x == 0) {
     sh.n_next = 0;
@@ -983,7 +1414,7 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
     const bool has_eps = eq[q];
     const int arc = (int)(unsigned)(k & 0xffffffffu);
     const float cost = funord((uint32_t)(k >> 32));
-    if (ok && cost < cutoff) {
+    if (ok && (a.kaldi || cost < cutoff)) {  // Kaldi order: every created token is a token
       int prev = -1;
       if (arc >= 0) {
         if (bp & kBpEps) {
@@ -993,18 +1424,22 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
           if (sv >= kHashCap || (sv < 0 && ~sv >= (1 << a.hbits))) {
             sh.bad |= 8;
           } else {
-            prev = base + slot_pos(t, T, nl_n, sv);
+            prev = base + slot_pos(a, t, T, nl_n, sv);
           }
         } else {
           prev = bp;
         }
       }
-      ag_st4(&p.arena[base + j], make_int4(prev, arc, __float_as_int(cost), s));
-      const int q = atomicAdd(&sh.n_next, 1);
+      // arena offset: the creation index, or the list position (Kaldi order,
+      // whose current-token arrays are in list order)
+      const int ao = a.kaldi ? slot_pos(a, t, T, nl_n, v) : j;
+      ag_st4(&p.arena[base + ao], make_int4(prev, arc, __float_as_int(cost), s));
+      const int qa = atomicAdd(&sh.n_next, 1);
+      const int q = a.kaldi ? ao : qa;
       if (q < a.max_tok) {  // the current-token arrays hold max_tok entries
         AG_ST(&p.cs[q], s);
         AG_ST(&p.cc[q], cost);
-        AG_ST(&p.cp[q], j);
+        AG_ST(&p.cp[q], ao);
       } else {
         sh.bad |= 1;
       }
@@ -1012,8 +1447,10 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
         TS[q] = s;
         TC[q] = cost;
       }
-      if (lat && has_eps) push_front(a, sh, t, p, 0, &sh.n_front, v);
-      const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)s;
+      // epsilon links: tokens Kaldi expands (cost below the cutoff)
+      if (lat && has_eps && cost < cutoff) push_front(a, sh, t, p, 0, &sh.n_front, v);
+      // GetCutoff's best token: the first minimum in list order (Kaldi), else the lowest state
+      const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)(a.kaldi ? q : s);
       bk = tk < bk ? tk : bk;
     } else if (ok) {
       ag_st4(&p.arena[base + j], make_int4(-2, -1, __float_as_int(cost), s));  // dead list entry
@@ -1029,7 +1466,8 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   *nlinks = (lat && ok) ? commit_eps_links(a, sh, t, T, p, st, slot, base, nl_n, neps, n_emit, cutoff) : 0;
   pr.mark(8);
   __syncthreads();
-  hbm_clear_listed(T, ng);
+  if (a.kaldi) kaldi_clear_buckets(a, slot, n);
+  hbm_clear_listed(a, T, ng);
   lds_clear_build(t);
   __syncthreads();
   pr.mark(9);
@@ -1405,7 +1843,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   __shared__ unsigned short t_hp[kHashCap];
   __shared__ int t_hst[kHashCap];
   __shared__ unsigned short t_nl[kHashCap];
-  __shared__ int t_fr[2][kFrontLds];
+  __shared__ __attribute__((aligned(16))) int t_fr[2][kFrontLds];  // (Kaldi order: 8-byte queue keys)
   FrameLds t;
   t.hs = t_hs;
   t.hk = t_hk;
@@ -1440,7 +1878,14 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
 
   if (job.reset) {  // InitDecoding: start token, closure with cutoff = beam
     __syncthreads();
-    if (st.err) hbm_clear_all(a, T);  // an overflow may have left unlisted entries
+    if (st.err) {  // an overflow may have left unlisted entries
+      hbm_clear_all(a, T);
+      if (a.kaldi)
+        for (int b = threadIdx.x; b < a.kb_cap; b += DT) {
+          AG_ST(&a.kb_first[(long long)slot * a.kb_cap + b], kNoStamp);
+          AG_ST(&a.kb_cnt[(long long)slot * a.kb_cap + b], 0);
+        }
+    }
     st.ntok = 0;
     st.cur_base = 0;
     st.arena_used = 0;
@@ -1451,6 +1896,9 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     st.lat_ovf = 0;
     st.prune_from = 0;
     st.last_prune = 0;
+    // Kaldi order: a new decoder's HashList holds 1000 buckets; InitDecoding
+    // (reset 1, a Recognizer's next segment) keeps the size it grew to
+    if (job.reset == 2 || st.khash <= 0) st.khash = 1000;
     __syncthreads();
     if (threadIdx.x == 0) {
       sh.n_new_l = 0;
@@ -1464,12 +1912,25 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
                             ((unsigned)a.sinfo[a.start_state].z - (unsigned)a.sinfo[a.start_state].y) != 0);
       t.fr0[0] = r.slot;
       sh.n_front = 1;
+      if (a.kaldi) {  // creation index 0
+        if (r.slot >= 0) t.hst[r.slot] = 0;
+        else AG_ST(&T.stamp[~r.slot], 0);
+        AG_ST(&a.kord[(long long)slot * a.kord_cap], r.slot);
+      }
     }
-    eps_closure(a, sh, t, T, p, st, a.beam, 1, &arcs_eps, pr);
+    if (a.kaldi) {
+      vm_drain();
+      __syncthreads();
+      kaldi_nonemitting(a, sh, t, T, p, TS, slot, st.khash, a.beam, 1, &arcs_eps, pr);
+    } else {
+      eps_closure(a, sh, t, T, p, st, a.beam, 1, &arcs_eps, pr);
+    }
     float b;
     int nl = 0;
     commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, &nl, false, pr);
-    st.commit_cutoff = a.beam;
+    // every current token's cost is below the commit's cutoff (GetCutoff's
+    // shortcut); Kaldi order keeps tokens above it
+    st.commit_cutoff = a.kaldi ? __int_as_float(0x7f800000) : a.beam;
     frame_done(a, sh, st, slot, 0, a.beam, 0.0f, nl);
   } else if (st.ntok > 0 && st.ntok <= kTokLds) {
     for (int i = threadIdx.x; i < st.ntok; i += DT) {
@@ -1507,7 +1968,18 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     // ---- GetCutoff (best token: min (cost, state), kept by the previous commit)
     const unsigned long long bk = st.best_key;
     const float best = funord((uint32_t)(bk >> 32));
-    const int best_state = (int)(unsigned)(bk & 0xffffffffu);
+    // the best token: its state (order-independent form), or its list
+    // position (Kaldi order: the first minimum in list order, best_elem)
+    const int bk_lo = (int)(unsigned)(bk & 0xffffffffu);
+    const int best_state = !a.kaldi ? bk_lo : lds ? TS[bk_lo] : AG_LD(&p.cs[bk_lo]);
+    if (a.kaldi) {  // PossiblyResizeHash(tok_cnt): the size the next frame's tokens hash with
+      const int nsz = (int)((float)ntok * 2.0f);
+      if (nsz > st.khash) st.khash = nsz;
+      if (st.khash > a.kb_cap) {  // (cannot happen: tokens <= max_tok, kb_cap > 2 * max_tok)
+        st.khash = a.kb_cap;
+        if (threadIdx.x == 0) sh.bad |= 1;
+      }
+    }
     const float beam_cutoff = best + a.beam;
     float max_cut = __int_as_float(0x7f800000), min_cut = __int_as_float(0x7f800000);
     float adaptive, cutoff;
@@ -1519,7 +1991,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     CostRegs cr;
     // every token's cost is below the last commit's cutoff: when that is at
     // most beam_cutoff, all ntok are < (and <=) beam_cutoff without counting
-    const bool all_in = st.commit_cutoff <= beam_cutoff;
+    const bool all_in = !a.kaldi && st.commit_cutoff <= beam_cutoff;
     if ((need_max || need_min) && !all_in) {
       unsigned long long cnt = 0;  // (# cost < beam_cutoff) << 32 | # cost <= beam_cutoff
       if (regs) {
@@ -1594,7 +2066,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     pr.mark(1);
     const float seed = sh.seed;
     int examined = 0;
-    const bool defer = a.links != nullptr && a.link_cap - st.links_used >= kDeferHeadroom;
+    const bool defer = !a.kaldi && a.links != nullptr && a.link_cap - st.links_used >= kDeferHeadroom;
     float next_cutoff, new_best;
     // one emitting pass relaxing below the seed bound (a superset), then the
     // epsilon closure; tokens whose best cost is not below the final
@@ -1602,7 +2074,13 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     // and are dropped at commit -- exactly the tokens a relax-below-
     // next_cutoff pass creates, with the same keys.  Without a finite seed
     // the exact two-pass form runs.
-    if (seed != __int_as_float(0x7f800000)) {
+    if (a.kaldi) {
+      int nc = 0;
+      next_cutoff = expand_emitting_kaldi(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, seed, adaptive,
+                                          &examined, st, slot, &nc, pr);
+      pr.count(11, sh.n_new_g);
+      kaldi_nonemitting(a, sh, t, T, p, TS, slot, st.khash, next_cutoff, nc, &arcs_eps, pr);
+    } else if (seed != __int_as_float(0x7f800000)) {
       const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed, adaptive,
                                       &examined, st, slot, defer, pr);
       next_cutoff = seed;
@@ -1616,10 +2094,12 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, next_cutoff, adaptive, &dummy, st,
                       slot, defer, pr);
     }
-    __syncthreads();
-    pr.mark(2);
-    pr.count(11, sh.n_new_g);  // tokens the emitting pass created in the HBM table
-    eps_closure(a, sh, t, T, p, st, next_cutoff, sh.n_front, &arcs_eps, pr);
+    if (!a.kaldi) {
+      __syncthreads();
+      pr.mark(2);
+      pr.count(11, sh.n_new_g);  // tokens the emitting pass created in the HBM table
+      eps_closure(a, sh, t, T, p, st, next_cutoff, sh.n_front, &arcs_eps, pr);
+    }
     __syncthreads();
     pr.mark(5);
     if (pf) {  // L is not read again in this frame
@@ -1631,7 +2111,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     }
     int nl = 0;
     commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, &nl, defer, pr);
-    st.commit_cutoff = next_cutoff;
+    st.commit_cutoff = a.kaldi ? __int_as_float(0x7f800000) : next_cutoff;
     pr.count(15, 1);
     frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset, nl);
     st.offset_sum += (double)cost_offset;
@@ -1709,7 +2189,7 @@ __global__ __launch_bounds__(256) void traceback_kernel(TraceArgs a) {
   for (int i = threadIdx.x; i < st.ntok; i += 256) {
     float c = cc[i];
     if (use_f) c = c + __int_as_float(a.sinfo[cs[i]].w);
-    const unsigned long long k = ((unsigned long long)ford(c) << 32) | (unsigned)cs[i];
+    const unsigned long long k = ((unsigned long long)ford(c) << 32) | (unsigned)(a.tie_pos ? i : cs[i]);
     bk = k < bk ? k : bk;
   }
   bk = wave_min_u64(bk);
@@ -1718,8 +2198,12 @@ __global__ __launch_bounds__(256) void traceback_kernel(TraceArgs a) {
   __syncthreads();
   bk = red[0];
   for (int i = 1; i < 4; i++) bk = red[i] < bk ? red[i] : bk;
-  for (int i = threadIdx.x; i < st.ntok; i += 256)
-    if (cs[i] == (int)(unsigned)(bk & 0xffffffffu)) endpos = i;
+  if (a.tie_pos) {
+    if (threadIdx.x == 0 && bk != kEmpty) endpos = (int)(unsigned)(bk & 0xffffffffu);
+  } else {
+    for (int i = threadIdx.x; i < st.ntok; i += 256)
+      if (cs[i] == (int)(unsigned)(bk & 0xffffffffu)) endpos = i;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     int n = 0;
@@ -1750,7 +2234,7 @@ __global__ __launch_bounds__(256) void traceback_kernel(TraceArgs a) {
     a.path_len[blockIdx.x] = n;
     a.end_cost[blockIdx.x] = endpos >= 0 ? funord((uint32_t)(bk >> 32)) : __int_as_float(0x7f800000);
     a.final_rel[blockIdx.x] = any_final ? bf - bn : __int_as_float(0x7f800000);
-    a.end_state[blockIdx.x] = endpos >= 0 ? (int)(unsigned)(bk & 0xffffffffu) : -1;
+    a.end_state[blockIdx.x] = endpos >= 0 ? cs[endpos] : -1;
   }
 }
 
@@ -1764,7 +2248,7 @@ __global__ void init_tables_kernel(int* state, unsigned long long* key, int* sta
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     state[i] = -1;
     key[i] = kEmpty;
-    stamp[i] = -1;
+    stamp[i] = kNoStamp;
   }
 }
 

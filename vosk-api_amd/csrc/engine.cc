@@ -720,6 +720,31 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     HIPCHECK(hipMemset(dec_.prof, 0, sizeof(long long) * kDecProf * S));
   }
   LaunchInitTables(dec_.ht_state, dec_.ht_key, dec_.ht_stamp, S * H, stream_);
+  // token-passing order: Kaldi's (default) or the
+  // order-independent form (VOSK_AMD_DEC_ORDER=parallel)
+  dec_.kaldi = cfg_.kaldi_order ? 1 : 0;
+  if (const char* o = getenv("VOSK_AMD_DEC_ORDER")) {
+    const std::string v(o);
+    if (v == "parallel" || v == "0" || v == "order-independent") dec_.kaldi = 0;
+    else if (v == "kaldi" || v == "1") dec_.kaldi = 1;
+  }
+  dec_.kb_cap = (int)(2 * MT + 1024);
+  dec_.kord_cap = (int)(MT + 4096);
+  if (dec_.kaldi) {
+    const size_t KB = (size_t)S * dec_.kb_cap, KO = (size_t)S * dec_.kord_cap;
+    dec_.kb_first = (int*)DevAlloc(sizeof(int) * KB);
+    dec_.kb_cnt = (int*)DevAlloc(sizeof(int) * KB);
+    dec_.kb_start = (int*)DevAlloc(sizeof(int) * KB);
+    dec_.kb_memb = (int*)DevAlloc(sizeof(int) * 4 * KB);
+    dec_.kord = (int*)DevAlloc(sizeof(int) * KO);
+    dec_.kbkt = (int*)DevAlloc(sizeof(int) * KO);
+    dec_.kstk = (int*)DevAlloc(sizeof(int) * KO);
+    HIPCHECK(hipMemset(dec_.kb_first, 0x7f, sizeof(int) * KB));  // 0x7f7f7f7f: empty (above any creation index)
+    HIPCHECK(hipMemset(dec_.kb_cnt, 0, sizeof(int) * KB));
+  } else {
+    dec_.kb_first = dec_.kb_cnt = dec_.kb_start = dec_.kb_memb = nullptr;
+    dec_.kord = dec_.kbkt = dec_.kstk = nullptr;
+  }
 
   // ---- staging
   stage_sample_cap_ = (size_t)S * cfg_.max_step_samples;
@@ -809,6 +834,7 @@ void Engine::ResetPipeline(int slot) {
   h.decoded = 0;
   h.finished = false;
   h.need_reset = true;
+  h.fresh_decoder = true;
   h.err = 0;
   if (h.resident) (void)hipFree(h.resident);
   h.resident = nullptr;
@@ -1149,8 +1175,11 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
     h.out_ready += dec_frames;
     if (dec_frames > 0 || h.need_reset) {
       if (dec_frames > 0 || h.samples > 0 || fin) {
+        // reset 2: a new decoder; 1: InitDecoding of the same decoder (a
+        // Recognizer's next segment keeps its HashList size, Kaldi order)
         st_dec_.push_back(DecJob{s, first_real < 0 ? 0 : first_real * opc, dec_frames,
-                                 h.need_reset ? 1 : 0, stats_rows, fin ? 1 : 0, 0, 0});
+                                 h.need_reset ? (h.fresh_decoder ? 2 : 1) : 0, stats_rows, fin ? 1 : 0, 0, 0});
+        if (h.need_reset) h.fresh_decoder = false;
         stats_rows += dec_frames;
         if (h.need_reset) h.decoded = 0;
         h.need_reset = false;
@@ -1203,7 +1232,9 @@ void Engine::FinishDecodeBatch(const DecBatch& b) {
                          sizeof(float) * n, hipMemcpyDeviceToHost));
     }
     if (cfg_.collect_stats) {
-      h.stats.assign(h_stats_ + j.stats_row0, h_stats_ + j.stats_row0 + j.nframes);
+      // the decoder segment's frames (a reset starts a new segment)
+      if (j.reset) h.stats.clear();
+      h.stats.insert(h.stats.end(), h_stats_ + j.stats_row0, h_stats_ + j.stats_row0 + j.nframes);
       for (int f = 0; f < j.nframes; f++) {
         const FrameStat& fs = h_stats_[j.stats_row0 + f];
         times_.dec[0]++;
@@ -1483,6 +1514,7 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
     t.use_final = use_final ? 1 : 0;
     t.max_tok = dec_.max_tok;
     t.arena_cap = dec_.arena_cap;
+    t.tie_pos = dec_.kaldi;
     t.path_cap = cap;
     t.path = (int*)(d + o_path);
     t.path_len = (int*)(d + o_len);
@@ -1755,6 +1787,7 @@ void Engine::ProbeEndpoints(const std::vector<int>& slots, std::vector<EndpointP
   HIPCHECK(hipMemcpyAsync(d_probe_, h_probe_, sizeof(int) * n, hipMemcpyHostToDevice, stream_));
   TraceArgs t;
   memset(&t, 0, sizeof(t));
+  t.tie_pos = dec_.kaldi;
   t.arc_sil = d_arc_sil_;
   t.sinfo = d_sinfo_;
   t.arena = dec_.arena;
@@ -1843,7 +1876,7 @@ void Engine::ResetDecoderAtNextJob(int slot) {
     DecBatch& db = *order[b];
     for (size_t i = 0; i < db.jobs.size(); i++) {
       if (db.jobs[i].slot != slot) continue;
-      db.jobs[i].reset = 1;
+      db.jobs[i].reset = 2;  // a batch segment starts a new decoder
       DecJob* d = (DecJob*)(d_stage_ + (size_t)db.buf * stage_bytes_ + db.o_ej) + i;
       HIPCHECK(hipMemcpy(d, &db.jobs[i], sizeof(DecJob), hipMemcpyHostToDevice));
       // frame counts of the new segment: this job's, then the later staged one's
@@ -1862,6 +1895,7 @@ void Engine::ResetDecoderAtNextJob(int slot) {
   }
   h.decoded = 0;
   h.need_reset = true;
+  h.fresh_decoder = true;
 }
 
 int Engine::IvectorFramesReady(int slot) const {
@@ -1967,7 +2001,8 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     st_iv_frames_ = 0;
     h.stats.clear();
     const bool rs = first && (reset || h.need_reset);
-    st_dec_.push_back(DecJob{slot, 0, n, rs ? 1 : 0, 0, 0, 0, 0});
+    st_dec_.push_back(DecJob{slot, 0, n, rs ? (reset || h.fresh_decoder ? 2 : 1) : 0, 0, 0, 0, 0});
+    if (rs) h.fresh_decoder = false;
     if (rs) h.decoded = 0;
     h.need_reset = false;
     h.decoded += n;

@@ -96,6 +96,10 @@ struct EngineConfig {
   long long lattice_links = 1 << 22;  // link arena per stream (16 B each)
   int lattice_frames = 1 << 14;       // frames per decoder segment with a lattice
   bool track_decoded = false;  // record completed decoder jobs for TakeDecoded
+  // token passing in Kaldi's sequential order (LatticeFasterDecoder's HashList
+  // order, running emitting cutoff, LIFO epsilon queue), else
+  // the order-independent form; env VOSK_AMD_DEC_ORDER=kaldi|parallel overrides
+  bool kaldi_order = true;
 };
 
 // HIP-event times accumulated on the engine stream (time_kernels).
@@ -371,6 +375,7 @@ class Engine {
     int dev_frames = 0;      // frames of the decoder segment decoded on the device
     bool finished = false;
     bool need_reset = true;
+    bool fresh_decoder = true;  // the pending reset starts a new decoder (Kaldi order: HashList size 1000)
     int err = 0;
     std::vector<FrameStat> stats;
     std::vector<float> llh;

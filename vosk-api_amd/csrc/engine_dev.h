@@ -129,6 +129,7 @@ struct DecSlot {
   long long links_used;         // lattice links in the stream's link arena
   int last_prune;   // frames decoded at the last pruning pass
   float commit_cutoff;  // cutoff of the last commit: every current token's cost is below it
+  int khash;        // Kaldi order: the decoder's HashList size (0 = a new decoder's 1000)
 };
 
 // ---- lattice (LatticeFasterDecoder forward links, kept in HBM per stream).
@@ -278,6 +279,20 @@ struct DecArgs {
   int debug;              // VOSK_AMD_DEC_DEBUG: invariant checks with printf (development)
   float* extra;           // [slots][arena_cap] Kaldi extra_cost per token (pruning)
   int* remap;             // [slots][arena_cap] pruning scratch (old -> new arena index)
+  // Kaldi order (decoder.hip): the frame's token list in
+  // LatticeFasterDecoder's HashList order (bucket state % khash in order of
+  // first occupancy, then creation), the emitting pass's running cutoff as a
+  // prefix minimum, the epsilon queue run as Kaldi's LIFO
+  int kaldi;              // 1: Kaldi order, 0: the order-independent form
+  int* kb_first;          // [slots][kb_cap] per bucket: first creation index (INT_MAX: empty)
+  int* kb_cnt;            // [slots][kb_cap] per bucket: tokens
+  int* kb_start;          // [slots][kb_cap] per bucket: list position of its first token
+  int* kb_memb;           // [slots][kb_cap][4] per bucket: creation indices of its first four tokens
+  int kb_cap;             // >= the largest HashList size (2 * max_tok + 1024)
+  int* kord;              // [slots][kord_cap] frame under construction: slot code by creation index
+  int* kbkt;              // [slots][kord_cap] bucket by creation index
+  int* kstk;              // [slots][kord_cap] epsilon queue entries past the LDS part
+  int kord_cap;           // >= tokens a frame may create (max_tok + LDS table slots)
 };
 
 struct TraceArgs {
@@ -301,6 +316,7 @@ struct TraceArgs {
   // emitting, 2 = other emitting; the walk stops at the first 2 and path_len
   // counts the trailing silence frames (no path is written)
   const unsigned char* arc_sil;
+  int tie_pos;           // end-token ties: 1 the first in list order (Kaldi order), 0 the lowest state
 };
 
 }  // namespace vamd
