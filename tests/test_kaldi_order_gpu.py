@@ -67,6 +67,12 @@ def _compare(gpu, ref, max_active):
     over = 0
     for k, (g, r) in enumerate(zip(gpu, ref)):
         st = g["stats"]
+        d = np.nonzero(st[:, 1].astype(np.int64) != r["ntok"][1:len(st) + 1])[0]
+        if len(d):
+            f = int(d[0])
+            print(f"stream {k}: first token-count difference at frame {f}: gpu {st[max(f - 2, 0):f + 3, 1]} "
+                  f"oracle {r['ntok'][max(f - 2, 0) + 1:f + 4]} cutoff gpu {st[f, 5]} oracle {r['cutoff'][f]} "
+                  f"next {st[f, 6]} / {r['next_cutoff'][f]} best {st[f, 4]} / {r['best'][f + 1]} in {st[f, 0]}")
         np.testing.assert_array_equal(st[:, 1].astype(np.int64), r["ntok"][1:], err_msg=f"stream {k} tokens")
         np.testing.assert_array_equal(st[:, 4], r["best"][1:], err_msg=f"stream {k} best costs")
         np.testing.assert_array_equal(st[:, 5], r["cutoff"], err_msg=f"stream {k} cutoffs")

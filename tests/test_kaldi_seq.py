@@ -1,13 +1,14 @@
-"""The order-independent token passing (GPU decoder == oracle.c orc_decode,
-bit-exact) against the Kaldi-sequential restatement (orc_decode_kaldi:
+"""The opt-in order-independent token passing (oracle.c orc_decode, the GPU's
+VOSK_AMD_DEC_ORDER=parallel) against the Kaldi-sequential restatement (orc_decode_kaldi:
 LatticeFasterDecoderTpl with its HashList order, running emitting cutoff and
 LIFO epsilon queue).  Kaldi creates a superset of tokens (those between the
 frame's final emitting cutoff and the running one); they are never expanded
 while the beam decides the cutoff, so without an active-token limit the two
 forms give the same 1-best.  With min_active / max_active the extra tokens
-enter Kaldi's nth_element and the searches diverge: the stated tolerance
- is asserted here on the synthetic model (flat
-random-nnet scores, the hard case)."""
+enter Kaldi's nth_element and the searches diverge: the opt-in form's
+tolerance is asserted here on the synthetic model (flat
+random-nnet scores, the hard case).  The GPU's default is the Kaldi order
+itself (tests/test_kaldi_order_gpu.py)."""
 import numpy as np
 import pytest
 
@@ -37,7 +38,7 @@ def llhs(synth_model, test_wave):
 def test_same_one_best_without_active_limits(llhs):
     o, ls = llhs
     for llh in ls:
-        a = o.graph.decode(llh, o.beam, 2 ** 31 - 1, 0, o.beam_delta, True)
+        a = o.graph.decode(llh, o.beam, 2 ** 31 - 1, 0, o.beam_delta, True, kaldi=False)
         b = o.graph.decode(llh, o.beam, 2 ** 31 - 1, 0, o.beam_delta, True, kaldi=True)
         assert a["words"] == b["words"]
         assert a["best_cost"] == pytest.approx(b["best_cost"], rel=1e-6)
@@ -49,7 +50,7 @@ def test_stated_tolerance_with_active_limits(llhs):
     same = errs = words = 0
     rel = []
     for llh in ls:
-        a = o.graph.decode(llh, o.beam, o.max_active, o.min_active, o.beam_delta, True)
+        a = o.graph.decode(llh, o.beam, o.max_active, o.min_active, o.beam_delta, True, kaldi=False)
         b = o.graph.decode(llh, o.beam, o.max_active, o.min_active, o.beam_delta, True, kaldi=True)
         same += a["words"] == b["words"]
         errs += _ed(b["words"], a["words"])

@@ -989,182 +989,428 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
   return sh.kcar[par];
 }
 
-// find-or-add of one epsilon relaxation by a single thread (the queue):
-// the slot, the key it had (kEmpty if created) and whether it was created;
-// the key becomes the minimum
-struct KRelax {
-  int slot;
-  bool created;
-  unsigned long long old;
+// LDS views for Kaldi's epsilon queue (kaldi_nonemitting): regions no other
+// phase uses between the emitting pass and the commit (the log-likelihood
+// row, the token cache, the block-scan arrays, the frontier arrays); entries
+// past the LDS capacities live in the stream's HBM scratch.
+constexpr int kKM = 1024;  // queue tokens held in LDS
+constexpr int kKE = 2048;  // their epsilon arcs held in LDS
+struct KaldiLds {
+  int* ms;     // [kKM] token: slot code
+  float* mc;   // [kKM] its cost during the queue
+  int* mo;     // [kKM] its productive epsilon arcs: offset
+  int* mn;     // [kKM]                              count
+  int* mcr;    // [kKM] creation index of a token of the emitting pass, -1 for one the queue creates
+  int* mord;   // [kKM] order in which the queue creates it (-1: not yet)
+  int* v0hi;   // [kKM] initial queue keys: bucket's first creation index
+  int* v0lo;   //                            creation index
+  int* stk;    // [kKM] the LIFO queue
+  int2* adj;   // [kKE] (destination token, arc weight bits)
 };
-__device__ __forceinline__ KRelax kaldi_find_or_add(const DecArgs& a, DecShared& sh, const FrameLds& t,
-                                                    const HbmTab& T, int dest, unsigned long long k, bool eps) {
-  const int nbk = a.lds_probe < 2 ? a.lds_probe : 2;
-  const unsigned b1 = bucket1(dest);
-  for (int nb = 0; nb < nbk; nb++) {
-    const int h0 = 4 * (int)(nb ? bucket2(dest, b1) : b1);
-    for (int i = 0; i < 4; i++) {
-      const int h = h0 + i;
-      const int c = t.hs[h];
-      if (c == dest) {
-        const unsigned long long old = t.hk[h];
-        if (k < old) t.hk[h] = k;
-        return KRelax{h, false, old};
-      }
-      if (c == -1) {  // buckets fill left to right
-        t.hs[h] = dest;
-        const int pos = sh.n_new_l++;
-        t.nl[pos] = (unsigned short)h;
-        t.hp[h] = (unsigned short)(pos | (eps ? kPosEps : 0));
-        t.hk[h] = k;
-        return KRelax{h, true, kEmpty};
-      }
-    }
+// member record in HBM past kKM: {slot, cost bits, offset, count, creation index, order}
+constexpr int kKMRec = 8;
+enum { kMSlot = 0, kMCost = 1, kMOff = 2, kMCnt = 3, kMC = 4, kMOrd = 5 };
+__device__ __forceinline__ int* km_lds(const KaldiLds& K, int i, int f) {
+  switch (f) {
+    case kMSlot: return &K.ms[i];
+    case kMCost: return reinterpret_cast<int*>(&K.mc[i]);
+    case kMOff: return &K.mo[i];
+    case kMCnt: return &K.mn[i];
+    case kMC: return &K.mcr[i];
+    default: return &K.mord[i];
   }
-  const unsigned hm = (1u << a.hbits) - 1u;
-  unsigned g = hbm_hash(dest, a.hbits);
-  for (int probe = 0; probe < a.hprobe; probe++) {
-    const int c = AG_LD(&T.state[g]);
-    if (c == dest) {
-      const unsigned long long old = AG_LD(&T.key[g]);
-      if (k < old) AG_ST(&T.key[g], k);
-      return KRelax{~(int)g, false, old};
-    }
-    if (c == -1) {
-      AG_ST(&T.state[g], dest);
-      const int pos = sh.n_new_g++;
-      if (pos < a.max_tok) {
-        AG_ST(&T.list[pos], (int)g);
-        AG_ST(&T.pos[g], pos | (eps ? kHPosEps : 0));
-      } else {
-        sh.bad |= 1;
-      }
-      AG_ST(&T.key[g], k);
-      return KRelax{~(int)g, true, kEmpty};
-    }
-    g = (g + 1) & hm;
-  }
-  sh.bad |= 1;
-  return KRelax{kNoSlot, false, 0};
+}
+__device__ __forceinline__ int km_get(const KaldiLds& K, int* KM, int i, int f) {
+  return i < kKM ? *km_lds(K, i, f) : AG_LD(&KM[(long long)(i - kKM) * kKMRec + f]);
+}
+__device__ __forceinline__ void km_set(const KaldiLds& K, int* KM, int i, int f, int v) {
+  if (i < kKM) *km_lds(K, i, f) = v;
+  else AG_ST(&KM[(long long)(i - kKM) * kKMRec + f], v);
 }
 
-// ProcessNonemitting in Kaldi order over the frame under construction, whose
-// tokens have creation indices [0, nc) (bucket state % khash); returns the
-// token count after the epsilon queue.  stk: LDS part of the queue.
-__device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh, const FrameLds& t,
-                                                 const HbmTab& T, const DecPtrs& p, int* stk, int slot, int khash,
-                                                 float cutoff, int nc, int* arcs_eps, Prof& pr) {
+// ProcessNonemitting in Kaldi order.  The frame under construction holds the
+// emitting pass's tokens, creation indices [0, ne) (bucket state % khash).
+// The epsilon closure itself (final token set, costs, backpointers and the
+// links of the final costs) is order-independent, so it runs in parallel
+// (eps_closure); the order in which Kaldi's LIFO queue CREATES tokens is
+// not, and decides their list positions.  The queue is replayed on one
+// thread over LDS-staged data: only tokens that can relax an epsilon arc
+// below the cutoff at their final cost matter (at any higher cost they relax
+// nothing), with those arcs, plus the tokens the closure created.  Their
+// queue costs start at the emitting pass's costs (+inf: not yet created).
+// Returns the frame's token count; the created tokens get creation indices
+// [ne, count) in the queue's order.
+__device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh, FrameLds& t, const HbmTab& T,
+                                                 const DecPtrs& p, DecSlot& st, const KaldiLds& K, int slot,
+                                                 int khash, float cutoff, int ne, int* arcs_eps, Prof& pr) {
   int* KO = a.kord + (long long)slot * a.kord_cap;
   int* KB = a.kbkt + (long long)slot * a.kord_cap;
   int* KS = a.kstk + (long long)slot * a.kord_cap;
+  float* KC = a.kcost0 + (long long)slot * a.kord_cap;
+  int* KM = a.kmem + (long long)slot * a.kord_cap * kKMRec;
+  int2* KA = a.kadj + (long long)slot * a.kadj_cap;
   int* BF = a.kb_first + (long long)slot * a.kb_cap;
   int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
   int* BM = a.kb_memb + (long long)slot * a.kb_cap * 4;
-  constexpr int kKeyLds = kFrontLds;  // queue keys in LDS over both frontier arrays
-  unsigned long long* KV = reinterpret_cast<unsigned long long*>(t.fr0);
-  unsigned long long* KVg = reinterpret_cast<unsigned long long*>(p.fg0);  // [max_tok] past the LDS part
-  // the buckets of the emitting pass's tokens
-  for (int c = threadIdx.x; c < nc; c += DT) {
+  const float kInf = __int_as_float(0x7f800000);
+  // the emitting pass's tokens: buckets, queue costs, stamps cleared for the
+  // closure's rounds, and the closure's first frontier (tokens with epsilon arcs)
+  if (threadIdx.x == 0) {
+    sh.n_front = 0;
+    sh.kn0 = 0;
+    sh.kne = 0;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < ne; c += DT) {
     const int v = AG_LD(&KO[c]);
     const int b = (int)((unsigned)slot_state(t, T, v) % (unsigned)khash);
     AG_ST(&KB[c], b);
     __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (m < 4) AG_ST(&BM[4 * b + m], c);
-  }
-  if (threadIdx.x == 0) sh.kn0 = 0;
-  vm_drain();
-  __syncthreads();
-  // Kaldi's initial queue, restricted to the tokens that can relax an
-  // epsilon arc below the cutoff, keyed by list order (bucket's first
-  // creation index, creation index)
-  for (int c = threadIdx.x; c < nc; c += DT) {
-    const int v = AG_LD(&KO[c]);
+    AG_ST(&KC[c], funord((uint32_t)(slot_key(t, T, v) >> 32)));
+    if (v >= 0) t.hst[v] = kNoStamp;
+    else AG_ST(&T.stamp[~v], kNoStamp);
     const bool eps = v >= 0 ? (t.hp[v] & kPosEps) != 0 : (AG_LD(&T.pos[~v]) & kHPosEps) != 0;
-    if (!eps) continue;
-    const float cost = funord((uint32_t)(slot_key(t, T, v) >> 32));
-    if (!(cost < cutoff)) continue;
-    const int4 si = a.sinfo[slot_state(t, T, v)];
-    bool prod = false;
-    for (int arc = si.y; arc < si.z && !prod; arc++) prod = cost + __int_as_float(a.arcs[arc].y) < cutoff;
-    if (!prod) continue;
-    const int q = atomicAdd(&sh.kn0, 1);
-    const unsigned long long key =
-        ((unsigned long long)(unsigned)AG_LD(&BF[AG_LD(&KB[c])]) << 32) | (unsigned)c;
-    if (q < kKeyLds) KV[q] = key;
-    else if (q - kKeyLds < a.max_tok) AG_ST(&KVg[q - kKeyLds], key);
-    else sh.bad |= 1;
+    if (eps) push_front(a, sh, t, p, 0, &sh.n_front, v);
   }
   vm_drain();
   __syncthreads();
-  int n0 = sh.kn0;
-  n0 = n0 < kKeyLds + a.max_tok ? n0 : kKeyLds + a.max_tok;
-  // list order: rank by counting (the queue holds few tokens)
-  for (int i = threadIdx.x; i < n0; i += DT) {
-    const unsigned long long ki = i < kKeyLds ? KV[i] : AG_LD(&KVg[i - kKeyLds]);
-    int r = 0;
-    for (int j = 0; j < n0; j++) r += (j < kKeyLds ? KV[j] : AG_LD(&KVg[j - kKeyLds])) < ki;
-    const int v = AG_LD(&KO[(int)(unsigned)(ki & 0xffffffffu)]);
-    if (r < kTokLds) stk[r] = v;
-    else if (r - kTokLds < a.kord_cap) AG_ST(&KS[r - kTokLds], v);
-  }
-  vm_drain();
+  const int nl_e = sh.n_new_l, ng_e = sh.n_new_g;
+  eps_closure(a, sh, t, T, p, st, cutoff, sh.n_front, arcs_eps, pr);
   __syncthreads();
   pr.mark(5);
-  // the LIFO queue (pop_back), one thread
-  if (threadIdx.x == 0) {
-    int sp = n0, ne = nc, ex = 0;
-    bool ok = true;
-    while (sp > 0 && ok) {
-      --sp;
-      const int v = sp < kTokLds ? stk[sp] : AG_LD(&KS[sp - kTokLds]);
-      const float cst = funord((uint32_t)(slot_key(t, T, v) >> 32));
-      if (!(cst < cutoff)) continue;
-      const int4 si = a.sinfo[slot_state(t, T, v)];
-      for (int arc = si.y; arc < si.z; arc++) {
-        const int4 A = a.arcs[arc];
-        ex++;
-        const float tot = cst + __int_as_float(A.y);
-        if (!(tot < cutoff)) continue;
-        const bool de = ((unsigned)A.w & kDestEps) != 0;
-        const unsigned long long kk = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
-        const KRelax r = kaldi_find_or_add(a, sh, t, T, A.x, kk, de);
-        if (r.slot == kNoSlot || ne >= a.kord_cap) {
-          sh.bad |= 1;
-          ok = false;
-          break;
-        }
-        if (kk < r.old) set_bp(t, T, r.slot, eps_bp(v));
-        if (r.created) {
-          const int c = ne++;
-          if (r.slot >= 0) t.hst[r.slot] = c;
-          else AG_ST(&T.stamp[~r.slot], c);
-          AG_ST(&KO[c], r.slot);
-          const int b = (int)((unsigned)A.x % (unsigned)khash);
-          AG_ST(&KB[c], b);
-          if (AG_LD(&BF[b]) > c) AG_ST(&BF[b], c);
-          const int m = AG_LD(&BC[b]);
-          AG_ST(&BC[b], m + 1);
-          if (m < 4) AG_ST(&BM[4 * b + m], c);
-        }
-        if (de && (r.created || tot < funord((uint32_t)(r.old >> 32)))) {  // FindOrAddToken's changed
-          if (sp < kTokLds) stk[sp] = r.slot;
-          else if (sp - kTokLds < a.kord_cap) AG_ST(&KS[sp - kTokLds], r.slot);
-          else {
-            sh.bad |= 1;
-            ok = false;
-            break;
-          }
-          sp++;
+  const int nl_n = sh.n_new_l, ng = sh.n_new_g < a.max_tok ? sh.n_new_g : a.max_tok;
+  const int n_eps = (nl_n - nl_e) + (ng - ng_e);
+  if (n_eps <= 1) {  // the creation order is the closure's (none or one)
+    if (n_eps == 1 && threadIdx.x == 0) {
+      const int v = nl_n > nl_e ? (int)t.nl[nl_e] : ~AG_LD(&T.list[ng_e]);
+      const int b = (int)((unsigned)slot_state(t, T, v) % (unsigned)khash);
+      AG_ST(&KO[ne], v);
+      AG_ST(&KB[ne], b);
+      if (AG_LD(&BF[b]) > ne) AG_ST(&BF[b], ne);
+      const int m = AG_LD(&BC[b]);
+      AG_ST(&BC[b], m + 1);
+      if (m < 4) AG_ST(&BM[4 * b + m], ne);
+    }
+    vm_drain();
+    __syncthreads();
+    return ne + n_eps;
+  }
+  // every entry's stamp cleared, then the queue's tokens numbered: tokens of
+  // the emitting pass that can relax an epsilon arc below the cutoff at
+  // their final cost, and every token the closure created
+  for (int j = threadIdx.x; j < nl_n + ng; j += DT) {
+    const int v = j < nl_n ? (int)t.nl[j] : ~AG_LD(&T.list[j - nl_n]);
+    if (v >= 0) t.hst[v] = kNoStamp;
+    else AG_ST(&T.stamp[~v], kNoStamp);
+  }
+  vm_drain();
+  __syncthreads();
+  const int cap_m = kKM + a.kord_cap;
+  for (int j = threadIdx.x; j < ne + n_eps; j += DT) {
+    int v, c;
+    if (j < ne) {
+      c = j;
+      v = AG_LD(&KO[c]);
+      const bool eps = v >= 0 ? (t.hp[v] & kPosEps) != 0 : (AG_LD(&T.pos[~v]) & kHPosEps) != 0;
+      if (!eps) continue;
+    } else {
+      const int q = j - ne;  // the closure's q-th created entry
+      c = -1;
+      v = q < nl_n - nl_e ? (int)t.nl[nl_e + q] : ~AG_LD(&T.list[ng_e + q - (nl_n - nl_e)]);
+    }
+    const float fc = funord((uint32_t)(slot_key(t, T, v) >> 32));
+    const int4 si = a.sinfo[slot_state(t, T, v)];
+    int cnt = 0;
+    if (fc < cutoff)
+      for (int arc = si.y; arc < si.z; arc++) cnt += fc + __int_as_float(a.arcs[arc].y) < cutoff;
+    if (c >= 0 && cnt == 0) continue;  // relaxes nothing at any cost: not a queue token
+    const int i = atomicAdd(&sh.kne, 1);
+    if (i >= cap_m) {
+      sh.bad |= 1;
+      continue;
+    }
+    if (v >= 0) t.hst[v] = i;
+    else AG_ST(&T.stamp[~v], i);
+    const float c0 = c >= 0 ? AG_LD(&KC[c]) : kInf;
+    km_set(K, KM, i, kMSlot, v);
+    km_set(K, KM, i, kMCost, __float_as_int(c0));
+    km_set(K, KM, i, kMCnt, cnt);
+    km_set(K, KM, i, kMC, c);
+    km_set(K, KM, i, kMOrd, -1);
+    // Kaldi's initial queue: a token of the emitting pass that relaxes an
+    // arc below the cutoff at its emitting cost, keyed by its list order
+    if (c >= 0 && c0 < cutoff) {
+      bool prod = false;
+      for (int arc = si.y; arc < si.z && !prod; arc++) prod = c0 + __int_as_float(a.arcs[arc].y) < cutoff;
+      if (prod) {
+        const int q = atomicAdd(&sh.kn0, 1);
+        if (q < kKM) {
+          K.v0hi[q] = AG_LD(&BF[AG_LD(&KB[c])]);
+          K.v0lo[q] = c;
+        } else {
+          reinterpret_cast<unsigned long long*>(p.fg0)[q - kKM] =
+              ((unsigned long long)(unsigned)AG_LD(&BF[AG_LD(&KB[c])]) << 32) | (unsigned)c;
         }
       }
     }
-    sh.kne = ne;
-    *arcs_eps += ex;
   }
   vm_drain();
   __syncthreads();
-  return sh.kne;
+  const int nm = sh.kne < cap_m ? sh.kne : cap_m;
+  const int n0 = sh.kn0 < nm ? sh.kn0 : nm;
+  // adjacency offsets (a scan over the members), then each member's
+  // productive arcs in graph order: (destination member or -1, weight)
+  {
+    int run = 0, par = 0;
+    for (int i0 = 0; i0 < nm; i0 += DT) {
+      const int i = i0 + threadIdx.x;
+      const int cnt = i < nm ? km_get(K, KM, i, kMCnt) : 0;
+      int tot;
+      const int off = run + kaldi_excl_sum(sh, cnt, par, &tot);
+      if (i < nm) km_set(K, KM, i, kMOff, off);
+      run += tot;
+      par ^= 1;
+    }
+    if (run > kKE + a.kadj_cap && threadIdx.x == 0) sh.bad |= 1;
+  }
+  vm_drain();
+  __syncthreads();
+  for (int i = threadIdx.x; i < nm; i += DT) {
+    const int cnt = km_get(K, KM, i, kMCnt);
+    if (cnt == 0) continue;
+    const int off = km_get(K, KM, i, kMOff);
+    const int v = km_get(K, KM, i, kMSlot);
+    const float fc = funord((uint32_t)(slot_key(t, T, v) >> 32));
+    const int4 si = a.sinfo[slot_state(t, T, v)];
+    int k = 0;
+    for (int arc = si.y; arc < si.z; arc++) {
+      const int4 A = a.arcs[arc];
+      if (!(fc + __int_as_float(A.y) < cutoff)) continue;
+      const int dv = frame_slot(a, t, T, A.x);
+      int d = -1;
+      if (dv != kNoSlot) {
+        const int h = dv >= 0 ? t.hst[dv] : AG_LD(&T.stamp[~dv]);
+        d = h == kNoStamp ? -1 : h;
+      }
+      const int e = off + k++;
+      const int2 rec = make_int2(d, A.y);
+      if (e < kKE) K.adj[e] = rec;
+      else if (e - kKE < a.kadj_cap) {
+        AG_ST(&reinterpret_cast<long long*>(KA)[e - kKE],
+              (long long)(((unsigned long long)(unsigned)rec.y << 32) | (unsigned)rec.x));
+      }
+    }
+  }
+  // the initial queue in list order (rank by counting: it is short)
+  for (int q = threadIdx.x; q < n0; q += DT) {
+    auto key = [&](int r) -> unsigned long long {
+      if (r < kKM) return ((unsigned long long)(unsigned)K.v0hi[r] << 32) | (unsigned)K.v0lo[r];
+      return reinterpret_cast<unsigned long long*>(p.fg0)[r - kKM];
+    };
+    const unsigned long long kq = key(q);
+    int r = 0;
+    for (int j = 0; j < n0; j++) r += key(j) < kq;
+    // the member of creation index c: its stamp
+    const int c = (int)(unsigned)(kq & 0xffffffffu);
+    const int v = AG_LD(&KO[c]);
+    const int i = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+    if (r < kKM) K.stk[r] = i;
+    else AG_ST(&KS[r - kKM], i);
+  }
+  vm_drain();
+  __syncthreads();
+  // the LIFO queue (pop_back), one thread, over the staged tokens: LDS only
+  // when everything fits (the common case), else through the HBM records
+  int adj_n = 0;
+  if (nm > 0) adj_n = km_get(K, KM, nm - 1, kMOff) + km_get(K, KM, nm - 1, kMCnt);
+  const bool fast = nm <= kKM && adj_n <= kKE && n0 <= kKM && !(a.debug & 4);
+  if (a.debug & 8) {  // development timing only: no replay (creation order = member order; wrong lists)
+    for (int i = threadIdx.x; i < nm; i += DT) K.mord[i] = -1;
+    if (threadIdx.x == 0) {
+      int created = 0;
+      for (int i = 0; i < nm; i++)
+        if (K.mcr[i] < 0) K.mord[i] = created++;
+      sh.kn0 = created;
+    }
+  } else if (fast && nm <= 256 && threadIdx.x < 64) {
+    // up to 256 tokens: wave 0 keeps their queue costs and counts in
+    // registers (token i: lane i & 63, register i >> 6) and the queue in two
+    // registers (depth 128); token and arc indices are wave-uniform, so every
+    // read is a v_readlane and every write a lane select (a ds_bpermute
+    // shuffle costs an LDS round trip); the arcs of a popped token are read by its lanes
+    // together.  Plain register variables: an indexed register array would
+    // live in scratch memory.
+    const int lane = threadIdx.x;
+    int c0 = __float_as_int(kInf), c1 = c0, c2 = c0, c3 = c0;
+    int n0r = 0, n1r = 0, n2r = 0, n3r = 0, o0 = 0, o1 = 0, o2 = 0, o3 = 0, d0 = -1, d1 = -1, d2 = -1, d3 = -1;
+    if (lane < nm) { c0 = __float_as_int(K.mc[lane]); n0r = K.mn[lane]; o0 = K.mo[lane]; }
+    if (lane + 64 < nm) { c1 = __float_as_int(K.mc[lane + 64]); n1r = K.mn[lane + 64]; o1 = K.mo[lane + 64]; }
+    if (lane + 128 < nm) { c2 = __float_as_int(K.mc[lane + 128]); n2r = K.mn[lane + 128]; o2 = K.mo[lane + 128]; }
+    if (lane + 192 < nm) { c3 = __float_as_int(K.mc[lane + 192]); n3r = K.mn[lane + 192]; o3 = K.mo[lane + 192]; }
+    int q0 = lane < n0 ? K.stk[lane] : 0, q1 = lane + 64 < n0 ? K.stk[lane + 64] : 0;
+#define KSEL(r, a0, a1, a2, a3) ((r) == 0 ? (a0) : (r) == 1 ? (a1) : (r) == 2 ? (a2) : (a3))
+#define KRD(r, i, a0, a1, a2, a3) __builtin_amdgcn_readlane(KSEL(r, a0, a1, a2, a3), (i))
+    int sp = n0 < 128 ? n0 : 128, created = 0;
+    bool ovf = n0 > 128;
+    while (sp > 0 && !ovf) {
+      --sp;
+      const int u = sp < 64 ? __builtin_amdgcn_readlane(q0, sp) : __builtin_amdgcn_readlane(q1, sp - 64);
+      const int ur = u >> 6, ul = u & 63;
+      const float cu = __int_as_float(KRD(ur, ul, c0, c1, c2, c3));
+      if (!(cu < cutoff)) continue;
+      const int cnt = KRD(ur, ul, n0r, n1r, n2r, n3r), off = KRD(ur, ul, o0, o1, o2, o3);
+      for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
+        const int2 rec = lane < cnt - k0 ? K.adj[off + k0 + lane] : make_int2(-1, 0);
+        const int kn = cnt - k0 < 64 ? cnt - k0 : 64;
+        for (int k = 0; k < kn; k++) {
+          const int d = __builtin_amdgcn_readlane(rec.x, k);
+          const float tot = cu + __int_as_float(__builtin_amdgcn_readlane(rec.y, k));
+          if (d < 0 || !(tot < cutoff)) continue;  // (d < 0: a token of the emitting pass that relaxes nothing)
+          const int dr = d >> 6, dl = d & 63;
+          const float old = __int_as_float(KRD(dr, dl, c0, c1, c2, c3));
+          if (!(tot < old)) continue;
+          const int tb = __float_as_int(tot);
+          if (dr == 0) c0 = (lane == (dl) ? (tb) : c0);
+          else if (dr == 1) c1 = (lane == (dl) ? (tb) : c1);
+          else if (dr == 2) c2 = (lane == (dl) ? (tb) : c2);
+          else c3 = (lane == (dl) ? (tb) : c3);
+          if (old == kInf) {  // FindOrAddToken creates it
+            if (dr == 0) d0 = (lane == (dl) ? (created) : d0);
+            else if (dr == 1) d1 = (lane == (dl) ? (created) : d1);
+            else if (dr == 2) d2 = (lane == (dl) ? (created) : d2);
+            else d3 = (lane == (dl) ? (created) : d3);
+            created++;
+          }
+          if (KRD(dr, dl, n0r, n1r, n2r, n3r) > 0) {  // changed: re-queued (tokens that relax arcs)
+            if (sp == 128) {
+              ovf = true;
+              break;
+            }
+            if (sp < 64) q0 = (lane == (sp) ? (d) : q0);
+            else q1 = (lane == (sp - 64) ? (d) : q1);
+            sp++;
+          }
+        }
+      }
+    }
+#undef KRD
+#undef KSEL
+    if (lane < nm) { K.mc[lane] = __int_as_float(c0); K.mord[lane] = d0; }
+    if (lane + 64 < nm) { K.mc[lane + 64] = __int_as_float(c1); K.mord[lane + 64] = d1; }
+    if (lane + 128 < nm) { K.mc[lane + 128] = __int_as_float(c2); K.mord[lane + 128] = d2; }
+    if (lane + 192 < nm) { K.mc[lane + 192] = __int_as_float(c3); K.mord[lane + 192] = d3; }
+    if (lane == 0) sh.kn0 = ovf ? -1 : created;
+  } else if (threadIdx.x == 0 && fast) {
+    int sp = n0, created = 0;
+    bool ovf = false;
+    while (sp > 0 && !ovf) {
+      const int u = K.stk[--sp];
+      const float cu = K.mc[u];
+      if (!(cu < cutoff)) continue;
+      const int e1 = K.mo[u] + K.mn[u];
+      for (int e = K.mo[u]; e < e1; e++) {
+        const int2 rec = K.adj[e];
+        const float tot = cu + __int_as_float(rec.y);
+        if (rec.x < 0 || !(tot < cutoff)) continue;
+        const float old = K.mc[rec.x];
+        if (tot < old) {
+          if (old == kInf) K.mord[rec.x] = created++;  // FindOrAddToken creates it
+          K.mc[rec.x] = tot;
+          if (K.mn[rec.x] > 0) {  // changed: re-queued (only tokens that relax arcs matter)
+            if (sp == kKM) {
+              ovf = true;
+              break;
+            }
+            K.stk[sp++] = rec.x;
+          }
+        }
+      }
+    }
+    sh.kn0 = ovf ? -1 : created;
+  }
+  __syncthreads();
+  const bool slow = !(a.debug & 8) && (!fast || sh.kn0 < 0);
+  if (slow && fast) {  // the LDS queue overflowed: start over through the HBM records
+    for (int i = threadIdx.x; i < nm; i += DT) {
+      const int c = K.mcr[i];
+      K.mc[i] = c >= 0 ? AG_LD(&KC[c]) : kInf;
+      K.mord[i] = -1;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < n0; q += DT) {  // the initial queue again (the LDS stack was consumed)
+      const unsigned long long kq = ((unsigned long long)(unsigned)K.v0hi[q] << 32) | (unsigned)K.v0lo[q];
+      int r = 0;
+      for (int j = 0; j < n0; j++) r += (((unsigned long long)(unsigned)K.v0hi[j] << 32) | (unsigned)K.v0lo[j]) < kq;
+      const int v = AG_LD(&KO[(int)(unsigned)(kq & 0xffffffffu)]);
+      const int i = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+      if (r < kKM) K.stk[r] = i;
+      else AG_ST(&KS[r - kKM], i);
+    }
+    vm_drain();
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && slow) {
+    int sp = n0, created = 0;
+    const int scap = kKM + a.kord_cap;
+    while (sp > 0) {
+      --sp;
+      const int u = sp < kKM ? K.stk[sp] : AG_LD(&KS[sp - kKM]);
+      const float cu = __int_as_float(km_get(K, KM, u, kMCost));
+      if (!(cu < cutoff)) continue;
+      const int cnt = km_get(K, KM, u, kMCnt), off = km_get(K, KM, u, kMOff);
+      for (int k = 0; k < cnt; k++) {
+        const int e = off + k;
+        int2 rec;
+        if (e < kKE) {
+          rec = K.adj[e];
+        } else {
+          const unsigned long long w = (unsigned long long)AG_LD(&reinterpret_cast<long long*>(KA)[e - kKE]);
+          rec = make_int2((int)(unsigned)w, (int)(unsigned)(w >> 32));
+        }
+        if (rec.x < 0) continue;  // a token of the emitting pass that relaxes nothing: no effect
+        const float tot = cu + __int_as_float(rec.y);
+        if (!(tot < cutoff)) continue;
+        const float old = __int_as_float(km_get(K, KM, rec.x, kMCost));
+        if (old == kInf) km_set(K, KM, rec.x, kMOrd, created++);  // FindOrAddToken creates it
+        if (tot < old) {
+          km_set(K, KM, rec.x, kMCost, __float_as_int(tot));
+          if (km_get(K, KM, rec.x, kMCnt) > 0) {  // changed: re-queued (only tokens that relax arcs matter)
+            if (sp < kKM) K.stk[sp] = rec.x;
+            else if (sp - kKM < a.kord_cap) AG_ST(&KS[sp - kKM], rec.x);
+            else sh.bad |= 1;
+            sp++;
+            if (sp >= scap) break;
+          }
+        }
+      }
+      if (sp >= scap) break;
+    }
+    sh.kn0 = created;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && sh.kn0 != n_eps) sh.bad |= 1;  // the queue must create exactly the closure's tokens
+  vm_drain();
+  __syncthreads();
+  // the created tokens' creation indices [ne, ne + n_eps) in the queue's order, and their buckets
+  for (int i = threadIdx.x; i < nm; i += DT) {
+    if (km_get(K, KM, i, kMC) >= 0) continue;
+    const int o = km_get(K, KM, i, kMOrd);
+    if (o < 0 || o >= n_eps) continue;
+    const int c = ne + o;
+    const int v = km_get(K, KM, i, kMSlot);
+    const int b = (int)((unsigned)slot_state(t, T, v) % (unsigned)khash);
+    AG_ST(&KO[c], v);
+    AG_ST(&KB[c], b);
+    __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (m < 4) AG_ST(&BM[4 * b + m], c);
+  }
+  vm_drain();
+  __syncthreads();
+  pr.mark(23);  // (Kaldi order: the queue replay in the "exp_links" slot)
+  return ne + n_eps;
 }
 
 // List positions of the frame's n tokens (HashList order: buckets by their
@@ -1186,8 +1432,9 @@ __device__ __forceinline__ void kaldi_positions(const DecArgs& a, DecShared& sh,
     bool lead = false;
     if (c < n) {
       b = AG_LD(&KB[c]);
-      lead = AG_LD(&BF[b]) == c;
-      if (lead) sz = AG_LD(&BC[b]);
+      const int bf = AG_LD(&BF[b]), bc = AG_LD(&BC[b]);  // (issued together)
+      lead = bf == c;
+      if (lead) sz = bc;
     }
     int tot;
     const int ex = run + kaldi_excl_sum(sh, sz, par, &tot);
@@ -1199,15 +1446,17 @@ __device__ __forceinline__ void kaldi_positions(const DecArgs& a, DecShared& sh,
   __syncthreads();
   for (int c = threadIdx.x; c < n; c += DT) {
     const int b = AG_LD(&KB[c]);
-    const int cnt = AG_LD(&BC[b]);
+    const int v = AG_LD(&KO[c]);
+    // (issued together)
+    const int cnt = AG_LD(&BC[b]), bs = AG_LD(&BS[b]);
+    const int4 mb = ag_ld4(reinterpret_cast<const int4*>(&BM[4 * b]));
     int rk = 0;
     if (cnt <= 4) {
-      for (int i = 0; i < cnt; i++) rk += AG_LD(&BM[4 * b + i]) < c;
+      rk = (cnt > 0 && mb.x < c) + (cnt > 1 && mb.y < c) + (cnt > 2 && mb.z < c) + (cnt > 3 && mb.w < c);
     } else {  // a crowded bucket: count its tokens created before
       for (int c2 = 0; c2 < c; c2++) rk += AG_LD(&KB[c2]) == b;
     }
-    const int pos = AG_LD(&BS[b]) + rk;
-    const int v = AG_LD(&KO[c]);
+    const int pos = bs + rk;
     if (v >= 0) t.hst[v] = pos;
     else AG_ST(&T.stamp[~v], pos);
   }
@@ -1353,7 +1602,7 @@ __device__ __forceinline__ int commit_eps_links(const DecArgs& a, DecShared& sh,
 // next_cutoff) keep an arena slot marked dead.  Then both tables are cleared.
 __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds& t, DecPtrs& p, DecSlot& st,
                        int* TS, float* TC, bool* lds, float cutoff, float* best_out, int slot,
-                       int* nlinks, bool defer, Prof& pr) {
+                       int* nlinks, bool defer, Prof& pr, float* max_out = nullptr) {
   __syncthreads();
   const HbmTab T = hbm_tab(a, slot);
   const int nl_n = sh.n_new_l;
@@ -1377,6 +1626,7 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   }
   __syncthreads();
   unsigned long long bk = kEmpty;
+  float mx = -__int_as_float(0x7f800000);  // the largest token cost (Kaldi order: GetCutoff's shortcut)
   for (int j0 = threadIdx.x; j0 < n; j0 += 2 * DT) {
    // two entries per thread: the HBM entries' dependent loads in flight together
    int sq[2], bpq[2], vq[2];
@@ -1452,12 +1702,14 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
       // GetCutoff's best token: the first minimum in list order (Kaldi), else the lowest state
       const unsigned long long tk = ((unsigned long long)ford(cost) << 32) | (unsigned)(a.kaldi ? q : s);
       bk = tk < bk ? tk : bk;
+      mx = fmaxf(mx, cost);
     } else if (ok) {
       ag_st4(&p.arena[base + j], make_int4(-2, -1, __float_as_int(cost), s));  // dead list entry
     }
    }
   }
   bk = block_min_u64(sh, bk);  // ends with a barrier
+  if (max_out) *max_out = -block_min_f(sh, -mx);
   pr.mark(6);
   pr.count(12, n);
   if (!ok) sh.bad |= 2;
@@ -1670,7 +1922,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
   pr.mark(16);
   pr.count(20, F - kmin);
   pr.count(21, 1);
-  if (a.debug && a.links) prune_check(a, LF, LK, kmin, F, slot, 1, false);
+  if ((a.debug & 1) && a.links) prune_check(a, LF, LK, kmin, F, slot, 1, false);
   // ---- token remap over the window [wb, arena_used): R[t - wb] = number of
   // kept tokens before t (kDropped: t itself is dropped)
   load_frame(sh, LF, kmin, -1);
@@ -1820,8 +2072,8 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
   }
   __syncthreads();
   pr.mark(19);
-  if (a.debug && a.links) prune_check(a, LF, LK, kmin, F, slot, 2, false);
-  if (a.debug && threadIdx.x == 0)
+  if ((a.debug & 1) && a.links) prune_check(a, LF, LK, kmin, F, slot, 2, false);
+  if ((a.debug & 1) && threadIdx.x == 0)
     printf("prune slot %d F %d pf %d kmin %d wb %d end %d new_end %d links %lld -> %lld\n", slot, F, pf, kmin,
            wb, end, new_end, lw, lout);
   st.cur_base = new_end - (endF - tbF);
@@ -1834,7 +2086,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
 template <bool PROF>
 __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   __shared__ DecShared sh;
-  __shared__ float L[kLlhLds];
+  __shared__ __attribute__((aligned(16))) float L[kLlhLds];
   __shared__ int TS[kTokLds];
   __shared__ float TC[kTokLds];
   __shared__ int t_hs[kHashCap];
@@ -1854,6 +2106,19 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   t.fr0 = t_fr[0];
   t.fr1 = t_fr[1];
   lds_clear_build(t);
+  // Kaldi order: the epsilon queue's LDS views (kaldi_nonemitting)
+  static_assert(kLlhLds >= 4 * kKM && kTokLds >= kKM && DT + 1 >= kKM && 2 * kFrontLds >= 2 * kKE, "LDS views");
+  KaldiLds K;
+  K.ms = reinterpret_cast<int*>(L);
+  K.mc = L + kKM;
+  K.mo = reinterpret_cast<int*>(L + 2 * kKM);
+  K.mn = reinterpret_cast<int*>(L + 3 * kKM);
+  K.mcr = sh.scan;
+  K.mord = sh.abeg;
+  K.v0lo = reinterpret_cast<int*>(sh.tcost);
+  K.v0hi = reinterpret_cast<int*>(TC);
+  K.stk = TS;
+  K.adj = reinterpret_cast<int2*>(&t_fr[0][0]);
   const DecJob job = a.jobs[blockIdx.x];
   const int slot = job.slot;
   DecSlot st = a.slots[slot];
@@ -1921,16 +2186,17 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     if (a.kaldi) {
       vm_drain();
       __syncthreads();
-      kaldi_nonemitting(a, sh, t, T, p, TS, slot, st.khash, a.beam, 1, &arcs_eps, pr);
+      kaldi_nonemitting(a, sh, t, T, p, st, K, slot, st.khash, a.beam, 1, &arcs_eps, pr);
     } else {
       eps_closure(a, sh, t, T, p, st, a.beam, 1, &arcs_eps, pr);
     }
     float b;
     int nl = 0;
-    commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, &nl, false, pr);
+    float mxc;
+    commit(a, sh, t, p, st, TS, TC, &lds, a.beam, &b, slot, &nl, false, pr, &mxc);
     // every current token's cost is below the commit's cutoff (GetCutoff's
-    // shortcut); Kaldi order keeps tokens above it
-    st.commit_cutoff = a.kaldi ? __int_as_float(0x7f800000) : a.beam;
+    // shortcut); Kaldi order keeps tokens above it: their largest cost
+    st.commit_cutoff = a.kaldi ? mxc : a.beam;
     frame_done(a, sh, st, slot, 0, a.beam, 0.0f, nl);
   } else if (st.ntok > 0 && st.ntok <= kTokLds) {
     for (int i = threadIdx.x; i < st.ntok; i += DT) {
@@ -1991,11 +2257,13 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     CostRegs cr;
     // every token's cost is below the last commit's cutoff: when that is at
     // most beam_cutoff, all ntok are < (and <=) beam_cutoff without counting
-    const bool all_in = !a.kaldi && st.commit_cutoff <= beam_cutoff;
+    // (Kaldi order: commit_cutoff is the largest token cost instead)
+    const bool all_in = a.kaldi ? st.commit_cutoff < beam_cutoff && !(a.debug & 2) : st.commit_cutoff <= beam_cutoff;
+    // the costs in registers for the radix passes (also when the count below is skipped)
+    if ((need_max || need_min) && regs) cr.load(tv, ntok);
     if ((need_max || need_min) && !all_in) {
       unsigned long long cnt = 0;  // (# cost < beam_cutoff) << 32 | # cost <= beam_cutoff
       if (regs) {
-        cr.load(tv, ntok);
 #pragma unroll
         for (int r = 0; r < kCutRegs; r++) {
           const float c = cr.c[r];
@@ -2079,7 +2347,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       next_cutoff = expand_emitting_kaldi(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, seed, adaptive,
                                           &examined, st, slot, &nc, pr);
       pr.count(11, sh.n_new_g);
-      kaldi_nonemitting(a, sh, t, T, p, TS, slot, st.khash, next_cutoff, nc, &arcs_eps, pr);
+      kaldi_nonemitting(a, sh, t, T, p, st, K, slot, st.khash, next_cutoff, nc, &arcs_eps, pr);
     } else if (seed != __int_as_float(0x7f800000)) {
       const float m = expand_emitting(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, 1, seed, adaptive,
                                       &examined, st, slot, defer, pr);
@@ -2110,8 +2378,9 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
       }
     }
     int nl = 0;
-    commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, &nl, defer, pr);
-    st.commit_cutoff = a.kaldi ? __int_as_float(0x7f800000) : next_cutoff;
+    float mxc;
+    commit(a, sh, t, p, st, TS, TC, &lds, next_cutoff, &new_best, slot, &nl, defer, pr, &mxc);
+    st.commit_cutoff = a.kaldi ? mxc : next_cutoff;
     pr.count(15, 1);
     frame_done(a, sh, st, slot, st.frames + 1, next_cutoff, cost_offset, nl);
     st.offset_sum += (double)cost_offset;

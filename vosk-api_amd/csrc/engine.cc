@@ -739,11 +739,18 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     dec_.kord = (int*)DevAlloc(sizeof(int) * KO);
     dec_.kbkt = (int*)DevAlloc(sizeof(int) * KO);
     dec_.kstk = (int*)DevAlloc(sizeof(int) * KO);
+    dec_.kcost0 = (float*)DevAlloc(sizeof(float) * KO);
+    dec_.kmem = (int*)DevAlloc(sizeof(int) * 8 * KO);
+    dec_.kadj_cap = 4 * dec_.kord_cap;
+    dec_.kadj = (int2*)DevAlloc(sizeof(int2) * (size_t)S * dec_.kadj_cap);
     HIPCHECK(hipMemset(dec_.kb_first, 0x7f, sizeof(int) * KB));  // 0x7f7f7f7f: empty (above any creation index)
     HIPCHECK(hipMemset(dec_.kb_cnt, 0, sizeof(int) * KB));
   } else {
     dec_.kb_first = dec_.kb_cnt = dec_.kb_start = dec_.kb_memb = nullptr;
-    dec_.kord = dec_.kbkt = dec_.kstk = nullptr;
+    dec_.kord = dec_.kbkt = dec_.kstk = dec_.kmem = nullptr;
+    dec_.kcost0 = nullptr;
+    dec_.kadj = nullptr;
+    dec_.kadj_cap = 0;
   }
 
   // ---- staging

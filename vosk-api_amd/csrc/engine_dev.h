@@ -276,7 +276,8 @@ struct DecArgs {
   float lattice_beam;     // pruning (PruneActiveTokens)
   int prune_interval;     // frames between pruning passes (0 = never)
   int prune_revisit;      // frames below the last pruned frame a pass may re-walk
-  int debug;              // VOSK_AMD_DEC_DEBUG: invariant checks with printf (development)
+  int debug;              // VOSK_AMD_DEC_DEBUG bits (development): 1 invariant checks with printf,
+                          // 2 no Kaldi-order GetCutoff shortcut, 4 Kaldi epsilon queue through HBM records
   float* extra;           // [slots][arena_cap] Kaldi extra_cost per token (pruning)
   int* remap;             // [slots][arena_cap] pruning scratch (old -> new arena index)
   // Kaldi order (decoder.hip): the frame's token list in
@@ -292,7 +293,11 @@ struct DecArgs {
   int* kord;              // [slots][kord_cap] frame under construction: slot code by creation index
   int* kbkt;              // [slots][kord_cap] bucket by creation index
   int* kstk;              // [slots][kord_cap] epsilon queue entries past the LDS part
+  float* kcost0;          // [slots][kord_cap] emitting pass cost by creation index
+  int* kmem;              // [slots][kord_cap][8] epsilon queue tokens past the LDS part
+  int2* kadj;             // [slots][kadj_cap] their epsilon arcs past the LDS part
   int kord_cap;           // >= tokens a frame may create (max_tok + LDS table slots)
+  int kadj_cap;
 };
 
 struct TraceArgs {
