@@ -1364,6 +1364,53 @@ static void kd_commit(const orc_graph* g, kdec* d, orc_dec_result* r, int k, flo
   }
 }
 
+/* best path of the current frame: its end with final costs if any token is
+   final (and use_final), else the lowest cost (the first minimum in list
+   order); the arcs in forward order into path[0 .. min(*len, cap)).  Returns
+   the end token's index in the current list, -1 if there is none. */
+static int kd_best_path(const orc_graph* g, const kdec* d, int use_final, int* path, long long cap, int* len,
+                        float* frc, float* end_tot, int* end_state) {
+  const int ncur = d->ncur;
+  int end = -1;
+  float end_cost = INFINITY, best_nofinal = INFINITY, best_final = INFINITY;
+  for (int i = 0; i < ncur; i++) {
+    const float c = d->cur_cost[i];
+    if (c < best_nofinal) best_nofinal = c;
+    const float fc = g->final_cost[d->cur_state[i]];
+    if (fc != INFINITY && c + fc < best_final) best_final = c + fc;
+  }
+  const int any_final = best_final != INFINITY;
+  for (int i = 0; i < ncur; i++) {
+    const float c = (use_final && any_final) ? d->cur_cost[i] + g->final_cost[d->cur_state[i]] : d->cur_cost[i];
+    if (c < end_cost) { end_cost = c; end = i; }
+  }
+  *frc = any_final ? best_final - best_nofinal : INFINITY;
+  *len = 0;
+  if (end >= 0) {
+    *end_state = d->cur_state[end];
+    *end_tot = end_cost;
+    int n = 0;
+    for (int k = d->cur_idx[end]; k >= 0 && d->a_arc[k] >= 0; k = d->a_prev[k]) n++;
+    *len = n;
+    int k = d->cur_idx[end];
+    for (int j = n - 1; j >= 0; j--) {
+      if (j < cap) path[j] = d->a_arc[k];
+      k = d->a_prev[k];
+    }
+  }
+  return end;
+}
+
+/* endpoint probe i after the current frame: the no-final best path appended */
+static void kd_probe(const orc_graph* g, const kdec* d, orc_dec_result* r, int i) {
+  const long long off = r->probe_off[i];
+  int len = 0, es = 0;
+  float tot = 0.0f;
+  const long long room = r->probe_path_cap - off > 0 ? r->probe_path_cap - off : 0;
+  kd_best_path(g, d, 0, r->probe_path + off, room, &len, &r->probe_frc[i], &tot, &es);
+  r->probe_off[i + 1] = off + len;
+}
+
 int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, const orc_dec_opts* o,
                      int use_final, orc_dec_result* r) {
   const int S = g->num_states;
@@ -1386,6 +1433,8 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
   double offsets_sum = 0.0;
   const float hash_ratio = 2.0f;
   if (r->lat_frame_begin) { r->lat_ntok = 0; r->lat_nlink = 0; }
+  int pi = 0;
+  if (r->nprobe > 0) r->probe_off[0] = 0;
 
   /* InitDecoding: start token, ProcessNonemitting(beam) */
   {
@@ -1394,6 +1443,7 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
     kd_nonemitting(g, &d, o->beam);
     kd_commit(g, &d, r, 0, o->beam, 0.0f);
   }
+  for (; pi < r->nprobe && r->probe_frames[pi] <= 0; pi++) kd_probe(g, &d, r, pi);
   if (r->ntok) r->ntok[0] = d.ncur;
   if (r->best) { float b = INFINITY; for (int i = 0; i < d.ncur; i++) if (d.cur_cost[i] < b) b = d.cur_cost[i]; r->best[0] = b; }
 
@@ -1471,39 +1521,16 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
     if (r->next_cutoff) r->next_cutoff[f] = next_cutoff;
     if (r->arcs_emit) r->arcs_emit[f] = examined;
     if (r->best) { float b = INFINITY; for (int i = 0; i < d.ncur; i++) if (d.cur_cost[i] < b) b = d.cur_cost[i]; r->best[f + 1] = b; }
+    for (; pi < r->nprobe && r->probe_frames[pi] <= f + 1; pi++) kd_probe(g, &d, r, pi);
+  }
+  for (; pi < r->nprobe; pi++) {  /* probes past the decoded frames: nothing */
+    r->probe_off[pi + 1] = r->probe_off[pi];
+    r->probe_frc[pi] = INFINITY;
   }
   r->hash_size = (int)h->hash_size;
-
-  /* best path end: with final costs if any token is final (first minimum in list order) */
-  const int ncur = d.ncur;
-  int end = -1;
-  float end_cost = INFINITY, best_nofinal = INFINITY, best_final = INFINITY;
-  for (int i = 0; i < ncur; i++) {
-    const float c = d.cur_cost[i];
-    if (c < best_nofinal) best_nofinal = c;
-    const float fc = g->final_cost[d.cur_state[i]];
-    if (fc != INFINITY && c + fc < best_final) best_final = c + fc;
-  }
-  const int any_final = best_final != INFINITY;
-  for (int i = 0; i < ncur; i++) {
-    const float c = (use_final && any_final) ? d.cur_cost[i] + g->final_cost[d.cur_state[i]] : d.cur_cost[i];
-    if (c < end_cost) { end_cost = c; end = i; }
-  }
-  r->final_relative_cost = any_final ? best_final - best_nofinal : INFINITY;
-  r->path_len = 0;
-  if (end >= 0) {
-    r->end_state = d.cur_state[end];
-    r->best_tot = end_cost;
-    r->best_cost = (double)end_cost - offsets_sum;
-    int n = 0;
-    for (int k = d.cur_idx[end]; k >= 0 && d.a_arc[k] >= 0; k = d.a_prev[k]) n++;
-    r->path_len = n;
-    int k = d.cur_idx[end];
-    for (int j = n - 1; j >= 0; j--) {
-      if (j < r->path_cap) r->path[j] = d.a_arc[k];
-      k = d.a_prev[k];
-    }
-  }
+  const int end = kd_best_path(g, &d, use_final, r->path, r->path_cap, &r->path_len, &r->final_relative_cost,
+                               &r->best_tot, &r->end_state);
+  if (end >= 0) r->best_cost = (double)r->best_tot - offsets_sum;
   free(h->where); free(h->st); free(h->cost); free(h->bp); free(h->arc); free(h->bucket); free(h->bucket_rank);
   free(d.a_prev); free(d.a_arc); free(d.cur_state); free(d.cur_cost); free(d.cur_idx); free(d.order);
   free(d.cnt); free(d.queue); free(d.elem_pos); free(tmp);

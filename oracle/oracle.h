@@ -190,6 +190,13 @@ typedef struct {
   int lat_link_cap, lat_nlink;
   float* lat_cost_offset; /* [F + 1] cost offset of the links into frame k */
   int hash_size;          /* orc_decode_kaldi: the HashList size at the end */
+  /* optional endpoint probes (orc_decode_kaldi; nprobe 0 = none): after
+     probe_frames[i] decoded frames (ascending), the best path WITHOUT final
+     costs (what an endpoint check traces back) as arc indices in
+     probe_path[probe_off[i] .. probe_off[i+1]), and the final relative cost
+     in probe_frc[i].  One decoding pass answers every probe of a segment. */
+  const int* probe_frames; int nprobe;
+  int* probe_path; long long probe_path_cap; long long* probe_off; float* probe_frc;
 } orc_dec_result;
 
 int orc_decode(const orc_graph* g, const float* llh, int num_frames, int llh_stride,

@@ -98,3 +98,58 @@ def batch_segments(oracle, wave, llh, right_context, priming, spc=8160):
     T = mfcc_num_frames(N, oracle.mfcc_conf, oracle.fbank)
     segs.append((seg0, -(-T // fss)))
     return segs
+
+
+def _chunk_checks(oracle, N, right_context, priming, spc):
+    """The frame count ready after each chunk where the lane checks the
+    rules (batch_segments' schedule); the last entry is the stream's end."""
+    from oracle_py import mfcc_num_frames
+    fpc, fss = oracle.fpc, oracle.fss
+    opc = fpc // fss
+    ivr = oracle.ivector.m.right if oracle.ivector is not None else 0
+    c, out_ready, checks = -priming, 0, []
+    for k in range(N // spc):
+        T = mfcc_num_frames((k + 1) * spc, oracle.mfcc_conf, oracle.fbank)
+        njobs = 0
+        while njobs < priming + 2 and T >= (max(c, 0) + 1) * fpc + right_context + ivr:
+            if c >= 0:
+                out_ready += opc
+            c += 1
+            njobs += 1
+        checks.append(out_ready)
+    T = mfcc_num_frames(N, oracle.mfcc_conf, oracle.fbank)
+    return checks, -(-T // fss)
+
+
+def batch_segments_fast(oracle, wave, llh, right_context, priming, spc=8160):
+    """batch_segments with one decoding pass per segment: the segment's
+    decoder is probed at every later chunk check (orc_decode_kaldi endpoint
+    probes: the state after n frames does not depend on the frames after
+    them), and ends at the first probe whose rules fire.  Same result as
+    batch_segments (tests/test_oracle.py), linear instead of quadratic in the
+    stream length."""
+    rules, sil = endpoint_config(oracle.model_conf)
+    shift = F32(F32(0.01) * F32(oracle.fss))
+    min_len = min(r[3] for r in rules)
+    g = oracle.graph
+    checks, end = _chunk_checks(oracle, len(wave), right_context, priming, spc)
+    seg0, segs, k = 0, [], 0
+    while True:
+        cand = [(i, x) for i, x in enumerate(checks) if i >= k and x - seg0 > 0 and F32(x - seg0) * shift >= min_len]
+        if not cand:
+            break
+        last = max(x for _, x in cand)
+        r = g.decode(llh[seg0:last], oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
+                     use_final=False, kaldi=True, probes=[x - seg0 for _, x in cand])
+        fired = None
+        for (i, x), (path, frc) in zip(cand, r["probes"]):
+            ts = trailing_silence(path, g.ilabel, oracle.tm.tid2phone, sil)
+            if rules_fire(rules, x - seg0, ts, shift, frc):
+                fired = (i, x)
+                break
+        if fired is None:
+            break
+        segs.append((seg0, fired[1]))
+        seg0, k = fired[1], fired[0] + 1
+    segs.append((seg0, end))
+    return segs

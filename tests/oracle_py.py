@@ -554,7 +554,9 @@ class OrcDecResult(C.Structure):
                 ("lat_link_frame", C.c_void_p), ("lat_link_src", C.c_void_p),
                 ("lat_link_arc", C.c_void_p), ("lat_link_ac", C.c_void_p),
                 ("lat_link_cap", C.c_int), ("lat_nlink", C.c_int), ("lat_cost_offset", C.c_void_p),
-                ("hash_size", C.c_int)]
+                ("hash_size", C.c_int),
+                ("probe_frames", C.c_void_p), ("nprobe", C.c_int), ("probe_path", C.c_void_p),
+                ("probe_path_cap", C.c_longlong), ("probe_off", C.c_void_p), ("probe_frc", C.c_void_p)]
 
 
 class OracleGraph:
@@ -582,13 +584,16 @@ class OracleGraph:
                           self.final.ctypes.data, self.tid2pdf.ctypes.data)
 
     def decode(self, llh: np.ndarray, beam=13.0, max_active=7000, min_active=200,
-               beam_delta=0.5, use_final=True, lattice=False, kaldi=None, hash_size=0):
+               beam_delta=0.5, use_final=True, lattice=False, kaldi=None, hash_size=0, probes=None):
         """kaldi=True: the Kaldi-sequential restatement (orc_decode_kaldi:
         HashList order, running emitting cutoff, LIFO epsilon queue), the
         GPU decoder's default; False: the order-independent form (the GPU's
         VOSK_AMD_DEC_ORDER=parallel mode); None: as the environment selects
         (decoder_order()).  hash_size: the Kaldi HashList size the decoder
-        starts with (0: a new decoder); out["hash_size"] is its size at the end."""
+        starts with (0: a new decoder); out["hash_size"] is its size at the end.
+        probes (Kaldi order only): ascending frame counts; out["probes"] is a
+        list of (path without final costs, final relative cost) after each,
+        from the same single pass (the endpoint checks of a segment)."""
         if kaldi is None:
             kaldi = decoder_order() == "kaldi"
         llh = np.ascontiguousarray(llh, np.float32)
@@ -615,6 +620,17 @@ class OracleGraph:
             res.lat_link_arc, res.lat_link_ac = lat["link_arc"].ctypes.data, lat["link_ac"].ctypes.data
             res.lat_link_cap = lcap
             res.lat_cost_offset = lat["cost_offset"].ctypes.data
+        if probes is not None:
+            assert kaldi, "endpoint probes: Kaldi order only"
+            pf = np.ascontiguousarray(probes, np.int32)
+            assert np.all(np.diff(pf) >= 0)
+            pcap = int(4 * pf.astype(np.int64).clip(0).sum() + 64)
+            ppath = np.zeros(pcap, np.int32)
+            poff = np.zeros(len(pf) + 1, np.int64)
+            pfrc = np.zeros(max(len(pf), 1), np.float32)
+            res.probe_frames, res.nprobe = pf.ctypes.data, len(pf)
+            res.probe_path, res.probe_path_cap = ppath.ctypes.data, pcap
+            res.probe_off, res.probe_frc = poff.ctypes.data, pfrc.ctypes.data
         o = OrcDecOpts(beam, beam_delta, max_active, min_active, int(hash_size))
         fn = lib().orc_decode_kaldi if kaldi else lib().orc_decode
         rc = fn(C.byref(self.g), llh.ctypes.data_as(C.c_void_p), C.c_int(F),
@@ -626,6 +642,9 @@ class OracleGraph:
                    arcs_emit=ex[:F], path=p, words=words, best_cost=res.best_cost,
                    best_tot=res.best_tot, end_state=res.end_state,
                    final_relative_cost=res.final_relative_cost, hash_size=res.hash_size)
+        if probes is not None:
+            assert poff[-1] <= pcap
+            out["probes"] = [(ppath[poff[i]:poff[i + 1]].copy(), float(pfrc[i])) for i in range(len(pf))]
         if lattice:
             assert res.lat_ntok <= res.lat_tok_cap and res.lat_nlink <= res.lat_link_cap
             nt, nl = res.lat_ntok, res.lat_nlink

@@ -1082,6 +1082,14 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   pr.mark(5);
   const int nl_n = sh.n_new_l, ng = sh.n_new_g < a.max_tok ? sh.n_new_g : a.max_tok;
   const int n_eps = (nl_n - nl_e) + (ng - ng_e);
+  // an overflow (unlisted HBM entries, creation indices past kord_cap): no
+  // replay, the commit stores nothing (sh.bad is uniform after the barrier)
+  if (sh.bad || ng_e > a.max_tok || n_eps < 0 || ne + n_eps > a.kord_cap) {
+    __syncthreads();
+    if (threadIdx.x == 0) sh.bad |= 1;
+    __syncthreads();
+    return ne;
+  }
   if (n_eps <= 1) {  // the creation order is the closure's (none or one)
     if (n_eps == 1 && threadIdx.x == 0) {
       const int v = nl_n > nl_e ? (int)t.nl[nl_e] : ~AG_LD(&T.list[ng_e]);
@@ -1609,10 +1617,14 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   const int ng = sh.n_new_g < a.max_tok ? sh.n_new_g : a.max_tok;
   const int n = nl_n + ng;
   const int base = st.arena_used;
-  const bool ok = (long long)base + n <= a.arena_cap;
+  // Kaldi order after an overflow (sh.bad: tokens created but not listed,
+  // creation indices past kord_cap): list positions are not defined, so
+  // nothing is committed (the stream stops with its error bits; the next
+  // reset clears every table)
+  const bool ok = (long long)base + n <= a.arena_cap && !(a.kaldi && sh.bad);
   const bool lat = a.links != nullptr;
   // Kaldi order: the tokens' list positions (slot_pos) first
-  if (a.kaldi) kaldi_positions(a, sh, t, T, slot, n);
+  if (a.kaldi && ok) kaldi_positions(a, sh, t, T, slot, n);
   // the emitting records first: with deferred winners they set the
   // backpointers the token commit below reads (Kaldi order: every record is
   // an accepted relaxation, kept)
@@ -1718,7 +1730,7 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   *nlinks = (lat && ok) ? commit_eps_links(a, sh, t, T, p, st, slot, base, nl_n, neps, n_emit, cutoff) : 0;
   pr.mark(8);
   __syncthreads();
-  if (a.kaldi) kaldi_clear_buckets(a, slot, n);
+  if (a.kaldi && ok) kaldi_clear_buckets(a, slot, n);
   hbm_clear_listed(a, T, ng);
   lds_clear_build(t);
   __syncthreads();

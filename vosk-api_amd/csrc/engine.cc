@@ -745,6 +745,9 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     dec_.kadj = (int2*)DevAlloc(sizeof(int2) * (size_t)S * dec_.kadj_cap);
     HIPCHECK(hipMemset(dec_.kb_first, 0x7f, sizeof(int) * KB));  // 0x7f7f7f7f: empty (above any creation index)
     HIPCHECK(hipMemset(dec_.kb_cnt, 0, sizeof(int) * KB));
+    // creation order / buckets: valid indices from the start (slot 0, bucket 0)
+    HIPCHECK(hipMemset(dec_.kord, 0, sizeof(int) * KO));
+    HIPCHECK(hipMemset(dec_.kbkt, 0, sizeof(int) * KO));
   } else {
     dec_.kb_first = dec_.kb_cnt = dec_.kb_start = dec_.kb_memb = nullptr;
     dec_.kord = dec_.kbkt = dec_.kstk = dec_.kmem = nullptr;
