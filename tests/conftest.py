@@ -149,6 +149,13 @@ def synth_bigram_2m():
 
 
 @pytest.fixture(scope="session")
+def synth_bigram_8m():
+    """A static HCLG several times the 2.4 M-state one (~7.7 M states),
+    standing in for vosk-model-en-us-0.22's graph (BASELINE config 4)."""
+    return _make_preset("bigram_8m")
+
+
+@pytest.fixture(scope="session")
 def synth_la_small_en_us():
     """vosk-model-small-en-us scale lookahead model (20 k-word HCLr + a
     29 k-history trigram Gr; ~1.9 M states once expanded at load)."""

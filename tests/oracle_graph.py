@@ -5,12 +5,17 @@ nothing in the product imports it).  Follows:
 
 * OpenFST composition of HCLr.fst with Gr.fst as the reference requests it,
   ``LookaheadComposeFst(*hcl_fst_, *g_fst_, disambig_)``
-  (``src/recognizer.cc:31-37``): the alternative sequence composition filter
-  (grammar epsilons before HCL output epsilons), disambiguation
-  transition-ids mapped to epsilon.  Unlike the C++ expansion this one does
-  NOT prune with label reachability: it expands every composed state and
-  then trims, so agreement with the product also checks that the lookahead
-  pruning removes only dead states.
+  (``src/recognizer.cc:31-37``): ComposeFst with an olabel_lookahead first
+  FST selects OpenFST's lookahead filter chain [O: compose.h CreateBase,
+  lookahead-filter.h DefaultLookAhead<StdArc, MATCH_OUTPUT>]: the
+  alternative sequence filter (grammar epsilons before HCL output epsilons),
+  label lookahead with weight pushing (FastLogAccumulator log-sums of the
+  reachable grammar arcs, quantized to 1/1024 in the filter state) and
+  label pushing (a single reachable grammar arc is taken early), then
+  disambiguation transition-ids mapped to epsilon.  The label reachability
+  is a plain per-state search here (the C++ uses strongly connected
+  components and a per-word index for wide states), and every HCL arc is
+  looked ahead (no index), so agreement checks those shortcuts too.
 * ``LanguageModelEstimator`` (``src/language_model.cc:27-211``) with the
   grammar recognizer's order 2 / discount 0.5 (``src/recognizer.cc:68-71``);
   float arithmetic as the C++ (``count * discount / total`` in float, logf).
@@ -43,60 +48,231 @@ def logf(x):
     return np.float32(_libm.logf(ctypes.c_float(float(x))))
 
 
+F32 = np.float32
+_DINF = float("inf")
+_ACC_LIMIT, _ACC_PERIOD = 20, 10
+
+
+def _log_pos_exp(x):
+    return 0.0 if x == _DINF else math.log(1.0 + math.exp(-x))
+
+
+def _log_minus_exp(x):
+    return 0.0 if x == _DINF else math.log(1.0 - math.exp(-x))
+
+
+def _logplus_w(w, v):
+    """FastLogAccumulator::LogPlus(Weight, Weight): double, rounded to float."""
+    f1, f2 = float(w), float(v)
+    if f1 == _DINF and f2 == _DINF:
+        return F32(np.inf)
+    return F32(f2 - _log_pos_exp(f1 - f2)) if f1 > f2 else F32(f1 - _log_pos_exp(f2 - f1))
+
+
+def _logplus_d(f1, v):
+    f2 = float(v)
+    if f1 == _DINF:
+        return f2
+    return f2 - _log_pos_exp(f1 - f2) if f1 > f2 else f1 - _log_pos_exp(f2 - f1)
+
+
+def _logminus_w(f1, f2):
+    return F32(f1) if f2 == _DINF else F32(f1 - _log_minus_exp(f2 - f1))
+
+
+def _acc_sum(s, wt, sw, begin, end):
+    """FastLogAccumulator::Sum(w, aiter, begin, end)."""
+    sb = se = end
+    if sw is not None:
+        ib = (begin - 1) // _ACC_PERIOD + 1 if begin > 0 else 0
+        ie = end // _ACC_PERIOD
+        sb, se = ib * _ACC_PERIOD, ie * _ACC_PERIOD
+    for p in range(begin, min(sb, end)):
+        s = _logplus_w(s, wt[p])
+    if sb < se:
+        f1, f2 = sw[ie], sw[ib]
+        if f1 < f2:
+            s = _logplus_w(s, _logminus_w(f1, f2))
+    for p in range(max(sb, se), end):
+        s = _logplus_w(s, wt[p])
+    return s
+
+
+def _quantize(v):
+    if not np.isfinite(v):
+        return F32(v)
+    d = F32(1.0) / F32(1024.0)
+    return F32(np.floor(F32(F32(v) / d) + F32(0.5)) * d)
+
+
+def _intervals(labels):
+    out = []
+    for l in sorted(labels):
+        if out and l <= out[-1][1] + 1:
+            out[-1][1] = max(out[-1][1], l)
+        else:
+            out.append([l, l])
+    return out
+
+
+def reach_sets(hcl: kf.Fst):
+    """Per HCLr state: the output labels reachable through output-epsilon
+    arcs (first non-epsilon output label of such a path) and whether a final
+    state is reachable that way -- a plain search from every state (the C++
+    computes it per strongly connected component)."""
+    S = hcl.num_states
+    labs, fins = [], []
+    for s0 in range(S):
+        seen, st, L, fin = {s0}, [s0], set(), False
+        while st:
+            u = st.pop()
+            fin = fin or bool(np.isfinite(hcl.final[u]))
+            for a in range(int(hcl.row[u]), int(hcl.row[u + 1])):
+                o = int(hcl.olabel[a])
+                if o != 0:
+                    L.add(o)
+                elif int(hcl.nextstate[a]) not in seen:
+                    seen.add(int(hcl.nextstate[a]))
+                    st.append(int(hcl.nextstate[a]))
+        labs.append(_intervals(L))
+        fins.append(fin)
+    return labs, fins
+
+
+def _member(iv, l):
+    return any(lo <= l <= hi for lo, hi in iv)
+
+
 def compose(hcl: kf.Fst, g: kf.Fst, disambig) -> kf.Fst:
+    """ComposeFst(HCLr, G) with OpenFST's default MATCH_OUTPUT lookahead
+    filter chain (PushLabels(PushWeights(LookAhead(AltSequence)))), states
+    (q1, q2, alt-sequence bit, quantized lookahead weight, pushed label);
+    see graph_compose.cc for the arc rules this restates."""
     dis = set(int(d) for d in disambig)
+    labs, fins = reach_sets(hcl)
     # grammar: epsilon arcs in order, non-epsilon arcs stably sorted by label
     SB = g.num_states
-    geps, gwords = [], []
+    gsort, gneps = [], []
+    acc = []
     for s in range(SB):
         b, e = int(g.row[s]), int(g.row[s + 1])
-        geps.append([a for a in range(b, e) if g.ilabel[a] == 0])
+        eps = [a for a in range(b, e) if g.ilabel[a] == 0]
         ws = sorted((a for a in range(b, e) if g.ilabel[a] != 0), key=lambda a: int(g.ilabel[a]))
-        by = {}
-        for a in ws:
-            by.setdefault(int(g.ilabel[a]), []).append(a)
-        gwords.append(by)
+        gsort.append(eps + ws)
+        gneps.append(len(eps))
+        if e - b >= _ACC_LIMIT:
+            sw, tot = [_DINF], _DINF
+            for n, a in enumerate(eps + ws, 1):
+                tot = _logplus_d(tot, g.weight[a])
+                if n % _ACC_PERIOD == 0:
+                    sw.append(tot)
+            acc.append(sw)
+        else:
+            acc.append(None)
     gfinal = np.isfinite(g.final)
-    has_eps = [len(x) > 0 for x in geps]
-    alleps = [len(gwords[s]) == 0 and not gfinal[s] for s in range(SB)]
+    has_eps = [n > 0 for n in gneps]
+    alleps = [gneps[s] == len(gsort[s]) and not gfinal[s] for s in range(SB)]
+
+    def lookahead(p, q):
+        iv, cf = labs[p], fins[p]
+        arcs = gsort[q]
+        lab = [int(g.ilabel[a]) for a in arcs]
+        wt = [F32(g.weight[a]) for a in arcs]
+        rfin = cf and bool(gfinal[q])
+        n, nint = len(arcs), len(iv) + (1 if cf else 0)
+        rb = re = -1
+        w = F32(np.inf)
+        if 2 * n < nint:
+            for k in range(n):
+                if _member(iv, lab[k]):
+                    rb = k if rb < 0 else rb
+                    re = k + 1
+                    w = _logplus_w(w, wt[k])
+        else:
+            lo = 0
+            for ilo, ihi in iv:
+                bl = lo + int(np.searchsorted(lab[lo:], ilo, "left"))
+                el = bl + int(np.searchsorted(lab[bl:], ihi + 1, "left"))
+                lo = el
+                if el > bl:
+                    rb = bl if rb < 0 else rb
+                    re = el
+                    w = _acc_sum(w, wt, acc[q], bl, el)
+        rarc = rb >= 0
+        prefix, lw = None, F32(0.0)
+        if rarc:
+            if re - rb == 1 and not rfin:
+                prefix = arcs[rb]
+            else:
+                lw = w
+        if rfin and prefix is None:
+            lw = min(lw, F32(g.final[q])) if rarc else F32(g.final[q])
+        return rarc or rfin, prefix, lw
 
     ids = {}
     keys = []
 
-    def sid(q1, q2, fs):
-        k = (q1, q2, fs)
+    def sid(q1, q2, sb, fw, fl):
+        k = (q1, q2, sb, F32(fw).tobytes(), fl)
         i = ids.get(k)
         if i is None:
             i = ids[k] = len(keys)
-            keys.append(k)
+            keys.append((q1, q2, sb, F32(fw), fl))
         return i
 
-    start = sid(int(hcl.start), int(g.start), 0)
+    start = sid(int(hcl.start), int(g.start), 0, 0.0, -1)
     finals, rows, il, ol, wt, nx = [], [0], [], [], [], []
+
+    def arc(i, o, w, d):
+        il.append(i); ol.append(o); wt.append(F32(w)); nx.append(d)
+
     s = 0
+    Z = F32(0.0)
     while s < len(keys):
-        q1, q2, fs = keys[s]
+        q1, q2, sb, fw, fl = keys[s]
         fa, fb = hcl.final[q1], g.final[q2]
-        finals.append(np.float32(fa + fb) if np.isfinite(fa) and np.isfinite(fb) else np.float32(np.inf))
-        if fs == 0:
-            for a in geps[q2]:
-                il.append(0); ol.append(int(g.olabel[a])); wt.append(np.float32(g.weight[a]))
-                nx.append(sid(q1, int(g.nextstate[a]), 0))
-        for a in range(int(hcl.row[q1]), int(hcl.row[q1 + 1])):
-            lab = int(hcl.ilabel[a])
-            lab = 0 if lab in dis else lab
-            p = int(hcl.nextstate[a])
-            o = int(hcl.olabel[a])
+        finals.append(F32(F32(F32(fa) - fw) + F32(fb)) if fl == -1 and np.isfinite(fa) and np.isfinite(fb)
+                      else F32(np.inf))
+        hrange = range(int(hcl.row[q1]), int(hcl.row[q1 + 1]))
+
+        def lab_in(a):
+            x = int(hcl.ilabel[a])
+            return 0 if x in dis else x
+
+        if fl != -1:
+            for a in hrange:
+                p, o, aw = int(hcl.nextstate[a]), int(hcl.olabel[a]), F32(hcl.weight[a])
+                if o == fl:
+                    arc(lab_in(a), 0, aw + Z, sid(p, q2, 0, 0.0, -1))
+                elif o == 0 and _member(labs[p], fl):
+                    arc(lab_in(a), 0, aw + Z, sid(p, q2, sb, fw, fl))
+            rows.append(len(il))
+            s += 1
+            continue
+        nfw = Z - fw
+        if sb == 0:
+            for a in gsort[q2][:gneps[q2]]:
+                arc(0, int(g.olabel[a]), Z + F32(F32(g.weight[a]) + nfw), sid(q1, int(g.nextstate[a]), 0, 0.0, -1))
+        nsb = 1 if has_eps[q2] else 0
+        for a in hrange:
+            p, o, aw = int(hcl.nextstate[a]), int(hcl.olabel[a]), F32(hcl.weight[a])
             if o == 0:
                 if alleps[q2]:
                     continue
-                il.append(lab); ol.append(0); wt.append(np.float32(hcl.weight[a]))
-                nx.append(sid(p, q2, 1 if has_eps[q2] else 0))
+                ok, pre, lw = lookahead(p, q2)
+                if not ok:
+                    continue
+                if pre is not None:
+                    arc(lab_in(a), int(g.olabel[pre]), aw + F32(F32(Z + nfw) + F32(g.weight[pre])),
+                        sid(p, int(g.nextstate[pre]), nsb, 0.0, int(g.ilabel[pre])))
+                else:
+                    arc(lab_in(a), 0, aw + F32(Z + F32(lw - fw)), sid(p, q2, nsb, _quantize(lw), -1))
             else:
-                for b in gwords[q2].get(o, []):
-                    il.append(lab); ol.append(int(g.olabel[b]))
-                    wt.append(np.float32(np.float32(hcl.weight[a]) + np.float32(g.weight[b])))
-                    nx.append(sid(p, int(g.nextstate[b]), 0))
+                for b in gsort[q2][gneps[q2]:]:
+                    if int(g.ilabel[b]) != o:
+                        continue
+                    arc(lab_in(a), int(g.olabel[b]), aw + F32(F32(g.weight[b]) + nfw),
+                        sid(p, int(g.nextstate[b]), 0, 0.0, -1))
         rows.append(len(il))
         s += 1
     c = kf.Fst(start, np.array(finals, np.float32), np.array(rows, np.int64), np.array(il, np.int32),

@@ -584,7 +584,8 @@ class OracleGraph:
                           self.final.ctypes.data, self.tid2pdf.ctypes.data)
 
     def decode(self, llh: np.ndarray, beam=13.0, max_active=7000, min_active=200,
-               beam_delta=0.5, use_final=True, lattice=False, kaldi=None, hash_size=0, probes=None):
+               beam_delta=0.5, use_final=True, lattice=False, kaldi=None, hash_size=0, probes=None,
+               lattice_caps=None):
         """kaldi=True: the Kaldi-sequential restatement (orc_decode_kaldi:
         HashList order, running emitting cutoff, LIFO epsilon queue), the
         GPU decoder's default; False: the order-independent form (the GPU's
@@ -608,7 +609,7 @@ class OracleGraph:
         res = OrcDecResult(ntok.ctypes.data, best.ctypes.data, cut.ctypes.data, ncut.ctypes.data,
                            ex.ctypes.data, path.ctypes.data, cap, 0, 0.0, 0.0, -1, 0.0)
         if lattice:
-            tcap, lcap = 4000 * (F + 1) + 4096, 16000 * (F + 1) + 16384
+            tcap, lcap = lattice_caps if lattice_caps else (4000 * (F + 1) + 4096, 16000 * (F + 1) + 16384)
             lat = dict(frame_begin=np.zeros(F + 2, np.int32), tok_state=np.zeros(tcap, np.int32),
                        tok_cost=np.zeros(tcap, np.float32), link_frame=np.zeros(lcap, np.int32),
                        link_src=np.zeros(lcap, np.int32), link_arc=np.zeros(lcap, np.int32),
@@ -645,8 +646,11 @@ class OracleGraph:
         if probes is not None:
             assert poff[-1] <= pcap
             out["probes"] = [(ppath[poff[i]:poff[i + 1]].copy(), float(pfrc[i])) for i in range(len(pf))]
+        if lattice and (res.lat_ntok > res.lat_tok_cap or res.lat_nlink > res.lat_link_cap):
+            # the counts past the capacities are exact: decode again with room
+            return self.decode(llh, beam, max_active, min_active, beam_delta, use_final, lattice, kaldi,
+                               hash_size, probes, lattice_caps=(res.lat_ntok + 1, res.lat_nlink + 1))
         if lattice:
-            assert res.lat_ntok <= res.lat_tok_cap and res.lat_nlink <= res.lat_link_cap
             nt, nl = res.lat_ntok, res.lat_nlink
             out["lattice"] = dict(
                 frame_begin=lat["frame_begin"], tok_state=lat["tok_state"][:nt],

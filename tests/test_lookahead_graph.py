@@ -184,3 +184,71 @@ def test_truncated_graph_files_fail_cleanly(lib, synth_lookahead, tmp_path):
     assert _cgraph(lib, d) is None
     os.remove(gr)
     assert _cgraph(lib, d) is None  # neither HCLG nor HCLr + Gr
+
+
+def _tiny_pair(model_src, out):
+    """A hand-built HCLr / G pair on a copy of a lookahead model: words 1 =
+    'a', 2 = 'a b', 3 = 'c' in a prefix tree (word labels on the word-end arcs
+    back to state 0, as the synthetic HCLr), G = unigram state 0 (final 1.0;
+    w1 1.0, w2 2.0, w3 3.0 -> history w3) and history w3 (backoff 0.5, w1
+    0.25)."""
+    import shutil
+    shutil.copytree(model_src, out)
+    gd = os.path.join(out, "graph")
+    # (src, tid, olabel, weight, dst), per state olabel-sorted
+    arcs = [(0, 1, 0, 0.0, 1), (0, 5, 0, 0.0, 3), (1, 3, 0, 0.0, 2), (1, 2, 1, 0.0, 0),
+            (2, 4, 2, 0.0, 0), (3, 6, 3, 0.0, 0)]
+    hcl = kf.Fst(0, np.array([0.0, np.inf, np.inf, np.inf], np.float32), np.array([0, 2, 4, 5, 6], np.int64),
+                 np.array([a[1] for a in arcs], np.int32), np.array([a[2] for a in arcs], np.int32),
+                 np.array([a[3] for a in arcs], np.float32), np.array([a[4] for a in arcs], np.int32))
+    kf.write_lookahead_fst(os.path.join(gd, "HCLr.fst"), hcl)
+    g = kf.Fst(0, np.array([1.0, np.inf], np.float32), np.array([0, 3, 5], np.int64),
+               np.array([1, 2, 3, 0, 1], np.int32), np.array([1, 2, 3, 0, 1], np.int32),
+               np.array([1.0, 2.0, 3.0, 0.5, 0.25], np.float32), np.array([0, 0, 1, 0, 0], np.int32))
+    kf.write_const_fst(os.path.join(gd, "Gr.fst"), g)
+    return out, hcl, g
+
+
+def test_lookahead_pushing_known_answer(lib, synth_lookahead, tmp_path):
+    """Per-arc pushed weights and pushed labels of OpenFST's lookahead
+    composition (PushWeights / PushLabels filters), worked by hand:
+    * 0 -a-> 1 reaches w1, w2 at G state 0: weight log-sum(1, 2) = 0.686738,
+      the state keeps Quantize(0.686738) = 703/1024;
+    * 0 -c-> 3 reaches w3 only: w3 (3.0) is output on this arc, G advances;
+    * 1 -(w1)-> 0 matched at G 0: 1.0 - 703/1024; 1 -b-> 2 reaches w2 only:
+      pushed, 2.0 - 703/1024; the word-end arcs of pushed words output nothing;
+    * at history w3: the backoff 0.5; 0 -a-> 1 reaches w1 only there: w1
+      (0.25) pushed; 'c' is not reachable at history w3."""
+    d, hcl, g = _tiny_pair(synth_lookahead, str(tmp_path / "m"))
+    lw = np.float32(1.0 - np.log(1.0 + np.exp(-1.0)))
+    q = np.float32(703.0 / 1024.0)
+    assert np.float32(np.floor(lw * np.float32(1024) + np.float32(0.5)) / np.float32(1024)) == q
+    want = sorted([(1, 0, lw), (5, 3, np.float32(3.0)), (2, 1, np.float32(1.0) - q), (3, 2, np.float32(2.0) - q),
+                   (4, 0, np.float32(0.0)), (6, 0, np.float32(0.0)), (0, 0, np.float32(0.5)),
+                   (1, 1, np.float32(0.25)), (2, 0, np.float32(0.0))])
+    for c in (OG.compose(hcl, g, []), _cgraph(lib, d)):
+        assert c is not None and c.num_states == 6
+        got = sorted(zip(c.ilabel.tolist(), c.olabel.tolist(), c.weight.tolist()))
+        assert [(a, b) for a, b, _ in got] == [(a, b) for a, b, _ in want]
+        np.testing.assert_array_equal(np.array([w for _, _, w in got], np.float32),
+                                      np.array([w for _, _, w in want], np.float32))
+        fin = c.final[np.isfinite(c.final)]
+        assert fin.tolist() == [1.0]
+    # the unpruned composition's path weights, up to the quantization residue
+    # of each pushed weight (lw - q), as OpenFST's filter leaves them
+
+
+def test_lookahead_pushing_is_exercised(synth_lookahead):
+    """On the synthetic lookahead model both pushes happen (labels output
+    before the word-end arc, fractional pushed weights on epsilon-output
+    arcs)."""
+    hcl = kf.read_fst(os.path.join(synth_lookahead, "graph", "HCLr.fst"))
+    g = kf.read_fst(os.path.join(synth_lookahead, "graph", "Gr.fst"))
+    dis = [int(x) for x in open(os.path.join(synth_lookahead, "graph", "disambig_tid.int")).read().split()]
+    c = OG.compose(hcl, g, dis)
+    # word-end transition-ids of HCLr (the arcs carrying word labels there)
+    wend = set(int(x) for x in hcl.ilabel[hcl.olabel != 0]) - set(dis) - {0}
+    pushed = (c.olabel != 0) & ~np.isin(c.ilabel, list(wend)) & (c.ilabel != 0)
+    assert pushed.sum() > 0
+    frac = (c.olabel == 0) & (c.ilabel != 0) & (c.weight != 0) & (np.abs(c.weight) < 50)
+    assert frac.sum() > 0

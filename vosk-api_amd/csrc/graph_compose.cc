@@ -9,7 +9,9 @@
 #include <functional>
 #include <sstream>
 #include <limits>
+#include <cstring>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <utility>
 
@@ -222,6 +224,85 @@ void ConnectCanonical(const HostFst& in, HostFst* out) {
 
 }  // namespace
 
+namespace {
+// OpenFST's FastLogAccumulator<StdArc> (arc_limit 20, arc_period 10), the
+// accumulator of the LabelReachable behind the olabel_lookahead matcher
+// [O: fst/accumulator.h]: log-semiring sums in double, rounded to float per
+// step; states with at least 20 arcs keep a cumulative sum every 10 arcs.
+constexpr double kDInf = std::numeric_limits<double>::infinity();
+constexpr float kFInf = std::numeric_limits<float>::infinity();
+constexpr int kAccLimit = 20, kAccPeriod = 10;
+double LogPosExp(double x) { return x == kDInf ? 0.0 : std::log(1.0F + std::exp(-x)); }
+double LogMinusExp(double x) { return x == kDInf ? 0.0 : std::log(1.0F - std::exp(-x)); }
+float LogPlusW(float w, float v) {  // Weight LogPlus(Weight, Weight)
+  if (w == kFInf && v == kFInf) return kFInf;
+  const double f1 = w, f2 = v;
+  return f1 > f2 ? (float)(f2 - LogPosExp(f1 - f2)) : (float)(f1 - LogPosExp(f2 - f1));
+}
+double LogPlusD(double f1, float v) {  // double LogPlus(double, Weight) (Init)
+  const double f2 = v;
+  if (f1 == kDInf) return f2;
+  return f1 > f2 ? f2 - LogPosExp(f1 - f2) : f1 - LogPosExp(f2 - f1);
+}
+float LogMinusW(double f1, double f2) {  // f1 < f2
+  if (f2 == kDInf) return (float)f1;
+  return (float)(f1 - LogMinusExp(f2 - f1));
+}
+// FastLogAccumulator::Sum(w, aiter, begin, end) over arc weights wt[] of a
+// state whose stored cumulative sums are sw (nullptr: fewer than 20 arcs)
+float AccSum(float sum, const float* wt, const double* sw, int64_t begin, int64_t end) {
+  int64_t ib = -1, ie = -1, sb = end, se = end;
+  if (sw) {
+    ib = begin > 0 ? (begin - 1) / kAccPeriod + 1 : 0;
+    ie = end / kAccPeriod;
+    sb = ib * kAccPeriod;
+    se = ie * kAccPeriod;
+  }
+  if (begin < sb)
+    for (int64_t p = begin, pe = std::min(sb, end); p < pe; p++) sum = LogPlusW(sum, wt[p]);
+  if (sb < se) {
+    const double f1 = sw[ie], f2 = sw[ib];
+    if (f1 < f2) sum = LogPlusW(sum, LogMinusW(f1, f2));
+  }
+  if (se < end)
+    for (int64_t p = std::max(sb, se); p < end; p++) sum = LogPlusW(sum, wt[p]);
+  return sum;
+}
+// TropicalWeight::Quantize(kDelta): the lookahead weight a filter state keeps
+float Quantize(float v) {
+  if (!std::isfinite(v)) return v;
+  const float delta = 1.0F / 1024.0F;
+  return std::floor(v / delta + 0.5F) * delta;
+}
+bool Member(const Intervals& iv, int l) {
+  auto it = std::upper_bound(iv.begin(), iv.end(), std::make_pair(l, std::numeric_limits<int>::max()));
+  return it != iv.begin() && std::prev(it)->second >= l;
+}
+}  // namespace
+
+// The composition the reference builds, ComposeFst(HCLr, G) with HCLr an
+// olabel_lookahead FST, uses OpenFST's default lookahead filter chain for
+// MATCH_OUTPUT [O: fst/lookahead-filter.h, compose.h CreateBase]:
+//   PushLabelsComposeFilter<PushWeightsComposeFilter<LookAheadComposeFilter<
+//     AltSequenceComposeFilter>>>
+// with the olabel_lookahead flags (output lookahead, weight, prefix,
+// epsilons, non-epsilon prefix).  A composed state is (HCLr state, G state,
+// alternative-sequence bit, quantized lookahead weight, pushed label):
+//  * G epsilon arcs (bit 0 only): weight g - fw, the lookahead weight reset;
+//  * HCLr output-epsilon arcs into p at G state q: LabelLookAheadMatcher::
+//    LookAheadFst over q's arcs whose labels p reaches (and q's final weight
+//    when p reaches a final state): none -> no arc; exactly one arc and no
+//    final -> that G arc is taken now (label pushing: its word is output on
+//    this arc, the G state advances, its weight is added, the state keeps
+//    the label HCLr still has to output); otherwise the arc weight becomes
+//    a + (lw - fw) with lw the log-sum of those arcs' weights (min'd with the
+//    final weight), and the state keeps Quantize(lw) (weight pushing);
+//  * HCLr word arcs matched with G arcs: a + (g - fw), lookahead weight reset;
+//  * with a pushed label L: only HCLr output-epsilon arcs whose destination
+//    reaches L (the state kept), or HCLr arcs outputting L, which become
+//    output-epsilon arcs back to the start filter state; never final;
+//  * final weight (f_HCLr - fw) + f_G.
+// Float operations follow the filters' Times / Divide order.
 void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>& disambig,
                       HostFst* out) {
   if (a.NumStates() == 0 || b.NumStates() == 0) VAMD_ERR("cannot compose an empty FST");
@@ -237,12 +318,16 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
   ComputeReach(a, &reach);
   auto t1 = std::chrono::steady_clock::now();
   // grammar side: per state the epsilon arcs in order and the non-epsilon
-  // arcs sorted by input label (stable)
+  // arcs sorted by input label (stable) -- the ilabel-sorted arc order the
+  // matcher and the accumulator see
   const int SB = b.NumStates();
   std::vector<int64_t> bsorted(b.NumArcs());
   std::vector<int64_t> beps_end(SB);  // arcs [row[s], beps_end[s]) of bsorted are epsilon
   std::vector<int> bword(b.NumArcs());
+  std::vector<float> bw(b.NumArcs());
   std::vector<char> b_has_eps(SB), b_alleps(SB);
+  std::vector<int64_t> acc_pos(SB, -1);
+  std::vector<double> acc_w;
   for (int s = 0; s < SB; s++) {
     int64_t o = b.row[s];
     for (int64_t e = b.row[s]; e < b.row[s + 1]; e++)
@@ -252,37 +337,88 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
       if (b.ilabel[e] != 0) bsorted[o++] = e;
     std::stable_sort(bsorted.begin() + beps_end[s], bsorted.begin() + b.row[s + 1],
                      [&](int64_t x, int64_t y) { return b.ilabel[x] < b.ilabel[y]; });
-    for (int64_t k = b.row[s]; k < b.row[s + 1]; k++) bword[k] = b.ilabel[bsorted[k]];
+    for (int64_t k = b.row[s]; k < b.row[s + 1]; k++) {
+      bword[k] = b.ilabel[bsorted[k]];
+      bw[k] = b.weight[bsorted[k]];
+    }
     b_has_eps[s] = beps_end[s] > b.row[s];
     b_alleps[s] = beps_end[s] == b.row[s + 1] && !std::isfinite(b.final_cost[s]);
-  }
-  // can a path from HCL state p (grammar state q, no further grammar epsilon
-  // moves) match a word q accepts, or end in a final state?
-  auto useful = [&](int p, int q) {
-    const int c = reach.comp[p];
-    if (reach.final[c] && std::isfinite(b.final_cost[q])) return true;
-    const Intervals& iv = reach.labels[c];
-    const int* wb = bword.data() + beps_end[q];
-    const int* we = bword.data() + b.row[q + 1];
-    if (iv.empty() || wb == we) return false;
-    if ((int64_t)iv.size() <= (int64_t)(we - wb)) {
-      for (const auto& r : iv) {
-        const int* it = std::lower_bound(wb, we, r.first);
-        if (it != we && *it <= r.second) return true;
-      }
-    } else {
-      for (const int* w = wb; w < we; w++) {
-        auto it = std::upper_bound(iv.begin(), iv.end(), std::make_pair(*w, std::numeric_limits<int>::max()));
-        if (it != iv.begin() && std::prev(it)->second >= *w) return true;
+    if (b.row[s + 1] - b.row[s] >= kAccLimit) {  // FastLogAccumulator::Init
+      acc_pos[s] = (int64_t)acc_w.size();
+      double sum = kDInf;
+      acc_w.push_back(sum);
+      int64_t n = 0;
+      for (int64_t k = b.row[s]; k < b.row[s + 1]; k++) {
+        sum = LogPlusD(sum, bw[k]);
+        if (++n % kAccPeriod == 0) acc_w.push_back(sum);
       }
     }
-    return false;
+  }
+  // LabelLookAheadMatcher::LookAheadFst for HCLr state p (component c) at G
+  // state q: ok (some label or the final reachable), the prefix arc (index
+  // into bsorted, -1 none) and the lookahead weight
+  struct LookAhead {
+    bool ok;
+    int64_t prefix;
+    float lw;
+  };
+  auto lookahead = [&](int c, int q) {
+    const Intervals& iv = reach.labels[c];
+    const bool rfin = reach.final[c] && std::isfinite(b.final_cost[q]);
+    const int64_t r0 = b.row[q], n = b.row[q + 1] - r0;
+    const int* lab = bword.data() + r0;
+    const float* wt = bw.data() + r0;
+    // LabelReachable::Reach: per arc when the arcs are fewer than half the
+    // intervals (the final label counts as one), else per interval
+    const int64_t nint = (int64_t)iv.size() + (reach.final[c] ? 1 : 0);
+    int64_t rb = -1, re = -1;
+    float w = kFInf;
+    if (2 * n < nint) {
+      int last = -1;
+      for (int64_t k = 0; k < n; k++) {
+        if (lab[k] == last || Member(iv, lab[k])) {
+          last = lab[k];
+          if (rb < 0) rb = k;
+          re = k + 1;
+          w = LogPlusW(w, wt[k]);
+        }
+      }
+    } else {
+      const double* sw = acc_pos[q] >= 0 ? acc_w.data() + acc_pos[q] : nullptr;
+      int64_t lo = 0;
+      for (const auto& r : iv) {
+        const int64_t bl = std::lower_bound(lab + lo, lab + n, r.first) - lab;
+        const long long hi1 = (long long)r.second + 1;
+        const int64_t el = std::lower_bound(lab + bl, lab + n, hi1, [](int x, long long v) { return x < v; }) - lab;
+        lo = el;
+        if (el > bl) {
+          if (rb < 0) rb = bl;
+          re = el;
+          w = AccSum(w, wt, sw, bl, el);
+        }
+      }
+    }
+    LookAhead la{false, -1, 0.0f};
+    const bool rarc = rb >= 0;
+    bool cw = true;
+    if (rarc) {
+      if (re - rb == 1 && !rfin) {
+        la.prefix = r0 + rb;
+        cw = false;
+      } else {
+        la.lw = w;
+      }
+    }
+    if (rfin && cw) la.lw = rarc ? std::min(la.lw, b.final_cost[q]) : b.final_cost[q];
+    la.ok = rarc || rfin;
+    return la;
   };
 
   // Wide HCL states (the word-start states: one output-epsilon arc per first
   // phone) are checked per grammar word instead of per arc: the label line is
   // cut into segments, each listing the arcs whose reachable labels cover it,
-  // and each word of the grammar state marks the arcs of its segment.
+  // and each word of the grammar state marks the arcs of its segment (the
+  // arcs LookAheadFst can accept; only those are looked ahead).
   struct ArcIndex {
     std::vector<int> seg_lo;      // segment starts (ascending); segment k = [seg_lo[k], seg_lo[k+1])
     std::vector<int> seg_begin;   // [nseg + 1] into arcs
@@ -328,40 +464,69 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
   };
   std::vector<char> mark;
 
-  HostFst c;
-  c.osyms = b.osyms;
-  StateTable table;
-  std::vector<uint64_t> keys;
-  auto key_of = [](int q1, int q2, int fs) {
-    return ((uint64_t)q1 << 33) | ((uint64_t)(uint32_t)q2 << 1) | (uint64_t)fs;
+  // composed states: key = (q1 << 32 | q2 | bit << 31, fw bits << 32 | pushed label)
+  struct Key {
+    uint64_t k0, k1;
   };
-  auto id_of = [&](int q1, int q2, int fs) {
-    const uint64_t k = key_of(q1, q2, fs);
-    bool added = false;
-    const int id = table.FindOrAdd(k, (int)keys.size(), &added);
-    if (added) {
+  std::vector<Key> keys;
+  struct KeyHash {
+    size_t operator()(const std::pair<uint64_t, uint64_t>& k) const {
+      return (size_t)StateTable::Mix(k.first ^ StateTable::Mix(k.second));
+    }
+  };
+  std::unordered_map<std::pair<uint64_t, uint64_t>, int, KeyHash> table;
+  table.reserve(1 << 20);
+  constexpr int kNoLabel = -1;
+  auto id_of = [&](int q1, int q2, int sb, float fw, int fl) {
+    uint32_t fwb;
+    std::memcpy(&fwb, &fw, 4);
+    const Key k{((uint64_t)q1 << 32) | (uint32_t)q2 | ((uint64_t)sb << 31), ((uint64_t)fwb << 32) | (uint32_t)fl};
+    auto it = table.emplace(std::make_pair(k.k0, k.k1), (int)keys.size());
+    if (it.second) {
       if (keys.size() >= (size_t)std::numeric_limits<int>::max() - 1) VAMD_ERR("composed graph too large");
       keys.push_back(k);
     }
-    return id;
+    return it.first->second;
   };
-  c.start = id_of(a.start, b.start, 0);
+  HostFst c;
+  c.osyms = b.osyms;
+  c.start = id_of(a.start, b.start, 0, 0.0f, kNoLabel);
   c.row.push_back(0);
   for (size_t s = 0; s < keys.size(); s++) {
-    const int q1 = (int)(keys[s] >> 33), q2 = (int)((keys[s] >> 1) & 0xffffffffu), fs = (int)(keys[s] & 1);
+    const int q1 = (int)(keys[s].k0 >> 32), q2 = (int)(keys[s].k0 & 0x7fffffffu);
+    const int sb = (int)((keys[s].k0 >> 31) & 1);
+    const uint32_t fwb = (uint32_t)(keys[s].k1 >> 32);
+    const int fl = (int)(uint32_t)(keys[s].k1 & 0xffffffffu);
+    float fw;
+    std::memcpy(&fw, &fwb, 4);
     const float fa = a.final_cost[q1], fb = b.final_cost[q2];
-    c.final_cost.push_back(std::isfinite(fa) && std::isfinite(fb) ? fa + fb
-                                                                   : std::numeric_limits<float>::infinity());
+    c.final_cost.push_back(fl == kNoLabel && std::isfinite(fa) && std::isfinite(fb) ? (fa - fw) + fb : kFInf);
     auto push = [&](int il, int ol, float w, int dst) {
       c.ilabel.push_back(il); c.olabel.push_back(ol); c.weight.push_back(w); c.nextstate.push_back(dst);
     };
-    if (fs == 0)  // the grammar moves alone on its epsilon (backoff) arcs
+    auto in_label = [&](int64_t e) {
+      return (a.ilabel[e] > 0 && a.ilabel[e] <= max_il && is_disambig[a.ilabel[e]]) ? 0 : a.ilabel[e];
+    };
+    if (fl != kNoLabel) {  // PushedLabelFilterArc: HCLr must still output fl
+      for (int64_t e = a.row[q1]; e < a.row[q1 + 1]; e++) {
+        const int p = a.nextstate[e];
+        if (a.olabel[e] == fl) {
+          push(in_label(e), 0, a.weight[e] + 0.0f, id_of(p, q2, 0, 0.0f, kNoLabel));
+        } else if (a.olabel[e] == 0 && Member(reach.labels[reach.comp[p]], fl)) {
+          push(in_label(e), 0, a.weight[e] + 0.0f, id_of(p, q2, sb, fw, fl));
+        }
+      }
+      c.row.push_back((int64_t)c.ilabel.size());
+      continue;
+    }
+    const float nfw = 0.0f - fw;  // Divide(One, fw)
+    if (sb == 0)  // the grammar moves alone on its epsilon (backoff) arcs
       for (int64_t k = b.row[q2]; k < beps_end[q2]; k++) {
         const int64_t e = bsorted[k];
-        push(0, b.olabel[e], b.weight[e], id_of(q1, b.nextstate[e], 0));
+        push(0, b.olabel[e], 0.0f + (bw[k] + nfw), id_of(q1, b.nextstate[e], 0, 0.0f, kNoLabel));
       }
     const ArcIndex* ix = b_alleps[q2] ? nullptr : index_of(q1);
-    if (ix) {  // mark the useful output-epsilon arcs of a wide HCL state
+    if (ix) {  // mark the output-epsilon arcs of a wide HCL state the lookahead can accept
       mark.assign(a.row[q1 + 1] - a.row[q1], 0);
       if (std::isfinite(b.final_cost[q2]))
         for (int k : ix->final_arcs) mark[k] = 1;
@@ -373,20 +538,30 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
         for (int j = ix->seg_begin[sg]; j < ix->seg_begin[sg + 1]; j++) mark[ix->arcs[j]] = 1;
       }
     }
+    const int nsb = b_has_eps[q2] ? 1 : 0;
     for (int64_t e = a.row[q1]; e < a.row[q1 + 1]; e++) {
-      const int il = (a.ilabel[e] > 0 && a.ilabel[e] <= max_il && is_disambig[a.ilabel[e]]) ? 0 : a.ilabel[e];
+      const int il = in_label(e);
       const int p = a.nextstate[e];
-      if (a.olabel[e] == 0) {  // HCL moves alone
+      if (a.olabel[e] == 0) {  // HCL moves alone, looking ahead into G
         if (b_alleps[q2]) continue;
-        if (ix ? !mark[e - a.row[q1]] : !useful(p, q2)) continue;
-        push(il, 0, a.weight[e], id_of(p, q2, b_has_eps[q2] ? 1 : 0));
+        if (ix && !mark[e - a.row[q1]]) continue;
+        const LookAhead la = lookahead(reach.comp[p], q2);
+        if (!la.ok) continue;
+        if (la.prefix >= 0) {  // label pushing: the single reachable G arc now
+          const int64_t g = bsorted[la.prefix];
+          push(il, b.olabel[g], a.weight[e] + ((0.0f + nfw) + bw[la.prefix]),
+               id_of(p, b.nextstate[g], nsb, 0.0f, bword[la.prefix]));
+        } else {  // weight pushing
+          push(il, 0, a.weight[e] + (0.0f + (la.lw - fw)), id_of(p, q2, nsb, Quantize(la.lw), kNoLabel));
+        }
       } else {  // matched word
         const int* wb = bword.data() + beps_end[q2];
         const int* we = bword.data() + b.row[q2 + 1];
         const int* lo = std::lower_bound(wb, we, a.olabel[e]);
         for (const int* it = lo; it != we && *it == a.olabel[e]; it++) {
-          const int64_t g = bsorted[it - bword.data()];
-          push(il, b.olabel[g], a.weight[e] + b.weight[g], id_of(p, b.nextstate[g], 0));
+          const int64_t k = it - bword.data();
+          const int64_t g = bsorted[k];
+          push(il, b.olabel[g], a.weight[e] + (bw[k] + nfw), id_of(p, b.nextstate[g], 0, 0.0f, kNoLabel));
         }
       }
     }

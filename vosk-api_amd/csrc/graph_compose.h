@@ -8,27 +8,34 @@
 // composes HCLr with a bigram estimated from the phrase list
 // (src/recognizer.cc:49-108, src/language_model.cc).  The GPU decoder walks a
 // CSR graph in HBM, so the composition is expanded once on the host into a
-// static graph with the same paths, labels and path weights:
+// static graph with the states and arcs of the reference's lazy one.
+// ComposeFst with an olabel_lookahead first FST runs OpenFST's default
+// MATCH_OUTPUT lookahead filter chain [O: compose.h CreateBase,
+// lookahead-filter.h], restated in graph_compose.cc:
 //
-//  * composition filter: OpenFST's alternative sequence filter (the one the
-//    lookahead composition builds on): the grammar's epsilon (backoff) arcs
-//    are taken before HCLr's output-epsilon arcs, never after them within one
-//    word;
-//  * lookahead: an HCLr move that cannot reach any output label the grammar
-//    state accepts (nor a final state when the grammar state is final) is not
-//    expanded; the reachable label sets are computed per strongly connected
-//    component of HCLr's output-epsilon subgraph, as sorted interval lists
-//    (the relabeling of lookahead graphs makes them a few intervals each);
+//  * alternative sequence filter: the grammar's epsilon (backoff) arcs are
+//    taken before HCLr's output-epsilon arcs, never after them within a word;
+//  * label lookahead: an HCLr output-epsilon move is expanded only if some
+//    output label reachable from its destination is on an arc of the grammar
+//    state (or a final state is reachable and the grammar state is final);
+//    reachable label sets per strongly connected component of HCLr's
+//    output-epsilon subgraph, as sorted interval lists;
+//  * weight pushing: such a move carries the log-sum of the reachable grammar
+//    arcs' weights (FastLogAccumulator) minus the weight pushed so far, which
+//    the state keeps quantized to 1/1024; word and backoff arcs subtract it;
+//  * label pushing: when exactly one grammar arc is reachable (and no final),
+//    that arc is taken on the move itself (its word output early, the grammar
+//    state advanced), and the state keeps the label HCLr must still output;
 //  * disambiguation transition-ids (disambig_tid.int) become epsilon;
 //  * the result is trimmed (states that reach no final state removed) and
 //    renumbered in breadth-first order from the start state over each
 //    state's emitting arcs then epsilon arcs (the canonical order
-//    tests/oracle_graph.py reproduces from an unpruned expansion).
+//    tests/oracle_graph.py reproduces).
 //
-// The reference's lookahead filter additionally pushes grammar weights and
-// output labels towards the word start (weight / label pushing): paths and
-// path weights are identical, intermediate token costs are not, so beam
-// pruning can differ slightly.
+// Not reproduced: the composed state numbering (OpenFST numbers states as
+// the decoder first visits them; Kaldi's HashList order depends on it) and
+// the exact interval count of the final label in OpenFST's reachability data
+// (it only selects between two summation orders of the lookahead weight).
 #pragma once
 #include <string>
 #include <vector>

@@ -800,6 +800,12 @@ PRESETS = {
     # BASELINE config 4's per-GPU share: a multi-million-state static HCLG
     "bigram_2m": dict(seed=21, vocab=20000, num_pdfs=2000, llh_std=1.5, graph="bigram",
                       graph_opts=dict(num_hist=2000, fut=300)),
+    # BASELINE config 4 stand-in several times the 2.4 M-state graph (the
+    # static HCLG of vosk-model-en-us-0.22 is larger than any graph the
+    # tests can build in seconds; what matters is that per-stream decoder
+    # state does not grow with the graph)
+    "bigram_8m": dict(seed=23, vocab=20000, num_pdfs=2000, llh_std=1.5, graph="bigram",
+                      graph_opts=dict(num_hist=6400, fut=300)),
     # vosk-model-small-en-us scale (BASELINE config 3): 20 k-word HCLr + a
     # ~29 k-history trigram Gr, expanded at load to ~1.9 M states
     "la_small_en_us": dict(seed=11, vocab=20000, num_pdfs=2000, llh_std=1.5, graph="lookahead",
