@@ -17,7 +17,7 @@ Model: no Vosk model is available offline, so a seeded synthetic model in
 the real Kaldi/OpenFST formats stands in for vosk-model-small-en-us: the
 recipe's TDNN-F topology (training/local/chain/run_tdnn.sh:98-129, random-init
 weights, BatchNorm calibrated on test.wav) with a 20 k-word lookahead graph
-(HCLr + a ~29 k-history trigram Gr, expanded at load to ~1.9 M states).
+(HCLr + a ~29 k-history trigram Gr, expanded at load to ~275 k states).
 Streams are test.wav tiled, shifted, gained and noised per BASELINE.md.
 
 Secondary keys: "engine_only" (the GPU engine stepped directly on
@@ -191,6 +191,8 @@ def main():
     ap.add_argument("--no-single-stream", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-lattice", action="store_true")
+    ap.add_argument("--order", choices=("parallel", "kaldi"), default="parallel",
+                    help="engine workloads: token-passing order (parallel = the BatchModel lanes' form)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline: seconds per stream")
     ap.add_argument("--lanes", default=None,
                     help="in-library lanes mode (one process, no torchrun): the BatchModel runs one lane "
@@ -420,7 +422,7 @@ def run_engine(args, model, dist, rank, world, base, steps):
     pipe = not args.no_pipeline
     warm = 5
     e = ve.Engine(model, frames_per_chunk=51, max_streams=S, stats=True, time_kernels=True,
-                  pipeline=pipe, lattice=not args.no_lattice)
+                  pipeline=pipe, lattice=not args.no_lattice, order=args.order)
     chunk = e.fpc * 160
     e.set_step_samples(chunk)
     total_steps = warm + steps + 2
@@ -565,7 +567,8 @@ def run_dynamic(args, model, dist, rank, world):
     from vosk import engine as ve
     from shard import AdmissionController
     S = args.streams
-    e = ve.Engine(model, frames_per_chunk=51, max_streams=S, stats=True, lattice=not args.no_lattice)
+    e = ve.Engine(model, frames_per_chunk=51, max_streams=S, stats=True, lattice=not args.no_lattice,
+                  order=args.order)
     chunk = e.fpc * 160
     e.set_step_samples(chunk)
     base = load_wave()

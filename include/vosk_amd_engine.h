@@ -87,7 +87,9 @@ int vamd_device_count(void);
  *        4 = HIP-event timing of each stage on the engine's stream,
  *        8 = two-stream pipeline (decoder of step i-1 beside the nnet of step
  *            i; decoder results lag one step, vamd_engine_flush drains),
- *       16 = lattice generation (vamd_stream_lattice). */
+ *       16 = lattice generation (vamd_stream_lattice),
+ *       32 = order-independent token passing (the BatchModel lanes' form)
+ *            instead of Kaldi's sequential order (VOSK_AMD_DEC_ORDER overrides). */
 VamdEngine *vamd_engine_new(const char *model_dir, int frames_per_chunk, int max_streams,
                             int flags);
 void vamd_engine_free(VamdEngine *e);
@@ -167,7 +169,7 @@ int vamd_engine_decoder_totals(VamdEngine *e, long long *out6);
  * exp_items, exp_winners, eps, commit_toks, commit_links] (s_memtime clocks;
  * the full list is vosk/engine.py Engine.PHASES) */
 int vamd_engine_decoder_phases(VamdEngine *e, long long *out8);
-/* all decoder phase counters: writes min(cap, N) values, returns N (24) */
+/* all decoder phase counters: writes min(cap, N) values, returns N (28) */
 int vamd_engine_decoder_phases_n(VamdEngine *e, long long *out, int cap);
 /* the N counters per stream slot: out[max_streams][N] */
 int vamd_engine_decoder_phases_per_stream(VamdEngine *e, long long *out);

@@ -993,6 +993,58 @@ static void lat_frame(const orc_graph* g, orc_dec_result* r, int k, const int* s
       if (co[i] + g->weight[a] < cutoff) lat_link(r, k, st[i], (int)a, 0.0f);
 }
 
+/* best path of the current frame (order-independent form): the lowest cost
+   (with final costs if any token is final and use_final), ties to the lowest
+   state; arcs in forward order into path[0 .. min(*len, cap)) */
+static int od_best_path(const orc_graph* g, const int* cur_state, const float* cur_cost, const int* cur_idx,
+                        int ncur, const orc_link* arena, int use_final, int* path, long long cap, int* len,
+                        float* frc, float* end_tot, int* end_state) {
+  int end = -1;
+  float end_cost = INFINITY, best_nofinal = INFINITY, best_final = INFINITY;
+  for (int i = 0; i < ncur; i++) {
+    float c = cur_cost[i];
+    if (c < best_nofinal) best_nofinal = c;
+    float fc = g->final_cost[cur_state[i]];
+    if (fc != INFINITY) {
+      float cf = c + fc;
+      if (cf < best_final) best_final = cf;
+    }
+  }
+  int any_final = best_final != INFINITY;
+  for (int i = 0; i < ncur; i++) {
+    float c = (use_final && any_final) ? cur_cost[i] + g->final_cost[cur_state[i]] : cur_cost[i];
+    if (c < end_cost || (c == end_cost && end >= 0 && cur_state[i] < cur_state[end])) {
+      end_cost = c;
+      end = i;
+    }
+  }
+  *frc = any_final ? best_final - best_nofinal : INFINITY;
+  *len = 0;
+  if (end >= 0) {
+    *end_state = cur_state[end];
+    *end_tot = end_cost;
+    int n = 0;
+    for (int k = cur_idx[end]; k >= 0 && arena[k].arc >= 0; k = arena[k].prev) n++;
+    *len = n;
+    int k = cur_idx[end];
+    for (int j = n - 1; j >= 0; j--) {
+      if (j < cap) path[j] = arena[k].arc;
+      k = arena[k].prev;
+    }
+  }
+  return end;
+}
+
+static void od_probe(const orc_graph* g, const int* cs, const float* cc, const int* ci, int ncur,
+                     const orc_link* arena, orc_dec_result* r, int i) {
+  const long long off = r->probe_off[i];
+  int len = 0, es = 0;
+  float tot = 0.0f;
+  const long long room = r->probe_path_cap - off > 0 ? r->probe_path_cap - off : 0;
+  od_best_path(g, cs, cc, ci, ncur, arena, 0, r->probe_path + off, room, &len, &r->probe_frc[i], &tot, &es);
+  r->probe_off[i + 1] = off + len;
+}
+
 int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const orc_dec_opts* o,
                int use_final, orc_dec_result* r) {
   const int S = g->num_states;
@@ -1028,6 +1080,9 @@ int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const or
     for (int i = 0; i < ncur; i++) if (cur_cost[i] < b) b = cur_cost[i];
     r->best[0] = b;
   }
+  int pi = 0;
+  if (r->nprobe > 0) r->probe_off[0] = 0;
+  for (; pi < r->nprobe && r->probe_frames[pi] <= 0; pi++) od_probe(g, cur_state, cur_cost, cur_idx, ncur, d.arena, r, pi);
 
   for (int f = 0; f < F; f++) {
     const float* L = llh + (size_t)f * stride;
@@ -1111,44 +1166,19 @@ int orc_decode(const orc_graph* g, const float* llh, int F, int stride, const or
       for (int i = 0; i < ncur; i++) if (cur_cost[i] < b) b = cur_cost[i];
       r->best[f + 1] = b;
     }
+    for (; pi < r->nprobe && r->probe_frames[pi] <= f + 1; pi++)
+      od_probe(g, cur_state, cur_cost, cur_idx, ncur, d.arena, r, pi);
     if (ncur == 0) break;
   }
 
+  for (; pi < r->nprobe; pi++) {  /* probes past the decoded frames: nothing */
+    r->probe_off[pi + 1] = r->probe_off[pi];
+    r->probe_frc[pi] = INFINITY;
+  }
   /* ---- best path end: with final costs if any token is final */
-  int end = -1;
-  float end_cost = INFINITY, best_nofinal = INFINITY, best_final = INFINITY;
-  for (int i = 0; i < ncur; i++) {
-    float c = cur_cost[i];
-    if (c < best_nofinal) best_nofinal = c;
-    float fc = g->final_cost[cur_state[i]];
-    if (fc != INFINITY) {
-      float cf = c + fc;
-      if (cf < best_final) best_final = cf;
-    }
-  }
-  int any_final = best_final != INFINITY;
-  for (int i = 0; i < ncur; i++) {
-    float c = (use_final && any_final) ? cur_cost[i] + g->final_cost[cur_state[i]] : cur_cost[i];
-    if (c < end_cost || (c == end_cost && end >= 0 && cur_state[i] < cur_state[end])) {
-      end_cost = c;
-      end = i;
-    }
-  }
-  r->final_relative_cost = any_final ? best_final - best_nofinal : INFINITY;
-  r->path_len = 0;
-  if (end >= 0) {
-    r->end_state = cur_state[end];
-    r->best_tot = end_cost;
-    r->best_cost = (double)end_cost - offsets_sum;
-    int n = 0;
-    for (int k = cur_idx[end]; k >= 0 && d.arena[k].arc >= 0; k = d.arena[k].prev) n++;
-    r->path_len = n;
-    int k = cur_idx[end];
-    for (int j = n - 1; j >= 0; j--) {
-      if (j < r->path_cap) r->path[j] = d.arena[k].arc;
-      k = d.arena[k].prev;
-    }
-  }
+  const int end = od_best_path(g, cur_state, cur_cost, cur_idx, ncur, d.arena, use_final, r->path, r->path_cap,
+                               &r->path_len, &r->final_relative_cost, &r->best_tot, &r->end_state);
+  if (end >= 0) r->best_cost = (double)r->best_tot - offsets_sum;
   free(d.key); free(d.prevtok); free(d.pos); free(d.inq); free(d.toks); free(d.arena);
   free(cur_state); free(cur_cost); free(cur_idx); free(tmp);
   return end >= 0 ? 0 : -1;

@@ -158,7 +158,8 @@ def synth_bigram_8m():
 @pytest.fixture(scope="session")
 def synth_la_small_en_us():
     """vosk-model-small-en-us scale lookahead model (20 k-word HCLr + a
-    29 k-history trigram Gr; ~1.9 M states once expanded at load)."""
+    29 k-history trigram Gr; ~275 k states once expanded at load with
+    OpenFST's weight and label pushing)."""
     return _make_preset("la_small_en_us")
 
 

@@ -65,10 +65,11 @@ def rules_fire(rules, frames, trailing_sil, shift, final_relative_cost):
     return False
 
 
-def batch_segments(oracle, wave, llh, right_context, priming, spc=8160):
+def batch_segments(oracle, wave, llh, right_context, priming, spc=8160, kaldi=False):
     """Decoder segments [(first frame, end frame)] of one BatchRecognizer
     stream fed `wave` and finished; llh = the stream's log-likelihood rows
-    (whole-stream, the batch chunking)."""
+    (whole-stream, the batch chunking); kaldi: the decoder order (the batch
+    lanes' default is the order-independent form)."""
     from oracle_py import mfcc_num_frames
     rules, sil = endpoint_config(oracle.model_conf)
     shift = F32(F32(0.01) * F32(oracle.fss))
@@ -90,7 +91,7 @@ def batch_segments(oracle, wave, llh, right_context, priming, spc=8160):
         frames = out_ready - seg0
         if frames <= 0 or F32(frames) * shift < min_len:
             continue
-        r = oracle.decode_llh(llh[seg0:out_ready], use_final=False)
+        r = oracle.decode_llh(llh[seg0:out_ready], use_final=False, kaldi=kaldi)
         ts = trailing_silence(r["path"], g.ilabel, oracle.tm.tid2phone, sil)
         if rules_fire(rules, frames, ts, shift, r["final_relative_cost"]):
             segs.append((seg0, out_ready))
@@ -121,7 +122,7 @@ def _chunk_checks(oracle, N, right_context, priming, spc):
     return checks, -(-T // fss)
 
 
-def batch_segments_fast(oracle, wave, llh, right_context, priming, spc=8160):
+def batch_segments_fast(oracle, wave, llh, right_context, priming, spc=8160, kaldi=False):
     """batch_segments with one decoding pass per segment: the segment's
     decoder is probed at every later chunk check (orc_decode_kaldi endpoint
     probes: the state after n frames does not depend on the frames after
@@ -140,7 +141,7 @@ def batch_segments_fast(oracle, wave, llh, right_context, priming, spc=8160):
             break
         last = max(x for _, x in cand)
         r = g.decode(llh[seg0:last], oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
-                     use_final=False, kaldi=True, probes=[x - seg0 for _, x in cand])
+                     use_final=False, kaldi=kaldi, probes=[x - seg0 for _, x in cand])
         fired = None
         for (i, x), (path, frc) in zip(cand, r["probes"]):
             ts = trailing_silence(path, g.ilabel, oracle.tm.tid2phone, sil)

@@ -666,14 +666,15 @@ def word_align(W, Fi, tables):
     return A, F
 
 
-def results(oracle, llh, use_final=True, graph_scale=0.9, nbest_n=0, rescore=None, hash_size=0):
+def results(oracle, llh, use_final=True, graph_scale=0.9, nbest_n=0, rescore=None, hash_size=0, kaldi=None):
     """The reference's result chain over the oracle decoder's lattice of
     `llh`: prune, determinize, graph scale, word alignment (when the model has
     word_boundary.int), then MBR (and n-best).  hash_size: the decoder's
-    HashList size at the segment start (Kaldi order; 0 = a new decoder)."""
+    HashList size at the segment start (Kaldi order; 0 = a new decoder).
+    kaldi: the decoder order (None: oracle_py.decoder_order())."""
     import os
     r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
-                            use_final, lattice=True, hash_size=hash_size)
+                            use_final, lattice=True, hash_size=hash_size, kaldi=kaldi)
     W, Fi = determinize(prune(raw_from_oracle(r, oracle.graph, use_final), 6.0),
                         oracle.graph.ilabel, oracle.graph.olabel)
     if rescore is not None:  # (W, Fi) -> rescored (W, Fi) or None (unchanged)

@@ -530,11 +530,12 @@ class OrcGraph(C.Structure):
                 ("tid2pdf", C.c_void_p)]
 
 
-def decoder_order():
+def decoder_order(batch=False):
     """The token-passing semantics the GPU decoder runs (VOSK_AMD_DEC_ORDER,
-    as the engine reads it): "kaldi" (default, LatticeFasterDecoder's
-    sequential order) or "parallel" (the order-independent form)."""
-    v = os.environ.get("VOSK_AMD_DEC_ORDER", "kaldi").strip().lower()
+    as the engine reads it): "kaldi" (LatticeFasterDecoder's sequential
+    order: engines and KaldiRecognizers by default) or "parallel" (the
+    order-independent form: BatchModel lanes by default, batch=True)."""
+    v = os.environ.get("VOSK_AMD_DEC_ORDER", "parallel" if batch else "kaldi").strip().lower()
     return "parallel" if v in ("parallel", "0", "order-independent") else "kaldi"
 
 
@@ -592,7 +593,7 @@ class OracleGraph:
         VOSK_AMD_DEC_ORDER=parallel mode); None: as the environment selects
         (decoder_order()).  hash_size: the Kaldi HashList size the decoder
         starts with (0: a new decoder); out["hash_size"] is its size at the end.
-        probes (Kaldi order only): ascending frame counts; out["probes"] is a
+        probes: ascending frame counts; out["probes"] is a
         list of (path without final costs, final relative cost) after each,
         from the same single pass (the endpoint checks of a segment)."""
         if kaldi is None:
@@ -622,7 +623,6 @@ class OracleGraph:
             res.lat_link_cap = lcap
             res.lat_cost_offset = lat["cost_offset"].ctypes.data
         if probes is not None:
-            assert kaldi, "endpoint probes: Kaldi order only"
             pf = np.ascontiguousarray(probes, np.int32)
             assert np.all(np.diff(pf) >= 0)
             pcap = int(4 * pf.astype(np.int64).clip(0).sum() + 64)
@@ -750,9 +750,9 @@ class OracleModel:
         ivt, t0 = self._ivec_of_time(feats.shape[0], len(iv))
         return self.net.forward(feats, iv, ivt, t0)
 
-    def decode_llh(self, llh, use_final=True, hash_size=0):
+    def decode_llh(self, llh, use_final=True, hash_size=0, kaldi=None):
         return self.graph.decode(llh, self.beam, self.max_active, self.min_active,
-                                 self.beam_delta, use_final, hash_size=hash_size)
+                                 self.beam_delta, use_final, hash_size=hash_size, kaldi=kaldi)
 
     def online(self, wave, chunk=None, rate=16000, silence_weighting=True, endpoints=False):
         """The single-stream Recognizer's online flow (src/recognizer.cc:297-

@@ -30,9 +30,9 @@ def _oracle_mbr(oracle, wave, chunk):
     return OL.results(oracle, oracle.online(wave, chunk=chunk)["llh"])["mbr"]
 
 
-def _oracle_mbr_text(oracle, wave):
+def _oracle_mbr_text(oracle, wave, batch=False):
     import oracle_lattice as OL
-    mb = OL.results(oracle, oracle.loglikes(wave))["mbr"]
+    mb = OL.results(oracle, oracle.loglikes(wave), kaldi=oracle_py.decoder_order(batch) == "kaldi")["mbr"]
     return " ".join(oracle.words[w] for w in mb["words"])
 
 
@@ -159,7 +159,7 @@ def test_batch_recognizer_matches_oracle(vosk_mod, synth_model_noep, test_wave, 
             texts[i] = (texts[i] + " " + json.loads(res)["text"]).strip()
         assert recs[i].GetPendingChunks() == 0
         # PushLattice: the MBR words of the stream's lattice (batch_recognizer.cc:43-107)
-        assert texts[i] == _oracle_mbr_text(oracle, waves[i]), i
+        assert texts[i] == _oracle_mbr_text(oracle, waves[i], batch=True), i
 
 
 def test_alternatives_and_nlsml_from_lattice(vosk_mod, synth_model_noep, test_wave):

@@ -39,10 +39,11 @@ def expected(synth_model_ep, test_wave):
     out = []
     for w in waves:
         llh = o.loglikes(w)
-        segs = OE.batch_segments(o, w, llh, info["right_context"], info["priming"])
+        kaldi = oracle_py.decoder_order(batch=True) == "kaldi"
+        segs = OE.batch_segments_fast(o, w, llh, info["right_context"], info["priming"], kaldi=kaldi)
         res = []
         for s0, s1 in segs:
-            mb = OL.results(o, llh[s0:s1])["mbr"]
+            mb = OL.results(o, llh[s0:s1], kaldi=kaldi)["mbr"]
             res.append(dict(text=" ".join(o.words[x] for x in mb["words"]), start=s0 * 0.03,
                             times=[(np.floor(a + 0.5) * 0.03, np.floor(b + 0.5) * 0.03) for a, b in mb["times"]]))
         out.append(res)

@@ -8,7 +8,7 @@ decoded together, with max-active engaged, on
 
 * the flat synthetic model (random nnet: flat scores, thousands of tokens),
   max-active lowered to 1500 so it binds in most frames, and
-* the vosk-model-small-en-us-scale lookahead model (1.9 M-state expansion,
+* the vosk-model-small-en-us-scale lookahead model (275 k-state expansion,
   beam 13 / max-active 7000).
 
 The order-independent form (VOSK_AMD_DEC_ORDER=parallel) stays available and

@@ -3,7 +3,8 @@ A10/A11): 64 streams decoded together through the pipelined engine with
 lattices (and PruneActiveTokens) on
 
 * a 2.4 M-state static HCLG (config 4's per-GPU share of a large model), and
-* the ~1.9 M-state static expansion of a vosk-model-small-en-us-scale
+* the ~275 k-state static expansion (label pushing merges histories) of a
+  vosk-model-small-en-us-scale
   lookahead model (config 3's model),
 
 both with flat enough scores that max-active 7000 engages (the oracle sees
@@ -79,7 +80,7 @@ def test_static_hclg_2m_states_64_streams(synth_bigram_2m, test_wave):
 
 def test_lookahead_expansion_64_streams(synth_la_small_en_us, test_wave, tmp_path):
     odir, S = _expanded_model(synth_la_small_en_us, str(tmp_path / "la_hclg"))
-    assert S > 1_000_000
+    assert S > 200_000
     waves, paths = _batch_decode(synth_la_small_en_us, test_wave)
     ref, max_active = _oracle_paths(odir, waves)
     for k in range(NSTREAMS):

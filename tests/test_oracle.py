@@ -121,7 +121,8 @@ def test_recognize_deterministic(oracle, test_wave):
     assert len(a["words"]) > 0
 
 
-def test_batch_segments_fast_equals_per_chunk_decodes(synth_model_ep, test_wave):
+@pytest.mark.parametrize("kaldi", [False, True], ids=["parallel", "kaldi"])
+def test_batch_segments_fast_equals_per_chunk_decodes(synth_model_ep, test_wave, kaldi):
     """The one-pass segmentation (endpoint probes inside one decode per
     segment) equals the per-chunk re-decodes it replaces (CPU)."""
     import oracle_endpoint as OE
@@ -133,19 +134,20 @@ def test_batch_segments_fast_equals_per_chunk_decodes(synth_model_ep, test_wave)
     for i in range(2):
         w = perturbed_stream(test_wave, 900 + i, seconds=9.0 + 0.7 * i)
         llh = o.loglikes(w)
-        a = OE.batch_segments(o, w, llh, info["right_context"], info["priming"])
-        b = OE.batch_segments_fast(o, w, llh, info["right_context"], info["priming"])
+        a = OE.batch_segments(o, w, llh, info["right_context"], info["priming"], kaldi=kaldi)
+        b = OE.batch_segments_fast(o, w, llh, info["right_context"], info["priming"], kaldi=kaldi)
         assert a == b
         nseg += len(a)
     assert nseg >= 4  # the rules fire
 
 
-def test_decoder_probes_equal_prefix_decodes(oracle, test_wave):
+@pytest.mark.parametrize("kaldi", [False, True], ids=["parallel", "kaldi"])
+def test_decoder_probes_equal_prefix_decodes(oracle, test_wave, kaldi):
     llh = oracle.loglikes(test_wave[:16000 * 3])
     g = oracle.graph
     probes = [0, 1, 17, 50, len(llh)]
-    r = g.decode(llh, use_final=False, kaldi=True, probes=probes)
+    r = g.decode(llh, use_final=False, kaldi=kaldi, probes=probes)
     for n, (path, frc) in zip(probes, r["probes"]):
-        ref = g.decode(llh[:n], use_final=False, kaldi=True)
+        ref = g.decode(llh[:n], use_final=False, kaldi=kaldi)
         np.testing.assert_array_equal(path, ref["path"])
         assert frc == ref["final_relative_cost"] or (math.isinf(frc) and math.isinf(ref["final_relative_cost"]))

@@ -878,13 +878,74 @@ __device__ __forceinline__ int kaldi_excl_sum(DecShared& sh, int v, int par, int
   return off + incl - v;
 }
 
+// the epsilon queue's HBM member records (kaldi_nonemitting), ints per record
+constexpr int kKMRec = 8;
+
+// Creation ranks of the emitting pass's new tokens (deferred form): each
+// created slot holds the index of its first accepted relaxation (hst /
+// stamp); its creation index is that item's rank among all such items -- a
+// bitmap over the pass's items and the popcount prefix sums of its words
+// (bits / pre: nw = ceil(nitems / 32) words each, LDS or HBM).  Returns the
+// number of created tokens.
+template <typename BitsT, typename PreT>
+__device__ __forceinline__ int kaldi_rank_creators(const DecArgs& a, DecShared& sh, const FrameLds& t,
+                                                   const HbmTab& T, int slot, int nitems, BitsT* bits, PreT* pre) {
+  int* KO = a.kord + (long long)slot * a.kord_cap;
+  const int nw = (nitems + 31) >> 5;
+  for (int w = threadIdx.x; w < nw; w += DT) bits[w] = 0u;
+  vm_drain();
+  __syncthreads();
+  const int nl = sh.n_new_l, ng = sh.n_new_g < a.max_tok ? sh.n_new_g : a.max_tok;
+  for (int j = threadIdx.x; j < nl + ng; j += DT) {
+    const int v = j < nl ? (int)t.nl[j] : ~AG_LD(&T.list[j - nl]);
+    const int it = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+    if (it >= 0 && it < nitems) atomicOr(&bits[it >> 5], 1u << (it & 31));
+  }
+  vm_drain();
+  __syncthreads();
+  int run = 0, par = 0;
+  for (int w0 = 0; w0 < nw; w0 += DT) {
+    const int w = w0 + threadIdx.x;
+    const int c = w < nw ? __popc(bits[w]) : 0;
+    int tot;
+    const int ex = run + kaldi_excl_sum(sh, c, par, &tot);
+    if (w < nw) pre[w] = ex;
+    run += tot;
+    par ^= 1;
+  }
+  vm_drain();
+  __syncthreads();
+  for (int j = threadIdx.x; j < nl + ng; j += DT) {
+    const int v = j < nl ? (int)t.nl[j] : ~AG_LD(&T.list[j - nl]);
+    const int it = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+    if (it < 0 || it >= nitems) {
+      sh.bad |= 1;
+      continue;
+    }
+    const int rk = pre[it >> 5] + __popc(bits[it >> 5] & ((1u << (it & 31)) - 1u));
+    if (rk < a.kord_cap) {
+      if (v >= 0) t.hst[v] = rk;
+      else AG_ST(&T.stamp[~v], rk);
+      AG_ST(&KO[rk], v);
+    } else {
+      sh.bad |= 1;
+    }
+  }
+  vm_drain();
+  __syncthreads();
+  return run;
+}
+
 // ProcessEmitting in list order (see above); returns next_cutoff.  The
 // created tokens get creation indices [0, *ncreated) (kord: index -> slot).
+// defer: backpointers are resolved at commit from the link records and the
+// creation ranks after the pass (one barrier per sub-round, the running
+// cutoff's); otherwise both are settled per sub-round.
 __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShared& sh, const FrameLds& t,
                                                        const HbmTab& T, const DecPtrs& p, const TokView& tv,
                                                        int ntok, float cutoff, float cost_offset, const float* Lp,
                                                        float seed, float adaptive, int* examined, const DecSlot& st,
-                                                       int slot, int* ncreated, Prof& pr) {
+                                                       int slot, int* ncreated, bool defer, float* Lbuf, Prof& pr) {
   const bool lat = a.links != nullptr;
   int* KO = a.kord + (long long)slot * a.kord_cap;
   if (threadIdx.x == 0) sh.kcar[0] = seed;  // read after the next barrier
@@ -955,6 +1016,8 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
                     sv, false);
       }
       pr.mark(22);
+      par ^= 1;
+      if (defer) continue;
       vm_drain();  // the relaxations' atomics (keys, creation indices) are complete at the barrier
       __syncthreads();
       // each slot's winner writes its backpointer; its creator (the slot's
@@ -977,16 +1040,40 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
       }
       vm_drain();
       nc += ncr;
-      par ^= 1;
       pr.mark(4);
     }
     ibase += total;
     __syncthreads();
     pr.mark(2);
   }
+  const float next_cutoff = sh.kcar[par];
+  if (defer) {
+    vm_drain();
+    __syncthreads();
+    // the item bitmap and its prefix sums in the staged log-likelihood row
+    // (no longer read in this frame) when they fit, else in the stream's
+    // epsilon-queue scratch (unused until the queue runs)
+    if (ibase <= 32 * (kLlhLds / 2)) {
+      unsigned* bits = reinterpret_cast<unsigned*>(Lbuf);
+      nc = kaldi_rank_creators(a, sh, t, T, slot, ibase, bits, reinterpret_cast<int*>(Lbuf) + kLlhLds / 2);
+    } else {
+      int* KM = a.kmem + (long long)slot * a.kord_cap * kKMRec;
+      const long long room = (long long)a.kord_cap * kKMRec;
+      const int nw = (ibase + 31) >> 5;
+      if (2LL * nw <= room) {
+        nc = kaldi_rank_creators(a, sh, t, T, slot, ibase, reinterpret_cast<unsigned*>(KM), KM + nw);
+      } else {
+        if (threadIdx.x == 0) sh.bad |= 1;
+        __syncthreads();
+        nc = 0;
+      }
+    }
+    pr.mark(4);
+  }
   __syncthreads();
+  if (nc > a.kord_cap && threadIdx.x == 0) sh.bad |= 1;
   *ncreated = nc < a.kord_cap ? nc : a.kord_cap;
-  return sh.kcar[par];
+  return next_cutoff;
 }
 
 // LDS views for Kaldi's epsilon queue (kaldi_nonemitting): regions no other
@@ -1008,7 +1095,6 @@ struct KaldiLds {
   int2* adj;   // [kKE] (destination token, arc weight bits)
 };
 // member record in HBM past kKM: {slot, cost bits, offset, count, creation index, order}
-constexpr int kKMRec = 8;
 enum { kMSlot = 0, kMCost = 1, kMOff = 2, kMCnt = 3, kMC = 4, kMOrd = 5 };
 __device__ __forceinline__ int* km_lds(const KaldiLds& K, int i, int f) {
   switch (f) {
@@ -1211,6 +1297,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
       }
     }
   }
+  pr.mark(24);
   // the initial queue in list order (rank by counting: it is short)
   for (int q = threadIdx.x; q < n0; q += DT) {
     auto key = [&](int r) -> unsigned long long {
@@ -1229,6 +1316,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   }
   vm_drain();
   __syncthreads();
+  pr.mark(25);
   // the LIFO queue (pop_back), one thread, over the staged tokens: LDS only
   // when everything fits (the common case), else through the HBM records
   int adj_n = 0;
@@ -1401,6 +1489,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   if (threadIdx.x == 0 && sh.kn0 != n_eps) sh.bad |= 1;  // the queue must create exactly the closure's tokens
   vm_drain();
   __syncthreads();
+  pr.mark(26);
   // the created tokens' creation indices [ne, ne + n_eps) in the queue's order, and their buckets
   for (int i = threadIdx.x; i < nm; i += DT) {
     if (km_get(K, KM, i, kMC) >= 0) continue;
@@ -1417,7 +1506,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   }
   vm_drain();
   __syncthreads();
-  pr.mark(23);  // (Kaldi order: the queue replay in the "exp_links" slot)
+  pr.mark(27);
   return ne + n_eps;
 }
 
@@ -2346,7 +2435,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     pr.mark(1);
     const float seed = sh.seed;
     int examined = 0;
-    const bool defer = !a.kaldi && a.links != nullptr && a.link_cap - st.links_used >= kDeferHeadroom;
+    const bool defer = a.links != nullptr && a.link_cap - st.links_used >= kDeferHeadroom;
     float next_cutoff, new_best;
     // one emitting pass relaxing below the seed bound (a superset), then the
     // epsilon closure; tokens whose best cost is not below the final
@@ -2357,7 +2446,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     if (a.kaldi) {
       int nc = 0;
       next_cutoff = expand_emitting_kaldi(a, sh, t, T, p, tv, ntok, cutoff, cost_offset, Lp, seed, adaptive,
-                                          &examined, st, slot, &nc, pr);
+                                          &examined, st, slot, &nc, defer, L, pr);
       pr.count(11, sh.n_new_g);
       kaldi_nonemitting(a, sh, t, T, p, st, K, slot, st.khash, next_cutoff, nc, &arcs_eps, pr);
     } else if (seed != __int_as_float(0x7f800000)) {

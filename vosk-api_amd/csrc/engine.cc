@@ -830,6 +830,13 @@ void Engine::FreeSlot(int slot) {
   slots_.at(slot).used = false;
 }
 
+int Engine::SlotsInUse() {
+  std::lock_guard<std::mutex> lk(mu_);
+  int n = 0;
+  for (const SlotHost& h : slots_) n += h.used ? 1 : 0;
+  return n;
+}
+
 void Engine::ResetPipeline(int slot) {
   std::lock_guard<std::mutex> lk(mu_);
   DEVICE_GUARD();

@@ -97,8 +97,10 @@ struct EngineConfig {
   int lattice_frames = 1 << 14;       // frames per decoder segment with a lattice
   bool track_decoded = false;  // record completed decoder jobs for TakeDecoded
   // token passing in Kaldi's sequential order (LatticeFasterDecoder's HashList
-  // order, running emitting cutoff, LIFO epsilon queue), else
-  // the order-independent form; env VOSK_AMD_DEC_ORDER=kaldi|parallel overrides
+  // order, running emitting cutoff, LIFO epsilon queue: the reference's
+  // KaldiRecognizer decoder), else the order-independent form (the
+  // deterministic form of the reference's batch CudaDecoder, BatchModel's
+  // default); env VOSK_AMD_DEC_ORDER=kaldi|parallel overrides
   bool kaldi_order = true;
 };
 
@@ -253,6 +255,7 @@ class Engine {
   int AllocSlot();
   int TryAllocSlot();  // -1 when every slot is in use
   void FreeSlot(int slot);
+  int SlotsInUse();
   // New utterance: features restart at sample 0, decoder restarts.
   void ResetPipeline(int slot);
   // InitDecoding: the decoder restarts, the feature/nnet pipeline continues.

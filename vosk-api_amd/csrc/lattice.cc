@@ -424,11 +424,20 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
   auto find_or_add = [&](std::vector<Elem>&& sub, int base, bool* added) {
     const std::string k = key_of(sub, base);
     auto& cand = index[k];
+    std::vector<int> ra, rb;
     for (int id : cand) {
       const auto& o = subsets[id];
       bool eq = true;
       for (size_t i = 0; i < o.size() && eq; i++)
         eq = std::fabs(o[i].w.g - sub[i].w.g) <= delta && std::fabs(o[i].w.a - sub[i].w.a) <= delta;
+      // the key holds residual lengths and hashes: the strings themselves
+      // are compared too (Kaldi compares them exactly)
+      for (size_t i = 0; i < o.size() && eq; i++) {
+        if (o[i].str == sub[i].str && bases[id] == base) continue;
+        R.Get(o[i].str, bases[id], &ra);
+        R.Get(sub[i].str, base, &rb);
+        eq = ra == rb;
+      }
       if (eq) {
         *added = false;
         return id;

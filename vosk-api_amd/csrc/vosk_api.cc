@@ -252,6 +252,7 @@ VamdEngine* vamd_engine_new(const char* model_dir, int fpc, int max_streams, int
   cfg.time_kernels = (flags & 4) != 0;
   cfg.pipeline = (flags & 8) != 0;
   cfg.lattice = (flags & 16) != 0;
+  cfg.kaldi_order = (flags & 32) == 0;
   const char* d = getenv("VOSK_AMD_DEVICE");
   cfg.device = d ? atoi(d) : 0;
   const char* at = getenv("VOSK_AMD_ARENA_TOKENS");

@@ -102,6 +102,12 @@ RecognizerGroup* Model::AllocStreamSlot(int* slot) {
     *slot = g->engine->TryAllocSlot();
     if (*slot >= 0) return g.get();
   }
+  // each engine holds the decoder state of all its slots (~140 MB per slot
+  // with lattices): the number of engines is capped
+  const int cap = EnvInt("VOSK_AMD_MAX_STREAM_ENGINES", 16);
+  if ((int)engines_.size() >= cap)
+    VAMD_ERR("all " << engines_.size() << " stream engines of the model are full "
+                    "(VOSK_AMD_MAX_STREAM_ENGINES x VOSK_AMD_MAX_STREAMS recognizers)");
   EngineConfig cfg;
   cfg.frames_per_chunk = md_->dcb.frames_per_chunk;
   cfg.max_slots = EnvInt("VOSK_AMD_MAX_STREAMS", 64);
@@ -111,6 +117,18 @@ RecognizerGroup* Model::AllocStreamSlot(int* slot) {
   engines_.emplace_back(new RecognizerGroup(new Engine(md_, cfg)));
   *slot = engines_.back()->engine->AllocSlot();
   return engines_.back().get();
+}
+
+void Model::FreeStreamSlot(RecognizerGroup* g, int slot) {
+  std::lock_guard<std::mutex> lk(mu_);
+  g->by_slot.at(slot) = nullptr;
+  g->engine->FreeSlot(slot);
+  // an emptied engine other than the first gives its device memory back
+  for (size_t i = 1; i < engines_.size(); i++)
+    if (engines_[i].get() == g && g->engine->SlotsInUse() == 0) {
+      engines_.erase(engines_.begin() + (long)i);
+      break;
+    }
 }
 
 RecognizerGroup* Model::GrammarEngine(const std::string& grammar) {
@@ -149,14 +167,23 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
     const size_t n = rs[i]->req_wave_ ? rs[i]->req_wave_->size() : 0;
     pieces = std::max(pieces, (n + step[i] - 1) / step[i]);
   }
+  // a stream whose own input fails (AcceptSamples) is dropped from the
+  // pass with its error kept for its caller; failures of the batched
+  // launches themselves reach every caller of the pass
   for (size_t p = 0; p < pieces; p++) {
     std::vector<int> sl, first;
     for (size_t i = 0; i < rs.size(); i++) {
       Recognizer* r = rs[i];
+      if (r->req_error_) continue;
       const size_t n = r->req_wave_ ? r->req_wave_->size() : 0;
       const size_t o = p * step[i];
       if (o < n) {
-        engine->AcceptSamples(r->slot_, r->req_wave_->data() + o, (int)std::min<size_t>(step[i], n - o));
+        try {
+          engine->AcceptSamples(r->slot_, r->req_wave_->data() + o, (int)std::min<size_t>(step[i], n - o));
+        } catch (...) {
+          r->req_error_ = std::current_exception();
+          continue;
+        }
       } else if (!(r->req_final_ && p == 0)) {
         continue;  // a FinalResult request runs in the first piece only
       }
@@ -172,7 +199,7 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
   std::vector<Recognizer*> er;
   for (Recognizer* r : rs) {
     r->req_endpoint_ = false;
-    if (!r->req_final_ && engine->NumFramesDecoded(r->slot_) > 0) {
+    if (!r->req_error_ && !r->req_final_ && engine->NumFramesDecoded(r->slot_) > 0) {
       ep.push_back(r->slot_);
       er.push_back(r);
     }
@@ -217,6 +244,7 @@ Recognizer::Recognizer(Model* model, float sr, const char* grammar)
     : model_(model), sample_frequency_(sr) {
   const int rate = InputRate(sr);
   group_ = grammar ? model->GrammarEngine(grammar) : nullptr;
+  grammar_group_ = group_ != nullptr;
   if (group_) slot_ = group_->engine->AllocSlot();
   else group_ = model->AllocStreamSlot(&slot_);
   engine_ = group_->engine.get();
@@ -224,7 +252,12 @@ Recognizer::Recognizer(Model* model, float sr, const char* grammar)
   try {
     engine_->SetSampleRate(slot_, rate);
   } catch (...) {
-    engine_->FreeSlot(slot_);
+    if (grammar_group_) {
+      group_->by_slot.at(slot_) = nullptr;
+      engine_->FreeSlot(slot_);
+    } else {
+      model_->FreeStreamSlot(group_, slot_);
+    }
     throw;
   }
   model_->Ref();
@@ -249,8 +282,12 @@ void Recognizer::SetSpkModel(SpkModel* spk) {
 }
 
 Recognizer::~Recognizer() {
-  group_->by_slot.at(slot_) = nullptr;
-  engine_->FreeSlot(slot_);
+  if (grammar_group_) {
+    group_->by_slot.at(slot_) = nullptr;
+    engine_->FreeSlot(slot_);
+  } else {
+    model_->FreeStreamSlot(group_, slot_);
+  }
   if (spk_) spk_->Unref();
   model_->Unref();
 }
@@ -328,8 +365,14 @@ bool Recognizer::AcceptWaveform(std::vector<float>& w) {  // src/recognizer.cc:2
 bool Recognizer::Submit(const std::vector<float>* wave, bool final) {
   req_wave_ = wave;
   req_final_ = final;
+  req_error_ = nullptr;
   group_->gc.Run(slot_, [this](const std::vector<int>& slots) { group_->Serve(slots); });
   req_wave_ = nullptr;
+  if (req_error_) {  // a failure of this stream alone (the others were served)
+    std::exception_ptr e = req_error_;
+    req_error_ = nullptr;
+    std::rethrow_exception(e);
+  }
   return req_endpoint_;
 }
 
@@ -713,6 +756,11 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
   cfg.max_step_samples = cfg.frames_per_chunk * md_->mfcc.WindowShift() + 512;
   cfg.arena_tokens = EnvInt("VOSK_AMD_ARENA_TOKENS", 1 << 22);
   cfg.lattice = true;  // PushLattice: MBR over each segment's lattice (batch_recognizer.cc:43-107)
+  // the reference's batch path decodes with Kaldi's CudaDecoder (parallel
+  // relaxation of all (token, arc) pairs against an atomically lowered
+  // cutoff, batch_model.cc:78-92), not LatticeFasterDecoder: the lanes run
+  // its deterministic form, the order-independent token passing
+  cfg.kaldi_order = false;
   cfg.pipeline = EnvInt("VOSK_AMD_BATCH_PIPELINE", 1) != 0;
   cfg.track_decoded = true;
   cfg.time_kernels = EnvInt("VOSK_AMD_BATCH_TIMING", 0) != 0;
@@ -1170,7 +1218,21 @@ void BatchModel::LaneLoop(Lane* L) {
       }
       if (!idle) continue;
       retire.push_back(r);
-      if (r->finishing_) finals.push_back(r);
+      if (r->finishing_) {
+        finals.push_back(r);
+      } else if (failed) {
+        // the step failed: the stream's decoder segment is lost.  Its engine
+        // slot is restarted (staged jobs and pending samples dropped, so the
+        // engine's state matches the retirement) and the segment ends with an
+        // empty result, so Result() reports the gap instead of staying silent
+        try {
+          e->ResetPipeline(r->slot_);
+        } catch (const std::exception& ex) {
+          VAMD_WARN("batch stream reset after a failed step: " << ex.what());
+        }
+        r->segment_offset_ = 0.0;
+        r->PublishResult(r->next_seq_++, r->FormatResult(MbrResult(), 0.0));
+      }
     }
     if (!finals.empty()) {
       try {

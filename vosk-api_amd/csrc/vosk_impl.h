@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <deque>
 #include <map>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <queue>
@@ -64,7 +65,10 @@ class Model {
   const std::shared_ptr<ModelData>& data() const { return md_; }
   // A free stream slot on one of the model's stream engines (created
   // lazily; a new engine of VOSK_AMD_MAX_STREAMS slots when all are full).
+  // At most VOSK_AMD_MAX_STREAM_ENGINES (default 16) engines; an engine
+  // other than the first is released when its last recognizer is freed.
   RecognizerGroup* AllocStreamSlot(int* slot);
+  void FreeStreamSlot(RecognizerGroup* g, int slot);
   // Engine of the grammar recognizers with this phrase list (JSON array of
   // strings, src/recognizer.cc:49-108): the runtime graph HCLr o G(grammar),
   // one engine per distinct grammar, created on first use.  Models without
@@ -141,11 +145,13 @@ class Recognizer {
 
   Model* model_;
   RecognizerGroup* group_ = nullptr;
+  bool grammar_group_ = false;  // a grammar engine's slot (else a model stream engine's)
   Engine* engine_;
   int slot_;
   // the request the group's batched pass serves (Submit)
   const std::vector<float>* req_wave_ = nullptr;
   bool req_final_ = false, req_endpoint_ = false;
+  std::exception_ptr req_error_;  // this stream's own failure in a group pass
   float sample_frequency_;
   int max_alternatives_ = 0;
   bool words_ = false, partial_words_ = false, nlsml_ = false;

@@ -807,7 +807,7 @@ PRESETS = {
     "bigram_8m": dict(seed=23, vocab=20000, num_pdfs=2000, llh_std=1.5, graph="bigram",
                       graph_opts=dict(num_hist=6400, fut=300)),
     # vosk-model-small-en-us scale (BASELINE config 3): 20 k-word HCLr + a
-    # ~29 k-history trigram Gr, expanded at load to ~1.9 M states
+    # ~29 k-history trigram Gr, expanded at load to ~275 k states (with pushing)
     "la_small_en_us": dict(seed=11, vocab=20000, num_pdfs=2000, llh_std=1.5, graph="lookahead",
                            graph_opts=dict(n_big=20000, fut_big=24, n_tri=3000)),
 }

@@ -229,9 +229,14 @@ def device_count():
 
 class Engine:
     def __init__(self, model_dir, frames_per_chunk=0, max_streams=8, stats=False, keep_llh=False,
-                 time_kernels=False, pipeline=False, lattice=False):
+                 time_kernels=False, pipeline=False, lattice=False, order="kaldi"):
+        """order: "kaldi" (LatticeFasterDecoder's sequential token passing,
+        the KaldiRecognizer path) or "parallel" (the order-independent form
+        the BatchModel lanes run); VOSK_AMD_DEC_ORDER overrides either."""
+        if order not in ("kaldi", "parallel"):
+            raise ValueError("order: 'kaldi' or 'parallel'")
         flags = ((1 if stats else 0) | (2 if keep_llh else 0) | (4 if time_kernels else 0)
-                 | (8 if pipeline else 0) | (16 if lattice else 0))
+                 | (8 if pipeline else 0) | (16 if lattice else 0) | (32 if order == "parallel" else 0))
         h = _c.vamd_engine_new(str(model_dir).encode(), frames_per_chunk, max_streams, flags)
         if not h:
             raise RuntimeError("vamd_engine_new failed: " + _err())
@@ -397,9 +402,10 @@ class Engine:
     PHASES = ("cutoff", "seed", "exp_tokens", "exp_items", "exp_winners", "eps", "commit_toks",
               "commit_links", "commit_eps_links", "commit_clear", "prune", "n_hbm_created",
               "n_created", "n_eps_rounds", "n_chunks", "frames", "prune_walk", "prune_remap",
-              "prune_links", "prune_move", "n_prune_frames", "n_prunes", "exp_relax", "exp_links")
-    PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19, 22, 23]  # the clock slots (the rest count)
-    PHASE_CLOCKS = PHASES[:11] + PHASES[16:20] + PHASES[22:24]
+              "prune_links", "prune_move", "n_prune_frames", "n_prunes", "exp_relax", "exp_links",
+              "kq_members", "kq_rank", "kq_replay", "kq_final")
+    PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19, 22, 23, 24, 25, 26, 27]  # clock slots (the rest count)
+    PHASE_CLOCKS = PHASES[:11] + PHASES[16:20] + PHASES[22:28]
 
     def decoder_phases_per_stream(self):
         """[max_streams, len(PHASES)] int64: decoder_phases() per stream slot."""
