@@ -71,7 +71,7 @@ def pcm(x):
 
 def bench_model(rank, dist, preset):
     import make_synth_model
-    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", f"bench_{preset}_v3")
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", f"bench_{preset}_v4")
     if rank == 0 and not os.path.exists(os.path.join(cache, "README")):
         tmp = cache + f".tmp{os.getpid()}"
         make_synth_model.make_preset(preset, tmp)

@@ -14,7 +14,7 @@ for p in (PKG, os.path.join(PKG, "tools"), os.path.join(REPO, "tests")):
 
 MODEL_CACHE = os.environ.get("VAMD_MODEL_CACHE", os.path.join(
     os.environ.get("TMPDIR", "/tmp"), "vamd_models"))
-SYNTH_VERSION = "v3"
+SYNTH_VERSION = "v4"
 
 
 def pytest_configure(config):

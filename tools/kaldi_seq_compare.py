@@ -52,7 +52,7 @@ def model_dir(name):
     if name == "la_small_en_us":
         import make_synth_model
         import oracle_graph as OG
-        path = os.path.join(conftest.MODEL_CACHE, "bench_la_small_en_us_v3")
+        path = os.path.join(conftest.MODEL_CACHE, "bench_la_small_en_us_v4")
         if not os.path.exists(os.path.join(path, "README")):
             make_synth_model.make_preset(name, path + ".tmp")
             os.rename(path + ".tmp", path)

@@ -47,6 +47,7 @@ struct Reach {
   std::vector<int> comp;               // per state
   std::vector<Intervals> labels;       // per component
   std::vector<char> final;             // per component
+  std::vector<int> cls;                // per component: id of its (labels, final) set
 };
 
 void ComputeReach(const HostFst& a, Reach* r) {
@@ -105,9 +106,14 @@ void ComputeReach(const HostFst& a, Reach* r) {
   }
   r->labels.assign(ncomp, Intervals());
   r->final.assign(ncomp, 0);
+  // components reaching the same set of successor components (word-boundary
+  // states: every word's first phone) share the merged successor lists
+  std::map<std::vector<int>, std::pair<Intervals, char>> merged;
+  std::vector<int> succ;
   for (int c = 0; c < ncomp; c++) {
     Intervals acc;
     char fin = 0;
+    succ.clear();
     for (int m = cbeg[c]; m < cbeg[c + 1]; m++) {
       const int v = members[m];
       if (std::isfinite(a.final_cost[v])) fin = 1;
@@ -116,16 +122,43 @@ void ComputeReach(const HostFst& a, Reach* r) {
           acc.push_back({a.olabel[e], a.olabel[e]});
         } else {
           const int d = r->comp[a.nextstate[e]];
-          if (d == c) continue;
-          fin |= r->final[d];
-          acc.insert(acc.end(), r->labels[d].begin(), r->labels[d].end());
+          if (d != c) succ.push_back(d);
         }
+      }
+    }
+    std::sort(succ.begin(), succ.end());
+    succ.erase(std::unique(succ.begin(), succ.end()), succ.end());
+    if (succ.size() >= 16) {
+      auto it = merged.find(succ);
+      if (it == merged.end()) {
+        Intervals u;
+        char f = 0;
+        for (int d : succ) {
+          f |= r->final[d];
+          u.insert(u.end(), r->labels[d].begin(), r->labels[d].end());
+        }
+        Coalesce(&u);
+        it = merged.emplace(succ, std::make_pair(std::move(u), f)).first;
+      }
+      fin |= it->second.second;
+      acc.insert(acc.end(), it->second.first.begin(), it->second.first.end());
+    } else {
+      for (int d : succ) {
+        fin |= r->final[d];
+        acc.insert(acc.end(), r->labels[d].begin(), r->labels[d].end());
       }
     }
     Coalesce(&acc);
     r->labels[c] = std::move(acc);
     r->final[c] = fin;
   }
+  // components with equal reachable sets (e.g. the word-end states, which
+  // all continue with every word) share a class: lookahead results and arc
+  // indexes depend only on the set
+  std::map<std::pair<Intervals, char>, int> classes;
+  r->cls.assign(ncomp, 0);
+  for (int c = 0; c < ncomp; c++)
+    r->cls[c] = classes.emplace(std::make_pair(r->labels[c], r->final[c]), (int)classes.size()).first->second;
 }
 
 // composed state -> id (open addressing; key = q1 << 33 | q2 << 1 | filter)
@@ -362,7 +395,12 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
     int64_t prefix;
     float lw;
   };
-  auto lookahead = [&](int c, int q) {
+  // LookAheadFst depends only on (reachability component, G state): memoized
+  struct LaHash {
+    size_t operator()(uint64_t k) const { return (size_t)StateTable::Mix(k); }
+  };
+  std::unordered_map<uint64_t, LookAhead, LaHash> la_memo;
+  auto lookahead_uncached = [&](int c, int q) {
     const Intervals& iv = reach.labels[c];
     const bool rfin = reach.final[c] && std::isfinite(b.final_cost[q]);
     const int64_t r0 = b.row[q], n = b.row[q + 1] - r0;
@@ -413,6 +451,14 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
     la.ok = rarc || rfin;
     return la;
   };
+  auto lookahead = [&](int c, int q) {
+    const uint64_t k = ((uint64_t)(uint32_t)reach.cls[c] << 32) | (uint32_t)q;
+    auto it = la_memo.find(k);
+    if (it != la_memo.end()) return it->second;
+    const LookAhead la = lookahead_uncached(c, q);
+    la_memo.emplace(k, la);
+    return la;
+  };
 
   // Wide HCL states (the word-start states: one output-epsilon arc per first
   // phone) are checked per grammar word instead of per arc: the label line is
@@ -424,17 +470,33 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
     std::vector<int> seg_begin;   // [nseg + 1] into arcs
     std::vector<int> arcs;        // local arc indices covering each segment
     std::vector<int> final_arcs;  // arcs that reach a final state
+    std::vector<std::pair<int, int>> labelled;  // (output label, arc) of the word arcs, sorted
+    // per G state: the arcs that can produce composed arcs there (the
+    // output-epsilon arcs LookAheadFst can accept, the word arcs the G state
+    // matches), in arc order
+    std::unordered_map<int, std::vector<int>> cand;
   };
   constexpr int kWide = 16;
-  std::vector<std::unique_ptr<ArcIndex>> arc_index(a.NumStates());
+  std::vector<ArcIndex*> arc_index(a.NumStates(), nullptr);
+  // states whose output-epsilon arcs reach the same components in the same
+  // order (the word-boundary states) share one index
+  std::map<std::vector<int>, std::unique_ptr<ArcIndex>> index_by_sig;
   auto index_of = [&](int q1) -> const ArcIndex* {
     const int64_t b0 = a.row[q1], n = a.row[q1 + 1] - b0;
     if (n < kWide) return nullptr;
-    if (arc_index[q1]) return arc_index[q1].get();
+    if (arc_index[q1]) return arc_index[q1];
+    std::vector<int> sig(n);
+    for (int64_t e = b0; e < b0 + n; e++)
+      sig[e - b0] = a.olabel[e] != 0 ? -1 - a.olabel[e] : reach.cls[reach.comp[a.nextstate[e]]];
+    auto found = index_by_sig.find(sig);
+    if (found != index_by_sig.end()) return arc_index[q1] = found->second.get();
     auto ix = std::make_unique<ArcIndex>();
     std::vector<std::pair<long long, int>> ev;  // (position, +arc+1 / -(arc+1))
     for (int64_t e = b0; e < b0 + n; e++) {
-      if (a.olabel[e] != 0) continue;
+      if (a.olabel[e] != 0) {
+        ix->labelled.push_back({a.olabel[e], (int)(e - b0)});
+        continue;
+      }
       const int c = reach.comp[a.nextstate[e]];
       if (reach.final[c]) ix->final_arcs.push_back((int)(e - b0));
       for (const auto& r : reach.labels[c]) {
@@ -459,8 +521,10 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
       ix->arcs.insert(ix->arcs.end(), sorted_active.begin(), sorted_active.end());
     }
     ix->seg_begin.push_back((int)ix->arcs.size());
-    arc_index[q1] = std::move(ix);
-    return arc_index[q1].get();
+    std::sort(ix->labelled.begin(), ix->labelled.end());
+    arc_index[q1] = ix.get();
+    index_by_sig.emplace(std::move(sig), std::move(ix));
+    return arc_index[q1];
   };
   std::vector<char> mark;
 
@@ -525,26 +589,50 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
         const int64_t e = bsorted[k];
         push(0, b.olabel[e], 0.0f + (bw[k] + nfw), id_of(q1, b.nextstate[e], 0, 0.0f, kNoLabel));
       }
-    const ArcIndex* ix = b_alleps[q2] ? nullptr : index_of(q1);
-    if (ix) {  // mark the output-epsilon arcs of a wide HCL state the lookahead can accept
-      mark.assign(a.row[q1 + 1] - a.row[q1], 0);
-      if (std::isfinite(b.final_cost[q2]))
-        for (int k : ix->final_arcs) mark[k] = 1;
-      for (int64_t k = beps_end[q2]; k < b.row[q2 + 1]; k++) {
-        const int w = bword[k];
-        auto it = std::upper_bound(ix->seg_lo.begin(), ix->seg_lo.end(), w);
-        if (it == ix->seg_lo.begin()) continue;
-        const size_t sg = (size_t)(it - ix->seg_lo.begin()) - 1;
-        for (int j = ix->seg_begin[sg]; j < ix->seg_begin[sg + 1]; j++) mark[ix->arcs[j]] = 1;
+    ArcIndex* ix = b_alleps[q2] ? nullptr : const_cast<ArcIndex*>(index_of(q1));
+    const std::vector<int>* cand = nullptr;
+    if (ix) {
+      auto ci = ix->cand.find(q2);
+      if (ci == ix->cand.end()) {
+        // mark the output-epsilon arcs the lookahead can accept, and the
+        // word arcs G matches (intersecting the smaller list into the larger)
+        const int n = (int)(a.row[q1 + 1] - a.row[q1]);
+        mark.assign(n, 0);
+        if (std::isfinite(b.final_cost[q2]))
+          for (int k : ix->final_arcs) mark[k] = 1;
+        for (int64_t k = beps_end[q2]; k < b.row[q2 + 1]; k++) {
+          const int w = bword[k];
+          auto it = std::upper_bound(ix->seg_lo.begin(), ix->seg_lo.end(), w);
+          if (it == ix->seg_lo.begin()) continue;
+          const size_t sg = (size_t)(it - ix->seg_lo.begin()) - 1;
+          for (int j = ix->seg_begin[sg]; j < ix->seg_begin[sg + 1]; j++) mark[ix->arcs[j]] = 1;
+        }
+        const int* wb = bword.data() + beps_end[q2];
+        const int* we = bword.data() + b.row[q2 + 1];
+        if ((size_t)(we - wb) < ix->labelled.size()) {
+          for (const int* w = wb; w < we; w++) {
+            auto it = std::lower_bound(ix->labelled.begin(), ix->labelled.end(), std::make_pair(*w, -1));
+            for (; it != ix->labelled.end() && it->first == *w; ++it) mark[it->second] = 1;
+          }
+        } else {
+          for (const auto& lw : ix->labelled)
+            if (std::binary_search(wb, we, lw.first)) mark[lw.second] = 1;
+        }
+        std::vector<int> v;
+        for (int k = 0; k < n; k++)
+          if (mark[k]) v.push_back(k);
+        ci = ix->cand.emplace(q2, std::move(v)).first;
       }
+      cand = &ci->second;
     }
     const int nsb = b_has_eps[q2] ? 1 : 0;
-    for (int64_t e = a.row[q1]; e < a.row[q1 + 1]; e++) {
+    const int64_t ncand = cand ? (int64_t)cand->size() : a.row[q1 + 1] - a.row[q1];
+    for (int64_t ki = 0; ki < ncand; ki++) {
+      const int64_t e = cand ? a.row[q1] + (*cand)[ki] : a.row[q1] + ki;
       const int il = in_label(e);
       const int p = a.nextstate[e];
       if (a.olabel[e] == 0) {  // HCL moves alone, looking ahead into G
         if (b_alleps[q2]) continue;
-        if (ix && !mark[e - a.row[q1]]) continue;
         const LookAhead la = lookahead(reach.comp[p], q2);
         if (!la.ok) continue;
         if (la.prefix >= 0) {  // label pushing: the single reachable G arc now

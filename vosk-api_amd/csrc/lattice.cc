@@ -196,6 +196,14 @@ struct StrRepo {
     const uint64_t sub = MulMod(hash[base], pw[len[id] - len[base]]);
     return hash[id] >= sub ? hash[id] - sub : hash[id] + kMod - sub;
   }
+  // residuals (ba -> a) and (bb -> b) of equal length: equal strings?
+  bool ResEqual(int a, int ba, int b, int bb) const {
+    int n = len[a] - len[ba];
+    if (n != len[b] - len[bb]) return false;
+    for (; n > 0 && a != b; n--, a = parent[a], b = parent[b])
+      if (label[a] != label[b]) return false;
+    return true;
+  }
   void Get(int id, int base, std::vector<int>* out) const {
     out->resize(len[id] - len[base]);
     for (int i = (int)out->size() - 1; i >= 0; i--, id = parent[id]) (*out)[i] = label[id];
@@ -424,20 +432,16 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
   auto find_or_add = [&](std::vector<Elem>&& sub, int base, bool* added) {
     const std::string k = key_of(sub, base);
     auto& cand = index[k];
-    std::vector<int> ra, rb;
     for (int id : cand) {
       const auto& o = subsets[id];
       bool eq = true;
       for (size_t i = 0; i < o.size() && eq; i++)
         eq = std::fabs(o[i].w.g - sub[i].w.g) <= delta && std::fabs(o[i].w.a - sub[i].w.a) <= delta;
       // the key holds residual lengths and hashes: the strings themselves
-      // are compared too (Kaldi compares them exactly)
-      for (size_t i = 0; i < o.size() && eq; i++) {
-        if (o[i].str == sub[i].str && bases[id] == base) continue;
-        R.Get(o[i].str, bases[id], &ra);
-        R.Get(sub[i].str, base, &rb);
-        eq = ra == rb;
-      }
+      // are compared too (Kaldi compares them exactly), walking both up the
+      // trie together until they meet (equal-length residuals ending in the
+      // same node are equal)
+      for (size_t i = 0; i < o.size() && eq; i++) eq = R.ResEqual(o[i].str, bases[id], sub[i].str, base);
       if (eq) {
         *added = false;
         return id;

@@ -787,11 +787,12 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
     const int omp = EnvInt("OMP_NUM_THREADS", 0);
     if (omp > 0) hc = std::min(hc, omp);
   }
-  // half of them: the feeding thread, the lanes and the HIP runtime keep
-  // theirs (more workers only contend: 8 vs 14 of 16 cores measured equal
-  // or better on the 60-s bench)
+  // all but two of them (the feeding thread and the lane threads keep
+  // theirs): a stream's final segments all arrive together at FinishStream,
+  // when the GPU side is idle, and their lattice work is the tail of the
+  // batch; during chunk rounds the workers only see endpoint segments
   const int cores = std::min(hc > 0 ? hc : 8, 16 * (int)lanes_.size());
-  int nt = EnvInt("VOSK_AMD_RESULT_THREADS", std::max(2, cores / 2));
+  int nt = EnvInt("VOSK_AMD_RESULT_THREADS", std::max(2, cores - 1 - (int)lanes_.size()));
   pool_.reset(new WorkerPool(nt));
   for (auto& L : lanes_) {
     Lane* l = L.get();

@@ -310,12 +310,21 @@ def build_bigram_graph(rng, tids, num_base, vocab, num_hist=1000, fut=400):
 
 def build_lookahead_graph(rng, tids, num_base, vocab, num_tids, n_big=40, fut_big=12, n_tri=12):
     """Lookahead graph pair (src/model.cc:281-285): an HCLr
-    transducer (the lexicon prefix tree over the chain HMMs with optional
-    silence, every word's output label on the arc back to the word-start
-    state; one word in 25 is a homophone of an earlier word, told apart by a
-    disambiguation transition-id on its word-end arc) and a backoff trigram
-    LM in the ngram trie form (write_ngram_fst).  Returns (hclr Fst, lm
-    dict, words, disambig ids)."""
+    transducer shaped as a determinized H o C o L is (Kaldi's lexicon puts a
+    word's label on its first phone arc; determinizing the transducer delays
+    it to where the pronunciation prefix becomes unique, utils/mkgraph_
+    lookahead.sh), and a backoff trigram LM in the ngram trie form
+    (write_ngram_fst).  HCLr: a prefix tree over the chain HMMs (entry
+    transition-id on the arc into a phone state, self-loop on the state);
+    each word's output label on the first arc into a state no other word
+    passes through; words end in a state shared by every word ending with the
+    same (previous phone, last phone) pair, which -- like the start state --
+    is final and continues with the first phones of every word or optional
+    silence (so word ends are emitting transitions, as in a real HCL).
+    Homophones (one word in 25 repeats an earlier pronunciation) share their
+    whole path and output their labels on epsilon arcs to the start state,
+    told apart by disambiguation transition-ids (Kaldi's #1, #2 ...).
+    Returns (hclr Fst, lm dict, words, disambig ids)."""
     words = []
     seen = {}
     while len(words) < vocab:
@@ -341,30 +350,67 @@ def build_lookahead_graph(rng, tids, num_base, vocab, num_tids, n_big=40, fut_bi
 
     sil_f, sil_s = tids(0, 1)
     s_sil = new_state()
+    # phone sequences (position-dependent) and how many words share each prefix
+    seqs = [[position_phone(b, j, len(pr), num_base) for j, b in enumerate(pr)] for pr in words]
+    nwords = {}
+    for sq in seqs:
+        for j in range(1, len(sq) + 1):
+            nwords[tuple(sq[:j])] = nwords.get(tuple(sq[:j]), 0) + 1
+    homo = {}  # pronunciation -> its words
+    for wi, pr in enumerate(words):
+        homo.setdefault(pr, []).append(wi)
+    children = {}  # (node, phone) -> tree state
+    ends = {}      # (previous phone, last phone) -> shared word-end state
+    tree_arcs = {}  # (node, phone) -> arc index (the label goes on it)
+    labels = {}
+    homo_end = {}
+    for wi, sq in enumerate(seqs):
+        pr = words[wi]
+        shared_pron = len(homo[pr]) > 1
+        node, prev = LOOP, 0
+        labelled = shared_pron
+        for j, ph in enumerate(sq):
+            last = j == len(sq) - 1
+            key = (node, ph)
+            if last and not shared_pron:
+                e = ends.get((prev, ph))
+                if e is None:
+                    e = ends[(prev, ph)] = new_state()
+                    arcs.append((e, tids(prev, ph)[1], 0, 0.0, e))
+                if key not in tree_arcs:
+                    tree_arcs[key] = len(arcs)
+                    arcs.append((node, tids(prev, ph)[0], 0, 0.0, e))
+                child = e
+            else:
+                if key not in children:
+                    child = children[key] = new_state()
+                    tree_arcs[key] = len(arcs)
+                    f, sl = tids(prev, ph)
+                    arcs.append((node, f, 0, 0.0, child))
+                    arcs.append((child, sl, 0, 0.0, child))
+                child = children[key]
+            if not labelled and (last or nwords[tuple(sq[:j + 1])] == 1):
+                labels[tree_arcs[key]] = wi + 1  # the first arc only this word takes
+                labelled = True
+            node, prev = child, ph
+        if shared_pron:
+            homo_end[wi] = node
+    for pr, ws in homo.items():
+        if len(ws) > 1:
+            for k, wi in enumerate(ws):
+                arcs.append((homo_end[wi], disambig[k - 1] if k else 0, wi + 1, 0.0, LOOP))
+    arcs = [(a[0], a[1], labels.get(i, a[2]), a[3], a[4]) for i, a in enumerate(arcs)]
+    # word boundaries (the start state, the shared word-end states, silence)
+    # continue with every word's first phone, or optional silence
+    boundary = list(ends.values()) + [s_sil]
+    loop_out = [a for a in arcs if a[0] == LOOP]
     arcs.append((LOOP, sil_f, 0, 0.7, s_sil))
     arcs.append((s_sil, sil_s, 0, 0.0, s_sil))
-    arcs.append((s_sil, 0, 0, 0.0, LOOP))
-    children = {}
-    ends = []
-    for wi, pron in enumerate(words):
-        node, prev = LOOP, 0
-        for j, bph in enumerate(pron):
-            ph = position_phone(bph, j, len(pron), num_base)
-            key = (node, ph)
-            if key not in children:
-                child = new_state()
-                children[key] = child
-                f, sl = tids(prev, ph)
-                arcs.append((node, f, 0, 0.0, child))
-                arcs.append((child, sl, 0, 0.0, child))
-            node = children[key]
-            prev = ph
-        ends.append(node)
-    homophone = {}
-    for wi, node in enumerate(ends):
-        k = homophone.get(node, 0)
-        homophone[node] = k + 1
-        arcs.append((node, disambig[k - 1] if k else 0, wi + 1, 0.0, LOOP))
+    for b in boundary:
+        for a in loop_out:
+            arcs.append((b, a[1], a[2], a[3], a[4]))
+        if b != s_sil:
+            arcs.append((b, sil_f, 0, 0.7, s_sil))
     S = n_states[0]
     arcs.sort(key=lambda a: a[0])
     row = np.zeros(S + 1, np.int64)
@@ -372,6 +418,8 @@ def build_lookahead_graph(rng, tids, num_base, vocab, num_tids, n_big=40, fut_bi
     row = np.cumsum(row)
     final = np.full(S, np.inf, np.float32)
     final[LOOP] = 0.0
+    for b in boundary:
+        final[b] = 0.0
     hclr = kf.Fst(LOOP, final, row,
                   np.array([a[1] for a in arcs], np.int32), np.array([a[2] for a in arcs], np.int32),
                   np.array([a[3] for a in arcs], np.float32), np.array([a[4] for a in arcs], np.int32))
