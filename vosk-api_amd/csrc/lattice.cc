@@ -321,14 +321,26 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
   W = WordLattice();
   const int N = (int)L.tok_state.size(), F = L.num_frames;
   if (N == 0) return true;
-  std::vector<std::vector<int>> outl(N);
-  for (int i = 0; i < (int)L.links.size(); i++) outl[L.links[i].src].push_back(i);
+  // out-links per token (CSR): the word-epsilon ones (closures) first, then
+  // the word links (transitions)
+  const int NL = (int)L.links.size();
+  std::vector<int> ob(N + 1, 0), oe(N, 0), ol(NL);
   // the labels of every link, gathered once (the graph's label arrays are
   // large: random reads of them in every closure miss the caches)
   std::vector<int> lin(L.links.size()), lout(L.links.size());
   for (size_t i = 0; i < L.links.size(); i++) {
     lin[i] = g.ilabel[L.links[i].arc];
     lout[i] = g.olabel[L.links[i].arc];
+  }
+  for (int i = 0; i < NL; i++) ob[L.links[i].src + 1]++;
+  for (int t = 0; t < N; t++) ob[t + 1] += ob[t];
+  {
+    std::vector<int> fill(ob.begin(), ob.end() - 1);
+    for (int i = 0; i < NL; i++)
+      if (lout[i] == 0) ol[fill[L.links[i].src]++] = i;
+    for (int t = 0; t < N; t++) oe[t] = fill[t];
+    for (int i = 0; i < NL; i++)
+      if (lout[i] != 0) ol[fill[L.links[i].src]++] = i;
   }
   std::vector<float> fin(N, INFINITY);
   for (int t = L.frame_begin[F]; t < L.frame_begin[F + 1]; t++)
@@ -353,6 +365,7 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
   for (int k = 0; k <= F; k++)
     for (int t = L.frame_begin[k]; t < L.frame_begin[k + 1]; t++) tframe[t] = k;
   std::vector<int> at_pos(N, -1);  // closure scratch: token -> element (reset after each closure)
+  std::vector<char> pending;      // closure scratch: element queued
   auto closure = [&](std::vector<Elem>* sub, int base) {
     struct AtMap {
       std::vector<int>& pos;
@@ -371,6 +384,7 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     } at{at_pos, {}};
     std::priority_queue<std::pair<int, int>, std::vector<std::pair<int, int>>, std::greater<std::pair<int, int>>>
         work;  // (frame, element), earliest frame first
+    pending.assign(sub->size(), 1);
     for (int i = 0; i < (int)sub->size(); i++) {
       at.set((*sub)[i].tok, i);
       work.push({tframe[(*sub)[i].tok], i});
@@ -378,11 +392,12 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     while (!work.empty()) {
       const int i = work.top().second;
       work.pop();
+      pending[i] = 0;  // an element improved while queued is expanded once, at its best
       const Elem e = (*sub)[i];
       dbg_ext++;
-      for (int li : outl[e.tok]) {
+      for (int k = ob[e.tok]; k < oe[e.tok]; k++) {
+        const int li = ol[k];
         const auto& l = L.links[li];
-        if (lout[li] != 0) continue;
         Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}),
                lin[li] != 0 ? R.Succ(e.str, lin[li]) : e.str};
         const int ei = at.find_idx(n.tok);
@@ -390,9 +405,13 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
           at.set(n.tok, (int)sub->size());
           work.push({tframe[n.tok], (int)sub->size()});
           sub->push_back(n);
+          pending.push_back(1);
         } else if (ElemBetter(R, base, n, (*sub)[ei])) {
           (*sub)[ei] = n;
-          work.push({tframe[n.tok], ei});
+          if (!pending[ei]) {
+            pending[ei] = 1;
+            work.push({tframe[n.tok], ei});
+          }
         }
       }
     }
@@ -470,10 +489,10 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     {
       const std::vector<Elem>& sub = subsets[sid];
       for (const Elem& e : sub)
-        for (int li : outl[e.tok]) {
+        for (int k = oe[e.tok]; k < ob[e.tok + 1]; k++) {
+          const int li = ol[k];
           const auto& l = L.links[li];
           const int w = lout[li];
-          if (w == 0) continue;
           Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}),
                  lin[li] != 0 ? R.Succ(e.str, lin[li]) : e.str};
           auto& v = by_word[w];
