@@ -57,6 +57,18 @@ void vamd_graph_free(void *graph);
  * frames selected; -1: error); *num_frames = the selected frame count. */
 int vamd_spk_extract(VoskSpkModel *spk, const float *samples, long long n, int rate, int first_frame,
                      const signed char *keep, int nkeep, float *out, int cap, int *num_frames);
+/* count such requests extracted as one batch (one launch sequence per up to
+ * 256 utterances; each vector equals vamd_spk_extract's bit for bit): vector
+ * i goes to out + i * cap, status[i] = its length (0: fewer than 50 frames).
+ * Returns count (-1: error).  Concurrent vamd_spk_extract / recognizer
+ * callers are batched the same way (group commit); vamd_spk_stats reports the
+ * launch sequences run, the utterances they extracted, and the frame-level
+ * layers' GEMM flops and HIP-event milliseconds (either pointer may be NULL). */
+int vamd_spk_extract_batch(VoskSpkModel *spk, int count, const float *const *samples, const long long *n,
+                           const int *rate, const int *first_frame, const signed char *const *keep,
+                           const int *nkeep, float *out, int cap, int *num_frames, int *status);
+int vamd_spk_stats(VoskSpkModel *spk, long long *batches, long long *utterances, double *layer_flops,
+                   double *layer_ms);
 
 /* host-only: LM rescoring (rescore.h) applied by vamd_lattice_words_json
  * after determinization (both paths NULL: off); vamd_carpa_logprob is a
@@ -169,7 +181,7 @@ int vamd_engine_decoder_totals(VamdEngine *e, long long *out6);
  * exp_items, exp_winners, eps, commit_toks, commit_links] (s_memtime clocks;
  * the full list is vosk/engine.py Engine.PHASES) */
 int vamd_engine_decoder_phases(VamdEngine *e, long long *out8);
-/* all decoder phase counters: writes min(cap, N) values, returns N (28) */
+/* all decoder phase counters: writes min(cap, N) values, returns N (34) */
 int vamd_engine_decoder_phases_n(VamdEngine *e, long long *out, int cap);
 /* the N counters per stream slot: out[max_streams][N] */
 int vamd_engine_decoder_phases_per_stream(VamdEngine *e, long long *out);

@@ -89,6 +89,7 @@ struct DecShared {
   float kcar[2];
   int ksum_w[2][DW];
   int kn0, kne;
+  int kpop_sum, kpop_max;  // component replay: pops over all lanes / on the longest lane
 };
 
 // optional phase clocks (VOSK_AMD_DEC_PROFILE): thread 0 stamps s_memtime
@@ -1114,6 +1115,49 @@ __device__ __forceinline__ void km_set(const KaldiLds& K, int* KM, int i, int f,
   else AG_ST(&KM[(long long)(i - kKM) * kKMRec + f], v);
 }
 
+// block-wide bitonic sorts in LDS (ascending; n <= DT, padded to a power of
+// two with the maximum key): 64-bit keys as (hi, lo) int pairs, 32-bit keys
+__device__ __forceinline__ void bitonic_sort64(int* hi, int* lo, int n) {
+  int np = 1;
+  while (np < n) np <<= 1;
+  for (int i = n + threadIdx.x; i < np; i += DT) {
+    hi[i] = 0x7fffffff;
+    lo[i] = 0x7fffffff;
+  }
+  __syncthreads();
+  for (int k = 2; k <= np; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int i = threadIdx.x, l = i ^ j;
+      if (i < np && l > i) {
+        const unsigned long long x = ((unsigned long long)(unsigned)hi[i] << 32) | (unsigned)lo[i];
+        const unsigned long long y = ((unsigned long long)(unsigned)hi[l] << 32) | (unsigned)lo[l];
+        if (((i & k) == 0) ? (x > y) : (x < y)) {
+          hi[i] = (int)(y >> 32); lo[i] = (int)(unsigned)y;
+          hi[l] = (int)(x >> 32); lo[l] = (int)(unsigned)x;
+        }
+      }
+      __syncthreads();
+    }
+}
+__device__ __forceinline__ void bitonic_sort32(unsigned* key, int n) {
+  int np = 1;
+  while (np < n) np <<= 1;
+  for (int i = n + threadIdx.x; i < np; i += DT) key[i] = 0xffffffffu;
+  __syncthreads();
+  for (int k = 2; k <= np; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int i = threadIdx.x, l = i ^ j;
+      if (i < np && l > i) {
+        const unsigned x = key[i], y = key[l];
+        if (((i & k) == 0) ? (x > y) : (x < y)) {
+          key[i] = y;
+          key[l] = x;
+        }
+      }
+      __syncthreads();
+    }
+}
+
 // ProcessNonemitting in Kaldi order.  The frame under construction holds the
 // emitting pass's tokens, creation indices [0, ne) (bucket state % khash).
 // The epsilon closure itself (final token set, costs, backpointers and the
@@ -1298,7 +1342,15 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     }
   }
   pr.mark(24);
-  // the initial queue in list order (rank by counting: it is short)
+  // the initial queue in list order: sorted in LDS when it fits, else ranked
+  // by counting
+  if (n0 <= kKM) {
+    bitonic_sort64(K.v0hi, K.v0lo, n0);
+    for (int r = threadIdx.x; r < n0; r += DT) {
+      const int v = AG_LD(&KO[K.v0lo[r]]);
+      K.stk[r] = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+    }
+  } else
   for (int q = threadIdx.x; q < n0; q += DT) {
     auto key = [&](int r) -> unsigned long long {
       if (r < kKM) return ((unsigned long long)(unsigned)K.v0hi[r] << 32) | (unsigned)K.v0lo[r];
@@ -1322,7 +1374,164 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   int adj_n = 0;
   if (nm > 0) adj_n = km_get(K, KM, nm - 1, kMOff) + km_get(K, KM, nm - 1, kMCnt);
   const bool fast = nm <= kKM && adj_n <= kKE && n0 <= kKM && !(a.debug & 4);
-  if (a.debug & 8) {  // development timing only: no replay (creation order = member order; wrong lists)
+  // Component-parallel replay.  The LIFO queue processes the initial tokens
+  // from the top (the last in list order first), each one's pushes before the
+  // next initial token; a token's expansion only touches tokens connected
+  // to it through productive epsilon arcs.  So the queue restricted to one
+  // connected component of those arcs is the queue of that component's own
+  // initial tokens, in the same order, and the components replay
+  // independently, one lane each: the creation order is by initial token
+  // (processing rank), then by creation within its expansion.  A component
+  // whose stack outgrows the lane's eight registers, or labels that do not
+  // settle, send the frame to the sequential replay below.
+  bool replayed = false;
+  if (fast && !(a.debug & (8 | 16))) {
+    int* comp = reinterpret_cast<int*>(K.v0lo);  // (the sort keys are consumed)
+    unsigned* key = reinterpret_cast<unsigned*>(K.v0hi);
+    int* mroot = sh.tsrc;
+    const float kInfL = __int_as_float(0x7f800000);
+    for (int i = threadIdx.x; i < nm; i += DT) comp[i] = i;
+    if (threadIdx.x == 0) {
+      sh.flag = 0;
+      sh.kpop_sum = 0;
+      sh.kpop_max = 0;
+    }
+    __syncthreads();
+    // connected components: minimum member index, propagated along the arcs
+    bool settled = false;
+    for (int it = 0; it < 64 && !settled; it++) {
+      if (threadIdx.x == 0) sh.kk = 0;
+      __syncthreads();
+      for (int u = threadIdx.x; u < nm; u += DT) {
+        const int e0 = K.mo[u], e1 = e0 + K.mn[u];
+        for (int e = e0; e < e1; e++) {
+          const int d = K.adj[e].x;
+          if (d < 0) continue;
+          const int cu = comp[u], cd = comp[d], m = cu < cd ? cu : cd;
+          if (cu > m) { atomicMin(&comp[u], m); sh.kk = 1; }
+          if (cd > m) { atomicMin(&comp[d], m); sh.kk = 1; }
+        }
+      }
+      __syncthreads();
+      settled = sh.kk == 0;
+      __syncthreads();
+    }
+    if (settled) {
+      // the initial tokens by (component, processing rank)
+      for (int r = threadIdx.x; r < n0; r += DT) {
+        const int u = K.stk[r];
+        key[r] = ((unsigned)comp[u] << 20) | ((unsigned)(n0 - 1 - r) << 10) | (unsigned)u;
+      }
+      __syncthreads();
+      bitonic_sort32(key, n0);
+      for (int i = threadIdx.x; i < nm; i += DT) mroot[i] = -1;
+      __syncthreads();
+      // one lane per component (the lane of its first initial token)
+      const int i = threadIdx.x;
+      if (i < n0 && (i == 0 || (key[i - 1] >> 20) != (key[i] >> 20))) {
+        const unsigned cmp = key[i] >> 20;
+        bool ovf = false;
+        int npop = 0;
+        for (int ri = i; ri < n0 && (key[ri] >> 20) == cmp && !ovf; ri++) {
+          const unsigned kr = key[ri];
+          const int prank = (int)((kr >> 10) & 1023u);
+          int s0 = (int)(kr & 1023u), s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0, s7 = 0;
+          int sp = 1, j = 0;
+          while (sp > 0) {
+            --sp;
+            npop++;
+            const int u = sp == 0 ? s0 : sp == 1 ? s1 : sp == 2 ? s2 : sp == 3 ? s3
+                        : sp == 4 ? s4 : sp == 5 ? s5 : sp == 6 ? s6 : s7;
+            const float cu = K.mc[u];
+            if (!(cu < cutoff)) continue;
+            const int e0 = K.mo[u], e1 = e0 + K.mn[u];
+            for (int e = e0; e < e1; e++) {
+              const int2 rec = K.adj[e];
+              if (rec.x < 0) continue;
+              const float tot = cu + __int_as_float(rec.y);
+              if (!(tot < cutoff)) continue;
+              const float old = K.mc[rec.x];
+              if (!(tot < old)) continue;
+              if (old == kInfL) {  // FindOrAddToken creates it
+                K.mord[rec.x] = j++;
+                mroot[rec.x] = prank;
+              }
+              K.mc[rec.x] = tot;
+              if (K.mn[rec.x] > 0) {  // changed: re-queued
+                if (sp == 8) {
+                  ovf = true;
+                  break;
+                }
+                s0 = sp == 0 ? rec.x : s0; s1 = sp == 1 ? rec.x : s1; s2 = sp == 2 ? rec.x : s2;
+                s3 = sp == 3 ? rec.x : s3; s4 = sp == 4 ? rec.x : s4; s5 = sp == 5 ? rec.x : s5;
+                s6 = sp == 6 ? rec.x : s6; s7 = sp == 7 ? rec.x : s7;
+                sp++;
+              }
+            }
+            if (ovf) break;
+          }
+          K.stk[prank] = j;  // this initial token's creations (the sequential path rebuilds the stack)
+        }
+        if (ovf) sh.flag = 1;
+        if (pr.on) {
+          atomicAdd(&sh.kpop_sum, npop);
+          atomicMax(&sh.kpop_max, npop);
+        }
+      }
+      __syncthreads();
+      if (sh.flag == 0) {
+        // creations per initial token in processing order (K.stk), then the
+        // global creation order = (processing rank offset) + creation within it
+        int tot;
+        const int c = threadIdx.x < n0 ? K.stk[threadIdx.x] : 0;
+        const int ex = kaldi_excl_sum(sh, c, 0, &tot);
+        __syncthreads();
+        if (threadIdx.x < n0) K.stk[threadIdx.x] = ex;
+        __syncthreads();
+        for (int m = threadIdx.x; m < nm; m += DT)
+          if (mroot[m] >= 0) K.mord[m] += K.stk[mroot[m]];
+        if (threadIdx.x == 0) sh.kn0 = tot;
+        __syncthreads();
+        replayed = true;
+      }
+    }
+    if (!replayed) {  // back to the sequential replay: the members' queue state reset
+      for (int m = threadIdx.x; m < nm; m += DT) {
+        const int c = K.mcr[m];
+        K.mc[m] = c >= 0 ? AG_LD(&KC[c]) : kInfL;
+        K.mord[m] = -1;
+      }
+      // the initial queue again (the sort keys were consumed)
+      __syncthreads();
+      if (threadIdx.x == 0) sh.kn0 = 0;
+      __syncthreads();
+      for (int m = threadIdx.x; m < nm; m += DT) {
+        const int c = K.mcr[m];
+        if (c < 0) continue;
+        const float c0 = AG_LD(&KC[c]);
+        if (!(c0 < cutoff)) continue;
+        const int v = K.ms[m];
+        const int4 si = a.sinfo[slot_state(t, T, v)];
+        bool prod = false;
+        for (int arc = si.y; arc < si.z && !prod; arc++) prod = c0 + __int_as_float(a.arcs[arc].y) < cutoff;
+        if (!prod) continue;
+        const int q = atomicAdd(&sh.kn0, 1);
+        K.v0hi[q] = AG_LD(&BF[AG_LD(&KB[c])]);
+        K.v0lo[q] = c;
+      }
+      vm_drain();
+      __syncthreads();
+      bitonic_sort64(K.v0hi, K.v0lo, n0);
+      for (int r = threadIdx.x; r < n0; r += DT) {
+        const int v = AG_LD(&KO[K.v0lo[r]]);
+        K.stk[r] = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+      }
+      vm_drain();
+      __syncthreads();
+    }
+  }
+  if (replayed) {
+  } else if (a.debug & 8) {  // development timing only: no replay (creation order = member order; wrong lists)
     for (int i = threadIdx.x; i < nm; i += DT) K.mord[i] = -1;
     if (threadIdx.x == 0) {
       int created = 0;
@@ -1427,7 +1636,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     sh.kn0 = ovf ? -1 : created;
   }
   __syncthreads();
-  const bool slow = !(a.debug & 8) && (!fast || sh.kn0 < 0);
+  const bool slow = !replayed && !(a.debug & 8) && (!fast || sh.kn0 < 0);
   if (slow && fast) {  // the LDS queue overflowed: start over through the HBM records
     for (int i = threadIdx.x; i < nm; i += DT) {
       const int c = K.mcr[i];
@@ -1490,6 +1699,14 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   vm_drain();
   __syncthreads();
   pr.mark(26);
+  pr.count(28, 1);
+  pr.count(29, fast ? 1 : 0);
+  pr.count(30, replayed ? 1 : 0);
+  pr.count(31, nm);
+  if (replayed) {
+    pr.count(32, sh.kpop_sum);
+    pr.count(33, sh.kpop_max);
+  }
   // the created tokens' creation indices [ne, ne + n_eps) in the queue's order, and their buckets
   for (int i = threadIdx.x; i < nm; i += DT) {
     if (km_get(K, KM, i, kMC) >= 0) continue;

@@ -693,6 +693,9 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   // pruning off (tests that compare the raw per-frame lattice with the oracle)
   dec_.prune_interval = m.dec.prune_interval;
   if (const char* pe = getenv("VOSK_AMD_DEC_PRUNE")) dec_.prune_interval = atoi(pe) ? m.dec.prune_interval : 0;
+  // a longer interval prunes less often (the lattice-beam prune of a result
+  // is exact either way; only the arenas grow between prunes)
+  if (const char* pi = getenv("VOSK_AMD_DEC_PRUNE_INTERVAL")) dec_.prune_interval = std::max(0, atoi(pi));
   // re-walk depth below the last pruned frame (Kaldi walks until the extra
   // costs settle; a shallower re-walk only prunes less, the final lattice-beam
   // prune is exact either way)

@@ -93,6 +93,13 @@ struct MfccJob {  // frames [first, first+count) of one slot; rows [row0, row0+c
   int slot, first, count, row0;
 };
 
+// one utterance of an x-vector batch (xvector.h): its selected frame indices
+// rows[rows0, rows0 + nsel), its pooled frame-level output rows
+// [pool_row0, pool_row0 + npool)
+struct XvecUtt {
+  int rows0, nsel, pool_row0, npool;
+};
+
 // windowed-sinc resampling (resample.h): output sample k of a stream is the
 // tap-ordered fma chain over raw[first[k % out_unit] + (k / out_unit) * in_unit + j]
 struct ResampleDev {
@@ -237,7 +244,7 @@ struct FrameStat {
   float best, cutoff, next_cutoff, adaptive_beam;
 };
 
-constexpr int kDecProf = 28;  // decoder phase-clock slots per stream (decoder.hip Prof)
+constexpr int kDecProf = 34;  // decoder phase-clock slots per stream (decoder.hip Prof)
 struct DecArgs {
   long long* prof;       // optional per-slot phase clocks [slots][kDecProf] (diagnostics)
   const int4* sinfo;     // per state {arc_begin, eps_begin, arc_end, final cost bits}

@@ -403,7 +403,8 @@ class Engine:
               "commit_links", "commit_eps_links", "commit_clear", "prune", "n_hbm_created",
               "n_created", "n_eps_rounds", "n_chunks", "frames", "prune_walk", "prune_remap",
               "prune_links", "prune_move", "n_prune_frames", "n_prunes", "exp_relax", "exp_links",
-              "kq_members", "kq_rank", "kq_replay", "kq_final")
+              "kq_members", "kq_rank", "kq_replay", "kq_final", "n_kq_frames", "n_kq_fast",
+              "n_kq_replayed", "n_kq_members", "n_kq_pops", "n_kq_pops_crit")
     PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19, 22, 23, 24, 25, 26, 27]  # clock slots (the rest count)
     PHASE_CLOCKS = PHASES[:11] + PHASES[16:20] + PHASES[22:28]
 
