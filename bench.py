@@ -181,10 +181,11 @@ def main():
     ap.add_argument("--streams", type=int, default=256, help="streams per GPU")
     ap.add_argument("--preset", default="la_small_en_us", help="synthetic model preset")
     ap.add_argument("--model", default=None, help="model directory (overrides --preset)")
-    ap.add_argument("--workload", choices=("api", "engine", "dynamic"), default="api",
+    ap.add_argument("--workload", choices=("api", "engine", "dynamic", "spk"), default="api",
                     help="api (default, the headline): test_gpu_batch.py through vosk_batch_*; "
                          "engine: the GPU engine stepped on HBM-resident audio; dynamic: "
-                         "variable-length utterances admitted per epoch across ranks")
+                         "variable-length utterances admitted per epoch across ranks; spk: "
+                         "config 5's speaker path, batched x-vector extraction")
     ap.add_argument("--engine-steps", type=int, default=20)
     ap.add_argument("--no-engine-line", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -220,6 +221,8 @@ def main():
         tdist.init_process_group(backend=backend)
         dist = tdist
 
+    if args.workload == "spk":
+        return run_spk(args, dist, rank, world)
     model = args.model or bench_model(rank, dist, args.preset)
     import vosk
     from vosk import engine as ve
@@ -633,6 +636,134 @@ def run_dynamic(args, model, dist, rank, world):
         dist.barrier()
         dist.destroy_process_group()
 
+
+
+# ---------------------------------------------------------------- config 5
+SPK_DIMS = dict(hidden=512, stats_dim=1500, embed=512, out=128)  # the sre16 x-vector recipe's sizes
+
+
+def spk_bench_model(rank, dist):
+    import make_synth_model
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamd_models", "bench_spk_xvector_v1")
+    if rank == 0 and not os.path.exists(os.path.join(cache, "README")):
+        tmp = cache + f".tmp{os.getpid()}"
+        make_synth_model.make_spk_model(tmp, **SPK_DIMS)
+        os.rename(tmp, cache)
+    if dist is not None:
+        dist.barrier()
+    return cache
+
+
+def _spk_cpu_init(model):
+    import oracle_xvector as OX
+    from threadpoolctl import threadpool_limits
+    _ORC["blas"] = threadpool_limits(1)  # one core per worker (the oracle's numpy GEMMs)
+    _ORC["spk"] = OX.OracleSpk(model)
+
+
+def _spk_cpu_job(w):
+    t = time.time()
+    _ORC["spk"].xvector(w, 0, [1] * 100000)
+    return time.time() - t
+
+
+def run_spk(args, dist, rank, world):
+    """BASELINE config 5's speaker path per GPU: 1024 streams / 8 GPUs = 128
+    utterances (10 s each, all frames selected) per step, extracted through
+    vamd_spk_extract_batch (speaker MFCC, sliding CMN, the frame-level TDNN
+    layers as one GEMM launch per layer over every utterance, statistics
+    pooling, head, whitening; xvector.h).  The value is audio seconds per
+    wall second over all ranks; the roofline is the frame-level layers'
+    fp32 GEMM flops over their HIP-event time on the extractor's stream."""
+    import ctypes as C
+    import vosk
+    from vosk import engine as ve
+    vosk.SetLogLevel(-1)
+    if ve.device_count() == 0:
+        raise SystemExit("bench.py: no HIP device visible")
+    model = spk_bench_model(rank, dist)
+    spk = vosk.SpkModel(model)
+    so = C.CDLL(os.path.join(os.path.dirname(vosk.__file__), "libvosk.so"))
+    so.vamd_spk_extract_batch.restype = C.c_int
+    so.vamd_spk_stats.restype = C.c_int
+    n = 1024 // 8 if args.streams == 256 else args.streams
+    secs = 10.0
+    base = load_wave()
+    waves = [np.ascontiguousarray(stream_audio(base, 20_000 + rank * n + i, int(secs * SR)), np.float32)
+             for i in range(n)]
+    keep = np.ones(int(secs * 100) // 3 + 8, np.int8)
+    wp = (C.c_void_p * n)(*[w.ctypes.data for w in waves])
+    kp = (C.c_void_p * n)(*([keep.ctypes.data] * n))
+    ln = np.array([len(w) for w in waves], np.int64)
+    rate = np.full(n, SR, np.int32)
+    first = np.zeros(n, np.int32)
+    nk = np.full(n, len(keep), np.int32)
+    cap = 1024
+    out = np.zeros((n, cap), np.float32)
+    nf = np.zeros(n, np.int32)
+    st = np.zeros(n, np.int32)
+
+    def step():
+        r = so.vamd_spk_extract_batch(C.c_void_p(spk._handle), n, wp, C.c_void_p(ln.ctypes.data),
+                                      C.c_void_p(rate.ctypes.data), C.c_void_p(first.ctypes.data), kp,
+                                      C.c_void_p(nk.ctypes.data), C.c_void_p(out.ctypes.data), cap,
+                                      C.c_void_p(nf.ctypes.data), C.c_void_p(st.ctypes.data))
+        if r != n or not (st > 0).all():
+            raise SystemExit(f"bench.py spk: extraction failed ({r}, {int((st > 0).sum())} vectors)")
+
+    def stats():
+        b, u, fl, ms = C.c_longlong(0), C.c_longlong(0), C.c_double(0), C.c_double(0)
+        so.vamd_spk_stats(C.c_void_p(spk._handle), C.byref(b), C.byref(u), C.byref(fl), C.byref(ms))
+        return b.value, u.value, fl.value, ms.value
+
+    steps = args.steps or 10
+    for _ in range(args.warmup):
+        step()
+    b0, u0, fl0, ms0 = stats()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.time()
+    for _ in range(steps):
+        step()
+    elapsed = _max_over_ranks(dist, time.time() - t0)
+    b1, u1, fl1, ms1 = stats()
+    audio = n * secs * steps * world
+    flops, lms = fl1 - fl0, ms1 - ms0
+    tf = flops / (lms * 1e-3) / 1e12 if lms > 0 else 0.0
+    res = {
+        "metric": "speaker x-vector extraction real-time factor (xRT), config 5 per-GPU share",
+        "value": round(audio / elapsed, 2), "unit": "xRT", "n_gpus": world, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic: test.wav tiled/perturbed per stream; random-init x-vector weights",
+        "config": {"workload": "spk_xvector_batch", "utterances_per_gpu_step": n, "utterance_seconds": secs,
+                   "model": "synthetic x-vector (tdnn 512 x4 -> 1500, stats pooling, embed 512, out 128)",
+                   "parallelism": f"dp{world}"},
+        "launch_sequences_per_step": (b1 - b0) / steps, "utterances_per_step": (u1 - u0) / steps,
+        "roofline": {"bound": "mfma", "kernel": "nnet GEMMs of the frame-level layers",
+                     "achieved": round(tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": tf / FP32_PEAK_TFLOPS, "traffic": None,
+                     "layers_ms_per_step": round(lms / steps, 3),
+                     "gflop_per_step": round(flops / steps / 1e9, 3)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import multiprocessing as mp
+        workers = cpu_workers()
+        sample = (waves * (1 + 8 * workers // n))[:8 * workers]
+        with mp.get_context("fork").Pool(workers, initializer=_spk_cpu_init, initargs=(model,)) as pool:
+            t = time.time()
+            pool.map(_spk_cpu_job, sample, chunksize=1)
+            wall = time.time() - t
+        res["cpu_baseline"] = {
+            "value": round(len(sample) * secs / wall, 3), "unit": "xRT", "cores": workers, "kind": "port",
+            "sample": f"{len(sample)} of the step's utterances ({secs:.0f} s each) through the oracle "
+                      f"(tests/oracle_xvector.py: numpy MFCC and frame layers, C CMN / pooling / head), "
+                      f"{workers} worker processes with one BLAS thread each"}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
 
 if __name__ == "__main__":
     main()

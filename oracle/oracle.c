@@ -460,7 +460,12 @@ long orc_resample(int rate_in, int rate_out, const float* x, long n, float* out,
   return nout;
 }
 
-int orc_kslices(int K) { return (K >= 512 && K % 256 == 0) ? K / 256 : 1; }
+int orc_kslices(int K) {  /* nnet_plan.h GemmKSlices: K / 256 down to a power of two, at most 8 */
+  if (K < 512 || K % 256) return 1;
+  int n = 1;
+  while (n < 8 && 2 * n <= K / 256) n *= 2;
+  return n;
+}
 
 float orc_logf(float x) {
   static const float C[11] = {1.000000000e+00f, -5.000000000e-01f, 3.333330154e-01f,

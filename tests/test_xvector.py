@@ -76,3 +76,17 @@ def test_spk_model_loads_through_the_abi(synth_spk, tmp_path):
     assert h
     lib.vosk_spk_model_free(h)
     assert not lib.vosk_spk_model_new(str(tmp_path / "missing").encode())
+
+
+def test_k_slice_rule():
+    """nnet_plan.h GemmKSlices / oracle orc_kslices: K / 256 rounded down to a
+    power of two, at most 8 (the streaming kernel's split-K reduction), so
+    every K of the recipes (768, 1536, 3000 ...) has a GPU kernel."""
+    import ctypes as C
+    import oracle_py
+    f = oracle_py.lib().orc_kslices
+    f.restype = C.c_int
+    want = {256: 1, 500: 1, 512: 2, 768: 2, 1024: 4, 1280: 4, 1536: 4, 2048: 8, 3072: 8, 4096: 8, 1000: 1}
+    for k, n in want.items():
+        assert f(k) == n, k
+        assert (k // n) % 32 == 0 or n == 1

@@ -111,3 +111,109 @@ def test_recognizer_result_carries_the_speaker_vector(vosk_mod, synth_model_noep
         rec2.AcceptWaveform(data[i:i + 8000])
     res2 = json.loads(rec2.FinalResult())
     assert res2.get("spk_frames") == nr
+
+
+def _extract_batch(vosk_mod, spk, reqs, cap=1024):
+    """reqs: (wave, rate, first, keep) per utterance -> vamd_spk_extract_batch"""
+    so = C.CDLL(os.path.join(os.path.dirname(vosk_mod.__file__), "libvosk.so"))
+    so.vamd_spk_extract_batch.restype = C.c_int
+    so.vamd_spk_extract_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    n = len(reqs)
+    ws = [np.ascontiguousarray(w, np.float32) for w, _, _, _ in reqs]
+    ks = [np.ascontiguousarray(k, np.int8) for _, _, _, k in reqs]
+    wp = (C.c_void_p * n)(*[w.ctypes.data for w in ws])
+    kp = (C.c_void_p * n)(*[k.ctypes.data for k in ks])
+    ln = np.array([len(w) for w in ws], np.int64)
+    rate = np.array([r for _, r, _, _ in reqs], np.int32)
+    first = np.array([f for _, _, f, _ in reqs], np.int32)
+    nk = np.array([len(k) for k in ks], np.int32)
+    out = np.zeros((n, cap), np.float32)
+    nf = np.zeros(n, np.int32)
+    st = np.zeros(n, np.int32)
+    r = so.vamd_spk_extract_batch(spk._handle, n, wp, ln.ctypes.data, rate.ctypes.data, first.ctypes.data, kp,
+                                  nk.ctypes.data, out.ctypes.data, cap, nf.ctypes.data, st.ctypes.data)
+    assert r == n
+    return [(out[i, :st[i]].copy() if st[i] > 0 else None, int(nf[i])) for i in range(n)]
+
+
+def _batch_cases(test_wave):
+    reqs = []
+    for i in range(24):
+        secs = [3.0, 6.5, 12.0, 25.0][i % 4] + 0.1 * i
+        w = perturbed_stream(test_wave, 900 + i, seconds=secs)
+        first = [0, 0, 61, 7][i % 3]
+        keep = [[1] * 10000, [1, 1, 0] * 4000, [0, 1] * 5000, [1] * 16 + [0] * 10000][(i // 2) % 4]
+        rate = 16000
+        if i % 6 == 5:
+            rate = [8000, 44100][(i // 6) % 2]
+            w = oracle_py.resample(w, 16000, rate)
+        reqs.append((w, rate, first, keep))
+    return reqs
+
+
+def test_xvector_batch_matches_oracle_and_single(vosk_mod, synth_spk, spk_oracle, test_wave):
+    """24 utterances of 3-27 s (some at 8 / 44.1 kHz, some with too few
+    frames) extracted as one batch: each vector equals the oracle's and the
+    one vamd_spk_extract gives for the utterance alone, bit for bit."""
+    spk = vosk_mod.SpkModel(synth_spk)
+    reqs = _batch_cases(test_wave)
+    got = _extract_batch(vosk_mod, spk, reqs)
+    nvec = 0
+    for i, ((w, rate, first, keep), (v, n)) in enumerate(zip(reqs, got)):
+        alone, na = _extract(vosk_mod, spk, w, first, keep, rate=rate)
+        assert n == na, i
+        if rate != 16000:
+            w = oracle_py.resample(w, rate, 16000)[:oracle_py.resample_num_outputs(rate, 16000, len(w), False)]
+        ref, nr = spk_oracle.xvector(w, first, keep)
+        assert n == nr, i
+        if ref is None:
+            assert v is None and alone is None, i
+            continue
+        nvec += 1
+        np.testing.assert_array_equal(v, ref, err_msg=f"utterance {i}")
+        np.testing.assert_array_equal(v, alone, err_msg=f"utterance {i}")
+    assert 12 <= nvec < len(reqs)
+
+
+def test_xvector_batch_split_by_ring_budget(vosk_mod, synth_spk, test_wave, monkeypatch):
+    """A ring budget below one long utterance's rings splits the batch into
+    several launch sequences; the vectors do not change."""
+    reqs = _batch_cases(test_wave)[:8]
+    spk = vosk_mod.SpkModel(synth_spk)
+    whole = _extract_batch(vosk_mod, spk, reqs)
+    monkeypatch.setenv("VOSK_AMD_XVEC_RING_MB", "1")
+    spk2 = vosk_mod.SpkModel(synth_spk)
+    split = _extract_batch(vosk_mod, spk2, reqs)
+    so = C.CDLL(os.path.join(os.path.dirname(vosk_mod.__file__), "libvosk.so"))
+    b, u = C.c_longlong(0), C.c_longlong(0)
+    assert so.vamd_spk_stats(C.c_void_p(spk2._handle), C.byref(b), C.byref(u), None, None) == 0
+    assert u.value == sum(1 for v, _ in whole if v is not None)
+    assert b.value > 1
+    for (v1, n1), (v2, n2) in zip(whole, split):
+        assert n1 == n2
+        if v1 is None:
+            assert v2 is None
+        else:
+            np.testing.assert_array_equal(v1, v2)
+
+
+@pytest.fixture(scope="module")
+def sre16_spk(tmp_path_factory):
+    """The sre16 x-vector recipe's sizes (tdnn 512 x4 -> 1500, stats pooling,
+    embedding 512, 128-dim output): K = 1536 layers split into 4 slices."""
+    import make_synth_model as msm
+    return msm.make_spk_model(str(tmp_path_factory.mktemp("spk_sre16")), hidden=512, stats_dim=1500,
+                              embed=512, out=128)
+
+
+def test_xvector_recipe_sized_model_matches_oracle(vosk_mod, sre16_spk, test_wave):
+    o = OX.OracleSpk(sre16_spk)
+    spk = vosk_mod.SpkModel(sre16_spk)
+    reqs = [(perturbed_stream(test_wave, 70 + i, seconds=4.0 + 3.0 * i), 16000, 0, [1, 1, 0] * 4000)
+            for i in range(3)]
+    got = _extract_batch(vosk_mod, spk, reqs)
+    for (w, _, first, keep), (v, n) in zip(reqs, got):
+        ref, nr = o.xvector(w, first, keep)
+        assert n == nr and ref is not None and len(ref) == 128
+        np.testing.assert_array_equal(v, ref)

@@ -31,14 +31,17 @@ void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s);
 void LaunchTraceback(const TraceArgs& a, int n, hipStream_t s);
 // speaker x-vectors (xvector.h): selection + sliding CMN, statistics
 // pooling, head ops, whitening
-void LaunchXvecCmn(const float* feats, int feat_mask, int D, const int* rows, int n, int window,
-                   float* out, int out_mask, int out_dim, hipStream_t s);
-void LaunchXvecPool(const float* rows, int ld, int r0, int n, int D, int nlog, int stddevs,
-                    float var_floor, float* out, hipStream_t s);
+// x-vector chain over a batch of utterances (XvecUtt per utterance; slot b
+// of the feature / input rings and row b of the pooled and head buffers)
+void LaunchXvecCmn(const float* feats, int feat_mask, int feat_slots, int D, const int* rows,
+                   const XvecUtt* utts, int nutt, int window, float* out, int out_mask,
+                   int out_slots, int out_dim, hipStream_t s);
+void LaunchXvecPool(const float* rows, int ld, const XvecUtt* utts, int nutt, int D, int nlog,
+                    int stddevs, float var_floor, float* out, int out_stride, hipStream_t s);
 void LaunchXvecAffine(const float* W, const float* b, const float* x, int K, int N, int kind,
-                      float* y, hipStream_t s);
-void LaunchXvecFinish(const float* x, const float* mean, int E, const float* T, int R, float* out,
-                      hipStream_t s);
+                      float* y, int stride, int nutt, hipStream_t s);
+void LaunchXvecFinish(const float* x, int xstride, const float* mean, int E, const float* T, int R,
+                      float* out, int nutt, hipStream_t s);
 void LaunchInitTables(int* state, unsigned long long* key, int* stamp, long long n, hipStream_t s);
 
 }  // namespace vamd

@@ -1266,17 +1266,27 @@ void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, h
 // ===========================================================================
 // Kaldi SlidingWindowCmn (feat/feature-functions.cc SlidingWindowCmnInternal
 // [K]) with the reference's options (centered 300-frame window, means only,
-// src/recognizer.cc:393-397), in double, over the selected frames: one lane
-// per feature dim walks the frames with the running window sum; out = x +
-// (-1 / frames) * sum.  Columns past D (input padding) are zero.
-__global__ void xvec_cmn_kernel(const float* feats, int feat_mask, int D, const int* rows, int n,
-                                int window, float* out, int out_mask, int out_dim) {
-  const int d = threadIdx.x;
+// src/recognizer.cc:393-397), in double, over each utterance's selected
+// frames: one block per utterance of the batch, one lane per feature dim
+// walking the frames with the running window sum; out = x + (-1 / frames) *
+// sum into the utterance's slot of the nnet input ring.  Columns past D
+// (input padding) are zero.
+__global__ void xvec_cmn_kernel(const float* feats, int feat_mask, int feat_slots, int D,
+                                const int* rows, const XvecUtt* utts, int window, float* out,
+                                int out_mask, int out_slots, int out_dim) {
+  const int d = threadIdx.x, b = blockIdx.x;
   if (d >= out_dim) return;
+  const XvecUtt u = utts[b];
+  const int n = u.nsel;
+  const int* rw = rows + u.rows0;
+  float* o = out + (size_t)b * out_dim + d;
+  const size_t ostride = (size_t)out_slots * out_dim;
   if (d >= D) {
-    for (int t = 0; t < n; t++) out[(size_t)(t & out_mask) * out_dim + d] = 0.0f;
+    for (int t = 0; t < n; t++) o[(size_t)(t & out_mask) * ostride] = 0.0f;
     return;
   }
+  const float* f = feats + (size_t)b * D + d;
+  const size_t fstride = (size_t)feat_slots * D;
   double sum = 0.0;
   int last_start = -1, last_end = -1;
   for (int t = 0; t < n; t++) {
@@ -1288,121 +1298,165 @@ __global__ void xvec_cmn_kernel(const float* feats, int feat_mask, int D, const 
       if (ws < 0) ws = 0;
     }
     if (last_start < 0) {
-      for (int u = ws; u < we; u++) sum = sum + (double)feats[(size_t)(rows[u] & feat_mask) * D + d];
+      for (int v = ws; v < we; v++) sum = sum + (double)f[(size_t)(rw[v] & feat_mask) * fstride];
     } else {
-      if (ws > last_start) sum = sum - (double)feats[(size_t)(rows[last_start] & feat_mask) * D + d];
-      if (we > last_end) sum = sum + (double)feats[(size_t)(rows[last_end] & feat_mask) * D + d];
+      if (ws > last_start) sum = sum - (double)f[(size_t)(rw[last_start] & feat_mask) * fstride];
+      if (we > last_end) sum = sum + (double)f[(size_t)(rw[last_end] & feat_mask) * fstride];
     }
     last_start = ws;
     last_end = we;
     const double alpha = -1.0 / (double)(we - ws);
-    const double x = (double)feats[(size_t)(rows[t] & feat_mask) * D + d];
-    out[(size_t)(t & out_mask) * out_dim + d] = (float)(x + alpha * sum);
+    const double x = (double)f[(size_t)(rw[t] & feat_mask) * fstride];
+    o[(size_t)(t & out_mask) * ostride] = (float)(x + alpha * sum);
   }
 }
 
 // statistics extraction + pooling (StatisticsExtractionComponent /
-// StatisticsPoolingComponent, nnet3/nnet-general-component.cc [K]) of rows
-// [r0, r0 + n): [log count x nlog], mean, stddev = sqrt(max(floor, E[x^2] -
+// StatisticsPoolingComponent, nnet3/nnet-general-component.cc [K]) of each
+// utterance's frame-level rows [pool_row0, pool_row0 + npool) (grid y = the
+// utterance): [log count x nlog], mean, stddev = sqrt(max(floor, E[x^2] -
 // mean^2)); double sums in row order
-__global__ void xvec_pool_kernel(const float* rows, int ld, int r0, int n, int D, int nlog,
-                                 int stddevs, float var_floor, float* out) {
+__global__ void xvec_pool_kernel(const float* rows, int ld, const XvecUtt* utts, int D, int nlog,
+                                 int stddevs, float var_floor, float* out, int out_stride) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d < nlog) out[d] = (float)log((double)n);
+  const XvecUtt u = utts[blockIdx.y];
+  const int n = u.npool;
+  float* o = out + (size_t)blockIdx.y * out_stride;
+  if (d < nlog) o[d] = (float)log((double)n);
   if (d >= D) return;
+  const float* r = rows + (size_t)u.pool_row0 * ld + d;
   double s = 0.0, s2 = 0.0;
   for (int t = 0; t < n; t++) {
-    const double x = (double)rows[(size_t)(r0 + t) * ld + d];
+    const double x = (double)r[(size_t)t * ld];
     s = s + x;
     s2 = s2 + x * x;
   }
   const double mean = s / (double)n;
-  out[nlog + d] = (float)mean;
+  o[nlog + d] = (float)mean;
   if (stddevs) {
     double var = s2 / (double)n - mean * mean;
     if (var < (double)var_floor) var = (double)var_floor;
-    out[nlog + D + d] = (float)sqrt(var);
+    o[nlog + D + d] = (float)sqrt(var);
   }
 }
 
 // one row of an affine map in the GEMM kernels' canonical order (nnet_plan.h
-// GemmKSlices; groups of eight walked 0,4,1,5,2,6,3,7), oracle canon_dot
-__device__ float xvec_canon_dot(const float* w, const float* x, int K) {
-  const int ns = (K >= 512 && K % 256 == 0) ? K / 256 : 1, kw = K / ns;  // GemmKSlices
-  float a = 0.0f;
+// GemmKSlices; groups of eight walked 0,4,1,5,2,6,3,7), oracle canon_dot,
+// for G inputs at once (x + g * xstride): each weight is loaded once and
+// every input keeps its own accumulator chain
+template <int G>
+__device__ void xvec_canon_dot(const float* w, const float* x, int xstride, int K, float* a) {
+  int ns = 1;  // GemmKSlices
+  if (K >= 512 && K % 256 == 0)
+    while (ns < 8 && 2 * ns <= K / 256) ns *= 2;
+  const int kw = K / ns;
   for (int z = 0; z < ns; z++) {
-    float p = 0.0f;
+    float p[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) p[g] = 0.0f;
     const int ke = (z + 1) * kw;
     for (int kg = z * kw; kg < ke; kg += 8)
       for (int i = 0; i < 8 && kg + i < ke; i++) {
         const int k = kg + 8 <= ke ? kg + ((i & 1) << 2) + (i >> 1) : kg + i;
-        p = __builtin_fmaf(x[k], w[k], p);
+        const float wk = w[k];
+#pragma unroll
+        for (int g = 0; g < G; g++) p[g] = __builtin_fmaf(x[(size_t)g * xstride + k], wk, p[g]);
       }
-    a = z == 0 ? p : a + p;
+#pragma unroll
+    for (int g = 0; g < G; g++) a[g] = z == 0 ? p[g] : a[g] + p[g];
   }
-  return a;
 }
 
-// head op of the pooled statistics: 1 affine (+ bias when b), 2 ReLU,
+constexpr int kXvecGroup = 4;  // utterances per thread of the head affine
+
+// head op of the pooled statistics, for the batch's utterances (grid y = a
+// group of kXvecGroup of them): 1 affine (+ bias when b), 2 ReLU,
 // 3 x * scale + offset
-__global__ void xvec_affine_kernel(const float* W, const float* b, const float* x, int K, int N,
-                                   int kind, float* y) {
+__global__ void xvec_affine_kernel(const float* W, const float* bias, const float* x, int K, int N,
+                                   int kind, float* y, int stride, int nutt) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int u0 = blockIdx.y * kXvecGroup;
   if (n >= N) return;
+  const int nu = nutt - u0 < kXvecGroup ? nutt - u0 : kXvecGroup;
+  const float* xu = x + (size_t)u0 * stride;
+  float* yu = y + (size_t)u0 * stride;
   if (kind == 1) {
-    const float a = xvec_canon_dot(W + (size_t)n * K, x, K);
-    y[n] = b ? a + b[n] : a;
+    float a[kXvecGroup];
+    if (nu == kXvecGroup) {
+      xvec_canon_dot<kXvecGroup>(W + (size_t)n * K, xu, stride, K, a);
+    } else {
+      for (int g = 0; g < nu; g++) xvec_canon_dot<1>(W + (size_t)n * K, xu + (size_t)g * stride, stride, K, a + g);
+    }
+    for (int g = 0; g < nu; g++) yu[(size_t)g * stride + n] = bias ? a[g] + bias[n] : a[g];
   } else if (kind == 2) {
-    y[n] = x[n] < 0.0f ? 0.0f : x[n];
+    for (int g = 0; g < nu; g++) {
+      const float v = xu[(size_t)g * stride + n];
+      yu[(size_t)g * stride + n] = v < 0.0f ? 0.0f : v;
+    }
   } else {
-    y[n] = x[n] * W[n] + b[n];
+    for (int g = 0; g < nu; g++) yu[(size_t)g * stride + n] = xu[(size_t)g * stride + n] * W[n] + bias[n];
   }
 }
 
-// whitening and length normalisation (src/recognizer.cc:406-416): x - mean,
-// transform rows (canonical order), norm = sqrt of the sequential float sum
-// of squares, ratio = norm / sqrt(R) and scale 1/ratio rounded through double
-__global__ __launch_bounds__(256) void xvec_finish_kernel(const float* x, const float* mean, int E,
-                                                          const float* T, int R, float* out) {
+// whitening and length normalisation (src/recognizer.cc:406-416), one block
+// per utterance: x - mean, transform rows (canonical order), norm = sqrt of
+// the sequential float sum of squares, ratio = norm / sqrt(R) and scale
+// 1/ratio rounded through double
+__global__ __launch_bounds__(256) void xvec_finish_kernel(const float* x, int xstride,
+                                                          const float* mean, int E, const float* T,
+                                                          int R, float* out) {
   __shared__ float xc[1024];
   __shared__ float scale;
-  for (int e = threadIdx.x; e < E; e += blockDim.x) xc[e] = x[e] - mean[e];
+  const float* xb = x + (size_t)blockIdx.x * xstride;
+  float* ob = out + (size_t)blockIdx.x * R;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) xc[e] = xb[e] - mean[e];
   __syncthreads();
-  for (int r = threadIdx.x; r < R; r += blockDim.x) out[r] = xvec_canon_dot(T + (size_t)r * E, xc, E);
+  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+    float a;
+    xvec_canon_dot<1>(T + (size_t)r * E, xc, 0, E, &a);
+    ob[r] = a;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     float ss = 0.0f;
-    for (int r = 0; r < R; r++) ss = ss + out[r] * out[r];
+    for (int r = 0; r < R; r++) ss = ss + ob[r] * ob[r];
     const float norm = sqrtf(ss);
     const float ratio = (float)((double)norm / sqrt((double)R));
     scale = (float)(1.0 / (double)ratio);
   }
   __syncthreads();
-  for (int r = threadIdx.x; r < R; r += blockDim.x) out[r] = out[r] * scale;
+  for (int r = threadIdx.x; r < R; r += blockDim.x) ob[r] = ob[r] * scale;
 }
 
-void LaunchXvecCmn(const float* feats, int feat_mask, int D, const int* rows, int n, int window,
-                   float* out, int out_mask, int out_dim, hipStream_t s) {
-  hipLaunchKernelGGL(xvec_cmn_kernel, dim3(1), dim3((out_dim + 63) / 64 * 64), 0, s, feats,
-                     feat_mask, D, rows, n, window, out, out_mask, out_dim);
+void LaunchXvecCmn(const float* feats, int feat_mask, int feat_slots, int D, const int* rows,
+                   const XvecUtt* utts, int nutt, int window, float* out, int out_mask,
+                   int out_slots, int out_dim, hipStream_t s) {
+  if (nutt <= 0) return;
+  hipLaunchKernelGGL(xvec_cmn_kernel, dim3(nutt), dim3((out_dim + 63) / 64 * 64), 0, s, feats,
+                     feat_mask, feat_slots, D, rows, utts, window, out, out_mask, out_slots,
+                     out_dim);
 }
 
-void LaunchXvecPool(const float* rows, int ld, int r0, int n, int D, int nlog, int stddevs,
-                    float var_floor, float* out, hipStream_t s) {
+void LaunchXvecPool(const float* rows, int ld, const XvecUtt* utts, int nutt, int D, int nlog,
+                    int stddevs, float var_floor, float* out, int out_stride, hipStream_t s) {
+  if (nutt <= 0) return;
   const int threads = D > nlog ? D : nlog;
-  hipLaunchKernelGGL(xvec_pool_kernel, dim3((threads + 255) / 256), dim3(256), 0, s, rows, ld, r0,
-                     n, D, nlog, stddevs, var_floor, out);
+  hipLaunchKernelGGL(xvec_pool_kernel, dim3((threads + 255) / 256, nutt), dim3(256), 0, s, rows,
+                     ld, utts, D, nlog, stddevs, var_floor, out, out_stride);
 }
 
 void LaunchXvecAffine(const float* W, const float* b, const float* x, int K, int N, int kind,
-                      float* y, hipStream_t s) {
-  hipLaunchKernelGGL(xvec_affine_kernel, dim3((N + 255) / 256), dim3(256), 0, s, W, b, x, K, N,
-                     kind, y);
+                      float* y, int stride, int nutt, hipStream_t s) {
+  if (nutt <= 0) return;
+  hipLaunchKernelGGL(xvec_affine_kernel, dim3((N + 255) / 256, (nutt + kXvecGroup - 1) / kXvecGroup),
+                     dim3(256), 0, s, W, b, x, K, N, kind, y, stride, nutt);
 }
 
-void LaunchXvecFinish(const float* x, const float* mean, int E, const float* T, int R, float* out,
-                      hipStream_t s) {
-  hipLaunchKernelGGL(xvec_finish_kernel, dim3(1), dim3(256), 0, s, x, mean, E, T, R, out);
+void LaunchXvecFinish(const float* x, int xstride, const float* mean, int E, const float* T, int R,
+                      float* out, int nutt, hipStream_t s) {
+  if (nutt <= 0) return;
+  hipLaunchKernelGGL(xvec_finish_kernel, dim3(nutt), dim3(256), 0, s, x, xstride, mean, E, T, R,
+                     out);
 }
 
 }  // namespace vamd

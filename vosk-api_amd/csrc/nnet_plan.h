@@ -77,7 +77,15 @@ struct Op {
 // right; the bias is added last.  Kaldi leaves the order to BLAS; fixing one
 // lets long reductions (K = 1024 bottlenecks) spread over more workgroups and
 // keeps GPU and oracle bit-identical.  Mirrored by orc_kslices() in oracle.c.
-inline int GemmKSlices(int K) { return (K >= 512 && K % 256 == 0) ? K / 256 : 1; }
+// The count is K / 256 rounded down to a power of two, at most 8 (the split-K
+// reduction of the streaming kernel): K = 1536 (a 768-dim TDNN-F layer
+// spliced twice, the sre16 x-vector layers) runs as 4 slices of 384.
+inline int GemmKSlices(int K) {
+  if (K < 512 || K % 256) return 1;
+  int n = 1;
+  while (n < 8 && 2 * n <= K / 256) n *= 2;
+  return n;
+}
 
 struct NnetPlan {
   int fpc = 0, fss = 1, opc = 0;  // frames per chunk, subsampling, outputs per chunk

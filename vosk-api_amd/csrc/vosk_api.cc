@@ -114,6 +114,49 @@ int vamd_spk_extract(VoskSpkModel* spk, const float* samples, long long n, int r
   API_CATCH(-1)
 }
 
+int vamd_spk_extract_batch(VoskSpkModel* spk, int count, const float* const* samples, const long long* n,
+                           const int* rate, const int* first_frame, const signed char* const* keep,
+                           const int* nkeep, float* out, int cap, int* num_frames, int* status) {
+  API_TRY
+  if (count < 0) VAMD_ERR("bad request count " << count);
+  SpkExtractor* ex = ((SpkModel*)spk)->Extractor();
+  if (ex->OutputDim() > cap) VAMD_ERR("output capacity");
+  std::vector<std::vector<char>> ks(count);
+  std::vector<std::vector<float>> xv(count);
+  std::vector<XvecRequest> rq(count);
+  std::vector<XvecRequest*> ptr(count);
+  for (int i = 0; i < count; i++) {
+    ks[i].assign(keep[i], keep[i] + nkeep[i]);
+    rq[i].samples = samples[i];
+    rq[i].n = n[i];
+    rq[i].rate = rate[i];
+    rq[i].first_frame = first_frame[i];
+    rq[i].keep = &ks[i];
+    rq[i].xvec = &xv[i];
+    ptr[i] = &rq[i];
+  }
+  ex->ExtractBatch(ptr);
+  for (int i = 0; i < count; i++) {
+    num_frames[i] = rq[i].num_frames;
+    status[i] = rq[i].ok ? (int)xv[i].size() : 0;
+    if (rq[i].ok) std::copy(xv[i].begin(), xv[i].end(), out + (size_t)i * cap);
+  }
+  return count;
+  API_CATCH(-1)
+}
+
+int vamd_spk_stats(VoskSpkModel* spk, long long* batches, long long* utterances, double* layer_flops,
+                   double* layer_ms) {
+  API_TRY
+  SpkExtractor* ex = ((SpkModel*)spk)->Extractor();
+  *batches = ex->Batches();
+  *utterances = ex->Utterances();
+  if (layer_flops) *layer_flops = ex->LayerFlops();
+  if (layer_ms) *layer_ms = ex->LayerMs();
+  return 0;
+  API_CATCH(-1)
+}
+
 void vosk_recognizer_set_max_alternatives(VoskRecognizer* r, int n) {
   if (r) ((Recognizer*)r)->SetMaxAlternatives(n);
 }

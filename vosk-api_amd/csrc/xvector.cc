@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 
@@ -224,6 +225,7 @@ SpkExtractor::SpkExtractor(std::shared_ptr<const SpkModelData> m, int device)
     : md_(std::move(m)), device_(device) {
   XV_HIPCHECK(hipSetDevice(device_));
   XV_HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  for (hipEvent_t& e : ev_) XV_HIPCHECK(hipEventCreate(&e));
   net_ = BuildXvectorNet(*md_, 64);
   MfccTables t = BuildMfccTables(md_->mfcc);
   mfcc_ = t.dev;
@@ -248,73 +250,135 @@ SpkExtractor::SpkExtractor(std::shared_ptr<const SpkModelData> m, int device)
     head_b_.push_back(h.b.empty() ? nullptr : Upload(h.b));
     head_max_ = std::max(head_max_, h.out);
   }
-  d_stats_ = (float*)DevAlloc(sizeof(float) * head_max_);
-  d_head_ = (float*)DevAlloc(sizeof(float) * 2 * head_max_);
   d_mean_ = Upload(md_->mean);
   d_transform_ = Upload(md_->transform.data);
-  d_xvec_ = (float*)DevAlloc(sizeof(float) * std::max(1, md_->transform.rows));
-  d_mjob_ = (MfccJob*)DevAlloc(sizeof(MfccJob));
 }
 
 SpkExtractor::~SpkExtractor() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   for (void* p : allocs_) (void)hipFree(p);
+  if (h_xvec_) (void)hipHostFree(h_xvec_);
+  for (hipEvent_t e : ev_)
+    if (e) (void)hipEventDestroy(e);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
-void SpkExtractor::Reserve(long long samples, int frames, int sel) {
-  const NnetPlan& plan = net_.frames;
-  if (samples + 1 > wave_cap_) {
-    long long c = 1024;
-    while (c < samples + 1) c <<= 1;
-    DevFree(d_wave_);
-    d_wave_ = (float*)DevAlloc(sizeof(float) * c);
-    wave_cap_ = c;
+namespace {
+long long Pow2Min(long long v, long long lo) {
+  long long c = lo;
+  while (c < v) c <<= 1;
+  return c;
+}
+// caps of one launch sequence: utterance slots, and the frame-level rings'
+// bytes (every node's ring holds an utterance's whole selection; the
+// operator may lower it through VOSK_AMD_XVEC_RING_MB)
+constexpr int kXvecMaxSlots = 256;
+long long RingBudgetBytes() {
+  const char* v = getenv("VOSK_AMD_XVEC_RING_MB");
+  const long long mb = v ? atoll(v) : 8192;
+  return std::max(1LL, mb) << 20;
+}
+}  // namespace
+
+long long SpkExtractor::RingBytesPerSlot(int jobs_per_slot) const {
+  long long dims = 0;
+  for (auto& nd : net_.frames.nodes) dims += nd.dim;
+  return (long long)net_.frames.RingFrames(jobs_per_slot) * dims * (long long)sizeof(float);
+}
+
+int SpkExtractor::TableIndex(int rate) {
+  for (size_t i = 0; i < table_rates_.size(); i++)
+    if (table_rates_[i] == rate) return (int)i;
+  const int spk_rate = (int)std::lround(md_->mfcc.samp_freq);
+  tables_.push_back(BuildResampleTable(rate, spk_rate));
+  table_rates_.push_back(rate);
+  std::vector<ResampleDev> devs;
+  for (const ResampleTable& t : tables_) {
+    ResampleDev td{};
+    td.first = Upload(t.first);
+    td.ntaps = Upload(t.ntaps);
+    td.w = Upload(t.w);
+    td.in_unit = t.in_unit;
+    td.out_unit = t.out_unit;
+    td.taps = t.taps;
+    devs.push_back(td);
   }
-  if (frames > feat_ring_) {
-    int c = 256;
-    while (c < frames) c <<= 1;
+  // the earlier tables' arrays are re-uploaded with the list (a handful of
+  // rates per process); the old ones stay allocated until the destructor
+  d_tables_ = Upload(devs);
+  return (int)tables_.size() - 1;
+}
+
+void SpkExtractor::Reserve(int slots, long long samples, long long raw, int frames, int sel,
+                           int jobs_per_slot, int jobs) {
+  const NnetPlan& plan = net_.frames;
+  const int R = std::max(1, md_->transform.rows);
+  const bool grow = slots > slot_cap_;
+  if (grow) {
+    slot_cap_ = (int)Pow2Min(slots, 1);
+    for (void* p : {(void*)d_utts_, (void*)d_mjobs_, (void*)d_stats_, (void*)d_head_, (void*)d_xvec_})
+      DevFree(p);
+    d_utts_ = (XvecUtt*)DevAlloc(sizeof(XvecUtt) * slot_cap_);
+    d_mjobs_ = (MfccJob*)DevAlloc(sizeof(MfccJob) * slot_cap_);
+    d_stats_ = (float*)DevAlloc(sizeof(float) * (size_t)slot_cap_ * head_max_);
+    d_head_ = (float*)DevAlloc(sizeof(float) * 2 * (size_t)slot_cap_ * head_max_);
+    d_xvec_ = (float*)DevAlloc(sizeof(float) * (size_t)slot_cap_ * R);
+    if (h_xvec_) (void)hipHostFree(h_xvec_);
+    h_xvec_ = nullptr;
+    XV_HIPCHECK(hipHostMalloc((void**)&h_xvec_, sizeof(float) * (size_t)slot_cap_ * R, hipHostMallocDefault));
+  }
+  if (grow || samples + 1 > wave_len_) {
+    wave_len_ = std::max(wave_len_, Pow2Min(samples + 1, 1024));
+    DevFree(d_wave_);
+    d_wave_ = (float*)DevAlloc(sizeof(float) * (size_t)slot_cap_ * wave_len_);
+  }
+  if (raw > 0 && (grow || raw + 1 > raw_len_)) {
+    raw_len_ = std::max(raw_len_, Pow2Min(raw + 1, 1024));
+    DevFree(d_raw_);
+    d_raw_ = (float*)DevAlloc(sizeof(float) * (size_t)slot_cap_ * raw_len_);
+  }
+  if (grow || frames > feat_ring_) {
+    feat_ring_ = std::max(feat_ring_, (int)Pow2Min(frames, 256));
     DevFree(d_feats_);
-    d_feats_ = (float*)DevAlloc(sizeof(float) * (size_t)c * md_->feat_dim);
-    feat_ring_ = c;
+    d_feats_ = (float*)DevAlloc(sizeof(float) * (size_t)feat_ring_ * slot_cap_ * md_->feat_dim);
   }
   if (sel > sel_cap_) {
-    int c = 256;
-    while (c < sel) c <<= 1;
+    sel_cap_ = (int)Pow2Min(sel, 256);
     DevFree(d_rows_);
-    d_rows_ = (int*)DevAlloc(sizeof(int) * c);
-    sel_cap_ = c;
+    d_rows_ = (int*)DevAlloc(sizeof(int) * sel_cap_);
   }
-  const int njobs = plan.priming_chunks + (sel + plan.fpc - 1) / plan.fpc;
-  const int ring = plan.RingFrames(njobs);
-  if (ring <= ring_ && njobs <= jobs_cap_) return;
-  // node rings, job list and frame-level output rows, and the op arguments
-  // that point into them
+  if (jobs > jobs_cap_) {
+    jobs_cap_ = (int)Pow2Min(jobs, 16);
+    DevFree(d_jobs_);
+    DevFree(d_out_);
+    d_jobs_ = (DevJob*)DevAlloc(sizeof(DevJob) * jobs_cap_);
+    d_out_ = (float*)DevAlloc(sizeof(float) * (size_t)jobs_cap_ * plan.fpc * net_.stats_in);
+  }
+  if (!grow && jobs_per_slot <= slot_jobs_cap_) return;
+  // node rings [ring][slot][dim] and the op arguments that point into them
+  slot_jobs_cap_ = std::max(slot_jobs_cap_, jobs_per_slot);
+  const int ring = plan.RingFrames(slot_jobs_cap_);
   for (float* p : ring_ptrs_) DevFree(p);
   ring_ptrs_.clear();
   std::vector<int> dims;
   for (auto& nd : plan.nodes) {
-    ring_ptrs_.push_back((float*)DevAlloc(sizeof(float) * (size_t)ring * nd.dim));
-    XV_HIPCHECK(hipMemset(ring_ptrs_.back(), 0, sizeof(float) * (size_t)ring * nd.dim));
+    const size_t bytes = sizeof(float) * (size_t)ring * slot_cap_ * nd.dim;
+    ring_ptrs_.push_back((float*)DevAlloc(bytes));
+    XV_HIPCHECK(hipMemset(ring_ptrs_.back(), 0, bytes));
     dims.push_back(nd.dim);
   }
   DevFree(d_ring_ptrs_);
   DevFree(d_ring_dims_);
   d_ring_ptrs_ = Upload(ring_ptrs_);
   d_ring_dims_ = Upload(dims);
-  DevFree(d_jobs_);
-  DevFree(d_out_);
-  d_jobs_ = (DevJob*)DevAlloc(sizeof(DevJob) * njobs);
-  d_out_ = (float*)DevAlloc(sizeof(float) * (size_t)njobs * plan.fpc * net_.stats_in);
   ring_ = ring;
-  jobs_cap_ = njobs;
   RingSet rs{};
   rs.base = d_ring_ptrs_;
   rs.dim = d_ring_dims_;
   rs.mask = ring - 1;
   rs.ring = ring;
-  rs.slots = 1;
+  rs.slots = slot_cap_;
   rs.input_node = plan.input_node;
   auto is_in = [&](int node) { return node == plan.input_node ? 1 : 0; };
   op_args_.clear();
@@ -389,109 +453,221 @@ void SpkExtractor::Reserve(long long samples, int frames, int sel) {
   }
 }
 
-bool SpkExtractor::Extract(const float* samples, long long n_in, int rate, int first_frame,
+bool SpkExtractor::Extract(const float* samples, long long n, int rate, int first_frame,
                            const std::vector<char>& keep, std::vector<float>* xvec, int* num_frames) {
-  std::lock_guard<std::mutex> lk(mu_);
+  if (rate <= 0) VAMD_ERR("bad sample rate " << rate);
+  if (n < 0) VAMD_ERR("bad sample count " << n);
+  XvecRequest r;
+  r.samples = samples;
+  r.n = n;
+  r.rate = rate;
+  r.first_frame = first_frame;
+  r.keep = &keep;
+  r.xvec = xvec;
+  Pending p{&r};
+  // group commit: the first caller to find no batch running takes the whole
+  // queue (its own request included) and runs it; the others wait
+  std::unique_lock<std::mutex> lk(qmu_);
+  queue_.push_back(&p);
+  while (!p.done) {
+    if (leader_) {
+      qcv_.wait(lk);
+      continue;
+    }
+    leader_ = true;
+    std::vector<Pending*> batch(queue_.begin(), queue_.end());
+    queue_.clear();
+    lk.unlock();
+    std::vector<XvecRequest*> reqs;
+    for (Pending* q : batch) reqs.push_back(q->r);
+    std::exception_ptr err;
+    try {
+      std::lock_guard<std::mutex> dev(mu_);
+      RunBatch(reqs);
+    } catch (...) {
+      err = std::current_exception();
+    }
+    lk.lock();
+    for (Pending* q : batch) {
+      q->done = true;
+      q->err = err;
+    }
+    leader_ = false;
+    qcv_.notify_all();
+  }
+  lk.unlock();
+  if (p.err) std::rethrow_exception(p.err);
+  *num_frames = r.num_frames;
+  return r.ok;
+}
+
+void SpkExtractor::ExtractBatch(const std::vector<XvecRequest*>& reqs) {
+  for (XvecRequest* r : reqs) {
+    if (r->rate <= 0) VAMD_ERR("bad sample rate " << r->rate);
+    if (r->n < 0) VAMD_ERR("bad sample count " << r->n);
+  }
+  std::lock_guard<std::mutex> dev(mu_);
+  RunBatch(reqs);
+}
+
+void SpkExtractor::RunBatch(const std::vector<XvecRequest*>& reqs) {
   XV_HIPCHECK(hipSetDevice(device_));
   const NnetPlan& plan = net_.frames;
   const int spk_rate = (int)std::lround(md_->mfcc.samp_freq);
-  long long n = n_in;
-  if (rate != spk_rate) {
-    if (rate <= 0) VAMD_ERR("bad sample rate " << rate);
-    if (table_rate_ != rate) {
-      table_ = BuildResampleTable(rate, spk_rate);
-      ResampleDev td{};
-      td.first = Upload(table_.first);
-      td.ntaps = Upload(table_.ntaps);
-      td.w = Upload(table_.w);
-      td.in_unit = table_.in_unit;
-      td.out_unit = table_.out_unit;
-      td.taps = table_.taps;
-      d_table_ = Upload(std::vector<ResampleDev>{td});
-      table_rate_ = rate;
-    }
-    n = table_.NumOutputSamples(n_in, false);
-  }
-  const int nfr = SpkNumFrames(md_->mfcc, n);
-  std::vector<int> rows;
-  for (int i = std::max(0, first_frame); i < nfr; i++) {
-    const size_t k = (size_t)((i - first_frame) / 3);
-    if (k < keep.size() && keep[k]) rows.push_back(i);
-  }
-  *num_frames = (int)rows.size();
-  if ((int)rows.size() < 50) return false;  // MIN_SPK_FEATS, src/recognizer.cc:354
-  const int sel = (int)rows.size();
-  Reserve(n, nfr, sel);
-  // the usable frame-level rows: computable from frames [0, sel) and inside
-  // the pooling window of output time 0
+  const int P = plan.priming_chunks, fpc = plan.fpc;
+  // the usable frame-level rows of an utterance: computable from its frames
+  // [0, sel) and inside the pooling window of output time 0
   const int r_lo = std::max(plan.left_context, -net_.pool_left);
-  const int r_hi = std::min(sel - 1 - plan.right_context, net_.pool_right);
-  if (r_lo > r_hi) return false;
-  if (rate == spk_rate) {
-    XV_HIPCHECK(hipMemcpyAsync(d_wave_, samples, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
-  } else {
-    if (n_in + 1 > raw_cap_) {
-      long long c = 1024;
-      while (c < n_in + 1) c <<= 1;
-      DevFree(d_raw_);
-      d_raw_ = (float*)DevAlloc(sizeof(float) * c);
-      raw_cap_ = c;
+  struct Utt {
+    XvecRequest* r;
+    long long n;  // samples at the speaker rate
+    int nfr, sel, rows0, njobs, table, r_hi;
+  };
+  std::vector<Utt> us;
+  std::vector<int> rows;
+  for (XvecRequest* r : reqs) {
+    r->ok = false;
+    r->num_frames = 0;
+    long long n = r->n;
+    int table = -1;
+    if (r->rate != spk_rate) {
+      table = TableIndex(r->rate);
+      n = tables_[table].NumOutputSamples(r->n, false);
     }
-    XV_HIPCHECK(hipMemcpyAsync(d_raw_, samples, sizeof(float) * n_in, hipMemcpyHostToDevice, stream_));
-    const int per = 4096;
-    const int nj = (int)((n + per - 1) / per);
-    if (nj > rjobs_cap_) {
-      DevFree(d_rjobs_);
-      d_rjobs_ = (ResampleJob*)DevAlloc(sizeof(ResampleJob) * nj);
-      rjobs_cap_ = nj;
+    const int nfr = SpkNumFrames(md_->mfcc, n);
+    const int rows0 = (int)rows.size();
+    const std::vector<char>& keep = *r->keep;
+    for (int i = std::max(0, r->first_frame); i < nfr; i++) {
+      const size_t k = (size_t)((i - r->first_frame) / 3);
+      if (k < keep.size() && keep[k]) rows.push_back(i);
     }
-    std::vector<ResampleJob> rj(nj);
-    for (int j = 0; j < nj; j++)
-      rj[j] = ResampleJob{0, j * per, (int)std::min<long long>(per, n - (long long)j * per), 0,
-                          (long long)j * per, n_in};
-    XV_HIPCHECK(hipMemcpyAsync(d_rjobs_, rj.data(), sizeof(ResampleJob) * nj, hipMemcpyHostToDevice, stream_));
-    LaunchResample(d_rjobs_, nj, d_table_, d_raw_, (int)raw_cap_, d_wave_, (int)wave_cap_, stream_);
-  }
-  MfccJob mj{0, 0, nfr, 0};
-  XV_HIPCHECK(hipMemcpyAsync(d_mjob_, &mj, sizeof(mj), hipMemcpyHostToDevice, stream_));
-  MfccDev m = mfcc_;
-  m.out = d_feats_;
-  RingSet fr{};
-  fr.mask = feat_ring_ - 1;
-  fr.ring = feat_ring_;
-  fr.slots = 1;
-  LaunchMfcc(m, d_mjob_, 1, nfr, d_wave_, (int)wave_cap_, fr, stream_);
-  XV_HIPCHECK(hipMemcpyAsync(d_rows_, rows.data(), sizeof(int) * sel, hipMemcpyHostToDevice, stream_));
-  LaunchXvecCmn(d_feats_, feat_ring_ - 1, md_->feat_dim, d_rows_, sel, 300,
-                ring_ptrs_[plan.input_node], ring_ - 1, md_->input_dim, stream_);
-  const int P = plan.priming_chunks, njobs = P + (sel + plan.fpc - 1) / plan.fpc;
-  std::vector<DevJob> jobs(njobs);
-  for (int j = 0; j < njobs; j++) jobs[j] = DevJob{0, (j - P) * plan.fpc, sel - 1, 0};
-  XV_HIPCHECK(hipMemcpyAsync(d_jobs_, jobs.data(), sizeof(DevJob) * njobs, hipMemcpyHostToDevice, stream_));
-  for (size_t i = 0; i < plan.ops.size(); i++) {
-    NnetOpArgs a = op_args_[i];
-    a.M = njobs * a.P;
-    a.jobs = d_jobs_;
-    a.llh = d_out_;
-    if (plan.ops[i].kind == Op::GEMM) LaunchNnetGemm(a, op_bk_[i], stream_);
-    else LaunchNnetGather(a, stream_);
-  }
-  // frame-level output row of time t: t + P * fpc (priming chunks first)
-  LaunchXvecPool(d_out_, net_.stats_in, r_lo + P * plan.fpc, r_hi - r_lo + 1, net_.stats_in,
-                 net_.num_log_count, net_.stddevs ? 1 : 0, net_.variance_floor, d_stats_, stream_);
-  const float* x = d_stats_;
-  for (size_t k = 0; k < net_.head.size(); k++) {
-    const auto& h = net_.head[k];
-    float* y = d_head_ + (k % 2) * head_max_;
-    LaunchXvecAffine(head_w_[k], head_b_[k], x, h.in, h.out, h.kind, y, stream_);
-    x = y;
+    const int sel = (int)rows.size() - rows0;
+    r->num_frames = sel;
+    const int r_hi = std::min(sel - 1 - plan.right_context, net_.pool_right);
+    if (sel < 50 || r_lo > r_hi) {  // MIN_SPK_FEATS, src/recognizer.cc:354
+      rows.resize(rows0);
+      continue;
+    }
+    us.push_back(Utt{r, n, nfr, sel, rows0, P + (sel + fpc - 1) / fpc, table, r_hi});
   }
   const int R = md_->transform.rows;
-  LaunchXvecFinish(x, d_mean_, net_.embed_dim, d_transform_, R, d_xvec_, stream_);
-  xvec->resize(R);
-  XV_HIPCHECK(hipMemcpyAsync(xvec->data(), d_xvec_, sizeof(float) * R, hipMemcpyDeviceToHost, stream_));
-  XV_HIPCHECK(hipStreamSynchronize(stream_));
-  return true;
+  const long long budget = RingBudgetBytes();
+  for (size_t a = 0; a < us.size();) {
+    // this launch sequence's utterances: up to the slot cap and ring budget
+    size_t b = a;
+    int max_jobs = 0;
+    while (b < us.size() && (int)(b - a) < kXvecMaxSlots) {
+      const int mj = std::max(max_jobs, us[b].njobs);
+      if (b > a && RingBytesPerSlot(mj) * (long long)Pow2Min((long long)(b - a + 1), 1) > budget) break;
+      max_jobs = mj;
+      b++;
+    }
+    const int B = (int)(b - a);
+    long long max_n = 0, max_raw = 0;
+    int max_nfr = 0, total_jobs = 0;
+    for (size_t k = a; k < b; k++) {
+      max_n = std::max(max_n, us[k].n);
+      if (us[k].table >= 0) max_raw = std::max(max_raw, us[k].r->n);
+      max_nfr = std::max(max_nfr, us[k].nfr);
+      total_jobs += us[k].njobs;
+    }
+    const int sel0 = us[a].rows0;
+    const int nsel = us[b - 1].rows0 + us[b - 1].sel - sel0;
+    Reserve(B, max_n, max_raw, max_nfr, nsel, max_jobs, total_jobs);
+    // samples (resampled per utterance where the rate differs)
+    const int per = 4096;
+    std::vector<ResampleJob> rj;
+    for (int k = 0; k < B; k++) {
+      const Utt& u = us[a + k];
+      if (u.table < 0) {
+        XV_HIPCHECK(hipMemcpyAsync(d_wave_ + (size_t)k * wave_len_, u.r->samples, sizeof(float) * u.n,
+                                   hipMemcpyHostToDevice, stream_));
+      } else {
+        XV_HIPCHECK(hipMemcpyAsync(d_raw_ + (size_t)k * raw_len_, u.r->samples, sizeof(float) * u.r->n,
+                                   hipMemcpyHostToDevice, stream_));
+        for (long long p0 = 0; p0 < u.n; p0 += per)
+          rj.push_back(ResampleJob{k, (int)p0, (int)std::min<long long>(per, u.n - p0), u.table, p0, u.r->n});
+      }
+    }
+    if (!rj.empty()) {
+      if ((int)rj.size() > rjobs_cap_) {
+        DevFree(d_rjobs_);
+        rjobs_cap_ = (int)Pow2Min((long long)rj.size(), 16);
+        d_rjobs_ = (ResampleJob*)DevAlloc(sizeof(ResampleJob) * rjobs_cap_);
+      }
+      XV_HIPCHECK(hipMemcpyAsync(d_rjobs_, rj.data(), sizeof(ResampleJob) * rj.size(), hipMemcpyHostToDevice,
+                                 stream_));
+      LaunchResample(d_rjobs_, (int)rj.size(), d_tables_, d_raw_, (int)raw_len_, d_wave_, (int)wave_len_,
+                     stream_);
+    }
+    // speaker MFCC of every frame of every utterance, slot k of the feature ring
+    std::vector<MfccJob> mj(B);
+    std::vector<XvecUtt> ut(B);
+    std::vector<DevJob> jobs;
+    int mrows = 0;
+    for (int k = 0; k < B; k++) {
+      const Utt& u = us[a + k];
+      mj[k] = MfccJob{k, 0, u.nfr, mrows};
+      mrows += u.nfr;
+      const int job0 = (int)jobs.size();
+      for (int j = 0; j < u.njobs; j++) jobs.push_back(DevJob{k, (j - P) * fpc, u.sel - 1, 0});
+      // frame-level output row of the utterance's time t: (job0 + P) * fpc + t
+      ut[k] = XvecUtt{u.rows0 - sel0, u.sel, (job0 + P) * fpc + r_lo, u.r_hi - r_lo + 1};
+    }
+    XV_HIPCHECK(hipMemcpyAsync(d_mjobs_, mj.data(), sizeof(MfccJob) * B, hipMemcpyHostToDevice, stream_));
+    XV_HIPCHECK(hipMemcpyAsync(d_utts_, ut.data(), sizeof(XvecUtt) * B, hipMemcpyHostToDevice, stream_));
+    XV_HIPCHECK(hipMemcpyAsync(d_rows_, rows.data() + sel0, sizeof(int) * nsel, hipMemcpyHostToDevice, stream_));
+    XV_HIPCHECK(hipMemcpyAsync(d_jobs_, jobs.data(), sizeof(DevJob) * jobs.size(), hipMemcpyHostToDevice,
+                               stream_));
+    MfccDev m = mfcc_;
+    m.out = d_feats_;
+    RingSet fr{};
+    fr.mask = feat_ring_ - 1;
+    fr.ring = feat_ring_;
+    fr.slots = slot_cap_;
+    LaunchMfcc(m, d_mjobs_, B, mrows, d_wave_, (int)wave_len_, fr, stream_);
+    LaunchXvecCmn(d_feats_, feat_ring_ - 1, slot_cap_, md_->feat_dim, d_rows_, d_utts_, B, 300,
+                  ring_ptrs_[plan.input_node], ring_ - 1, slot_cap_, md_->input_dim, stream_);
+    // the frame-level layers: every op over all utterances' jobs at once
+    // (HIP events on the extractor's stream bracket them: the GEMM roofline)
+    XV_HIPCHECK(hipEventRecord(ev_[0], stream_));
+    for (size_t i = 0; i < plan.ops.size(); i++) {
+      NnetOpArgs op = op_args_[i];
+      op.M = total_jobs * op.P;
+      op.jobs = d_jobs_;
+      op.llh = d_out_;
+      if (plan.ops[i].kind == Op::GEMM) {
+        LaunchNnetGemm(op, op_bk_[i], stream_);
+        gemm_flops_ += 2.0 * op.M * (double)op.N * (double)op.K;
+      } else {
+        LaunchNnetGather(op, stream_);
+      }
+    }
+    XV_HIPCHECK(hipEventRecord(ev_[1], stream_));
+    LaunchXvecPool(d_out_, net_.stats_in, d_utts_, B, net_.stats_in, net_.num_log_count, net_.stddevs ? 1 : 0,
+                   net_.variance_floor, d_stats_, head_max_, stream_);
+    const float* x = d_stats_;
+    for (size_t k = 0; k < net_.head.size(); k++) {
+      const auto& h = net_.head[k];
+      float* y = d_head_ + (k % 2) * (size_t)slot_cap_ * head_max_;
+      LaunchXvecAffine(head_w_[k], head_b_[k], x, h.in, h.out, h.kind, y, head_max_, B, stream_);
+      x = y;
+    }
+    LaunchXvecFinish(x, head_max_, d_mean_, net_.embed_dim, d_transform_, R, d_xvec_, B, stream_);
+    XV_HIPCHECK(hipMemcpyAsync(h_xvec_, d_xvec_, sizeof(float) * (size_t)B * R, hipMemcpyDeviceToHost, stream_));
+    XV_HIPCHECK(hipStreamSynchronize(stream_));
+    float ms = 0.0f;
+    XV_HIPCHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+    layers_ms_ += ms;
+    for (int k = 0; k < B; k++) {
+      XvecRequest* r = us[a + k].r;
+      r->xvec->assign(h_xvec_ + (size_t)k * R, h_xvec_ + (size_t)(k + 1) * R);
+      r->ok = true;
+    }
+    batches_++;
+    utterances_ += B;
+    a = b;
+  }
 }
 
 }  // namespace vamd

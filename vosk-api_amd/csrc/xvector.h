@@ -15,6 +15,9 @@
 // plan whose "output" is that node), the pooling (xvec_pool_kernel) and the
 // head / whitening (xvec_affine_kernel, xvec_finish_kernel).
 #pragma once
+#include <condition_variable>
+#include <deque>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -61,7 +64,27 @@ XvectorNet BuildXvectorNet(const SpkModelData& m, int frames_per_chunk);
 // Kaldi FeatureWindow frame count of an online (not flushed) front end.
 int SpkNumFrames(const MfccOptions& o, long long num_samples);
 
-// GPU x-vector extraction for one speaker model on one device (serialised).
+// One x-vector request (the arguments of GetSpkVector's extraction).
+struct XvecRequest {
+  const float* samples = nullptr;
+  long long n = 0;
+  int rate = 0;
+  int first_frame = 0;
+  const std::vector<char>* keep = nullptr;
+  std::vector<float>* xvec = nullptr;  // out
+  int num_frames = 0;                  // out: selected frames
+  bool ok = false;                     // out: a vector was produced
+};
+
+// GPU x-vector extraction for one speaker model on one device.  Requests are
+// batched across utterances: every kernel of the chain takes the utterance
+// as a grid dimension (one ring slot, one MFCC job list, one block of jobs
+// per utterance), and concurrent Extract callers are group-committed -- the
+// first caller to find the extractor idle runs everything queued (up to the
+// slot and ring-memory caps) as one launch sequence while later callers wait
+// for their result.  Each utterance's arithmetic is independent of the batch
+// it runs in (row-independent GEMM order, per-utterance reductions), so a
+// batched vector equals the one extracted alone bit for bit.
 class SpkExtractor {
  public:
   SpkExtractor(std::shared_ptr<const SpkModelData> m, int device);
@@ -74,11 +97,28 @@ class SpkExtractor {
   // min(rates)/2, 6 zeros, not flushed: the online feature's resampler).
   bool Extract(const float* samples, long long n, int rate, int first_frame,
                const std::vector<char>& keep, std::vector<float>* xvec, int* num_frames);
+  // a batch of requests, extracted together (split only by the caps)
+  void ExtractBatch(const std::vector<XvecRequest*>& reqs);
   int OutputDim() const { return md_->transform.rows; }
   const XvectorNet& net() const { return net_; }
+  // launch sequences run and utterances extracted so far (group-commit probe)
+  long long Batches() const { return batches_; }
+  long long Utterances() const { return utterances_; }
+  // frame-level layers: GEMM flops launched and their HIP-event time
+  double LayerFlops() const { return gemm_flops_; }
+  double LayerMs() const { return layers_ms_; }
 
  private:
-  void Reserve(long long samples, int frames, int sel);
+  struct Pending {
+    XvecRequest* r;
+    bool done = false;
+    std::exception_ptr err;
+  };
+  void RunBatch(const std::vector<XvecRequest*>& reqs);  // under mu_
+  void Reserve(int slots, long long samples, long long raw, int frames, int sel, int jobs_per_slot,
+               int jobs);
+  int TableIndex(int rate);  // resampling table of an input rate in d_tables_
+  long long RingBytesPerSlot(int jobs_per_slot) const;
   template <class T> T* Upload(const std::vector<T>& v);
   void* DevAlloc(size_t bytes);
   void DevFree(void* p);
@@ -95,35 +135,46 @@ class SpkExtractor {
   std::vector<const int*> patterns_;
   std::vector<NnetOpArgs> op_args_;
   std::vector<int> op_bk_;
-  int jobs_cap_ = 0;
-  // per-extraction buffers (grown on demand)
-  long long wave_cap_ = 0;
-  int frame_cap_ = 0, sel_cap_ = 0, ring_ = 0;
-  float* d_wave_ = nullptr;
-  float* d_raw_ = nullptr;       // input before resampling
-  long long raw_cap_ = 0;
-  int table_rate_ = 0;           // rate of the cached resampling table
-  ResampleDev* d_table_ = nullptr;
+  // per-batch buffers (grown on demand); slot b = the batch's utterance b
+  int slot_cap_ = 0;             // utterance slots of the rings and buffers
+  int jobs_cap_ = 0;             // nnet jobs over all slots
+  int slot_jobs_cap_ = 0;        // nnet jobs of one slot the rings hold
+  int ring_ = 0;
+  long long wave_len_ = 0;       // per-slot sample buffer (power of two)
+  long long raw_len_ = 0;        // per-slot raw input before resampling
+  int feat_ring_ = 0;            // per-slot MFCC rows (power of two)
+  int frame_cap_ = 0, sel_cap_ = 0, rjobs_cap_ = 0;
+  float* d_wave_ = nullptr;      // [slot][wave_len_]
+  float* d_raw_ = nullptr;       // [slot][raw_len_]
+  std::vector<ResampleTable> tables_;  // per input rate seen so far
+  std::vector<int> table_rates_;
+  ResampleDev* d_tables_ = nullptr;
   ResampleJob* d_rjobs_ = nullptr;
-  int rjobs_cap_ = 0;
-  float* d_feats_ = nullptr;     // [frame ring][1][feat_dim]
-  int feat_ring_ = 0;
-  int* d_rows_ = nullptr;        // selected frame indices
+  float* d_feats_ = nullptr;     // [frame ring][slot][feat_dim]
+  int* d_rows_ = nullptr;        // selected frame indices, per slot back to back
+  XvecUtt* d_utts_ = nullptr;    // [slot]
   float* d_out_ = nullptr;       // frame-level output rows [jobs * fpc][stats_in]
   DevJob* d_jobs_ = nullptr;
-  MfccJob* d_mjob_ = nullptr;
+  MfccJob* d_mjobs_ = nullptr;   // [slot]
   std::vector<float*> ring_ptrs_;
   float** d_ring_ptrs_ = nullptr;
   int* d_ring_dims_ = nullptr;
   std::vector<float*> head_w_, head_b_;
-  float* d_stats_ = nullptr;     // pooled statistics
-  float* d_head_ = nullptr;      // head ping-pong [2][head_max_]
+  float* d_stats_ = nullptr;     // pooled statistics [slot][head_max_]
+  float* d_head_ = nullptr;      // head ping-pong [2][slot][head_max_]
   float* d_mean_ = nullptr;
   float* d_transform_ = nullptr;
-  float* d_xvec_ = nullptr;
+  float* d_xvec_ = nullptr;      // [slot][R]
+  float* h_xvec_ = nullptr;      // pinned copy of d_xvec_
   int head_max_ = 0;
-  ResampleTable table_;
-  std::mutex mu_;
+  std::mutex mu_;                // the device buffers and stream
+  std::mutex qmu_;               // the request queue
+  std::condition_variable qcv_;
+  std::deque<Pending*> queue_;
+  bool leader_ = false;
+  long long batches_ = 0, utterances_ = 0;
+  double gemm_flops_ = 0.0, layers_ms_ = 0.0;
+  hipEvent_t ev_[2] = {nullptr, nullptr};
 };
 
 }  // namespace vamd
