@@ -181,7 +181,7 @@ int vamd_engine_decoder_totals(VamdEngine *e, long long *out6);
  * exp_items, exp_winners, eps, commit_toks, commit_links] (s_memtime clocks;
  * the full list is vosk/engine.py Engine.PHASES) */
 int vamd_engine_decoder_phases(VamdEngine *e, long long *out8);
-/* all decoder phase counters: writes min(cap, N) values, returns N (41) */
+/* all decoder phase counters: writes min(cap, N) values, returns N (43) */
 int vamd_engine_decoder_phases_n(VamdEngine *e, long long *out, int cap);
 /* the N counters per stream slot: out[max_streams][N] */
 int vamd_engine_decoder_phases_per_stream(VamdEngine *e, long long *out);

@@ -1095,8 +1095,9 @@ struct KaldiLds {
   int* stk;    // [kKM] the LIFO queue
   int2* adj;   // [kKE] (destination token, arc weight bits)
 };
-// member record in HBM past kKM: {slot, cost bits, offset, count, creation index, order}
-enum { kMSlot = 0, kMCost = 1, kMOff = 2, kMCnt = 3, kMC = 4, kMOrd = 5 };
+// member record in HBM past kKM: {slot, cost bits, offset, count, creation index, order,
+// component label, root rank} (the last two: the component replay)
+enum { kMSlot = 0, kMCost = 1, kMOff = 2, kMCnt = 3, kMC = 4, kMOrd = 5, kMComp = 6, kMRoot = 7 };
 __device__ __forceinline__ int* km_lds(const KaldiLds& K, int i, int f) {
   switch (f) {
     case kMSlot: return &K.ms[i];
@@ -1342,13 +1343,58 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     }
   }
   pr.mark(24);
-  // the initial queue in list order: sorted in LDS when it fits, else ranked
-  // by counting
+  // the initial queue in list order: sorted in LDS when it fits; else
+  // chunks of kKM sorted in LDS into the frontier scratch (after the keys
+  // past kKM already there), each key ranked by its chunk index plus a binary
+  // search in every other chunk (keys are unique: creation index); ranked by
+  // counting when the scratch is too small
+  long long* const SK = reinterpret_cast<long long*>(p.fg0);  // [max_tok] 8-byte entries over fg0, fg1
   if (n0 <= kKM) {
     bitonic_sort64(K.v0hi, K.v0lo, n0);
     for (int r = threadIdx.x; r < n0; r += DT) {
       const int v = AG_LD(&KO[K.v0lo[r]]);
       K.stk[r] = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+    }
+  } else if (2 * n0 - kKM <= a.max_tok) {
+    long long* const S = SK + (n0 - kKM);  // sorted chunks
+    const int nch = (n0 + kKM - 1) / kKM;
+    for (int ch = 0; ch < nch; ch++) {
+      const int c0 = ch * kKM, len = n0 - c0 < kKM ? n0 - c0 : kKM;
+      if (ch > 0) {
+        for (int r = threadIdx.x; r < len; r += DT) {
+          const unsigned long long k = (unsigned long long)AG_LD(&SK[c0 + r - kKM]);
+          K.v0hi[r] = (int)(unsigned)(k >> 32);
+          K.v0lo[r] = (int)(unsigned)k;
+        }
+        vm_drain();
+        __syncthreads();
+      }
+      bitonic_sort64(K.v0hi, K.v0lo, len);
+      for (int r = threadIdx.x; r < len; r += DT)
+        AG_ST(&S[c0 + r], (long long)(((unsigned long long)(unsigned)K.v0hi[r] << 32) | (unsigned)K.v0lo[r]));
+      vm_drain();
+      __syncthreads();
+    }
+    for (int x = threadIdx.x; x < n0; x += DT) {
+      const unsigned long long kx = (unsigned long long)AG_LD(&S[x]);
+      const int own = x / kKM;
+      int r = x - own * kKM;
+      for (int ch = 0; ch < nch; ch++) {
+        if (ch == own) continue;
+        int lo = ch * kKM, hi = lo + (n0 - lo < kKM ? n0 - lo : kKM);
+        const int first = lo;
+        while (lo < hi) {  // first entry of the chunk not below kx
+          const int mid = (lo + hi) >> 1;
+          if ((unsigned long long)AG_LD(&S[mid]) < kx) lo = mid + 1;
+          else hi = mid;
+        }
+        r += lo - first;
+      }
+      const int c = (int)(unsigned)(kx & 0xffffffffu);
+      const int v = AG_LD(&KO[c]);
+      const int i = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+      if (r < kKM) K.stk[r] = i;
+      else AG_ST(&KS[r - kKM], i);
     }
   } else
   for (int q = threadIdx.x; q < n0; q += DT) {
@@ -1385,17 +1431,35 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   // whose stack outgrows the lane's eight registers, or labels that do not
   // settle, send the frame to the sequential replay below.
   bool replayed = false;
-  if (fast && !(a.debug & (8 | 16))) {
-    int* comp = reinterpret_cast<int*>(K.v0lo);  // (the sort keys are consumed)
+  if (n0 <= a.max_tok && nm < (1 << 22) && !(a.debug & (8 | 16))) {
+    // members past kKM keep their component label and root in the HBM
+    // record (fields kMComp, kMRoot), their arcs past kKE in the HBM adjacency
+    int* comp = K.v0lo;    // members < kKM (the sort keys are consumed)
     unsigned* key = reinterpret_cast<unsigned*>(K.v0hi);
-    int* mroot = sh.tsrc;
+    int* mroot = sh.tsrc;  // members < kKM
     const float kInfL = __int_as_float(0x7f800000);
-    for (int i = threadIdx.x; i < nm; i += DT) comp[i] = i;
+    auto rec_at = [&](int i, int f) -> int* { return &KM[(long long)(i - kKM) * kKMRec + f]; };
+    auto cget = [&](int i) -> int { return i < kKM ? comp[i] : AG_LD(rec_at(i, kMComp)); };
+    auto rget = [&](int i) -> int { return i < kKM ? mroot[i] : AG_LD(rec_at(i, kMRoot)); };
+    auto rset = [&](int i, int v) {
+      if (i < kKM) mroot[i] = v;
+      else AG_ST(rec_at(i, kMRoot), v);
+    };
+    auto adj_at = [&](int e) -> int2 {
+      if (e < kKE) return K.adj[e];
+      const unsigned long long w = (unsigned long long)AG_LD(&reinterpret_cast<long long*>(KA)[e - kKE]);
+      return make_int2((int)(unsigned)w, (int)(unsigned)(w >> 32));
+    };
+    for (int i = threadIdx.x; i < nm; i += DT) {
+      if (i < kKM) comp[i] = i;
+      else AG_ST(rec_at(i, kMComp), i);
+    }
     if (threadIdx.x == 0) {
       sh.flag = 0;
       sh.kpop_sum = 0;
       sh.kpop_max = 0;
     }
+    vm_drain();
     __syncthreads();
     // connected components: minimum member index, propagated along the arcs
     bool settled = false;
@@ -1403,114 +1467,180 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
       if (threadIdx.x == 0) sh.kk = 0;
       __syncthreads();
       for (int u = threadIdx.x; u < nm; u += DT) {
-        const int e0 = K.mo[u], e1 = e0 + K.mn[u];
+        const int e0 = km_get(K, KM, u, kMOff), e1 = e0 + km_get(K, KM, u, kMCnt);
         for (int e = e0; e < e1; e++) {
-          const int d = K.adj[e].x;
+          const int d = adj_at(e).x;
           if (d < 0) continue;
-          const int cu = comp[u], cd = comp[d], m = cu < cd ? cu : cd;
-          if (cu > m) { atomicMin(&comp[u], m); sh.kk = 1; }
-          if (cd > m) { atomicMin(&comp[d], m); sh.kk = 1; }
+          const int cu = cget(u), cd = cget(d), m = cu < cd ? cu : cd;
+          if (cu > m) {
+            if (u < kKM) atomicMin(&comp[u], m);
+            else __hip_atomic_fetch_min(rec_at(u, kMComp), m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh.kk = 1;
+          }
+          if (cd > m) {
+            if (d < kKM) atomicMin(&comp[d], m);
+            else __hip_atomic_fetch_min(rec_at(d, kMComp), m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh.kk = 1;
+          }
         }
       }
+      vm_drain();
       __syncthreads();
       settled = sh.kk == 0;
       __syncthreads();
+      pr.count(36, 1);
     }
+    pr.mark(34);
+    pr.count(40, settled ? 0 : 1);
     if (settled) {
-      // the initial tokens by (component, processing rank)
-      for (int r = threadIdx.x; r < n0; r += DT) {
-        const int u = K.stk[r];
-        key[r] = ((unsigned)comp[u] << 20) | ((unsigned)(n0 - 1 - r) << 10) | (unsigned)u;
-      }
+      // the component of the initial token of each processing rank q (the
+      // initial token of rank q is the queue entry n0 - 1 - q: the top of
+      // the LIFO first), in the frontier scratch (free after the closure)
+      int* CQ = p.fg1;
+      auto stk_at = [&](int r) -> int { return r < kKM ? K.stk[r] : AG_LD(&KS[r - kKM]); };
+      for (int q = threadIdx.x; q < n0; q += DT) AG_ST(&CQ[q], cget(stk_at(n0 - 1 - q)));
+      vm_drain();
       __syncthreads();
-      bitonic_sort32(key, n0);
-      for (int i = threadIdx.x; i < nm; i += DT) mroot[i] = -1;
+      for (int i = threadIdx.x; i < nm; i += DT) rset(i, -1);
+      vm_drain();
       __syncthreads();
-      // one lane per component (the lane of its first initial token)
-      const int i = threadIdx.x;
-      if (i < n0 && (i == 0 || (key[i - 1] >> 20) != (key[i] >> 20))) {
-        const unsigned cmp = key[i] >> 20;
-        bool ovf = false;
+      // segments of kKM processing ranks in order: the queue restricted to a
+      // segment starts from the costs the earlier segments left
+      int created_total = 0;
+      for (int base = 0; base < n0 && sh.flag == 0; base += kKM) {
+        const int ns = n0 - base < kKM ? n0 - base : kKM;
+        for (int r = threadIdx.x; r < ns; r += DT) key[r] = ((unsigned)AG_LD(&CQ[base + r]) << 10) | (unsigned)r;
+        __syncthreads();
+        bitonic_sort32(key, ns);
+        pr.mark(41);
+        // one wave per component: the waves claim 64 sorted positions at a
+        // time and replay every component that starts there.  A popped
+        // token's arcs are read by the wave's lanes together (records, then
+        // the destinations' costs and arc counts), then applied in arc order
+        // (v_readlane; a later arc to the same token sees the new cost); the
+        // LIFO stack lives one entry per lane (depth 64).  A rank's creation
+        // count goes to K.v0lo[rank - base] (the labels were consumed into CQ).
+        const int lane = threadIdx.x & 63;
+        if (threadIdx.x == 0) sh.kk = 0;
+        __syncthreads();
         int npop = 0;
-        for (int ri = i; ri < n0 && (key[ri] >> 20) == cmp && !ovf; ri++) {
-          const unsigned kr = key[ri];
-          const int prank = (int)((kr >> 10) & 1023u);
-          int s0 = (int)(kr & 1023u), s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0, s7 = 0;
-          int sp = 1, j = 0;
-          while (sp > 0) {
-            --sp;
-            npop++;
-            const int u = sp == 0 ? s0 : sp == 1 ? s1 : sp == 2 ? s2 : sp == 3 ? s3
-                        : sp == 4 ? s4 : sp == 5 ? s5 : sp == 6 ? s6 : s7;
-            const float cu = K.mc[u];
-            if (!(cu < cutoff)) continue;
-            const int e0 = K.mo[u], e1 = e0 + K.mn[u];
-            for (int e = e0; e < e1; e++) {
-              const int2 rec = K.adj[e];
-              if (rec.x < 0) continue;
-              const float tot = cu + __int_as_float(rec.y);
-              if (!(tot < cutoff)) continue;
-              const float old = K.mc[rec.x];
-              if (!(tot < old)) continue;
-              if (old == kInfL) {  // FindOrAddToken creates it
-                K.mord[rec.x] = j++;
-                mroot[rec.x] = prank;
-              }
-              K.mc[rec.x] = tot;
-              if (K.mn[rec.x] > 0) {  // changed: re-queued
-                if (sp == 8) {
-                  ovf = true;
-                  break;
+        bool ovf = false;
+        while (!ovf) {
+          int c0 = 0;
+          if (lane == 0) c0 = atomicAdd(&sh.kk, 64);
+          c0 = __builtin_amdgcn_readfirstlane(c0);
+          if (c0 >= ns) break;
+          const int pos = c0 + lane;
+          const bool head = pos < ns && (pos == 0 || (key[pos - 1] >> 10) != (key[pos] >> 10));
+          unsigned long long hm = __ballot(head);
+          while (hm && !ovf) {
+            const int h = c0 + __ffsll((long long)hm) - 1;
+            hm &= hm - 1;
+            const unsigned cmp = key[h] >> 10;
+            for (int ri = h; ri < ns && (key[ri] >> 10) == cmp && !ovf; ri++) {
+              const int prank = (int)(key[ri] & 1023u);
+              int stk = lane == 0 ? stk_at(n0 - 1 - (base + prank)) : 0;
+              int sp = 1, j = 0;
+              while (sp > 0 && !ovf) {
+                --sp;
+                npop++;
+                const int u = __builtin_amdgcn_readlane(stk, sp);
+                const float cu = __int_as_float(km_get(K, KM, u, kMCost));
+                if (!(cu < cutoff)) continue;
+                const int off = km_get(K, KM, u, kMOff), cnt = km_get(K, KM, u, kMCnt);
+                for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
+                  const int kn = cnt - k0 < 64 ? cnt - k0 : 64;
+                  const int2 rec = lane < kn ? adj_at(off + k0 + lane) : make_int2(-1, 0);
+                  int oldl = __float_as_int(kInfL), cntl = 0;
+                  if (rec.x >= 0) {
+                    oldl = km_get(K, KM, rec.x, kMCost);
+                    cntl = km_get(K, KM, rec.x, kMCnt);
+                  }
+                  for (int k = 0; k < kn; k++) {
+                    const int d = __builtin_amdgcn_readlane(rec.x, k);
+                    if (d < 0) continue;
+                    const float tot = cu + __int_as_float(__builtin_amdgcn_readlane(rec.y, k));
+                    if (!(tot < cutoff)) continue;
+                    const float old = __int_as_float(__builtin_amdgcn_readlane(oldl, k));
+                    if (!(tot < old)) continue;
+                    if (rec.x == d) oldl = __float_as_int(tot);
+                    if (lane == k) {
+                      if (old == kInfL) {  // FindOrAddToken creates it
+                        km_set(K, KM, d, kMOrd, j);
+                        rset(d, prank);
+                      }
+                      km_set(K, KM, d, kMCost, __float_as_int(tot));
+                    }
+                    if (old == kInfL) j++;
+                    if (__builtin_amdgcn_readlane(cntl, k) > 0) {  // changed: re-queued
+                      if (sp == 64) {
+                        ovf = true;
+                        break;
+                      }
+                      if (lane == sp) stk = d;
+                      sp++;
+                    }
+                  }
                 }
-                s0 = sp == 0 ? rec.x : s0; s1 = sp == 1 ? rec.x : s1; s2 = sp == 2 ? rec.x : s2;
-                s3 = sp == 3 ? rec.x : s3; s4 = sp == 4 ? rec.x : s4; s5 = sp == 5 ? rec.x : s5;
-                s6 = sp == 6 ? rec.x : s6; s7 = sp == 7 ? rec.x : s7;
-                sp++;
               }
+              if (lane == 0) K.v0lo[prank] = j;
             }
-            if (ovf) break;
           }
-          K.stk[prank] = j;  // this initial token's creations (the sequential path rebuilds the stack)
         }
-        if (ovf) sh.flag = 1;
-        if (pr.on) {
-          atomicAdd(&sh.kpop_sum, npop);
-          atomicMax(&sh.kpop_max, npop);
+        if (lane == 0) {
+          if (ovf) sh.flag = 1;
+          if (npop > 0) {
+            atomicAdd(&sh.kpop_sum, npop);
+            atomicMax(&sh.kpop_max, npop);
+          }
+        }
+        vm_drain();
+        __syncthreads();
+        pr.mark(42);
+        if (sh.flag == 0) {
+          // creations per initial token in processing order, then the global
+          // creation order = (earlier segments) + (rank offset) + creation
+          // within the rank's expansion
+          int tot;
+          const int c = threadIdx.x < ns ? K.v0lo[threadIdx.x] : 0;
+          const int ex = kaldi_excl_sum(sh, c, 0, &tot);
+          __syncthreads();
+          if (threadIdx.x < ns) K.v0lo[threadIdx.x] = ex;
+          __syncthreads();
+          for (int m = threadIdx.x; m < nm; m += DT) {
+            const int r = rget(m);
+            if (r < 0) continue;
+            km_set(K, KM, m, kMOrd, km_get(K, KM, m, kMOrd) + created_total + K.v0lo[r]);
+            rset(m, -1);
+          }
+          created_total += tot;
+          vm_drain();
+          __syncthreads();
         }
       }
-      __syncthreads();
       if (sh.flag == 0) {
-        // creations per initial token in processing order (K.stk), then the
-        // global creation order = (processing rank offset) + creation within it
-        int tot;
-        const int c = threadIdx.x < n0 ? K.stk[threadIdx.x] : 0;
-        const int ex = kaldi_excl_sum(sh, c, 0, &tot);
-        __syncthreads();
-        if (threadIdx.x < n0) K.stk[threadIdx.x] = ex;
-        __syncthreads();
-        for (int m = threadIdx.x; m < nm; m += DT)
-          if (mroot[m] >= 0) K.mord[m] += K.stk[mroot[m]];
-        if (threadIdx.x == 0) sh.kn0 = tot;
+        if (threadIdx.x == 0) sh.kn0 = created_total;
         __syncthreads();
         replayed = true;
       }
     }
     if (!replayed) {  // back to the sequential replay: the members' queue state reset
       for (int m = threadIdx.x; m < nm; m += DT) {
-        const int c = K.mcr[m];
-        K.mc[m] = c >= 0 ? AG_LD(&KC[c]) : kInfL;
-        K.mord[m] = -1;
+        const int c = km_get(K, KM, m, kMC);
+        km_set(K, KM, m, kMCost, __float_as_int(c >= 0 ? AG_LD(&KC[c]) : kInfL));
+        km_set(K, KM, m, kMOrd, -1);
       }
-      // the initial queue again (the sort keys were consumed)
+      // the initial queue's sort keys again (consumed; K.stk / KS are intact)
+      vm_drain();
       __syncthreads();
       if (threadIdx.x == 0) sh.kn0 = 0;
       __syncthreads();
-      for (int m = threadIdx.x; m < nm; m += DT) {
-        const int c = K.mcr[m];
+      for (int m = threadIdx.x; m < nm && n0 <= kKM; m += DT) {
+        const int c = km_get(K, KM, m, kMC);
         if (c < 0) continue;
         const float c0 = AG_LD(&KC[c]);
         if (!(c0 < cutoff)) continue;
-        const int v = K.ms[m];
+        const int v = km_get(K, KM, m, kMSlot);
         const int4 si = a.sinfo[slot_state(t, T, v)];
         bool prod = false;
         for (int arc = si.y; arc < si.z && !prod; arc++) prod = c0 + __int_as_float(a.arcs[arc].y) < cutoff;
@@ -1521,15 +1651,15 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
       }
       vm_drain();
       __syncthreads();
-      bitonic_sort64(K.v0hi, K.v0lo, n0);
-      for (int r = threadIdx.x; r < n0; r += DT) {
-        const int v = AG_LD(&KO[K.v0lo[r]]);
-        K.stk[r] = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
-      }
-      vm_drain();
+      if (n0 <= kKM) bitonic_sort64(K.v0hi, K.v0lo, n0);
+      if (threadIdx.x == 0) sh.kn0 = n0;
       __syncthreads();
     }
   }
+  pr.mark(35);
+  pr.count(37, n0);
+  pr.count(38, n0 > kKM ? 1 : 0);
+  pr.count(39, (n0 <= kKM && !replayed && sh.flag) ? 1 : 0);
   if (replayed) {
   } else if (a.debug & 8) {  // development timing only: no replay (creation order = member order; wrong lists)
     for (int i = threadIdx.x; i < nm; i += DT) K.mord[i] = -1;

@@ -244,7 +244,7 @@ struct FrameStat {
   float best, cutoff, next_cutoff, adaptive_beam;
 };
 
-constexpr int kDecProf = 34;  // decoder phase-clock slots per stream (decoder.hip Prof)
+constexpr int kDecProf = 43;  // decoder phase-clock slots per stream (decoder.hip Prof)
 struct DecArgs {
   long long* prof;       // optional per-slot phase clocks [slots][kDecProf] (diagnostics)
   const int4* sinfo;     // per state {arc_begin, eps_begin, arc_end, final cost bits}

@@ -143,7 +143,7 @@ class SpkExtractor {
   long long wave_len_ = 0;       // per-slot sample buffer (power of two)
   long long raw_len_ = 0;        // per-slot raw input before resampling
   int feat_ring_ = 0;            // per-slot MFCC rows (power of two)
-  int frame_cap_ = 0, sel_cap_ = 0, rjobs_cap_ = 0;
+  int sel_cap_ = 0, rjobs_cap_ = 0;
   float* d_wave_ = nullptr;      // [slot][wave_len_]
   float* d_raw_ = nullptr;       // [slot][raw_len_]
   std::vector<ResampleTable> tables_;  // per input rate seen so far

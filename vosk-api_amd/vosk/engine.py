@@ -404,9 +404,11 @@ class Engine:
               "n_created", "n_eps_rounds", "n_chunks", "frames", "prune_walk", "prune_remap",
               "prune_links", "prune_move", "n_prune_frames", "n_prunes", "exp_relax", "exp_links",
               "kq_members", "kq_rank", "kq_replay", "kq_final", "n_kq_frames", "n_kq_fast",
-              "n_kq_replayed", "n_kq_members", "n_kq_pops", "n_kq_pops_crit")
-    PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19, 22, 23, 24, 25, 26, 27]  # clock slots (the rest count)
-    PHASE_CLOCKS = PHASES[:11] + PHASES[16:20] + PHASES[22:28]
+              "n_kq_replayed", "n_kq_members", "n_kq_pops", "n_kq_pops_crit", "kq_label", "kq_lanes",
+              "n_kq_label_iters", "n_kq_init", "n_kq_big_init", "n_kq_stack_ovf", "n_kq_unsettled",
+              "kq_seg_sort", "kq_seg_lanes")
+    PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19, 22, 23, 24, 25, 26, 27, 34, 35, 41, 42]  # clock slots
+    PHASE_CLOCKS = PHASES[:11] + PHASES[16:20] + PHASES[22:28] + PHASES[34:36] + PHASES[41:43]
 
     def decoder_phases_per_stream(self):
         """[max_streams, len(PHASES)] int64: decoder_phases() per stream slot."""
