@@ -204,6 +204,8 @@ def determinize(L, ilabel, olabel):
                 elif _better(n, sub[at[d]]):
                     sub[at[d]] = n
                     work.append(at[d])
+        # Kaldi's ConvertToMinimal: tokens with word links or a final cost
+        sub = [e for e in sub if fin[e[0]] != INF or any(olabel[links[li][2]] != 0 for li in outl[e[0]])]
         sub.sort(key=lambda e: e[0])
         return sub
 
@@ -263,6 +265,8 @@ def determinize(L, ilabel, olabel):
                     v.append(n)
         for w in sorted(by_word):
             sub = closure(by_word[w])
+            if not sub:
+                continue
             sub, tot, prefix = normalize(sub)
             dst, added = find_or_add(sub)
             if added:

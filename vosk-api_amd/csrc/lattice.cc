@@ -366,6 +366,21 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     for (int t = L.frame_begin[k]; t < L.frame_begin[k + 1]; t++) tframe[t] = k;
   std::vector<int> at_pos(N, -1);  // closure scratch: token -> element (reset after each closure)
   std::vector<char> pending;      // closure scratch: element queued
+  // per link: the last (string, extended string) of R.Succ through it -- a
+  // token reached by the same path from any subset has the same trie node,
+  // so most extensions repeat (the trie's hash table is large and cold)
+  std::vector<int> memo_in(NL, -1), memo_out(NL, -1);
+  auto extend = [&](int str, int li) {
+    if (lin[li] == 0) return str;
+    if (memo_in[li] == str) return memo_out[li];
+    const int n = R.Succ(str, lin[li]);
+    memo_in[li] = str;
+    memo_out[li] = n;
+    return n;
+  };
+  // closure work queue: elements bucketed by token frame (links go forward
+  // in time or stay in the frame), earliest frame first, FIFO within a frame
+  std::vector<std::vector<int>> fbucket(F + 1);
   auto closure = [&](std::vector<Elem>* sub, int base) {
     struct AtMap {
       std::vector<int>& pos;
@@ -382,39 +397,55 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
         for (int t : touched) pos[t] = -1;
       }
     } at{at_pos, {}};
-    std::priority_queue<std::pair<int, int>, std::vector<std::pair<int, int>>, std::greater<std::pair<int, int>>>
-        work;  // (frame, element), earliest frame first
     pending.assign(sub->size(), 1);
+    int fmin = F + 1, fmax = -1;
+    auto push = [&](int i) {
+      const int f = tframe[(*sub)[i].tok];
+      fbucket[f].push_back(i);
+      fmin = f < fmin ? f : fmin;
+      fmax = f > fmax ? f : fmax;
+    };
     for (int i = 0; i < (int)sub->size(); i++) {
       at.set((*sub)[i].tok, i);
-      work.push({tframe[(*sub)[i].tok], i});
+      push(i);
     }
-    while (!work.empty()) {
-      const int i = work.top().second;
-      work.pop();
-      pending[i] = 0;  // an element improved while queued is expanded once, at its best
-      const Elem e = (*sub)[i];
-      dbg_ext++;
-      for (int k = ob[e.tok]; k < oe[e.tok]; k++) {
-        const int li = ol[k];
-        const auto& l = L.links[li];
-        Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}),
-               lin[li] != 0 ? R.Succ(e.str, lin[li]) : e.str};
-        const int ei = at.find_idx(n.tok);
-        if (ei < 0) {
-          at.set(n.tok, (int)sub->size());
-          work.push({tframe[n.tok], (int)sub->size()});
-          sub->push_back(n);
-          pending.push_back(1);
-        } else if (ElemBetter(R, base, n, (*sub)[ei])) {
-          (*sub)[ei] = n;
-          if (!pending[ei]) {
-            pending[ei] = 1;
-            work.push({tframe[n.tok], ei});
+    for (int f = fmin; f <= fmax; f++) {
+      std::vector<int>& bq = fbucket[f];
+      for (size_t qi = 0; qi < bq.size(); qi++) {  // (grows while walked: same-frame links)
+        const int i = bq[qi];
+        pending[i] = 0;  // an element improved while queued is expanded once, at its best
+        const Elem e = (*sub)[i];
+        dbg_ext++;
+        for (int k = ob[e.tok]; k < oe[e.tok]; k++) {
+          const int li = ol[k];
+          const auto& l = L.links[li];
+          Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}), extend(e.str, li)};
+          const int ei = at.find_idx(n.tok);
+          if (ei < 0) {
+            at.set(n.tok, (int)sub->size());
+            sub->push_back(n);
+            pending.push_back(1);
+            push((int)sub->size() - 1);
+          } else if (ElemBetter(R, base, n, (*sub)[ei])) {
+            (*sub)[ei] = n;
+            if (!pending[ei]) {
+              pending[ei] = 1;
+              push(ei);
+            }
           }
         }
       }
+      bq.clear();
     }
+    // Kaldi's ConvertToMinimal: only tokens with word links or a final cost
+    // matter past the closure (transitions and finals); the subset's weight,
+    // common prefix and identity are those of the rest
+    size_t m = 0;
+    for (size_t i = 0; i < sub->size(); i++) {
+      const int t = (*sub)[i].tok;
+      if (oe[t] < ob[t + 1] || fin[t] != INFINITY) (*sub)[m++] = (*sub)[i];
+    }
+    sub->resize(m);
     std::sort(sub->begin(), sub->end(), [](const Elem& x, const Elem& y) { return x.tok < y.tok; });
   };
   // normalization: the best weight and the common string prefix move to the
@@ -493,8 +524,7 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
           const int li = ol[k];
           const auto& l = L.links[li];
           const int w = lout[li];
-          Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}),
-                 lin[li] != 0 ? R.Succ(e.str, lin[li]) : e.str};
+          Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}), extend(e.str, li)};
           auto& v = by_word[w];
           bool merged = false;
           for (auto& x : v)
@@ -511,6 +541,7 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
       auto t0 = dclk::now();
       closure(&sub, sbase);
       dt_clo += dms(t0);
+      if (sub.empty()) continue;  // a dead end (cannot occur on a pruned lattice)
       LW tot;
       std::vector<int> prefix;
       t0 = dclk::now();
