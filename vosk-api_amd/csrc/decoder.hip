@@ -2271,10 +2271,19 @@ __device__ void prune_check(const DecArgs& a, const LatFrame* LF, const int4* LK
   __syncthreads();
 }
 
+// fin: the segment's last prune (Kaldi FinalizeDecoding: PruneForwardLinksFinal
+// then every frame with delta 0): the frontier's extra costs are its tokens'
+// cost (plus the final cost when any token is final) above the best such
+// total, and the walk goes back to frame 0.  Links into frontier tokens past
+// the beam are dropped; the frontier tokens themselves stay (the current-token
+// arrays keep their positions).
+template <bool fin>
 __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, DecSlot& st, const DecPtrs& p, int slot,
-                                              Prof& pr) {
+                                              Prof& pr, bool use_final = false) {
   const int F = st.frames;
   if (F <= 0 || F >= a.lat_frame_cap || st.err) return;
+  if constexpr (fin)
+    if (a.links == nullptr || st.lat_ovf) return;
   LatFrame* LF = a.lat_frames + (long long)slot * a.lat_frame_cap;
   float* X = a.extra + (long long)slot * a.arena_cap;
   int* R = a.remap + (long long)slot * a.arena_cap;
@@ -2287,12 +2296,56 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
   const int pf = st.prune_from;
   load_frame(sh, LF, F, -1);
   const int tbF = sh.fr.tok_base, endF = sh.fr.tok_base + sh.fr.ntok;
-  for (int t = tbF + threadIdx.x; t < endF; t += DT) AG_ST(&X[t], 0.0f);
+  if constexpr (!fin) {
+    for (int t = tbF + threadIdx.x; t < endF; t += DT) AG_ST(&X[t], 0.0f);
+  } else {
+    float bn = kInf, bf = kInf;
+    for (int t = tbF + threadIdx.x; t < endF; t += DT) {
+      const int4 r = ag_ld4(&AR[t]);
+      if (r.x == -2) continue;  // a dead list entry
+      const float c = __int_as_float(r.z);
+      bn = fminf(bn, c);
+      bf = fminf(bf, c + __int_as_float(a.sinfo[r.w].w));
+    }
+    bn = block_min_f(sh, bn);
+    bf = block_min_f(sh, bf);
+    const bool use_f = use_final && bf != kInf;
+    const float best = use_f ? bf : bn;
+    for (int t = tbF + threadIdx.x; t < endF; t += DT) {
+      const int4 r = ag_ld4(&AR[t]);
+      float x = kInf;
+      if (r.x != -2) {
+        const float c = __int_as_float(r.z), fc = use_f ? __int_as_float(a.sinfo[r.w].w) : 0.0f;
+        if (fc != kInf) x = fmaxf(0.0f, (c + fc) - best);
+      }
+      AG_ST(&X[t], x);
+    }
+    __syncthreads();
+    // through the frontier's epsilon links (a non-final token that reaches a
+    // final one within the frame has that token's extra cost plus the link's)
+    FixRound fx;
+    fx.base = 3 * (F & 1);
+    if (threadIdx.x == 0) sh.fl[fx.base] = 0;
+    __syncthreads();
+    do {
+      fx.begin(sh);
+      for (long long i = sh.fr.link_begin + threadIdx.x; i < sh.fr.link_end; i += DT) {
+        const int src = LK[i].x;
+        if (src < tbF) continue;
+        const float le = AG_LD(&X[LK[i].y]) + __int_as_float(LDd[i]);
+        if (le <= beamp && le < AG_LD(&X[src])) {
+          atomic_min_pos(&X[src], le);
+          fx.mark(sh);
+        }
+      }
+    } while (fx.end(sh));
+  }
   int kmin = F;
   // Frames below prune_from are revisited at most prune_revisit deep: a
   // frame past that keeps the extra costs of its last walk, which are never
-  // above the current ones (safe, it is only pruned less).
-  const int kstop = pf - a.prune_revisit > 0 ? pf - a.prune_revisit : 0;
+  // above the current ones (safe, it is only pruned less).  The final prune
+  // walks every frame.
+  const int kstop = fin ? 0 : (pf - a.prune_revisit > 0 ? pf - a.prune_revisit : 0);
   for (int k = F - 1; k >= kstop; k--) {
     // frame records read by every thread (nothing writes them during this walk)
     const LatFrame fk = LF[k], fk1 = LF[k + 1];
@@ -2360,7 +2413,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
       // this frame moved by more than it, the frames below keep theirs.  A
       // kept extra cost is never above the current one (they only grow), so
       // it prunes less, never more.  Backpointer marks compare exactly.
-      const float delta = lat ? a.lattice_beam * 0.1f : 0.0f;
+      const float delta = (lat && !fin) ? a.lattice_beam * 0.1f : 0.0f;
       for (int t = tb + threadIdx.x; t < te; t += DT)
         if (fabsf(AG_LD(&X[t]) - __int_as_float(AG_LD(&R[t]))) > delta) sh.fl[cf] = 1;
       __syncthreads();
@@ -2499,8 +2552,16 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
           x[u] = AG_LD(&X[t]);
           if (rec[u].x >= wb) {
             const int np = AG_LD(&R[rec[u].x - wb]);
-            if (np & kDropped) sh.bad |= 16;
-            rec[u].x = np & ~kDropped;
+            if (!(np & kDropped)) {
+              rec[u].x = np;
+            } else if (fin && t >= tbF) {
+              // the final prune keeps every frontier token, also those past
+              // the beam whose predecessors it dropped: no backpointer
+              rec[u].x = -1;
+            } else {
+              sh.bad |= 16;
+              rec[u].x = np & ~kDropped;
+            }
           }
         }
       }
@@ -2855,7 +2916,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   // PruneActiveTokens every prune_interval frames (at the end of a launch)
   if (a.prune_interval > 0 && !st.err && st.frames - st.last_prune >= a.prune_interval) {
     pr.mark(10);
-    prune_segment(a, sh, st, p, slot, pr);
+    prune_segment<false>(a, sh, st, p, slot, pr);
     __syncthreads();
     if (sh.bad) st.err |= sh.bad;
   }
@@ -2863,6 +2924,34 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   if (threadIdx.x == 0) a.slots[slot] = st;
   if (pr.on)
     for (int i = 0; i < kDecProf; i++) a.prof[slot * kDecProf + i] += pr.acc[i];
+}
+
+// the final prune of segments that end (before their lattice copy), one
+// workgroup per listed stream
+__global__ __launch_bounds__(DT) void prune_final_kernel(DecArgs a, const int* slots, int use_final) {
+  __shared__ DecShared sh;
+  const int slot = slots[blockIdx.x];
+  DecSlot st = a.slots[slot];
+  DecPtrs p;
+  p.cs = a.cur_state + (long long)slot * a.max_tok;
+  p.cc = a.cur_cost + (long long)slot * a.max_tok;
+  p.cp = a.cur_pos + (long long)slot * a.max_tok;
+  p.arena = a.arena + (long long)slot * a.arena_cap;
+  p.fg0 = a.front_g + ((long long)slot * 2) * a.max_tok;
+  p.fg1 = p.fg0 + a.max_tok;
+  Prof pr;
+  pr.init(false);
+  if (threadIdx.x == 0) sh.bad = 0;
+  __syncthreads();
+  prune_segment<true>(a, sh, st, p, slot, pr, use_final != 0);
+  __syncthreads();
+  if (sh.bad) st.err |= sh.bad;
+  if (threadIdx.x == 0) a.slots[slot] = st;
+}
+
+void LaunchPruneFinal(const DecArgs& a, const int* slots, int n, bool use_final, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(prune_final_kernel, dim3(n), dim3(DT), 0, s, a, slots, use_final ? 1 : 0);
 }
 
 int DecoderLdsProbe() { return kMaxProbe; }

@@ -1733,6 +1733,16 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
   if (!copy_ev_) HIPCHECK(hipEventCreateWithFlags(&copy_ev_, hipEventDisableTiming));
   if (!h_copy_slots_)  // own snapshot: h_slots_ may be the target of a decoder batch's read-back
     HIPCHECK(hipHostMalloc((void**)&h_copy_slots_, sizeof(DecSlot) * slots_.size(), hipHostMallocDefault));
+  // the segments end (each stream's decoder restarts after its copy): their
+  // last lattice prune (final costs, every frame) on the copy stream, so the
+  // copies below take the pruned records
+  const bool final_prune = !getenv("VOSK_AMD_FINAL_PRUNE") || atoi(getenv("VOSK_AMD_FINAL_PRUNE")) != 0;
+  if (final_prune) {
+    if (!d_prune_slots_) d_prune_slots_ = (int*)DevAlloc(sizeof(int) * slots_.size());
+    HIPCHECK(hipMemcpyAsync(d_prune_slots_, slots.data(), sizeof(int) * slots.size(), hipMemcpyHostToDevice,
+                            copy_stream_));
+    LaunchPruneFinal(dec_, d_prune_slots_, (int)slots.size(), true, copy_stream_);
+  }
   HIPCHECK(hipMemcpyAsync(h_copy_slots_, d_slots_, sizeof(DecSlot) * slots_.size(), hipMemcpyDeviceToHost,
                           copy_stream_));
   HIPCHECK(hipStreamSynchronize(copy_stream_));

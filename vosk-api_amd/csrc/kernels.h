@@ -28,6 +28,8 @@ void LaunchIvectorStats(const IvArgs& a, const float* ll, int rows, int njobs, h
 // token passing (decoder.hip)
 int DecoderLdsProbe();  // default LDS probe limit of the frame table
 void LaunchDecode(const DecArgs& a, int njobs, hipStream_t s);
+// the last lattice prune of ending segments (slots: device list of n streams)
+void LaunchPruneFinal(const DecArgs& a, const int* slots, int n, bool use_final, hipStream_t s);
 void LaunchTraceback(const TraceArgs& a, int n, hipStream_t s);
 // speaker x-vectors (xvector.h): selection + sliding CMN, statistics
 // pooling, head ops, whitening
