@@ -76,6 +76,12 @@ int vamd_spk_stats(VoskSpkModel *spk, long long *batches, long long *utterances,
 int vamd_lattice_set_rescore(const char *g_fst, const char *g_carpa);
 float vamd_carpa_logprob(const char *g_carpa, int word, const int *hist, int nhist);
 
+/* host-only: with ntids > 0, vamd_lattice_words_json determinizes as the
+ * reference's GetLattice (DeterminizeLatticePhonePrunedWrapper: a phone +
+ * word pass, then words; per transition-id its phone and whether it is a
+ * phone's first transition-id); ntids == 0: word level only (the default). */
+int vamd_lattice_set_phones(const int *tid2phone, const signed char *tid_first, int ntids);
+
 /* host-only: the result pipeline over a state-level lattice (the arrays of
  * vamd_stream_lattice; arc_ilabel / arc_olabel index the graph's arcs):
  * lattice-beam pruning, word determinization, graph scaling, word alignment

@@ -163,25 +163,105 @@ def _better(e, f):  # (weight, string) order
     return e[2] < f[2]
 
 
-def determinize(L, ilabel, olabel):
-    """-> (arcs per state [(word, next, g, a, tids)], finals [(g, a, tids) | None]),
-    states topologically sorted as the C++ does."""
+def _graph_from_raw(L, ilabel, olabel):
+    """The determinizer's input from a raw lattice: (n, links [(src, dst, tid,
+    label, g, a)], finals [(g, a) | None], start)."""
     N = len(L["tok_state"])
     F = L["num_frames"]
     fb = L["frame_begin"]
-    if N == 0:
+    links = [(s, d, int(ilabel[a]), int(olabel[a]), g, x) for s, d, a, g, x in
+             zip(L["link_src"].tolist(), L["link_dst"].tolist(), L["link_arc"].tolist(),
+                 L["link_graph"], L["link_ac"])]
+    fin = [None] * N
+    for t in range(fb[F], fb[F + 1]):
+        c = F32(0) if len(L["final_cost"]) == 0 else L["final_cost"][t - fb[F]]
+        fin[t] = None if c == INF else (c, F32(0))
+    start = next((t for t in range(fb[0], fb[1]) if L["tok_cost"][t] == 0.0), -1) if N else -1
+    return N, links, fin, start
+
+
+def determinize(L, ilabel, olabel):
+    """-> (arcs per state [(word, next, g, a, tids)], finals [(g, a, tids) | None]),
+    states topologically sorted as the C++ does (word level only)."""
+    return _determinize(*_graph_from_raw(L, ilabel, olabel))
+
+
+def determinize_phone(L, ilabel, olabel, tid2phone, tid_first):
+    """Kaldi DeterminizeLatticePhonePrunedWrapper (the reference's GetLattice,
+    src/recognizer.cc:678): DeterminizeLatticeInsertPhones (phone label
+    first_phone_label + phone at a phone's first transition-id -- HMM state 0,
+    not a self-loop -- on the link when it has no word, else on a new link
+    after it), determinization on phones + words, the result written out as a
+    lattice (LatticeDeterminizerPruned::Output: a chain per arc string, label
+    and weight on the first link; a final string as a chain to a new final
+    state), DeterminizeLatticeDeletePhones, then word-level determinization."""
+    n, links, fin, start = _graph_from_raw(L, ilabel, olabel)
+    first = max([1] + [l[3] + 1 for l in links])
+    out = []
+    for (s, d, t, w, g, a) in links:
+        if t <= 0 or t >= len(tid_first) or not tid_first[t]:
+            out.append((s, d, t, w, g, a))
+            continue
+        ph = first + int(tid2phone[t])
+        if w == 0:
+            out.append((s, d, t, ph, g, a))
+        else:
+            x = n
+            n += 1
+            fin.append(None)
+            out.append((s, x, t, w, g, a))
+            out.append((x, d, 0, ph, F32(0), F32(0)))
+    W, Fi = _determinize(n, out, fin, start)
+    if not W:
+        return W, Fi
+    S = len(W)
+    lab = lambda w: 0 if w >= first else w
+    n2, links2, fin2 = S, [], [None] * S
+    for s in range(S):
+        for (w, d, g, a, tids) in W[s]:
+            if not tids:
+                links2.append((s, d, 0, lab(w), g, a))
+                continue
+            cur = s
+            for i, t in enumerate(tids):
+                if i + 1 == len(tids):
+                    nx = d
+                else:
+                    nx = n2
+                    n2 += 1
+                    fin2.append(None)
+                links2.append((cur, nx, int(t), lab(w) if i == 0 else 0, g if i == 0 else F32(0),
+                               a if i == 0 else F32(0)))
+                cur = nx
+        f = Fi[s]
+        if f is None:
+            continue
+        if not f[2]:
+            fin2[s] = (f[0], f[1])
+            continue
+        cur = s
+        for i, t in enumerate(f[2]):
+            nx = n2
+            n2 += 1
+            fin2.append(None)
+            links2.append((cur, nx, int(t), 0, f[0] if i == 0 else F32(0), f[1] if i == 0 else F32(0)))
+            cur = nx
+        fin2[cur] = (F32(0), F32(0))
+    return _determinize(n2, links2, fin2, 0)
+
+
+def tid_first(tm):
+    """Per transition-id: a phone's first one (out of HMM state 0, not a
+    self-loop; Kaldi TransitionIdToHmmState == 0 && !IsSelfLoop)."""
+    return (np.asarray(tm.tid2hmmstate) == 0) & (np.asarray(tm.tid_is_selfloop) == 0)
+
+
+def _determinize(N, links, fin, start):
+    if N == 0 or start < 0:
         return [], []
     outl = [[] for _ in range(N)]
-    links = list(zip(L["link_src"].tolist(), L["link_dst"].tolist(), L["link_arc"].tolist(),
-                     L["link_graph"], L["link_ac"]))
     for i, l in enumerate(links):
         outl[l[0]].append(i)
-    fin = [INF] * N
-    for t in range(fb[F], fb[F + 1]):
-        fin[t] = F32(0) if len(L["final_cost"]) == 0 else L["final_cost"][t - fb[F]]
-    start = next((t for t in range(fb[0], fb[1]) if L["tok_cost"][t] == 0.0), -1)
-    if start < 0:
-        return [], []
 
     def times(w, g, a):
         return (F32(w[0] + F32(g)), F32(w[1] + F32(a)))
@@ -193,10 +273,10 @@ def determinize(L, ilabel, olabel):
             i = work.pop()
             e = sub[i]
             for li in outl[e[0]]:
-                s, d, a, g, x = links[li]
-                if olabel[a] != 0:
+                s, d, t, w, g, x = links[li]
+                if w != 0:
                     continue
-                n = (d, times(e[1], g, x), e[2] + ((int(ilabel[a]),) if ilabel[a] != 0 else ()))
+                n = (d, times(e[1], g, x), e[2] + ((t,) if t != 0 else ()))
                 if d not in at:
                     at[d] = len(sub)
                     work.append(len(sub))
@@ -205,7 +285,7 @@ def determinize(L, ilabel, olabel):
                     sub[at[d]] = n
                     work.append(at[d])
         # Kaldi's ConvertToMinimal: tokens with word links or a final cost
-        sub = [e for e in sub if fin[e[0]] != INF or any(olabel[links[li][2]] != 0 for li in outl[e[0]])]
+        sub = [e for e in sub if fin[e[0]] is not None or any(links[li][3] != 0 for li in outl[e[0]])]
         sub.sort(key=lambda e: e[0])
         return sub
 
@@ -250,11 +330,10 @@ def determinize(L, ilabel, olabel):
         by_word = {}
         for e in subsets[sid]:
             for li in outl[e[0]]:
-                s, d, a, g, x = links[li]
-                w = int(olabel[a])
+                s, d, t, w, g, x = links[li]
                 if w == 0:
                     continue
-                n = (d, times(e[1], g, x), e[2] + ((int(ilabel[a]),) if ilabel[a] != 0 else ()))
+                n = (d, times(e[1], g, x), e[2] + ((t,) if t != 0 else ()))
                 v = by_word.setdefault(w, [])
                 for j, y in enumerate(v):
                     if y[0] == d:
@@ -278,9 +357,9 @@ def determinize(L, ilabel, olabel):
     for s in range(S):
         best = None
         for e in subsets[s]:
-            if fin[e[0]] == INF:
+            if fin[e[0]] is None:
                 continue
-            c = (e[0], (F32(e[1][0] + F32(fin[e[0]])), e[1][1]), e[2])
+            c = (e[0], (F32(e[1][0] + F32(fin[e[0]][0])), F32(e[1][1] + F32(fin[e[0]][1]))), e[2])
             if best is None or _better(c, best):
                 best = c
         if best is not None:
@@ -679,8 +758,9 @@ def results(oracle, llh, use_final=True, graph_scale=0.9, nbest_n=0, rescore=Non
     import os
     r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
                             use_final, lattice=True, hash_size=hash_size, kaldi=kaldi)
-    W, Fi = determinize(prune(raw_from_oracle(r, oracle.graph, use_final), 6.0),
-                        oracle.graph.ilabel, oracle.graph.olabel)
+    W, Fi = determinize_phone(prune(raw_from_oracle(r, oracle.graph, use_final), 6.0),
+                              oracle.graph.ilabel, oracle.graph.olabel, oracle.tm.tid2phone,
+                              tid_first(oracle.tm))
     if rescore is not None:  # (W, Fi) -> rescored (W, Fi) or None (unchanged)
         rr = rescore(W, Fi)
         if rr is not None:

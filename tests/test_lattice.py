@@ -126,3 +126,39 @@ def test_word_alignment_matches_restatement(synth_model, test_wave, secs):
                 assert ty[tids[0]] in (2, 5)
                 ends = [t for t in tids if ty[t] in (3, 5) and fin[t]]
                 assert ends or d == len(A) - 1
+
+
+@pytest.mark.parametrize("secs,use_final", [(1.5, True), (4, True), (8.3, True), (5, False)])
+def test_phone_pass_determinization_matches_restatement(synth_model, test_wave, secs, use_final):
+    """The reference's GetLattice determinization (DeterminizeLatticePhonePrunedWrapper:
+    phone + word pass, phones deleted, word pass; src/recognizer.cc:678) in the
+    C++ vs its restatement: same determinized lattice size, MBR and n-best.
+    And what determinization preserves: the word-level n-best (word sequences,
+    best costs) equals the word-only determinization's."""
+    from vosk import engine
+    o, r, L = _lattice(synth_model, test_wave[:int(16000 * secs)], use_final)
+    scale = 0.9 if use_final else 1.0
+    first = OL.tid_first(o.tm)
+    assert first.sum() > 0
+    word_only = engine.lattice_words(L, o.graph.ilabel, o.graph.olabel, 6.0, scale, 8)
+    engine.set_phones(o.tm.tid2phone, first)
+    try:
+        got = engine.lattice_words(L, o.graph.ilabel, o.graph.olabel, 6.0, scale, 8)
+    finally:
+        engine.set_phones(None)
+    W, Fi = OL.determinize_phone(OL.prune(L, 6.0), o.graph.ilabel, o.graph.olabel, o.tm.tid2phone, first)
+    assert got["det_ok"] == 1
+    assert got["det_states"] == len(W)
+    assert got["det_arcs"] == sum(len(v) for v in W)
+    if scale != 1.0:
+        W, Fi = OL.scale_graph(W, Fi, scale)
+    mb, nb = OL.mbr(W, Fi), OL.nbest(W, Fi, 8)
+    assert got["mbr"]["words"] == mb["words"]
+    np.testing.assert_allclose(got["mbr"]["conf"], mb["conf"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(np.reshape(got["mbr"]["times"], (-1, 2)),
+                               np.reshape(mb["times"], (-1, 2)), rtol=0, atol=1e-4)
+    assert [x["words"] for x in got["nbest"]] == [x["words"] for x in nb]
+    assert [x["spans"] for x in got["nbest"]] == [[list(s) for s in x["spans"]] for x in nb]
+    assert [x["words"] for x in got["nbest"]] == [x["words"] for x in word_only["nbest"]]
+    np.testing.assert_allclose([x["graph"] + x["acoustic"] for x in got["nbest"]],
+                               [x["graph"] + x["acoustic"] for x in word_only["nbest"]], rtol=1e-6, atol=1e-3)

@@ -316,40 +316,75 @@ void PruneRawLattice(RawLattice* lat, float beam) {
   L = std::move(out);
 }
 
-bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOptions& opt, WordLattice* out) {
-  WordLattice& W = *out;
-  W = WordLattice();
+namespace {
+
+// The determinizer's input: an acceptor on `lout` (words, or phones in the
+// first pass) whose arcs carry one transition-id (`lin`, 0 = none) as the
+// string side -- Kaldi's Lattice after Invert (DeterminizeLatticePhonePrunedWrapper).
+// frame: per state, a bucket such that every link goes to the same or a
+// later bucket (the closure's work order).
+struct DetGraph {
+  int n = 0, start = -1;
+  std::vector<int> frame;
+  struct Link {
+    int src, dst, lin, lout;
+    float g, a;
+  };
+  std::vector<Link> links;
+  std::vector<LW> fin;  // +inf graph: not final
+  int AddState(int f) {
+    frame.push_back(f);
+    fin.push_back(LW{kInf, 0.0f});
+    return n++;
+  }
+};
+
+DetGraph FromRaw(const RawLattice& L, const Graph& g) {
+  DetGraph D;
   const int N = (int)L.tok_state.size(), F = L.num_frames;
-  if (N == 0) return true;
-  // out-links per token (CSR): the word-epsilon ones (closures) first, then
-  // the word links (transitions)
-  const int NL = (int)L.links.size();
-  std::vector<int> ob(N + 1, 0), oe(N, 0), ol(NL);
+  D.n = N;
+  D.frame.resize(N);
+  for (int k = 0; k <= F; k++)
+    for (int t = L.frame_begin[k]; t < L.frame_begin[k + 1]; t++) D.frame[t] = k;
+  D.fin.assign(N, LW{kInf, 0.0f});
+  for (int t = L.frame_begin[F]; t < L.frame_begin[F + 1]; t++)
+    D.fin[t].g = L.final_cost.empty() ? 0.0f : L.final_cost[t - L.frame_begin[F]];
+  for (int t = L.frame_begin[0]; t < L.frame_begin[1]; t++)
+    if (L.tok_cost[t] == 0.0f) { D.start = t; break; }
   // the labels of every link, gathered once (the graph's label arrays are
   // large: random reads of them in every closure miss the caches)
-  std::vector<int> lin(L.links.size()), lout(L.links.size());
+  D.links.resize(L.links.size());
   for (size_t i = 0; i < L.links.size(); i++) {
-    lin[i] = g.ilabel[L.links[i].arc];
-    lout[i] = g.olabel[L.links[i].arc];
+    const auto& l = L.links[i];
+    D.links[i] = DetGraph::Link{l.src, l.dst, g.ilabel[l.arc], g.olabel[l.arc], l.graph_cost, l.acoustic_cost};
   }
-  for (int i = 0; i < NL; i++) ob[L.links[i].src + 1]++;
+  return D;
+}
+
+bool Determinize(const DetGraph& D, const LatticeOptions& opt, WordLattice* out) {
+  WordLattice& W = *out;
+  W = WordLattice();
+  const int N = D.n;
+  if (N == 0 || D.start < 0) return true;
+  int F = 0;
+  for (int f : D.frame) F = f > F ? f : F;
+  const std::vector<DetGraph::Link>& links = D.links;
+  // out-links per token (CSR): the word-epsilon ones (closures) first, then
+  // the word links (transitions)
+  const int NL = (int)links.size();
+  std::vector<int> ob(N + 1, 0), oe(N, 0), ol(NL);
+  for (int i = 0; i < NL; i++) ob[links[i].src + 1]++;
   for (int t = 0; t < N; t++) ob[t + 1] += ob[t];
   {
     std::vector<int> fill(ob.begin(), ob.end() - 1);
     for (int i = 0; i < NL; i++)
-      if (lout[i] == 0) ol[fill[L.links[i].src]++] = i;
+      if (links[i].lout == 0) ol[fill[links[i].src]++] = i;
     for (int t = 0; t < N; t++) oe[t] = fill[t];
     for (int i = 0; i < NL; i++)
-      if (lout[i] != 0) ol[fill[L.links[i].src]++] = i;
+      if (links[i].lout != 0) ol[fill[links[i].src]++] = i;
   }
-  std::vector<float> fin(N, INFINITY);
-  for (int t = L.frame_begin[F]; t < L.frame_begin[F + 1]; t++)
-    fin[t] = L.final_cost.empty() ? 0.0f : L.final_cost[t - L.frame_begin[F]];
-  int start = -1;
-  for (int t = L.frame_begin[0]; t < L.frame_begin[1]; t++)
-    if (L.tok_cost[t] == 0.0f) { start = t; break; }
-  if (start < 0) return true;
-
+  const std::vector<LW>& fin = D.fin;
+  const int start = D.start;
   StrRepo R;
   long long dbg_ext = 0;
   double dt_clo = 0, dt_norm = 0, dt_bw = 0, dt_find = 0;
@@ -361,9 +396,7 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
   // from frame k to k + 1, or within frame k), so a token is expanded once its
   // frame's predecessors are final -- not once per improvement along every
   // path (the same fixpoint: the best (weight, string) per token)
-  std::vector<int> tframe(N);
-  for (int k = 0; k <= F; k++)
-    for (int t = L.frame_begin[k]; t < L.frame_begin[k + 1]; t++) tframe[t] = k;
+  const std::vector<int>& tframe = D.frame;
   std::vector<int> at_pos(N, -1);  // closure scratch: token -> element (reset after each closure)
   std::vector<char> pending;      // closure scratch: element queued
   // per link: the last (string, extended string) of R.Succ through it -- a
@@ -371,9 +404,9 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
   // so most extensions repeat (the trie's hash table is large and cold)
   std::vector<int> memo_in(NL, -1), memo_out(NL, -1);
   auto extend = [&](int str, int li) {
-    if (lin[li] == 0) return str;
+    if (links[li].lin == 0) return str;
     if (memo_in[li] == str) return memo_out[li];
-    const int n = R.Succ(str, lin[li]);
+    const int n = R.Succ(str, links[li].lin);
     memo_in[li] = str;
     memo_out[li] = n;
     return n;
@@ -418,8 +451,8 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
         dbg_ext++;
         for (int k = ob[e.tok]; k < oe[e.tok]; k++) {
           const int li = ol[k];
-          const auto& l = L.links[li];
-          Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}), extend(e.str, li)};
+          const auto& l = links[li];
+          Elem n{l.dst, Times(e.w, LW{l.g, l.a}), extend(e.str, li)};
           const int ei = at.find_idx(n.tok);
           if (ei < 0) {
             at.set(n.tok, (int)sub->size());
@@ -443,7 +476,7 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     size_t m = 0;
     for (size_t i = 0; i < sub->size(); i++) {
       const int t = (*sub)[i].tok;
-      if (oe[t] < ob[t + 1] || fin[t] != INFINITY) (*sub)[m++] = (*sub)[i];
+      if (oe[t] < ob[t + 1] || fin[t].g != kInf) (*sub)[m++] = (*sub)[i];
     }
     sub->resize(m);
     std::sort(sub->begin(), sub->end(), [](const Elem& x, const Elem& y) { return x.tok < y.tok; });
@@ -522,9 +555,9 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
       for (const Elem& e : sub)
         for (int k = oe[e.tok]; k < ob[e.tok + 1]; k++) {
           const int li = ol[k];
-          const auto& l = L.links[li];
-          const int w = lout[li];
-          Elem n{l.dst, Times(e.w, LW{l.graph_cost, l.acoustic_cost}), extend(e.str, li)};
+          const auto& l = links[li];
+          const int w = l.lout;
+          Elem n{l.dst, Times(e.w, LW{l.g, l.a}), extend(e.str, li)};
           auto& v = by_word[w];
           bool merged = false;
           for (auto& x : v)
@@ -563,7 +596,7 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     long long el = 0;
     for (auto& x : subsets) el += (long long)x.size();
     fprintf(stderr, "det: tokens %d links %zu subsets %d elems %lld expansions %lld strings %zu clo %.2f norm %.2f find %.2f\n",
-            N, L.links.size(), S, el, dbg_ext, R.parent.size(), dt_clo, dt_norm, dt_find);
+            N, links.size(), S, el, dbg_ext, R.parent.size(), dt_clo, dt_norm, dt_find);
   }
   std::vector<LW> fw(S);
   std::vector<std::vector<int>> fs(S);
@@ -572,8 +605,8 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     bool have = false;
     Elem best{0, LW{}, 0};
     for (const Elem& e : subsets[s]) {
-      if (fin[e.tok] == INFINITY) continue;
-      Elem c{e.tok, Times(e.w, LW{fin[e.tok], 0.0f}), e.str};
+      if (fin[e.tok].g == kInf) continue;
+      Elem c{e.tok, Times(e.w, fin[e.tok]), e.str};
       if (!have || ElemBetter(R, bases[s], c, best)) {
         best = c;
         have = true;
@@ -618,6 +651,90 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
     }
   }
   return true;
+}
+
+}  // namespace
+
+bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOptions& opt, WordLattice* out) {
+  return Determinize(FromRaw(L, g), opt, out);
+}
+
+bool DeterminizePhonePruned(const RawLattice& L, const Graph& g, const std::vector<int>& tid2phone,
+                            const std::vector<char>& tid_first, const LatticeOptions& opt, WordLattice* out) {
+  DetGraph D = FromRaw(L, g);
+  // DeterminizeLatticeInsertPhones: a phone label (first_phone_label + phone,
+  // first_phone_label = the highest word label + 1) at the first
+  // transition-id of every phone (HMM state 0, not a self-loop); on the link
+  // itself when it has no word, else on a new link after it (through a new
+  // state), weight One
+  int first = 1;
+  for (const auto& l : D.links) first = std::max(first, l.lout + 1);
+  const size_t nl = D.links.size();
+  for (size_t i = 0; i < nl; i++) {
+    const int t = D.links[i].lin;
+    if (t <= 0 || t >= (int)tid_first.size() || !tid_first[t]) continue;
+    const int ph = first + tid2phone[t];
+    if (D.links[i].lout == 0) {
+      D.links[i].lout = ph;
+    } else {
+      const int dst = D.links[i].dst;
+      const int x = D.AddState(D.frame[dst]);
+      D.links[i].dst = x;
+      D.links.push_back(DetGraph::Link{x, dst, 0, ph, 0.0f, 0.0f});
+    }
+  }
+  // first pass: determinization on phones + words
+  WordLattice P;
+  if (!Determinize(D, opt, &P)) return false;
+  if (P.NumStates() == 0) {
+    *out = WordLattice();
+    return true;
+  }
+  // LatticeDeterminizerPruned::Output to a Lattice: each arc's string as a
+  // chain of one-transition-id links, label and weight on the first; a final
+  // string as a chain to a new final state (weight on its first link);
+  // DeterminizeLatticeDeletePhones: phone labels -> 0
+  const int S = P.NumStates();
+  DetGraph E;
+  E.n = S;
+  E.start = 0;
+  E.frame.assign(S, 0);
+  E.fin.assign(S, LW{kInf, 0.0f});
+  for (int s = 0; s < S; s++)  // topologically sorted: frames forward
+    for (const auto& a : P.arcs[s]) E.frame[a.next] = std::max(E.frame[a.next], E.frame[s] + (int)a.tids.size());
+  auto label = [&](int w) { return w >= first ? 0 : w; };
+  for (int s = 0; s < S; s++) {
+    for (const auto& a : P.arcs[s]) {
+      const int n = (int)a.tids.size();
+      if (n == 0) {
+        E.links.push_back(DetGraph::Link{s, a.next, 0, label(a.word), a.graph, a.acoustic});
+        continue;
+      }
+      int cur = s;
+      for (int i = 0; i < n; i++) {
+        const int nx = i + 1 == n ? a.next : E.AddState(E.frame[s] + i + 1);
+        E.links.push_back(DetGraph::Link{cur, nx, a.tids[i], i == 0 ? label(a.word) : 0, i == 0 ? a.graph : 0.0f,
+                                         i == 0 ? a.acoustic : 0.0f});
+        cur = nx;
+      }
+    }
+    if (P.final_graph[s] == kInf) continue;
+    const std::vector<int>& ft = P.final_tids[s];
+    if (ft.empty()) {
+      E.fin[s] = LW{P.final_graph[s], P.final_acoustic[s]};
+      continue;
+    }
+    int cur = s;
+    for (size_t i = 0; i < ft.size(); i++) {
+      const int nx = E.AddState(E.frame[s] + (int)i + 1);
+      E.links.push_back(DetGraph::Link{cur, nx, ft[i], 0, i == 0 ? P.final_graph[s] : 0.0f,
+                                       i == 0 ? P.final_acoustic[s] : 0.0f});
+      cur = nx;
+    }
+    E.fin[cur] = LW{0.0f, 0.0f};
+  }
+  // second pass: word level (DeterminizeLatticePruned)
+  return Determinize(E, opt, out);
 }
 
 void ScaleGraph(WordLattice* lat, float scale) {

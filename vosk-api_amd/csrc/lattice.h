@@ -88,6 +88,16 @@ void PruneRawLattice(RawLattice* lat, float lattice_beam);
 bool DeterminizeToWords(const RawLattice& lat, const Graph& g, const LatticeOptions& opt,
                         WordLattice* out);
 
+// Kaldi's DeterminizeLatticePhonePrunedWrapper, the determinization of the
+// reference's GetLattice (src/recognizer.cc:678; batch lattices through the
+// CUDA pipeline's determinize step): a phone label inserted at the first
+// transition-id of every phone (tid_first: HMM state 0, not a self-loop),
+// determinization on phones + words, the result expanded back to a
+// one-transition-id-per-link lattice with the phone labels deleted, then
+// word-level determinization of that.  False if a guard tripped.
+bool DeterminizePhonePruned(const RawLattice& lat, const Graph& g, const std::vector<int>& tid2phone,
+                            const std::vector<char>& tid_first, const LatticeOptions& opt, WordLattice* out);
+
 // Word alignment (Kaldi lat/word-align-lattice.cc WordAlignLattice [K], with
 // WordBoundaryInfo from word_boundary.int and reorder = true; the reference
 // aligns before MBR and n-best, src/recognizer.cc:433-434,555-558,

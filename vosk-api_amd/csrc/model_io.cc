@@ -608,6 +608,7 @@ void ReadFinalMdl(const std::string& path, TransitionModel* tm, Nnet* nnet) {
   tm->tid2phone.assign(1, 0);
   tm->tid2selfloop.assign(1, 0);
   tm->tid2final.assign(1, 0);
+  tm->tid2first.assign(1, 0);
   int max_pdf = -1;
   for (int i = 0; i < n_tuples; i++) {
     int phone = r.I32(), hmm_state = r.I32(), fpdf = r.I32();
@@ -622,6 +623,7 @@ void ReadFinalMdl(const std::string& path, TransitionModel* tm, Nnet* nnet) {
       tm->tid2phone.push_back(phone);
       tm->tid2selfloop.push_back(self_loop ? 1 : 0);
       tm->tid2final.push_back(dst == (int)entries[phone2idx[phone]].size() - 1 ? 1 : 0);
+      tm->tid2first.push_back(hmm_state == 0 && !self_loop ? 1 : 0);
       max_pdf = std::max(max_pdf, pdf);
     }
   }

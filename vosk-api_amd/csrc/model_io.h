@@ -94,6 +94,7 @@ struct TransitionModel {
   std::vector<int> tid2pdf;    // index 0 unused
   std::vector<int> tid2phone;  // index 0 unused
   std::vector<char> tid2selfloop;  // transition back to its own HMM state (index 0 unused)
+  std::vector<char> tid2first;     // out of HMM state 0, not a self-loop: a phone's first transition-id
   std::vector<char> tid2final;     // transition into the HMM's final state (IsFinal)
   int num_pdfs = 0;
   int NumTransitionIds() const { return (int)tid2pdf.size() - 1; }

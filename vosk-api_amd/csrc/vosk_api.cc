@@ -411,6 +411,18 @@ int vamd_lattice_set_rescore(const char* g_fst, const char* g_carpa) {
   API_CATCH(-1)
 }
 
+static std::vector<int> g_host_tid2phone;  // vamd_lattice_set_phones (tests)
+static std::vector<char> g_host_tid_first;
+
+int vamd_lattice_set_phones(const int* tid2phone, const signed char* tid_first, int ntids) {
+  API_TRY
+  if (ntids > 0 && (!tid2phone || !tid_first)) VAMD_ERR("null transition-id tables");
+  g_host_tid2phone.assign(tid2phone, tid2phone + std::max(ntids, 0));
+  g_host_tid_first.assign(tid_first, tid_first + std::max(ntids, 0));
+  return 0;
+  API_CATCH(-1)
+}
+
 float vamd_carpa_logprob(const char* g_carpa, int word, const int* hist, int nhist) {
   static std::string loaded;
   static ConstArpaLm lm;
@@ -455,7 +467,9 @@ const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, cons
   WordLattice wl;
   LatticeOptions opt;
   opt.lattice_beam = lattice_beam;
-  const bool ok = DeterminizeToWords(L, g, opt, &wl);
+  const bool ok = g_host_tid2phone.empty()
+                      ? DeterminizeToWords(L, g, opt, &wl)
+                      : DeterminizePhonePruned(L, g, g_host_tid2phone, g_host_tid_first, opt, &wl);
   const auto t2 = clk::now();
   os << ", \"det_ok\": " << (ok ? 1 : 0) << ", \"det_states\": " << wl.NumStates();
   int det_arcs = 0;

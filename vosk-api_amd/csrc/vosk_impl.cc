@@ -380,7 +380,7 @@ bool Recognizer::Submit(const std::vector<float>* wave, bool final) {
 // lattice -> words (src/recognizer.cc:422-482 MbrResult, :669-729 GetResult)
 // ---------------------------------------------------------------------------
 // A decoder segment's raw lattice pruned at the lattice beam and determinized
-// on words; false if unusable (overflow, determinization guard).  Then the
+// as GetLattice does (phone + word pass, then words); false if unusable (overflow, determinization guard).  Then the
 // graph scale, and word alignment when the model has word_boundary.int
 // (WordAlignLattice, src/recognizer.cc:433-434; CopyLatticeForMbr otherwise).
 static bool WordLatticeFromRaw(RawLattice& raw, const ModelData& m, float graph_scale, WordLattice* wl,
@@ -389,7 +389,8 @@ static bool WordLatticeFromRaw(RawLattice& raw, const ModelData& m, float graph_
   PruneRawLattice(&raw, m.dec.lattice_beam);
   LatticeOptions opt;
   opt.lattice_beam = m.dec.lattice_beam;
-  if (!DeterminizeToWords(raw, m.graph, opt, wl) || wl->NumStates() == 0) return false;
+  if (!DeterminizePhonePruned(raw, m.graph, m.tm.tid2phone, m.tm.tid2first, opt, wl) || wl->NumStates() == 0)
+    return false;
   if (rescore && m.rescore) {  // src/recognizer.cc:680-711
     WordLattice r;
     if (RescoreLattice(*wl, *m.rescore, opt, &r)) *wl = std::move(r);

@@ -290,6 +290,7 @@ class TransitionModel:
     tid_is_selfloop: np.ndarray = field(default=None)
     tid_is_final: np.ndarray = field(default=None)  # into the HMM's final state (IsFinal)
     tuple_first_tid: np.ndarray = field(default=None)
+    tid2hmmstate: np.ndarray = field(default=None)  # the transition's source HMM state
 
     def derive(self):
         """Transition-id numbering (1-based): tuple i owns one id per
@@ -300,6 +301,7 @@ class TransitionModel:
         phone = [0]
         sl = [0]
         fin = [0]
+        hmm = [0]
         first = []
         for (ph, hs, fpdf, spdf) in self.tuples:
             first.append(len(pdf))
@@ -311,11 +313,13 @@ class TransitionModel:
                 phone.append(ph)
                 sl.append(1 if is_sl else 0)
                 fin.append(1 if dst == len(entry) - 1 else 0)
+                hmm.append(hs)
         self.tid2pdf = np.array(pdf, np.int32)
         self.tid2phone = np.array(phone, np.int32)
         self.tid_is_selfloop = np.array(sl, np.int32)
         self.tid_is_final = np.array(fin, np.int32)
         self.tuple_first_tid = np.array(first, np.int32)
+        self.tid2hmmstate = np.array(hmm, np.int32)
         return self
 
     @property

@@ -60,6 +60,7 @@ _SIGS = {
     "vamd_engine_set_step_samples": (C.c_int, [_vp, C.c_int]),
     "vamd_engine_stage_times": (C.c_int, [_vp, _vp, _vp, C.c_int]),
     "vamd_lattice_set_rescore": (C.c_int, [C.c_char_p, C.c_char_p]),
+    "vamd_lattice_set_phones": (C.c_int, [_vp, _vp, C.c_int]),
     "vamd_carpa_logprob": (C.c_float, [C.c_char_p, C.c_int, _vp, C.c_int]),
     "vamd_batch_lanes": (C.c_int, [_vp]),
     "vamd_batch_lane_stats": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, C.c_int]),
@@ -429,6 +430,19 @@ def set_rescore(g_fst=None, g_carpa=None):
                                     g_carpa.encode() if g_carpa else None)
     if r != 0:
         raise RuntimeError("vamd_lattice_set_rescore failed: " + _err())
+
+
+def set_phones(tid2phone=None, tid_first=None):
+    """Host-only: phone + word determinization (as GetLattice) inside
+    lattice_words; None: word level only."""
+    if tid2phone is None:
+        r = _c.vamd_lattice_set_phones(None, None, 0)
+    else:
+        p = np.ascontiguousarray(tid2phone, np.int32)
+        f = np.ascontiguousarray(tid_first, np.int8)
+        r = _c.vamd_lattice_set_phones(p.ctypes.data, f.ctypes.data, len(p))
+    if r != 0:
+        raise RuntimeError("vamd_lattice_set_phones failed: " + _err())
 
 
 def carpa_logprob(g_carpa, word, hist):
