@@ -50,3 +50,53 @@ def test_recognizer_8khz_matches_oracle(synth_model_noep, test_wave):
     for i in range(0, len(data), 4000):
         rec.AcceptWaveform(data[i:i + 4000])
     assert json.loads(rec.FinalResult())["text"] == ref["text"]
+
+
+@pytest.mark.parametrize("rate,call_bytes", [(8000, 4000), (44100, 8000), (22050, 3000)])
+def test_batch_recognizer_resamples_each_call(synth_model_noep, test_wave, monkeypatch, rate, call_bytes):
+    """BatchRecognizer at another rate: each AcceptWaveform call resampled on
+    its own with the end flush (LinearResample::Resample(input, true),
+    src/batch_recognizer.cc:27-29,157-158), the model-rate samples chunked.
+    The oracle: each call through the whole-signal resampler, concatenated,
+    decoded (batch order), MBR text of the lattice."""
+    import vosk
+    import oracle_lattice as OL
+    vosk.SetLogLevel(-1)
+    monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_model_noep)
+    o = oracle_py.OracleModel(synth_model_noep, fpc=51)
+    vosk.GpuInit()
+    model = vosk.BatchModel()
+    n = 3
+    waves = [_at_rate(test_wave[int(16000 * 0.7 * i):], rate)[:int(rate * (3.0 + 0.6 * i))] for i in range(n)]
+    datas = [x.astype("<i2").tobytes() for x in waves]
+    recs = [vosk.BatchRecognizer(model, rate) for _ in range(n)]
+    texts = [""] * n
+    pos = [0] * n
+    ended = set()
+    while len(ended) < n:
+        for i in range(n):
+            if i in ended:
+                continue
+            chunk = datas[i][pos[i]:pos[i] + call_bytes]
+            pos[i] += call_bytes
+            if not chunk:
+                recs[i].FinishStream()
+                ended.add(i)
+                continue
+            recs[i].AcceptWaveform(chunk)
+        model.Wait()
+        for i in range(n):
+            res = recs[i].Result()
+            if res:
+                texts[i] = (texts[i] + " " + json.loads(res)["text"]).strip()
+    model.Wait()
+    for i in range(n):
+        res = recs[i].Result()
+        if res:
+            texts[i] = (texts[i] + " " + json.loads(res)["text"]).strip()
+        x = waves[i]
+        step = call_bytes // 2
+        y = np.concatenate([oracle_py.resample(x[j:j + step], rate, 16000) for j in range(0, len(x), step)])
+        mb = OL.results(o, o.loglikes(y), kaldi=oracle_py.decoder_order(batch=True) == "kaldi")["mbr"]
+        assert texts[i] == " ".join(o.words[w] for w in mb["words"]), (i, texts[i])
+        assert texts[i]

@@ -806,6 +806,11 @@ Engine::~Engine() {
   if (stream_) (void)hipStreamDestroy(stream_);
   if (dstream_) (void)hipStreamDestroy(dstream_);
   if (fstream_) (void)hipStreamDestroy(fstream_);
+  if (call_stream_) (void)hipStreamSynchronize(call_stream_);
+  if (d_call_raw_) (void)hipFree(d_call_raw_);
+  if (d_call_out_) (void)hipFree(d_call_out_);
+  if (d_call_jobs_) (void)hipFree(d_call_jobs_);
+  if (call_stream_) (void)hipStreamDestroy(call_stream_);
 }
 
 int Engine::TryAllocSlot() {
@@ -921,6 +926,12 @@ void Engine::SetSampleRate(int slot, int rate) {
     h.table = -1;
     return;
   }
+  h.rate = rate;
+  h.table = ResampleTableLocked(rate);
+}
+
+int Engine::ResampleTableLocked(int rate) {
+  const int model_rate = (int)std::lround(md_->mfcc.samp_freq);
   int t = -1;
   for (size_t i = 0; i < res_tables_.size(); i++)
     if (res_tables_[i].rate_in == rate) t = (int)i;
@@ -941,9 +952,57 @@ void Engine::SetSampleRate(int slot, int rate) {
     VAMD_LOG_VERBOSE("resampling " << rate << " -> " << model_rate << " Hz, " << res_tables_[t].taps
                                    << " taps");
   }
-  h.rate = rate;
-  h.table = t;
+  return t;
 }
+
+std::vector<float> Engine::ResampleCall(int rate, const float* x, int n) {
+  int t;
+  long long n_out;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    DEVICE_GUARD();
+    t = ResampleTableLocked(rate);
+    n_out = res_tables_[t].NumOutputSamples(n, true);
+  }
+  std::vector<float> out((size_t)n_out);
+  if (n_out == 0) return out;
+  std::lock_guard<std::mutex> lk(call_mu_);
+  DEVICE_GUARD();
+  if (!call_stream_) HIPCHECK(hipStreamCreateWithFlags(&call_stream_, hipStreamNonBlocking));
+  // the kernel indexes its input and output as rings (power-of-two lengths)
+  auto pow2 = [](long long v) {
+    size_t p = 1024;
+    while ((long long)p < v) p <<= 1;
+    return p;
+  };
+  const size_t raw_len = pow2(n), out_len = pow2(n_out);
+  constexpr int kPer = 2048;  // outputs per workgroup
+  const size_t njobs = (size_t)((n_out + kPer - 1) / kPer);
+  auto grow = [&](auto** p, size_t* cap, size_t want, size_t elem) {
+    if (*cap >= want) return;
+    if (*p) HIPCHECK(hipFree(*p));
+    HIPCHECK(hipMalloc((void**)p, want * elem));
+    *cap = want;
+  };
+  grow(&d_call_raw_, &call_cap_raw_, raw_len, sizeof(float));
+  grow(&d_call_out_, &call_cap_out_, out_len, sizeof(float));
+  grow(&d_call_jobs_, &call_cap_jobs_, njobs, sizeof(ResampleJob));
+  std::vector<ResampleJob> jobs(njobs);
+  for (size_t k = 0; k < njobs; k++) {
+    const long long o = (long long)k * kPer;
+    jobs[k] = ResampleJob{0, (int)o, (int)std::min<long long>(kPer, n_out - o), t, o, (long long)n};
+  }
+  HIPCHECK(hipMemcpyAsync(d_call_raw_, x, sizeof(float) * n, hipMemcpyHostToDevice, call_stream_));
+  HIPCHECK(hipMemcpyAsync(d_call_jobs_, jobs.data(), sizeof(ResampleJob) * njobs, hipMemcpyHostToDevice,
+                          call_stream_));
+  LaunchResample(d_call_jobs_, (int)njobs, d_res_tables_, d_call_raw_, (int)raw_len, d_call_out_, (int)out_len,
+                 call_stream_);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemcpyAsync(out.data(), d_call_out_, sizeof(float) * n_out, hipMemcpyDeviceToHost, call_stream_));
+  HIPCHECK(hipStreamSynchronize(call_stream_));
+  return out;
+}
+
 
 void Engine::PreloadSamples(int slot, const float* x, long long n, bool finished) {
   std::lock_guard<std::mutex> lk(mu_);

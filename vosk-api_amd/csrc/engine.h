@@ -263,6 +263,12 @@ class Engine {
   // Input sample rate of a stream (default: the model's); other rates are
   // resampled on the GPU (resample.h).  Set before the stream's first samples.
   void SetSampleRate(int slot, int rate);
+  // One AcceptWaveform call of the batch path resampled on its own, flushed
+  // at its end (the reference's BatchRecognizer: LinearResample::Resample(
+  // input, flush = true) per call, src/batch_recognizer.cc:27-29,157-158):
+  // the call's samples to the device, resample_kernel over the whole call,
+  // the model-rate samples back.  Thread-safe; its own HIP stream.
+  std::vector<float> ResampleCall(int rate, const float* x, int n);
   void AcceptSamples(int slot, const float* x, int n);
   // The same, taking the buffer (no copy when the stream's pending samples
   // are all consumed, the batch lane's usual case)
@@ -458,6 +464,13 @@ class Engine {
   int* d_probe_ = nullptr;              // ProbeEndpoints buffers
   int* h_probe_ = nullptr;
   hipStream_t copy_stream_ = nullptr;  // segment lattice copies
+  int ResampleTableLocked(int rate);    // the table of an input rate (created on first use)
+  std::mutex call_mu_;                 // ResampleCall's stream and buffers
+  hipStream_t call_stream_ = nullptr;
+  float* d_call_raw_ = nullptr;
+  float* d_call_out_ = nullptr;
+  ResampleJob* d_call_jobs_ = nullptr;
+  size_t call_cap_raw_ = 0, call_cap_out_ = 0, call_cap_jobs_ = 0;
   char* h_lat_stage_ = nullptr;        // pinned staging of segment lattice copies
   size_t lat_stage_bytes_ = 0;
   long long copy_us_[4] = {0, 0, 0, 0}, copy_calls_ = 0;  // development (VOSK_AMD_COPY_DEBUG)

@@ -1276,10 +1276,14 @@ void BatchModel::LaneLoop(Lane* L) {
 }
 
 BatchRecognizer::BatchRecognizer(BatchModel* model, float sr) : model_(model), sample_frequency_(sr) {
-  // the reference resamples each call independently (flush per call,
-  // src/batch_recognizer.cc:27-29,157-158); here the stream is resampled
-  // continuously on the GPU (no discontinuity at call boundaries)
-  model_->Admit(this, InputRate(sr));
+  // the reference resamples each call on its own, flushed at the call's end
+  // (src/batch_recognizer.cc:27-29,157-158), and chunks the model-rate
+  // samples: the stream's engine slot runs at the model rate and each call
+  // at another rate goes through Engine::ResampleCall (GPU) first
+  const int rate = InputRate(sr);
+  const int model_rate = (int)std::lround(model_->data().mfcc.samp_freq);
+  call_rate_ = rate == model_rate ? 0 : rate;
+  model_->Admit(this, model_rate);
   model_->Ref();
 }
 
@@ -1290,7 +1294,13 @@ BatchRecognizer::~BatchRecognizer() {
 
 void BatchRecognizer::AcceptWaveform(const char* data, int len) {  // batch_recognizer.cc:115-181
   const short* s = reinterpret_cast<const short*>(data);
-  buffer_.insert(buffer_.end(), s, s + len / 2);
+  if (call_rate_) {
+    std::vector<float> x(s, s + len / 2);
+    std::vector<float> y = model_->lane_engine(lane_)->ResampleCall(call_rate_, x.data(), (int)x.size());
+    buffer_.insert(buffer_.end(), y.begin(), y.end());
+  } else {
+    buffer_.insert(buffer_.end(), s, s + len / 2);
+  }
   const int spc = model_->samples_per_chunk();
   size_t i = 0;
   while (i + spc <= buffer_.size()) {

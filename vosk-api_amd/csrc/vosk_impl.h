@@ -299,7 +299,8 @@ class BatchRecognizer {
   BatchModel* model_;
   float sample_frequency_;
   bool nlsml_ = false;
-  std::vector<float> buffer_;
+  std::vector<float> buffer_;  // model-rate samples not yet pushed as a chunk
+  int call_rate_ = 0;          // input rate resampled per call (0: the model's rate)
   // lane state (guarded by the lane's mutex)
   int lane_ = -1, slot_ = -1;
   std::deque<Chunk> queue_;
