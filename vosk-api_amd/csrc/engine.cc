@@ -785,6 +785,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
 }
 
 Engine::~Engine() {
+  if (step_prof_n_ && getenv("VOSK_AMD_STEP_PROFILE"))
+    fprintf(stderr, "[engine] steps %lld: build %.3f ms, sync wait %.3f ms, after sync %.3f ms, total %.3f ms per step\n",
+            step_prof_n_, step_prof_[0] / step_prof_n_, step_prof_[1] / step_prof_n_, step_prof_[2] / step_prof_n_,
+            step_prof_[3] / step_prof_n_);
   (void)hipSetDevice(cfg_.device);
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (dstream_) (void)hipStreamSynchronize(dstream_);
@@ -1460,11 +1464,14 @@ void Engine::RunStep(bool allow_pipeline) {
   if (db) LaunchDecodeBatch(*db, ds);
   if (tk) HIPCHECK(hipEventRecord(ev_[6], ds));
   HIPCHECK(hipGetLastError());
+  const auto tq0 = std::chrono::steady_clock::now();
   HIPCHECK(hipStreamSynchronize(ns));
   if (pipe) {
     HIPCHECK(hipStreamSynchronize(fs));
     HIPCHECK(hipStreamSynchronize(ds));
   }
+  const auto tq1 = std::chrono::steady_clock::now();
+  step_prof_[1] += std::chrono::duration<double, std::milli>(tq1 - tq0).count();
   if (tk) {
     float a = 0, b = 0, c = 0, t1 = 0, t2 = 0, t3 = 0;
     HIPCHECK(hipEventElapsedTime(&a, ev_[1], ev_[2]));
@@ -1485,6 +1492,7 @@ void Engine::RunStep(bool allow_pipeline) {
   counters_.frames_mfcc += st_mfcc_total_;
   counters_.chunk_jobs += st_jobs_.size();
   if (db) FinishDecodeBatch(*db);
+  step_prof_[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq1).count();
   if (cfg_.collect_llh && !st_iv_reqs_.empty()) {
     const int Si = plan_.ivector_dim;
     std::vector<float> rows((size_t)st_jobs_.size() * Si);
@@ -1547,12 +1555,18 @@ void Engine::FlushLocked() {
 bool Engine::Step(const std::vector<int>& slots, bool allow_pipeline) {
   std::lock_guard<std::mutex> lk(mu_);
   DEVICE_GUARD();
+  const auto t0 = std::chrono::steady_clock::now();
   if (!BuildStep(slots)) {
     if (!pendn_active_ && !pend_active_) return false;
     DrainOnce();  // pipeline tail: only pending nnet / decoder passes are left
     return true;
   }
+  const auto t1 = std::chrono::steady_clock::now();
   RunStep(allow_pipeline);
+  // host-side step profile (VOSK_AMD_STEP_PROFILE): build, total
+  step_prof_[0] += std::chrono::duration<double, std::milli>(t1 - t0).count();
+  step_prof_[3] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  step_prof_n_++;
   return true;
 }
 
