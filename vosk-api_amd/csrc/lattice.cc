@@ -383,8 +383,12 @@ bool Determinize(const DetGraph& D, const LatticeOptions& opt, WordLattice* out)
     for (int i = 0; i < NL; i++)
       if (links[i].lout != 0) ol[fill[links[i].src]++] = i;
   }
+  // the links in that order, packed (the closures walk them sequentially)
+  std::vector<DetGraph::Link> cl(NL);
+  for (int k = 0; k < NL; k++) cl[k] = links[ol[k]];
   const std::vector<LW>& fin = D.fin;
   const int start = D.start;
+  const bool dbg = getenv("VOSK_AMD_DET_DEBUG") != nullptr;
   StrRepo R;
   long long dbg_ext = 0;
   double dt_clo = 0, dt_norm = 0, dt_bw = 0, dt_find = 0;
@@ -402,13 +406,14 @@ bool Determinize(const DetGraph& D, const LatticeOptions& opt, WordLattice* out)
   // per link: the last (string, extended string) of R.Succ through it -- a
   // token reached by the same path from any subset has the same trie node,
   // so most extensions repeat (the trie's hash table is large and cold)
+  // (indexed by packed link position)
   std::vector<int> memo_in(NL, -1), memo_out(NL, -1);
-  auto extend = [&](int str, int li) {
-    if (links[li].lin == 0) return str;
-    if (memo_in[li] == str) return memo_out[li];
-    const int n = R.Succ(str, links[li].lin);
-    memo_in[li] = str;
-    memo_out[li] = n;
+  auto extend = [&](int str, int k) {
+    if (cl[k].lin == 0) return str;
+    if (memo_in[k] == str) return memo_out[k];
+    const int n = R.Succ(str, cl[k].lin);
+    memo_in[k] = str;
+    memo_out[k] = n;
     return n;
   };
   // closure work queue: elements bucketed by token frame (links go forward
@@ -450,9 +455,8 @@ bool Determinize(const DetGraph& D, const LatticeOptions& opt, WordLattice* out)
         const Elem e = (*sub)[i];
         dbg_ext++;
         for (int k = ob[e.tok]; k < oe[e.tok]; k++) {
-          const int li = ol[k];
-          const auto& l = links[li];
-          Elem n{l.dst, Times(e.w, LW{l.g, l.a}), extend(e.str, li)};
+          const auto& l = cl[k];
+          Elem n{l.dst, Times(e.w, LW{l.g, l.a}), extend(e.str, k)};
           const int ei = at.find_idx(n.tok);
           if (ei < 0) {
             at.set(n.tok, (int)sub->size());
@@ -497,27 +501,30 @@ bool Determinize(const DetGraph& D, const LatticeOptions& opt, WordLattice* out)
   // subsets are equal with the same tokens and strings and weights within
   // delta (Kaldi's determinizer, delta = kDelta = 1/1024)
   const float delta = 1.0f / 1024.0f;
-  std::unordered_map<std::string, std::vector<int>> index;
+  std::unordered_map<uint64_t, std::vector<int>> index;
   std::vector<std::vector<Elem>> subsets;
   std::vector<int> bases;  // per subset: the base node of its residual strings
+  // key: a hash of the (token, residual length, residual hash) sequence; a
+  // hit is confirmed element by element (tokens, weights within delta,
+  // residual strings exactly)
   auto key_of = [&](const std::vector<Elem>& sub, int base) {
-    std::string k;
-    k.reserve(sub.size() * 16);
+    uint64_t k = 0x9e3779b97f4a7c15ull ^ sub.size();
     for (auto& e : sub) {
-      const int n = R.ResLen(e.str, base);
       const uint64_t h = R.ResHash(e.str, base);
-      k.append((const char*)&e.tok, sizeof(int));
-      k.append((const char*)&n, sizeof(int));
-      k.append((const char*)&h, sizeof(h));
+      k = (k ^ (uint64_t)(uint32_t)e.tok) * 0xff51afd7ed558ccdull;
+      k = (k ^ (uint64_t)(uint32_t)R.ResLen(e.str, base)) * 0xc4ceb9fe1a85ec53ull;
+      k = (k ^ h) * 0xff51afd7ed558ccdull;
+      k ^= k >> 29;
     }
     return k;
   };
   auto find_or_add = [&](std::vector<Elem>&& sub, int base, bool* added) {
-    const std::string k = key_of(sub, base);
+    const uint64_t k = key_of(sub, base);
     auto& cand = index[k];
     for (int id : cand) {
       const auto& o = subsets[id];
-      bool eq = true;
+      bool eq = o.size() == sub.size();
+      for (size_t i = 0; i < o.size() && eq; i++) eq = o[i].tok == sub[i].tok;
       for (size_t i = 0; i < o.size() && eq; i++)
         eq = std::fabs(o[i].w.g - sub[i].w.g) <= delta && std::fabs(o[i].w.a - sub[i].w.a) <= delta;
       // the key holds residual lengths and hashes: the strings themselves
@@ -545,54 +552,54 @@ bool Determinize(const DetGraph& D, const LatticeOptions& opt, WordLattice* out)
   find_or_add(std::move(s0), 0, &added);
   std::vector<std::vector<WordLattice::Arc>> arcs(1);
   std::vector<int> queue{0};
+  std::vector<std::pair<int, Elem>> tr_scratch;
   for (size_t qi = 0; qi < queue.size(); qi++) {
     const int sid = queue[qi];
     const int sbase = bases[sid];
-    // transitions per word label, in label order
-    std::map<int, std::vector<Elem>> by_word;
-    {
-      const std::vector<Elem>& sub = subsets[sid];
-      for (const Elem& e : sub)
-        for (int k = oe[e.tok]; k < ob[e.tok + 1]; k++) {
-          const int li = ol[k];
-          const auto& l = links[li];
-          const int w = l.lout;
-          Elem n{l.dst, Times(e.w, LW{l.g, l.a}), extend(e.str, li)};
-          auto& v = by_word[w];
-          bool merged = false;
-          for (auto& x : v)
-            if (x.tok == n.tok) {
-              if (ElemBetter(R, sbase, n, x)) x = n;
-              merged = true;
-              break;
-            }
-          if (!merged) v.push_back(n);
-        }
-    }
-    for (auto& kv : by_word) {
-      std::vector<Elem> sub = std::move(kv.second);
-      auto t0 = dclk::now();
+    // transitions per word label, in label order: (word, element) pairs,
+    // sorted by (word, token), one element per (word, token) -- the better
+    std::vector<std::pair<int, Elem>>& tr = tr_scratch;
+    tr.clear();
+    for (const Elem& e : subsets[sid])
+      for (int k = oe[e.tok]; k < ob[e.tok + 1]; k++) {
+        const auto& l = cl[k];
+        tr.push_back({l.lout, Elem{l.dst, Times(e.w, LW{l.g, l.a}), extend(e.str, k)}});
+      }
+    std::sort(tr.begin(), tr.end(), [&](const std::pair<int, Elem>& x, const std::pair<int, Elem>& y) {
+      if (x.first != y.first) return x.first < y.first;
+      if (x.second.tok != y.second.tok) return x.second.tok < y.second.tok;
+      return ElemBetter(R, sbase, x.second, y.second);
+    });
+    for (size_t g0 = 0; g0 < tr.size();) {
+      const int word = tr[g0].first;
+      size_t g1 = g0;
+      std::vector<Elem> sub;
+      for (; g1 < tr.size() && tr[g1].first == word; g1++)
+        if (sub.empty() || sub.back().tok != tr[g1].second.tok) sub.push_back(tr[g1].second);
+      g0 = g1;
+      dclk::time_point t0;
+      if (dbg) t0 = dclk::now();
       closure(&sub, sbase);
-      dt_clo += dms(t0);
+      if (dbg) dt_clo += dms(t0);
       if (sub.empty()) continue;  // a dead end (cannot occur on a pruned lattice)
       LW tot;
       std::vector<int> prefix;
-      t0 = dclk::now();
+      if (dbg) t0 = dclk::now();
       const int nbase = normalize(&sub, sbase, &tot, &prefix);
-      dt_norm += dms(t0);
-      t0 = dclk::now();
+      if (dbg) dt_norm += dms(t0);
+      if (dbg) t0 = dclk::now();
       const int dst = find_or_add(std::move(sub), nbase, &added);
-      dt_find += dms(t0);
+      if (dbg) dt_find += dms(t0);
       if (added) {
         if ((int)subsets.size() > opt.max_states) return false;
         queue.push_back(dst);
         arcs.emplace_back();
       }
-      arcs[sid].push_back(WordLattice::Arc{kv.first, dst, tot.g, tot.a, std::move(prefix)});
+      arcs[sid].push_back(WordLattice::Arc{word, dst, tot.g, tot.a, std::move(prefix)});
     }
   }
   const int S = (int)subsets.size();
-  if (getenv("VOSK_AMD_DET_DEBUG")) {
+  if (dbg) {
     long long el = 0;
     for (auto& x : subsets) el += (long long)x.size();
     fprintf(stderr, "det: tokens %d links %zu subsets %d elems %lld expansions %lld strings %zu clo %.2f norm %.2f find %.2f\n",
