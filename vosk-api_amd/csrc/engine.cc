@@ -811,6 +811,8 @@ Engine::~Engine() {
   if (dstream_) (void)hipStreamDestroy(dstream_);
   if (fstream_) (void)hipStreamDestroy(fstream_);
   if (call_stream_) (void)hipStreamSynchronize(call_stream_);
+  if (d_pack_) (void)hipFree(d_pack_);
+  if (d_pack_items_) (void)hipFree(d_pack_items_);
   if (d_call_raw_) (void)hipFree(d_call_raw_);
   if (d_call_out_) (void)hipFree(d_call_out_);
   if (d_call_jobs_) (void)hipFree(d_call_jobs_);
@@ -1843,19 +1845,39 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
     cb->pool = pinned_;
     cb->device = cfg_.device;
     cb->block = pinned_->Take(bytes, &cb->cap);
+    // the records gathered into one device block in the host layout (a
+    // workgroup per record range), then one copy to the pinned block
+    std::vector<CopyItem> items;
+    items.reserve(copied.size() * 3);
+    auto add = [&](const void* src, size_t off, size_t nbytes) {
+      if (nbytes == 0) return;
+      if ((nbytes | off) & 3) VAMD_ERR("segment copy: unaligned record range");
+      items.push_back(CopyItem{(const unsigned*)src, (long long)(off / 4), (long long)(nbytes / 4)});
+    };
     for (int i : copied) {
       SegmentCopy& c = *(*out)[i];
       c.batch = cb;
       const size_t s = (size_t)slots[i];
-      if (c.nf > 0)
-        HIPCHECK(hipMemcpyAsync(cb->block + c.f, dec_.lat_frames + s * dec_.lat_frame_cap,
-                                sizeof(LatFrame) * c.nf, hipMemcpyDeviceToHost, copy_stream_));
-      if (c.na > 0)
-        HIPCHECK(hipMemcpyAsync(cb->block + c.a, dec_.arena + s * dec_.arena_cap, sizeof(int4) * c.na,
-                                hipMemcpyDeviceToHost, copy_stream_));
-      if (c.nl > 0)
-        HIPCHECK(hipMemcpyAsync(cb->block + c.l, dec_.links + s * dec_.link_cap, sizeof(int4) * c.nl,
-                                hipMemcpyDeviceToHost, copy_stream_));
+      add(dec_.lat_frames + s * dec_.lat_frame_cap, c.f, sizeof(LatFrame) * c.nf);
+      add(dec_.arena + s * dec_.arena_cap, c.a, sizeof(int4) * c.na);
+      add(dec_.links + s * dec_.link_cap, c.l, sizeof(int4) * c.nl);
+    }
+    if (bytes > pack_cap_) {
+      if (d_pack_) HIPCHECK(hipFree(d_pack_));
+      pack_cap_ = bytes + bytes / 4;
+      HIPCHECK(hipMalloc((void**)&d_pack_, pack_cap_));
+    }
+    if (items.size() > pack_items_cap_) {
+      if (d_pack_items_) HIPCHECK(hipFree(d_pack_items_));
+      pack_items_cap_ = items.size() + items.size() / 4 + 16;
+      HIPCHECK(hipMalloc((void**)&d_pack_items_, sizeof(CopyItem) * pack_items_cap_));
+    }
+    if (!items.empty()) {
+      HIPCHECK(hipMemcpyAsync(d_pack_items_, items.data(), sizeof(CopyItem) * items.size(),
+                              hipMemcpyHostToDevice, copy_stream_));
+      LaunchGatherCopy(d_pack_items_, (int)items.size(), d_pack_, copy_stream_);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(cb->block, d_pack_, bytes, hipMemcpyDeviceToHost, copy_stream_));
     }
     // a waiting worker sleeps, not spins
     HIPCHECK(hipEventCreateWithFlags(&cb->done, hipEventDisableTiming | hipEventBlockingSync));

@@ -478,7 +478,10 @@ class Engine {
   long long copy_us_[4] = {0, 0, 0, 0}, copy_calls_ = 0;  // development (VOSK_AMD_COPY_DEBUG)
   std::shared_ptr<PinnedPool> pinned_ = std::make_shared<PinnedPool>();
   DecSlot* h_copy_slots_ = nullptr;  // decoder-state snapshot of the segment copies
-  int* d_prune_slots_ = nullptr;     // stream list of the segments' final prune
+  int* d_prune_slots_ = nullptr;
+  unsigned* d_pack_ = nullptr;     // segment copies: records gathered on the device
+  CopyItem* d_pack_items_ = nullptr;
+  size_t pack_cap_ = 0, pack_items_cap_ = 0;     // stream list of the segments' final prune
   hipEvent_t copy_ev_ = nullptr;  // last asynchronous segment copy (decoder launches wait for it)
   bool copy_pending_ = false;
   // device: per-stream state

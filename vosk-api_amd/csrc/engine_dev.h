@@ -113,6 +113,11 @@ struct ResampleJob {  // outputs [out_first, out_first + count) into the sample 
   long long out_first, raw_total;  // raw samples available (later ones read as 0)
 };
 
+struct CopyItem {  // gather copy: nwords 32-bit words from src to dst + dst_off
+  const unsigned* src;
+  long long dst_off, nwords;
+};
+
 struct SampleJob {  // append count samples from src[] to ring position pos
   int slot, pos, count, pad;
   const float* src;  // staging buffer (host-fed) or the stream's HBM-resident audio

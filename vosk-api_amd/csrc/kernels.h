@@ -9,6 +9,9 @@ namespace vamd {
 
 void LaunchAppendSamples(const SampleJob* jobs, int njobs, float* ring, int ring_len,
                          hipStream_t s);
+// One workgroup per item: the segments' lattice records gathered into one
+// contiguous block (one device-to-host copy instead of three per segment).
+void LaunchGatherCopy(const CopyItem* items, int nitems, unsigned* dst, hipStream_t s);
 void LaunchResample(const ResampleJob* jobs, int njobs, const ResampleDev* tables, const float* raw,
                     int raw_len, float* ring, int ring_len, hipStream_t s);
 void LaunchMfcc(const MfccDev& m, const MfccJob* jobs, int njobs, int total_frames,

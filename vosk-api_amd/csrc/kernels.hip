@@ -104,6 +104,17 @@ __global__ __launch_bounds__(256) void resample_kernel(const ResampleJob* jobs,
   }
 }
 
+__global__ __launch_bounds__(256) void gather_copy_kernel(const CopyItem* items, unsigned* dst) {
+  const CopyItem it = items[blockIdx.x];
+  unsigned* d = dst + it.dst_off;
+  for (long long i = threadIdx.x; i < it.nwords; i += blockDim.x) d[i] = it.src[i];
+}
+
+void LaunchGatherCopy(const CopyItem* items, int nitems, unsigned* dst, hipStream_t s) {
+  if (nitems <= 0) return;
+  hipLaunchKernelGGL(gather_copy_kernel, dim3(nitems), dim3(256), 0, s, items, dst);
+}
+
 void LaunchResample(const ResampleJob* jobs, int njobs, const ResampleDev* tables, const float* raw,
                     int raw_len, float* ring, int ring_len, hipStream_t s) {
   if (njobs <= 0) return;
