@@ -777,6 +777,15 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   HIPCHECK(hipHostMalloc((void**)&h_slots_, sizeof(DecSlot) * S, hipHostMallocDefault));
   HIPCHECK(hipHostMalloc((void**)&h_stats_, sizeof(FrameStat) * max_dec_frames_, hipHostMallocDefault));
   for (auto& ev : ev_) HIPCHECK(hipEventCreate(&ev));
+  // the segment copies' pinned pool starts with one block (128 KB per
+  // channel, at most 128 MB): pinning host memory when the first segments end
+  // costs ~5 ms per 20 MB on the lane thread
+  if (cfg_.lattice) {
+    const size_t want = std::min<size_t>((size_t)S << 17, (size_t)128 << 20);
+    char* blk = nullptr;
+    HIPCHECK(hipHostMalloc((void**)&blk, want, hipHostMallocDefault));
+    pinned_->Give(blk, want);
+  }
   HIPCHECK(hipStreamSynchronize(stream_));
   slots_.resize(S);
   VAMD_LOG("engine: slots=" << S << " fpc=" << fpc << " priming=" << plan_.priming_chunks
@@ -789,6 +798,9 @@ Engine::~Engine() {
     fprintf(stderr, "[engine] steps %lld: build %.3f ms, sync wait %.3f ms, after sync %.3f ms, total %.3f ms per step\n",
             step_prof_n_, step_prof_[0] / step_prof_n_, step_prof_[1] / step_prof_n_, step_prof_[2] / step_prof_n_,
             step_prof_[3] / step_prof_n_);
+  if (copy_prof_n_ && getenv("VOSK_AMD_STEP_PROFILE"))
+    fprintf(stderr, "[engine] segment copy calls %lld: prune + state read %.3f ms, pinned take %.3f ms, after %.3f ms (total over calls)\n",
+            copy_prof_n_, copy_prof_[0], copy_prof_[1], copy_prof_[2]);
   (void)hipSetDevice(cfg_.device);
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (dstream_) (void)hipStreamSynchronize(dstream_);
@@ -1818,9 +1830,12 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
                             copy_stream_));
     LaunchPruneFinal(dec_, d_prune_slots_, (int)slots.size(), true, copy_stream_);
   }
+  const auto tc0 = std::chrono::steady_clock::now();
   HIPCHECK(hipMemcpyAsync(h_copy_slots_, d_slots_, sizeof(DecSlot) * slots_.size(), hipMemcpyDeviceToHost,
                           copy_stream_));
   HIPCHECK(hipStreamSynchronize(copy_stream_));
+  const auto tc1 = std::chrono::steady_clock::now();
+  copy_prof_[0] += std::chrono::duration<double, std::milli>(tc1 - tc0).count();
   // one pinned block and one completion event for all of the call's segments
   size_t bytes = 0;
   std::vector<int> copied;
@@ -1844,7 +1859,9 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
     auto cb = std::make_shared<CopyBatch>();
     cb->pool = pinned_;
     cb->device = cfg_.device;
+    const auto tt0 = std::chrono::steady_clock::now();
     cb->block = pinned_->Take(bytes, &cb->cap);
+    copy_prof_[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tt0).count();
     // the records gathered into one device block in the host layout (a
     // workgroup per record range), then one copy to the pinned block
     std::vector<CopyItem> items;
@@ -1887,6 +1904,8 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
   // records) waits for the copies on the device
   HIPCHECK(hipEventRecord(copy_ev_, copy_stream_));
   copy_pending_ = true;
+  copy_prof_[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc1).count();
+  copy_prof_n_++;
 }
 
 void Engine::TakeDecoded(std::vector<DecodedJob>* out) {

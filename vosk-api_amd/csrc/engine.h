@@ -466,6 +466,8 @@ class Engine {
   hipStream_t copy_stream_ = nullptr;  // segment lattice copies
   double step_prof_[4] = {0, 0, 0, 0};  // Step host profile: build, sync wait, after sync, total (ms)
   long long step_prof_n_ = 0;
+  double copy_prof_[3] = {0, 0, 0};  // StartSegmentCopies: prune + state read, pinned take, rest (ms)
+  long long copy_prof_n_ = 0;
   int ResampleTableLocked(int rate);    // the table of an input rate (created on first use)
   std::mutex call_mu_;                 // ResampleCall's stream and buffers
   hipStream_t call_stream_ = nullptr;
