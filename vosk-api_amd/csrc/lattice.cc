@@ -456,14 +456,21 @@ bool Determinize(const DetGraph& D, const LatticeOptions& opt, WordLattice* out)
         dbg_ext++;
         for (int k = ob[e.tok]; k < oe[e.tok]; k++) {
           const auto& l = cl[k];
-          Elem n{l.dst, Times(e.w, LW{l.g, l.a}), extend(e.str, k)};
-          const int ei = at.find_idx(n.tok);
+          const LW w = Times(e.w, LW{l.g, l.a});
+          const int ei = at.find_idx(l.dst);
           if (ei < 0) {
-            at.set(n.tok, (int)sub->size());
-            sub->push_back(n);
+            at.set(l.dst, (int)sub->size());
+            sub->push_back(Elem{l.dst, w, extend(e.str, k)});
             pending.push_back(1);
             push((int)sub->size() - 1);
-          } else if (ElemBetter(R, base, n, (*sub)[ei])) {
+            continue;
+          }
+          // the string only when the weight does not decide (ElemBetter's
+          // order): a losing candidate adds no trie node
+          const int c = CompareLW(w, (*sub)[ei].w);
+          if (c < 0) continue;
+          const Elem n{l.dst, w, extend(e.str, k)};
+          if (c > 0 || R.Less(n.str, (*sub)[ei].str, base)) {
             (*sub)[ei] = n;
             if (!pending[ei]) {
               pending[ei] = 1;
