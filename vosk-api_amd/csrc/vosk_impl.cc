@@ -1008,7 +1008,16 @@ void BatchModel::EmitSegments(Lane* L, const std::vector<BatchRecognizer*>& rs, 
   if (!cslots.empty()) e->StartSegmentCopies(cslots, &started);
   for (size_t k = 0; k < ci.size(); k++) copies[ci[k]] = started[k];
   prof_[2] += ns(tc, clk::now());
-  for (size_t i = 0; i < rs.size(); i++) {
+  // the largest lattices first (longest-processing-time order over the
+  // result workers: the batch's tail is not one big segment started last);
+  // each stream has one segment here, so its results stay in order
+  std::vector<size_t> order(rs.size());
+  for (size_t i = 0; i < rs.size(); i++) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
+    const long long nx = copies[x] ? copies[x]->nl : 0, ny = copies[y] ? copies[y]->nl : 0;
+    return nx > ny;
+  });
+  for (size_t i : order) {
     prof_[0]++;
     if (copies[i]) prof_[1] += copies[i]->nl;
     EmitSegment(L, rs[i], final_segment, copies[i], frames[i]);
