@@ -1,5 +1,9 @@
 // Vosk object layer (see vosk_impl.h).
 #include "vosk_impl.h"
+
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include "graph_compose.h"
 
 #include <sched.h>
@@ -650,8 +654,14 @@ const char* Recognizer::StoreReturn(const std::string& s) {
 // ---------------------------------------------------------------------------
 // WorkerPool
 // ---------------------------------------------------------------------------
-WorkerPool::WorkerPool(int n) {
-  for (int i = 0; i < std::max(1, n); i++) threads_.emplace_back([this] { Run(); });
+WorkerPool::WorkerPool(int n, int nice) {
+  for (int i = 0; i < std::max(1, n); i++)
+    threads_.emplace_back([this, nice] {
+      // result work yields to the lanes and the callers' threads when the
+      // cores are contended (a thread may always lower its own priority)
+      if (nice > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice);
+      Run();
+    });
 }
 
 WorkerPool::~WorkerPool() {
@@ -788,13 +798,14 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
     const int omp = EnvInt("OMP_NUM_THREADS", 0);
     if (omp > 0) hc = std::min(hc, omp);
   }
-  // all but two of them (the feeding thread and the lane threads keep
-  // theirs): a stream's final segments all arrive together at FinishStream,
-  // when the GPU side is idle, and their lattice work is the tail of the
-  // batch; during chunk rounds the workers only see endpoint segments
+  // all but the lane threads' (the feeding thread sleeps in Wait() while
+  // the tail runs): a stream's final segments all arrive together at
+  // FinishStream, when the GPU side is idle, and their lattice work is the
+  // tail of the batch; during chunk rounds the workers only see endpoint
+  // segments, at a lower priority (nice 5) than the lanes and the callers
   const int cores = std::min(hc > 0 ? hc : 8, 16 * (int)lanes_.size());
-  int nt = EnvInt("VOSK_AMD_RESULT_THREADS", std::max(2, cores - 1 - (int)lanes_.size()));
-  pool_.reset(new WorkerPool(nt));
+  int nt = EnvInt("VOSK_AMD_RESULT_THREADS", std::max(2, cores - (int)lanes_.size()));
+  pool_.reset(new WorkerPool(nt, 5));
   for (auto& L : lanes_) {
     Lane* l = L.get();
     l->thread = std::thread([this, l] { LaneLoop(l); });

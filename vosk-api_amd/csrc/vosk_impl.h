@@ -185,7 +185,7 @@ bool FeedingRoundIncomplete(const std::vector<std::array<long long, 3>>& streams
 // threads, src/batch_model.cc:69, callback src/batch_recognizer.cc:138-149).
 class WorkerPool {
  public:
-  explicit WorkerPool(int threads);
+  explicit WorkerPool(int threads, int nice = 0);
   ~WorkerPool();
   void Submit(std::function<void()> task);
   void WaitIdle();
