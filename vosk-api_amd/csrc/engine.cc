@@ -973,15 +973,16 @@ int Engine::ResampleTableLocked(int rate) {
   return t;
 }
 
-std::vector<float> Engine::ResampleCall(int rate, const float* x, int n) {
-  int t;
-  long long n_out;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    DEVICE_GUARD();
-    t = ResampleTableLocked(rate);
-    n_out = res_tables_[t].NumOutputSamples(n, true);
-  }
+int Engine::ResampleTableFor(int rate, ResampleTable* copy) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
+  const int t = ResampleTableLocked(rate);
+  *copy = res_tables_[t];
+  return t;
+}
+
+std::vector<float> Engine::ResampleCall(int t, const ResampleTable& T, const float* x, int n) {
+  const long long n_out = T.NumOutputSamples(n, true);
   std::vector<float> out((size_t)n_out);
   if (n_out == 0) return out;
   std::lock_guard<std::mutex> lk(call_mu_);

@@ -268,7 +268,11 @@ class Engine {
   // input, flush = true) per call, src/batch_recognizer.cc:27-29,157-158):
   // the call's samples to the device, resample_kernel over the whole call,
   // the model-rate samples back.  Thread-safe; its own HIP stream.
-  std::vector<float> ResampleCall(int rate, const float* x, int n);
+  // ResampleTableFor: the table of an input rate (created on first use) and
+  // a copy of it (its NumOutputSamples); ResampleCall then takes only the
+  // calls' own lock, never the engine's (a lane step holds that one).
+  int ResampleTableFor(int rate, ResampleTable* copy);
+  std::vector<float> ResampleCall(int table, const ResampleTable& T, const float* x, int n);
   void AcceptSamples(int slot, const float* x, int n);
   // The same, taking the buffer (no copy when the stream's pending samples
   // are all consumed, the batch lane's usual case)

@@ -1304,6 +1304,7 @@ BatchRecognizer::BatchRecognizer(BatchModel* model, float sr) : model_(model), s
   const int model_rate = (int)std::lround(model_->data().mfcc.samp_freq);
   call_rate_ = rate == model_rate ? 0 : rate;
   model_->Admit(this, model_rate);
+  if (call_rate_) call_table_ = model_->lane_engine(lane_)->ResampleTableFor(call_rate_, &call_tab_);
   model_->Ref();
 }
 
@@ -1316,7 +1317,7 @@ void BatchRecognizer::AcceptWaveform(const char* data, int len) {  // batch_reco
   const short* s = reinterpret_cast<const short*>(data);
   if (call_rate_) {
     std::vector<float> x(s, s + len / 2);
-    std::vector<float> y = model_->lane_engine(lane_)->ResampleCall(call_rate_, x.data(), (int)x.size());
+    std::vector<float> y = model_->lane_engine(lane_)->ResampleCall(call_table_, call_tab_, x.data(), (int)x.size());
     buffer_.insert(buffer_.end(), y.begin(), y.end());
   } else {
     buffer_.insert(buffer_.end(), s, s + len / 2);

@@ -301,6 +301,8 @@ class BatchRecognizer {
   bool nlsml_ = false;
   std::vector<float> buffer_;  // model-rate samples not yet pushed as a chunk
   int call_rate_ = 0;          // input rate resampled per call (0: the model's rate)
+  int call_table_ = -1;        // its table on the lane's engine (and a host copy)
+  ResampleTable call_tab_;
   // lane state (guarded by the lane's mutex)
   int lane_ = -1, slot_ = -1;
   std::deque<Chunk> queue_;
