@@ -817,6 +817,7 @@ Engine::~Engine() {
   if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
   if (h_lat_stage_) (void)hipHostFree(h_lat_stage_);
   if (h_copy_slots_) (void)hipHostFree(h_copy_slots_);
+  if (h_copy_stage_) (void)hipHostFree(h_copy_stage_);
   if (copy_ev_) (void)hipEventDestroy(copy_ev_);
   if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -1827,7 +1828,15 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
   const bool final_prune = !getenv("VOSK_AMD_FINAL_PRUNE") || atoi(getenv("VOSK_AMD_FINAL_PRUNE")) != 0;
   if (final_prune) {
     if (!d_prune_slots_) d_prune_slots_ = (int*)DevAlloc(sizeof(int) * slots_.size());
-    HIPCHECK(hipMemcpyAsync(d_prune_slots_, slots.data(), sizeof(int) * slots.size(), hipMemcpyHostToDevice,
+    // from pinned staging (a pageable source makes the copy synchronous):
+    // [slots][items]; the slot part's last reader is the previous call's
+    // copy, finished at that call's synchronization below
+    if (!h_copy_stage_)
+      HIPCHECK(hipHostMalloc((void**)&h_copy_stage_,
+                             Align256(sizeof(int) * slots_.size()) + sizeof(CopyItem) * 3 * slots_.size(),
+                             hipHostMallocDefault));
+    memcpy(h_copy_stage_, slots.data(), sizeof(int) * slots.size());
+    HIPCHECK(hipMemcpyAsync(d_prune_slots_, h_copy_stage_, sizeof(int) * slots.size(), hipMemcpyHostToDevice,
                             copy_stream_));
     LaunchPruneFinal(dec_, d_prune_slots_, (int)slots.size(), true, copy_stream_);
   }
@@ -1891,8 +1900,14 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
       HIPCHECK(hipMalloc((void**)&d_pack_items_, sizeof(CopyItem) * pack_items_cap_));
     }
     if (!items.empty()) {
-      HIPCHECK(hipMemcpyAsync(d_pack_items_, items.data(), sizeof(CopyItem) * items.size(),
-                              hipMemcpyHostToDevice, copy_stream_));
+      const CopyItem* src = items.data();
+      if (h_copy_stage_ && items.size() <= 3 * slots_.size()) {  // (every earlier copy is finished here)
+        CopyItem* st = (CopyItem*)(h_copy_stage_ + Align256(sizeof(int) * slots_.size()));
+        memcpy(st, items.data(), sizeof(CopyItem) * items.size());
+        src = st;
+      }
+      HIPCHECK(hipMemcpyAsync(d_pack_items_, src, sizeof(CopyItem) * items.size(), hipMemcpyHostToDevice,
+                              copy_stream_));
       LaunchGatherCopy(d_pack_items_, (int)items.size(), d_pack_, copy_stream_);
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipMemcpyAsync(cb->block, d_pack_, bytes, hipMemcpyDeviceToHost, copy_stream_));

@@ -484,6 +484,7 @@ class Engine {
   long long copy_us_[4] = {0, 0, 0, 0}, copy_calls_ = 0;  // development (VOSK_AMD_COPY_DEBUG)
   std::shared_ptr<PinnedPool> pinned_ = std::make_shared<PinnedPool>();
   DecSlot* h_copy_slots_ = nullptr;  // decoder-state snapshot of the segment copies
+  char* h_copy_stage_ = nullptr;     // pinned staging of the segment copies' slot list and gather items
   int* d_prune_slots_ = nullptr;
   unsigned* d_pack_ = nullptr;     // segment copies: records gathered on the device
   CopyItem* d_pack_items_ = nullptr;
