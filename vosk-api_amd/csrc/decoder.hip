@@ -32,6 +32,27 @@
 
 namespace vamd {
 
+// Per-stream scratch in global memory (frame tables, token lists, Kaldi-order
+// bookkeeping) is private to the stream's workgroup during a launch: its
+// plain loads and stores need only workgroup scope (the CU's vector L1 is
+// shared by the workgroup's waves and write-through), not the agent scope of
+// dev_util.h, which sends every load to L2.  Launch boundaries order it
+// across kernels.
+#undef AG_LD
+#undef AG_ST
+#define AG_LD(p) __hip_atomic_load((p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#define AG_ST(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+__device__ __forceinline__ int4 wg_ld4(const int4* p) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(const_cast<int4*>(p));
+  const unsigned long long lo = AG_LD(q), hi = AG_LD(q + 1);
+  return make_int4((int)(unsigned)lo, (int)(unsigned)(lo >> 32), (int)(unsigned)hi, (int)(unsigned)(hi >> 32));
+}
+__device__ __forceinline__ void wg_st4(int4* p, int4 v) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  AG_ST(q, (unsigned long long)(unsigned)v.x | ((unsigned long long)(unsigned)v.y << 32));
+  AG_ST(q + 1, (unsigned long long)(unsigned)v.z | ((unsigned long long)(unsigned)v.w << 32));
+}
+
 #ifndef VAMD_DEC_THREADS
 #define VAMD_DEC_THREADS 1024
 #endif
@@ -90,17 +111,23 @@ struct DecShared {
   int ksum_w[2][DW];
   int kn0, kne;
   int kpop_sum, kpop_max;  // component replay: pops over all lanes / on the longest lane
+  int kcomp_n, kcomp_max;  // component replay: components / pops of the largest (profile)
 };
 
 // optional phase clocks (VOSK_AMD_DEC_PROFILE): thread 0 stamps s_memtime
 // at phase ends; slots as vosk/engine.py Engine.PHASES
+// The accumulators live in LDS (a register array of kDecProf 64-bit values
+// per thread would spill the whole kernel to scratch and time a different
+// program); only thread 0 touches them.
 struct Prof {
   bool on;
   long long t;
-  long long acc[kDecProf];
-  __device__ __forceinline__ void init(bool o) {
+  long long* acc;  // [kDecProf] in LDS
+  __device__ __forceinline__ void init(bool o, long long* lds_acc) {
     on = o;
-    for (int i = 0; i < kDecProf; i++) acc[i] = 0;
+    acc = lds_acc;
+    if (on)
+      for (int i = 0; i < kDecProf; i++) acc[i] = 0;
     t = on ? (long long)__builtin_amdgcn_s_memtime() : 0;
   }
   __device__ __forceinline__ void mark(int i) {
@@ -1182,7 +1209,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   int2* KA = a.kadj + (long long)slot * a.kadj_cap;
   int* BF = a.kb_first + (long long)slot * a.kb_cap;
   int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
-  int* BM = a.kb_memb + (long long)slot * a.kb_cap * 4;
+  int* BM = a.kb_memb + (long long)slot * a.kb_cap * kKbMemb;
   const float kInf = __int_as_float(0x7f800000);
   // the emitting pass's tokens: buckets, queue costs, stamps cleared for the
   // closure's rounds, and the closure's first frontier (tokens with epsilon arcs)
@@ -1198,7 +1225,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     AG_ST(&KB[c], b);
     __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (m < 4) AG_ST(&BM[4 * b + m], c);
+    if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], c);
     AG_ST(&KC[c], funord((uint32_t)(slot_key(t, T, v) >> 32)));
     if (v >= 0) t.hst[v] = kNoStamp;
     else AG_ST(&T.stamp[~v], kNoStamp);
@@ -1208,6 +1235,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   vm_drain();
   __syncthreads();
   const int nl_e = sh.n_new_l, ng_e = sh.n_new_g;
+  pr.mark(47);
   eps_closure(a, sh, t, T, p, st, cutoff, sh.n_front, arcs_eps, pr);
   __syncthreads();
   pr.mark(5);
@@ -1230,7 +1258,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
       if (AG_LD(&BF[b]) > ne) AG_ST(&BF[b], ne);
       const int m = AG_LD(&BC[b]);
       AG_ST(&BC[b], m + 1);
-      if (m < 4) AG_ST(&BM[4 * b + m], ne);
+      if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], ne);
     }
     vm_drain();
     __syncthreads();
@@ -1458,6 +1486,8 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
       sh.flag = 0;
       sh.kpop_sum = 0;
       sh.kpop_max = 0;
+      sh.kcomp_n = 0;
+      sh.kcomp_max = 0;
     }
     vm_drain();
     __syncthreads();
@@ -1513,8 +1543,9 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
         __syncthreads();
         bitonic_sort32(key, ns);
         pr.mark(41);
-        // one wave per component: the waves claim 64 sorted positions at a
-        // time and replay every component that starts there.  A popped
+        // one wave per component: the waves claim kWin sorted positions at a
+        // time and replay every component that starts there (a small window:
+        // the components spread over all waves).  A popped
         // token's arcs are read by the wave's lanes together (records, then
         // the destinations' costs and arc counts), then applied in arc order
         // (v_readlane; a later arc to the same token sees the new cost); the
@@ -1526,28 +1557,36 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
         int npop = 0;
         bool ovf = false;
         while (!ovf) {
+          constexpr int kWin = 4;
           int c0 = 0;
-          if (lane == 0) c0 = atomicAdd(&sh.kk, 64);
+          if (lane == 0) c0 = atomicAdd(&sh.kk, kWin);
           c0 = __builtin_amdgcn_readfirstlane(c0);
           if (c0 >= ns) break;
           const int pos = c0 + lane;
-          const bool head = pos < ns && (pos == 0 || (key[pos - 1] >> 10) != (key[pos] >> 10));
+          const bool head = lane < kWin && pos < ns && (pos == 0 || (key[pos - 1] >> 10) != (key[pos] >> 10));
           unsigned long long hm = __ballot(head);
           while (hm && !ovf) {
             const int h = c0 + __ffsll((long long)hm) - 1;
             hm &= hm - 1;
-            const unsigned cmp = key[h] >> 10;
-            for (int ri = h; ri < ns && (key[ri] >> 10) == cmp && !ovf; ri++) {
-              const int prank = (int)(key[ri] & 1023u);
+            // (LDS values the whole wave reads are made scalar: branching on
+            // them would otherwise make the replay loop divergent, every
+            // v_readlane a waterfall loop)
+            const unsigned cmp = (unsigned)__builtin_amdgcn_readfirstlane((int)(key[h] >> 10));
+            const int npop0 = npop;
+            for (int ri = h; ri < ns && !ovf; ri++) {
+              const unsigned kr = (unsigned)__builtin_amdgcn_readfirstlane((int)key[ri]);
+              if ((kr >> 10) != cmp) break;
+              const int prank = (int)(kr & 1023u);
               int stk = lane == 0 ? stk_at(n0 - 1 - (base + prank)) : 0;
               int sp = 1, j = 0;
               while (sp > 0 && !ovf) {
                 --sp;
                 npop++;
                 const int u = __builtin_amdgcn_readlane(stk, sp);
-                const float cu = __int_as_float(km_get(K, KM, u, kMCost));
+                const float cu = __int_as_float(__builtin_amdgcn_readfirstlane(km_get(K, KM, u, kMCost)));
                 if (!(cu < cutoff)) continue;
-                const int off = km_get(K, KM, u, kMOff), cnt = km_get(K, KM, u, kMCnt);
+                const int off = __builtin_amdgcn_readfirstlane(km_get(K, KM, u, kMOff));
+                const int cnt = __builtin_amdgcn_readfirstlane(km_get(K, KM, u, kMCnt));
                 for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
                   const int kn = cnt - k0 < 64 ? cnt - k0 : 64;
                   const int2 rec = lane < kn ? adj_at(off + k0 + lane) : make_int2(-1, 0);
@@ -1584,6 +1623,10 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
                 }
               }
               if (lane == 0) K.v0lo[prank] = j;
+            }
+            if (lane == 0) {
+              atomicAdd(&sh.kcomp_n, 1);
+              atomicMax(&sh.kcomp_max, npop - npop0);
             }
           }
         }
@@ -1836,6 +1879,8 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   if (replayed) {
     pr.count(32, sh.kpop_sum);
     pr.count(33, sh.kpop_max);
+    pr.count(45, sh.kcomp_n);
+    pr.count(46, sh.kcomp_max);
   }
   // the created tokens' creation indices [ne, ne + n_eps) in the queue's order, and their buckets
   for (int i = threadIdx.x; i < nm; i += DT) {
@@ -1849,7 +1894,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     AG_ST(&KB[c], b);
     __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (m < 4) AG_ST(&BM[4 * b + m], c);
+    if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], c);
   }
   vm_drain();
   __syncthreads();
@@ -1862,13 +1907,15 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
 // stamp (slot_pos).  Bucket starts: a scan over the creation order in which
 // each bucket's first token contributes the bucket's size.
 __device__ __forceinline__ void kaldi_positions(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
-                                                int slot, int n) {
+                                                int slot, int n, Prof& pr) {
+  int crowded = 0;
+  if (threadIdx.x == 0) sh.kk = 0;  // crowded buckets (profile count; visible after the scans' barriers)
   const int* KO = a.kord + (long long)slot * a.kord_cap;
   const int* KB = a.kbkt + (long long)slot * a.kord_cap;
   int* BF = a.kb_first + (long long)slot * a.kb_cap;
   int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
   int* BS = a.kb_start + (long long)slot * a.kb_cap;
-  int* BM = a.kb_memb + (long long)slot * a.kb_cap * 4;
+  int* BM = a.kb_memb + (long long)slot * a.kb_cap * kKbMemb;
   int run = 0, par = 0;
   for (int c0 = 0; c0 < n; c0 += DT) {
     const int c = c0 + threadIdx.x;
@@ -1893,19 +1940,25 @@ __device__ __forceinline__ void kaldi_positions(const DecArgs& a, DecShared& sh,
     const int v = AG_LD(&KO[c]);
     // (issued together)
     const int cnt = AG_LD(&BC[b]), bs = AG_LD(&BS[b]);
-    const int4 mb = ag_ld4(reinterpret_cast<const int4*>(&BM[4 * b]));
     int rk = 0;
-    if (cnt <= 4) {
-      rk = (cnt > 0 && mb.x < c) + (cnt > 1 && mb.y < c) + (cnt > 2 && mb.z < c) + (cnt > 3 && mb.w < c);
-    } else {  // a crowded bucket: count its tokens created before
+    if (cnt > 1 && cnt <= kKbMemb) {  // the bucket's members created before c
+      for (int m = 0; m < cnt; m += 4) {
+        const int4 q = wg_ld4(reinterpret_cast<const int4*>(&BM[kKbMemb * b + m]));
+        rk += (q.x < c) + (m + 1 < cnt && q.y < c) + (m + 2 < cnt && q.z < c) + (m + 3 < cnt && q.w < c);
+      }
+    } else if (cnt > kKbMemb) {  // a crowded bucket: count its tokens created before
+      crowded++;
       for (int c2 = 0; c2 < c; c2++) rk += AG_LD(&KB[c2]) == b;
     }
     const int pos = bs + rk;
     if (v >= 0) t.hst[v] = pos;
     else AG_ST(&T.stamp[~v], pos);
   }
+  if (crowded) atomicAdd(&sh.kk, crowded);
   vm_drain();
   __syncthreads();
+  pr.count(44, sh.kk);
+  pr.mark(43);
 }
 
 // the buckets the frame used, emptied for the next one
@@ -2060,7 +2113,7 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   const bool ok = (long long)base + n <= a.arena_cap && !(a.kaldi && sh.bad);
   const bool lat = a.links != nullptr;
   // Kaldi order: the tokens' list positions (slot_pos) first
-  if (a.kaldi && ok) kaldi_positions(a, sh, t, T, slot, n);
+  if (a.kaldi && ok) kaldi_positions(a, sh, t, T, slot, n, pr);
   // the emitting records first: with deferred winners they set the
   // backpointers the token commit below reads (Kaldi order: every record is
   // an accepted relaxation, kept)
@@ -2131,7 +2184,7 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
       // arena offset: the creation index, or the list position (Kaldi order,
       // whose current-token arrays are in list order)
       const int ao = a.kaldi ? slot_pos(a, t, T, nl_n, v) : j;
-      ag_st4(&p.arena[base + ao], make_int4(prev, arc, __float_as_int(cost), s));
+      wg_st4(&p.arena[base + ao], make_int4(prev, arc, __float_as_int(cost), s));
       const int qa = atomicAdd(&sh.n_next, 1);
       const int q = a.kaldi ? ao : qa;
       if (q < a.max_tok) {  // the current-token arrays hold max_tok entries
@@ -2152,7 +2205,7 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
       bk = tk < bk ? tk : bk;
       mx = fmaxf(mx, cost);
     } else if (ok) {
-      ag_st4(&p.arena[base + j], make_int4(-2, -1, __float_as_int(cost), s));  // dead list entry
+      wg_st4(&p.arena[base + j], make_int4(-2, -1, __float_as_int(cost), s));  // dead list entry
     }
    }
   }
@@ -2301,7 +2354,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
   } else {
     float bn = kInf, bf = kInf;
     for (int t = tbF + threadIdx.x; t < endF; t += DT) {
-      const int4 r = ag_ld4(&AR[t]);
+      const int4 r = wg_ld4(&AR[t]);
       if (r.x == -2) continue;  // a dead list entry
       const float c = __int_as_float(r.z);
       bn = fminf(bn, c);
@@ -2312,7 +2365,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
     const bool use_f = use_final && bf != kInf;
     const float best = use_f ? bf : bn;
     for (int t = tbF + threadIdx.x; t < endF; t += DT) {
-      const int4 r = ag_ld4(&AR[t]);
+      const int4 r = wg_ld4(&AR[t]);
       float x = kInf;
       if (r.x != -2) {
         const float c = __int_as_float(r.z), fc = use_f ? __int_as_float(a.sinfo[r.w].w) : 0.0f;
@@ -2548,7 +2601,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
         const int rv = AG_LD(&R[t - wb]);
         if ((rv & kDropped) == 0) {
           nt[u] = rv;
-          rec[u] = ag_ld4(&AR[t]);
+          rec[u] = wg_ld4(&AR[t]);
           x[u] = AG_LD(&X[t]);
           if (rec[u].x >= wb) {
             const int np = AG_LD(&R[rec[u].x - wb]);
@@ -2570,7 +2623,7 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
 #pragma unroll
     for (int u = 0; u < kPI; u++)
       if (nt[u] >= 0) {
-        ag_st4(&AR[nt[u]], rec[u]);
+        wg_st4(&AR[nt[u]], rec[u]);
         AG_ST(&X[nt[u]], x[u]);
       }
     __syncthreads();
@@ -2648,7 +2701,8 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   int arcs_eps = 0;
   bool lds = false;
   Prof pr;
-  pr.init(PROF && threadIdx.x == 0);
+  __shared__ long long prof_acc[PROF ? kDecProf : 1];
+  pr.init(PROF && threadIdx.x == 0, prof_acc);
 
   if (job.reset) {  // InitDecoding: start token, closure with cutoff = beam
     __syncthreads();
@@ -2940,7 +2994,7 @@ __global__ __launch_bounds__(DT) void prune_final_kernel(DecArgs a, const int* s
   p.fg0 = a.front_g + ((long long)slot * 2) * a.max_tok;
   p.fg1 = p.fg0 + a.max_tok;
   Prof pr;
-  pr.init(false);
+  pr.init(false, nullptr);
   if (threadIdx.x == 0) sh.bad = 0;
   __syncthreads();
   prune_segment<true>(a, sh, st, p, slot, pr, use_final != 0);

@@ -738,7 +738,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     dec_.kb_first = (int*)DevAlloc(sizeof(int) * KB);
     dec_.kb_cnt = (int*)DevAlloc(sizeof(int) * KB);
     dec_.kb_start = (int*)DevAlloc(sizeof(int) * KB);
-    dec_.kb_memb = (int*)DevAlloc(sizeof(int) * 4 * KB);
+    dec_.kb_memb = (int*)DevAlloc(sizeof(int) * kKbMemb * KB);
     dec_.kord = (int*)DevAlloc(sizeof(int) * KO);
     dec_.kbkt = (int*)DevAlloc(sizeof(int) * KO);
     dec_.kstk = (int*)DevAlloc(sizeof(int) * KO);

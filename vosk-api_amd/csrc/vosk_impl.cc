@@ -1044,6 +1044,7 @@ void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment,
   };
   const double offset = r->segment_offset_;
   r->segment_offset_ = final_segment ? 0.0 : r->segment_offset_ + frames * shift;
+  if (final_segment) r->utt_samples_ = 0;
   const uint64_t seq = r->next_seq_++;
   {
     std::lock_guard<std::mutex> lk(L->mu);
@@ -1154,6 +1155,7 @@ void BatchModel::LaneLoop(Lane* L) {
         if (r->queue_.empty()) L->streams_queued--;
         r->handed_++;
         r->taken_++;
+        r->utt_samples_ += (long long)batch.back().second.data.size();
         L->handed++;
         if (!r->busy_) {
           r->busy_ = true;
@@ -1252,8 +1254,11 @@ void BatchModel::LaneLoop(Lane* L) {
         } catch (const std::exception& ex) {
           VAMD_WARN("batch stream reset after a failed step: " << ex.what());
         }
-        r->segment_offset_ = 0.0;
-        r->PublishResult(r->next_seq_++, r->FormatResult(MbrResult(), 0.0));
+        // later segments keep the stream's time base: they start after every
+        // sample handed to the engine so far (the dropped chunk included)
+        const double gap_start = r->segment_offset_;
+        r->segment_offset_ = (double)r->utt_samples_ / md_->mfcc.samp_freq;
+        r->PublishResult(r->next_seq_++, r->FormatResult(MbrResult(), gap_start));
       }
     }
     if (!finals.empty()) {
@@ -1304,7 +1309,16 @@ BatchRecognizer::BatchRecognizer(BatchModel* model, float sr) : model_(model), s
   const int model_rate = (int)std::lround(model_->data().mfcc.samp_freq);
   call_rate_ = rate == model_rate ? 0 : rate;
   model_->Admit(this, model_rate);
-  if (call_rate_) call_table_ = model_->lane_engine(lane_)->ResampleTableFor(call_rate_, &call_tab_);
+  if (call_rate_) {
+    // a failed table lookup (too many distinct rates, an upload error) must
+    // not leave this half-built recognizer admitted on the lane
+    try {
+      call_table_ = model_->lane_engine(lane_)->ResampleTableFor(call_rate_, &call_tab_);
+    } catch (...) {
+      model_->Release(this);
+      throw;
+    }
+  }
   model_->Ref();
 }
 

@@ -314,6 +314,7 @@ class BatchRecognizer {
   int tasks_ = 0;           // results in production on the worker pool
   bool ended_ = false;      // FinishStream pushed: Wait() also covers its results in production
   double segment_offset_ = 0;  // seconds at the start of the current segment
+  long long utt_samples_ = 0;  // model-rate samples handed to the engine since the utterance began
   uint64_t next_seq_ = 0;
   // results
   std::mutex rmu_;

@@ -407,9 +407,10 @@ class Engine:
               "kq_members", "kq_rank", "kq_replay", "kq_final", "n_kq_frames", "n_kq_fast",
               "n_kq_replayed", "n_kq_members", "n_kq_pops", "n_kq_pops_crit", "kq_label", "kq_lanes",
               "n_kq_label_iters", "n_kq_init", "n_kq_big_init", "n_kq_stack_ovf", "n_kq_unsettled",
-              "kq_seg_sort", "kq_seg_lanes")
-    PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19, 22, 23, 24, 25, 26, 27, 34, 35, 41, 42]  # clock slots
-    PHASE_CLOCKS = PHASES[:11] + PHASES[16:20] + PHASES[22:28] + PHASES[34:36] + PHASES[41:43]
+              "kq_seg_sort", "kq_seg_lanes", "kpos", "n_kpos_crowded", "n_kq_components",
+              "n_kq_comp_max_pops", "keps_pre")
+    PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19, 22, 23, 24, 25, 26, 27, 34, 35, 41, 42, 43, 47]  # clock slots
+    PHASE_CLOCKS = tuple(map(PHASES.__getitem__, PHASE_CLOCK_IDX))
 
     def decoder_phases_per_stream(self):
         """[max_streams, len(PHASES)] int64: decoder_phases() per stream slot."""
