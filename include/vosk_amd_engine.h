@@ -82,6 +82,11 @@ float vamd_carpa_logprob(const char *g_carpa, int word, const int *hist, int nhi
  * phone's first transition-id); ntids == 0: word level only (the default). */
 int vamd_lattice_set_phones(const int *tid2phone, const signed char *tid_first, int ntids);
 
+/* host-only: the pruned determinization's memory limit in bytes
+ * (DeterminizeLatticePhonePrunedOptions::max_mem, default 50000000; a smaller
+ * one exercises the narrower-beam retry). */
+int vamd_lattice_set_det_max_mem(long long bytes);
+
 /* host-only: the result pipeline over a state-level lattice (the arrays of
  * vamd_stream_lattice; arc_ilabel / arc_olabel index the graph's arcs):
  * lattice-beam pruning, word determinization, graph scaling, word alignment

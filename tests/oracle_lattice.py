@@ -186,7 +186,7 @@ def determinize(L, ilabel, olabel):
     return _determinize(*_graph_from_raw(L, ilabel, olabel))
 
 
-def determinize_phone(L, ilabel, olabel, tid2phone, tid_first):
+def determinize_phone(L, ilabel, olabel, tid2phone, tid_first, beam=6.0, max_mem=50000000):
     """Kaldi DeterminizeLatticePhonePrunedWrapper (the reference's GetLattice,
     src/recognizer.cc:678): DeterminizeLatticeInsertPhones (phone label
     first_phone_label + phone at a phone's first transition-id -- HMM state 0,
@@ -199,7 +199,7 @@ def determinize_phone(L, ilabel, olabel, tid2phone, tid_first):
     first = max([1] + [l[3] + 1 for l in links])
     out = []
     for (s, d, t, w, g, a) in links:
-        if t <= 0 or t >= len(tid_first) or not tid_first[t]:
+        if s == start or t <= 0 or t >= len(tid_first) or not tid_first[t]:  # (no phone on the start's arcs)
             out.append((s, d, t, w, g, a))
             continue
         ph = first + int(tid2phone[t])
@@ -211,7 +211,10 @@ def determinize_phone(L, ilabel, olabel, tid2phone, tid_first):
             fin.append(None)
             out.append((s, x, t, w, g, a))
             out.append((x, d, 0, ph, F32(0), F32(0)))
-    W, Fi = _determinize(n, out, fin, start)
+    r = determinize_pruned(n, out, fin, start, beam, max_mem)
+    if r is None:
+        return None
+    W, Fi = r
     if not W:
         return W, Fi
     S = len(W)
@@ -247,7 +250,428 @@ def determinize_phone(L, ilabel, olabel, tid2phone, tid_first):
             links2.append((cur, nx, int(t), 0, f[0] if i == 0 else F32(0), f[1] if i == 0 else F32(0)))
             cur = nx
         fin2[cur] = (F32(0), F32(0))
-    return _determinize(n2, links2, fin2, 0)
+    return determinize_pruned(n2, links2, fin2, 0, beam, max_mem)
+
+
+# ------------------------------------------------- pruned determinization
+# Kaldi lat/determinize-lattice-pruned.{h,cc} [K]: LatticeDeterminizerPruned
+# (the determinization of the reference's GetLattice, src/recognizer.cc:678,
+# through DeterminizeLatticePhonePrunedWrapper, and of the batch pipeline's
+# lattice callback, src/batch_recognizer.cc:138-149) and the retry loop of
+# DeterminizeLatticePruned.  Restated as csrc/lattice.cc PrunedDeterminizer:
+# element strings are absolute transition-id tuples, a subset's base the
+# common prefix its residuals hang off; the string repository's size is the
+# number of distinct strings ever created (csrc StrRepo nodes).
+
+def _cmp_k(x, y):  # fst::Compare(LatticeWeight): total cost, then graph cost
+    fx, fy = F32(x[0] + x[1]), F32(y[0] + y[1])
+    if fx < fy:
+        return 1
+    if fx > fy:
+        return -1
+    if x[0] < y[0]:
+        return 1
+    if x[0] > y[0]:
+        return -1
+    return 0
+
+
+def _cmp_det(e, eb, f, fb):
+    """The determinizer's Compare on (weight, residual string): 1 if e is
+    better; weight, then the shorter string, then the lexicographically larger."""
+    c = _cmp_k(e[1], f[1])
+    if c:
+        return c
+    x, y = e[2][len(eb):], f[2][len(fb):]
+    if len(x) != len(y):
+        return 1 if len(x) < len(y) else -1
+    if x == y:
+        return 0
+    return 1 if x > y else -1
+
+
+def _approx_eq(x, y, delta):  # LatticeWeight ApproxEqual
+    if x[0] == y[0] and x[1] == y[1]:
+        return True
+    return abs(F32(F32(x[0] + x[1]) - F32(y[0] + y[1]))) <= F32(delta)
+
+
+def _cost(w):  # ConvertToCost: in double
+    return float(w[0]) + float(w[1])
+
+
+def _topo(N, links):
+    indeg = [0] * N
+    out = [[] for _ in range(N)]
+    for (s, d, *_r) in links:
+        indeg[d] += 1
+        out[s].append(d)
+    order, st = [], [s for s in range(N - 1, -1, -1) if indeg[s] == 0]
+    while st:
+        s = st.pop()
+        order.append(s)
+        for d in reversed(out[s]):
+            indeg[d] -= 1
+            if indeg[d] == 0:
+                st.append(d)
+    assert len(order) == N, "lattice has a cycle"
+    return order
+
+
+def _prune_det_input(N, links, fin, start, topo, beam):
+    """kaldi::PruneLattice on the determinizer's input."""
+    out = [[] for _ in range(N)]
+    for i, l in enumerate(links):
+        out[l[0]].append(i)
+    fw = [INF] * N
+    fw[start] = 0.0
+    best = INF
+    for s in topo:
+        for i in out[s]:
+            d, g, a = links[i][1], links[i][4], links[i][5]
+            fw[d] = min(fw[d], fw[s] + _cost((g, a)))
+        if fin[s] is not None:
+            best = min(best, fw[s] + _cost(fin[s]))
+    cut = best + beam
+    keep = [True] * len(links)
+    fin2 = list(fin)
+    bw = [INF] * N
+    for s in reversed(topo):
+        b = INF if fin[s] is None else _cost(fin[s])
+        if b != INF and b + fw[s] > cut:
+            fin2[s] = None
+        for i in out[s]:
+            d, g, a = links[i][1], links[i][4], links[i][5]
+            ab = _cost((g, a)) + bw[d]
+            if ab < b:
+                b = ab
+            if fw[s] + ab > cut:
+                keep[i] = False
+        bw[s] = b
+    return [l for l, k in zip(links, keep) if k], fin2
+
+
+class _PrunedDet:
+    def __init__(self, N, links, fin, start, topo, beam, max_mem, max_states=100000, delta=1.0 / 1024.0):
+        self.N, self.links, self.fin, self.start = N, links, fin, start
+        self.beam, self.max_mem, self.max_states, self.delta = beam, max_mem, max_states, delta
+        self.outl = [[] for _ in range(N)]
+        for i, l in enumerate(links):
+            self.outl[l[0]].append(i)
+        # per state: label-epsilon links first, then label links (graph order within each)
+        self.outl = [[i for i in v if links[i][3] == 0] + [i for i in v if links[i][3] != 0] for v in self.outl]
+        self.has_label = [any(links[i][3] != 0 for i in v) for v in self.outl]
+        self.bwd = [INF] * N
+        for s in reversed(topo):
+            c = INF if fin[s] is None else _cost(fin[s])
+            for i in self.outl[s]:
+                l = links[i]
+                c = min(c, _cost((l[4], l[5])) + self.bwd[l[1]])
+            self.bwd[s] = c
+        self.cutoff = self.bwd[start] + beam
+        self.states = []     # dict(sub, base, fwd, arcs)
+        self.minimal = {}
+        self.initial = {}
+        self.queue = []
+        self.seq = 0
+        self.num_elems = 0
+        self.num_arcs = 0
+        self.nodes = set()   # distinct non-empty strings created (the repository)
+        self.eff = beam
+        self.guard = False
+
+    def _ext(self, s, t):
+        if t == 0:
+            return s
+        n = s + (t,)
+        self.nodes.add(n)
+        return n
+
+    @staticmethod
+    def _times(w, g, a):
+        return (F32(w[0] + F32(g)), F32(w[1] + F32(a)))
+
+    def closure(self, sub, base):
+        at = {e[0]: i for i, e in enumerate(sub)}
+        work = list(range(len(sub)))
+        while work:
+            i = work.pop()
+            e = sub[i]
+            for li in self.outl[e[0]]:
+                s, d, t, w, g, x = self.links[li]
+                if w != 0:
+                    break
+                n = (d, self._times(e[1], g, x), self._ext(e[2], t))
+                if d not in at:
+                    at[d] = len(sub)
+                    work.append(len(sub))
+                    sub.append(n)
+                elif _cmp_det(n, base, sub[at[d]], base) > 0:
+                    sub[at[d]] = n
+                    work.append(at[d])
+        return sub
+
+    def minimal_form(self, sub):
+        sub = [e for e in sub if self.fin[e[0]] is not None or self.has_label[e[0]]]
+        sub.sort(key=lambda e: e[0])
+        return sub
+
+    def normalize(self, sub, base):
+        tot = sub[0][1]
+        n = len(sub[0][2])
+        for e in sub[1:]:
+            if _cmp_k(tot, e[1]) < 0:
+                tot = e[1]
+        for e in sub:
+            j = 0
+            while j < n and j < len(e[2]) and e[2][j] == sub[0][2][j]:
+                j += 1
+            n = j
+        nbase = sub[0][2][:n]
+        out = [(e[0], (F32(e[1][0] - tot[0]), F32(e[1][1] - tot[1])), e[2]) for e in sub]
+        return out, nbase, tot
+
+    def _key(self, sub, base):
+        return tuple((e[0], e[2][len(base):]) for e in sub)
+
+    def _eq(self, x, bx, y, by):
+        return len(x) == len(y) and all(
+            a[0] == b[0] and _approx_eq(a[1], b[1], self.delta) and a[2][len(bx):] == b[2][len(by):]
+            for a, b in zip(x, y))
+
+    def process_final(self, sid):
+        st = self.states[sid]
+        best = None
+        for e in st["sub"]:
+            if self.fin[e[0]] is None:
+                continue
+            c = (e[0], self._times(e[1], *self.fin[e[0]]), e[2])
+            if best is None or _cmp_det(c, st["base"], best, st["base"]) > 0:
+                best = c
+        if best is not None and _cost(best[1]) + st["fwd"] <= self.cutoff:
+            st["arcs"].append((0, -1, best[1], best[2]))
+            self.num_arcs += 1
+
+    def process_transitions(self, sid):
+        import heapq
+        import functools
+        st = self.states[sid]
+        base = st["base"]
+        allp = []
+        for e in st["sub"]:
+            for li in self.outl[e[0]]:
+                s, d, t, w, g, x = self.links[li]
+                if w == 0:
+                    continue
+                allp.append((w, (d, self._times(e[1], g, x), self._ext(e[2], t))))
+
+        def order(p, q):
+            if p[0] != q[0]:
+                return -1 if p[0] < q[0] else 1
+            if p[1][0] != q[1][0]:
+                return -1 if p[1][0] < q[1][0] else 1
+            return -_cmp_det(p[1], base, q[1], base)
+        allp.sort(key=functools.cmp_to_key(order))
+        i = 0
+        while i < len(allp):
+            label = allp[i][0]
+            prio = INF
+            sub = []
+            while i < len(allp) and allp[i][0] == label:
+                e = allp[i][1]
+                prio = min(prio, _cost(e[1]) + self.bwd[e[0]])
+                if not sub or sub[-1][0] != e[0]:
+                    sub.append(e)
+                i += 1
+            prio += st["fwd"]
+            if prio > self.cutoff:
+                continue
+            self.num_elems += len(sub)
+            heapq.heappush(self.queue, (prio, self.seq, sid, label, sub, base))
+            self.seq += 1
+
+    def minimal_to_state(self, sub, base, fwd):
+        key = self._key(sub, base)
+        for sid in self.minimal.get(key, []):
+            o = self.states[sid]
+            if self._eq(o["sub"], o["base"], sub, base):
+                return sid
+        sid = len(self.states)
+        self.num_elems += len(sub)
+        self.states.append(dict(sub=sub, base=base, fwd=fwd, arcs=[]))
+        self.minimal.setdefault(key, []).append(sid)
+        self.process_final(sid)
+        self.process_transitions(sid)
+        return sid
+
+    def initial_to_state(self, sub, base, fwd):
+        key = self._key(sub, base)
+        for (csub, cbase, sid, rem, rstr, rbase) in self.initial.get(key, []):
+            if self._eq(csub, cbase, sub, base):
+                return sid, rem, rstr[len(rbase):]
+        cur = self.minimal_form(self.closure(list(sub), base))
+        if not cur:
+            return -1, None, None
+        cur, nbase, w2 = self.normalize(cur, base)
+        sid = self.minimal_to_state(cur, nbase, fwd + _cost(w2))
+        self.num_elems += len(sub)
+        self.initial.setdefault(key, []).append((sub, base, sid, w2, nbase, base))
+        return sid, w2, nbase[len(base):]
+
+    def check_memory(self):
+        arcs, elems = self.num_arcs * 32, self.num_elems * 24
+        repo = (len(self.nodes) + 1) * 32
+        if self.max_mem <= 0 or repo + arcs + elems <= self.max_mem:
+            return True
+        live = set()
+
+        def mark(s):
+            for k in range(1, len(s) + 1):
+                live.add(s[:k])
+        for st in self.states:
+            for e in st["sub"]:
+                mark(e[2])
+            mark(st["base"])
+            for a in st["arcs"]:
+                mark(a[3])
+        for v in self.initial.values():
+            for (csub, cbase, sid, rem, rstr, rbase) in v:
+                for e in csub:
+                    mark(e[2])
+                mark(rstr)
+        for t in self.queue:
+            for e in t[4]:
+                mark(e[2])
+        repo = len(live) * 32
+        if repo + arcs + elems > int(self.max_mem * 0.8):
+            if self.queue:
+                self.eff = min(self.queue)[0] - self.bwd[self.start]
+            return False
+        return True
+
+    def run(self):
+        import heapq
+        s0 = self.minimal_form(self.closure([(self.start, (F32(0), F32(0)), ())], ()))
+        self.num_elems += len(s0)
+        self.states.append(dict(sub=s0, base=(), fwd=0.0, arcs=[]))
+        self.minimal.setdefault(self._key(s0, ()), []).append(0)
+        self.process_final(0)
+        self.process_transitions(0)
+        done = True
+        while self.queue:
+            ns = len(self.states)
+            if self.max_states > 0 and ns > self.max_states:
+                self.guard = True
+                return False
+            if ns % 10 == 0 and not self.check_memory():
+                done = False
+                break
+            prio, _, sid, label, sub, sbase = heapq.heappop(self.queue)
+            fwd = self.states[sid]["fwd"]
+            sub, b1, w1 = self.normalize(sub, sbase)
+            fwd += _cost(w1)
+            nxt, w2, rest = self.initial_to_state(sub, b1, fwd)
+            if nxt < 0:
+                continue
+            full = b1 + tuple(rest)
+            for k in range(len(b1) + 1, len(full) + 1):
+                self.nodes.add(full[:k])
+            self.states[sid]["arcs"].append((label, nxt, (F32(w1[0] + w2[0]), F32(w1[1] + w2[1])), full))
+            self.num_arcs += 1
+        return done
+
+    def output(self):
+        """Creation order, trimmed to start -> final paths (fst::Connect), then
+        the topological renumbering of csrc/lattice.cc."""
+        S = len(self.states)
+        acc, coacc = [False] * S, [False] * S
+        acc[0] = True
+        st = [0]
+        while st:
+            s = st.pop()
+            for a in self.states[s]["arcs"]:
+                if a[1] >= 0 and not acc[a[1]]:
+                    acc[a[1]] = True
+                    st.append(a[1])
+        rev = [[] for _ in range(S)]
+        for s in range(S):
+            for a in self.states[s]["arcs"]:
+                if a[1] >= 0:
+                    rev[a[1]].append(s)
+                else:
+                    coacc[s] = True
+        st = [s for s in range(S) if coacc[s]]
+        while st:
+            s = st.pop()
+            for q in rev[s]:
+                if not coacc[q]:
+                    coacc[q] = True
+                    st.append(q)
+        if not (acc[0] and coacc[0]):
+            return [], []
+        keep = [-1] * S
+        K = 0
+        for s in range(S):
+            if acc[s] and coacc[s]:
+                keep[s] = K
+                K += 1
+        orig = [0] * K
+        for s in range(S):
+            if keep[s] >= 0:
+                orig[keep[s]] = s
+        indeg = [0] * K
+        for s in range(S):
+            if keep[s] < 0:
+                continue
+            for a in self.states[s]["arcs"]:
+                if a[1] >= 0 and keep[a[1]] >= 0:
+                    indeg[keep[a[1]]] += 1
+        order, stk = [], [0]
+        while stk:
+            k = stk.pop()
+            order.append(k)
+            for a in reversed(self.states[orig[k]]["arcs"]):
+                if a[1] >= 0 and keep[a[1]] >= 0:
+                    indeg[keep[a[1]]] -= 1
+                    if indeg[keep[a[1]]] == 0:
+                        stk.append(keep[a[1]])
+        assert len(order) == K
+        pos = [0] * K
+        for i, k in enumerate(order):
+            pos[k] = i
+        W, Fi = [[] for _ in range(K)], [None] * K
+        for k in range(K):
+            stt = self.states[orig[k]]
+            p = pos[k]
+            for (label, nxt, w, full) in stt["arcs"]:
+                res = list(full[len(stt["base"]):])
+                if nxt < 0:
+                    Fi[p] = (w[0], w[1], res)
+                elif keep[nxt] >= 0:
+                    W[p].append((label, pos[keep[nxt]], w[0], w[1], res))
+        return W, Fi
+
+
+def determinize_pruned(N, links, fin, start, beam=6.0, max_mem=50000000):
+    """DeterminizeLatticePruned: LatticeDeterminizerPruned at `beam`; when its
+    memory estimate stops it short of 0.7 x beam, the input is pruned at a
+    narrower beam (beam x sqrt(effective / beam), at least beam / 4) and the
+    determinization retried (at most 10 times).  -> (W, Fi) as _determinize."""
+    if N == 0 or start < 0:
+        return [], []
+    topo = _topo(N, links)
+    cur_links, cur_fin = links, fin
+    for it in range(10):
+        d = _PrunedDet(N, cur_links, cur_fin, start, topo, beam, max_mem)
+        d.run()
+        if d.guard:
+            return None
+        if d.eff >= beam * 0.7 or beam == INF or it + 1 == 10:
+            return d.output()
+        nb = beam * math.sqrt(max(d.eff, 0.0) / beam)  # (rounding can put eff just below 0: Kaldi would take NaN)
+        beam = max(nb, 0.25 * beam)
+        cur_links, cur_fin = _prune_det_input(N, cur_links, cur_fin, start, topo, beam)
+    return None
 
 
 def tid_first(tm):

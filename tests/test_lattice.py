@@ -162,3 +162,72 @@ def test_phone_pass_determinization_matches_restatement(synth_model, test_wave, 
     assert [x["words"] for x in got["nbest"]] == [x["words"] for x in word_only["nbest"]]
     np.testing.assert_allclose([x["graph"] + x["acoustic"] for x in got["nbest"]],
                                [x["graph"] + x["acoustic"] for x in word_only["nbest"]], rtol=1e-6, atol=1e-3)
+
+
+def _pruning_lattice():
+    """Hand-made lattice where the exact determinization keeps a word
+    sequence the pruned one drops.  Frame 1: token 1 after X (cost 0) or B
+    (5), token 2 after B (5.5); frame 2 (final): C from token 1 (0), D from
+    token 2 (0), E from token 1 (5.5).  Every link lies on a path within the
+    beam (6): XC 0, BC 5, BD 5.5, XE 5.5; but B followed by E costs 10.5.
+    Exact determinization: the prefixes X ({1}) and B ({1, 2}) are different
+    states and B's keeps E (BE = 10.5); Kaldi's pruned one drops that
+    transition (forward 5 + 5.5 > best + beam)."""
+    L = dict(num_frames=2, frame_begin=np.array([0, 1, 3, 6], np.int32),
+             tok_state=np.array([0, 1, 2, 3, 4, 5], np.int32), tok_cost=np.array([0, 0, 5.5, 0, 5.5, 5.5], np.float32),
+             link_src=np.array([0, 0, 0, 1, 2, 1], np.int32), link_dst=np.array([1, 1, 2, 3, 4, 5], np.int32),
+             link_arc=np.arange(6, dtype=np.int32),
+             link_graph=np.array([0, 5, 5.5, 0, 0, 5.5], np.float32), link_ac=np.zeros(6, np.float32),
+             final_cost=np.zeros(3, np.float32))
+    ilabel = np.array([5, 6, 7, 8, 9, 10], np.int32)
+    olabel = np.array([11, 12, 12, 13, 14, 15], np.int32)
+    return L, ilabel, olabel
+
+
+def test_pruned_determinization_known_answer():
+    from vosk import engine
+    L, il, ol = _pruning_lattice()
+    exact = engine.lattice_words(L, il, ol, 6.0, 1.0, 10)
+    assert sorted(tuple(x["words"]) for x in exact["nbest"]) == [(11, 13), (11, 15), (12, 13), (12, 14), (12, 15)]
+    zeros = np.zeros(11, np.int32)
+    engine.set_phones(zeros, zeros.astype(np.int8))  # no phone starts: both passes on words, pruned
+    try:
+        got = engine.lattice_words(L, il, ol, 6.0, 1.0, 10)
+    finally:
+        engine.set_phones(None)
+    assert got["det_ok"] == 1
+    assert sorted(tuple(x["words"]) for x in got["nbest"]) == [(11, 13), (11, 15), (12, 13), (12, 14)]
+    costs = {tuple(x["words"]): x["graph"] + x["acoustic"] for x in got["nbest"]}
+    assert costs[(11, 13)] == 0.0 and costs[(12, 13)] == 5.0 and costs[(12, 14)] == 5.5 and costs[(11, 15)] == 5.5
+    W, Fi = OL.determinize_phone(OL.prune(L, 6.0), il, ol, zeros, zeros.astype(bool))
+    assert got["det_states"] == len(W) and got["det_arcs"] == sum(len(v) for v in W)
+    assert sorted(tuple(x["words"]) for x in OL.nbest(W, Fi, 10)) == sorted(costs)
+
+
+@pytest.mark.parametrize("secs,max_mem", [(6, 20000), (8.3, 20000), (8.3, 30000)])
+def test_pruned_determinization_memory_retry(synth_model, test_wave, secs, max_mem):
+    """A memory limit the determinization passes: it stops, reports the beam it
+    reached, and DeterminizeLatticePruned retries on the input pruned at a
+    narrower beam -- the C++ and the restatement agree step for step, and the
+    best path survives."""
+    from vosk import engine
+    o, r, L = _lattice(synth_model, test_wave[:int(16000 * secs)])
+    first = OL.tid_first(o.tm)
+    engine.set_phones(o.tm.tid2phone, first)
+    engine.set_det_max_mem(max_mem)
+    try:
+        got = engine.lattice_words(L, o.graph.ilabel, o.graph.olabel, 6.0, 1.0, 6)
+        full = None
+        engine.set_det_max_mem()
+        full = engine.lattice_words(L, o.graph.ilabel, o.graph.olabel, 6.0, 1.0, 6)
+    finally:
+        engine.set_phones(None)
+        engine.set_det_max_mem()
+    W, Fi = OL.determinize_phone(OL.prune(L, 6.0), o.graph.ilabel, o.graph.olabel, o.tm.tid2phone, first,
+                                 max_mem=max_mem)
+    assert got["det_ok"] == 1
+    assert got["det_states"] == len(W) and got["det_arcs"] == sum(len(v) for v in W)
+    assert got["det_states"] < full["det_states"] or got["det_arcs"] < full["det_arcs"]  # the limit bit
+    nb = OL.nbest(W, Fi, 6)
+    assert [x["words"] for x in got["nbest"]] == [x["words"] for x in nb]
+    assert got["nbest"][0]["words"] == full["nbest"][0]["words"] == r["words"]

@@ -667,6 +667,695 @@ bool Determinize(const DetGraph& D, const LatticeOptions& opt, WordLattice* out)
   return true;
 }
 
+
+// ---------------------------------------------------------------------------
+// Kaldi's pruned lattice determinization (lat/determinize-lattice-pruned.{h,cc}
+// [K]: LatticeDeterminizerPruned + DeterminizeLatticePruned), the
+// determinization of the reference's GetLattice (src/recognizer.cc:678) and
+// of its batch lattice callback (src/batch_recognizer.cc:138-149 ->
+// DeterminizeLatticePhonePrunedWrapper).  Unlike the exact subset
+// construction above it
+//  - keeps each input state's backward cost (best cost to a final state) and
+//    each output state's forward cost (set when the state is created);
+//  - turns every (output state, label) transition into a task whose
+//    priority is forward cost + min over the elements of (weight + backward
+//    cost), drops tasks beyond cutoff = best path cost + beam, and runs the
+//    rest best first (priority queue; equal priorities in push order);
+//  - normalizes a transition's subset before its closure (weight and common
+//    prefix onto the arc), again after it, and caches the closure of each
+//    normalized initial subset (Kaldi's initial_hash_);
+//  - stores a final weight only when it is within the cutoff;
+//  - stops when its memory estimate passes max_mem (checked every tenth
+//    state, after a repository rebuild), reporting the effective beam; the
+//    caller then prunes the input at a narrower beam and retries
+//    (DeterminizeLatticePruned, retry_cutoff 0.7, at most 10 tries);
+//  - writes states in creation order and trims what is not on a path from
+//    the start to a final state (fst::Connect in the wrapper).
+// Element order ties: (weight, string) with Kaldi's Compare -- lower total
+// cost, then lower graph cost, then the shorter string, then the
+// lexicographically larger one.
+// ---------------------------------------------------------------------------
+struct PrunedDetOptions {
+  double beam = 6.0;
+  float delta = 1.0f / 1024.0f;   // kDelta
+  long long max_mem = 50000000;   // DeterminizeLatticePhonePrunedOptions default
+  int max_states = 100000;        // this build's guard (Kaldi: -1)
+};
+
+// LatticeWeight ApproxEqual: identical, or total costs within delta
+inline bool ApproxEqualLW(const LW& x, const LW& y, float delta) {
+  if (x.g == y.g && x.a == y.a) return true;
+  return std::fabs((x.g + x.a) - (y.g + y.a)) <= delta;
+}
+// fst::Compare(LatticeWeight): total cost, then graph cost (no third key)
+inline int CompareLWK(const LW& x, const LW& y) {
+  const float fx = x.g + x.a, fy = y.g + y.a;
+  if (fx < fy) return 1;
+  if (fx > fy) return -1;
+  if (x.g < y.g) return 1;
+  if (x.g > y.g) return -1;
+  return 0;
+}
+inline double CostOf(const LW& w) { return (double)w.g + (double)w.a; }
+
+class PrunedDeterminizer {
+ public:
+  PrunedDeterminizer(const DetGraph& D, const std::vector<int>& topo, const PrunedDetOptions& o)
+      : D_(D), topo_(topo), opt_(o) {}
+
+  // Determinize(): false when it stopped early (memory / state guard)
+  bool Run(double* effective_beam);
+  void Output(WordLattice* out);  // creation order, Connect-trimmed, then topologically renumbered
+  bool guard_tripped() const { return guard_; }
+
+ private:
+  struct OArc {
+    int label, next;  // next -1: the final weight
+    LW w;
+    int str, base;    // arc string = residual base -> str
+  };
+  struct OState {
+    std::vector<Elem> sub;  // minimal normalized subset, sorted by token
+    int base;               // residuals relative to this node
+    double fwd;             // forward cost at creation
+    std::vector<OArc> arcs;
+  };
+  struct Task {
+    double prio;
+    long long seq;
+    int state, label;
+    std::vector<Elem> sub;  // unnormalized, unique per token, sorted; strings relative to the state's base
+  };
+  struct TaskLess {
+    bool operator()(const Task* a, const Task* b) const {
+      if (a->prio != b->prio) return a->prio > b->prio;
+      return a->seq > b->seq;
+    }
+  };
+  struct Cached {  // initial_hash_ entry: the normalized initial subset -> state, remaining weight and string
+    std::vector<Elem> sub;
+    int base;
+    int state;
+    LW rem;
+    int rem_str, rem_base;
+  };
+
+  int Compare(const Elem& x, int bx, const Elem& y, int by) const;  // 1: x better (Kaldi Compare)
+  void Closure(std::vector<Elem>* sub, int base);
+  void ConvertToMinimal(std::vector<Elem>* sub) const;
+  LW Normalize(std::vector<Elem>* sub, int* base);  // returns the total weight; *base -> the new base
+  int MinimalToState(std::vector<Elem>&& sub, int base, double fwd);
+  int InitialToState(const std::vector<Elem>& sub, int base, double fwd, LW* rem, int* rem_str, int* rem_base);
+  void ProcessFinal(int s);
+  void ProcessTransitions(int s);
+  void ProcessTransition(Task* t);
+  bool CheckMemory(double* eff);
+  uint64_t SubKey(const std::vector<Elem>& sub, int base) const;
+  bool SubEqual(const std::vector<Elem>& x, int bx, const std::vector<Elem>& y, int by) const;
+  int AppendString(int node, int from_base, int to_node) ;  // node ++ (from_base -> to_node)
+
+  const DetGraph& D_;
+  const std::vector<int>& topo_;
+  PrunedDetOptions opt_;
+  StrRepo R_;
+  std::vector<int> ob_, oe_;
+  std::vector<DetGraph::Link> cl_;
+  std::vector<double> bwd_;
+  double cutoff_ = 0;
+  std::vector<OState> states_;
+  std::unordered_map<uint64_t, std::vector<int>> minimal_;
+  std::unordered_map<uint64_t, std::vector<int>> initial_;
+  std::vector<Cached> cached_;
+  std::priority_queue<Task*, std::vector<Task*>, TaskLess> queue_;
+  long long seq_ = 0, num_elems_ = 0, num_arcs_ = 0;
+  double eff_beam_ = 0;
+  bool guard_ = false;
+  std::vector<int> at_pos_;
+  std::vector<char> pending_;
+  std::vector<std::vector<int>> fbucket_;
+  std::vector<int> memo_in_, memo_out_;
+};
+
+int PrunedDeterminizer::Compare(const Elem& x, int bx, const Elem& y, int by) const {
+  const int c = CompareLWK(x.w, y.w);
+  if (c != 0) return c;
+  const int lx = R_.ResLen(x.str, bx), ly = R_.ResLen(y.str, by);
+  if (lx > ly) return -1;  // the shorter string wins
+  if (lx < ly) return 1;
+  if (lx == 0) return 0;
+  std::vector<int> a, b;
+  R_.Get(x.str, bx, &a);
+  R_.Get(y.str, by, &b);
+  for (int i = 0; i < lx; i++) {
+    if (a[i] < b[i]) return -1;  // then the lexicographically larger one
+    if (a[i] > b[i]) return 1;
+  }
+  return 0;
+}
+
+// EpsilonClosure: the best (weight, string) per input state reachable through
+// label-epsilon links (the fixpoint; states visited in topological buckets)
+void PrunedDeterminizer::Closure(std::vector<Elem>* sub, int base) {
+  const std::vector<int>& tframe = D_.frame;
+  std::vector<int> touched;
+  pending_.assign(sub->size(), 1);
+  int fmin = (int)fbucket_.size(), fmax = -1;
+  auto push = [&](int i) {
+    const int f = tframe[(*sub)[i].tok];
+    fbucket_[f].push_back(i);
+    fmin = f < fmin ? f : fmin;
+    fmax = f > fmax ? f : fmax;
+  };
+  for (int i = 0; i < (int)sub->size(); i++) {
+    at_pos_[(*sub)[i].tok] = i;
+    touched.push_back((*sub)[i].tok);
+    push(i);
+  }
+  auto extend = [&](int str, int k) {
+    if (cl_[k].lin == 0) return str;
+    if (memo_in_[k] == str) return memo_out_[k];
+    const int n = R_.Succ(str, cl_[k].lin);
+    memo_in_[k] = str;
+    memo_out_[k] = n;
+    return n;
+  };
+  for (int f = fmin; f <= fmax; f++) {
+    std::vector<int>& bq = fbucket_[f];
+    for (size_t qi = 0; qi < bq.size(); qi++) {
+      const int i = bq[qi];
+      pending_[i] = 0;
+      const Elem e = (*sub)[i];
+      for (int k = ob_[e.tok]; k < oe_[e.tok]; k++) {
+        const auto& l = cl_[k];
+        const LW w = Times(e.w, LW{l.g, l.a});
+        const int ei = at_pos_[l.dst];
+        if (ei < 0) {
+          at_pos_[l.dst] = (int)sub->size();
+          touched.push_back(l.dst);
+          sub->push_back(Elem{l.dst, w, extend(e.str, k)});
+          pending_.push_back(1);
+          push((int)sub->size() - 1);
+          continue;
+        }
+        const int c = CompareLWK(w, (*sub)[ei].w);
+        if (c < 0) continue;
+        const Elem n{l.dst, w, extend(e.str, k)};
+        if (c > 0 || Compare(n, base, (*sub)[ei], base) > 0) {
+          (*sub)[ei] = n;
+          if (!pending_[ei]) {
+            pending_[ei] = 1;
+            push(ei);
+          }
+        }
+      }
+    }
+    bq.clear();
+  }
+  for (int t : touched) at_pos_[t] = -1;
+}
+
+// ConvertToMinimal: only states with label links or a final weight remain
+void PrunedDeterminizer::ConvertToMinimal(std::vector<Elem>* sub) const {
+  size_t m = 0;
+  for (size_t i = 0; i < sub->size(); i++) {
+    const int t = (*sub)[i].tok;
+    if (oe_[t] < ob_[t + 1] || D_.fin[t].g != kInf) (*sub)[m++] = (*sub)[i];
+  }
+  sub->resize(m);
+  std::sort(sub->begin(), sub->end(), [](const Elem& x, const Elem& y) { return x.tok < y.tok; });
+}
+
+// NormalizeSubset: the best weight (Plus) and the common prefix move out;
+// *base becomes the prefix's node
+LW PrunedDeterminizer::Normalize(std::vector<Elem>* sub, int* base) {
+  LW tot = (*sub)[0].w;
+  int common = (*sub)[0].str;
+  for (size_t i = 1; i < sub->size(); i++) {
+    if (CompareLWK(tot, (*sub)[i].w) < 0) tot = (*sub)[i].w;
+    common = R_.Lca(common, (*sub)[i].str);
+  }
+  for (auto& e : *sub) e.w = Divide(e.w, tot);
+  *base = common;
+  return tot;
+}
+
+uint64_t PrunedDeterminizer::SubKey(const std::vector<Elem>& sub, int base) const {
+  uint64_t k = 0x9e3779b97f4a7c15ull ^ sub.size();
+  for (auto& e : sub) {
+    k = (k ^ (uint64_t)(uint32_t)e.tok) * 0xff51afd7ed558ccdull;
+    k = (k ^ (uint64_t)(uint32_t)R_.ResLen(e.str, base)) * 0xc4ceb9fe1a85ec53ull;
+    k = (k ^ R_.ResHash(e.str, base)) * 0xff51afd7ed558ccdull;
+    k ^= k >> 29;
+  }
+  return k;
+}
+
+// SubsetEqual: same states and strings, weights ApproxEqual within delta
+bool PrunedDeterminizer::SubEqual(const std::vector<Elem>& x, int bx, const std::vector<Elem>& y, int by) const {
+  if (x.size() != y.size()) return false;
+  for (size_t i = 0; i < x.size(); i++)
+    if (x[i].tok != y[i].tok || !ApproxEqualLW(x[i].w, y[i].w, opt_.delta)) return false;
+  for (size_t i = 0; i < x.size(); i++)
+    if (!R_.ResEqual(x[i].str, bx, y[i].str, by)) return false;
+  return true;
+}
+
+int PrunedDeterminizer::AppendString(int node, int from_base, int to_node) {
+  if (from_base == to_node) return node;
+  std::vector<int> labels;
+  R_.Get(to_node, from_base, &labels);
+  for (int l : labels) node = R_.Succ(node, l);
+  return node;
+}
+
+void PrunedDeterminizer::ProcessFinal(int s) {
+  OState& st = states_[s];
+  bool is_final = false;
+  Elem best{0, LW{}, 0};
+  for (const Elem& e : st.sub) {
+    if (D_.fin[e.tok].g == kInf) continue;
+    const Elem c{e.tok, Times(e.w, D_.fin[e.tok]), e.str};
+    if (!is_final || Compare(c, st.base, best, st.base) > 0) {
+      best = c;
+      is_final = true;
+    }
+  }
+  if (is_final && CostOf(best.w) + st.fwd <= cutoff_) {
+    st.arcs.push_back(OArc{0, -1, best.w, best.str, st.base});
+    num_arcs_++;
+  }
+}
+
+void PrunedDeterminizer::ProcessTransitions(int s) {
+  // (label, element) pairs of every label link out of the subset, sorted by
+  // (label, state); one element per (label, state): the better one
+  std::vector<std::pair<int, Elem>> all;
+  {
+    const OState& st = states_[s];
+    for (const Elem& e : st.sub)
+      for (int k = oe_[e.tok]; k < ob_[e.tok + 1]; k++) {
+        const auto& l = cl_[k];
+        int str = e.str;
+        if (l.lin != 0) {
+          if (memo_in_[k] == str) str = memo_out_[k];
+          else {
+            const int n = R_.Succ(str, l.lin);
+            memo_in_[k] = str;
+            memo_out_[k] = n;
+            str = n;
+          }
+        }
+        all.push_back({l.lout, Elem{l.dst, Times(e.w, LW{l.g, l.a}), str}});
+      }
+  }
+  const int base = states_[s].base;
+  std::sort(all.begin(), all.end(), [&](const std::pair<int, Elem>& x, const std::pair<int, Elem>& y) {
+    if (x.first != y.first) return x.first < y.first;
+    if (x.second.tok != y.second.tok) return x.second.tok < y.second.tok;
+    return Compare(x.second, base, y.second, base) > 0;
+  });
+  const double fwd = states_[s].fwd;
+  for (size_t g0 = 0; g0 < all.size();) {
+    const int label = all[g0].first;
+    double prio = std::numeric_limits<double>::infinity();
+    size_t g1 = g0;
+    std::vector<Elem> sub;
+    for (; g1 < all.size() && all[g1].first == label; g1++) {
+      const Elem& e = all[g1].second;
+      prio = std::min(prio, CostOf(e.w) + bwd_[e.tok]);
+      if (sub.empty() || sub.back().tok != e.tok) sub.push_back(e);  // MakeSubsetUnique (sorted best first)
+    }
+    g0 = g1;
+    prio += fwd;
+    if (prio > cutoff_) continue;  // past the pruning cutoff: never done
+    num_elems_ += (long long)sub.size();
+    queue_.push(new Task{prio, seq_++, s, label, std::move(sub)});
+  }
+}
+
+int PrunedDeterminizer::MinimalToState(std::vector<Elem>&& sub, int base, double fwd) {
+  const uint64_t k = SubKey(sub, base);
+  auto& cand = minimal_[k];
+  for (int id : cand)
+    if (SubEqual(states_[id].sub, states_[id].base, sub, base)) return id;
+  const int id = (int)states_.size();
+  num_elems_ += (long long)sub.size();
+  states_.push_back(OState{std::move(sub), base, fwd, {}});
+  cand.push_back(id);
+  ProcessFinal(id);
+  ProcessTransitions(id);
+  return id;
+}
+
+int PrunedDeterminizer::InitialToState(const std::vector<Elem>& sub, int base, double fwd, LW* rem, int* rem_str,
+                                       int* rem_base) {
+  const uint64_t k = SubKey(sub, base);
+  auto& cand = initial_[k];
+  for (int ci : cand) {
+    const Cached& c = cached_[ci];
+    if (SubEqual(c.sub, c.base, sub, base)) {
+      *rem = c.rem;
+      *rem_str = c.rem_str;
+      *rem_base = c.rem_base;
+      return c.state;
+    }
+  }
+  std::vector<Elem> cur(sub);
+  Closure(&cur, base);
+  ConvertToMinimal(&cur);
+  if (cur.empty()) return -1;  // (cannot happen on a trimmed lattice)
+  int nbase = base;
+  const LW w2 = Normalize(&cur, &nbase);
+  const int id = MinimalToState(std::move(cur), nbase, fwd + CostOf(w2));
+  *rem = w2;
+  *rem_str = nbase;
+  *rem_base = base;
+  num_elems_ += (long long)sub.size();
+  initial_[k].push_back((int)cached_.size());
+  cached_.push_back(Cached{sub, base, id, w2, nbase, base});
+  return id;
+}
+
+void PrunedDeterminizer::ProcessTransition(Task* t) {
+  const int s = t->state;
+  double fwd = states_[s].fwd;
+  int b1 = states_[s].base;
+  const LW w1 = Normalize(&t->sub, &b1);  // prefix 1: state base -> b1
+  fwd += CostOf(w1);
+  LW w2;
+  int s2 = 0, b2 = 0;
+  const int next = InitialToState(t->sub, b1, fwd, &w2, &s2, &b2);
+  if (next < 0) return;
+  // the arc string: prefix 1 followed by the remaining prefix (b2 -> s2)
+  const int str = AppendString(b1, b2, s2);
+  states_[s].arcs.push_back(OArc{t->label, next, Times(w1, w2), str, states_[s].base});
+  num_arcs_++;
+}
+
+// memory estimate (Kaldi CheckMemoryUsage: string repository + 32-byte temp
+// arcs + 24-byte elements; the repository counted as 32 bytes per string in
+// use after a rebuild)
+bool PrunedDeterminizer::CheckMemory(double* eff) {
+  const long long arcs = num_arcs_ * 32, elems = num_elems_ * 24;
+  long long repo = (long long)R_.parent.size() * 32;
+  if (opt_.max_mem <= 0 || repo + arcs + elems <= opt_.max_mem) return true;
+  // rebuild: only strings referenced by states, arcs, tasks and the cache
+  std::vector<char> used(R_.parent.size(), 0);
+  auto mark = [&](int n) {
+    while (n > 0 && !used[n]) {
+      used[n] = 1;
+      n = R_.parent[n];
+    }
+  };
+  for (const OState& st : states_) {
+    for (const Elem& e : st.sub) mark(e.str);
+    mark(st.base);
+    for (const OArc& a : st.arcs) mark(a.str);
+  }
+  for (const Cached& c : cached_) {
+    for (const Elem& e : c.sub) mark(e.str);
+    mark(c.rem_str);
+  }
+  std::vector<Task*> tmp;
+  while (!queue_.empty()) {
+    tmp.push_back(queue_.top());
+    queue_.pop();
+  }
+  for (Task* t : tmp) {
+    for (const Elem& e : t->sub) mark(e.str);
+    queue_.push(t);
+  }
+  long long live = 0;
+  for (char u : used) live += u;
+  repo = live * 32;
+  if (repo + arcs + elems > (long long)(opt_.max_mem * 0.8)) {
+    if (!queue_.empty()) *eff = queue_.top()->prio - bwd_[D_.start];
+    return false;
+  }
+  return true;
+}
+
+bool PrunedDeterminizer::Run(double* effective_beam) {
+  const int N = D_.n;
+  eff_beam_ = opt_.beam;
+  // out-links per state (CSR): label-epsilon links first, then label links
+  const int NL = (int)D_.links.size();
+  ob_.assign(N + 1, 0);
+  oe_.assign(N, 0);
+  std::vector<int> ol(NL);
+  for (int i = 0; i < NL; i++) ob_[D_.links[i].src + 1]++;
+  for (int t = 0; t < N; t++) ob_[t + 1] += ob_[t];
+  {
+    std::vector<int> fill(ob_.begin(), ob_.end() - 1);
+    for (int i = 0; i < NL; i++)
+      if (D_.links[i].lout == 0) ol[fill[D_.links[i].src]++] = i;
+    for (int t = 0; t < N; t++) oe_[t] = fill[t];
+    for (int i = 0; i < NL; i++)
+      if (D_.links[i].lout != 0) ol[fill[D_.links[i].src]++] = i;
+  }
+  cl_.resize(NL);
+  for (int k = 0; k < NL; k++) cl_[k] = D_.links[ol[k]];
+  memo_in_.assign(NL, -1);
+  memo_out_.assign(NL, -1);
+  at_pos_.assign(N, -1);
+  int F = 0;
+  for (int f : D_.frame) F = f > F ? f : F;
+  fbucket_.assign(F + 1, {});
+  // ComputeBackwardWeight (reverse topological order) and the cutoff
+  bwd_.assign(N, std::numeric_limits<double>::infinity());
+  for (int i = (int)topo_.size() - 1; i >= 0; i--) {
+    const int s = topo_[i];
+    double c = D_.fin[s].g == kInf ? std::numeric_limits<double>::infinity() : CostOf(D_.fin[s]);
+    for (int k = ob_[s]; k < ob_[s + 1]; k++) c = std::min(c, CostOf(LW{cl_[k].g, cl_[k].a}) + bwd_[cl_[k].dst]);
+    bwd_[s] = c;
+  }
+  cutoff_ = bwd_[D_.start] + opt_.beam;
+  // the start state: closure of the start, minimal, not normalized, forward cost 0
+  {
+    std::vector<Elem> s0{Elem{D_.start, LW{}, 0}};
+    Closure(&s0, 0);
+    ConvertToMinimal(&s0);
+    num_elems_ += (long long)s0.size();
+    states_.push_back(OState{std::move(s0), 0, 0.0, {}});
+    minimal_[SubKey(states_[0].sub, 0)].push_back(0);
+    ProcessFinal(0);
+    ProcessTransitions(0);
+  }
+  bool done = true;
+  while (!queue_.empty()) {
+    const size_t ns = states_.size();
+    if ((opt_.max_states > 0 && (int)ns > opt_.max_states)) {
+      guard_ = true;
+      done = false;
+      break;
+    }
+    if (ns % 10 == 0 && !CheckMemory(&eff_beam_)) {
+      done = false;
+      break;
+    }
+    Task* t = queue_.top();
+    queue_.pop();
+    ProcessTransition(t);
+    delete t;
+  }
+  while (!queue_.empty()) {
+    delete queue_.top();
+    queue_.pop();
+  }
+  *effective_beam = eff_beam_;
+  return done;
+}
+
+void PrunedDeterminizer::Output(WordLattice* out) {
+  WordLattice& W = *out;
+  W = WordLattice();
+  const int S = (int)states_.size();
+  if (S == 0) return;
+  // fst::Connect: states on a path from the start to a final weight
+  std::vector<char> acc(S, 0), coacc(S, 0);
+  {
+    std::vector<int> st{0};
+    acc[0] = 1;
+    while (!st.empty()) {
+      const int s = st.back();
+      st.pop_back();
+      for (const OArc& a : states_[s].arcs)
+        if (a.next >= 0 && !acc[a.next]) {
+          acc[a.next] = 1;
+          st.push_back(a.next);
+        }
+    }
+    std::vector<std::vector<int>> rev(S);
+    for (int s = 0; s < S; s++)
+      for (const OArc& a : states_[s].arcs) {
+        if (a.next >= 0) rev[a.next].push_back(s);
+        else coacc[s] = 1;
+      }
+    for (int s = 0; s < S; s++)
+      if (coacc[s]) st.push_back(s);
+    while (!st.empty()) {
+      const int s = st.back();
+      st.pop_back();
+      for (int p : rev[s])
+        if (!coacc[p]) {
+          coacc[p] = 1;
+          st.push_back(p);
+        }
+    }
+  }
+  if (!acc[0] || !coacc[0]) return;  // nothing within the beam reaches a final state
+  std::vector<int> keep(S, -1);
+  int K = 0;
+  for (int s = 0; s < S; s++)
+    if (acc[s] && coacc[s]) keep[s] = K++;
+  // topological order (the lattice is acyclic), start state first: the
+  // same DFS renumbering as the exact determinizer's output
+  std::vector<int> indeg(K, 0), order;
+  for (int s = 0; s < S; s++) {
+    if (keep[s] < 0) continue;
+    for (const OArc& a : states_[s].arcs)
+      if (a.next >= 0 && keep[a.next] >= 0) indeg[keep[a.next]]++;
+  }
+  std::vector<int> orig(K);
+  for (int s = 0; s < S; s++)
+    if (keep[s] >= 0) orig[keep[s]] = s;
+  std::vector<int> stk{0};
+  while (!stk.empty()) {
+    const int k = stk.back();
+    stk.pop_back();
+    order.push_back(k);
+    const auto& arcs = states_[orig[k]].arcs;
+    for (auto it = arcs.rbegin(); it != arcs.rend(); ++it)
+      if (it->next >= 0 && keep[it->next] >= 0 && --indeg[keep[it->next]] == 0) stk.push_back(keep[it->next]);
+  }
+  if ((int)order.size() != K) VAMD_ERR("lattice determinization produced a cycle");
+  std::vector<int> pos(K);
+  for (int i = 0; i < K; i++) pos[order[i]] = i;
+  W.arcs.resize(K);
+  W.final_graph.assign(K, INFINITY);
+  W.final_acoustic.assign(K, 0.0f);
+  W.final_tids.resize(K);
+  for (int k = 0; k < K; k++) {
+    const OState& st = states_[orig[k]];
+    const int p = pos[k];
+    for (const OArc& a : st.arcs) {
+      if (a.next < 0) {
+        W.final_graph[p] = a.w.g;
+        W.final_acoustic[p] = a.w.a;
+        R_.Get(a.str, a.base, &W.final_tids[p]);
+        continue;
+      }
+      if (keep[a.next] < 0) continue;
+      WordLattice::Arc b;
+      b.word = a.label;
+      b.next = pos[keep[a.next]];
+      b.graph = a.w.g;
+      b.acoustic = a.w.a;
+      R_.Get(a.str, a.base, &b.tids);
+      W.arcs[p].push_back(std::move(b));
+    }
+  }
+}
+
+// topological order of a determinizer input (Kahn; links go forward in time
+// or within a frame without cycles)
+bool TopoOrder(const DetGraph& D, std::vector<int>* order) {
+  std::vector<int> indeg(D.n, 0), ob(D.n + 1, 0), adj(D.links.size());
+  for (const auto& l : D.links) {
+    indeg[l.dst]++;
+    ob[l.src + 1]++;
+  }
+  for (int s = 0; s < D.n; s++) ob[s + 1] += ob[s];
+  {
+    std::vector<int> fill(ob.begin(), ob.end() - 1);
+    for (const auto& l : D.links) adj[fill[l.src]++] = l.dst;
+  }
+  order->clear();
+  std::vector<int> st;
+  for (int s = D.n - 1; s >= 0; s--)
+    if (indeg[s] == 0) st.push_back(s);
+  while (!st.empty()) {
+    const int s = st.back();
+    st.pop_back();
+    order->push_back(s);
+    for (int k = ob[s + 1] - 1; k >= ob[s]; k--)
+      if (--indeg[adj[k]] == 0) st.push_back(adj[k]);
+  }
+  return (int)order->size() == D.n;
+}
+
+// kaldi::PruneLattice on a determinizer input: links (and final weights)
+// whose best path through them is beyond best + beam are dropped, then the
+// states off every start -> final path
+DetGraph PruneDetGraph(const DetGraph& D, const std::vector<int>& topo, double beam) {
+  const int N = D.n;
+  const double inf = std::numeric_limits<double>::infinity();
+  std::vector<double> fw(N, inf), bw(N, inf);
+  std::vector<std::vector<int>> out(N);
+  for (int i = 0; i < (int)D.links.size(); i++) out[D.links[i].src].push_back(i);
+  fw[D.start] = 0.0;
+  double best = inf;
+  for (int s : topo) {
+    for (int i : out[s]) {
+      const auto& l = D.links[i];
+      fw[l.dst] = std::min(fw[l.dst], fw[s] + CostOf(LW{l.g, l.a}));
+    }
+    if (D.fin[s].g != kInf) best = std::min(best, fw[s] + CostOf(D.fin[s]));
+  }
+  const double cut = best + beam;
+  std::vector<char> keep_link(D.links.size(), 1);
+  DetGraph P = D;
+  for (int k = N - 1; k >= 0; k--) {
+    const int s = topo[k];
+    double b = D.fin[s].g == kInf ? inf : CostOf(D.fin[s]);
+    if (b != inf && b + fw[s] > cut) P.fin[s] = LW{kInf, 0.0f};
+    for (int i : out[s]) {
+      const auto& l = D.links[i];
+      const double ab = CostOf(LW{l.g, l.a}) + bw[l.dst];
+      if (ab < b) b = ab;
+      if (fw[s] + ab > cut) keep_link[i] = 0;
+    }
+    bw[s] = b;
+  }
+  P.links.clear();
+  for (size_t i = 0; i < D.links.size(); i++)
+    if (keep_link[i]) P.links.push_back(D.links[i]);
+  return P;  // (unreachable states stay, isolated: the determinizer never visits them)
+}
+
+// DeterminizeLatticePruned: retry at a narrower beam when memory stopped the
+// determinization short of beam * retry_cutoff
+bool DeterminizePrunedRetry(const DetGraph& D, double beam, const LatticeOptions& opt, WordLattice* out) {
+  WordLattice& W = *out;
+  W = WordLattice();
+  if (D.n == 0 || D.start < 0) return true;
+  std::vector<int> topo;
+  if (!TopoOrder(D, &topo)) VAMD_ERR("lattice determinization: input has a cycle");
+  const int kMaxIters = 10;
+  const double retry_cutoff = 0.7;
+  DetGraph tmp;
+  for (int iter = 0; iter < kMaxIters; iter++) {
+    PrunedDetOptions po;
+    po.beam = beam;
+    po.max_states = opt.max_states;
+    po.max_mem = opt.det_max_mem;
+    PrunedDeterminizer det(iter == 0 ? D : tmp, topo, po);
+    double eff = beam;
+    const bool ok = det.Run(&eff);
+    if (det.guard_tripped()) return false;
+    if (eff >= beam * retry_cutoff || std::isinf(beam) || iter + 1 == kMaxIters) {
+      det.Output(out);
+      (void)ok;  // stopped at a narrower beam: still the lattice Kaldi returns (and uses)
+      return true;
+    }
+    double nb = beam * std::sqrt(std::max(eff, 0.0) / beam);  // (rounding can put eff just below 0: Kaldi would take NaN)
+    if (nb < 0.25 * beam) nb = 0.25 * beam;
+    beam = nb;
+    tmp = PruneDetGraph(iter == 0 ? D : tmp, topo, beam);
+  }
+  return false;
+}
+
 }  // namespace
 
 bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOptions& opt, WordLattice* out) {
@@ -686,6 +1375,7 @@ bool DeterminizePhonePruned(const RawLattice& L, const Graph& g, const std::vect
   const size_t nl = D.links.size();
   for (size_t i = 0; i < nl; i++) {
     const int t = D.links[i].lin;
+    if (D.links[i].src == D.start) continue;  // the start state's arcs get no phone (Kaldi skips them)
     if (t <= 0 || t >= (int)tid_first.size() || !tid_first[t]) continue;
     const int ph = first + tid2phone[t];
     if (D.links[i].lout == 0) {
@@ -697,9 +1387,9 @@ bool DeterminizePhonePruned(const RawLattice& L, const Graph& g, const std::vect
       D.links.push_back(DetGraph::Link{x, dst, 0, ph, 0.0f, 0.0f});
     }
   }
-  // first pass: determinization on phones + words
+  // first pass: pruned determinization on phones + words
   WordLattice P;
-  if (!Determinize(D, opt, &P)) return false;
+  if (!DeterminizePrunedRetry(D, opt.lattice_beam, opt, &P)) return false;
   if (P.NumStates() == 0) {
     *out = WordLattice();
     return true;
@@ -748,7 +1438,7 @@ bool DeterminizePhonePruned(const RawLattice& L, const Graph& g, const std::vect
     E.fin[cur] = LW{0.0f, 0.0f};
   }
   // second pass: word level (DeterminizeLatticePruned)
-  return Determinize(E, opt, out);
+  return DeterminizePrunedRetry(E, opt.lattice_beam, opt, out);
 }
 
 void ScaleGraph(WordLattice* lat, float scale) {

@@ -73,8 +73,9 @@ struct WordLattice {
 };
 
 struct LatticeOptions {
-  float lattice_beam = 6.0f;
+  float lattice_beam = 6.0f;  // also the pruned determinization's beam (GetLattice)
   int max_states = 100000;  // determinization guard (falls back to the best path)
+  long long det_max_mem = 50000000;  // DeterminizeLatticePhonePrunedOptions::max_mem [K]
 };
 
 // Lattice-beam pruning of the raw lattice (PruneForwardLinks /
@@ -94,7 +95,10 @@ bool DeterminizeToWords(const RawLattice& lat, const Graph& g, const LatticeOpti
 // transition-id of every phone (tid_first: HMM state 0, not a self-loop),
 // determinization on phones + words, the result expanded back to a
 // one-transition-id-per-link lattice with the phone labels deleted, then
-// word-level determinization of that.  False if a guard tripped.
+// word-level determinization of that.  Both passes are Kaldi's pruned
+// determinization (LatticeDeterminizerPruned at beam lattice_beam: best-first
+// transitions within the beam, max_mem with the narrower-beam retry; see
+// lattice.cc).  False if a guard tripped.
 bool DeterminizePhonePruned(const RawLattice& lat, const Graph& g, const std::vector<int>& tid2phone,
                             const std::vector<char>& tid_first, const LatticeOptions& opt, WordLattice* out);
 

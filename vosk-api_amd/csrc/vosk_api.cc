@@ -413,6 +413,14 @@ int vamd_lattice_set_rescore(const char* g_fst, const char* g_carpa) {
 
 static std::vector<int> g_host_tid2phone;  // vamd_lattice_set_phones (tests)
 static std::vector<char> g_host_tid_first;
+static long long g_host_det_max_mem = LatticeOptions().det_max_mem;  // vamd_lattice_set_det_max_mem
+
+int vamd_lattice_set_det_max_mem(long long bytes) {
+  API_TRY
+  g_host_det_max_mem = bytes;
+  return 0;
+  API_CATCH(-1)
+}
 
 int vamd_lattice_set_phones(const int* tid2phone, const signed char* tid_first, int ntids) {
   API_TRY
@@ -467,6 +475,7 @@ const char* vamd_lattice_words_json(int num_frames, const int* frame_begin, cons
   WordLattice wl;
   LatticeOptions opt;
   opt.lattice_beam = lattice_beam;
+  opt.det_max_mem = g_host_det_max_mem;
   const bool ok = g_host_tid2phone.empty()
                       ? DeterminizeToWords(L, g, opt, &wl)
                       : DeterminizePhonePruned(L, g, g_host_tid2phone, g_host_tid_first, opt, &wl);

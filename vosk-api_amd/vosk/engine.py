@@ -61,6 +61,7 @@ _SIGS = {
     "vamd_engine_stage_times": (C.c_int, [_vp, _vp, _vp, C.c_int]),
     "vamd_lattice_set_rescore": (C.c_int, [C.c_char_p, C.c_char_p]),
     "vamd_lattice_set_phones": (C.c_int, [_vp, _vp, C.c_int]),
+    "vamd_lattice_set_det_max_mem": (C.c_int, [C.c_longlong]),
     "vamd_carpa_logprob": (C.c_float, [C.c_char_p, C.c_int, _vp, C.c_int]),
     "vamd_batch_lanes": (C.c_int, [_vp]),
     "vamd_batch_lane_stats": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, C.c_int]),
@@ -444,6 +445,12 @@ def set_phones(tid2phone=None, tid_first=None):
         r = _c.vamd_lattice_set_phones(p.ctypes.data, f.ctypes.data, len(p))
     if r != 0:
         raise RuntimeError("vamd_lattice_set_phones failed: " + _err())
+
+
+def set_det_max_mem(nbytes=50000000):
+    """Host-only: the pruned determinization's memory limit (max_mem)."""
+    if _c.vamd_lattice_set_det_max_mem(int(nbytes)) != 0:
+        raise RuntimeError("vamd_lattice_set_det_max_mem failed: " + _err())
 
 
 def carpa_logprob(g_carpa, word, hist):
