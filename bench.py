@@ -192,8 +192,11 @@ def main():
     ap.add_argument("--no-single-stream", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--no-lattice", action="store_true")
-    ap.add_argument("--order", choices=("parallel", "kaldi"), default="parallel",
-                    help="engine workloads: token-passing order (parallel = the BatchModel lanes' form)")
+    ap.add_argument("--order", choices=("parallel", "kaldi"), default="kaldi",
+                    help="engine workloads: token-passing order (kaldi = the CPU reference's "
+                         "LatticeFasterDecoder order, the BatchModel lanes' default)")
+    ap.add_argument("--no-order-line", action="store_true",
+                    help="skip the secondary API line in the other token-passing order")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline: seconds per stream")
     ap.add_argument("--lanes", default=None,
                     help="in-library lanes mode (one process, no torchrun): the BatchModel runs one lane "
@@ -236,6 +239,20 @@ def main():
         out = run_engine(args, model, dist, rank, world, base, args.steps or 40)
     else:
         out = run_api(args, model, dist, rank, world, base)
+        if not args.no_order_line:
+            # the same workload with the lanes in the other token-passing order
+            # (VOSK_AMD_DEC_ORDER is read when the BatchModel's engines are built)
+            other = "parallel" if (out or {}).get("decoder_order", "kaldi") == "kaldi" else "kaldi"
+            os.environ["VOSK_AMD_DEC_ORDER"] = other
+            try:
+                alt = run_api(args, model, dist, rank, world, base)
+            finally:
+                os.environ.pop("VOSK_AMD_DEC_ORDER", None)
+            if alt is not None:
+                key = "kaldi_order" if other == "kaldi" else "order_independent"
+                out[key] = {k: alt[k] for k in ("value", "unit", "ms_per_step", "finish_ms", "decoder_order",
+                                                "p50_chunk_latency_ms", "p99_chunk_latency_ms", "roofline",
+                                                "gpu_ms_per_step", "decoder", "results")}
         if not args.no_engine_line:
             eng = run_engine(args, model, dist, rank, world, base, args.engine_steps)
             if eng is not None:
@@ -255,9 +272,10 @@ def main():
                 "value": round(v, 3), "unit": "xRT", "cores": workers, "kind": "port",
                 "nproc": nproc, "cpu_model": cpu_model,
                 "sample": f"{workers} synthetic streams x {args.cpu_seconds:.0f} s through the C oracle "
-                          f"(MFCC + i-vectors + nnet3 + token passing on the same graph, no lattice "
-                          f"results), one stream per worker process, {workers} processes "
-                          f"(affinity/OMP share of {nproc} CPUs), {a:.0f} s audio in {w:.1f} s wall"}
+                          f"(MFCC + i-vectors + nnet3 + token passing on the same graph), one stream per "
+                          f"worker process, {workers} processes (affinity/OMP share of {nproc} CPUs), "
+                          f"{a:.0f} s audio in {w:.1f} s wall.  Not the same work as the GPU line: no "
+                          f"lattices, endpointing, determinization or MBR results on this leg"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -350,6 +368,7 @@ def run_api(args, model, dist, rank, world, base):
     elapsed = _max_over_ranks(dist, t1 - t0)
     audio_s = K * FEED_BYTES / 2 / SR * S * world
     nl = ve.batch_lanes(bm)
+    order = ve.batch_lane_order(bm, 0)
     lane_streams = [sum(1 for r in recs if ve.batch_recognizer_lane(r) == li) for li in range(nl)]
     st = ve.batch_lane_stats(bm, 0)
     rprof = ve.batch_result_profile(bm)
@@ -390,6 +409,9 @@ def run_api(args, model, dist, rank, world, base):
                    "pipeline": "lane thread: front(s) || nnet(s-1) || decoder(s-2) on 3 HIP streams "
                                "while chunks are queued; a round with nothing behind it runs its "
                                "stages in order; MBR results on host worker threads"},
+        "decoder_order": order,
+        "decoder_order_note": ("kaldi: LatticeFasterDecoder's sequential token passing, the CPU reference's "
+                               "1-best (DESIGN.md §4); parallel: the order-independent form"),
         "step": "one feeding round: 8000 bytes to every stream, Wait(), Result() of every stream",
         "timed_region": "rounds W..W+K, then FinishStream + Wait + final results",
         "p50_chunk_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),

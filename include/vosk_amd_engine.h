@@ -210,6 +210,9 @@ int vamd_batch_lanes(struct VoskBatchModel *m);
  * is quiescent (after vosk_batch_model_wait). */
 int vamd_batch_lane_stats(struct VoskBatchModel *m, int lane, int *load3, double *ms4,
                           long long *launches4, long long *dec6, int reset);
+/* the lane's token-passing order: 1 Kaldi's sequential order (the CPU
+ * reference's LatticeFasterDecoder), 0 the order-independent form */
+int vamd_batch_lane_kaldi_order(struct VoskBatchModel *m, int lane);
 /* result production totals: {segments, lattice links copied, ms copying
  * (lane threads), ms building raw lattices, ms prune + determinize + align,
  * ms MBR, ms formatting} */

@@ -533,9 +533,10 @@ class OrcGraph(C.Structure):
 def decoder_order(batch=False):
     """The token-passing semantics the GPU decoder runs (VOSK_AMD_DEC_ORDER,
     as the engine reads it): "kaldi" (LatticeFasterDecoder's sequential
-    order: engines and KaldiRecognizers by default) or "parallel" (the
-    order-independent form: BatchModel lanes by default, batch=True)."""
-    v = os.environ.get("VOSK_AMD_DEC_ORDER", "parallel" if batch else "kaldi").strip().lower()
+    order: the default of engines, KaldiRecognizers and BatchModel lanes) or
+    "parallel" (the order-independent form, opt-in).  `batch` is kept for
+    the call sites: both paths default to Kaldi's order."""
+    v = os.environ.get("VOSK_AMD_DEC_ORDER", "kaldi").strip().lower()
     return "parallel" if v in ("parallel", "0", "order-independent") else "kaldi"
 
 

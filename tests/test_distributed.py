@@ -147,3 +147,86 @@ def test_library_admission_exactly_once_over_two_lanes():
     assert (fast == 0).sum() > 1.5 * (fast == 1).sum()
     # equal loads: fewest streams, then the lower index
     assert engine.admission_replay([0, 0], [5, 5, 5, 5]).tolist() == [0, 1, 0, 1]
+
+
+# ---- the product path over two processes (one BatchModel lane each)
+def _lane_worker(rank, world, port, model, nstreams, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), VOSK_AMD_DEVICE="0",
+                      VOSK_BATCH_MODEL_DIR=model)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = _batch_texts(shard(rank, world, nstreams))
+    gathered = [None] * world
+    dist.all_gather_object(gathered, res)
+    if rank == 0:
+        merged = {}
+        for g in gathered:
+            merged.update(g)
+        out.put(merged)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _batch_texts(ids):
+    """Every result message of each stream, through libvosk.so's batch API
+    (the test_gpu_batch.py loop), for the global stream ids `ids`."""
+    import json
+    import vosk
+    import bench
+    from conftest import perturbed_stream
+    vosk.SetLogLevel(-1)
+    base = bench.load_wave()
+    datas = {i: bench.pcm(perturbed_stream(base, 4000 + i, seconds=4.0 + 0.5 * i)) for i in ids}
+    vosk.GpuInit()
+    bm = vosk.BatchModel()
+    recs = {i: vosk.BatchRecognizer(bm, 16000) for i in ids}
+    got = {i: [] for i in ids}
+
+    def collect():
+        for i in ids:
+            while True:
+                r = recs[i].Result()
+                if not r:
+                    break
+                got[i].append(json.loads(r))
+    n = max(len(d) for d in datas.values())
+    for pos in range(0, n, 8000):
+        for i in ids:
+            if pos < len(datas[i]):
+                recs[i].AcceptWaveform(datas[i][pos:pos + 8000])
+        bm.Wait()
+        collect()
+    for i in ids:
+        recs[i].FinishStream()
+    bm.Wait()
+    collect()
+    del recs
+    del bm
+    return got
+
+
+@pytest.mark.gpu
+def test_two_processes_of_batch_lanes_match_one(synth_model):
+    """bench.py's N > 1 structure on the product path: two processes (gloo
+    world 2), each with its own libvosk.so BatchModel lane (both on device 0
+    here, one GPU per rank on a node) decoding its shard of the streams; the
+    gathered results equal one process decoding every stream."""
+    n = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lane_worker, args=(r, 2, port, synth_model, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    merged = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    os.environ["VOSK_BATCH_MODEL_DIR"] = synth_model
+    try:
+        one = _batch_texts(list(range(n)))
+    finally:
+        os.environ.pop("VOSK_BATCH_MODEL_DIR", None)
+    assert sorted(merged) == list(range(n))
+    for i in range(n):
+        assert merged[i] == one[i], i
+    assert sum(len(v) for v in one.values()) >= n

@@ -108,6 +108,9 @@ struct DecShared {
   // alternating sub-rounds), creator-rank scan, epsilon queue bookkeeping
   float kmin_w[2][DW];
   float kcar[2];
+  // emitting pass running cutoff by decoupled look-back (kaldi_lookback_min):
+  // per (sub-round, wave) index q, {q << 1 | inclusive, ordered min} in a ring
+  unsigned long long kls[4 * DW];
   int ksum_w[2][DW];
   int kn0, kne;
   int kpop_sum, kpop_max;  // component replay: pops over all lanes / on the longest lane
@@ -470,14 +473,15 @@ __device__ __forceinline__ Relax relax(const DecArgs& a, DecShared& sh, const Fr
 // (one CAS per probe); keys by atomic min without waiting for the result
 // (the winners are found after the sub-round's barrier).  Output per item:
 // slot (kNoSlot: no relaxation) and created.
+template <int NU = kUnroll>
 __device__ __forceinline__ void relax_batch(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
                                             const int* dest, const unsigned long long* key, const bool* eps,
                                             const bool* want, int* slot_out, bool* created) {
-  bool pend[kUnroll];
-  unsigned g[kUnroll];
+  bool pend[NU];
+  unsigned g[NU];
   bool any = false;
 #pragma unroll
-  for (int u = 0; u < kUnroll; u++) {
+  for (int u = 0; u < NU; u++) {
     slot_out[u] = kNoSlot;
     created[u] = false;
     pend[u] = false;
@@ -494,13 +498,13 @@ __device__ __forceinline__ void relax_batch(const DecArgs& a, DecShared& sh, con
   }
   const unsigned hm = (1u << a.hbits) - 1u;
   for (int probe = 0; any && probe < a.hprobe; probe++) {
-    int cur[kUnroll];
+    int cur[NU];
 #pragma unroll
-    for (int u = 0; u < kUnroll; u++)
+    for (int u = 0; u < NU; u++)
       if (pend[u]) cur[u] = atomicCAS(&T.state[g[u]], -1, dest[u]);
     any = false;
 #pragma unroll
-    for (int u = 0; u < kUnroll; u++) {
+    for (int u = 0; u < NU; u++) {
       if (!pend[u]) continue;
       if (cur[u] == -1) {
         hbm_created(a, sh, T, g[u], key[u], eps[u]);
@@ -518,7 +522,7 @@ __device__ __forceinline__ void relax_batch(const DecArgs& a, DecShared& sh, con
     }
   }
 #pragma unroll
-  for (int u = 0; u < kUnroll; u++)
+  for (int u = 0; u < NU; u++)
     if (pend[u]) sh.bad |= 1;
 }
 
@@ -886,6 +890,65 @@ __device__ __forceinline__ float kaldi_excl_min(DecShared& sh, float v, int par)
   return fminf(pre, excl);
 }
 
+// The same running minimum without a block barrier (decoupled look-back,
+// Merrill & Garland's single-pass scan): wave w of sub-round s is item block
+// q = s * DW + w; it publishes its block minimum, then walks back over the
+// published blocks (spinning on one not yet published) until one carries
+// its inclusive prefix (or q = 0, whose carry-in is `seed`), and publishes
+// its own inclusive prefix.  A wave never waits for another wave's
+// relaxations, only for its block minimum.  Returns the exclusive running
+// minimum before this lane's item; *incl_out (wave-uniform) the inclusive
+// prefix through this block.  The ring holds four sub-rounds: a wave can be
+// at most one sub-round ahead of the slowest (it needs that wave's block
+// minimum to finish its own look-back).
+constexpr unsigned kLbIncl = 1u;
+__device__ __forceinline__ float kaldi_lookback_min(DecShared& sh, float v, int q, float seed, float* incl_out) {
+  const int lane = threadIdx.x & 63;
+  float incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const float u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl = fminf(incl, u);
+  }
+  float excl = __shfl_up(incl, 1, 64);
+  if (lane == 0) excl = __int_as_float(0x7f800000);
+  const float agg = __shfl(incl, 63, 64);
+  constexpr int R = 4 * DW;
+  auto pack = [](int qq, unsigned fl, float x) {
+    return ((unsigned long long)(((unsigned)qq << 1) | fl) << 32) | (unsigned long long)ford(x);
+  };
+  if (lane == 0)
+    __hip_atomic_store(&sh.kls[q % R], pack(q, 0u, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  float carry = __int_as_float(0x7f800000);
+  if (q == 0) {
+    carry = seed;
+  } else {
+    int k = q - 1;
+    while (true) {
+      unsigned long long st = 0;
+      if (lane == 0) {
+        while (true) {
+          st = __hip_atomic_load(&sh.kls[k % R], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if ((int)((unsigned)(st >> 32) >> 1) == k) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      st = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(st >> 32)) << 32) |
+           (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)st);
+      carry = fminf(carry, funord((uint32_t)st));
+      if (((unsigned)(st >> 32) & kLbIncl) || k == 0) {
+        if (!((unsigned)(st >> 32) & kLbIncl)) carry = fminf(carry, seed);  // block 0's aggregate: add the seed
+        break;
+      }
+      k--;
+    }
+  }
+  const float inc = fminf(carry, agg);
+  if (lane == 0)
+    __hip_atomic_store(&sh.kls[q % R], pack(q, kLbIncl, inc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  *incl_out = inc;
+  return fminf(carry, excl);
+}
+
 // exclusive prefix sum over the block in thread order; *total = the block's sum
 __device__ __forceinline__ int kaldi_excl_sum(DecShared& sh, int v, int par, int* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -977,7 +1040,9 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
   const bool lat = a.links != nullptr;
   int* KO = a.kord + (long long)slot * a.kord_cap;
   if (threadIdx.x == 0) sh.kcar[0] = seed;  // read after the next barrier
-  int par = 0, ibase = 0, nc = 0;
+  for (int i = threadIdx.x; i < 4 * DW; i += DT) sh.kls[i] = ~0ull;  // no block published (cleared before the first chunk's barrier)
+  int par = 0, ibase = 0, nc = 0, qsub = 0;
+  float incl_last = seed;
   float cn = 0.0f;
   int sn = 0, pn = 0;
   if ((int)threadIdx.x < ntok) {
@@ -1012,30 +1077,53 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
     pr.count(14, 1);
     const int total = sh.total;
     *examined += total;
+    // software pipeline: a sub-round's item (owner search, arc load) is
+    // fetched before the previous sub-round's scan barrier, so the arc
+    // latency overlaps the barrier and the relaxations
+    int jn = 0, arcn = 0;
+    int4 An = make_int4(0, 0, 0, 0);
+    if ((int)threadIdx.x < total) {
+      jn = owner(sh, threadIdx.x);
+      arcn = sh.abeg[jn] + ((int)threadIdx.x - sh.scan[jn]);
+      An = a.arcs[arcn];
+    }
     for (int sb = 0; sb < total; sb += DT) {
       const int it = sb + (int)threadIdx.x;
       const bool valid = it < total;
-      int j = 0, arc = 0;
-      int4 A = make_int4(0, 0, 0, 0);
+      const int j = jn, arc = arcn;
+      const int4 A = An;
       float ac = 0.0f, tot = __int_as_float(0x7f800000);
       if (valid) {
-        j = owner(sh, it);
-        arc = sh.abeg[j] + (it - sh.scan[j]);
-        A = a.arcs[arc];
         ac = cost_offset - Lp[A.z];
         tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
       }
+      if (it + DT < total) {
+        jn = owner(sh, it + DT);
+        arcn = sh.abeg[jn] + (it + DT - sh.scan[jn]);
+        An = a.arcs[arcn];
+      }
       pr.mark(3);
-      const float run = kaldi_excl_min(sh, valid ? tot + adaptive : __int_as_float(0x7f800000), par);
+      // defer: the running cutoff by look-back (no barrier per sub-round)
+      const float run = defer ? kaldi_lookback_min(sh, valid ? tot + adaptive : __int_as_float(0x7f800000),
+                                                   qsub * DW + (int)(threadIdx.x >> 6), seed, &incl_last)
+                              : kaldi_excl_min(sh, valid ? tot + adaptive : __int_as_float(0x7f800000), par);
+      qsub++;
       const bool want = valid && tot < run;
       const int item = ibase + it;
       const unsigned long long kv = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
       int sv = kNoSlot;
       if (want) {
+        // key minima without waiting for the old values (no-return atomics;
+        // only the slot matters here)
         const bool de = ((unsigned)A.w & kDestEps) != 0;
-        const Relax r = relax(a, sh, t, T, A.x, tot, arc, de);
-        if (r.flags >= 0) {
-          sv = r.slot;
+        const int dsts[1] = {A.x};
+        const unsigned long long keys[1] = {((unsigned long long)ford(tot) << 32) | (unsigned)arc};
+        const bool des[1] = {de}, wants[1] = {true};
+        int svs[1];
+        bool crs[1];
+        relax_batch<1>(a, sh, t, T, dsts, keys, des, wants, svs, crs);
+        if (svs[0] != kNoSlot) {
+          sv = svs[0];
           if (sv >= 0) atomicMin(&t.hst[sv], item);
           else __hip_atomic_fetch_min(&T.stamp[~sv], item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1074,6 +1162,10 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
     __syncthreads();
     pr.mark(2);
   }
+  // the running cutoff after every item: the last block's inclusive prefix
+  // (defer; the last wave of the last sub-round), else the barrier scan's carry
+  if (defer && qsub > 0 && (threadIdx.x >> 6) == DW - 1 && (threadIdx.x & 63) == 0) sh.kcar[par] = incl_last;
+  __syncthreads();
   const float next_cutoff = sh.kcar[par];
   if (defer) {
     vm_drain();

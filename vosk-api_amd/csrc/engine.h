@@ -286,6 +286,7 @@ class Engine {
   bool Step(const std::vector<int>& slots, bool allow_pipeline = true);
   void SetStepSamples(int n) { cfg_.max_step_samples = n; }
   const StageTimes& stage_times() const { return times_; }
+  bool kaldi_order() const { return dec_.kaldi != 0; }  // the decoder's token-passing order
   void ResetStageTimes() { times_ = StageTimes(); }
   void InputFinished(int slot);
   // Runs batched steps until the given streams have no runnable work

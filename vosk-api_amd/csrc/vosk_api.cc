@@ -852,6 +852,14 @@ int vamd_batch_lane_stats(VoskBatchModel* m, int lane, int* load3, double* ms4, 
   API_CATCH(-1)
 }
 
+int vamd_batch_lane_kaldi_order(VoskBatchModel* m, int lane) {
+  API_TRY
+  BatchModel* bm = (BatchModel*)m;
+  if (lane < 0 || lane >= bm->num_lanes()) VAMD_ERR("bad lane " << lane);
+  return bm->lane_engine(lane)->kaldi_order() ? 1 : 0;
+  API_CATCH(-1)
+}
+
 int vamd_batch_result_profile(VoskBatchModel* m, double* out13) {
   API_TRY
   ((BatchModel*)m)->ResultProfile(out13);

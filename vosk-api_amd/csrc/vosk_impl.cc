@@ -767,11 +767,12 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
   cfg.max_step_samples = cfg.frames_per_chunk * md_->mfcc.WindowShift() + 512;
   cfg.arena_tokens = EnvInt("VOSK_AMD_ARENA_TOKENS", 1 << 22);
   cfg.lattice = true;  // PushLattice: MBR over each segment's lattice (batch_recognizer.cc:43-107)
-  // the reference's batch path decodes with Kaldi's CudaDecoder (parallel
-  // relaxation of all (token, arc) pairs against an atomically lowered
-  // cutoff, batch_model.cc:78-92), not LatticeFasterDecoder: the lanes run
-  // its deterministic form, the order-independent token passing
-  cfg.kaldi_order = false;
+  // Kaldi's sequential token-passing order (LatticeFasterDecoder, the CPU
+  // reference's 1-best, as north_star asks).  The reference's
+  // own batch path decodes with Kaldi's CudaDecoder, whose token set depends
+  // on thread timing; its deterministic limit, the order-independent form,
+  // stays available (VOSK_AMD_DEC_ORDER=parallel).
+  cfg.kaldi_order = true;
   cfg.pipeline = EnvInt("VOSK_AMD_BATCH_PIPELINE", 1) != 0;
   cfg.track_decoded = true;
   cfg.time_kernels = EnvInt("VOSK_AMD_BATCH_TIMING", 0) != 0;

@@ -64,6 +64,7 @@ _SIGS = {
     "vamd_lattice_set_det_max_mem": (C.c_int, [C.c_longlong]),
     "vamd_carpa_logprob": (C.c_float, [C.c_char_p, C.c_int, _vp, C.c_int]),
     "vamd_batch_lanes": (C.c_int, [_vp]),
+    "vamd_batch_lane_kaldi_order": (C.c_int, [_vp, C.c_int]),
     "vamd_batch_lane_stats": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, C.c_int]),
     "vamd_batch_recognizer_lane": (C.c_int, [_vp]),
     "vamd_batch_result_profile": (C.c_int, [_vp, _vp]),
@@ -119,6 +120,11 @@ def batch_batching_counters(model):
 def batch_lanes(model):
     """Number of GPU lanes of a vosk.BatchModel."""
     return _chk(_c.vamd_batch_lanes(model._handle))
+
+
+def batch_lane_order(model, lane=0):
+    """"kaldi" or "parallel": the token-passing order of a batch lane."""
+    return "kaldi" if _chk(_c.vamd_batch_lane_kaldi_order(model._handle, lane)) else "parallel"
 
 
 def batch_lane_stats(model, lane, reset=False):
