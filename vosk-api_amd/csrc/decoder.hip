@@ -1303,6 +1303,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
   int* BM = a.kb_memb + (long long)slot * a.kb_cap * kKbMemb;
   const float kInf = __int_as_float(0x7f800000);
+  const long long t_nonemit0 = pr.on ? (long long)__builtin_amdgcn_s_memtime() : 0;
   // the emitting pass's tokens: buckets, queue costs, stamps cleared for the
   // closure's rounds, and the closure's first frontier (tokens with epsilon arcs)
   if (threadIdx.x == 0) {
@@ -1418,6 +1419,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   vm_drain();
   __syncthreads();
   const int nm = sh.kne < cap_m ? sh.kne : cap_m;
+  long long t_lanes = 0;  // (profile) replay clocks of this frame
   const int n0 = sh.kn0 < nm ? sh.kn0 : nm;
   // adjacency offsets (a scan over the members), then each member's
   // productive arcs in graph order: (destination member or -1, weight)
@@ -1635,6 +1637,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
         __syncthreads();
         bitonic_sort32(key, ns);
         pr.mark(41);
+        const long long t_l0 = pr.on ? (long long)__builtin_amdgcn_s_memtime() : 0;
         // one wave per component: the waves claim kWin sorted positions at a
         // time and replay every component that starts there (a small window:
         // the components spread over all waves).  A popped
@@ -1732,6 +1735,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
         vm_drain();
         __syncthreads();
         pr.mark(42);
+        if (pr.on) t_lanes += (long long)__builtin_amdgcn_s_memtime() - t_l0;
         if (sh.flag == 0) {
           // creations per initial token in processing order, then the global
           // creation order = (earlier segments) + (rank offset) + creation
@@ -1991,6 +1995,11 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   vm_drain();
   __syncthreads();
   pr.mark(27);
+  if (pr.on && nm > kKM) {  // frames whose queue members overflow the LDS records
+    pr.count(48, (long long)__builtin_amdgcn_s_memtime() - t_nonemit0);
+    pr.count(49, 1);
+    pr.count(50, t_lanes);
+  }
   return ne + n_eps;
 }
 
