@@ -1995,6 +1995,11 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   vm_drain();
   __syncthreads();
   pr.mark(27);
+  if (pr.on) {
+    pr.count(51, nm > 1536 ? 1 : 0);
+    pr.count(52, nm > 2048 ? 1 : 0);
+    pr.count(53, adj_n > kKE ? 1 : 0);
+  }
   if (pr.on && nm > kKM) {  // frames whose queue members overflow the LDS records
     pr.count(48, (long long)__builtin_amdgcn_s_memtime() - t_nonemit0);
     pr.count(49, 1);
