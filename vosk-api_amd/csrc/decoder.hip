@@ -115,6 +115,7 @@ struct DecShared {
   int kn0, kne;
   int kpop_sum, kpop_max;  // component replay: pops over all lanes / on the longest lane
   int kcomp_n, kcomp_max;  // component replay: components / pops of the largest (profile)
+  int karc_sum, karc_max, khbm_pops;  // wave replay: arcs iterated (all waves / the busiest), pops of HBM members
 };
 
 // optional phase clocks (VOSK_AMD_DEC_PROFILE): thread 0 stamps s_memtime
@@ -1582,6 +1583,9 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
       sh.kpop_max = 0;
       sh.kcomp_n = 0;
       sh.kcomp_max = 0;
+      sh.karc_sum = 0;
+      sh.karc_max = 0;
+      sh.khbm_pops = 0;
     }
     vm_drain();
     __syncthreads();
@@ -1638,6 +1642,65 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
         bitonic_sort32(key, ns);
         pr.mark(41);
         const long long t_l0 = pr.on ? (long long)__builtin_amdgcn_s_memtime() : 0;
+        // Components with a single initial token in this segment (most of
+        // them) replay one per lane, all at once: the same pops and arc
+        // order as the wave form below, the lane's LIFO in a four-deep shift
+        // register (a deeper queue sends the frame to the sequential replay).
+        // Components are disjoint, so the lanes never touch the same member.
+        {
+          const int pos = threadIdx.x;
+          bool single = false;
+          if (pos < ns) {
+            const unsigned kc = key[pos] >> 10;
+            single = (pos == 0 || (key[pos - 1] >> 10) != kc) && (pos == ns - 1 || (key[pos + 1] >> 10) != kc);
+          }
+          if (single) {
+            const int prank = (int)(key[pos] & 1023u);
+            int s0 = stk_at(n0 - 1 - (base + prank)), s1 = 0, s2 = 0, s3 = 0;
+            int sp = 1, j = 0, np = 0;
+            bool lovf = false;
+            while (sp > 0) {
+              const int u = s0;  // pop
+              s0 = s1;
+              s1 = s2;
+              s2 = s3;
+              sp--;
+              np++;
+              const float cu = __int_as_float(km_get(K, KM, u, kMCost));
+              if (!(cu < cutoff)) continue;
+              const int off = km_get(K, KM, u, kMOff), cnt = km_get(K, KM, u, kMCnt);
+              for (int k = 0; k < cnt; k++) {
+                const int2 rec = adj_at(off + k);
+                const int d = rec.x;
+                if (d < 0) continue;
+                const float tot = cu + __int_as_float(rec.y);
+                if (!(tot < cutoff)) continue;
+                const float old = __int_as_float(km_get(K, KM, d, kMCost));
+                if (!(tot < old)) continue;
+                if (old == kInfL) {  // FindOrAddToken creates it
+                  km_set(K, KM, d, kMOrd, j++);
+                  rset(d, prank);
+                }
+                km_set(K, KM, d, kMCost, __float_as_int(tot));
+                if (km_get(K, KM, d, kMCnt) > 0) {  // changed: re-queued
+                  if (sp == 4) {
+                    lovf = true;
+                    break;
+                  }
+                  s3 = s2;  // push
+                  s2 = s1;
+                  s1 = s0;
+                  s0 = d;
+                  sp++;
+                }
+              }
+              if (lovf) break;
+            }
+            K.v0lo[prank] = j;
+            if (lovf) sh.flag = 1;
+            atomicAdd(&sh.kpop_sum, np);
+          }
+        }
         // one wave per component: the waves claim kWin sorted positions at a
         // time and replay every component that starts there (a small window:
         // the components spread over all waves).  A popped
@@ -1649,7 +1712,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
         const int lane = threadIdx.x & 63;
         if (threadIdx.x == 0) sh.kk = 0;
         __syncthreads();
-        int npop = 0;
+        int npop = 0, narc = 0, nhbm = 0;
         bool ovf = false;
         while (!ovf) {
           constexpr int kWin = 4;
@@ -1658,7 +1721,9 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
           c0 = __builtin_amdgcn_readfirstlane(c0);
           if (c0 >= ns) break;
           const int pos = c0 + lane;
-          const bool head = lane < kWin && pos < ns && (pos == 0 || (key[pos - 1] >> 10) != (key[pos] >> 10));
+          // (heads of single-token components were replayed by their lanes)
+          const bool head = lane < kWin && pos < ns && (pos == 0 || (key[pos - 1] >> 10) != (key[pos] >> 10)) &&
+                            !(pos == ns - 1 || (key[pos + 1] >> 10) != (key[pos] >> 10));
           unsigned long long hm = __ballot(head);
           while (hm && !ovf) {
             const int h = c0 + __ffsll((long long)hm) - 1;
@@ -1682,6 +1747,8 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
                 if (!(cu < cutoff)) continue;
                 const int off = __builtin_amdgcn_readfirstlane(km_get(K, KM, u, kMOff));
                 const int cnt = __builtin_amdgcn_readfirstlane(km_get(K, KM, u, kMCnt));
+                narc += cnt;
+                if (u >= kKM) nhbm++;
                 for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
                   const int kn = cnt - k0 < 64 ? cnt - k0 : 64;
                   const int2 rec = lane < kn ? adj_at(off + k0 + lane) : make_int2(-1, 0);
@@ -1724,6 +1791,12 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
               atomicMax(&sh.kcomp_max, npop - npop0);
             }
           }
+        }
+        if (lane == 0 && pr.on) {}
+        if (lane == 0 && npop > 0) {
+          atomicAdd(&sh.karc_sum, narc);
+          atomicMax(&sh.karc_max, narc);
+          atomicAdd(&sh.khbm_pops, nhbm);
         }
         if (lane == 0) {
           if (ovf) sh.flag = 1;
@@ -1977,6 +2050,9 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     pr.count(33, sh.kpop_max);
     pr.count(45, sh.kcomp_n);
     pr.count(46, sh.kcomp_max);
+    pr.count(54, sh.karc_sum);
+    pr.count(55, sh.karc_max);
+    pr.count(56, sh.khbm_pops);
   }
   // the created tokens' creation indices [ne, ne + n_eps) in the queue's order, and their buckets
   for (int i = threadIdx.x; i < nm; i += DT) {
