@@ -732,7 +732,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     else if (v == "kaldi" || v == "1") dec_.kaldi = 1;
   }
   dec_.kb_cap = (int)(2 * MT + 1024);
-  dec_.kord_cap = (int)(MT + 4096);
+  dec_.kord_cap = (int)((MT + 4096 + 3) & ~3LL);  // (a multiple of 4: 16-byte loads of four entries)
   if (dec_.kaldi) {
     const size_t KB = (size_t)S * dec_.kb_cap, KO = (size_t)S * dec_.kord_cap;
     dec_.kb_first = (int*)DevAlloc(sizeof(int) * KB);
