@@ -116,6 +116,8 @@ struct DecShared {
   int kpop_sum, kpop_max;  // component replay: pops over all lanes / on the longest lane
   int kcomp_n, kcomp_max;  // component replay: components / pops of the largest (profile)
   int karc_sum, karc_max, khbm_pops;  // wave replay: arcs iterated (all waves / the busiest), pops of HBM members
+  int kheads;                         // wave replay: multi-token component heads listed in hist[]
+  int kcomp_clk;                      // (profile) clocks of the longest component replay
 };
 
 // optional phase clocks (VOSK_AMD_DEC_PROFILE): thread 0 stamps s_memtime
@@ -1204,10 +1206,10 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
 constexpr int kKM = 1024;  // queue tokens held in LDS
 constexpr int kKE = 2048;  // their epsilon arcs held in LDS
 struct KaldiLds {
-  int* ms;     // [kKM] token: slot code
-  float* mc;   // [kKM] its cost during the queue
-  int* mo;     // [kKM] its productive epsilon arcs: offset
-  int* mn;     // [kKM]                              count
+  // [kKM] per member one 16-byte record {slot code, cost during the queue (float
+  // bits), productive epsilon arcs: offset, count} -- the layout of the first
+  // four fields of an HBM member record, so a pop reads a member in one load
+  int4* rec;
   int* mcr;    // [kKM] creation index of a token of the emitting pass, -1 for one the queue creates
   int* mord;   // [kKM] order in which the queue creates it (-1: not yet)
   int* v0hi;   // [kKM] initial queue keys: bucket's first creation index
@@ -1220,16 +1222,20 @@ struct KaldiLds {
 enum { kMSlot = 0, kMCost = 1, kMOff = 2, kMCnt = 3, kMC = 4, kMOrd = 5, kMComp = 6, kMRoot = 7 };
 __device__ __forceinline__ int* km_lds(const KaldiLds& K, int i, int f) {
   switch (f) {
-    case kMSlot: return &K.ms[i];
-    case kMCost: return reinterpret_cast<int*>(&K.mc[i]);
-    case kMOff: return &K.mo[i];
-    case kMCnt: return &K.mn[i];
+    case kMSlot: return &K.rec[i].x;
+    case kMCost: return &K.rec[i].y;
+    case kMOff: return &K.rec[i].z;
+    case kMCnt: return &K.rec[i].w;
     case kMC: return &K.mcr[i];
     default: return &K.mord[i];
   }
 }
 __device__ __forceinline__ int km_get(const KaldiLds& K, int* KM, int i, int f) {
   return i < kKM ? *km_lds(K, i, f) : AG_LD(&KM[(long long)(i - kKM) * kKMRec + f]);
+}
+// a member's {slot, cost, offset, count} in one 16-byte load (LDS or HBM record)
+__device__ __forceinline__ int4 km_rec4(const KaldiLds& K, int* KM, int i) {
+  return i < kKM ? K.rec[i] : wg_ld4(reinterpret_cast<const int4*>(&KM[(long long)(i - kKM) * kKMRec]));
 }
 __device__ __forceinline__ void km_set(const KaldiLds& K, int* KM, int i, int f, int v) {
   if (i < kKM) *km_lds(K, i, f) = v;
@@ -1583,6 +1589,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
       sh.kpop_max = 0;
       sh.kcomp_n = 0;
       sh.kcomp_max = 0;
+      sh.kcomp_clk = 0;
       sh.karc_sum = 0;
       sh.karc_max = 0;
       sh.khbm_pops = 0;
@@ -1626,6 +1633,84 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
       // the LIFO first), in the frontier scratch (free after the closure)
       int* CQ = p.fg1;
       auto stk_at = [&](int r) -> int { return r < kKM ? K.stk[r] : AG_LD(&KS[r - kKM]); };
+      // Hot-first renumbering when the members overflow the LDS records:
+      // members of components with two or more initial tokens -- the ones
+      // the waves replay pop by pop -- move to the low (LDS) indices;
+      // single-token components replay one per lane, their HBM records'
+      // latency overlapped across lanes.  Records, adjacency destinations,
+      // the initial queue and the slots' member stamps are rewritten; the
+      // component labels stay (they are only ids from here on).
+      if (nm > kKM && nm <= a.max_tok && 2LL * nm - kKM <= (long long)a.kord_cap) {
+        int* CC = p.fg0;       // [nm] initial tokens per component label (fg0..fg1: 2 * max_tok ints)
+        int* NI = p.fg0 + nm;  // [nm] new index of each member
+        int* TM = KM + (long long)(nm - kKM) * kKMRec;  // [nm] record copies, past the records in use
+        auto cset = [&](int i, int v) {
+          if (i < kKM) comp[i] = v;
+          else AG_ST(rec_at(i, kMComp), v);
+        };
+        for (int i = threadIdx.x; i < nm; i += DT) AG_ST(&CC[i], 0);
+        vm_drain();
+        __syncthreads();
+        for (int q = threadIdx.x; q < n0; q += DT)
+          __hip_atomic_fetch_add(&CC[cget(stk_at(q))], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vm_drain();
+        __syncthreads();
+        int hot_n = 0;
+        for (int pass = 0; pass < 2; pass++) {  // hot members, then the rest, each in member order
+          int run = pass == 0 ? 0 : hot_n, par = 0;
+          for (int i0 = 0; i0 < nm; i0 += DT) {
+            const int i = i0 + threadIdx.x;
+            const bool hot = i < nm && AG_LD(&CC[cget(i)]) >= 2;
+            const bool take = i < nm && (pass == 0 ? hot : !hot);
+            int tot;
+            const int ex = run + kaldi_excl_sum(sh, take ? 1 : 0, par, &tot);
+            if (take) AG_ST(&NI[i], ex);
+            run += tot;
+            par ^= 1;
+          }
+          if (pass == 0) hot_n = run;
+        }
+        vm_drain();
+        __syncthreads();
+        if (hot_n > 0) {
+          for (int i = threadIdx.x; i < nm; i += DT) {
+            for (int f = kMSlot; f <= kMOrd; f++) AG_ST(&TM[(long long)i * kKMRec + f], km_get(K, KM, i, f));
+            AG_ST(&TM[(long long)i * kKMRec + kMComp], cget(i));
+          }
+          vm_drain();
+          __syncthreads();
+          for (int i = threadIdx.x; i < nm; i += DT) {
+            const int j = AG_LD(&NI[i]);
+            for (int f = kMSlot; f <= kMOrd; f++) km_set(K, KM, j, f, AG_LD(&TM[(long long)i * kKMRec + f]));
+            cset(j, AG_LD(&TM[(long long)i * kKMRec + kMComp]));
+          }
+          for (int e = threadIdx.x; e < adj_n; e += DT) {
+            int2 rec = adj_at(e);
+            if (rec.x < 0) continue;
+            rec.x = AG_LD(&NI[rec.x]);
+            if (e < kKE) K.adj[e] = rec;
+            else
+              AG_ST(&reinterpret_cast<long long*>(KA)[e - kKE],
+                    (long long)(((unsigned long long)(unsigned)rec.y << 32) | (unsigned)rec.x));
+          }
+          for (int r = threadIdx.x; r < n0; r += DT) {
+            const int j = AG_LD(&NI[stk_at(r)]);
+            if (r < kKM) K.stk[r] = j;
+            else AG_ST(&KS[r - kKM], j);
+          }
+          vm_drain();
+          __syncthreads();
+          for (int j = threadIdx.x; j < nm; j += DT) {  // slot -> member stamps (the sequential fallback reads them)
+            const int v = km_get(K, KM, j, kMSlot);
+            if (v >= 0) t.hst[v] = j;
+            else AG_ST(&T.stamp[~v], j);
+          }
+          vm_drain();
+          __syncthreads();
+        }
+        pr.count(57, hot_n);
+        pr.count(58, 1);
+      }
       for (int q = threadIdx.x; q < n0; q += DT) AG_ST(&CQ[q], cget(stk_at(n0 - 1 - q)));
       vm_drain();
       __syncthreads();
@@ -1647,12 +1732,19 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
         // order as the wave form below, the lane's LIFO in a four-deep shift
         // register (a deeper queue sends the frame to the sequential replay).
         // Components are disjoint, so the lanes never touch the same member.
+        if (threadIdx.x == 0) sh.kheads = 0;
+        __syncthreads();
         {
           const int pos = threadIdx.x;
           bool single = false;
           if (pos < ns) {
             const unsigned kc = key[pos] >> 10;
-            single = (pos == 0 || (key[pos - 1] >> 10) != kc) && (pos == ns - 1 || (key[pos + 1] >> 10) != kc);
+            const bool hd = pos == 0 || (key[pos - 1] >> 10) != kc;
+            single = hd && (pos == ns - 1 || (key[pos + 1] >> 10) != kc);
+            if (hd && !single) {  // a multi-token component: listed for the waves
+              const int q = atomicAdd(&sh.kheads, 1);
+              if (q < 256) sh.hist[q] = (unsigned)pos;
+            }
           }
           if (single) {
             const int prank = (int)(key[pos] & 1023u);
@@ -1666,23 +1758,25 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
               s2 = s3;
               sp--;
               np++;
-              const float cu = __int_as_float(km_get(K, KM, u, kMCost));
+              const int4 ur = km_rec4(K, KM, u);
+              const float cu = __int_as_float(ur.y);
               if (!(cu < cutoff)) continue;
-              const int off = km_get(K, KM, u, kMOff), cnt = km_get(K, KM, u, kMCnt);
+              const int off = ur.z, cnt = ur.w;
               for (int k = 0; k < cnt; k++) {
                 const int2 rec = adj_at(off + k);
                 const int d = rec.x;
                 if (d < 0) continue;
                 const float tot = cu + __int_as_float(rec.y);
                 if (!(tot < cutoff)) continue;
-                const float old = __int_as_float(km_get(K, KM, d, kMCost));
+                const int4 dr = km_rec4(K, KM, d);
+                const float old = __int_as_float(dr.y);
                 if (!(tot < old)) continue;
                 if (old == kInfL) {  // FindOrAddToken creates it
                   km_set(K, KM, d, kMOrd, j++);
                   rset(d, prank);
                 }
                 km_set(K, KM, d, kMCost, __float_as_int(tot));
-                if (km_get(K, KM, d, kMCnt) > 0) {  // changed: re-queued
+                if (dr.w > 0) {  // changed: re-queued
                   if (sp == 4) {
                     lovf = true;
                     break;
@@ -1712,27 +1806,37 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
         const int lane = threadIdx.x & 63;
         if (threadIdx.x == 0) sh.kk = 0;
         __syncthreads();
+        if (pr.on) {  // the lane phase (all lanes done at the barrier)
+          pr.count(59, (long long)__builtin_amdgcn_s_memtime() - t_l0);
+          pr.count(60, 1);
+        }
         int npop = 0, narc = 0, nhbm = 0;
         bool ovf = false;
+        // the multi-token components' heads: from the list (one claim per
+        // component), or by windows of kWin positions when it overflowed
+        const int nheads = sh.kheads;
+        const bool listed = nheads <= 256;
         while (!ovf) {
           constexpr int kWin = 4;
           int c0 = 0;
-          if (lane == 0) c0 = atomicAdd(&sh.kk, kWin);
+          if (lane == 0) c0 = atomicAdd(&sh.kk, listed ? 1 : kWin);
           c0 = __builtin_amdgcn_readfirstlane(c0);
-          if (c0 >= ns) break;
-          const int pos = c0 + lane;
+          if (c0 >= (listed ? nheads : ns)) break;
+          const int pos = listed ? (int)sh.hist[c0] : c0 + lane;
           // (heads of single-token components were replayed by their lanes)
-          const bool head = lane < kWin && pos < ns && (pos == 0 || (key[pos - 1] >> 10) != (key[pos] >> 10)) &&
-                            !(pos == ns - 1 || (key[pos + 1] >> 10) != (key[pos] >> 10));
+          const bool head = listed ? lane == 0
+                                   : lane < kWin && pos < ns && (pos == 0 || (key[pos - 1] >> 10) != (key[pos] >> 10)) &&
+                                         !(pos == ns - 1 || (key[pos + 1] >> 10) != (key[pos] >> 10));
           unsigned long long hm = __ballot(head);
           while (hm && !ovf) {
-            const int h = c0 + __ffsll((long long)hm) - 1;
+            const int h = listed ? pos : c0 + __ffsll((long long)hm) - 1;
             hm &= hm - 1;
             // (LDS values the whole wave reads are made scalar: branching on
             // them would otherwise make the replay loop divergent, every
             // v_readlane a waterfall loop)
             const unsigned cmp = (unsigned)__builtin_amdgcn_readfirstlane((int)(key[h] >> 10));
             const int npop0 = npop;
+            const long long tc0 = (long long)__builtin_amdgcn_s_memtime();
             for (int ri = h; ri < ns && !ovf; ri++) {
               const unsigned kr = (unsigned)__builtin_amdgcn_readfirstlane((int)key[ri]);
               if ((kr >> 10) != cmp) break;
@@ -1743,10 +1847,11 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
                 --sp;
                 npop++;
                 const int u = __builtin_amdgcn_readlane(stk, sp);
-                const float cu = __int_as_float(__builtin_amdgcn_readfirstlane(km_get(K, KM, u, kMCost)));
+                const int4 ur = km_rec4(K, KM, u);  // cost, offset and count in one load
+                const float cu = __int_as_float(__builtin_amdgcn_readfirstlane(ur.y));
                 if (!(cu < cutoff)) continue;
-                const int off = __builtin_amdgcn_readfirstlane(km_get(K, KM, u, kMOff));
-                const int cnt = __builtin_amdgcn_readfirstlane(km_get(K, KM, u, kMCnt));
+                const int off = __builtin_amdgcn_readfirstlane(ur.z);
+                const int cnt = __builtin_amdgcn_readfirstlane(ur.w);
                 narc += cnt;
                 if (u >= kKM) nhbm++;
                 for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
@@ -1754,8 +1859,9 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
                   const int2 rec = lane < kn ? adj_at(off + k0 + lane) : make_int2(-1, 0);
                   int oldl = __float_as_int(kInfL), cntl = 0;
                   if (rec.x >= 0) {
-                    oldl = km_get(K, KM, rec.x, kMCost);
-                    cntl = km_get(K, KM, rec.x, kMCnt);
+                    const int4 dr = km_rec4(K, KM, rec.x);
+                    oldl = dr.y;
+                    cntl = dr.w;
                   }
                   for (int k = 0; k < kn; k++) {
                     const int d = __builtin_amdgcn_readlane(rec.x, k);
@@ -1789,6 +1895,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
             if (lane == 0) {
               atomicAdd(&sh.kcomp_n, 1);
               atomicMax(&sh.kcomp_max, npop - npop0);
+              atomicMax(&sh.kcomp_clk, (int)((long long)__builtin_amdgcn_s_memtime() - tc0));
             }
           }
         }
@@ -1892,10 +1999,10 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     const int lane = threadIdx.x;
     int c0 = __float_as_int(kInf), c1 = c0, c2 = c0, c3 = c0;
     int n0r = 0, n1r = 0, n2r = 0, n3r = 0, o0 = 0, o1 = 0, o2 = 0, o3 = 0, d0 = -1, d1 = -1, d2 = -1, d3 = -1;
-    if (lane < nm) { c0 = __float_as_int(K.mc[lane]); n0r = K.mn[lane]; o0 = K.mo[lane]; }
-    if (lane + 64 < nm) { c1 = __float_as_int(K.mc[lane + 64]); n1r = K.mn[lane + 64]; o1 = K.mo[lane + 64]; }
-    if (lane + 128 < nm) { c2 = __float_as_int(K.mc[lane + 128]); n2r = K.mn[lane + 128]; o2 = K.mo[lane + 128]; }
-    if (lane + 192 < nm) { c3 = __float_as_int(K.mc[lane + 192]); n3r = K.mn[lane + 192]; o3 = K.mo[lane + 192]; }
+    if (lane < nm) { c0 = __float_as_int((*reinterpret_cast<float*>(&K.rec[lane].y))); n0r = K.rec[lane].w; o0 = K.rec[lane].z; }
+    if (lane + 64 < nm) { c1 = __float_as_int((*reinterpret_cast<float*>(&K.rec[lane + 64].y))); n1r = K.rec[lane + 64].w; o1 = K.rec[lane + 64].z; }
+    if (lane + 128 < nm) { c2 = __float_as_int((*reinterpret_cast<float*>(&K.rec[lane + 128].y))); n2r = K.rec[lane + 128].w; o2 = K.rec[lane + 128].z; }
+    if (lane + 192 < nm) { c3 = __float_as_int((*reinterpret_cast<float*>(&K.rec[lane + 192].y))); n3r = K.rec[lane + 192].w; o3 = K.rec[lane + 192].z; }
     int q0 = lane < n0 ? K.stk[lane] : 0, q1 = lane + 64 < n0 ? K.stk[lane + 64] : 0;
 #define KSEL(r, a0, a1, a2, a3) ((r) == 0 ? (a0) : (r) == 1 ? (a1) : (r) == 2 ? (a2) : (a3))
 #define KRD(r, i, a0, a1, a2, a3) __builtin_amdgcn_readlane(KSEL(r, a0, a1, a2, a3), (i))
@@ -1944,28 +2051,28 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     }
 #undef KRD
 #undef KSEL
-    if (lane < nm) { K.mc[lane] = __int_as_float(c0); K.mord[lane] = d0; }
-    if (lane + 64 < nm) { K.mc[lane + 64] = __int_as_float(c1); K.mord[lane + 64] = d1; }
-    if (lane + 128 < nm) { K.mc[lane + 128] = __int_as_float(c2); K.mord[lane + 128] = d2; }
-    if (lane + 192 < nm) { K.mc[lane + 192] = __int_as_float(c3); K.mord[lane + 192] = d3; }
+    if (lane < nm) { (*reinterpret_cast<float*>(&K.rec[lane].y)) = __int_as_float(c0); K.mord[lane] = d0; }
+    if (lane + 64 < nm) { (*reinterpret_cast<float*>(&K.rec[lane + 64].y)) = __int_as_float(c1); K.mord[lane + 64] = d1; }
+    if (lane + 128 < nm) { (*reinterpret_cast<float*>(&K.rec[lane + 128].y)) = __int_as_float(c2); K.mord[lane + 128] = d2; }
+    if (lane + 192 < nm) { (*reinterpret_cast<float*>(&K.rec[lane + 192].y)) = __int_as_float(c3); K.mord[lane + 192] = d3; }
     if (lane == 0) sh.kn0 = ovf ? -1 : created;
   } else if (threadIdx.x == 0 && fast) {
     int sp = n0, created = 0;
     bool ovf = false;
     while (sp > 0 && !ovf) {
       const int u = K.stk[--sp];
-      const float cu = K.mc[u];
+      const float cu = (*reinterpret_cast<float*>(&K.rec[u].y));
       if (!(cu < cutoff)) continue;
-      const int e1 = K.mo[u] + K.mn[u];
-      for (int e = K.mo[u]; e < e1; e++) {
+      const int e1 = K.rec[u].z + K.rec[u].w;
+      for (int e = K.rec[u].z; e < e1; e++) {
         const int2 rec = K.adj[e];
         const float tot = cu + __int_as_float(rec.y);
         if (rec.x < 0 || !(tot < cutoff)) continue;
-        const float old = K.mc[rec.x];
+        const float old = (*reinterpret_cast<float*>(&K.rec[rec.x].y));
         if (tot < old) {
           if (old == kInf) K.mord[rec.x] = created++;  // FindOrAddToken creates it
-          K.mc[rec.x] = tot;
-          if (K.mn[rec.x] > 0) {  // changed: re-queued (only tokens that relax arcs matter)
+          (*reinterpret_cast<float*>(&K.rec[rec.x].y)) = tot;
+          if (K.rec[rec.x].w > 0) {  // changed: re-queued (only tokens that relax arcs matter)
             if (sp == kKM) {
               ovf = true;
               break;
@@ -1982,7 +2089,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   if (slow && fast) {  // the LDS queue overflowed: start over through the HBM records
     for (int i = threadIdx.x; i < nm; i += DT) {
       const int c = K.mcr[i];
-      K.mc[i] = c >= 0 ? AG_LD(&KC[c]) : kInf;
+      (*reinterpret_cast<float*>(&K.rec[i].y)) = c >= 0 ? AG_LD(&KC[c]) : kInf;
       K.mord[i] = -1;
     }
     __syncthreads();
@@ -2050,6 +2157,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     pr.count(33, sh.kpop_max);
     pr.count(45, sh.kcomp_n);
     pr.count(46, sh.kcomp_max);
+    pr.count(61, sh.kcomp_clk);
     pr.count(54, sh.karc_sum);
     pr.count(55, sh.karc_max);
     pr.count(56, sh.khbm_pops);
@@ -2853,10 +2961,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   // Kaldi order: the epsilon queue's LDS views (kaldi_nonemitting)
   static_assert(kLlhLds >= 4 * kKM && kTokLds >= kKM && DT + 1 >= kKM && 2 * kFrontLds >= 2 * kKE, "LDS views");
   KaldiLds K;
-  K.ms = reinterpret_cast<int*>(L);
-  K.mc = L + kKM;
-  K.mo = reinterpret_cast<int*>(L + 2 * kKM);
-  K.mn = reinterpret_cast<int*>(L + 3 * kKM);
+  K.rec = reinterpret_cast<int4*>(L);
   K.mcr = sh.scan;
   K.mord = sh.abeg;
   K.v0lo = reinterpret_cast<int*>(sh.tcost);
