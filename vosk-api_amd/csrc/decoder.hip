@@ -23,6 +23,7 @@
 // later winner writes after that barrier, so the last write is the final
 // winner's.  The commit therefore never reloads an arc or looks a source up.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include <cstdint>
 
@@ -152,9 +153,39 @@ struct Prof {
 // atomics included, has completed (gfx9 encoding: expcnt 7, lgkmcnt 15)
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
-__device__ __forceinline__ float wave_min_f(float v) {
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+// Wave-wide inclusive scans by DPP: row shifts by 1, 2, 4, 8 within each
+// 16-lane row, then CDNA's row broadcasts (lane 15 into the next row, lane 31
+// into the upper half).  VALU moves only -- a __shfl is an LDS round trip
+// (ds_bpermute) per step.  Lanes without a source keep the identity (`old`).
+template <int CTRL, int ROWM>
+__device__ __forceinline__ int dpp_mov(int old, int x) {
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, ROWM, 0xf, false);
+}
+__device__ __forceinline__ float wave_incl_min(float v) {
+  constexpr int kI = 0x7f800000;  // +inf
+  v = fminf(v, __int_as_float(dpp_mov<0x111, 0xf>(kI, __float_as_int(v))));
+  v = fminf(v, __int_as_float(dpp_mov<0x112, 0xf>(kI, __float_as_int(v))));
+  v = fminf(v, __int_as_float(dpp_mov<0x114, 0xf>(kI, __float_as_int(v))));
+  v = fminf(v, __int_as_float(dpp_mov<0x118, 0xf>(kI, __float_as_int(v))));
+  v = fminf(v, __int_as_float(dpp_mov<0x142, 0xa>(kI, __float_as_int(v))));
+  v = fminf(v, __int_as_float(dpp_mov<0x143, 0xc>(kI, __float_as_int(v))));
   return v;
+}
+__device__ __forceinline__ int wave_incl_sum(int v) {
+  v += dpp_mov<0x111, 0xf>(0, v);
+  v += dpp_mov<0x112, 0xf>(0, v);
+  v += dpp_mov<0x114, 0xf>(0, v);
+  v += dpp_mov<0x118, 0xf>(0, v);
+  v += dpp_mov<0x142, 0xa>(0, v);
+  v += dpp_mov<0x143, 0xc>(0, v);
+  return v;
+}
+// the value of the lane below (lane 0: fill)
+__device__ __forceinline__ float wave_shr1(float v, float fill) {
+  return __int_as_float(dpp_mov<0x138, 0xf>(__float_as_int(fill), __float_as_int(v)));
+}
+__device__ __forceinline__ float wave_min_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wave_incl_min(v)), 63));
 }
 __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
   for (int o = 32; o > 0; o >>= 1) {
@@ -200,11 +231,7 @@ __device__ __forceinline__ unsigned long long block_sum_u64(DecShared& sh, unsig
 // exclusive scan of deg over the block; writes sh.scan[0..DT], sh.total
 __device__ __forceinline__ void block_scan(DecShared& sh, int deg) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int v = deg;
-  for (int o = 1; o < 64; o <<= 1) {
-    int u = __shfl_up(v, o, 64);
-    if (lane >= o) v += u;
-  }
+  const int v = wave_incl_sum(deg);
   __syncthreads();
   if (lane == 63) sh.red_i[w] = v;
   __syncthreads();
@@ -294,11 +321,7 @@ __device__ __forceinline__ float kth_smallest(DecShared& sh, const TokView& tv, 
       const int h0 = sh.hist[4 * l], h1 = sh.hist[4 * l + 1], h2 = sh.hist[4 * l + 2],
                 h3 = sh.hist[4 * l + 3];
       const int tot = h0 + h1 + h2 + h3;
-      int incl = tot;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(incl, o, 64);
-        if (l >= o) incl += u;
-      }
+      const int incl = wave_incl_sum(tot);
       const int excl = incl - tot;
       const int kk = sh.sel_k;
       if (kk >= excl && kk < incl) {  // exactly one lane holds the bucket
@@ -605,7 +628,7 @@ __device__ __forceinline__ void emit_link(const DecArgs& a, DecShared& sh, long 
   const int leader = __ffsll((long long)m) - 1;
   int base = 0;
   if (lane == leader) base = atomicAdd(&sh.n_links, __popcll(m));
-  base = __shfl(base, leader, 64);
+  base = __builtin_amdgcn_readlane(base, leader);
   const int off = __popcll(m & ((1ull << lane) - 1ull));
   const long long pos = used + base + off;
   if (pos < a.link_cap) {
@@ -878,13 +901,8 @@ __device__ __forceinline__ void hbm_clear_all(const DecArgs& a, const HbmTab& T)
 // sh.kcar[par]; leaves the running minimum after the block in sh.kcar[par ^ 1]
 __device__ __forceinline__ float kaldi_excl_min(DecShared& sh, float v, int par) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float incl = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const float u = __shfl_up(incl, o, 64);
-    if (lane >= o) incl = fminf(incl, u);
-  }
-  float excl = __shfl_up(incl, 1, 64);
-  if (lane == 0) excl = __int_as_float(0x7f800000);
+  const float incl = wave_incl_min(v);
+  const float excl = wave_shr1(incl, __int_as_float(0x7f800000));
   if (lane == 63) sh.kmin_w[par][w] = incl;
   __syncthreads();
   float pre = sh.kcar[par];
@@ -905,49 +923,71 @@ __device__ __forceinline__ float kaldi_excl_min(DecShared& sh, float v, int par)
 // at most one sub-round ahead of the slowest (it needs that wave's block
 // minimum to finish its own look-back).
 constexpr unsigned kLbIncl = 1u;
+__device__ __forceinline__ unsigned long long kaldi_lb_pack(int q, unsigned fl, float x) {
+  return ((unsigned long long)(((unsigned)q << 1) | fl) << 32) | (unsigned long long)ford(x);
+}
+// a block's aggregate published before its look-back (lane 0)
+__device__ __forceinline__ void kaldi_lb_publish(DecShared& sh, int q, float agg) {
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_store(&sh.kls[q % (4 * DW)], kaldi_lb_pack(q, 0u, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ float kaldi_lookback_min(DecShared& sh, float v, int q, float seed, float* incl_out) {
   const int lane = threadIdx.x & 63;
-  float incl = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const float u = __shfl_up(incl, o, 64);
-    if (lane >= o) incl = fminf(incl, u);
-  }
-  float excl = __shfl_up(incl, 1, 64);
-  if (lane == 0) excl = __int_as_float(0x7f800000);
-  const float agg = __shfl(incl, 63, 64);
+  const float incl = wave_incl_min(v);
+  const float excl = wave_shr1(incl, __int_as_float(0x7f800000));
+  const float agg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
   constexpr int R = 4 * DW;
-  auto pack = [](int qq, unsigned fl, float x) {
-    return ((unsigned long long)(((unsigned)qq << 1) | fl) << 32) | (unsigned long long)ford(x);
-  };
-  if (lane == 0)
-    __hip_atomic_store(&sh.kls[q % R], pack(q, 0u, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  kaldi_lb_publish(sh, q, agg);
   float carry = __int_as_float(0x7f800000);
   if (q == 0) {
     carry = seed;
   } else {
+    // the look-back reads a window of kLbWin blocks at once, one per lane
+    // (blocks k - lane), and folds the window up to its nearest inclusive
+    // prefix when every block before it is published.  A wave is never more
+    // than DW blocks ahead of the slowest, so the ring's R >= 2 kLbWin
+    // entries in the window are the blocks named, or not yet published.
+    constexpr int kLbWin = 32;
+    static_assert(R >= 2 * kLbWin && kLbWin >= DW, "look-back window");
     int k = q - 1;
     while (true) {
+      const int kb = k - lane;
+      const bool in = lane < kLbWin && kb >= 0;
       unsigned long long st = 0;
-      if (lane == 0) {
-        while (true) {
-          st = __hip_atomic_load(&sh.kls[k % R], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if ((int)((unsigned)(st >> 32) >> 1) == k) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
+      if (in) st = __hip_atomic_load(&sh.kls[kb % R], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const unsigned hi = (unsigned)(st >> 32);
+      const bool have = in && (int)(hi >> 1) == kb;
+      const bool stop = have && ((hi & kLbIncl) || kb == 0);
+      const unsigned long long hv = __ballot(have), hs = __ballot(stop);
+      const int nin = k + 1 < kLbWin ? k + 1 : kLbWin;
+      const unsigned long long need = hs ? ((hs & (0ull - hs)) << 1) - 1ull : (1ull << nin) - 1ull;
+      if ((hv & need) != need) {
+        // a block before the nearest prefix is not published yet: one lane
+        // waits for the nearest such block (spinning lanes would take LDS
+        // bandwidth from the relaxations), then the window is read again
+        const int km = k - (__ffsll((long long)(need & ~hv)) - 1);
+        if (lane == 0)
+          while ((int)((unsigned)(__hip_atomic_load(&sh.kls[km % R], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
+                                  32) >> 1) != km)
+            __builtin_amdgcn_s_sleep(1);
+        continue;
       }
-      st = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(st >> 32)) << 32) |
-           (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)st);
-      carry = fminf(carry, funord((uint32_t)st));
-      if (((unsigned)(st >> 32) & kLbIncl) || k == 0) {
-        if (!((unsigned)(st >> 32) & kLbIncl)) carry = fminf(carry, seed);  // block 0's aggregate: add the seed
+      // fold the needed lanes (usually one or two) with scalar lane reads
+      const int lo = (int)(unsigned)st;
+      for (unsigned long long mm = need; mm; mm &= mm - 1ull)
+        carry = fminf(carry, funord((uint32_t)__builtin_amdgcn_readlane(lo, __ffsll((long long)mm) - 1)));
+      if (hs) {
+        const int lf = __ffsll((long long)hs) - 1;
+        if (k == lf && !((unsigned)__builtin_amdgcn_readlane((int)hi, lf) & kLbIncl))
+          carry = fminf(carry, seed);  // block 0's aggregate: add the seed
         break;
       }
-      k--;
+      k -= kLbWin;
     }
   }
   const float inc = fminf(carry, agg);
   if (lane == 0)
-    __hip_atomic_store(&sh.kls[q % R], pack(q, kLbIncl, inc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&sh.kls[q % R], kaldi_lb_pack(q, kLbIncl, inc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   *incl_out = inc;
   return fminf(carry, excl);
 }
@@ -955,11 +995,7 @@ __device__ __forceinline__ float kaldi_lookback_min(DecShared& sh, float v, int 
 // exclusive prefix sum over the block in thread order; *total = the block's sum
 __device__ __forceinline__ int kaldi_excl_sum(DecShared& sh, int v, int par, int* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int incl = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += u;
-  }
+  const int incl = wave_incl_sum(v);
   if (lane == 63) sh.ksum_w[par][w] = incl;
   __syncthreads();
   int off = 0, tot = 0;
@@ -1111,6 +1147,7 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
                                                    qsub * DW + (int)(threadIdx.x >> 6), seed, &incl_last)
                               : kaldi_excl_min(sh, valid ? tot + adaptive : __int_as_float(0x7f800000), par);
       qsub++;
+      pr.mark(62);
       const bool want = valid && tot < run;
       const int item = ibase + it;
       const unsigned long long kv = ((unsigned long long)ford(tot) << 32) | (unsigned)arc;
@@ -1242,8 +1279,8 @@ __device__ __forceinline__ void km_set(const KaldiLds& K, int* KM, int i, int f,
   else AG_ST(&KM[(long long)(i - kKM) * kKMRec + f], v);
 }
 
-// block-wide bitonic sorts in LDS (ascending; n <= DT, padded to a power of
-// two with the maximum key): 64-bit keys as (hi, lo) int pairs, 32-bit keys
+// block-wide bitonic sort in LDS (ascending; n <= DT, padded to a power of
+// two with the maximum key) of 64-bit keys as (hi, lo) int pairs
 __device__ __forceinline__ void bitonic_sort64(int* hi, int* lo, int n) {
   int np = 1;
   while (np < n) np <<= 1;
@@ -1261,24 +1298,6 @@ __device__ __forceinline__ void bitonic_sort64(int* hi, int* lo, int n) {
         if (((i & k) == 0) ? (x > y) : (x < y)) {
           hi[i] = (int)(y >> 32); lo[i] = (int)(unsigned)y;
           hi[l] = (int)(x >> 32); lo[l] = (int)(unsigned)x;
-        }
-      }
-      __syncthreads();
-    }
-}
-__device__ __forceinline__ void bitonic_sort32(unsigned* key, int n) {
-  int np = 1;
-  while (np < n) np <<= 1;
-  for (int i = n + threadIdx.x; i < np; i += DT) key[i] = 0xffffffffu;
-  __syncthreads();
-  for (int k = 2; k <= np; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int i = threadIdx.x, l = i ^ j;
-      if (i < np && l > i) {
-        const unsigned x = key[i], y = key[l];
-        if (((i & k) == 0) ? (x > y) : (x < y)) {
-          key[i] = y;
-          key[l] = x;
         }
       }
       __syncthreads();
@@ -1719,178 +1738,215 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
       __syncthreads();
       // segments of kKM processing ranks in order: the queue restricted to a
       // segment starts from the costs the earlier segments left
-      int created_total = 0;
-      for (int base = 0; base < n0 && sh.flag == 0; base += kKM) {
-        const int ns = n0 - base < kKM ? n0 - base : kKM;
-        for (int r = threadIdx.x; r < ns; r += DT) key[r] = ((unsigned)AG_LD(&CQ[base + r]) << 10) | (unsigned)r;
-        __syncthreads();
-        bitonic_sort32(key, ns);
-        pr.mark(41);
-        const long long t_l0 = pr.on ? (long long)__builtin_amdgcn_s_memtime() : 0;
-        // Components with a single initial token in this segment (most of
-        // them) replay one per lane, all at once: the same pops and arc
-        // order as the wave form below, the lane's LIFO in a four-deep shift
-        // register (a deeper queue sends the frame to the sequential replay).
-        // Components are disjoint, so the lanes never touch the same member.
-        if (threadIdx.x == 0) sh.kheads = 0;
-        __syncthreads();
-        {
-          const int pos = threadIdx.x;
-          bool single = false;
-          if (pos < ns) {
-            const unsigned kc = key[pos] >> 10;
-            const bool hd = pos == 0 || (key[pos - 1] >> 10) != kc;
-            single = hd && (pos == ns - 1 || (key[pos + 1] >> 10) != kc);
-            if (hd && !single) {  // a multi-token component: listed for the waves
+      // the segments' replay, specialised for frames whose members and arcs
+      // all fit the LDS records (no HBM address branches in the pop loops)
+      auto replay_segments = [&](auto lds_only) -> int {
+        constexpr bool L = decltype(lds_only)::value;
+        auto rec4 = [&](int i) -> int4 {
+          return (L || i < kKM) ? K.rec[i] : wg_ld4(reinterpret_cast<const int4*>(rec_at(i, 0)));
+        };
+        auto setf = [&](int i, int f, int v) {
+          if (L || i < kKM) *km_lds(K, i, f) = v;
+          else AG_ST(rec_at(i, f), v);
+        };
+        auto getf = [&](int i, int f) -> int { return (L || i < kKM) ? *km_lds(K, i, f) : AG_LD(rec_at(i, f)); };
+        auto adj = [&](int e) -> int2 { return (L || e < kKE) ? K.adj[e] : adj_at(e); };
+        auto rootg = [&](int i) -> int { return (L || i < kKM) ? mroot[i] : AG_LD(rec_at(i, kMRoot)); };
+        auto roots = [&](int i, int v) {
+          if (L || i < kKM) mroot[i] = v;
+          else AG_ST(rec_at(i, kMRoot), v);
+        };
+        auto stk2 = [&](int r) -> int { return (L || r < kKM) ? K.stk[r] : AG_LD(&KS[r - kKM]); };
+        int created_total = 0;
+        for (int base = 0; base < n0 && sh.flag == 0; base += kKM) {
+          const int ns = n0 - base < kKM ? n0 - base : kKM;
+          // the segment's component labels by processing rank (one rank per
+          // thread: ns <= kKM = DT); the ranks of each component are counted
+          // in its label member's root field (-1 + count; the field is -1
+          // between replays), and a component's second rank lists it for the
+          // waves (past 256 heads: in the frontier scratch, free here)
+          static_assert(kKM <= DT, "one processing rank per thread");
+          int* HL = p.fg0;
+          if (threadIdx.x == 0) sh.kheads = 0;
+          int myc = -1, before = 0;
+          if ((int)threadIdx.x < ns) {
+            myc = AG_LD(&CQ[base + threadIdx.x]);
+            key[threadIdx.x] = (unsigned)myc;
+          }
+          __syncthreads();
+          if (myc >= 0) {
+            before = (L || myc < kKM) ? atomicAdd(&mroot[myc], 1)
+                               : __hip_atomic_fetch_add(rec_at(myc, kMRoot), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (before == 0) {
               const int q = atomicAdd(&sh.kheads, 1);
-              if (q < 256) sh.hist[q] = (unsigned)pos;
+              if (q < 256) sh.hist[q] = (unsigned)myc;
+              else AG_ST(&HL[q - 256], myc);
             }
           }
-          if (single) {
-            const int prank = (int)(key[pos] & 1023u);
-            int s0 = stk_at(n0 - 1 - (base + prank)), s1 = 0, s2 = 0, s3 = 0;
-            int sp = 1, j = 0, np = 0;
-            bool lovf = false;
-            while (sp > 0) {
-              const int u = s0;  // pop
-              s0 = s1;
-              s1 = s2;
-              s2 = s3;
-              sp--;
-              np++;
-              const int4 ur = km_rec4(K, KM, u);
-              const float cu = __int_as_float(ur.y);
-              if (!(cu < cutoff)) continue;
-              const int off = ur.z, cnt = ur.w;
-              for (int k = 0; k < cnt; k++) {
-                const int2 rec = adj_at(off + k);
-                const int d = rec.x;
-                if (d < 0) continue;
-                const float tot = cu + __int_as_float(rec.y);
-                if (!(tot < cutoff)) continue;
-                const int4 dr = km_rec4(K, KM, d);
-                const float old = __int_as_float(dr.y);
-                if (!(tot < old)) continue;
-                if (old == kInfL) {  // FindOrAddToken creates it
-                  km_set(K, KM, d, kMOrd, j++);
-                  rset(d, prank);
-                }
-                km_set(K, KM, d, kMCost, __float_as_int(tot));
-                if (dr.w > 0) {  // changed: re-queued
-                  if (sp == 4) {
-                    lovf = true;
-                    break;
-                  }
-                  s3 = s2;  // push
-                  s2 = s1;
-                  s1 = s0;
-                  s0 = d;
-                  sp++;
-                }
-              }
-              if (lovf) break;
-            }
-            K.v0lo[prank] = j;
-            if (lovf) sh.flag = 1;
-            atomicAdd(&sh.kpop_sum, np);
-          }
-        }
-        // one wave per component: the waves claim kWin sorted positions at a
-        // time and replay every component that starts there (a small window:
-        // the components spread over all waves).  A popped
-        // token's arcs are read by the wave's lanes together (records, then
-        // the destinations' costs and arc counts), then applied in arc order
-        // (v_readlane; a later arc to the same token sees the new cost); the
-        // LIFO stack lives one entry per lane (depth 64).  A rank's creation
-        // count goes to K.v0lo[rank - base] (the labels were consumed into CQ).
-        const int lane = threadIdx.x & 63;
-        if (threadIdx.x == 0) sh.kk = 0;
-        __syncthreads();
-        if (pr.on) {  // the lane phase (all lanes done at the barrier)
-          pr.count(59, (long long)__builtin_amdgcn_s_memtime() - t_l0);
-          pr.count(60, 1);
-        }
-        int npop = 0, narc = 0, nhbm = 0;
-        bool ovf = false;
-        // the multi-token components' heads: from the list (one claim per
-        // component), or by windows of kWin positions when it overflowed
-        const int nheads = sh.kheads;
-        const bool listed = nheads <= 256;
-        while (!ovf) {
-          constexpr int kWin = 4;
-          int c0 = 0;
-          if (lane == 0) c0 = atomicAdd(&sh.kk, listed ? 1 : kWin);
-          c0 = __builtin_amdgcn_readfirstlane(c0);
-          if (c0 >= (listed ? nheads : ns)) break;
-          const int pos = listed ? (int)sh.hist[c0] : c0 + lane;
-          // (heads of single-token components were replayed by their lanes)
-          const bool head = listed ? lane == 0
-                                   : lane < kWin && pos < ns && (pos == 0 || (key[pos - 1] >> 10) != (key[pos] >> 10)) &&
-                                         !(pos == ns - 1 || (key[pos + 1] >> 10) != (key[pos] >> 10));
-          unsigned long long hm = __ballot(head);
-          while (hm && !ovf) {
-            const int h = listed ? pos : c0 + __ffsll((long long)hm) - 1;
-            hm &= hm - 1;
-            // (LDS values the whole wave reads are made scalar: branching on
-            // them would otherwise make the replay loop divergent, every
-            // v_readlane a waterfall loop)
-            const unsigned cmp = (unsigned)__builtin_amdgcn_readfirstlane((int)(key[h] >> 10));
-            const int npop0 = npop;
-            const long long tc0 = (long long)__builtin_amdgcn_s_memtime();
-            for (int ri = h; ri < ns && !ovf; ri++) {
-              const unsigned kr = (unsigned)__builtin_amdgcn_readfirstlane((int)key[ri]);
-              if ((kr >> 10) != cmp) break;
-              const int prank = (int)(kr & 1023u);
-              int stk = lane == 0 ? stk_at(n0 - 1 - (base + prank)) : 0;
-              int sp = 1, j = 0;
-              while (sp > 0 && !ovf) {
-                --sp;
-                npop++;
-                const int u = __builtin_amdgcn_readlane(stk, sp);
-                const int4 ur = km_rec4(K, KM, u);  // cost, offset and count in one load
-                const float cu = __int_as_float(__builtin_amdgcn_readfirstlane(ur.y));
+          vm_drain();
+          __syncthreads();
+          const bool single = myc >= 0 && rootg(myc) == 0;
+          vm_drain();
+          __syncthreads();
+          if (before == -1) roots(myc, -1);  // the component's first rank restores the field
+          vm_drain();
+          __syncthreads();
+          pr.mark(41);
+          const long long t_l0 = pr.on ? (long long)__builtin_amdgcn_s_memtime() : 0;
+          // Components with a single initial token in this segment (most of
+          // them) replay one per lane, all at once: the same pops and arc
+          // order as the wave form below, the lane's LIFO in a four-deep shift
+          // register (a deeper queue sends the frame to the sequential replay).
+          // Components are disjoint, so the lanes never touch the same member.
+          {
+            if (single) {
+              const int prank = (int)threadIdx.x;
+              int s0 = stk2(n0 - 1 - (base + prank)), s1 = 0, s2 = 0, s3 = 0;
+              int sp = 1, j = 0, np = 0;
+              bool lovf = false;
+              while (sp > 0) {
+                const int u = s0;  // pop
+                s0 = s1;
+                s1 = s2;
+                s2 = s3;
+                sp--;
+                np++;
+                const int4 ur = rec4(u);
+                const float cu = __int_as_float(ur.y);
                 if (!(cu < cutoff)) continue;
-                const int off = __builtin_amdgcn_readfirstlane(ur.z);
-                const int cnt = __builtin_amdgcn_readfirstlane(ur.w);
-                narc += cnt;
-                if (u >= kKM) nhbm++;
-                for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
-                  const int kn = cnt - k0 < 64 ? cnt - k0 : 64;
-                  const int2 rec = lane < kn ? adj_at(off + k0 + lane) : make_int2(-1, 0);
-                  int oldl = __float_as_int(kInfL), cntl = 0;
-                  if (rec.x >= 0) {
-                    const int4 dr = km_rec4(K, KM, rec.x);
-                    oldl = dr.y;
-                    cntl = dr.w;
-                  }
-                  for (int k = 0; k < kn; k++) {
-                    const int d = __builtin_amdgcn_readlane(rec.x, k);
-                    if (d < 0) continue;
-                    const float tot = cu + __int_as_float(__builtin_amdgcn_readlane(rec.y, k));
+                const int off = ur.z, cnt = ur.w;
+                // arcs four at a time: their records, then their destinations'
+                // records, in flight together; applied in arc order (a later
+                // arc of the group to the same token sees the new cost)
+                for (int k0 = 0; k0 < cnt && !lovf; k0 += 4) {
+                  int2 r4[4];
+                  int4 d4[4];
+  #pragma unroll
+                  for (int m = 0; m < 4; m++) r4[m] = k0 + m < cnt ? adj(off + k0 + m) : make_int2(-1, 0);
+  #pragma unroll
+                  for (int m = 0; m < 4; m++)
+                    d4[m] = r4[m].x >= 0 ? rec4(r4[m].x) : make_int4(0, 0, 0, 0);
+  #pragma unroll
+                  for (int m = 0; m < 4; m++) {
+                    const int d = r4[m].x;
+                    if (d < 0 || lovf) continue;
+                    const float tot = cu + __int_as_float(r4[m].y);
                     if (!(tot < cutoff)) continue;
-                    const float old = __int_as_float(__builtin_amdgcn_readlane(oldl, k));
+                    const float old = __int_as_float(d4[m].y);
                     if (!(tot < old)) continue;
-                    if (rec.x == d) oldl = __float_as_int(tot);
-                    if (lane == k) {
-                      if (old == kInfL) {  // FindOrAddToken creates it
-                        km_set(K, KM, d, kMOrd, j);
-                        rset(d, prank);
-                      }
-                      km_set(K, KM, d, kMCost, __float_as_int(tot));
+  #pragma unroll
+                    for (int m2 = m + 1; m2 < 4; m2++)
+                      if (r4[m2].x == d) d4[m2].y = __float_as_int(tot);
+                    if (old == kInfL) {  // FindOrAddToken creates it
+                      setf(d, kMOrd, j++);
+                      roots(d, prank);
                     }
-                    if (old == kInfL) j++;
-                    if (__builtin_amdgcn_readlane(cntl, k) > 0) {  // changed: re-queued
-                      if (sp == 64) {
-                        ovf = true;
-                        break;
+                    setf(d, kMCost, __float_as_int(tot));
+                    if (d4[m].w > 0) {  // changed: re-queued
+                      if (sp == 4) {
+                        lovf = true;
+                        continue;
                       }
-                      if (lane == sp) stk = d;
+                      s3 = s2;  // push
+                      s2 = s1;
+                      s1 = s0;
+                      s0 = d;
                       sp++;
                     }
                   }
                 }
+                if (lovf) break;
               }
-              if (lane == 0) K.v0lo[prank] = j;
+              K.v0lo[prank] = j;
+              if (lovf) sh.flag = 1;
+              atomicAdd(&sh.kpop_sum, np);
+            }
+          }
+          // one wave per multi-token component, claimed from the list.  A popped
+          // token's arcs are read by the wave's lanes together (records, then
+          // the destinations' costs and arc counts), then applied in arc order
+          // (v_readlane; a later arc to the same token sees the new cost); the
+          // LIFO stack lives one entry per lane (depth 64).  A rank's creation
+          // count goes to K.v0lo[rank - base] (the labels were consumed into CQ).
+          const int lane = threadIdx.x & 63;
+          if (threadIdx.x == 0) sh.kk = 0;
+          __syncthreads();
+          if (pr.on) {  // the lane phase (all lanes done at the barrier)
+            pr.count(59, (long long)__builtin_amdgcn_s_memtime() - t_l0);
+            pr.count(60, 1);
+          }
+          int npop = 0, narc = 0, nhbm = 0;
+          bool ovf = false;
+          // the multi-token components, one claim each from the list; a
+          // component's ranks in processing order by a ballot over the labels
+          const int nheads = sh.kheads;
+          while (!ovf) {
+            int c0 = 0;
+            if (lane == 0) c0 = atomicAdd(&sh.kk, 1);
+            c0 = __builtin_amdgcn_readfirstlane(c0);
+            if (c0 >= nheads) break;
+            // (LDS values the whole wave reads are made scalar: branching on
+            // them would otherwise make the replay loop divergent, every
+            // v_readlane a waterfall loop)
+            const int cmp = __builtin_amdgcn_readfirstlane(c0 < 256 ? (int)sh.hist[c0] : AG_LD(&HL[c0 - 256]));
+            const int npop0 = npop;
+            const long long tc0 = (long long)__builtin_amdgcn_s_memtime();
+            for (int ch = 0; ch < ns && !ovf; ch += 64) {
+              unsigned long long rm = __ballot(ch + lane < ns && (int)key[ch + lane] == cmp);
+              while (rm && !ovf) {
+                const int prank = ch + __ffsll((long long)rm) - 1;
+                rm &= rm - 1;
+                int stk = lane == 0 ? stk2(n0 - 1 - (base + prank)) : 0;
+                int sp = 1, j = 0;
+                while (sp > 0 && !ovf) {
+                  --sp;
+                  npop++;
+                  const int u = __builtin_amdgcn_readlane(stk, sp);
+                  const int4 ur = rec4(u);  // cost, offset and count in one load
+                  const float cu = __int_as_float(__builtin_amdgcn_readfirstlane(ur.y));
+                  if (!(cu < cutoff)) continue;
+                  const int off = __builtin_amdgcn_readfirstlane(ur.z);
+                  const int cnt = __builtin_amdgcn_readfirstlane(ur.w);
+                  narc += cnt;
+                  if (!L && u >= kKM) nhbm++;
+                  for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
+                    const int kn = cnt - k0 < 64 ? cnt - k0 : 64;
+                    const int2 rec = lane < kn ? adj(off + k0 + lane) : make_int2(-1, 0);
+                    int oldl = __float_as_int(kInfL), cntl = 0;
+                    if (rec.x >= 0) {
+                      const int4 dr = rec4(rec.x);
+                      oldl = dr.y;
+                      cntl = dr.w;
+                    }
+                    for (int k = 0; k < kn; k++) {
+                      const int d = __builtin_amdgcn_readlane(rec.x, k);
+                      if (d < 0) continue;
+                      const float tot = cu + __int_as_float(__builtin_amdgcn_readlane(rec.y, k));
+                      if (!(tot < cutoff)) continue;
+                      const float old = __int_as_float(__builtin_amdgcn_readlane(oldl, k));
+                      if (!(tot < old)) continue;
+                      if (rec.x == d) oldl = __float_as_int(tot);
+                      if (lane == k) {
+                        if (old == kInfL) {  // FindOrAddToken creates it
+                          setf(d, kMOrd, j);
+                          roots(d, prank);
+                        }
+                        setf(d, kMCost, __float_as_int(tot));
+                      }
+                      if (old == kInfL) j++;
+                      if (__builtin_amdgcn_readlane(cntl, k) > 0) {  // changed: re-queued
+                        if (sp == 64) {
+                          ovf = true;
+                          break;
+                        }
+                        if (lane == sp) stk = d;
+                        sp++;
+                      }
+                    }
+                  }
+                }
+                if (lane == 0) K.v0lo[prank] = j;
+              }
             }
             if (lane == 0) {
               atomicAdd(&sh.kcomp_n, 1);
@@ -1898,45 +1954,47 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
               atomicMax(&sh.kcomp_clk, (int)((long long)__builtin_amdgcn_s_memtime() - tc0));
             }
           }
-        }
-        if (lane == 0 && pr.on) {}
-        if (lane == 0 && npop > 0) {
-          atomicAdd(&sh.karc_sum, narc);
-          atomicMax(&sh.karc_max, narc);
-          atomicAdd(&sh.khbm_pops, nhbm);
-        }
-        if (lane == 0) {
-          if (ovf) sh.flag = 1;
-          if (npop > 0) {
-            atomicAdd(&sh.kpop_sum, npop);
-            atomicMax(&sh.kpop_max, npop);
+          if (lane == 0 && npop > 0) {
+            atomicAdd(&sh.karc_sum, narc);
+            atomicMax(&sh.karc_max, narc);
+            atomicAdd(&sh.khbm_pops, nhbm);
           }
-        }
-        vm_drain();
-        __syncthreads();
-        pr.mark(42);
-        if (pr.on) t_lanes += (long long)__builtin_amdgcn_s_memtime() - t_l0;
-        if (sh.flag == 0) {
-          // creations per initial token in processing order, then the global
-          // creation order = (earlier segments) + (rank offset) + creation
-          // within the rank's expansion
-          int tot;
-          const int c = threadIdx.x < ns ? K.v0lo[threadIdx.x] : 0;
-          const int ex = kaldi_excl_sum(sh, c, 0, &tot);
-          __syncthreads();
-          if (threadIdx.x < ns) K.v0lo[threadIdx.x] = ex;
-          __syncthreads();
-          for (int m = threadIdx.x; m < nm; m += DT) {
-            const int r = rget(m);
-            if (r < 0) continue;
-            km_set(K, KM, m, kMOrd, km_get(K, KM, m, kMOrd) + created_total + K.v0lo[r]);
-            rset(m, -1);
+          if (lane == 0) {
+            if (ovf) sh.flag = 1;
+            if (npop > 0) {
+              atomicAdd(&sh.kpop_sum, npop);
+              atomicMax(&sh.kpop_max, npop);
+            }
           }
-          created_total += tot;
           vm_drain();
           __syncthreads();
+          pr.mark(42);
+          if (pr.on) t_lanes += (long long)__builtin_amdgcn_s_memtime() - t_l0;
+          if (sh.flag == 0) {
+            // creations per initial token in processing order, then the global
+            // creation order = (earlier segments) + (rank offset) + creation
+            // within the rank's expansion
+            int tot;
+            const int c = threadIdx.x < ns ? K.v0lo[threadIdx.x] : 0;
+            const int ex = kaldi_excl_sum(sh, c, 0, &tot);
+            __syncthreads();
+            if (threadIdx.x < ns) K.v0lo[threadIdx.x] = ex;
+            __syncthreads();
+            for (int m = threadIdx.x; m < nm; m += DT) {
+              const int r = rootg(m);
+              if (r < 0) continue;
+              setf(m, kMOrd, getf(m, kMOrd) + created_total + K.v0lo[r]);
+              roots(m, -1);
+            }
+            created_total += tot;
+            vm_drain();
+            __syncthreads();
+          }
         }
-      }
+        return created_total;
+      };
+      const int created_total = (nm <= kKM && adj_n <= kKE) ? replay_segments(std::true_type{})
+                                                            : replay_segments(std::false_type{});
       if (sh.flag == 0) {
         if (threadIdx.x == 0) sh.kn0 = created_total;
         __syncthreads();
@@ -2365,7 +2423,7 @@ __device__ __forceinline__ int commit_eps_links(const DecArgs& a, DecShared& sh,
         const int leader = __ffsll((long long)m) - 1;
         int w0 = 0;
         if (lane == leader) w0 = atomicAdd(&sh.n_eps, __popcll(m));
-        w0 = __shfl(w0, leader, 64);
+        w0 = __builtin_amdgcn_readlane(w0, leader);
         const long long pos = lb + out + w0 + __popcll(m & ((1ull << lane) - 1ull));
         if (pos < a.link_cap && v != kNoSlot) {
           L[pos] = make_int4(sh.tsrc[j], base + slot_pos(a, t, T, nl_n, v), arc, 0);

@@ -249,7 +249,7 @@ struct FrameStat {
   float best, cutoff, next_cutoff, adaptive_beam;
 };
 
-constexpr int kDecProf = 62;  // decoder phase-clock slots per stream (decoder.hip Prof)
+constexpr int kDecProf = 63;  // decoder phase-clock slots per stream (decoder.hip Prof)
 constexpr int kKbMemb = 32;   // Kaldi order: members kept per hash bucket (more: counted by a scan)
 struct DecArgs {
   long long* prof;       // optional per-slot phase clocks [slots][kDecProf] (diagnostics)
