@@ -100,3 +100,33 @@ def test_batch_recognizer_resamples_each_call(synth_model_noep, test_wave, monke
         mb = OL.results(o, o.loglikes(y), kaldi=oracle_py.decoder_order(batch=True) == "kaldi")["mbr"]
         assert texts[i] == " ".join(o.words[w] for w in mb["words"]), (i, texts[i])
         assert texts[i]
+
+
+def test_batch_rate_table_overflow_leaves_the_lane_usable(synth_model_noep, test_wave, monkeypatch):
+    """A lane holds kMaxResampleTables (32) input rates: the recognizer at a
+    33rd rate fails to construct, and the lane keeps no pointer to it (its
+    slot is released before the constructor rethrows); the other recognizers
+    keep decoding."""
+    import vosk
+    vosk.SetLogLevel(-1)
+    monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_model_noep)
+    vosk.GpuInit()
+    model = vosk.BatchModel()
+    recs = [vosk.BatchRecognizer(model, 8000 + 250 * i) for i in range(32)]  # 8000 .. 15750 Hz
+    with pytest.raises(Exception):
+        vosk.BatchRecognizer(model, 7000)
+    rec = vosk.BatchRecognizer(model, 16000)
+    data = test_wave[:16000 * 3].astype("<i2").tobytes()
+    for i in range(0, len(data), 8000):
+        rec.AcceptWaveform(data[i:i + 8000])
+        recs[0].AcceptWaveform(data[i // 2:i // 2 + 4000])
+        model.Wait()
+        rec.Result()
+        recs[0].Result()
+    rec.FinishStream()
+    recs[0].FinishStream()
+    model.Wait()
+    for r in (rec, recs[0]):
+        json.loads(r.Result() or "{}")
+    del recs, rec
+    model.Wait()
