@@ -1010,6 +1010,8 @@ __device__ __forceinline__ int kaldi_excl_sum(DecShared& sh, int v, int par, int
 
 // the epsilon queue's HBM member records (kaldi_nonemitting), ints per record
 constexpr int kKMRec = 8;
+// HashList bookkeeping loops: creation indices per thread in flight together
+constexpr int kHlU = 4;
 
 // Creation ranks of the emitting pass's new tokens (deferred form): each
 // created slot holds the index of its first accepted relaxation (hst /
@@ -1338,18 +1340,42 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     sh.kne = 0;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < ne; c += DT) {
-    const int v = AG_LD(&KO[c]);
-    const int b = (int)((unsigned)slot_state(t, T, v) % (unsigned)khash);
-    AG_ST(&KB[c], b);
-    __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], c);
-    AG_ST(&KC[c], funord((uint32_t)(slot_key(t, T, v) >> 32)));
-    if (v >= 0) t.hst[v] = kNoStamp;
-    else AG_ST(&T.stamp[~v], kNoStamp);
-    const bool eps = v >= 0 ? (t.hp[v] & kPosEps) != 0 : (AG_LD(&T.pos[~v]) & kHPosEps) != 0;
-    if (eps) push_front(a, sh, t, p, 0, &sh.n_front, v);
+  // kHlU creation indices per thread at a time, each step's loads (slot,
+  // then state / key / flags, then the bucket count) in flight together
+  for (int c0 = 0; c0 < ne; c0 += kHlU * DT) {
+    int v[kHlU], b[kHlU], m[kHlU];
+    unsigned long long key[kHlU];
+    bool eps[kHlU];
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      v[u] = c < ne ? AG_LD(&KO[c]) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      if (c >= ne) continue;
+      b[u] = (int)((unsigned)slot_state(t, T, v[u]) % (unsigned)khash);
+      key[u] = slot_key(t, T, v[u]);
+      eps[u] = v[u] >= 0 ? (t.hp[v[u]] & kPosEps) != 0 : (AG_LD(&T.pos[~v[u]]) & kHPosEps) != 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      if (c >= ne) continue;
+      AG_ST(&KB[c], b[u]);
+      __hip_atomic_fetch_min(&BF[b[u]], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      m[u] = __hip_atomic_fetch_add(&BC[b[u]], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      AG_ST(&KC[c], funord((uint32_t)(key[u] >> 32)));
+      if (v[u] >= 0) t.hst[v[u]] = kNoStamp;
+      else AG_ST(&T.stamp[~v[u]], kNoStamp);
+      if (eps[u]) push_front(a, sh, t, p, 0, &sh.n_front, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      if (c < ne && m[u] < kKbMemb) AG_ST(&BM[kKbMemb * b[u] + m[u]], c);
+    }
   }
   vm_drain();
   __syncthreads();
@@ -2264,43 +2290,74 @@ __device__ __forceinline__ void kaldi_positions(const DecArgs& a, DecShared& sh,
   int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
   int* BS = a.kb_start + (long long)slot * a.kb_cap;
   int* BM = a.kb_memb + (long long)slot * a.kb_cap * kKbMemb;
+  // kHlU creation indices per thread at a time, each step's loads in flight
+  // together (bucket, then its first index and size; the scans in order)
   int run = 0, par = 0;
-  for (int c0 = 0; c0 < n; c0 += DT) {
-    const int c = c0 + threadIdx.x;
-    int b = 0, sz = 0;
-    bool lead = false;
-    if (c < n) {
-      b = AG_LD(&KB[c]);
-      const int bf = AG_LD(&BF[b]), bc = AG_LD(&BC[b]);  // (issued together)
-      lead = bf == c;
-      if (lead) sz = bc;
+  for (int c0 = 0; c0 < n; c0 += kHlU * DT) {
+    int b[kHlU], bf[kHlU], bc[kHlU];
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      b[u] = c < n ? AG_LD(&KB[c]) : 0;
     }
-    int tot;
-    const int ex = run + kaldi_excl_sum(sh, sz, par, &tot);
-    if (lead) AG_ST(&BS[b], ex);
-    run += tot;
-    par ^= 1;
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      bf[u] = -1;
+      bc[u] = 0;
+      if (c < n) {
+        bf[u] = AG_LD(&BF[b[u]]);
+        bc[u] = AG_LD(&BC[b[u]]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      if (c0 + u * DT >= n) break;
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      const bool lead = c < n && bf[u] == c;
+      int tot;
+      const int ex = run + kaldi_excl_sum(sh, lead ? bc[u] : 0, par, &tot);
+      if (lead) AG_ST(&BS[b[u]], ex);
+      run += tot;
+      par ^= 1;
+    }
   }
   vm_drain();
   __syncthreads();
-  for (int c = threadIdx.x; c < n; c += DT) {
-    const int b = AG_LD(&KB[c]);
-    const int v = AG_LD(&KO[c]);
-    // (issued together)
-    const int cnt = AG_LD(&BC[b]), bs = AG_LD(&BS[b]);
-    int rk = 0;
-    if (cnt > 1 && cnt <= kKbMemb) {  // the bucket's members created before c
-      for (int m = 0; m < cnt; m += 4) {
-        const int4 q = wg_ld4(reinterpret_cast<const int4*>(&BM[kKbMemb * b + m]));
-        rk += (q.x < c) + (m + 1 < cnt && q.y < c) + (m + 2 < cnt && q.z < c) + (m + 3 < cnt && q.w < c);
-      }
-    } else if (cnt > kKbMemb) {  // a crowded bucket: count its tokens created before
-      crowded++;
-      for (int c2 = 0; c2 < c; c2++) rk += AG_LD(&KB[c2]) == b;
+  for (int c0 = 0; c0 < n; c0 += kHlU * DT) {
+    int b[kHlU], v[kHlU], cnt[kHlU], bs[kHlU];
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      if (c >= n) continue;
+      b[u] = AG_LD(&KB[c]);
+      v[u] = AG_LD(&KO[c]);
     }
-    const int pos = bs + rk;
-    if (v >= 0) t.hst[v] = pos;
-    else AG_ST(&T.stamp[~v], pos);
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      if (c >= n) continue;
+      cnt[u] = AG_LD(&BC[b[u]]);
+      bs[u] = AG_LD(&BS[b[u]]);
+    }
+#pragma unroll
+    for (int u = 0; u < kHlU; u++) {
+      const int c = c0 + u * DT + (int)threadIdx.x;
+      if (c >= n) continue;
+      int rk = 0;
+      if (cnt[u] > 1 && cnt[u] <= kKbMemb) {  // the bucket's members created before c
+        for (int m = 0; m < cnt[u]; m += 4) {
+          const int4 q = wg_ld4(reinterpret_cast<const int4*>(&BM[kKbMemb * b[u] + m]));
+          rk += (q.x < c) + (m + 1 < cnt[u] && q.y < c) + (m + 2 < cnt[u] && q.z < c) + (m + 3 < cnt[u] && q.w < c);
+        }
+      } else if (cnt[u] > kKbMemb) {  // a crowded bucket: count its tokens created before
+        crowded++;
+        for (int c2 = 0; c2 < c; c2++) rk += AG_LD(&KB[c2]) == b[u];
+      }
+      const int pos = bs[u] + rk;
+      if (v[u] >= 0) t.hst[v[u]] = pos;
+      else AG_ST(&T.stamp[~v[u]], pos);
+    }
   }
   if (crowded) atomicAdd(&sh.kk, crowded);
   vm_drain();
