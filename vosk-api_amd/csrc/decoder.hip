@@ -255,6 +255,30 @@ __device__ __forceinline__ int owner(const DecShared& sh, int it) {
   return lo;
 }
 
+// Block-start owners of a chunk's items (sh.hist, free during the emitting
+// passes): BO[b] = the token owning item 64 b, written by that token's thread
+// after the scan.  An item's owner then lies between its block's and the next
+// block's starts -- a search over the few tokens starting inside one block
+// instead of over the whole chunk (10 dependent LDS reads).
+constexpr int kOwnBlk = 256;
+__device__ __forceinline__ void owner_blocks(DecShared& sh) {
+  const int s = sh.scan[threadIdx.x], e = sh.scan[threadIdx.x + 1];
+  int* BO = reinterpret_cast<int*>(sh.hist);
+  for (int b = (s + 63) >> 6; (b << 6) < e && b < kOwnBlk; b++) BO[b] = (int)threadIdx.x;
+}
+// nbo = the chunk's block count when it is at most kOwnBlk, else 0 (plain search)
+__device__ __forceinline__ int owner_bo(const DecShared& sh, int nbo, int it) {
+  const int b = it >> 6;
+  if (b >= nbo) return owner(sh, it);
+  const int* BO = reinterpret_cast<const int*>(sh.hist);
+  int lo = BO[b], hi = b + 1 < nbo ? BO[b + 1] : DT - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (sh.scan[mid] <= it) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
 // current-frame tokens: LDS cache when they fit, else global (agent loads)
 struct TokView {
   int* gs;
@@ -683,6 +707,7 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
       }
     }
     block_scan(sh, deg);
+    owner_blocks(sh);
     sh.abeg[threadIdx.x] = ab;
     sh.tcost[threadIdx.x] = c;
     sh.tsrc[threadIdx.x] = src;
@@ -695,6 +720,7 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
     pr.mark(2);
     pr.count(14, 1);
     const int total = sh.total;
+    const int nbo = (total + 63) >> 6 <= kOwnBlk ? (total + 63) >> 6 : 0;
     *examined += total;
     for (int sb = 0; sb < total; sb += DT * kUnroll) {
       int4 A[kUnroll];
@@ -704,7 +730,7 @@ __device__ __forceinline__ float expand_emitting(const DecArgs& a, DecShared& sh
         const int it = sb + u * DT + (int)threadIdx.x;
         jv[u] = -1;
         if (it < total) {
-          const int j = owner(sh, it);
+          const int j = owner_bo(sh, nbo, it);
           jv[u] = j;
           arcv[u] = sh.abeg[j] + (it - sh.scan[j]);
           A[u] = a.arcs[arcv[u]];
@@ -1105,6 +1131,7 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
       }
     }
     block_scan(sh, deg);
+    owner_blocks(sh);
     sh.abeg[threadIdx.x] = ab;
     sh.tcost[threadIdx.x] = c;
     sh.tsrc[threadIdx.x] = src;
@@ -1117,6 +1144,7 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
     pr.mark(2);
     pr.count(14, 1);
     const int total = sh.total;
+    const int nbo = (total + 63) >> 6 <= kOwnBlk ? (total + 63) >> 6 : 0;
     *examined += total;
     // software pipeline: a sub-round's item (owner search, arc load) is
     // fetched before the previous sub-round's scan barrier, so the arc
@@ -1124,7 +1152,7 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
     int jn = 0, arcn = 0;
     int4 An = make_int4(0, 0, 0, 0);
     if ((int)threadIdx.x < total) {
-      jn = owner(sh, threadIdx.x);
+      jn = owner_bo(sh, nbo, threadIdx.x);
       arcn = sh.abeg[jn] + ((int)threadIdx.x - sh.scan[jn]);
       An = a.arcs[arcn];
     }
@@ -1139,7 +1167,7 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
         tot = (sh.tcost[j] + ac) + __int_as_float(A.y);
       }
       if (it + DT < total) {
-        jn = owner(sh, it + DT);
+        jn = owner_bo(sh, nbo, it + DT);
         arcn = sh.abeg[jn] + (it + DT - sh.scan[jn]);
         An = a.arcs[arcn];
       }
@@ -1837,10 +1865,9 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
                 s2 = s3;
                 sp--;
                 np++;
-                const int4 ur = rec4(u);
+                const int4 ur = rec4(u);  // (one read: no branch before its fields' uses)
                 const float cu = __int_as_float(ur.y);
-                if (!(cu < cutoff)) continue;
-                const int off = ur.z, cnt = ur.w;
+                const int off = ur.z, cnt = cu < cutoff ? ur.w : 0;
                 // arcs four at a time: their records, then their destinations'
                 // records, in flight together; applied in arc order (a later
                 // arc of the group to the same token sees the new cost)
@@ -1928,13 +1955,15 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
                   --sp;
                   npop++;
                   const int u = __builtin_amdgcn_readlane(stk, sp);
-                  const int4 ur = rec4(u);  // cost, offset and count in one load
+                  // cost, offset and count in one load: no branch between
+                  // them (a token at or above the cutoff relaxes no arc), so
+                  // the compiler does not split the record into two reads
+                  const int4 ur = rec4(u);
                   const float cu = __int_as_float(__builtin_amdgcn_readfirstlane(ur.y));
-                  if (!(cu < cutoff)) continue;
                   const int off = __builtin_amdgcn_readfirstlane(ur.z);
-                  const int cnt = __builtin_amdgcn_readfirstlane(ur.w);
+                  const int cnt = cu < cutoff ? __builtin_amdgcn_readfirstlane(ur.w) : 0;
                   narc += cnt;
-                  if (!L && u >= kKM) nhbm++;
+                  if (!L && u >= kKM && cnt > 0) nhbm++;
                   for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
                     const int kn = cnt - k0 < 64 ? cnt - k0 : 64;
                     const int2 rec = lane < kn ? adj(off + k0 + lane) : make_int2(-1, 0);
