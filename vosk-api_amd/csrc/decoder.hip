@@ -1867,7 +1867,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
                 np++;
                 const int4 ur = rec4(u);  // (one read: no branch before its fields' uses)
                 const float cu = __int_as_float(ur.y);
-                const int off = ur.z, cnt = cu < cutoff ? ur.w : 0;
+                const int off = ur.z, cnt = ur.w & -(int)(cu < cutoff);
                 // arcs four at a time: their records, then their destinations'
                 // records, in flight together; applied in arc order (a later
                 // arc of the group to the same token sees the new cost)
@@ -1961,7 +1961,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
                   const int4 ur = rec4(u);
                   const float cu = __int_as_float(__builtin_amdgcn_readfirstlane(ur.y));
                   const int off = __builtin_amdgcn_readfirstlane(ur.z);
-                  const int cnt = cu < cutoff ? __builtin_amdgcn_readfirstlane(ur.w) : 0;
+                  const int cnt = __builtin_amdgcn_readfirstlane(ur.w) & -(int)(cu < cutoff);
                   narc += cnt;
                   if (!L && u >= kKM && cnt > 0) nhbm++;
                   for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
