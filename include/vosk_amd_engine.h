@@ -219,8 +219,9 @@ int vamd_batch_lane_kaldi_order(struct VoskBatchModel *m, int lane);
 int vamd_batch_result_profile(struct VoskBatchModel *m, double *out13);
 /* dynamic batching: {lane steps, bounded waits that expired (a feeding
  * round split in two steps), waits ended by a vosk_batch_model_wait caller
- * before the round was complete} */
-int vamd_batch_batching_counters(struct VoskBatchModel *m, long long *out3);
+ * before the round was complete, decoder jobs of one stream completed with
+ * no endpoint probe between them (must stay 0)} */
+int vamd_batch_batching_counters(struct VoskBatchModel *m, long long *out4);
 /* the lane's dynamic batching rule (host only, no GPU): 1 if a step would
  * still wait for streams of the feeding round, given each stream's chunks
  * pushed, chunks handed to the engine and input-ended flag */

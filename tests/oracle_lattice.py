@@ -519,8 +519,12 @@ class _PrunedDet:
         return sid, w2, nbase[len(base):]
 
     def check_memory(self):
+        # (the repository as Kaldi's RebuildRepository leaves it: the strings
+        # live at the last rebuild plus those added since)
         arcs, elems = self.num_arcs * 32, self.num_elems * 24
-        repo = (len(self.nodes) + 1) * 32
+        n = len(self.nodes) + 1
+        rebuilt = getattr(self, "rebuilt", None)
+        repo = (n if rebuilt is None else rebuilt[0] + n - rebuilt[1]) * 32
         if self.max_mem <= 0 or repo + arcs + elems <= self.max_mem:
             return True
         live = set()
@@ -542,6 +546,7 @@ class _PrunedDet:
         for t in self.queue:
             for e in t[4]:
                 mark(e[2])
+        self.rebuilt = (len(live), n)
         repo = len(live) * 32
         if repo + arcs + elems > int(self.max_mem * 0.8):
             if self.queue:

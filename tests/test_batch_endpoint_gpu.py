@@ -14,10 +14,8 @@ import json
 import numpy as np
 import pytest
 
+import batch_expect
 from conftest import perturbed_stream
-import oracle_endpoint as OE
-import oracle_lattice as OL
-import oracle_py
 
 pytestmark = pytest.mark.gpu
 N = 6
@@ -32,36 +30,14 @@ def vosk_mod():
 
 @pytest.fixture(scope="module")
 def expected(synth_model_ep, test_wave):
-    from vosk import engine
-    info = engine.plan_info(synth_model_ep, 51)
-    o = oracle_py.OracleModel(synth_model_ep, fpc=51)
     waves = [perturbed_stream(test_wave, 900 + i, seconds=9.0 + 0.7 * i) for i in range(N)]
-    out = []
-    for w in waves:
-        llh = o.loglikes(w)
-        kaldi = oracle_py.decoder_order(batch=True) == "kaldi"
-        segs = OE.batch_segments_fast(o, w, llh, info["right_context"], info["priming"], kaldi=kaldi)
-        res = []
-        for s0, s1 in segs:
-            mb = OL.results(o, llh[s0:s1], kaldi=kaldi)["mbr"]
-            res.append(dict(text=" ".join(o.words[x] for x in mb["words"]), start=s0 * 0.03,
-                            times=[(np.floor(a + 0.5) * 0.03, np.floor(b + 0.5) * 0.03) for a, b in mb["times"]]))
-        out.append(res)
+    out = batch_expect.expected(synth_model_ep, waves)
     assert sum(len(r) for r in out) >= 3 * N  # the rules fire
     return waves, out
 
 
 def _pcm(x):
     return np.asarray(x, np.float32).astype("<i2").tobytes()
-
-
-def _check(results, exp):
-    assert len(results) == len(exp), ([r["text"] for r in results], [e["text"] for e in exp])
-    for r, e in zip(results, exp):
-        assert r["text"] == e["text"]
-        for w, (tb, te) in zip(r.get("result", []), e["times"]):
-            assert w["start"] == pytest.approx(e["start"] + tb, abs=1e-4)
-            assert w["end"] == pytest.approx(e["start"] + te, abs=1e-4)
 
 
 @pytest.mark.parametrize("feeding", ["wait_per_round", "queued_upfront"])
@@ -96,4 +72,4 @@ def test_batch_endpoint_segments_match_oracle(vosk_mod, synth_model_ep, expected
     collect()
     for i in range(N):
         assert recs[i].GetPendingChunks() == 0
-        _check(results[i], exp[i])
+        batch_expect.check(results[i], exp[i], f"stream {i}")

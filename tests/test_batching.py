@@ -114,6 +114,7 @@ def test_free_right_after_finish_stream(synth_model_noep, test_wave, monkeypatch
 
 
 def _decode_batch(vosk, waves, pattern):
+    from vosk import engine
     model = vosk.BatchModel()
     recs = [vosk.BatchRecognizer(model, 16000) for _ in waves]
     datas = [np.clip(w, -32768, 32767).astype("<i2").tobytes() for w in waves]
@@ -139,32 +140,58 @@ def _decode_batch(vosk, waves, pattern):
         r.FinishStream()
     model.Wait()
     collect()
-    from vosk import engine
     lanes = [engine.batch_recognizer_lane(r) for r in recs]
     nl = engine.batch_lanes(model)
+    counters = engine.batch_batching_counters(model)
     del recs
     del model
-    return out, lanes, nl
+    return out, lanes, nl, counters
+
+
+@pytest.fixture(scope="module")
+def lane_streams(synth_model_ep, test_wave):
+    import batch_expect
+    waves = [perturbed_stream(test_wave, 300 + i, seconds=5.0 + 0.9 * i) for i in range(10)]
+    exp = batch_expect.expected(synth_model_ep, waves)
+    assert sum(len(r) for r in exp) >= 2 * len(waves)  # the rules fire
+    return waves, exp
+
+
+# (lane devices, feeding pattern, VOSK_AMD_BATCH_SCHEDULE seed; 0 = the
+# lane's own schedule)
+LANE_CASES = [("0", "wait_per_round", 0), ("0,0", "wait_per_round", 0),
+              ("0", "queued_upfront", 0), ("0,0", "queued_upfront", 0),
+              ("0", "wait_per_round", 11), ("0,0", "wait_per_round", 12),
+              ("0", "queued_upfront", 13), ("0,0", "queued_upfront", 14)]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pattern", ["wait_per_round", "queued_upfront"])
-def test_two_lanes_on_one_device_equal_one_lane(synth_model_ep, test_wave, monkeypatch, pattern):
-    """The in-library multi-GPU path (BatchModel lanes, admission by
-    PickLane; src/batch_model.cc:23-100) on the one GPU available: two lanes
-    on device 0 (VOSK_AMD_BATCH_DEVICES=0,0) give every stream the same result
-    messages as one lane, and both lanes take streams."""
+@pytest.mark.parametrize("devices,pattern,schedule", LANE_CASES,
+                         ids=[f"{d.replace(',', '+')}-{p}-s{k}" for d, p, k in LANE_CASES])
+def test_lane_configurations_equal_oracle(synth_model_ep, lane_streams, monkeypatch, devices, pattern, schedule):
+    """Every stream's result messages -- segment boundaries, words and times
+    -- equal the oracle's (tests/batch_expect.py) whatever the lane
+    configuration: one lane or two lanes on device 0 (the in-library
+    multi-GPU path, admission by PickLane; src/batch_model.cc:23-100), the
+    feeding pattern (Wait() per round: in-order steps and split rounds;
+    everything queued up front: pipelined steps with resets patched into
+    staged jobs), and a seeded random lane schedule (chunks left for later
+    steps at random, random in-order / pipelined steps)."""
+    import batch_expect
     import vosk
     vosk.SetLogLevel(-1)
+    waves, exp = lane_streams
     monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_model_ep)
     monkeypatch.delenv("VOSK_AMD_DEVICE", raising=False)
     monkeypatch.delenv("LOCAL_RANK", raising=False)
-    waves = [perturbed_stream(test_wave, 300 + i, seconds=5.0 + 0.9 * i) for i in range(10)]
-    monkeypatch.setenv("VOSK_AMD_BATCH_DEVICES", "0")
-    one, lanes1, n1 = _decode_batch(vosk, waves, pattern)
-    monkeypatch.setenv("VOSK_AMD_BATCH_DEVICES", "0,0")
-    two, lanes2, n2 = _decode_batch(vosk, waves, pattern)
-    assert (n1, n2) == (1, 2)
-    assert set(lanes1) == {0} and set(lanes2) == {0, 1}, lanes2
-    assert all(len(r) >= 1 for r in one)
-    assert one == two
+    monkeypatch.setenv("VOSK_AMD_BATCH_DEVICES", devices)
+    if schedule:
+        monkeypatch.setenv("VOSK_AMD_BATCH_SCHEDULE", str(schedule))
+    else:
+        monkeypatch.delenv("VOSK_AMD_BATCH_SCHEDULE", raising=False)
+    out, lanes, nl, counters = _decode_batch(vosk, waves, pattern)
+    assert nl == len(devices.split(","))
+    assert set(lanes) == set(range(nl)), lanes
+    assert counters["merged_probes"] == 0, counters
+    for i in range(len(waves)):
+        batch_expect.check(out[i], exp[i], f"stream {i} (lane {lanes[i]})")

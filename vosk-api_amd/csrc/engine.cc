@@ -190,8 +190,17 @@ void ModelData::LoadBatchLayout(const std::string& path) {
 // ---------------------------------------------------------------------------
 void* Engine::DevAlloc(size_t bytes) {
   void* p = nullptr;
-  HIPCHECK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+  const hipError_t err = hipMalloc(&p, std::max<size_t>(bytes, 16));
+  if (err != hipSuccess) {
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    VAMD_ERR("device allocation of " << (bytes >> 20) << " MB failed (" << hipGetErrorString(err) << "): this engine holds "
+                                     << (dev_bytes_ >> 20) << " MB, " << (fr >> 20) << " MB of " << (tot >> 20)
+                                     << " MB free; fewer channels (VOSK_AMD_BATCH_SLOTS) or tokens "
+                                        "(max-active) need less");
+  }
   dev_allocs_.push_back(p);
+  dev_bytes_ += bytes;
   return p;
 }
 
@@ -733,6 +742,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   }
   dec_.kb_cap = (int)(2 * MT + 1024);
   dec_.kord_cap = (int)((MT + 4096 + 3) & ~3LL);  // (a multiple of 4: 16-byte loads of four entries)
+  size_t kaldi_bytes = dev_bytes_;
   if (dec_.kaldi) {
     const size_t KB = (size_t)S * dec_.kb_cap, KO = (size_t)S * dec_.kord_cap;
     dec_.kb_first = (int*)DevAlloc(sizeof(int) * KB);
@@ -751,7 +761,9 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     // creation order / buckets: valid indices from the start (slot 0, bucket 0)
     HIPCHECK(hipMemset(dec_.kord, 0, sizeof(int) * KO));
     HIPCHECK(hipMemset(dec_.kbkt, 0, sizeof(int) * KO));
+    kaldi_bytes = dev_bytes_ - kaldi_bytes;
   } else {
+    kaldi_bytes = 0;
     dec_.kb_first = dec_.kb_cnt = dec_.kb_start = dec_.kb_memb = nullptr;
     dec_.kord = dec_.kbkt = dec_.kstk = dec_.kmem = nullptr;
     dec_.kcost0 = nullptr;
@@ -786,9 +798,12 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     HIPCHECK(hipHostMalloc((void**)&blk, want, hipHostMallocDefault));
     pinned_->Give(blk, want);
   }
-  HIPCHECK(hipStreamSynchronize(stream_));
+  // the tables above were cleared with null-stream memsets, which the
+  // engine's non-blocking streams are not ordered after
+  HIPCHECK(hipDeviceSynchronize());
   slots_.resize(S);
-  VAMD_LOG("engine: slots=" << S << " fpc=" << fpc << " priming=" << plan_.priming_chunks
+  VAMD_LOG("engine: device memory " << (dev_bytes_ >> 20) << " MB (Kaldi-order scratch "
+                                    << (kaldi_bytes >> 20) << " MB), slots=" << S << " fpc=" << fpc << " priming=" << plan_.priming_chunks
                             << " ring=" << ring_ << " ops=" << plan_.ops.size()
                             << " graph states=" << NS << " arcs=" << g.NumArcs());
 }
@@ -2037,8 +2052,15 @@ void Engine::ResetDecoderAtNextJob(int slot) {
     for (size_t i = 0; i < db.jobs.size(); i++) {
       if (db.jobs[i].slot != slot) continue;
       db.jobs[i].reset = 2;  // a batch segment starts a new decoder
-      DecJob* d = (DecJob*)(d_stage_ + (size_t)db.buf * stage_bytes_ + db.o_ej) + i;
-      HIPCHECK(hipMemcpy(d, &db.jobs[i], sizeof(DecJob), hipMemcpyHostToDevice));
+      // the patch goes through the batch's pinned staging copy, ordered on
+      // the decoder stream: every staged decoder batch launches on dstream_
+      // (the next pipelined step, or a drain), so the launch reads the
+      // patched job whatever else is in flight (a synchronous copy from
+      // pageable memory on the null stream is not ordered with the engine's
+      // non-blocking streams)
+      const size_t o = (size_t)db.buf * stage_bytes_ + db.o_ej + sizeof(DecJob) * i;
+      memcpy(h_stage_ + o, &db.jobs[i], sizeof(DecJob));
+      HIPCHECK(hipMemcpyAsync(d_stage_ + o, h_stage_ + o, sizeof(DecJob), hipMemcpyHostToDevice, dstream_));
       // frame counts of the new segment: this job's, then the later staged one's
       int n = db.jobs[i].nframes;
       db.expect[i] = n;

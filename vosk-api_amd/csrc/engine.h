@@ -458,6 +458,7 @@ class Engine {
   // device: model
   MfccDev mfcc_{};
   std::vector<void*> dev_allocs_;
+  size_t dev_bytes_ = 0;  // DevAlloc total (logged at construction)
   std::vector<NnetOpArgs> op_args_;
   std::vector<int> op_bk_;
   float** d_ring_ptrs_ = nullptr;

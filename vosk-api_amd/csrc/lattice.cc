@@ -746,6 +746,11 @@ class PrunedDeterminizer {
     int state, label;
     std::vector<Elem> sub;  // unnormalized, unique per token, sorted; strings relative to the state's base
   };
+  // Kaldi's TaskCompare orders by priority_cost only and std::priority_queue
+  // leaves ties unordered; ties here go in push order (deterministic).  Which
+  // tasks run before a max_mem / max_states stop can therefore differ from
+  // Kaldi on exactly tied priorities (parity with LatticeDeterminizerPruned is
+  // unpinned: no Kaldi build or fixture here).
   struct TaskLess {
     bool operator()(const Task* a, const Task* b) const {
       if (a->prio != b->prio) return a->prio > b->prio;
@@ -790,6 +795,10 @@ class PrunedDeterminizer {
   long long seq_ = 0, num_elems_ = 0, num_arcs_ = 0;
   double eff_beam_ = 0;
   bool guard_ = false;
+  // the repository as Kaldi's RebuildRepository leaves it: the strings live
+  // at the last rebuild plus every string added since (-1: never rebuilt)
+  long long rebuilt_live_ = -1;
+  size_t rebuilt_at_ = 0;
   std::vector<int> at_pos_;
   std::vector<char> pending_;
   std::vector<std::vector<int>> fbucket_;
@@ -1053,11 +1062,15 @@ void PrunedDeterminizer::ProcessTransition(Task* t) {
 }
 
 // memory estimate (Kaldi CheckMemoryUsage: string repository + 32-byte temp
-// arcs + 24-byte elements; the repository counted as 32 bytes per string in
-// use after a rebuild)
+// arcs + 24-byte elements; the repository counted as 32 bytes per string,
+// and after a rebuild as the strings then in use plus those added since, as
+// RebuildRepository leaves Kaldi's repository -- so a check after a rebuild
+// is cheap until the repository has grown past max_mem again)
 bool PrunedDeterminizer::CheckMemory(double* eff) {
   const long long arcs = num_arcs_ * 32, elems = num_elems_ * 24;
-  long long repo = (long long)R_.parent.size() * 32;
+  const long long nstr = rebuilt_live_ < 0 ? (long long)R_.parent.size()
+                                           : rebuilt_live_ + (long long)(R_.parent.size() - rebuilt_at_);
+  long long repo = nstr * 32;
   if (opt_.max_mem <= 0 || repo + arcs + elems <= opt_.max_mem) return true;
   // rebuild: only strings referenced by states, arcs, tasks and the cache
   std::vector<char> used(R_.parent.size(), 0);
@@ -1087,6 +1100,8 @@ bool PrunedDeterminizer::CheckMemory(double* eff) {
   }
   long long live = 0;
   for (char u : used) live += u;
+  rebuilt_live_ = live;
+  rebuilt_at_ = R_.parent.size();
   repo = live * 32;
   if (repo + arcs + elems > (long long)(opt_.max_mem * 0.8)) {
     if (!queue_.empty()) *eff = queue_.top()->prio - bwd_[D_.start];

@@ -867,9 +867,9 @@ int vamd_batch_result_profile(VoskBatchModel* m, double* out13) {
   API_CATCH(-1)
 }
 
-int vamd_batch_batching_counters(VoskBatchModel* m, long long* out3) {
+int vamd_batch_batching_counters(VoskBatchModel* m, long long* out4) {
   API_TRY
-  ((BatchModel*)m)->BatchingCounters(out3);
+  ((BatchModel*)m)->BatchingCounters(out4);
   return 0;
   API_CATCH(-1)
 }

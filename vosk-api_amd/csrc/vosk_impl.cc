@@ -848,7 +848,7 @@ void BatchModel::ResultProfile(double* out) const {
 int BatchModel::LaneOf(const BatchRecognizer* r) const { return r->lane_; }
 
 void BatchModel::BatchingCounters(long long* out) const {
-  for (int i = 0; i < 3; i++) out[i] = batching_[i];
+  for (int i = 0; i < 4; i++) out[i] = batching_[i];
 }
 
 bool FeedingRoundIncomplete(const std::vector<std::array<long long, 3>>& s) {
@@ -1110,6 +1110,20 @@ void BatchModel::LaneLoop(Lane* L) {
   std::vector<EndpointProbe> pr;
   bool pipelined = false;
   const bool trace = EnvInt("VOSK_AMD_BATCH_TRACE", 0) != 0;  // development: one line per lane step
+  // test hook (VOSK_AMD_BATCH_SCHEDULE=<seed>): a seeded random lane schedule.
+  // Each queued stream's chunk is taken or left for a later step at random,
+  // the bounded wait for the feeding round is skipped, and a step with an
+  // idle pipeline runs in order or pipelined at random.  Segment boundaries
+  // and results must not depend on any of it (tests/test_batching.py).
+  uint64_t rng = (uint64_t)(unsigned)EnvInt("VOSK_AMD_BATCH_SCHEDULE", 0) * 0x9E3779B97F4A7C15ull;
+  const bool sched = rng != 0;
+  auto rnd = [&rng]() {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return rng >> 11;
+  };
+  std::vector<int> seen_slot(L->by_slot.size(), 0);
   long long iter = 0;
   using clk = std::chrono::steady_clock;
   auto ns = [](clk::time_point a, clk::time_point b) {
@@ -1133,7 +1147,7 @@ void BatchModel::LaneLoop(Lane* L) {
       // second step as long as its slowest stream; the next round is whole
       // again, since the rule looks at sequence numbers, not at the last
       // batch's size.
-      if (L->queued > 0 && !e->PipelineBusy()) {
+      if (!sched && L->queued > 0 && !e->PipelineBusy()) {
         const auto t0 = clk::now();
         auto last_push = t0;
         while (!L->stop && L->waiters == 0 && RoundIncomplete(L->recs)) {
@@ -1148,8 +1162,7 @@ void BatchModel::LaneLoop(Lane* L) {
         }
         if (L->waiters > 0 && RoundIncomplete(L->recs)) batching_[2]++;
       }
-      for (BatchRecognizer* r : L->recs) {  // one chunk per stream per step
-        if (r->queue_.empty()) continue;
+      auto take = [&](BatchRecognizer* r) {
         batch.emplace_back(r, std::move(r->queue_.front()));
         r->queue_.pop_front();
         L->queued--;
@@ -1163,10 +1176,21 @@ void BatchModel::LaneLoop(Lane* L) {
           L->busy++;
           active.push_back(r);
         }
+      };
+      BatchRecognizer* first_queued = nullptr;
+      for (BatchRecognizer* r : L->recs) {  // one chunk per stream per step
+        if (r->queue_.empty()) continue;
+        if (!first_queued) first_queued = r;
+        if (sched && (rnd() & 1)) continue;  // left for a later step
+        take(r);
       }
+      // (the random schedule always takes a chunk when nothing else would run)
+      if (sched && batch.empty() && active.empty() && first_queued) take(first_queued);
       // pipeline the stages while a backlog keeps them fed; a batch with
       // nothing queued behind it runs its stages in order (one sync, not three)
       pipelined = L->queued > 0 || e->PipelineBusy();
+      // (an in-order step drains the pipeline first: only with it idle)
+      if (sched && !e->PipelineBusy()) pipelined = (rnd() & 1) != 0;
     }
     const auto ts = clk::now();
     prof_[7] += ns(tw, ts);
@@ -1196,6 +1220,13 @@ void BatchModel::LaneLoop(Lane* L) {
       e->TakeDecoded(&decoded);
       probe.clear();
       probe_r.clear();
+      // every decoder job of a stream is followed by its own probe: a step
+      // completes at most one job per stream (one decoder batch per step, one
+      // job per stream in a batch), so the rules always see the state after
+      // each chunk -- counted if that ever fails to hold
+      for (const Engine::DecodedJob& dj : decoded)
+        if (seen_slot[dj.slot]++) batching_[3]++;
+      for (const Engine::DecodedJob& dj : decoded) seen_slot[dj.slot] = 0;
       for (const Engine::DecodedJob& dj : decoded) {
         const int s = dj.slot;
         BatchRecognizer* r = L->by_slot[s];

@@ -239,7 +239,7 @@ class BatchModel {
   // ms MBR, ms formatting}
   void ResultProfile(double* out7) const;
   int LaneOf(const BatchRecognizer* r) const;
-  void BatchingCounters(long long* out3) const;
+  void BatchingCounters(long long* out4) const;
 
  private:
   struct Lane;
@@ -269,7 +269,7 @@ class BatchModel {
   std::atomic<long long> prof_[13] = {};
   // dynamic batching: {steps, bounded waits that expired (split rounds),
   // waits ended by a Wait() caller}
-  std::atomic<long long> batching_[3] = {};
+  std::atomic<long long> batching_[4] = {};  // steps, split rounds, released by Wait, merged probes
   ~BatchModel();
 };
 

@@ -111,10 +111,12 @@ def feeding_round_incomplete(pushed, taken, ended):
 
 
 def batch_batching_counters(model):
-    """{steps, split_rounds, released_by_wait} of a vosk.BatchModel's lanes."""
-    o = np.zeros(3, np.int64)
+    """{steps, split_rounds, released_by_wait, merged_probes} of a
+    vosk.BatchModel's lanes (merged_probes: decoder jobs of one stream that
+    completed without an endpoint probe between them; must stay 0)."""
+    o = np.zeros(4, np.int64)
     _chk(_c.vamd_batch_batching_counters(model._handle, o.ctypes.data))
-    return dict(zip(("steps", "split_rounds", "released_by_wait"), (int(x) for x in o)))
+    return dict(zip(("steps", "split_rounds", "released_by_wait", "merged_probes"), (int(x) for x in o)))
 
 
 def batch_lanes(model):
