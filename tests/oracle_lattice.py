@@ -25,6 +25,108 @@ INF = float("inf")
 
 
 def raw_from_oracle(r, graph, use_final=True):
+    """Oracle decode(lattice=True) -> the arrays of vamd_stream_lattice
+    (numpy form of raw_from_oracle_loop, which states it link by link; the
+    same arrays, tests/test_lattice.py)."""
+    L = r["lattice"]
+    fb = np.asarray(L["frame_begin"], np.int64)
+    F = len(fb) - 2
+    ts = np.asarray(L["tok_state"], np.int64)
+    NS = int(max(int(ts.max()) if len(ts) else 0, int(np.max(graph.nextstate)) if len(graph.nextstate) else 0)) + 1
+    tf = np.repeat(np.arange(F + 1, dtype=np.int64), np.diff(fb[:F + 2]))
+    key = tf * NS + ts
+    order = np.argsort(key, kind="stable")
+    skey = key[order]
+    lk = np.asarray(L["link_frame"], np.int64)
+    la = np.asarray(L["link_arc"], np.int64)
+    ls = np.asarray(L["link_src"], np.int64)
+    lx = np.asarray(L["link_ac"], np.float32)
+    il = np.asarray(graph.ilabel)[la]
+    emit = il != 0
+    sk = (lk - emit.astype(np.int64)) * NS + ls
+    dk = lk * NS + np.asarray(graph.nextstate, np.int64)[la]
+    sid = order[np.searchsorted(skey, sk)]
+    did = order[np.searchsorted(skey, dk)]
+    assert np.array_equal(skey[np.searchsorted(skey, sk)], sk) and np.array_equal(skey[np.searchsorted(skey, dk)], dk)
+    co = np.asarray(L["cost_offset"], np.float32)[lk]
+    acx = np.where(emit, (lx - co).astype(np.float32), np.float32(0)).astype(np.float32)
+    srt = np.lexsort((la, sid, lk))  # per frame, by (source, arc); stable
+    last = ts[fb[F]:fb[F + 1]]
+    fin = graph.final[last].astype(np.float32)
+    final = fin if (use_final and np.isfinite(fin).any()) else np.zeros(0, np.float32)
+    return dict(num_frames=F, frame_begin=np.asarray(fb, np.int32),
+                tok_state=np.asarray(L["tok_state"], np.int32), tok_cost=np.asarray(L["tok_cost"], np.float32),
+                link_src=sid[srt].astype(np.int32), link_dst=did[srt].astype(np.int32),
+                link_arc=la[srt].astype(np.int32),
+                link_graph=np.asarray(graph.weight, np.float32)[la][srt], link_ac=acx[srt], final_cost=final)
+
+
+# ---------------------------------------------------------------- pruning
+def prune(L, beam):
+    """Lattice-beam pruning (numpy form of prune_loop: per frame, the
+    cross-frame links' relaxations, then the within-frame (epsilon) links
+    relaxed to their fixpoint -- min-plus shortest paths, whose float values
+    do not depend on the relaxation order -- backwards the same; the same
+    arrays, tests/test_lattice.py)."""
+    F = L["num_frames"]
+    fb = np.asarray(L["frame_begin"], np.int64)
+    N = len(L["tok_state"])
+    frame = np.repeat(np.arange(F + 1, dtype=np.int64), np.diff(fb[:F + 2]))
+    src = np.asarray(L["link_src"], np.int64)
+    dst = np.asarray(L["link_dst"], np.int64)
+    g32 = np.asarray(L["link_graph"], np.float32)
+    x32 = np.asarray(L["link_ac"], np.float32)
+    cost = (g32 + x32).astype(np.float32).astype(np.float64)
+    lf = frame[dst] if len(dst) else np.zeros(0, np.int64)
+    within = frame[src] == lf if len(dst) else np.zeros(0, bool)
+    byf = np.argsort(lf, kind="stable")
+    lb = np.searchsorted(lf[byf], np.arange(F + 2))
+    alpha = np.full(N, INF)
+    beta = np.full(N, INF)
+    tc = np.asarray(L["tok_cost"], np.float32)
+    z = np.nonzero(tc[fb[0]:fb[1]] == 0.0)[0]
+    if len(z):
+        alpha[fb[0] + z[0]] = 0.0
+    for k in range(F + 1):
+        idx = byf[lb[k]:lb[k + 1]]
+        cr, wi = idx[~within[idx]], idx[within[idx]]
+        if len(cr):
+            np.minimum.at(alpha, dst[cr], alpha[src[cr]] + cost[cr])
+        while len(wi):
+            cand = alpha[src[wi]] + cost[wi]
+            if not (cand < alpha[dst[wi]]).any():
+                break
+            np.minimum.at(alpha, dst[wi], cand)
+    fin = L["final_cost"]
+    fc = np.zeros(fb[F + 1] - fb[F]) if len(fin) == 0 else np.asarray(fin, np.float32).astype(np.float64)
+    beta[fb[F]:fb[F + 1]] = fc
+    best = float(np.min(alpha[fb[F]:fb[F + 1]] + fc)) if fb[F + 1] > fb[F] else INF
+    for k in range(F, -1, -1):
+        idx = byf[lb[k]:lb[k + 1]]
+        cr, wi = idx[~within[idx]], idx[within[idx]]
+        while len(wi):
+            cand = cost[wi] + beta[dst[wi]]
+            if not (cand < beta[src[wi]]).any():
+                break
+            np.minimum.at(beta, src[wi], cand)
+        if len(cr):
+            np.minimum.at(beta, src[cr], cost[cr] + beta[dst[cr]])
+    keep = alpha + beta - best <= beam
+    remap = np.full(N, -1, np.int64)
+    remap[keep] = np.arange(int(keep.sum()))
+    nfb = np.zeros(F + 2, np.int64)
+    ck = np.concatenate([[0], np.cumsum(keep)])
+    nfb[:F + 2] = ck[fb[:F + 2]]
+    lk = (remap[src] >= 0) & (remap[dst] >= 0) & (alpha[src] + cost + beta[dst] - best <= beam)
+    nfin = np.asarray(fin, np.float32)[keep[fb[F]:fb[F + 1]]] if len(fin) else np.zeros(0, np.float32)
+    return dict(num_frames=F, frame_begin=nfb.astype(np.int32),
+                tok_state=np.asarray(L["tok_state"], np.int32)[keep], tok_cost=tc[keep],
+                link_src=remap[src[lk]].astype(np.int32), link_dst=remap[dst[lk]].astype(np.int32),
+                link_arc=np.asarray(L["link_arc"], np.int32)[lk], link_graph=g32[lk], link_ac=x32[lk],
+                final_cost=nfin.astype(np.float32))
+
+
+def raw_from_oracle_loop(r, graph, use_final=True):
     """Oracle decode(lattice=True) -> the arrays of vamd_stream_lattice."""
     L = r["lattice"]
     fb = L["frame_begin"]
@@ -59,7 +161,7 @@ def raw_from_oracle(r, graph, use_final=True):
 
 
 # ---------------------------------------------------------------- pruning
-def prune(L, beam):
+def prune_loop(L, beam):
     F = L["num_frames"]
     fb = L["frame_begin"]
     N = len(L["tok_state"])

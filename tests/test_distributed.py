@@ -205,11 +205,14 @@ def _batch_texts(ids):
 
 
 @pytest.mark.gpu
-def test_two_processes_of_batch_lanes_match_one(synth_model):
+def test_two_processes_of_batch_lanes_match_oracle(synth_model, test_wave):
     """bench.py's N > 1 structure on the product path: two processes (gloo
     world 2), each with its own libvosk.so BatchModel lane (both on device 0
     here, one GPU per rank on a node) decoding its shard of the streams; the
-    gathered results equal one process decoding every stream."""
+    gathered results equal the oracle's for every stream
+    (tests/batch_expect.py: segments, words and times)."""
+    import batch_expect
+    from conftest import perturbed_stream
     n = 8
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -221,12 +224,8 @@ def test_two_processes_of_batch_lanes_match_one(synth_model):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    os.environ["VOSK_BATCH_MODEL_DIR"] = synth_model
-    try:
-        one = _batch_texts(list(range(n)))
-    finally:
-        os.environ.pop("VOSK_BATCH_MODEL_DIR", None)
     assert sorted(merged) == list(range(n))
+    waves = [perturbed_stream(test_wave, 4000 + i, seconds=4.0 + 0.5 * i) for i in range(n)]
+    exp = batch_expect.expected(synth_model, waves)
     for i in range(n):
-        assert merged[i] == one[i], i
-    assert sum(len(v) for v in one.values()) >= n
+        batch_expect.check(merged[i], exp[i], f"stream {i}")

@@ -57,6 +57,20 @@ def test_cpp_pipeline_matches_restatement(synth_model, test_wave, secs, use_fina
     assert unscaled["nbest"][0]["words"] == r["words"]
 
 
+@pytest.mark.parametrize("secs,use_final", [(4, True), (6, False)])
+def test_numpy_raw_lattice_and_prune_equal_the_loop_restatement(synth_model, test_wave, secs, use_final):
+    """raw_from_oracle / prune (numpy) give exactly the arrays of their
+    link-by-link statements (raw_from_oracle_loop / prune_loop)."""
+    o, r, L = _lattice(synth_model, test_wave[:int(16000 * secs)], use_final)
+    L0 = OL.raw_from_oracle_loop(r, o.graph, use_final)
+    for k in L0:
+        np.testing.assert_array_equal(np.asarray(L[k]), np.asarray(L0[k]), err_msg=k)
+    for beam in (6.0, 2.0):
+        P, P0 = OL.prune(L, beam), OL.prune_loop(L, beam)
+        for k in P0:
+            np.testing.assert_array_equal(np.asarray(P[k]), np.asarray(P0[k]), err_msg=f"{k} beam {beam}")
+
+
 def test_pruning_keeps_best_path_and_shrinks(synth_model, test_wave):
     o, r, L = _lattice(synth_model, test_wave[:16000 * 3])
     P = OL.prune(L, 6.0)

@@ -124,6 +124,67 @@ def test_config3_256_batch_recognizers_match_oracle(synth_la_small_en_us, test_w
     assert sum(1 for e in exp for x in e if x["text"]) >= NSTREAMS
 
 
+# ------------------------------------------------- SURVEY §8d's stream shape
+def test_section8d_32_streams_of_60s_match_oracle(synth_la_small_en_us, test_wave, tmp_path, monkeypatch):
+    """§8d's workload shape: 60-s streams (stream i = test.wav tiled, shifted
+    by i * 7919, gain and N(0, 10 LSB) noise from default_rng(1234 + i)), 32
+    of them through vosk_batch_* on the bench model, fed the test_gpu_batch.py
+    way (8000-byte calls, Wait() and Result() per round, FinishStream at the
+    end).  Every result message -- the endpoint segments of the default rules
+    (20-s segments), each segment's MBR words and times after Kaldi's pruned
+    phone + word determinization -- equals the oracle chain's."""
+    import oracle_graph as OG
+    import vosk
+    from vosk import engine
+    vosk.SetLogLevel(-1)
+    n = 32
+    waves = [perturbed_stream(test_wave, i, seconds=60.0) for i in range(n)]
+    monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_la_small_en_us)
+    model = vosk.BatchModel()
+    recs = [vosk.BatchRecognizer(model, 16000) for _ in range(n)]
+    datas = [_pcm(w) for w in waves]
+    got = [[] for _ in range(n)]
+
+    def collect():
+        for i in range(n):
+            while True:
+                r = recs[i].Result()
+                if not r:
+                    break
+                got[i].append(json.loads(r))
+
+    for pos in range(0, len(datas[0]), 8000):
+        for i in range(n):
+            recs[i].AcceptWaveform(datas[i][pos:pos + 8000])
+        model.Wait()
+        collect()
+    for r in recs:
+        r.FinishStream()
+    model.Wait()
+    collect()
+    del recs
+    odir, _ = OG.expanded_hclg_model(synth_la_small_en_us, str(tmp_path / "la_hclg"))
+    _ORC.update(o=oracle_py.OracleModel(odir, fpc=51), info=engine.plan_info(synth_la_small_en_us, 51),
+                waves=waves)
+    try:
+        exp = _pool_map(_batch_expected_job, n)
+    finally:
+        _ORC.clear()
+    for i in range(n):
+        g, e = got[i], exp[i]
+        assert len(g) == len(e), (i, [r["text"] for r in g], [x["text"] for x in e])
+        for r, x in zip(g, e):
+            assert r["text"] == x["text"], i
+            ws = r.get("result", [])
+            assert len(ws) == len(x["times"]), i
+            for w, (tb, te) in zip(ws, x["times"]):
+                assert w["start"] == pytest.approx(x["start"] + tb, abs=1e-4), i
+                assert w["end"] == pytest.approx(x["start"] + te, abs=1e-4), i
+    # the default rules end segments inside every 60-s stream
+    assert all(len(e) >= 2 for e in exp)
+    assert sum(len(w["text"].split()) for e in exp for w in e) >= 20 * n
+
+
 # ---------------------------------------------------------------- config 4
 def _best_path_job(i):
     r = _ORC["o"].recognize(_ORC["waves"][i])
