@@ -1221,6 +1221,7 @@ typedef struct {
   int* bucket_rank; /* per bucket: first-occupancy rank in this frame, -1 */
   int nranks;
   size_t hash_size, bucket_cap;
+  const int* ids;   /* bucketing id per state (lazy numbering), NULL: the state */
 } khash;
 
 static void kh_reserve(khash* h, int n) {
@@ -1257,7 +1258,7 @@ static int kh_find_or_add(khash* h, int s, float tot, int bp, int arc, int* chan
     e = h->n++;
     h->where[s] = e;
     h->st[e] = s; h->cost[e] = tot; h->bp[e] = bp; h->arc[e] = arc;
-    int b = (int)((size_t)s % h->hash_size);
+    int b = (int)((size_t)(h->ids ? h->ids[s] : s) % h->hash_size);
     h->bucket[e] = b;
     if (h->bucket_rank[b] < 0) h->bucket_rank[b] = h->nranks++;
     *changed = 1;
@@ -1292,6 +1293,9 @@ void orc_kaldi_stats(long long* out, int reset) {
 
 typedef struct {
   khash h;
+  /* OpenFST lazy numbering (orc_dec_opts.lazy_next): id per state, -1 none */
+  int* disc; char* expanded; int next_id;
+  const int64_t* lazy_row; const int* lazy_next;
   int* order; int* cnt; int ocap, ccap;
   int* queue; int qcap;
   int* elem_pos;     /* element -> list position (frame being committed) */
@@ -1306,6 +1310,17 @@ static void kd_list_order(kdec* d) {
   kh_order(h, d->order, d->cnt);
 }
 
+/* the composed FST expands state s (its arcs computed): destinations
+   without an id are numbered in arc order (OpenFST's lazy numbering) */
+static void kd_expand(kdec* d, int s) {
+  if (!d->disc || d->expanded[s]) return;
+  d->expanded[s] = 1;
+  for (int64_t a = d->lazy_row[s]; a < d->lazy_row[s + 1]; a++) {
+    const int t = d->lazy_next[a];
+    if (d->disc[t] < 0) d->disc[t] = d->next_id++;
+  }
+}
+
 /* ProcessNonemitting over the frame being built */
 static void kd_nonemitting(const orc_graph* g, kdec* d, float cutoff) {
   khash* h = &d->h;
@@ -1313,6 +1328,7 @@ static void kd_nonemitting(const orc_graph* g, kdec* d, float cutoff) {
   int qn = 0;
   for (int q = 0; q < h->n; q++) {
     const int s = h->st[d->order[q]];
+    kd_expand(d, s);  /* fst_->NumInputEpsilons(state) */
     if (g->eps_begin[s] < g->arc_begin[s + 1]) {
       if (qn + 1 > d->qcap) { d->qcap = 2 * (qn + 1); d->queue = (int*)realloc(d->queue, sizeof(int) * d->qcap); }
       d->queue[qn++] = s;
@@ -1335,6 +1351,7 @@ static void kd_nonemitting(const orc_graph* g, kdec* d, float cutoff) {
         g_kstats[6]++;
         if (h->n > nb) g_kstats[7]++;
         else if (ch) g_kstats[8]++;
+        if (ch) kd_expand(d, dst);  /* (changed && fst_->NumInputEpsilons(nextstate)) */
         if (ch && g->eps_begin[dst] < g->arc_begin[dst + 1]) {
           if (qn + 1 > d->qcap) { d->qcap = 2 * (qn + 1); d->queue = (int*)realloc(d->queue, sizeof(int) * d->qcap); }
           d->queue[qn++] = dst;
@@ -1458,6 +1475,16 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
   h->st = (int*)malloc(sizeof(int) * h->cap); h->cost = (float*)malloc(sizeof(float) * h->cap);
   h->bp = (int*)malloc(sizeof(int) * h->cap); h->arc = (int*)malloc(sizeof(int) * h->cap);
   h->bucket = (int*)malloc(sizeof(int) * h->cap);
+  if (o->lazy_next) {
+    d.disc = (int*)malloc(sizeof(int) * S);
+    for (int s = 0; s < S; s++) d.disc[s] = -1;
+    d.expanded = (char*)calloc(S, 1);
+    d.lazy_row = o->lazy_row;
+    d.lazy_next = o->lazy_next;
+    d.disc[g->start] = 0;  /* ComposeFst::Start() */
+    d.next_id = 1;
+    h->ids = d.disc;
+  }
   /* a new decoder's toks_.SetSize(1000), or the size the decoder had (InitDecoding keeps it) */
   kh_set_size(h, o->hash_size > 0 ? (size_t)o->hash_size : 1000);
   d.acap = 1 << 16;
@@ -1522,6 +1549,7 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
     const float cost_offset = -best;
     {
       const int s = cur_state[best_i];
+      kd_expand(&d, s);  /* ArcIterator (expanded when created: a no-op) */
       for (int64_t a = g->arc_begin[s]; a < g->eps_begin[s]; a++) {
         const float nw = ((g->weight[a] + cost_offset) - L[g->tid2pdf[g->ilabel[a]]]) + best;
         if (nw + adaptive < next_cutoff) next_cutoff = nw + adaptive;
@@ -1568,7 +1596,7 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
   if (end >= 0) r->best_cost = (double)r->best_tot - offsets_sum;
   free(h->where); free(h->st); free(h->cost); free(h->bp); free(h->arc); free(h->bucket); free(h->bucket_rank);
   free(d.a_prev); free(d.a_arc); free(d.cur_state); free(d.cur_cost); free(d.cur_idx); free(d.order);
-  free(d.cnt); free(d.queue); free(d.elem_pos); free(tmp);
+  free(d.cnt); free(d.queue); free(d.elem_pos); free(tmp); free(d.disc); free(d.expanded);
   return end >= 0 ? 0 : -1;
 }
 

@@ -155,6 +155,18 @@ typedef struct {
   float beam, beam_delta;
   int max_active, min_active;
   int hash_size;  /* orc_decode_kaldi: the HashList size at the start (0: a new decoder's 1000) */
+  /* orc_decode_kaldi, optional (NULL: state ids as numbered in the graph):
+     OpenFST's lazy ComposeFst numbering.  The graph's states are renumbered
+     for HashList bucketing as the decoder first expands them: the start is
+     0, and a state's arc destinations without an id take the next ids in
+     the order of the state's arcs, lazy_next[lazy_row[s] .. lazy_row[s+1])
+     (the composed FST's own arc order, emitting and epsilon arcs
+     interleaved).  Kaldi's decoder expands a state when it first iterates
+     its arcs or asks NumInputEpsilons (ProcessNonemitting's queue fill over
+     every new token in list order, then each token the queue creates or
+     improves). */
+  const int64_t* lazy_row;
+  const int* lazy_next;
 } orc_dec_opts;
 
 typedef struct {

@@ -542,7 +542,8 @@ def decoder_order(batch=False):
 
 class OrcDecOpts(C.Structure):
     _fields_ = [("beam", C.c_float), ("beam_delta", C.c_float), ("max_active", C.c_int),
-                ("min_active", C.c_int), ("hash_size", C.c_int)]
+                ("min_active", C.c_int), ("hash_size", C.c_int), ("lazy_row", C.c_void_p),
+                ("lazy_next", C.c_void_p)]
 
 
 class OrcDecResult(C.Structure):
@@ -587,7 +588,7 @@ class OracleGraph:
 
     def decode(self, llh: np.ndarray, beam=13.0, max_active=7000, min_active=200,
                beam_delta=0.5, use_final=True, lattice=False, kaldi=None, hash_size=0, probes=None,
-               lattice_caps=None):
+               lattice_caps=None, lazy=None):
         """kaldi=True: the Kaldi-sequential restatement (orc_decode_kaldi:
         HashList order, running emitting cutoff, LIFO epsilon queue), the
         GPU decoder's default; False: the order-independent form (the GPU's
@@ -596,7 +597,10 @@ class OracleGraph:
         starts with (0: a new decoder); out["hash_size"] is its size at the end.
         probes: ascending frame counts; out["probes"] is a
         list of (path without final costs, final relative cost) after each,
-        from the same single pass (the endpoint checks of a segment)."""
+        from the same single pass (the endpoint checks of a segment).
+        lazy: (row, nextstate) of the graph in its own arc order -- Kaldi
+        order buckets by OpenFST's lazy ComposeFst numbering (orc_dec_opts
+        lazy_row / lazy_next) instead of the graph's state ids."""
         if kaldi is None:
             kaldi = decoder_order() == "kaldi"
         llh = np.ascontiguousarray(llh, np.float32)
@@ -634,6 +638,10 @@ class OracleGraph:
             res.probe_path, res.probe_path_cap = ppath.ctypes.data, pcap
             res.probe_off, res.probe_frc = poff.ctypes.data, pfrc.ctypes.data
         o = OrcDecOpts(beam, beam_delta, max_active, min_active, int(hash_size))
+        if lazy is not None:
+            lrow = np.ascontiguousarray(lazy[0], np.int64)
+            lnext = np.ascontiguousarray(lazy[1], np.int32)
+            o.lazy_row, o.lazy_next = lrow.ctypes.data, lnext.ctypes.data
         fn = lib().orc_decode_kaldi if kaldi else lib().orc_decode
         rc = fn(C.byref(self.g), llh.ctypes.data_as(C.c_void_p), C.c_int(F),
                               C.c_int(llh.shape[1]), C.byref(o), C.c_int(int(use_final)),

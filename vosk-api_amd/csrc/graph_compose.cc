@@ -657,6 +657,13 @@ void ComposeLookahead(const HostFst& a, const HostFst& b, const std::vector<int>
   }
   VAMD_LOG("Composed lookahead graph: " << c.NumStates() << " states, " << c.NumArcs() << " arcs expanded");
   auto t2 = std::chrono::steady_clock::now();
+  if (getenv("VOSK_AMD_GRAPH_RAW")) {
+    // measurement hook (tools/numbering_discovery.py): the composition as
+    // OpenFST's ComposeFst holds it -- untrimmed, its own arc order, states
+    // numbered in expansion order -- instead of the decoding graph
+    *out = std::move(c);
+    return;
+  }
   ConnectCanonical(c, out);
   auto t3 = std::chrono::steady_clock::now();
   VAMD_LOG_VERBOSE("compose timing: reach " << std::chrono::duration<double>(t1 - t0).count() << " s, expand " << std::chrono::duration<double>(t2 - t1).count() << " s, connect " << std::chrono::duration<double>(t3 - t2).count() << " s");
