@@ -142,7 +142,7 @@ def oracle_model_dir(model):
         return model
     import oracle_graph as OG
     out = model.rstrip("/") + "_oracle_hclg"
-    if not os.path.exists(os.path.join(out, "graph", "HCLG.fst")):
+    if not os.path.exists(os.path.join(out, "graph", "lazy_ids.npz")):
         OG.expanded_hclg_model(model, out + ".tmp")
         os.rename(out + ".tmp", out)
     return out

@@ -47,6 +47,11 @@ void *vamd_graph_new(const char *model_dir, const char *grammar);
 int vamd_graph_dims(void *graph, int *start, long long *num_arcs);
 int vamd_graph_copy(void *graph, float *final_cost, long long *arc_begin, int *ilabel, int *olabel,
                     float *weight, int *nextstate);
+/* OpenFST's lazy ComposeFst numbering of a composed (lookahead) graph: per
+ * state its arc destinations in the composition's own arc order, as ids
+ * [0, ids) (the graph's states, then states the trim dropped).  Returns ids
+ * (0: not a composed graph); fills row [S+1] and next [row[S]] when non-NULL. */
+int vamd_graph_lazy(void *graph, long long *row, int *next);
 void vamd_graph_free(void *graph);
 
 /* speaker x-vector of a sample sequence (the GPU path GetSpkVector uses,

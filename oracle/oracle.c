@@ -1475,14 +1475,26 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
   h->st = (int*)malloc(sizeof(int) * h->cap); h->cost = (float*)malloc(sizeof(float) * h->cap);
   h->bp = (int*)malloc(sizeof(int) * h->cap); h->arc = (int*)malloc(sizeof(int) * h->cap);
   h->bucket = (int*)malloc(sizeof(int) * h->cap);
+  const int own_lazy = o->lazy_next && !o->lazy_disc;
   if (o->lazy_next) {
-    d.disc = (int*)malloc(sizeof(int) * S);
-    for (int s = 0; s < S; s++) d.disc[s] = -1;
-    d.expanded = (char*)calloc(S, 1);
+    const int64_t nids_max = S + (o->lazy_row[S] > 0 ? o->lazy_row[S] : 0);  /* (dead ids < S + arcs) */
+    if (own_lazy) {
+      d.disc = (int*)malloc(sizeof(int) * nids_max);
+      d.expanded = (char*)malloc(S);
+    } else {
+      d.disc = o->lazy_disc;
+      d.expanded = o->lazy_expanded;
+    }
     d.lazy_row = o->lazy_row;
     d.lazy_next = o->lazy_next;
-    d.disc[g->start] = 0;  /* ComposeFst::Start() */
-    d.next_id = 1;
+    if (own_lazy || *o->lazy_count <= 0) {
+      for (int64_t s = 0; s < nids_max; s++) d.disc[s] = -1;
+      memset(d.expanded, 0, S);
+      d.disc[g->start] = 0;  /* ComposeFst::Start() */
+      d.next_id = 1;
+    } else {
+      d.next_id = *o->lazy_count;
+    }
     h->ids = d.disc;
   }
   /* a new decoder's toks_.SetSize(1000), or the size the decoder had (InitDecoding keeps it) */
@@ -1596,7 +1608,9 @@ int orc_decode_kaldi(const orc_graph* g, const float* llh, int F, int stride, co
   if (end >= 0) r->best_cost = (double)r->best_tot - offsets_sum;
   free(h->where); free(h->st); free(h->cost); free(h->bp); free(h->arc); free(h->bucket); free(h->bucket_rank);
   free(d.a_prev); free(d.a_arc); free(d.cur_state); free(d.cur_cost); free(d.cur_idx); free(d.order);
-  free(d.cnt); free(d.queue); free(d.elem_pos); free(tmp); free(d.disc); free(d.expanded);
+  free(d.cnt); free(d.queue); free(d.elem_pos); free(tmp);
+  if (own_lazy) { free(d.disc); free(d.expanded); }
+  else if (o->lazy_next) *o->lazy_count = d.next_id;
   return end >= 0 ? 0 : -1;
 }
 

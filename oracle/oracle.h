@@ -167,6 +167,13 @@ typedef struct {
      improves). */
   const int64_t* lazy_row;
   const int* lazy_next;
+  /* optional with lazy_next: the numbering state carried across decodes (a
+     recognizer's ComposeFst outlives its decoder's InitDecoding): ids
+     [lazy_ids], expanded flags [states], the next id (0: start fresh);
+     updated in place.  NULL: a fresh numbering for this decode. */
+  int* lazy_disc;
+  char* lazy_expanded;
+  int* lazy_count;
 } orc_dec_opts;
 
 typedef struct {

@@ -22,10 +22,12 @@ def expected(model_dir, waves):
     out = []
     for w in waves:
         llh = o.loglikes(w)
-        segs = OE.batch_segments_fast(o, w, llh, info["right_context"], info["priming"], kaldi=kaldi)
+        states = []  # the stream's lazy numbering at each segment's start
+        segs = OE.batch_segments_fast(o, w, llh, info["right_context"], info["priming"], kaldi=kaldi,
+                                      lazy_states=states)
         res = []
-        for s0, s1 in segs:
-            mb = OL.results(o, llh[s0:s1], kaldi=kaldi)["mbr"]
+        for (s0, s1), ls in zip(segs, states):
+            mb = OL.results(o, llh[s0:s1], kaldi=kaldi, lazy_state=ls)["mbr"]
             res.append(dict(text=" ".join(o.words[x] for x in mb["words"]), start=s0 * 0.03,
                             times=[(np.floor(a + 0.5) * 0.03, np.floor(b + 0.5) * 0.03) for a, b in mb["times"]]))
         out.append(res)

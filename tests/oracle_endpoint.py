@@ -122,26 +122,35 @@ def _chunk_checks(oracle, N, right_context, priming, spc):
     return checks, -(-T // fss)
 
 
-def batch_segments_fast(oracle, wave, llh, right_context, priming, spc=8160, kaldi=False):
+def batch_segments_fast(oracle, wave, llh, right_context, priming, spc=8160, kaldi=False, lazy_states=None):
     """batch_segments with one decoding pass per segment: the segment's
     decoder is probed at every later chunk check (orc_decode_kaldi endpoint
     probes: the state after n frames does not depend on the frames after
     them), and ends at the first probe whose rules fire.  Same result as
     batch_segments (tests/test_oracle.py), linear instead of quadratic in the
-    stream length."""
+    stream length.  On a graph with OpenFST's lazy numbering (Kaldi order)
+    the stream's numbering carries from segment to segment (the stream's
+    ComposeFst outlives its decoder resets; the GPU keeps it per slot):
+    lazy_states, a list, receives the numbering at each segment's start."""
     rules, sil = endpoint_config(oracle.model_conf)
     shift = F32(F32(0.01) * F32(oracle.fss))
     min_len = min(r[3] for r in rules)
     g = oracle.graph
+    import oracle_py
+    lazy_on = kaldi and g.lazy is not None and __import__("os").environ.get("VOSK_AMD_LAZY_IDS", "1") != "0"
+    ls = oracle_py.LazyState(g) if lazy_on else None
     checks, end = _chunk_checks(oracle, len(wave), right_context, priming, spc)
     seg0, segs, k = 0, [], 0
     while True:
+        if lazy_states is not None:
+            lazy_states.append(ls.copy() if ls is not None else None)
         cand = [(i, x) for i, x in enumerate(checks) if i >= k and x - seg0 > 0 and F32(x - seg0) * shift >= min_len]
         if not cand:
             break
         last = max(x for _, x in cand)
         r = g.decode(llh[seg0:last], oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
-                     use_final=False, kaldi=kaldi, probes=[x - seg0 for _, x in cand])
+                     use_final=False, kaldi=kaldi, probes=[x - seg0 for _, x in cand],
+                     lazy_state=ls.copy() if ls is not None else None)
         fired = None
         for (i, x), (path, frc) in zip(cand, r["probes"]):
             ts = trailing_silence(path, g.ilabel, oracle.tm.tid2phone, sil)
@@ -151,6 +160,11 @@ def batch_segments_fast(oracle, wave, llh, right_context, priming, spc=8160, kal
         if fired is None:
             break
         segs.append((seg0, fired[1]))
+        if ls is not None:  # the numbering after the segment's frames
+            g.decode(llh[seg0:fired[1]], oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
+                     use_final=False, kaldi=kaldi, lazy_state=ls)
         seg0, k = fired[1], fired[0] + 1
     segs.append((seg0, end))
+    if lazy_states is not None:
+        del lazy_states[len(segs):]
     return segs

@@ -317,8 +317,33 @@ def connect_canonical(f: kf.Fst) -> kf.Fst:
             il.append(int(f.ilabel[a])); ol.append(int(f.olabel[a])); wt.append(f.weight[a]); nx.append(nid[d])
         rows.append(len(il))
         i += 1
-    return kf.Fst(0, np.array(finals, np.float32), np.array(rows, np.int64), np.array(il, np.int32),
-                  np.array(ol, np.int32), np.array(wt, np.float32), np.array(nx, np.int32))
+    out = kf.Fst(0, np.array(finals, np.float32), np.array(rows, np.int64), np.array(il, np.int32),
+                 np.array(ol, np.int32), np.array(wt, np.float32), np.array(nx, np.int32))
+    # OpenFST's lazy numbering (graph_compose.cc ConnectCanonical): per state
+    # its destinations in the composition's own arc order, states the trim
+    # dropped numbered past the graph's
+    NS = len(order)
+    dead, lrow, lnext = {}, [0], []
+    for s in order:
+        for a in range(int(f.row[s]), int(f.row[s + 1])):
+            d = int(f.nextstate[a])
+            if d in nid:
+                lnext.append(nid[d])
+            else:
+                if d not in dead:
+                    dead[d] = NS + len(dead)
+                lnext.append(dead[d])
+        lrow.append(len(lnext))
+    out.lazy = (np.array(lrow, np.int64), np.array(lnext, np.int32), NS + len(dead))
+    return out
+
+
+def write_lazy(out_dir, lazy):
+    """graph/lazy_ids.npz next to an expanded graph/HCLG.fst: the oracle then
+    buckets Kaldi's HashList by OpenFST's lazy ids (oracle_py.OracleGraph)."""
+    row, nxt, ids = lazy
+    if ids:
+        np.savez(os.path.join(out_dir, "graph", "lazy_ids.npz"), row=row, next=nxt, ids=np.int64(ids))
 
 
 def estimate_grammar_lm(sentences, order=2, discount=0.5) -> kf.Fst:
@@ -490,8 +515,35 @@ def write_hclg_model(src_dir, out_dir, grammar=None):
     if os.path.exists(out_dir):
         shutil.rmtree(out_dir)
     shutil.copytree(src_dir, out_dir, ignore=shutil.ignore_patterns("HCLr.fst", "Gr.fst", "disambig_tid.int"))
-    kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), model_graph(src_dir, grammar))
+    g = model_graph(src_dir, grammar)
+    kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), g)
+    write_lazy(out_dir, g.lazy)
     return out_dir
+
+
+def lazy_csr(model_dir):
+    """libvosk's OpenFST lazy-numbering CSR of a lookahead model's composed
+    graph (vamd_graph_lazy): (row [S+1] int64, next int32, ids) -- per state
+    of the decoding graph, its arc destinations in the composition's own arc
+    order."""
+    import ctypes as C
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "vosk-api_amd", "vosk",
+                              "libvosk.so"))
+    lib.vamd_graph_new.restype = C.c_void_p
+    lib.vamd_graph_new.argtypes = [C.c_char_p, C.c_char_p]
+    lib.vamd_graph_dims.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]
+    lib.vamd_graph_lazy.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.vamd_graph_free.argtypes = [C.c_void_p]
+    h = lib.vamd_graph_new(model_dir.encode(), None)
+    assert h
+    st, na = C.c_int(), C.c_longlong()
+    S = lib.vamd_graph_dims(h, C.byref(st), C.byref(na))
+    row = np.zeros(S + 1, np.int64)
+    ids = lib.vamd_graph_lazy(h, row.ctypes.data, None)
+    nxt = np.zeros(int(row[-1]), np.int32)
+    lib.vamd_graph_lazy(h, row.ctypes.data, nxt.ctypes.data)
+    lib.vamd_graph_free(h)
+    return row, nxt, ids
 
 
 def expanded_hclg_model(model_dir, out_dir):
@@ -517,9 +569,16 @@ def expanded_hclg_model(model_dir, out_dir):
                np.zeros(A, np.int32), np.zeros(A, np.float32), np.zeros(A, np.int32))
     lib.vamd_graph_copy(h, g.final.ctypes.data, g.row.ctypes.data, g.ilabel.ctypes.data,
                         g.olabel.ctypes.data, g.weight.ctypes.data, g.nextstate.ctypes.data)
+    lib.vamd_graph_lazy.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lrow = np.zeros(S + 1, np.int64)
+    ids = lib.vamd_graph_lazy(h, lrow.ctypes.data, None)
+    lnext = np.zeros(int(lrow[-1]) if ids else 0, np.int32)
+    if ids:
+        lib.vamd_graph_lazy(h, lrow.ctypes.data, lnext.ctypes.data)
     lib.vamd_graph_free(h)
     if os.path.exists(out_dir):
         shutil.rmtree(out_dir)
     shutil.copytree(model_dir, out_dir, ignore=shutil.ignore_patterns("HCLr.fst", "Gr.fst", "disambig_tid.int"))
     kf.write_const_fst(os.path.join(out_dir, "graph", "HCLG.fst"), g)
+    write_lazy(out_dir, (lrow, lnext, ids))
     return out_dir, S

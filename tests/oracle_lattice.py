@@ -1280,15 +1280,18 @@ def word_align(W, Fi, tables):
     return A, F
 
 
-def results(oracle, llh, use_final=True, graph_scale=0.9, nbest_n=0, rescore=None, hash_size=0, kaldi=None):
+def results(oracle, llh, use_final=True, graph_scale=0.9, nbest_n=0, rescore=None, hash_size=0, kaldi=None,
+            lazy_state=None):
     """The reference's result chain over the oracle decoder's lattice of
     `llh`: prune, determinize, graph scale, word alignment (when the model has
     word_boundary.int), then MBR (and n-best).  hash_size: the decoder's
     HashList size at the segment start (Kaldi order; 0 = a new decoder).
-    kaldi: the decoder order (None: oracle_py.decoder_order())."""
+    kaldi: the decoder order (None: oracle_py.decoder_order()).  lazy_state:
+    the stream's OpenFST lazy numbering at the segment start
+    (oracle_py.LazyState, updated in place; None: a fresh one)."""
     import os
     r = oracle.graph.decode(llh, oracle.beam, oracle.max_active, oracle.min_active, oracle.beam_delta,
-                            use_final, lattice=True, hash_size=hash_size, kaldi=kaldi)
+                            use_final, lattice=True, hash_size=hash_size, kaldi=kaldi, lazy_state=lazy_state)
     W, Fi = determinize_phone(prune(raw_from_oracle(r, oracle.graph, use_final), 6.0),
                               oracle.graph.ilabel, oracle.graph.olabel, oracle.tm.tid2phone,
                               tid_first(oracle.tm))

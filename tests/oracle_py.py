@@ -543,7 +543,25 @@ def decoder_order(batch=False):
 class OrcDecOpts(C.Structure):
     _fields_ = [("beam", C.c_float), ("beam_delta", C.c_float), ("max_active", C.c_int),
                 ("min_active", C.c_int), ("hash_size", C.c_int), ("lazy_row", C.c_void_p),
-                ("lazy_next", C.c_void_p)]
+                ("lazy_next", C.c_void_p), ("lazy_disc", C.c_void_p), ("lazy_expanded", C.c_void_p),
+                ("lazy_count", C.c_void_p)]
+
+
+class LazyState:
+    """OpenFST's lazy numbering carried across decodes of one stream (a
+    recognizer's ComposeFst outlives its decoder's InitDecoding; the GPU keeps
+    it per stream slot): ids, expanded flags, next id (0: not started)."""
+
+    def __init__(self, graph):
+        row = graph.lazy[0]
+        self.disc = np.full(graph.num_states + int(row[-1]), -1, np.int32)
+        self.exp = np.zeros(graph.num_states, np.int8)
+        self.count = np.zeros(1, np.int32)
+
+    def copy(self):
+        c = LazyState.__new__(LazyState)
+        c.disc, c.exp, c.count = self.disc.copy(), self.exp.copy(), self.count.copy()
+        return c
 
 
 class OrcDecResult(C.Structure):
@@ -581,6 +599,7 @@ class OracleGraph:
         self.tid2pdf = np.ascontiguousarray(tid2pdf, np.int32)
         self.start = fst.start
         self.num_states = S
+        self.lazy = None  # OpenFST lazy numbering table (OracleModel loads graph/lazy_ids.npz)
         self.g = OrcGraph(S, fst.start, self.arc_begin.ctypes.data, self.eps_begin.ctypes.data,
                           self.ilabel.ctypes.data, self.olabel.ctypes.data,
                           self.nextstate.ctypes.data, self.weight.ctypes.data,
@@ -588,7 +607,7 @@ class OracleGraph:
 
     def decode(self, llh: np.ndarray, beam=13.0, max_active=7000, min_active=200,
                beam_delta=0.5, use_final=True, lattice=False, kaldi=None, hash_size=0, probes=None,
-               lattice_caps=None, lazy=None):
+               lattice_caps=None, lazy="auto", lazy_state=None):
         """kaldi=True: the Kaldi-sequential restatement (orc_decode_kaldi:
         HashList order, running emitting cutoff, LIFO epsilon queue), the
         GPU decoder's default; False: the order-independent form (the GPU's
@@ -600,7 +619,15 @@ class OracleGraph:
         from the same single pass (the endpoint checks of a segment).
         lazy: (row, nextstate) of the graph in its own arc order -- Kaldi
         order buckets by OpenFST's lazy ComposeFst numbering (orc_dec_opts
-        lazy_row / lazy_next) instead of the graph's state ids."""
+        lazy_row / lazy_next) instead of the graph's state ids; "auto": the
+        graph's own lazy table (graph/lazy_ids.npz of an expanded lookahead
+        model, as the GPU decoder uses by default; VOSK_AMD_LAZY_IDS=0
+        turns both off), None: off."""
+        if isinstance(lazy, str):
+            off = os.environ.get("VOSK_AMD_LAZY_IDS", "1").strip() == "0"
+            lazy = None if off else self.lazy
+        # lazy_state: a LazyState updated in place (the numbering carried
+        # from the stream's earlier decodes), None: a fresh numbering
         if kaldi is None:
             kaldi = decoder_order() == "kaldi"
         llh = np.ascontiguousarray(llh, np.float32)
@@ -642,6 +669,11 @@ class OracleGraph:
             lrow = np.ascontiguousarray(lazy[0], np.int64)
             lnext = np.ascontiguousarray(lazy[1], np.int32)
             o.lazy_row, o.lazy_next = lrow.ctypes.data, lnext.ctypes.data
+            if lazy_state is not None and kaldi:
+                o.lazy_disc = lazy_state.disc.ctypes.data
+                o.lazy_expanded = lazy_state.exp.ctypes.data
+                o.lazy_count = lazy_state.count.ctypes.data
+        ls0 = lazy_state.copy() if (lazy_state is not None and lattice) else None
         fn = lib().orc_decode_kaldi if kaldi else lib().orc_decode
         rc = fn(C.byref(self.g), llh.ctypes.data_as(C.c_void_p), C.c_int(F),
                               C.c_int(llh.shape[1]), C.byref(o), C.c_int(int(use_final)),
@@ -657,8 +689,11 @@ class OracleGraph:
             out["probes"] = [(ppath[poff[i]:poff[i + 1]].copy(), float(pfrc[i])) for i in range(len(pf))]
         if lattice and (res.lat_ntok > res.lat_tok_cap or res.lat_nlink > res.lat_link_cap):
             # the counts past the capacities are exact: decode again with room
+            if ls0 is not None:  # the numbering as it was before this attempt
+                lazy_state.disc[:], lazy_state.exp[:], lazy_state.count[:] = ls0.disc, ls0.exp, ls0.count
             return self.decode(llh, beam, max_active, min_active, beam_delta, use_final, lattice, kaldi,
-                               hash_size, probes, lattice_caps=(res.lat_ntok + 1, res.lat_nlink + 1))
+                               hash_size, probes, lattice_caps=(res.lat_ntok + 1, res.lat_nlink + 1),
+                               lazy=lazy, lazy_state=lazy_state)
         if lattice:
             nt, nl = res.lat_ntok, res.lat_nlink
             out["lattice"] = dict(
@@ -698,6 +733,10 @@ class OracleModel:
         self.beam_delta = float(mc.get("beam-delta", 0.5))
         self.net = OracleNet(self.nn, self.acoustic_scale, self.fss)
         self.graph = OracleGraph(self.fst, self.tm.tid2pdf)
+        lz = os.path.join(model_dir, "graph", "lazy_ids.npz")
+        if os.path.exists(lz):  # an expanded lookahead model (oracle_graph.write_lazy)
+            with np.load(lz) as z:
+                self.graph.lazy = (np.ascontiguousarray(z["row"], np.int64), np.ascontiguousarray(z["next"], np.int32))
         fpc = int(fpc or mc.get("frames-per-chunk", 20))
         self.fpc = fpc + (-fpc) % self.fss
         idir = os.path.join(model_dir, "ivector")

@@ -32,14 +32,14 @@ _ORC = {}
 def _orc_job(i):
     o = _ORC["o"]
     r = o.graph.decode(_ORC["llh"][i], o.beam, o.max_active, o.min_active, o.beam_delta, True,
-                       kaldi=_ORC["kaldi"])
+                       kaldi=_ORC["kaldi"], lazy=_ORC["lazy"])
     return dict(ntok=r["ntok"], best=r["best"], cutoff=r["cutoff"], next_cutoff=r["next_cutoff"],
                 path=r["path"], cost=r["best_cost"])
 
 
-def _oracle(oracle_dir, llhs, kaldi=True):
+def _oracle(oracle_dir, llhs, kaldi=True, lazy=None):
     o = oracle_py.OracleModel(oracle_dir, fpc=51)
-    _ORC.update(o=o, llh=llhs, kaldi=kaldi)
+    _ORC.update(o=o, llh=llhs, kaldi=kaldi, lazy=lazy)
     workers = max(1, min(16, len(os.sched_getaffinity(0))))
     with mp.get_context("fork").Pool(workers) as pool:
         res = pool.map(_orc_job, range(len(llhs)), chunksize=1)
@@ -103,15 +103,39 @@ def test_flat_model_64_streams(flat_model, test_wave, monkeypatch):
 
 
 def test_lookahead_model_64_streams(synth_la_small_en_us, test_wave, monkeypatch):
+    """The same with the static graph's own ids (VOSK_AMD_LAZY_IDS=0)."""
     import oracle_graph as OG
     monkeypatch.delenv("VOSK_AMD_DEC_ORDER", raising=False)
+    monkeypatch.setenv("VOSK_AMD_LAZY_IDS", "0")
     waves = [perturbed_stream(test_wave, 5000 + i, seconds=4.0 + 0.05 * i) for i in range(NSTREAMS)]
     gpu = _gpu(synth_la_small_en_us, waves)
     out = synth_la_small_en_us.rstrip("/") + "_oracle_hclg"
-    if not os.path.exists(os.path.join(out, "graph", "HCLG.fst")):
+    if not os.path.exists(os.path.join(out, "graph", "lazy_ids.npz")):
         OG.expanded_hclg_model(synth_la_small_en_us, out + ".tmp")
         os.rename(out + ".tmp", out)
     ref, max_active = _oracle(out, [g["llh"] for g in gpu])
+    _compare(gpu, ref, max_active)
+
+
+def test_lookahead_model_lazy_numbering_64_streams(synth_la_small_en_us, test_wave, monkeypatch):
+    """OpenFST's lazy ComposeFst numbering (src/recognizer.cc:31-37):
+    the GPU buckets its HashList by the ids OpenFST would give the composed
+    states as the decoder expands them (libvosk's lazy CSR, vamd_graph_lazy);
+    the oracle decodes the same graph with the same CSR (oracle.c kd_expand;
+    that this equals decoding the untrimmed composition in its own arc order
+    is tests/test_lazy_numbering.py)."""
+    import oracle_graph as OG
+    monkeypatch.delenv("VOSK_AMD_DEC_ORDER", raising=False)
+    monkeypatch.delenv("VOSK_AMD_LAZY_IDS", raising=False)
+    waves = [perturbed_stream(test_wave, 5000 + i, seconds=4.0 + 0.05 * i) for i in range(NSTREAMS)]
+    gpu = _gpu(synth_la_small_en_us, waves)
+    out = synth_la_small_en_us.rstrip("/") + "_oracle_hclg"
+    if not os.path.exists(os.path.join(out, "graph", "lazy_ids.npz")):
+        OG.expanded_hclg_model(synth_la_small_en_us, out + ".tmp")
+        os.rename(out + ".tmp", out)
+    row, nxt, ids = OG.lazy_csr(synth_la_small_en_us)
+    assert ids > 0
+    ref, max_active = _oracle(out, [g["llh"] for g in gpu], lazy=(row, nxt))
     _compare(gpu, ref, max_active)
 
 

@@ -45,12 +45,23 @@ def _cgraph(lib, model, grammar=None):
                  np.zeros(A, np.int32), np.zeros(A, np.float32), np.zeros(A, np.int32))
     lib.vamd_graph_copy(h, out.final.ctypes.data, out.row.ctypes.data, out.ilabel.ctypes.data,
                         out.olabel.ctypes.data, out.weight.ctypes.data, out.nextstate.ctypes.data)
+    # OpenFST's lazy numbering table (vamd_graph_lazy)
+    lib.vamd_graph_lazy.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lrow = np.zeros(S + 1, np.int64)
+    ids = lib.vamd_graph_lazy(h, lrow.ctypes.data, None)
+    lnext = np.zeros(int(lrow[-1]), np.int32)
+    lib.vamd_graph_lazy(h, lrow.ctypes.data, lnext.ctypes.data)
+    out.lazy = (lrow, lnext, ids)
     lib.vamd_graph_free(h)
     return out
 
 
 def _assert_same_fst(a, b):
     assert a.start == b.start
+    if hasattr(a, "lazy") and hasattr(b, "lazy"):  # the lazy numbering tables
+        np.testing.assert_array_equal(a.lazy[0], b.lazy[0])
+        np.testing.assert_array_equal(a.lazy[1], b.lazy[1])
+        assert a.lazy[2] == b.lazy[2] and a.lazy[2] >= a.num_states
     np.testing.assert_array_equal(a.row, b.row)
     np.testing.assert_array_equal(a.ilabel, b.ilabel)
     np.testing.assert_array_equal(a.olabel, b.olabel)

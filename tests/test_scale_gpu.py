@@ -51,8 +51,10 @@ def _batch_expected_job(i):
     llh = o.loglikes(w)
     kaldi = oracle_py.decoder_order(batch=True) == "kaldi"
     out = []
-    for s0, s1 in OE.batch_segments_fast(o, w, llh, info["right_context"], info["priming"], kaldi=kaldi):
-        mb = OL.results(o, llh[s0:s1], kaldi=kaldi)["mbr"]
+    states = []  # the stream's lazy numbering at each segment's start
+    segs = OE.batch_segments_fast(o, w, llh, info["right_context"], info["priming"], kaldi=kaldi, lazy_states=states)
+    for (s0, s1), ls in zip(segs, states):
+        mb = OL.results(o, llh[s0:s1], kaldi=kaldi, lazy_state=ls)["mbr"]
         out.append(dict(text=" ".join(o.words[x] for x in mb["words"]), start=s0 * 0.03,
                         times=[(np.floor(a + 0.5) * 0.03, np.floor(b + 0.5) * 0.03) for a, b in mb["times"]]))
     return out

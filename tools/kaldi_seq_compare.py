@@ -57,7 +57,7 @@ def model_dir(name):
             make_synth_model.make_preset(name, path + ".tmp")
             os.rename(path + ".tmp", path)
         out = path + "_oracle_hclg"
-        if not os.path.exists(os.path.join(out, "graph", "HCLG.fst")):
+        if not os.path.exists(os.path.join(out, "graph", "lazy_ids.npz")):
             OG.expanded_hclg_model(path, out + ".tmp")
             os.rename(out + ".tmp", out)
         return out

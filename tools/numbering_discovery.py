@@ -82,7 +82,7 @@ def main():
     out_json = sys.argv[3] if len(sys.argv) > 3 else ""
     model = conftest._make_preset("la_small_en_us")
     canon = model.rstrip("/") + "_oracle_hclg"
-    if not os.path.exists(os.path.join(canon, "graph", "HCLG.fst")):
+    if not os.path.exists(os.path.join(canon, "graph", "lazy_ids.npz")):
         OG.expanded_hclg_model(model, canon + ".tmp")
         os.rename(canon + ".tmp", canon)
     raw = model.rstrip("/") + "_oracle_raw"

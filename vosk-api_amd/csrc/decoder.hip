@@ -114,6 +114,7 @@ struct DecShared {
   unsigned long long kls[4 * DW];
   int ksum_w[2][DW];
   int kn0, kne;
+  int klazy_ne;  // lazy numbering: the frame's tokens created by the emitting pass
   int kpop_sum, kpop_max;  // component replay: pops over all lanes / on the longest lane
   int kcomp_n, kcomp_max;  // component replay: components / pops of the largest (profile)
   int karc_sum, karc_max, khbm_pops;  // wave replay: arcs iterated (all waves / the busiest), pops of HBM members
@@ -1036,6 +1037,13 @@ __device__ __forceinline__ int kaldi_excl_sum(DecShared& sh, int v, int par, int
 
 // the epsilon queue's HBM member records (kaldi_nonemitting), ints per record
 constexpr int kKMRec = 8;
+
+// a state's HashList bucket: its id % khash -- OpenFST's lazy id on a
+// composed graph (DecArgs::lazy_id), else the graph's
+__device__ __forceinline__ int kbucket(const DecArgs& a, int slot, int state, int khash) {
+  const int id = a.lazy_id ? AG_LD(&a.lazy_id[(long long)slot * a.lazy_ids + state]) : state;
+  return (int)((unsigned)id % (unsigned)khash);
+}
 // HashList bookkeeping loops: creation indices per thread in flight together
 constexpr int kHlU = 4;
 
@@ -1366,6 +1374,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     sh.n_front = 0;
     sh.kn0 = 0;
     sh.kne = 0;
+    sh.klazy_ne = ne;
   }
   __syncthreads();
   // kHlU creation indices per thread at a time, each step's loads (slot,
@@ -1383,7 +1392,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     for (int u = 0; u < kHlU; u++) {
       const int c = c0 + u * DT + (int)threadIdx.x;
       if (c >= ne) continue;
-      b[u] = (int)((unsigned)slot_state(t, T, v[u]) % (unsigned)khash);
+      b[u] = kbucket(a, slot, slot_state(t, T, v[u]), khash);
       key[u] = slot_key(t, T, v[u]);
       eps[u] = v[u] >= 0 ? (t.hp[v[u]] & kPosEps) != 0 : (AG_LD(&T.pos[~v[u]]) & kHPosEps) != 0;
     }
@@ -1425,7 +1434,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   if (n_eps <= 1) {  // the creation order is the closure's (none or one)
     if (n_eps == 1 && threadIdx.x == 0) {
       const int v = nl_n > nl_e ? (int)t.nl[nl_e] : ~AG_LD(&T.list[ng_e]);
-      const int b = (int)((unsigned)slot_state(t, T, v) % (unsigned)khash);
+      const int b = kbucket(a, slot, slot_state(t, T, v), khash);
       AG_ST(&KO[ne], v);
       AG_ST(&KB[ne], b);
       if (AG_LD(&BF[b]) > ne) AG_ST(&BF[b], ne);
@@ -2282,7 +2291,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     if (o < 0 || o >= n_eps) continue;
     const int c = ne + o;
     const int v = km_get(K, KM, i, kMSlot);
-    const int b = (int)((unsigned)slot_state(t, T, v) % (unsigned)khash);
+    const int b = kbucket(a, slot, slot_state(t, T, v), khash);
     AG_ST(&KO[c], v);
     AG_ST(&KB[c], b);
     __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2393,6 +2402,163 @@ __device__ __forceinline__ void kaldi_positions(const DecArgs& a, DecShared& sh,
   __syncthreads();
   pr.count(44, sh.kk);
   pr.mark(43);
+}
+
+// OpenFST's lazy ComposeFst numbering, in two parts.
+// Kaldi's decoder expands a composed state (its arcs computed, their
+// destinations numbered) when it first iterates its arcs or asks for its
+// input epsilons: per frame, ProcessNonemitting's queue fill asks every token
+// of the emitting pass in list order, then every token the queue creates, in
+// creation order (a token's state is expanded when the token appears; the
+// emitting pass of the next frame and GetCutoff only revisit them).
+// kaldi_lazy_order (the frame's tables intact, after kaldi_positions): the
+// frame's states in that order into kstk.  kaldi_lazy_number (end of the
+// commit): the states not yet expanded number their destinations without an
+// id, in order (state, arc): the first arc to reach a destination -- an
+// atomic minimum of its dense arc number -- gives it the next id, the ids
+// ranked by a bitmap over the arc numbers and its prefix popcounts.
+__device__ __forceinline__ void kaldi_lazy_order(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
+                                                 int slot, int n) {
+  const int* KO = a.kord + (long long)slot * a.kord_cap;
+  int* SQ = a.kstk + (long long)slot * a.kord_cap;
+  int* FL = reinterpret_cast<int*>(a.kcost0 + (long long)slot * a.kord_cap);
+  const int ne = sh.klazy_ne;
+  for (int c = threadIdx.x; c < n; c += DT) {
+    const int v = AG_LD(&KO[c]);
+    const int s = slot_state(t, T, v);
+    const int pos = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+    if (pos < 0 || pos >= n) {
+      sh.bad |= 1;
+      continue;
+    }
+    if (c < ne) {
+      AG_ST(&FL[pos], s + 1);
+    } else {
+      AG_ST(&FL[pos], 0);
+      AG_ST(&SQ[c], s);
+    }
+  }
+  vm_drain();
+  __syncthreads();
+  int run = 0, par = 0;
+  for (int p0 = 0; p0 < n; p0 += DT) {  // the emitting pass's tokens in list order
+    const int p = p0 + threadIdx.x;
+    const int x = p < n ? AG_LD(&FL[p]) : 0;
+    int tot;
+    const int ex = run + kaldi_excl_sum(sh, x > 0 ? 1 : 0, par, &tot);
+    if (x > 0) AG_ST(&SQ[ex], x - 1);
+    run += tot;
+    par ^= 1;
+  }
+  vm_drain();
+  __syncthreads();
+}
+
+// the arcs (destination, dense arc number) of the frame's states not yet
+// expanded, one item per arc over chunks of DT states (owner search as the
+// emitting pass), fn(d, q)
+template <class Fn>
+__device__ __forceinline__ void lazy_arcs(const DecArgs& a, DecShared& sh, const int* SQ, const int* Q0, int n,
+                                          Fn&& fn) {
+  for (int c0 = 0; c0 < n; c0 += DT) {
+    const int i = c0 + threadIdx.x;
+    int deg = 0, q0 = -1, b = 0;
+    if (i < n) {
+      q0 = AG_LD(&Q0[i]);
+      if (q0 >= 0) {
+        const int s = AG_LD(&SQ[i]);
+        b = (int)a.lazy_row[s];
+        deg = (int)(a.lazy_row[s + 1] - a.lazy_row[s]);
+      }
+    }
+    block_scan(sh, deg);
+    owner_blocks(sh);
+    sh.abeg[threadIdx.x] = b;
+    sh.tsrc[threadIdx.x] = q0;
+    __syncthreads();
+    const int total = sh.total;
+    const int nbo = (total + 63) >> 6 <= kOwnBlk ? (total + 63) >> 6 : 0;
+    for (int it = threadIdx.x; it < total; it += DT) {
+      const int j = owner_bo(sh, nbo, it);
+      const int k = it - sh.scan[j];
+      fn(a.lazy_next[sh.abeg[j] + k], sh.tsrc[j] + k);
+    }
+    vm_drain();
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void kaldi_lazy_number(const DecArgs& a, DecShared& sh, DecSlot& st, int slot, int n) {
+  const int* SQ = a.kstk + (long long)slot * a.kord_cap;
+  int* Q0 = reinterpret_cast<int*>(a.kcost0 + (long long)slot * a.kord_cap);
+  int* ID = a.lazy_id + (long long)slot * a.lazy_ids;
+  int* CA = a.lazy_cand + (long long)slot * a.lazy_ids;
+  int* EX = a.lazy_exp + (long long)slot * a.num_states;
+  const long long room = (long long)a.kord_cap * kKMRec / 2;  // words of the bitmap and of its prefix sums
+  unsigned* BITS = reinterpret_cast<unsigned*>(a.kmem + (long long)slot * a.kord_cap * kKMRec);
+  int* PRE = reinterpret_cast<int*>(BITS + room);
+  // the states to expand and their first dense arc numbers
+  int run = 0, par = 0;
+  for (int i0 = 0; i0 < n; i0 += DT) {
+    const int i = i0 + threadIdx.x;
+    int deg = 0;
+    bool nw = false;
+    if (i < n) {
+      const int s = AG_LD(&SQ[i]);
+      nw = AG_LD(&EX[s]) == 0;
+      if (nw) deg = (int)(a.lazy_row[s + 1] - a.lazy_row[s]);
+    }
+    int tot;
+    const int ex = run + kaldi_excl_sum(sh, deg, par, &tot);
+    if (i < n) AG_ST(&Q0[i], nw ? ex : -1);
+    run += tot;
+    par ^= 1;
+  }
+  const int nq = run;
+  const int nw = (nq + 31) >> 5;
+  if ((long long)nw > room) {  // (capacity: arcs of one frame's new states)
+    if (threadIdx.x == 0) sh.bad |= 1;
+    __syncthreads();
+    return;
+  }
+  for (int w = threadIdx.x; w < nw; w += DT) AG_ST(&BITS[w], 0u);
+  vm_drain();
+  __syncthreads();
+  // each destination without an id: its first arc number
+  lazy_arcs(a, sh, SQ, Q0, n, [&](int d, int q) {
+    if (AG_LD(&ID[d]) < 0) __hip_atomic_fetch_min(&CA[d], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  });
+  lazy_arcs(a, sh, SQ, Q0, n, [&](int d, int q) {
+    if (AG_LD(&ID[d]) < 0 && AG_LD(&CA[d]) == q)
+      __hip_atomic_fetch_or(&BITS[q >> 5], 1u << (q & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  });
+  run = 0;
+  par = 0;
+  for (int w0 = 0; w0 < nw; w0 += DT) {
+    const int w = w0 + threadIdx.x;
+    const int c = w < nw ? __popc(AG_LD(&BITS[w])) : 0;
+    int tot;
+    const int ex = run + kaldi_excl_sum(sh, c, par, &tot);
+    if (w < nw) AG_ST(&PRE[w], ex);
+    run += tot;
+    par ^= 1;
+  }
+  const int numbered = run;
+  vm_drain();
+  __syncthreads();
+  const int base = st.lazy_count;
+  lazy_arcs(a, sh, SQ, Q0, n, [&](int d, int q) {
+    if (AG_LD(&ID[d]) < 0 && AG_LD(&CA[d]) == q) {
+      const unsigned bw = AG_LD(&BITS[q >> 5]);
+      AG_ST(&ID[d], base + AG_LD(&PRE[q >> 5]) + __popc(bw & ((1u << (q & 31)) - 1u)));
+      AG_ST(&CA[d], 0x7fffffff);
+    }
+  });
+  for (int i = threadIdx.x; i < n; i += DT)
+    if (AG_LD(&Q0[i]) >= 0) AG_ST(&EX[AG_LD(&SQ[i])], 1);
+  vm_drain();
+  __syncthreads();
+  st.lazy_count = base + numbered;
 }
 
 // the buckets the frame used, emptied for the next one
@@ -2548,6 +2714,7 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   const bool lat = a.links != nullptr;
   // Kaldi order: the tokens' list positions (slot_pos) first
   if (a.kaldi && ok) kaldi_positions(a, sh, t, T, slot, n, pr);
+  if (a.kaldi && a.lazy_id && ok) kaldi_lazy_order(a, sh, t, T, slot, n);
   // the emitting records first: with deferred winners they set the
   // backpointers the token commit below reads (Kaldi order: every record is
   // an accepted relaxation, kept)
@@ -2658,6 +2825,10 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   lds_clear_build(t);
   __syncthreads();
   pr.mark(9);
+  if (a.kaldi && a.lazy_id && ok) {
+    kaldi_lazy_number(a, sh, st, slot, n);
+    pr.mark(63);
+  }
   if (ok) {
     st.cur_base = base;
     st.arena_used = base + n;
@@ -3157,7 +3328,19 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     st.last_prune = 0;
     // Kaldi order: a new decoder's HashList holds 1000 buckets; InitDecoding
     // (reset 1, a Recognizer's next segment) keeps the size it grew to
-    if (job.reset == 2 || st.khash <= 0) st.khash = 1000;
+    if (job.reset >= 2 || st.khash <= 0) st.khash = 1000;
+    if (job.reset == 3 && a.lazy_id) {  // a new stream: OpenFST numbers from its start state
+      int* ID = a.lazy_id + (long long)slot * a.lazy_ids;
+      int* CA = a.lazy_cand + (long long)slot * a.lazy_ids;
+      int* EX = a.lazy_exp + (long long)slot * a.num_states;
+      for (int i = threadIdx.x; i < a.lazy_ids; i += DT) {
+        AG_ST(&ID[i], i == a.start_state ? 0 : -1);
+        AG_ST(&CA[i], 0x7fffffff);
+      }
+      for (int i = threadIdx.x; i < a.num_states; i += DT) AG_ST(&EX[i], 0);
+      st.lazy_count = 1;
+      vm_drain();
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       sh.n_new_l = 0;

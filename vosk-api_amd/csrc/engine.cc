@@ -756,6 +756,19 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     dec_.kmem = (int*)DevAlloc(sizeof(int) * 8 * KO);
     dec_.kadj_cap = 4 * dec_.kord_cap;
     dec_.kadj = (int2*)DevAlloc(sizeof(int2) * (size_t)S * dec_.kadj_cap);
+    // OpenFST's lazy numbering of a composed graph:
+    // VOSK_AMD_LAZY_IDS=0 buckets by the static graph's ids instead
+    const char* le = getenv("VOSK_AMD_LAZY_IDS");
+    if (g.lazy_ids > 0 && !(le && atoi(le) == 0)) {
+      if ((int64_t)g.lazy_row.size() != (int64_t)NS + 1 || g.lazy_row.back() >= (1LL << 31))
+        VAMD_ERR("lazy numbering table does not match the graph");
+      dec_.lazy_ids = g.lazy_ids;
+      dec_.lazy_row = Upload(std::vector<long long>(g.lazy_row.begin(), g.lazy_row.end()));
+      dec_.lazy_next = Upload(g.lazy_next);
+      dec_.lazy_id = (int*)DevAlloc(sizeof(int) * (size_t)S * g.lazy_ids);
+      dec_.lazy_cand = (int*)DevAlloc(sizeof(int) * (size_t)S * g.lazy_ids);
+      dec_.lazy_exp = (int*)DevAlloc(sizeof(int) * (size_t)S * NS);
+    }
     HIPCHECK(hipMemset(dec_.kb_first, 0x7f, sizeof(int) * KB));  // 0x7f7f7f7f: empty (above any creation index)
     HIPCHECK(hipMemset(dec_.kb_cnt, 0, sizeof(int) * KB));
     // creation order / buckets: valid indices from the start (slot 0, bucket 0)
@@ -769,6 +782,12 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     dec_.kcost0 = nullptr;
     dec_.kadj = nullptr;
     dec_.kadj_cap = 0;
+  }
+  if (!dec_.lazy_id) {
+    dec_.lazy_row = nullptr;
+    dec_.lazy_next = nullptr;
+    dec_.lazy_cand = dec_.lazy_exp = nullptr;
+    dec_.lazy_ids = 0;
   }
 
   // ---- staging
@@ -814,8 +833,8 @@ Engine::~Engine() {
             step_prof_n_, step_prof_[0] / step_prof_n_, step_prof_[1] / step_prof_n_, step_prof_[2] / step_prof_n_,
             step_prof_[3] / step_prof_n_);
   if (copy_prof_n_ && getenv("VOSK_AMD_STEP_PROFILE"))
-    fprintf(stderr, "[engine] segment copy calls %lld: prune + state read %.3f ms, pinned take %.3f ms, after %.3f ms (total over calls)\n",
-            copy_prof_n_, copy_prof_[0], copy_prof_[1], copy_prof_[2]);
+    fprintf(stderr, "[engine] segment copy calls %lld: prune + state read %.3f ms, pinned take %.3f ms, after %.3f ms, %.1f MB (totals over calls)\n",
+            copy_prof_n_, copy_prof_[0], copy_prof_[1], copy_prof_[2], copy_prof_[3]);
   (void)hipSetDevice(cfg_.device);
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (dstream_) (void)hipStreamSynchronize(dstream_);
@@ -1292,8 +1311,9 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
         // reset 2: a new decoder; 1: InitDecoding of the same decoder (a
         // Recognizer's next segment keeps its HashList size, Kaldi order)
         st_dec_.push_back(DecJob{s, first_real < 0 ? 0 : first_real * opc, dec_frames,
-                                 h.need_reset ? (h.fresh_decoder ? 2 : 1) : 0, stats_rows, fin ? 1 : 0, 0, 0});
-        if (h.need_reset) h.fresh_decoder = false;
+                                 h.need_reset ? (h.fresh_stream ? 3 : h.fresh_decoder ? 2 : 1) : 0, stats_rows,
+                                 fin ? 1 : 0, 0, 0});
+        if (h.need_reset) h.fresh_decoder = h.fresh_stream = false;
         stats_rows += dec_frames;
         if (h.need_reset) h.decoded = 0;
         h.need_reset = false;
@@ -1886,6 +1906,7 @@ void Engine::StartSegmentCopies(const std::vector<int>& slots, std::vector<std::
     cb->device = cfg_.device;
     const auto tt0 = std::chrono::steady_clock::now();
     cb->block = pinned_->Take(bytes, &cb->cap);
+    copy_prof_[3] += bytes / 1048576.0;
     copy_prof_[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tt0).count();
     // the records gathered into one device block in the host layout (a
     // workgroup per record range), then one copy to the pinned block
@@ -2033,6 +2054,16 @@ std::string Engine::DescribeSlot(int slot) const {
   return o.str();
 }
 
+bool Engine::ChunkReadyAfter(int slot, long long extra) const {
+  std::lock_guard<std::mutex> lk(const_cast<std::mutex&>(mu_));
+  const SlotHost& h = slots_.at(slot);
+  if (!h.used || h.rate != 0 || h.resident || h.finished) return true;
+  const long long samples = h.samples + (long long)(h.pending.size() - h.pending_pos) + extra;
+  const int T = NumFramesFor(samples);
+  const int iv_wait = use_iv_ ? iv_.m.right : 0;
+  return T >= (std::max(h.next_chunk, 0) + 1) * plan_.fpc + plan_.right_context + iv_wait;
+}
+
 bool Engine::StreamIdle(int slot) const {
   std::lock_guard<std::mutex> lk(const_cast<std::mutex&>(mu_));
   return !SlotInFlight(slot) && !HasRunnableWork(slots_.at(slot));
@@ -2051,7 +2082,7 @@ void Engine::ResetDecoderAtNextJob(int slot) {
     DecBatch& db = *order[b];
     for (size_t i = 0; i < db.jobs.size(); i++) {
       if (db.jobs[i].slot != slot) continue;
-      db.jobs[i].reset = 2;  // a batch segment starts a new decoder
+      db.jobs[i].reset = std::max(db.jobs[i].reset, 2);  // a batch segment starts a new decoder
       // the patch goes through the batch's pinned staging copy, ordered on
       // the decoder stream: every staged decoder batch launches on dstream_
       // (the next pipelined step, or a drain), so the launch reads the
@@ -2183,8 +2214,10 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     st_iv_frames_ = 0;
     h.stats.clear();
     const bool rs = first && (reset || h.need_reset);
-    st_dec_.push_back(DecJob{slot, 0, n, rs ? (reset || h.fresh_decoder ? 2 : 1) : 0, 0, 0, 0, 0});
-    if (rs) h.fresh_decoder = false;
+    // (a decode from scratch is a new stream: lazy numbering starts over)
+    st_dec_.push_back(DecJob{slot, 0, n, rs ? (reset || h.fresh_stream ? 3 : h.fresh_decoder ? 2 : 1) : 0, 0, 0, 0,
+                             0});
+    if (rs) h.fresh_decoder = h.fresh_stream = false;
     if (rs) h.decoded = 0;
     h.need_reset = false;
     h.decoded += n;

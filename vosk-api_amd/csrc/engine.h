@@ -12,12 +12,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <exception>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine_dev.h"
@@ -184,18 +187,34 @@ constexpr int kMaxResampleTables = 32;  // distinct input sample rates per engin
 // caller leads; each Run returns once a batch that started after its call
 // has served its stream (the batch's exception, if any, is rethrown in every
 // caller it served).
+//
+// Coalescing window: the callers a batch served come back with their next
+// request right after it (vosk-server's shape: one thread per stream calling
+// in a loop), while the next batch would start at once with only the
+// requests that arrived during the last one -- the streams would settle into
+// groups served by alternating batches, each decoder launch with a fraction
+// of them.  So a batch waits, bounded by window_us after the previous batch
+// ended, until the streams the previous batch served have posted again (a
+// stream whose caller stops is waited for at most that long, once).  The
+// serving order of each stream's requests is unchanged (results too: streams
+// are independent in every kernel).
 class SlotGroupCommit {
  public:
   void Resize(int slots) {
     req_.assign(slots, 0);
     done_.assign(slots, 0);
     err_.assign(slots, nullptr);
+    owner_.assign(slots, std::thread::id());
   }
+  void SetWindowUs(int us) { window_us_ = us; }
   template <class BatchFn>
   void Run(int slot, BatchFn&& fn) {
     std::unique_lock<std::mutex> lk(mu_);
     const long long ticket = ++req_.at(slot);
     pending_.push_back(slot);
+    owner_[slot] = std::this_thread::get_id();
+    timed_out_.erase(slot);
+    if (leader_ && waiting_) cv_lead_.notify_one();
     while (done_[slot] < ticket) {
       if (leader_) {
         cv_.wait(lk);
@@ -203,6 +222,22 @@ class SlotGroupCommit {
       }
       leader_ = true;  // lead batches until this caller's stream is served
       while (done_[slot] < ticket && !pending_.empty()) {
+        if (window_us_ > 0 && !last_.empty()) {
+          const auto deadline = last_end_ + std::chrono::microseconds(window_us_);
+          // (a stream whose caller is this thread cannot post meanwhile)
+          const std::thread::id me = std::this_thread::get_id();
+          auto all_back = [&] {
+            for (int s : last_)
+              if (req_[s] <= done_[s] && owner_[s] != me) return false;
+            return true;
+          };
+          waiting_ = true;
+          while (!all_back() && std::chrono::steady_clock::now() < deadline) cv_lead_.wait_until(lk, deadline);
+          waiting_ = false;
+          for (int s : last_)
+            if (req_[s] <= done_[s] && owner_[s] != me) timed_out_.insert(s);
+          last_.clear();
+        }
         std::vector<int> batch;
         batch.swap(pending_);
         std::vector<long long> tick;
@@ -219,6 +254,12 @@ class SlotGroupCommit {
           done_[batch[i]] = std::max(done_[batch[i]], tick[i]);
           err_[batch[i]] = e;
         }
+        // the streams to wait for next time: those served, except one that
+        // never came back within the last window (its caller stopped)
+        last_.clear();
+        for (int s : batch)
+          if (!timed_out_.count(s)) last_.push_back(s);
+        last_end_ = std::chrono::steady_clock::now();
         cv_.notify_all();
       }
       leader_ = false;
@@ -235,9 +276,17 @@ class SlotGroupCommit {
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<long long> req_, done_;  // per stream: request / served tickets
+  std::vector<std::thread::id> owner_;  // per stream: the thread of its last request
   std::vector<std::exception_ptr> err_;
   std::vector<int> pending_;
   bool leader_ = false;
+  // coalescing window (see above)
+  int window_us_ = 0;
+  bool waiting_ = false;
+  std::condition_variable cv_lead_;
+  std::vector<int> last_;
+  std::set<int> timed_out_;
+  std::chrono::steady_clock::time_point last_end_{};
 };
 
 class Engine {
@@ -345,6 +394,10 @@ class Engine {
   int DeviceFramesDecoded(int slot) const { return slots_.at(slot).dev_frames; }
   // Nothing of the stream is in the pipeline and nothing is runnable.
   bool StreamIdle(int slot) const;
+  // Whether `extra` more host-fed samples would make a chunk of the stream
+  // ready for the nnet and decoder (a prediction for batching decoder
+  // launches; true when it cannot tell cheaply, e.g. a resampled stream)
+  bool ChunkReadyAfter(int slot, long long extra) const;
   std::string DescribeSlot(int slot) const;  // development tracing
   bool PipelineBusy() const { return pendn_active_ || pend_active_; }
   // Ends the decoder segment after the frames decoded on the device so far:
@@ -390,6 +443,7 @@ class Engine {
     bool finished = false;
     bool need_reset = true;
     bool fresh_decoder = true;  // the pending reset starts a new decoder (Kaldi order: HashList size 1000)
+    bool fresh_stream = true;   // ... of a new stream (reset 3: OpenFST's lazy numbering starts over)
     int err = 0;
     std::vector<FrameStat> stats;
     std::vector<float> llh;
@@ -472,7 +526,7 @@ class Engine {
   hipStream_t copy_stream_ = nullptr;  // segment lattice copies
   double step_prof_[4] = {0, 0, 0, 0};  // Step host profile: build, sync wait, after sync, total (ms)
   long long step_prof_n_ = 0;
-  double copy_prof_[3] = {0, 0, 0};  // StartSegmentCopies: prune + state read, pinned take, rest (ms)
+  double copy_prof_[4] = {0, 0, 0, 0};  // StartSegmentCopies: prune + state read, pinned take, rest (ms), MB copied
   long long copy_prof_n_ = 0;
   int ResampleTableLocked(int rate);    // the table of an input rate (created on first use)
   std::mutex call_mu_;                 // ResampleCall's stream and buffers

@@ -142,6 +142,7 @@ struct DecSlot {
   int last_prune;   // frames decoded at the last pruning pass
   float commit_cutoff;  // cutoff of the last commit: every current token's cost is below it
   int khash;        // Kaldi order: the decoder's HashList size (0 = a new decoder's 1000)
+  int lazy_count;   // Kaldi order on a composed graph: state ids OpenFST has given so far
 };
 
 // ---- lattice (LatticeFasterDecoder forward links, kept in HBM per stream).
@@ -239,7 +240,7 @@ struct IvArgs {
 };
 
 struct DecJob {
-  int slot, llh_row0, nframes, reset, stats_row0;
+  int slot, llh_row0, nframes, reset, stats_row0;  // reset: 1 InitDecoding, 2 a new decoder, 3 a new stream
   int pad0;  // host bookkeeping: 1 = built after the stream's input ended (not read by the kernel)
   int pad1, pad2;
 };
@@ -249,7 +250,7 @@ struct FrameStat {
   float best, cutoff, next_cutoff, adaptive_beam;
 };
 
-constexpr int kDecProf = 63;  // decoder phase-clock slots per stream (decoder.hip Prof)
+constexpr int kDecProf = 64;  // decoder phase-clock slots per stream (decoder.hip Prof)
 constexpr int kKbMemb = 32;   // Kaldi order: members kept per hash bucket (more: counted by a scan)
 struct DecArgs {
   long long* prof;       // optional per-slot phase clocks [slots][kDecProf] (diagnostics)
@@ -311,6 +312,16 @@ struct DecArgs {
   int2* kadj;             // [slots][kadj_cap] their epsilon arcs past the LDS part
   int kord_cap;           // >= tokens a frame may create (max_tok + LDS table slots)
   int kadj_cap;
+  // OpenFST's lazy ComposeFst numbering (Graph::lazy_*; nullptr: the graph's
+  // ids): HashList buckets are lazy_id % khash.  Per stream, kept for the
+  // stream's life (a recognizer's ComposeFst, src/recognizer.cc:31-37): a new
+  // stream's first job (reset 3) clears it
+  const long long* lazy_row;  // [states + 1] arcs of a state in the composition's order
+  const int* lazy_next;       // their destinations as ids [0, lazy_ids)
+  int* lazy_id;               // [slots][lazy_ids] OpenFST's id (-1: none yet)
+  int* lazy_cand;             // [slots][lazy_ids] numbering scratch (INT_MAX between frames)
+  int* lazy_exp;              // [slots][states] expanded (1)
+  int lazy_ids;
 };
 
 struct TraceArgs {

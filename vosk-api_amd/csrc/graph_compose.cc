@@ -253,6 +253,28 @@ void ConnectCanonical(const HostFst& in, HostFst* out) {
     }
     out->row.push_back((int64_t)out->ilabel.size());
   }
+  // OpenFST's lazy numbering needs each state's destinations in the
+  // composition's own arc order (emitting and epsilon arcs interleaved) and
+  // the states the trim dropped: those take ids past the graph's (a source's
+  // expansion numbers them too; the decoder never reaches them)
+  const int NS = (int)order.size();
+  std::vector<int> dead(S, -1);
+  int ndead = 0;
+  out->lazy_row.assign(1, 0);
+  for (int i = 0; i < NS; i++) {
+    const int s = order[i];
+    for (int64_t e = in.row[s]; e < in.row[s + 1]; e++) {
+      const int d = in.nextstate[e];
+      int id = nid[d];
+      if (id < 0) {
+        if (dead[d] < 0) dead[d] = NS + ndead++;
+        id = dead[d];
+      }
+      out->lazy_next.push_back(id);
+    }
+    out->lazy_row.push_back((int64_t)out->lazy_next.size());
+  }
+  out->lazy_ids = NS + ndead;
 }
 
 }  // namespace

@@ -961,6 +961,9 @@ void ToGraph(const HostFst& f, Graph* g, const std::string& what) {
     }
   }
   g->arc_begin[S] = o;
+  g->lazy_row = f.lazy_row;
+  g->lazy_next = f.lazy_next;
+  g->lazy_ids = f.lazy_ids;
 }
 
 void ReadFstGraph(const std::string& path, Graph* g) {

@@ -166,6 +166,15 @@ struct Graph {
   std::vector<int> ilabel, olabel, nextstate;
   std::vector<float> weight;
   std::map<int, std::string> osyms;  // from the FST header, if present
+  // OpenFST's lazy numbering of a composed graph (lookahead models; empty
+  // otherwise): per state, its arc destinations in the composition's own arc
+  // order (emitting and epsilon arcs interleaved), as ids in [0, lazy_ids):
+  // the graph's states, then states the trim dropped (numbered when a
+  // source is expanded, never expanded themselves).  The decoder buckets its
+  // HashList by the ids OpenFST's ComposeFst would give.
+  std::vector<int64_t> lazy_row;
+  std::vector<int> lazy_next;
+  int lazy_ids = 0;
   int NumStates() const { return (int)final_cost.size(); }
   int64_t NumArcs() const { return (int64_t)ilabel.size(); }
 };
@@ -182,6 +191,10 @@ struct HostFst {
   std::vector<int> ilabel, olabel, nextstate;
   std::vector<float> weight;
   std::map<int, std::string> osyms;  // output symbols from the header, if present
+  // lazy numbering CSR of a composed graph (Graph::lazy_*; set by ComposeLookahead)
+  std::vector<int64_t> lazy_row;
+  std::vector<int> lazy_next;
+  int lazy_ids = 0;
   int NumStates() const { return (int)final_cost.size(); }
   int64_t NumArcs() const { return (int64_t)ilabel.size(); }
 };

@@ -367,6 +367,16 @@ int vamd_graph_copy(void* graph, float* final_cost, long long* arc_begin, int* i
   return g->NumStates();
 }
 
+// OpenFST lazy numbering CSR of a composed graph: returns lazy_ids (0: none);
+// row [S+1] and next [row[S]] filled when non-NULL
+int vamd_graph_lazy(void* graph, long long* row, int* next) {
+  const Graph* g = (const Graph*)graph;
+  if (g->lazy_ids == 0) return 0;
+  if (row) std::copy(g->lazy_row.begin(), g->lazy_row.end(), row);
+  if (next) std::copy(g->lazy_next.begin(), g->lazy_next.end(), next);
+  return g->lazy_ids;
+}
+
 void vamd_graph_free(void* graph) { delete (Graph*)graph; }
 
 int vamd_silence_weighting_run(int ncalls, const int* num_frames_ready, const int* first_decoder_frame,

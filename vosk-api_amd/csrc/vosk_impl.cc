@@ -98,6 +98,8 @@ int Model::FindWord(const std::string& w) const { return md_->words.Find(w); }
 
 RecognizerGroup::RecognizerGroup(Engine* e) : engine(e), by_slot(e->config().max_slots, nullptr) {
   gc.Resize(e->config().max_slots);
+  // coalescing window of the group commit (engine.h SlotGroupCommit)
+  gc.SetWindowUs(EnvInt("VOSK_AMD_GROUP_WINDOW_US", 1000));
 }
 
 RecognizerGroup* Model::AllocStreamSlot(int* slot) {
@@ -163,24 +165,46 @@ RecognizerGroup* Model::GrammarEngine(const std::string& grammar) {
 void RecognizerGroup::Serve(const std::vector<int>& slots) {
   std::vector<Recognizer*> rs;
   for (int s : slots) rs.push_back(by_slot.at(s));
-  // pieces of 0.2 s as the reference's AcceptWaveform loop (src/recognizer.cc:305-311)
+  // pieces of 0.2 s as the reference's AcceptWaveform loop (src/recognizer.cc:305-311):
+  // per stream, in order, UpdateSilenceWeights then AdvanceDecoding of each
+  // piece.  Streams are independent, so pieces of different streams need not
+  // share a pass: a pass takes, for every stream, its next piece -- first
+  // only the streams whose next piece readies no chunk (no decoder work),
+  // then all the others together, so the call's decoder launches are shared
+  // by every stream that decodes (a 0.25 s call is a 0.2 s and a 0.05 s
+  // piece, and streams at different phases ready their chunk in either)
   std::vector<int> step(rs.size());
-  size_t pieces = 1;
+  std::vector<size_t> npiece(rs.size()), cur(rs.size(), 0);
   for (size_t i = 0; i < rs.size(); i++) {
     step[i] = (int)(rs[i]->sample_frequency_ * 0.2f);
     const size_t n = rs[i]->req_wave_ ? rs[i]->req_wave_->size() : 0;
-    pieces = std::max(pieces, (n + step[i] - 1) / step[i]);
+    npiece[i] = (n + step[i] - 1) / step[i];
+    if (rs[i]->req_final_ && npiece[i] == 0) npiece[i] = 1;  // a FinalResult request: one piece, no samples
   }
   // a stream whose own input fails (AcceptSamples) is dropped from the
   // pass with its error kept for its caller; failures of the batched
   // launches themselves reach every caller of the pass
-  for (size_t p = 0; p < pieces; p++) {
-    std::vector<int> sl, first;
+  std::vector<size_t> quiet, busy;
+  while (true) {
+    quiet.clear();
+    busy.clear();
     for (size_t i = 0; i < rs.size(); i++) {
       Recognizer* r = rs[i];
-      if (r->req_error_) continue;
+      if (r->req_error_ || cur[i] >= npiece[i]) continue;
       const size_t n = r->req_wave_ ? r->req_wave_->size() : 0;
-      const size_t o = p * step[i];
+      const size_t o = cur[i] * step[i];
+      const long long add = o < n ? (long long)std::min<size_t>(step[i], n - o) : 0;
+      const bool decodes = r->req_final_ || engine->ChunkReadyAfter(r->slot_, add);
+      (decodes ? busy : quiet).push_back(i);
+    }
+    const std::vector<size_t>& run = !quiet.empty() ? quiet : busy;
+    if (run.empty()) break;
+    std::vector<int> sl, first;
+    for (size_t i : run) {
+      Recognizer* r = rs[i];
+      const size_t n = r->req_wave_ ? r->req_wave_->size() : 0;
+      const size_t o = cur[i] * step[i];
+      cur[i]++;
       if (o < n) {
         try {
           engine->AcceptSamples(r->slot_, r->req_wave_->data() + o, (int)std::min<size_t>(step[i], n - o));
@@ -188,8 +212,6 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
           r->req_error_ = std::current_exception();
           continue;
         }
-      } else if (!(r->req_final_ && p == 0)) {
-        continue;  // a FinalResult request runs in the first piece only
       }
       sl.push_back(r->slot_);
       first.push_back(r->frame_offset_ * 3);  // src/recognizer.cc:309, :825
