@@ -144,6 +144,7 @@ def oracle_model_dir(model):
     out = model.rstrip("/") + "_oracle_hclg"
     if not os.path.exists(os.path.join(out, "graph", "lazy_ids.npz")):
         OG.expanded_hclg_model(model, out + ".tmp")
+        __import__("shutil").rmtree(out, ignore_errors=True)
         os.rename(out + ".tmp", out)
     return out
 

@@ -112,6 +112,7 @@ def test_lookahead_model_64_streams(synth_la_small_en_us, test_wave, monkeypatch
     out = synth_la_small_en_us.rstrip("/") + "_oracle_hclg"
     if not os.path.exists(os.path.join(out, "graph", "lazy_ids.npz")):
         OG.expanded_hclg_model(synth_la_small_en_us, out + ".tmp")
+        __import__("shutil").rmtree(out, ignore_errors=True)
         os.rename(out + ".tmp", out)
     ref, max_active = _oracle(out, [g["llh"] for g in gpu])
     _compare(gpu, ref, max_active)
@@ -132,6 +133,7 @@ def test_lookahead_model_lazy_numbering_64_streams(synth_la_small_en_us, test_wa
     out = synth_la_small_en_us.rstrip("/") + "_oracle_hclg"
     if not os.path.exists(os.path.join(out, "graph", "lazy_ids.npz")):
         OG.expanded_hclg_model(synth_la_small_en_us, out + ".tmp")
+        __import__("shutil").rmtree(out, ignore_errors=True)
         os.rename(out + ".tmp", out)
     row, nxt, ids = OG.lazy_csr(synth_la_small_en_us)
     assert ids > 0

@@ -59,6 +59,7 @@ def model_dir(name):
         out = path + "_oracle_hclg"
         if not os.path.exists(os.path.join(out, "graph", "lazy_ids.npz")):
             OG.expanded_hclg_model(path, out + ".tmp")
+            __import__("shutil").rmtree(out, ignore_errors=True)
             os.rename(out + ".tmp", out)
         return out
     return name

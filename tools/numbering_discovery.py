@@ -84,6 +84,7 @@ def main():
     canon = model.rstrip("/") + "_oracle_hclg"
     if not os.path.exists(os.path.join(canon, "graph", "lazy_ids.npz")):
         OG.expanded_hclg_model(model, canon + ".tmp")
+        __import__("shutil").rmtree(canon, ignore_errors=True)
         os.rename(canon + ".tmp", canon)
     raw = model.rstrip("/") + "_oracle_raw"
     if not os.path.exists(os.path.join(raw, "graph", "HCLG.fst")):

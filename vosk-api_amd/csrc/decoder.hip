@@ -1354,6 +1354,8 @@ __device__ __forceinline__ void bitonic_sort64(int* hi, int* lo, int n) {
 // queue costs start at the emitting pass's costs (+inf: not yet created).
 // Returns the frame's token count; the created tokens get creation indices
 // [ne, count) in the queue's order.
+__device__ __forceinline__ void kaldi_lazy_frame(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
+                                                 DecSlot& st, int slot, int ne, int n_eps, int khash, Prof& pr);
 __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh, FrameLds& t, const HbmTab& T,
                                                  const DecPtrs& p, DecSlot& st, const KaldiLds& K, int slot,
                                                  int khash, float cutoff, int ne, int* arcs_eps, Prof& pr) {
@@ -1434,16 +1436,19 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   if (n_eps <= 1) {  // the creation order is the closure's (none or one)
     if (n_eps == 1 && threadIdx.x == 0) {
       const int v = nl_n > nl_e ? (int)t.nl[nl_e] : ~AG_LD(&T.list[ng_e]);
-      const int b = kbucket(a, slot, slot_state(t, T, v), khash);
       AG_ST(&KO[ne], v);
-      AG_ST(&KB[ne], b);
-      if (AG_LD(&BF[b]) > ne) AG_ST(&BF[b], ne);
-      const int m = AG_LD(&BC[b]);
-      AG_ST(&BC[b], m + 1);
-      if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], ne);
+      if (!a.lazy_id) {
+        const int b = kbucket(a, slot, slot_state(t, T, v), khash);
+        AG_ST(&KB[ne], b);
+        if (AG_LD(&BF[b]) > ne) AG_ST(&BF[b], ne);
+        const int m = AG_LD(&BC[b]);
+        AG_ST(&BC[b], m + 1);
+        if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], ne);
+      }
     }
     vm_drain();
     __syncthreads();
+    if (a.lazy_id) kaldi_lazy_frame(a, sh, t, T, st, slot, ne, n_eps, khash, pr);
     return ne + n_eps;
   }
   // every entry's stamp cleared, then the queue's tokens numbered: tokens of
@@ -2291,8 +2296,9 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     if (o < 0 || o >= n_eps) continue;
     const int c = ne + o;
     const int v = km_get(K, KM, i, kMSlot);
-    const int b = kbucket(a, slot, slot_state(t, T, v), khash);
     AG_ST(&KO[c], v);
+    if (a.lazy_id) continue;  // (buckets after the frame's lazy numbering)
+    const int b = kbucket(a, slot, slot_state(t, T, v), khash);
     AG_ST(&KB[c], b);
     __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2301,6 +2307,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   vm_drain();
   __syncthreads();
   pr.mark(27);
+  if (a.lazy_id && sh.bad == 0) kaldi_lazy_frame(a, sh, t, T, st, slot, ne, n_eps, khash, pr);
   if (pr.on) {
     pr.count(51, nm > 1536 ? 1 : 0);
     pr.count(52, nm > 2048 ? 1 : 0);
@@ -2410,13 +2417,17 @@ __device__ __forceinline__ void kaldi_positions(const DecArgs& a, DecShared& sh,
 // input epsilons: per frame, ProcessNonemitting's queue fill asks every token
 // of the emitting pass in list order, then every token the queue creates, in
 // creation order (a token's state is expanded when the token appears; the
-// emitting pass of the next frame and GetCutoff only revisit them).
-// kaldi_lazy_order (the frame's tables intact, after kaldi_positions): the
-// frame's states in that order into kstk.  kaldi_lazy_number (end of the
-// commit): the states not yet expanded number their destinations without an
-// id, in order (state, arc): the first arc to reach a destination -- an
-// atomic minimum of its dense arc number -- gives it the next id, the ids
-// ranked by a bitmap over the arc numbers and its prefix popcounts.
+// emitting pass of the next frame and GetCutoff only revisit them).  A
+// token the queue creates may take an id its source's expansion gives in the
+// same frame, so the queue's tokens join their HashList buckets only after
+// (kaldi_lazy_frame, at the end of kaldi_nonemitting): the emitting pass's
+// tokens' list positions among themselves (kaldi_positions over them), then
+// kaldi_lazy_order: the frame's states in expansion order into kstk; then
+// kaldi_lazy_number: the states not yet expanded number their destinations
+// without an id, in order (state, arc): the first arc to reach a destination
+// -- an atomic minimum of its dense arc number -- gives it the next id, the
+// ids ranked by a bitmap over the arc numbers and its prefix popcounts; then
+// the queue's tokens' buckets.
 __device__ __forceinline__ void kaldi_lazy_order(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
                                                  int slot, int n) {
   const int* KO = a.kord + (long long)slot * a.kord_cap;
@@ -2426,24 +2437,23 @@ __device__ __forceinline__ void kaldi_lazy_order(const DecArgs& a, DecShared& sh
   for (int c = threadIdx.x; c < n; c += DT) {
     const int v = AG_LD(&KO[c]);
     const int s = slot_state(t, T, v);
-    const int pos = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
-    if (pos < 0 || pos >= n) {
+    if (c >= ne) {  // the queue's tokens in creation order
+      AG_ST(&SQ[c], s);
+      continue;
+    }
+    const int pos = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);  // (list position among the emitting pass's)
+    if (pos < 0 || pos >= ne) {
       sh.bad |= 1;
       continue;
     }
-    if (c < ne) {
-      AG_ST(&FL[pos], s + 1);
-    } else {
-      AG_ST(&FL[pos], 0);
-      AG_ST(&SQ[c], s);
-    }
+    AG_ST(&FL[pos], s + 1);
   }
   vm_drain();
   __syncthreads();
   int run = 0, par = 0;
-  for (int p0 = 0; p0 < n; p0 += DT) {  // the emitting pass's tokens in list order
+  for (int p0 = 0; p0 < ne; p0 += DT) {  // the emitting pass's tokens in list order
     const int p = p0 + threadIdx.x;
-    const int x = p < n ? AG_LD(&FL[p]) : 0;
+    const int x = p < ne ? AG_LD(&FL[p]) : 0;
     int tot;
     const int ex = run + kaldi_excl_sum(sh, x > 0 ? 1 : 0, par, &tot);
     if (x > 0) AG_ST(&SQ[ex], x - 1);
@@ -2559,6 +2569,30 @@ __device__ __forceinline__ void kaldi_lazy_number(const DecArgs& a, DecShared& s
   vm_drain();
   __syncthreads();
   st.lazy_count = base + numbered;
+}
+
+// the lazy numbering of a frame (see above); the queue's created tokens
+// (creation indices [ne, ne + n_eps), kord set) join their buckets last
+__device__ __forceinline__ void kaldi_lazy_frame(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
+                                                 DecSlot& st, int slot, int ne, int n_eps, int khash, Prof& pr) {
+  kaldi_positions(a, sh, t, T, slot, ne, pr);
+  kaldi_lazy_order(a, sh, t, T, slot, ne + n_eps);
+  kaldi_lazy_number(a, sh, st, slot, ne + n_eps);
+  const int* KO = a.kord + (long long)slot * a.kord_cap;
+  int* KB = a.kbkt + (long long)slot * a.kord_cap;
+  int* BF = a.kb_first + (long long)slot * a.kb_cap;
+  int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
+  int* BM = a.kb_memb + (long long)slot * a.kb_cap * kKbMemb;
+  for (int c = ne + (int)threadIdx.x; c < ne + n_eps; c += DT) {
+    const int b = kbucket(a, slot, slot_state(t, T, AG_LD(&KO[c])), khash);
+    AG_ST(&KB[c], b);
+    __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], c);
+  }
+  vm_drain();
+  __syncthreads();
+  pr.mark(63);
 }
 
 // the buckets the frame used, emptied for the next one
@@ -2714,7 +2748,6 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   const bool lat = a.links != nullptr;
   // Kaldi order: the tokens' list positions (slot_pos) first
   if (a.kaldi && ok) kaldi_positions(a, sh, t, T, slot, n, pr);
-  if (a.kaldi && a.lazy_id && ok) kaldi_lazy_order(a, sh, t, T, slot, n);
   // the emitting records first: with deferred winners they set the
   // backpointers the token commit below reads (Kaldi order: every record is
   // an accepted relaxation, kept)
@@ -2825,10 +2858,6 @@ __device__ __forceinline__ void commit(const DecArgs& a, DecShared& sh, FrameLds
   lds_clear_build(t);
   __syncthreads();
   pr.mark(9);
-  if (a.kaldi && a.lazy_id && ok) {
-    kaldi_lazy_number(a, sh, st, slot, n);
-    pr.mark(63);
-  }
   if (ok) {
     st.cur_base = base;
     st.arena_used = base + n;
