@@ -115,6 +115,8 @@ struct DecShared {
   int ksum_w[2][DW];
   int kn0, kne;
   int klazy_ne;  // lazy numbering: the frame's tokens created by the emitting pass
+  int klazy_k;   // lazy numbering: the frame's states not yet expanded
+  int klazy_def; // lazy numbering: queue tokens whose state has no id yet
   int kpop_sum, kpop_max;  // component replay: pops over all lanes / on the longest lane
   int kcomp_n, kcomp_max;  // component replay: components / pops of the largest (profile)
   int karc_sum, karc_max, khbm_pops;  // wave replay: arcs iterated (all waves / the busiest), pops of HBM members
@@ -1040,9 +1042,16 @@ constexpr int kKMRec = 8;
 
 // a state's HashList bucket: its id % khash -- OpenFST's lazy id on a
 // composed graph (DecArgs::lazy_id), else the graph's
+// (the expanded flag masked off)
+static_assert(DT <= kLazyNewCap, "lazy_new holds a frame's new emitting tokens up to DT");
+__device__ __forceinline__ int kid(const DecArgs& a, int slot, int state) {
+  return a.lazy_id ? AG_LD(&a.lazy_id[(long long)slot * a.lazy_ids + state]) : state;
+}
+__device__ __forceinline__ int kbucket_of(int id, int khash) {
+  return (int)((unsigned)(id & (kLazyExpanded - 1)) % (unsigned)khash);
+}
 __device__ __forceinline__ int kbucket(const DecArgs& a, int slot, int state, int khash) {
-  const int id = a.lazy_id ? AG_LD(&a.lazy_id[(long long)slot * a.lazy_ids + state]) : state;
-  return (int)((unsigned)id % (unsigned)khash);
+  return kbucket_of(kid(a, slot, state), khash);
 }
 // HashList bookkeeping loops: creation indices per thread in flight together
 constexpr int kHlU = 4;
@@ -1377,6 +1386,8 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     sh.kn0 = 0;
     sh.kne = 0;
     sh.klazy_ne = ne;
+    sh.klazy_k = 0;
+    sh.klazy_def = 0;
   }
   __syncthreads();
   // kHlU creation indices per thread at a time, each step's loads (slot,
@@ -1394,7 +1405,18 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     for (int u = 0; u < kHlU; u++) {
       const int c = c0 + u * DT + (int)threadIdx.x;
       if (c >= ne) continue;
-      b[u] = kbucket(a, slot, slot_state(t, T, v[u]), khash);
+      const int s = slot_state(t, T, v[u]);
+      const int id = kid(a, slot, s);
+      b[u] = kbucket_of(id, khash);
+      if (a.lazy_id && !(id & kLazyExpanded)) {  // (lazy numbering: a state to expand this frame)
+        const int at = atomicAdd(&sh.klazy_k, 1);
+        if (at < DT) {
+          int* LN = a.lazy_new + (long long)slot * 3 * kLazyNewCap;
+          AG_ST(&LN[at], c);
+          AG_ST(&LN[kLazyNewCap + at], b[u]);
+          AG_ST(&LN[2 * kLazyNewCap + at], s);
+        }
+      }
       key[u] = slot_key(t, T, v[u]);
       eps[u] = v[u] >= 0 ? (t.hp[v[u]] & kPosEps) != 0 : (AG_LD(&T.pos[~v[u]]) & kHPosEps) != 0;
     }
@@ -2434,6 +2456,11 @@ __device__ __forceinline__ void kaldi_lazy_order(const DecArgs& a, DecShared& sh
   int* SQ = a.kstk + (long long)slot * a.kord_cap;
   int* FL = reinterpret_cast<int*>(a.kcost0 + (long long)slot * a.kord_cap);
   const int ne = sh.klazy_ne;
+  // (the positions leave gaps: the buckets' counts include the queue's
+  // numbered tokens, which joined them already; the order is the list's)
+  for (int p = threadIdx.x; p < n; p += DT) AG_ST(&FL[p], 0);
+  vm_drain();
+  __syncthreads();
   for (int c = threadIdx.x; c < n; c += DT) {
     const int v = AG_LD(&KO[c]);
     const int s = slot_state(t, T, v);
@@ -2441,8 +2468,8 @@ __device__ __forceinline__ void kaldi_lazy_order(const DecArgs& a, DecShared& sh
       AG_ST(&SQ[c], s);
       continue;
     }
-    const int pos = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);  // (list position among the emitting pass's)
-    if (pos < 0 || pos >= ne) {
+    const int pos = v >= 0 ? t.hst[v] : AG_LD(&T.stamp[~v]);
+    if (pos < 0 || pos >= n) {
       sh.bad |= 1;
       continue;
     }
@@ -2451,9 +2478,9 @@ __device__ __forceinline__ void kaldi_lazy_order(const DecArgs& a, DecShared& sh
   vm_drain();
   __syncthreads();
   int run = 0, par = 0;
-  for (int p0 = 0; p0 < ne; p0 += DT) {  // the emitting pass's tokens in list order
+  for (int p0 = 0; p0 < n; p0 += DT) {  // the emitting pass's tokens in list order
     const int p = p0 + threadIdx.x;
-    const int x = p < ne ? AG_LD(&FL[p]) : 0;
+    const int x = p < n ? AG_LD(&FL[p]) : 0;
     int tot;
     const int ex = run + kaldi_excl_sum(sh, x > 0 ? 1 : 0, par, &tot);
     if (x > 0) AG_ST(&SQ[ex], x - 1);
@@ -2503,10 +2530,6 @@ __device__ __forceinline__ void kaldi_lazy_number(const DecArgs& a, DecShared& s
   int* Q0 = reinterpret_cast<int*>(a.kcost0 + (long long)slot * a.kord_cap);
   int* ID = a.lazy_id + (long long)slot * a.lazy_ids;
   int* CA = a.lazy_cand + (long long)slot * a.lazy_ids;
-  int* EX = a.lazy_exp + (long long)slot * a.num_states;
-  const long long room = (long long)a.kord_cap * kKMRec / 2;  // words of the bitmap and of its prefix sums
-  unsigned* BITS = reinterpret_cast<unsigned*>(a.kmem + (long long)slot * a.kord_cap * kKMRec);
-  int* PRE = reinterpret_cast<int*>(BITS + room);
   // the states to expand and their first dense arc numbers
   int run = 0, par = 0;
   for (int i0 = 0; i0 < n; i0 += DT) {
@@ -2515,7 +2538,8 @@ __device__ __forceinline__ void kaldi_lazy_number(const DecArgs& a, DecShared& s
     bool nw = false;
     if (i < n) {
       const int s = AG_LD(&SQ[i]);
-      nw = AG_LD(&EX[s]) == 0;
+      const int id = AG_LD(&ID[s]);  // (-1: a queue token's state numbered this frame)
+      nw = id < 0 || !(id & kLazyExpanded);
       if (nw) deg = (int)(a.lazy_row[s + 1] - a.lazy_row[s]);
     }
     int tot;
@@ -2525,20 +2549,38 @@ __device__ __forceinline__ void kaldi_lazy_number(const DecArgs& a, DecShared& s
     par ^= 1;
   }
   const int nq = run;
+  // kmem (free after the queue): the bitmap over the arc numbers, its prefix
+  // popcounts, and when there is room each arc's destination by arc number
+  // (the later passes then skip the owner search)
   const int nw = (nq + 31) >> 5;
-  if ((long long)nw > room) {  // (capacity: arcs of one frame's new states)
+  const long long words = (long long)a.kord_cap * kKMRec;
+  if (2LL * nw > words) {  // (capacity: arcs of one frame's new states)
     if (threadIdx.x == 0) sh.bad |= 1;
     __syncthreads();
     return;
   }
+  unsigned* BITS = reinterpret_cast<unsigned*>(a.kmem + (long long)slot * words);
+  int* PRE = reinterpret_cast<int*>(BITS + nw);
+  int* DST = PRE + nw;
+  const bool flat = 2LL * nw + nq <= words;
   for (int w = threadIdx.x; w < nw; w += DT) AG_ST(&BITS[w], 0u);
   vm_drain();
   __syncthreads();
   // each destination without an id: its first arc number
   lazy_arcs(a, sh, SQ, Q0, n, [&](int d, int q) {
+    if (flat) AG_ST(&DST[q], d);
     if (AG_LD(&ID[d]) < 0) __hip_atomic_fetch_min(&CA[d], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   });
-  lazy_arcs(a, sh, SQ, Q0, n, [&](int d, int q) {
+  auto arcs = [&](auto&& fn) {
+    if (flat) {
+      for (int q = threadIdx.x; q < nq; q += DT) fn(AG_LD(&DST[q]), q);
+      vm_drain();
+      __syncthreads();
+    } else {
+      lazy_arcs(a, sh, SQ, Q0, n, fn);
+    }
+  };
+  arcs([&](int d, int q) {
     if (AG_LD(&ID[d]) < 0 && AG_LD(&CA[d]) == q)
       __hip_atomic_fetch_or(&BITS[q >> 5], 1u << (q & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   });
@@ -2557,38 +2599,165 @@ __device__ __forceinline__ void kaldi_lazy_number(const DecArgs& a, DecShared& s
   vm_drain();
   __syncthreads();
   const int base = st.lazy_count;
-  lazy_arcs(a, sh, SQ, Q0, n, [&](int d, int q) {
+  arcs([&](int d, int q) {
     if (AG_LD(&ID[d]) < 0 && AG_LD(&CA[d]) == q) {
       const unsigned bw = AG_LD(&BITS[q >> 5]);
       AG_ST(&ID[d], base + AG_LD(&PRE[q >> 5]) + __popc(bw & ((1u << (q & 31)) - 1u)));
       AG_ST(&CA[d], 0x7fffffff);
     }
   });
+  vm_drain();
+  __syncthreads();
   for (int i = threadIdx.x; i < n; i += DT)
-    if (AG_LD(&Q0[i]) >= 0) AG_ST(&EX[AG_LD(&SQ[i])], 1);
+    if (AG_LD(&Q0[i]) >= 0)
+      __hip_atomic_fetch_or(&ID[AG_LD(&SQ[i])], kLazyExpanded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   vm_drain();
   __syncthreads();
   st.lazy_count = base + numbered;
 }
 
-// the lazy numbering of a frame (see above); the queue's created tokens
-// (creation indices [ne, ne + n_eps), kord set) join their buckets last
+// the lazy numbering of a frame (see above).  Most frames expand few states
+// (~170 of ~2500 tokens on the bench model): the emitting pass's are listed
+// as its tokens take their buckets (lazy_new: creation index, bucket, state);
+// the queue's tokens join their buckets here when their state has an id
+// already (else after the numbering) and add theirs.  Their expansion order is
+// the order of (key, creation index): an emitting token's key is its bucket's
+// first creation index -- HashList's list is the buckets in first-insertion
+// order -- a queue token's is ne (after every emitting one).  Up to DT of them
+// are ranked in LDS and numbered in one chunk: their arcs by dense number q
+// (owner search over the ranked degrees), each destination without an id its
+// first arc by atomic minimum, then the winners' ids by a scan over q.  More
+// (a stream's first frames) take the list positions and the chunked passes.
 __device__ __forceinline__ void kaldi_lazy_frame(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
                                                  DecSlot& st, int slot, int ne, int n_eps, int khash, Prof& pr) {
-  kaldi_positions(a, sh, t, T, slot, ne, pr);
-  kaldi_lazy_order(a, sh, t, T, slot, ne + n_eps);
-  kaldi_lazy_number(a, sh, st, slot, ne + n_eps);
+  const int n = ne + n_eps;
   const int* KO = a.kord + (long long)slot * a.kord_cap;
   int* KB = a.kbkt + (long long)slot * a.kord_cap;
   int* BF = a.kb_first + (long long)slot * a.kb_cap;
   int* BC = a.kb_cnt + (long long)slot * a.kb_cap;
   int* BM = a.kb_memb + (long long)slot * a.kb_cap * kKbMemb;
-  for (int c = ne + (int)threadIdx.x; c < ne + n_eps; c += DT) {
-    const int b = kbucket(a, slot, slot_state(t, T, AG_LD(&KO[c])), khash);
-    AG_ST(&KB[c], b);
-    __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], c);
+  int* ID = a.lazy_id + (long long)slot * a.lazy_ids;
+  int* CA = a.lazy_cand + (long long)slot * a.lazy_ids;
+  const int* LN = a.lazy_new + (long long)slot * 3 * kLazyNewCap;
+  int* SQ = a.kstk + (long long)slot * a.kord_cap;
+  int* KI = reinterpret_cast<int*>(sh.tcost);  // (LDS, free here) states of the listed tokens
+  const long long words = (long long)a.kord_cap * kKMRec;
+  int* DST = a.kmem + (long long)slot * words;  // (free after the queue) destination by arc number
+  const int ke = sh.klazy_k;                    // the emitting pass's (listed when at most DT)
+  __syncthreads();
+  if (ke <= DT && (int)threadIdx.x < ke) {
+    const int c = AG_LD(&LN[threadIdx.x]);
+    const int b = AG_LD(&LN[kLazyNewCap + threadIdx.x]);
+    KI[threadIdx.x] = AG_LD(&LN[2 * kLazyNewCap + threadIdx.x]);
+    sh.abeg[threadIdx.x] = AG_LD(&BF[b]);
+    sh.tsrc[threadIdx.x] = c;
+  }
+  for (int c = ne + (int)threadIdx.x; c < n; c += DT) {  // the queue's tokens
+    const int s = slot_state(t, T, AG_LD(&KO[c]));
+    const int id = AG_LD(&ID[s]);
+    if (id >= 0) {
+      const int b = kbucket_of(id, khash);
+      AG_ST(&KB[c], b);
+      __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], c);
+    } else {
+      AG_ST(&KB[c], -1);
+      atomicAdd(&sh.klazy_def, 1);
+    }
+    if (id < 0 || !(id & kLazyExpanded)) {
+      const int at = atomicAdd(&sh.klazy_k, 1);
+      if (at < DT) {
+        KI[at] = s;
+        sh.abeg[at] = ne;
+        sh.tsrc[at] = c;
+      }
+    }
+  }
+  vm_drain();
+  __syncthreads();
+  const int k = sh.klazy_k;
+  pr.count(64, k);
+  pr.count(65, k > DT ? 1 : 0);
+  pr.mark(66);
+  if (k > DT) {
+    kaldi_positions(a, sh, t, T, slot, ne, pr);
+    kaldi_lazy_order(a, sh, t, T, slot, n);
+    kaldi_lazy_number(a, sh, st, slot, n);
+    pr.mark(70);
+  } else if (k > 0) {
+    int rk = 0, s = -1, b = 0, deg = 0;
+    if ((int)threadIdx.x < k) {
+      const int kh = sh.abeg[threadIdx.x], kl = sh.tsrc[threadIdx.x];
+      s = KI[threadIdx.x];
+      b = (int)a.lazy_row[s];
+      deg = (int)(a.lazy_row[s + 1] - b);
+#pragma unroll 8
+      for (int j = 0; j < k; j++) {
+        const int h = sh.abeg[j];
+        rk += h < kh || (h == kh && sh.tsrc[j] < kl);
+      }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < k) {
+      sh.abeg[rk] = b;
+      sh.tsrc[rk] = deg;
+    }
+    __syncthreads();
+    pr.mark(67);
+    const int dj = (int)threadIdx.x < k ? sh.tsrc[threadIdx.x] : 0;
+    block_scan(sh, dj);
+    const int nq = sh.total;
+    if (nq > words) {  // (the general passes re-expand instead of keeping destinations)
+      if (s >= 0) AG_ST(&SQ[rk], s);
+      vm_drain();
+      __syncthreads();
+      kaldi_lazy_number(a, sh, st, slot, k);
+    } else {
+      owner_blocks(sh);
+      __syncthreads();
+      const int nbo = (nq + 63) >> 6 <= kOwnBlk ? (nq + 63) >> 6 : 0;
+      for (int q = threadIdx.x; q < nq; q += DT) {
+        const int j = owner_bo(sh, nbo, q);
+        const int d = a.lazy_next[sh.abeg[j] + q - sh.scan[j]];
+        const bool open = AG_LD(&ID[d]) < 0;
+        AG_ST(&DST[q], open ? d : -1);
+        if (open) __hip_atomic_fetch_min(&CA[d], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      vm_drain();
+      __syncthreads();
+      pr.mark(68);
+      const int base = st.lazy_count;
+      int run = 0, par = 0;
+      for (int q0 = 0; q0 < nq; q0 += DT) {
+        const int q = q0 + threadIdx.x;
+        const int d = q < nq ? AG_LD(&DST[q]) : -1;
+        const bool win = d >= 0 && AG_LD(&CA[d]) == q;
+        int tot;
+        const int ex = run + kaldi_excl_sum(sh, win ? 1 : 0, par, &tot);
+        if (win) {
+          AG_ST(&ID[d], base + ex);
+          AG_ST(&CA[d], 0x7fffffff);
+        }
+        run += tot;
+        par ^= 1;
+      }
+      vm_drain();
+      __syncthreads();
+      if (s >= 0) __hip_atomic_fetch_or(&ID[s], kLazyExpanded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      st.lazy_count = base + run;
+      pr.mark(69);
+    }
+  }
+  if (sh.klazy_def) {  // the queue's tokens whose state this frame numbered
+    for (int c = ne + (int)threadIdx.x; c < n; c += DT) {
+      if (AG_LD(&KB[c]) >= 0) continue;
+      const int b = kbucket(a, slot, slot_state(t, T, AG_LD(&KO[c])), khash);
+      AG_ST(&KB[c], b);
+      __hip_atomic_fetch_min(&BF[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int m = __hip_atomic_fetch_add(&BC[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (m < kKbMemb) AG_ST(&BM[kKbMemb * b + m], c);
+    }
   }
   vm_drain();
   __syncthreads();
@@ -3361,12 +3530,10 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     if (job.reset == 3 && a.lazy_id) {  // a new stream: OpenFST numbers from its start state
       int* ID = a.lazy_id + (long long)slot * a.lazy_ids;
       int* CA = a.lazy_cand + (long long)slot * a.lazy_ids;
-      int* EX = a.lazy_exp + (long long)slot * a.num_states;
       for (int i = threadIdx.x; i < a.lazy_ids; i += DT) {
         AG_ST(&ID[i], i == a.start_state ? 0 : -1);
         AG_ST(&CA[i], 0x7fffffff);
       }
-      for (int i = threadIdx.x; i < a.num_states; i += DT) AG_ST(&EX[i], 0);
       st.lazy_count = 1;
       vm_drain();
     }

@@ -760,14 +760,15 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     // VOSK_AMD_LAZY_IDS=0 buckets by the static graph's ids instead
     const char* le = getenv("VOSK_AMD_LAZY_IDS");
     if (g.lazy_ids > 0 && !(le && atoi(le) == 0)) {
-      if ((int64_t)g.lazy_row.size() != (int64_t)NS + 1 || g.lazy_row.back() >= (1LL << 31))
+      if ((int64_t)g.lazy_row.size() != (int64_t)NS + 1 || g.lazy_row.back() >= (1LL << 31) ||
+          g.lazy_ids >= kLazyExpanded)
         VAMD_ERR("lazy numbering table does not match the graph");
       dec_.lazy_ids = g.lazy_ids;
       dec_.lazy_row = Upload(std::vector<long long>(g.lazy_row.begin(), g.lazy_row.end()));
       dec_.lazy_next = Upload(g.lazy_next);
       dec_.lazy_id = (int*)DevAlloc(sizeof(int) * (size_t)S * g.lazy_ids);
       dec_.lazy_cand = (int*)DevAlloc(sizeof(int) * (size_t)S * g.lazy_ids);
-      dec_.lazy_exp = (int*)DevAlloc(sizeof(int) * (size_t)S * NS);
+      dec_.lazy_new = (int*)DevAlloc(sizeof(int) * (size_t)S * 3 * kLazyNewCap);
     }
     HIPCHECK(hipMemset(dec_.kb_first, 0x7f, sizeof(int) * KB));  // 0x7f7f7f7f: empty (above any creation index)
     HIPCHECK(hipMemset(dec_.kb_cnt, 0, sizeof(int) * KB));
@@ -786,7 +787,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   if (!dec_.lazy_id) {
     dec_.lazy_row = nullptr;
     dec_.lazy_next = nullptr;
-    dec_.lazy_cand = dec_.lazy_exp = nullptr;
+    dec_.lazy_cand = dec_.lazy_new = nullptr;
     dec_.lazy_ids = 0;
   }
 
@@ -816,10 +817,39 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     char* blk = nullptr;
     HIPCHECK(hipHostMalloc((void**)&blk, want, hipHostMallocDefault));
     pinned_->Give(blk, want);
+    // and the rest of StartSegmentCopies' buffers: allocated on the lane
+    // thread, they were ~10 ms of the first segments' tail
+    HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+    HIPCHECK(hipEventCreateWithFlags(&copy_ev_, hipEventDisableTiming));
+    HIPCHECK(hipHostMalloc((void**)&h_copy_slots_, sizeof(DecSlot) * S, hipHostMallocDefault));
+    d_prune_slots_ = (int*)DevAlloc(sizeof(int) * S);
+    HIPCHECK(hipHostMalloc((void**)&h_copy_stage_, Align256(sizeof(int) * S) + sizeof(CopyItem) * 3 * S,
+                           hipHostMallocDefault));
+    pack_cap_ = want;
+    HIPCHECK(hipMalloc((void**)&d_pack_, pack_cap_));
+    pack_items_cap_ = 3 * (size_t)S + 16;
+    HIPCHECK(hipMalloc((void**)&d_pack_items_, sizeof(CopyItem) * pack_items_cap_));
   }
   // the tables above were cleared with null-stream memsets, which the
   // engine's non-blocking streams are not ordered after
   HIPCHECK(hipDeviceSynchronize());
+  if (cfg_.lattice) {
+    // the segment copies' path run once on an idle slot (frames 0: the
+    // prune returns at once): the copy stream's first commands and first
+    // launches cost ~9 ms each on the host, paid here instead of in the first
+    // segments' tail
+    memset(h_copy_stage_, 0, sizeof(int));
+    HIPCHECK(hipMemcpyAsync(d_prune_slots_, h_copy_stage_, sizeof(int), hipMemcpyHostToDevice, copy_stream_));
+    LaunchPruneFinal(dec_, d_prune_slots_, 1, true, copy_stream_);
+    HIPCHECK(hipMemcpyAsync(h_copy_slots_, d_slots_, sizeof(DecSlot) * S, hipMemcpyDeviceToHost, copy_stream_));
+    CopyItem* it = (CopyItem*)(h_copy_stage_ + Align256(sizeof(int) * S));
+    *it = CopyItem{(const unsigned*)d_slots_, 0, 1};
+    HIPCHECK(hipMemcpyAsync(d_pack_items_, it, sizeof(CopyItem), hipMemcpyHostToDevice, copy_stream_));
+    LaunchGatherCopy(d_pack_items_, 1, d_pack_, copy_stream_);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(h_copy_slots_, d_pack_, sizeof(unsigned), hipMemcpyDeviceToHost, copy_stream_));
+    HIPCHECK(hipStreamSynchronize(copy_stream_));
+  }
   slots_.resize(S);
   VAMD_LOG("engine: device memory " << (dev_bytes_ >> 20) << " MB (Kaldi-order scratch "
                                     << (kaldi_bytes >> 20) << " MB), slots=" << S << " fpc=" << fpc << " priming=" << plan_.priming_chunks

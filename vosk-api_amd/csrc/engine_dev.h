@@ -250,7 +250,9 @@ struct FrameStat {
   float best, cutoff, next_cutoff, adaptive_beam;
 };
 
-constexpr int kDecProf = 64;  // decoder phase-clock slots per stream (decoder.hip Prof)
+constexpr int kDecProf = 71;
+constexpr int kLazyExpanded = 1 << 30;  // lazy_id flag: the state's arcs are numbered
+constexpr int kLazyNewCap = 1024;       // lazy_new entries per list (>= decoder threads)  // decoder phase-clock slots per stream (decoder.hip Prof)
 constexpr int kKbMemb = 32;   // Kaldi order: members kept per hash bucket (more: counted by a scan)
 struct DecArgs {
   long long* prof;       // optional per-slot phase clocks [slots][kDecProf] (diagnostics)
@@ -318,9 +320,9 @@ struct DecArgs {
   // stream's first job (reset 3) clears it
   const long long* lazy_row;  // [states + 1] arcs of a state in the composition's order
   const int* lazy_next;       // their destinations as ids [0, lazy_ids)
-  int* lazy_id;               // [slots][lazy_ids] OpenFST's id (-1: none yet)
+  int* lazy_id;               // [slots][lazy_ids] OpenFST's id (-1: none yet) | kLazyExpanded
   int* lazy_cand;             // [slots][lazy_ids] numbering scratch (INT_MAX between frames)
-  int* lazy_exp;              // [slots][states] expanded (1)
+  int* lazy_new;              // [slots][3][kLazyNewCap] a frame's emitting tokens not yet expanded
   int lazy_ids;
 };
 

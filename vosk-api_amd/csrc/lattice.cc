@@ -122,9 +122,13 @@ struct StrRepo {
   // and common-prefix queries)
   std::vector<int> parent{-1}, label{0}, len{0}, jump{0};
   std::vector<uint64_t> hash{0}, pw{1};
-  // (node, label) -> successor node: open addressing, linear probing
-  std::vector<uint64_t> skey = std::vector<uint64_t>(1024, ~0ull);
-  std::vector<int> sval = std::vector<int>(1024, -1);
+  // (node, label) -> successor node: open addressing, linear probing (key
+  // and value side by side: one cache line per probe)
+  struct Slot {
+    uint64_t key;
+    int val;
+  };
+  std::vector<Slot> slot = std::vector<Slot>(1024, Slot{~0ull, -1});
   size_t sused = 0;
   static size_t Mix(uint64_t k) {
     k ^= k >> 33;
@@ -133,17 +137,14 @@ struct StrRepo {
     return (size_t)k;
   }
   void Grow() {
-    std::vector<uint64_t> ok(skey.size() * 2, ~0ull);
-    std::vector<int> ov(skey.size() * 2, -1);
-    ok.swap(skey);
-    ov.swap(sval);
-    const size_t m = skey.size() - 1;
-    for (size_t i = 0; i < ok.size(); i++)
-      if (ok[i] != ~0ull) {
-        size_t h = Mix(ok[i]) & m;
-        while (skey[h] != ~0ull) h = (h + 1) & m;
-        skey[h] = ok[i];
-        sval[h] = ov[i];
+    std::vector<Slot> old(slot.size() * 2, Slot{~0ull, -1});
+    old.swap(slot);
+    const size_t m = slot.size() - 1;
+    for (const Slot& o : old)
+      if (o.key != ~0ull) {
+        size_t h = Mix(o.key) & m;
+        while (slot[h].key != ~0ull) h = (h + 1) & m;
+        slot[h] = o;
       }
   }
   static uint64_t MulMod(uint64_t x, uint64_t y) {
@@ -153,15 +154,14 @@ struct StrRepo {
   }
   int Succ(int id, int lab) {
     const uint64_t k = ((uint64_t)(uint32_t)id << 32) | (uint32_t)lab;
-    size_t m = skey.size() - 1, q = Mix(k) & m;
-    while (skey[q] != ~0ull) {
-      if (skey[q] == k) return sval[q];
+    size_t m = slot.size() - 1, q = Mix(k) & m;
+    while (slot[q].key != ~0ull) {
+      if (slot[q].key == k) return slot[q].val;
       q = (q + 1) & m;
     }
     const int n = (int)parent.size();
-    skey[q] = k;
-    sval[q] = n;
-    if (2 * ++sused > skey.size()) Grow();
+    slot[q] = Slot{k, n};
+    if (2 * ++sused > slot.size()) Grow();
     parent.push_back(id);
     label.push_back(lab);
     len.push_back(len[id] + 1);

@@ -829,6 +829,7 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
   const int cores = std::min(hc > 0 ? hc : 8, 16 * (int)lanes_.size());
   int nt = EnvInt("VOSK_AMD_RESULT_THREADS", std::max(2, cores - (int)lanes_.size()));
   pool_.reset(new WorkerPool(nt, 5));
+  fin_trace_ = EnvInt("VOSK_AMD_FINISH_TRACE", 0) != 0;
   for (auto& L : lanes_) {
     Lane* l = L.get();
     l->thread = std::thread([this, l] { LaneLoop(l); });
@@ -1042,6 +1043,9 @@ void BatchModel::EmitSegments(Lane* L, const std::vector<BatchRecognizer*>& rs, 
   if (!cslots.empty()) e->StartSegmentCopies(cslots, &started);
   for (size_t k = 0; k < ci.size(); k++) copies[ci[k]] = started[k];
   prof_[2] += ns(tc, clk::now());
+  if (fin_trace_ && fin_t0_ && final_segment)
+    fprintf(stderr, "[finish] +%.2f ms segment copies started (%.2f ms)\n",
+            (clk::now().time_since_epoch().count() - fin_t0_) * 1e-6, ns(tc, clk::now()) * 1e-6);
   // the largest lattices first (longest-processing-time order over the
   // result workers: the batch's tail is not one big segment started last);
   // each stream has one segment here, so its results stay in order
@@ -1108,11 +1112,15 @@ void BatchModel::EmitSegment(Lane* L, BatchRecognizer* r, bool final_segment,
     std::string js = r->FormatResult(res, offset);
     prof_[6] += ns(tf, clk::now());
     r->PublishResult(seq, std::move(js));
+    int left;
     {
       std::lock_guard<std::mutex> lk(L->mu);
       r->tasks_--;
-      L->tasks--;
+      left = --L->tasks;
     }
+    if (fin_trace_ && fin_t0_ && left == 0)
+      fprintf(stderr, "[finish] +%.2f ms last result task done\n",
+              (clk::now().time_since_epoch().count() - fin_t0_) * 1e-6);
     L->done_cv.notify_all();
   });
 }
@@ -1224,17 +1232,28 @@ void BatchModel::LaneLoop(Lane* L) {
       fprintf(stderr, "[lane %d] batch=%zu active=%zu queued=%d busy=%d tasks=%d pipelined=%d pipe_busy=%d\n",
               L->index, batch.size(), active.size(), L->queued, L->busy, L->tasks, (int)pipelined,
               (int)e->PipelineBusy());
+    auto fin_ms = [&]() { return (clk::now().time_since_epoch().count() - fin_t0_) * 1e-6; };
+    bool fin_step = false;
     try {
       for (auto& [r, c] : batch) {
         if (!c.data.empty()) e->AcceptSamples(r->slot_, std::move(c.data));
         if (c.last) {
           e->InputFinished(r->slot_);
           r->finishing_ = true;
+          if (fin_trace_ && !fin_t0_) fin_t0_ = (long long)ts.time_since_epoch().count();
         }
       }
       slots.clear();
-      for (BatchRecognizer* r : active) slots.push_back(r->slot_);
+      for (BatchRecognizer* r : active) {
+        slots.push_back(r->slot_);
+        fin_step = fin_step || r->finishing_;
+      }
+      fin_step = fin_step && fin_trace_ && fin_t0_;
+      if (fin_step)
+        fprintf(stderr, "[finish] +%.2f ms step: batch %zu active %zu pipelined %d\n", fin_ms(), batch.size(),
+                active.size(), (int)pipelined);
       e->Step(slots, pipelined);
+      if (fin_step) fprintf(stderr, "[finish] +%.2f ms step returned\n", fin_ms());
       prof_[8] += ns(ts, clk::now());
       const auto tp = clk::now();
       // reset_on_endpoint (batch_model.cc:72): streams whose decoder job just
@@ -1319,7 +1338,9 @@ void BatchModel::LaneLoop(Lane* L) {
       try {
         slots.clear();
         for (BatchRecognizer* r : finals) slots.push_back(r->slot_);
+        if (fin_step) fprintf(stderr, "[finish] +%.2f ms %zu finals, segment copies\n", fin_ms(), finals.size());
         EmitSegments(L, finals, true);
+        if (fin_step) fprintf(stderr, "[finish] +%.2f ms segment tasks submitted\n", fin_ms());
         for (BatchRecognizer* r : finals) e->ResetPipeline(r->slot_);  // a later AcceptWaveform: new utterance
       } catch (const std::exception& ex) {
         // every finished stream still gets a (empty) final result
@@ -1446,16 +1467,25 @@ void BatchRecognizer::PublishResult(uint64_t seq, std::string&& json) {
   }
 }
 
+// The bindings read a result as FrontResult() then Pop() (python/vosk
+// BatchRecognizer.Result).  A Pop() right after a FrontResult() that found
+// nothing pops nothing: a result published by a worker in between stays for
+// the next read instead of being dropped unseen.
 const char* BatchRecognizer::FrontResult() {
   std::lock_guard<std::mutex> lk(rmu_);
-  if (results_.empty()) return "";
+  if (results_.empty()) {
+    front_state_ = 0;
+    return "";
+  }
   front_ = results_.front();
+  front_state_ = 1;
   return front_.c_str();
 }
 
 void BatchRecognizer::Pop() {
   std::lock_guard<std::mutex> lk(rmu_);
-  if (!results_.empty()) results_.pop_front();
+  if (front_state_ != 0 && !results_.empty()) results_.pop_front();
+  front_state_ = -1;
 }
 
 }  // namespace vamd

@@ -269,6 +269,9 @@ class BatchModel {
   std::atomic<long long> prof_[13] = {};
   // dynamic batching: {steps, bounded waits that expired (split rounds),
   // waits ended by a Wait() caller}
+  // development (VOSK_AMD_FINISH_TRACE): the FinishStream tail's timeline on stderr
+  bool fin_trace_ = false;
+  std::atomic<long long> fin_t0_{0}, fin_last_{0};
   std::atomic<long long> batching_[4] = {};  // steps, split rounds, released by Wait, merged probes
   ~BatchModel();
 };
@@ -322,6 +325,7 @@ class BatchRecognizer {
   std::map<uint64_t, std::string> reorder_;
   std::deque<std::string> results_;
   std::string front_;
+  int front_state_ = -1;  // last FrontResult: 1 a result, 0 none (Pop then pops nothing), -1 not read
 };
 
 }  // namespace vamd
