@@ -102,18 +102,41 @@ RecognizerGroup::RecognizerGroup(Engine* e) : engine(e), by_slot(e->config().max
   gc.SetWindowUs(EnvInt("VOSK_AMD_GROUP_WINDOW_US", 1000));
 }
 
+// Recognizers share one engine (its group commit batches the recognizers
+// that call together) until it is full; VOSK_AMD_STREAM_ENGINES > 1 spreads
+// them over that many engines first, each stepping on its own HIP streams.
+// Measured (profiles/r05_concurrent_recognizers.json): 32 threads 596 x RT on
+// one engine, 215 spread over 4 -- the engines' launches share the process's
+// 4 hardware queues (GPU_MAX_HW_QUEUES), so one engine's step waits behind
+// another's decoder launch instead of running beside it.  More engines are
+// created when all are full (VOSK_AMD_MAX_STREAM_ENGINES).
 RecognizerGroup* Model::AllocStreamSlot(int* slot) {
   std::lock_guard<std::mutex> lk(mu_);
+  const int spread = std::max(1, EnvInt("VOSK_AMD_STREAM_ENGINES", 1));
+  RecognizerGroup* best = nullptr;
+  int best_use = 0;
   for (auto& g : engines_) {
-    *slot = g->engine->TryAllocSlot();
-    if (*slot >= 0) return g.get();
+    const int use = g->engine->SlotsInUse();
+    if (use < g->engine->config().max_slots && (!best || use < best_use)) {
+      best = g.get();
+      best_use = use;
+    }
+  }
+  if (best && (best_use == 0 || (int)engines_.size() >= spread)) {
+    *slot = best->engine->TryAllocSlot();
+    if (*slot >= 0) return best;
   }
   // each engine holds the decoder state of all its slots (~140 MB per slot
   // with lattices): the number of engines is capped
   const int cap = EnvInt("VOSK_AMD_MAX_STREAM_ENGINES", 16);
-  if ((int)engines_.size() >= cap)
+  if ((int)engines_.size() >= cap) {
+    for (auto& g : engines_) {  // (a full spread: any free slot)
+      *slot = g->engine->TryAllocSlot();
+      if (*slot >= 0) return g.get();
+    }
     VAMD_ERR("all " << engines_.size() << " stream engines of the model are full "
                     "(VOSK_AMD_MAX_STREAM_ENGINES x VOSK_AMD_MAX_STREAMS recognizers)");
+  }
   EngineConfig cfg;
   cfg.frames_per_chunk = md_->dcb.frames_per_chunk;
   cfg.max_slots = EnvInt("VOSK_AMD_MAX_STREAMS", 64);
@@ -129,8 +152,9 @@ void Model::FreeStreamSlot(RecognizerGroup* g, int slot) {
   std::lock_guard<std::mutex> lk(mu_);
   g->by_slot.at(slot) = nullptr;
   g->engine->FreeSlot(slot);
-  // an emptied engine other than the first gives its device memory back
-  for (size_t i = 1; i < engines_.size(); i++)
+  // an emptied engine past the spread gives its device memory back
+  const size_t keep = (size_t)std::max(1, EnvInt("VOSK_AMD_STREAM_ENGINES", 1));
+  for (size_t i = keep; i < engines_.size(); i++)
     if (engines_[i].get() == g && g->engine->SlotsInUse() == 0) {
       engines_.erase(engines_.begin() + (long)i);
       break;
