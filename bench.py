@@ -215,6 +215,15 @@ def main():
         os.environ.pop("VOSK_AMD_DEVICE", None)
     else:
         os.environ["VOSK_AMD_DEVICE"] = str(local_rank)  # one BatchModel lane (GPU) per rank
+    # torchrun exports OMP_NUM_THREADS=1 to every rank when the environment
+    # sets none; the library caps its result workers by it (it reads it as the
+    # process's CPU share), which would leave each rank two workers for the
+    # final segments' lattices.  Give each rank its share of this node's cores
+    # instead (at most the 16 of a one-GPU box).
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    if world > 1 and os.environ.get("OMP_NUM_THREADS") == "1" and "VOSK_AMD_RESULT_THREADS" not in os.environ:
+        share = max(2, min(16, len(os.sched_getaffinity(0)) // max(local_world, 1)))
+        os.environ["VOSK_AMD_RESULT_THREADS"] = str(max(2, share - 1))
     dist = None
     if world > 1:
         import torch
