@@ -87,7 +87,7 @@ def test_raw_lattice_across_launches_with_pruning_matches_oracle_after_beam_prun
     """Streaming engine (17-frame launches, pruning between them) vs the
     oracle's unpruned lattice: identical results after the lattice-beam prune."""
     from vosk import engine
-    monkeypatch.delenv("VOSK_AMD_DEC_PRUNE", raising=False)
+    monkeypatch.setenv("VOSK_AMD_DEC_PRUNE", "1")  # (Kaldi's schedule: a pass every interval)
     o = oracle_py.OracleModel(synth_model, fpc=51)
     wave = perturbed_stream(test_wave, 9, seconds=15.0)
     llh = o.loglikes(wave)
@@ -105,3 +105,27 @@ def test_raw_lattice_across_launches_with_pruning_matches_oracle_after_beam_prun
     # the oracle's unpruned lattice through the same host pipeline (exact
     # lattice-beam prune, determinization, MBR, n-best)
     assert _words(L, o) == _words(OL.raw_from_oracle(r, o.graph, False), o)
+
+
+def test_default_policy_prunes_only_when_an_arena_fills(synth_model, test_wave, monkeypatch):
+    """The default schedule (engine.cc: a pass at the interval once the token
+    or link arena is VOSK_AMD_DEC_PRUNE_FILL percent full, 50): a 4-s stream
+    on the default arenas (2 M tokens) runs none, a 1 % fill threshold runs them at the
+    interval; the best path and the lattice's results equal the unpruned
+    decode's either way."""
+    o = oracle_py.OracleModel(synth_model)
+    llh = o.loglikes(perturbed_stream(test_wave, 5, seconds=4.0))
+    e0, s0 = _decode(synth_model, llh, False, True, monkeypatch)
+    ref = (_words(e0.lattice(s0, True), o), e0.best_path(s0, use_final=True)[0])
+    for fill, pruned in (("50", False), ("1", True)):
+        monkeypatch.delenv("VOSK_AMD_DEC_PRUNE", raising=False)
+        monkeypatch.setenv("VOSK_AMD_DEC_PRUNE_FILL", fill)
+        from vosk import engine
+        e = engine.Engine(synth_model, max_streams=2, lattice=True)
+        s = e.new_stream()
+        e.decode_llh(s, llh, reset=True)
+        st = e.decoder_state(s)
+        assert st["err"] == 0 and st["lat_ovf"] == 0
+        assert (st["last_prune"] > 0) == pruned, (fill, st)
+        assert _words(e.lattice(s, True), o) == ref[0]
+        np.testing.assert_array_equal(e.best_path(s, use_final=True)[0], ref[1])

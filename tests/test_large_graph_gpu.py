@@ -51,7 +51,17 @@ def _expanded_model(model_dir, out_dir):
 def _batch_decode(model_dir, test_wave):
     from vosk import engine
     waves = [perturbed_stream(test_wave, 100 + i, seconds=SECS + 0.05 * i) for i in range(NSTREAMS)]
-    e = engine.Engine(model_dir, frames_per_chunk=51, max_streams=NSTREAMS, pipeline=True, lattice=True)
+    # pruning passes at Kaldi's interval (the default schedule would not run
+    # them on these short streams; the best paths must not depend on them)
+    old = os.environ.get("VOSK_AMD_DEC_PRUNE")
+    os.environ["VOSK_AMD_DEC_PRUNE"] = "1"
+    try:
+        e = engine.Engine(model_dir, frames_per_chunk=51, max_streams=NSTREAMS, pipeline=True, lattice=True)
+    finally:
+        if old is None:
+            os.environ.pop("VOSK_AMD_DEC_PRUNE")
+        else:
+            os.environ["VOSK_AMD_DEC_PRUNE"] = old
     e.set_step_samples(51 * 160)
     ss = [e.new_stream() for _ in range(NSTREAMS)]
     for s, w in zip(ss, waves):
@@ -90,8 +100,10 @@ def test_lookahead_expansion_64_streams(synth_la_small_en_us, test_wave, tmp_pat
 
 def test_60s_stream_without_endpoint_stays_bounded(synth_bigram_2m, test_wave):
     """One decoder segment of 60 s (2000 frames, thousands of tokens per
-    frame): pruning keeps the arena and link arena small and nothing
-    overflows; the best path equals the oracle's."""
+    frame): pruning keeps the arena and link arena bounded and nothing
+    overflows; the best path equals the oracle's.  (The default schedule
+    prunes once an arena is half full, engine.cc: the 2 M-token arena and the
+    4 M-link arena stay near half.)"""
     from vosk import engine
     w = perturbed_stream(test_wave, 4242, seconds=60.0)
     e = engine.Engine(synth_bigram_2m, frames_per_chunk=51, max_streams=2, lattice=True)
@@ -103,7 +115,8 @@ def test_60s_stream_without_endpoint_stays_bounded(synth_bigram_2m, test_wave):
     assert st["err"] == 0 and st["lat_ovf"] == 0, st
     assert st["frames"] >= 1990
     # ~2000 frames of several thousand tokens each without pruning
-    assert st["arena_used"] < 1_000_000 and st["links_used"] < 2_000_000, st
+    assert st["last_prune"] > 0, st
+    assert st["arena_used"] < 1_300_000 and st["links_used"] < 2_600_000, st
     o = oracle_py.OracleModel(synth_bigram_2m, fpc=51)
     r = o.recognize(w)
     np.testing.assert_array_equal(e.best_path(s, use_final=True)[0], r["path"])
