@@ -900,6 +900,8 @@ Engine::~Engine() {
   if (dstream_) (void)hipStreamDestroy(dstream_);
   if (fstream_) (void)hipStreamDestroy(fstream_);
   if (call_stream_) (void)hipStreamSynchronize(call_stream_);
+  if (d_bp_) (void)hipFree(d_bp_);
+  if (h_bp_) (void)hipHostFree(h_bp_);
   if (d_pack_) (void)hipFree(d_pack_);
   if (d_pack_items_) (void)hipFree(d_pack_items_);
   if (d_call_raw_) (void)hipFree(d_call_raw_);
@@ -1679,9 +1681,19 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
   for (int attempt = 0; attempt < 3; attempt++) {
     size_t bytes = Align256(sizeof(int) * n) + Align256(sizeof(int) * (size_t)n * cap) +
                    4 * Align256(sizeof(int) * n);
-    char* d = nullptr;
-    HIPCHECK(hipMalloc((void**)&d, bytes));
-    std::vector<char> h(bytes);
+    if (bytes > bp_cap_) {
+      if (d_bp_) HIPCHECK(hipFree(d_bp_));
+      if (h_bp_) HIPCHECK(hipHostFree(h_bp_));
+      d_bp_ = nullptr;
+      h_bp_ = nullptr;
+      bp_cap_ = 0;
+      const size_t want = std::max<size_t>(bytes + bytes / 2, (size_t)1 << 20);
+      HIPCHECK(hipMalloc((void**)&d_bp_, want));
+      HIPCHECK(hipHostMalloc((void**)&h_bp_, want, hipHostMallocDefault));
+      bp_cap_ = want;
+    }
+    char* d = d_bp_;
+    char* h = h_bp_;
     size_t o_req = 0, o_path = Align256(sizeof(int) * n);
     size_t o_len = o_path + Align256(sizeof(int) * (size_t)n * cap);
     size_t o_cost = o_len + Align256(sizeof(int) * n);
@@ -1708,26 +1720,25 @@ void Engine::BestPaths(const std::vector<int>& slots, bool use_final,
     t.final_rel = (float*)(d + o_rel);
     t.end_state = (int*)(d + o_st);
     LaunchTraceback(t, n, stream_);
-    HIPCHECK(hipMemcpyAsync(h.data(), d, bytes, hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, stream_));
     HIPCHECK(hipMemcpyAsync(h_slots_, d_slots_, sizeof(DecSlot) * slots_.size(),
                             hipMemcpyDeviceToHost, stream_));
     HIPCHECK(hipStreamSynchronize(stream_));
-    HIPCHECK(hipFree(d));
     bool retry = false;
     for (int i = 0; i < n; i++) {
-      int len = ((int*)(h.data() + o_len))[i];
+      int len = ((int*)(h + o_len))[i];
       if (len > cap) { retry = true; cap = len + 64; }
     }
     if (retry) continue;
     for (int i = 0; i < n; i++) {
       PathResult& r = (*out)[i];
-      int len = ((int*)(h.data() + o_len))[i];
-      const int* p = (const int*)(h.data() + o_path) + (size_t)i * cap;
+      int len = ((int*)(h + o_len))[i];
+      const int* p = (const int*)(h + o_path) + (size_t)i * cap;
       r.arcs.assign(p, p + len);
       std::reverse(r.arcs.begin(), r.arcs.end());
-      r.end_cost = ((float*)(h.data() + o_cost))[i];
-      r.final_relative_cost = ((float*)(h.data() + o_rel))[i];
-      r.end_state = ((int*)(h.data() + o_st))[i];
+      r.end_cost = ((float*)(h + o_cost))[i];
+      r.final_relative_cost = ((float*)(h + o_rel))[i];
+      r.end_state = ((int*)(h + o_st))[i];
       r.cost = (double)r.end_cost - h_slots_[slots[i]].offset_sum;
       if (frames_of(slots[i]) == 0) r.arcs.clear();
     }

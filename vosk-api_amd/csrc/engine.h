@@ -531,6 +531,12 @@ class Engine {
   int ResampleTableLocked(int rate);    // the table of an input rate (created on first use)
   std::mutex call_mu_;                 // ResampleCall's stream and buffers
   hipStream_t call_stream_ = nullptr;
+  // BestPaths' request / path block (device) and its read-back (pinned),
+  // grown on demand: a per-call hipMalloc / hipFree would synchronize the
+  // device on every partial result
+  char* d_bp_ = nullptr;
+  char* h_bp_ = nullptr;
+  size_t bp_cap_ = 0;
   float* d_call_raw_ = nullptr;
   float* d_call_out_ = nullptr;
   ResampleJob* d_call_jobs_ = nullptr;
