@@ -108,10 +108,11 @@ def test_raw_lattice_across_launches_with_pruning_matches_oracle_after_beam_prun
 
 
 def test_default_policy_prunes_only_when_an_arena_fills(synth_model, test_wave, monkeypatch):
-    """The default schedule (engine.cc: a pass at the interval once the token
-    or link arena is VOSK_AMD_DEC_PRUNE_FILL percent full, 50): a 4-s stream
-    on the default arenas (2 M tokens) runs none, a 1 % fill threshold runs them at the
-    interval; the best path and the lattice's results equal the unpruned
+    """The default schedule (engine.cc: a pass at the interval once the
+    segment is VOSK_AMD_DEC_PRUNE_START frames long, 300, or the token or link
+    arena VOSK_AMD_DEC_PRUNE_FILL percent full, 50): a 4-s stream on the
+    default arenas (2 M tokens) runs none, a 1 % fill threshold runs them at
+    the interval; the best path and the lattice's results equal the unpruned
     decode's either way."""
     o = oracle_py.OracleModel(synth_model)
     llh = o.loglikes(perturbed_stream(test_wave, 5, seconds=4.0))

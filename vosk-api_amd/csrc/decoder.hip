@@ -3778,8 +3778,9 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   if (sh.bad) st.err |= sh.bad;
   if (st.ntok == 0 && !st.err) st.err |= 4;
   // PruneActiveTokens every prune_interval frames (at the end of a launch),
-  // once an arena is prune_fill_pct full
-  const bool full = a.prune_fill_pct <= 0 || (long long)st.arena_used * 100 >= (long long)a.arena_cap * a.prune_fill_pct ||
+  // once the segment is prune_start frames long or an arena prune_fill_pct full
+  const bool full = a.prune_fill_pct <= 0 || st.frames >= a.prune_start ||
+                    (long long)st.arena_used * 100 >= (long long)a.arena_cap * a.prune_fill_pct ||
                     (a.links && (long long)st.links_used * 100 >= (long long)a.link_cap * a.prune_fill_pct);
   if (a.prune_interval > 0 && !st.err && st.frames - st.last_prune >= a.prune_interval && full) {
     pr.mark(10);

@@ -701,19 +701,24 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   // Kaldi prunes every prune_interval (25) frames; VOSK_AMD_DEC_PRUNE=0 turns
   // pruning off (tests that compare the raw per-frame lattice with the oracle)
   dec_.prune_interval = m.dec.prune_interval;
-  // By default a pass runs at the interval only once the stream's token or
-  // link arena is half full: the pass only bounds memory (the lattice a
-  // result is built from is the same with or without it), and
-  // a segment that fits runs no pass at all (+5 % on the bench's API line;
-  // its lattice is pruned once, by the segment's final prune).
-  // VOSK_AMD_DEC_PRUNE=1 prunes at every interval (Kaldi's schedule),
-  // VOSK_AMD_DEC_PRUNE_FILL sets the fill percentage.
+  // By default the passes start once the segment is 300 frames (9 s) long,
+  // or earlier if the stream's token or link arena is half full: a pass only
+  // bounds memory (the lattice a result is built from is the same with or
+  // without it), so a shorter segment runs none (its lattice
+  // is pruned once, by the segment's final prune; +3-5 % on the bench's API
+  // line) and a longer one pays one walk over its first 300 frames, then
+  // Kaldi's interval.  VOSK_AMD_DEC_PRUNE=1 prunes at every interval from the
+  // start (Kaldi's schedule); VOSK_AMD_DEC_PRUNE_START / _FILL set the
+  // thresholds.
   dec_.prune_fill_pct = 50;
+  dec_.prune_start = 300;
   if (const char* pe = getenv("VOSK_AMD_DEC_PRUNE")) {
     dec_.prune_interval = atoi(pe) ? m.dec.prune_interval : 0;
     dec_.prune_fill_pct = 0;
+    dec_.prune_start = 0;
   }
   if (const char* pf = getenv("VOSK_AMD_DEC_PRUNE_FILL")) dec_.prune_fill_pct = std::max(0, atoi(pf));
+  if (const char* ps = getenv("VOSK_AMD_DEC_PRUNE_START")) dec_.prune_start = std::max(0, atoi(ps));
   // a longer interval prunes less often (the lattice-beam prune of a result
   // is exact either way; only the arenas grow between prunes)
   if (const char* pi = getenv("VOSK_AMD_DEC_PRUNE_INTERVAL")) dec_.prune_interval = std::max(0, atoi(pi));

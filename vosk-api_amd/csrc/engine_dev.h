@@ -291,7 +291,8 @@ struct DecArgs {
   int lat_frame_cap;
   float lattice_beam;     // pruning (PruneActiveTokens)
   int prune_interval;     // frames between pruning passes (0 = never)
-  int prune_fill_pct;     // and only once the token or link arena is this full (percent; 0: always)
+  int prune_fill_pct;     // and only once the token or link arena is this full (percent; 0: always) ...
+  int prune_start;        // ... or the segment is this many frames long
   int prune_revisit;      // frames below the last pruned frame a pass may re-walk
   int debug;              // VOSK_AMD_DEC_DEBUG bits (development): 1 invariant checks with printf,
                           // 2 no Kaldi-order GetCutoff shortcut, 4 Kaldi epsilon queue through HBM records
