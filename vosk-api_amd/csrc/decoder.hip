@@ -1363,8 +1363,10 @@ __device__ __forceinline__ void bitonic_sort64(int* hi, int* lo, int n) {
 // queue costs start at the emitting pass's costs (+inf: not yet created).
 // Returns the frame's token count; the created tokens get creation indices
 // [ne, count) in the queue's order.
+struct KaldiLds;
 __device__ __forceinline__ void kaldi_lazy_frame(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
-                                                 DecSlot& st, int slot, int ne, int n_eps, int khash, Prof& pr);
+                                                 const KaldiLds& K, DecSlot& st, int slot, int ne, int n_eps, int khash,
+                                                 Prof& pr);
 __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh, FrameLds& t, const HbmTab& T,
                                                  const DecPtrs& p, DecSlot& st, const KaldiLds& K, int slot,
                                                  int khash, float cutoff, int ne, int* arcs_eps, Prof& pr) {
@@ -1470,7 +1472,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     }
     vm_drain();
     __syncthreads();
-    if (a.lazy_id) kaldi_lazy_frame(a, sh, t, T, st, slot, ne, n_eps, khash, pr);
+    if (a.lazy_id) kaldi_lazy_frame(a, sh, t, T, K, st, slot, ne, n_eps, khash, pr);
     return ne + n_eps;
   }
   // every entry's stamp cleared, then the queue's tokens numbered: tokens of
@@ -2329,7 +2331,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
   vm_drain();
   __syncthreads();
   pr.mark(27);
-  if (a.lazy_id && sh.bad == 0) kaldi_lazy_frame(a, sh, t, T, st, slot, ne, n_eps, khash, pr);
+  if (a.lazy_id && sh.bad == 0) kaldi_lazy_frame(a, sh, t, T, K, st, slot, ne, n_eps, khash, pr);
   if (pr.on) {
     pr.count(51, nm > 1536 ? 1 : 0);
     pr.count(52, nm > 2048 ? 1 : 0);
@@ -2629,7 +2631,8 @@ __device__ __forceinline__ void kaldi_lazy_number(const DecArgs& a, DecShared& s
 // first arc by atomic minimum, then the winners' ids by a scan over q.  More
 // (a stream's first frames) take the list positions and the chunked passes.
 __device__ __forceinline__ void kaldi_lazy_frame(const DecArgs& a, DecShared& sh, const FrameLds& t, const HbmTab& T,
-                                                 DecSlot& st, int slot, int ne, int n_eps, int khash, Prof& pr) {
+                                                 const KaldiLds& K, DecSlot& st, int slot, int ne, int n_eps, int khash,
+                                                 Prof& pr) {
   const int n = ne + n_eps;
   const int* KO = a.kord + (long long)slot * a.kord_cap;
   int* KB = a.kbkt + (long long)slot * a.kord_cap;
@@ -2643,18 +2646,26 @@ __device__ __forceinline__ void kaldi_lazy_frame(const DecArgs& a, DecShared& sh
   int* KI = reinterpret_cast<int*>(sh.tcost);  // (LDS, free here) states of the listed tokens
   const long long words = (long long)a.kord_cap * kKMRec;
   int* DST = a.kmem + (long long)slot * words;  // (free after the queue) destination by arc number
+  // (the queue's LDS, free after it: each listed state's first arc and degree)
+  int* KR = K.stk;
+  int* KD = K.v0hi;
   const int ke = sh.klazy_k;                    // the emitting pass's (listed when at most DT)
   __syncthreads();
   if (ke <= DT && (int)threadIdx.x < ke) {
     const int c = AG_LD(&LN[threadIdx.x]);
     const int b = AG_LD(&LN[kLazyNewCap + threadIdx.x]);
-    KI[threadIdx.x] = AG_LD(&LN[2 * kLazyNewCap + threadIdx.x]);
+    const int s = AG_LD(&LN[2 * kLazyNewCap + threadIdx.x]);
+    const long long r0 = a.lazy_row[s], r1 = a.lazy_row[s + 1];
+    KI[threadIdx.x] = s;
     sh.abeg[threadIdx.x] = AG_LD(&BF[b]);
     sh.tsrc[threadIdx.x] = c;
+    KR[threadIdx.x] = (int)r0;
+    KD[threadIdx.x] = (int)(r1 - r0);
   }
   for (int c = ne + (int)threadIdx.x; c < n; c += DT) {  // the queue's tokens
     const int s = slot_state(t, T, AG_LD(&KO[c]));
     const int id = AG_LD(&ID[s]);
+    const long long r0 = a.lazy_row[s], r1 = a.lazy_row[s + 1];  // (in flight with the id)
     if (id >= 0) {
       const int b = kbucket_of(id, khash);
       AG_ST(&KB[c], b);
@@ -2671,6 +2682,8 @@ __device__ __forceinline__ void kaldi_lazy_frame(const DecArgs& a, DecShared& sh
         KI[at] = s;
         sh.abeg[at] = ne;
         sh.tsrc[at] = c;
+        KR[at] = (int)r0;
+        KD[at] = (int)(r1 - r0);
       }
     }
   }
@@ -2690,8 +2703,8 @@ __device__ __forceinline__ void kaldi_lazy_frame(const DecArgs& a, DecShared& sh
     if ((int)threadIdx.x < k) {
       const int kh = sh.abeg[threadIdx.x], kl = sh.tsrc[threadIdx.x];
       s = KI[threadIdx.x];
-      b = (int)a.lazy_row[s];
-      deg = (int)(a.lazy_row[s + 1] - b);
+      b = KR[threadIdx.x];
+      deg = KD[threadIdx.x];
 #pragma unroll 8
       for (int j = 0; j < k; j++) {
         const int h = sh.abeg[j];
