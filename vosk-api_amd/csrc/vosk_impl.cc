@@ -768,6 +768,7 @@ struct BatchModel::Lane {
   int handed = 0;  // chunks handed to the engine, work not finished
   int busy = 0;     // streams with work in the engine
   int tasks = 0;    // results in production
+  bool round_wait = false;  // the lane waits for the rest of a feeding round
   bool stop = false;
   std::thread thread;
 };
@@ -969,6 +970,7 @@ void BatchModel::Release(BatchRecognizer* r) {
 
 void BatchModel::Push(BatchRecognizer* r, std::vector<float>&& chunk, bool last) {
   Lane* L = lanes_.at(r->lane_).get();
+  bool wake;
   {
     std::lock_guard<std::mutex> lk(L->mu);
     if (r->queue_.empty()) L->streams_queued++;
@@ -976,8 +978,13 @@ void BatchModel::Push(BatchRecognizer* r, std::vector<float>&& chunk, bool last)
     r->pushed_++;
     L->queued++;
     r->ended_ = last;  // a chunk after FinishStream starts a new utterance
+    // a lane waiting for the rest of a feeding round polls every millisecond
+    // and is released by Wait(): a push wakes it only when every stream of
+    // the lane has a chunk queued (the round's usual completion) -- a wake per
+    // push made the lane and the feeding thread take turns on the lock
+    wake = !L->round_wait || L->streams_queued >= (int)L->recs.size();
   }
-  L->cv.notify_one();
+  if (wake) L->cv.notify_one();
 }
 
 int BatchModel::PendingChunks(const BatchRecognizer* r) {
@@ -1204,6 +1211,7 @@ void BatchModel::LaneLoop(Lane* L) {
       if (!sched && L->queued > 0 && !e->PipelineBusy()) {
         const auto t0 = clk::now();
         auto last_push = t0;
+        L->round_wait = true;
         while (!L->stop && L->waiters == 0 && RoundIncomplete(L->recs)) {
           const int before = L->queued;
           L->cv.wait_for(lk, std::chrono::microseconds(1000));
@@ -1214,6 +1222,7 @@ void BatchModel::LaneLoop(Lane* L) {
             break;
           }
         }
+        L->round_wait = false;
         if (L->waiters > 0 && RoundIncomplete(L->recs)) batching_[2]++;
       }
       auto take = [&](BatchRecognizer* r) {
