@@ -1667,6 +1667,11 @@ bool Engine::Step(const std::vector<int>& slots, bool allow_pipeline) {
   step_prof_[0] += std::chrono::duration<double, std::milli>(t1 - t0).count();
   step_prof_[3] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   step_prof_n_++;
+  static const bool print_prof = getenv("VOSK_AMD_STEP_PROFILE") != nullptr;
+  if (print_prof && step_prof_n_ % 10 == 0)
+    fprintf(stderr, "[engine] steps %lld: build %.3f ms, sync wait %.3f ms, after sync %.3f ms, total %.3f ms per step\n",
+            step_prof_n_, step_prof_[0] / step_prof_n_, step_prof_[1] / step_prof_n_, step_prof_[2] / step_prof_n_,
+            step_prof_[3] / step_prof_n_);
   return true;
 }
 
