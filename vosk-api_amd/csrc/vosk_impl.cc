@@ -732,6 +732,24 @@ void WorkerPool::WaitIdle() {
   idle_cv_.wait(lk, [&] { return tasks_.empty() && busy_ == 0; });
 }
 
+bool WorkerPool::RunOne() {
+  std::function<void()> t;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (tasks_.empty()) return false;
+    t = std::move(tasks_.front());
+    tasks_.pop_front();
+    busy_++;
+  }
+  t();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    busy_--;
+  }
+  idle_cv_.notify_all();
+  return true;
+}
+
 void WorkerPool::Run() {
   while (true) {
     std::function<void()> t;
@@ -1028,13 +1046,23 @@ void BatchModel::WaitForCompletion() {
     }
   } leave{lanes_};
   for (auto& L : lanes_) {
-    std::unique_lock<std::mutex> lk(L->mu);
-    L->done_cv.wait(lk, [&] {
+    auto done = [&] {
       if (L->queued != 0 || L->busy != 0) return false;
       for (const BatchRecognizer* r : L->recs)
         if (r->ended_ && r->tasks_ > 0) return false;
       return true;
-    });
+    };
+    while (true) {
+      {
+        std::lock_guard<std::mutex> lk(L->mu);
+        if (done()) break;
+      }
+      // the caller's thread is idle here: it takes queued result work
+      // (final segments arrive together at FinishStream) before sleeping
+      if (pool_->RunOne()) continue;
+      std::unique_lock<std::mutex> lk(L->mu);
+      L->done_cv.wait_for(lk, std::chrono::milliseconds(1), done);
+    }
   }
 }
 
@@ -1195,6 +1223,16 @@ void BatchModel::LaneLoop(Lane* L) {
     clk::time_point tw;
     {
       std::unique_lock<std::mutex> lk(L->mu);
+      // idle with every stream finished (FinishStream): the lane's thread
+      // helps with the final segments' result work (no chunk can be waiting
+      // for it; a push ends the help after the task at hand)
+      while (!L->stop && L->queued == 0 && active.empty() && !L->recs.empty() &&
+             std::all_of(L->recs.begin(), L->recs.end(), [](const BatchRecognizer* r) { return r->ended_; })) {
+        lk.unlock();
+        const bool ran = pool_->RunOne();
+        lk.lock();
+        if (!ran) break;
+      }
       L->cv.wait(lk, [&] { return L->stop || L->queued > 0 || !active.empty(); });
       if (L->stop) return;
       tw = clk::now();

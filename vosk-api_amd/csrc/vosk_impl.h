@@ -189,6 +189,9 @@ class WorkerPool {
   ~WorkerPool();
   void Submit(std::function<void()> task);
   void WaitIdle();
+  // runs one queued task on the calling thread (an idle lane or a caller
+  // waiting in Wait() helps with the final segments); false: none queued
+  bool RunOne();
   int size() const { return (int)threads_.size(); }
 
  private:
