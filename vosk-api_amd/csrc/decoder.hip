@@ -3235,25 +3235,63 @@ __device__ __forceinline__ void prune_segment(const DecArgs& a, DecShared& sh, D
     __syncthreads();
     if (lat) {
       // emitting out-links of frame k (stored with frame k + 1: sources below its tokens)
+      // (kPI links per thread at a time: the records, then the destinations'
+      // extra costs, in flight together -- a frame's links are one chain of
+      // dependent loads, not one per DT links)
       const int tb1 = fk1.tok_base;
-      for (long long i = fk1.link_begin + threadIdx.x; i < fk1.link_end; i += DT) {
-        const int src = LK[i].x;
-        if (src >= tb1) continue;
-        const float le = AG_LD(&X[LK[i].y]) + __int_as_float(LDd[i]);
-        if (le <= beamp) atomic_min_pos(&X[src], le);
+      for (long long c0 = fk1.link_begin; c0 < fk1.link_end; c0 += kPI * DT) {
+        int2 r[kPI];
+        float le[kPI];
+#pragma unroll
+        for (int u = 0; u < kPI; u++) {
+          const long long i = c0 + u * DT + threadIdx.x;
+          r[u] = make_int2(-1, 0);
+          if (i < fk1.link_end) {
+            const int4 l = LK[i];
+            r[u] = make_int2(l.x < tb1 ? l.x : -1, l.y);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kPI; u++) {
+          const long long i = c0 + u * DT + threadIdx.x;
+          le[u] = r[u].x >= 0 ? AG_LD(&X[r[u].y]) + __int_as_float(LDd[i]) : kInf;
+        }
+#pragma unroll
+        for (int u = 0; u < kPI; u++)
+          if (r[u].x >= 0 && le[u] <= beamp) atomic_min_pos(&X[r[u].x], le[u]);
       }
       __syncthreads();
       // epsilon links within frame k, to a fixpoint
       do {
         fx.begin(sh);
-        for (long long i = fk.link_begin + threadIdx.x; i < fk.link_end; i += DT) {
-          const int src = LK[i].x;
-          if (src < tb) continue;
-          const float le = AG_LD(&X[LK[i].y]) + __int_as_float(LDd[i]);
-          if (le <= beamp && le < AG_LD(&X[src])) {
-            atomic_min_pos(&X[src], le);
-            fx.mark(sh);
+        for (long long c0 = fk.link_begin; c0 < fk.link_end; c0 += kPI * DT) {
+          int2 r[kPI];
+          float le[kPI], xs[kPI];
+#pragma unroll
+          for (int u = 0; u < kPI; u++) {
+            const long long i = c0 + u * DT + threadIdx.x;
+            r[u] = make_int2(-1, 0);
+            if (i < fk.link_end) {
+              const int4 l = LK[i];
+              r[u] = make_int2(l.x >= tb ? l.x : -1, l.y);
+            }
           }
+#pragma unroll
+          for (int u = 0; u < kPI; u++) {
+            const long long i = c0 + u * DT + threadIdx.x;
+            le[u] = kInf;
+            xs[u] = 0.0f;
+            if (r[u].x >= 0) {
+              le[u] = AG_LD(&X[r[u].y]) + __int_as_float(LDd[i]);
+              xs[u] = AG_LD(&X[r[u].x]);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < kPI; u++)
+            if (r[u].x >= 0 && le[u] <= beamp && le[u] < xs[u]) {
+              atomic_min_pos(&X[r[u].x], le[u]);
+              fx.mark(sh);
+            }
         }
       } while (fx.end(sh));
     } else {
