@@ -1111,6 +1111,12 @@ __device__ __forceinline__ int kaldi_rank_creators(const DecArgs& a, DecShared& 
   return run;
 }
 
+// the deferred emitting pass takes two consecutive items per thread per sub-round
+#ifndef VAMD_EMIT2
+#define VAMD_EMIT2 1
+#endif
+constexpr bool kEmit2 = VAMD_EMIT2 != 0;
+
 // ProcessEmitting in list order (see above); returns next_cutoff.  The
 // created tokens get creation indices [0, *ncreated) (kord: index -> slot).
 // defer: backpointers are resolved at commit from the link records and the
@@ -1163,6 +1169,89 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
     const int total = sh.total;
     const int nbo = (total + 63) >> 6 <= kOwnBlk ? (total + 63) >> 6 : 0;
     *examined += total;
+    if (defer && kEmit2) {
+      // deferred winners: two consecutive items per thread per sub-round --
+      // half the sub-rounds, so half the look-back blocks in the running
+      // cutoff's chain (the lane's pair minimum feeds the look-back; the
+      // second item's running cutoff adds the first item's)
+      const float kInfE = __int_as_float(0x7f800000);
+      int jn0 = 0, an0 = 0, jn1 = 0, an1 = 0;
+      int4 A0n = make_int4(0, 0, 0, 0), A1n = make_int4(0, 0, 0, 0);
+      {
+        const int i0 = 2 * (int)threadIdx.x, i1 = i0 + 1;
+        if (i0 < total) {
+          jn0 = owner_bo(sh, nbo, i0);
+          an0 = sh.abeg[jn0] + (i0 - sh.scan[jn0]);
+          A0n = a.arcs[an0];
+        }
+        if (i1 < total) {
+          jn1 = owner_bo(sh, nbo, i1);
+          an1 = sh.abeg[jn1] + (i1 - sh.scan[jn1]);
+          A1n = a.arcs[an1];
+        }
+      }
+      for (int sb = 0; sb < total; sb += 2 * DT) {
+        const int it0 = sb + 2 * (int)threadIdx.x, it1 = it0 + 1;
+        const bool v0 = it0 < total, v1 = it1 < total;
+        const int j0 = jn0, j1 = jn1, arc0 = an0, arc1 = an1;
+        const int4 A0 = A0n, A1 = A1n;
+        float ac0 = 0.0f, ac1 = 0.0f, tot0 = kInfE, tot1 = kInfE;
+        if (v0) {
+          ac0 = cost_offset - Lp[A0.z];
+          tot0 = (sh.tcost[j0] + ac0) + __int_as_float(A0.y);
+        }
+        if (v1) {
+          ac1 = cost_offset - Lp[A1.z];
+          tot1 = (sh.tcost[j1] + ac1) + __int_as_float(A1.y);
+        }
+        if (it0 + 2 * DT < total) {
+          jn0 = owner_bo(sh, nbo, it0 + 2 * DT);
+          an0 = sh.abeg[jn0] + (it0 + 2 * DT - sh.scan[jn0]);
+          A0n = a.arcs[an0];
+        }
+        if (it1 + 2 * DT < total) {
+          jn1 = owner_bo(sh, nbo, it1 + 2 * DT);
+          an1 = sh.abeg[jn1] + (it1 + 2 * DT - sh.scan[jn1]);
+          A1n = a.arcs[an1];
+        }
+        pr.mark(3);
+        const float x0 = v0 ? tot0 + adaptive : kInfE, x1 = v1 ? tot1 + adaptive : kInfE;
+        const float run0 = kaldi_lookback_min(sh, fminf(x0, x1), qsub * DW + (int)(threadIdx.x >> 6), seed, &incl_last);
+        const float run1 = fminf(run0, x0);
+        qsub++;
+        pr.mark(62);
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const bool want = u ? (v1 && tot1 < run1) : (v0 && tot0 < run0);
+          if (!want) continue;
+          const int4 A = u ? A1 : A0;
+          const int arc = u ? arc1 : arc0, j = u ? j1 : j0;
+          const float tot = u ? tot1 : tot0, ac = u ? ac1 : ac0;
+          const int item = ibase + (u ? it1 : it0);
+          const int dsts[1] = {A.x};
+          const unsigned long long keys[1] = {((unsigned long long)ford(tot) << 32) | (unsigned)arc};
+          const bool des[1] = {((unsigned)A.w & kDestEps) != 0}, wants[1] = {true};
+          int svs[1];
+          bool crs[1];
+          relax_batch<1>(a, sh, t, T, dsts, keys, des, wants, svs, crs);
+          int sv = kNoSlot;
+          if (svs[0] != kNoSlot) {
+            sv = svs[0];
+            if (sv >= 0) atomicMin(&t.hst[sv], item);
+            else __hip_atomic_fetch_min(&T.stamp[~sv], item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (lat)
+            emit_link(a, sh, st.links_used, slot, make_int4(sh.tsrc[j], __float_as_int(tot), arc, __float_as_int(ac)),
+                      sv, false);
+        }
+        pr.mark(22);
+        par ^= 1;
+      }
+      ibase += total;
+      __syncthreads();
+      pr.mark(2);
+      continue;
+    }
     // software pipeline: a sub-round's item (owner search, arc load) is
     // fetched before the previous sub-round's scan barrier, so the arc
     // latency overlaps the barrier and the relaxations
