@@ -1111,11 +1111,11 @@ __device__ __forceinline__ int kaldi_rank_creators(const DecArgs& a, DecShared& 
   return run;
 }
 
-// the deferred emitting pass takes two consecutive items per thread per sub-round
-#ifndef VAMD_EMIT2
-#define VAMD_EMIT2 1
+// consecutive items per thread per sub-round of the deferred emitting pass
+#ifndef VAMD_EMIT_ITEMS
+#define VAMD_EMIT_ITEMS 2
 #endif
-constexpr bool kEmit2 = VAMD_EMIT2 != 0;
+constexpr int kEmitU = VAMD_EMIT_ITEMS;
 
 // ProcessEmitting in list order (see above); returns next_cutoff.  The
 // created tokens get creation indices [0, *ncreated) (kord: index -> slot).
@@ -1169,68 +1169,70 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
     const int total = sh.total;
     const int nbo = (total + 63) >> 6 <= kOwnBlk ? (total + 63) >> 6 : 0;
     *examined += total;
-    if (defer && kEmit2) {
-      // deferred winners: two consecutive items per thread per sub-round --
-      // half the sub-rounds, so half the look-back blocks in the running
-      // cutoff's chain (the lane's pair minimum feeds the look-back; the
-      // second item's running cutoff adds the first item's)
+    if (defer && kEmitU > 1) {
+      // deferred winners: kEmitU consecutive items per thread per sub-round
+      // -- fewer sub-rounds, so fewer look-back blocks in the running
+      // cutoff's chain (the lane's minimum over its items feeds the
+      // look-back; each item's running cutoff adds its predecessors')
+      constexpr int U = kEmitU;
       const float kInfE = __int_as_float(0x7f800000);
-      int jn0 = 0, an0 = 0, jn1 = 0, an1 = 0;
-      int4 A0n = make_int4(0, 0, 0, 0), A1n = make_int4(0, 0, 0, 0);
-      {
-        const int i0 = 2 * (int)threadIdx.x, i1 = i0 + 1;
-        if (i0 < total) {
-          jn0 = owner_bo(sh, nbo, i0);
-          an0 = sh.abeg[jn0] + (i0 - sh.scan[jn0]);
-          A0n = a.arcs[an0];
-        }
-        if (i1 < total) {
-          jn1 = owner_bo(sh, nbo, i1);
-          an1 = sh.abeg[jn1] + (i1 - sh.scan[jn1]);
-          A1n = a.arcs[an1];
+      int jn[U], an[U];
+      int4 An[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int i = U * (int)threadIdx.x + u;
+        jn[u] = 0;
+        an[u] = 0;
+        An[u] = make_int4(0, 0, 0, 0);
+        if (i < total) {
+          jn[u] = owner_bo(sh, nbo, i);
+          an[u] = sh.abeg[jn[u]] + (i - sh.scan[jn[u]]);
+          An[u] = a.arcs[an[u]];
         }
       }
-      for (int sb = 0; sb < total; sb += 2 * DT) {
-        const int it0 = sb + 2 * (int)threadIdx.x, it1 = it0 + 1;
-        const bool v0 = it0 < total, v1 = it1 < total;
-        const int j0 = jn0, j1 = jn1, arc0 = an0, arc1 = an1;
-        const int4 A0 = A0n, A1 = A1n;
-        float ac0 = 0.0f, ac1 = 0.0f, tot0 = kInfE, tot1 = kInfE;
-        if (v0) {
-          ac0 = cost_offset - Lp[A0.z];
-          tot0 = (sh.tcost[j0] + ac0) + __int_as_float(A0.y);
+      for (int sb = 0; sb < total; sb += U * DT) {
+        const int it0 = sb + U * (int)threadIdx.x;
+        int jj[U], aa[U];
+        int4 AA[U];
+        float ac[U], tot[U], x[U];
+        float lane_min = kInfE;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          jj[u] = jn[u];
+          aa[u] = an[u];
+          AA[u] = An[u];
+          ac[u] = 0.0f;
+          tot[u] = kInfE;
+          x[u] = kInfE;
+          if (it0 + u < total) {
+            ac[u] = cost_offset - Lp[AA[u].z];
+            tot[u] = (sh.tcost[jj[u]] + ac[u]) + __int_as_float(AA[u].y);
+            x[u] = tot[u] + adaptive;
+          }
+          lane_min = fminf(lane_min, x[u]);
         }
-        if (v1) {
-          ac1 = cost_offset - Lp[A1.z];
-          tot1 = (sh.tcost[j1] + ac1) + __int_as_float(A1.y);
-        }
-        if (it0 + 2 * DT < total) {
-          jn0 = owner_bo(sh, nbo, it0 + 2 * DT);
-          an0 = sh.abeg[jn0] + (it0 + 2 * DT - sh.scan[jn0]);
-          A0n = a.arcs[an0];
-        }
-        if (it1 + 2 * DT < total) {
-          jn1 = owner_bo(sh, nbo, it1 + 2 * DT);
-          an1 = sh.abeg[jn1] + (it1 + 2 * DT - sh.scan[jn1]);
-          A1n = a.arcs[an1];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int i = it0 + U * DT + u;
+          if (i < total) {
+            jn[u] = owner_bo(sh, nbo, i);
+            an[u] = sh.abeg[jn[u]] + (i - sh.scan[jn[u]]);
+            An[u] = a.arcs[an[u]];
+          }
         }
         pr.mark(3);
-        const float x0 = v0 ? tot0 + adaptive : kInfE, x1 = v1 ? tot1 + adaptive : kInfE;
-        const float run0 = kaldi_lookback_min(sh, fminf(x0, x1), qsub * DW + (int)(threadIdx.x >> 6), seed, &incl_last);
-        const float run1 = fminf(run0, x0);
+        float run = kaldi_lookback_min(sh, lane_min, qsub * DW + (int)(threadIdx.x >> 6), seed, &incl_last);
         qsub++;
         pr.mark(62);
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-          const bool want = u ? (v1 && tot1 < run1) : (v0 && tot0 < run0);
+        for (int u = 0; u < U; u++) {
+          const bool want = it0 + u < total && tot[u] < run;
+          run = fminf(run, x[u]);
           if (!want) continue;
-          const int4 A = u ? A1 : A0;
-          const int arc = u ? arc1 : arc0, j = u ? j1 : j0;
-          const float tot = u ? tot1 : tot0, ac = u ? ac1 : ac0;
-          const int item = ibase + (u ? it1 : it0);
-          const int dsts[1] = {A.x};
-          const unsigned long long keys[1] = {((unsigned long long)ford(tot) << 32) | (unsigned)arc};
-          const bool des[1] = {((unsigned)A.w & kDestEps) != 0}, wants[1] = {true};
+          const int item = ibase + it0 + u;
+          const int dsts[1] = {AA[u].x};
+          const unsigned long long keys[1] = {((unsigned long long)ford(tot[u]) << 32) | (unsigned)aa[u]};
+          const bool des[1] = {((unsigned)AA[u].w & kDestEps) != 0}, wants[1] = {true};
           int svs[1];
           bool crs[1];
           relax_batch<1>(a, sh, t, T, dsts, keys, des, wants, svs, crs);
@@ -1241,8 +1243,8 @@ __device__ __forceinline__ float expand_emitting_kaldi(const DecArgs& a, DecShar
             else __hip_atomic_fetch_min(&T.stamp[~sv], item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
           if (lat)
-            emit_link(a, sh, st.links_used, slot, make_int4(sh.tsrc[j], __float_as_int(tot), arc, __float_as_int(ac)),
-                      sv, false);
+            emit_link(a, sh, st.links_used, slot,
+                      make_int4(sh.tsrc[jj[u]], __float_as_int(tot[u]), aa[u], __float_as_int(ac[u])), sv, false);
         }
         pr.mark(22);
         par ^= 1;
