@@ -4,7 +4,8 @@ src/recognizer.cc:297-323 per call).  Their AcceptWaveform/FinalResult calls
 are coalesced into shared batched engine steps (Engine::AdvanceCoalesced);
 every stream's results must equal those of the same stream decoded alone.
 The second case caps the stream engine at 4 slots so the recognizers spread
-over several engines (Model::AllocStreamSlot)."""
+over several engines (Model::AllocStreamSlot); the third spreads them over 3
+engines from the start (VOSK_AMD_STREAM_ENGINES, the least-loaded engine)."""
 import json
 import os
 import threading
@@ -30,11 +31,14 @@ def _run(rec, data, out, key):
     out[key] = res
 
 
-@pytest.mark.parametrize("max_streams", [None, 4])
+@pytest.mark.parametrize("max_streams", [None, 4, "spread3"])
 def test_concurrent_recognizers_match_sequential(synth_model_ep, test_wave, max_streams, monkeypatch):
     import vosk
     vosk.SetLogLevel(-1)
-    if max_streams:
+    if max_streams == "spread3":
+        monkeypatch.setenv("VOSK_AMD_STREAM_ENGINES", "3")
+        monkeypatch.setenv("VOSK_AMD_MAX_STREAMS", "8")
+    elif max_streams:
         monkeypatch.setenv("VOSK_AMD_MAX_STREAMS", str(max_streams))
     waves = [_pcm(perturbed_stream(test_wave, 40 + i, seconds=8.0)) for i in range(10)]
     m = vosk.Model(synth_model_ep)
