@@ -195,3 +195,47 @@ def test_lane_configurations_equal_oracle(synth_model_ep, lane_streams, monkeypa
     assert counters["merged_probes"] == 0, counters
     for i in range(len(waves)):
         batch_expect.check(out[i], exp[i], f"stream {i} (lane {lanes[i]})")
+
+
+@pytest.mark.gpu
+def test_idle_stream_does_not_stall_the_round(synth_model_noep, test_wave, monkeypatch):
+    """A lane waiting for the rest of a feeding round is woken by a push only
+    once every stream has a chunk queued (BatchModel::Push); with one
+    admitted stream that never feeds, the rounds still complete -- released by
+    Wait() and the lane's millisecond polls -- and the fed streams' results
+    equal the same streams decoded without the idle one."""
+    import vosk
+    vosk.SetLogLevel(-1)
+    monkeypatch.setenv("VOSK_BATCH_MODEL_DIR", synth_model_noep)
+    datas = [np.clip(perturbed_stream(test_wave, 60 + i, seconds=3.0), -32768, 32767).astype("<i2").tobytes()
+             for i in range(3)]
+
+    def decode(with_idle):
+        model = vosk.BatchModel()
+        recs = [vosk.BatchRecognizer(model, 16000) for _ in datas]
+        idle = vosk.BatchRecognizer(model, 16000) if with_idle else None
+        out = [[] for _ in datas]
+        worst = 0.0
+        for o in range(0, max(len(d) for d in datas), 8000):
+            for r, d in zip(recs, datas):
+                if o < len(d):
+                    r.AcceptWaveform(d[o:o + 8000])
+            t0 = time.perf_counter()
+            model.Wait()
+            worst = max(worst, time.perf_counter() - t0)
+        for r in recs:
+            r.FinishStream()
+        model.Wait()
+        for i, r in enumerate(recs):
+            while True:
+                res = r.Result()
+                if not res:
+                    break
+                out[i].append(res)
+        del recs, idle, model
+        return out, worst
+
+    ref, _ = decode(False)
+    got, worst = decode(True)
+    assert got == ref
+    assert worst < 2.0, worst
