@@ -107,6 +107,27 @@ const char *vamd_lattice_words_json(int num_frames, const int *frame_begin, cons
                                     int nbest, const signed char *tid_type, const signed char *tid_final,
                                     const signed char *tid_loop, int ntids);
 
+/* host-only: the KaldiRecognizer's incremental lattice (incremental.h:
+ * LatticeIncrementalDecoder's PruneActiveTokens schedule and
+ * LatticeIncrementalDeterminizer) over per-frame decoder records: tokens of
+ * frame k = [frame_begin[k], frame_begin[k+1]) in list order, links of frame k
+ * (emitting links into it, epsilon links inside it) with frame-local source /
+ * destination indices and the raw acoustic cost; the phone tables of
+ * vamd_lattice_set_phones.  Events: type 0 = decode up to ev_arg frames then
+ * UpdateLatticeDeterminization, 1 = GetLattice(NumFramesInLattice(), false),
+ * 2 = FinalizeDecoding + GetLattice(NumFramesDecoded(), true).  Returns a JSON
+ * list, per query {nfl, ok, chunks, arcs: per state [[word, next, graph,
+ * acoustic, [tids]]], finals: per state [graph, acoustic, [tids]] | null}. */
+const char *vamd_incremental_json(int nframes, const int *frame_begin, const int *tok_state,
+                                  const float *tok_cost, const float *cost_offset, int nlink,
+                                  const int *link_frame, const int *link_src, const int *link_dst,
+                                  const int *link_arc, const float *link_ac, int narcs,
+                                  const int *arc_ilabel, const int *arc_olabel,
+                                  const float *arc_weight, int nstates, const float *final_cost,
+                                  int start_state, float lattice_beam, int prune_interval,
+                                  float prune_scale, int max_delay, int min_chunk, int nev,
+                                  const int *ev_type, const int *ev_arg);
+
 const char *vamd_last_error(void);
 int vamd_device_count(void);
 

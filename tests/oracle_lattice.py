@@ -298,6 +298,15 @@ def determinize_phone(L, ilabel, olabel, tid2phone, tid_first, beam=6.0, max_mem
     and weight on the first link; a final string as a chain to a new final
     state), DeterminizeLatticeDeletePhones, then word-level determinization."""
     n, links, fin, start = _graph_from_raw(L, ilabel, olabel)
+    return determinize_phone_graph(n, links, fin, start, tid2phone, tid_first, beam, max_mem)
+
+
+def determinize_phone_graph(n, links, fin, start, tid2phone, tid_first, beam=6.0, max_mem=50000000):
+    """determinize_phone on a determinizer input (n, links [(src, dst, tid,
+    label, g, a)], finals, start) built by the caller (csrc/lattice.cc
+    DeterminizePhonePrunedGraph; labels above the words -- the incremental
+    determinizer's state and token labels -- are words to it)."""
+    links, fin = list(links), list(fin)
     first = max([1] + [l[3] + 1 for l in links])
     out = []
     for (s, d, t, w, g, a) in links:

@@ -711,7 +711,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   // start (Kaldi's schedule); VOSK_AMD_DEC_PRUNE_START / _FILL set the
   // thresholds.
   dec_.prune_fill_pct = 50;
-  dec_.prune_start = 300;
+  dec_.prune_start = cfg_.host_lattice ? (1 << 30) : 300;
   if (const char* pe = getenv("VOSK_AMD_DEC_PRUNE")) {
     dec_.prune_interval = atoi(pe) ? m.dec.prune_interval : 0;
     dec_.prune_fill_pct = 0;
@@ -1853,6 +1853,47 @@ void Engine::CopySegmentLattices(const std::vector<int>& slots, const std::vecto
   if (getenv("VOSK_AMD_COPY_DEBUG") && ++copy_calls_ % 20 == 0)
     fprintf(stderr, "segment copies: %lld calls, states %lld us, records %lld us, host %lld us, %lld MB\n",
             copy_calls_, copy_us_[0], copy_us_[1], copy_us_[2], copy_us_[3] >> 20);
+}
+
+void Engine::CopySegmentTail(int slot, int from, SegmentLattice* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  DEVICE_GUARD();
+  FlushLocked();
+  out->frames.clear();
+  out->arena.clear();
+  out->links.clear();
+  out->overflow = false;
+  out->first_frame = from;
+  out->arena_base = 0;
+  out->link_base = 0;
+  if (!dec_.links) return;
+  if (!copy_stream_) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+  DecSlot st;
+  HIPCHECK(hipMemcpyAsync(&st, d_slots_ + slot, sizeof(DecSlot), hipMemcpyDeviceToHost, copy_stream_));
+  HIPCHECK(hipStreamSynchronize(copy_stream_));
+  out->overflow = st.lat_ovf || st.frames + 1 > dec_.lat_frame_cap || st.err;
+  const int nf = std::min(st.frames + 1, dec_.lat_frame_cap);
+  if (from >= nf || from < 0) return;
+  out->frames.resize(nf - from);
+  HIPCHECK(hipMemcpyAsync(out->frames.data(), dec_.lat_frames + (size_t)slot * dec_.lat_frame_cap + from,
+                          sizeof(LatFrame) * (nf - from), hipMemcpyDeviceToHost, copy_stream_));
+  HIPCHECK(hipStreamSynchronize(copy_stream_));
+  const LatFrame& f0 = out->frames[0];
+  const int a0 = std::max(0, f0.tok_base);
+  const long long l0 = std::max(0ll, f0.link_begin);
+  const int na = std::max(0, st.arena_used - a0);
+  const long long nl = std::max(0ll, std::min(st.links_used, dec_.link_cap) - l0);
+  out->arena_base = a0;
+  out->link_base = l0;
+  out->arena.resize(na);
+  out->links.resize(nl);
+  if (na > 0)
+    HIPCHECK(hipMemcpyAsync(out->arena.data(), dec_.arena + (size_t)slot * dec_.arena_cap + a0, sizeof(int4) * na,
+                            hipMemcpyDeviceToHost, copy_stream_));
+  if (nl > 0)
+    HIPCHECK(hipMemcpyAsync(out->links.data(), dec_.links + (size_t)slot * dec_.link_cap + l0, sizeof(int4) * nl,
+                            hipMemcpyDeviceToHost, copy_stream_));
+  HIPCHECK(hipStreamSynchronize(copy_stream_));
 }
 
 PinnedPool::~PinnedPool() {

@@ -98,6 +98,11 @@ struct EngineConfig {
   bool lattice = false;
   long long lattice_links = 1 << 22;  // link arena per stream (16 B each)
   int lattice_frames = 1 << 14;       // frames per decoder segment with a lattice
+  // The KaldiRecognizer's incremental lattice is kept on the host
+  // (incremental.h), which reads a segment's records as they come: the
+  // in-kernel pruning passes (which compact the arenas) then run only when a
+  // stream's arena is half full, never by segment length.
+  bool host_lattice = false;
   bool track_decoded = false;  // record completed decoder jobs for TakeDecoded
   // token passing in Kaldi's sequential order (LatticeFasterDecoder's HashList
   // order, running emitting cutoff, LIFO epsilon queue: the reference's
@@ -130,6 +135,10 @@ struct SegmentLattice {
   std::vector<LatFrame> frames;
   std::vector<int4> arena, links;
   bool overflow = false;  // link arena / frame table overflow or decoder error
+  // CopySegmentTail: frames from first_frame, arena from arena_base, links
+  // from link_base (0 for a whole segment)
+  int first_frame = 0, arena_base = 0;
+  long long link_base = 0;
 };
 
 // Endpoint inputs of a stream (OnlineEndpoint [K]): decoder-segment frames,
@@ -372,6 +381,9 @@ class Engine {
   void GetRawLattice(int slot, bool use_final, RawLattice* out);
   // The segment's lattice records (drain as BestPaths); empty without a lattice.
   void CopySegmentLattice(int slot, SegmentLattice* out, bool drain = true);
+  // Frames [from, decoded] of the segment with their tokens and links (the
+  // recognizer's incremental lattice takes them as they come; drains).
+  void CopySegmentTail(int slot, int from, SegmentLattice* out);
   // The same for several streams with the copies batched.
   void CopySegmentLattices(const std::vector<int>& slots, const std::vector<SegmentLattice*>& outs,
                            bool drain = true);

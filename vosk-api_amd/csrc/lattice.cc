@@ -93,9 +93,7 @@ namespace vamd {
 namespace {
 
 // Kaldi LatticeWeight order: smaller total cost is better; ties by graph cost
-struct LW {
-  float g = 0.0f, a = 0.0f;
-};
+// (LW: lattice.h)
 inline int CompareLW(const LW& x, const LW& y) {  // 1: x better, -1: y better
   const float fx = x.g + x.a, fy = y.g + y.a;
   if (fx < fy) return 1;
@@ -317,27 +315,6 @@ void PruneRawLattice(RawLattice* lat, float beam) {
 }
 
 namespace {
-
-// The determinizer's input: an acceptor on `lout` (words, or phones in the
-// first pass) whose arcs carry one transition-id (`lin`, 0 = none) as the
-// string side -- Kaldi's Lattice after Invert (DeterminizeLatticePhonePrunedWrapper).
-// frame: per state, a bucket such that every link goes to the same or a
-// later bucket (the closure's work order).
-struct DetGraph {
-  int n = 0, start = -1;
-  std::vector<int> frame;
-  struct Link {
-    int src, dst, lin, lout;
-    float g, a;
-  };
-  std::vector<Link> links;
-  std::vector<LW> fin;  // +inf graph: not final
-  int AddState(int f) {
-    frame.push_back(f);
-    fin.push_back(LW{kInf, 0.0f});
-    return n++;
-  }
-};
 
 DetGraph FromRaw(const RawLattice& L, const Graph& g) {
   DetGraph D;
@@ -1379,7 +1356,11 @@ bool DeterminizeToWords(const RawLattice& L, const Graph& g, const LatticeOption
 
 bool DeterminizePhonePruned(const RawLattice& L, const Graph& g, const std::vector<int>& tid2phone,
                             const std::vector<char>& tid_first, const LatticeOptions& opt, WordLattice* out) {
-  DetGraph D = FromRaw(L, g);
+  return DeterminizePhonePrunedGraph(FromRaw(L, g), tid2phone, tid_first, opt, out);
+}
+
+bool DeterminizePhonePrunedGraph(DetGraph D, const std::vector<int>& tid2phone, const std::vector<char>& tid_first,
+                                 const LatticeOptions& opt, WordLattice* out) {
   // DeterminizeLatticeInsertPhones: a phone label (first_phone_label + phone,
   // first_phone_label = the highest word label + 1) at the first
   // transition-id of every phone (HMM state 0, not a self-loop); on the link

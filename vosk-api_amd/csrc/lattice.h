@@ -12,6 +12,7 @@
 #pragma once
 #include <algorithm>
 #include <cstdint>
+#include <limits>
 #include <string>
 #include <utility>
 #include <vector>
@@ -101,6 +102,36 @@ bool DeterminizeToWords(const RawLattice& lat, const Graph& g, const LatticeOpti
 // lattice.cc).  False if a guard tripped.
 bool DeterminizePhonePruned(const RawLattice& lat, const Graph& g, const std::vector<int>& tid2phone,
                             const std::vector<char>& tid_first, const LatticeOptions& opt, WordLattice* out);
+
+// The determinizer's input: an acceptor on `lout` (words, or phones in the
+// first pass; any label above the words -- the incremental determinizer's
+// state and token labels -- is a word to it) whose links carry one
+// transition-id (`lin`, 0 = none) as the string side: Kaldi's Lattice after
+// Invert (DeterminizeLatticePhonePrunedWrapper).  frame: per state, a bucket
+// such that every link goes to the same or a later bucket (the closure's work
+// order).  LW: a LatticeWeight (graph, acoustic).
+struct LW {
+  float g = 0.0f, a = 0.0f;
+};
+struct DetGraph {
+  int n = 0, start = -1;
+  std::vector<int> frame;
+  struct Link {
+    int src, dst, lin, lout;
+    float g, a;
+  };
+  std::vector<Link> links;
+  std::vector<LW> fin;  // +inf graph: not final
+  int AddState(int f) {
+    frame.push_back(f);
+    fin.push_back(LW{std::numeric_limits<float>::infinity(), 0.0f});
+    return n++;
+  }
+};
+// DeterminizePhonePruned on a determinizer input built by the caller (the
+// start state's links get no phone label, as DeterminizeLatticeInsertPhones).
+bool DeterminizePhonePrunedGraph(DetGraph D, const std::vector<int>& tid2phone, const std::vector<char>& tid_first,
+                                 const LatticeOptions& opt, WordLattice* out);
 
 // Word alignment (Kaldi lat/word-align-lattice.cc WordAlignLattice [K], with
 // WordBoundaryInfo from word_boundary.int and reorder = true; the reference

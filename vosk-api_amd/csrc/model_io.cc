@@ -108,6 +108,9 @@ void ApplyModelOptions(const std::map<std::string, std::string>& kv, DecoderOpti
     else if (k == "prune-interval") dec->prune_interval = std::stoi(v);
     else if (k == "beam-delta") dec->beam_delta = std::stof(v);
     else if (k == "hash-ratio") dec->hash_ratio = std::stof(v);
+    else if (k == "determinize-max-delay") dec->determinize_max_delay = std::stoi(v);
+    else if (k == "determinize-min-chunk-size") dec->determinize_min_chunk_size = std::stoi(v);
+    else if (k == "determinize-max-active") {}  // (not read by UpdateLatticeDeterminization)
     else if (k == "acoustic-scale") dcb->acoustic_scale = std::stof(v);
     else if (k == "frame-subsampling-factor") dcb->frame_subsampling_factor = std::stoi(v);
     else if (k == "frames-per-chunk") dcb->frames_per_chunk = std::stoi(v);

@@ -60,6 +60,8 @@ struct MfccOptions {
 struct DecoderOptions {  // LatticeIncrementalDecoderConfig defaults [K]
   float beam = 16.f, lattice_beam = 10.f, beam_delta = 0.5f, hash_ratio = 2.f;
   int max_active = std::numeric_limits<int>::max(), min_active = 200, prune_interval = 25;
+  // the incremental determinization (UpdateLatticeDeterminization)
+  int determinize_max_delay = 60, determinize_min_chunk_size = 20;
 };
 
 struct DecodableOptions {  // NnetSimpleLoopedComputationOptions defaults [K]

@@ -15,6 +15,7 @@
 
 #include "common.h"
 #include "graph_compose.h"
+#include "incremental.h"
 #include "vosk_impl.h"
 #include "../../include/vosk_api.h"
 #include "../../include/vosk_amd_engine.h"
@@ -439,6 +440,99 @@ int vamd_lattice_set_phones(const int* tid2phone, const signed char* tid_first, 
   g_host_tid_first.assign(tid_first, tid_first + std::max(ntids, 0));
   return 0;
   API_CATCH(-1)
+}
+
+// host-only: the KaldiRecognizer's incremental lattice (incremental.h) over
+// per-frame decoder records, driven by a script of events
+const char* vamd_incremental_json(int nframes, const int* frame_begin, const int* tok_state, const float* tok_cost,
+                                  const float* cost_offset, int nlink, const int* link_frame, const int* link_src,
+                                  const int* link_dst, const int* link_arc, const float* link_ac, int narcs,
+                                  const int* arc_ilabel, const int* arc_olabel, const float* arc_weight,
+                                  int nstates, const float* final_cost, int start_state, float lattice_beam,
+                                  int prune_interval, float prune_scale, int max_delay, int min_chunk, int nev,
+                                  const int* ev_type, const int* ev_arg) {
+  static thread_local std::string out;
+  API_TRY
+  Graph g;
+  g.ilabel.assign(arc_ilabel, arc_ilabel + narcs);
+  g.olabel.assign(arc_olabel, arc_olabel + narcs);
+  g.weight.assign(arc_weight, arc_weight + narcs);
+  g.final_cost.assign(final_cost, final_cost + nstates);
+  g.start = start_state;
+  IncrementalOptions o;
+  o.lattice_beam = lattice_beam;
+  o.prune_interval = prune_interval;
+  o.prune_scale = prune_scale;
+  o.determinize_max_delay = max_delay;
+  o.determinize_min_chunk_size = min_chunk;
+  o.det_max_mem = g_host_det_max_mem;
+  IncrementalLattice inc;
+  inc.Init(&g, &g_host_tid2phone, &g_host_tid_first, o);
+  // links per frame (link_frame ascending)
+  std::vector<std::vector<IncFrameIn::Link>> fl(std::max(nframes, 0));
+  for (int i = 0; i < nlink; i++) {
+    if (link_frame[i] < 0 || link_frame[i] >= nframes) VAMD_ERR("link frame out of range");
+    fl[link_frame[i]].push_back(IncFrameIn::Link{link_src[i], link_dst[i], link_arc[i], link_ac[i]});
+  }
+  auto add = [&](int k) {
+    IncFrameIn f;
+    f.state = tok_state + frame_begin[k];
+    f.cost = tok_cost + frame_begin[k];
+    f.ntok = frame_begin[k + 1] - frame_begin[k];
+    f.cost_offset = cost_offset[k];
+    f.links = fl[k].data();
+    f.nlinks = (int)fl[k].size();
+    inc.AddFrame(f);
+  };
+  std::ostringstream os;
+  os.precision(9);
+  os << "[";
+  bool firstq = true;
+  for (int e = 0; e < nev; e++) {
+    if (ev_type[e] == 0) {  // frames up to ev_arg decoded, then the AdvanceDecoding end
+      if (ev_arg[e] >= nframes) VAMD_ERR("event past the records");
+      while (inc.NumFramesDecoded() < ev_arg[e]) add(inc.NumFramesDecoded() + 1);
+      inc.AdvanceEnd();
+      continue;
+    }
+    WordLattice wl;
+    bool ok;
+    if (ev_type[e] == 1) {
+      ok = inc.GetLattice(inc.NumFramesInLattice(), false, &wl);
+    } else {
+      inc.FinalizeDecoding();
+      ok = inc.GetLattice(inc.NumFramesDecoded(), true, &wl);
+    }
+    os << (firstq ? "" : ", ") << "{\"nfl\": " << inc.NumFramesInLattice() << ", \"ok\": " << (ok ? 1 : 0)
+       << ", \"chunks\": " << inc.chunks() << ", \"arcs\": [";
+    firstq = false;
+    for (int s = 0; s < wl.NumStates(); s++) {
+      os << (s ? ", " : "") << "[";
+      for (size_t i = 0; i < wl.arcs[s].size(); i++) {
+        const auto& a = wl.arcs[s][i];
+        os << (i ? ", " : "") << "[" << a.word << ", " << a.next << ", " << a.graph << ", " << a.acoustic << ", [";
+        for (size_t j = 0; j < a.tids.size(); j++) os << (j ? ", " : "") << a.tids[j];
+        os << "]]";
+      }
+      os << "]";
+    }
+    os << "], \"finals\": [";
+    for (int s = 0; s < wl.NumStates(); s++) {
+      os << (s ? ", " : "");
+      if (wl.final_graph[s] == INFINITY) {
+        os << "null";
+        continue;
+      }
+      os << "[" << wl.final_graph[s] << ", " << wl.final_acoustic[s] << ", [";
+      for (size_t j = 0; j < wl.final_tids[s].size(); j++) os << (j ? ", " : "") << wl.final_tids[s][j];
+      os << "]]";
+    }
+    os << "]}";
+  }
+  os << "]";
+  out = os.str();
+  return out.c_str();
+  API_CATCH(nullptr)
 }
 
 float vamd_carpa_logprob(const char* g_carpa, int word, const int* hist, int nhist) {

@@ -143,6 +143,7 @@ RecognizerGroup* Model::AllocStreamSlot(int* slot) {
   cfg.device = DeviceFromEnv();
   cfg.max_step_samples = 4096;
   cfg.lattice = true;  // results come from the segment's lattice (MBR)
+  cfg.host_lattice = true;  // the incremental lattice reads the records as they come
   engines_.emplace_back(new RecognizerGroup(new Engine(md_, cfg)));
   *slot = engines_.back()->engine->AllocSlot();
   return engines_.back().get();
@@ -181,6 +182,7 @@ RecognizerGroup* Model::GrammarEngine(const std::string& grammar) {
   cfg.device = DeviceFromEnv();
   cfg.max_step_samples = 4096;
   cfg.lattice = true;
+  cfg.host_lattice = true;
   RecognizerGroup* grp = new RecognizerGroup(new Engine(md, cfg));
   grammar_engines_[grammar].reset(grp);
   return grp;
@@ -224,6 +226,7 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
     const std::vector<size_t>& run = !quiet.empty() ? quiet : busy;
     if (run.empty()) break;
     std::vector<int> sl, first;
+    std::vector<Recognizer*> sr;
     for (size_t i : run) {
       Recognizer* r = rs[i];
       const size_t n = r->req_wave_ ? r->req_wave_->size() : 0;
@@ -238,11 +241,15 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
         }
       }
       sl.push_back(r->slot_);
+      sr.push_back(r);
       first.push_back(r->frame_offset_ * 3);  // src/recognizer.cc:309, :825
     }
     if (sl.empty()) continue;
     engine->UpdateSilenceWeights(sl, first);
     engine->Advance(sl);
+    // each stream's AdvanceDecoding ended here: its incremental lattice runs
+    // UpdateLatticeDeterminization at this frame count (replayed lazily)
+    for (Recognizer* r : sr) r->adv_ends_.push_back(engine->NumFramesDecoded(r->slot_));
   }
   // EndpointDetected (src/recognizer.cc:318) of the AcceptWaveform requests
   std::vector<int> ep;
@@ -375,6 +382,7 @@ bool Recognizer::GetSpkVector(std::vector<float>* xvec, int* num_frames) {
 
 void Recognizer::CleanUp() {  // src/recognizer.cc:188-224
   frame_offset_ += engine_->NumFramesDecoded(slot_);
+  ResetLattice();  // a new decoder (InitDecoding)
   if (state_ == RECOGNIZER_FINALIZED || frame_offset_ > 20000) {
     samples_round_start_ += samples_processed_;
     samples_processed_ = 0;
@@ -433,6 +441,8 @@ bool Recognizer::Submit(const std::vector<float>* wave, bool final) {
 // as GetLattice does (phone + word pass, then words); false if unusable (overflow, determinization guard).  Then the
 // graph scale, and word alignment when the model has word_boundary.int
 // (WordAlignLattice, src/recognizer.cc:433-434; CopyLatticeForMbr otherwise).
+static void FinishWordLattice(WordLattice* wl, const ModelData& m, float graph_scale, bool rescore);
+
 static bool WordLatticeFromRaw(RawLattice& raw, const ModelData& m, float graph_scale, WordLattice* wl,
                                bool rescore) {
   if (raw.overflow || raw.tok_state.empty()) return false;
@@ -441,6 +451,17 @@ static bool WordLatticeFromRaw(RawLattice& raw, const ModelData& m, float graph_
   opt.lattice_beam = m.dec.lattice_beam;
   if (!DeterminizePhonePruned(raw, m.graph, m.tm.tid2phone, m.tm.tid2first, opt, wl) || wl->NumStates() == 0)
     return false;
+  FinishWordLattice(wl, m, graph_scale, rescore);
+  return true;
+}
+
+// After determinization: LM rescoring (final results), the graph scale, word
+// alignment when the model has word_boundary.int (WordAlignLattice /
+// WordAlignLatticePartial: the same aligner, a word cut at the lattice's end
+// forced out with its label; CopyLatticeForMbr otherwise)
+static void FinishWordLattice(WordLattice* wl, const ModelData& m, float graph_scale, bool rescore) {
+  LatticeOptions opt;
+  opt.lattice_beam = m.dec.lattice_beam;
   if (rescore && m.rescore) {  // src/recognizer.cc:680-711
     WordLattice r;
     if (RescoreLattice(*wl, *m.rescore, opt, &r)) *wl = std::move(r);
@@ -451,11 +472,10 @@ static bool WordLatticeFromRaw(RawLattice& raw, const ModelData& m, float graph_
     if (!WordAlignLattice(*wl, m.tid_boundary, m.tm.tid2final, m.tm.tid2selfloop, opt.max_states, &al) ||
         al.NumStates() == 0) {
       VAMD_WARN("word alignment failed; using the unaligned lattice");
-      return true;
+      return;
     }
     *wl = std::move(al);
   }
-  return true;
 }
 
 // The decoder segment's lattice (kept on the GPU) as a word lattice.
@@ -551,6 +571,101 @@ std::string Recognizer::WordsText(const std::vector<WordSeg>& w) const {
   return text.str();
 }
 
+// ---------------------------------------------------------------------------
+// The decoder segment's incremental lattice (incremental.h)
+// ---------------------------------------------------------------------------
+void Recognizer::ResetLattice() {
+  if (inc_init_) inc_.Reset();
+  adv_ends_.clear();
+  adv_done_ = 0;
+  inc_next_frame_ = 0;
+  inc_last_ = LatFrame{};
+  inc_bad_ = false;
+}
+
+bool Recognizer::SyncLattice() {
+  const ModelData& m = engine_->model();
+  if (!inc_init_) {
+    IncrementalOptions o;  // LatticeIncrementalDecoderConfig with the model's options
+    o.lattice_beam = m.dec.lattice_beam;
+    o.prune_interval = m.dec.prune_interval;
+    o.determinize_max_delay = m.dec.determinize_max_delay;
+    o.determinize_min_chunk_size = m.dec.determinize_min_chunk_size;
+    inc_.Init(&m.graph, &m.tm.tid2phone, &m.tm.tid2first, o);
+    inc_init_ = true;
+  }
+  if (inc_bad_) return false;
+  const int F = engine_->NumFramesDecoded(slot_);
+  if (F <= 0) return true;
+  if (adv_done_ >= adv_ends_.size()) return true;  // nothing new since the last replay
+  // the frames decoded since the last call, with one frame of overlap (the
+  // previous frame's arena offset checks that the records were not
+  // compacted by a pruning pass in between)
+  const int from = std::max(0, inc_next_frame_ - 1);
+  SegmentLattice sl;
+  engine_->CopySegmentTail(slot_, from, &sl);
+  if (sl.overflow || sl.frames.empty() || (int)sl.frames.size() + from - 1 < adv_ends_.back() ||
+      (inc_next_frame_ > 0 && (sl.frames[0].tok_base != inc_last_.tok_base || sl.frames[0].ntok != inc_last_.ntok ||
+                               sl.frames[0].link_begin != inc_last_.link_begin ||
+                               sl.frames[0].link_end != inc_last_.link_end))) {
+    VAMD_WARN("recognizer lattice records unusable (overflow or compacted): results from the best path");
+    inc_bad_ = true;
+    return false;
+  }
+  std::vector<int> st;
+  std::vector<float> co;
+  std::vector<IncFrameIn::Link> ln;
+  auto add = [&](int k) {
+    const LatFrame& fr = sl.frames[k - from];
+    const int a = fr.tok_base - sl.arena_base;
+    if (a < 0 || a + fr.ntok > (int)sl.arena.size()) VAMD_ERR("recognizer lattice: arena range");
+    st.resize(fr.ntok);
+    co.resize(fr.ntok);
+    for (int i = 0; i < fr.ntok; i++) {
+      const int4 e = sl.arena[a + i];
+      if (e.x == -2) VAMD_ERR("recognizer lattice: a dead token in Kaldi order");
+      st[i] = e.w;
+      co[i] = BitsToFloat(e.z);
+    }
+    ln.clear();
+    const long long lb = fr.link_begin - sl.link_base, le = fr.link_end - sl.link_base;
+    if (lb < 0 || le > (long long)sl.links.size()) VAMD_ERR("recognizer lattice: link range");
+    const int prev_base = k > 0 ? sl.frames[k - 1 - from].tok_base : 0;
+    for (long long i = lb; i < le; i++) {
+      const int4 r = sl.links[i];
+      const bool emit = m.graph.ilabel[r.z] != 0;
+      ln.push_back(IncFrameIn::Link{r.x - (emit ? prev_base : fr.tok_base), r.y - fr.tok_base, r.z,
+                                    BitsToFloat(r.w)});
+    }
+    IncFrameIn f;
+    f.state = st.data();
+    f.cost = co.data();
+    f.ntok = fr.ntok;
+    f.cost_offset = fr.cost_offset;
+    f.links = ln.data();
+    f.nlinks = (int)ln.size();
+    inc_.AddFrame(f);
+    inc_last_ = fr;
+    inc_next_frame_ = k + 1;
+  };
+  for (; adv_done_ < adv_ends_.size(); adv_done_++) {
+    const int c = adv_ends_[adv_done_];
+    while (inc_.NumFramesDecoded() < c) add(inc_.NumFramesDecoded() + 1);
+    inc_.AdvanceEnd();
+  }
+  return !inc_.failed();
+}
+
+// The incremental lattice after determinization -> MBR: rescoring, graph
+// scale, alignment, then Kaldi's MBR
+bool Recognizer::LatticeMbr(WordLattice&& wl, float graph_scale, bool rescore, MbrResult* r) const {
+  *r = MbrResult();
+  if (wl.NumStates() == 0) return false;
+  FinishWordLattice(&wl, engine_->model(), graph_scale, rescore);
+  MinimumBayesRisk(wl, r);
+  return true;
+}
+
 const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
   if (engine_->NumFramesDecoded(slot_) == 0) return StoreEmptyReturn();
   const ModelData& m = engine_->model();
@@ -561,8 +676,15 @@ const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
     for (size_t i = 0; i < words.size(); i++) text << (i ? " " : "") << m.words.Find(words[i]);
     return text.str();
   };
+  // FinalizeDecoding, then GetLattice(NumFramesDecoded(), true) over the
+  // incremental determinizer (:678); an unusable record set falls back to the
+  // one-shot lattice / best path of the segment
+  WordLattice clat;
+  const bool inc = SyncLattice() && (inc_.FinalizeDecoding(), inc_.GetLattice(inc_.NumFramesDecoded(), true, &clat));
+  if (inc && clat.NumStates() == 0) return StoreEmptyReturn();  // (rlat.Start() != 0, :714-716)
   if (max_alternatives_ == 0) {  // MbrResult, :429-482
-    const MbrResult r = SegmentMbr(engine_, slot_, m, true, 0.9f, true);
+    MbrResult r;
+    if (!inc || !LatticeMbr(std::move(clat), 0.9f, true, &r)) r = SegmentMbr(engine_, slot_, m, true, 0.9f, true);
     Json obj;
     for (size_t i = 0; i < r.words.size(); i++) {
       if (!words_) continue;
@@ -588,7 +710,15 @@ const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
   // paths of the graph-scaled word lattice, likelihood = -(graph + acoustic)
   std::vector<NbestPath> nb;
   WordLattice wl;
-  if (SegmentWordLattice(engine_, slot_, m, true, 0.9f, &wl, true)) {
+  bool have = false;
+  if (inc) {
+    wl = std::move(clat);
+    FinishWordLattice(&wl, m, 0.9f, true);
+    have = true;
+  } else {
+    have = SegmentWordLattice(engine_, slot_, m, true, 0.9f, &wl, true);
+  }
+  if (have) {
     NbestPaths(wl, max_alternatives_, &nb);
   } else {
     std::vector<PathResult> pr;
@@ -640,8 +770,25 @@ const char* Recognizer::PartialResult() {  // src/recognizer.cc:732-806
     return StoreReturn(res.Dump());
   }
   const ModelData& m = engine_->model();
-  if (partial_words_) {  // MBR over the partial lattice, no final costs, no graph scale (:740-780)
-    const MbrResult r = SegmentMbr(engine_, slot_, m, false, 1.0f);
+  if (partial_words_) {
+    // the frames the incremental determinizer has covered: "" until its
+    // first chunk, then MBR over GetLattice(NumFramesInLattice(), false)
+    // word-aligned (WordAlignLatticePartial), no graph scale (:740-780)
+    MbrResult r;
+    if (SyncLattice()) {
+      if (inc_.NumFramesInLattice() == 0) {
+        res["partial"] = Json::Str("");
+        return StoreReturn(res.Dump());
+      }
+      WordLattice clat;
+      if (inc_.GetLattice(inc_.NumFramesInLattice(), false, &clat)) {
+        LatticeMbr(std::move(clat), 1.0f, false, &r);
+      } else {
+        r = SegmentMbr(engine_, slot_, m, false, 1.0f);
+      }
+    } else {
+      r = SegmentMbr(engine_, slot_, m, false, 1.0f);
+    }
     const double shift = 0.01 * m.dcb.frame_subsampling_factor;
     std::ostringstream text;
     for (size_t i = 0; i < r.words.size(); i++) {

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "incremental.h"
 #include "xvector.h"
 #include "json_out.h"
 
@@ -142,6 +143,16 @@ class Recognizer {
   friend struct RecognizerGroup;
   // AcceptWaveform / FinalResult through the group's batched pass
   bool Submit(const std::vector<float>* wave, bool final);
+  // The decoder segment's incremental lattice (incremental.h): the group's
+  // passes record every AdvanceDecoding end (the segment's decoded frames
+  // after it); SyncLattice copies the frames decoded since the last call and
+  // replays those ends on them.  False if the records are unusable (lattice
+  // overflow): the results fall back to the best path.
+  bool SyncLattice();
+  void ResetLattice();
+  // the MBR of an incremental lattice (graph scale, rescoring, alignment as
+  // the reference's GetResult / PartialResult); false: empty lattice
+  bool LatticeMbr(WordLattice&& wl, float graph_scale, bool rescore, MbrResult* r) const;
 
   Model* model_;
   RecognizerGroup* group_ = nullptr;
@@ -158,7 +169,12 @@ class Recognizer {
   int frame_offset_ = 0;
   long long samples_processed_ = 0, samples_round_start_ = 0;
   RecognizerState state_ = RECOGNIZER_INITIALIZED;
-  bool finalized_decoder_ = false;
+  IncrementalLattice inc_;
+  bool inc_init_ = false, inc_bad_ = false;
+  std::vector<int> adv_ends_;  // AdvanceDecoding ends of the segment (decoded frames)
+  size_t adv_done_ = 0;        // ends replayed
+  int inc_next_frame_ = 0;     // the next frame record to ingest
+  LatFrame inc_last_{};        // the last ingested frame's record (a compaction check)
   std::string last_result_;
   std::vector<float> resample_buf_;
   SpkModel* spk_ = nullptr;

@@ -69,6 +69,9 @@ _SIGS = {
     "vamd_batch_recognizer_lane": (C.c_int, [_vp]),
     "vamd_batch_result_profile": (C.c_int, [_vp, _vp]),
     "vamd_admission_replay": (C.c_int, [C.c_int, _vp, C.c_int, _vp, _vp]),
+    "vamd_incremental_json": (C.c_char_p, [C.c_int] + [_vp] * 4 + [C.c_int] + [_vp] * 5 + [C.c_int] + [_vp] * 3 +
+                              [C.c_int, _vp, C.c_int, C.c_float, C.c_int, C.c_float, C.c_int, C.c_int, C.c_int,
+                               _vp, _vp]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(_c, _name)
@@ -190,6 +193,42 @@ def lattice_words(L, arc_ilabel, arc_olabel, lattice_beam=6.0, graph_scale=0.9, 
     if not timings:
         d.pop("ms", None)  # host stage times (vary run to run)
     return d
+
+
+def incremental_lattice(frames, graph, events, lattice_beam=6.0, prune_interval=25, prune_scale=0.01,
+                        max_delay=60, min_chunk=20):
+    """Host-only: the KaldiRecognizer's incremental lattice (csrc/incremental.h)
+    over per-frame records [(states, costs, links [(src, dst, arc, ac)],
+    cost_offset)] (tests/oracle_incremental.frames_from_oracle), driven by
+    events [(0, frames) | (1, None) | (2, None)]; returns one dict per query
+    (1: the partial lattice, 2: the final one): {nfl, ok, chunks, arcs,
+    finals}.  Phones from vamd_lattice_set_phones."""
+    import json
+    fb = np.zeros(len(frames) + 1, np.int32)
+    fb[1:] = np.cumsum([len(f[0]) for f in frames])
+    ts = np.ascontiguousarray(np.concatenate([f[0] for f in frames]) if frames else np.zeros(0), np.int32)
+    tc = np.ascontiguousarray(np.concatenate([f[1] for f in frames]) if frames else np.zeros(0), np.float32)
+    co = np.ascontiguousarray([f[3] for f in frames], np.float32)
+    lk = [(k, *l) for k, f in enumerate(frames) for l in f[2]]
+    lf = np.ascontiguousarray([l[0] for l in lk] or [0], np.int32)
+    ls = np.ascontiguousarray([l[1] for l in lk] or [0], np.int32)
+    ld = np.ascontiguousarray([l[2] for l in lk] or [0], np.int32)
+    la = np.ascontiguousarray([l[3] for l in lk] or [0], np.int32)
+    lx = np.ascontiguousarray([l[4] for l in lk] or [0], np.float32)
+    il = np.ascontiguousarray(graph.ilabel, np.int32)
+    ol = np.ascontiguousarray(graph.olabel, np.int32)
+    w = np.ascontiguousarray(graph.weight, np.float32)
+    fin = np.ascontiguousarray(graph.final, np.float32)
+    et = np.ascontiguousarray([e[0] for e in events] or [0], np.int32)
+    ea = np.ascontiguousarray([e[1] if e[1] is not None else 0 for e in events] or [0], np.int32)
+    r = _c.vamd_incremental_json(len(frames), fb.ctypes.data, ts.ctypes.data, tc.ctypes.data, co.ctypes.data,
+                                 len(lk), lf.ctypes.data, ls.ctypes.data, ld.ctypes.data, la.ctypes.data,
+                                 lx.ctypes.data, len(il), il.ctypes.data, ol.ctypes.data, w.ctypes.data,
+                                 len(fin), fin.ctypes.data, int(graph.start), lattice_beam, prune_interval,
+                                 prune_scale, max_delay, min_chunk, len(events), et.ctypes.data, ea.ctypes.data)
+    if r is None:
+        raise RuntimeError("vamd_incremental_json failed: " + _err())
+    return json.loads(r.decode())
 
 
 def silence_weighting_run(calls, tid_is_silence, silence_weight=1e-3, fss=3):
