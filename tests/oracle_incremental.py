@@ -598,3 +598,105 @@ def frames_from_oracle(r, graph):
         out.append((np.asarray(ts[fb[k]:fb[k + 1]], np.int32), np.asarray(tc[fb[k]:fb[k + 1]], np.float32),
                     per[k], F32(L["cost_offset"][k])))
     return out
+
+
+# ------------------------------------------------- the recognizer's outputs
+def final_result(o, wave, chunk=4000, rescore=None, nbest_n=0, on=None):
+    """The FinalResult of a stream fed `chunk`-sample calls without endpoints
+    (the incremental chain of recognizer_run): {mbr: {words, conf, times in
+    frames}, nbest: [...] (nbest_n > 0)}; rescore: (W, Fi) -> (W, Fi) | None
+    (LM rescoring of the final lattice before the graph scale)."""
+    detail = []
+    recognizer_run(o, wave, chunk=chunk, endpoints=False, rescore=rescore, nbest_n=nbest_n, detail=detail, on=on)
+    return detail[-1]
+
+
+def recognizer_run(o, wave, chunk=4000, partial_words=False, endpoints=True, rescore=None, nbest_n=0,
+                   detail=None, on=None):
+    """The outputs of the reference's test_simple.py loop (python/example):
+    per AcceptWaveform call of `chunk` samples either Result() (the call
+    returned 1: an endpoint) or PartialResult(), then FinalResult().  Each
+    output: ("partial" | "result", words [(word id, start, end, conf)],
+    text ids) with times in seconds (frame offset of the segment included);
+    a partial without partial words carries conf None (best path, no times).
+    Decoding: oracle_py.OracleModel.online (pieces, silence weighting,
+    endpoints); each decoder segment is decoded once with its lattice records
+    and probes at the calls' ends (GetBestPath(false) of a partial).  The
+    incremental lattice replays the segment's AdvanceDecoding ends."""
+    import os
+    if on is None:  # (a caller's own online(wave, chunk, endpoints=endpoints) run)
+        on = o.online(wave, chunk=chunk, endpoints=endpoints)
+    llh, calls = on["llh"], on["calls"]
+    segs = on["segments"] if endpoints else [(0, len(llh))]
+    hs = on["segment_hash_sizes"] if endpoints else [0]
+    g = o.graph
+    first = OL.tid_first(o.tm)
+    wb = os.path.join(o.dir, "graph", "phones", "word_boundary.int")
+    tables = OL.align_tables(o.tm, wb) if os.path.exists(wb) else None
+    shift = 0.01 * o.fss
+    out = []
+    by_seg = {}
+    for c in calls:
+        by_seg.setdefault(c["segment"], []).append(c)
+    for si, (s0, s1) in enumerate(segs):
+        cs = by_seg.get(si, [])
+        probes = sorted(set(c["pieces"][-1] - s0 for c in cs if c["pieces"] and c["pieces"][-1] > s0))
+        r = None
+        if s1 > s0:
+            r = g.decode(llh[s0:s1], o.beam, o.max_active, o.min_active, o.beam_delta, True, lattice=True, kaldi=True,
+                         hash_size=hs[si], probes=probes or None)
+        frames = frames_from_oracle(r, g) if r is not None else []
+        pr = dict(zip(probes, r["probes"])) if (r is not None and probes) else {}
+        inc = IncrementalLattice(g, o.tm.tid2phone, first)
+
+        def words_of(W, Fi, scale, resc=None):
+            if resc is not None:
+                rr = resc(W, Fi)
+                if rr is not None:
+                    W, Fi = rr
+            if scale != 1.0:
+                W, Fi = OL.scale_graph(W, Fi, scale)
+            if tables is not None:
+                W, Fi = OL.word_align(W, Fi, tables)
+            mb = OL.mbr(W, Fi)
+            return [(w, (s0 + a) * shift, (s0 + b) * shift, c) for w, (a, b), c in
+                    zip(mb["words"], mb["times"], mb["conf"])], W, Fi
+
+        for c in cs:
+            for d in c["pieces"]:
+                while inc.num_decoded() < d - s0:
+                    k = inc.num_decoded() + 1
+                    inc.add_frame(*frames[k][:2], frames[k][2], frames[k][3])
+                inc.advance_end()
+            n = (c["pieces"][-1] if c["pieces"] else s0) - s0
+            if c["endpoint"] or c["final"]:
+                W = Fi = None
+                if n > 0:
+                    inc.finalize()
+                    W, Fi = inc.get_lattice(inc.num_decoded(), True)
+                if not W:
+                    out.append(("result", [], []))
+                    if detail is not None:
+                        detail.append(dict(mbr=dict(words=[], conf=[], times=[]), nbest=[]))
+                    continue
+                ws, W2, Fi2 = words_of(W, Fi, 0.9, rescore)
+                out.append(("result", ws, [w[0] for w in ws]))
+                if detail is not None:
+                    mb = OL.mbr(W2, Fi2)
+                    detail.append(dict(mbr=mb, nbest=OL.nbest(W2, Fi2, nbest_n) if nbest_n else []))
+                continue
+            if n == 0:
+                out.append(("partial", [], []))
+                continue
+            if partial_words:
+                if inc.nil == 0:
+                    out.append(("partial", [], []))
+                    continue
+                W, Fi = inc.get_lattice(inc.nil, False)
+                ws = words_of(W, Fi, 1.0)[0] if W else []
+                out.append(("partial", ws, [w[0] for w in ws]))
+                continue
+            path = pr[n][0]
+            ids = [int(g.olabel[a]) for a in path if int(g.olabel[a]) != 0]
+            out.append(("partial", [(w, None, None, None) for w in ids], ids))
+    return out

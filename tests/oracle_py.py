@@ -851,11 +851,14 @@ class OracleModel:
             calls.append([n + j + min(step, m - j) for j in range(0, m, step)])
             n += m
         calls.append(None)  # FinalResult
+        call_log = []
         for call in calls:
             if call is not None and reset_next:  # CleanUp: InitDecoding, new OnlineSilenceWeighting
                 seg0, reset_next = dec, False
                 hs_seg = hs_last
                 sw = SilenceWeighting(lambda tid: int(tm.tid2phone[tid]) in sil, 1e-3, fss)
+            log = dict(segment=len(segs), seg0=seg0, pieces=[], endpoint=False, final=call is None)
+            call_log.append(log)
             for n, fin in ([(x, False) for x in call] if call is not None else [(len(wave), True)]):
                 n_out = n if rate == model_rate else resample_num_outputs(rate, model_rate, n, fin)
                 T = mfcc_num_frames(n_out, self.mfcc_conf, self.fbank)
@@ -898,6 +901,7 @@ class OracleModel:
                     nf = self.nnet_features(feats)
                     ivt, t0 = self._ivec_of_time(T, len(ivecs))
                     llh = self.net.forward(nf, ivecs, ivt, t0)[:dec]
+                log["pieces"].append(dec)  # an AdvanceDecoding ends here
             if endpoints and call is not None and dec > seg0:
                 r = self.decode_llh(llh[seg0:dec], use_final=False, hash_size=hs_seg)
                 hs_last = r["hash_size"]
@@ -906,12 +910,13 @@ class OracleModel:
                     segs.append((seg0, dec))
                     seg_hash.append(hs_seg)
                     reset_next = True
+                    log["endpoint"] = True
         if endpoints:
             segs.append((seg0, dec))
             seg_hash.append(hs_seg)
         r = self.decode_llh(llh[seg0:], hash_size=hs_seg) if endpoints else self.decode_llh(llh)
         return dict(ivectors=ivecs, llh=llh, decode=r, requests=reqs, entries=ents, segments=segs,
-                    segment_hash_sizes=seg_hash)
+                    segment_hash_sizes=seg_hash, calls=call_log)
 
     def recognize(self, wave):
         r = self.decode_llh(self.loglikes(wave))

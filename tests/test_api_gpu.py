@@ -26,8 +26,10 @@ def _pcm(x):
 
 
 def _oracle_mbr(oracle, wave, chunk):
-    import oracle_lattice as OL
-    return OL.results(oracle, oracle.online(wave, chunk=chunk)["llh"])["mbr"]
+    # the recognizer's final result: the incremental determinizer's lattice
+    # (src/recognizer.cc:678; tests/oracle_incremental.py)
+    import oracle_incremental as OI
+    return OI.final_result(oracle, wave, chunk)["mbr"]
 
 
 def _oracle_mbr_text(oracle, wave, batch=False):
@@ -166,10 +168,10 @@ def test_alternatives_and_nlsml_from_lattice(vosk_mod, synth_model_noep, test_wa
     """SetMaxAlternatives: the n-best word sequences of the segment's lattice
     with likelihood -(graph + acoustic) (NbestResult, src/recognizer.cc:526-
     607); NLSML carries the same texts and likelihoods (:609-667)."""
-    import oracle_lattice as OL
+    import oracle_incremental as OI
     oracle = oracle_py.OracleModel(synth_model_noep)
     x = test_wave[:16000 * 5]
-    nb = OL.results(oracle, oracle.online(x, chunk=4000)["llh"], nbest_n=3)["nbest"]
+    nb = OI.final_result(oracle, x, 4000, nbest_n=3)["nbest"]
     m = vosk_mod.Model(synth_model_noep)
     outs = {}
     for nlsml in (False, True):

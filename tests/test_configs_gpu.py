@@ -129,7 +129,7 @@ def test_config4_256_batch_recognizers_on_a_7m_state_hclg(synth_bigram_8m, test_
 
 # ---------------------------------------------------------------- config 5
 def _spk_expected_job(i):
-    import oracle_lattice as OL
+    import oracle_incremental as OI
     o, ox, sil = _ORC["o"], _ORC["ox"], _ORC["sil"]
     w = _ORC["waves"][i]
     on = o.online(w, chunk=4000)
@@ -137,7 +137,8 @@ def _spk_expected_job(i):
     g, tm = o.graph, o.tm
     keep = [0 if int(tm.tid2phone[g.ilabel[a]]) in sil else 1 for a in dec["path"] if g.ilabel[a] != 0]
     ref, nr = ox.xvector(w, 0, keep)
-    mb = OL.results(o, on["llh"])["mbr"]  # the final result's text: MBR over the segment's lattice
+    # the final result's text: MBR over the incremental determinizer's lattice
+    mb = OI.final_result(o, w, 4000, on=on)["mbr"]
     return " ".join(o.words[x] for x in mb["words"]), (None if ref is None else ref.astype(np.float64)), nr
 
 

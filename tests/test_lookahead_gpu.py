@@ -73,8 +73,8 @@ def _final_text(vosk_mod, model, wave, grammar=None):
 
 
 def _oracle_text(oracle, wave):
-    import oracle_lattice as OL
-    mb = OL.results(oracle, oracle.online(wave, chunk=4000)["llh"])["mbr"]
+    import oracle_incremental as OI  # the recognizer's incremental lattice
+    mb = OI.final_result(oracle, wave, 4000)["mbr"]
     return " ".join(oracle.words[w] for w in mb["words"])
 
 

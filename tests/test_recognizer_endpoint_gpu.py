@@ -5,14 +5,15 @@ rules fire every few seconds.  Every Result() taken when AcceptWaveform
 returns 1, and the FinalResult, equals the oracle's MBR over the same
 decoder segment (oracle_py.OracleModel.online(endpoints=True): the rules
 after every call, decoder and silence weighting restarted at the next call,
-features and i-vector statistics continuing), with the segment's times."""
+features and i-vector statistics continuing), with the segment's times (the segment's lattice: the incremental
+determinizer's, tests/oracle_incremental.py)."""
 import json
 
 import numpy as np
 import pytest
 
 from conftest import perturbed_stream
-import oracle_lattice as OL
+import oracle_incremental as OI
 import oracle_py
 
 pytestmark = pytest.mark.gpu
@@ -31,11 +32,11 @@ def test_recognizer_endpoint_segments_match_oracle(synth_model_ep, test_wave, se
     on = o.online(wave, chunk=4000, endpoints=True)
     segs = on["segments"]
     assert len(segs) >= 3  # the rules fire
-    exp = []
-    for (s0, s1), hs in zip(segs, on["segment_hash_sizes"]):
-        mb = OL.results(o, on["llh"][s0:s1], hash_size=hs)["mbr"]
-        exp.append((" ".join(o.words[w] for w in mb["words"]),
-                    [((s0 + a) * 0.03, (s0 + b) * 0.03) for a, b in mb["times"]]))
+    # each segment's Result: the incremental determinizer's lattice over the
+    # segment (FinalizeDecoding + GetLattice, tests/oracle_incremental.py)
+    exp = [(" ".join(o.words[w] for w in ids), [(a, b) for _, a, b, _ in ws])
+           for kind, ws, ids in OI.recognizer_run(o, wave, chunk=4000, on=on) if kind == "result"]
+    assert len(exp) == len(segs)
     m = vosk.Model(synth_model_ep)
     rec = vosk.KaldiRecognizer(m, 16000)
     rec.SetWords(True)

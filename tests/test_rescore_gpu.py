@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 
 import kaldi_formats as kf
-import oracle_lattice as OL
+import oracle_incremental as OI
+import oracle_lattice as OL  # noqa: F401
 import oracle_py
 import oracle_rescore as ORS
 
@@ -31,8 +32,9 @@ def test_recognizer_rescored_result_matches_oracle(synth_model_rescore, test_wav
         for i in range(0, len(data), 8000):
             assert rec.AcceptWaveform(data[i:i + 8000]) == 0
         final = json.loads(rec.FinalResult())
-        llh = oracle.online(wave, chunk=4000)["llh"]
-        mb = OL.results(oracle, llh, rescore=lambda W, Fi: ORS.rescore(W, Fi, G, lm))["mbr"]
+        on = oracle.online(wave, chunk=4000)
+        resc = lambda W, Fi: ORS.rescore(W, Fi, G, lm)  # noqa: E731
+        mb = OI.final_result(oracle, wave, 4000, rescore=resc, on=on)["mbr"]
         assert final["text"] == " ".join(oracle.words[w] for w in mb["words"])
         for w, c, (tb, te) in zip(final.get("result", []), mb["conf"], mb["times"]):
             assert w["conf"] == pytest.approx(c, abs=1e-5)
@@ -44,5 +46,5 @@ def test_recognizer_rescored_result_matches_oracle(synth_model_rescore, test_wav
         for i in range(0, len(data), 8000):
             rec.AcceptWaveform(data[i:i + 8000])
         alts = json.loads(rec.FinalResult())["alternatives"]
-        nb = OL.results(oracle, llh, rescore=lambda W, Fi: ORS.rescore(W, Fi, G, lm), nbest_n=3)["nbest"]
+        nb = OI.final_result(oracle, wave, 4000, rescore=resc, nbest_n=3, on=on)["nbest"]
         assert [a["text"] for a in alts] == [" ".join(oracle.words[w] for w in x["words"]) for x in nb]

@@ -1939,8 +1939,12 @@ void SegmentCopy::Finish(SegmentLattice* out) {
   out->links.clear();
   out->overflow = overflow;
   if (!batch) return;
+  int prev = -1;  // the caller's current device is restored (a waiting caller may run this)
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
   (void)hipSetDevice(batch->device);
-  HIPCHECK(hipEventSynchronize(batch->done));
+  const hipError_t se = hipEventSynchronize(batch->done);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  HIPCHECK(se);
   const char* block = batch->block;
   const LatFrame* F = (const LatFrame*)(block + f);
   const int4* A = (const int4*)(block + a);

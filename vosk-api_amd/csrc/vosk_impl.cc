@@ -879,6 +879,25 @@ void WorkerPool::WaitIdle() {
   idle_cv_.wait(lk, [&] { return tasks_.empty() && busy_ == 0; });
 }
 
+// A task's end, also when it throws: busy_ back down (WaitIdle would block
+// for ever otherwise) and the caller's current HIP device restored (a task
+// may switch devices: SegmentCopy::Finish of a lane on another GPU).
+struct WorkerPool::TaskScope {
+  WorkerPool* p;
+  int dev = -1;
+  explicit TaskScope(WorkerPool* pool) : p(pool) {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  ~TaskScope() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+    {
+      std::lock_guard<std::mutex> lk(p->mu_);
+      p->busy_--;
+    }
+    p->idle_cv_.notify_all();
+  }
+};
+
 bool WorkerPool::RunOne() {
   std::function<void()> t;
   {
@@ -888,12 +907,8 @@ bool WorkerPool::RunOne() {
     tasks_.pop_front();
     busy_++;
   }
+  TaskScope scope(this);
   t();
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    busy_--;
-  }
-  idle_cv_.notify_all();
   return true;
 }
 
@@ -908,12 +923,12 @@ void WorkerPool::Run() {
       tasks_.pop_front();
       busy_++;
     }
-    t();
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      busy_--;
+    TaskScope scope(this);
+    try {
+      t();
+    } catch (const std::exception& e) {  // (tasks publish their own failures)
+      VAMD_WARN("result worker task failed: " << e.what());
     }
-    idle_cv_.notify_all();
   }
 }
 

@@ -212,6 +212,7 @@ class WorkerPool {
 
  private:
   void Run();
+  struct TaskScope;
   std::mutex mu_;
   std::condition_variable cv_, idle_cv_;
   std::deque<std::function<void()>> tasks_;
