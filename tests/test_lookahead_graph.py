@@ -263,3 +263,38 @@ def test_lookahead_pushing_is_exercised(synth_lookahead):
     assert pushed.sum() > 0
     frac = (c.olabel == 0) & (c.ilabel != 0) & (c.weight != 0) & (np.abs(c.weight) < 50)
     assert frac.sum() > 0
+
+
+def test_lazy_numbering_hand_built(lib, synth_lookahead, tmp_path):
+    """OpenFST's lazy ComposeFst numbering order on the hand-built pair of
+    test_lookahead_pushing_known_answer, worked by hand from the model
+    graph_compose.cc implements: ComposeFstImpl::Expand -> OrderedExpand
+    over HCLr's arcs (MATCH_BOTH resolved to matching G's input, as
+    ComposeFstImpl::MatchInput does when HCLr's state has no more arcs than
+    G's): first the "loop" -- G's epsilon (backoff) arcs against HCLr's
+    implicit self-loop --, then each HCLr arc in arc order against G (an
+    output-epsilon arc against G's implicit loop, with the lookahead /
+    pushing filters; with a pushed label pending only the arcs towards it).
+    States (by their arcs): A = (h0, G0) start, B = (h1, G0) after 'a' with
+    the pushed weight, C = (h3, G1) with w3 pending, D = (h2, G0) with w2
+    pending, E = (h0, G1), F = (h1, G0) with w1 pending.  Destinations in
+    composition order: A: B C; B: D A; C: E; D: A; E: A F (G1's backoff
+    first, then 'a' with w1 pushed); F: A.  This pins the lazy table
+    (vamd_graph_lazy) independently of the oracle, which decodes with the
+    same table; that OpenFST resolves MATCH_BOTH to this side on every
+    state is this restatement's reading, unpinned."""
+    d, hcl, g = _tiny_pair(synth_lookahead, str(tmp_path / "m"))
+    c = _cgraph(lib, d)
+    assert c is not None and c.num_states == 6
+    sig = {}
+    for s in range(c.num_states):
+        sig[s] = tuple(sorted(zip(c.ilabel[c.row[s]:c.row[s + 1]].tolist(),
+                                  c.olabel[c.row[s]:c.row[s + 1]].tolist())))
+    names = {((1, 0), (5, 3)): "A", ((2, 1), (3, 2)): "B", ((6, 0),): "C", ((4, 0),): "D",
+             ((0, 0), (1, 1)): "E", ((2, 0),): "F"}
+    name = {s: names[sig[s]] for s in range(c.num_states)}
+    assert name[c.start] == "A"
+    lrow, lnext, nids = c.lazy
+    assert nids == c.num_states  # no dead state in this composition
+    got = {name[s]: "".join(name[int(t)] for t in lnext[lrow[s]:lrow[s + 1]]) for s in range(c.num_states)}
+    assert got == {"A": "BC", "B": "DA", "C": "E", "D": "A", "E": "AF", "F": "A"}

@@ -214,6 +214,8 @@ class SlotGroupCommit {
     done_.assign(slots, 0);
     err_.assign(slots, nullptr);
     owner_.assign(slots, std::thread::id());
+    served_.assign(slots, std::chrono::steady_clock::time_point{});
+    gap_us_.assign(slots, -1.0);
   }
   void SetWindowUs(int us) { window_us_ = us; }
   template <class BatchFn>
@@ -223,6 +225,14 @@ class SlotGroupCommit {
     pending_.push_back(slot);
     owner_[slot] = std::this_thread::get_id();
     timed_out_.erase(slot);
+    // the caller's gap between being served and posting again (a running
+    // mean): a caller that does host work between its calls (e.g. a
+    // PartialResult after every AcceptWaveform) longer than the window is not
+    // waited for -- each batch would otherwise wait the whole window for it
+    if (done_[slot] > 0) {
+      const double g = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - served_[slot]).count();
+      gap_us_[slot] = gap_us_[slot] < 0 ? g : 0.5 * gap_us_[slot] + 0.5 * g;
+    }
     if (leader_ && waiting_) cv_lead_.notify_one();
     while (done_[slot] < ticket) {
       if (leader_) {
@@ -264,11 +274,14 @@ class SlotGroupCommit {
           err_[batch[i]] = e;
         }
         // the streams to wait for next time: those served, except one that
-        // never came back within the last window (its caller stopped)
-        last_.clear();
-        for (int s : batch)
-          if (!timed_out_.count(s)) last_.push_back(s);
+        // never came back within the last window (its caller stopped) or
+        // whose caller usually comes back later than the window
         last_end_ = std::chrono::steady_clock::now();
+        last_.clear();
+        for (int s : batch) {
+          served_[s] = last_end_;
+          if (!timed_out_.count(s) && gap_us_[s] < (double)window_us_) last_.push_back(s);
+        }
         cv_.notify_all();
       }
       leader_ = false;
@@ -296,6 +309,8 @@ class SlotGroupCommit {
   std::vector<int> last_;
   std::set<int> timed_out_;
   std::chrono::steady_clock::time_point last_end_{};
+  std::vector<std::chrono::steady_clock::time_point> served_;  // per stream: end of its last batch
+  std::vector<double> gap_us_;  // per stream: running mean of served -> next post (-1: none yet)
 };
 
 class Engine {

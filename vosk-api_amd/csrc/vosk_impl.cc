@@ -1159,10 +1159,11 @@ void BatchModel::Push(BatchRecognizer* r, std::vector<float>&& chunk, bool last)
     L->queued++;
     r->ended_ = last;  // a chunk after FinishStream starts a new utterance
     // a lane waiting for the rest of a feeding round polls every millisecond
-    // and is released by Wait(): a push wakes it only when every stream of
-    // the lane has a chunk queued (the round's usual completion) -- a wake per
-    // push made the lane and the feeding thread take turns on the lock
-    wake = !L->round_wait || L->streams_queued >= (int)L->recs.size();
+    // and is released by Wait(): a push wakes it only when the round it waits
+    // for is complete (the lane's own predicate; an idle, ended or slower
+    // stream does not hold it back) -- a wake per push made the lane and the
+    // feeding thread take turns on the lock
+    wake = !L->round_wait || !RoundIncomplete(L->recs);
   }
   if (wake) L->cv.notify_one();
 }
