@@ -86,6 +86,17 @@ void IncrementalLattice::Reset() {
 // ---------------------------------------------------------------------------
 // token bookkeeping (LatticeIncrementalDecoderTpl)
 // ---------------------------------------------------------------------------
+template <class F>
+void IncrementalLattice::ForLinks(int t, F&& f) {
+  const HTok& tk = toks_[t];
+  HFrame& fr = frames_[tk.frame];
+  if (!fr.emit_begin.empty())
+    for (int i = fr.emit_begin[tk.local]; i < fr.emit_begin[tk.local + 1]; i++)
+      if (fr.emit[i].arc >= 0) f(fr.emit[i]);
+  for (int i = fr.eps_begin[tk.local]; i < fr.eps_begin[tk.local + 1]; i++)
+    if (fr.eps[i].arc >= 0) f(fr.eps[i]);
+}
+
 void IncrementalLattice::AddFrame(const IncFrameIn& in) {
   const int k = (int)frames_.size();
   if (k > 0) {
@@ -94,29 +105,48 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
     if (opt_.prune_interval > 0 && (k - 1) % opt_.prune_interval == 0) PruneActiveTokens(Delta());
     frames_[k - 1].cost_offset = in.cost_offset;
   }
-  const int first_prev = k > 0 ? frames_[k - 1].first : 0;
   frames_.emplace_back();
   HFrame& fr = frames_.back();
   const int base = (int)toks_.size();
   fr.first = base;
   fr.toks.reserve(in.ntok);
   for (int i = 0; i < in.ntok; i++) {
-    toks_.push_back(HTok{in.state[i], in.cost[i], 0.0f, true, {}});
+    toks_.push_back(HTok{in.state[i], in.cost[i], 0.0f, true, k, i});
     fr.toks.push_back(base + i);
   }
+  // split the links: emitting ones belong to the previous frame's tokens
+  const int prev_n = k > 0 ? base - frames_[k - 1].first : 0;
+  std::vector<int> ce(prev_n + 1, 0), cp(in.ntok + 1, 0);
   for (int i = 0; i < in.nlinks; i++) {
     const IncFrameIn::Link& l = in.links[i];
     const bool emit = g_->ilabel[l.arc] != 0;
     if (emit && k == 0) VAMD_ERR("incremental lattice: an emitting link into frame 0");
-    const int src = (emit ? first_prev : base) + l.src, dst = base + l.dst;
-    if (src < 0 || src >= (int)toks_.size() || dst < base || dst >= (int)toks_.size())
+    if (l.dst < 0 || l.dst >= in.ntok || l.src < 0 || l.src >= (emit ? prev_n : in.ntok))
       VAMD_ERR("incremental lattice: link to a missing token");
-    toks_[src].links.push_back(HLink{dst, l.arc, g_->weight[l.arc], emit ? l.ac : 0.0f});
+    (emit ? ce : cp)[l.src + 1]++;
+  }
+  for (int i = 0; i < prev_n; i++) ce[i + 1] += ce[i];
+  for (int i = 0; i < in.ntok; i++) cp[i + 1] += cp[i];
+  std::vector<HLink> em(ce[prev_n]), ep(cp[in.ntok]);
+  {
+    std::vector<int> fe(ce.begin(), ce.end() - 1), fp(cp.begin(), cp.end() - 1);
+    for (int i = 0; i < in.nlinks; i++) {
+      const IncFrameIn::Link& l = in.links[i];
+      const bool emit = g_->ilabel[l.arc] != 0;
+      const HLink h{base + l.dst, l.arc, g_->weight[l.arc], emit ? l.ac : 0.0f};
+      if (emit) em[fe[l.src]++] = h;
+      else ep[fp[l.src]++] = h;
+    }
   }
   auto by_arc = [](const HLink& a, const HLink& b) { return a.arc < b.arc; };
-  if (k > 0)
-    for (int t : frames_[k - 1].toks) std::sort(toks_[t].links.begin(), toks_[t].links.end(), by_arc);
-  for (int t : fr.toks) std::sort(toks_[t].links.begin(), toks_[t].links.end(), by_arc);
+  for (int i = 0; i < prev_n; i++) std::sort(em.begin() + ce[i], em.begin() + ce[i + 1], by_arc);
+  for (int i = 0; i < in.ntok; i++) std::sort(ep.begin() + cp[i], ep.begin() + cp[i + 1], by_arc);
+  fr.eps.swap(ep);
+  fr.eps_begin.swap(cp);
+  if (k > 0) {
+    frames_[k - 1].emit.swap(em);
+    frames_[k - 1].emit_begin.swap(ce);
+  }
 }
 
 // PruneForwardLinks: the extra costs of frame f's tokens from their links'
@@ -131,20 +161,17 @@ void IncrementalLattice::PruneForwardLinks(int f, bool* extra_costs_changed, boo
     for (int t : frames_[f].toks) {
       HTok& tk = toks_[t];
       float tok_extra = kInf;
-      size_t m = 0;
-      for (size_t i = 0; i < tk.links.size(); i++) {
-        const HLink& l = tk.links[i];
+      ForLinks(t, [&](HLink& l) {
         const HTok& nt = toks_[l.dst];
         float link_extra = nt.extra + ((tk.tot + l.ac + l.graph) - nt.tot);
         if (!nt.alive || link_extra > opt_.lattice_beam) {  // excise
           *links_pruned = true;
-          continue;
+          l.arc = -1;
+          return;
         }
         if (link_extra < 0.0f) link_extra = 0.0f;
         if (link_extra < tok_extra) tok_extra = link_extra;
-        tk.links[m++] = l;
-      }
-      tk.links.resize(m);
+      });
       if (std::fabs(tok_extra - tk.extra) > delta) changed = true;
       tk.extra = tok_extra;
     }
@@ -159,7 +186,6 @@ void IncrementalLattice::PruneTokensForFrame(int f) {
     HTok& tk = toks_[fr.toks[i]];
     if (tk.extra == kInf) {
       tk.alive = false;
-      std::vector<HLink>().swap(tk.links);
       continue;
     }
     fr.toks[m++] = fr.toks[i];
@@ -222,17 +248,16 @@ void IncrementalLattice::PruneForwardLinksFinal() {
         final_cost = it != final_costs_.end() ? it->second : kInf;
       }
       float tok_extra = (tk.tot + final_cost) - final_best_cost_;
-      size_t m = 0;
-      for (size_t i = 0; i < tk.links.size(); i++) {
-        const HLink& l = tk.links[i];
+      ForLinks(t, [&](HLink& l) {
         const HTok& nt = toks_[l.dst];
         float link_extra = nt.extra + ((tk.tot + l.ac + l.graph) - nt.tot);
-        if (!nt.alive || link_extra > opt_.lattice_beam) continue;
+        if (!nt.alive || link_extra > opt_.lattice_beam) {
+          l.arc = -1;
+          return;
+        }
         if (link_extra < 0.0f) link_extra = 0.0f;
         if (link_extra < tok_extra) tok_extra = link_extra;
-        tk.links[m++] = l;
-      }
-      tk.links.resize(m);
+      });
       if (tok_extra > opt_.lattice_beam) tok_extra = kInf;
       if (!ApproxEqual(tk.extra, tok_extra, delta)) changed = true;
       tk.extra = tok_extra;
@@ -374,12 +399,12 @@ void IncrementalLattice::BuildChunk(int M) {
     const float off = frames_[f].cost_offset;
     for (int t : frames_[f].toks) {
       const int s = t2s[t];
-      for (const HLink& l : toks_[t].links) {
+      ForLinks(t, [&](HLink& l) {
         auto it = t2s.find(l.dst);
-        if (it == t2s.end()) continue;  // emitting links out of the last frame
+        if (it == t2s.end()) return;  // emitting links out of the last frame
         const int il = g_->ilabel[l.arc];
         D.links.push_back(DetGraph::Link{s, it->second, il, g_->olabel[l.arc], l.graph, il != 0 ? l.ac - off : l.ac});
-      }
+      });
     }
   }
   // the last frame: token labels, final states with the final costs (after

@@ -488,6 +488,7 @@ const char* vamd_incremental_json(int nframes, const int* frame_begin, const int
   os.precision(9);
   os << "[";
   bool firstq = true;
+  const auto t_start = std::chrono::steady_clock::now();
   for (int e = 0; e < nev; e++) {
     if (ev_type[e] == 0) {  // frames up to ev_arg decoded, then the AdvanceDecoding end
       if (ev_arg[e] >= nframes) VAMD_ERR("event past the records");
@@ -503,7 +504,8 @@ const char* vamd_incremental_json(int nframes, const int* frame_begin, const int
       inc.FinalizeDecoding();
       ok = inc.GetLattice(inc.NumFramesDecoded(), true, &wl);
     }
-    os << (firstq ? "" : ", ") << "{\"nfl\": " << inc.NumFramesInLattice() << ", \"ok\": " << (ok ? 1 : 0)
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    os << (firstq ? "" : ", ") << "{\"ms\": " << ms << ", \"nfl\": " << inc.NumFramesInLattice() << ", \"ok\": " << (ok ? 1 : 0)
        << ", \"chunks\": " << inc.chunks() << ", \"arcs\": [";
     firstq = false;
     for (int s = 0; s < wl.NumStates(); s++) {
