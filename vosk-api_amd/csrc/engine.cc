@@ -1855,10 +1855,20 @@ void Engine::CopySegmentLattices(const std::vector<int>& slots, const std::vecto
             copy_calls_, copy_us_[0], copy_us_[1], copy_us_[2], copy_us_[3] >> 20);
 }
 
-void Engine::CopySegmentTail(int slot, int from, SegmentLattice* out) {
-  std::lock_guard<std::mutex> lk(mu_);
-  DEVICE_GUARD();
-  FlushLocked();
+void Engine::CopySegmentTail(int slot, int from, SegmentLattice* out, int upto, bool concurrent) {
+  std::unique_lock<std::mutex> lk(mu_, std::defer_lock);
+  if (!concurrent) lk.lock();
+  int prev_dev = -1;
+  if (hipGetDevice(&prev_dev) != hipSuccess) prev_dev = -1;
+  HIPCHECK(hipSetDevice(cfg_.device));
+  struct Restore {
+    int d;
+    ~Restore() {
+      if (d >= 0) (void)hipSetDevice(d);
+    }
+  } restore{concurrent ? prev_dev : -1};
+  if (concurrent && cfg_.pipeline) VAMD_ERR("concurrent segment copies need an engine without pipelining");
+  if (!concurrent) FlushLocked();
   out->frames.clear();
   out->arena.clear();
   out->links.clear();
@@ -1867,33 +1877,46 @@ void Engine::CopySegmentTail(int slot, int from, SegmentLattice* out) {
   out->arena_base = 0;
   out->link_base = 0;
   if (!dec_.links) return;
-  if (!copy_stream_) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
-  DecSlot st;
-  HIPCHECK(hipMemcpyAsync(&st, d_slots_ + slot, sizeof(DecSlot), hipMemcpyDeviceToHost, copy_stream_));
-  HIPCHECK(hipStreamSynchronize(copy_stream_));
+  auto copy = [&](void* dst, const void* src, size_t bytes) {
+    if (concurrent) {
+      HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    } else {
+      HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, copy_stream_));
+    }
+  };
+  auto sync = [&] {
+    if (!concurrent) HIPCHECK(hipStreamSynchronize(copy_stream_));
+  };
+  if (!concurrent && !copy_stream_) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+  DecSlot st, st2;
+  copy(&st, d_slots_ + slot, sizeof(DecSlot));
+  sync();
   out->overflow = st.lat_ovf || st.frames + 1 > dec_.lat_frame_cap || st.err;
-  const int nf = std::min(st.frames + 1, dec_.lat_frame_cap);
+  out->last_prune = st.last_prune;
+  int nf = std::min(st.frames + 1, dec_.lat_frame_cap);
+  if (upto >= 0) nf = std::min(nf, upto + 1);
   if (from >= nf || from < 0) return;
   out->frames.resize(nf - from);
-  HIPCHECK(hipMemcpyAsync(out->frames.data(), dec_.lat_frames + (size_t)slot * dec_.lat_frame_cap + from,
-                          sizeof(LatFrame) * (nf - from), hipMemcpyDeviceToHost, copy_stream_));
-  HIPCHECK(hipStreamSynchronize(copy_stream_));
+  copy(out->frames.data(), dec_.lat_frames + (size_t)slot * dec_.lat_frame_cap + from, sizeof(LatFrame) * (nf - from));
+  sync();
   const LatFrame& f0 = out->frames[0];
+  const LatFrame& fl = out->frames.back();
   const int a0 = std::max(0, f0.tok_base);
   const long long l0 = std::max(0ll, f0.link_begin);
-  const int na = std::max(0, st.arena_used - a0);
-  const long long nl = std::max(0ll, std::min(st.links_used, dec_.link_cap) - l0);
+  // the wanted frames' records only (later frames may be in the making)
+  const int na = std::max(0, fl.tok_base + fl.ntok - a0);
+  const long long nl = std::max(0ll, std::min(fl.link_end, dec_.link_cap) - l0);
   out->arena_base = a0;
   out->link_base = l0;
   out->arena.resize(na);
   out->links.resize(nl);
-  if (na > 0)
-    HIPCHECK(hipMemcpyAsync(out->arena.data(), dec_.arena + (size_t)slot * dec_.arena_cap + a0, sizeof(int4) * na,
-                            hipMemcpyDeviceToHost, copy_stream_));
-  if (nl > 0)
-    HIPCHECK(hipMemcpyAsync(out->links.data(), dec_.links + (size_t)slot * dec_.link_cap + l0, sizeof(int4) * nl,
-                            hipMemcpyDeviceToHost, copy_stream_));
-  HIPCHECK(hipStreamSynchronize(copy_stream_));
+  if (na > 0) copy(out->arena.data(), dec_.arena + (size_t)slot * dec_.arena_cap + a0, sizeof(int4) * na);
+  if (nl > 0) copy(out->links.data(), dec_.links + (size_t)slot * dec_.link_cap + l0, sizeof(int4) * nl);
+  sync();
+  if (concurrent) {  // a pruning pass may have compacted the records meanwhile
+    copy(&st2, d_slots_ + slot, sizeof(DecSlot));
+    if (st2.last_prune != st.last_prune || st2.frames < st.frames || st2.lat_ovf || st2.err) out->overflow = true;
+  }
 }
 
 PinnedPool::~PinnedPool() {

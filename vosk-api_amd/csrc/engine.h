@@ -139,6 +139,7 @@ struct SegmentLattice {
   // from link_base (0 for a whole segment)
   int first_frame = 0, arena_base = 0;
   long long link_base = 0;
+  int last_prune = 0;  // DecSlot::last_prune (a pruning pass compacts the records: it changes)
 };
 
 // Endpoint inputs of a stream (OnlineEndpoint [K]): decoder-segment frames,
@@ -398,7 +399,13 @@ class Engine {
   void CopySegmentLattice(int slot, SegmentLattice* out, bool drain = true);
   // Frames [from, decoded] of the segment with their tokens and links (the
   // recognizer's incremental lattice takes them as they come; drains).
-  void CopySegmentTail(int slot, int from, SegmentLattice* out);
+  // upto: the last frame wanted (-1: every decoded frame).  concurrent: for
+  // a stream engine without pipelining, from a thread other than the
+  // stream's while passes over other streams run: no engine lock, plain
+  // copies on the null stream, only frames <= upto read (their records are
+  // final); out->overflow is also set when a pruning pass compacted the
+  // stream's records meanwhile.
+  void CopySegmentTail(int slot, int from, SegmentLattice* out, int upto = -1, bool concurrent = false);
   // The same for several streams with the copies batched.
   void CopySegmentLattices(const std::vector<int>& slots, const std::vector<SegmentLattice*>& outs,
                            bool drain = true);

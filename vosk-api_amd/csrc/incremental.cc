@@ -4,13 +4,24 @@
 #include "incremental.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <limits>
+#include <memory>
 
 #include "common.h"
 #include "model_io.h"
 
 namespace vamd {
+
+// per-thread phase times (the host-only test ABI reports them)
+thread_local double vamd_inc_prof[6];  // (development) ms: add frame, prune, chunk build, determinize, accept, set finals
+struct IncProf {
+  int k;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit IncProf(int i) : k(i) {}
+  ~IncProf() { vamd_inc_prof[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+};
 
 namespace {
 constexpr float kInf = std::numeric_limits<float>::infinity();
@@ -105,6 +116,7 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
     if (opt_.prune_interval > 0 && (k - 1) % opt_.prune_interval == 0) PruneActiveTokens(Delta());
     frames_[k - 1].cost_offset = in.cost_offset;
   }
+  IncProf prof(0);
   frames_.emplace_back();
   HFrame& fr = frames_.back();
   const int base = (int)toks_.size();
@@ -115,14 +127,21 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
     fr.toks.push_back(base + i);
   }
   // split the links: emitting ones belong to the previous frame's tokens
+  // (one pass over the graph's label / weight arrays: their reads are the
+  // scattered ones)
   const int prev_n = k > 0 ? base - frames_[k - 1].first : 0;
+  std::vector<HLink> tmp(in.nlinks);
+  std::vector<char> emit_of(in.nlinks);
   std::vector<int> ce(prev_n + 1, 0), cp(in.ntok + 1, 0);
   for (int i = 0; i < in.nlinks; i++) {
     const IncFrameIn::Link& l = in.links[i];
-    const bool emit = g_->ilabel[l.arc] != 0;
+    const int il = g_->ilabel[l.arc];
+    const bool emit = il != 0;
     if (emit && k == 0) VAMD_ERR("incremental lattice: an emitting link into frame 0");
     if (l.dst < 0 || l.dst >= in.ntok || l.src < 0 || l.src >= (emit ? prev_n : in.ntok))
       VAMD_ERR("incremental lattice: link to a missing token");
+    tmp[i] = HLink{base + l.dst, l.arc, il, g_->olabel[l.arc], g_->weight[l.arc], emit ? l.ac : 0.0f};
+    emit_of[i] = emit;
     (emit ? ce : cp)[l.src + 1]++;
   }
   for (int i = 0; i < prev_n; i++) ce[i + 1] += ce[i];
@@ -131,16 +150,20 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
   {
     std::vector<int> fe(ce.begin(), ce.end() - 1), fp(cp.begin(), cp.end() - 1);
     for (int i = 0; i < in.nlinks; i++) {
-      const IncFrameIn::Link& l = in.links[i];
-      const bool emit = g_->ilabel[l.arc] != 0;
-      const HLink h{base + l.dst, l.arc, g_->weight[l.arc], emit ? l.ac : 0.0f};
-      if (emit) em[fe[l.src]++] = h;
-      else ep[fp[l.src]++] = h;
+      if (emit_of[i]) em[fe[in.links[i].src]++] = tmp[i];
+      else ep[fp[in.links[i].src]++] = tmp[i];
     }
   }
-  auto by_arc = [](const HLink& a, const HLink& b) { return a.arc < b.arc; };
-  for (int i = 0; i < prev_n; i++) std::sort(em.begin() + ce[i], em.begin() + ce[i + 1], by_arc);
-  for (int i = 0; i < in.ntok; i++) std::sort(ep.begin() + cp[i], ep.begin() + cp[i + 1], by_arc);
+  auto sort_range = [](HLink* a, int n) {  // by graph arc; ranges are short (insertion sort)
+    for (int i = 1; i < n; i++) {
+      const HLink x = a[i];
+      int j = i - 1;
+      for (; j >= 0 && a[j].arc > x.arc; j--) a[j + 1] = a[j];
+      a[j + 1] = x;
+    }
+  };
+  for (int i = 0; i < prev_n; i++) sort_range(em.data() + ce[i], ce[i + 1] - ce[i]);
+  for (int i = 0; i < in.ntok; i++) sort_range(ep.data() + cp[i], cp[i + 1] - cp[i]);
   fr.eps.swap(ep);
   fr.eps_begin.swap(cp);
   if (k > 0) {
@@ -195,6 +218,7 @@ void IncrementalLattice::PruneTokensForFrame(int f) {
 }
 
 void IncrementalLattice::PruneActiveTokens(float delta) {
+  IncProf prof(1);
   const int cur = NumFramesDecoded();
   prune_passes_++;
   // the current frame's tokens are not pruned, so they are counted here
@@ -337,6 +361,7 @@ bool IncrementalLattice::GetLattice(int M, bool use_final, WordLattice* out) {
 // re-determinized state 1 + its depth in the re-determinized part, then one
 // per frame from N, then the token-final states.
 void IncrementalLattice::BuildChunk(int M) {
+  std::unique_ptr<IncProf> prof(new IncProf(2));
   const int N = num_in_lattice_;
   DetGraph D;
   std::unordered_map<int, int> label2state;  // token_label2state
@@ -379,7 +404,11 @@ void IncrementalLattice::BuildChunk(int M) {
       cfin_[r] = CFin{};
     }
   }
-  std::unordered_map<int, int> t2s;
+  // token -> chunk state (the chunk's tokens are the toks_ range of its frames)
+  const int tbase = frames_[N].first;
+  const int tend = M + 1 < (int)frames_.size() ? frames_[M + 1].first : (int)toks_.size();
+  std::vector<int> t2s_v(tend - tbase, -1);
+  auto t2s_of = [&](int t) { return t >= tbase && t < tend ? t2s_v[t - tbase] : -1; };
   for (int f = N; f <= M; f++) {
     const int bucket = T0 + (f - N);
     for (int t : frames_[f].toks) {
@@ -392,18 +421,17 @@ void IncrementalLattice::BuildChunk(int M) {
         }
       }
       if (s < 0) s = D.AddState(bucket);
-      t2s[t] = s;
+      t2s_v[t - tbase] = s;
     }
   }
   for (int f = N; f <= M; f++) {
     const float off = frames_[f].cost_offset;
     for (int t : frames_[f].toks) {
-      const int s = t2s[t];
+      const int s = t2s_v[t - tbase];
       ForLinks(t, [&](HLink& l) {
-        auto it = t2s.find(l.dst);
-        if (it == t2s.end()) return;  // emitting links out of the last frame
-        const int il = g_->ilabel[l.arc];
-        D.links.push_back(DetGraph::Link{s, it->second, il, g_->olabel[l.arc], l.graph, il != 0 ? l.ac - off : l.ac});
+        const int d = t2s_of(l.dst);
+        if (d < 0) return;  // emitting links out of the last frame
+        D.links.push_back(DetGraph::Link{s, d, l.il, l.ol, l.graph, l.il != 0 ? l.ac - off : l.ac});
       });
     }
   }
@@ -428,13 +456,13 @@ void IncrementalLattice::BuildChunk(int M) {
     const int lab = next_label_++;
     next_t2l[t] = lab;
     const int fs = D.AddState(fbucket);
-    D.links.push_back(DetGraph::Link{t2s[t], fs, 0, lab, 0.0f, 0.0f});
+    D.links.push_back(DetGraph::Link{t2s_v[t - tbase], fs, 0, lab, 0.0f, 0.0f});
     D.fin[fs] = LW{fc, 0.0f};
   }
   if (N == 0) {
     for (int t : frames_[0].toks)
       if (toks_[t].state == g_->start) {
-        D.start = t2s[t];
+        D.start = t2s_v[t - tbase];
         break;
       }
     if (D.start < 0) {  // no start token: an empty lattice
@@ -444,6 +472,7 @@ void IncrementalLattice::BuildChunk(int M) {
     }
   }
   token2label_.swap(next_t2l);
+  prof.reset();
   AcceptRawLatticeChunk(D);
 }
 
@@ -490,7 +519,10 @@ bool IncrementalLattice::AcceptRawLatticeChunk(const DetGraph& raw) {
   lo.det_max_mem = opt_.det_max_mem;
   lo.max_states = opt_.max_states;
   WordLattice chunk;
-  if (!DeterminizePhonePrunedGraph(raw, *tid2phone_, *tid_first_, lo, &chunk)) {
+  std::unique_ptr<IncProf> prof(new IncProf(3));
+  const bool det_ok = DeterminizePhonePrunedGraph(raw, *tid2phone_, *tid_first_, lo, &chunk);
+  prof.reset(new IncProf(4));
+  if (!det_ok) {
     failed_ = true;
     DetInit();
     return false;

@@ -82,6 +82,10 @@ struct IncFrameIn {
   int nlinks = 0;
 };
 
+// per-thread phase times in ms (add frame, prune, chunk build, determinize,
+// append), accumulated for diagnostics (vamd_incremental_json reports them)
+extern thread_local double vamd_inc_prof[6];
+
 class IncrementalLattice {
  public:
   enum { kStateLabelOffset = 100000000, kTokenLabelOffset = 200000000, kMaxTokenLabel = 300000000 };
@@ -113,6 +117,7 @@ class IncrementalLattice {
  private:
   struct HLink {
     int dst, arc;  // arc -1: excised
+    int il, ol;    // the arc's labels
     float graph, ac;
   };
   struct HTok {

@@ -444,6 +444,7 @@ int vamd_lattice_set_phones(const int* tid2phone, const signed char* tid_first, 
 
 // host-only: the KaldiRecognizer's incremental lattice (incremental.h) over
 // per-frame decoder records, driven by a script of events
+
 const char* vamd_incremental_json(int nframes, const int* frame_begin, const int* tok_state, const float* tok_cost,
                                   const float* cost_offset, int nlink, const int* link_frame, const int* link_src,
                                   const int* link_dst, const int* link_arc, const float* link_ac, int narcs,
@@ -453,6 +454,7 @@ const char* vamd_incremental_json(int nframes, const int* frame_begin, const int
                                   const int* ev_type, const int* ev_arg) {
   static thread_local std::string out;
   API_TRY
+  for (double& x : vamd::vamd_inc_prof) x = 0;
   Graph g;
   g.ilabel.assign(arc_ilabel, arc_ilabel + narcs);
   g.olabel.assign(arc_olabel, arc_olabel + narcs);
@@ -505,7 +507,8 @@ const char* vamd_incremental_json(int nframes, const int* frame_begin, const int
       ok = inc.GetLattice(inc.NumFramesDecoded(), true, &wl);
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
-    os << (firstq ? "" : ", ") << "{\"ms\": " << ms << ", \"nfl\": " << inc.NumFramesInLattice() << ", \"ok\": " << (ok ? 1 : 0)
+    os << (firstq ? "" : ", ") << "{\"ms\": " << ms << ", \"prof\": [" << vamd::vamd_inc_prof[0] << ", " << vamd::vamd_inc_prof[1]
+       << ", " << vamd::vamd_inc_prof[2] << ", " << vamd::vamd_inc_prof[3] << ", " << vamd::vamd_inc_prof[4] << "], \"nfl\": " << inc.NumFramesInLattice() << ", \"ok\": " << (ok ? 1 : 0)
        << ", \"chunks\": " << inc.chunks() << ", \"arcs\": [";
     firstq = false;
     for (int s = 0; s < wl.NumStates(); s++) {

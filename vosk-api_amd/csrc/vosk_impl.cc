@@ -249,7 +249,10 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
     engine->Advance(sl);
     // each stream's AdvanceDecoding ended here: its incremental lattice runs
     // UpdateLatticeDeterminization at this frame count (replayed lazily)
-    for (Recognizer* r : sr) r->adv_ends_.push_back(engine->NumFramesDecoded(r->slot_));
+    for (Recognizer* r : sr) {
+      std::lock_guard<std::mutex> lk(r->inc_mu_);
+      r->adv_ends_.push_back(engine->NumFramesDecoded(r->slot_));
+    }
   }
   // EndpointDetected (src/recognizer.cc:318) of the AcceptWaveform requests
   std::vector<int> ep;
@@ -339,6 +342,7 @@ void Recognizer::SetSpkModel(SpkModel* spk) {
 }
 
 Recognizer::~Recognizer() {
+  WaitLattice();
   if (grammar_group_) {
     group_->by_slot.at(slot_) = nullptr;
     engine_->FreeSlot(slot_);
@@ -415,6 +419,7 @@ bool Recognizer::AcceptWaveform(std::vector<float>& w) {  // src/recognizer.cc:2
   if (!(state_ == RECOGNIZER_RUNNING || state_ == RECOGNIZER_INITIALIZED)) CleanUp();
   state_ = RECOGNIZER_RUNNING;
   const bool endpoint = Submit(&w, false);  // pieces, silence weights, decoding, endpoint
+  KickLattice();  // the lattice replay of the new frames, in the background
   samples_processed_ += w.size();
   if (spk_) spk_samples_.insert(spk_samples_.end(), w.begin(), w.end());  // src/recognizer.cc:314-316
   return endpoint;
@@ -575,15 +580,57 @@ std::string Recognizer::WordsText(const std::vector<WordSeg>& w) const {
 // The decoder segment's incremental lattice (incremental.h)
 // ---------------------------------------------------------------------------
 void Recognizer::ResetLattice() {
+  WaitLattice();
   if (inc_init_) inc_.Reset();
+  std::lock_guard<std::mutex> lk(inc_mu_);
   adv_ends_.clear();
   adv_done_ = 0;
   inc_next_frame_ = 0;
   inc_last_ = LatFrame{};
+  inc_last_prune_ = 0;
   inc_bad_ = false;
 }
 
+// the recognizers' lattice replays between calls (VOSK_AMD_LATTICE_THREADS,
+// default a quarter of the host threads, 2 to 8)
+static WorkerPool& LatticeWorkers() {
+  static WorkerPool pool([] {
+    const int hw = (int)std::thread::hardware_concurrency();
+    return EnvInt("VOSK_AMD_LATTICE_THREADS", std::max(2, std::min(8, hw / 4)));
+  }());
+  return pool;
+}
+
+void Recognizer::WaitLattice() {
+  std::unique_lock<std::mutex> lk(inc_mu_);
+  inc_cv_.wait(lk, [&] { return !inc_busy_; });
+}
+
+void Recognizer::KickLattice() {
+  {
+    std::lock_guard<std::mutex> lk(inc_mu_);
+    if (inc_busy_ || inc_bad_ || adv_done_ >= adv_ends_.size()) return;
+    inc_busy_ = true;
+  }
+  LatticeWorkers().Submit([this] {
+    try {
+      SyncLatticeWork(true);
+    } catch (const std::exception& e) {
+      VAMD_WARN("recognizer lattice replay failed: " << e.what());
+      inc_bad_ = true;
+    }
+    std::lock_guard<std::mutex> lk(inc_mu_);
+    inc_busy_ = false;
+    inc_cv_.notify_all();
+  });
+}
+
 bool Recognizer::SyncLattice() {
+  WaitLattice();
+  return SyncLatticeWork(false);
+}
+
+bool Recognizer::SyncLatticeWork(bool background) {
   const ModelData& m = engine_->model();
   if (!inc_init_) {
     IncrementalOptions o;  // LatticeIncrementalDecoderConfig with the model's options
@@ -595,23 +642,36 @@ bool Recognizer::SyncLattice() {
     inc_init_ = true;
   }
   if (inc_bad_) return false;
-  const int F = engine_->NumFramesDecoded(slot_);
-  if (F <= 0) return true;
-  if (adv_done_ >= adv_ends_.size()) return true;  // nothing new since the last replay
-  // the frames decoded since the last call, with one frame of overlap (the
-  // previous frame's arena offset checks that the records were not
-  // compacted by a pruning pass in between)
+  // the AdvanceDecoding ends recorded since the last replay (the passes
+  // append to adv_ends_ under inc_mu_)
+  std::vector<int> ends;
+  {
+    std::lock_guard<std::mutex> lk(inc_mu_);
+    ends.assign(adv_ends_.begin() + (long)adv_done_, adv_ends_.end());
+  }
+  if (ends.empty() || ends.back() <= 0) {
+    adv_done_ += ends.size();
+    return true;
+  }
+  // the frames decoded since the last replay, with one frame of overlap (its
+  // record and the stream's last pruning pass check that the records were
+  // not compacted in between: a compacted segment falls back)
   const int from = std::max(0, inc_next_frame_ - 1);
   SegmentLattice sl;
-  engine_->CopySegmentTail(slot_, from, &sl);
-  if (sl.overflow || sl.frames.empty() || (int)sl.frames.size() + from - 1 < adv_ends_.back() ||
-      (inc_next_frame_ > 0 && (sl.frames[0].tok_base != inc_last_.tok_base || sl.frames[0].ntok != inc_last_.ntok ||
-                               sl.frames[0].link_begin != inc_last_.link_begin ||
+  // (no engine lock: a recognizer engine does not pipeline, and passes over
+  // other streams -- or this one's next call, when the replay runs in the
+  // background -- only append to the records read here)
+  (void)background;
+  engine_->CopySegmentTail(slot_, from, &sl, ends.back(), true);
+  if (sl.overflow || sl.frames.empty() || (int)sl.frames.size() + from - 1 < ends.back() ||
+      (inc_next_frame_ > 0 && (sl.last_prune != inc_last_prune_ || sl.frames[0].tok_base != inc_last_.tok_base ||
+                               sl.frames[0].ntok != inc_last_.ntok || sl.frames[0].link_begin != inc_last_.link_begin ||
                                sl.frames[0].link_end != inc_last_.link_end))) {
     VAMD_WARN("recognizer lattice records unusable (overflow or compacted): results from the best path");
     inc_bad_ = true;
     return false;
   }
+  inc_last_prune_ = sl.last_prune;
   std::vector<int> st;
   std::vector<float> co;
   std::vector<IncFrameIn::Link> ln;
@@ -648,10 +708,10 @@ bool Recognizer::SyncLattice() {
     inc_last_ = fr;
     inc_next_frame_ = k + 1;
   };
-  for (; adv_done_ < adv_ends_.size(); adv_done_++) {
-    const int c = adv_ends_[adv_done_];
+  for (int c : ends) {
     while (inc_.NumFramesDecoded() < c) add(inc_.NumFramesDecoded() + 1);
     inc_.AdvanceEnd();
+    adv_done_++;
   }
   return !inc_.failed();
 }

@@ -150,6 +150,12 @@ class Recognizer {
   // overflow): the results fall back to the best path.
   bool SyncLattice();
   void ResetLattice();
+  // The replay also runs in the background between calls (a lattice worker
+  // after each AcceptWaveform), so a result finds most of it done; every
+  // foreground use waits for a running task first.
+  void KickLattice();
+  void WaitLattice();
+  bool SyncLatticeWork(bool background);
   // the MBR of an incremental lattice (graph scale, rescoring, alignment as
   // the reference's GetResult / PartialResult); false: empty lattice
   bool LatticeMbr(WordLattice&& wl, float graph_scale, bool rescore, MbrResult* r) const;
@@ -170,11 +176,15 @@ class Recognizer {
   long long samples_processed_ = 0, samples_round_start_ = 0;
   RecognizerState state_ = RECOGNIZER_INITIALIZED;
   IncrementalLattice inc_;
+  std::mutex inc_mu_;  // adv_ends_ (appended by the group's passes), inc_busy_
+  std::condition_variable inc_cv_;
+  bool inc_busy_ = false;  // a background replay is running
   bool inc_init_ = false, inc_bad_ = false;
   std::vector<int> adv_ends_;  // AdvanceDecoding ends of the segment (decoded frames)
   size_t adv_done_ = 0;        // ends replayed
   int inc_next_frame_ = 0;     // the next frame record to ingest
   LatFrame inc_last_{};        // the last ingested frame's record (a compaction check)
+  int inc_last_prune_ = 0;     // DecSlot::last_prune at the last copy (another compaction check)
   std::string last_result_;
   std::vector<float> resample_buf_;
   SpkModel* spk_ = nullptr;
