@@ -127,33 +127,33 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
     fr.toks.push_back(base + i);
   }
   // split the links: emitting ones belong to the previous frame's tokens
-  // (one pass over the graph's label / weight arrays: their reads are the
-  // scattered ones)
+  // (the graph's weights are the only scattered reads; labels are read for
+  // the links a chunk keeps)
   const int prev_n = k > 0 ? base - frames_[k - 1].first : 0;
-  std::vector<HLink> tmp(in.nlinks);
-  std::vector<char> emit_of(in.nlinks);
-  std::vector<int> ce(prev_n + 1, 0), cp(in.ntok + 1, 0);
+  std::vector<int>& ce = scratch_ce_;
+  std::vector<int>& cp = scratch_cp_;
+  ce.assign(prev_n + 1, 0);
+  cp.assign(in.ntok + 1, 0);
   for (int i = 0; i < in.nlinks; i++) {
     const IncFrameIn::Link& l = in.links[i];
-    const int il = g_->ilabel[l.arc];
-    const bool emit = il != 0;
-    if (emit && k == 0) VAMD_ERR("incremental lattice: an emitting link into frame 0");
-    if (l.dst < 0 || l.dst >= in.ntok || l.src < 0 || l.src >= (emit ? prev_n : in.ntok))
+    if (l.emit && k == 0) VAMD_ERR("incremental lattice: an emitting link into frame 0");
+    if (l.dst < 0 || l.dst >= in.ntok || l.src < 0 || l.src >= (l.emit ? prev_n : in.ntok))
       VAMD_ERR("incremental lattice: link to a missing token");
-    tmp[i] = HLink{base + l.dst, l.arc, il, g_->olabel[l.arc], g_->weight[l.arc], emit ? l.ac : 0.0f};
-    emit_of[i] = emit;
-    (emit ? ce : cp)[l.src + 1]++;
+    (l.emit ? ce : cp)[l.src + 1]++;
   }
   for (int i = 0; i < prev_n; i++) ce[i + 1] += ce[i];
   for (int i = 0; i < in.ntok; i++) cp[i + 1] += cp[i];
   std::vector<HLink> em(ce[prev_n]), ep(cp[in.ntok]);
-  {
-    std::vector<int> fe(ce.begin(), ce.end() - 1), fp(cp.begin(), cp.end() - 1);
-    for (int i = 0; i < in.nlinks; i++) {
-      if (emit_of[i]) em[fe[in.links[i].src]++] = tmp[i];
-      else ep[fp[in.links[i].src]++] = tmp[i];
-    }
+  for (int i = 0; i < in.nlinks; i++) {
+    const IncFrameIn::Link& l = in.links[i];
+    const HLink h{base + l.dst, l.arc, g_->weight[l.arc], l.emit ? l.ac : 0.0f};
+    if (l.emit) em[ce[l.src]++] = h;
+    else ep[cp[l.src]++] = h;
   }
+  for (int i = prev_n; i > 0; i--) ce[i] = ce[i - 1];  // back to begin offsets
+  if (prev_n >= 0) ce[0] = 0;
+  for (int i = in.ntok; i > 0; i--) cp[i] = cp[i - 1];
+  cp[0] = 0;
   auto sort_range = [](HLink* a, int n) {  // by graph arc; ranges are short (insertion sort)
     for (int i = 1; i < n; i++) {
       const HLink x = a[i];
@@ -165,10 +165,10 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
   for (int i = 0; i < prev_n; i++) sort_range(em.data() + ce[i], ce[i + 1] - ce[i]);
   for (int i = 0; i < in.ntok; i++) sort_range(ep.data() + cp[i], cp[i + 1] - cp[i]);
   fr.eps.swap(ep);
-  fr.eps_begin.swap(cp);
+  fr.eps_begin.assign(cp.begin(), cp.end());
   if (k > 0) {
     frames_[k - 1].emit.swap(em);
-    frames_[k - 1].emit_begin.swap(ce);
+    frames_[k - 1].emit_begin.assign(ce.begin(), ce.end());
   }
 }
 
@@ -178,27 +178,53 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
 void IncrementalLattice::PruneForwardLinks(int f, bool* extra_costs_changed, bool* links_pruned, float delta) {
   *extra_costs_changed = false;
   *links_pruned = false;
-  bool changed = true;
+  HFrame& fr = frames_[f];
+  const bool has_emit = !fr.emit_begin.empty();
+  // one sweep over the frame's tokens in list order (Gauss-Seidel: an epsilon
+  // link sees the destination's value of this sweep when it came earlier)
+  auto sweep = [&](int t) {
+    HTok& tk = toks_[t];
+    float tok_extra = kInf;
+    auto link = [&](HLink& l) {
+      const HTok& nt = toks_[l.dst];
+      float link_extra = nt.extra + ((tk.tot + l.ac + l.graph) - nt.tot);
+      if (!nt.alive || link_extra > opt_.lattice_beam) {  // excise
+        *links_pruned = true;
+        l.arc = -1;
+        return;
+      }
+      if (link_extra < 0.0f) link_extra = 0.0f;
+      if (link_extra < tok_extra) tok_extra = link_extra;
+    };
+    if (has_emit)
+      for (int i = fr.emit_begin[tk.local]; i < fr.emit_begin[tk.local + 1]; i++)
+        if (fr.emit[i].arc >= 0) link(fr.emit[i]);
+    bool eps = false;
+    for (int i = fr.eps_begin[tk.local]; i < fr.eps_begin[tk.local + 1]; i++)
+      if (fr.eps[i].arc >= 0) {
+        link(fr.eps[i]);
+        eps |= fr.eps[i].arc >= 0;
+      }
+    const bool ch = std::fabs(tok_extra - tk.extra) > delta;
+    tk.extra = tok_extra;
+    return std::make_pair(ch, eps);
+  };
+  // the first sweep visits every token; a later one (Kaldi's loop "until no
+  // extra cost moved by more than delta") only the tokens with epsilon links
+  // left: a token with emitting links only gets the same value again (the
+  // next frame's extra costs do not move here), so skipping it changes
+  // nothing
+  bool changed = false;
+  std::vector<int> eps_toks;
+  for (int t : fr.toks) {
+    const auto r = sweep(t);
+    changed |= r.first;
+    if (r.second) eps_toks.push_back(t);
+  }
   while (changed) {
+    *extra_costs_changed = true;
     changed = false;
-    for (int t : frames_[f].toks) {
-      HTok& tk = toks_[t];
-      float tok_extra = kInf;
-      ForLinks(t, [&](HLink& l) {
-        const HTok& nt = toks_[l.dst];
-        float link_extra = nt.extra + ((tk.tot + l.ac + l.graph) - nt.tot);
-        if (!nt.alive || link_extra > opt_.lattice_beam) {  // excise
-          *links_pruned = true;
-          l.arc = -1;
-          return;
-        }
-        if (link_extra < 0.0f) link_extra = 0.0f;
-        if (link_extra < tok_extra) tok_extra = link_extra;
-      });
-      if (std::fabs(tok_extra - tk.extra) > delta) changed = true;
-      tk.extra = tok_extra;
-    }
-    if (changed) *extra_costs_changed = true;
+    for (int t : eps_toks) changed |= sweep(t).first;
   }
 }
 
@@ -431,7 +457,8 @@ void IncrementalLattice::BuildChunk(int M) {
       ForLinks(t, [&](HLink& l) {
         const int d = t2s_of(l.dst);
         if (d < 0) return;  // emitting links out of the last frame
-        D.links.push_back(DetGraph::Link{s, d, l.il, l.ol, l.graph, l.il != 0 ? l.ac - off : l.ac});
+        const int il = g_->ilabel[l.arc];
+        D.links.push_back(DetGraph::Link{s, d, il, g_->olabel[l.arc], l.graph, il != 0 ? l.ac - off : l.ac});
       });
     }
   }

@@ -77,6 +77,7 @@ struct IncFrameIn {
     int src, dst;  // frame-local token indices (src in the previous frame if the arc emits)
     int arc;
     float ac;
+    bool emit;     // the arc has a transition-id (src in the previous frame)
   };
   const Link* links = nullptr;
   int nlinks = 0;
@@ -117,7 +118,6 @@ class IncrementalLattice {
  private:
   struct HLink {
     int dst, arc;  // arc -1: excised
-    int il, ol;    // the arc's labels
     float graph, ac;
   };
   struct HTok {
@@ -172,6 +172,7 @@ class IncrementalLattice {
   IncrementalOptions opt_;
   std::vector<HTok> toks_;
   std::vector<HFrame> frames_;
+  std::vector<int> scratch_ce_, scratch_cp_;  // AddFrame's link counts
   bool finalized_ = false, failed_ = false;
   std::unordered_map<int, float> final_costs_;
   float final_best_cost_ = 0;

@@ -474,7 +474,8 @@ const char* vamd_incremental_json(int nframes, const int* frame_begin, const int
   std::vector<std::vector<IncFrameIn::Link>> fl(std::max(nframes, 0));
   for (int i = 0; i < nlink; i++) {
     if (link_frame[i] < 0 || link_frame[i] >= nframes) VAMD_ERR("link frame out of range");
-    fl[link_frame[i]].push_back(IncFrameIn::Link{link_src[i], link_dst[i], link_arc[i], link_ac[i]});
+    fl[link_frame[i]].push_back(IncFrameIn::Link{link_src[i], link_dst[i], link_arc[i], link_ac[i],
+                                                 arc_ilabel[link_arc[i]] != 0});
   }
   auto add = [&](int k) {
     IncFrameIn f;

@@ -592,11 +592,11 @@ void Recognizer::ResetLattice() {
 }
 
 // the recognizers' lattice replays between calls (VOSK_AMD_LATTICE_THREADS,
-// default a quarter of the host threads, 2 to 8)
+// default a quarter of the host threads, 2 to 16)
 static WorkerPool& LatticeWorkers() {
   static WorkerPool pool([] {
     const int hw = (int)std::thread::hardware_concurrency();
-    return EnvInt("VOSK_AMD_LATTICE_THREADS", std::max(2, std::min(8, hw / 4)));
+    return EnvInt("VOSK_AMD_LATTICE_THREADS", std::max(2, std::min(16, hw / 4)));
   }());
   return pool;
 }
@@ -693,9 +693,9 @@ bool Recognizer::SyncLatticeWork(bool background) {
     const int prev_base = k > 0 ? sl.frames[k - 1 - from].tok_base : 0;
     for (long long i = lb; i < le; i++) {
       const int4 r = sl.links[i];
-      const bool emit = m.graph.ilabel[r.z] != 0;
+      const bool emit = r.x < fr.tok_base;  // a source in the previous frame: an emitting arc
       ln.push_back(IncFrameIn::Link{r.x - (emit ? prev_base : fr.tok_base), r.y - fr.tok_base, r.z,
-                                    BitsToFloat(r.w)});
+                                    BitsToFloat(r.w), emit});
     }
     IncFrameIn f;
     f.state = st.data();
