@@ -219,6 +219,7 @@ class SlotGroupCommit {
     gap_us_.assign(slots, -1.0);
   }
   void SetWindowUs(int us) { window_us_ = us; }
+  void SetAdaptive(bool on) { adaptive_ = on; }
   template <class BatchFn>
   void Run(int slot, BatchFn&& fn) {
     std::unique_lock<std::mutex> lk(mu_);
@@ -281,7 +282,7 @@ class SlotGroupCommit {
         last_.clear();
         for (int s : batch) {
           served_[s] = last_end_;
-          if (!timed_out_.count(s) && gap_us_[s] < (double)window_us_) last_.push_back(s);
+          if (!timed_out_.count(s) && (!adaptive_ || gap_us_[s] < (double)window_us_)) last_.push_back(s);
         }
         cv_.notify_all();
       }
@@ -305,6 +306,7 @@ class SlotGroupCommit {
   bool leader_ = false;
   // coalescing window (see above)
   int window_us_ = 0;
+  bool adaptive_ = true;  // skip streams whose callers come back later than the window
   bool waiting_ = false;
   std::condition_variable cv_lead_;
   std::vector<int> last_;

@@ -144,9 +144,11 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
   for (int i = 0; i < prev_n; i++) ce[i + 1] += ce[i];
   for (int i = 0; i < in.ntok; i++) cp[i + 1] += cp[i];
   std::vector<HLink> em(ce[prev_n]), ep(cp[in.ntok]);
+  const float* wt = g_->weight.data();
   for (int i = 0; i < in.nlinks; i++) {
     const IncFrameIn::Link& l = in.links[i];
-    const HLink h{base + l.dst, l.arc, g_->weight[l.arc], l.emit ? l.ac : 0.0f};
+    if (i + 16 < in.nlinks) __builtin_prefetch(wt + in.links[i + 16].arc);  // scattered graph reads
+    const HLink h{base + l.dst, l.arc, wt[l.arc], l.emit ? l.ac : 0.0f};
     if (l.emit) em[ce[l.src]++] = h;
     else ep[cp[l.src]++] = h;
   }

@@ -100,6 +100,7 @@ RecognizerGroup::RecognizerGroup(Engine* e) : engine(e), by_slot(e->config().max
   gc.Resize(e->config().max_slots);
   // coalescing window of the group commit (engine.h SlotGroupCommit)
   gc.SetWindowUs(EnvInt("VOSK_AMD_GROUP_WINDOW_US", 1000));
+  gc.SetAdaptive(EnvInt("VOSK_AMD_GROUP_ADAPTIVE", 1) != 0);
 }
 
 // Recognizers share one engine (its group commit batches the recognizers
@@ -144,6 +145,12 @@ RecognizerGroup* Model::AllocStreamSlot(int* slot) {
   cfg.max_step_samples = 4096;
   cfg.lattice = true;  // results come from the segment's lattice (MBR)
   cfg.host_lattice = true;  // the incremental lattice reads the records as they come
+  // the records of a whole utterance stay on the device (the in-kernel
+  // pruning compacts them only at half full): 4 M tokens / 8 M links per
+  // stream keep ~25 s at the bench model's density (~2 200 tokens, ~3 100
+  // links per frame), past the 20-s endpoint rule
+  cfg.arena_tokens = EnvInt("VOSK_AMD_REC_ARENA_TOKENS", 1 << 22);
+  cfg.lattice_links = EnvInt("VOSK_AMD_REC_LINKS", 1 << 23);
   engines_.emplace_back(new RecognizerGroup(new Engine(md_, cfg)));
   *slot = engines_.back()->engine->AllocSlot();
   return engines_.back().get();
@@ -183,6 +190,8 @@ RecognizerGroup* Model::GrammarEngine(const std::string& grammar) {
   cfg.max_step_samples = 4096;
   cfg.lattice = true;
   cfg.host_lattice = true;
+  cfg.arena_tokens = EnvInt("VOSK_AMD_REC_ARENA_TOKENS", 1 << 22);
+  cfg.lattice_links = EnvInt("VOSK_AMD_REC_LINKS", 1 << 23);
   RecognizerGroup* grp = new RecognizerGroup(new Engine(md, cfg));
   grammar_engines_[grammar].reset(grp);
   return grp;
@@ -607,6 +616,8 @@ void Recognizer::WaitLattice() {
 }
 
 void Recognizer::KickLattice() {
+  static const bool on = EnvInt("VOSK_AMD_LATTICE_BACKGROUND", 1) != 0;
+  if (!on) return;
   {
     std::lock_guard<std::mutex> lk(inc_mu_);
     if (inc_busy_ || inc_bad_ || adv_done_ >= adv_ends_.size()) return;
