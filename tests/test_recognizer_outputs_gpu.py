@@ -82,6 +82,22 @@ def test_test_simple_outputs_long_segment(synth_model, test_wave, partial_words)
         assert partials[:6] == [""] * 6
 
 
+def test_test_simple_outputs_compacted_records(synth_model, test_wave, monkeypatch):
+    """Arenas a fraction of the segment's records (64 K tokens, 128 K links
+    per stream; the 15-s segment makes ~230 K tokens, ~280 K links): the
+    engine's pruning pass compacts them many times while the incremental
+    lattice reads them (gated on the frames the host has read,
+    Engine::SetHostRead) -- every output still equals the oracle chain's, no
+    best-path fallback."""
+    monkeypatch.setenv("VOSK_AMD_REC_ARENA_TOKENS", str(1 << 16))
+    monkeypatch.setenv("VOSK_AMD_REC_LINKS", str(1 << 17))
+    wave = perturbed_stream(test_wave, 31, seconds=15.0)
+    o = oracle_py.OracleModel(synth_model)
+    exp = OI.recognizer_run(o, wave, chunk=4000, partial_words=True)
+    got = _run_library(synth_model, wave, True)
+    assert _compare(o, got, exp, True) > 10
+
+
 @pytest.mark.parametrize("partial_words", [False, True])
 def test_test_simple_outputs_with_endpoints(synth_model_ep, test_wave, partial_words):
     """Endpoints every few seconds: each Result() closes a decoder segment,

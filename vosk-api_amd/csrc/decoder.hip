@@ -3646,6 +3646,25 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   __shared__ long long prof_acc[PROF ? kDecProf : 1];
   pr.init(PROF && threadIdx.x == 0, prof_acc);
 
+  // PruneActiveTokens every prune_interval frames, once the segment is
+  // prune_start frames long or an arena prune_fill_pct full
+  auto prune_due = [&](const DecSlot& s) {
+    const bool full = a.prune_fill_pct <= 0 || s.frames >= a.prune_start ||
+                      (long long)s.arena_used * 100 >= (long long)a.arena_cap * a.prune_fill_pct ||
+                      (a.links && (long long)s.links_used * 100 >= (long long)a.link_cap * a.prune_fill_pct);
+    return a.prune_interval > 0 && !s.err && s.frames - s.last_prune >= a.prune_interval && full;
+  };
+  // records the host reads as they come (host_gate): the pass runs before
+  // this launch's frames, once the host has read every frame decoded so far
+  // -- the compaction then moves only records it holds, and the frontier's
+  // tokens (which the next frame's links point into) as one block, in order
+  if (a.host_gate && !job.reset && job.host_read >= st.frames && prune_due(st)) {
+    prune_segment<false>(a, sh, st, p, slot, pr);
+    __syncthreads();
+    if (sh.bad) st.err |= sh.bad;
+    __syncthreads();
+  }
+
   if (job.reset) {  // InitDecoding: start token, closure with cutoff = beam
     __syncthreads();
     if (st.err) {  // an overflow may have left unlisted entries
@@ -3919,12 +3938,8 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   __syncthreads();
   if (sh.bad) st.err |= sh.bad;
   if (st.ntok == 0 && !st.err) st.err |= 4;
-  // PruneActiveTokens every prune_interval frames (at the end of a launch),
-  // once the segment is prune_start frames long or an arena prune_fill_pct full
-  const bool full = a.prune_fill_pct <= 0 || st.frames >= a.prune_start ||
-                    (long long)st.arena_used * 100 >= (long long)a.arena_cap * a.prune_fill_pct ||
-                    (a.links && (long long)st.links_used * 100 >= (long long)a.link_cap * a.prune_fill_pct);
-  if (a.prune_interval > 0 && !st.err && st.frames - st.last_prune >= a.prune_interval && full) {
+  // PruneActiveTokens at the end of a launch (host_gate: at the start of one)
+  if (!a.host_gate && prune_due(st)) {
     pr.mark(10);
     prune_segment<false>(a, sh, st, p, slot, pr);
     __syncthreads();

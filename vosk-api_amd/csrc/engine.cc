@@ -725,6 +725,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   // re-walk depth below the last pruned frame (Kaldi walks until the extra
   // costs settle; a shallower re-walk only prunes less, the final lattice-beam
   // prune is exact either way)
+  dec_.host_gate = cfg_.host_lattice ? 1 : 0;
   dec_.prune_revisit = getenv("VOSK_AMD_DEC_PRUNE_REVISIT") ? atoi(getenv("VOSK_AMD_DEC_PRUNE_REVISIT")) : 5;
   dec_.debug = getenv("VOSK_AMD_DEC_DEBUG") ? atoi(getenv("VOSK_AMD_DEC_DEBUG")) : 0;
   dec_.arena_cap = cfg_.arena_tokens;
@@ -868,6 +869,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     HIPCHECK(hipStreamSynchronize(copy_stream_));
   }
   slots_.resize(S);
+  host_read_.reset(new std::atomic<int>[S]);
+  for (int i = 0; i < S; i++) host_read_[i].store(-1);
   VAMD_LOG("engine: device memory " << (dev_bytes_ >> 20) << " MB (Kaldi-order scratch "
                                     << (kaldi_bytes >> 20) << " MB), slots=" << S << " fpc=" << fpc << " priming=" << plan_.priming_chunks
                             << " ring=" << ring_ << " ops=" << plan_.ops.size()
@@ -1359,9 +1362,10 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
       if (dec_frames > 0 || h.samples > 0 || fin) {
         // reset 2: a new decoder; 1: InitDecoding of the same decoder (a
         // Recognizer's next segment keeps its HashList size, Kaldi order)
+        if (h.need_reset) host_read_[s].store(-1);  // a new segment: nothing read yet
         st_dec_.push_back(DecJob{s, first_real < 0 ? 0 : first_real * opc, dec_frames,
                                  h.need_reset ? (h.fresh_stream ? 3 : h.fresh_decoder ? 2 : 1) : 0, stats_rows,
-                                 fin ? 1 : 0, 0, 0});
+                                 fin ? 1 : 0, host_read_[s].load(std::memory_order_acquire), 0});
         if (h.need_reset) h.fresh_decoder = h.fresh_stream = false;
         stats_rows += dec_frames;
         if (h.need_reset) h.decoded = 0;
@@ -2346,7 +2350,7 @@ void Engine::DecodeExternal(int slot, const float* llh, int nframes, bool reset)
     h.stats.clear();
     const bool rs = first && (reset || h.need_reset);
     // (a decode from scratch is a new stream: lazy numbering starts over)
-    st_dec_.push_back(DecJob{slot, 0, n, rs ? (reset || h.fresh_stream ? 3 : h.fresh_decoder ? 2 : 1) : 0, 0, 0, 0,
+    st_dec_.push_back(DecJob{slot, 0, n, rs ? (reset || h.fresh_stream ? 3 : h.fresh_decoder ? 2 : 1) : 0, 0, 0, -1,
                              0});
     if (rs) h.fresh_decoder = h.fresh_stream = false;
     if (rs) h.decoded = 0;

@@ -16,6 +16,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <exception>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <set>
@@ -371,6 +372,10 @@ class Engine {
   // Pipeline mode: runs the pending decoder step, if any.
   void Flush();
   int NumFramesDecoded(int slot) const;
+  // host_lattice: the last frame of the stream's decoder segment whose
+  // records the host has read (-1: none).  The in-kernel pruning pass, which
+  // compacts the records, waits until it covers every decoded frame.
+  void SetHostRead(int slot, int frame) { host_read_[slot].store(frame, std::memory_order_release); }
   int NumFramesReady(int slot) const;  // output frames available to the decoder
   bool InputIsFinished(int slot) const;
   int PendingSamples(int slot) const;
@@ -536,6 +541,7 @@ class Engine {
   hipStream_t fstream_ = nullptr;  // front-end stream (pipeline mode)
   int ring_ = 0, sample_ring_ = 0, jobs_per_slot_ = 0;
   std::vector<SlotHost> slots_;
+  std::unique_ptr<std::atomic<int>[]> host_read_;  // SetHostRead, per slot
   EngineCounters counters_;
   StageTimes times_;
   hipEvent_t ev_[7] = {};

@@ -242,7 +242,8 @@ struct IvArgs {
 struct DecJob {
   int slot, llh_row0, nframes, reset, stats_row0;  // reset: 1 InitDecoding, 2 a new decoder, 3 a new stream
   int pad0;  // host bookkeeping: 1 = built after the stream's input ended (not read by the kernel)
-  int pad1, pad2;
+  int host_read;  // DecArgs::host_gate: the last frame whose records the host has read (-1: none)
+  int pad2;
 };
 
 struct FrameStat {
@@ -294,6 +295,9 @@ struct DecArgs {
   int prune_fill_pct;     // and only once the token or link arena is this full (percent; 0: always) ...
   int prune_start;        // ... or the segment is this many frames long
   int prune_revisit;      // frames below the last pruned frame a pass may re-walk
+  int host_gate;          // 1: the host reads the records as they come (EngineConfig::host_lattice):
+                          // a pass runs at the start of a launch, only when DecJob::host_read
+                          // covers every decoded frame (a compaction never moves unread records)
   int debug;              // VOSK_AMD_DEC_DEBUG bits (development): 1 invariant checks with printf,
                           // 2 no Kaldi-order GetCutoff shortcut, 4 Kaldi epsilon queue through HBM records
   float* extra;           // [slots][arena_cap] Kaldi extra_cost per token (pruning)

@@ -321,12 +321,20 @@ void IncrementalLattice::FinalizeDecoding() {
   if (frames_.empty() || finalized_) return;
   const int F = NumFramesDecoded();
   PruneForwardLinksFinal();
-  for (int f = F - 1; f >= 0; f--) {
+  // Kaldi walks every frame.  What the walk does below frame N - 1 (N =
+  // NumFramesInLattice(), already determinized) reaches no later output: the
+  // final chunk holds frames N.., whose tokens' extra costs come from the
+  // frames after them, and the walk's step at N - 1 prunes frame N's tokens.
+  // So the walk stops there -- unless the next GetLattice starts over from
+  // frame 0 (no chunk yet, or a final start state).
+  const bool restart = num_in_lattice_ == 0 || carcs_.empty() || cfin_[0].is;
+  const int lo = restart ? 0 : num_in_lattice_ - 1;
+  for (int f = F - 1; f >= lo; f--) {
     bool b1, b2;
     PruneForwardLinks(f, &b1, &b2, 0.0f);
     PruneTokensForFrame(f + 1);
   }
-  PruneTokensForFrame(0);
+  if (lo == 0) PruneTokensForFrame(0);
 }
 
 // UpdateLatticeDeterminization

@@ -145,10 +145,11 @@ RecognizerGroup* Model::AllocStreamSlot(int* slot) {
   cfg.max_step_samples = 4096;
   cfg.lattice = true;  // results come from the segment's lattice (MBR)
   cfg.host_lattice = true;  // the incremental lattice reads the records as they come
-  // the records of a whole utterance stay on the device (the in-kernel
-  // pruning compacts them only at half full): 4 M tokens / 8 M links per
-  // stream keep ~25 s at the bench model's density (~2 200 tokens, ~3 100
-  // links per frame), past the 20-s endpoint rule
+  // the records stay on the device until the in-kernel pruning compacts
+  // them at half full, once the host has read them all (Engine::SetHostRead):
+  // 4 M tokens / 8 M links per stream hold ~15 s at the bench model's density
+  // (~2 200 tokens, ~3 100 links per frame) before the first compaction, and
+  // leave room for the host's replay to lag behind the decoder
   cfg.arena_tokens = EnvInt("VOSK_AMD_REC_ARENA_TOKENS", 1 << 22);
   cfg.lattice_links = EnvInt("VOSK_AMD_REC_LINKS", 1 << 23);
   engines_.emplace_back(new RecognizerGroup(new Engine(md_, cfg)));
@@ -591,6 +592,7 @@ std::string Recognizer::WordsText(const std::vector<WordSeg>& w) const {
 void Recognizer::ResetLattice() {
   WaitLattice();
   if (inc_init_) inc_.Reset();
+  if (engine_ && slot_ >= 0) engine_->SetHostRead(slot_, -1);
   std::lock_guard<std::mutex> lk(inc_mu_);
   adv_ends_.clear();
   adv_done_ = 0;
@@ -660,13 +662,18 @@ bool Recognizer::SyncLatticeWork(bool background) {
     std::lock_guard<std::mutex> lk(inc_mu_);
     ends.assign(adv_ends_.begin() + (long)adv_done_, adv_ends_.end());
   }
-  if (ends.empty() || ends.back() <= 0) {
-    adv_done_ += ends.size();
-    return true;
+  if (ends.empty() || ends.back() <= 0 || ends.back() < inc_next_frame_) {  // no new frames: nothing to read
+    for (size_t i = 0; i < ends.size(); i++, adv_done_++)
+      if (ends[i] > 0) inc_.AdvanceEnd();
+    return !inc_.failed();
   }
-  // the frames decoded since the last replay, with one frame of overlap (its
-  // record and the stream's last pruning pass check that the records were
-  // not compacted in between: a compacted segment falls back)
+  // the frames decoded since the last replay, with one frame of overlap: the
+  // last frame read before, whose tokens the new frame's links point into.
+  // The engine's pruning pass compacts the records only once this replay's
+  // frames have all been read (Engine::SetHostRead), so between two reads it
+  // runs at most once, at the last frame read, moving that frame's tokens as
+  // one block in order: its record then has a new base and the same tokens.
+  // Anything else (an overflow) falls back.
   const int from = std::max(0, inc_next_frame_ - 1);
   SegmentLattice sl;
   // (no engine lock: a recognizer engine does not pipeline, and passes over
@@ -674,11 +681,22 @@ bool Recognizer::SyncLatticeWork(bool background) {
   // background -- only append to the records read here)
   (void)background;
   engine_->CopySegmentTail(slot_, from, &sl, ends.back(), true);
-  if (sl.overflow || sl.frames.empty() || (int)sl.frames.size() + from - 1 < ends.back() ||
-      (inc_next_frame_ > 0 && (sl.last_prune != inc_last_prune_ || sl.frames[0].tok_base != inc_last_.tok_base ||
-                               sl.frames[0].ntok != inc_last_.ntok || sl.frames[0].link_begin != inc_last_.link_begin ||
-                               sl.frames[0].link_end != inc_last_.link_end))) {
-    VAMD_WARN("recognizer lattice records unusable (overflow or compacted): results from the best path");
+  const char* bad = nullptr;
+  if (sl.overflow) {
+    bad = "lattice arena overflow";
+  } else if (sl.frames.empty() || (int)sl.frames.size() + from - 1 < ends.back()) {
+    bad = "frames missing";
+  } else if (inc_next_frame_ > 0) {
+    const LatFrame& f0 = sl.frames[0];
+    if (sl.last_prune != inc_last_prune_) {
+      if (sl.last_prune != from || f0.ntok != inc_last_.ntok) bad = "records compacted past the last frame read";
+    } else if (f0.tok_base != inc_last_.tok_base || f0.ntok != inc_last_.ntok ||
+               f0.link_begin != inc_last_.link_begin || f0.link_end != inc_last_.link_end) {
+      bad = "records moved";
+    }
+  }
+  if (bad) {
+    VAMD_WARN("recognizer lattice records unusable (" << bad << "): results from the best path");
     inc_bad_ = true;
     return false;
   }
@@ -724,6 +742,7 @@ bool Recognizer::SyncLatticeWork(bool background) {
     inc_.AdvanceEnd();
     adv_done_++;
   }
+  engine_->SetHostRead(slot_, inc_next_frame_ - 1);
   return !inc_.failed();
 }
 
