@@ -870,7 +870,11 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   }
   slots_.resize(S);
   host_read_.reset(new std::atomic<int>[S]);
-  for (int i = 0; i < S; i++) host_read_[i].store(-1);
+  prune_wait_.reset(new std::atomic<char>[S]);
+  for (int i = 0; i < S; i++) {
+    host_read_[i].store(-1);
+    prune_wait_[i].store(0);
+  }
   VAMD_LOG("engine: device memory " << (dev_bytes_ >> 20) << " MB (Kaldi-order scratch "
                                     << (kaldi_bytes >> 20) << " MB), slots=" << S << " fpc=" << fpc << " priming=" << plan_.priming_chunks
                             << " ring=" << ring_ << " ops=" << plan_.ops.size()
@@ -1362,7 +1366,10 @@ bool Engine::BuildStep(const std::vector<int>& slots) {
       if (dec_frames > 0 || h.samples > 0 || fin) {
         // reset 2: a new decoder; 1: InitDecoding of the same decoder (a
         // Recognizer's next segment keeps its HashList size, Kaldi order)
-        if (h.need_reset) host_read_[s].store(-1);  // a new segment: nothing read yet
+        if (h.need_reset) {  // a new segment: nothing read yet
+          host_read_[s].store(-1);
+          prune_wait_[s].store(0);
+        }
         st_dec_.push_back(DecJob{s, first_real < 0 ? 0 : first_real * opc, dec_frames,
                                  h.need_reset ? (h.fresh_stream ? 3 : h.fresh_decoder ? 2 : 1) : 0, stats_rows,
                                  fin ? 1 : 0, host_read_[s].load(std::memory_order_acquire), 0});
@@ -1409,6 +1416,13 @@ void Engine::FinishDecodeBatch(const DecBatch& b) {
                                                          << b.expect[i]);
     h.err = ds.err;
     h.dev_frames = ds.frames;
+    if (dec_.host_gate) {  // decode_kernel's prune_due: a pass waiting for the host's read
+      const bool full = dec_.prune_fill_pct <= 0 || ds.frames >= dec_.prune_start ||
+                        (long long)ds.arena_used * 100 >= (long long)dec_.arena_cap * dec_.prune_fill_pct ||
+                        (dec_.links && ds.links_used * 100 >= dec_.link_cap * dec_.prune_fill_pct);
+      prune_wait_[j.slot].store(dec_.prune_interval > 0 && !ds.err && ds.frames - ds.last_prune >= dec_.prune_interval &&
+                                full);
+    }
     if (cfg_.track_decoded) decoded_.push_back(DecodedJob{j.slot, j.pad0 != 0});
     if (ds.err) VAMD_WARN("decoder error flags " << ds.err << " on stream slot " << j.slot);
     counters_.frames_decoded += j.nframes;
@@ -1882,8 +1896,18 @@ void Engine::CopySegmentTail(int slot, int from, SegmentLattice* out, int upto, 
   out->link_base = 0;
   if (!dec_.links) return;
   auto copy = [&](void* dst, const void* src, size_t bytes) {
-    if (concurrent) {
-      HIPCHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    if (concurrent) {  // the calling thread's stream, through a pinned block (direct DMA)
+      size_t cap = 0;
+      char* pin = pinned_->Take(bytes, &cap);
+      struct Back {
+        PinnedPool* pool;
+        char* p;
+        size_t cap;
+        ~Back() { pool->Give(p, cap); }
+      } back{pinned_.get(), pin, cap};
+      HIPCHECK(hipMemcpyAsync(pin, src, bytes, hipMemcpyDeviceToHost, hipStreamPerThread));
+      HIPCHECK(hipStreamSynchronize(hipStreamPerThread));
+      memcpy(dst, pin, bytes);
     } else {
       HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, copy_stream_));
     }

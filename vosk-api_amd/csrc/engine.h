@@ -143,8 +143,6 @@ struct SegmentLattice {
   int last_prune = 0;  // DecSlot::last_prune (a pruning pass compacts the records: it changes)
 };
 
-// Endpoint inputs of a stream (OnlineEndpoint [K]): decoder-segment frames,
-// trailing silence frames on the best path, final relative cost.
 // Pinned host blocks for asynchronous segment copies, shared by an engine
 // and the copies in flight (thread-safe; blocks are reused by size).
 class PinnedPool {
@@ -376,6 +374,10 @@ class Engine {
   // records the host has read (-1: none).  The in-kernel pruning pass, which
   // compacts the records, waits until it covers every decoded frame.
   void SetHostRead(int slot, int frame) { host_read_[slot].store(frame, std::memory_order_release); }
+  // ... and true once that pass is due and waits for the host (as of the
+  // stream's last launch): the host should read the records before the next
+  // one, or the arenas fill up
+  bool PruneWaiting(int slot) const { return prune_wait_[slot].load(std::memory_order_acquire) != 0; }
   int NumFramesReady(int slot) const;  // output frames available to the decoder
   bool InputIsFinished(int slot) const;
   int PendingSamples(int slot) const;
@@ -541,7 +543,8 @@ class Engine {
   hipStream_t fstream_ = nullptr;  // front-end stream (pipeline mode)
   int ring_ = 0, sample_ring_ = 0, jobs_per_slot_ = 0;
   std::vector<SlotHost> slots_;
-  std::unique_ptr<std::atomic<int>[]> host_read_;  // SetHostRead, per slot
+  std::unique_ptr<std::atomic<int>[]> host_read_;    // SetHostRead, per slot
+  std::unique_ptr<std::atomic<char>[]> prune_wait_;  // PruneWaiting, per slot
   EngineCounters counters_;
   StageTimes times_;
   hipEvent_t ev_[7] = {};

@@ -428,6 +428,9 @@ bool Recognizer::AcceptWaveform(const float* data, int len) {
 bool Recognizer::AcceptWaveform(std::vector<float>& w) {  // src/recognizer.cc:297-323
   if (!(state_ == RECOGNIZER_RUNNING || state_ == RECOGNIZER_INITIALIZED)) CleanUp();
   state_ = RECOGNIZER_RUNNING;
+  // the engine's pruning pass waits for the host to read the records
+  // (Engine::SetHostRead): read them now, or the arenas fill up
+  if (engine_->PruneWaiting(slot_)) SyncLattice();
   const bool endpoint = Submit(&w, false);  // pieces, silence weights, decoding, endpoint
   KickLattice();  // the lattice replay of the new frames, in the background
   samples_processed_ += w.size();
