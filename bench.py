@@ -381,6 +381,7 @@ def run_api(args, model, dist, rank, world, base):
     order = ve.batch_lane_order(bm, 0)
     lane_streams = [sum(1 for r in recs if ve.batch_recognizer_lane(r) == li) for li in range(nl)]
     st = ve.batch_lane_stats(bm, 0)
+    mem = ve.batch_lane_memory(bm, 0)
     rprof = ve.batch_result_profile(bm)
     nonempty = sum(1 for t in texts if t.strip())
     words = sum(len(t.split()) for t in texts)
@@ -443,6 +444,7 @@ def run_api(args, model, dist, rank, world, base):
                     "tokens_per_frame": round(tot["tok_out"] / max(tot["frames"], 1), 1),
                     "arcs_per_frame": round((tot["arcs_emit"] + tot["arcs_eps"]) / max(tot["frames"], 1), 1),
                     "lattice_links_per_frame": round(tot["links"] / max(tot["frames"], 1), 1)},
+        "lane_memory": mem,
         "results": {"streams_with_text": nonempty, "words": words, "result_messages": nres[0]},
         "result_production": {k: round(v, 2) for k, v in rprof.items()},
     }

@@ -236,6 +236,10 @@ int vamd_batch_lanes(struct VoskBatchModel *m);
  * is quiescent (after vosk_batch_model_wait). */
 int vamd_batch_lane_stats(struct VoskBatchModel *m, int lane, int *load3, double *ms4,
                           long long *launches4, long long *dec6, int reset);
+/* one lane's device memory: {bytes allocated, token arena per stream, link
+ * arena per stream, the highest token / link arena fill of any stream after
+ * a decoder launch (the in-kernel pruning compacts them)} */
+int vamd_batch_lane_memory(struct VoskBatchModel *m, int lane, long long *out5);
 /* the lane's token-passing order: 1 Kaldi's sequential order (the CPU
  * reference's LatticeFasterDecoder), 0 the order-independent form */
 int vamd_batch_lane_kaldi_order(struct VoskBatchModel *m, int lane);

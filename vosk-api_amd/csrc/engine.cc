@@ -1416,6 +1416,8 @@ void Engine::FinishDecodeBatch(const DecBatch& b) {
                                                          << b.expect[i]);
     h.err = ds.err;
     h.dev_frames = ds.frames;
+    arena_hwm_ = std::max(arena_hwm_, (long long)ds.arena_used);
+    links_hwm_ = std::max(links_hwm_, ds.links_used);
     if (dec_.host_gate) {  // decode_kernel's prune_due: a pass waiting for the host's read
       const bool full = dec_.prune_fill_pct <= 0 || ds.frames >= dec_.prune_start ||
                         (long long)ds.arena_used * 100 >= (long long)dec_.arena_cap * dec_.prune_fill_pct ||

@@ -207,6 +207,11 @@ constexpr int kMaxResampleTables = 32;  // distinct input sample rates per engin
 // stream whose caller stops is waited for at most that long, once).  The
 // serving order of each stream's requests is unchanged (results too: streams
 // are independent in every kernel).
+//
+// Carried requests: the batched call may leave a request unfinished (it marks
+// the finished ones in `complete`); an unfinished request leads the next batch
+// (its caller keeps waiting), so a request's later work shares a batch with
+// the requests posted meanwhile instead of running alone.
 class SlotGroupCommit {
  public:
   void Resize(int slots) {
@@ -241,7 +246,7 @@ class SlotGroupCommit {
         continue;
       }
       leader_ = true;  // lead batches until this caller's stream is served
-      while (done_[slot] < ticket && !pending_.empty()) {
+      while (done_[slot] < ticket && (!pending_.empty() || !carry_.empty())) {
         if (window_us_ > 0 && !last_.empty()) {
           const auto deadline = last_end_ + std::chrono::microseconds(window_us_);
           // (a stream whose caller is this thread cannot post meanwhile)
@@ -259,27 +264,34 @@ class SlotGroupCommit {
           last_.clear();
         }
         std::vector<int> batch;
-        batch.swap(pending_);
+        batch.swap(carry_);
+        batch.insert(batch.end(), pending_.begin(), pending_.end());
+        pending_.clear();
         std::vector<long long> tick;
         for (int s : batch) tick.push_back(req_[s]);
         lk.unlock();
         std::exception_ptr e;
+        std::vector<char> complete(batch.size(), 1);
         try {
-          fn(batch);
+          fn(batch, &complete);
         } catch (...) {
           e = std::current_exception();
+          complete.assign(batch.size(), 1);
         }
         lk.lock();
-        for (size_t i = 0; i < batch.size(); i++) {
-          done_[batch[i]] = std::max(done_[batch[i]], tick[i]);
-          err_[batch[i]] = e;
-        }
         // the streams to wait for next time: those served, except one that
         // never came back within the last window (its caller stopped) or
         // whose caller usually comes back later than the window
         last_end_ = std::chrono::steady_clock::now();
         last_.clear();
-        for (int s : batch) {
+        for (size_t i = 0; i < batch.size(); i++) {
+          const int s = batch[i];
+          if (!complete[i]) {
+            carry_.push_back(s);
+            continue;
+          }
+          done_[s] = std::max(done_[s], tick[i]);
+          err_[s] = e;
           served_[s] = last_end_;
           if (!timed_out_.count(s) && (!adaptive_ || gap_us_[s] < (double)window_us_)) last_.push_back(s);
         }
@@ -302,6 +314,7 @@ class SlotGroupCommit {
   std::vector<std::thread::id> owner_;  // per stream: the thread of its last request
   std::vector<std::exception_ptr> err_;
   std::vector<int> pending_;
+  std::vector<int> carry_;  // unfinished requests of the last batch (they lead the next)
   bool leader_ = false;
   // coalescing window (see above)
   int window_us_ = 0;
@@ -393,6 +406,15 @@ class Engine {
   // Optional per-frame decoder statistics of the last Advance (collect_stats).
   const std::vector<FrameStat>& LastStats(int slot) const;
   const EngineCounters& counters() const { return counters_; }
+  // {device bytes, token arena per stream, link arena per stream, highest
+  // token arena fill of any stream after a launch, highest link arena fill}
+  void MemoryStats(long long* out5) const {
+    out5[0] = (long long)dev_bytes_;
+    out5[1] = cfg_.arena_tokens;
+    out5[2] = cfg_.lattice ? cfg_.lattice_links : 0;
+    out5[3] = arena_hwm_;
+    out5[4] = links_hwm_;
+  }
   // Tests: feature rows from the device ring; LLH rows decoded so far
   // (collect_llh); decoding of externally supplied log-likelihoods.
   void DebugFeatures(int slot, int first_frame, int n, std::vector<float>* out);
@@ -558,6 +580,7 @@ class Engine {
   MfccDev mfcc_{};
   std::vector<void*> dev_allocs_;
   size_t dev_bytes_ = 0;  // DevAlloc total (logged at construction)
+  long long arena_hwm_ = 0, links_hwm_ = 0;  // MemoryStats
   std::vector<NnetOpArgs> op_args_;
   std::vector<int> op_bk_;
   float** d_ring_ptrs_ = nullptr;

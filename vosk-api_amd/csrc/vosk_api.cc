@@ -962,6 +962,15 @@ int vamd_batch_lane_stats(VoskBatchModel* m, int lane, int* load3, double* ms4, 
   API_CATCH(-1)
 }
 
+int vamd_batch_lane_memory(VoskBatchModel* m, int lane, long long* out5) {
+  API_TRY
+  BatchModel* bm = (BatchModel*)m;
+  if (lane < 0 || lane >= bm->num_lanes()) VAMD_ERR("bad lane " << lane);
+  bm->lane_engine(lane)->MemoryStats(out5);
+  return 0;
+  API_CATCH(-1)
+}
+
 int vamd_batch_lane_kaldi_order(VoskBatchModel* m, int lane) {
   API_TRY
   BatchModel* bm = (BatchModel*)m;

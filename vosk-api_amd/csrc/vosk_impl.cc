@@ -198,17 +198,20 @@ RecognizerGroup* Model::GrammarEngine(const std::string& grammar) {
   return grp;
 }
 
-void RecognizerGroup::Serve(const std::vector<int>& slots) {
+void RecognizerGroup::Serve(const std::vector<int>& slots, std::vector<char>* complete) {
   std::vector<Recognizer*> rs;
   for (int s : slots) rs.push_back(by_slot.at(s));
   // pieces of 0.2 s as the reference's AcceptWaveform loop (src/recognizer.cc:305-311):
   // per stream, in order, UpdateSilenceWeights then AdvanceDecoding of each
   // piece.  Streams are independent, so pieces of different streams need not
-  // share a pass: a pass takes, for every stream, its next piece -- first
+  // share a round: a round takes, for every stream, its next piece -- first
   // only the streams whose next piece readies no chunk (no decoder work),
-  // then all the others together, so the call's decoder launches are shared
-  // by every stream that decodes (a 0.25 s call is a 0.2 s and a 0.05 s
-  // piece, and streams at different phases ready their chunk in either)
+  // then all the others together, so the decoder launch is shared by every
+  // stream that decodes.  A pass runs one such decoder round: a request whose
+  // later piece readies another chunk (a 0.25 s call is a 0.2 s and a 0.05 s
+  // piece, and either may complete a chunk) is carried into the next pass,
+  // whose decoder round it shares with the requests posted meanwhile, instead
+  // of a round of its own.
   std::vector<int> step(rs.size());
   std::vector<size_t> npiece(rs.size()), cur(rs.size(), 0);
   for (size_t i = 0; i < rs.size(); i++) {
@@ -216,11 +219,18 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
     const size_t n = rs[i]->req_wave_ ? rs[i]->req_wave_->size() : 0;
     npiece[i] = (n + step[i] - 1) / step[i];
     if (rs[i]->req_final_ && npiece[i] == 0) npiece[i] = 1;  // a FinalResult request: one piece, no samples
+    cur[i] = rs[i]->req_piece_;
   }
   // a stream whose own input fails (AcceptSamples) is dropped from the
   // pass with its error kept for its caller; failures of the batched
   // launches themselves reach every caller of the pass
   std::vector<size_t> quiet, busy;
+  // development: each pass's rounds on stderr (streams, which ran, ms)
+  static const bool trace = EnvInt("VOSK_AMD_GROUP_TRACE", 0) != 0;
+  std::ostringstream tr;
+  const auto ts0 = std::chrono::steady_clock::now();
+  if (trace) tr << "[group] pass " << rs.size() << ":";
+  bool decoded = false;
   while (true) {
     quiet.clear();
     busy.clear();
@@ -233,8 +243,10 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
       const bool decodes = r->req_final_ || engine->ChunkReadyAfter(r->slot_, add);
       (decodes ? busy : quiet).push_back(i);
     }
+    if (quiet.empty() && decoded) break;  // the next pieces decode: the next pass
     const std::vector<size_t>& run = !quiet.empty() ? quiet : busy;
     if (run.empty()) break;
+    if (quiet.empty()) decoded = true;
     std::vector<int> sl, first;
     std::vector<Recognizer*> sr;
     for (size_t i : run) {
@@ -256,7 +268,11 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
     }
     if (sl.empty()) continue;
     engine->UpdateSilenceWeights(sl, first);
+    const auto ta = std::chrono::steady_clock::now();
     engine->Advance(sl);
+    if (trace)
+      tr << " " << (!quiet.empty() ? "q" : "b") << sl.size() << "/"
+         << std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count();
     // each stream's AdvanceDecoding ended here: its incremental lattice runs
     // UpdateLatticeDeterminization at this frame count (replayed lazily)
     for (Recognizer* r : sr) {
@@ -264,6 +280,20 @@ void RecognizerGroup::Serve(const std::vector<int>& slots) {
       r->adv_ends_.push_back(engine->NumFramesDecoded(r->slot_));
     }
   }
+  // the requests with every piece done are complete; the others are carried
+  std::vector<Recognizer*> done;
+  complete->assign(rs.size(), 1);
+  for (size_t i = 0; i < rs.size(); i++) {
+    rs[i]->req_piece_ = cur[i];
+    if (!rs[i]->req_error_ && cur[i] < npiece[i]) (*complete)[i] = 0;
+    else done.push_back(rs[i]);
+  }
+  if (trace) {
+    tr << " done " << done.size() << " total "
+       << std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
+    fprintf(stderr, "%s\n", tr.str().c_str());
+  }
+  rs.swap(done);
   // EndpointDetected (src/recognizer.cc:318) of the AcceptWaveform requests
   std::vector<int> ep;
   std::vector<Recognizer*> er;
@@ -442,7 +472,10 @@ bool Recognizer::Submit(const std::vector<float>* wave, bool final) {
   req_wave_ = wave;
   req_final_ = final;
   req_error_ = nullptr;
-  group_->gc.Run(slot_, [this](const std::vector<int>& slots) { group_->Serve(slots); });
+  req_piece_ = 0;
+  group_->gc.Run(slot_, [this](const std::vector<int>& slots, std::vector<char>* complete) {
+    group_->Serve(slots, complete);
+  });
   req_wave_ = nullptr;
   if (req_error_) {  // a failure of this stream alone (the others were served)
     std::exception_ptr e = req_error_;
@@ -1086,6 +1119,7 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
   cfg.max_slots = EnvInt("VOSK_AMD_BATCH_SLOTS", 600);
   cfg.max_step_samples = cfg.frames_per_chunk * md_->mfcc.WindowShift() + 512;
   cfg.arena_tokens = EnvInt("VOSK_AMD_ARENA_TOKENS", 1 << 22);
+  cfg.lattice_links = EnvInt("VOSK_AMD_BATCH_LINKS", 1 << 22);
   cfg.lattice = true;  // PushLattice: MBR over each segment's lattice (batch_recognizer.cc:43-107)
   // Kaldi's sequential token-passing order (LatticeFasterDecoder, the CPU
   // reference's 1-best, as north_star asks).  The reference's

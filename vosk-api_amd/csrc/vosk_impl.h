@@ -52,7 +52,9 @@ struct RecognizerGroup {
   std::unique_ptr<Engine> engine;
   SlotGroupCommit gc;
   std::vector<Recognizer*> by_slot;
-  void Serve(const std::vector<int>& slots);  // the leader's batched pass
+  // the leader's batched pass; a request with pieces left after the pass's
+  // decoder round is not complete (carried into the next pass)
+  void Serve(const std::vector<int>& slots, std::vector<char>* complete);
 };
 
 class Model {
@@ -168,6 +170,7 @@ class Recognizer {
   // the request the group's batched pass serves (Submit)
   const std::vector<float>* req_wave_ = nullptr;
   bool req_final_ = false, req_endpoint_ = false;
+  size_t req_piece_ = 0;  // the request's next 0.2-s piece (carried across passes)
   std::exception_ptr req_error_;  // this stream's own failure in a group pass
   float sample_frequency_;
   int max_alternatives_ = 0;

@@ -26,7 +26,8 @@ def open_dll():
     dlldir = os.path.abspath(os.path.dirname(__file__))
     if sys.platform != "linux":
         raise TypeError("Unsupported platform")
-    path = os.path.join(dlldir, "libvosk.so")
+    # (VOSK_AMD_LIB: another build of the library, for A/B measurements)
+    path = os.getenv("VOSK_AMD_LIB") or os.path.join(dlldir, "libvosk.so")
     if not os.path.exists(path):
         raise OSError(f"cannot load library {path}: build it with `make -C vosk-api_amd`")
     return C.CDLL(path)

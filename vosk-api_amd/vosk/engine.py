@@ -66,6 +66,7 @@ _SIGS = {
     "vamd_batch_lanes": (C.c_int, [_vp]),
     "vamd_batch_lane_kaldi_order": (C.c_int, [_vp, C.c_int]),
     "vamd_batch_lane_stats": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, C.c_int]),
+    "vamd_batch_lane_memory": (C.c_int, [_vp, C.c_int, _vp]),
     "vamd_batch_recognizer_lane": (C.c_int, [_vp]),
     "vamd_batch_result_profile": (C.c_int, [_vp, _vp]),
     "vamd_admission_replay": (C.c_int, [C.c_int, _vp, C.c_int, _vp, _vp]),
@@ -145,6 +146,14 @@ def batch_lane_stats(model, lane, reset=False):
             "stages": {k: (float(ms[i]), int(ln[i])) for i, k in enumerate(names)},
             "decoder": dict(zip(("frames", "tok_in", "tok_out", "arcs_emit", "arcs_eps", "links"),
                                 (int(x) for x in dec)))}
+
+
+def batch_lane_memory(model, lane=0):
+    """{device bytes, token / link arena per stream, their highest fill} of a lane."""
+    o = np.zeros(5, np.int64)
+    _chk(_c.vamd_batch_lane_memory(model._handle, lane, o.ctypes.data))
+    return dict(zip(("device_bytes", "arena_tokens", "arena_links", "arena_tokens_high", "arena_links_high"),
+                    (int(x) for x in o)))
 
 
 def batch_result_profile(model):
