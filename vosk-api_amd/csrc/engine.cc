@@ -201,6 +201,10 @@ void* Engine::DevAlloc(size_t bytes) {
   }
   dev_allocs_.push_back(p);
   dev_bytes_ += bytes;
+  static const bool trace = getenv("VOSK_AMD_MEM_TRACE") != nullptr;  // development: allocations in order
+  if (trace && bytes >= (1u << 20))
+    fprintf(stderr, "[mem] #%zu %.1f MB (total %.1f MB)\n", dev_allocs_.size() - 1, bytes / 1048576.0,
+            dev_bytes_ / 1048576.0);
   return p;
 }
 
@@ -710,7 +714,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   // Kaldi's interval.  VOSK_AMD_DEC_PRUNE=1 prunes at every interval from the
   // start (Kaldi's schedule); VOSK_AMD_DEC_PRUNE_START / _FILL set the
   // thresholds.
-  dec_.prune_fill_pct = 50;
+  dec_.prune_fill_pct = cfg_.prune_fill_pct;
   dec_.prune_start = cfg_.host_lattice ? (1 << 30) : 300;
   if (const char* pe = getenv("VOSK_AMD_DEC_PRUNE")) {
     dec_.prune_interval = atoi(pe) ? m.dec.prune_interval : 0;

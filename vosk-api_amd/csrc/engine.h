@@ -104,6 +104,9 @@ struct EngineConfig {
   // in-kernel pruning passes (which compact the arenas) then run only when a
   // stream's arena is half full, never by segment length.
   bool host_lattice = false;
+  // the in-kernel pruning also starts once a stream's token or link arena is
+  // this full (percent; VOSK_AMD_DEC_PRUNE_FILL overrides)
+  int prune_fill_pct = 50;
   bool track_decoded = false;  // record completed decoder jobs for TakeDecoded
   // token passing in Kaldi's sequential order (LatticeFasterDecoder's HashList
   // order, running emitting cutoff, LIFO epsilon queue: the reference's

@@ -254,7 +254,7 @@ struct FrameStat {
 constexpr int kDecProf = 71;               // decoder phase-clock slots per stream (decoder.hip Prof)
 constexpr int kLazyExpanded = 1 << 30;  // lazy_id flag: the state's arcs are numbered
 constexpr int kLazyNewCap = 1024;       // lazy_new entries per list (>= decoder threads)
-constexpr int kKbMemb = 32;   // Kaldi order: members kept per hash bucket (more: counted by a scan)
+constexpr int kKbMemb = 8;    // Kaldi order: members kept per hash bucket (more: counted by a scan; a multiple of 4)
 struct DecArgs {
   long long* prof;       // optional per-slot phase clocks [slots][kDecProf] (diagnostics)
   const int4* sinfo;     // per state {arc_begin, eps_begin, arc_end, final cost bits}

@@ -1118,8 +1118,16 @@ BatchModel::BatchModel(const std::string& dir) : md_(std::make_shared<ModelData>
   // channels per GPU: the reference's num_channels = 600 (batch_model.cc:71)
   cfg.max_slots = EnvInt("VOSK_AMD_BATCH_SLOTS", 600);
   cfg.max_step_samples = cfg.frames_per_chunk * md_->mfcc.WindowShift() + 512;
-  cfg.arena_tokens = EnvInt("VOSK_AMD_ARENA_TOKENS", 1 << 22);
-  cfg.lattice_links = EnvInt("VOSK_AMD_BATCH_LINKS", 1 << 22);
+  // per stream: a 1.5 M-token backpointer arena and 2 M lattice links; the
+  // in-kernel pruning starts at 300 frames or once one is 3/4 full (~1.1 M
+  // tokens / ~1.5 M links: ~370 frames of the bench model, ~2 700 tokens and
+  // ~4 000 links per frame), and a quarter is left for the 25 frames between
+  // passes (measured high-water marks of the pruned records: 0.86 M tokens /
+  // 1.25 M links on the driver's bench, 1.2 M / 1.8 M on 60-s streams with
+  // 4 M arenas)
+  cfg.arena_tokens = EnvInt("VOSK_AMD_ARENA_TOKENS", 3 << 19);
+  cfg.lattice_links = EnvInt("VOSK_AMD_BATCH_LINKS", 1 << 21);
+  cfg.prune_fill_pct = 75;
   cfg.lattice = true;  // PushLattice: MBR over each segment's lattice (batch_recognizer.cc:43-107)
   // Kaldi's sequential token-passing order (LatticeFasterDecoder, the CPU
   // reference's 1-best, as north_star asks).  The reference's
