@@ -52,7 +52,7 @@ FP32_PEAK_TFLOPS = 157.3   # dense fp32 MFMA peak (MI355X_MICROARCH.md)
 SR = 16000
 FEED_BYTES = 8000          # test_gpu_batch.py:33 reads 8000 bytes per stream per round
 METRIC = "aggregate real-time factor (xRT) + p50 per-chunk latency, vosk-model-small-en-us"
-PMC_PROFILE = os.path.join(REPO, "profiles", "r05_final_decode_pmc.json")
+PMC_PROFILE = os.path.join(REPO, "profiles", "r06_final_decode_pmc.json")
 
 
 def load_wave():
