@@ -496,7 +496,16 @@ class _PrunedDet:
             return s
         n = s + (t,)
         self.nodes.add(n)
+        self._revive(n)
         return n
+
+    def _revive(self, n):
+        # after a rebuild, a string Kaldi's RebuildRepository deleted and that
+        # is referenced again is re-added: counted as added since the rebuild
+        rb = getattr(self, "rb_nodes", None)
+        if rb is not None and n in rb and n not in self.rb_live:
+            self.rb_live.add(n)
+            self.revived += 1
 
     @staticmethod
     def _times(w, g, a):
@@ -635,7 +644,7 @@ class _PrunedDet:
         arcs, elems = self.num_arcs * 32, self.num_elems * 24
         n = len(self.nodes) + 1
         rebuilt = getattr(self, "rebuilt", None)
-        repo = (n if rebuilt is None else rebuilt[0] + n - rebuilt[1]) * 32
+        repo = (n if rebuilt is None else rebuilt[0] + self.revived + n - rebuilt[1]) * 32
         if self.max_mem <= 0 or repo + arcs + elems <= self.max_mem:
             return True
         live = set()
@@ -658,6 +667,7 @@ class _PrunedDet:
             for e in t[4]:
                 mark(e[2])
         self.rebuilt = (len(live), n)
+        self.rb_nodes, self.rb_live, self.revived = set(self.nodes), live, 0
         repo = len(live) * 32
         if repo + arcs + elems > int(self.max_mem * 0.8):
             if self.queue:
@@ -692,6 +702,7 @@ class _PrunedDet:
             full = b1 + tuple(rest)
             for k in range(len(b1) + 1, len(full) + 1):
                 self.nodes.add(full[:k])
+                self._revive(full[:k])
             self.states[sid]["arcs"].append((label, nxt, (F32(w1[0] + w2[0]), F32(w1[1] + w2[1])), full))
             self.num_arcs += 1
         return done

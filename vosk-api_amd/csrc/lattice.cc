@@ -773,9 +773,20 @@ class PrunedDeterminizer {
   double eff_beam_ = 0;
   bool guard_ = false;
   // the repository as Kaldi's RebuildRepository leaves it: the strings live
-  // at the last rebuild plus every string added since (-1: never rebuilt)
-  long long rebuilt_live_ = -1;
+  // at the last rebuild, plus every string added since -- new nodes, and
+  // nodes the rebuild would have deleted that are referenced again (Kaldi
+  // re-adds those; here they still exist: Revive counts them) (-1: never
+  // rebuilt)
+  long long rebuilt_live_ = -1, revived_ = 0;
   size_t rebuilt_at_ = 0;
+  std::vector<char> rebuilt_mark_;  // nodes below rebuilt_at_ live at the rebuild (or revived)
+  int Revive(int n) {
+    if (rebuilt_live_ >= 0 && n > 0 && (size_t)n < rebuilt_at_ && !rebuilt_mark_[n]) {
+      rebuilt_mark_[n] = 1;
+      revived_++;
+    }
+    return n;
+  }
   std::vector<int> at_pos_;
   std::vector<char> pending_;
   std::vector<std::vector<int>> fbucket_;
@@ -819,8 +830,8 @@ void PrunedDeterminizer::Closure(std::vector<Elem>* sub, int base) {
   }
   auto extend = [&](int str, int k) {
     if (cl_[k].lin == 0) return str;
-    if (memo_in_[k] == str) return memo_out_[k];
-    const int n = R_.Succ(str, cl_[k].lin);
+    if (memo_in_[k] == str) return Revive(memo_out_[k]);
+    const int n = Revive(R_.Succ(str, cl_[k].lin));
     memo_in_[k] = str;
     memo_out_[k] = n;
     return n;
@@ -910,7 +921,7 @@ int PrunedDeterminizer::AppendString(int node, int from_base, int to_node) {
   if (from_base == to_node) return node;
   std::vector<int> labels;
   R_.Get(to_node, from_base, &labels);
-  for (int l : labels) node = R_.Succ(node, l);
+  for (int l : labels) node = Revive(R_.Succ(node, l));
   return node;
 }
 
@@ -943,9 +954,9 @@ void PrunedDeterminizer::ProcessTransitions(int s) {
         const auto& l = cl_[k];
         int str = e.str;
         if (l.lin != 0) {
-          if (memo_in_[k] == str) str = memo_out_[k];
+          if (memo_in_[k] == str) str = Revive(memo_out_[k]);
           else {
-            const int n = R_.Succ(str, l.lin);
+            const int n = Revive(R_.Succ(str, l.lin));
             memo_in_[k] = str;
             memo_out_[k] = n;
             str = n;
@@ -1046,7 +1057,7 @@ void PrunedDeterminizer::ProcessTransition(Task* t) {
 bool PrunedDeterminizer::CheckMemory(double* eff) {
   const long long arcs = num_arcs_ * 32, elems = num_elems_ * 24;
   const long long nstr = rebuilt_live_ < 0 ? (long long)R_.parent.size()
-                                           : rebuilt_live_ + (long long)(R_.parent.size() - rebuilt_at_);
+                                           : rebuilt_live_ + revived_ + (long long)(R_.parent.size() - rebuilt_at_);
   long long repo = nstr * 32;
   if (opt_.max_mem <= 0 || repo + arcs + elems <= opt_.max_mem) return true;
   // rebuild: only strings referenced by states, arcs, tasks and the cache
@@ -1078,7 +1089,9 @@ bool PrunedDeterminizer::CheckMemory(double* eff) {
   long long live = 0;
   for (char u : used) live += u;
   rebuilt_live_ = live;
+  revived_ = 0;
   rebuilt_at_ = R_.parent.size();
+  rebuilt_mark_.swap(used);
   repo = live * 32;
   if (repo + arcs + elems > (long long)(opt_.max_mem * 0.8)) {
     if (!queue_.empty()) *eff = queue_.top()->prio - bwd_[D_.start];
