@@ -1591,9 +1591,17 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     }
     const float fc = funord((uint32_t)(slot_key(t, T, v) >> 32));
     const int4 si = a.sinfo[slot_state(t, T, v)];
+    const float c0 = c >= 0 ? AG_LD(&KC[c]) : kInf;
+    // one walk over the epsilon arcs: the productive ones at the final cost,
+    // and whether one is productive at the emitting cost (c0 >= fc)
     int cnt = 0;
+    bool prod = false;
     if (fc < cutoff)
-      for (int arc = si.y; arc < si.z; arc++) cnt += fc + __int_as_float(a.arcs[arc].y) < cutoff;
+      for (int arc = si.y; arc < si.z; arc++) {
+        const float w = __int_as_float(a.arcs[arc].y);
+        cnt += fc + w < cutoff;
+        prod = prod || c0 + w < cutoff;
+      }
     if (c >= 0 && cnt == 0) continue;  // relaxes nothing at any cost: not a queue token
     const int i = atomicAdd(&sh.kne, 1);
     if (i >= cap_m) {
@@ -1602,7 +1610,6 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     }
     if (v >= 0) t.hst[v] = i;
     else AG_ST(&T.stamp[~v], i);
-    const float c0 = c >= 0 ? AG_LD(&KC[c]) : kInf;
     km_set(K, KM, i, kMSlot, v);
     km_set(K, KM, i, kMCost, __float_as_int(c0));
     km_set(K, KM, i, kMCnt, cnt);
@@ -1611,8 +1618,6 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     // Kaldi's initial queue: a token of the emitting pass that relaxes an
     // arc below the cutoff at its emitting cost, keyed by its list order
     if (c >= 0 && c0 < cutoff) {
-      bool prod = false;
-      for (int arc = si.y; arc < si.z && !prod; arc++) prod = c0 + __int_as_float(a.arcs[arc].y) < cutoff;
       if (prod) {
         const int q = atomicAdd(&sh.kn0, 1);
         if (q < kKM) {
