@@ -1744,7 +1744,7 @@ void BatchModel::LaneLoop(Lane* L) {
   }
 }
 
-BatchRecognizer::BatchRecognizer(BatchModel* model, float sr) : model_(model), sample_frequency_(sr) {
+BatchRecognizer::BatchRecognizer(BatchModel* model, float sr) : model_(model) {
   // the reference resamples each call on its own, flushed at the call's end
   // (src/batch_recognizer.cc:27-29,157-158), and chunks the model-rate
   // samples: the stream's engine slot runs at the model rate and each call

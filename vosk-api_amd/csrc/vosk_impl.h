@@ -333,7 +333,6 @@ class BatchRecognizer {
   std::string FormatResult(const MbrResult& r, double offset_s) const;  // PushLattice
 
   BatchModel* model_;
-  float sample_frequency_;
   bool nlsml_ = false;
   std::vector<float> buffer_;  // model-rate samples not yet pushed as a chunk
   int call_rate_ = 0;          // input rate resampled per call (0: the model's rate)
