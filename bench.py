@@ -484,7 +484,7 @@ def run_engine(args, model, dist, rank, world, base, steps):
     phases = None
     if os.environ.get("VOSK_AMD_DEC_PROFILE"):
         ph = e.decoder_phases()
-        phases = {k: round(v / max(ph["frames"], 1), 1) for k, v in ph.items() if k != "frames"}
+        phases = {k: round(v / max(ph["frames"], 1), 4) for k, v in ph.items() if k != "frames"}
         per = e.decoder_phases_per_stream()[:S]
         clk = per[:, e.PHASE_CLOCK_IDX].sum(1).astype(np.float64)
         phases["stream_clock_max_over_mean"] = round(float(clk.max() / max(clk.mean(), 1.0)), 3)

@@ -122,6 +122,7 @@ struct DecShared {
   int karc_sum, karc_max, khbm_pops;  // wave replay: arcs iterated (all waves / the busiest), pops of HBM members
   int kheads;                         // wave replay: multi-token component heads listed in hist[]
   int kcomp_clk;                      // (profile) clocks of the longest component replay
+  int kbig;                           // (profile) this frame's queue members overflow the LDS records
 };
 
 // optional phase clocks (VOSK_AMD_DEC_PROFILE): thread 0 stamps s_memtime
@@ -2433,6 +2434,7 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
     pr.count(52, nm > 2048 ? 1 : 0);
     pr.count(53, adj_n > kKE ? 1 : 0);
   }
+  if (pr.on && threadIdx.x == 0) sh.kbig = nm > kKM;
   if (pr.on && nm > kKM) {  // frames whose queue members overflow the LDS records
     pr.count(48, (long long)__builtin_amdgcn_s_memtime() - t_nonemit0);
     pr.count(49, 1);
@@ -3649,6 +3651,7 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   bool lds = false;
   Prof pr;
   __shared__ long long prof_acc[PROF ? kDecProf : 1];
+  __shared__ long long prof_snap[PROF ? kDecProf : 1];  // (VOSK_AMD_DEC_DEBUG 32: the frame's start values)
   pr.init(PROF && threadIdx.x == 0, prof_acc);
 
   // PruneActiveTokens every prune_interval frames, once the segment is
@@ -3757,6 +3760,10 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
   }
   for (int f = 0; f < job.nframes; f++) {
     if (st.ntok == 0 || st.err) break;
+    const long long t_frame0 = pr.on ? (long long)__builtin_amdgcn_s_memtime() : 0;
+    if (pr.on && threadIdx.x == 0) sh.kbig = 0;
+    if (PROF && pr.on && (a.debug & 32))
+      for (int i = 0; i < kDecProf; i++) prof_snap[i] = pr.acc[i];
     const float* llh = a.llh + (size_t)(job.llh_row0 + f) * a.P;
     const float* Lp = stage_llh ? L : llh;
     const bool pf = stage_llh && f + 1 < job.nframes;
@@ -3939,6 +3946,14 @@ __global__ __launch_bounds__(DT) void decode_kernel(DecArgs a) {
     arcs_eps = 0;
     __syncthreads();
     if (sh.bad) st.err |= sh.bad;
+    if (pr.on) {  // whole-frame clocks, all frames and the big-queue ones
+      const long long dt = (long long)__builtin_amdgcn_s_memtime() - t_frame0;
+      pr.count(71, dt);
+      if (sh.kbig) pr.count(72, dt);
+      // development (VOSK_AMD_DEC_DEBUG 32): the phases of the big-queue frames only
+      if (PROF && (a.debug & 32) && !sh.kbig)
+        for (int i = 0; i < 71; i++) pr.acc[i] = prof_snap[i];
+    }
   }
   __syncthreads();
   if (sh.bad) st.err |= sh.bad;

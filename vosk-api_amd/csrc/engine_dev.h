@@ -251,7 +251,7 @@ struct FrameStat {
   float best, cutoff, next_cutoff, adaptive_beam;
 };
 
-constexpr int kDecProf = 71;               // decoder phase-clock slots per stream (decoder.hip Prof)
+constexpr int kDecProf = 73;               // decoder phase-clock slots per stream (decoder.hip Prof)
 constexpr int kLazyExpanded = 1 << 30;  // lazy_id flag: the state's arcs are numbered
 constexpr int kLazyNewCap = 1024;       // lazy_new entries per list (>= decoder threads)
 constexpr int kKbMemb = 8;    // Kaldi order: members kept per hash bucket (more: counted by a scan; a multiple of 4)

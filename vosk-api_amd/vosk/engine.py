@@ -469,7 +469,7 @@ class Engine:
               "n_members_gt2048", "n_adj_gt_lds", "n_kq_wave_arcs", "n_kq_wave_arcs_crit", "n_kq_wave_hbm_pops",
               "n_kq_hot_members", "n_kq_renumbered", "n_kq_lane_phase_clk", "n_kq_segments", "n_kq_comp_max_clk",
               "exp_lookback", "lazy_ids", "n_lazy_new", "n_lazy_general", "lazy_keys", "lazy_rank",
-              "lazy_arcs", "lazy_scan", "lazy_general")
+              "lazy_arcs", "lazy_scan", "lazy_general", "n_frame_clk_all", "n_frame_clk_big")
     PHASE_CLOCK_IDX = list(range(11)) + [16, 17, 18, 19, 22, 23, 24, 25, 26, 27, 34, 35, 41, 42, 43, 47, 62,
                                           63, 66, 67, 68, 69, 70]  # clock slots
     PHASE_CLOCKS = tuple(map(PHASES.__getitem__, PHASE_CLOCK_IDX))
