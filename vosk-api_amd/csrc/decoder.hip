@@ -2518,8 +2518,9 @@ __device__ __forceinline__ void kaldi_positions(const DecArgs& a, DecShared& sh,
           rk += (q.x < c) + (m + 1 < cnt[u] && q.y < c) + (m + 2 < cnt[u] && q.z < c) + (m + 3 < cnt[u] && q.w < c);
         }
       } else if (cnt[u] > kKbMemb) {  // a crowded bucket: count its tokens created before
+        // (from the bucket's first creation index: none of its tokens is older)
         crowded++;
-        for (int c2 = 0; c2 < c; c2++) rk += AG_LD(&KB[c2]) == b[u];
+        for (int c2 = AG_LD(&BF[b[u]]); c2 < c; c2++) rk += AG_LD(&KB[c2]) == b[u];
       }
       const int pos = bs[u] + rk;
       if (v[u] >= 0) t.hst[v[u]] = pos;
