@@ -79,3 +79,83 @@ def test_concurrent_recognizers_match_sequential(synth_model_ep, test_wave, max_
             for x, y in zip(wa, wb):
                 assert x["start"] == y["start"] and x["end"] == y["end"]
                 assert x["conf"] == pytest.approx(y["conf"], abs=1e-5)
+
+
+def _script(seed, nbytes):
+    """A seeded caller: AcceptWaveform calls of 0.0625-0.75 s (one to four
+    0.2-s pieces, so batched passes carry requests over), PartialResult after
+    some, one Reset for some streams, Result on endpoints, FinalResult."""
+    rng = np.random.default_rng(seed)
+    ops, o = [], 0
+    reset_at = int(rng.integers(nbytes // 3, 2 * nbytes // 3)) if seed % 3 == 0 else -1
+    while o < nbytes:
+        n = int(rng.choice([2000, 4000, 8000, 12000, 24000]))
+        ops.append(("accept", o, min(o + n, nbytes)))
+        if rng.random() < 0.35:
+            ops.append(("partial",))
+        if reset_at >= 0 and o <= reset_at < o + n:
+            ops.append(("reset",))
+        o += n
+    ops.append(("final",))
+    return ops
+
+
+def _play(rec, data, ops):
+    out = []
+    for op in ops:
+        if op[0] == "accept":
+            if rec.AcceptWaveform(data[op[1]:op[2]]):
+                out.append(("result", json.loads(rec.Result())))
+        elif op[0] == "partial":
+            out.append(("partial", json.loads(rec.PartialResult())))
+        elif op[0] == "reset":
+            rec.Reset()
+        else:
+            out.append(("final", json.loads(rec.FinalResult())))
+    return out
+
+
+def test_concurrent_mixed_calls_match_sequential(synth_model_ep, test_wave):
+    """Twelve recognizers on twelve threads with their own call sizes,
+    partial results (partial words on for half of them), resets and endpoint
+    results: every output -- partials included, word times and confidences --
+    equals the same calls made alone (the batched passes' carried requests
+    and the background lattice replays change nothing)."""
+    import vosk
+    vosk.SetLogLevel(-1)
+    n = 12
+    waves = [_pcm(perturbed_stream(test_wave, 70 + i, seconds=6.0)) for i in range(n)]
+    scripts = [_script(100 + i, len(waves[i])) for i in range(n)]
+    m = vosk.Model(synth_model_ep)
+
+    def make(i):
+        r = vosk.KaldiRecognizer(m, 16000)
+        r.SetWords(True)
+        r.SetPartialWords(i % 2 == 0)
+        return r
+
+    alone = []
+    for i in range(n):
+        r = make(i)
+        alone.append(_play(r, waves[i], scripts[i]))
+        del r
+    recs = [make(i) for i in range(n)]
+    together, errs = [None] * n, []
+
+    def work(i):
+        try:
+            together[i] = _play(recs[i], waves[i], scripts[i])
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=180)
+    assert not any(t.is_alive() for t in th)
+    assert not errs, errs
+    for i in range(n):
+        assert [k for k, _ in together[i]] == [k for k, _ in alone[i]], i
+        assert together[i] == alone[i], i
+    assert sum(1 for i in range(n) for k, v in alone[i] if k == "partial" and v.get("partial")) > n
