@@ -2099,6 +2099,36 @@ __device__ __forceinline__ int kaldi_nonemitting(const DecArgs& a, DecShared& sh
                   const int cnt = __builtin_amdgcn_readfirstlane(ur.w) & -(int)(cu < cutoff);
                   narc += cnt;
                   if (!L && u >= kKM && cnt > 0) nhbm++;
+                  if (cnt == 1) {
+                    // one productive arc (most pops): the same steps with
+                    // wave-uniform values only -- no per-lane arc and
+                    // destination reads, no v_readlane extraction
+                    const int2 r1 = adj(off);
+                    const int d = __builtin_amdgcn_readfirstlane(r1.x);
+                    if (d < 0) continue;
+                    const float tot = cu + __int_as_float(__builtin_amdgcn_readfirstlane(r1.y));
+                    if (!(tot < cutoff)) continue;
+                    const int4 dr = rec4(d);
+                    const float old = __int_as_float(__builtin_amdgcn_readfirstlane(dr.y));
+                    if (!(tot < old)) continue;
+                    if (lane == 0) {
+                      if (old == kInfL) {  // FindOrAddToken creates it
+                        setf(d, kMOrd, j);
+                        roots(d, prank);
+                      }
+                      setf(d, kMCost, __float_as_int(tot));
+                    }
+                    if (old == kInfL) j++;
+                    if (__builtin_amdgcn_readfirstlane(dr.w) > 0) {  // changed: re-queued
+                      if (sp == 64) {
+                        ovf = true;
+                        continue;
+                      }
+                      if (lane == sp) stk = d;
+                      sp++;
+                    }
+                    continue;
+                  }
                   for (int k0 = 0; k0 < cnt && !ovf; k0 += 64) {
                     const int kn = cnt - k0 < 64 ? cnt - k0 : 64;
                     const int2 rec = lane < kn ? adj(off + k0 + lane) : make_int2(-1, 0);
