@@ -9,6 +9,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <limits>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -667,6 +668,7 @@ void Recognizer::KickLattice() {
     } catch (const std::exception& e) {
       VAMD_WARN("recognizer lattice replay failed: " << e.what());
       inc_bad_ = true;
+      engine_->SetHostRead(slot_, std::numeric_limits<int>::max());  // nothing reads the records now
     }
     std::lock_guard<std::mutex> lk(inc_mu_);
     inc_busy_ = false;
@@ -734,6 +736,9 @@ bool Recognizer::SyncLatticeWork(bool background) {
   if (bad) {
     VAMD_WARN("recognizer lattice records unusable (" << bad << "): results from the best path");
     inc_bad_ = true;
+    // the segment's results come from the best path: the engine's pruning
+    // need not wait for reads any more (it would let the arenas fill up)
+    engine_->SetHostRead(slot_, std::numeric_limits<int>::max());
     return false;
   }
   inc_last_prune_ = sl.last_prune;
