@@ -308,8 +308,16 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     VAMD_ERR("no HIP device available: the MI355X engine requires a GPU (there is no CPU fallback)");
   HIPCHECK(hipSetDevice(cfg_.device));
   HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  HIPCHECK(hipStreamCreateWithFlags(&dstream_, hipStreamNonBlocking));
-  HIPCHECK(hipStreamCreateWithFlags(&fstream_, hipStreamNonBlocking));
+  // an engine that does not pipeline runs its stages in order on one stream:
+  // the HIP runtime hands streams hardware queues in turn (GPU_MAX_HW_QUEUES,
+  // 4 by default), so every stream an engine creates but does not need makes
+  // another engine's work share a queue with it (and wait behind it)
+  if (cfg_.pipeline) {
+    HIPCHECK(hipStreamCreateWithFlags(&dstream_, hipStreamNonBlocking));
+    HIPCHECK(hipStreamCreateWithFlags(&fstream_, hipStreamNonBlocking));
+  } else {
+    dstream_ = fstream_ = stream_;
+  }
   const ModelData& m = *md_;
   const int fss = m.dcb.frame_subsampling_factor;
   int fpc = cfg_.frames_per_chunk;
@@ -840,8 +848,10 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     HIPCHECK(hipHostMalloc((void**)&blk, want, hipHostMallocDefault));
     pinned_->Give(blk, want);
     // and the rest of StartSegmentCopies' buffers: allocated on the lane
-    // thread, they were ~10 ms of the first segments' tail
-    HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+    // thread, they were ~10 ms of the first segments' tail (a recognizer
+    // engine reads its records on the caller's stream: no copy stream of its
+    // own unless a fallback needs one, created then)
+    if (!cfg_.host_lattice) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
     HIPCHECK(hipEventCreateWithFlags(&copy_ev_, hipEventDisableTiming));
     HIPCHECK(hipHostMalloc((void**)&h_copy_slots_, sizeof(DecSlot) * S, hipHostMallocDefault));
     d_prune_slots_ = (int*)DevAlloc(sizeof(int) * S);
@@ -855,7 +865,7 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   // the tables above were cleared with null-stream memsets, which the
   // engine's non-blocking streams are not ordered after
   HIPCHECK(hipDeviceSynchronize());
-  if (cfg_.lattice) {
+  if (cfg_.lattice && !cfg_.host_lattice) {
     // the segment copies' path run once on an idle slot (frames 0: the
     // prune returns at once): the copy stream's first commands and first
     // launches cost ~9 ms each on the host, paid here instead of in the first
@@ -912,9 +922,9 @@ Engine::~Engine() {
   if (h_copy_stage_) (void)hipHostFree(h_copy_stage_);
   if (copy_ev_) (void)hipEventDestroy(copy_ev_);
   if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
+  if (dstream_ && dstream_ != stream_) (void)hipStreamDestroy(dstream_);
+  if (fstream_ && fstream_ != stream_) (void)hipStreamDestroy(fstream_);
   if (stream_) (void)hipStreamDestroy(stream_);
-  if (dstream_) (void)hipStreamDestroy(dstream_);
-  if (fstream_) (void)hipStreamDestroy(fstream_);
   if (call_stream_) (void)hipStreamSynchronize(call_stream_);
   if (d_bp_) (void)hipFree(d_bp_);
   if (h_bp_) (void)hipHostFree(h_bp_);

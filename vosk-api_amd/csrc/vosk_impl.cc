@@ -104,17 +104,18 @@ RecognizerGroup::RecognizerGroup(Engine* e) : engine(e), by_slot(e->config().max
   gc.SetAdaptive(EnvInt("VOSK_AMD_GROUP_ADAPTIVE", 1) != 0);
 }
 
-// Recognizers share one engine (its group commit batches the recognizers
-// that call together) until it is full; VOSK_AMD_STREAM_ENGINES > 1 spreads
-// them over that many engines first, each stepping on its own HIP streams.
-// Measured (profiles/r05_concurrent_recognizers.json): 32 threads 596 x RT on
-// one engine, 215 spread over 4 -- the engines' launches share the process's
-// 4 hardware queues (GPU_MAX_HW_QUEUES), so one engine's step waits behind
-// another's decoder launch instead of running beside it.  More engines are
-// created when all are full (VOSK_AMD_MAX_STREAM_ENGINES).
+// Recognizers are spread over VOSK_AMD_STREAM_ENGINES (2) engines of
+// VOSK_AMD_MAX_STREAMS (32) slots, the least-loaded first; each engine's
+// group commit batches the recognizers that call together, and the two
+// engines' passes run beside each other on the GPU (one HIP stream each: the
+// runtime's 4 hardware queues are handed out in turn, so more streams per
+// engine, or more engines, make one engine's pass wait behind another's).
+// Measured (profiles/r06_stream_engines.log, 20-s streams): 32 threads 669 x
+// RT on two engines vs 551 on one, 8 threads 311 vs 256, 4 engines 463 / 226.
+// More engines are created when all are full (VOSK_AMD_MAX_STREAM_ENGINES).
 RecognizerGroup* Model::AllocStreamSlot(int* slot) {
   std::lock_guard<std::mutex> lk(mu_);
-  const int spread = std::max(1, EnvInt("VOSK_AMD_STREAM_ENGINES", 1));
+  const int spread = std::max(1, EnvInt("VOSK_AMD_STREAM_ENGINES", 2));
   RecognizerGroup* best = nullptr;
   int best_use = 0;
   for (auto& g : engines_) {
@@ -130,7 +131,7 @@ RecognizerGroup* Model::AllocStreamSlot(int* slot) {
   }
   // each engine holds the decoder state of all its slots (~140 MB per slot
   // with lattices): the number of engines is capped
-  const int cap = EnvInt("VOSK_AMD_MAX_STREAM_ENGINES", 16);
+  const int cap = EnvInt("VOSK_AMD_MAX_STREAM_ENGINES", 32);
   if ((int)engines_.size() >= cap) {
     for (auto& g : engines_) {  // (a full spread: any free slot)
       *slot = g->engine->TryAllocSlot();
@@ -141,7 +142,7 @@ RecognizerGroup* Model::AllocStreamSlot(int* slot) {
   }
   EngineConfig cfg;
   cfg.frames_per_chunk = md_->dcb.frames_per_chunk;
-  cfg.max_slots = EnvInt("VOSK_AMD_MAX_STREAMS", 64);
+  cfg.max_slots = EnvInt("VOSK_AMD_MAX_STREAMS", 32);
   cfg.device = DeviceFromEnv();
   cfg.max_step_samples = 4096;
   cfg.lattice = true;  // results come from the segment's lattice (MBR)
@@ -163,7 +164,7 @@ void Model::FreeStreamSlot(RecognizerGroup* g, int slot) {
   g->by_slot.at(slot) = nullptr;
   g->engine->FreeSlot(slot);
   // an emptied engine past the spread gives its device memory back
-  const size_t keep = (size_t)std::max(1, EnvInt("VOSK_AMD_STREAM_ENGINES", 1));
+  const size_t keep = (size_t)std::max(1, EnvInt("VOSK_AMD_STREAM_ENGINES", 2));
   for (size_t i = keep; i < engines_.size(); i++)
     if (engines_[i].get() == g && g->engine->SlotsInUse() == 0) {
       engines_.erase(engines_.begin() + (long)i);
