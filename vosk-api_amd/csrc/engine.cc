@@ -318,6 +318,11 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
   } else {
     dstream_ = fstream_ = stream_;
   }
+  // a recognizer engine's record reads (CopySegmentTail from the lattice
+  // workers) get a queue of their own, next to the engine's: two engines
+  // take the 4 hardware queues without sharing (per-thread streams would be
+  // handed queues the engines' passes hold)
+  if (cfg_.host_lattice) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
   const ModelData& m = *md_;
   const int fss = m.dcb.frame_subsampling_factor;
   int fpc = cfg_.frames_per_chunk;
@@ -1911,8 +1916,14 @@ void Engine::CopySegmentTail(int slot, int from, SegmentLattice* out, int upto, 
   out->arena_base = 0;
   out->link_base = 0;
   if (!dec_.links) return;
+  // concurrent: the engine's copy stream, one read at a time
+  std::unique_lock<std::mutex> tl(tail_mu_, std::defer_lock);
+  if (concurrent) {
+    tl.lock();
+    if (!copy_stream_) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+  }
   auto copy = [&](void* dst, const void* src, size_t bytes) {
-    if (concurrent) {  // the calling thread's stream, through a pinned block (direct DMA)
+    if (concurrent) {  // through a pinned block (direct DMA)
       size_t cap = 0;
       char* pin = pinned_->Take(bytes, &cap);
       struct Back {
@@ -1921,8 +1932,8 @@ void Engine::CopySegmentTail(int slot, int from, SegmentLattice* out, int upto, 
         size_t cap;
         ~Back() { pool->Give(p, cap); }
       } back{pinned_.get(), pin, cap};
-      HIPCHECK(hipMemcpyAsync(pin, src, bytes, hipMemcpyDeviceToHost, hipStreamPerThread));
-      HIPCHECK(hipStreamSynchronize(hipStreamPerThread));
+      HIPCHECK(hipMemcpyAsync(pin, src, bytes, hipMemcpyDeviceToHost, copy_stream_));
+      HIPCHECK(hipStreamSynchronize(copy_stream_));
       memcpy(dst, pin, bytes);
     } else {
       HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, copy_stream_));

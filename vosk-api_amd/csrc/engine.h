@@ -595,6 +595,7 @@ class Engine {
   int* d_probe_ = nullptr;              // ProbeEndpoints buffers
   int* h_probe_ = nullptr;
   hipStream_t copy_stream_ = nullptr;  // segment lattice copies
+  std::mutex tail_mu_;                  // host_lattice: CopySegmentTail's concurrent copies on copy_stream_
   double step_prof_[4] = {0, 0, 0, 0};  // Step host profile: build, sync wait, after sync, total (ms)
   long long step_prof_n_ = 0;
   double copy_prof_[4] = {0, 0, 0, 0};  // StartSegmentCopies: prune + state read, pinned take, rest (ms), MB copied
