@@ -854,9 +854,8 @@ Engine::Engine(std::shared_ptr<const ModelData> md, const EngineConfig& cfg) : m
     pinned_->Give(blk, want);
     // and the rest of StartSegmentCopies' buffers: allocated on the lane
     // thread, they were ~10 ms of the first segments' tail (a recognizer
-    // engine reads its records on the caller's stream: no copy stream of its
-    // own unless a fallback needs one, created then)
-    if (!cfg_.host_lattice) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+    // engine created its copy stream beside its main stream, above)
+    if (!copy_stream_) HIPCHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
     HIPCHECK(hipEventCreateWithFlags(&copy_ev_, hipEventDisableTiming));
     HIPCHECK(hipHostMalloc((void**)&h_copy_slots_, sizeof(DecSlot) * S, hipHostMallocDefault));
     d_prune_slots_ = (int*)DevAlloc(sizeof(int) * S);
