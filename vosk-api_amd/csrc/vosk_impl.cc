@@ -812,11 +812,23 @@ const char* Recognizer::GetResult() {  // src/recognizer.cc:669-729
   // incremental determinizer (:678); an unusable record set falls back to the
   // one-shot lattice / best path of the segment
   WordLattice clat;
-  const bool inc = SyncLattice() && (inc_.FinalizeDecoding(), inc_.GetLattice(inc_.NumFramesDecoded(), true, &clat));
+  // development (VOSK_AMD_RESULT_TRACE=1): the result's parts on stderr
+  static const bool trace = EnvInt("VOSK_AMD_RESULT_TRACE", 0) != 0;
+  using clk = std::chrono::steady_clock;
+  const auto tr0 = clk::now();
+  const bool synced = SyncLattice();
+  const auto tr1 = clk::now();
+  const bool inc = synced && (inc_.FinalizeDecoding(), inc_.GetLattice(inc_.NumFramesDecoded(), true, &clat));
+  const auto tr2 = clk::now();
   if (inc && clat.NumStates() == 0) return StoreEmptyReturn();  // (rlat.Start() != 0, :714-716)
   if (max_alternatives_ == 0) {  // MbrResult, :429-482
     MbrResult r;
     if (!inc || !LatticeMbr(std::move(clat), 0.9f, true, &r)) r = SegmentMbr(engine_, slot_, m, true, 0.9f, true);
+    if (trace) {
+      auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+      fprintf(stderr, "[result] frames %d sync %.2f final %.2f mbr %.2f ms\n", inc_.NumFramesDecoded(), ms(tr0, tr1),
+              ms(tr1, tr2), ms(tr2, clk::now()));
+    }
     Json obj;
     for (size_t i = 0; i < r.words.size(); i++) {
       if (!words_) continue;
