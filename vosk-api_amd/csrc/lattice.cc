@@ -120,8 +120,15 @@ struct StrRepo {
   // and common-prefix queries)
   std::vector<int> parent{-1}, label{0}, len{0}, jump{0};
   std::vector<uint64_t> hash{0}, pw{1};
-  // (node, label) -> successor node: open addressing, linear probing (key
-  // and value side by side: one cache line per probe)
+  // each node's first successor (label, node; label -1: none yet) beside it:
+  // most nodes get one (a transition-id string mostly extends one way), and
+  // the table below then holds only the later ones
+  struct Child {
+    int lab, val;
+  };
+  std::vector<Child> first{Child{-1, -1}};
+  // (node, label) -> successor node beyond the first: open addressing,
+  // linear probing (key and value side by side: one cache line per probe)
   struct Slot {
     uint64_t key;
     int val;
@@ -151,15 +158,22 @@ struct StrRepo {
     return r >= kMod ? r - kMod : r;
   }
   int Succ(int id, int lab) {
-    const uint64_t k = ((uint64_t)(uint32_t)id << 32) | (uint32_t)lab;
-    size_t m = slot.size() - 1, q = Mix(k) & m;
-    while (slot[q].key != ~0ull) {
-      if (slot[q].key == k) return slot[q].val;
-      q = (q + 1) & m;
-    }
+    Child& fc = first[id];
+    if (fc.lab == lab) return fc.val;
     const int n = (int)parent.size();
-    slot[q] = Slot{k, n};
-    if (2 * ++sused > slot.size()) Grow();
+    if (fc.lab < 0) {
+      fc = Child{lab, n};
+    } else {
+      const uint64_t k = ((uint64_t)(uint32_t)id << 32) | (uint32_t)lab;
+      size_t m = slot.size() - 1, q = Mix(k) & m;
+      while (slot[q].key != ~0ull) {
+        if (slot[q].key == k) return slot[q].val;
+        q = (q + 1) & m;
+      }
+      slot[q] = Slot{k, n};
+      if (2 * ++sused > slot.size()) Grow();
+    }
+    first.push_back(Child{-1, -1});
     parent.push_back(id);
     label.push_back(lab);
     len.push_back(len[id] + 1);
