@@ -101,10 +101,10 @@ template <class F>
 void IncrementalLattice::ForLinks(int t, F&& f) {
   const HTok& tk = toks_[t];
   HFrame& fr = frames_[tk.frame];
-  if (!fr.emit_begin.empty())
-    for (int i = fr.emit_begin[tk.local]; i < fr.emit_begin[tk.local + 1]; i++)
+  if (!fr.emit_rng.empty())
+    for (int i = fr.emit_rng[tk.local].b; i < fr.emit_rng[tk.local].e; i++)
       if (fr.emit[i].arc >= 0) f(fr.emit[i]);
-  for (int i = fr.eps_begin[tk.local]; i < fr.eps_begin[tk.local + 1]; i++)
+  for (int i = fr.eps_rng[tk.local].b; i < fr.eps_rng[tk.local].e; i++)
     if (fr.eps[i].arc >= 0) f(fr.eps[i]);
 }
 
@@ -152,10 +152,14 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
     if (l.emit) em[ce[l.src]++] = h;
     else ep[cp[l.src]++] = h;
   }
-  for (int i = prev_n; i > 0; i--) ce[i] = ce[i - 1];  // back to begin offsets
-  if (prev_n >= 0) ce[0] = 0;
-  for (int i = in.ntok; i > 0; i--) cp[i] = cp[i - 1];
-  cp[0] = 0;
+  // ce[i] / cp[i] now end source i's links (and begin i + 1's)
+  std::vector<Rng>& rp = fr.eps_rng;
+  rp.resize(in.ntok);
+  for (int i = 0; i < in.ntok; i++) rp[i] = Rng{i ? cp[i - 1] : 0, cp[i]};
+  std::vector<Rng> re_none;
+  std::vector<Rng>& re = k > 0 ? frames_[k - 1].emit_rng : re_none;
+  re.resize(prev_n);
+  for (int i = 0; i < prev_n; i++) re[i] = Rng{i ? ce[i - 1] : 0, ce[i]};
   auto sort_range = [](HLink* a, int n) {  // by graph arc; ranges are short (insertion sort)
     for (int i = 1; i < n; i++) {
       const HLink x = a[i];
@@ -164,14 +168,10 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
       a[j + 1] = x;
     }
   };
-  for (int i = 0; i < prev_n; i++) sort_range(em.data() + ce[i], ce[i + 1] - ce[i]);
-  for (int i = 0; i < in.ntok; i++) sort_range(ep.data() + cp[i], cp[i + 1] - cp[i]);
+  for (int i = 0; i < prev_n; i++) sort_range(em.data() + re[i].b, re[i].e - re[i].b);
+  for (int i = 0; i < in.ntok; i++) sort_range(ep.data() + rp[i].b, rp[i].e - rp[i].b);
   fr.eps.swap(ep);
-  fr.eps_begin.assign(cp.begin(), cp.end());
-  if (k > 0) {
-    frames_[k - 1].emit.swap(em);
-    frames_[k - 1].emit_begin.assign(ce.begin(), ce.end());
-  }
+  if (k > 0) frames_[k - 1].emit.swap(em);
 }
 
 // PruneForwardLinks: the extra costs of frame f's tokens from their links'
@@ -181,35 +181,40 @@ void IncrementalLattice::PruneForwardLinks(int f, bool* extra_costs_changed, boo
   *extra_costs_changed = false;
   *links_pruned = false;
   HFrame& fr = frames_[f];
-  const bool has_emit = !fr.emit_begin.empty();
+  const bool has_emit = !fr.emit_rng.empty();
+  HTok* const T = toks_.data();
+  const float beam = opt_.lattice_beam;
+  bool pruned = false;
+  // a token's links of one kind: an excised one leaves its range (the rest
+  // move down in order), so later passes do not visit it again
+  auto links = [&](HLink* a, Rng& r, float tot, float* tok_extra) {
+    int w = r.b;
+    for (int i = r.b; i < r.e; i++) {
+      const HLink l = a[i];
+      if (l.arc < 0) continue;  // (excised by PruneForwardLinksFinal)
+      const HTok& nt = T[l.dst];
+      float link_extra = nt.extra + ((tot + l.ac + l.graph) - nt.tot);
+      if (!nt.alive || link_extra > beam) {  // excise
+        pruned = true;
+        continue;
+      }
+      if (link_extra < 0.0f) link_extra = 0.0f;
+      if (link_extra < *tok_extra) *tok_extra = link_extra;
+      a[w++] = l;
+    }
+    r.e = w;
+  };
   // one sweep over the frame's tokens in list order (Gauss-Seidel: an epsilon
   // link sees the destination's value of this sweep when it came earlier)
   auto sweep = [&](int t) {
-    HTok& tk = toks_[t];
+    HTok& tk = T[t];
     float tok_extra = kInf;
-    auto link = [&](HLink& l) {
-      const HTok& nt = toks_[l.dst];
-      float link_extra = nt.extra + ((tk.tot + l.ac + l.graph) - nt.tot);
-      if (!nt.alive || link_extra > opt_.lattice_beam) {  // excise
-        *links_pruned = true;
-        l.arc = -1;
-        return;
-      }
-      if (link_extra < 0.0f) link_extra = 0.0f;
-      if (link_extra < tok_extra) tok_extra = link_extra;
-    };
-    if (has_emit)
-      for (int i = fr.emit_begin[tk.local]; i < fr.emit_begin[tk.local + 1]; i++)
-        if (fr.emit[i].arc >= 0) link(fr.emit[i]);
-    bool eps = false;
-    for (int i = fr.eps_begin[tk.local]; i < fr.eps_begin[tk.local + 1]; i++)
-      if (fr.eps[i].arc >= 0) {
-        link(fr.eps[i]);
-        eps |= fr.eps[i].arc >= 0;
-      }
+    if (has_emit) links(fr.emit.data(), fr.emit_rng[tk.local], tk.tot, &tok_extra);
+    Rng& rp = fr.eps_rng[tk.local];
+    links(fr.eps.data(), rp, tk.tot, &tok_extra);
     const bool ch = std::fabs(tok_extra - tk.extra) > delta;
     tk.extra = tok_extra;
-    return std::make_pair(ch, eps);
+    return std::make_pair(ch, rp.e > rp.b);
   };
   // the first sweep visits every token; a later one (Kaldi's loop "until no
   // extra cost moved by more than delta") only the tokens with epsilon links
@@ -228,6 +233,7 @@ void IncrementalLattice::PruneForwardLinks(int f, bool* extra_costs_changed, boo
     changed = false;
     for (int t : eps_toks) changed |= sweep(t).first;
   }
+  *links_pruned = pruned;
 }
 
 void IncrementalLattice::PruneTokensForFrame(int f) {

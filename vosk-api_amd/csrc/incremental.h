@@ -129,14 +129,17 @@ class IncrementalLattice {
   // A token's forward links: its emitting links (recorded with the next
   // frame) then its epsilon links, each by graph arc (emitting arcs come
   // first in the graph's per-state arc order, so this is arc order)
+  struct Rng {
+    int b, e;
+  };
   struct HFrame {
     int first = 0;          // toks_ index of the frame's first token (frame-local index 0)
     std::vector<int> toks;  // live tokens, list order
     bool must_prune_fl = true, must_prune_tok = true;
     int num_toks = -1;
     float cost_offset = 0;  // of the emitting links out of this frame (Kaldi cost_offsets_[frame])
-    std::vector<HLink> emit, eps;             // links out of the frame's tokens, grouped by source
-    std::vector<int> emit_begin, eps_begin;  // per local token [begin, end) (size ntok + 1)
+    std::vector<HLink> emit, eps;         // links out of the frame's tokens, grouped by source
+    std::vector<Rng> emit_rng, eps_rng;  // per local token: its links [b, e) (e drops as links are pruned)
   };
   template <class F> void ForLinks(int t, F&& f);  // f(HLink&) over a token's live links
   struct CArc {
