@@ -104,18 +104,26 @@ RecognizerGroup::RecognizerGroup(Engine* e) : engine(e), by_slot(e->config().max
   gc.SetAdaptive(EnvInt("VOSK_AMD_GROUP_ADAPTIVE", 1) != 0);
 }
 
-// Recognizers are spread over VOSK_AMD_STREAM_ENGINES (2) engines of
+// Recognizers are spread over VOSK_AMD_STREAM_ENGINES engines of
 // VOSK_AMD_MAX_STREAMS (32) slots, the least-loaded first; each engine's
-// group commit batches the recognizers that call together, and the two
-// engines' passes run beside each other on the GPU (one HIP stream each: the
-// runtime's 4 hardware queues are handed out in turn, so more streams per
-// engine, or more engines, make one engine's pass wait behind another's).
-// Measured (profiles/r06_stream_engines.log, 20-s streams): 32 threads 669 x
-// RT on two engines vs 551 on one, 8 threads 311 vs 256, 4 engines 463 / 226.
-// More engines are created when all are full (VOSK_AMD_MAX_STREAM_ENGINES).
+// group commit batches the recognizers that call together, and the engines'
+// passes run beside each other on the GPU.  Each engine holds a HIP stream
+// and a copy stream, and the runtime hands its GPU_MAX_HW_QUEUES hardware
+// queues (4 unless the process sets a number; the Python package asks for 8
+// when unset) to streams in turn, so the default spread is queues / 2 (at
+// most 4): more engines than that make one engine's pass wait behind
+// another's.  Measured (profiles/r06_stream_engines.log,
+// r06_conc_queues.log, 20-s streams, 32 threads): 4 queues: one engine 551 x
+// RT, two 669, four 463; 8 queues: two 716-720, four 744-810.  More engines
+// are created when all are full (VOSK_AMD_MAX_STREAM_ENGINES).
+static int StreamEngineSpread() {
+  const int queues = std::max(1, EnvInt("GPU_MAX_HW_QUEUES", 4));
+  return std::max(1, EnvInt("VOSK_AMD_STREAM_ENGINES", std::max(1, std::min(4, queues / 2))));
+}
+
 RecognizerGroup* Model::AllocStreamSlot(int* slot) {
   std::lock_guard<std::mutex> lk(mu_);
-  const int spread = std::max(1, EnvInt("VOSK_AMD_STREAM_ENGINES", 2));
+  const int spread = StreamEngineSpread();
   RecognizerGroup* best = nullptr;
   int best_use = 0;
   for (auto& g : engines_) {
@@ -164,7 +172,7 @@ void Model::FreeStreamSlot(RecognizerGroup* g, int slot) {
   g->by_slot.at(slot) = nullptr;
   g->engine->FreeSlot(slot);
   // an emptied engine past the spread gives its device memory back
-  const size_t keep = (size_t)std::max(1, EnvInt("VOSK_AMD_STREAM_ENGINES", 2));
+  const size_t keep = (size_t)StreamEngineSpread();
   for (size_t i = keep; i < engines_.size(); i++)
     if (engines_[i].get() == g && g->engine->SlotsInUse() == 0) {
       engines_.erase(engines_.begin() + (long)i);

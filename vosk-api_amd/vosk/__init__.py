@@ -22,10 +22,30 @@ MODEL_DIRS = [os.getenv("VOSK_MODEL_PATH"), Path("/usr/share/vosk"),
               Path.home() / "AppData/Local/vosk", Path.home() / ".cache/vosk"]
 
 
+def _hardware_queues():
+    """HIP gives a process GPU_MAX_HW_QUEUES hardware queues (4 by default)
+    and hands them to its streams in turn; streams beyond that share a queue,
+    one's launches waiting behind another's.  KaldiRecognizers are spread over
+    up to 4 engines of two streams each (csrc/vosk_impl.cc StreamEngineSpread,
+    from this variable), so ask for 8 -- unless the process chose a number or
+    has started the HIP runtime already (it reads the variable when it
+    starts: the first HIP call)."""
+    if "GPU_MAX_HW_QUEUES" in os.environ:
+        return
+    torch = sys.modules.get("torch")
+    try:
+        if torch is not None and torch.cuda.is_initialized():
+            return
+    except Exception:
+        return
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
+
 def open_dll():
     dlldir = os.path.abspath(os.path.dirname(__file__))
     if sys.platform != "linux":
         raise TypeError("Unsupported platform")
+    _hardware_queues()
     # (VOSK_AMD_LIB: another build of the library, for A/B measurements)
     path = os.getenv("VOSK_AMD_LIB") or os.path.join(dlldir, "libvosk.so")
     if not os.path.exists(path):
