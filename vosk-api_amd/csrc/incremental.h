@@ -119,6 +119,8 @@ class IncrementalLattice {
   struct HLink {
     int dst, arc;  // arc -1: excised
     float graph, ac;
+    HLink() {}  // (no zero fill: a frame's arrays are written in full right after their allocation)
+    HLink(int d, int a, float g, float x) : dst(d), arc(a), graph(g), ac(x) {}
   };
   struct HTok {
     int state;
@@ -131,6 +133,8 @@ class IncrementalLattice {
   // first in the graph's per-state arc order, so this is arc order)
   struct Rng {
     int b, e;
+    Rng() {}  // (as HLink)
+    Rng(int b0, int e0) : b(b0), e(e0) {}
   };
   struct HFrame {
     int first = 0;          // toks_ index of the frame's first token (frame-local index 0)
@@ -162,7 +166,7 @@ class IncrementalLattice {
   void BuildChunk(int num_frames_to_include);  // GetLattice's chunk + AcceptRawLatticeChunk
   // LatticeIncrementalDeterminizer
   void DetInit();
-  bool AcceptRawLatticeChunk(const DetGraph& raw);
+  bool AcceptRawLatticeChunk(DetGraph&& raw);
   void SetFinalCosts(const std::unordered_map<int, float>* token_label2final_cost);
   int AddStateToClat();
   void AddArcToClat(int state, const CArc& arc);
