@@ -11,7 +11,7 @@ import bench  # noqa: E402
 def main():
     threads = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "32").split(",")]
     seconds = float(sys.argv[2]) if len(sys.argv) > 2 else 20.0
-    model = bench.bench_model(0, None, "la_small_en_us")
+    model = sys.argv[3] if len(sys.argv) > 3 else bench.bench_model(0, None, "la_small_en_us")
     import vosk
     vosk.SetLogLevel(-1)
     base = bench.load_wave()
