@@ -95,6 +95,7 @@ void IncrementalLattice::Reset() {
   token2label_.clear();
   next_label_ = kTokenLabelOffset;
   chunks_ = prune_passes_ = 0;
+  deferred_.clear();
   DetInit();
 }
 
@@ -255,6 +256,17 @@ void IncrementalLattice::PruneTokensForFrame(int f) {
   fr.num_toks = (int)m;
 }
 
+// PruneActiveTokens.  The next chunk holds frames N = NumFramesInLattice()
+// on; the walk's steps below N (forward links of frames B = N - 1 and down,
+// tokens of frames N - 1 and down) are read again only when a GetLattice
+// starts over from frame 0 (a final start state; FinalizeDecoding then too).
+// So that part of each pass is deferred: the pass records where it would
+// continue (B, delta, whether frame B's flag was raised, and frame N's extra
+// costs and liveness as the step read them), prunes frame N's tokens (the
+// step's other half, which the chunk reads), and ReplayDeferred runs the
+// recorded parts in order before a start-over, which then finds every frame
+// as the eager walk leaves it (the deferred part reads nothing above frame
+// N, and nothing else writes frames below it).
 void IncrementalLattice::PruneActiveTokens(float delta) {
   IncProf prof(1);
   const int cur = NumFramesDecoded();
@@ -262,7 +274,28 @@ void IncrementalLattice::PruneActiveTokens(float delta) {
   // the current frame's tokens are not pruned, so they are counted here
   // (UpdateLatticeDeterminization reads every frame's count)
   if (frames_[cur].num_toks == -1) frames_[cur].num_toks = (int)frames_[cur].toks.size();
+  const int B = num_in_lattice_ - 1;
   for (int f = cur - 1; f >= 0; f--) {
+    if (f == B && B + 1 < cur) {
+      DeferredPass d;
+      d.B = B;
+      d.delta = delta;
+      d.fl = frames_[B].must_prune_fl;
+      frames_[B].must_prune_fl = false;  // (raised again from d.fl when the part runs)
+      const int t0 = frames_[B + 1].first, t1 = frames_[B + 2].first;
+      d.extra.resize(t1 - t0);
+      d.alive.resize(t1 - t0);
+      for (int t = t0; t < t1; t++) {
+        d.extra[t - t0] = toks_[t].extra;
+        d.alive[t - t0] = toks_[t].alive;
+      }
+      deferred_.push_back(std::move(d));
+      if (frames_[B + 1].must_prune_tok) {  // the step's eager half: frame B + 1's tokens
+        PruneTokensForFrame(B + 1);
+        frames_[B + 1].must_prune_tok = false;
+      }
+      break;
+    }
     if (frames_[f].must_prune_fl) {
       bool ec = false, lp = false;
       PruneForwardLinks(f, &ec, &lp, delta);
@@ -275,6 +308,40 @@ void IncrementalLattice::PruneActiveTokens(float delta) {
       frames_[f + 1].must_prune_tok = false;
     }
   }
+}
+
+void IncrementalLattice::ReplayDeferred() {
+  for (DeferredPass& d : deferred_) {
+    const int B = d.B, t0 = frames_[B + 1].first;
+    std::vector<float> x(d.extra.size());
+    std::vector<char> al(d.alive.size());
+    for (size_t i = 0; i < x.size(); i++) {  // frame B + 1 as the pass saw it
+      HTok& tk = toks_[t0 + i];
+      x[i] = tk.extra;
+      al[i] = tk.alive;
+      tk.extra = d.extra[i];
+      tk.alive = d.alive[i];
+    }
+    if (d.fl) frames_[B].must_prune_fl = true;
+    for (int f = B; f >= 0; f--) {
+      if (frames_[f].must_prune_fl) {
+        bool ec = false, lp = false;
+        PruneForwardLinks(f, &ec, &lp, d.delta);
+        if (ec && f > 0) frames_[f - 1].must_prune_fl = true;
+        if (lp) frames_[f].must_prune_tok = true;
+        frames_[f].must_prune_fl = false;
+      }
+      if (f < B && frames_[f + 1].must_prune_tok) {
+        PruneTokensForFrame(f + 1);
+        frames_[f + 1].must_prune_tok = false;
+      }
+    }
+    for (size_t i = 0; i < x.size(); i++) {
+      toks_[t0 + i].extra = x[i];
+      toks_[t0 + i].alive = al[i];
+    }
+  }
+  deferred_.clear();
 }
 
 // ComputeFinalCosts over the last frame's tokens (list order)
@@ -339,6 +406,7 @@ void IncrementalLattice::FinalizeDecoding() {
   // frame 0 (no chunk yet, or a final start state).
   const bool restart = num_in_lattice_ == 0 || carcs_.empty() || cfin_[0].is;
   const int lo = restart ? 0 : num_in_lattice_ - 1;
+  if (restart) ReplayDeferred();
   for (int f = F - 1; f >= lo; f--) {
     bool b1, b2;
     PruneForwardLinks(f, &b1, &b2, 0.0f);
@@ -378,6 +446,7 @@ bool IncrementalLattice::GetLattice(int M, bool use_final, WordLattice* out) {
     // a start state that is final (the previous chunk's start reached its
     // last frame without a word) cannot be re-determinized: start over
     if (carcs_.empty() || cfin_[0].is) {
+      ReplayDeferred();
       num_in_lattice_ = 0;
       DetInit();
     }

@@ -162,6 +162,7 @@ class IncrementalLattice {
   void PruneForwardLinksFinal();
   void PruneTokensForFrame(int f);
   void PruneActiveTokens(float delta);
+  void ReplayDeferred();  // the deferred parts of the passes, in order (before a start-over)
   void ComputeFinalCosts(std::unordered_map<int, float>* fc, float* final_best_cost) const;
   void BuildChunk(int num_frames_to_include);  // GetLattice's chunk + AcceptRawLatticeChunk
   // LatticeIncrementalDeterminizer
@@ -180,6 +181,14 @@ class IncrementalLattice {
   std::vector<HTok> toks_;
   std::vector<HFrame> frames_;
   std::vector<int> scratch_ce_, scratch_cp_;  // AddFrame's link counts
+  struct DeferredPass {  // PruneActiveTokens' part below the next chunk
+    int B;
+    float delta;
+    bool fl;                  // frame B's must_prune_fl at the step
+    std::vector<float> extra;  // frame B + 1's tokens as the step read them
+    std::vector<char> alive;
+  };
+  std::vector<DeferredPass> deferred_;
   bool finalized_ = false, failed_ = false;
   std::unordered_map<int, float> final_costs_;
   float final_best_cost_ = 0;
