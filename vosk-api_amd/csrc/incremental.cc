@@ -78,9 +78,9 @@ void IncrementalLattice::Init(const Graph* g, const std::vector<int>* tid2phone,
   tid2phone_ = tid2phone;
   tid_first_ = tid_first;
   opt_ = opt;
-  // address space for ~15 s of tokens at the bench model's density up front:
-  // the pages are touched only as tokens come, and the array is never moved
-  // while it grows (a 20-s segment's 1.4 M tokens moved ~1x their 33 MB)
+  // address space for ~20 s of tokens at the bench model's density up front
+  // (32 MB): the pages are touched only as tokens come, and the array is
+  // never moved while it grows (a 20-s segment has ~1.4 M tokens)
   if (toks_.capacity() < (1u << 21)) toks_.reserve(1u << 21);
   Reset();
 }
@@ -106,10 +106,11 @@ template <class F>
 void IncrementalLattice::ForLinks(int t, F&& f) {
   const HTok& tk = toks_[t];
   HFrame& fr = frames_[tk.frame];
+  const int local = t - fr.first;
   if (!fr.emit_rng.empty())
-    for (int i = fr.emit_rng[tk.local].b; i < fr.emit_rng[tk.local].e; i++)
+    for (int i = fr.emit_rng[local].b; i < fr.emit_rng[local].e; i++)
       if (fr.emit[i].arc >= 0) f(fr.emit[i]);
-  for (int i = fr.eps_rng[tk.local].b; i < fr.eps_rng[tk.local].e; i++)
+  for (int i = fr.eps_rng[local].b; i < fr.eps_rng[local].e; i++)
     if (fr.eps[i].arc >= 0) f(fr.eps[i]);
 }
 
@@ -128,7 +129,7 @@ void IncrementalLattice::AddFrame(const IncFrameIn& in) {
   fr.first = base;
   fr.toks.reserve(in.ntok);
   for (int i = 0; i < in.ntok; i++) {
-    toks_.push_back(HTok{in.state[i], in.cost[i], 0.0f, true, k, i});
+    toks_.push_back(HTok{in.state[i], in.cost[i], 0.0f, k, true});
     fr.toks.push_back(base + i);
   }
   // split the links: emitting ones belong to the previous frame's tokens
@@ -214,8 +215,9 @@ void IncrementalLattice::PruneForwardLinks(int f, bool* extra_costs_changed, boo
   auto sweep = [&](int t) {
     HTok& tk = T[t];
     float tok_extra = kInf;
-    if (has_emit) links(fr.emit.data(), fr.emit_rng[tk.local], tk.tot, &tok_extra);
-    Rng& rp = fr.eps_rng[tk.local];
+    const int local = t - fr.first;
+    if (has_emit) links(fr.emit.data(), fr.emit_rng[local], tk.tot, &tok_extra);
+    Rng& rp = fr.eps_rng[local];
     links(fr.eps.data(), rp, tk.tot, &tok_extra);
     const bool ch = std::fabs(tok_extra - tk.extra) > delta;
     tk.extra = tok_extra;

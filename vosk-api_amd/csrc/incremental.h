@@ -122,12 +122,13 @@ class IncrementalLattice {
     HLink() {}  // (no zero fill: a frame's arrays are written in full right after their allocation)
     HLink(int d, int a, float g, float x) : dst(d), arc(a), graph(g), ac(x) {}
   };
-  struct HTok {
+  struct HTok {  // 16 bytes (its index in the frame: the toks_ index - the frame's first)
     int state;
     float tot, extra;
-    bool alive;
-    int frame, local;  // its frame and index there
+    int frame : 31;
+    bool alive : 1;
   };
+  static_assert(sizeof(HTok) == 16, "token record layout");
   // A token's forward links: its emitting links (recorded with the next
   // frame) then its epsilon links, each by graph arc (emitting arcs come
   // first in the graph's per-state arc order, so this is arc order)
